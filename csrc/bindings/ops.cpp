@@ -1,0 +1,393 @@
+// tiresias_amd — torch custom-op registration for the HIP kernel library.
+// Every op validates device / dtype / layout and fails loudly; all launches go
+// to the caller's current HIP stream (so they compose with RCCL side streams
+// and hipGraph capture).
+#include <ATen/ATen.h>
+#include <c10/hip/HIPStream.h>
+#include <torch/library.h>
+
+#include "tam/kernels.h"
+#include "tam/launch.h"
+
+using at::Tensor;
+using c10::optional;
+
+namespace {
+
+hipStream_t cur_stream(const Tensor& t) {
+  return c10::hip::getCurrentHIPStream(t.device().index()).stream();
+}
+
+void check_dev(const Tensor& t, const char* name) {
+  TORCH_CHECK(t.defined(), "tam: ", name, " is undefined");
+  TORCH_CHECK(t.is_cuda(), "tam: ", name, " must be a GPU tensor (HIP), got ", t.device());
+}
+void check_bf16(const Tensor& t, const char* name) {
+  check_dev(t, name);
+  TORCH_CHECK(t.scalar_type() == at::kBFloat16, "tam: ", name, " must be bfloat16, got ",
+              t.scalar_type());
+}
+void check_f32(const Tensor& t, const char* name) {
+  check_dev(t, name);
+  TORCH_CHECK(t.scalar_type() == at::kFloat, "tam: ", name, " must be float32, got ", t.scalar_type());
+}
+void check_contig(const Tensor& t, const char* name) {
+  TORCH_CHECK(t.is_contiguous(), "tam: ", name, " must be contiguous");
+}
+const tam::bf16_t* bp(const Tensor& t) { return reinterpret_cast<const tam::bf16_t*>(t.data_ptr()); }
+tam::bf16_t* bpm(const Tensor& t) { return reinterpret_cast<tam::bf16_t*>(t.data_ptr()); }
+template <class T>
+T* opt_ptr(const optional<Tensor>& t) {
+  return (t.has_value() && t->defined()) ? reinterpret_cast<T*>(t->data_ptr()) : nullptr;
+}
+
+// ------------------------------------------------------------------ GEMM
+// a: (M,K) if a_kmajor else (K,M); b: (N,K) if b_kmajor else (K,N); c: (M,N)
+void gemm_op(const Tensor& a, bool a_kmajor, const Tensor& b, bool b_kmajor, const Tensor& c,
+             int64_t mode, const optional<Tensor>& bias, bool relu, const optional<Tensor>& mask,
+             double alpha, bool allow_split) {
+  check_bf16(a, "a");
+  check_bf16(b, "b");
+  check_dev(c, "c");
+  TORCH_CHECK(a.dim() == 2 && b.dim() == 2 && c.dim() == 2, "tam.gemm: 2-D operands required");
+  TORCH_CHECK(a.stride(1) == 1 && b.stride(1) == 1 && c.stride(1) == 1,
+              "tam.gemm: inner dim must be unit-stride");
+  const int64_t M = a_kmajor ? a.size(0) : a.size(1);
+  const int64_t K = a_kmajor ? a.size(1) : a.size(0);
+  const int64_t N = b_kmajor ? b.size(0) : b.size(1);
+  const int64_t Kb = b_kmajor ? b.size(1) : b.size(0);
+  TORCH_CHECK(K == Kb, "tam.gemm: K mismatch ", K, " vs ", Kb);
+  TORCH_CHECK(c.size(0) == M && c.size(1) == N, "tam.gemm: C shape mismatch");
+  TORCH_CHECK(K % 8 == 0, "tam.gemm: K must be a multiple of 8");
+  TORCH_CHECK(a_kmajor || M % 8 == 0, "tam.gemm: M-major A needs M % 8 == 0");
+  TORCH_CHECK(b_kmajor || N % 8 == 0, "tam.gemm: N-major B needs N % 8 == 0");
+  TORCH_CHECK(a.stride(0) % 8 == 0 && b.stride(0) % 8 == 0, "tam.gemm: 16-byte aligned rows needed");
+  tam::Epi ep;
+  ep.c = c.data_ptr();
+  ep.ldc = c.stride(0);
+  ep.c_f32 = c.scalar_type() == at::kFloat;
+  TORCH_CHECK(ep.c_f32 || c.scalar_type() == at::kBFloat16, "tam.gemm: C must be f32 or bf16");
+  ep.mode = (int)mode;
+  TORCH_CHECK(mode == 0 || mode == 1 || (mode == 2 && ep.c_f32), "tam.gemm: bad mode");
+  if (bias.has_value() && bias->defined()) {
+    check_bf16(*bias, "bias");
+    TORCH_CHECK(bias->numel() == N, "tam.gemm: bias size");
+  }
+  ep.bias = bias.has_value() && bias->defined() ? bp(*bias) : nullptr;
+  ep.relu = relu;
+  if (mask.has_value() && mask->defined()) {
+    check_bf16(*mask, "mask");
+    TORCH_CHECK(mask->dim() == 2 && mask->size(0) == M && mask->size(1) == N && mask->stride(1) == 1,
+                "tam.gemm: mask shape");
+    ep.mask = bp(*mask);
+    ep.ldm = mask->stride(0);
+  }
+  ep.alpha = (float)alpha;
+  tam::gemm(bp(a), a.stride(0), a_kmajor, bp(b), b.stride(0), b_kmajor, (int)M, (int)N, (int)K, ep,
+            allow_split, cur_stream(a));
+}
+
+// ------------------------------------------------------------------ conv
+tam::ConvGeom geom(const Tensor& x, const Tensor& w, const Tensor& y, int64_t stride, int64_t pad,
+                   int64_t dil) {
+  tam::ConvGeom g;
+  g.N = (int)x.size(0); g.H = (int)x.size(1); g.W = (int)x.size(2); g.C = (int)x.size(3);
+  g.K = (int)w.size(0); g.R = (int)w.size(1); g.S = (int)w.size(2);
+  g.P = (int)y.size(1); g.Q = (int)y.size(2);
+  g.stride = (int)stride; g.pad = (int)pad; g.dil = (int)dil;
+  TORCH_CHECK(w.size(3) == g.C, "tam.conv: weight C mismatch");
+  TORCH_CHECK(y.size(0) == g.N && y.size(3) == g.K, "tam.conv: output shape mismatch");
+  TORCH_CHECK(g.P == (g.H + 2 * g.pad - g.dil * (g.R - 1) - 1) / g.stride + 1 &&
+                  g.Q == (g.W + 2 * g.pad - g.dil * (g.S - 1) - 1) / g.stride + 1,
+              "tam.conv: output spatial size inconsistent with geometry");
+  TORCH_CHECK(g.C % 8 == 0 && g.K % 8 == 0, "tam.conv: C and K must be multiples of 8");
+  return g;
+}
+
+void conv_fwd_op(const Tensor& x, const Tensor& w, const Tensor& y, int64_t stride, int64_t pad,
+                 int64_t dil, const optional<Tensor>& bias, bool relu) {
+  check_bf16(x, "x"); check_bf16(w, "w"); check_bf16(y, "y");
+  check_contig(x, "x"); check_contig(w, "w"); check_contig(y, "y");
+  tam::ConvGeom g = geom(x, w, y, stride, pad, dil);
+  tam::Epi ep;
+  ep.c = y.data_ptr(); ep.ldc = g.K; ep.c_f32 = 0; ep.mode = 0;
+  ep.bias = opt_ptr<const tam::bf16_t>(bias);
+  ep.relu = relu;
+  tam::conv_fwd(bp(x), bp(w), g, ep, cur_stream(x));
+}
+
+void conv_dgrad_op(const Tensor& dy, const Tensor& w, const Tensor& wt, const Tensor& dx,
+                   int64_t stride, int64_t pad, int64_t dil, const optional<Tensor>& mask) {
+  check_bf16(dy, "dy"); check_bf16(w, "w"); check_bf16(dx, "dx");
+  check_contig(dy, "dy"); check_contig(w, "w"); check_contig(dx, "dx");
+  tam::ConvGeom g = geom(dx, w, dy, stride, pad, dil);
+  const bool pointwise = g.R == 1 && g.S == 1 && g.stride == 1 && g.pad == 0;
+  if (!pointwise) {
+    check_bf16(wt, "wt");
+    TORCH_CHECK(wt.numel() == w.numel(), "tam.conv_dgrad: wt workspace size");
+    tam::conv_weight_t(bp(w), bpm(wt), g, cur_stream(dy));
+  }
+  tam::Epi ep;
+  ep.c = dx.data_ptr(); ep.ldc = g.C; ep.c_f32 = 0; ep.mode = 0;
+  if (mask.has_value() && mask->defined()) {
+    check_bf16(*mask, "mask");
+    TORCH_CHECK(mask->numel() == dx.numel(), "tam.conv_dgrad: mask size");
+    ep.mask = bp(*mask); ep.ldm = g.C;
+  }
+  tam::conv_dgrad(bp(dy), bp(w), pointwise ? nullptr : bp(wt), g, ep, cur_stream(dy));
+}
+
+void conv_wgrad_op(const Tensor& dy, const Tensor& x, const Tensor& dw, int64_t stride, int64_t pad,
+                   int64_t dil, int64_t mode) {
+  check_bf16(dy, "dy"); check_bf16(x, "x"); check_f32(dw, "dw");
+  check_contig(dy, "dy"); check_contig(x, "x"); check_contig(dw, "dw");
+  TORCH_CHECK(dw.dim() == 4, "tam.conv_wgrad: dw must be [K,R,S,C]");
+  tam::ConvGeom g = geom(x, dw, dy, stride, pad, dil);
+  tam::Epi ep;
+  ep.c = dw.data_ptr(); ep.ldc = g.R * g.S * g.C; ep.c_f32 = 1; ep.mode = (int)mode;
+  tam::conv_wgrad(bp(dy), bp(x), g, ep, cur_stream(dy));
+}
+
+// ------------------------------------------------------------------ norms
+void bn_forward_op(const Tensor& x, const optional<Tensor>& res, const Tensor& y, const Tensor& gamma,
+                   const Tensor& beta, const optional<Tensor>& run_mean,
+                   const optional<Tensor>& run_var, const Tensor& save_mean,
+                   const Tensor& save_rstd, const Tensor& ws_d, const Tensor& ws_f, double eps,
+                   double momentum, bool relu) {
+  check_bf16(x, "x"); check_bf16(y, "y"); check_contig(x, "x"); check_contig(y, "y");
+  check_f32(gamma, "gamma"); check_f32(beta, "beta");
+  const int64_t C = x.size(-1);
+  const int64_t M = x.numel() / C;
+  TORCH_CHECK(C % 8 == 0 && C <= 2048, "tam.bn: C must be a multiple of 8 and <= 2048");
+  TORCH_CHECK(ws_d.scalar_type() == at::kDouble && ws_d.numel() >= 2 * C, "tam.bn: ws_d");
+  TORCH_CHECK(ws_f.numel() >= 2 * C, "tam.bn: ws_f");
+  if (res.has_value() && res->defined()) { check_bf16(*res, "res"); check_contig(*res, "res"); }
+  tam::bn_forward(bp(x), opt_ptr<const tam::bf16_t>(res), bpm(y), M, (int)C, (float)eps,
+                  (float)momentum, gamma.data_ptr<float>(), beta.data_ptr<float>(),
+                  opt_ptr<float>(run_mean), opt_ptr<float>(run_var), save_mean.data_ptr<float>(),
+                  save_rstd.data_ptr<float>(), ws_d.data_ptr<double>(), ws_f.data_ptr<float>(),
+                  relu, cur_stream(x));
+}
+
+void bn_backward_op(const Tensor& dy, const optional<Tensor>& y, const Tensor& x, const Tensor& mean,
+                    const Tensor& rstd, const Tensor& gamma, const Tensor& dx,
+                    const optional<Tensor>& dres, const optional<Tensor>& dgamma,
+                    const optional<Tensor>& dbeta, const Tensor& ws_d, const Tensor& ws_f,
+                    bool relu) {
+  check_bf16(dy, "dy"); check_bf16(x, "x"); check_bf16(dx, "dx");
+  check_contig(dy, "dy"); check_contig(x, "x"); check_contig(dx, "dx");
+  const int64_t C = x.size(-1);
+  const int64_t M = x.numel() / C;
+  TORCH_CHECK(!relu || (y.has_value() && y->defined()), "tam.bn_backward: relu needs y");
+  TORCH_CHECK(ws_d.numel() >= 2 * C && ws_f.numel() >= 3 * C, "tam.bn_backward: workspace");
+  tam::bn_backward(bp(dy), opt_ptr<const tam::bf16_t>(y), bp(x), mean.data_ptr<float>(),
+                   rstd.data_ptr<float>(), gamma.data_ptr<float>(), M, (int)C, relu, bpm(dx),
+                   opt_ptr<tam::bf16_t>(dres), opt_ptr<float>(dgamma), opt_ptr<float>(dbeta),
+                   ws_d.data_ptr<double>(), ws_f.data_ptr<float>(), cur_stream(x));
+}
+
+void ln_forward_op(const Tensor& x, const Tensor& g, const Tensor& b, const Tensor& y,
+                   const Tensor& mean, const Tensor& rstd, double eps) {
+  check_bf16(x, "x"); check_bf16(y, "y"); check_contig(x, "x"); check_contig(y, "y");
+  check_f32(g, "g"); check_f32(b, "b");
+  const int64_t D = x.size(-1);
+  TORCH_CHECK(D % 8 == 0 && D <= 2048, "tam.ln: D must be a multiple of 8 and <= 2048");
+  tam::ln_forward(bp(x), g.data_ptr<float>(), b.data_ptr<float>(), bpm(y), mean.data_ptr<float>(),
+                  rstd.data_ptr<float>(), x.numel() / D, (int)D, (float)eps, cur_stream(x));
+}
+
+void ln_backward_op(const Tensor& dy, const Tensor& x, const Tensor& g, const Tensor& mean,
+                    const Tensor& rstd, const Tensor& dx, const Tensor& dg, const Tensor& db) {
+  check_bf16(dy, "dy"); check_bf16(x, "x"); check_bf16(dx, "dx");
+  check_contig(dy, "dy"); check_contig(x, "x"); check_contig(dx, "dx");
+  check_f32(dg, "dg"); check_f32(db, "db");
+  const int64_t D = x.size(-1);
+  tam::ln_backward(bp(dy), bp(x), g.data_ptr<float>(), mean.data_ptr<float>(),
+                   rstd.data_ptr<float>(), bpm(dx), dg.data_ptr<float>(), db.data_ptr<float>(),
+                   x.numel() / D, (int)D, cur_stream(x));
+}
+
+// ------------------------------------------------------------------ pooling
+void maxpool_forward_op(const Tensor& x, const Tensor& y, const Tensor& idx, int64_t R, int64_t S,
+                        int64_t st, int64_t pad) {
+  check_bf16(x, "x"); check_bf16(y, "y"); check_contig(x, "x"); check_contig(y, "y");
+  TORCH_CHECK(idx.scalar_type() == at::kByte && idx.numel() == y.numel(), "tam.maxpool: idx");
+  tam::maxpool_forward(bp(x), bpm(y), idx.data_ptr<uint8_t>(), (int)x.size(0), (int)x.size(1),
+                       (int)x.size(2), (int)x.size(3), (int)y.size(1), (int)y.size(2), (int)R,
+                       (int)S, (int)st, (int)pad, cur_stream(x));
+}
+void maxpool_backward_op(const Tensor& dy, const Tensor& idx, const Tensor& dx, int64_t R, int64_t S,
+                         int64_t st, int64_t pad) {
+  check_bf16(dy, "dy"); check_bf16(dx, "dx");
+  tam::maxpool_backward(bp(dy), idx.data_ptr<uint8_t>(), bpm(dx), (int)dx.size(0), (int)dx.size(1),
+                        (int)dx.size(2), (int)dx.size(3), (int)dy.size(1), (int)dy.size(2), (int)R,
+                        (int)S, (int)st, (int)pad, cur_stream(dy));
+}
+void avgpool_forward_op(const Tensor& x, const Tensor& y) {
+  check_bf16(x, "x"); check_bf16(y, "y"); check_contig(x, "x");
+  tam::avgpool_forward(bp(x), bpm(y), (int)x.size(0), (int)(x.size(1) * x.size(2)), (int)x.size(3),
+                       cur_stream(x));
+}
+void avgpool_backward_op(const Tensor& dy, const Tensor& dx) {
+  check_bf16(dy, "dy"); check_bf16(dx, "dx"); check_contig(dx, "dx");
+  tam::avgpool_backward(bp(dy), bpm(dx), (int)dx.size(0), (int)(dx.size(1) * dx.size(2)),
+                        (int)dx.size(3), cur_stream(dy));
+}
+
+// ------------------------------------------------------------------ loss / embed / misc
+void softmax_xent_op(const Tensor& logits, const Tensor& labels, const optional<Tensor>& dlogits,
+                     const Tensor& loss_rows, double smoothing, double grad_scale,
+                     int64_t ignore_index) {
+  check_bf16(logits, "logits"); check_contig(logits, "logits");
+  TORCH_CHECK(labels.scalar_type() == at::kLong && labels.is_cuda(), "tam.xent: labels int64 GPU");
+  check_f32(loss_rows, "loss_rows");
+  const int64_t V = logits.size(-1), rows = logits.numel() / V;
+  TORCH_CHECK(labels.numel() == rows && loss_rows.numel() == rows, "tam.xent: row count");
+  tam::softmax_xent(bp(logits), labels.data_ptr<int64_t>(), opt_ptr<tam::bf16_t>(dlogits),
+                    loss_rows.data_ptr<float>(), rows, (int)V, (float)smoothing, (float)grad_scale,
+                    ignore_index, cur_stream(logits));
+}
+
+void embedding_forward_op(const Tensor& table, const Tensor& ids, const Tensor& out, double scale) {
+  check_bf16(table, "table"); check_bf16(out, "out"); check_contig(table, "table");
+  TORCH_CHECK(ids.scalar_type() == at::kLong && ids.is_contiguous(), "tam.embedding: ids");
+  const int64_t D = table.size(1);
+  TORCH_CHECK(D % 8 == 0, "tam.embedding: D % 8");
+  tam::embedding_forward(bp(table), ids.data_ptr<int64_t>(), bpm(out), ids.numel(), (int)D,
+                         (float)scale, cur_stream(table));
+}
+void embedding_backward_op(const Tensor& dout, const Tensor& ids, const Tensor& gtable, double scale) {
+  check_bf16(dout, "dout"); check_f32(gtable, "gtable"); check_contig(dout, "dout");
+  tam::embedding_backward(bp(dout), ids.data_ptr<int64_t>(), gtable.data_ptr<float>(), ids.numel(),
+                          (int)gtable.size(1), (float)scale, cur_stream(dout));
+}
+
+void colsum_op(const Tensor& x, const Tensor& out) {
+  check_bf16(x, "x"); check_f32(out, "out"); check_contig(x, "x");
+  const int64_t C = x.size(-1);
+  tam::colsum(bp(x), out.data_ptr<float>(), x.numel() / C, (int)C, cur_stream(x));
+}
+void relu_backward_op(const Tensor& dy, const Tensor& y, const Tensor& dx) {
+  check_bf16(dy, "dy"); check_bf16(y, "y"); check_bf16(dx, "dx");
+  tam::relu_backward(bp(dy), bp(y), bpm(dx), dy.numel(), cur_stream(dy));
+}
+void add_op(const Tensor& a, const Tensor& b, const Tensor& y) {
+  check_bf16(a, "a"); check_bf16(b, "b"); check_bf16(y, "y");
+  TORCH_CHECK(a.numel() % 8 == 0, "tam.add: numel % 8");
+  tam::add_bf16(bp(a), bp(b), bpm(y), a.numel(), cur_stream(a));
+}
+void cast_op(const Tensor& x, const Tensor& y) {
+  check_f32(x, "x"); check_bf16(y, "y");
+  tam::cast_f32_bf16(x.data_ptr<float>(), bpm(y), x.numel(), cur_stream(x));
+}
+
+// ------------------------------------------------------------------ optimizers
+void sgd_op(const Tensor& w, const Tensor& g, const Tensor& mom, const Tensor& wb, double lr,
+            double momentum, double wd, double gscale, bool nesterov, bool zero_grad) {
+  check_f32(w, "w"); check_f32(g, "g"); check_f32(mom, "mom"); check_bf16(wb, "wb");
+  TORCH_CHECK(w.numel() % 4 == 0 && g.numel() == w.numel() && mom.numel() == w.numel() &&
+                  wb.numel() == w.numel(),
+              "tam.sgd: sizes");
+  tam::sgd_step(w.data_ptr<float>(), g.data_ptr<float>(), mom.data_ptr<float>(), bpm(wb), w.numel(),
+                (float)lr, (float)momentum, (float)wd, (float)gscale, nesterov, zero_grad,
+                cur_stream(w));
+}
+void adam_op(const Tensor& w, const Tensor& g, const Tensor& m, const Tensor& v, const Tensor& wb,
+             double lr, double b1, double b2, double eps, double wd, int64_t step, double gscale,
+             bool zero_grad) {
+  check_f32(w, "w"); check_f32(g, "g"); check_f32(m, "m"); check_f32(v, "v"); check_bf16(wb, "wb");
+  TORCH_CHECK(w.numel() % 4 == 0, "tam.adam: numel % 4");
+  tam::adam_step(w.data_ptr<float>(), g.data_ptr<float>(), m.data_ptr<float>(), v.data_ptr<float>(),
+                 bpm(wb), w.numel(), (float)lr, (float)b1, (float)b2, (float)eps, (float)wd,
+                 (int)step, (float)gscale, zero_grad, cur_stream(w));
+}
+
+// ------------------------------------------------------------------ attention
+// q,k,v,o: [B,S,H,64] views (unit stride on d, stride 64 on heads)
+void check_attn_view(const Tensor& t, const char* name) {
+  check_bf16(t, name);
+  TORCH_CHECK(t.dim() == 4 && t.size(3) == 64 && t.stride(3) == 1 && t.stride(2) == 64,
+              "tam.attn: ", name, " must be a [B,S,H,64] view with packed heads");
+  TORCH_CHECK(t.stride(0) == t.size(1) * t.stride(1), "tam.attn: ", name, " batch stride");
+  TORCH_CHECK(t.stride(1) % 8 == 0, "tam.attn: ", name, " token stride alignment");
+}
+void attn_forward_op(const Tensor& q, const Tensor& k, const Tensor& v, const Tensor& o,
+                     const Tensor& lse, bool causal, double scale, const optional<Tensor>& kv_len) {
+  check_attn_view(q, "q"); check_attn_view(k, "k"); check_attn_view(v, "v"); check_attn_view(o, "o");
+  TORCH_CHECK(k.stride(1) == v.stride(1), "tam.attn: k/v token strides differ");
+  check_f32(lse, "lse");
+  const int B = (int)q.size(0), Sq = (int)q.size(1), H = (int)q.size(2), Sk = (int)k.size(1);
+  TORCH_CHECK(lse.numel() == (int64_t)B * H * Sq, "tam.attn: lse size");
+  tam::attn_forward(bp(q), bp(k), bp(v), bpm(o), lse.data_ptr<float>(), B, H, Sq, Sk, q.stride(1),
+                    k.stride(1), o.stride(1), causal, (float)scale, opt_ptr<const int>(kv_len),
+                    cur_stream(q));
+}
+void attn_backward_op(const Tensor& q, const Tensor& k, const Tensor& v, const Tensor& o,
+                      const Tensor& dout, const Tensor& lse, const Tensor& dq, const Tensor& dk,
+                      const Tensor& dv, const Tensor& dq_acc, const Tensor& delta, bool causal,
+                      double scale, const optional<Tensor>& kv_len) {
+  check_attn_view(q, "q"); check_attn_view(k, "k"); check_attn_view(v, "v"); check_attn_view(o, "o");
+  check_attn_view(dout, "dout"); check_attn_view(dq, "dq"); check_attn_view(dk, "dk");
+  check_attn_view(dv, "dv");
+  TORCH_CHECK(dout.stride(1) == o.stride(1), "tam.attn_bwd: dout must match o layout");
+  TORCH_CHECK(dq.stride(1) == q.stride(1) && dk.stride(1) == k.stride(1) && dv.stride(1) == k.stride(1),
+              "tam.attn_bwd: grads must match input layouts");
+  const int B = (int)q.size(0), Sq = (int)q.size(1), H = (int)q.size(2), Sk = (int)k.size(1);
+  check_f32(dq_acc, "dq_acc"); check_f32(delta, "delta");
+  TORCH_CHECK(dq_acc.numel() >= (int64_t)B * Sq * H * 64 && delta.numel() >= (int64_t)B * H * Sq,
+              "tam.attn_bwd: workspace sizes");
+  tam::attn_backward(bp(q), bp(k), bp(v), bp(o), bp(dout), lse.data_ptr<float>(), bpm(dq), bpm(dk),
+                     bpm(dv), dq_acc.data_ptr<float>(), delta.data_ptr<float>(), B, H, Sq, Sk,
+                     q.stride(1), k.stride(1), o.stride(1), causal, (float)scale,
+                     opt_ptr<const int>(kv_len), cur_stream(q));
+}
+
+// ------------------------------------------------------------------ LSTM
+void lstm_fwd_op(const Tensor& gates, const optional<Tensor>& c_prev, const Tensor& c_out,
+                 const Tensor& h_out, const optional<Tensor>& h_f32, const Tensor& act) {
+  check_f32(gates, "gates"); check_f32(c_out, "c_out"); check_bf16(h_out, "h_out"); check_f32(act, "act");
+  const int B = (int)gates.size(0), Hd = (int)(gates.size(1) / 4);
+  tam::lstm_cell_forward(gates.data_ptr<float>(), opt_ptr<const float>(c_prev), c_out.data_ptr<float>(),
+                         bpm(h_out), opt_ptr<float>(h_f32), act.data_ptr<float>(), B, Hd,
+                         cur_stream(gates));
+}
+void lstm_bwd_op(const Tensor& act, const optional<Tensor>& c_prev, const optional<Tensor>& dh,
+                 const optional<Tensor>& dc_next, const optional<Tensor>& dgates,
+                 const optional<Tensor>& dc_prev, const optional<Tensor>& dgates_bf16) {
+  check_f32(act, "act");
+  const int B = (int)act.size(0), Hd = (int)(act.size(1) / 5);
+  tam::lstm_cell_backward(act.data_ptr<float>(), opt_ptr<const float>(c_prev), nullptr,
+                          opt_ptr<const float>(dh), opt_ptr<const float>(dc_next),
+                          opt_ptr<float>(dgates), opt_ptr<float>(dc_prev),
+                          opt_ptr<tam::bf16_t>(dgates_bf16), B, Hd, c10::hip::getCurrentHIPStream(act.device().index()).stream());
+}
+
+}  // namespace
+
+TORCH_LIBRARY(tam, m) {
+  m.def("gemm(Tensor a, bool a_kmajor, Tensor b, bool b_kmajor, Tensor(a!) c, int mode, Tensor? bias, bool relu, Tensor? mask, float alpha, bool allow_split) -> ()", &gemm_op);
+  m.def("conv_fwd(Tensor x, Tensor w, Tensor(a!) y, int stride, int pad, int dil, Tensor? bias, bool relu) -> ()", &conv_fwd_op);
+  m.def("conv_dgrad(Tensor dy, Tensor w, Tensor(a!) wt, Tensor(b!) dx, int stride, int pad, int dil, Tensor? mask) -> ()", &conv_dgrad_op);
+  m.def("conv_wgrad(Tensor dy, Tensor x, Tensor(a!) dw, int stride, int pad, int dil, int mode) -> ()", &conv_wgrad_op);
+  m.def("bn_forward(Tensor x, Tensor? res, Tensor(a!) y, Tensor gamma, Tensor beta, Tensor(b!)? run_mean, Tensor(c!)? run_var, Tensor(d!) save_mean, Tensor(e!) save_rstd, Tensor(f!) ws_d, Tensor(g!) ws_f, float eps, float momentum, bool relu) -> ()", &bn_forward_op);
+  m.def("bn_backward(Tensor dy, Tensor? y, Tensor x, Tensor mean, Tensor rstd, Tensor gamma, Tensor(a!) dx, Tensor(b!)? dres, Tensor(c!)? dgamma, Tensor(d!)? dbeta, Tensor(e!) ws_d, Tensor(f!) ws_f, bool relu) -> ()", &bn_backward_op);
+  m.def("ln_forward(Tensor x, Tensor g, Tensor b, Tensor(a!) y, Tensor(b!) mean, Tensor(c!) rstd, float eps) -> ()", &ln_forward_op);
+  m.def("ln_backward(Tensor dy, Tensor x, Tensor g, Tensor mean, Tensor rstd, Tensor(a!) dx, Tensor(b!) dg, Tensor(c!) db) -> ()", &ln_backward_op);
+  m.def("maxpool_forward(Tensor x, Tensor(a!) y, Tensor(b!) idx, int R, int S, int stride, int pad) -> ()", &maxpool_forward_op);
+  m.def("maxpool_backward(Tensor dy, Tensor idx, Tensor(a!) dx, int R, int S, int stride, int pad) -> ()", &maxpool_backward_op);
+  m.def("avgpool_forward(Tensor x, Tensor(a!) y) -> ()", &avgpool_forward_op);
+  m.def("avgpool_backward(Tensor dy, Tensor(a!) dx) -> ()", &avgpool_backward_op);
+  m.def("softmax_xent(Tensor logits, Tensor labels, Tensor(a!)? dlogits, Tensor(b!) loss_rows, float smoothing, float grad_scale, int ignore_index) -> ()", &softmax_xent_op);
+  m.def("embedding_forward(Tensor table, Tensor ids, Tensor(a!) out, float scale) -> ()", &embedding_forward_op);
+  m.def("embedding_backward(Tensor dout, Tensor ids, Tensor(a!) gtable, float scale) -> ()", &embedding_backward_op);
+  m.def("colsum(Tensor x, Tensor(a!) out) -> ()", &colsum_op);
+  m.def("relu_backward(Tensor dy, Tensor y, Tensor(a!) dx) -> ()", &relu_backward_op);
+  m.def("add(Tensor a, Tensor b, Tensor(a!) y) -> ()", &add_op);
+  m.def("cast_f32_bf16(Tensor x, Tensor(a!) y) -> ()", &cast_op);
+  m.def("sgd_step(Tensor(a!) w, Tensor(b!) g, Tensor(c!) mom, Tensor(d!) wb, float lr, float momentum, float wd, float gscale, bool nesterov, bool zero_grad) -> ()", &sgd_op);
+  m.def("adam_step(Tensor(a!) w, Tensor(b!) g, Tensor(c!) m, Tensor(d!) v, Tensor(e!) wb, float lr, float b1, float b2, float eps, float wd, int step, float gscale, bool zero_grad) -> ()", &adam_op);
+  m.def("attn_forward(Tensor q, Tensor k, Tensor v, Tensor(a!) o, Tensor(b!) lse, bool causal, float scale, Tensor? kv_len) -> ()", &attn_forward_op);
+  m.def("attn_backward(Tensor q, Tensor k, Tensor v, Tensor o, Tensor dout, Tensor lse, Tensor(a!) dq, Tensor(b!) dk, Tensor(c!) dv, Tensor(d!) dq_acc, Tensor(e!) delta, bool causal, float scale, Tensor? kv_len) -> ()", &attn_backward_op);
+  m.def("lstm_cell_forward(Tensor gates, Tensor? c_prev, Tensor(a!) c_out, Tensor(b!) h_out, Tensor(c!)? h_f32, Tensor(d!) act) -> ()", &lstm_fwd_op);
+  m.def("lstm_cell_backward(Tensor act, Tensor? c_prev, Tensor? dh, Tensor? dc_next, Tensor(a!)? dgates, Tensor(b!)? dc_prev, Tensor(c!)? dgates_bf16) -> ()", &lstm_bwd_op);
+}

@@ -1,0 +1,235 @@
+// tiresias_amd — checkpoint spill/restore engine for preempted jobs.
+//
+// A preempted job's state (flat fp32 master params + optimizer state) stays
+// resident in HBM while memory allows ("suspend in place": resume is a
+// pointer swap). When the scheduler needs the HBM, the state is spilled to a
+// pinned host pool with hipMemcpyAsync on a dedicated LOW-priority side
+// stream, ordered after the producer stream by an event, so the spill
+// overlaps the next job's compute. Restore is the reverse (H2D on the side
+// stream; the consumer stream waits on an event, never the host).
+//
+// The pinned pool is carved from large hipHostMalloc'd chunks with a
+// first-fit free list (coalescing on free) so spills never call the
+// (synchronising, expensive) pinned allocator on the hot path.
+#include <ATen/ATen.h>
+#include <c10/hip/HIPStream.h>
+#include <torch/custom_class.h>
+#include <torch/library.h>
+
+#include <chrono>
+#include <map>
+#include <mutex>
+#include <vector>
+
+#include "tam/common.h"
+
+namespace {
+
+struct Block { size_t off, size; };
+
+class PinnedPool {
+ public:
+  explicit PinnedPool(size_t chunk) : chunk_(chunk) {}
+  ~PinnedPool() {
+    for (auto& c : chunks_) (void)hipHostFree(c.base);
+  }
+  // returns host pointer; grows by whole chunks (>= request)
+  char* alloc(size_t n) {
+    n = (n + 255) & ~size_t(255);
+    for (auto& c : chunks_) {
+      for (size_t i = 0; i < c.free.size(); ++i) {
+        if (c.free[i].size >= n) {
+          char* p = c.base + c.free[i].off;
+          c.free[i].off += n;
+          c.free[i].size -= n;
+          if (c.free[i].size == 0) c.free.erase(c.free.begin() + i);
+          used_ += n;
+          return p;
+        }
+      }
+    }
+    const size_t sz = n > chunk_ ? n : chunk_;
+    Chunk c;
+    TAM_HIP_CHECK(hipHostMalloc((void**)&c.base, sz, hipHostMallocDefault));
+    c.size = sz;
+    c.free.push_back({n, sz - n});
+    if (c.free.back().size == 0) c.free.pop_back();
+    chunks_.push_back(std::move(c));
+    reserved_ += sz;
+    used_ += n;
+    return chunks_.back().base;
+  }
+  void free(char* p, size_t n) {
+    n = (n + 255) & ~size_t(255);
+    for (auto& c : chunks_) {
+      if (p >= c.base && p < c.base + c.size) {
+        Block b{(size_t)(p - c.base), n};
+        auto it = c.free.begin();
+        while (it != c.free.end() && it->off < b.off) ++it;
+        it = c.free.insert(it, b);
+        // coalesce with next
+        if (it + 1 != c.free.end() && it->off + it->size == (it + 1)->off) {
+          it->size += (it + 1)->size;
+          c.free.erase(it + 1);
+        }
+        // coalesce with prev
+        if (it != c.free.begin() && (it - 1)->off + (it - 1)->size == it->off) {
+          (it - 1)->size += it->size;
+          c.free.erase(it);
+        }
+        used_ -= n;
+        return;
+      }
+    }
+    TORCH_CHECK(false, "PinnedPool: pointer not owned by pool");
+  }
+  size_t reserved() const { return reserved_; }
+  size_t used() const { return used_; }
+
+ private:
+  struct Chunk { char* base = nullptr; size_t size = 0; std::vector<Block> free; };
+  size_t chunk_;
+  std::vector<Chunk> chunks_;
+  size_t reserved_ = 0, used_ = 0;
+};
+
+struct Spill {
+  char* host = nullptr;
+  size_t bytes = 0;
+  hipEvent_t done = nullptr;
+  std::vector<int64_t> shape;
+  at::ScalarType dtype;
+};
+
+class CkptEngine : public torch::CustomClassHolder {
+ public:
+  CkptEngine(int64_t device, int64_t chunk_bytes) : device_((int)device), pool_((size_t)chunk_bytes) {
+    TAM_HIP_CHECK(hipSetDevice(device_));
+    int lo = 0, hi = 0;
+    TAM_HIP_CHECK(hipDeviceGetStreamPriorityRange(&lo, &hi));
+    // numerically larger value = lower priority on HIP
+    TAM_HIP_CHECK(hipStreamCreateWithPriority(&side_, hipStreamNonBlocking, lo));
+  }
+  ~CkptEngine() override {
+    for (auto& kv : spills_) {
+      if (kv.second.done) (void)hipEventDestroy(kv.second.done);
+    }
+    (void)hipStreamDestroy(side_);
+  }
+
+  // Asynchronously copy `src` (GPU) to pinned host memory. Ordered after all
+  // work already queued on the caller's current stream.
+  int64_t spill(const at::Tensor& src) {
+    TORCH_CHECK(src.is_cuda() && src.is_contiguous(), "ckpt.spill: contiguous GPU tensor required");
+    std::lock_guard<std::mutex> g(mu_);
+    Spill s;
+    s.bytes = src.numel() * src.element_size();
+    s.host = pool_.alloc(s.bytes);
+    s.shape = src.sizes().vec();
+    s.dtype = src.scalar_type();
+    hipStream_t prod = c10::hip::getCurrentHIPStream(src.device().index()).stream();
+    hipEvent_t ready;
+    TAM_HIP_CHECK(hipEventCreateWithFlags(&ready, hipEventDisableTiming));
+    TAM_HIP_CHECK(hipEventRecord(ready, prod));
+    TAM_HIP_CHECK(hipStreamWaitEvent(side_, ready, 0));
+    TAM_HIP_CHECK(hipMemcpyAsync(s.host, src.data_ptr(), s.bytes, hipMemcpyDeviceToHost, side_));
+    TAM_HIP_CHECK(hipEventCreateWithFlags(&s.done, hipEventDisableTiming));
+    TAM_HIP_CHECK(hipEventRecord(s.done, side_));
+    TAM_HIP_CHECK(hipEventDestroy(ready));
+    const int64_t h = next_++;
+    spills_[h] = s;
+    bytes_d2h_ += s.bytes;
+    return h;
+  }
+
+  // Restore a spill into `dst` (GPU, same byte size). The caller's current
+  // stream waits (device-side) for the copy; the host never blocks.
+  void restore(int64_t h, const at::Tensor& dst) {
+    std::lock_guard<std::mutex> g(mu_);
+    auto it = spills_.find(h);
+    TORCH_CHECK(it != spills_.end(), "ckpt.restore: unknown handle ", h);
+    Spill& s = it->second;
+    TORCH_CHECK(dst.is_cuda() && dst.is_contiguous() &&
+                    (size_t)(dst.numel() * dst.element_size()) == s.bytes,
+                "ckpt.restore: destination size mismatch");
+    hipStream_t cons = c10::hip::getCurrentHIPStream(dst.device().index()).stream();
+    // the destination may still be in use by earlier work on the consumer stream
+    hipEvent_t free_ev;
+    TAM_HIP_CHECK(hipEventCreateWithFlags(&free_ev, hipEventDisableTiming));
+    TAM_HIP_CHECK(hipEventRecord(free_ev, cons));
+    TAM_HIP_CHECK(hipStreamWaitEvent(side_, free_ev, 0));
+    TAM_HIP_CHECK(hipStreamWaitEvent(side_, s.done, 0));
+    TAM_HIP_CHECK(hipMemcpyAsync(dst.data_ptr(), s.host, s.bytes, hipMemcpyHostToDevice, side_));
+    TAM_HIP_CHECK(hipEventRecord(s.done, side_));
+    TAM_HIP_CHECK(hipStreamWaitEvent(cons, s.done, 0));
+    TAM_HIP_CHECK(hipEventDestroy(free_ev));
+    bytes_h2d_ += s.bytes;
+  }
+
+  bool ready(int64_t h) {
+    std::lock_guard<std::mutex> g(mu_);
+    auto it = spills_.find(h);
+    TORCH_CHECK(it != spills_.end(), "ckpt.ready: unknown handle");
+    return hipEventQuery(it->second.done) == hipSuccess;
+  }
+
+  void wait(int64_t h) {
+    hipEvent_t e;
+    {
+      std::lock_guard<std::mutex> g(mu_);
+      auto it = spills_.find(h);
+      TORCH_CHECK(it != spills_.end(), "ckpt.wait: unknown handle");
+      e = it->second.done;
+    }
+    TAM_HIP_CHECK(hipEventSynchronize(e));
+  }
+
+  // Free the host copy (after restore completes or when the job finished).
+  void release(int64_t h) {
+    std::lock_guard<std::mutex> g(mu_);
+    auto it = spills_.find(h);
+    if (it == spills_.end()) return;
+    TAM_HIP_CHECK(hipEventSynchronize(it->second.done));
+    TAM_HIP_CHECK(hipEventDestroy(it->second.done));
+    pool_.free(it->second.host, it->second.bytes);
+    spills_.erase(it);
+  }
+
+  // Host-side view of a spill (for tests / persisting to disk): a CPU tensor
+  // aliasing the pinned buffer. Waits for the D2H to complete.
+  at::Tensor host_view(int64_t h) {
+    wait(h);
+    std::lock_guard<std::mutex> g(mu_);
+    Spill& s = spills_.at(h);
+    return at::from_blob(s.host, s.shape, at::TensorOptions().dtype(s.dtype).device(at::kCPU));
+  }
+
+  std::vector<int64_t> stats() {
+    std::lock_guard<std::mutex> g(mu_);
+    return {(int64_t)pool_.reserved(), (int64_t)pool_.used(), (int64_t)bytes_d2h_,
+            (int64_t)bytes_h2d_, (int64_t)spills_.size()};
+  }
+
+ private:
+  int device_;
+  hipStream_t side_ = nullptr;
+  PinnedPool pool_;
+  std::map<int64_t, Spill> spills_;
+  int64_t next_ = 1;
+  size_t bytes_d2h_ = 0, bytes_h2d_ = 0;
+  std::mutex mu_;
+};
+
+}  // namespace
+
+TORCH_LIBRARY_FRAGMENT(tam, m) {
+  m.class_<CkptEngine>("CkptEngine")
+      .def(torch::init<int64_t, int64_t>())
+      .def("spill", &CkptEngine::spill)
+      .def("restore", &CkptEngine::restore)
+      .def("ready", &CkptEngine::ready)
+      .def("wait", &CkptEngine::wait)
+      .def("release", &CkptEngine::release)
+      .def("host_view", &CkptEngine::host_view)
+      .def("stats", &CkptEngine::stats);
+}

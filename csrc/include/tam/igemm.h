@@ -1,0 +1,381 @@
+// tiresias_amd — generic MFMA implicit-GEMM core for gfx950.
+//
+//   C[M,N] (+)= alpha * sum_k A(m,k) * B(k,n)        bf16 in, fp32 accumulate
+//
+// One template serves plain GEMM (all four operand majorities) and the three
+// NHWC convolution passes (fwd / dgrad / wgrad): only the operand *loaders*
+// differ. Design (CDNA4-first, see cdna_hip_programming.md §5):
+//   * 256 threads = 4 waves in a 2x2 grid; each wave owns a (BM/2)x(BN/2)
+//     sub-tile built from v_mfma_f32_16x16x32_bf16 (16x16 outputs, K=32).
+//   * BK = 64; A and B tiles are register-staged (16-byte global loads issued
+//     *before* the MFMA phase of the current tile, written to the other LDS
+//     buffer *after* it: async-STAGE split, guide T14) into a 2-deep LDS ring,
+//     one barrier per K-tile.
+//   * K-major operands live in LDS as [rows][64] bf16 with the 16-B chunk
+//     XOR-swizzled by (row>>1)&7 -> ds_read_b128 fragment reads conflict-free
+//     for the gfx950 ds_read_b128 lane groups (checked exhaustively offline).
+//   * MN-major operands (the transposed operand of dgrad/wgrad GEMMs) live in
+//     LDS as [64][cols] and are read with ds_read_b64_tr_b16 (hardware
+//     transpose, guide T10), 8-B chunk XOR-swizzled per row so both the 16-B
+//     register-staged writes and the transposed reads are conflict-free.
+//   * Workgroup ids are XCD-remapped (bijective, T1) and then grouped along M
+//     so consecutive tiles on one XCD share A panels in that XCD's L2.
+//   * Split-K over blockIdx.z with fp32 atomics for reduction-heavy shapes
+//     (conv wgrad, Linear dW).
+#pragma once
+#include "tam/common.h"
+
+namespace tam {
+
+constexpr int IG_BK = 64;
+constexpr int IG_THREADS = 256;
+
+struct Epi {
+  void* c = nullptr;        // output base
+  long ldc = 0;             // output row stride (elements)
+  int c_f32 = 0;            // 1: fp32 output, 0: bf16 output
+  int mode = 0;             // 0: store, 1: accumulate (C += .), 2: fp32 atomic add
+  const bf16_t* bias = nullptr;  // per-column bias (bf16), added once
+  int relu = 0;             // apply max(.,0) after bias
+  const bf16_t* mask = nullptr;  // relu-backward mask: zero where mask<=0
+  long ldm = 0;
+  float alpha = 1.f;
+};
+
+// ---------------------------------------------------------------------------
+// LDS image addressing
+// ---------------------------------------------------------------------------
+// K-major tile image: [rows][64] bf16, 128-B rows, 16-B chunk c of row r at
+// chunk (c ^ ((r>>1)&7)).
+__device__ __forceinline__ int kmaj_off(int r, int c16) {
+  return r * 128 + ((c16 ^ ((r >> 1) & 7)) << 4);
+}
+// MN-major tile image: [64][COLS] bf16. 8-B chunk index XOR-ed with a per-row
+// value (multiple of 4 so 16-B pairs stay contiguous).
+template <int COLS>
+__device__ __forceinline__ int mnmaj_swz(int r) {
+  if constexpr (COLS == 128) return 4 * ((r & 3) | (((r >> 3) & 1) << 2));
+  else return (4 * ((r >> 1) & 1)) ^ (8 * ((r >> 3) & 1));   // COLS == 64
+}
+template <int COLS>
+__device__ __forceinline__ int mnmaj_off(int r, int c8) {
+  return r * (COLS * 2) + ((c8 ^ mnmaj_swz<COLS>(r)) << 3);
+}
+
+typedef __attribute__((address_space(3))) s16x4_t lds_s16x4;
+
+template <int COLS>
+__device__ __forceinline__ s16x8_t read_frag_mn(const char* tile, int lane, int kbase, int colbase) {
+  // lane (g = lane>>4, t = lane&15, q = t>>2, p = t&3) supplies row
+  // kbase + 8g + 4h + q, columns colbase + 4p..4p+3; receives column
+  // colbase + t, k = kbase + 8g + 4h + q  (q = element index)
+  const int g = lane >> 4, t = lane & 15, q = t >> 2, p = t & 3;
+  const int c8 = (colbase >> 2) + p;
+  const int r0 = kbase + 8 * g + q;
+  s16x4_t lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+      (lds_s16x4*)(tile + mnmaj_off<COLS>(r0, c8)));
+  s16x4_t hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+      (lds_s16x4*)(tile + mnmaj_off<COLS>(r0 + 4, c8)));
+  s16x8_t r;
+  r[0] = lo[0]; r[1] = lo[1]; r[2] = lo[2]; r[3] = lo[3];
+  r[4] = hi[0]; r[5] = hi[1]; r[6] = hi[2]; r[7] = hi[3];
+  return r;
+}
+
+__device__ __forceinline__ s16x8_t read_frag_k(const char* tile, int lane, int rowbase, int kk) {
+  const int r = rowbase + (lane & 15);
+  const int c = 4 * kk + (lane >> 4);
+  return *(const s16x8_t*)(tile + kmaj_off(r, c));
+}
+
+__device__ __forceinline__ uint4 ld16(const bf16_t* p) { return *(const uint4*)p; }
+
+// ---------------------------------------------------------------------------
+// Loaders. Each exposes:
+//   static constexpr bool kKMajor;
+//   init(int tile0, int tid)  -- per-thread precompute for this block's tile
+//   uint4 load(int pass, int kglob)
+// K-major, ROWS-row tile: thread t, pass p -> row (t>>3)+32p, k = kglob
+//   (kglob = k0 + 8*(t&7) is computed by the kernel).
+// MN-major, COLS-col tile: thread t, pass p -> k-row kglob (= k0 + t/CPR +
+//   p*256/CPR computed by the kernel), column chunk (t%CPR)*8.
+// ---------------------------------------------------------------------------
+
+// Dense K-major: elem(row, k) = p[row*ld + k]
+template <int ROWS>
+struct LdKMajor {
+  static constexpr bool kKMajor = true;
+  static constexpr int P = ROWS / 32;
+  const bf16_t* p; long ld; int rows; int K;
+  const bf16_t* rp[P]; bool rv[P];
+  __device__ void init(int row0, int tid) {
+#pragma unroll
+    for (int i = 0; i < P; ++i) {
+      int r = row0 + (tid >> 3) + 32 * i;
+      rv[i] = r < rows;
+      rp[i] = p + (long)(rv[i] ? r : 0) * ld;
+    }
+  }
+  __device__ uint4 load(int i, int k) const {
+    if (rv[i] && k < K) return ld16(rp[i] + k);
+    return make_uint4(0, 0, 0, 0);
+  }
+};
+
+// Dense MN-major: elem(k, col) = p[k*ld + col]
+template <int COLS>
+struct LdMNMajor {
+  static constexpr bool kKMajor = false;
+  const bf16_t* p; long ld; int cols; int K;
+  int col; bool cv;
+  __device__ void init(int col0, int tid) {
+    col = col0 + (tid % (COLS / 8)) * 8;
+    cv = col < cols;
+  }
+  __device__ uint4 load(int, int k) const {
+    if (cv && k < K) return ld16(p + (long)k * ld + col);
+    return make_uint4(0, 0, 0, 0);
+  }
+};
+
+struct ConvGeom {
+  int N, H, W, C;      // input NHWC
+  int K, R, S;         // filters [K][R][S][C]
+  int P, Q;            // output spatial
+  int stride, pad, dil;
+};
+
+// conv fwd A operand: rows = output pixels (n,p,q), k = (r,s,c) c fastest.
+// K-major gather from X (requires C % 8 == 0).
+template <int ROWS>
+struct LdConvFwdA {
+  static constexpr bool kKMajor = true;
+  static constexpr int P_ = ROWS / 32;
+  const bf16_t* x; ConvGeom g; int M; int Kdim;
+  int nb[P_], h0[P_], w0[P_];
+  __device__ void init(int row0, int tid) {
+#pragma unroll
+    for (int i = 0; i < P_; ++i) {
+      int m = row0 + (tid >> 3) + 32 * i;
+      if (m < M) {
+        int q = m % g.Q; int t = m / g.Q; int pp = t % g.P; int n = t / g.P;
+        nb[i] = n; h0[i] = pp * g.stride - g.pad; w0[i] = q * g.stride - g.pad;
+      } else {
+        nb[i] = -1; h0[i] = 0; w0[i] = 0;
+      }
+    }
+  }
+  __device__ uint4 load(int i, int k) const {
+    if (nb[i] < 0 || k >= Kdim) return make_uint4(0, 0, 0, 0);
+    int c = k % g.C; int rs = k / g.C; int s = rs % g.S; int r = rs / g.S;
+    int h = h0[i] + r * g.dil, w = w0[i] + s * g.dil;
+    if ((unsigned)h >= (unsigned)g.H || (unsigned)w >= (unsigned)g.W) return make_uint4(0, 0, 0, 0);
+    return ld16(x + (((long)nb[i] * g.H + h) * g.W + w) * g.C + c);
+  }
+};
+
+// conv dgrad A operand: rows = input pixels (n,h,w), k = (r,s,ko) ko fastest.
+// dX(n,h,w,c) = sum dY(n,p,q,ko) W(ko,r,s,c) over (h+pad-r*dil) = p*stride.
+// K-major gather from dY (requires K % 8 == 0).
+template <int ROWS>
+struct LdConvDgradA {
+  static constexpr bool kKMajor = true;
+  static constexpr int P_ = ROWS / 32;
+  const bf16_t* dy; ConvGeom g; int M; int Kdim;
+  int nb[P_], hh[P_], ww[P_];
+  __device__ void init(int row0, int tid) {
+#pragma unroll
+    for (int i = 0; i < P_; ++i) {
+      int m = row0 + (tid >> 3) + 32 * i;
+      if (m < M) {
+        int w = m % g.W; int t = m / g.W; int h = t % g.H; int n = t / g.H;
+        nb[i] = n; hh[i] = h + g.pad; ww[i] = w + g.pad;
+      } else {
+        nb[i] = -1; hh[i] = 0; ww[i] = 0;
+      }
+    }
+  }
+  __device__ uint4 load(int i, int k) const {
+    if (nb[i] < 0 || k >= Kdim) return make_uint4(0, 0, 0, 0);
+    int ko = k % g.K; int rs = k / g.K; int s = rs % g.S; int r = rs / g.S;
+    int pn = hh[i] - r * g.dil, qn = ww[i] - s * g.dil;
+    if (pn < 0 || qn < 0) return make_uint4(0, 0, 0, 0);
+    int pp = pn / g.stride, qq = qn / g.stride;
+    if (pp * g.stride != pn || qq * g.stride != qn || pp >= g.P || qq >= g.Q)
+      return make_uint4(0, 0, 0, 0);
+    return ld16(dy + (((long)nb[i] * g.P + pp) * g.Q + qq) * g.K + ko);
+  }
+};
+
+// conv wgrad B operand: k-rows = output pixels m=(n,p,q) (reduction), cols =
+// (r,s,c) c fastest. MN-major gather from X (requires C % 8 == 0).
+template <int COLS>
+struct LdConvWgradB {
+  static constexpr bool kKMajor = false;
+  const bf16_t* x; ConvGeom g; int Mred; int Ncols;
+  int cr, cs, cc; bool cv;
+  __device__ void init(int col0, int tid) {
+    int col = col0 + (tid % (COLS / 8)) * 8;
+    cv = col < Ncols;
+    int c = col % g.C; int rs = col / g.C;
+    cc = c; cs = rs % g.S; cr = rs / g.S;
+  }
+  __device__ uint4 load(int, int m) const {
+    if (!cv || m >= Mred) return make_uint4(0, 0, 0, 0);
+    int q = m % g.Q; int t = m / g.Q; int pp = t % g.P; int n = t / g.P;
+    int h = pp * g.stride - g.pad + cr * g.dil, w = q * g.stride - g.pad + cs * g.dil;
+    if ((unsigned)h >= (unsigned)g.H || (unsigned)w >= (unsigned)g.W) return make_uint4(0, 0, 0, 0);
+    return ld16(x + (((long)n * g.H + h) * g.W + w) * g.C + cc);
+  }
+};
+
+// ---------------------------------------------------------------------------
+// The kernel
+// ---------------------------------------------------------------------------
+template <class L, int EXT>
+struct Stager {
+  // EXT = tile extent along the operand's M (or N) dimension
+  static constexpr int P = EXT / 32;   // 16-B loads per thread per K-tile
+  __device__ static void fetch(const L& l, uint4 (&r)[P], int k0, int tid) {
+    if constexpr (L::kKMajor) {
+      const int k = k0 + 8 * (tid & 7);
+#pragma unroll
+      for (int i = 0; i < P; ++i) r[i] = l.load(i, k);
+    } else {
+      constexpr int CPR = EXT / 8, RPP = IG_THREADS / CPR;
+#pragma unroll
+      for (int i = 0; i < P; ++i) r[i] = l.load(i, k0 + tid / CPR + i * RPP);
+    }
+  }
+  __device__ static void store(char* tile, const uint4 (&r)[P], int tid) {
+    if constexpr (L::kKMajor) {
+#pragma unroll
+      for (int i = 0; i < P; ++i) {
+        const int row = (tid >> 3) + 32 * i, c = tid & 7;
+        *(uint4*)(tile + kmaj_off(row, c)) = r[i];
+      }
+    } else {
+      constexpr int CPR = EXT / 8, RPP = IG_THREADS / CPR;
+#pragma unroll
+      for (int i = 0; i < P; ++i) {
+        const int row = tid / CPR + i * RPP, c16 = tid % CPR;
+        *(uint4*)(tile + mnmaj_off<EXT>(row, 2 * c16)) = r[i];
+      }
+    }
+  }
+  __device__ static s16x8_t frag(const char* tile, int lane, int base, int kk) {
+    if constexpr (L::kKMajor) return read_frag_k(tile, lane, base, kk);
+    else return read_frag_mn<EXT>(tile, lane, 32 * kk, base);
+  }
+};
+
+template <int BM, int BN, class LA, class LB>
+__global__ void __launch_bounds__(IG_THREADS, 2)
+igemm_kernel(LA la, LB lb, int M, int N, int K, int ktiles_per_split, Epi ep) {
+  constexpr int BK = IG_BK;
+  constexpr int A_BYTES = BM * BK * 2, B_BYTES = BN * BK * 2;
+  constexpr int TM = BM / 32, TN = BN / 32;   // 16x16 MFMA tiles per wave
+  __shared__ __attribute__((aligned(16))) char smem[2 * (A_BYTES + B_BYTES)];
+
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int wr = wid >> 1, wc = wid & 1;
+  const int tiles_m = (M + BM - 1) / BM, tiles_n = (N + BN - 1) / BN;
+  const int nwg = gridDim.x;
+  const int bid = xcd_remap(blockIdx.x, nwg);
+  constexpr int GROUP = 8;
+  const int per_group = GROUP * tiles_n;
+  const int grp = bid / per_group;
+  const int first_m = grp * GROUP;
+  const int gsize = min(tiles_m - first_m, GROUP);
+  const int tm = first_m + (bid % per_group) % gsize;
+  const int tn = (bid % per_group) / gsize;
+  const int m0 = tm * BM, n0 = tn * BN;
+
+  const int ktiles = (K + BK - 1) / BK;
+  const int kt0 = blockIdx.z * ktiles_per_split;
+  const int kt1 = min(ktiles, kt0 + ktiles_per_split);
+
+  la.init(m0, tid);
+  lb.init(n0, tid);
+
+  using SA = Stager<LA, BM>;
+  using SB = Stager<LB, BN>;
+  uint4 ra[SA::P], rb[SB::P];
+
+  f32x4_t acc[TM][TN];
+#pragma unroll
+  for (int i = 0; i < TM; ++i)
+#pragma unroll
+    for (int j = 0; j < TN; ++j) acc[i][j] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+
+  if (kt0 < kt1) {
+    SA::fetch(la, ra, kt0 * BK, tid);
+    SB::fetch(lb, rb, kt0 * BK, tid);
+    SA::store(smem, ra, tid);
+    SB::store(smem + 2 * A_BYTES, rb, tid);
+    __syncthreads();
+    for (int kt = kt0; kt < kt1; ++kt) {
+      const int cur = (kt - kt0) & 1;
+      const bool more = kt + 1 < kt1;
+      if (more) {
+        SA::fetch(la, ra, (kt + 1) * BK, tid);
+        SB::fetch(lb, rb, (kt + 1) * BK, tid);
+      }
+      const char* ta = smem + cur * A_BYTES;
+      const char* tb = smem + 2 * A_BYTES + cur * B_BYTES;
+#pragma unroll
+      for (int kk = 0; kk < BK / 32; ++kk) {
+        s16x8_t fa[TM], fb[TN];
+#pragma unroll
+        for (int i = 0; i < TM; ++i) fa[i] = SA::frag(ta, lane, wr * (BM / 2) + 16 * i, kk);
+#pragma unroll
+        for (int j = 0; j < TN; ++j) fb[j] = SB::frag(tb, lane, wc * (BN / 2) + 16 * j, kk);
+#pragma unroll
+        for (int i = 0; i < TM; ++i)
+#pragma unroll
+          for (int j = 0; j < TN; ++j)
+            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(
+                __builtin_bit_cast(bf16x8_t, fa[i]), __builtin_bit_cast(bf16x8_t, fb[j]),
+                acc[i][j], 0, 0, 0);
+      }
+      if (more) {
+        SA::store(smem + (cur ^ 1) * A_BYTES, ra, tid);
+        SB::store(smem + 2 * A_BYTES + (cur ^ 1) * B_BYTES, rb, tid);
+      }
+      __syncthreads();
+    }
+  }
+
+  // ---- epilogue: C/D map of 16x16x32: col = lane&15, row = (lane>>4)*4 + r
+  const bool add_bias = ep.bias != nullptr && blockIdx.z == 0;
+#pragma unroll
+  for (int j = 0; j < TN; ++j) {
+    const int col = n0 + wc * (BN / 2) + 16 * j + (lane & 15);
+    if (col >= N) continue;
+    const float bv = add_bias ? bf2f(ep.bias[col]) : 0.f;
+#pragma unroll
+    for (int i = 0; i < TM; ++i) {
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int row = m0 + wr * (BM / 2) + 16 * i + 4 * (lane >> 4) + r;
+        if (row >= M) continue;
+        float v = acc[i][j][r] * ep.alpha + bv;
+        if (ep.relu) v = fmaxf(v, 0.f);
+        if (ep.mask && bf2f(ep.mask[(long)row * ep.ldm + col]) <= 0.f) v = 0.f;
+        const long off = (long)row * ep.ldc + col;
+        if (ep.c_f32) {
+          float* c = (float*)ep.c;
+          if (ep.mode == 2) atomicAdd(c + off, v);
+          else if (ep.mode == 1) c[off] += v;
+          else c[off] = v;
+        } else {
+          bf16_t* c = (bf16_t*)ep.c;
+          if (ep.mode == 1) v += bf2f(c[off]);
+          c[off] = f2bf(v);
+        }
+      }
+    }
+  }
+}
+
+}  // namespace tam

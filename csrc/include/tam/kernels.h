@@ -1,0 +1,77 @@
+// tiresias_amd — host launch API for the non-GEMM kernels.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+#include "tam/common.h"
+
+namespace tam {
+
+// BatchNorm (NHWC rows=M=N*H*W, C channels, C % 8 == 0, C <= 2048)
+void bn_forward(const bf16_t* x, const bf16_t* res, bf16_t* y, long M, int C, float eps,
+                float momentum, const float* gamma, const float* beta, float* run_mean,
+                float* run_var, float* save_mean, float* save_rstd, double* ws, float* ws_f,
+                int relu, hipStream_t s);
+void bn_infer(const bf16_t* x, const bf16_t* res, bf16_t* y, long M, int C, const float* scale,
+              const float* shift, int relu, hipStream_t s);
+void bn_backward(const bf16_t* dy, const bf16_t* y, const bf16_t* x, const float* mean,
+                 const float* rstd, const float* gamma, long M, int C, int relu, bf16_t* dx,
+                 bf16_t* dres, float* dgamma, float* dbeta, double* ws, float* ws_f,
+                 hipStream_t s);
+
+// LayerNorm over last dim D (D % 8 == 0, D <= 2048)
+void ln_forward(const bf16_t* x, const float* g, const float* b, bf16_t* y, float* mean,
+                float* rstd, long rows, int D, float eps, hipStream_t s);
+void ln_backward(const bf16_t* dy, const bf16_t* x, const float* g, const float* mean,
+                 const float* rstd, bf16_t* dx, float* dg, float* db, long rows, int D,
+                 hipStream_t s);
+
+// pooling
+void maxpool_forward(const bf16_t* x, bf16_t* y, uint8_t* idx, int N, int H, int W, int C, int P,
+                     int Q, int R, int S, int st, int pad, hipStream_t s);
+void maxpool_backward(const bf16_t* dy, const uint8_t* idx, bf16_t* dx, int N, int H, int W, int C,
+                      int P, int Q, int R, int S, int st, int pad, hipStream_t s);
+void avgpool_forward(const bf16_t* x, bf16_t* y, int N, int HW, int C, hipStream_t s);
+void avgpool_backward(const bf16_t* dy, bf16_t* dx, int N, int HW, int C, hipStream_t s);
+
+// fused softmax cross-entropy (forward + backward)
+void softmax_xent(const bf16_t* logits, const long* labels, bf16_t* dlogits, float* loss_rows,
+                  long rows, int V, float smoothing, float grad_scale, long ignore_index,
+                  hipStream_t s);
+
+// embedding
+void embedding_forward(const bf16_t* table, const long* ids, bf16_t* out, long T, int D,
+                       float scale, hipStream_t s);
+void embedding_backward(const bf16_t* dout, const long* ids, float* gtable, long T, int D,
+                        float scale, hipStream_t s);
+
+// misc
+void colsum(const bf16_t* x, float* out, long R, int C, hipStream_t s);
+void relu_backward(const bf16_t* dy, const bf16_t* y, bf16_t* dx, long n, hipStream_t s);
+void add_bf16(const bf16_t* a, const bf16_t* b, bf16_t* y, long n, hipStream_t s);
+void cast_f32_bf16(const float* x, bf16_t* y, long n, hipStream_t s);
+
+// optimizers over flat arenas (n % 4 == 0)
+void sgd_step(float* w, float* g, float* mom, bf16_t* wb, long n, float lr, float momentum,
+              float wd, float gscale, int nesterov, int zero_grad, hipStream_t s);
+void adam_step(float* w, float* g, float* m, float* v, bf16_t* wb, long n, float lr, float b1,
+               float b2, float eps, float wd, int step, float gscale, int zero_grad,
+               hipStream_t s);
+
+// fused attention (bf16, head_dim 64), layout [B][S][H][64] (token-major)
+void attn_forward(const bf16_t* q, const bf16_t* k, const bf16_t* v, bf16_t* o, float* lse, int B,
+                  int H, int Sq, int Sk, long q_stride, long kv_stride, long o_stride, int causal,
+                  float scale, const int* kv_len, hipStream_t s);
+void attn_backward(const bf16_t* q, const bf16_t* k, const bf16_t* v, const bf16_t* o,
+                   const bf16_t* dout, const float* lse, bf16_t* dq, bf16_t* dk, bf16_t* dv,
+                   float* dq_acc, float* delta, int B, int H, int Sq, int Sk, long q_stride,
+                   long kv_stride, long o_stride, int causal, float scale, const int* kv_len,
+                   hipStream_t s);
+
+// LSTM cell pointwise (gates = x W_ih^T + h W_hh^T + b precomputed, fp32)
+void lstm_cell_forward(const float* gates, const float* c_prev, float* c_out, bf16_t* h_out,
+                       float* h_out_f32, float* act_cache, int B, int Hd, hipStream_t s);
+void lstm_cell_backward(const float* act_cache, const float* c_prev, const float* c_out,
+                        const float* dh, const float* dc_next, float* dgates, float* dc_prev,
+                        bf16_t* dgates_bf16, int B, int Hd, hipStream_t s);
+
+}  // namespace tam

@@ -1,0 +1,27 @@
+// tiresias_amd — host-side launch API of the HIP kernel library.
+// Plain C++ over raw device pointers + hipStream_t; the torch binding layer
+// (csrc/bindings/ops.cpp) is the only TU that sees ATen.
+#pragma once
+#include <hip/hip_runtime.h>
+#include "tam/igemm.h"
+
+namespace tam {
+
+// C[M,N] (op)= alpha * A(m,k) B(k,n) (+bias)(relu)(mask)
+//   A(m,k) = a_kmajor ? A[m*lda+k] : A[k*lda+m]
+//   B(k,n) = b_kmajor ? B[n*ldb+k] : B[k*ldb+n]
+// allow_split: permit split-K (fp32 atomic output; C is zeroed first when
+// ep.mode == 0, requires ldc == N).
+void gemm(const bf16_t* A, long lda, bool a_kmajor, const bf16_t* B, long ldb, bool b_kmajor,
+          int M, int N, int K, Epi ep, bool allow_split, hipStream_t s);
+
+// NHWC convolutions, weights [K][R][S][C] (C, K multiples of 8)
+void conv_fwd(const bf16_t* x, const bf16_t* w, const ConvGeom& g, Epi ep, hipStream_t s);
+// dx[N*H*W][C]; wt = conv_weight_t(w) laid out [C][R][S][K] (ignored for 1x1/s1)
+void conv_dgrad(const bf16_t* dy, const bf16_t* w, const bf16_t* wt, const ConvGeom& g, Epi ep,
+                hipStream_t s);
+// dw[K][R*S*C] fp32, ep.mode 0 (overwrite) or 1 (accumulate)
+void conv_wgrad(const bf16_t* dy, const bf16_t* x, const ConvGeom& g, Epi ep, hipStream_t s);
+void conv_weight_t(const bf16_t* w, bf16_t* wt, const ConvGeom& g, hipStream_t s);
+
+}  // namespace tam

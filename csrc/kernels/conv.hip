@@ -1,0 +1,118 @@
+// tiresias_amd — NHWC convolution passes as MFMA implicit GEMMs.
+//   fwd  : Y[n,p,q,k]  = sum_{r,s,c} X[n,h(p,r),w(q,s),c] W[k,r,s,c]
+//          M = N*P*Q, N_gemm = K, Kdim = R*S*C    (A gathered from X)
+//   dgrad: dX[n,h,w,c] = sum_{r,s,k} dY[n,p,q,k] W[k,r,s,c]
+//          M = N*H*W, N_gemm = C, Kdim = R*S*K    (A gathered from dY, stride-
+//          aware zero taps; B = W^T laid out [C][R][S][K], K-major)
+//   wgrad: dW[k,r,s,c] = sum_{n,p,q} dY[n,p,q,k] X[n,h,w,c]
+//          M = K, N_gemm = R*S*C, Kdim = N*P*Q    (both operands MN-major,
+//          split-K over output pixels with fp32 atomics)
+// 1x1 / stride-1 / pad-0 convolutions go straight to the dense GEMM.
+#include "tam/launch.h"
+#include "tam/tiles.h"
+
+namespace tam {
+
+template <int BM, int BN>
+static void fwd_tile(const bf16_t* x, const bf16_t* w, const ConvGeom& g, const Epi& ep, int sp,
+                     hipStream_t s) {
+  const int M = g.N * g.P * g.Q, Kd = g.R * g.S * g.C;
+  LdConvFwdA<BM> la{x, g, M, Kd};
+  LdKMajor<BN> lb{w, Kd, g.K, Kd};
+  launch_igemm<BM, BN>(la, lb, M, g.K, Kd, ep, sp, s);
+}
+
+static bool is_pointwise(const ConvGeom& g) {
+  return g.R == 1 && g.S == 1 && g.stride == 1 && g.pad == 0;
+}
+
+void conv_fwd(const bf16_t* x, const bf16_t* w, const ConvGeom& g, Epi ep, hipStream_t s) {
+  const int M = g.N * g.P * g.Q, Kd = g.R * g.S * g.C;
+  if (is_pointwise(g)) {
+    gemm(x, g.C, true, w, g.C, true, M, g.K, g.C, ep, false, s);
+    return;
+  }
+  TileChoice t = choose_tiles(M, g.K, Kd, false);
+  switch (t.cfg) {
+    case 0: fwd_tile<128, 128>(x, w, g, ep, 1, s); break;
+    case 1: fwd_tile<128, 64>(x, w, g, ep, 1, s); break;
+    case 2: fwd_tile<64, 128>(x, w, g, ep, 1, s); break;
+    default: fwd_tile<64, 64>(x, w, g, ep, 1, s); break;
+  }
+}
+
+template <int BM, int BN>
+static void dgrad_tile(const bf16_t* dy, const bf16_t* wt, const ConvGeom& g, const Epi& ep,
+                       hipStream_t s) {
+  const int M = g.N * g.H * g.W, Kd = g.R * g.S * g.K;
+  LdConvDgradA<BM> la{dy, g, M, Kd};
+  LdKMajor<BN> lb{wt, Kd, g.C, Kd};
+  launch_igemm<BM, BN>(la, lb, M, g.C, Kd, ep, 1, s);
+}
+
+void conv_dgrad(const bf16_t* dy, const bf16_t* w, const bf16_t* wt, const ConvGeom& g, Epi ep,
+                hipStream_t s) {
+  const int M = g.N * g.H * g.W, Kd = g.R * g.S * g.K;
+  if (is_pointwise(g)) {
+    // dX[m][c] = sum_k dY[m][k] W[k][c]  -> B(k,n) = W[k*C + c], MN-major
+    gemm(dy, g.K, true, w, g.C, false, M, g.C, g.K, ep, false, s);
+    return;
+  }
+  TileChoice t = choose_tiles(M, g.C, Kd, false);
+  switch (t.cfg) {
+    case 0: dgrad_tile<128, 128>(dy, wt, g, ep, s); break;
+    case 1: dgrad_tile<128, 64>(dy, wt, g, ep, s); break;
+    case 2: dgrad_tile<64, 128>(dy, wt, g, ep, s); break;
+    default: dgrad_tile<64, 64>(dy, wt, g, ep, s); break;
+  }
+}
+
+template <int BM, int BN>
+static void wgrad_tile(const bf16_t* dy, const bf16_t* x, const ConvGeom& g, const Epi& ep, int sp,
+                       hipStream_t s) {
+  const int Mred = g.N * g.P * g.Q, Nc = g.R * g.S * g.C;
+  LdMNMajor<BM> la{dy, g.K, g.K, Mred};
+  LdConvWgradB<BN> lb{x, g, Mred, Nc};
+  launch_igemm<BM, BN>(la, lb, g.K, Nc, Mred, ep, sp, s);
+}
+
+void conv_wgrad(const bf16_t* dy, const bf16_t* x, const ConvGeom& g, Epi ep, hipStream_t s) {
+  const int Mred = g.N * g.P * g.Q, Nc = g.R * g.S * g.C;
+  if (is_pointwise(g)) {
+    // dW[k][c] = sum_m dY[m][k] X[m][c]: A(k', m) = dY[m*K + k'], B(m, c) = X[m*C + c]
+    gemm(dy, g.K, false, x, g.C, false, g.K, g.C, Mred, ep, true, s);
+    return;
+  }
+  TileChoice t = choose_tiles(g.K, Nc, Mred, true);
+  prepare_split(ep, t.splits, g.K, Nc, s);
+  switch (t.cfg) {
+    case 0: wgrad_tile<128, 128>(dy, x, g, ep, t.splits, s); break;
+    case 1: wgrad_tile<128, 64>(dy, x, g, ep, t.splits, s); break;
+    case 2: wgrad_tile<64, 128>(dy, x, g, ep, t.splits, s); break;
+    default: wgrad_tile<64, 64>(dy, x, g, ep, t.splits, s); break;
+  }
+}
+
+// wt[c][(r*S+s)*K + k] = w[k][(r*S+s)*C + c]
+__global__ void conv_weight_t_kernel(const bf16_t* __restrict__ w, bf16_t* __restrict__ wt, int K,
+                                     int RS, int C) {
+  const long total = (long)K * RS * C;
+  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < total;
+       i += (long)gridDim.x * blockDim.x) {
+    const int k = (int)(i % K);
+    const long t = i / K;
+    const int rs = (int)(t % RS);
+    const int c = (int)(t / RS);
+    wt[i] = w[((long)k * RS + rs) * C + c];
+  }
+}
+
+void conv_weight_t(const bf16_t* w, bf16_t* wt, const ConvGeom& g, hipStream_t s) {
+  const long total = (long)g.K * g.R * g.S * g.C;
+  int blocks = (int)((total + 255) / 256);
+  if (blocks > 4096) blocks = 4096;
+  hipLaunchKernelGGL(conv_weight_t_kernel, dim3(blocks), dim3(256), 0, s, w, wt, g.K, g.R * g.S,
+                     g.C);
+}
+
+}  // namespace tam

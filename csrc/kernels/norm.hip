@@ -1,0 +1,410 @@
+// tiresias_amd — BatchNorm (NHWC, training) and LayerNorm kernels.
+//
+// BatchNorm is split into a stats pass (per-channel sum / sum-of-squares,
+// fp32 per block -> fp64 global atomics so E[x^2]-E[x]^2 does not cancel at
+// N*H*W ~ 10^5) and a fused apply pass (scale/shift + optional residual add +
+// optional ReLU) reading 16 B per lane. Backward mirrors it: one reduction
+// pass producing dgamma/dbeta (and the two row-means the input gradient
+// needs), one fused pass producing dx (and the residual-branch gradient).
+#include "tam/common.h"
+#include "tam/kernels.h"
+
+namespace tam {
+
+__device__ __forceinline__ void unpack8(const uint4 v, float (&f)[8]) {
+  const uint32_t w[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    f[2 * i] = __uint_as_float(w[i] << 16);
+    f[2 * i + 1] = __uint_as_float(w[i] & 0xffff0000u);
+  }
+}
+__device__ __forceinline__ uint4 pack8(const float (&f)[8]) {
+  return make_uint4(pack_bf2(f[0], f[1]), pack_bf2(f[2], f[3]), pack_bf2(f[4], f[5]),
+                    pack_bf2(f[6], f[7]));
+}
+
+// ---------------------------------------------------------------- BN stats
+// grid.x blocks each own a contiguous row range; thread = (row lane, 8-ch group)
+__global__ void __launch_bounds__(256) bn_stats_kernel(const bf16_t* __restrict__ x, long M, int C,
+                                                        long rows_per_block,
+                                                        double* __restrict__ sum,
+                                                        double* __restrict__ sumsq) {
+  __shared__ float red[256 * 16];
+  const int tpr = C / 8;                 // threads per row
+  const int rpb = 256 / tpr;             // rows per pass (C <= 2048)
+  const int cg = threadIdx.x % tpr, rl = threadIdx.x / tpr;
+  float s[8], q[8];
+#pragma unroll
+  for (int i = 0; i < 8; ++i) s[i] = q[i] = 0.f;
+  const long r0 = blockIdx.x * rows_per_block;
+  const long r1 = min(M, r0 + rows_per_block);
+  if (rl < rpb) {
+    for (long r = r0 + rl; r < r1; r += rpb) {
+      float f[8];
+      unpack8(*(const uint4*)(x + r * C + cg * 8), f);
+#pragma unroll
+      for (int i = 0; i < 8; ++i) { s[i] += f[i]; q[i] += f[i] * f[i]; }
+    }
+  }
+#pragma unroll
+  for (int i = 0; i < 8; ++i) { red[threadIdx.x * 16 + i] = s[i]; red[threadIdx.x * 16 + 8 + i] = q[i]; }
+  __syncthreads();
+  if (rl == 0) {
+    for (int j = 1; j < rpb; ++j) {
+      const int t = j * tpr + cg;
+#pragma unroll
+      for (int i = 0; i < 8; ++i) { s[i] += red[t * 16 + i]; q[i] += red[t * 16 + 8 + i]; }
+    }
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      atomicAdd(sum + cg * 8 + i, (double)s[i]);
+      atomicAdd(sumsq + cg * 8 + i, (double)q[i]);
+    }
+  }
+}
+
+// mean/rstd + fused scale/shift + running-stat update
+__global__ void bn_finalize_kernel(const double* __restrict__ sum, const double* __restrict__ sumsq,
+                                   long M, int C, float eps, float momentum,
+                                   const float* __restrict__ gamma, const float* __restrict__ beta,
+                                   float* __restrict__ mean_out, float* __restrict__ rstd_out,
+                                   float* __restrict__ scale, float* __restrict__ shift,
+                                   float* __restrict__ run_mean, float* __restrict__ run_var) {
+  const int c = blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= C) return;
+  const double mean = sum[c] / (double)M;
+  double var = sumsq[c] / (double)M - mean * mean;
+  if (var < 0) var = 0;
+  const float rstd = (float)(1.0 / sqrt(var + (double)eps));
+  mean_out[c] = (float)mean;
+  rstd_out[c] = rstd;
+  const float sc = gamma[c] * rstd;
+  scale[c] = sc;
+  shift[c] = beta[c] - (float)mean * sc;
+  if (run_mean) {
+    const double unb = M > 1 ? var * (double)M / (double)(M - 1) : var;
+    run_mean[c] = (1.f - momentum) * run_mean[c] + momentum * (float)mean;
+    run_var[c] = (1.f - momentum) * run_var[c] + momentum * (float)unb;
+  }
+}
+
+// y = x*scale + shift (+res) (relu), 8 channels per thread
+__global__ void __launch_bounds__(256) bn_apply_kernel(const bf16_t* __restrict__ x,
+                                                        const bf16_t* __restrict__ res,
+                                                        const float* __restrict__ scale,
+                                                        const float* __restrict__ shift,
+                                                        bf16_t* __restrict__ y, long total8, int C,
+                                                        int relu) {
+  const int cg8 = C / 8;
+  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < total8;
+       i += (long)gridDim.x * blockDim.x) {
+    const int c0 = (int)(i % cg8) * 8;
+    float f[8];
+    unpack8(((const uint4*)x)[i], f);
+    float rr[8];
+    if (res) unpack8(((const uint4*)res)[i], rr);
+    const float4 sa = *(const float4*)(scale + c0), sb = *(const float4*)(scale + c0 + 4);
+    const float4 ha = *(const float4*)(shift + c0), hb = *(const float4*)(shift + c0 + 4);
+    const float sc[8] = {sa.x, sa.y, sa.z, sa.w, sb.x, sb.y, sb.z, sb.w};
+    const float sh[8] = {ha.x, ha.y, ha.z, ha.w, hb.x, hb.y, hb.z, hb.w};
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      float v = f[j] * sc[j] + sh[j];
+      if (res) v += rr[j];
+      if (relu) v = fmaxf(v, 0.f);
+      f[j] = v;
+    }
+    ((uint4*)y)[i] = pack8(f);
+  }
+}
+
+// ---------------------------------------------------------------- BN backward
+// dyr = dy * (y > 0 if relu); accum sum(dyr), sum(dyr * xhat) per channel
+__global__ void __launch_bounds__(256) bn_bwd_reduce_kernel(
+    const bf16_t* __restrict__ dy, const bf16_t* __restrict__ y, const bf16_t* __restrict__ x,
+    const float* __restrict__ mean, const float* __restrict__ rstd, long M, int C,
+    long rows_per_block, int relu, double* __restrict__ sdy, double* __restrict__ sdyx) {
+  __shared__ float red[256 * 16];
+  const int tpr = C / 8, rpb = 256 / tpr;
+  const int cg = threadIdx.x % tpr, rl = threadIdx.x / tpr;
+  float a[8], b[8], mu[8], rs[8];
+#pragma unroll
+  for (int i = 0; i < 8; ++i) { a[i] = b[i] = 0.f; mu[i] = mean[cg * 8 + i]; rs[i] = rstd[cg * 8 + i]; }
+  const long r0 = blockIdx.x * rows_per_block;
+  const long r1 = min(M, r0 + rows_per_block);
+  if (rl < rpb) {
+    for (long r = r0 + rl; r < r1; r += rpb) {
+      const long off = r * C + cg * 8;
+      float fd[8], fx[8], fy[8];
+      unpack8(*(const uint4*)(dy + off), fd);
+      unpack8(*(const uint4*)(x + off), fx);
+      if (relu) unpack8(*(const uint4*)(y + off), fy);
+#pragma unroll
+      for (int i = 0; i < 8; ++i) {
+        const float d = (relu && fy[i] <= 0.f) ? 0.f : fd[i];
+        a[i] += d;
+        b[i] += d * (fx[i] - mu[i]) * rs[i];
+      }
+    }
+  }
+#pragma unroll
+  for (int i = 0; i < 8; ++i) { red[threadIdx.x * 16 + i] = a[i]; red[threadIdx.x * 16 + 8 + i] = b[i]; }
+  __syncthreads();
+  if (rl == 0) {
+    for (int j = 1; j < rpb; ++j) {
+      const int t = j * tpr + cg;
+#pragma unroll
+      for (int i = 0; i < 8; ++i) { a[i] += red[t * 16 + i]; b[i] += red[t * 16 + 8 + i]; }
+    }
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      atomicAdd(sdy + cg * 8 + i, (double)a[i]);
+      atomicAdd(sdyx + cg * 8 + i, (double)b[i]);
+    }
+  }
+}
+
+// dgamma/dbeta accumulate into fp32 grads; coefficient prep for the apply pass
+__global__ void bn_bwd_finalize_kernel(const double* __restrict__ sdy, const double* __restrict__ sdyx,
+                                       long M, int C, const float* __restrict__ gamma,
+                                       const float* __restrict__ rstd, float* __restrict__ dgamma,
+                                       float* __restrict__ dbeta, float* __restrict__ k1,
+                                       float* __restrict__ k2, float* __restrict__ k3) {
+  const int c = blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= C) return;
+  const float a = (float)sdy[c], b = (float)sdyx[c];
+  if (dgamma) dgamma[c] += b;
+  if (dbeta) dbeta[c] += a;
+  // dx = g*rstd*(dyr - a/M - xhat*b/M) = k1*dyr + k2*xhat + k3
+  const float gr = gamma[c] * rstd[c];
+  k1[c] = gr;
+  k2[c] = -gr * b / (float)M;
+  k3[c] = -gr * a / (float)M;
+}
+
+__global__ void __launch_bounds__(256) bn_bwd_apply_kernel(
+    const bf16_t* __restrict__ dy, const bf16_t* __restrict__ y, const bf16_t* __restrict__ x,
+    const float* __restrict__ mean, const float* __restrict__ rstd, const float* __restrict__ k1,
+    const float* __restrict__ k2, const float* __restrict__ k3, bf16_t* __restrict__ dx,
+    bf16_t* __restrict__ dres, long total8, int C, int relu) {
+  const int cg8 = C / 8;
+  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < total8;
+       i += (long)gridDim.x * blockDim.x) {
+    const int c0 = (int)(i % cg8) * 8;
+    float fd[8], fx[8], fy[8];
+    unpack8(((const uint4*)dy)[i], fd);
+    unpack8(((const uint4*)x)[i], fx);
+    if (relu) {
+      unpack8(((const uint4*)y)[i], fy);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) fd[j] = fy[j] <= 0.f ? 0.f : fd[j];
+    }
+    if (dres) ((uint4*)dres)[i] = pack8(fd);
+    float o[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const int c = c0 + j;
+      const float xh = (fx[j] - mean[c]) * rstd[c];
+      o[j] = k1[c] * fd[j] + k2[c] * xh + k3[c];
+    }
+    ((uint4*)dx)[i] = pack8(o);
+  }
+}
+
+static int grid_for(long n, int per_thread_vec = 1) {
+  long b = (n + 255) / 256;
+  if (b > 2048) b = 2048;
+  if (b < 1) b = 1;
+  return (int)b;
+}
+
+static long bn_rows_per_block(long M, int C) {
+  // ~ 1024 blocks in flight (4/CU) for the reduction passes
+  long rpb = (M + 1023) / 1024;
+  const long minr = 256 / (C / 8) * 4;
+  if (rpb < minr) rpb = minr;
+  return rpb;
+}
+
+void bn_forward(const bf16_t* x, const bf16_t* res, bf16_t* y, long M, int C, float eps,
+                float momentum, const float* gamma, const float* beta, float* run_mean,
+                float* run_var, float* save_mean, float* save_rstd, double* ws, float* ws_f,
+                int relu, hipStream_t s) {
+  // ws: 2*C doubles; ws_f: 2*C floats (scale, shift)
+  TAM_HIP_CHECK(hipMemsetAsync(ws, 0, sizeof(double) * 2 * C, s));
+  const long rpb = bn_rows_per_block(M, C);
+  const int nb = (int)((M + rpb - 1) / rpb);
+  hipLaunchKernelGGL(bn_stats_kernel, dim3(nb), dim3(256), 0, s, x, M, C, rpb, ws, ws + C);
+  hipLaunchKernelGGL(bn_finalize_kernel, dim3((C + 255) / 256), dim3(256), 0, s, ws, ws + C, M, C,
+                     eps, momentum, gamma, beta, save_mean, save_rstd, ws_f, ws_f + C, run_mean,
+                     run_var);
+  const long total8 = M * C / 8;
+  hipLaunchKernelGGL(bn_apply_kernel, dim3(grid_for(total8)), dim3(256), 0, s, x, res, ws_f,
+                     ws_f + C, y, total8, C, relu);
+}
+
+void bn_infer(const bf16_t* x, const bf16_t* res, bf16_t* y, long M, int C, const float* scale,
+              const float* shift, int relu, hipStream_t s) {
+  const long total8 = M * C / 8;
+  hipLaunchKernelGGL(bn_apply_kernel, dim3(grid_for(total8)), dim3(256), 0, s, x, res, scale,
+                     shift, y, total8, C, relu);
+}
+
+void bn_backward(const bf16_t* dy, const bf16_t* y, const bf16_t* x, const float* mean,
+                 const float* rstd, const float* gamma, long M, int C, int relu, bf16_t* dx,
+                 bf16_t* dres, float* dgamma, float* dbeta, double* ws, float* ws_f,
+                 hipStream_t s) {
+  // ws: 2*C doubles; ws_f: 3*C floats
+  TAM_HIP_CHECK(hipMemsetAsync(ws, 0, sizeof(double) * 2 * C, s));
+  const long rpb = bn_rows_per_block(M, C);
+  const int nb = (int)((M + rpb - 1) / rpb);
+  hipLaunchKernelGGL(bn_bwd_reduce_kernel, dim3(nb), dim3(256), 0, s, dy, y, x, mean, rstd, M, C,
+                     rpb, relu, ws, ws + C);
+  hipLaunchKernelGGL(bn_bwd_finalize_kernel, dim3((C + 255) / 256), dim3(256), 0, s, ws, ws + C, M,
+                     C, gamma, rstd, dgamma, dbeta, ws_f, ws_f + C, ws_f + 2 * C);
+  const long total8 = M * C / 8;
+  hipLaunchKernelGGL(bn_bwd_apply_kernel, dim3(grid_for(total8)), dim3(256), 0, s, dy, y, x, mean,
+                     rstd, ws_f, ws_f + C, ws_f + 2 * C, dx, dres, total8, C, relu);
+}
+
+// ---------------------------------------------------------------- LayerNorm
+// One wave per row; D <= 64*8*ROWVEC. Vectorized 8 bf16 per lane-step.
+template <int VEC>
+__global__ void __launch_bounds__(256) ln_fwd_kernel(const bf16_t* __restrict__ x,
+                                                      const float* __restrict__ g,
+                                                      const float* __restrict__ b,
+                                                      bf16_t* __restrict__ y,
+                                                      float* __restrict__ mean_o,
+                                                      float* __restrict__ rstd_o, long rows, int D,
+                                                      float eps) {
+  const int lane = threadIdx.x & 63;
+  const long row = blockIdx.x * 4L + (threadIdx.x >> 6);
+  if (row >= rows) return;
+  const bf16_t* xr = x + row * D;
+  float f[VEC][8];
+  float s = 0.f;
+#pragma unroll
+  for (int v = 0; v < VEC; ++v) {
+    const int c = (v * 64 + lane) * 8;
+    if (c < D) unpack8(*(const uint4*)(xr + c), f[v]);
+    else {
+#pragma unroll
+      for (int j = 0; j < 8; ++j) f[v][j] = 0.f;
+    }
+#pragma unroll
+    for (int j = 0; j < 8; ++j) s += f[v][j];
+  }
+  const float mu = wave_sum(s) / D;
+  float q = 0.f;
+#pragma unroll
+  for (int v = 0; v < VEC; ++v) {
+    const int c = (v * 64 + lane) * 8;
+    if (c < D) {
+#pragma unroll
+      for (int j = 0; j < 8; ++j) { const float d = f[v][j] - mu; q += d * d; }
+    }
+  }
+  const float rstd = rsqrtf(wave_sum(q) / D + eps);
+  if (lane == 0) { mean_o[row] = mu; rstd_o[row] = rstd; }
+#pragma unroll
+  for (int v = 0; v < VEC; ++v) {
+    const int c = (v * 64 + lane) * 8;
+    if (c < D) {
+      float o[8];
+#pragma unroll
+      for (int j = 0; j < 8; ++j) o[j] = (f[v][j] - mu) * rstd * g[c + j] + b[c + j];
+      *(uint4*)(y + row * D + c) = pack8(o);
+    }
+  }
+}
+
+template <int VEC>
+__global__ void __launch_bounds__(256) ln_bwd_kernel(const bf16_t* __restrict__ dy,
+                                                      const bf16_t* __restrict__ x,
+                                                      const float* __restrict__ g,
+                                                      const float* __restrict__ mean,
+                                                      const float* __restrict__ rstd,
+                                                      bf16_t* __restrict__ dx,
+                                                      float* __restrict__ dg_part,
+                                                      float* __restrict__ db_part, long rows,
+                                                      int D, int rows_per_block) {
+  // each wave processes rows_per_block/4 rows, accumulating dgamma/dbeta in regs,
+  // then atomically adds its partials (fp32) — grid sized to ~1024 waves.
+  const int lane = threadIdx.x & 63;
+  const int w = threadIdx.x >> 6;
+  float dgacc[VEC][8], dbacc[VEC][8];
+#pragma unroll
+  for (int v = 0; v < VEC; ++v)
+#pragma unroll
+    for (int j = 0; j < 8; ++j) dgacc[v][j] = dbacc[v][j] = 0.f;
+  const long r0 = (long)blockIdx.x * rows_per_block;
+  for (long row = r0 + w; row < min(rows, r0 + rows_per_block); row += 4) {
+    const float mu = mean[row], rs = rstd[row];
+    float fx[VEC][8], fd[VEC][8];
+    float s1 = 0.f, s2 = 0.f;
+#pragma unroll
+    for (int v = 0; v < VEC; ++v) {
+      const int c = (v * 64 + lane) * 8;
+      if (c < D) {
+        unpack8(*(const uint4*)(x + row * D + c), fx[v]);
+        unpack8(*(const uint4*)(dy + row * D + c), fd[v]);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          const float xh = (fx[v][j] - mu) * rs;
+          fx[v][j] = xh;
+          const float gd = fd[v][j] * g[c + j];
+          s1 += gd;
+          s2 += gd * xh;
+          dgacc[v][j] += fd[v][j] * xh;
+          dbacc[v][j] += fd[v][j];
+        }
+      }
+    }
+    s1 = wave_sum(s1) / D;
+    s2 = wave_sum(s2) / D;
+#pragma unroll
+    for (int v = 0; v < VEC; ++v) {
+      const int c = (v * 64 + lane) * 8;
+      if (c < D) {
+        float o[8];
+#pragma unroll
+        for (int j = 0; j < 8; ++j) o[j] = rs * (fd[v][j] * g[c + j] - s1 - fx[v][j] * s2);
+        *(uint4*)(dx + row * D + c) = pack8(o);
+      }
+    }
+  }
+#pragma unroll
+  for (int v = 0; v < VEC; ++v) {
+    const int c = (v * 64 + lane) * 8;
+    if (c < D) {
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        atomicAdd(dg_part + c + j, dgacc[v][j]);
+        atomicAdd(db_part + c + j, dbacc[v][j]);
+      }
+    }
+  }
+}
+
+void ln_forward(const bf16_t* x, const float* g, const float* b, bf16_t* y, float* mean,
+                float* rstd, long rows, int D, float eps, hipStream_t s) {
+  const int blocks = (int)((rows + 3) / 4);
+  if (D <= 512) hipLaunchKernelGGL(ln_fwd_kernel<1>, dim3(blocks), dim3(256), 0, s, x, g, b, y, mean, rstd, rows, D, eps);
+  else if (D <= 1024) hipLaunchKernelGGL(ln_fwd_kernel<2>, dim3(blocks), dim3(256), 0, s, x, g, b, y, mean, rstd, rows, D, eps);
+  else hipLaunchKernelGGL(ln_fwd_kernel<4>, dim3(blocks), dim3(256), 0, s, x, g, b, y, mean, rstd, rows, D, eps);
+}
+
+void ln_backward(const bf16_t* dy, const bf16_t* x, const float* g, const float* mean,
+                 const float* rstd, bf16_t* dx, float* dg, float* db, long rows, int D,
+                 hipStream_t s) {
+  int rpb = (int)((rows + 1023) / 1024);
+  rpb = ((rpb + 3) / 4) * 4;
+  if (rpb < 16) rpb = 16;
+  const int blocks = (int)((rows + rpb - 1) / rpb);
+  if (D <= 512) hipLaunchKernelGGL(ln_bwd_kernel<1>, dim3(blocks), dim3(256), 0, s, dy, x, g, mean, rstd, dx, dg, db, rows, D, rpb);
+  else if (D <= 1024) hipLaunchKernelGGL(ln_bwd_kernel<2>, dim3(blocks), dim3(256), 0, s, dy, x, g, mean, rstd, dx, dg, db, rows, D, rpb);
+  else hipLaunchKernelGGL(ln_bwd_kernel<4>, dim3(blocks), dim3(256), 0, s, dy, x, g, mean, rstd, dx, dg, db, rows, D, rpb);
+}
+
+}  // namespace tam

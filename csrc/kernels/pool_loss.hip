@@ -1,0 +1,308 @@
+// tiresias_amd — pooling (NHWC), fused softmax cross-entropy, embedding and
+// small elementwise kernels.
+#include "tam/common.h"
+#include "tam/kernels.h"
+
+namespace tam {
+
+static int grid_cap(long n, int cap = 4096) {
+  long b = (n + 255) / 256;
+  if (b > cap) b = cap;
+  return (int)(b < 1 ? 1 : b);
+}
+
+// ------------------------------------------------------------------ max pool
+// y[n,p,q,c] = max over window; idx stores the argmax tap (r*S+s) as uint8.
+__global__ void maxpool_fwd_kernel(const bf16_t* __restrict__ x, bf16_t* __restrict__ y,
+                                   uint8_t* __restrict__ idx, int N, int H, int W, int C, int P,
+                                   int Q, int R, int S, int st, int pad) {
+  const long total = (long)N * P * Q * C;
+  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < total;
+       i += (long)gridDim.x * blockDim.x) {
+    const int c = (int)(i % C);
+    long t = i / C;
+    const int q = (int)(t % Q); t /= Q;
+    const int p = (int)(t % P);
+    const int n = (int)(t / P);
+    float best = -INFINITY;
+    int bi = 0;
+    for (int r = 0; r < R; ++r) {
+      const int h = p * st - pad + r;
+      if ((unsigned)h >= (unsigned)H) continue;
+      for (int s = 0; s < S; ++s) {
+        const int w = q * st - pad + s;
+        if ((unsigned)w >= (unsigned)W) continue;
+        const float v = bf2f(x[(((long)n * H + h) * W + w) * C + c]);
+        if (v > best) { best = v; bi = r * S + s; }
+      }
+    }
+    y[i] = f2bf(best);
+    idx[i] = (uint8_t)bi;
+  }
+}
+
+// gather-form backward: each input element sums the outputs whose argmax it is
+__global__ void maxpool_bwd_kernel(const bf16_t* __restrict__ dy, const uint8_t* __restrict__ idx,
+                                   bf16_t* __restrict__ dx, int N, int H, int W, int C, int P,
+                                   int Q, int R, int S, int st, int pad) {
+  const long total = (long)N * H * W * C;
+  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < total;
+       i += (long)gridDim.x * blockDim.x) {
+    const int c = (int)(i % C);
+    long t = i / C;
+    const int w = (int)(t % W); t /= W;
+    const int h = (int)(t % H);
+    const int n = (int)(t / H);
+    float acc = 0.f;
+    for (int r = 0; r < R; ++r) {
+      const int pn = h + pad - r;
+      if (pn < 0 || pn % st) continue;
+      const int p = pn / st;
+      if (p >= P) continue;
+      for (int s = 0; s < S; ++s) {
+        const int qn = w + pad - s;
+        if (qn < 0 || qn % st) continue;
+        const int q = qn / st;
+        if (q >= Q) continue;
+        const long o = (((long)n * P + p) * Q + q) * C + c;
+        if (idx[o] == r * S + s) acc += bf2f(dy[o]);
+      }
+    }
+    dx[i] = f2bf(acc);
+  }
+}
+
+void maxpool_forward(const bf16_t* x, bf16_t* y, uint8_t* idx, int N, int H, int W, int C, int P,
+                     int Q, int R, int S, int st, int pad, hipStream_t s) {
+  hipLaunchKernelGGL(maxpool_fwd_kernel, dim3(grid_cap((long)N * P * Q * C)), dim3(256), 0, s, x, y,
+                     idx, N, H, W, C, P, Q, R, S, st, pad);
+}
+void maxpool_backward(const bf16_t* dy, const uint8_t* idx, bf16_t* dx, int N, int H, int W, int C,
+                      int P, int Q, int R, int S, int st, int pad, hipStream_t s) {
+  hipLaunchKernelGGL(maxpool_bwd_kernel, dim3(grid_cap((long)N * H * W * C)), dim3(256), 0, s, dy,
+                     idx, dx, N, H, W, C, P, Q, R, S, st, pad);
+}
+
+// ------------------------------------------------------------ global avgpool
+// x [N][HW][C] -> y [N][C]; one thread per (n, c)
+__global__ void avgpool_fwd_kernel(const bf16_t* __restrict__ x, bf16_t* __restrict__ y, int N,
+                                   int HW, int C) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= N * C) return;
+  const int n = i / C, c = i % C;
+  float s = 0.f;
+  for (int p = 0; p < HW; ++p) s += bf2f(x[((long)n * HW + p) * C + c]);
+  y[i] = f2bf(s / HW);
+}
+__global__ void avgpool_bwd_kernel(const bf16_t* __restrict__ dy, bf16_t* __restrict__ dx, int N,
+                                   int HW, int C) {
+  const long total = (long)N * HW * C;
+  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < total;
+       i += (long)gridDim.x * blockDim.x) {
+    const int c = (int)(i % C);
+    const int n = (int)(i / ((long)HW * C));
+    dx[i] = f2bf(bf2f(dy[(long)n * C + c]) / HW);
+  }
+}
+void avgpool_forward(const bf16_t* x, bf16_t* y, int N, int HW, int C, hipStream_t s) {
+  hipLaunchKernelGGL(avgpool_fwd_kernel, dim3((N * C + 255) / 256), dim3(256), 0, s, x, y, N, HW, C);
+}
+void avgpool_backward(const bf16_t* dy, bf16_t* dx, int N, int HW, int C, hipStream_t s) {
+  hipLaunchKernelGGL(avgpool_bwd_kernel, dim3(grid_cap((long)N * HW * C)), dim3(256), 0, s, dy, dx,
+                     N, HW, C);
+}
+
+// ------------------------------------------------- softmax cross-entropy fused
+// One 256-thread block per row. Forward and backward in one kernel: the loss
+// is the graph's sink, so dlogits = (softmax - target) * grad_scale is known.
+// Label smoothing eps: target = (1-eps) onehot + eps/V. ignore_index rows
+// contribute 0 loss / 0 grad.
+__global__ void __launch_bounds__(256) xent_kernel(const bf16_t* __restrict__ logits,
+                                                    const long* __restrict__ labels,
+                                                    bf16_t* __restrict__ dlogits,
+                                                    float* __restrict__ loss_rows, int V,
+                                                    float smoothing, float grad_scale,
+                                                    long ignore_index) {
+  __shared__ float scratch[16];
+  const long row = blockIdx.x;
+  const bf16_t* lr = logits + row * V;
+  const long lab = labels[row];
+  const bool ign = lab == ignore_index;
+  // pass 1: online max / sum-exp, vectorized 8-wide when aligned
+  float m = -INFINITY, s = 0.f, sum_logit = 0.f;
+  const bool vec = (V % 8) == 0;
+  if (vec) {
+    for (int c = threadIdx.x * 8; c < V; c += 256 * 8) {
+      const uint4 u = *(const uint4*)(lr + c);
+      const uint32_t w[4] = {u.x, u.y, u.z, u.w};
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        const float a = __uint_as_float(w[k] << 16), b = __uint_as_float(w[k] & 0xffff0000u);
+        sum_logit += a + b;
+        const float mn = fmaxf(m, fmaxf(a, b));
+        s = s * __expf(m - mn) + __expf(a - mn) + __expf(b - mn);
+        m = mn;
+      }
+    }
+  } else {
+    for (int c = threadIdx.x; c < V; c += 256) {
+      const float a = bf2f(lr[c]);
+      sum_logit += a;
+      const float mn = fmaxf(m, a);
+      s = s * __expf(m - mn) + __expf(a - mn);
+      m = mn;
+    }
+  }
+  const float M = block_max(m, scratch);
+  float sc = (m == -INFINITY) ? 0.f : s * __expf(m - M);
+  const float S = block_sum(sc, scratch);
+  const float SL = block_sum(sum_logit, scratch);
+  const float lse = M + __logf(S);
+  if (threadIdx.x == 0) {
+    float loss = 0.f;
+    if (!ign) {
+      const float lt = bf2f(lr[lab]);
+      loss = (1.f - smoothing) * (lse - lt) + smoothing * (lse - SL / V);
+    }
+    loss_rows[row] = loss;
+  }
+  if (!dlogits) return;
+  bf16_t* dr = dlogits + row * V;
+  const float inv = 1.f / S;
+  const float eps_v = smoothing / V;
+  if (vec) {
+    for (int c = threadIdx.x * 8; c < V; c += 256 * 8) {
+      const uint4 u = *(const uint4*)(lr + c);
+      const uint32_t w[4] = {u.x, u.y, u.z, u.w};
+      uint32_t o[4];
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        const int c0 = c + 2 * k;
+        float a = __expf(__uint_as_float(w[k] << 16) - M) * inv - eps_v;
+        float b = __expf(__uint_as_float(w[k] & 0xffff0000u) - M) * inv - eps_v;
+        if (c0 == lab) a -= 1.f - smoothing;
+        if (c0 + 1 == lab) b -= 1.f - smoothing;
+        if (ign) { a = 0.f; b = 0.f; }
+        o[k] = pack_bf2(a * grad_scale, b * grad_scale);
+      }
+      *(uint4*)(dr + c) = make_uint4(o[0], o[1], o[2], o[3]);
+    }
+  } else {
+    for (int c = threadIdx.x; c < V; c += 256) {
+      float a = __expf(bf2f(lr[c]) - M) * inv - eps_v;
+      if (c == lab) a -= 1.f - smoothing;
+      if (ign) a = 0.f;
+      dr[c] = f2bf(a * grad_scale);
+    }
+  }
+}
+
+void softmax_xent(const bf16_t* logits, const long* labels, bf16_t* dlogits, float* loss_rows,
+                  long rows, int V, float smoothing, float grad_scale, long ignore_index,
+                  hipStream_t s) {
+  hipLaunchKernelGGL(xent_kernel, dim3(rows), dim3(256), 0, s, logits, labels, dlogits, loss_rows,
+                     V, smoothing, grad_scale, ignore_index);
+}
+
+// ------------------------------------------------------------------ embedding
+// out[t][:] = table[ids[t]][:] * scale  (D % 8 == 0), 16 B per lane
+__global__ void embed_fwd_kernel(const bf16_t* __restrict__ table, const long* __restrict__ ids,
+                                 bf16_t* __restrict__ out, long T, int D, float scale) {
+  const int d8 = D / 8;
+  const long total = T * d8;
+  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < total;
+       i += (long)gridDim.x * blockDim.x) {
+    const long t = i / d8;
+    const int c = (int)(i % d8) * 8;
+    const uint4 u = *(const uint4*)(table + ids[t] * D + c);
+    if (scale == 1.f) {
+      *(uint4*)(out + t * D + c) = u;
+    } else {
+      const uint32_t w[4] = {u.x, u.y, u.z, u.w};
+      uint32_t o[4];
+#pragma unroll
+      for (int k = 0; k < 4; ++k)
+        o[k] = pack_bf2(__uint_as_float(w[k] << 16) * scale, __uint_as_float(w[k] & 0xffff0000u) * scale);
+      *(uint4*)(out + t * D + c) = make_uint4(o[0], o[1], o[2], o[3]);
+    }
+  }
+}
+// grad_table[ids[t]] += dout[t] * scale  (fp32 atomics; rows of D contiguous)
+__global__ void embed_bwd_kernel(const bf16_t* __restrict__ dout, const long* __restrict__ ids,
+                                 float* __restrict__ gtable, long T, int D, float scale) {
+  const long total = T * D;
+  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < total;
+       i += (long)gridDim.x * blockDim.x) {
+    const long t = i / D;
+    const int c = (int)(i % D);
+    atomicAdd(gtable + ids[t] * D + c, bf2f(dout[i]) * scale);
+  }
+}
+void embedding_forward(const bf16_t* table, const long* ids, bf16_t* out, long T, int D,
+                       float scale, hipStream_t s) {
+  hipLaunchKernelGGL(embed_fwd_kernel, dim3(grid_cap(T * D / 8)), dim3(256), 0, s, table, ids, out,
+                     T, D, scale);
+}
+void embedding_backward(const bf16_t* dout, const long* ids, float* gtable, long T, int D,
+                        float scale, hipStream_t s) {
+  hipLaunchKernelGGL(embed_bwd_kernel, dim3(grid_cap(T * D)), dim3(256), 0, s, dout, ids, gtable, T,
+                     D, scale);
+}
+
+// ------------------------------------------------------------- column sums
+// out[c] (+)= sum_r x[r][c] (bias gradients), fp32 accumulate, relu-mask opt.
+__global__ void colsum_kernel(const bf16_t* __restrict__ x, float* __restrict__ out, long R, int C,
+                              long rows_per_block) {
+  const long r0 = blockIdx.y * rows_per_block;
+  const long r1 = min(R, r0 + rows_per_block);
+  for (int c = blockIdx.x * blockDim.x + threadIdx.x; c < C; c += gridDim.x * blockDim.x) {
+    float s = 0.f;
+    for (long r = r0; r < r1; ++r) s += bf2f(x[r * C + c]);
+    atomicAdd(out + c, s);
+  }
+}
+void colsum(const bf16_t* x, float* out, long R, int C, hipStream_t s) {
+  const int bx = (C + 255) / 256;
+  long rpb = 64;
+  long by = (R + rpb - 1) / rpb;
+  if (by * bx > 4096) { by = 4096 / bx; if (by < 1) by = 1; rpb = (R + by - 1) / by; by = (R + rpb - 1) / rpb; }
+  hipLaunchKernelGGL(colsum_kernel, dim3(bx, by), dim3(256), 0, s, x, out, R, C, rpb);
+}
+
+// ---------------------------------------------------------------- elementwise
+// y = relu(x) ; dx = dy * (y > 0); y = a + b ; fp32 -> bf16 cast
+__global__ void relu_bwd_kernel(const bf16_t* __restrict__ dy, const bf16_t* __restrict__ y,
+                                bf16_t* __restrict__ dx, long n) {
+  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < n; i += (long)gridDim.x * blockDim.x)
+    dx[i] = bf2f(y[i]) > 0.f ? dy[i] : (bf16_t)0;
+}
+void relu_backward(const bf16_t* dy, const bf16_t* y, bf16_t* dx, long n, hipStream_t s) {
+  hipLaunchKernelGGL(relu_bwd_kernel, dim3(grid_cap(n)), dim3(256), 0, s, dy, y, dx, n);
+}
+
+__global__ void add_kernel(const bf16_t* __restrict__ a, const bf16_t* __restrict__ b,
+                           bf16_t* __restrict__ y, long n8) {
+  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < n8; i += (long)gridDim.x * blockDim.x) {
+    const uint4 u = ((const uint4*)a)[i], v = ((const uint4*)b)[i];
+    const uint32_t wa[4] = {u.x, u.y, u.z, u.w}, wb[4] = {v.x, v.y, v.z, v.w};
+    uint32_t o[4];
+#pragma unroll
+    for (int k = 0; k < 4; ++k)
+      o[k] = pack_bf2(__uint_as_float(wa[k] << 16) + __uint_as_float(wb[k] << 16),
+                      __uint_as_float(wa[k] & 0xffff0000u) + __uint_as_float(wb[k] & 0xffff0000u));
+    ((uint4*)y)[i] = make_uint4(o[0], o[1], o[2], o[3]);
+  }
+}
+void add_bf16(const bf16_t* a, const bf16_t* b, bf16_t* y, long n, hipStream_t s) {
+  hipLaunchKernelGGL(add_kernel, dim3(grid_cap(n / 8)), dim3(256), 0, s, a, b, y, n / 8);
+}
+
+__global__ void cast_f32_bf16_kernel(const float* __restrict__ x, bf16_t* __restrict__ y, long n) {
+  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < n; i += (long)gridDim.x * blockDim.x)
+    y[i] = f2bf(x[i]);
+}
+void cast_f32_bf16(const float* x, bf16_t* y, long n, hipStream_t s) {
+  hipLaunchKernelGGL(cast_f32_bf16_kernel, dim3(grid_cap(n)), dim3(256), 0, s, x, y, n);
+}
+
+}  // namespace tam

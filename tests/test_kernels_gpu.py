@@ -1,0 +1,401 @@
+"""Numerics of every hand-written HIP kernel against a plain fp32 PyTorch
+reference of the same op (run on the MI355X box via gpurun)."""
+import math
+
+import pytest
+import torch
+import torch.nn.functional as F
+
+pytestmark = pytest.mark.gpu
+BF = torch.bfloat16
+
+
+def rel_err(a, b):
+    a = a.float()
+    b = b.float()
+    return ((a - b).norm() / (b.norm() + 1e-12)).item()
+
+
+def T():
+    return torch.ops.tam
+
+
+# ------------------------------------------------------------------ GEMM
+@pytest.mark.parametrize("M,N,K", [(256, 256, 256), (200, 136, 72), (1000, 64, 520), (64, 1000, 64),
+                                   (4096, 1024, 512), (33, 40, 8)])
+@pytest.mark.parametrize("ak,bk", [(True, True), (True, False), (False, True), (False, False)])
+def test_gemm_layouts(gpu, M, N, K, ak, bk):
+    if (not ak and M % 8) or (not bk and N % 8):
+        pytest.skip("MN-major operand needs multiple of 8")
+    torch.manual_seed(0)
+    A = torch.randn(M, K, device=gpu).to(BF)
+    B = torch.randn(K, N, device=gpu).to(BF)
+    a = A if ak else A.t().contiguous()
+    b = B.t().contiguous() if bk else B
+    ref = A.float() @ B.float()
+    c = torch.empty(M, N, device=gpu, dtype=torch.float32)
+    T().gemm(a, ak, b, bk, c, 0, None, False, None, 1.0, False)
+    assert rel_err(c, ref) < 1e-5
+    cb = torch.empty(M, N, device=gpu, dtype=BF)
+    T().gemm(a, ak, b, bk, cb, 0, None, False, None, 1.0, False)
+    assert rel_err(cb, ref) < 1e-2
+
+
+def test_gemm_identity_asymmetric(gpu):
+    # A = I with an asymmetric B catches a transposed C-write (guide §3)
+    n = 128
+    A = torch.eye(n, device=gpu).to(BF)
+    B = (torch.arange(n * n, device=gpu).reshape(n, n) % 97).float().to(BF)
+    c = torch.empty(n, n, device=gpu)
+    T().gemm(A, True, B.t().contiguous(), True, c, 0, None, False, None, 1.0, False)
+    assert torch.equal(c, B.float())
+
+
+def test_gemm_epilogues(gpu):
+    torch.manual_seed(1)
+    M, N, K = 384, 192, 256
+    A = torch.randn(M, K, device=gpu).to(BF)
+    W = torch.randn(N, K, device=gpu).to(BF)
+    bias = torch.randn(N, device=gpu).to(BF)
+    mask = torch.randn(M, N, device=gpu).to(BF)
+    ref = A.float() @ W.float().t() + bias.float()
+    y = torch.empty(M, N, device=gpu, dtype=BF)
+    T().gemm(A, True, W, True, y, 0, bias, True, None, 1.0, False)
+    assert rel_err(y, ref.clamp_min(0)) < 1e-2
+    T().gemm(A, True, W, True, y, 0, None, False, mask, 0.5, False)
+    assert rel_err(y, (0.5 * (A.float() @ W.float().t())) * (mask.float() > 0)) < 1e-2
+    acc = torch.randn(M, N, device=gpu)
+    ref2 = acc + A.float() @ W.float().t()
+    T().gemm(A, True, W, True, acc, 1, None, False, None, 1.0, False)
+    assert rel_err(acc, ref2) < 1e-5
+
+
+def test_gemm_splitk(gpu):
+    torch.manual_seed(2)
+    M, N, K = 64, 96, 16384
+    A = torch.randn(K, M, device=gpu).to(BF)     # MN-major A (like dW = dY^T X)
+    B = torch.randn(K, N, device=gpu).to(BF)
+    ref = A.float().t() @ B.float()
+    c = torch.full((M, N), 7.0, device=gpu)
+    T().gemm(A, False, B, False, c, 0, None, False, None, 1.0, True)
+    assert rel_err(c, ref) < 1e-5
+    c2 = torch.ones(M, N, device=gpu)
+    T().gemm(A, False, B, False, c2, 1, None, False, None, 1.0, True)
+    assert rel_err(c2, ref + 1) < 1e-5
+
+
+# ------------------------------------------------------------------ conv
+CONVS = [  # N,H,W,C,K,R,stride,pad
+    (2, 16, 16, 64, 64, 3, 1, 1),
+    (2, 15, 17, 32, 48, 3, 2, 1),
+    (2, 14, 14, 64, 128, 1, 1, 0),
+    (2, 14, 14, 64, 128, 1, 2, 0),
+    (2, 32, 32, 8, 64, 7, 2, 3),
+    (1, 7, 7, 512, 512, 3, 1, 1),
+    (4, 28, 28, 128, 128, 3, 1, 1),
+]
+
+
+def _ref_conv(x, w, stride, pad):
+    return F.conv2d(x.float().permute(0, 3, 1, 2), w.float().permute(0, 3, 1, 2), stride=stride,
+                    padding=pad).permute(0, 2, 3, 1)
+
+
+@pytest.mark.parametrize("cfg", CONVS)
+def test_conv_fwd_dgrad_wgrad(gpu, cfg):
+    N, H, W, C, K, R, st, pd = cfg
+    torch.manual_seed(3)
+    x = torch.randn(N, H, W, C, device=gpu).to(BF)
+    w = (torch.randn(K, R, R, C, device=gpu) / math.sqrt(R * R * C)).to(BF)
+    P = (H + 2 * pd - R) // st + 1
+    Q = (W + 2 * pd - R) // st + 1
+    y = torch.empty(N, P, Q, K, device=gpu, dtype=BF)
+    T().conv_fwd(x, w, y, st, pd, 1, None, False)
+    xf = x.float().permute(0, 3, 1, 2).requires_grad_(True)
+    wf = w.float().permute(0, 3, 1, 2).requires_grad_(True)
+    yf = F.conv2d(xf, wf, stride=st, padding=pd)
+    assert rel_err(y, yf.permute(0, 2, 3, 1)) < 1e-2
+    dy = torch.randn(N, P, Q, K, device=gpu).to(BF)
+    gx, gw = torch.autograd.grad(yf, [xf, wf], dy.float().permute(0, 3, 1, 2))
+    dx = torch.empty_like(x)
+    wt = torch.empty_like(w)
+    T().conv_dgrad(dy, w, wt, dx, st, pd, 1, None)
+    assert rel_err(dx, gx.permute(0, 2, 3, 1)) < 1e-2
+    dw = torch.zeros(K, R, R, C, device=gpu)
+    T().conv_wgrad(dy, x, dw, st, pd, 1, 0)
+    assert rel_err(dw, gw.permute(0, 2, 3, 1)) < 1e-4
+
+
+def test_conv_bias_relu_mask(gpu):
+    torch.manual_seed(4)
+    x = torch.randn(2, 8, 8, 16, device=gpu).to(BF)
+    w = (torch.randn(32, 3, 3, 16, device=gpu) * 0.1).to(BF)
+    b = torch.randn(32, device=gpu).to(BF)
+    y = torch.empty(2, 8, 8, 32, device=gpu, dtype=BF)
+    T().conv_fwd(x, w, y, 1, 1, 1, b, True)
+    ref = (_ref_conv(x, w, 1, 1) + b.float()).clamp_min(0)
+    assert rel_err(y, ref) < 1e-2
+    # dgrad masked by the input (relu-backward of the producer fused in)
+    dy = torch.randn_like(y)
+    dx = torch.empty_like(x)
+    T().conv_dgrad(dy, w, torch.empty_like(w), dx, 1, 1, 1, x)
+    xf = x.float().permute(0, 3, 1, 2).requires_grad_(True)
+    g, = torch.autograd.grad(F.conv2d(xf, w.float().permute(0, 3, 1, 2), padding=1), [xf],
+                             dy.float().permute(0, 3, 1, 2))
+    assert rel_err(dx, g.permute(0, 2, 3, 1) * (x.float() > 0)) < 1e-2
+
+
+# ------------------------------------------------------------------ BN / LN
+@pytest.mark.parametrize("relu,res", [(False, False), (True, False), (True, True)])
+def test_batchnorm(gpu, relu, res):
+    torch.manual_seed(5)
+    N, H, W, C = 8, 14, 14, 64
+    x = (torch.randn(N, H, W, C, device=gpu) * 3 + 1).to(BF)
+    r = torch.randn(N, H, W, C, device=gpu).to(BF) if res else None
+    g = torch.rand(C, device=gpu) + 0.5
+    b = torch.randn(C, device=gpu)
+    rm, rv = torch.zeros(C, device=gpu), torch.ones(C, device=gpu)
+    y = torch.empty_like(x)
+    mean = torch.empty(C, device=gpu); rstd = torch.empty(C, device=gpu)
+    T().bn_forward(x, r, y, g, b, rm, rv, mean, rstd, torch.empty(2 * C, device=gpu, dtype=torch.float64),
+                   torch.empty(2 * C, device=gpu), 1e-5, 0.1, relu)
+    xf = x.float().requires_grad_(True)
+    gf = g.clone().requires_grad_(True)
+    bf = b.clone().requires_grad_(True)
+    yf = F.batch_norm(xf.permute(0, 3, 1, 2), None, None, gf, bf, True, 0.1, 1e-5).permute(0, 2, 3, 1)
+    rf = None
+    if res:
+        rf = r.float().requires_grad_(True)
+        yf = yf + rf
+    if relu:
+        yf = yf.clamp_min(0)
+    assert rel_err(y, yf) < 1e-2
+    dy = torch.randn_like(x)
+    dx = torch.empty_like(x)
+    dres = torch.empty_like(x) if res else None
+    dg = torch.zeros(C, device=gpu); db = torch.zeros(C, device=gpu)
+    T().bn_backward(dy, y, x, mean, rstd, g, dx, dres, dg, db, torch.empty(2 * C, device=gpu, dtype=torch.float64),
+                    torch.empty(3 * C, device=gpu), relu)
+    grads = torch.autograd.grad(yf, [xf, gf, bf] + ([rf] if res else []), dy.float())
+    assert rel_err(dx, grads[0]) < 2e-2
+    assert rel_err(dg, grads[1]) < 1e-2
+    assert rel_err(db, grads[2]) < 1e-2
+    if res:
+        assert rel_err(dres, grads[3]) < 1e-2
+    xs = x.float().reshape(-1, C)
+    assert rel_err(rm, 0.1 * xs.mean(0)) < 1e-4
+
+
+@pytest.mark.parametrize("D", [512, 1024, 320])
+def test_layernorm(gpu, D):
+    torch.manual_seed(6)
+    rows = 777
+    x = (torch.randn(rows, D, device=gpu) * 2 + 0.5).to(BF)
+    g = torch.rand(D, device=gpu) + 0.5
+    b = torch.randn(D, device=gpu)
+    y = torch.empty_like(x)
+    mean = torch.empty(rows, device=gpu); rstd = torch.empty(rows, device=gpu)
+    T().ln_forward(x, g, b, y, mean, rstd, 1e-5)
+    xf = x.float().requires_grad_(True)
+    gf = g.clone().requires_grad_(True); bf = b.clone().requires_grad_(True)
+    yf = F.layer_norm(xf, (D,), gf, bf, 1e-5)
+    assert rel_err(y, yf) < 1e-2
+    dy = torch.randn_like(x)
+    dx = torch.empty_like(x)
+    dg = torch.zeros(D, device=gpu); db = torch.zeros(D, device=gpu)
+    T().ln_backward(dy, x, g, mean, rstd, dx, dg, db)
+    gx, gg, gb = torch.autograd.grad(yf, [xf, gf, bf], dy.float())
+    assert rel_err(dx, gx) < 2e-2
+    assert rel_err(dg, gg) < 1e-2 and rel_err(db, gb) < 1e-2
+
+
+# ------------------------------------------------------------------ pooling / loss
+def test_maxpool(gpu):
+    torch.manual_seed(7)
+    x = torch.randn(2, 17, 18, 16, device=gpu).to(BF)
+    P = (17 + 2 - 3) // 2 + 1; Q = (18 + 2 - 3) // 2 + 1
+    y = torch.empty(2, P, Q, 16, device=gpu, dtype=BF)
+    idx = torch.empty(2, P, Q, 16, device=gpu, dtype=torch.uint8)
+    T().maxpool_forward(x, y, idx, 3, 3, 2, 1)
+    xf = x.float().permute(0, 3, 1, 2).requires_grad_(True)
+    yf = F.max_pool2d(xf, 3, 2, 1)
+    assert torch.equal(y.float(), yf.permute(0, 2, 3, 1))
+    dy = torch.randn_like(y)
+    dx = torch.empty_like(x)
+    T().maxpool_backward(dy, idx, dx, 3, 3, 2, 1)
+    g, = torch.autograd.grad(yf, [xf], dy.float().permute(0, 3, 1, 2))
+    assert rel_err(dx, g.permute(0, 2, 3, 1)) < 1e-2
+
+
+def test_avgpool(gpu):
+    x = torch.randn(4, 7, 7, 64, device=gpu).to(BF)
+    y = torch.empty(4, 64, device=gpu, dtype=BF)
+    T().avgpool_forward(x, y)
+    assert rel_err(y, x.float().mean((1, 2))) < 1e-2
+    dy = torch.randn(4, 64, device=gpu).to(BF)
+    dx = torch.empty_like(x)
+    T().avgpool_backward(dy, dx)
+    assert rel_err(dx, (dy.float() / 49)[:, None, None, :].expand_as(dx)) < 1e-2
+
+
+@pytest.mark.parametrize("V,smooth", [(1000, 0.0), (32000, 0.1), (999, 0.0)])
+def test_softmax_xent(gpu, V, smooth):
+    torch.manual_seed(8)
+    rows = 300
+    logits = (torch.randn(rows, V, device=gpu) * 3).to(BF)
+    labels = torch.randint(0, V, (rows,), device=gpu)
+    labels[5] = -100
+    loss_rows = torch.empty(rows, device=gpu)
+    dlog = torch.empty_like(logits)
+    T().softmax_xent(logits, labels, dlog, loss_rows, smooth, 1.0 / rows, -100)
+    lf = logits.float().requires_grad_(True)
+    ref = F.cross_entropy(lf, labels, reduction="none", label_smoothing=smooth, ignore_index=-100)
+    assert rel_err(loss_rows, ref) < 1e-4
+    g, = torch.autograd.grad(ref.sum() / rows, [lf])
+    assert rel_err(dlog, g) < 1e-2
+
+
+def test_embedding(gpu):
+    torch.manual_seed(9)
+    table = torch.randn(1000, 64, device=gpu).to(BF)
+    ids = torch.randint(0, 1000, (4, 37), device=gpu)
+    out = torch.empty(4 * 37, 64, device=gpu, dtype=BF)
+    T().embedding_forward(table, ids.reshape(-1), out, 2.0)
+    assert torch.allclose(out.float(), table.float()[ids.reshape(-1)] * 2, rtol=1e-2)
+    g = torch.zeros(1000, 64, device=gpu)
+    dout = torch.randn(4 * 37, 64, device=gpu).to(BF)
+    T().embedding_backward(dout, ids.reshape(-1), g, 2.0)
+    ref = torch.zeros(1000, 64, device=gpu).index_add_(0, ids.reshape(-1), dout.float() * 2)
+    assert rel_err(g, ref) < 1e-5
+
+
+# ------------------------------------------------------------------ optimizers
+def test_sgd_adam(gpu):
+    torch.manual_seed(10)
+    n = 4096 + 64
+    w = torch.randn(n, device=gpu); g = torch.randn(n, device=gpu); m = torch.randn(n, device=gpu)
+    wb = torch.empty(n, device=gpu, dtype=BF)
+    w0, g0, m0 = w.clone(), g.clone(), m.clone()
+    T().sgd_step(w, g, m, wb, 0.1, 0.9, 1e-4, 0.5, False, True)
+    d = g0 * 0.5 + 1e-4 * w0
+    m_ref = 0.9 * m0 + d
+    w_ref = w0 - 0.1 * m_ref
+    assert torch.allclose(m, m_ref, atol=1e-6) and torch.allclose(w, w_ref, atol=1e-6)
+    assert torch.count_nonzero(g) == 0
+    assert torch.equal(wb, w_ref.to(BF))
+    # Adam
+    w = torch.randn(n, device=gpu); g = torch.randn(n, device=gpu)
+    mm = torch.zeros(n, device=gpu); vv = torch.zeros(n, device=gpu)
+    p = w.clone().requires_grad_(True)
+    opt = torch.optim.AdamW([p], lr=1e-3, betas=(0.9, 0.98), eps=1e-9, weight_decay=0.01)
+    gg = g.clone()
+    for step in range(1, 4):
+        p.grad = gg.clone()
+        opt.step()
+        T().adam_step(w, g, mm, vv, wb, 1e-3, 0.9, 0.98, 1e-9, 0.01, step, 1.0, False)
+    assert rel_err(w, p.detach()) < 1e-5
+
+
+# ------------------------------------------------------------------ attention
+def _attn_ref(q, k, v, causal, kv_len=None):
+    qf, kf, vf = (t.float().permute(0, 2, 1, 3) for t in (q, k, v))
+    s = qf @ kf.transpose(-1, -2) / 8.0
+    Sq, Sk = s.shape[-2:]
+    if causal:
+        s = s.masked_fill(torch.triu(torch.ones(Sq, Sk, dtype=torch.bool, device=s.device), 1), float("-inf"))
+    if kv_len is not None:
+        km = torch.arange(Sk, device=s.device)[None, :] >= kv_len[:, None]
+        s = s.masked_fill(km[:, None, None, :], float("-inf"))
+    p = torch.softmax(s, -1)
+    return (p @ vf).permute(0, 2, 1, 3), torch.logsumexp(s, -1)
+
+
+@pytest.mark.parametrize("B,H,Sq,Sk,causal", [(2, 4, 128, 128, False), (2, 8, 128, 128, True),
+                                              (3, 2, 100, 77, False), (1, 4, 65, 65, True),
+                                              (2, 8, 256, 200, False)])
+def test_attention(gpu, B, H, Sq, Sk, causal):
+    if causal and Sq != Sk:
+        pytest.skip()
+    torch.manual_seed(11)
+    qkv = torch.randn(B, Sq, 3, H, 64, device=gpu).to(BF) if Sq == Sk else None
+    if qkv is not None:
+        q, k, v = qkv[:, :, 0], qkv[:, :, 1], qkv[:, :, 2]
+    else:
+        q = torch.randn(B, Sq, H, 64, device=gpu).to(BF)
+        kv = torch.randn(B, Sk, 2, H, 64, device=gpu).to(BF)
+        k, v = kv[:, :, 0], kv[:, :, 1]
+    o = torch.empty(B, Sq, H, 64, device=gpu, dtype=BF)
+    lse = torch.empty(B, H, Sq, device=gpu)
+    T().attn_forward(q, k, v, o, lse, causal, 0.125, None)
+    qf, kf, vf = (t.float().requires_grad_(True) for t in (q, k, v))
+    of, lref = _attn_ref(qf, kf, vf, causal)
+    assert rel_err(o, of) < 1e-2
+    assert rel_err(lse, lref) < 1e-3
+    do = torch.randn_like(o)
+    dq = torch.empty_like(q) if qkv is None else None
+    if qkv is not None:
+        dqkv = torch.empty_like(qkv)
+        dq, dk, dv = dqkv[:, :, 0], dqkv[:, :, 1], dqkv[:, :, 2]
+    else:
+        dkv = torch.empty_like(kv)
+        dk, dv = dkv[:, :, 0], dkv[:, :, 1]
+    T().attn_backward(q, k, v, o, do, lse, dq, dk, dv,
+                      torch.empty(B, Sq, H, 64, device=gpu), torch.empty(B, H, Sq, device=gpu),
+                      causal, 0.125, None)
+    gq, gk, gv = torch.autograd.grad(of, [qf, kf, vf], do.float())
+    assert rel_err(dq, gq) < 2e-2
+    assert rel_err(dk, gk) < 2e-2
+    assert rel_err(dv, gv) < 2e-2
+
+
+def test_attention_kvlen(gpu):
+    torch.manual_seed(12)
+    B, H, S = 3, 2, 96
+    q = torch.randn(B, S, H, 64, device=gpu).to(BF)
+    k = torch.randn(B, S, H, 64, device=gpu).to(BF)
+    v = torch.randn(B, S, H, 64, device=gpu).to(BF)
+    kl = torch.tensor([96, 50, 7], device=gpu, dtype=torch.int32)
+    o = torch.empty_like(q); lse = torch.empty(B, H, S, device=gpu)
+    T().attn_forward(q, k, v, o, lse, False, 0.125, kl)
+    of, _ = _attn_ref(q, k, v, False, kl.long())
+    assert rel_err(o, of) < 1e-2
+
+
+# ------------------------------------------------------------------ LSTM cell
+def test_lstm_cell(gpu):
+    torch.manual_seed(13)
+    B, Hd = 16, 128
+    gates = torch.randn(B, 4 * Hd, device=gpu)
+    c_prev = torch.randn(B, Hd, device=gpu)
+    c = torch.empty(B, Hd, device=gpu); h = torch.empty(B, Hd, device=gpu, dtype=BF)
+    hf = torch.empty(B, Hd, device=gpu); act = torch.empty(B, 5 * Hd, device=gpu)
+    T().lstm_cell_forward(gates, c_prev, c, h, hf, act)
+    gr = gates.clone().requires_grad_(True); cr = c_prev.clone().requires_grad_(True)
+    i, f, gg, o = gr.chunk(4, 1)
+    c_ref = torch.sigmoid(f) * cr + torch.sigmoid(i) * torch.tanh(gg)
+    h_ref = torch.sigmoid(o) * torch.tanh(c_ref)
+    assert rel_err(c, c_ref) < 1e-5 and rel_err(hf, h_ref) < 1e-5
+    dh = torch.randn(B, Hd, device=gpu); dcn = torch.randn(B, Hd, device=gpu)
+    dG = torch.empty(B, 4 * Hd, device=gpu); dcp = torch.empty(B, Hd, device=gpu)
+    T().lstm_cell_backward(act, c_prev, dh, dcn, dG, dcp, None)
+    g1, g2 = torch.autograd.grad([h_ref, c_ref], [gr, cr], [dh, dcn])
+    assert rel_err(dG, g1) < 1e-4 and rel_err(dcp, g2) < 1e-4
+
+
+# ------------------------------------------------------------------ checkpoint engine
+def test_ckpt_engine_roundtrip(gpu):
+    eng = torch.classes.tam.CkptEngine(0, 64 << 20)
+    src = torch.randn(3 << 20, device=gpu)
+    h = eng.spill(src)
+    h2 = eng.spill(src[:1000].contiguous())
+    host = eng.host_view(h)
+    assert torch.equal(host, src.cpu())
+    dst = torch.empty_like(src)
+    eng.restore(h, dst)
+    torch.cuda.synchronize()
+    assert torch.equal(dst, src)
+    st = eng.stats()
+    assert st[2] >= src.numel() * 4
+    eng.release(h)
+    eng.release(h2)
+    assert eng.stats()[1] == 0

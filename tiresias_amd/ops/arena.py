@@ -1,0 +1,141 @@
+"""Flat parameter arena: the MI355X-native parameter store of one job.
+
+Every job owns exactly four device buffers::
+
+    master  fp32 [N]   optimizer-owned weights
+    shadow  bf16 [N]   compute copy every kernel reads (rewritten by the fused
+                       optimizer step, never by a separate cast pass)
+    grad    fp32 [N]   backward kernels ACCUMULATE straight into it (conv wgrad
+                       split-K atomics, GEMM epilogues, BN/LN reductions); the
+                       bucketed all-reduce reduces it in place; the optimizer
+                       step zeroes it
+    state   fp32 [k*N] optimizer state (momentum / Adam m,v)
+
+so a checkpoint is four memcpys, a preemption spill is one contiguous D2H per
+buffer, a DDP bucket is a contiguous slice, and the optimizer is one launch.
+
+Layout: weight-decayed params first (in registration = forward order), then
+the no-decay params (norm scales/shifts, biases). Every param is padded to
+64 elements so each view starts 256-B aligned (16-B vector loads).
+"""
+from __future__ import annotations
+
+import math
+from dataclasses import dataclass, field
+from typing import Callable, List, Optional, Sequence
+
+import torch
+
+_ALIGN = 64
+
+
+@dataclass
+class Param:
+    name: str
+    shape: tuple
+    init: str = "normal"
+    std: float = 0.02
+    decay: bool = True
+    fp32_compute: bool = False     # kernels read the fp32 master (norm params)
+    offset: int = 0
+    numel: int = 0
+    # views (set by Arena.materialize)
+    w: Optional[torch.Tensor] = None        # bf16 shadow view
+    master: Optional[torch.Tensor] = None   # fp32 master view
+    grad: Optional[torch.Tensor] = None     # fp32 grad view
+    arena: Optional["Arena"] = field(default=None, repr=False)
+
+    @property
+    def value(self) -> torch.Tensor:
+        """The tensor kernels consume (fp32 master for norm params, bf16 shadow otherwise)."""
+        return self.master if self.fp32_compute else self.w
+
+    def grad_ready(self) -> None:
+        if self.arena is not None and self.arena.on_grad_ready is not None:
+            self.arena.on_grad_ready(self)
+
+
+def _padded(n: int) -> int:
+    return (n + _ALIGN - 1) // _ALIGN * _ALIGN
+
+
+class Arena:
+    def __init__(self, device: torch.device | str = "cpu", seed: int = 0):
+        self.device = torch.device(device)
+        self.params: List[Param] = []
+        self.seed = seed
+        self.master = self.shadow = self.grad = None
+        self.numel = 0
+        self.n_decay = 0
+        self.on_grad_ready: Optional[Callable[[Param], None]] = None
+        # autograd anchor: every param-consuming op takes it as an input so
+        # outputs require grad even when the data input does not.
+        self.token = torch.zeros(1, device=self.device, requires_grad=True)
+
+    # ----------------------------------------------------------------- build
+    def add(self, name: str, shape: Sequence[int], init: str = "normal", std: float = 0.02,
+            decay: bool = True, fp32_compute: bool = False) -> Param:
+        p = Param(name=name, shape=tuple(int(s) for s in shape), init=init, std=std, decay=decay,
+                  fp32_compute=fp32_compute)
+        p.numel = int(math.prod(p.shape))
+        p.arena = self
+        self.params.append(p)
+        return p
+
+    def _order(self) -> List[Param]:
+        return [p for p in self.params if p.decay] + [p for p in self.params if not p.decay]
+
+    def materialize(self) -> "Arena":
+        off = 0
+        order = self._order()
+        for p in order:
+            p.offset = off
+            off += _padded(p.numel)
+            if p.decay:
+                self.n_decay = off
+        self.numel = max(off, _ALIGN)
+        dev = self.device
+        self.master = torch.zeros(self.numel, dtype=torch.float32, device=dev)
+        self.shadow = torch.zeros(self.numel, dtype=torch.bfloat16, device=dev)
+        self.grad = torch.zeros(self.numel, dtype=torch.float32, device=dev)
+        g = torch.Generator(device="cpu")
+        g.manual_seed(self.seed)
+        for p in order:
+            p.master = self.master[p.offset:p.offset + p.numel].view(p.shape)
+            p.w = self.shadow[p.offset:p.offset + p.numel].view(p.shape)
+            p.grad = self.grad[p.offset:p.offset + p.numel].view(p.shape)
+            p.master.copy_(self._init_value(p, g))
+        self.shadow.copy_(self.master.to(torch.bfloat16))
+        return self
+
+    @staticmethod
+    def _init_value(p: Param, g: torch.Generator) -> torch.Tensor:
+        if p.init == "zeros":
+            return torch.zeros(p.shape)
+        if p.init == "ones":
+            return torch.ones(p.shape)
+        if p.init == "kaiming":
+            # fan_in over all dims but the first (conv [K,R,S,C], linear [out,in])
+            fan_in = max(1, p.numel // p.shape[0])
+            return torch.randn(p.shape, generator=g) * math.sqrt(2.0 / fan_in)
+        if p.init == "xavier":
+            fan_in = max(1, p.numel // p.shape[0])
+            fan_out = p.shape[0]
+            a = math.sqrt(6.0 / (fan_in + fan_out))
+            return (torch.rand(p.shape, generator=g) * 2 - 1) * a
+        if p.init == "uniform":
+            return (torch.rand(p.shape, generator=g) * 2 - 1) * p.std
+        return torch.randn(p.shape, generator=g) * p.std
+
+    # ----------------------------------------------------------------- state
+    def zero_grad(self) -> None:
+        self.grad.zero_()
+
+    def state_bytes(self) -> int:
+        return self.numel * (4 + 2 + 4)
+
+    def named(self):
+        return {p.name: p for p in self.params}
+
+    def sync_shadow(self) -> None:
+        self.shadow.copy_(self.master.to(torch.bfloat16))

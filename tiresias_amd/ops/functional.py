@@ -1,0 +1,583 @@
+"""Autograd-aware ops over the HIP kernel library.
+
+Conventions (MI355X-first):
+  * activations are bf16; convolutions are NHWC ([N,H,W,C], C % 8 == 0);
+  * parameters come from an :class:`~tiresias_amd.ops.arena.Arena`; backward
+    kernels ACCUMULATE weight gradients directly into the arena's flat fp32
+    grad buffer (no per-param grad tensors, no copies before the all-reduce)
+    and then call ``param.grad_ready()`` so the DDP bucketer can launch the
+    bucket's RCCL all-reduce while backward continues;
+  * ReLU is fused into the producing kernel's epilogue; its backward mask is
+    applied by the *consumer's* input-gradient epilogue when the consumer is
+    told ``in_relu=True`` (no separate relu-backward pass).
+
+On GPU tensors every op runs the hand-written gfx950 kernels (the library is
+required and loaded eagerly); on CPU tensors the ops run an fp32 PyTorch
+reference of the same math (CPU test-suite, gloo rehearsals, numerics refs).
+"""
+from __future__ import annotations
+
+import math
+from typing import Optional, Tuple
+
+import torch
+import torch.nn.functional as F
+from torch.autograd import Function
+
+from . import _lib
+from .arena import Param
+
+BF16 = torch.bfloat16
+
+
+def _T():
+    return _lib.ops()
+
+
+def _cpu_gemm_f32(a: torch.Tensor, b: torch.Tensor) -> torch.Tensor:
+    return a.float() @ b.float()
+
+
+# ============================================================ Linear
+class _Linear(Function):
+    @staticmethod
+    def forward(ctx, x, token, w: Param, b: Optional[Param], relu: bool, in_relu: bool,
+                mask_own_relu: bool):
+        M = x.shape[0]
+        out = w.shape[0]
+        if x.is_cuda:
+            y = torch.empty(M, out, dtype=BF16, device=x.device)
+            _T().gemm(x, True, w.w, True, y, 0, b.w if b is not None else None, relu, None, 1.0, False)
+        else:
+            yf = _cpu_gemm_f32(x, w.w.t())
+            if b is not None:
+                yf = yf + b.w.float()
+            if relu:
+                yf = yf.clamp_min(0)
+            y = yf.to(BF16)
+        ctx.w, ctx.b, ctx.relu, ctx.in_relu, ctx.mask_own = w, b, relu, in_relu, mask_own_relu
+        ctx.save_for_backward(x, y if (relu and mask_own_relu) else None)
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        x, y = ctx.saved_tensors
+        w, b = ctx.w, ctx.b
+        dy = dy.contiguous()
+        if y is not None:
+            if dy.is_cuda:
+                dyr = torch.empty_like(dy)
+                _T().relu_backward(dy, y, dyr)
+                dy = dyr
+            else:
+                dy = (dy.float() * (y.float() > 0)).to(BF16)
+        dx = None
+        if ctx.needs_input_grad[0]:
+            if dy.is_cuda:
+                dx = torch.empty_like(x)
+                _T().gemm(dy, True, w.w, False, dx, 0, None, False, x if ctx.in_relu else None, 1.0, False)
+            else:
+                dxf = _cpu_gemm_f32(dy, w.w)
+                if ctx.in_relu:
+                    dxf = dxf * (x.float() > 0)
+                dx = dxf.to(BF16)
+        if dy.is_cuda:
+            _T().gemm(dy, False, x, False, w.grad, 1, None, False, None, 1.0, True)
+            if b is not None:
+                _T().colsum(dy, b.grad)
+        else:
+            w.grad += _cpu_gemm_f32(dy.t(), x)
+            if b is not None:
+                b.grad += dy.float().sum(0)
+        w.grad_ready()
+        if b is not None:
+            b.grad_ready()
+        return dx, None, None, None, None, None, None
+
+
+def linear(x: torch.Tensor, w: Param, b: Optional[Param] = None, relu: bool = False,
+           in_relu: bool = False, mask_own_relu: bool = True) -> torch.Tensor:
+    """y = x W^T (+b) (relu). x: [..., in] bf16 -> [..., out].
+
+    in_relu: x is a ReLU output; mask the input-gradient by (x > 0).
+    mask_own_relu: apply this layer's own ReLU mask in backward (set False when
+    the consumer was built with in_relu=True, which already masks).
+    """
+    shp = x.shape
+    x2 = x.reshape(-1, shp[-1])
+    if not x2.is_contiguous():
+        x2 = x2.contiguous()
+    y = _Linear.apply(x2, w.arena.token, w, b, relu, in_relu, mask_own_relu)
+    return y.view(*shp[:-1], w.shape[0])
+
+
+# ============================================================ Conv2d (NHWC)
+def _conv_out(h: int, k: int, s: int, p: int, d: int = 1) -> int:
+    return (h + 2 * p - d * (k - 1) - 1) // s + 1
+
+
+class _Conv(Function):
+    @staticmethod
+    def forward(ctx, x, token, w: Param, b: Optional[Param], stride: int, pad: int, relu: bool,
+                in_relu: bool, mask_own_relu: bool):
+        N, H, W, C = x.shape
+        K, R, S, _ = w.shape
+        P, Q = _conv_out(H, R, stride, pad), _conv_out(W, S, stride, pad)
+        if x.is_cuda:
+            y = torch.empty(N, P, Q, K, dtype=BF16, device=x.device)
+            _T().conv_fwd(x, w.w, y, stride, pad, 1, b.w if b is not None else None, relu)
+        else:
+            yf = F.conv2d(x.float().permute(0, 3, 1, 2), w.w.float().permute(0, 3, 1, 2),
+                          b.w.float() if b is not None else None, stride=stride, padding=pad)
+            if relu:
+                yf = yf.clamp_min(0)
+            y = yf.permute(0, 2, 3, 1).contiguous().to(BF16)
+        ctx.w, ctx.b, ctx.stride, ctx.pad, ctx.in_relu = w, b, stride, pad, in_relu
+        ctx.save_for_backward(x, y if (relu and mask_own_relu) else None)
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        x, y = ctx.saved_tensors
+        w, b, st, pd = ctx.w, ctx.b, ctx.stride, ctx.pad
+        dy = dy.contiguous()
+        if y is not None:
+            if dy.is_cuda:
+                dyr = torch.empty_like(dy)
+                _T().relu_backward(dy, y, dyr)
+                dy = dyr
+            else:
+                dy = (dy.float() * (y.float() > 0)).to(BF16)
+        dx = None
+        if dy.is_cuda:
+            if ctx.needs_input_grad[0]:
+                dx = torch.empty_like(x)
+                wt = torch.empty_like(w.w)
+                _T().conv_dgrad(dy, w.w, wt, dx, st, pd, 1, x if ctx.in_relu else None)
+            _T().conv_wgrad(dy, x, w.grad, st, pd, 1, 1)
+            if b is not None:
+                _T().colsum(dy, b.grad)
+        else:
+            xf = x.float().permute(0, 3, 1, 2).requires_grad_(ctx.needs_input_grad[0])
+            wf = w.w.float().permute(0, 3, 1, 2).requires_grad_(True)
+            with torch.enable_grad():
+                yf = F.conv2d(xf, wf, stride=st, padding=pd)
+                grads = torch.autograd.grad(yf, [xf, wf] if ctx.needs_input_grad[0] else [wf],
+                                            dy.float().permute(0, 3, 1, 2))
+            if ctx.needs_input_grad[0]:
+                dxf = grads[0].permute(0, 2, 3, 1)
+                if ctx.in_relu:
+                    dxf = dxf * (x.float() > 0)
+                dx = dxf.contiguous().to(BF16)
+            w.grad += grads[-1].permute(0, 2, 3, 1)
+            if b is not None:
+                b.grad += dy.float().sum((0, 1, 2))
+        w.grad_ready()
+        if b is not None:
+            b.grad_ready()
+        return dx, None, None, None, None, None, None, None, None
+
+
+def conv2d(x: torch.Tensor, w: Param, b: Optional[Param] = None, stride: int = 1, pad: int = 0,
+           relu: bool = False, in_relu: bool = False, mask_own_relu: bool = True) -> torch.Tensor:
+    """NHWC conv, weights [K,R,S,C]."""
+    if not x.is_contiguous():
+        x = x.contiguous()
+    return _Conv.apply(x, w.arena.token, w, b, stride, pad, relu, in_relu, mask_own_relu)
+
+
+# ============================================================ BatchNorm (NHWC)
+class _BN(Function):
+    @staticmethod
+    def forward(ctx, x, res, token, g: Param, b: Param, run_mean, run_var, relu: bool, eps: float,
+                momentum: float, training: bool):
+        C = x.shape[-1]
+        if x.is_cuda:
+            y = torch.empty_like(x)
+            if training:
+                mean = torch.empty(C, dtype=torch.float32, device=x.device)
+                rstd = torch.empty_like(mean)
+                ws_d = torch.empty(2 * C, dtype=torch.float64, device=x.device)
+                ws_f = torch.empty(2 * C, dtype=torch.float32, device=x.device)
+                _T().bn_forward(x, res, y, g.master, b.master, run_mean, run_var, mean, rstd, ws_d,
+                                ws_f, eps, momentum, relu)
+            else:
+                rstd_i = torch.rsqrt(run_var + eps)
+                scale = g.master * rstd_i
+                shift = b.master - run_mean * scale
+                mean, rstd = run_mean, rstd_i
+                y = _bn_infer_gpu(x, res, scale, shift, relu)
+        else:
+            xf = x.float().reshape(-1, C)
+            if training:
+                mean = xf.mean(0)
+                var = xf.var(0, unbiased=False)
+                if run_mean is not None:
+                    n = xf.shape[0]
+                    run_mean.mul_(1 - momentum).add_(momentum * mean)
+                    run_var.mul_(1 - momentum).add_(momentum * var * n / max(n - 1, 1))
+            else:
+                mean, var = run_mean, run_var
+            rstd = torch.rsqrt(var + eps)
+            yf = (xf - mean) * rstd * g.master + b.master
+            if res is not None:
+                yf = yf + res.float().reshape(-1, C)
+            if relu:
+                yf = yf.clamp_min(0)
+            y = yf.reshape(x.shape).to(BF16)
+        ctx.g, ctx.b, ctx.relu, ctx.has_res = g, b, relu, res is not None
+        ctx.save_for_backward(x, y if relu else None, mean, rstd)
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        x, y, mean, rstd = ctx.saved_tensors
+        g, b = ctx.g, ctx.b
+        dy = dy.contiguous()
+        C = x.shape[-1]
+        if dy.is_cuda:
+            dx = torch.empty_like(x)
+            dres = torch.empty_like(x) if ctx.has_res and ctx.relu else None
+            ws_d = torch.empty(2 * C, dtype=torch.float64, device=x.device)
+            ws_f = torch.empty(3 * C, dtype=torch.float32, device=x.device)
+            _T().bn_backward(dy, y, x, mean, rstd, g.master, dx, dres, g.grad, b.grad, ws_d, ws_f,
+                             ctx.relu)
+            if ctx.has_res and not ctx.relu:
+                dres = dy
+        else:
+            dyf = dy.float().reshape(-1, C)
+            if ctx.relu:
+                dyf = dyf * (y.float().reshape(-1, C) > 0)
+            xh = (x.float().reshape(-1, C) - mean) * rstd
+            M = dyf.shape[0]
+            sdy = dyf.sum(0)
+            sdyx = (dyf * xh).sum(0)
+            g.grad += sdyx
+            b.grad += sdy
+            dxf = g.master * rstd * (dyf - sdy / M - xh * sdyx / M)
+            dx = dxf.reshape(x.shape).to(BF16)
+            dres = dyf.reshape(x.shape).to(BF16) if ctx.has_res else None
+        g.grad_ready()
+        b.grad_ready()
+        return dx, dres, None, None, None, None, None, None, None, None, None
+
+
+def _bn_infer_gpu(x, res, scale, shift, relu):
+    # inference-only path (not on the training hot path)
+    yf = x.float() * scale + shift
+    if res is not None:
+        yf = yf + res.float()
+    if relu:
+        yf = yf.clamp_min(0)
+    return yf.to(BF16)
+
+
+def batchnorm(x: torch.Tensor, g: Param, b: Param, run_mean: Optional[torch.Tensor] = None,
+              run_var: Optional[torch.Tensor] = None, relu: bool = False,
+              residual: Optional[torch.Tensor] = None, eps: float = 1e-5, momentum: float = 0.1,
+              training: bool = True) -> torch.Tensor:
+    """y = relu(BN(x) + residual) over the last (channel) dim of an NHWC tensor."""
+    if not x.is_contiguous():
+        x = x.contiguous()
+    if residual is not None and not residual.is_contiguous():
+        residual = residual.contiguous()
+    return _BN.apply(x, residual, g.arena.token, g, b, run_mean, run_var, relu, eps, momentum,
+                     training)
+
+
+# ============================================================ LayerNorm
+class _LN(Function):
+    @staticmethod
+    def forward(ctx, x, token, g: Param, b: Param, eps: float):
+        D = x.shape[-1]
+        rows = x.numel() // D
+        if x.is_cuda:
+            y = torch.empty_like(x)
+            mean = torch.empty(rows, dtype=torch.float32, device=x.device)
+            rstd = torch.empty_like(mean)
+            _T().ln_forward(x, g.master, b.master, y, mean, rstd, eps)
+        else:
+            xf = x.float().reshape(rows, D)
+            mean = xf.mean(1)
+            rstd = torch.rsqrt(xf.var(1, unbiased=False) + eps)
+            y = (((xf - mean[:, None]) * rstd[:, None]) * g.master + b.master).reshape(x.shape).to(BF16)
+        ctx.g, ctx.b = g, b
+        ctx.save_for_backward(x, mean, rstd)
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        x, mean, rstd = ctx.saved_tensors
+        g, b = ctx.g, ctx.b
+        dy = dy.contiguous()
+        D = x.shape[-1]
+        if dy.is_cuda:
+            dx = torch.empty_like(x)
+            _T().ln_backward(dy, x, g.master, mean, rstd, dx, g.grad, b.grad)
+        else:
+            rows = x.numel() // D
+            xh = (x.float().reshape(rows, D) - mean[:, None]) * rstd[:, None]
+            dyf = dy.float().reshape(rows, D)
+            g.grad += (dyf * xh).sum(0)
+            b.grad += dyf.sum(0)
+            gd = dyf * g.master
+            dxf = rstd[:, None] * (gd - gd.mean(1, keepdim=True) - xh * (gd * xh).mean(1, keepdim=True))
+            dx = dxf.reshape(x.shape).to(BF16)
+        g.grad_ready()
+        b.grad_ready()
+        return dx, None, None, None, None
+
+
+def layernorm(x: torch.Tensor, g: Param, b: Param, eps: float = 1e-5) -> torch.Tensor:
+    if not x.is_contiguous():
+        x = x.contiguous()
+    return _LN.apply(x, g.arena.token, g, b, eps)
+
+
+# ============================================================ pooling
+class _MaxPool(Function):
+    @staticmethod
+    def forward(ctx, x, k: int, s: int, p: int):
+        N, H, W, C = x.shape
+        P, Q = _conv_out(H, k, s, p), _conv_out(W, k, s, p)
+        if x.is_cuda:
+            y = torch.empty(N, P, Q, C, dtype=BF16, device=x.device)
+            idx = torch.empty(N, P, Q, C, dtype=torch.uint8, device=x.device)
+            _T().maxpool_forward(x, y, idx, k, k, s, p)
+            ctx.save_for_backward(idx)
+        else:
+            yf, ind = F.max_pool2d(x.float().permute(0, 3, 1, 2), k, s, p, return_indices=True)
+            y = yf.permute(0, 2, 3, 1).contiguous().to(BF16)
+            ctx.save_for_backward(ind)
+        ctx.cfg = (k, s, p, x.shape)
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        (idx,) = ctx.saved_tensors
+        k, s, p, shape = ctx.cfg
+        dy = dy.contiguous()
+        if dy.is_cuda:
+            dx = torch.empty(shape, dtype=BF16, device=dy.device)
+            _T().maxpool_backward(dy, idx, dx, k, k, s, p)
+        else:
+            N, H, W, C = shape
+            dxf = F.max_unpool2d(dy.float().permute(0, 3, 1, 2), idx, k, s, p, output_size=(H, W))
+            dx = dxf.permute(0, 2, 3, 1).contiguous().to(BF16)
+        return dx, None, None, None
+
+
+def maxpool2d(x: torch.Tensor, k: int, s: int, p: int = 0) -> torch.Tensor:
+    return _MaxPool.apply(x.contiguous(), k, s, p)
+
+
+class _AvgPool(Function):
+    @staticmethod
+    def forward(ctx, x):
+        N, H, W, C = x.shape
+        if x.is_cuda:
+            y = torch.empty(N, C, dtype=BF16, device=x.device)
+            _T().avgpool_forward(x, y)
+        else:
+            y = x.float().mean((1, 2)).to(BF16)
+        ctx.shape = x.shape
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        N, H, W, C = ctx.shape
+        dy = dy.contiguous()
+        if dy.is_cuda:
+            dx = torch.empty(ctx.shape, dtype=BF16, device=dy.device)
+            _T().avgpool_backward(dy, dx)
+        else:
+            dx = (dy.float()[:, None, None, :] / (H * W)).expand(N, H, W, C).contiguous().to(BF16)
+        return dx
+
+
+def global_avgpool(x: torch.Tensor) -> torch.Tensor:
+    return _AvgPool.apply(x.contiguous())
+
+
+# ============================================================ loss
+def softmax_xent(logits: torch.Tensor, labels: torch.Tensor, smoothing: float = 0.0,
+                 ignore_index: int = -100) -> Tuple[torch.Tensor, torch.Tensor]:
+    """Fused softmax cross-entropy. Returns (mean loss, dlogits) WITHOUT autograd:
+    the loss is the graph sink, so the training step calls
+    ``logits.backward(dlogits)`` directly (no extra scale pass over the logits).
+    """
+    V = logits.shape[-1]
+    l2 = logits.reshape(-1, V).contiguous()
+    lab = labels.reshape(-1).contiguous()
+    rows = l2.shape[0]
+    count = (lab != ignore_index).sum().clamp_min(1)
+    if l2.is_cuda:
+        loss_rows = torch.empty(rows, dtype=torch.float32, device=l2.device)
+        dlog = torch.empty_like(l2)
+        # grad scale must be a host float: use the static row count when no
+        # ignore_index rows are expected, else the exact count (one sync)
+        if ignore_index is None or ignore_index < 0 and not bool((lab == ignore_index).any()):
+            n = rows
+        else:
+            n = int(count.item())
+        _T().softmax_xent(l2.detach(), lab, dlog, loss_rows, smoothing, 1.0 / n,
+                          ignore_index if ignore_index is not None else -(1 << 62))
+        loss = loss_rows.sum() / n
+        return loss, dlog.view(logits.shape)
+    lf = l2.detach().float()
+    logp = torch.log_softmax(lf, -1)
+    valid = (lab != ignore_index)
+    safe = torch.where(valid, lab, torch.zeros_like(lab))
+    nll = -logp.gather(1, safe[:, None])[:, 0]
+    smooth = -logp.mean(1)
+    lrow = ((1 - smoothing) * nll + smoothing * smooth) * valid
+    n = int(count.item())
+    loss = lrow.sum() / n
+    p = logp.exp()
+    tgt = torch.zeros_like(p).scatter_(1, safe[:, None], 1.0) * (1 - smoothing) + smoothing / V
+    dlog = ((p - tgt) * valid[:, None] / n).to(BF16)
+    return loss, dlog.view(logits.shape)
+
+
+# ============================================================ embedding
+class _Embed(Function):
+    @staticmethod
+    def forward(ctx, ids, token, table: Param, scale: float):
+        D = table.shape[1]
+        flat = ids.reshape(-1).contiguous()
+        if flat.is_cuda:
+            out = torch.empty(flat.numel(), D, dtype=BF16, device=flat.device)
+            _T().embedding_forward(table.w, flat, out, scale)
+        else:
+            out = (table.w.float()[flat] * scale).to(BF16)
+        ctx.table, ctx.scale = table, scale
+        ctx.save_for_backward(flat)
+        return out.view(*ids.shape, D)
+
+    @staticmethod
+    def backward(ctx, dout):
+        (flat,) = ctx.saved_tensors
+        t = ctx.table
+        d2 = dout.reshape(-1, t.shape[1]).contiguous()
+        if d2.is_cuda:
+            _T().embedding_backward(d2, flat, t.grad, ctx.scale)
+        else:
+            t.grad.index_add_(0, flat, d2.float() * ctx.scale)
+        t.grad_ready()
+        return None, None, None, None
+
+
+def embedding(ids: torch.Tensor, table: Param, scale: float = 1.0) -> torch.Tensor:
+    return _Embed.apply(ids, table.arena.token, table, scale)
+
+
+# ============================================================ attention
+def _attn_ref(q, k, v, causal, scale, kv_len):
+    # q [B,Sq,H,64], k/v [B,Sk,H,64] -> o [B,Sq,H,64], lse [B,H,Sq]
+    qf, kf, vf = (t.float().permute(0, 2, 1, 3) for t in (q, k, v))
+    s = qf @ kf.transpose(-1, -2) * scale
+    Sq, Sk = s.shape[-2], s.shape[-1]
+    mask = torch.zeros(Sq, Sk, dtype=torch.bool, device=s.device)
+    if causal:
+        mask = torch.triu(torch.ones(Sq, Sk, dtype=torch.bool, device=s.device), 1)
+    s = s.masked_fill(mask, float("-inf"))
+    if kv_len is not None:
+        km = torch.arange(Sk, device=s.device)[None, :] >= kv_len[:, None].to(s.device)
+        s = s.masked_fill(km[:, None, None, :], float("-inf"))
+    lse = torch.logsumexp(s, -1)
+    p = torch.exp(s - lse[..., None])
+    o = (p @ vf).permute(0, 2, 1, 3)
+    return o, lse
+
+
+class _Attn(Function):
+    """q_src: [B,Sq,nq*H*64], kv_src: [B,Sk,nkv*H*64]; q at slot q_slot of q_src,
+    k / v at slots k_slot / v_slot of kv_src (self-attention passes the same
+    packed qkv tensor for both, slots 0/1/2). Gradients come back packed."""
+
+    @staticmethod
+    def forward(ctx, q_src, kv_src, H: int, q_slot: int, nq: int, k_slot: int, v_slot: int,
+                nkv: int, causal: bool, kv_len):
+        same = q_src is kv_src
+        B, Sq, _ = q_src.shape
+        Sk = kv_src.shape[1]
+        qv = q_src.view(B, Sq, nq, H, 64)[:, :, q_slot]
+        kvv = kv_src.view(B, Sk, nkv, H, 64)
+        kv_, vv = kvv[:, :, k_slot], kvv[:, :, v_slot]
+        scale = 1.0 / math.sqrt(64)
+        if q_src.is_cuda:
+            o = torch.empty(B, Sq, H, 64, dtype=BF16, device=q_src.device)
+            lse = torch.empty(B, H, Sq, dtype=torch.float32, device=q_src.device)
+            _T().attn_forward(qv, kv_, vv, o, lse, causal, scale, kv_len)
+        else:
+            of, lse = _attn_ref(qv, kv_, vv, causal, scale, kv_len)
+            o = of.to(BF16).contiguous()
+        ctx.cfg = (same, H, q_slot, nq, k_slot, v_slot, nkv, causal, scale)
+        ctx.save_for_backward(q_src, kv_src, o, lse, kv_len)
+        return o.view(B, Sq, H * 64)
+
+    @staticmethod
+    def backward(ctx, do):
+        q_src, kv_src, o, lse, kv_len = ctx.saved_tensors
+        same, H, q_slot, nq, k_slot, v_slot, nkv, causal, scale = ctx.cfg
+        B, Sq, _ = q_src.shape
+        Sk = kv_src.shape[1]
+        do = do.contiguous().view(B, Sq, H, 64)
+        alloc = torch.empty_like if q_src.is_cuda else torch.zeros_like
+        dq_src = alloc(q_src)
+        dkv_src = dq_src if same else alloc(kv_src)
+        qv = q_src.view(B, Sq, nq, H, 64)[:, :, q_slot]
+        kvv = kv_src.view(B, Sk, nkv, H, 64)
+        dqv = dq_src.view(B, Sq, nq, H, 64)[:, :, q_slot]
+        dkvv = dkv_src.view(B, Sk, nkv, H, 64)
+        if q_src.is_cuda:
+            dq_acc = torch.empty(B, Sq, H, 64, dtype=torch.float32, device=q_src.device)
+            delta = torch.empty(B, H, Sq, dtype=torch.float32, device=q_src.device)
+            _T().attn_backward(qv, kvv[:, :, k_slot], kvv[:, :, v_slot], o, do, lse, dqv,
+                               dkvv[:, :, k_slot], dkvv[:, :, v_slot], dq_acc, delta, causal, scale,
+                               kv_len)
+        else:
+            qf = qv.float().requires_grad_(True)
+            kf = kvv[:, :, k_slot].float().requires_grad_(True)
+            vf = kvv[:, :, v_slot].float().requires_grad_(True)
+            with torch.enable_grad():
+                of, _ = _attn_ref(qf, kf, vf, causal, scale, kv_len)
+                gq, gk, gv = torch.autograd.grad(of, [qf, kf, vf], do.float())
+            dqv.copy_(gq.to(BF16))
+            dkvv[:, :, k_slot].copy_(gk.to(BF16))
+            dkvv[:, :, v_slot].copy_(gv.to(BF16))
+        if same:
+            return dq_src, None, None, None, None, None, None, None, None, None
+        return dq_src, dkv_src, None, None, None, None, None, None, None, None
+
+
+def self_attention(qkv: torch.Tensor, heads: int, causal: bool = False,
+                   kv_len: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """qkv: [B,S,3*H*64] packed projection output -> [B,S,H*64]."""
+    qkv = qkv.contiguous()
+    return _Attn.apply(qkv, qkv, heads, 0, 3, 1, 2, 3, causal, kv_len)
+
+
+def cross_attention(q: torch.Tensor, kv: torch.Tensor, heads: int,
+                    kv_len: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """q: [B,Sq,H*64], kv: [B,Sk,2*H*64] -> [B,Sq,H*64]."""
+    return _Attn.apply(q, kv, heads, 0, 1, 0, 1, 2, False, kv_len)
+
+
+# ============================================================ residual add
+class _Add(Function):
+    @staticmethod
+    def forward(ctx, a, b):
+        if a.is_cuda and a.numel() % 8 == 0:
+            y = torch.empty_like(a)
+            _T().add(a.contiguous(), b.contiguous(), y)
+            return y
+        return (a.float() + b.float()).to(BF16)
+
+    @staticmethod
+    def backward(ctx, dy):
+        return dy, dy
+
+
+def add(a: torch.Tensor, b: torch.Tensor) -> torch.Tensor:
+    return _Add.apply(a, b)
