@@ -58,7 +58,8 @@ void gemm_op(const Tensor& a, bool a_kmajor, const Tensor& b, bool b_kmajor, con
   const int64_t Kb = b_kmajor ? b.size(1) : b.size(0);
   TORCH_CHECK(K == Kb, "tam.gemm: K mismatch ", K, " vs ", Kb);
   TORCH_CHECK(c.size(0) == M && c.size(1) == N, "tam.gemm: C shape mismatch");
-  TORCH_CHECK(K % 8 == 0, "tam.gemm: K must be a multiple of 8");
+  TORCH_CHECK((!a_kmajor && !b_kmajor) || K % 8 == 0,
+              "tam.gemm: K must be a multiple of 8 for a K-major operand");
   TORCH_CHECK(a_kmajor || M % 8 == 0, "tam.gemm: M-major A needs M % 8 == 0");
   TORCH_CHECK(b_kmajor || N % 8 == 0, "tam.gemm: N-major B needs N % 8 == 0");
   TORCH_CHECK(a.stride(0) % 8 == 0 && b.stride(0) % 8 == 0, "tam.gemm: 16-byte aligned rows needed");

@@ -1,0 +1,165 @@
+"""One job's training engine on one GPU rank (a DDP gang member).
+
+A ``Trainer`` owns the job's flat parameter arena, optimizer state, static
+synthetic batch, the bucketed all-reduce (when the gang spans >1 GPU) and an
+optional hipGraph of forward+backward. It is what the cluster executor
+time-slices: ``run(iters)`` advances the job, ``state_tensors()`` exposes the
+four flat buffers a preemption checkpoints, ``release()`` frees HBM.
+"""
+from __future__ import annotations
+
+import time
+from typing import Dict, List, Optional
+
+import torch
+
+from ..models import MODELS, make_model, samples_per_batch, synthetic_batch
+from ..ops import _lib
+from ..ops import functional as Fx
+from ..ops.arena import Arena
+from ..parallel.ddp import GradBucketer
+
+
+class Trainer:
+    def __init__(self, model: str, device, batch: Optional[int] = None, group=None, seed: int = 0,
+                 data_seed: Optional[int] = None, use_graph: bool = False, bucket_mb: float = 32.0,
+                 model_kwargs: Optional[dict] = None, lr: Optional[float] = None):
+        self.model_name = model
+        self.spec = MODELS[model]
+        self.device = torch.device(device)
+        if self.device.type == "cuda":
+            _lib.load(required=True)
+        self.batch = batch or self.spec.batch
+        self.arena = Arena(self.device, seed=seed)
+        self.model = make_model(model, self.arena, **(model_kwargs or {}))
+        self.arena.materialize()
+        n = self.arena.numel
+        self.opt = self.spec.opt
+        self.lr = lr if lr is not None else self.spec.lr
+        if self.opt == "sgd":
+            self.opt_state = [torch.zeros(n, dtype=torch.float32, device=self.device)]
+        else:
+            self.opt_state = [torch.zeros(n, dtype=torch.float32, device=self.device),
+                              torch.zeros(n, dtype=torch.float32, device=self.device)]
+        self.step_count = 0
+        self.data = synthetic_batch(model, self.batch, self.device,
+                                    seed=seed if data_seed is None else data_seed)
+        self.group = group
+        self.ddp = None
+        if group is not None:
+            import torch.distributed as dist
+
+            if dist.get_world_size(group) > 1:
+                self.ddp = GradBucketer(self.arena, group, bucket_mb=bucket_mb)
+        self.use_graph = use_graph and self.device.type == "cuda" and self.ddp is None
+        self._graph = None
+        self._g_loss = None
+        self.last_loss: Optional[torch.Tensor] = None
+
+    # ------------------------------------------------------------ one step
+    def _fwd_bwd(self) -> torch.Tensor:
+        d = self.data
+        if self.spec.kind == "image":
+            logits = self.model.forward(d["x"])
+        else:
+            logits = self.model.forward(d)
+        labels = d["labels"]
+        rows = labels.numel()
+        loss, dlog = Fx.softmax_xent(logits, labels, smoothing=self.spec.smoothing,
+                                     ignore_index=-100, normalizer=rows)
+        logits.backward(dlog)
+        return loss
+
+    def _opt_step(self):
+        A = self.arena
+        gscale = self.ddp.grad_scale if self.ddp is not None else 1.0
+        self.step_count += 1
+        regions = [(0, A.n_decay, self.spec.wd), (A.n_decay, A.numel, 0.0)]
+        for lo, hi, wd in regions:
+            if hi <= lo:
+                continue
+            w, g, wb = A.master[lo:hi], A.grad[lo:hi], A.shadow[lo:hi]
+            if self.device.type == "cuda":
+                T = _lib.ops()
+                if self.opt == "sgd":
+                    T.sgd_step(w, g, self.opt_state[0][lo:hi], wb, self.lr, 0.9, wd, gscale, False, True)
+                else:
+                    T.adam_step(w, g, self.opt_state[0][lo:hi], self.opt_state[1][lo:hi], wb, self.lr,
+                                0.9, 0.98, 1e-9, wd, self.step_count, gscale, True)
+            else:
+                _cpu_opt(self.opt, w, g, self.opt_state, lo, hi, wb, self.lr, wd, gscale, self.step_count)
+
+    def step(self) -> torch.Tensor:
+        if self.use_graph:
+            loss = self._graph_step()
+        else:
+            loss = self._fwd_bwd()
+            if self.ddp is not None:
+                self.ddp.finish()
+        self._opt_step()
+        self.last_loss = loss
+        return loss
+
+    def _graph_step(self) -> torch.Tensor:
+        if self._graph is None:
+            # warm up on a side stream (allocator pools, lazy init), then capture
+            s = torch.cuda.Stream(self.device)
+            s.wait_stream(torch.cuda.current_stream(self.device))
+            with torch.cuda.stream(s):
+                for _ in range(2):
+                    self._fwd_bwd()
+                    self.arena.grad.zero_()
+            torch.cuda.current_stream(self.device).wait_stream(s)
+            g = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(g):
+                self._g_loss = self._fwd_bwd()
+            self._graph = g
+        self._graph.replay()
+        return self._g_loss
+
+    def run(self, iters: int) -> float:
+        """Run ``iters`` steps; returns wall seconds (device-synchronised)."""
+        t0 = time.perf_counter()
+        for _ in range(iters):
+            self.step()
+        if self.device.type == "cuda":
+            torch.cuda.synchronize(self.device)
+        return time.perf_counter() - t0
+
+    def samples_per_step(self) -> int:
+        return samples_per_batch(self.model_name, self.batch)
+
+    # ------------------------------------------------------------ state
+    def state_tensors(self) -> Dict[str, torch.Tensor]:
+        st = {"master": self.arena.master, "shadow": self.arena.shadow}
+        for i, t in enumerate(self.opt_state):
+            st[f"opt{i}"] = t
+        for k, v in self.model.buffers().items():
+            st["buf." + k] = v
+        return st
+
+    def state_bytes(self) -> int:
+        return sum(t.numel() * t.element_size() for t in self.state_tensors().values())
+
+    def release(self) -> None:
+        self._graph = None
+        self._g_loss = None
+        self.arena.on_grad_ready = None
+
+
+def _cpu_opt(opt, w, g, state, lo, hi, wb, lr, wd, gscale, step):
+    gg = g * gscale
+    if opt == "sgd":
+        m = state[0][lo:hi]
+        d = gg + wd * w
+        m.mul_(0.9).add_(d)
+        w.sub_(lr * m)
+    else:
+        m, v = state[0][lo:hi], state[1][lo:hi]
+        m.mul_(0.9).add_(0.1 * gg)
+        v.mul_(0.98).add_(0.02 * gg * gg)
+        mh = m / (1 - 0.9 ** step)
+        vh = v / (1 - 0.98 ** step)
+        w.sub_(lr * (mh / (vh.sqrt() + 1e-9) + wd * w))
+    g.zero_()
+    wb.copy_(w.to(torch.bfloat16))

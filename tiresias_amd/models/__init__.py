@@ -1,0 +1,92 @@
+"""Model zoo: the DL workloads the cluster scheduler runs as real jobs.
+
+``MODELS[name]`` gives the builder, default per-GPU batch and the optimizer
+recipe; ``make_model(name, arena, **over)`` instantiates it; ``synthetic_batch``
+creates a fixed random batch of the right shape (no datasets on the box).
+Reference: the simulated model table ``/root/reference/core/models.py:8-26``
+and ``model/model_factory.py:19-55`` (sizes only).
+"""
+from __future__ import annotations
+
+from dataclasses import dataclass, field
+from typing import Any, Callable, Dict
+
+import torch
+
+from .cnn import ResNet50, VGG16
+from .gnmt import GNMT
+from .transformer import TransformerBase
+
+
+@dataclass
+class ModelSpec:
+    builder: Callable
+    kind: str                      # "image" | "seq2seq"
+    batch: int                     # per-GPU batch (images / sentences)
+    opt: str                       # "sgd" | "adam"
+    lr: float
+    wd: float
+    kwargs: Dict[str, Any] = field(default_factory=dict)
+    image: int = 224
+    classes: int = 1000
+    seq: int = 128
+    vocab: int = 32000
+    smoothing: float = 0.0
+
+
+MODELS: Dict[str, ModelSpec] = {
+    "resnet50": ModelSpec(ResNet50, "image", 64, "sgd", 0.1, 1e-4),
+    "vgg16": ModelSpec(VGG16, "image", 32, "sgd", 0.01, 5e-4),
+    "transformer": ModelSpec(TransformerBase, "seq2seq", 32, "adam", 5e-4, 0.0, seq=128,
+                             smoothing=0.1),
+    "gnmt": ModelSpec(GNMT, "seq2seq", 64, "adam", 1e-3, 0.0, seq=50),
+    # tiny variants (CPU tests / gloo rehearsals / smoke)
+    "resnet_tiny": ModelSpec(ResNet50, "image", 4, "sgd", 0.1, 1e-4,
+                             dict(layers=(1, 1, 1, 1), width=8, num_classes=16), image=32, classes=16),
+    "vgg_tiny": ModelSpec(VGG16, "image", 4, "sgd", 0.01, 5e-4,
+                          dict(cfg=[16, "M", 32, "M"], image=16, fc=64, num_classes=16),
+                          image=16, classes=16),
+    "transformer_tiny": ModelSpec(TransformerBase, "seq2seq", 4, "adam", 1e-3, 0.0,
+                                  dict(vocab=512, d=64, heads=1, ffn=128, enc_layers=1,
+                                       dec_layers=1, max_len=64), seq=16, vocab=512, smoothing=0.1),
+    "gnmt_tiny": ModelSpec(GNMT, "seq2seq", 4, "adam", 1e-3, 0.0,
+                           dict(vocab=512, hidden=64, enc_layers=3, dec_layers=2, heads=1),
+                           seq=8, vocab=512),
+}
+
+# model family for the reference's model names (core/models.py:20, model_factory.py)
+FAMILY = {
+    "resnet50": "resnet50", "resnet101": "resnet50", "resnet152": "resnet50",
+    "vgg16": "vgg16", "vgg19": "vgg16", "vgg11": "vgg16", "alexnet": "vgg16",
+    "inception3": "resnet50", "inception4": "resnet50",
+    "transformer": "transformer", "bert": "transformer", "gnmt": "gnmt", "lstm": "gnmt",
+}
+
+
+def make_model(name: str, arena, **over):
+    spec = MODELS[name]
+    kw = dict(spec.kwargs)
+    kw.update(over)
+    return spec.builder(arena, **kw)
+
+
+def synthetic_batch(name: str, batch: int, device, seed: int = 0) -> Dict[str, torch.Tensor]:
+    spec = MODELS[name]
+    g = torch.Generator(device="cpu")
+    g.manual_seed(seed)
+    if spec.kind == "image":
+        x = torch.zeros(batch, spec.image, spec.image, 8)
+        x[..., :3] = torch.randn(batch, spec.image, spec.image, 3, generator=g)
+        y = torch.randint(0, spec.classes, (batch,), generator=g)
+        return {"x": x.to(device=device, dtype=torch.bfloat16), "labels": y.to(device)}
+    S = spec.seq
+    src = torch.randint(1, spec.vocab, (batch, S), generator=g)
+    tgt = torch.randint(1, spec.vocab, (batch, S + 1), generator=g)
+    return {"src": src.to(device), "tgt_in": tgt[:, :-1].contiguous().to(device),
+            "labels": tgt[:, 1:].contiguous().to(device)}
+
+
+def samples_per_batch(name: str, batch: int) -> int:
+    """Throughput unit: images for CNNs, target tokens for seq2seq."""
+    spec = MODELS[name]
+    return batch if spec.kind == "image" else batch * spec.seq

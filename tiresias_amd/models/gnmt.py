@@ -1,0 +1,207 @@
+"""GNMT-style LSTM seq2seq (Wu et al. 2016, as in the MLPerf GNMT reference:
+hidden 1024, 4 encoder layers with a bidirectional first layer and residual
+connections from layer 3, 4 decoder layers, attention from the first decoder
+layer's output fed to every later layer) on the tiresias_amd kernels.
+
+Attention is multi-head scaled dot-product (16 heads x 64) so it runs on the
+flash-attention kernel; training uses teacher forcing, so the first decoder
+layer runs over the whole target sequence before attention (exactly GNMT's
+data flow).
+
+The LSTM layer is one autograd Function over the whole sequence:
+  * the input projection X W_ih^T + b for ALL timesteps is one MFMA GEMM
+    (fp32 gate pre-activations);
+  * per step: h_{t-1} W_hh^T accumulated in place into that step's gate slice
+    (GEMM epilogue mode=accumulate) + the fused cell kernel;
+  * backward per step: fused cell backward, dh_{t-1} += dG_t W_hh accumulated
+    in place; the weight gradients are two large GEMMs over all timesteps.
+The per-step loop is launch-bound, so the job runner captures the whole
+training step into a hipGraph.
+"""
+from __future__ import annotations
+
+import torch
+from torch.autograd import Function
+
+from ..ops import _lib
+from ..ops import functional as Fx
+from ..ops.arena import Arena, Param
+
+BF16 = torch.bfloat16
+
+
+def _T():
+    return _lib.ops()
+
+
+class _LSTMLayer(Function):
+    @staticmethod
+    def forward(ctx, x, token, w_ih: Param, w_hh: Param, b: Param, reverse: bool):
+        T, B, I = x.shape
+        Hd = w_hh.shape[1]
+        dev = x.device
+        x2 = x.reshape(T * B, I)
+        G = torch.empty(T * B, 4 * Hd, dtype=torch.float32, device=dev)
+        Hs = torch.empty(T, B, Hd, dtype=BF16, device=dev)
+        Cs = torch.empty(T, B, Hd, dtype=torch.float32, device=dev)
+        act = torch.empty(T, B, 5 * Hd, dtype=torch.float32, device=dev)
+        steps = range(T - 1, -1, -1) if reverse else range(T)
+        if dev.type == "cuda":
+            _T().gemm(x2, True, w_ih.w, True, G, 0, b.w, False, None, 1.0, False)
+            Gv = G.view(T, B, 4 * Hd)
+            prev = None
+            for t in steps:
+                if prev is not None:
+                    _T().gemm(Hs[prev], True, w_hh.w, True, Gv[t], 1, None, False, None, 1.0, False)
+                _T().lstm_cell_forward(Gv[t], Cs[prev] if prev is not None else None, Cs[t], Hs[t],
+                                       None, act[t])
+                prev = t
+        else:
+            G = x2.float() @ w_ih.w.float().t() + b.w.float()
+            Gv = G.view(T, B, 4 * Hd)
+            prev = None
+            for t in steps:
+                g = Gv[t].clone()
+                if prev is not None:
+                    g += Hs[prev].float() @ w_hh.w.float().t()
+                i, f, gg, o = g.chunk(4, 1)
+                i, f, gg, o = torch.sigmoid(i), torch.sigmoid(f), torch.tanh(gg), torch.sigmoid(o)
+                c = f * (Cs[prev] if prev is not None else 0) + i * gg
+                tc = torch.tanh(c)
+                Cs[t] = c
+                Hs[t] = (o * tc).to(BF16)
+                act[t] = torch.cat([i, f, gg, o, tc], 1)
+                prev = t
+        ctx.save_for_backward(x, Hs, Cs, act)
+        ctx.p = (w_ih, w_hh, b, reverse)
+        return Hs
+
+    @staticmethod
+    def backward(ctx, dH):
+        x, Hs, Cs, act = ctx.saved_tensors
+        w_ih, w_hh, b, reverse = ctx.p
+        T, B, I = x.shape
+        Hd = Hs.shape[2]
+        dev = x.device
+        dHf = dH.float().contiguous()              # dh accumulator (fp32), updated in place
+        dG = torch.empty(T, B, 4 * Hd, dtype=BF16, device=dev)
+        dc = torch.zeros(B, Hd, dtype=torch.float32, device=dev)
+        dc2 = torch.empty_like(dc)
+        order = list(range(T - 1, -1, -1) if reverse else range(T))
+        rev_order = order[::-1]
+        if dev.type == "cuda":
+            for k, t in enumerate(rev_order):
+                prev = rev_order[k + 1] if k + 1 < T else None   # the step that ran before t
+                _T().lstm_cell_backward(act[t], Cs[prev] if prev is not None else None, dHf[t], dc,
+                                        None, dc2, dG[t])
+                dc, dc2 = dc2, dc
+                if prev is not None:
+                    _T().gemm(dG[t], True, w_hh.w, False, dHf[prev], 1, None, False, None, 1.0, False)
+            dG2 = dG.view(T * B, 4 * Hd)
+            # h_{t-1} for each t (zero for the first step in processing order)
+            Hprev = torch.zeros_like(Hs)
+            if T > 1:
+                if reverse:
+                    Hprev[:-1] = Hs[1:]
+                else:
+                    Hprev[1:] = Hs[:-1]
+            _T().gemm(dG2, False, Hprev.view(T * B, Hd), False, w_hh.grad, 1, None, False, None, 1.0, True)
+            _T().gemm(dG2, False, x.reshape(T * B, I), False, w_ih.grad, 1, None, False, None, 1.0, True)
+            _T().colsum(dG2, b.grad)
+            dx = None
+            if ctx.needs_input_grad[0]:
+                dx = torch.empty(T * B, I, dtype=BF16, device=dev)
+                _T().gemm(dG2, True, w_ih.w, False, dx, 0, None, False, None, 1.0, False)
+                dx = dx.view(T, B, I)
+        else:
+            Whh = w_hh.w.float()
+            dGf = torch.empty(T, B, 4 * Hd)
+            for k, t in enumerate(rev_order):
+                prev = rev_order[k + 1] if k + 1 < T else None
+                i, f, gg, o, tc = act[t].chunk(5, 1)
+                dh = dHf[t]
+                dcc = dh * o * (1 - tc * tc) + dc
+                cp = Cs[prev] if prev is not None else torch.zeros_like(dc)
+                di = dcc * gg * i * (1 - i)
+                df = dcc * cp * f * (1 - f)
+                dg_ = dcc * i * (1 - gg * gg)
+                do = dh * tc * o * (1 - o)
+                g4 = torch.cat([di, df, dg_, do], 1)
+                dGf[t] = g4
+                dG[t] = g4.to(BF16)
+                dc = dcc * f
+                if prev is not None:
+                    dHf[prev] += dG[t].float() @ Whh
+            Hprev = torch.zeros_like(Hs)
+            if T > 1:
+                if reverse:
+                    Hprev[:-1] = Hs[1:]
+                else:
+                    Hprev[1:] = Hs[:-1]
+            dG2 = dG.view(T * B, 4 * Hd).float()
+            w_hh.grad += dG2.t() @ Hprev.view(T * B, Hd).float()
+            w_ih.grad += dG2.t() @ x.reshape(T * B, I).float()
+            b.grad += dG2.sum(0)
+            dx = (dG2 @ w_ih.w.float()).to(BF16).view(T, B, I) if ctx.needs_input_grad[0] else None
+        w_ih.grad_ready()
+        w_hh.grad_ready()
+        b.grad_ready()
+        return dx, None, None, None, None, None
+
+
+def lstm(x, p, reverse=False):
+    """x: [T,B,I] bf16 -> [T,B,H] bf16."""
+    return _LSTMLayer.apply(x.contiguous(), p[0].arena.token, p[0], p[1], p[2], reverse)
+
+
+class GNMT:
+    name = "gnmt"
+
+    def __init__(self, arena: Arena, vocab: int = 32000, hidden: int = 1024, enc_layers: int = 4,
+                 dec_layers: int = 4, heads: int = 16):
+        assert hidden == heads * 64
+        A = arena
+        H = hidden
+        self.arena, self.H, self.heads, self.vocab = arena, H, heads, vocab
+        self.src_emb = A.add("src_emb", (vocab, H), init="uniform", std=0.1)
+        self.tgt_emb = A.add("tgt_emb", (vocab, H), init="uniform", std=0.1)
+
+        def lstm_p(n, i):
+            return (A.add(n + ".w_ih", (4 * H, i), init="uniform", std=0.1),
+                    A.add(n + ".w_hh", (4 * H, H), init="uniform", std=0.1),
+                    A.add(n + ".b", (4 * H,), init="zeros", decay=False))
+
+        self.enc = [lstm_p("enc0.fw", H), lstm_p("enc0.bw", H), lstm_p("enc1", 2 * H)]
+        self.enc += [lstm_p(f"enc{i}", H) for i in range(2, enc_layers)]
+        self.dec = [lstm_p("dec0", H)] + [lstm_p(f"dec{i}", 2 * H) for i in range(1, dec_layers)]
+        self.att_q = A.add("att.q", (H, H), init="xavier")
+        self.att_kv = A.add("att.kv", (2 * H, H), init="xavier")
+        self.cls_w = A.add("cls.w", (vocab, 2 * H), init="uniform", std=0.1)
+        self.cls_b = A.add("cls.b", (vocab,), init="zeros", decay=False)
+        self.training = True
+
+    def forward(self, batch):
+        src, tgt_in = batch["src"], batch["tgt_in"]       # [B,S] token ids
+        # time-major activations [T,B,H]
+        x = Fx.embedding(src.t().contiguous(), self.src_emb)
+        fw = lstm(x, self.enc[0])
+        bw = lstm(x, self.enc[1], reverse=True)
+        h = lstm(torch.cat([fw, bw], 2), self.enc[2])
+        for i, p in enumerate(self.enc[3:]):
+            o = lstm(h, p)
+            h = Fx.add(h, o) if i >= 0 else o          # residual from layer 3 on
+        mem = h.transpose(0, 1).contiguous()             # [B,S,H]
+        y = Fx.embedding(tgt_in.t().contiguous(), self.tgt_emb)
+        d0 = lstm(y, self.dec[0])                        # [T,B,H]
+        q = Fx.linear(d0.transpose(0, 1).contiguous(), self.att_q)   # [B,T,H]
+        kv = Fx.linear(mem, self.att_kv)                 # [B,S,2H]
+        ctxv = Fx.cross_attention(q, kv, self.heads).transpose(0, 1).contiguous()  # [T,B,H]
+        h = d0
+        for i, p in enumerate(self.dec[1:]):
+            o = lstm(torch.cat([h, ctxv], 2), p)
+            h = Fx.add(h, o) if i >= 1 else o
+        out = torch.cat([h, ctxv], 2).transpose(0, 1).contiguous()   # [B,T,2H]
+        return Fx.linear(out, self.cls_w, self.cls_b)
+
+    def buffers(self):
+        return {}

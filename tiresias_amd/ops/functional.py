@@ -401,37 +401,36 @@ def global_avgpool(x: torch.Tensor) -> torch.Tensor:
 
 # ============================================================ loss
 def softmax_xent(logits: torch.Tensor, labels: torch.Tensor, smoothing: float = 0.0,
-                 ignore_index: int = -100) -> Tuple[torch.Tensor, torch.Tensor]:
+                 ignore_index: Optional[int] = -100,
+                 normalizer: Optional[int] = None) -> Tuple[torch.Tensor, torch.Tensor]:
     """Fused softmax cross-entropy. Returns (mean loss, dlogits) WITHOUT autograd:
     the loss is the graph sink, so the training step calls
     ``logits.backward(dlogits)`` directly (no extra scale pass over the logits).
+
+    ``normalizer``: number of non-ignored rows when known statically (keeps the
+    step free of host syncs, i.e. capturable in a hipGraph); otherwise counted.
     """
     V = logits.shape[-1]
     l2 = logits.reshape(-1, V).contiguous()
     lab = labels.reshape(-1).contiguous()
     rows = l2.shape[0]
-    count = (lab != ignore_index).sum().clamp_min(1)
+    ign = ignore_index if ignore_index is not None else -(1 << 62)
+    if normalizer is None:
+        normalizer = max(1, int((lab != ign).sum().item()))
+    n = normalizer
     if l2.is_cuda:
         loss_rows = torch.empty(rows, dtype=torch.float32, device=l2.device)
         dlog = torch.empty_like(l2)
-        # grad scale must be a host float: use the static row count when no
-        # ignore_index rows are expected, else the exact count (one sync)
-        if ignore_index is None or ignore_index < 0 and not bool((lab == ignore_index).any()):
-            n = rows
-        else:
-            n = int(count.item())
-        _T().softmax_xent(l2.detach(), lab, dlog, loss_rows, smoothing, 1.0 / n,
-                          ignore_index if ignore_index is not None else -(1 << 62))
+        _T().softmax_xent(l2.detach(), lab, dlog, loss_rows, smoothing, 1.0 / n, ign)
         loss = loss_rows.sum() / n
         return loss, dlog.view(logits.shape)
     lf = l2.detach().float()
     logp = torch.log_softmax(lf, -1)
-    valid = (lab != ignore_index)
+    valid = (lab != ign)
     safe = torch.where(valid, lab, torch.zeros_like(lab))
     nll = -logp.gather(1, safe[:, None])[:, 0]
     smooth = -logp.mean(1)
     lrow = ((1 - smoothing) * nll + smoothing * smooth) * valid
-    n = int(count.item())
     loss = lrow.sum() / n
     p = logp.exp()
     tgt = torch.zeros_like(p).scatter_(1, safe[:, None], 1.0) * (1 - smoothing) + smoothing / V
