@@ -1,0 +1,353 @@
+"""Real-GPU cluster runtime: the Tiresias scheduler driving DDP training jobs
+on one MI355X node, one process per GPU.
+
+Topology (SPMD, ``torch.distributed``):
+  * world NCCL (= RCCL over xGMI) group over all N ranks — DDP gangs get
+    sub-communicators (``new_group``, created in the same order on every
+    rank because every rank applies the same broadcast plan), state moves
+    use xGMI P2P (``batch_isend_irecv``);
+  * a gloo control group carries the round plan (broadcast) and the worker
+    reports (gather) — the heartbeat: a rank that stops reporting trips the
+    gloo timeout and the controller aborts the replay (failure detection).
+
+Rank 0 additionally runs the CONTROLLER: the same Policy / Placement /
+Cluster objects as the simulator (``LiveScheduler`` subclasses the event
+engine), fed with *measured* time: a job's attained service is the wall time
+it spent running (x #GPUs for 2D-LAS), its progress the iterations its gang
+actually completed. Scheduling happens at round boundaries (every
+``quantum`` seconds of wall time): gangs stop at an iteration boundary, so a
+preemption never interrupts an in-flight collective.
+
+Preemption = suspension in HBM: the job's ``Trainer`` (flat param arena +
+optimizer state, 288 GB per GPU leaves plenty of room) stays resident on its
+ranks; resuming on the same GPUs is a pointer swap, resuming elsewhere moves
+the flat buffers GPU->GPU over xGMI; with ``spill_host`` the state goes to
+pinned host DRAM through the native checkpoint engine instead.
+"""
+from __future__ import annotations
+
+import math
+import os
+import time
+from dataclasses import dataclass, field
+from typing import Dict, List, Optional, Tuple
+
+import torch
+import torch.distributed as dist
+
+from ..config import ClusterSpec, SimConfig
+from ..core.job import Job, JobSpec, JobState
+from ..engine.sim import Simulator
+from ..metrics.logger import MetricsLogger
+from .trainer import Trainer
+
+# nominal per-iteration seconds on one MI355X (tools/bench_models.py,
+# profiles/model_bench_r1_*.json); refined online from measurements
+NOMINAL_ITER_S = {"resnet50": 0.028, "vgg16": 0.015, "transformer": 0.016, "gnmt": 0.037,
+                  "resnet_tiny": 0.004, "vgg_tiny": 0.002, "transformer_tiny": 0.006,
+                  "gnmt_tiny": 0.01}
+
+
+def gang_ranks(alloc: Dict[str, List[int]], gpn: int) -> Tuple[int, ...]:
+    """(virtual) node id + device -> global GPU rank."""
+    out = []
+    for nid, devs in alloc.items():
+        for d in devs:
+            out.append((int(nid) - 1) * gpn + d)
+    return tuple(sorted(out))
+
+
+class LiveScheduler(Simulator):
+    """The event engine driven by measured progress instead of a model:
+    progress only moves when workers report iterations (rate 0)."""
+
+    def __init__(self, cfg, specs, logger=None, prior=None):
+        super().__init__(cfg, specs, logger=logger, prior=prior)
+        self.actions: List[dict] = []
+
+    def _start(self, j: Job, plan) -> None:
+        alloc = self.cluster.commit(j, plan)
+        j.start(self.now, alloc, rate=0.0, restore_cost=0.0)
+        j.extra["run_start"] = self.now
+        self.actions.append({"op": "start", "job": j.job_id})
+        self.log.decision(self.now, "start", j.job_id, gpus=j.num_gpu,
+                          ranks=list(gang_ranks(alloc, self.cluster.spec.num_gpu_p_node)))
+
+    def _preempt(self, j: Job, reason: str = "priority") -> None:
+        j.extra["last_ranks"] = gang_ranks(j.allocation, self.cluster.spec.num_gpu_p_node)
+        self.cluster.release(j)
+        j.preempt(self.now, 0.0, 0.0)
+        self.actions.append({"op": "suspend", "job": j.job_id})
+        self.log.decision(self.now, "preempt", j.job_id, reason=reason)
+
+    def _refresh_rates(self) -> None:
+        for j in self.active:
+            if j.is_running:
+                j.rate = 0.0
+
+
+@dataclass
+class ReplayJob:
+    spec: JobSpec
+    model: str
+    iterations: int
+    batch: Optional[int] = None
+
+
+class Controller:
+    def __init__(self, cfg: SimConfig, jobs: List[ReplayJob], world: int, quantum: float,
+                 logger: Optional[MetricsLogger] = None):
+        self.cfg = cfg
+        self.rjobs = {rj.spec.job_id: rj for rj in jobs}
+        specs = []
+        for rj in jobs:
+            s = rj.spec
+            # duration in work units = iterations (progress is reported in iterations)
+            specs.append(JobSpec(**{**s.__dict__, "duration": float(rj.iterations)}))
+        self.sched = LiveScheduler(cfg, specs, logger=logger,
+                                   prior=sorted(rj.iterations * self._iter_est(rj.model, rj.spec.num_gpu)
+                                                * rj.spec.num_gpu for rj in jobs))
+        self.world = world
+        self.quantum = quantum
+        self.gpn = self.sched.cluster.spec.num_gpu_p_node
+        self.holders: Dict[str, Tuple[int, ...]] = {}      # job -> ranks holding its state
+        self.groups_made: set = set()
+        self.est: Dict[Tuple[str, int], float] = {}
+        self.done_iters: Dict[str, int] = {j: 0 for j in self.rjobs}
+        self.round = 0
+        self.t0 = None
+
+    def _iter_est(self, model: str, gpus: int) -> float:
+        return getattr(self, "est", {}).get((model, gpus), NOMINAL_ITER_S.get(model, 0.03) *
+                                             (1.0 if gpus == 1 else 1.08))
+
+    def start_clock(self):
+        self.t0 = time.perf_counter()
+
+    def now(self) -> float:
+        return time.perf_counter() - self.t0
+
+    # ---------------------------------------------------------------- reports
+    def apply_reports(self, reports: List[dict]) -> None:
+        seen = set()
+        for r in reports:
+            if not r or r.get("job") is None:
+                continue
+            jid = r["job"]
+            if jid in seen:
+                continue
+            seen.add(jid)
+            self.done_iters[jid] += r["iters"]
+            rj = self.rjobs[jid]
+            if r["iters"] > 0 and r["run_s"] > 0:
+                k = (rj.model, rj.spec.num_gpu)
+                per = r["run_s"] / r["iters"]
+                self.est[k] = per if k not in self.est else 0.7 * self.est[k] + 0.3 * per
+            j = self.sched.jobs[jid]
+            j.progress = float(min(self.done_iters[jid], rj.iterations))
+
+    # ---------------------------------------------------------------- planning
+    def plan_round(self) -> dict:
+        s = self.sched
+        s.actions = []
+        t = max(self.now(), s.now)
+        if s.events == 0 or t > s.now:
+            s.step(t)
+        else:
+            s.step(s.now)
+        finished = [j for j in s.finished if j.extra.get("reported") is None]
+        actions: List[dict] = []
+        for j in finished:
+            j.extra["reported"] = True
+            if j.job_id in self.holders:
+                actions.append({"op": "drop", "job": j.job_id, "ranks": self.holders.pop(j.job_id)})
+        for a in s.actions:
+            j = s.jobs[a["job"]]
+            if a["op"] == "start" and j.is_running:
+                ranks = gang_ranks(j.allocation, self.gpn)
+                if len(ranks) > 1 and ranks not in self.groups_made:
+                    self.groups_made.add(ranks)
+                    actions.append({"op": "group", "ranks": ranks})
+                old = self.holders.get(j.job_id)
+                rj = self.rjobs[j.job_id]
+                act = {"op": "start", "job": j.job_id, "ranks": ranks, "model": rj.model,
+                       "batch": rj.batch, "seed": int(j.job_id) if j.job_id.isdigit() else hash(j.job_id) % 100000}
+                if old is None:
+                    act["source"] = "fresh"
+                elif old == ranks:
+                    act["source"] = "resident"
+                else:
+                    # every new rank without a replica receives one from a holder
+                    donors = {}
+                    for i, r in enumerate(ranks):
+                        if r not in old:
+                            donors[r] = old[i % len(old)]
+                    act["source"] = "p2p"
+                    act["donors"] = donors
+                    act["old"] = old
+                self.holders[j.job_id] = ranks
+                actions.append(act)
+        # assignments: running jobs -> iterations this round
+        assign: Dict[int, Tuple[str, int]] = {}
+        for j in s.active:
+            if not j.is_running:
+                continue
+            rj = self.rjobs[j.job_id]
+            left = rj.iterations - self.done_iters[j.job_id]
+            if left <= 0:
+                continue
+            n = max(1, int(round(self.quantum / self._iter_est(rj.model, j.num_gpu))))
+            n = min(n, left)
+            for r in gang_ranks(j.allocation, self.gpn):
+                assign[r] = (j.job_id, n)
+        self.round += 1
+        stop = not s.active and s.reader.remaining() == 0
+        wait = 0.0
+        if not assign and not stop:
+            # idle cluster: sleep until the next arrival instead of spinning
+            wait = max(0.0, min(self.quantum, s.reader.next_time() - self.now()))
+        return {"round": self.round, "actions": actions, "assign": assign, "stop": stop, "wait": wait}
+
+
+class Worker:
+    def __init__(self, rank: int, world: int, device: torch.device, world_pg=None, use_graph=False,
+                 gang_backend: Optional[str] = None):
+        self.gang_backend = gang_backend or ("nccl" if device.type == "cuda" else "gloo")
+        self.rank = rank
+        self.world = world
+        self.device = device
+        self.world_pg = world_pg
+        self.trainers: Dict[str, Trainer] = {}
+        self.groups: Dict[Tuple[int, ...], object] = {}
+        self.use_graph = use_graph
+
+    def _group(self, ranks):
+        if len(ranks) <= 1:
+            return None
+        return self.groups[tuple(ranks)]
+
+    def _make_trainer(self, act) -> Trainer:
+        ranks = tuple(act["ranks"])
+        data_seed = act["seed"] * 1000 + ranks.index(self.rank)
+        return Trainer(act["model"], self.device, batch=act.get("batch"), group=self._group(ranks),
+                       seed=act["seed"], data_seed=data_seed,
+                       use_graph=self.use_graph and len(ranks) == 1)
+
+    def apply(self, plan: dict) -> None:
+        p2p_ops = []
+        for a in plan["actions"]:
+            op = a["op"]
+            if op == "group":
+                pg = dist.new_group(list(a["ranks"]), backend=self.gang_backend)
+                self.groups[tuple(a["ranks"])] = pg
+            elif op == "drop":
+                t = self.trainers.pop(a["job"], None)
+                if t is not None:
+                    t.release()
+            elif op == "start":
+                ranks = tuple(a["ranks"])
+                src = a["source"]
+                if src == "fresh":
+                    if self.rank in ranks:
+                        self.trainers[a["job"]] = self._make_trainer(a)
+                elif src == "resident":
+                    pass
+                elif src == "p2p":
+                    donors = {int(k): v for k, v in a["donors"].items()}
+                    old = tuple(a["old"])
+                    if self.rank in donors:        # receiver
+                        t = self._make_trainer(a)
+                        self.trainers[a["job"]] = t
+                        for _, buf in sorted(t.state_tensors().items()):
+                            p2p_ops.append(dist.P2POp(dist.irecv, buf, donors[self.rank]))
+                    for recv, donor in donors.items():
+                        if donor == self.rank:
+                            t = self.trainers[a["job"]]
+                            for _, buf in sorted(t.state_tensors().items()):
+                                p2p_ops.append(dist.P2POp(dist.isend, buf, recv))
+                    # replicas that stay: rebind their DDP bucketer to the new gang
+                    if self.rank in ranks and self.rank in old:
+                        self.trainers[a["job"]].rebind(self._group(ranks))
+        if p2p_ops:
+            for w in dist.batch_isend_irecv(p2p_ops):
+                w.wait()
+        # holders that are no longer members free their replica after sending
+        for a in plan["actions"]:
+            if a["op"] == "start" and a["source"] == "p2p":
+                if self.rank in a["old"] and self.rank not in a["ranks"]:
+                    t = self.trainers.pop(a["job"], None)
+                    if t is not None:
+                        t.release()
+
+    def run(self, plan: dict) -> dict:
+        a = plan["assign"].get(self.rank)
+        if a is None:
+            return {"rank": self.rank, "job": None}
+        jid, n = a
+        t = self.trainers[jid]
+        t0 = time.perf_counter()
+        for _ in range(n):
+            t.step()
+        if self.device.type == "cuda":
+            torch.cuda.synchronize(self.device)
+        dt = time.perf_counter() - t0
+        return {"rank": self.rank, "job": jid, "iters": n, "run_s": dt,
+                "loss": float(t.last_loss) if t.last_loss is not None else None}
+
+    def clear(self):
+        for t in self.trainers.values():
+            t.release()
+        self.trainers.clear()
+
+
+def _bcast(obj, src, pg):
+    lst = [obj]
+    dist.broadcast_object_list(lst, src=src, group=pg)
+    return lst[0]
+
+
+def run_replay(cfg: SimConfig, jobs: List[ReplayJob], rank: int, world: int, device: torch.device,
+               ctrl_pg=None, world_pg=None, worker: Optional[Worker] = None, quantum: float = 0.4,
+               out_dir: Optional[str] = None, use_graph: bool = False, max_rounds: int = 100000) -> Optional[dict]:
+    """Replay ``jobs`` on the live cluster. Returns the summary on rank 0."""
+    distributed = world > 1
+    ctrl = None
+    log = None
+    if rank == 0:
+        log = MetricsLogger(out_dir, node_logs=False)
+        ctrl = Controller(cfg, jobs, world, quantum, logger=log)
+    w = worker or Worker(rank, world, device, world_pg, use_graph=use_graph)
+    if distributed:
+        dist.barrier(group=ctrl_pg)
+    if ctrl:
+        ctrl.start_clock()
+    t_start = time.perf_counter()
+    rounds = 0
+    while rounds < max_rounds:
+        plan = ctrl.plan_round() if ctrl else None
+        if distributed:
+            plan = _bcast(plan, 0, ctrl_pg)
+        if plan["stop"]:
+            break
+        w.apply(plan)
+        rep = w.run(plan)
+        if plan.get("wait", 0) > 0 and rep["job"] is None:
+            time.sleep(plan["wait"])
+        if distributed:
+            reps = [None] * world if rank == 0 else None
+            dist.gather_object(rep, reps, dst=0, group=ctrl_pg)
+        else:
+            reps = [rep]
+        if ctrl:
+            ctrl.apply_reports(reps)
+        rounds += 1
+    wall = time.perf_counter() - t_start
+    w.clear()
+    if device.type == "cuda":
+        torch.cuda.synchronize(device)
+    if ctrl:
+        s = ctrl.sched.summary()
+        s.update(rounds=rounds, replay_wall_s=wall, iter_est={f"{k[0]}x{k[1]}": v for k, v in ctrl.est.items()})
+        log.close()
+        return s
+    return None

@@ -46,6 +46,7 @@ class Trainer:
                                     seed=seed if data_seed is None else data_seed)
         self.group = group
         self.ddp = None
+        self._bucket_mb = bucket_mb
         if group is not None:
             import torch.distributed as dist
 
@@ -140,6 +141,19 @@ class Trainer:
 
     def state_bytes(self) -> int:
         return sum(t.numel() * t.element_size() for t in self.state_tensors().values())
+
+    def rebind(self, group) -> None:
+        """Move the job to a new DDP gang (after a preemption resumed it on
+        different GPUs): new communicator, fresh bucketer."""
+        self.group = group
+        self.arena.on_grad_ready = None
+        self.ddp = None
+        if group is not None:
+            import torch.distributed as dist
+
+            if dist.get_world_size(group) > 1:
+                self.ddp = GradBucketer(self.arena, group, bucket_mb=self._bucket_mb)
+        self._graph = None
 
     def release(self) -> None:
         self._graph = None

@@ -98,34 +98,37 @@ class Arena:
         self.master = torch.zeros(self.numel, dtype=torch.float32, device=dev)
         self.shadow = torch.zeros(self.numel, dtype=torch.bfloat16, device=dev)
         self.grad = torch.zeros(self.numel, dtype=torch.float32, device=dev)
-        g = torch.Generator(device="cpu")
+        # initialise on the device itself (a 138M-param VGG-16 job starts in
+        # milliseconds instead of seconds of host RNG + H2D copy)
+        g = torch.Generator(device=dev)
         g.manual_seed(self.seed)
         for p in order:
             p.master = self.master[p.offset:p.offset + p.numel].view(p.shape)
             p.w = self.shadow[p.offset:p.offset + p.numel].view(p.shape)
             p.grad = self.grad[p.offset:p.offset + p.numel].view(p.shape)
-            p.master.copy_(self._init_value(p, g))
+            self._init_into(p, g)
         self.shadow.copy_(self.master.to(torch.bfloat16))
         return self
 
     @staticmethod
-    def _init_value(p: Param, g: torch.Generator) -> torch.Tensor:
+    def _init_into(p: Param, g: torch.Generator) -> None:
+        t = p.master
         if p.init == "zeros":
-            return torch.zeros(p.shape)
-        if p.init == "ones":
-            return torch.ones(p.shape)
-        if p.init == "kaiming":
+            t.zero_()
+        elif p.init == "ones":
+            t.fill_(1.0)
+        elif p.init == "kaiming":
             # fan_in over all dims but the first (conv [K,R,S,C], linear [out,in])
             fan_in = max(1, p.numel // p.shape[0])
-            return torch.randn(p.shape, generator=g) * math.sqrt(2.0 / fan_in)
-        if p.init == "xavier":
+            t.normal_(0.0, math.sqrt(2.0 / fan_in), generator=g)
+        elif p.init == "xavier":
             fan_in = max(1, p.numel // p.shape[0])
-            fan_out = p.shape[0]
-            a = math.sqrt(6.0 / (fan_in + fan_out))
-            return (torch.rand(p.shape, generator=g) * 2 - 1) * a
-        if p.init == "uniform":
-            return (torch.rand(p.shape, generator=g) * 2 - 1) * p.std
-        return torch.randn(p.shape, generator=g) * p.std
+            a = math.sqrt(6.0 / (fan_in + p.shape[0]))
+            t.uniform_(-a, a, generator=g)
+        elif p.init == "uniform":
+            t.uniform_(-p.std, p.std, generator=g)
+        else:
+            t.normal_(0.0, p.std, generator=g)
 
     # ----------------------------------------------------------------- state
     def zero_grad(self) -> None:
