@@ -52,10 +52,12 @@ TINY = {"resnet50": "resnet_tiny", "vgg16": "vgg_tiny", "transformer": "transfor
 GPU_DIST = [(1, 0.70), (2, 0.10), (4, 0.10), (8, 0.07), (16, 0.03)]
 
 
-def bench_trace(n_gpus: int, jobs_per_gpu: int, seed: int, median_s: float = 1.2, load: float = 1.5,
-                tiny: bool = False):
+def bench_trace(n_gpus: int, jobs_per_gpu: int, seed: int, median_s: float = 0.6, sigma: float = 1.8,
+                load: float = 1.3, tiny: bool = False):
     """Philly-shaped mini trace: ~70% 1-GPU jobs with a power-of-two gang
-    tail, log-normal service times, Poisson arrivals at ``load`` x capacity."""
+    tail, heavy-tailed log-normal service times (sigma 1.8, i.e. most jobs
+    short, a few 25x longer, as in the NSDI'19 trace), Poisson arrivals at
+    ``load`` x capacity. Durations are compressed to seconds."""
     rng = random.Random(seed)
     n = jobs_per_gpu * n_gpus
     dist_ = [(g, p) for g, p in GPU_DIST if g <= n_gpus]
@@ -66,7 +68,7 @@ def bench_trace(n_gpus: int, jobs_per_gpu: int, seed: int, median_s: float = 1.2
     for i in range(n):
         m = rng.choices(names, weights=ws)[0]
         g = rng.choices(gs, weights=ps)[0]
-        svc = min(6.0, max(0.3, rng.lognormvariate(math.log(median_s), 0.9)))
+        svc = min(15.0, max(0.2, rng.lognormvariate(math.log(median_s), sigma)))
         it_s = NOMINAL_ITER_S[m] * (1.0 if g == 1 else 1.1)
         iters = max(4, int(round(svc / it_s)))
         rows.append((m, g, svc, iters))
@@ -84,7 +86,7 @@ def bench_trace(n_gpus: int, jobs_per_gpu: int, seed: int, median_s: float = 1.2
 
 
 def make_cfg(policy: str, scheme: str, n_gpus: int, seed: int) -> SimConfig:
-    return SimConfig(schedule=policy, scheme=scheme, num_queue=3, queue_limits=[1.0, 4.0],
+    return SimConfig(schedule=policy, scheme=scheme, num_queue=2, queue_limits=[1.0], gittins_delta=1.0,
                      solve_starvation=0.0, seed=seed, ckpt_policy="none",
                      cluster=ClusterSpec(num_switch=1, num_node_p_switch=1, num_gpu_p_node=n_gpus,
                                          num_cpu_p_node=max(128, 16 * n_gpus),
@@ -101,8 +103,8 @@ def main():
     ap.add_argument("--baseline-policy", default="fifo")
     ap.add_argument("--baseline-placement", default="yarn")
     ap.add_argument("--no-baseline", action="store_true")
-    ap.add_argument("--jobs-per-gpu", type=int, default=5)
-    ap.add_argument("--quantum", type=float, default=0.4)
+    ap.add_argument("--jobs-per-gpu", type=int, default=8)
+    ap.add_argument("--quantum", type=float, default=0.25)
     ap.add_argument("--seed", type=int, default=2019)
     ap.add_argument("--cpu", action="store_true", help="gloo/CPU rehearsal with tiny models")
     ap.add_argument("--out", default=None, help="directory for job.csv / summary.json of the last step")
@@ -203,6 +205,7 @@ def main():
             "baseline_avg_jct_s": round(base["avg_jct"], 4) if base else None,
             "baseline_makespan_s": round(base["makespan"], 4) if base else None,
             "gpu_utilization": round(sums[-1]["gpu_utilization"], 4),
+            "runtime_breakdown_s": sums[-1].get("runtime_breakdown"),
             "device": torch.cuda.get_device_name(device) if use_cuda else "cpu",
         }
         print(json.dumps(line), flush=True)

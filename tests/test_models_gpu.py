@@ -20,6 +20,7 @@ def test_model_grads_match_reference(gpu, model):
     # same initial weights (device RNG streams differ between CPU and GPU)
     tc.arena.master.copy_(tg.arena.master.cpu())
     tc.arena.shadow.copy_(tg.arena.shadow.cpu())
+    tc.data = {k: v.cpu() for k, v in tg.data.items()}
     lg = tg._fwd_bwd()
     lc = tc._fwd_bwd()
     assert abs(float(lg) - float(lc)) < 0.02 * max(1.0, abs(float(lc)))

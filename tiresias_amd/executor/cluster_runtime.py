@@ -323,14 +323,24 @@ def run_replay(cfg: SimConfig, jobs: List[ReplayJob], rank: int, world: int, dev
         ctrl.start_clock()
     t_start = time.perf_counter()
     rounds = 0
+    prof = {"plan_s": 0.0, "bcast_s": 0.0, "apply_s": 0.0, "run_s": 0.0, "gather_s": 0.0}
     while rounds < max_rounds:
+        ta = time.perf_counter()
         plan = ctrl.plan_round() if ctrl else None
+        tb = time.perf_counter()
         if distributed:
             plan = _bcast(plan, 0, ctrl_pg)
+        tc = time.perf_counter()
         if plan["stop"]:
             break
         w.apply(plan)
+        td = time.perf_counter()
         rep = w.run(plan)
+        te = time.perf_counter()
+        prof["plan_s"] += tb - ta
+        prof["bcast_s"] += tc - tb
+        prof["apply_s"] += td - tc
+        prof["run_s"] += te - td
         if plan.get("wait", 0) > 0 and rep["job"] is None:
             time.sleep(plan["wait"])
         if distributed:
@@ -340,6 +350,7 @@ def run_replay(cfg: SimConfig, jobs: List[ReplayJob], rank: int, world: int, dev
             reps = [rep]
         if ctrl:
             ctrl.apply_reports(reps)
+        prof["gather_s"] += time.perf_counter() - te
         rounds += 1
     wall = time.perf_counter() - t_start
     w.clear()
@@ -347,7 +358,8 @@ def run_replay(cfg: SimConfig, jobs: List[ReplayJob], rank: int, world: int, dev
         torch.cuda.synchronize(device)
     if ctrl:
         s = ctrl.sched.summary()
-        s.update(rounds=rounds, replay_wall_s=wall, iter_est={f"{k[0]}x{k[1]}": v for k, v in ctrl.est.items()})
+        s.update(rounds=rounds, replay_wall_s=wall, iter_est={f"{k[0]}x{k[1]}": v for k, v in ctrl.est.items()},
+                 runtime_breakdown={k: round(v, 4) for k, v in prof.items()})
         log.close()
         return s
     return None

@@ -71,19 +71,20 @@ def make_model(name: str, arena, **over):
 
 
 def synthetic_batch(name: str, batch: int, device, seed: int = 0) -> Dict[str, torch.Tensor]:
+    """Fixed random batch generated ON the device (no host RNG / H2D on job start)."""
     spec = MODELS[name]
-    g = torch.Generator(device="cpu")
+    dev = torch.device(device)
+    g = torch.Generator(device=dev)
     g.manual_seed(seed)
     if spec.kind == "image":
-        x = torch.zeros(batch, spec.image, spec.image, 8)
-        x[..., :3] = torch.randn(batch, spec.image, spec.image, 3, generator=g)
-        y = torch.randint(0, spec.classes, (batch,), generator=g)
-        return {"x": x.to(device=device, dtype=torch.bfloat16), "labels": y.to(device)}
+        x = torch.zeros(batch, spec.image, spec.image, 8, device=dev, dtype=torch.bfloat16)
+        x[..., :3] = torch.randn(batch, spec.image, spec.image, 3, generator=g, device=dev)
+        y = torch.randint(0, spec.classes, (batch,), generator=g, device=dev)
+        return {"x": x, "labels": y}
     S = spec.seq
-    src = torch.randint(1, spec.vocab, (batch, S), generator=g)
-    tgt = torch.randint(1, spec.vocab, (batch, S + 1), generator=g)
-    return {"src": src.to(device), "tgt_in": tgt[:, :-1].contiguous().to(device),
-            "labels": tgt[:, 1:].contiguous().to(device)}
+    src = torch.randint(1, spec.vocab, (batch, S), generator=g, device=dev)
+    tgt = torch.randint(1, spec.vocab, (batch, S + 1), generator=g, device=dev)
+    return {"src": src, "tgt_in": tgt[:, :-1].contiguous(), "labels": tgt[:, 1:].contiguous()}
 
 
 def samples_per_batch(name: str, batch: int) -> int:
