@@ -129,3 +129,37 @@ def test_live_replay_with_gangs():
     assert s["finished"] == s["jobs"] == 6 and s["failed"] == 0
     assert s["avg_jct"] > 0 and s["makespan"] > 0
     assert res[1] is None
+
+
+def _fault_worker(rank, world, port, outdir):
+    import datetime
+
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world, timeout=datetime.timedelta(seconds=20))
+    torch.set_num_threads(1)
+    ctrl = dist.new_group(backend="gloo", timeout=datetime.timedelta(seconds=20))
+    import bench
+    from tiresias_amd.executor.cluster_runtime import Worker, run_replay
+
+    jobs = bench.bench_trace(world, 3, seed=5, tiny=True)
+    cfg = bench.make_cfg("dlas-gpu", "count", world, 5)
+    w = Worker(rank, world, torch.device("cpu"), dist.group.WORLD)
+    s = run_replay(cfg, jobs, rank, world, torch.device("cpu"), ctrl_pg=ctrl, world_pg=dist.group.WORLD,
+                   worker=w, quantum=0.1, fault={"rank": 1, "round": 3})
+    torch.save(s, os.path.join(outdir, f"f{rank}.pt"))
+    os._exit(0)
+
+
+def test_rank_failure_is_detected(tmp_path):
+    world = 2
+    port = _free_port()
+    ctx = mp.get_context("spawn")
+    ps = [ctx.Process(target=_fault_worker, args=(r, world, port, str(tmp_path))) for r in range(world)]
+    for p in ps:
+        p.start()
+    for p in ps:
+        p.join(120)
+    assert ps[1].exitcode == 17
+    s = torch.load(tmp_path / "f0.pt", weights_only=False)
+    assert s["aborted"] and "rank lost" in s["reason"]

@@ -1,0 +1,140 @@
+"""CLI, profilers, RL environment and utility tests (CPU)."""
+import json
+import os
+import socket
+
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+from tiresias_amd.config import ClusterSpec, SimConfig
+from tiresias_amd.core.job import JobSpec
+
+
+def test_run_sim_cli_writes_outputs(tmp_path):
+    from tiresias_amd.cli import run_sim
+    from tiresias_amd.config import FLAGS
+
+    FLAGS.reset()
+    s = run_sim.main(["--synthetic", "60", "--schedule", "dlas-gpu", "--scheme", "tiresias",
+                      "--num_switch", "1", "--num_node_p_switch", "4", "--num_gpu_p_node", "8",
+                      "--queue_limits", "3600", "--log_path", str(tmp_path / "run")])
+    assert s["finished"] == 60
+    for f in ("cluster.csv", "job.csv", "summary.json", "output.log", "decisions.jsonl"):
+        assert (tmp_path / "run" / f).exists()
+    FLAGS.reset()
+
+
+def test_run_sim_reads_reference_trace_schema(tmp_path):
+    from tiresias_amd.cli import run_sim
+    from tiresias_amd.config import FLAGS
+    from tiresias_amd.trace import readers, synth
+
+    p = tmp_path / "tr.csv"
+    readers.write_tiresias_trace(str(p), synth.SampleTraceGenerator(0).generate_specs(30, max_gpu=8))
+    FLAGS.reset()
+    s = run_sim.main(["--trace_file", str(p), "--schedule", "gittins", "--num_node_p_switch", "2",
+                      "--log_path", str(tmp_path / "g")])
+    assert s["finished"] == 30
+    FLAGS.reset()
+
+
+def test_tick_engine_reference_semantics():
+    from tiresias_amd.engine.sim import simulate
+
+    specs = [JobSpec(str(i), float(i), 5.0, 2, gpu_util_avg=10 * i) for i in range(6)]
+    c = SimConfig(schedule="horus", scheme="horus", engine="tick",
+                  cluster=ClusterSpec(num_switch=1, num_node_p_switch=1, num_gpu_p_node=4))
+    s = simulate(c, specs)
+    assert s["finished"] == 6
+    c2 = SimConfig(schedule="gandiva", scheme="gandiva", engine="tick", timeslice=3,
+                   cluster=ClusterSpec(num_switch=1, num_node_p_switch=1, num_gpu_p_node=2))
+    s2 = simulate(c2, [JobSpec(str(i), 0.0, 7.0, 2, gpu_mem_max=20000.0) for i in range(3)])
+    assert s2["finished"] == 3 and s2["preemptions"] > 0
+
+
+def test_plot_trace_cdf(tmp_path):
+    from tiresias_amd.cli import plot_trace
+
+    rows = plot_trace.main(["--synthetic", "200", "--out", str(tmp_path)])
+    assert (tmp_path / "cdf.csv").exists() and rows[0][0] == "duration"
+
+
+def test_sweep_runs_grid(tmp_path):
+    from tiresias_amd.cli import sweep
+
+    res = sweep.main(["--schedules", "fifo,dlas-gpu", "--schemes", "yarn", "--num_queues", "2",
+                      "--jobs", "2", "--out", str(tmp_path), "--synthetic", "40",
+                      "--num_node_p_switch", "2"])
+    assert len(res) == 2 and (tmp_path / "sweep.csv").exists()
+
+
+def test_scheduling_env_episode():
+    from tiresias_amd.engine.env import SchedulingEnv
+
+    specs = [JobSpec(str(i), float(i), 3.0, 1) for i in range(6)]
+    env = SchedulingEnv(SimConfig(cluster=ClusterSpec(num_switch=1, num_node_p_switch=1, num_gpu_p_node=2)),
+                        specs)
+    obs = env.reset()
+    total, done, n = 0.0, False, 0
+    while not done and n < 1000:
+        obs, r, done, info = env.step(0)
+        total += r
+        n += 1
+    assert done and total < 0
+
+
+def test_memory_estimates_and_utils():
+    from tiresias_amd.profiler import memory
+    from tiresias_amd.utils import misc
+
+    e = memory.estimate_gpu_memory("vgg16", batch=32)
+    assert e["weights_mb"] > 500 and 0 < e["fraction"] < 1
+    assert misc.convert_bytes(2 ** 30, "GiB") == 1.0
+    assert misc.search_dict_list([{"t": 1}, {"t": 2}], "t", 2) == {"t": 2}
+    with pytest.raises(misc.SchedulerError):
+        misc.print_fn("boom", misc.LOG_LEVEL_ERROR)
+
+
+def test_model_profiles_skew():
+    from tiresias_amd.profiler.skew import SensitivityOracle, model_profile
+
+    v, r = model_profile("vgg16"), model_profile("resnet50")
+    assert v.skew > 0.5 > r.skew                       # VGG's FC layer dominates
+    assert 24e6 < r.params < 27e6 and 130e6 < v.params < 145e6
+    o = SensitivityOracle(0.5)
+    from tiresias_amd.core.job import Job
+
+    assert o(Job(JobSpec("0", 0, 1, 2, model="vgg16"))) and not o(Job(JobSpec("1", 0, 1, 2, model="resnet50")))
+    assert model_profile("alexnet").skew > 0.5     # legacy table still served
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _comm_worker(rank, world, port, outdir):
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    from tiresias_amd.profiler.comm import CommProfiler
+
+    p = CommProfiler(dist.group.WORLD, device=torch.device("cpu"), iters=2, warmup=1)
+    res = p.sweep([0.25, 1.0], {"consolidated": [0, 1], "spread": [0, 2]})
+    if rank == 0:
+        cls = p.classify_models(["resnet50", "vgg16"], res)
+        torch.save({"res": res, "cls": cls}, os.path.join(outdir, "comm.pt"))
+    dist.destroy_process_group()
+
+
+def test_comm_profiler_gloo(tmp_path):
+    world = 3
+    mp.spawn(_comm_worker, args=(world, _free_port(), str(tmp_path)), nprocs=world, join=True)
+    d = torch.load(tmp_path / "comm.pt", weights_only=False)
+    assert set(d["res"]) == {"consolidated", "spread"} and len(d["res"]["consolidated"]) == 2
+    assert d["cls"]["vgg16"]["consolidated_s"] > d["cls"]["resnet50"]["consolidated_s"]

@@ -300,16 +300,42 @@ class Worker:
         self.trainers.clear()
 
 
+def _abort(ctrl: "Controller", log, rounds: int, reason: str) -> dict:
+    s = ctrl.sched
+    lost = []
+    for j in list(s.active):
+        if j.job_id in ctrl.holders:
+            j.state = JobState.FAILED
+            lost.append(j.job_id)
+    summ = s.summary()
+    summ.update(aborted=True, reason=reason, rounds=rounds, lost_jobs=lost)
+    if log:
+        log.decision(s.now, "abort", "-", reason=reason)
+        log.close()
+    return summ
+
+
 def _bcast(obj, src, pg):
     lst = [obj]
     dist.broadcast_object_list(lst, src=src, group=pg)
     return lst[0]
 
 
+class RankLost(RuntimeError):
+    pass
+
+
 def run_replay(cfg: SimConfig, jobs: List[ReplayJob], rank: int, world: int, device: torch.device,
                ctrl_pg=None, world_pg=None, worker: Optional[Worker] = None, quantum: float = 0.4,
-               out_dir: Optional[str] = None, use_graph: bool = False, max_rounds: int = 100000) -> Optional[dict]:
-    """Replay ``jobs`` on the live cluster. Returns the summary on rank 0."""
+               out_dir: Optional[str] = None, use_graph: bool = False, max_rounds: int = 100000,
+               fault: Optional[dict] = None) -> Optional[dict]:
+    """Replay ``jobs`` on the live cluster. Returns the summary on rank 0.
+
+    ``fault={"rank": r, "round": k}`` injects a crash of rank r at round k
+    (failure-detection test): the per-round gather doubles as the heartbeat,
+    so the controller sees the lost rank as a collective error / timeout,
+    marks the jobs that had state on it FAILED and aborts the replay cleanly.
+    """
     distributed = world > 1
     ctrl = None
     log = None
@@ -333,6 +359,8 @@ def run_replay(cfg: SimConfig, jobs: List[ReplayJob], rank: int, world: int, dev
         tc = time.perf_counter()
         if plan["stop"]:
             break
+        if fault and fault.get("rank") == rank and rounds >= fault.get("round", 0):
+            os._exit(17)                         # simulated node/rank crash
         w.apply(plan)
         td = time.perf_counter()
         rep = w.run(plan)
@@ -345,7 +373,12 @@ def run_replay(cfg: SimConfig, jobs: List[ReplayJob], rank: int, world: int, dev
             time.sleep(plan["wait"])
         if distributed:
             reps = [None] * world if rank == 0 else None
-            dist.gather_object(rep, reps, dst=0, group=ctrl_pg)
+            try:
+                dist.gather_object(rep, reps, dst=0, group=ctrl_pg)
+            except Exception as e:                 # heartbeat lost
+                if ctrl:
+                    return _abort(ctrl, log, rounds, f"rank lost during round {rounds}: {e}")
+                raise RankLost(str(e))
         else:
             reps = [rep]
         if ctrl:
