@@ -153,38 +153,34 @@ void conv_wgrad_op(const Tensor& dy, const Tensor& x, const Tensor& dw, int64_t 
 void bn_forward_op(const Tensor& x, const optional<Tensor>& res, const Tensor& y, const Tensor& gamma,
                    const Tensor& beta, const optional<Tensor>& run_mean,
                    const optional<Tensor>& run_var, const Tensor& save_mean,
-                   const Tensor& save_rstd, const Tensor& ws_d, const Tensor& ws_f, double eps,
-                   double momentum, bool relu) {
+                   const Tensor& save_rstd, double eps, double momentum, bool relu) {
   check_bf16(x, "x"); check_bf16(y, "y"); check_contig(x, "x"); check_contig(y, "y");
   check_f32(gamma, "gamma"); check_f32(beta, "beta");
   const int64_t C = x.size(-1);
   const int64_t M = x.numel() / C;
   TORCH_CHECK(C % 8 == 0 && C <= 2048, "tam.bn: C must be a multiple of 8 and <= 2048");
-  TORCH_CHECK(ws_d.scalar_type() == at::kDouble && ws_d.numel() >= 2 * C, "tam.bn: ws_d");
-  TORCH_CHECK(ws_f.numel() >= 2 * C, "tam.bn: ws_f");
+  Tensor ws_f = at::empty({(2 + 2 * tam::BN_MAX_BLOCKS) * C}, x.options().dtype(at::kFloat));
   if (res.has_value() && res->defined()) { check_bf16(*res, "res"); check_contig(*res, "res"); }
   tam::bn_forward(bp(x), opt_ptr<const tam::bf16_t>(res), bpm(y), M, (int)C, (float)eps,
                   (float)momentum, gamma.data_ptr<float>(), beta.data_ptr<float>(),
                   opt_ptr<float>(run_mean), opt_ptr<float>(run_var), save_mean.data_ptr<float>(),
-                  save_rstd.data_ptr<float>(), ws_d.data_ptr<double>(), ws_f.data_ptr<float>(),
-                  relu, cur_stream(x));
+                  save_rstd.data_ptr<float>(), ws_f.data_ptr<float>(), relu, cur_stream(x));
 }
 
 void bn_backward_op(const Tensor& dy, const optional<Tensor>& y, const Tensor& x, const Tensor& mean,
                     const Tensor& rstd, const Tensor& gamma, const Tensor& dx,
                     const optional<Tensor>& dres, const optional<Tensor>& dgamma,
-                    const optional<Tensor>& dbeta, const Tensor& ws_d, const Tensor& ws_f,
-                    bool relu) {
+                    const optional<Tensor>& dbeta, bool relu) {
   check_bf16(dy, "dy"); check_bf16(x, "x"); check_bf16(dx, "dx");
   check_contig(dy, "dy"); check_contig(x, "x"); check_contig(dx, "dx");
   const int64_t C = x.size(-1);
   const int64_t M = x.numel() / C;
   TORCH_CHECK(!relu || (y.has_value() && y->defined()), "tam.bn_backward: relu needs y");
-  TORCH_CHECK(ws_d.numel() >= 2 * C && ws_f.numel() >= 3 * C, "tam.bn_backward: workspace");
+  Tensor ws_f = at::empty({(3 + 2 * tam::BN_MAX_BLOCKS) * C}, x.options().dtype(at::kFloat));
   tam::bn_backward(bp(dy), opt_ptr<const tam::bf16_t>(y), bp(x), mean.data_ptr<float>(),
                    rstd.data_ptr<float>(), gamma.data_ptr<float>(), M, (int)C, relu, bpm(dx),
                    opt_ptr<tam::bf16_t>(dres), opt_ptr<float>(dgamma), opt_ptr<float>(dbeta),
-                   ws_d.data_ptr<double>(), ws_f.data_ptr<float>(), cur_stream(x));
+                   ws_f.data_ptr<float>(), cur_stream(x));
 }
 
 void ln_forward_op(const Tensor& x, const Tensor& g, const Tensor& b, const Tensor& y,
@@ -203,9 +199,10 @@ void ln_backward_op(const Tensor& dy, const Tensor& x, const Tensor& g, const Te
   check_contig(dy, "dy"); check_contig(x, "x"); check_contig(dx, "dx");
   check_f32(dg, "dg"); check_f32(db, "db");
   const int64_t D = x.size(-1);
+  Tensor ws = at::empty({(int64_t)tam::LN_MAX_BLOCKS * 2 * D}, x.options().dtype(at::kFloat));
   tam::ln_backward(bp(dy), bp(x), g.data_ptr<float>(), mean.data_ptr<float>(),
                    rstd.data_ptr<float>(), bpm(dx), dg.data_ptr<float>(), db.data_ptr<float>(),
-                   x.numel() / D, (int)D, cur_stream(x));
+                   ws.data_ptr<float>(), x.numel() / D, (int)D, cur_stream(x));
 }
 
 // ------------------------------------------------------------------ pooling
@@ -370,8 +367,8 @@ TORCH_LIBRARY(tam, m) {
   m.def("conv_fwd(Tensor x, Tensor w, Tensor(a!) y, int stride, int pad, int dil, Tensor? bias, bool relu) -> ()", &conv_fwd_op);
   m.def("conv_dgrad(Tensor dy, Tensor w, Tensor(a!) wt, Tensor(b!) dx, int stride, int pad, int dil, Tensor? mask) -> ()", &conv_dgrad_op);
   m.def("conv_wgrad(Tensor dy, Tensor x, Tensor(a!) dw, int stride, int pad, int dil, int mode) -> ()", &conv_wgrad_op);
-  m.def("bn_forward(Tensor x, Tensor? res, Tensor(a!) y, Tensor gamma, Tensor beta, Tensor(b!)? run_mean, Tensor(c!)? run_var, Tensor(d!) save_mean, Tensor(e!) save_rstd, Tensor(f!) ws_d, Tensor(g!) ws_f, float eps, float momentum, bool relu) -> ()", &bn_forward_op);
-  m.def("bn_backward(Tensor dy, Tensor? y, Tensor x, Tensor mean, Tensor rstd, Tensor gamma, Tensor(a!) dx, Tensor(b!)? dres, Tensor(c!)? dgamma, Tensor(d!)? dbeta, Tensor(e!) ws_d, Tensor(f!) ws_f, bool relu) -> ()", &bn_backward_op);
+  m.def("bn_forward(Tensor x, Tensor? res, Tensor(a!) y, Tensor gamma, Tensor beta, Tensor(b!)? run_mean, Tensor(c!)? run_var, Tensor(d!) save_mean, Tensor(e!) save_rstd, float eps, float momentum, bool relu) -> ()", &bn_forward_op);
+  m.def("bn_backward(Tensor dy, Tensor? y, Tensor x, Tensor mean, Tensor rstd, Tensor gamma, Tensor(a!) dx, Tensor(b!)? dres, Tensor(c!)? dgamma, Tensor(d!)? dbeta, bool relu) -> ()", &bn_backward_op);
   m.def("ln_forward(Tensor x, Tensor g, Tensor b, Tensor(a!) y, Tensor(b!) mean, Tensor(c!) rstd, float eps) -> ()", &ln_forward_op);
   m.def("ln_backward(Tensor dy, Tensor x, Tensor g, Tensor mean, Tensor rstd, Tensor(a!) dx, Tensor(b!) dg, Tensor(c!) db) -> ()", &ln_backward_op);
   m.def("maxpool_forward(Tensor x, Tensor(a!) y, Tensor(b!) idx, int R, int S, int stride, int pad) -> ()", &maxpool_forward_op);

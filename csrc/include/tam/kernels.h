@@ -6,23 +6,25 @@
 
 namespace tam {
 
-// BatchNorm (NHWC rows=M=N*H*W, C channels, C % 8 == 0, C <= 2048)
+// BatchNorm (NHWC rows=M=N*H*W, C channels, C % 8 == 0, C <= 2048).
+// Reductions write per-block partial rows (<= BN_MAX_BLOCKS), no atomics.
+constexpr int BN_MAX_BLOCKS = 512;
+constexpr int LN_MAX_BLOCKS = 512;
 void bn_forward(const bf16_t* x, const bf16_t* res, bf16_t* y, long M, int C, float eps,
                 float momentum, const float* gamma, const float* beta, float* run_mean,
-                float* run_var, float* save_mean, float* save_rstd, double* ws, float* ws_f,
-                int relu, hipStream_t s);
+                float* run_var, float* save_mean, float* save_rstd, float* ws_f, int relu,
+                hipStream_t s);
 void bn_infer(const bf16_t* x, const bf16_t* res, bf16_t* y, long M, int C, const float* scale,
               const float* shift, int relu, hipStream_t s);
 void bn_backward(const bf16_t* dy, const bf16_t* y, const bf16_t* x, const float* mean,
                  const float* rstd, const float* gamma, long M, int C, int relu, bf16_t* dx,
-                 bf16_t* dres, float* dgamma, float* dbeta, double* ws, float* ws_f,
-                 hipStream_t s);
+                 bf16_t* dres, float* dgamma, float* dbeta, float* ws_f, hipStream_t s);
 
 // LayerNorm over last dim D (D % 8 == 0, D <= 2048)
 void ln_forward(const bf16_t* x, const float* g, const float* b, bf16_t* y, float* mean,
                 float* rstd, long rows, int D, float eps, hipStream_t s);
 void ln_backward(const bf16_t* dy, const bf16_t* x, const float* g, const float* mean,
-                 const float* rstd, bf16_t* dx, float* dg, float* db, long rows, int D,
+                 const float* rstd, bf16_t* dx, float* dg, float* db, float* ws, long rows, int D,
                  hipStream_t s);
 
 // pooling

@@ -28,8 +28,8 @@ __device__ __forceinline__ uint4 pack8(const float (&f)[8]) {
 // grid.x blocks each own a contiguous row range; thread = (row lane, 8-ch group)
 __global__ void __launch_bounds__(256) bn_stats_kernel(const bf16_t* __restrict__ x, long M, int C,
                                                         long rows_per_block,
-                                                        double* __restrict__ sum,
-                                                        double* __restrict__ sumsq) {
+                                                        float* __restrict__ psum,
+                                                        float* __restrict__ psq) {
   __shared__ float red[256 * 16];
   const int tpr = C / 8;                 // threads per row
   const int rpb = 256 / tpr;             // rows per pass (C <= 2048)
@@ -56,25 +56,30 @@ __global__ void __launch_bounds__(256) bn_stats_kernel(const bf16_t* __restrict_
 #pragma unroll
       for (int i = 0; i < 8; ++i) { s[i] += red[t * 16 + i]; q[i] += red[t * 16 + 8 + i]; }
     }
+    // one partial row per block: no atomics, deterministic
+    float* ps = psum + (long)blockIdx.x * C + cg * 8;
+    float* pq = psq + (long)blockIdx.x * C + cg * 8;
 #pragma unroll
-    for (int i = 0; i < 8; ++i) {
-      atomicAdd(sum + cg * 8 + i, (double)s[i]);
-      atomicAdd(sumsq + cg * 8 + i, (double)q[i]);
-    }
+    for (int i = 0; i < 8; ++i) { ps[i] = s[i]; pq[i] = q[i]; }
   }
 }
 
 // mean/rstd + fused scale/shift + running-stat update
-__global__ void bn_finalize_kernel(const double* __restrict__ sum, const double* __restrict__ sumsq,
-                                   long M, int C, float eps, float momentum,
+__global__ void bn_finalize_kernel(const float* __restrict__ psum, const float* __restrict__ psq,
+                                   int nblk, long M, int C, float eps, float momentum,
                                    const float* __restrict__ gamma, const float* __restrict__ beta,
                                    float* __restrict__ mean_out, float* __restrict__ rstd_out,
                                    float* __restrict__ scale, float* __restrict__ shift,
                                    float* __restrict__ run_mean, float* __restrict__ run_var) {
   const int c = blockIdx.x * blockDim.x + threadIdx.x;
   if (c >= C) return;
-  const double mean = sum[c] / (double)M;
-  double var = sumsq[c] / (double)M - mean * mean;
+  double sm = 0.0, sq = 0.0;
+  for (int b = 0; b < nblk; ++b) {
+    sm += (double)psum[(long)b * C + c];
+    sq += (double)psq[(long)b * C + c];
+  }
+  const double mean = sm / (double)M;
+  double var = sq / (double)M - mean * mean;
   if (var < 0) var = 0;
   const float rstd = (float)(1.0 / sqrt(var + (double)eps));
   mean_out[c] = (float)mean;
@@ -124,7 +129,7 @@ __global__ void __launch_bounds__(256) bn_apply_kernel(const bf16_t* __restrict_
 __global__ void __launch_bounds__(256) bn_bwd_reduce_kernel(
     const bf16_t* __restrict__ dy, const bf16_t* __restrict__ y, const bf16_t* __restrict__ x,
     const float* __restrict__ mean, const float* __restrict__ rstd, long M, int C,
-    long rows_per_block, int relu, double* __restrict__ sdy, double* __restrict__ sdyx) {
+    long rows_per_block, int relu, float* __restrict__ pdy, float* __restrict__ pdyx) {
   __shared__ float red[256 * 16];
   const int tpr = C / 8, rpb = 256 / tpr;
   const int cg = threadIdx.x % tpr, rl = threadIdx.x / tpr;
@@ -157,23 +162,27 @@ __global__ void __launch_bounds__(256) bn_bwd_reduce_kernel(
 #pragma unroll
       for (int i = 0; i < 8; ++i) { a[i] += red[t * 16 + i]; b[i] += red[t * 16 + 8 + i]; }
     }
+    float* pa = pdy + (long)blockIdx.x * C + cg * 8;
+    float* pb = pdyx + (long)blockIdx.x * C + cg * 8;
 #pragma unroll
-    for (int i = 0; i < 8; ++i) {
-      atomicAdd(sdy + cg * 8 + i, (double)a[i]);
-      atomicAdd(sdyx + cg * 8 + i, (double)b[i]);
-    }
+    for (int i = 0; i < 8; ++i) { pa[i] = a[i]; pb[i] = b[i]; }
   }
 }
 
 // dgamma/dbeta accumulate into fp32 grads; coefficient prep for the apply pass
-__global__ void bn_bwd_finalize_kernel(const double* __restrict__ sdy, const double* __restrict__ sdyx,
-                                       long M, int C, const float* __restrict__ gamma,
+__global__ void bn_bwd_finalize_kernel(const float* __restrict__ pdy, const float* __restrict__ pdyx,
+                                       int nblk, long M, int C, const float* __restrict__ gamma,
                                        const float* __restrict__ rstd, float* __restrict__ dgamma,
                                        float* __restrict__ dbeta, float* __restrict__ k1,
                                        float* __restrict__ k2, float* __restrict__ k3) {
   const int c = blockIdx.x * blockDim.x + threadIdx.x;
   if (c >= C) return;
-  const float a = (float)sdy[c], b = (float)sdyx[c];
+  double da = 0.0, db = 0.0;
+  for (int k = 0; k < nblk; ++k) {
+    da += (double)pdy[(long)k * C + c];
+    db += (double)pdyx[(long)k * C + c];
+  }
+  const float a = (float)da, b = (float)db;
   if (dgamma) dgamma[c] += b;
   if (dbeta) dbeta[c] += a;
   // dx = g*rstd*(dyr - a/M - xhat*b/M) = k1*dyr + k2*xhat + k3
@@ -220,8 +229,9 @@ static int grid_for(long n, int per_thread_vec = 1) {
 }
 
 static long bn_rows_per_block(long M, int C) {
-  // ~ 1024 blocks in flight (4/CU) for the reduction passes
-  long rpb = (M + 1023) / 1024;
+  // <= BN_MAX_BLOCKS partial rows (2 blocks per CU on 256 CUs); each block
+  // streams >= 4 passes of its thread grid so the loads stay 16 B/lane
+  long rpb = (M + BN_MAX_BLOCKS - 1) / BN_MAX_BLOCKS;
   const long minr = 256 / (C / 8) * 4;
   if (rpb < minr) rpb = minr;
   return rpb;
@@ -229,16 +239,17 @@ static long bn_rows_per_block(long M, int C) {
 
 void bn_forward(const bf16_t* x, const bf16_t* res, bf16_t* y, long M, int C, float eps,
                 float momentum, const float* gamma, const float* beta, float* run_mean,
-                float* run_var, float* save_mean, float* save_rstd, double* ws, float* ws_f,
-                int relu, hipStream_t s) {
-  // ws: 2*C doubles; ws_f: 2*C floats (scale, shift)
-  TAM_HIP_CHECK(hipMemsetAsync(ws, 0, sizeof(double) * 2 * C, s));
+                float* run_var, float* save_mean, float* save_rstd, float* ws_f, int relu,
+                hipStream_t s) {
+  // ws_f: (2 + 2*BN_MAX_BLOCKS) * C floats: scale, shift, partial sums / sums of squares
   const long rpb = bn_rows_per_block(M, C);
   const int nb = (int)((M + rpb - 1) / rpb);
-  hipLaunchKernelGGL(bn_stats_kernel, dim3(nb), dim3(256), 0, s, x, M, C, rpb, ws, ws + C);
-  hipLaunchKernelGGL(bn_finalize_kernel, dim3((C + 255) / 256), dim3(256), 0, s, ws, ws + C, M, C,
-                     eps, momentum, gamma, beta, save_mean, save_rstd, ws_f, ws_f + C, run_mean,
-                     run_var);
+  float* part = ws_f + 2 * C;
+  hipLaunchKernelGGL(bn_stats_kernel, dim3(nb), dim3(256), 0, s, x, M, C, rpb, part,
+                     part + (long)nb * C);
+  hipLaunchKernelGGL(bn_finalize_kernel, dim3((C + 255) / 256), dim3(256), 0, s, part,
+                     part + (long)nb * C, nb, M, C, eps, momentum, gamma, beta, save_mean, save_rstd,
+                     ws_f, ws_f + C, run_mean, run_var);
   const long total8 = M * C / 8;
   hipLaunchKernelGGL(bn_apply_kernel, dim3(grid_for(total8)), dim3(256), 0, s, x, res, ws_f,
                      ws_f + C, y, total8, C, relu);
@@ -253,16 +264,16 @@ void bn_infer(const bf16_t* x, const bf16_t* res, bf16_t* y, long M, int C, cons
 
 void bn_backward(const bf16_t* dy, const bf16_t* y, const bf16_t* x, const float* mean,
                  const float* rstd, const float* gamma, long M, int C, int relu, bf16_t* dx,
-                 bf16_t* dres, float* dgamma, float* dbeta, double* ws, float* ws_f,
-                 hipStream_t s) {
-  // ws: 2*C doubles; ws_f: 3*C floats
-  TAM_HIP_CHECK(hipMemsetAsync(ws, 0, sizeof(double) * 2 * C, s));
+                 bf16_t* dres, float* dgamma, float* dbeta, float* ws_f, hipStream_t s) {
+  // ws_f: (3 + 2*BN_MAX_BLOCKS) * C floats: k1, k2, k3, partials
   const long rpb = bn_rows_per_block(M, C);
   const int nb = (int)((M + rpb - 1) / rpb);
+  float* part = ws_f + 3 * C;
   hipLaunchKernelGGL(bn_bwd_reduce_kernel, dim3(nb), dim3(256), 0, s, dy, y, x, mean, rstd, M, C,
-                     rpb, relu, ws, ws + C);
-  hipLaunchKernelGGL(bn_bwd_finalize_kernel, dim3((C + 255) / 256), dim3(256), 0, s, ws, ws + C, M,
-                     C, gamma, rstd, dgamma, dbeta, ws_f, ws_f + C, ws_f + 2 * C);
+                     rpb, relu, part, part + (long)nb * C);
+  hipLaunchKernelGGL(bn_bwd_finalize_kernel, dim3((C + 255) / 256), dim3(256), 0, s, part,
+                     part + (long)nb * C, nb, M, C, gamma, rstd, dgamma, dbeta, ws_f, ws_f + C,
+                     ws_f + 2 * C);
   const long total8 = M * C / 8;
   hipLaunchKernelGGL(bn_bwd_apply_kernel, dim3(grid_for(total8)), dim3(256), 0, s, dy, y, x, mean,
                      rstd, ws_f, ws_f + C, ws_f + 2 * C, dx, dres, total8, C, relu);
@@ -326,11 +337,12 @@ __global__ void __launch_bounds__(256) ln_bwd_kernel(const bf16_t* __restrict__ 
                                                       const float* __restrict__ mean,
                                                       const float* __restrict__ rstd,
                                                       bf16_t* __restrict__ dx,
-                                                      float* __restrict__ dg_part,
-                                                      float* __restrict__ db_part, long rows,
+                                                      float* __restrict__ part, long rows,
                                                       int D, int rows_per_block) {
-  // each wave processes rows_per_block/4 rows, accumulating dgamma/dbeta in regs,
-  // then atomically adds its partials (fp32) — grid sized to ~1024 waves.
+  // each wave processes rows_per_block/4 rows, accumulating dgamma/dbeta in
+  // registers; the 4 waves combine through LDS and the block writes ONE
+  // partial row [2*D] (no atomics; a column-reduce kernel finishes).
+  __shared__ float red[4 * 2 * VEC * 64 * 8];
   const int lane = threadIdx.x & 63;
   const int w = threadIdx.x >> 6;
   float dgacc[VEC][8], dbacc[VEC][8];
@@ -374,17 +386,36 @@ __global__ void __launch_bounds__(256) ln_bwd_kernel(const bf16_t* __restrict__ 
       }
     }
   }
+  // LDS layout: [wave][2][VEC*64*8]
+  const int W = VEC * 64 * 8;
 #pragma unroll
-  for (int v = 0; v < VEC; ++v) {
-    const int c = (v * 64 + lane) * 8;
-    if (c < D) {
+  for (int v = 0; v < VEC; ++v)
 #pragma unroll
-      for (int j = 0; j < 8; ++j) {
-        atomicAdd(dg_part + c + j, dgacc[v][j]);
-        atomicAdd(db_part + c + j, dbacc[v][j]);
-      }
+    for (int j = 0; j < 8; ++j) {
+      const int c = (v * 64 + lane) * 8 + j;
+      red[(w * 2 + 0) * W + c] = dgacc[v][j];
+      red[(w * 2 + 1) * W + c] = dbacc[v][j];
     }
+  __syncthreads();
+  float* out = part + (long)blockIdx.x * 2 * D;
+  for (int c = threadIdx.x; c < D; c += 256) {
+    float g = 0.f, b = 0.f;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) { g += red[(k * 2) * W + c]; b += red[(k * 2 + 1) * W + c]; }
+    out[c] = g;
+    out[D + c] = b;
   }
+}
+
+// dg[c] += sum_b part[b][c]; db[c] += sum_b part[b][D + c]
+__global__ void ln_grad_reduce_kernel(const float* __restrict__ part, int nblk, int D,
+                                      float* __restrict__ dg, float* __restrict__ db) {
+  const int c = blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= 2 * D) return;
+  float s = 0.f;
+  for (int b = 0; b < nblk; ++b) s += part[(long)b * 2 * D + c];
+  if (c < D) dg[c] += s;
+  else db[c - D] += s;
 }
 
 void ln_forward(const bf16_t* x, const float* g, const float* b, bf16_t* y, float* mean,
@@ -396,15 +427,18 @@ void ln_forward(const bf16_t* x, const float* g, const float* b, bf16_t* y, floa
 }
 
 void ln_backward(const bf16_t* dy, const bf16_t* x, const float* g, const float* mean,
-                 const float* rstd, bf16_t* dx, float* dg, float* db, long rows, int D,
+                 const float* rstd, bf16_t* dx, float* dg, float* db, float* ws, long rows, int D,
                  hipStream_t s) {
-  int rpb = (int)((rows + 1023) / 1024);
+  // ws: LN_MAX_BLOCKS * 2 * D floats of per-block partial dgamma / dbeta
+  int rpb = (int)((rows + LN_MAX_BLOCKS - 1) / LN_MAX_BLOCKS);
   rpb = ((rpb + 3) / 4) * 4;
-  if (rpb < 16) rpb = 16;
+  if (rpb < 8) rpb = 8;
   const int blocks = (int)((rows + rpb - 1) / rpb);
-  if (D <= 512) hipLaunchKernelGGL(ln_bwd_kernel<1>, dim3(blocks), dim3(256), 0, s, dy, x, g, mean, rstd, dx, dg, db, rows, D, rpb);
-  else if (D <= 1024) hipLaunchKernelGGL(ln_bwd_kernel<2>, dim3(blocks), dim3(256), 0, s, dy, x, g, mean, rstd, dx, dg, db, rows, D, rpb);
-  else hipLaunchKernelGGL(ln_bwd_kernel<4>, dim3(blocks), dim3(256), 0, s, dy, x, g, mean, rstd, dx, dg, db, rows, D, rpb);
+  if (D <= 512) hipLaunchKernelGGL(ln_bwd_kernel<1>, dim3(blocks), dim3(256), 0, s, dy, x, g, mean, rstd, dx, ws, rows, D, rpb);
+  else if (D <= 1024) hipLaunchKernelGGL(ln_bwd_kernel<2>, dim3(blocks), dim3(256), 0, s, dy, x, g, mean, rstd, dx, ws, rows, D, rpb);
+  else hipLaunchKernelGGL(ln_bwd_kernel<4>, dim3(blocks), dim3(256), 0, s, dy, x, g, mean, rstd, dx, ws, rows, D, rpb);
+  hipLaunchKernelGGL(ln_grad_reduce_kernel, dim3((2 * D + 255) / 256), dim3(256), 0, s, ws, blocks, D,
+                     dg, db);
 }
 
 }  // namespace tam

@@ -72,13 +72,107 @@ __global__ void maxpool_bwd_kernel(const bf16_t* __restrict__ dy, const uint8_t*
   }
 }
 
+// 8-channel vector forms (C % 8 == 0): one (n,h,w,8c) tuple per thread, 16 B
+// loads of x/dy and 8 B loads of idx; index math amortised over 8 channels.
+__global__ void maxpool_fwd8_kernel(const bf16_t* __restrict__ x, bf16_t* __restrict__ y,
+                                    uint8_t* __restrict__ idx, int N, int H, int W, int C, int P,
+                                    int Q, int R, int S, int st, int pad) {
+  const int C8 = C / 8;
+  const long total = (long)N * P * Q * C8;
+  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < total;
+       i += (long)gridDim.x * blockDim.x) {
+    const int c = (int)(i % C8) * 8;
+    long t = i / C8;
+    const int q = (int)(t % Q); t /= Q;
+    const int p = (int)(t % P);
+    const int n = (int)(t / P);
+    float best[8];
+    uint32_t bi[8];
+#pragma unroll
+    for (int k = 0; k < 8; ++k) { best[k] = -INFINITY; bi[k] = 0; }
+    for (int r = 0; r < R; ++r) {
+      const int h = p * st - pad + r;
+      if ((unsigned)h >= (unsigned)H) continue;
+      for (int s = 0; s < S; ++s) {
+        const int w = q * st - pad + s;
+        if ((unsigned)w >= (unsigned)W) continue;
+        const uint4 v = *(const uint4*)(x + (((long)n * H + h) * W + w) * C + c);
+        const uint32_t wv[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+          const float a = __uint_as_float(wv[k] << 16), b = __uint_as_float(wv[k] & 0xffff0000u);
+          if (a > best[2 * k]) { best[2 * k] = a; bi[2 * k] = r * S + s; }
+          if (b > best[2 * k + 1]) { best[2 * k + 1] = b; bi[2 * k + 1] = r * S + s; }
+        }
+      }
+    }
+    const long o = i * 8;
+    *(uint4*)(y + o) = make_uint4(pack_bf2(best[0], best[1]), pack_bf2(best[2], best[3]),
+                                  pack_bf2(best[4], best[5]), pack_bf2(best[6], best[7]));
+    *(uint2*)(idx + o) = make_uint2(bi[0] | (bi[1] << 8) | (bi[2] << 16) | (bi[3] << 24),
+                                    bi[4] | (bi[5] << 8) | (bi[6] << 16) | (bi[7] << 24));
+  }
+}
+
+__global__ void maxpool_bwd8_kernel(const bf16_t* __restrict__ dy, const uint8_t* __restrict__ idx,
+                                    bf16_t* __restrict__ dx, int N, int H, int W, int C, int P,
+                                    int Q, int R, int S, int st, int pad) {
+  const int C8 = C / 8;
+  const long total = (long)N * H * W * C8;
+  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < total;
+       i += (long)gridDim.x * blockDim.x) {
+    const int c = (int)(i % C8) * 8;
+    long t = i / C8;
+    const int w = (int)(t % W); t /= W;
+    const int h = (int)(t % H);
+    const int n = (int)(t / H);
+    float acc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+    for (int r = 0; r < R; ++r) {
+      const int pn = h + pad - r;
+      if (pn < 0 || pn % st) continue;
+      const int p = pn / st;
+      if (p >= P) continue;
+      for (int s = 0; s < S; ++s) {
+        const int qn = w + pad - s;
+        if (qn < 0 || qn % st) continue;
+        const int q = qn / st;
+        if (q >= Q) continue;
+        const long o = (((long)n * P + p) * Q + q) * C + c;
+        const uint2 ix = *(const uint2*)(idx + o);
+        const uint4 d = *(const uint4*)(dy + o);
+        const uint32_t wd[4] = {d.x, d.y, d.z, d.w};
+        const uint32_t tap = (uint32_t)(r * S + s);
+#pragma unroll
+        for (int k = 0; k < 8; ++k) {
+          const uint32_t b = ((k < 4 ? ix.x : ix.y) >> (8 * (k & 3))) & 0xffu;
+          const uint32_t wk = wd[k >> 1];
+          const float g = __uint_as_float((k & 1) ? (wk & 0xffff0000u) : (wk << 16));
+          if (b == tap) acc[k] += g;
+        }
+      }
+    }
+    *(uint4*)(dx + i * 8) = make_uint4(pack_bf2(acc[0], acc[1]), pack_bf2(acc[2], acc[3]),
+                                       pack_bf2(acc[4], acc[5]), pack_bf2(acc[6], acc[7]));
+  }
+}
+
 void maxpool_forward(const bf16_t* x, bf16_t* y, uint8_t* idx, int N, int H, int W, int C, int P,
                      int Q, int R, int S, int st, int pad, hipStream_t s) {
+  if (C % 8 == 0) {
+    hipLaunchKernelGGL(maxpool_fwd8_kernel, dim3(grid_cap((long)N * P * Q * (C / 8))), dim3(256), 0,
+                       s, x, y, idx, N, H, W, C, P, Q, R, S, st, pad);
+    return;
+  }
   hipLaunchKernelGGL(maxpool_fwd_kernel, dim3(grid_cap((long)N * P * Q * C)), dim3(256), 0, s, x, y,
                      idx, N, H, W, C, P, Q, R, S, st, pad);
 }
 void maxpool_backward(const bf16_t* dy, const uint8_t* idx, bf16_t* dx, int N, int H, int W, int C,
                       int P, int Q, int R, int S, int st, int pad, hipStream_t s) {
+  if (C % 8 == 0) {
+    hipLaunchKernelGGL(maxpool_bwd8_kernel, dim3(grid_cap((long)N * H * W * (C / 8))), dim3(256), 0,
+                       s, dy, idx, dx, N, H, W, C, P, Q, R, S, st, pad);
+    return;
+  }
   hipLaunchKernelGGL(maxpool_bwd_kernel, dim3(grid_cap((long)N * H * W * C)), dim3(256), 0, s, dy,
                      idx, dx, N, H, W, C, P, Q, R, S, st, pad);
 }
@@ -253,6 +347,7 @@ void embedding_backward(const bf16_t* dout, const long* ids, float* gtable, long
 // out[c] (+)= sum_r x[r][c] (bias gradients), fp32 accumulate, relu-mask opt.
 __global__ void colsum_kernel(const bf16_t* __restrict__ x, float* __restrict__ out, long R, int C,
                               long rows_per_block) {
+  // scalar path for C % 8 != 0
   const long r0 = blockIdx.y * rows_per_block;
   const long r1 = min(R, r0 + rows_per_block);
   for (int c = blockIdx.x * blockDim.x + threadIdx.x; c < C; c += gridDim.x * blockDim.x) {
@@ -261,7 +356,60 @@ __global__ void colsum_kernel(const bf16_t* __restrict__ x, float* __restrict__ 
     atomicAdd(out + c, s);
   }
 }
+
+// C % 8 == 0: block = (row lane rl, 8-column group cg) over a <=2048-column
+// chunk, 16 B loads, LDS combine over row lanes, one atomic per column/block.
+__global__ void __launch_bounds__(256) colsum8_kernel(const bf16_t* __restrict__ x,
+                                                       float* __restrict__ out, long R, int C,
+                                                       long rows_per_block) {
+  __shared__ float red[256 * 8];
+  const int c0 = blockIdx.x * 2048;
+  const int cw = min(2048, C - c0);
+  const int tpr = cw / 8 < 256 ? cw / 8 : 256;
+  const int rpp = 256 / tpr;
+  const int cg = threadIdx.x % tpr, rl = threadIdx.x / tpr;
+  const long r0 = blockIdx.y * rows_per_block;
+  const long r1 = min(R, r0 + rows_per_block);
+  for (int cb = 0; cb < cw; cb += tpr * 8) {
+    const int c = c0 + cb + cg * 8;
+    float s[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+    if (rl < rpp && c < c0 + cw) {
+      for (long r = r0 + rl; r < r1; r += rpp) {
+        const uint4 v = *(const uint4*)(x + r * C + c);
+        const uint32_t w[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+          s[2 * k] += __uint_as_float(w[k] << 16);
+          s[2 * k + 1] += __uint_as_float(w[k] & 0xffff0000u);
+        }
+      }
+    }
+#pragma unroll
+    for (int k = 0; k < 8; ++k) red[threadIdx.x * 8 + k] = s[k];
+    __syncthreads();
+    if (rl == 0 && c < c0 + cw) {
+      for (int j = 1; j < rpp; ++j)
+#pragma unroll
+        for (int k = 0; k < 8; ++k) s[k] += red[(j * tpr + cg) * 8 + k];
+#pragma unroll
+      for (int k = 0; k < 8; ++k) atomicAdd(out + c + k, s[k]);
+    }
+    __syncthreads();
+  }
+}
+
 void colsum(const bf16_t* x, float* out, long R, int C, hipStream_t s) {
+  if (C % 8 == 0) {
+    const int bx = (C + 2047) / 2048;
+    // ~512 blocks total, >= 32 rows each
+    long by = 512 / bx;
+    if (by < 1) by = 1;
+    long rpb = (R + by - 1) / by;
+    if (rpb < 32) rpb = 32;
+    by = (R + rpb - 1) / rpb;
+    hipLaunchKernelGGL(colsum8_kernel, dim3(bx, by), dim3(256), 0, s, x, out, R, C, rpb);
+    return;
+  }
   const int bx = (C + 255) / 256;
   long rpb = 64;
   long by = (R + rpb - 1) / rpb;
@@ -276,7 +424,27 @@ __global__ void relu_bwd_kernel(const bf16_t* __restrict__ dy, const bf16_t* __r
   for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < n; i += (long)gridDim.x * blockDim.x)
     dx[i] = bf2f(y[i]) > 0.f ? dy[i] : (bf16_t)0;
 }
+__global__ void relu_bwd8_kernel(const uint4* __restrict__ dy, const uint4* __restrict__ y,
+                                 uint4* __restrict__ dx, long n8) {
+  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < n8; i += (long)gridDim.x * blockDim.x) {
+    const uint4 d = dy[i], v = y[i];
+    const uint32_t wd[4] = {d.x, d.y, d.z, d.w}, wy[4] = {v.x, v.y, v.z, v.w};
+    uint32_t o[4];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      const uint32_t lo = (int16_t)(wy[k] & 0xffffu) > 0 ? 0x0000ffffu : 0u;   // bf16 > 0 <=> int16 > 0
+      const uint32_t hi = (int32_t)(wy[k] & 0xffff0000u) > 0 ? 0xffff0000u : 0u;
+      o[k] = wd[k] & (lo | hi);
+    }
+    dx[i] = make_uint4(o[0], o[1], o[2], o[3]);
+  }
+}
 void relu_backward(const bf16_t* dy, const bf16_t* y, bf16_t* dx, long n, hipStream_t s) {
+  if (n % 8 == 0) {
+    hipLaunchKernelGGL(relu_bwd8_kernel, dim3(grid_cap(n / 8)), dim3(256), 0, s, (const uint4*)dy,
+                       (const uint4*)y, (uint4*)dx, n / 8);
+    return;
+  }
   hipLaunchKernelGGL(relu_bwd_kernel, dim3(grid_cap(n)), dim3(256), 0, s, dy, y, dx, n);
 }
 

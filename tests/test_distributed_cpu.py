@@ -163,3 +163,48 @@ def test_rank_failure_is_detected(tmp_path):
     assert ps[1].exitcode == 17
     s = torch.load(tmp_path / "f0.pt", weights_only=False)
     assert s["aborted"] and "rank lost" in s["reason"]
+
+
+def test_trainer_offload_restore_roundtrip_cpu():
+    from tiresias_amd.executor.cluster_runtime import _HostEngine
+    from tiresias_amd.executor.trainer import Trainer
+
+    t = Trainer("resnet_tiny", "cpu", seed=1)
+    t.step()
+    before = t.arena.master.clone()
+    mom = t.opt_state[0].clone()
+    eng = _HostEngine()
+    n = t.offload(eng)
+    assert n > 0 and t.arena.master.untyped_storage().nbytes() == 0
+    t.restore()
+    assert torch.equal(t.arena.master, before) and torch.equal(t.opt_state[0], mom)
+    assert torch.equal(t.arena.shadow, before.to(torch.bfloat16))
+    t.step()   # keeps training after the round trip
+
+
+def _spill_replay_worker(rank, world, port, outdir):
+    _init(rank, world, port)
+    ctrl = dist.new_group(backend="gloo")
+    import bench
+    from tiresias_amd.executor.cluster_runtime import Worker, run_replay
+
+    jobs = bench.bench_trace(world, 4, seed=9, tiny=True)
+    cfg = bench.make_cfg("dlas-gpu", "count", world, 9)
+    cfg.ckpt_policy = "host"
+    w = Worker(rank, world, torch.device("cpu"), dist.group.WORLD)
+    s = run_replay(cfg, jobs, rank, world, torch.device("cpu"), ctrl_pg=ctrl,
+                   world_pg=dist.group.WORLD, worker=w, quantum=0.1)
+    torch.save({"s": s, "spilled": w.spilled_bytes, "restored": w.restored_bytes},
+               os.path.join(outdir, f"s{rank}.pt"))
+    dist.destroy_process_group()
+
+
+def test_live_replay_with_host_spill(tmp_path):
+    world = 2
+    mp.spawn(_spill_replay_worker, args=(world, _free_port(), str(tmp_path)), nprocs=world, join=True)
+    r0 = torch.load(tmp_path / "s0.pt", weights_only=False)
+    r1 = torch.load(tmp_path / "s1.pt", weights_only=False)
+    s = r0["s"]
+    assert s["finished"] == s["jobs"] and s["preemptions"] > 0
+    assert r0["spilled"] + r1["spilled"] > 0
+    assert r0["restored"] + r1["restored"] > 0

@@ -146,10 +146,12 @@ def test_conv_bias_relu_mask(gpu):
 
 
 # ------------------------------------------------------------------ BN / LN
+@pytest.mark.parametrize("shape", [(8, 14, 14, 64), (32, 28, 28, 128), (16, 7, 7, 2048),
+                                   (64, 56, 56, 64)])
 @pytest.mark.parametrize("relu,res", [(False, False), (True, False), (True, True)])
-def test_batchnorm(gpu, relu, res):
+def test_batchnorm(gpu, relu, res, shape):
     torch.manual_seed(5)
-    N, H, W, C = 8, 14, 14, 64
+    N, H, W, C = shape
     x = (torch.randn(N, H, W, C, device=gpu) * 3 + 1).to(BF)
     r = torch.randn(N, H, W, C, device=gpu).to(BF) if res else None
     g = torch.rand(C, device=gpu) + 0.5
@@ -157,8 +159,7 @@ def test_batchnorm(gpu, relu, res):
     rm, rv = torch.zeros(C, device=gpu), torch.ones(C, device=gpu)
     y = torch.empty_like(x)
     mean = torch.empty(C, device=gpu); rstd = torch.empty(C, device=gpu)
-    T().bn_forward(x, r, y, g, b, rm, rv, mean, rstd, torch.empty(2 * C, device=gpu, dtype=torch.float64),
-                   torch.empty(2 * C, device=gpu), 1e-5, 0.1, relu)
+    T().bn_forward(x, r, y, g, b, rm, rv, mean, rstd, 1e-5, 0.1, relu)
     xf = x.float().requires_grad_(True)
     gf = g.clone().requires_grad_(True)
     bf = b.clone().requires_grad_(True)
@@ -174,8 +175,7 @@ def test_batchnorm(gpu, relu, res):
     dx = torch.empty_like(x)
     dres = torch.empty_like(x) if res else None
     dg = torch.zeros(C, device=gpu); db = torch.zeros(C, device=gpu)
-    T().bn_backward(dy, y, x, mean, rstd, g, dx, dres, dg, db, torch.empty(2 * C, device=gpu, dtype=torch.float64),
-                    torch.empty(3 * C, device=gpu), relu)
+    T().bn_backward(dy, y, x, mean, rstd, g, dx, dres, dg, db, relu)
     grads = torch.autograd.grad(yf, [xf, gf, bf] + ([rf] if res else []), dy.float())
     assert rel_err(dx, grads[0]) < 2e-2
     assert rel_err(dg, grads[1]) < 1e-2
@@ -186,10 +186,10 @@ def test_batchnorm(gpu, relu, res):
     assert rel_err(rm, 0.1 * xs.mean(0)) < 1e-4
 
 
-@pytest.mark.parametrize("D", [512, 1024, 320])
-def test_layernorm(gpu, D):
+@pytest.mark.parametrize("D,rows", [(512, 777), (1024, 777), (320, 777), (512, 16384),
+                                    (1024, 4100), (2048, 3000)])
+def test_layernorm(gpu, D, rows):
     torch.manual_seed(6)
-    rows = 777
     x = (torch.randn(rows, D, device=gpu) * 2 + 0.5).to(BF)
     g = torch.rand(D, device=gpu) + 0.5
     b = torch.randn(D, device=gpu)
@@ -210,12 +210,13 @@ def test_layernorm(gpu, D):
 
 
 # ------------------------------------------------------------------ pooling / loss
-def test_maxpool(gpu):
+@pytest.mark.parametrize("C", [16, 64, 5])
+def test_maxpool(gpu, C):
     torch.manual_seed(7)
-    x = torch.randn(2, 17, 18, 16, device=gpu).to(BF)
+    x = torch.randn(2, 17, 18, C, device=gpu).to(BF)
     P = (17 + 2 - 3) // 2 + 1; Q = (18 + 2 - 3) // 2 + 1
-    y = torch.empty(2, P, Q, 16, device=gpu, dtype=BF)
-    idx = torch.empty(2, P, Q, 16, device=gpu, dtype=torch.uint8)
+    y = torch.empty(2, P, Q, C, device=gpu, dtype=BF)
+    idx = torch.empty(2, P, Q, C, device=gpu, dtype=torch.uint8)
     T().maxpool_forward(x, y, idx, 3, 3, 2, 1)
     xf = x.float().permute(0, 3, 1, 2).requires_grad_(True)
     yf = F.max_pool2d(xf, 3, 2, 1)
@@ -267,6 +268,27 @@ def test_embedding(gpu):
     T().embedding_backward(dout, ids.reshape(-1), g, 2.0)
     ref = torch.zeros(1000, 64, device=gpu).index_add_(0, ids.reshape(-1), dout.float() * 2)
     assert rel_err(g, ref) < 1e-5
+
+
+@pytest.mark.parametrize("R,C", [(4096, 2048), (3200, 32000), (100, 24), (777, 512), (64, 4096),
+                                 (50000, 64)])
+def test_colsum(gpu, R, C):
+    torch.manual_seed(10)
+    x = torch.randn(R, C, device=gpu).to(BF)
+    out = torch.full((C,), 0.5, device=gpu)
+    T().colsum(x, out)
+    assert rel_err(out, x.float().sum(0) + 0.5) < 1e-4
+
+
+@pytest.mark.parametrize("n", [4096 * 33, 1001])
+def test_relu_backward(gpu, n):
+    torch.manual_seed(11)
+    y = torch.randn(n, device=gpu).clamp_min(0).to(BF)
+    y[:7] = -0.0
+    dy = torch.randn(n, device=gpu).to(BF)
+    dx = torch.empty_like(dy)
+    T().relu_backward(dy, y, dx)
+    assert torch.equal(dx, torch.where(y.float() > 0, dy, torch.zeros_like(dy)))
 
 
 # ------------------------------------------------------------------ optimizers

@@ -1,0 +1,44 @@
+"""The native event core must reproduce the Python engine job-for-job
+(count placement), and be much faster on large traces."""
+import time
+
+import numpy as np
+import pytest
+
+from tiresias_amd.config import ClusterSpec, SimConfig
+from tiresias_amd.engine import native
+from tiresias_amd.engine.sim import Simulator
+from tiresias_amd.trace.synth import philly_like_trace
+
+pytestmark = pytest.mark.skipif(not native.available(), reason="native core not built")
+
+
+def _cfg(policy, gpus=32):
+    return SimConfig(schedule=policy, scheme="count", num_queue=3, queue_limits=[2000.0, 20000.0],
+                     gittins_delta=1500.0, solve_starvation=2.0 if policy.startswith("dlas") else 0.0,
+                     cluster=ClusterSpec(num_switch=1, num_node_p_switch=1, num_gpu_p_node=gpus,
+                                         num_cpu_p_node=100000, mem_p_node=100000))
+
+
+@pytest.mark.parametrize("policy", list(native.SUPPORTED))
+@pytest.mark.parametrize("seed", [0, 1])
+def test_native_matches_python(policy, seed):
+    specs = philly_like_trace(250, 32, load=1.4, seed=seed, median_duration=400)
+    c = _cfg(policy)
+    sim = Simulator(c, specs)
+    ps = sim.run()
+    ns = native.simulate_native(c, specs)
+    py_end = np.array([sim.jobs[s.job_id].end_time for s in specs])
+    py_pre = np.array([sim.jobs[s.job_id].preempt_count for s in specs])
+    assert ns["finished"] == ps["finished"]
+    np.testing.assert_allclose(ns["per_job"]["end"], py_end, rtol=1e-9, atol=1e-6)
+    np.testing.assert_array_equal(ns["per_job"]["preempt"], py_pre)
+    assert ns["avg_jct"] == pytest.approx(ps["avg_jct"], rel=1e-9)
+
+
+def test_native_large_trace_fast():
+    specs = philly_like_trace(20000, 512, load=1.1, seed=3, median_duration=900)
+    t = time.perf_counter()
+    s = native.simulate_native(_cfg("dlas-gpu", gpus=512), specs)
+    assert s["finished"] == 20000
+    assert time.perf_counter() - t < 60

@@ -104,6 +104,25 @@ def build(force: bool = False, jobs: int | None = None, verbose: bool = False) -
     return LIB
 
 
+def build_sched_core(force: bool = False) -> Path:
+    """Native event-engine core (pure C++17 + pybind11, no GPU code)."""
+    import pybind11
+
+    src = CSRC / "sched_core" / "sched_core.cpp"
+    out = PKG / ("_sched_core" + (sysconfig.get_config_var("EXT_SUFFIX") or ".so"))
+    if not force and out.exists() and out.stat().st_mtime >= src.stat().st_mtime:
+        return out
+    cxx = shutil.which("g++") or shutil.which("c++") or _hipcc()
+    cmd = [cxx, "-O3", "-std=c++17", "-shared", "-fPIC", f"-I{pybind11.get_include()}",
+           f"-I{sysconfig.get_paths()['include']}", str(src), "-o", str(out) + ".tmp"]
+    r = subprocess.run(cmd, capture_output=True, text=True)
+    if r.returncode != 0:
+        print(r.stderr[-6000:], file=sys.stderr)
+        raise RuntimeError("sched_core build failed")
+    os.replace(str(out) + ".tmp", out)
+    return out
+
+
 def main() -> None:
     ap = argparse.ArgumentParser()
     ap.add_argument("--force", action="store_true")
@@ -112,6 +131,7 @@ def main() -> None:
     a = ap.parse_args()
     p = build(force=a.force, jobs=a.j, verbose=a.v)
     print(p)
+    print(build_sched_core(force=a.force))
 
 
 if __name__ == "__main__":

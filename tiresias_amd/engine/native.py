@@ -1,0 +1,60 @@
+"""Python front-end of the native event core (``csrc/sched_core``).
+
+``simulate_native(cfg, specs)`` returns the same summary dict as
+``engine.sim.simulate`` for the count placement and the policies the core
+implements; use it for month-scale trace sweeps (10^5 jobs in seconds).
+"""
+from __future__ import annotations
+
+import statistics
+import time
+from typing import Dict, List, Optional
+
+import numpy as np
+
+from ..config import SimConfig
+from ..core.job import JobSpec
+from ..metrics.logger import percentile
+
+SUPPORTED = ("fifo", "fjf", "sjf", "shortest", "shortest-gpu", "dlas", "dlas-gpu", "dlas-gpu-gittins",
+             "gittins")
+
+
+def available() -> bool:
+    try:
+        from .. import _sched_core  # noqa: F401
+        return True
+    except ImportError:
+        return False
+
+
+def simulate_native(cfg: SimConfig, specs: List[JobSpec], prior: Optional[List[float]] = None) -> Dict:
+    from .. import _sched_core
+    from ..policy.las import default_limits
+
+    if cfg.schedule not in SUPPORTED:
+        raise ValueError(f"native core supports {SUPPORTED}, not {cfg.schedule}")
+    limits = list(cfg.queue_limits) or default_limits(cfg.num_queue if cfg.num_queue > 1 else 2, 3600.0)
+    if prior is None:
+        prior = sorted(s.duration * s.num_gpu for s in specs)
+    eng = _sched_core.Engine(cfg.schedule, cfg.cluster.num_gpus, [float(x) for x in limits],
+                             float(cfg.solve_starvation), float(cfg.gittins_delta or 3250.0),
+                             [float(x) for x in prior])
+    t0 = time.perf_counter()
+    out = eng.run(np.array([s.submit_time for s in specs], dtype=np.float64),
+                  np.array([s.duration for s in specs], dtype=np.float64),
+                  np.array([s.num_gpu for s in specs], dtype=np.int32))
+    wall = time.perf_counter() - t0
+    sub = np.array([s.submit_time for s in specs])
+    end, start = out["end"], out["start"]
+    done = end >= 0
+    jct = (end - sub)[done]
+    t_first = float(sub.min()) if len(sub) else 0.0
+    return dict(jobs=len(specs), finished=int(done.sum()), failed=int((~done).sum()),
+                avg_jct=float(jct.mean()) if len(jct) else 0.0,
+                median_jct=float(statistics.median(jct.tolist())) if len(jct) else 0.0,
+                p95_jct=percentile(jct.tolist(), 95), makespan=float(end.max() - t_first) if done.any() else 0.0,
+                avg_queueing_delay=float((start - sub)[done].mean()) if done.any() else 0.0,
+                preemptions=int(out["preempt"].sum()), promotions=int(out["promote"].sum()),
+                events=int(out["events"]), wall_s=wall, schedule=cfg.schedule, scheme="count",
+                per_job={"start": start, "end": end, "preempt": out["preempt"]})

@@ -116,6 +116,7 @@ class Controller:
         self.done_iters: Dict[str, int] = {j: 0 for j in self.rjobs}
         self.round = 0
         self.t0 = None
+        self.spill = getattr(cfg, "ckpt_policy", "none") == "host"
 
     def _iter_est(self, model: str, gpus: int) -> float:
         return getattr(self, "est", {}).get((model, gpus), NOMINAL_ITER_S.get(model, 0.03) *
@@ -163,6 +164,8 @@ class Controller:
                 actions.append({"op": "drop", "job": j.job_id, "ranks": self.holders.pop(j.job_id)})
         for a in s.actions:
             j = s.jobs[a["job"]]
+            if a["op"] == "suspend" and self.spill and j.is_pending and j.job_id in self.holders:
+                actions.append({"op": "spill", "job": j.job_id, "ranks": self.holders[j.job_id]})
             if a["op"] == "start" and j.is_running:
                 ranks = gang_ranks(j.allocation, self.gpn)
                 if len(ranks) > 1 and ranks not in self.groups_made:
@@ -220,6 +223,17 @@ class Worker:
         self.trainers: Dict[str, Trainer] = {}
         self.groups: Dict[Tuple[int, ...], object] = {}
         self.use_graph = use_graph
+        self.spilled_bytes = 0
+        self.restored_bytes = 0
+        self._engine = None
+
+    def _ckpt_engine(self):
+        if self._engine is None:
+            if self.device.type == "cuda":
+                self._engine = torch.classes.tam.CkptEngine(self.device.index, 1 << 30)
+            else:
+                self._engine = _HostEngine()
+        return self._engine
 
     def _group(self, ranks):
         if len(ranks) <= 1:
@@ -244,6 +258,10 @@ class Worker:
                 t = self.trainers.pop(a["job"], None)
                 if t is not None:
                     t.release()
+            elif op == "spill":
+                t = self.trainers.get(a["job"])
+                if t is not None:
+                    self.spilled_bytes += t.offload(self._ckpt_engine())
             elif op == "start":
                 ranks = tuple(a["ranks"])
                 src = a["source"]
@@ -251,10 +269,15 @@ class Worker:
                     if self.rank in ranks:
                         self.trainers[a["job"]] = self._make_trainer(a)
                 elif src == "resident":
-                    pass
+                    t = self.trainers.get(a["job"])
+                    if t is not None and getattr(t, "_spilled", None):
+                        self.restored_bytes += t.restore()
                 elif src == "p2p":
                     donors = {int(k): v for k, v in a["donors"].items()}
                     old = tuple(a["old"])
+                    if self.rank in old and self.trainers.get(a["job"]) is not None \
+                            and getattr(self.trainers[a["job"]], "_spilled", None):
+                        self.restored_bytes += self.trainers[a["job"]].restore()
                     if self.rank in donors:        # receiver
                         t = self._make_trainer(a)
                         self.trainers[a["job"]] = t
@@ -298,6 +321,28 @@ class Worker:
         for t in self.trainers.values():
             t.release()
         self.trainers.clear()
+
+
+class _HostEngine:
+    """CPU stand-in for the native engine (tests / gloo rehearsals)."""
+
+    def __init__(self):
+        self.store = {}
+        self.n = 0
+
+    def spill(self, t):
+        self.n += 1
+        self.store[self.n] = t.detach().clone()
+        return self.n
+
+    def wait(self, h):
+        pass
+
+    def restore(self, h, dst):
+        dst.copy_(self.store[h])
+
+    def release(self, h):
+        self.store.pop(h, None)
 
 
 def _abort(ctrl: "Controller", log, rounds: int, reason: str) -> dict:

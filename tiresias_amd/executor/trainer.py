@@ -142,6 +142,57 @@ class Trainer:
     def state_bytes(self) -> int:
         return sum(t.numel() * t.element_size() for t in self.state_tensors().values())
 
+    # ------------------------------------------------------------ host spill
+    def _spill_buffers(self):
+        bufs = [self.arena.master] + list(self.opt_state)
+        bufs += [v for v in self.model.buffers().values()]
+        return bufs
+
+    def offload(self, engine) -> int:
+        """Spill the job's state to pinned host DRAM through the native
+        checkpoint engine (D2H on its low-priority side stream), then release
+        the HBM by shrinking the flat buffers' storages to zero bytes (every
+        parameter view shares those storages, so nothing else changes).
+        The bf16 shadow and the grad buffer are not saved: the shadow is
+        rebuilt from the master on restore, the grad buffer is zero between
+        steps. Returns bytes spilled."""
+        if getattr(self, "_spilled", None):
+            return 0
+        self._graph = None
+        handles, nbytes = [], 0
+        for b in self._spill_buffers():
+            handles.append((b, engine.spill(b), b.untyped_storage().nbytes()))
+            nbytes += b.numel() * b.element_size()
+        for b, h, _ in handles:
+            engine.wait(h)                       # D2H finished before the HBM is released
+        for b in [self.arena.master, self.arena.shadow, self.arena.grad] + list(self.opt_state):
+            b.untyped_storage().resize_(0)
+        self._spilled = handles
+        self._engine = engine
+        return nbytes
+
+    def restore(self) -> int:
+        """Re-allocate the HBM and copy the state back (H2D on the engine's
+        side stream; the compute stream waits on its event, the host does not)."""
+        handles = getattr(self, "_spilled", None)
+        if not handles:
+            return 0
+        A = self.arena
+        for b, n in ((A.master, A.numel * 4), (A.shadow, A.numel * 2), (A.grad, A.numel * 4)):
+            b.untyped_storage().resize_(n)
+        for t in self.opt_state:
+            t.untyped_storage().resize_(t.numel() * 4)
+        nbytes = 0
+        for b, h, _ in handles:
+            self._engine.restore(h, b)
+            nbytes += b.numel() * b.element_size()
+        A.grad.zero_()
+        A.shadow.copy_(A.master.to(torch.bfloat16))
+        for _, h, _ in handles:
+            self._engine.release(h)
+        self._spilled = None
+        return nbytes
+
     def rebind(self, group) -> None:
         """Move the job to a new DDP gang (after a preemption resumed it on
         different GPUs): new communicator, fresh bucketer."""

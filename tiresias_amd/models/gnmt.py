@@ -52,7 +52,7 @@ class _LSTMLayer(Function):
             prev = None
             for t in steps:
                 if prev is not None:
-                    _T().gemm(Hs[prev], True, w_hh.w, True, Gv[t], 1, None, False, None, 1.0, False)
+                    _T().gemm(Hs[prev], True, w_hh.w, True, Gv[t], 1, None, False, None, 1.0, True)
                 _T().lstm_cell_forward(Gv[t], Cs[prev] if prev is not None else None, Cs[t], Hs[t],
                                        None, act[t])
                 prev = t
@@ -96,7 +96,7 @@ class _LSTMLayer(Function):
                                         None, dc2, dG[t])
                 dc, dc2 = dc2, dc
                 if prev is not None:
-                    _T().gemm(dG[t], True, w_hh.w, False, dHf[prev], 1, None, False, None, 1.0, False)
+                    _T().gemm(dG[t], True, w_hh.w, False, dHf[prev], 1, None, False, None, 1.0, True)
             dG2 = dG.view(T * B, 4 * Hd)
             # h_{t-1} for each t (zero for the first step in processing order)
             Hprev = torch.zeros_like(Hs)

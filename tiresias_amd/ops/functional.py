@@ -197,10 +197,8 @@ class _BN(Function):
             if training:
                 mean = torch.empty(C, dtype=torch.float32, device=x.device)
                 rstd = torch.empty_like(mean)
-                ws_d = torch.empty(2 * C, dtype=torch.float64, device=x.device)
-                ws_f = torch.empty(2 * C, dtype=torch.float32, device=x.device)
-                _T().bn_forward(x, res, y, g.master, b.master, run_mean, run_var, mean, rstd, ws_d,
-                                ws_f, eps, momentum, relu)
+                _T().bn_forward(x, res, y, g.master, b.master, run_mean, run_var, mean, rstd, eps,
+                                momentum, relu)
             else:
                 rstd_i = torch.rsqrt(run_var + eps)
                 scale = g.master * rstd_i
@@ -238,10 +236,7 @@ class _BN(Function):
         if dy.is_cuda:
             dx = torch.empty_like(x)
             dres = torch.empty_like(x) if ctx.has_res and ctx.relu else None
-            ws_d = torch.empty(2 * C, dtype=torch.float64, device=x.device)
-            ws_f = torch.empty(3 * C, dtype=torch.float32, device=x.device)
-            _T().bn_backward(dy, y, x, mean, rstd, g.master, dx, dres, g.grad, b.grad, ws_d, ws_f,
-                             ctx.relu)
+            _T().bn_backward(dy, y, x, mean, rstd, g.master, dx, dres, g.grad, b.grad, ctx.relu)
             if ctx.has_res and not ctx.relu:
                 dres = dy
         else:
@@ -346,24 +341,27 @@ class _MaxPool(Function):
             _T().maxpool_forward(x, y, idx, k, k, s, p)
             ctx.save_for_backward(idx)
         else:
-            yf, ind = F.max_pool2d(x.float().permute(0, 3, 1, 2), k, s, p, return_indices=True)
-            y = yf.permute(0, 2, 3, 1).contiguous().to(BF16)
-            ctx.save_for_backward(ind)
+            y = F.max_pool2d(x.float().permute(0, 3, 1, 2), k, s, p).permute(0, 2, 3, 1).contiguous().to(BF16)
+            ctx.save_for_backward(x)
         ctx.cfg = (k, s, p, x.shape)
         return y
 
     @staticmethod
     def backward(ctx, dy):
-        (idx,) = ctx.saved_tensors
+        (saved,) = ctx.saved_tensors
         k, s, p, shape = ctx.cfg
         dy = dy.contiguous()
         if dy.is_cuda:
             dx = torch.empty(shape, dtype=BF16, device=dy.device)
-            _T().maxpool_backward(dy, idx, dx, k, k, s, p)
+            _T().maxpool_backward(dy, saved, dx, k, k, s, p)
         else:
-            N, H, W, C = shape
-            dxf = F.max_unpool2d(dy.float().permute(0, 3, 1, 2), idx, k, s, p, output_size=(H, W))
-            dx = dxf.permute(0, 2, 3, 1).contiguous().to(BF16)
+            # overlapping windows (3x3/s2) route several outputs to one input:
+            # the gradient must SUM them (max_unpool2d would overwrite)
+            xf = saved.float().permute(0, 3, 1, 2).requires_grad_(True)
+            with torch.enable_grad():
+                yf = F.max_pool2d(xf, k, s, p)
+                (g,) = torch.autograd.grad(yf, [xf], dy.float().permute(0, 3, 1, 2))
+            dx = g.permute(0, 2, 3, 1).contiguous().to(BF16)
         return dx, None, None, None
 
 
