@@ -56,7 +56,7 @@ GPU_DIST = [(1, 0.70), (2, 0.10), (4, 0.10), (8, 0.07), (16, 0.03)]
 TRACE_ITER_S = {"resnet50": 0.028, "vgg16": 0.015, "transformer": 0.016, "gnmt": 0.037}
 
 
-def bench_trace(n_gpus: int, jobs_per_gpu: int, seed: int, median_s: float = 0.6, sigma: float = 1.8,
+def bench_trace(n_gpus: int, jobs_per_gpu: int, seed: int, median_s: float = 0.3, sigma: float = 1.8,
                 load: float = 1.3, tiny: bool = False):
     """Philly-shaped mini trace: ~70% 1-GPU jobs with a power-of-two gang
     tail, heavy-tailed log-normal service times (sigma 1.8, i.e. most jobs
@@ -107,7 +107,7 @@ def main():
     ap.add_argument("--baseline-policy", default="fifo")
     ap.add_argument("--baseline-placement", default="yarn")
     ap.add_argument("--no-baseline", action="store_true")
-    ap.add_argument("--jobs-per-gpu", type=int, default=8)
+    ap.add_argument("--jobs-per-gpu", type=int, default=16)
     ap.add_argument("--quantum", type=float, default=0.25)
     ap.add_argument("--seed", type=int, default=2019)
     ap.add_argument("--cpu", action="store_true", help="gloo/CPU rehearsal with tiny models")

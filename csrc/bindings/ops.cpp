@@ -159,7 +159,7 @@ void bn_forward_op(const Tensor& x, const optional<Tensor>& res, const Tensor& y
   const int64_t C = x.size(-1);
   const int64_t M = x.numel() / C;
   TORCH_CHECK(C % 8 == 0 && C <= 2048, "tam.bn: C must be a multiple of 8 and <= 2048");
-  Tensor ws_f = at::empty({(2 + 2 * tam::BN_MAX_BLOCKS) * C}, x.options().dtype(at::kFloat));
+  Tensor ws_f = at::empty({(6 + 2 * tam::BN_MAX_BLOCKS) * C}, x.options().dtype(at::kFloat));
   if (res.has_value() && res->defined()) { check_bf16(*res, "res"); check_contig(*res, "res"); }
   tam::bn_forward(bp(x), opt_ptr<const tam::bf16_t>(res), bpm(y), M, (int)C, (float)eps,
                   (float)momentum, gamma.data_ptr<float>(), beta.data_ptr<float>(),
@@ -176,7 +176,7 @@ void bn_backward_op(const Tensor& dy, const optional<Tensor>& y, const Tensor& x
   const int64_t C = x.size(-1);
   const int64_t M = x.numel() / C;
   TORCH_CHECK(!relu || (y.has_value() && y->defined()), "tam.bn_backward: relu needs y");
-  Tensor ws_f = at::empty({(3 + 2 * tam::BN_MAX_BLOCKS) * C}, x.options().dtype(at::kFloat));
+  Tensor ws_f = at::empty({(8 + 2 * tam::BN_MAX_BLOCKS) * C}, x.options().dtype(at::kFloat));
   tam::bn_backward(bp(dy), opt_ptr<const tam::bf16_t>(y), bp(x), mean.data_ptr<float>(),
                    rstd.data_ptr<float>(), gamma.data_ptr<float>(), M, (int)C, relu, bpm(dx),
                    opt_ptr<tam::bf16_t>(dres), opt_ptr<float>(dgamma), opt_ptr<float>(dbeta),
@@ -260,10 +260,15 @@ void embedding_backward_op(const Tensor& dout, const Tensor& ids, const Tensor& 
                           (int)gtable.size(1), (float)scale, cur_stream(dout));
 }
 
+void gemm_force_op(int64_t cfg, int64_t splits) { tam::gemm_force((int)cfg, (int)splits); }
+
 void colsum_op(const Tensor& x, const Tensor& out) {
   check_bf16(x, "x"); check_f32(out, "out"); check_contig(x, "x");
   const int64_t C = x.size(-1);
-  tam::colsum(bp(x), out.data_ptr<float>(), x.numel() / C, (int)C, cur_stream(x));
+  Tensor ws = at::empty({C % 8 == 0 ? (int64_t)tam::COLSUM_MAX_BLOCKS * C : 1},
+                        x.options().dtype(at::kFloat));
+  tam::colsum(bp(x), out.data_ptr<float>(), ws.data_ptr<float>(), x.numel() / C, (int)C,
+              cur_stream(x));
 }
 void relu_backward_op(const Tensor& dy, const Tensor& y, const Tensor& dx) {
   check_bf16(dy, "dy"); check_bf16(y, "y"); check_bf16(dx, "dx");
@@ -379,6 +384,7 @@ TORCH_LIBRARY(tam, m) {
   m.def("embedding_forward(Tensor table, Tensor ids, Tensor(a!) out, float scale) -> ()", &embedding_forward_op);
   m.def("embedding_backward(Tensor dout, Tensor ids, Tensor(a!) gtable, float scale) -> ()", &embedding_backward_op);
   m.def("colsum(Tensor x, Tensor(a!) out) -> ()", &colsum_op);
+  m.def("gemm_force(int cfg, int splits) -> ()", &gemm_force_op);
   m.def("relu_backward(Tensor dy, Tensor y, Tensor(a!) dx) -> ()", &relu_backward_op);
   m.def("add(Tensor a, Tensor b, Tensor(a!) y) -> ()", &add_op);
   m.def("cast_f32_bf16(Tensor x, Tensor(a!) y) -> ()", &cast_op);

@@ -10,6 +10,12 @@ namespace tam {
 // Reductions write per-block partial rows (<= BN_MAX_BLOCKS), no atomics.
 constexpr int BN_MAX_BLOCKS = 512;
 constexpr int LN_MAX_BLOCKS = 512;
+constexpr int COLSUM_MAX_BLOCKS = 256;
+// out[c] = sum over nblk partial rows part[b][c] (width W): fp64 store, or fp32
+// accumulate into out0[c] (c < split) / out1[c - split]
+void col_reduce_f64(const float* part, int nblk, int W, double* out, hipStream_t s);
+void col_reduce_acc(const float* part, int nblk, int W, float* out0, float* out1, int split,
+                    hipStream_t s);
 void bn_forward(const bf16_t* x, const bf16_t* res, bf16_t* y, long M, int C, float eps,
                 float momentum, const float* gamma, const float* beta, float* run_mean,
                 float* run_var, float* save_mean, float* save_rstd, float* ws_f, int relu,
@@ -47,7 +53,8 @@ void embedding_backward(const bf16_t* dout, const long* ids, float* gtable, long
                         float scale, hipStream_t s);
 
 // misc
-void colsum(const bf16_t* x, float* out, long R, int C, hipStream_t s);
+// out[c] += sum_r x[r][c]; ws: COLSUM_MAX_BLOCKS * C floats (C % 8 == 0 path)
+void colsum(const bf16_t* x, float* out, float* ws, long R, int C, hipStream_t s);
 void relu_backward(const bf16_t* dy, const bf16_t* y, bf16_t* dx, long n, hipStream_t s);
 void add_bf16(const bf16_t* a, const bf16_t* b, bf16_t* y, long n, hipStream_t s);
 void cast_f32_bf16(const float* x, bf16_t* y, long n, hipStream_t s);

@@ -14,6 +14,7 @@ namespace tam {
 // ep.mode == 0, requires ldc == N).
 void gemm(const bf16_t* A, long lda, bool a_kmajor, const bf16_t* B, long ldb, bool b_kmajor,
           int M, int N, int K, Epi ep, bool allow_split, hipStream_t s);
+void gemm_force(int cfg, int splits);   // tuning hook (-1 = heuristic)
 
 // NHWC convolutions, weights [K][R][S][C] (C, K multiples of 8)
 void conv_fwd(const bf16_t* x, const bf16_t* w, const ConvGeom& g, Epi ep, hipStream_t s);

@@ -33,6 +33,30 @@ inline TileChoice choose_tiles(int M, int N, int K, bool can_split) {
   return t;
 }
 
+// Plain-GEMM policy, fitted to tools/sweep_gemm.py over the zoo's linear
+// shapes on MI355X (profiles/sweep_gemm_r1.json; within 0.3% of the per-shape
+// best vs 9.8% for choose_tiles): 128x128 only when K is deep enough to
+// amortise its prologue/epilogue AND there are >=1 tile per CU; otherwise
+// 64x64 (4x the workgroups, better latency hiding); split-K to ~512 WGs.
+inline TileChoice choose_tiles_gemm(int M, int N, int K, bool can_split) {
+  const long t128 = (long)cdiv(M, 128) * cdiv(N, 128);
+  const bool big = M > 64 && N > 64 &&
+                   ((K >= 2048 && t128 >= 256) || (K >= 1024 && t128 >= 1024));
+  TileChoice t{big ? 0 : 3, 1};
+  if (can_split) {
+    const int b = big ? 128 : 64;
+    const long tiles = (long)cdiv(M, b) * cdiv(N, b);
+    const int ktiles = cdiv(K, IG_BK);
+    if (tiles < 512 && ktiles >= 8) {
+      int sp = (int)((512 + tiles - 1) / tiles);
+      if (sp > ktiles / 4) sp = ktiles / 4;
+      if (sp > 32) sp = 32;
+      t.splits = sp < 1 ? 1 : sp;
+    }
+  }
+  return t;
+}
+
 inline void prepare_split(Epi& ep, int splits, int M, int N, hipStream_t s) {
   if (splits <= 1) return;
   if (ep.mode == 0) {

@@ -23,10 +23,18 @@ static void gemm_tile(const bf16_t* A, long lda, bool ak, const bf16_t* B, long 
   }
 }
 
+// tuning hook: force tile config / split count (-1 = heuristic); used by
+// tools/sweep_gemm.py to measure the policy, never set in training
+static int g_force_cfg = -1, g_force_splits = -1;
+void gemm_force(int cfg, int splits) { g_force_cfg = cfg; g_force_splits = splits; }
+
 void gemm(const bf16_t* A, long lda, bool ak, const bf16_t* B, long ldb, bool bk, int M, int N,
           int K, Epi ep, bool allow_split, hipStream_t s) {
   if (M <= 0 || N <= 0) return;
-  TileChoice t = choose_tiles(M, N, K, allow_split && ep.c_f32 && !ep.relu && !ep.mask);
+  const bool can_split = allow_split && ep.c_f32 && !ep.relu && !ep.mask;
+  TileChoice t = choose_tiles_gemm(M, N, K, can_split);
+  if (g_force_cfg >= 0) t.cfg = g_force_cfg;
+  if (g_force_splits >= 1) t.splits = can_split ? g_force_splits : 1;
   prepare_split(ep, t.splits, M, N, s);
   switch (t.cfg) {
     case 0: gemm_tile<128, 128>(A, lda, ak, B, ldb, bk, M, N, K, ep, t.splits, s); break;

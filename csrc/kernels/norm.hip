@@ -24,12 +24,58 @@ __device__ __forceinline__ uint4 pack8(const float (&f)[8]) {
                     pack_bf2(f[6], f[7]));
 }
 
+// ---------------------------------------------------------------- column reduce
+// Second stage of every atomic-free reduction here: out[c] = sum_b part[b][c]
+// over nblk partial rows of width W, in fp64. Block = 16 columns x 16 row
+// lanes (64 B coalesced segments), 8 independent loads in flight per lane so
+// the pass is not a serial chain of HBM round trips.
+template <int MODE>   // 0: fp64 store to out64; 1: fp32 accumulate into out0[c<split] / out1[c-split]
+__global__ void __launch_bounds__(256) col_reduce_kernel(const float* __restrict__ part, int nblk,
+                                                          int W, double* __restrict__ out64,
+                                                          float* __restrict__ out0,
+                                                          float* __restrict__ out1, int split) {
+  __shared__ double red[16][17];
+  const int cx = threadIdx.x & 15, ly = threadIdx.x >> 4;
+  const int c = blockIdx.x * 16 + cx;
+  double s = 0.0;
+  if (c < W) {
+    int b = ly;
+    for (; b + 7 * 16 < nblk; b += 8 * 16) {
+      float v[8];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) v[u] = part[(long)(b + u * 16) * W + c];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) s += (double)v[u];
+    }
+    for (; b < nblk; b += 16) s += (double)part[(long)b * W + c];
+  }
+  red[ly][cx] = s;
+  __syncthreads();
+  if (ly == 0 && c < W) {
+    double t = 0.0;
+#pragma unroll
+    for (int k = 0; k < 16; ++k) t += red[k][cx];
+    if (MODE == 0) out64[c] = t;
+    else if (c < split) out0[c] += (float)t;
+    else out1[c - split] += (float)t;
+  }
+}
+
+void col_reduce_f64(const float* part, int nblk, int W, double* out, hipStream_t s) {
+  hipLaunchKernelGGL(col_reduce_kernel<0>, dim3((W + 15) / 16), dim3(256), 0, s, part, nblk, W, out,
+                     (float*)nullptr, (float*)nullptr, W);
+}
+void col_reduce_acc(const float* part, int nblk, int W, float* out0, float* out1, int split,
+                    hipStream_t s) {
+  hipLaunchKernelGGL(col_reduce_kernel<1>, dim3((W + 15) / 16), dim3(256), 0, s, part, nblk, W,
+                     (double*)nullptr, out0, out1, split);
+}
+
 // ---------------------------------------------------------------- BN stats
 // grid.x blocks each own a contiguous row range; thread = (row lane, 8-ch group)
 __global__ void __launch_bounds__(256) bn_stats_kernel(const bf16_t* __restrict__ x, long M, int C,
                                                         long rows_per_block,
-                                                        float* __restrict__ psum,
-                                                        float* __restrict__ psq) {
+                                                        float* __restrict__ part) {
   __shared__ float red[256 * 16];
   const int tpr = C / 8;                 // threads per row
   const int rpb = 256 / tpr;             // rows per pass (C <= 2048)
@@ -57,29 +103,24 @@ __global__ void __launch_bounds__(256) bn_stats_kernel(const bf16_t* __restrict_
       for (int i = 0; i < 8; ++i) { s[i] += red[t * 16 + i]; q[i] += red[t * 16 + 8 + i]; }
     }
     // one partial row per block: no atomics, deterministic
-    float* ps = psum + (long)blockIdx.x * C + cg * 8;
-    float* pq = psq + (long)blockIdx.x * C + cg * 8;
+    float* ps = part + (long)blockIdx.x * 2 * C + cg * 8;
+    float* pq = ps + C;
 #pragma unroll
     for (int i = 0; i < 8; ++i) { ps[i] = s[i]; pq[i] = q[i]; }
   }
 }
 
 // mean/rstd + fused scale/shift + running-stat update
-__global__ void bn_finalize_kernel(const float* __restrict__ psum, const float* __restrict__ psq,
-                                   int nblk, long M, int C, float eps, float momentum,
+__global__ void bn_finalize_kernel(const double* __restrict__ sums, long M, int C, float eps,
+                                   float momentum,
                                    const float* __restrict__ gamma, const float* __restrict__ beta,
                                    float* __restrict__ mean_out, float* __restrict__ rstd_out,
                                    float* __restrict__ scale, float* __restrict__ shift,
                                    float* __restrict__ run_mean, float* __restrict__ run_var) {
   const int c = blockIdx.x * blockDim.x + threadIdx.x;
   if (c >= C) return;
-  double sm = 0.0, sq = 0.0;
-  for (int b = 0; b < nblk; ++b) {
-    sm += (double)psum[(long)b * C + c];
-    sq += (double)psq[(long)b * C + c];
-  }
-  const double mean = sm / (double)M;
-  double var = sq / (double)M - mean * mean;
+  const double mean = sums[c] / (double)M;
+  double var = sums[C + c] / (double)M - mean * mean;
   if (var < 0) var = 0;
   const float rstd = (float)(1.0 / sqrt(var + (double)eps));
   mean_out[c] = (float)mean;
@@ -129,7 +170,7 @@ __global__ void __launch_bounds__(256) bn_apply_kernel(const bf16_t* __restrict_
 __global__ void __launch_bounds__(256) bn_bwd_reduce_kernel(
     const bf16_t* __restrict__ dy, const bf16_t* __restrict__ y, const bf16_t* __restrict__ x,
     const float* __restrict__ mean, const float* __restrict__ rstd, long M, int C,
-    long rows_per_block, int relu, float* __restrict__ pdy, float* __restrict__ pdyx) {
+    long rows_per_block, int relu, float* __restrict__ part) {
   __shared__ float red[256 * 16];
   const int tpr = C / 8, rpb = 256 / tpr;
   const int cg = threadIdx.x % tpr, rl = threadIdx.x / tpr;
@@ -162,27 +203,22 @@ __global__ void __launch_bounds__(256) bn_bwd_reduce_kernel(
 #pragma unroll
       for (int i = 0; i < 8; ++i) { a[i] += red[t * 16 + i]; b[i] += red[t * 16 + 8 + i]; }
     }
-    float* pa = pdy + (long)blockIdx.x * C + cg * 8;
-    float* pb = pdyx + (long)blockIdx.x * C + cg * 8;
+    float* pa = part + (long)blockIdx.x * 2 * C + cg * 8;
+    float* pb = pa + C;
 #pragma unroll
     for (int i = 0; i < 8; ++i) { pa[i] = a[i]; pb[i] = b[i]; }
   }
 }
 
 // dgamma/dbeta accumulate into fp32 grads; coefficient prep for the apply pass
-__global__ void bn_bwd_finalize_kernel(const float* __restrict__ pdy, const float* __restrict__ pdyx,
-                                       int nblk, long M, int C, const float* __restrict__ gamma,
+__global__ void bn_bwd_finalize_kernel(const double* __restrict__ sums, long M, int C,
+                                       const float* __restrict__ gamma,
                                        const float* __restrict__ rstd, float* __restrict__ dgamma,
                                        float* __restrict__ dbeta, float* __restrict__ k1,
                                        float* __restrict__ k2, float* __restrict__ k3) {
   const int c = blockIdx.x * blockDim.x + threadIdx.x;
   if (c >= C) return;
-  double da = 0.0, db = 0.0;
-  for (int k = 0; k < nblk; ++k) {
-    da += (double)pdy[(long)k * C + c];
-    db += (double)pdyx[(long)k * C + c];
-  }
-  const float a = (float)da, b = (float)db;
+  const float a = (float)sums[c], b = (float)sums[C + c];
   if (dgamma) dgamma[c] += b;
   if (dbeta) dbeta[c] += a;
   // dx = g*rstd*(dyr - a/M - xhat*b/M) = k1*dyr + k2*xhat + k3
@@ -241,15 +277,15 @@ void bn_forward(const bf16_t* x, const bf16_t* res, bf16_t* y, long M, int C, fl
                 float momentum, const float* gamma, const float* beta, float* run_mean,
                 float* run_var, float* save_mean, float* save_rstd, float* ws_f, int relu,
                 hipStream_t s) {
-  // ws_f: (2 + 2*BN_MAX_BLOCKS) * C floats: scale, shift, partial sums / sums of squares
+  // ws_f: 2*C floats scale/shift | 2*C doubles column sums | BN_MAX_BLOCKS*2*C partials
   const long rpb = bn_rows_per_block(M, C);
   const int nb = (int)((M + rpb - 1) / rpb);
-  float* part = ws_f + 2 * C;
-  hipLaunchKernelGGL(bn_stats_kernel, dim3(nb), dim3(256), 0, s, x, M, C, rpb, part,
-                     part + (long)nb * C);
-  hipLaunchKernelGGL(bn_finalize_kernel, dim3((C + 255) / 256), dim3(256), 0, s, part,
-                     part + (long)nb * C, nb, M, C, eps, momentum, gamma, beta, save_mean, save_rstd,
-                     ws_f, ws_f + C, run_mean, run_var);
+  double* sums = (double*)(ws_f + 2 * C);
+  float* part = ws_f + 6 * C;
+  hipLaunchKernelGGL(bn_stats_kernel, dim3(nb), dim3(256), 0, s, x, M, C, rpb, part);
+  col_reduce_f64(part, nb, 2 * C, sums, s);
+  hipLaunchKernelGGL(bn_finalize_kernel, dim3((C + 255) / 256), dim3(256), 0, s, sums, M, C, eps,
+                     momentum, gamma, beta, save_mean, save_rstd, ws_f, ws_f + C, run_mean, run_var);
   const long total8 = M * C / 8;
   hipLaunchKernelGGL(bn_apply_kernel, dim3(grid_for(total8)), dim3(256), 0, s, x, res, ws_f,
                      ws_f + C, y, total8, C, relu);
@@ -265,15 +301,16 @@ void bn_infer(const bf16_t* x, const bf16_t* res, bf16_t* y, long M, int C, cons
 void bn_backward(const bf16_t* dy, const bf16_t* y, const bf16_t* x, const float* mean,
                  const float* rstd, const float* gamma, long M, int C, int relu, bf16_t* dx,
                  bf16_t* dres, float* dgamma, float* dbeta, float* ws_f, hipStream_t s) {
-  // ws_f: (3 + 2*BN_MAX_BLOCKS) * C floats: k1, k2, k3, partials
+  // ws_f: 4*C floats k1/k2/k3(+pad) | 2*C doubles column sums | BN_MAX_BLOCKS*2*C partials
   const long rpb = bn_rows_per_block(M, C);
   const int nb = (int)((M + rpb - 1) / rpb);
-  float* part = ws_f + 3 * C;
+  double* sums = (double*)(ws_f + 4 * C);
+  float* part = ws_f + 8 * C;
   hipLaunchKernelGGL(bn_bwd_reduce_kernel, dim3(nb), dim3(256), 0, s, dy, y, x, mean, rstd, M, C,
-                     rpb, relu, part, part + (long)nb * C);
-  hipLaunchKernelGGL(bn_bwd_finalize_kernel, dim3((C + 255) / 256), dim3(256), 0, s, part,
-                     part + (long)nb * C, nb, M, C, gamma, rstd, dgamma, dbeta, ws_f, ws_f + C,
-                     ws_f + 2 * C);
+                     rpb, relu, part);
+  col_reduce_f64(part, nb, 2 * C, sums, s);
+  hipLaunchKernelGGL(bn_bwd_finalize_kernel, dim3((C + 255) / 256), dim3(256), 0, s, sums, M, C,
+                     gamma, rstd, dgamma, dbeta, ws_f, ws_f + C, ws_f + 2 * C);
   const long total8 = M * C / 8;
   hipLaunchKernelGGL(bn_bwd_apply_kernel, dim3(grid_for(total8)), dim3(256), 0, s, dy, y, x, mean,
                      rstd, ws_f, ws_f + C, ws_f + 2 * C, dx, dres, total8, C, relu);
@@ -407,16 +444,6 @@ __global__ void __launch_bounds__(256) ln_bwd_kernel(const bf16_t* __restrict__ 
   }
 }
 
-// dg[c] += sum_b part[b][c]; db[c] += sum_b part[b][D + c]
-__global__ void ln_grad_reduce_kernel(const float* __restrict__ part, int nblk, int D,
-                                      float* __restrict__ dg, float* __restrict__ db) {
-  const int c = blockIdx.x * blockDim.x + threadIdx.x;
-  if (c >= 2 * D) return;
-  float s = 0.f;
-  for (int b = 0; b < nblk; ++b) s += part[(long)b * 2 * D + c];
-  if (c < D) dg[c] += s;
-  else db[c - D] += s;
-}
 
 void ln_forward(const bf16_t* x, const float* g, const float* b, bf16_t* y, float* mean,
                 float* rstd, long rows, int D, float eps, hipStream_t s) {
@@ -437,8 +464,7 @@ void ln_backward(const bf16_t* dy, const bf16_t* x, const float* g, const float*
   if (D <= 512) hipLaunchKernelGGL(ln_bwd_kernel<1>, dim3(blocks), dim3(256), 0, s, dy, x, g, mean, rstd, dx, ws, rows, D, rpb);
   else if (D <= 1024) hipLaunchKernelGGL(ln_bwd_kernel<2>, dim3(blocks), dim3(256), 0, s, dy, x, g, mean, rstd, dx, ws, rows, D, rpb);
   else hipLaunchKernelGGL(ln_bwd_kernel<4>, dim3(blocks), dim3(256), 0, s, dy, x, g, mean, rstd, dx, ws, rows, D, rpb);
-  hipLaunchKernelGGL(ln_grad_reduce_kernel, dim3((2 * D + 255) / 256), dim3(256), 0, s, ws, blocks, D,
-                     dg, db);
+  col_reduce_acc(ws, blocks, 2 * D, dg, db, D, s);
 }
 
 }  // namespace tam

@@ -358,9 +358,10 @@ __global__ void colsum_kernel(const bf16_t* __restrict__ x, float* __restrict__ 
 }
 
 // C % 8 == 0: block = (row lane rl, 8-column group cg) over a <=2048-column
-// chunk, 16 B loads, LDS combine over row lanes, one atomic per column/block.
+// chunk, 16 B loads, LDS combine over row lanes; block (x, y) writes its
+// columns of partial row y (no atomics), col_reduce_acc finishes.
 __global__ void __launch_bounds__(256) colsum8_kernel(const bf16_t* __restrict__ x,
-                                                       float* __restrict__ out, long R, int C,
+                                                       float* __restrict__ part, long R, int C,
                                                        long rows_per_block) {
   __shared__ float red[256 * 8];
   const int c0 = blockIdx.x * 2048;
@@ -391,23 +392,25 @@ __global__ void __launch_bounds__(256) colsum8_kernel(const bf16_t* __restrict__
       for (int j = 1; j < rpp; ++j)
 #pragma unroll
         for (int k = 0; k < 8; ++k) s[k] += red[(j * tpr + cg) * 8 + k];
-#pragma unroll
-      for (int k = 0; k < 8; ++k) atomicAdd(out + c + k, s[k]);
+      float* pr = part + (long)blockIdx.y * C + c;
+      *(float4*)pr = make_float4(s[0], s[1], s[2], s[3]);
+      *(float4*)(pr + 4) = make_float4(s[4], s[5], s[6], s[7]);
     }
     __syncthreads();
   }
 }
 
-void colsum(const bf16_t* x, float* out, long R, int C, hipStream_t s) {
+void colsum(const bf16_t* x, float* out, float* ws, long R, int C, hipStream_t s) {
   if (C % 8 == 0) {
     const int bx = (C + 2047) / 2048;
-    // ~512 blocks total, >= 32 rows each
-    long by = 512 / bx;
-    if (by < 1) by = 1;
+    // >= ~512 blocks in flight, >= 32 rows each, <= COLSUM_MAX_BLOCKS partial rows
+    long by = (512 + bx - 1) / bx;
+    if (by > COLSUM_MAX_BLOCKS) by = COLSUM_MAX_BLOCKS;
     long rpb = (R + by - 1) / by;
     if (rpb < 32) rpb = 32;
     by = (R + rpb - 1) / rpb;
-    hipLaunchKernelGGL(colsum8_kernel, dim3(bx, by), dim3(256), 0, s, x, out, R, C, rpb);
+    hipLaunchKernelGGL(colsum8_kernel, dim3(bx, by), dim3(256), 0, s, x, ws, R, C, rpb);
+    col_reduce_acc(ws, (int)by, C, out, out, C, s);
     return;
   }
   const int bx = (C + 255) / 256;
