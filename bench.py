@@ -111,6 +111,8 @@ def main():
     ap.add_argument("--quantum", type=float, default=0.25)
     ap.add_argument("--seed", type=int, default=2019)
     ap.add_argument("--cpu", action="store_true", help="gloo/CPU rehearsal with tiny models")
+    ap.add_argument("--no-graph", action="store_true",
+                    help="disable hipGraph capture of 1-GPU jobs' fwd+bwd (eager launches)")
     ap.add_argument("--out", default=None, help="directory for job.csv / summary.json of the last step")
     a = ap.parse_args()
 
@@ -142,7 +144,7 @@ def main():
 
     jobs = bench_trace(n, a.jobs_per_gpu, a.seed, tiny=not use_cuda)
     cfg = make_cfg(a.policy, a.placement, n, a.seed)
-    worker = Worker(rank, world, device, world_pg)
+    worker = Worker(rank, world, device, world_pg, use_graph=use_cuda and not a.no_graph)
 
     def sync():
         if world > 1:
@@ -196,6 +198,7 @@ def main():
                 "seq_len": "128 (transformer), 50 (gnmt)",
                 "parallelism": f"dp (gang DDP over RCCL), {n} GPU cluster",
                 "trace_jobs": len(jobs),
+                "hip_graph_1gpu_jobs": bool(use_cuda and not a.no_graph),
                 "jobs_per_gpu": a.jobs_per_gpu,
                 "policy": f"{a.policy} + {a.placement} placement (Tiresias)",
                 "baseline": f"{a.baseline_policy} + {a.baseline_placement}",

@@ -6,6 +6,12 @@
 #include <c10/hip/HIPStream.h>
 #include <torch/library.h>
 
+#include <functional>
+#include <map>
+#include <mutex>
+#include <sstream>
+#include <tuple>
+
 #include "tam/kernels.h"
 #include "tam/launch.h"
 
@@ -42,6 +48,58 @@ T* opt_ptr(const optional<Tensor>& t) {
 }
 
 // ------------------------------------------------------------------ GEMM
+// Measured routing for PLAIN GEMMs (no fused relu / relu-mask epilogue): the
+// hand-written MFMA kernel vs hipBLASLt reached through ATen (mm / addmm with
+// an fp32 out_dtype, so fp32 grad accumulation stays one library call). Each
+// (shape, majorities, epilogue) key is timed ONCE on scratch output with HIP
+// events, outside graph capture, and cached per process; fused epilogues and
+// small problems always take the MFMA kernel. Policy: -1 measured (default),
+// 0 MFMA only, 1 library whenever eligible.
+using GemmKey = std::tuple<int64_t, int64_t, int64_t, bool, bool, int64_t, bool, bool>;
+std::map<GemmKey, int> g_route;          // 0 = MFMA kernel, 1 = library
+std::map<GemmKey, std::pair<float, float>> g_route_ms;
+std::mutex g_route_mu;
+int g_lib_policy = -1;
+bool g_forced = false;   // tile/split forced for tuning: never route to the library
+
+void run_mfma(const Tensor& a, bool ak, const Tensor& b, bool bk, int64_t M, int64_t N, int64_t K,
+              const tam::Epi& ep, bool allow_split) {
+  tam::gemm(bp(a), a.stride(0), ak, bp(b), b.stride(0), bk, (int)M, (int)N, (int)K, ep, allow_split,
+            cur_stream(a));
+}
+
+void run_lib(const Tensor& a, bool ak, const Tensor& b, bool bk, const Tensor& c, int64_t mode,
+             const optional<Tensor>& bias) {
+  const Tensor Ae = ak ? a : a.t();   // [M][K]
+  const Tensor Be = bk ? b.t() : b;   // [K][N]
+  Tensor out = c;
+  if (mode == 1) {
+    at::addmm_out(out, c, Ae, Be, at::kFloat, 1, 1);
+  } else if (bias.has_value() && bias->defined()) {
+    at::addmm_out(out, *bias, Ae, Be);
+  } else if (c.scalar_type() == at::kFloat) {
+    at::mm_out(out, Ae, Be, at::kFloat);
+  } else {
+    at::mm_out(out, Ae, Be);
+  }
+}
+
+float time_ms(hipStream_t s, const std::function<void()>& fn) {
+  fn();   // warm (library heuristics / our first launch)
+  hipEvent_t e0, e1;
+  TAM_HIP_CHECK(hipEventCreate(&e0));
+  TAM_HIP_CHECK(hipEventCreate(&e1));
+  TAM_HIP_CHECK(hipEventRecord(e0, s));
+  for (int i = 0; i < 3; ++i) fn();
+  TAM_HIP_CHECK(hipEventRecord(e1, s));
+  TAM_HIP_CHECK(hipEventSynchronize(e1));
+  float ms = 0.f;
+  TAM_HIP_CHECK(hipEventElapsedTime(&ms, e0, e1));
+  TAM_HIP_CHECK(hipEventDestroy(e0));
+  TAM_HIP_CHECK(hipEventDestroy(e1));
+  return ms / 3.f;
+}
+
 // a: (M,K) if a_kmajor else (K,M); b: (N,K) if b_kmajor else (K,N); c: (M,N)
 void gemm_op(const Tensor& a, bool a_kmajor, const Tensor& b, bool b_kmajor, const Tensor& c,
              int64_t mode, const optional<Tensor>& bias, bool relu, const optional<Tensor>& mask,
@@ -84,8 +142,70 @@ void gemm_op(const Tensor& a, bool a_kmajor, const Tensor& b, bool b_kmajor, con
     ep.ldm = mask->stride(0);
   }
   ep.alpha = (float)alpha;
-  tam::gemm(bp(a), a.stride(0), a_kmajor, bp(b), b.stride(0), b_kmajor, (int)M, (int)N, (int)K, ep,
-            allow_split, cur_stream(a));
+  const bool has_bias = ep.bias != nullptr;
+  const bool lib_ok = g_lib_policy != 0 && !g_forced && !relu && ep.mask == nullptr && alpha == 1.0 &&
+                      (mode == 0 || (mode == 1 && ep.c_f32)) && !(has_bias && ep.c_f32) &&
+                      (double)M * N * K >= (double)(1 << 27) && M >= 16 && N >= 16;
+  if (!lib_ok) {
+    run_mfma(a, a_kmajor, b, b_kmajor, M, N, K, ep, allow_split);
+    return;
+  }
+  if (g_lib_policy == 1) {
+    run_lib(a, a_kmajor, b, b_kmajor, c, mode, bias);
+    return;
+  }
+  const GemmKey key{M, N, K, a_kmajor, b_kmajor, mode, (bool)ep.c_f32, has_bias};
+  int route = -1;
+  {
+    std::lock_guard<std::mutex> g(g_route_mu);
+    auto it = g_route.find(key);
+    if (it != g_route.end()) route = it->second;
+  }
+  if (route < 0) {
+    hipStream_t s = cur_stream(a);
+    hipStreamCaptureStatus cap = hipStreamCaptureStatusNone;
+    TAM_HIP_CHECK(hipStreamIsCapturing(s, &cap));
+    if (cap != hipStreamCaptureStatusNone) {
+      run_mfma(a, a_kmajor, b, b_kmajor, M, N, K, ep, allow_split);   // never tune in a graph
+      return;
+    }
+    // time both on scratch output so an accumulating C is untouched
+    Tensor scratch = at::empty_like(c);
+    tam::Epi es = ep;
+    es.c = scratch.data_ptr();
+    es.ldc = scratch.stride(0);
+    const float t_mfma =
+        time_ms(s, [&] { run_mfma(a, a_kmajor, b, b_kmajor, M, N, K, es, allow_split); });
+    float t_lib = 1e30f;
+    try {
+      t_lib = time_ms(s, [&] { run_lib(a, a_kmajor, b, b_kmajor, scratch, mode, bias); });
+    } catch (const std::exception&) {
+      t_lib = 1e30f;   // library path unsupported for this dtype combo: keep MFMA
+    }
+    route = t_lib < 0.95f * t_mfma ? 1 : 0;
+    std::lock_guard<std::mutex> g(g_route_mu);
+    g_route[key] = route;
+    g_route_ms[key] = {t_mfma, t_lib};
+  }
+  if (route == 1) run_lib(a, a_kmajor, b, b_kmajor, c, mode, bias);
+  else run_mfma(a, a_kmajor, b, b_kmajor, M, N, K, ep, allow_split);
+}
+
+void gemm_lib_policy_op(int64_t p) { g_lib_policy = (int)p; }
+
+// cached routing decisions: "M N K layout mode f32 bias route t_mfma_ms t_lib_ms" per line
+std::string gemm_routes_op() {
+  std::lock_guard<std::mutex> g(g_route_mu);
+  std::ostringstream o;
+  for (const auto& kv : g_route) {
+    const auto& k = kv.first;
+    const auto t = g_route_ms[k];
+    o << std::get<0>(k) << " " << std::get<1>(k) << " " << std::get<2>(k) << " "
+      << (std::get<3>(k) ? "K" : "M") << (std::get<4>(k) ? "K" : "N") << " " << std::get<5>(k)
+      << " " << std::get<6>(k) << " " << std::get<7>(k) << " " << (kv.second ? "lib" : "mfma")
+      << " " << t.first << " " << t.second << "\n";
+  }
+  return o.str();
 }
 
 // ------------------------------------------------------------------ conv
@@ -260,7 +380,10 @@ void embedding_backward_op(const Tensor& dout, const Tensor& ids, const Tensor& 
                           (int)gtable.size(1), (float)scale, cur_stream(dout));
 }
 
-void gemm_force_op(int64_t cfg, int64_t splits) { tam::gemm_force((int)cfg, (int)splits); }
+void gemm_force_op(int64_t cfg, int64_t splits) {
+  tam::gemm_force((int)cfg, (int)splits);
+  g_forced = cfg >= 0 || splits >= 1;
+}
 
 void colsum_op(const Tensor& x, const Tensor& out) {
   check_bf16(x, "x"); check_f32(out, "out"); check_contig(x, "x");
@@ -385,6 +508,8 @@ TORCH_LIBRARY(tam, m) {
   m.def("embedding_backward(Tensor dout, Tensor ids, Tensor(a!) gtable, float scale) -> ()", &embedding_backward_op);
   m.def("colsum(Tensor x, Tensor(a!) out) -> ()", &colsum_op);
   m.def("gemm_force(int cfg, int splits) -> ()", &gemm_force_op);
+  m.def("gemm_lib_policy(int policy) -> ()", &gemm_lib_policy_op);
+  m.def("gemm_routes() -> str", &gemm_routes_op);
   m.def("relu_backward(Tensor dy, Tensor y, Tensor(a!) dx) -> ()", &relu_backward_op);
   m.def("add(Tensor a, Tensor b, Tensor(a!) y) -> ()", &add_op);
   m.def("cast_f32_bf16(Tensor x, Tensor(a!) y) -> ()", &cast_op);

@@ -2,6 +2,7 @@
 // tile / split-K selection heuristic shared with the conv passes.
 #include "tam/launch.h"
 #include "tam/tiles.h"
+#include "tam/gemm256.h"
 
 namespace tam {
 
@@ -35,6 +36,23 @@ void gemm(const bf16_t* A, long lda, bool ak, const bf16_t* B, long ldb, bool bk
   TileChoice t = choose_tiles_gemm(M, N, K, can_split);
   if (g_force_cfg >= 0) t.cfg = g_force_cfg;
   if (g_force_splits >= 1) t.splits = can_split ? g_force_splits : 1;
+  // 256x256 LDS-DMA kernel for large K-major x K-major problems
+  const long t256 = (long)cdiv(M, 256) * cdiv(N, 256);
+  const bool big = gemm256_ok(ak, bk, M, N, K, lda, ldb) &&
+                   (t.cfg == 4 || (g_force_cfg < 0 && t256 >= 192 && K >= 1024));
+  if (big) {
+    int sp = 1;
+    if (g_force_splits >= 1) sp = t.splits;
+    else if (can_split && t256 < 256 && K / 64 >= 8) {
+      sp = (int)((256 + t256 - 1) / t256);
+      if (sp > K / 64 / 4) sp = K / 64 / 4;
+      if (sp < 1) sp = 1;
+    }
+    prepare_split(ep, sp, M, N, s);
+    launch_gemm256(A, lda, B, ldb, M, N, K, ep, sp, s);
+    return;
+  }
+  if (t.cfg > 3) t.cfg = 0;
   prepare_split(ep, t.splits, M, N, s);
   switch (t.cfg) {
     case 0: gemm_tile<128, 128>(A, lda, ak, B, ldb, bk, M, N, K, ep, t.splits, s); break;

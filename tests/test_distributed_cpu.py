@@ -188,7 +188,7 @@ def _spill_replay_worker(rank, world, port, outdir):
     import bench
     from tiresias_amd.executor.cluster_runtime import Worker, run_replay
 
-    jobs = bench.bench_trace(world, 4, seed=9, tiny=True)
+    jobs = bench.bench_trace(world, 4, seed=9, median_s=0.6, tiny=True)
     cfg = bench.make_cfg("dlas-gpu", "count", world, 9)
     cfg.ckpt_policy = "host"
     w = Worker(rank, world, torch.device("cpu"), dist.group.WORLD)

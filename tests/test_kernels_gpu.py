@@ -20,6 +20,37 @@ def T():
     return torch.ops.tam
 
 
+
+@pytest.fixture(autouse=True)
+def _mfma_only(gpu):
+    """Kernel numerics must exercise the hand-written MFMA path, not the
+    measured hipBLASLt route of plain GEMMs."""
+    T().gemm_lib_policy(0)
+    yield
+    T().gemm_lib_policy(-1)
+
+
+def test_gemm_routing(gpu):
+    """Measured MFMA/hipBLASLt routing: every route gives the same numbers,
+    accumulate-mode tuning leaves C untouched, and the decision is cached."""
+    torch.manual_seed(12)
+    M, N, K = 1024, 2048, 1024
+    A = torch.randn(M, K, device=gpu).to(BF)
+    W = torch.randn(N, K, device=gpu).to(BF)
+    bias = torch.randn(N, device=gpu).to(BF)
+    ref = A.float() @ W.float().t()
+    for pol in (1, -1):
+        T().gemm_lib_policy(pol)
+        y = torch.empty(M, N, device=gpu, dtype=BF)
+        T().gemm(A, True, W, True, y, 0, bias, False, None, 1.0, False)
+        assert rel_err(y, ref + bias.float()) < 1e-2
+        acc = torch.full((M, N), 2.0, device=gpu)
+        T().gemm(A.t().contiguous(), False, W, True, acc, 1, None, False, None, 1.0, True)
+        assert rel_err(acc, ref + 2.0) < 1e-4
+    routes = T().gemm_routes()
+    assert "1024 2048 1024 KK 0 0 1" in routes and "1024 2048 1024 MK 1 1 0" in routes
+
+
 # ------------------------------------------------------------------ GEMM
 @pytest.mark.parametrize("M,N,K", [(256, 256, 256), (200, 136, 72), (1000, 64, 520), (64, 1000, 64),
                                    (4096, 1024, 512), (33, 40, 8)])
@@ -82,6 +113,31 @@ def test_gemm_splitk(gpu):
     c2 = torch.ones(M, N, device=gpu)
     T().gemm(A, False, B, False, c2, 1, None, False, None, 1.0, True)
     assert rel_err(c2, ref + 1) < 1e-5
+
+
+@pytest.mark.parametrize("M,N,K,splits", [(512, 512, 64, 1), (512, 768, 128, 1), (300, 700, 192, 1),
+                                          (1024, 1024, 1024, 1), (4096, 512, 2048, 1),
+                                          (640, 384, 4096, 4), (257, 129, 320, 1)])
+def test_gemm256(gpu, M, N, K, splits):
+    """256x256 LDS-DMA kernel (forced), edges / 1-3 K-tiles / split-K / epilogues."""
+    torch.manual_seed(3)
+    A = torch.randn(M, K, device=gpu).to(BF)
+    W = torch.randn(N, K, device=gpu).to(BF)
+    bias = torch.randn(N, device=gpu).to(BF)
+    ref = A.float() @ W.float().t()
+    try:
+        T().gemm_force(4, splits)
+        y = torch.empty(M, N, device=gpu, dtype=BF)
+        T().gemm(A, True, W, True, y, 0, bias, True, None, 1.0, False)
+        assert rel_err(y, (ref + bias.float()).clamp_min(0)) < 1e-2
+        c = torch.full((M, N), 3.0, device=gpu)
+        T().gemm(A, True, W, True, c, 1, None, False, None, 1.0, True)
+        assert rel_err(c, ref + 3.0) < 1e-5
+        c0 = torch.full((M, N), 5.0, device=gpu)
+        T().gemm(A, True, W, True, c0, 0, None, False, None, 1.0, True)
+        assert rel_err(c0, ref) < 1e-5
+    finally:
+        T().gemm_force(-1, -1)
 
 
 # ------------------------------------------------------------------ conv

@@ -394,7 +394,9 @@ def run_replay(cfg: SimConfig, jobs: List[ReplayJob], rank: int, world: int, dev
         ctrl.start_clock()
     t_start = time.perf_counter()
     rounds = 0
-    prof = {"plan_s": 0.0, "bcast_s": 0.0, "apply_s": 0.0, "run_s": 0.0, "gather_s": 0.0}
+    # idle_s = sleeping because no job is runnable (arrival gaps), not overhead
+    prof = {"plan_s": 0.0, "bcast_s": 0.0, "apply_s": 0.0, "run_s": 0.0, "idle_s": 0.0,
+            "gather_s": 0.0}
     while rounds < max_rounds:
         ta = time.perf_counter()
         plan = ctrl.plan_round() if ctrl else None
@@ -416,6 +418,8 @@ def run_replay(cfg: SimConfig, jobs: List[ReplayJob], rank: int, world: int, dev
         prof["run_s"] += te - td
         if plan.get("wait", 0) > 0 and rep["job"] is None:
             time.sleep(plan["wait"])
+        tf = time.perf_counter()
+        prof["idle_s"] += tf - te
         if distributed:
             reps = [None] * world if rank == 0 else None
             try:
@@ -428,7 +432,7 @@ def run_replay(cfg: SimConfig, jobs: List[ReplayJob], rank: int, world: int, dev
             reps = [rep]
         if ctrl:
             ctrl.apply_reports(reps)
-        prof["gather_s"] += time.perf_counter() - te
+        prof["gather_s"] += time.perf_counter() - tf
         rounds += 1
     wall = time.perf_counter() - t_start
     w.clear()

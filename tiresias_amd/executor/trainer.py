@@ -52,9 +52,12 @@ class Trainer:
 
             if dist.get_world_size(group) > 1:
                 self.ddp = GradBucketer(self.arena, group, bucket_mb=bucket_mb)
-        self.use_graph = use_graph and self.device.type == "cuda" and self.ddp is None
+        self._want_graph = use_graph and self.device.type == "cuda"
+        self.use_graph = self._want_graph and self.ddp is None   # graphs for 1-GPU jobs only
         self._graph = None
         self._g_loss = None
+        self._warm = 0           # eager steps done before graph capture
+        self._side = None
         self.last_loss: Optional[torch.Tensor] = None
 
     # ------------------------------------------------------------ one step
@@ -91,6 +94,20 @@ class Trainer:
                 _cpu_opt(self.opt, w, g, self.opt_state, lo, hi, wb, self.lr, wd, gscale, self.step_count)
 
     def step(self) -> torch.Tensor:
+        if self.use_graph and self._graph is None and self._warm < 2:
+            # the first two steps are REAL steps run eagerly on a side stream
+            # (allocator pools, library handles/workspaces, GEMM route tuning
+            # happen outside capture); no work is thrown away
+            s = self._side or torch.cuda.Stream(self.device)
+            self._side = s
+            s.wait_stream(torch.cuda.current_stream(self.device))
+            with torch.cuda.stream(s):
+                loss = self._fwd_bwd()
+                self._opt_step()
+            torch.cuda.current_stream(self.device).wait_stream(s)
+            self._warm += 1
+            self.last_loss = loss
+            return loss
         if self.use_graph:
             loss = self._graph_step()
         else:
@@ -103,14 +120,7 @@ class Trainer:
 
     def _graph_step(self) -> torch.Tensor:
         if self._graph is None:
-            # warm up on a side stream (allocator pools, lazy init), then capture
-            s = torch.cuda.Stream(self.device)
-            s.wait_stream(torch.cuda.current_stream(self.device))
-            with torch.cuda.stream(s):
-                for _ in range(2):
-                    self._fwd_bwd()
-                    self.arena.grad.zero_()
-            torch.cuda.current_stream(self.device).wait_stream(s)
+            # capture fwd+bwd once (capture itself runs no kernels), then replay
             g = torch.cuda.CUDAGraph()
             with torch.cuda.graph(g):
                 self._g_loss = self._fwd_bwd()
@@ -204,6 +214,7 @@ class Trainer:
 
             if dist.get_world_size(group) > 1:
                 self.ddp = GradBucketer(self.arena, group, bucket_mb=self._bucket_mb)
+        self.use_graph = self._want_graph and self.ddp is None
         self._graph = None
 
     def release(self) -> None:

@@ -127,6 +127,7 @@ def main():
     a = ap.parse_args()
     _lib.load(required=True)
     T = torch.ops.tam
+    T.gemm_lib_policy(0)   # measure the MFMA kernels themselves
     dev = torch.device("cuda", 0)
     torch.manual_seed(0)
     res = []

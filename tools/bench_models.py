@@ -38,14 +38,23 @@ def main():
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--graph", action="store_true")
     ap.add_argument("--out", default=None)
+    ap.add_argument("--lib", type=int, default=-1,
+                    help="plain-GEMM routing: -1 measured MFMA/hipBLASLt, 0 MFMA only, 1 library")
     a = ap.parse_args()
+    import torch
+    from tiresias_amd.ops import _lib
+    _lib.load(required=True)
+    torch.ops.tam.gemm_lib_policy(a.lib)
     res = []
     for m in a.models.split(","):
         r = bench(m, steps=a.steps, warmup=a.warmup, graph=a.graph)
         print(json.dumps(r), flush=True)
         res.append(r)
+    routes = torch.ops.tam.gemm_routes().strip().splitlines()
+    print(f"gemm routes ({sum('lib' in r for r in routes)} of {len(routes)} plain-GEMM shapes -> hipBLASLt):")
+    print("\n".join(routes))
     if a.out:
-        json.dump(res, open(a.out, "w"), indent=1)
+        json.dump({"models": res, "lib_policy": a.lib, "gemm_routes": routes}, open(a.out, "w"), indent=1)
 
 
 if __name__ == "__main__":

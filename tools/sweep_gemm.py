@@ -16,7 +16,7 @@ from tiresias_amd.ops import _lib  # noqa: E402
 from tools.bench_kernels import timeit  # noqa: E402
 
 BF = torch.bfloat16
-CFG = {0: "128x128", 1: "128x64", 2: "64x128", 3: "64x64"}
+CFG = {0: "128x128", 1: "128x64", 2: "64x128", 3: "64x64", 4: "256x256"}
 
 
 def model_shapes():
@@ -43,6 +43,7 @@ def main():
     a = ap.parse_args()
     _lib.load(required=True)
     T = torch.ops.tam
+    T.gemm_lib_policy(0)   # measure the MFMA kernels themselves
     dev = torch.device("cuda", 0)
     res = []
     for (name, M, N, K, ak, bk, f32) in model_shapes():
@@ -63,7 +64,9 @@ def main():
         t_auto = timeit(run, iters=10, warmup=3)
         best = (t_auto, "auto")
         grid = {}
-        for cfg in range(4):
+        for cfg in range(5):
+            if cfg == 4 and not (ak and bk and K % 64 == 0 and M >= 128 and N >= 128):
+                continue
             for sp in ((1, 2, 4, 8, 16, 32) if f32 else (1,)):
                 T.gemm_force(cfg, sp)
                 t = timeit(run, iters=10, warmup=2)
