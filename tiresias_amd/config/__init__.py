@@ -30,7 +30,7 @@ def define_flags() -> None:
                     "horus|horus+|gandiva|pack|tiresias|lp")
     D.DEFINE_string("schedule", "fifo", "policy: fifo|fjf|sjf|lpjf|shortest|shortest-gpu|"
                     "shortest-expected|dlas|dlas-gpu|dlas-gpu-gittins|gittins|multi-dlas-gpu|"
-                    "dlas-gpu-pack|horus|horus+|gandiva")
+                    "dlas-gpu-pack|horus|horus+|gandiva|gandiva-ns (legacy node-set engine)")
     D.DEFINE_boolean("pack", False, "allow GPU sharing (co-location) in placement")
     D.DEFINE_integer("num_switch", 1, "racks (switches)")
     D.DEFINE_integer("num_node_p_switch", 32, "nodes per rack")
@@ -66,6 +66,9 @@ def define_flags() -> None:
     D.DEFINE_integer("lookahead", 5, "horus/horus+ look-ahead window")
     D.DEFINE_float("timeslice", 100.0, "gandiva time-slice quantum (time units)")
     D.DEFINE_float("replan_interval", 600.0, "multi-dlas reservation re-plan interval")
+    D.DEFINE_float("gandiva_tick", 10.0, "gandiva-ns: engine tick (s)")
+    D.DEFINE_float("gandiva_slice", 60.0, "gandiva-ns: time-slice rotation period (s)")
+    D.DEFINE_string("gandiva_mem_util", "one", "gandiva-ns job slot size: one|legacy|measured")
     D.DEFINE_boolean("replace_all", False, "re-place every runnable job at each event (legacy Tiresias)")
     D.DEFINE_float("skew_threshold", 0.5, "placement-sensitivity threshold (largest tensor / total)")
     D.DEFINE_string("throughput_table", "", "json of measured per-model iteration times (MI355X)")
@@ -142,6 +145,9 @@ class SimConfig:
     lookahead: int = 5
     timeslice: float = 100.0
     replan_interval: float = 600.0
+    gandiva_tick: float = 10.0
+    gandiva_slice: float = 60.0
+    gandiva_mem_util: str = "one"
     replace_all: bool = False
     skew_threshold: float = 0.5
     virtual_nodes: str = ""

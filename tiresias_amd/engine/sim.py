@@ -362,6 +362,14 @@ class TickSimulator(Simulator):
 def simulate(cfg: SimConfig, specs: List[JobSpec], out_dir: Optional[str] = None,
              prior: Optional[List[float]] = None, check_invariants: bool = False) -> Dict:
     log = MetricsLogger(out_dir)
+    if cfg.schedule == "gandiva-ns":
+        from .gandiva_ns import GandivaNodeSetSim
+
+        try:
+            return GandivaNodeSetSim(cfg, specs, logger=log, tick=cfg.gandiva_tick,
+                                     slice_s=cfg.gandiva_slice, mem_util=cfg.gandiva_mem_util).run()
+        finally:
+            log.close()
     cls = TickSimulator if cfg.engine == "tick" else Simulator
     sim = cls(cfg, specs, logger=log, prior=prior, check_invariants=check_invariants)
     try:

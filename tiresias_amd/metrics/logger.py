@@ -117,6 +117,21 @@ class MetricsLogger:
                 self._writers["cpu"].writerow([round(t, 6), n.node_id, n.cpu_used, n.cpu_count])
                 self._writers["memory"].writerow([round(t, 6), n.node_id, n.mem_used, n.mem_size])
 
+    GANDIVA_CLASSES = (1, 2, 4, 8, 16, 32, 64)
+
+    def gandiva_row(self, t: float, free_nodes: int, used_gpus: int, idle_gpus: int, n_pending: int,
+                    n_running: int, sets_per_class: Dict[int, int]) -> None:
+        """Node-set engine row (reference ``log.py`` gandiva checkpoint):
+        free nodes, used / idle GPUs, pending / running jobs, #sets per class."""
+        if not self.out_dir:
+            return
+        if "gandiva" not in self._writers:
+            self._open("gandiva", ["time", "free_nodes", "used_gpus", "idle_gpus", "pending_jobs",
+                                   "running_jobs"] + [f"node_g{g}" for g in self.GANDIVA_CLASSES])
+        self._writers["gandiva"].writerow([round(t, 6), free_nodes, used_gpus, idle_gpus, n_pending,
+                                           n_running] + [sets_per_class.get(g, 0)
+                                                         for g in self.GANDIVA_CLASSES])
+
     def network_row(self, t: float, job_id: str, nodes: int, rate: float) -> None:
         if self.node_logs:
             self._writers["network"].writerow([round(t, 6), job_id, nodes, round(rate, 6)])
