@@ -236,6 +236,16 @@ class Cluster:
                     return True
         return False
 
+    def neighbours(self, job_id: str) -> set:
+        """Ids of the other jobs sharing at least one device with ``job_id``."""
+        out = set()
+        for nid, devs in self.placed.get(job_id) or []:
+            for d in devs:
+                for t in self.nodes[nid].devices[d].tasks.values():
+                    if t.job_id != job_id:
+                        out.add(t.job_id)
+        return out
+
     def check_invariants(self) -> None:
         for n in self.nodes.values():
             cpu = mem = 0

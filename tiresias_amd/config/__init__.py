@@ -61,6 +61,8 @@ def define_flags() -> None:
     D.DEFINE_float("ckpt_hbm_budget_gb", 200.0, "HBM per GPU reserved for suspended jobs")
     D.DEFINE_string("virtual_nodes", "", "partition the MI355X box, e.g. 2x4 or 4x2")
     D.DEFINE_float("interference", 0.2, "co-location slowdown factor (reference infra/interference.py)")
+    D.DEFINE_string("interference_table", "", "measured per-model-pair slowdowns (JSON from "
+                    "tools/measure_interference.py); overrides the constant factor per pair")
     D.DEFINE_integer("max_tasks_per_gpu", 3, "co-location limit per GPU")
     D.DEFINE_float("gpu_mem_headroom_mb", 500.0, "free memory a GPU must keep when packing")
     D.DEFINE_integer("lookahead", 5, "horus/horus+ look-ahead window")
@@ -140,6 +142,7 @@ class SimConfig:
     enable_network_costs: bool = False
     enable_migration: bool = False
     interference: float = 0.2
+    interference_table: str = ""
     max_tasks_per_gpu: int = 3
     gpu_mem_headroom_mb: float = 500.0
     lookahead: int = 5

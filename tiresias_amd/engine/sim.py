@@ -36,7 +36,8 @@ import random
 import time
 from typing import Dict, List, Optional
 
-from ..cluster.network import interference_rate, network_rate
+from ..cluster.interference import InterferenceModel
+from ..cluster.network import network_rate
 from ..cluster.topology import Cluster, PlacementError
 from ..config import SimConfig
 from ..core.job import Job, JobSpec, JobState
@@ -78,6 +79,8 @@ class Simulator:
         self.reader = StreamingReader(specs)
         self.log = logger or MetricsLogger(None)
         self.ckpt = CkptCostModel(cfg.ckpt_policy, cfg.ckpt_bw_gbps, cfg.ckpt_hbm_budget_gb)
+        self.interf = (InterferenceModel.load(cfg.interference_table, cfg.interference)
+                       if cfg.interference_table else InterferenceModel(cfg.interference))
         self.now = 0.0
         self.active: List[Job] = []
         self.finished: List[Job] = []
@@ -104,8 +107,10 @@ class Simulator:
         if self.cfg.enable_network_costs and len(nodes) > 1:
             r *= network_rate(j, len(nodes), self.cluster.spec.bandwidth_mbps,
                               self.cluster.spec.internode_latency)
-        if self.cluster.pack and self.cluster.shared_devices(j.job_id):
-            r *= interference_rate(True, self.cfg.interference)
+        if self.cluster.pack:
+            nb = self.cluster.neighbours(j.job_id)
+            if nb:
+                r *= self.interf.rate(j.spec.model or "", [self.jobs[k].spec.model or "" for k in nb])
         return r
 
     def _start(self, j: Job, plan) -> None:

@@ -98,6 +98,7 @@ class Controller:
     def __init__(self, cfg: SimConfig, jobs: List[ReplayJob], world: int, quantum: float,
                  logger: Optional[MetricsLogger] = None):
         self.cfg = cfg
+        self.log = logger
         self.rjobs = {rj.spec.job_id: rj for rj in jobs}
         specs = []
         for rj in jobs:
@@ -132,6 +133,10 @@ class Controller:
     def apply_reports(self, reports: List[dict]) -> None:
         seen = set()
         for r in reports:
+            if r and r.get("dev") and self.log is not None:
+                d = r["dev"]
+                self.log.device_row(self.now(), r["rank"], d.get("util_pct"), d.get("free_mb"),
+                                    d.get("total_mb"), r.get("job"))
             if not r or r.get("job") is None:
                 continue
             jid = r["job"]
@@ -214,7 +219,7 @@ class Controller:
 
 class Worker:
     def __init__(self, rank: int, world: int, device: torch.device, world_pg=None, use_graph=False,
-                 gang_backend: Optional[str] = None):
+                 gang_backend: Optional[str] = None, monitor_period: float = 5.0):
         self.gang_backend = gang_backend or ("nccl" if device.type == "cuda" else "gloo")
         self.rank = rank
         self.world = world
@@ -226,6 +231,13 @@ class Worker:
         self.spilled_bytes = 0
         self.restored_bytes = 0
         self._engine = None
+        # real-device sampling (HIP mem info + amd-smi) for gpu_live.csv
+        self.monitor = None
+        self._mon_t = -1e9
+        if device.type == "cuda" and monitor_period > 0:
+            from ..cluster.device import DeviceMonitor
+
+            self.monitor = DeviceMonitor(period=monitor_period)
 
     def _ckpt_engine(self):
         if self._engine is None:
@@ -302,10 +314,25 @@ class Worker:
                     if t is not None:
                         t.release()
 
+    def _dev_sample(self) -> Optional[dict]:
+        """Real HBM / activity of this rank's GPU (hipMemGetInfo + amd-smi),
+        at most every monitor period; None on CPU."""
+        if self.monitor is None:
+            return None
+        now = time.monotonic()
+        if now - self._mon_t < self.monitor.period:
+            return None
+        self._mon_t = now
+        for d in self.monitor.sample(force=True):
+            if d.index == self.device.index:
+                return {"util_pct": d.util_pct, "free_mb": round(d.free_mb, 1),
+                        "total_mb": round(d.total_mb, 1)}
+        return None
+
     def run(self, plan: dict) -> dict:
         a = plan["assign"].get(self.rank)
         if a is None:
-            return {"rank": self.rank, "job": None}
+            return {"rank": self.rank, "job": None, "dev": self._dev_sample()}
         jid, n = a
         t = self.trainers[jid]
         t0 = time.perf_counter()
@@ -315,7 +342,8 @@ class Worker:
             torch.cuda.synchronize(self.device)
         dt = time.perf_counter() - t0
         return {"rank": self.rank, "job": jid, "iters": n, "run_s": dt,
-                "loss": float(t.last_loss) if t.last_loss is not None else None}
+                "loss": float(t.last_loss) if t.last_loss is not None else None,
+                "dev": self._dev_sample()}
 
     def clear(self):
         for t in self.trainers.values():

@@ -117,6 +117,16 @@ class MetricsLogger:
                 self._writers["cpu"].writerow([round(t, 6), n.node_id, n.cpu_used, n.cpu_count])
                 self._writers["memory"].writerow([round(t, 6), n.node_id, n.mem_used, n.mem_size])
 
+    def device_row(self, t: float, rank: int, util_pct, free_mb, total_mb, job_id) -> None:
+        """Live runtime: measured state of one rank's GPU (hipMemGetInfo +
+        amd-smi activity), replacing the reference's sampled utilisation."""
+        if not self.out_dir:
+            return
+        if "gpu_live" not in self._writers:
+            self._open("gpu_live", ["time", "rank", "util_pct", "free_mb", "total_mb", "job_id"])
+        self._writers["gpu_live"].writerow([round(t, 6), rank, "" if util_pct is None else util_pct,
+                                            free_mb, total_mb, job_id or ""])
+
     GANDIVA_CLASSES = (1, 2, 4, 8, 16, 32, 64)
 
     def gandiva_row(self, t: float, free_nodes: int, used_gpus: int, idle_gpus: int, n_pending: int,
