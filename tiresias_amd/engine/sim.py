@@ -100,6 +100,16 @@ class Simulator:
         # history file, use the trace's own GPU-service distribution
         return sorted(s.duration * s.num_gpu for s in specs)
 
+    def submit(self, spec: JobSpec) -> Job:
+        """Online job submission (live runtime's spool API): registers the job;
+        it arrives at ``spec.submit_time`` through the normal arrival path."""
+        if spec.job_id in self.jobs:
+            raise ValueError(f"duplicate job id {spec.job_id}")
+        j = Job(spec)
+        self.jobs[spec.job_id] = j
+        self.reader.add(spec)
+        return j
+
     # ------------------------------------------------------------------ helpers
     def _rate(self, j: Job) -> float:
         r = 1.0

@@ -29,6 +29,7 @@ from __future__ import annotations
 import math
 import os
 import time
+import zlib
 from dataclasses import dataclass, field
 from typing import Dict, List, Optional, Tuple
 
@@ -96,8 +97,10 @@ class ReplayJob:
 
 class Controller:
     def __init__(self, cfg: SimConfig, jobs: List[ReplayJob], world: int, quantum: float,
-                 logger: Optional[MetricsLogger] = None):
+                 logger: Optional[MetricsLogger] = None, spool=None):
         self.cfg = cfg
+        self.spool = spool            # executor.spool.Spool: online job submission
+        self._status_t = -1e9
         self.log = logger
         self.rjobs = {rj.spec.job_id: rj for rj in jobs}
         specs = []
@@ -105,9 +108,10 @@ class Controller:
             s = rj.spec
             # duration in work units = iterations (progress is reported in iterations)
             specs.append(JobSpec(**{**s.__dict__, "duration": float(rj.iterations)}))
-        self.sched = LiveScheduler(cfg, specs, logger=logger,
-                                   prior=sorted(rj.iterations * self._iter_est(rj.model, rj.spec.num_gpu)
-                                                * rj.spec.num_gpu for rj in jobs))
+        prior = sorted(rj.iterations * self._iter_est(rj.model, rj.spec.num_gpu) * rj.spec.num_gpu
+                       for rj in jobs)
+        # serve-only clusters start with no history: a one-point prior until jobs finish
+        self.sched = LiveScheduler(cfg, specs, logger=logger, prior=prior or [1.0])
         self.world = world
         self.quantum = quantum
         self.gpn = self.sched.cluster.spec.num_gpu_p_node
@@ -152,10 +156,66 @@ class Controller:
             j = self.sched.jobs[jid]
             j.progress = float(min(self.done_iters[jid], rj.iterations))
 
+    # ---------------------------------------------------------------- submission
+    def _poll_spool(self) -> None:
+        from ..models import MODELS
+
+        now = self.now()
+        for req in self.spool.poll():
+            jid = str(req.get("job_id") or "")
+            model = req.get("model")
+            g = int(req.get("num_gpu") or 1)
+            why = ""
+            if not jid or jid in self.rjobs:
+                why = f"duplicate or empty job id {jid!r}"
+            elif model not in MODELS:
+                why = f"unknown model {model!r} (known: {sorted(MODELS)})"
+            elif not 1 <= g <= self.world:
+                why = f"num_gpu {g} outside 1..{self.world}"
+            iters = req.get("iterations")
+            if not why:
+                if iters is None:
+                    dur = float(req.get("duration") or 0.0)
+                    iters = int(round(dur / self._iter_est(model, g))) if dur > 0 else 0
+                iters = int(iters)
+                if iters <= 0:
+                    why = "iterations/duration must be positive"
+            if why:
+                self.spool.resolve(req, False, why)
+                if self.log is not None:
+                    self.log.decision(now, "reject", jid or "?", reason=why)
+                continue
+            spec = JobSpec(job_id=jid, submit_time=now, duration=iters * self._iter_est(model, g),
+                           num_gpu=g, model=model, iterations=iters)
+            self.rjobs[jid] = ReplayJob(spec=spec, model=model, iterations=iters, batch=req.get("batch"))
+            self.done_iters[jid] = 0
+            self.sched.submit(JobSpec(**{**spec.__dict__, "duration": float(iters)}))
+            self.spool.resolve(req, True)
+            if self.log is not None:
+                self.log.decision(now, "submit", jid, gpus=g, model=model, iterations=iters)
+
+    def status(self) -> dict:
+        s = self.sched
+        jobs = {}
+        for jid, j in s.jobs.items():
+            if j.state.name == "SUBMITTED":
+                continue
+            jobs[jid] = {"state": j.state.name, "model": self.rjobs[jid].model, "num_gpu": j.num_gpu,
+                         "iterations_done": self.done_iters.get(jid, 0),
+                         "iterations": self.rjobs[jid].iterations, "queue": j.queue,
+                         "preempted": j.preempt_count,
+                         "jct_s": round(j.jct, 4) if j.jct is not None else None}
+        return {"time_s": round(self.now(), 3), "round": self.round, "jobs": jobs,
+                "running": sum(1 for j in s.active if j.is_running),
+                "pending": sum(1 for j in s.active if j.is_pending),
+                "finished": len(s.finished)}
+
     # ---------------------------------------------------------------- planning
     def plan_round(self) -> dict:
         s = self.sched
         s.actions = []
+        if self.spool is not None:
+            self._poll_spool()
         t = max(self.now(), s.now)
         if s.events == 0 or t > s.now:
             s.step(t)
@@ -179,7 +239,7 @@ class Controller:
                 old = self.holders.get(j.job_id)
                 rj = self.rjobs[j.job_id]
                 act = {"op": "start", "job": j.job_id, "ranks": ranks, "model": rj.model,
-                       "batch": rj.batch, "seed": int(j.job_id) if j.job_id.isdigit() else hash(j.job_id) % 100000}
+                       "batch": rj.batch, "seed": int(j.job_id) if j.job_id.isdigit() else zlib.crc32(j.job_id.encode()) % 100000}
                 if old is None:
                     act["source"] = "fresh"
                 elif old == ranks:
@@ -210,6 +270,11 @@ class Controller:
                 assign[r] = (j.job_id, n)
         self.round += 1
         stop = not s.active and s.reader.remaining() == 0
+        if self.spool is not None:
+            stop = stop and self.spool.shutdown_requested()
+            if time.perf_counter() - self._status_t > 0.5 or stop:
+                self._status_t = time.perf_counter()
+                self.spool.publish(self.status())
         wait = 0.0
         if not assign and not stop:
             # idle cluster: sleep until the next arrival instead of spinning
@@ -401,7 +466,7 @@ class RankLost(RuntimeError):
 def run_replay(cfg: SimConfig, jobs: List[ReplayJob], rank: int, world: int, device: torch.device,
                ctrl_pg=None, world_pg=None, worker: Optional[Worker] = None, quantum: float = 0.4,
                out_dir: Optional[str] = None, use_graph: bool = False, max_rounds: int = 100000,
-               fault: Optional[dict] = None) -> Optional[dict]:
+               fault: Optional[dict] = None, spool=None) -> Optional[dict]:
     """Replay ``jobs`` on the live cluster. Returns the summary on rank 0.
 
     ``fault={"rank": r, "round": k}`` injects a crash of rank r at round k
@@ -414,7 +479,7 @@ def run_replay(cfg: SimConfig, jobs: List[ReplayJob], rank: int, world: int, dev
     log = None
     if rank == 0:
         log = MetricsLogger(out_dir, node_logs=False)
-        ctrl = Controller(cfg, jobs, world, quantum, logger=log)
+        ctrl = Controller(cfg, jobs, world, quantum, logger=log, spool=spool)
     w = worker or Worker(rank, world, device, world_pg, use_graph=use_graph)
     if distributed:
         dist.barrier(group=ctrl_pg)

@@ -143,6 +143,15 @@ class StreamingReader:
             self.cursor += 1
         return out
 
+    def add(self, spec: JobSpec) -> None:
+        """Online submission: insert among the not-yet-released rows, in
+        submit-time order (a spec dated in the past is released next)."""
+        import bisect
+
+        keys = [s.submit_time for s in self.specs[self.cursor:]]
+        i = self.cursor + bisect.bisect_right(keys, spec.submit_time)
+        self.specs.insert(i, spec)
+
     def next_time(self) -> float:
         return self.specs[self.cursor].submit_time if self.cursor < len(self.specs) else float("inf")
 
