@@ -59,6 +59,8 @@ def define_flags() -> None:
     D.DEFINE_string("ckpt_policy", "none", "none | hbm | host | measured: preemption cost model")
     D.DEFINE_float("ckpt_bw_gbps", 50.0, "spill/restore bandwidth GB/s for ckpt_policy=host")
     D.DEFINE_float("ckpt_hbm_budget_gb", 200.0, "HBM per GPU reserved for suspended jobs")
+    D.DEFINE_string("ckpt_table", "profiles/ckpt_mi355x.json",
+                    "measured spill/restore/peer bandwidths for ckpt_policy=measured (python -m tiresias_amd.ckpt)")
     D.DEFINE_string("virtual_nodes", "", "partition the MI355X box, e.g. 2x4 or 4x2")
     D.DEFINE_float("interference", 0.2, "co-location slowdown factor (reference infra/interference.py)")
     D.DEFINE_string("interference_table", "", "measured per-model-pair slowdowns (JSON from "
@@ -139,6 +141,7 @@ class SimConfig:
     ckpt_policy: str = "none"
     ckpt_bw_gbps: float = 50.0
     ckpt_hbm_budget_gb: float = 200.0
+    ckpt_table: str = "profiles/ckpt_mi355x.json"
     enable_network_costs: bool = False
     enable_migration: bool = False
     interference: float = 0.2

@@ -32,14 +32,16 @@ class CkptCostModel:
         self.policy = policy
         self.host_gbps = host_gbps
         self.xgmi_gbps = XGMI_GBPS
+        self.h2d_gbps = host_gbps
         self.budget = hbm_budget_gb * 1e9
         self.resident: Dict[Tuple[str, int], float] = {}     # (node, dev) -> bytes of suspended state
         self.where: Dict[str, Tuple[str, Optional[dict]]] = {}  # job -> ("hbm"|"host", alloc)
         if table_path and os.path.exists(table_path):
             with open(table_path) as f:
                 t = json.load(f)
-            self.host_gbps = float(t.get("d2h_gbps", self.host_gbps))
-            self.xgmi_gbps = float(t.get("p2p_gbps", self.xgmi_gbps))
+            self.host_gbps = float(t.get("d2h_gbps") or self.host_gbps)
+            self.h2d_gbps = float(t.get("h2d_gbps") or self.host_gbps)
+            self.xgmi_gbps = float(t.get("p2p_gbps") or self.xgmi_gbps)
 
     def state_bytes_per_gpu(self, job) -> float:
         try:
@@ -81,7 +83,7 @@ class CkptCostModel:
             if old == alloc:
                 return 0.0, 0.0
             return b / (self.xgmi_gbps * 1e9), b * job.num_gpu
-        return b / (self.host_gbps * 1e9), b * job.num_gpu
+        return b / (self.h2d_gbps * 1e9), b * job.num_gpu
 
     def on_finish(self, job) -> None:
         loc = self.where.pop(job.job_id, None)

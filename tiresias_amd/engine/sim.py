@@ -78,7 +78,8 @@ class Simulator:
             self.jobs[s.job_id] = Job(s)
         self.reader = StreamingReader(specs)
         self.log = logger or MetricsLogger(None)
-        self.ckpt = CkptCostModel(cfg.ckpt_policy, cfg.ckpt_bw_gbps, cfg.ckpt_hbm_budget_gb)
+        self.ckpt = CkptCostModel(cfg.ckpt_policy, cfg.ckpt_bw_gbps, cfg.ckpt_hbm_budget_gb,
+                                  table_path=cfg.ckpt_table if cfg.ckpt_policy == "measured" else "")
         self.interf = (InterferenceModel.load(cfg.interference_table, cfg.interference)
                        if cfg.interference_table else InterferenceModel(cfg.interference))
         self.now = 0.0
