@@ -477,6 +477,33 @@ void lstm_fwd_op(const Tensor& gates, const optional<Tensor>& c_prev, const Tens
                          bpm(h_out), opt_ptr<float>(h_f32), act.data_ptr<float>(), B, Hd,
                          cur_stream(gates));
 }
+// fused timestep: gx [B][4Hd] f32 (x-projection + bias), w_hh [4Hd][Hd] bf16
+void lstm_step_fwd_op(const Tensor& gx, const Tensor& w_hh, const optional<Tensor>& h_prev,
+                      const optional<Tensor>& c_prev, const Tensor& c_out, const Tensor& h_out,
+                      const Tensor& act) {
+  check_f32(gx, "gx"); check_bf16(w_hh, "w_hh"); check_f32(c_out, "c_out"); check_bf16(h_out, "h_out");
+  check_f32(act, "act");
+  const int64_t B = gx.size(0), Hd = w_hh.size(1);
+  TORCH_CHECK(gx.dim() == 2 && gx.size(1) == 4 * Hd && gx.stride(1) == 1 && gx.stride(0) == 4 * Hd,
+              "tam.lstm_step_forward: gx must be contiguous [B][4*Hd]");
+  TORCH_CHECK(w_hh.is_contiguous() && w_hh.size(0) == 4 * Hd, "tam.lstm_step_forward: w_hh [4Hd][Hd]");
+  TORCH_CHECK(B % 16 == 0 && Hd % 256 == 0, "tam.lstm_step_forward: needs B % 16 == 0, Hd % 256 == 0");
+  TORCH_CHECK(c_out.numel() == B * Hd && h_out.numel() == B * Hd && act.numel() == 5 * B * Hd &&
+              c_out.is_contiguous() && h_out.is_contiguous() && act.is_contiguous(),
+              "tam.lstm_step_forward: output shapes");
+  if (h_prev.has_value() && h_prev->defined()) {
+    check_bf16(*h_prev, "h_prev");
+    TORCH_CHECK(h_prev->is_contiguous() && h_prev->numel() == B * Hd, "tam.lstm_step_forward: h_prev");
+  }
+  if (c_prev.has_value() && c_prev->defined()) {
+    check_f32(*c_prev, "c_prev");
+    TORCH_CHECK(c_prev->is_contiguous() && c_prev->numel() == B * Hd, "tam.lstm_step_forward: c_prev");
+  }
+  tam::lstm_step_forward(gx.data_ptr<float>(), bp(w_hh), opt_ptr<const tam::bf16_t>(h_prev),
+                         opt_ptr<const float>(c_prev), c_out.data_ptr<float>(), bpm(h_out),
+                         act.data_ptr<float>(), (int)B, (int)Hd, cur_stream(gx));
+}
+
 void lstm_bwd_op(const Tensor& act, const optional<Tensor>& c_prev, const optional<Tensor>& dh,
                  const optional<Tensor>& dc_next, const optional<Tensor>& dgates,
                  const optional<Tensor>& dc_prev, const optional<Tensor>& dgates_bf16) {
@@ -517,6 +544,7 @@ TORCH_LIBRARY(tam, m) {
   m.def("adam_step(Tensor(a!) w, Tensor(b!) g, Tensor(c!) m, Tensor(d!) v, Tensor(e!) wb, float lr, float b1, float b2, float eps, float wd, int step, float gscale, bool zero_grad) -> ()", &adam_op);
   m.def("attn_forward(Tensor q, Tensor k, Tensor v, Tensor(a!) o, Tensor(b!) lse, bool causal, float scale, Tensor? kv_len) -> ()", &attn_forward_op);
   m.def("attn_backward(Tensor q, Tensor k, Tensor v, Tensor o, Tensor dout, Tensor lse, Tensor(a!) dq, Tensor(b!) dk, Tensor(c!) dv, Tensor(d!) dq_acc, Tensor(e!) delta, bool causal, float scale, Tensor? kv_len) -> ()", &attn_backward_op);
+  m.def("lstm_step_forward(Tensor gx, Tensor w_hh, Tensor? h_prev, Tensor? c_prev, Tensor(a!) c_out, Tensor(b!) h_out, Tensor(c!) act) -> ()", &lstm_step_fwd_op);
   m.def("lstm_cell_forward(Tensor gates, Tensor? c_prev, Tensor(a!) c_out, Tensor(b!) h_out, Tensor(c!)? h_f32, Tensor(d!) act) -> ()", &lstm_fwd_op);
   m.def("lstm_cell_backward(Tensor act, Tensor? c_prev, Tensor? dh, Tensor? dc_next, Tensor(a!)? dgates, Tensor(b!)? dc_prev, Tensor(c!)? dgates_bf16) -> ()", &lstm_bwd_op);
 }

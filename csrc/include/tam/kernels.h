@@ -79,6 +79,9 @@ void attn_backward(const bf16_t* q, const bf16_t* k, const bf16_t* v, const bf16
 // LSTM cell pointwise (gates = x W_ih^T + h W_hh^T + b precomputed, fp32)
 void lstm_cell_forward(const float* gates, const float* c_prev, float* c_out, bf16_t* h_out,
                        float* h_out_f32, float* act_cache, int B, int Hd, hipStream_t s);
+// fused forward timestep (B % 16 == 0, Hd % 256 == 0): h_out/c_out/act for one t
+void lstm_step_forward(const float* gx, const bf16_t* w_hh, const bf16_t* h_prev, const float* c_prev,
+                       float* c_out, bf16_t* h_out, float* act, int B, int Hd, hipStream_t s);
 void lstm_cell_backward(const float* act_cache, const float* c_prev, const float* c_out,
                         const float* dh, const float* dc_next, float* dgates, float* dc_prev,
                         bf16_t* dgates_bf16, int B, int Hd, hipStream_t s);

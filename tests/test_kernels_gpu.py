@@ -460,6 +460,28 @@ def test_lstm_cell(gpu):
     assert rel_err(dG, g1) < 1e-4 and rel_err(dcp, g2) < 1e-4
 
 
+@pytest.mark.parametrize("B,Hd,first", [(64, 1024, False), (64, 1024, True), (32, 512, False),
+                                        (16, 768, False), (128, 256, False)])
+def test_lstm_step_fused(gpu, B, Hd, first):
+    """Fused timestep (recurrent MFMA GEMM + cell) vs fp32 torch."""
+    torch.manual_seed(14)
+    gx = torch.randn(B, 4 * Hd, device=gpu)
+    w = (torch.randn(4 * Hd, Hd, device=gpu) / Hd ** 0.5).to(BF)
+    hp = None if first else torch.randn(B, Hd, device=gpu).to(BF)
+    cp = None if first else torch.randn(B, Hd, device=gpu)
+    c = torch.empty(B, Hd, device=gpu); h = torch.empty(B, Hd, device=gpu, dtype=BF)
+    act = torch.empty(B, 5 * Hd, device=gpu)
+    T().lstm_step_forward(gx, w, hp, cp, c, h, act)
+    g = gx + (hp.float() @ w.float().t() if hp is not None else 0.0)
+    i, f, gg, o = g.chunk(4, 1)
+    c_ref = torch.sigmoid(f) * (cp if cp is not None else 0.0) + torch.sigmoid(i) * torch.tanh(gg)
+    h_ref = torch.sigmoid(o) * torch.tanh(c_ref)
+    assert rel_err(c, c_ref) < 1e-4 and rel_err(h, h_ref) < 1e-2
+    a_ref = torch.cat([torch.sigmoid(i), torch.sigmoid(f), torch.tanh(gg), torch.sigmoid(o),
+                       torch.tanh(c_ref)], 1)
+    assert rel_err(act, a_ref) < 1e-4
+
+
 # ------------------------------------------------------------------ checkpoint engine
 def test_ckpt_engine_roundtrip(gpu):
     eng = torch.classes.tam.CkptEngine(0, 64 << 20)

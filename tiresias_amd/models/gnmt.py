@@ -34,6 +34,9 @@ def _T():
     return _lib.ops()
 
 
+FUSED_STEP = False
+
+
 class _LSTMLayer(Function):
     @staticmethod
     def forward(ctx, x, token, w_ih: Param, w_hh: Param, b: Param, reverse: bool):
@@ -50,11 +53,21 @@ class _LSTMLayer(Function):
             _T().gemm(x2, True, w_ih.w, True, G, 0, b.w, False, None, 1.0, False)
             Gv = G.view(T, B, 4 * Hd)
             prev = None
+            # the fused per-timestep kernel (lstm_step_forward) ties GEMM + cell +
+            # launch boundary on MI355X (12.8 us vs 8.4 + 2.8 us: its 4-units-per-WG
+            # split re-reads h_{t-1} in every CU, 4x the split-K GEMM's L2 traffic),
+            # so it is opt-in
+            fused = FUSED_STEP and B % 16 == 0 and Hd % 256 == 0
             for t in steps:
-                if prev is not None:
-                    _T().gemm(Hs[prev], True, w_hh.w, True, Gv[t], 1, None, False, None, 1.0, True)
-                _T().lstm_cell_forward(Gv[t], Cs[prev] if prev is not None else None, Cs[t], Hs[t],
-                                       None, act[t])
+                if fused:
+                    # one launch per timestep: recurrent MFMA GEMM + cell (lstm.hip)
+                    _T().lstm_step_forward(Gv[t], w_hh.w, Hs[prev] if prev is not None else None,
+                                           Cs[prev] if prev is not None else None, Cs[t], Hs[t], act[t])
+                else:
+                    if prev is not None:
+                        _T().gemm(Hs[prev], True, w_hh.w, True, Gv[t], 1, None, False, None, 1.0, True)
+                    _T().lstm_cell_forward(Gv[t], Cs[prev] if prev is not None else None, Cs[t], Hs[t],
+                                           None, act[t])
                 prev = t
         else:
             G = x2.float() @ w_ih.w.float().t() + b.w.float()
