@@ -380,6 +380,8 @@ void embedding_backward_op(const Tensor& dout, const Tensor& ids, const Tensor& 
                           (int)gtable.size(1), (float)scale, cur_stream(dout));
 }
 
+void conv_dma_policy_op(int64_t p) { tam::conv_dma_policy((int)p); }
+
 void gemm_force_op(int64_t cfg, int64_t splits) {
   tam::gemm_force((int)cfg, (int)splits);
   g_forced = cfg >= 0 || splits >= 1;
@@ -536,6 +538,7 @@ TORCH_LIBRARY(tam, m) {
   m.def("colsum(Tensor x, Tensor(a!) out) -> ()", &colsum_op);
   m.def("gemm_force(int cfg, int splits) -> ()", &gemm_force_op);
   m.def("gemm_lib_policy(int policy) -> ()", &gemm_lib_policy_op);
+  m.def("conv_dma_policy(int policy) -> ()", &conv_dma_policy_op);
   m.def("gemm_routes() -> str", &gemm_routes_op);
   m.def("relu_backward(Tensor dy, Tensor y, Tensor(a!) dx) -> ()", &relu_backward_op);
   m.def("add(Tensor a, Tensor b, Tensor(a!) y) -> ()", &add_op);

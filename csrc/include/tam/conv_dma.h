@@ -1,0 +1,480 @@
+// tiresias_amd — LDS-DMA implicit-GEMM convolution (fwd and stride-1 dgrad)
+// for NHWC bf16 when the gathered operand has C % 64 == 0.
+//
+//   fwd  : Y[m=(n,p,q)][k]  = sum_{r,s,c} X[n, p*st-pad+r, q*st-pad+s, c] W[k][r][s][c]
+//   dgrad: dX[m=(n,h,w)][c] = sum_{r,s,k} dY[n, h+pad-r, w+pad-s, k] Wt[c][r][s][k]
+//
+// Why a second conv core (the register-staged igemm in igemm.h stays for odd
+// shapes): a 128x128 tile at full MFMA rate needs ~39 TB/s of operand traffic
+// (over the 34.5 TB/s L2), and its per-load div/mod gather is VALU work in the
+// MFMA gaps. Here:
+//   * BM = 256 output rows x BN (64/128/256) columns, BK = 64; waves 4 (M) x WN,
+//     each wave a 64 x (BN/WN) block of 16x16x32 MFMAs;
+//   * since C % 64 == 0 a whole K-tile is ONE filter tap (r,s) and 64 channels,
+//     so the tap is wave-uniform (scalar bookkeeping per K-tile) and every row of
+//     the tile is one contiguous 128-B segment: pixel base (precomputed once per
+//     row per thread) + tap offset, or the 128-B zero row for padding taps;
+//   * both operands go HBM/L2 -> LDS with global_load_lds_dwordx4 (lane-linear
+//     1 KiB per wave instruction = 8 rows), the XOR bank swizzle applied on the
+//     SOURCE chunk; fragment reads are the conflict-free read_frag_k;
+//   * a 3-stage ring (BN <= 128; 2 stages at BN = 256) with one raw barrier per
+//     K-tile: counted `s_waitcnt vmcnt` retires tile t (tile t+1 stays in
+//     flight across the barrier), then tile t+2 is issued into the stage tile
+//     t-1 used, then tile t is computed;
+//   * XCD-aware bijective workgroup remap, grouped-M tile order.
+#pragma once
+#include "tam/igemm.h"
+
+namespace tam {
+
+typedef __attribute__((address_space(3))) void cd_lds_void_t;
+
+// 256 B of zeros: the source of every padding tap / pixel-tail row (device
+// globals are zero-initialised at load; never written)
+static __device__ __attribute__((aligned(256))) bf16_t g_cd_zero[128];
+
+struct CDArgs {
+  const bf16_t* src;   // gathered operand, NHWC [.][Hs][Ws][Cs]
+  const bf16_t* wgt;   // B operand, K-major [Ng][Kd]
+  int M, Ng, Kd;       // GEMM dims (Kd = R*S*Cs)
+  int Hs, Ws, Cs;      // gather source geometry
+  int P, Q;            // rows m = (n, p, q) over a P x Q grid
+  int S;               // filter width
+  int stride, pad;
+};
+
+template <int N>
+__device__ __forceinline__ void cd_vm_wait() {
+  asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
+}
+
+__device__ __forceinline__ void cd_barrier() {
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+  asm volatile("" ::: "memory");
+}
+
+template <int BN, int WN, bool FWD>
+__global__ void __launch_bounds__(256 * WN, 1) conv_dma_kernel(CDArgs a, Epi ep) {
+  constexpr int W = 4 * WN;               // waves
+  constexpr int BM = 256, BK = 64;
+  constexpr int STAGES = BN <= 128 ? 3 : 2;
+  constexpr int A_BYTES = BM * BK * 2, B_BYTES = BN * BK * 2, STAGE = A_BYTES + B_BYTES;
+  constexpr int AG = 32 / W;              // A 8-row groups per wave
+  constexpr int BG = BN / 8 / W;          // B 8-row groups per wave
+  constexpr int D = AG + BG;              // DMA instructions per thread per K-tile
+  constexpr int WCOLS = BN / WN;          // columns per wave
+  constexpr int TN = WCOLS / 16, TM = 4;
+  __shared__ __attribute__((aligned(1024))) char smem[STAGES * STAGE];
+
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int wm = wid & 3, wn = wid >> 2;
+
+  const int tiles_m = (a.M + BM - 1) / BM, tiles_n = (a.Ng + BN - 1) / BN;
+  const int bid = xcd_remap(blockIdx.x, gridDim.x);
+  constexpr int GROUP = 8;
+  const int per_group = GROUP * tiles_n;
+  const int grp = bid / per_group;
+  const int first_m = grp * GROUP;
+  const int gsize = min(tiles_m - first_m, GROUP);
+  const int tm = first_m + (bid % per_group) % gsize;
+  const int tn = (bid % per_group) / gsize;
+  const int m0 = tm * BM, n0 = tn * BN;
+
+  // ---- per-thread row state (rows fixed for the whole K loop)
+  const int lrow = lane >> 3;
+  int abase[AG], ah[AG], aw[AG];
+#pragma unroll
+  for (int j = 0; j < AG; ++j) {
+    const int rr = (wid + W * j) * 8 + lrow;
+    const int c = (lane & 7) ^ ((rr >> 1) & 7);
+    const int m = m0 + rr;
+    if (m < a.M) {
+      const int q = m % a.Q, t = m / a.Q, p = t % a.P, n = t / a.P;
+      const int hb = FWD ? p * a.stride - a.pad : p + a.pad;
+      const int wb = FWD ? q * a.stride - a.pad : q + a.pad;
+      ah[j] = hb;
+      aw[j] = wb;
+      abase[j] = ((n * a.Hs + hb) * a.Ws + wb) * a.Cs + c * 8;
+    } else {
+      ah[j] = -(1 << 28);                  // every tap out of range -> zero row
+      aw[j] = 0;
+      abase[j] = c * 8;
+    }
+  }
+  const bf16_t* bptr[BG];
+#pragma unroll
+  for (int j = 0; j < BG; ++j) {
+    const int rr = (wid + W * j) * 8 + lrow;
+    const int c = (lane & 7) ^ ((rr >> 1) & 7);
+    int n = n0 + rr;
+    n = n < a.Ng ? n : a.Ng - 1;           // clamp: columns past the edge are never stored
+    bptr[j] = a.wgt + (long)n * a.Kd + c * 8;
+  }
+  const int ctiles = a.Cs / BK;
+  const int nk = a.Kd / BK;
+
+  auto issue = [&](int kt, int st) {
+    char* sa = smem + st * STAGE;
+    char* sb = sa + A_BYTES;
+    const int ct = kt % ctiles, rs = kt / ctiles;
+    const int r = rs / a.S, s = rs % a.S;
+    const int dh = FWD ? r : -r, dw = FWD ? s : -s;
+    const int toff = (dh * a.Ws + dw) * a.Cs + ct * BK;
+#pragma unroll
+    for (int j = 0; j < AG; ++j) {
+      const int h = ah[j] + dh, w = aw[j] + dw;
+      const bool ok = (unsigned)h < (unsigned)a.Hs && (unsigned)w < (unsigned)a.Ws;
+      const int rr = (wid + W * j) * 8 + lrow;
+      const bf16_t* p = ok ? a.src + (abase[j] + toff)
+                           : g_cd_zero + (((lane & 7) ^ ((rr >> 1) & 7)) * 8);
+      __builtin_amdgcn_global_load_lds((const void*)p, (cd_lds_void_t*)(sa + (wid + W * j) * 1024),
+                                       16, 0, 0);
+    }
+#pragma unroll
+    for (int j = 0; j < BG; ++j)
+      __builtin_amdgcn_global_load_lds((const void*)(bptr[j] + kt * BK),
+                                       (cd_lds_void_t*)(sb + (wid + W * j) * 1024), 16, 0, 0);
+  };
+
+  f32x4_t acc[TM][TN];
+#pragma unroll
+  for (int i = 0; i < TM; ++i)
+#pragma unroll
+    for (int j = 0; j < TN; ++j) acc[i][j] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+
+  if (nk > 0) {
+#pragma unroll
+    for (int t = 0; t < STAGES - 1; ++t)
+      if (t < nk) issue(t, t);
+    for (int t = 0; t < nk; ++t) {
+      // retire tile t; leave the (STAGES-2) younger tiles in flight
+      if constexpr (STAGES == 3) {
+        if (t + 1 < nk) cd_vm_wait<D>();
+        else cd_vm_wait<0>();
+      } else {
+        cd_vm_wait<0>();
+      }
+      cd_barrier();
+      if (t + STAGES - 1 < nk) issue(t + STAGES - 1, (t + STAGES - 1) % STAGES);
+      const int st = t % STAGES;
+      const char* ta = smem + st * STAGE;
+      const char* tb = ta + A_BYTES;
+#pragma unroll
+      for (int kk = 0; kk < BK / 32; ++kk) {
+        s16x8_t fa[TM], fb[TN];
+#pragma unroll
+        for (int i = 0; i < TM; ++i) fa[i] = read_frag_k(ta, lane, wm * 64 + 16 * i, kk);
+#pragma unroll
+        for (int j = 0; j < TN; ++j) fb[j] = read_frag_k(tb, lane, wn * WCOLS + 16 * j, kk);
+        __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+        for (int i = 0; i < TM; ++i)
+#pragma unroll
+          for (int j = 0; j < TN; ++j)
+            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(
+                __builtin_bit_cast(bf16x8_t, fa[i]), __builtin_bit_cast(bf16x8_t, fb[j]), acc[i][j],
+                0, 0, 0);
+        __builtin_amdgcn_s_setprio(0);
+      }
+    }
+  }
+
+  // ---- epilogue: C/D map of 16x16x32: col = lane&15, row = (lane>>4)*4 + r
+  const bool add_bias = ep.bias != nullptr;
+#pragma unroll
+  for (int j = 0; j < TN; ++j) {
+    const int col = n0 + wn * WCOLS + 16 * j + (lane & 15);
+    if (col >= a.Ng) continue;
+    const float bv = add_bias ? bf2f(ep.bias[col]) : 0.f;
+#pragma unroll
+    for (int i = 0; i < TM; ++i) {
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int row = m0 + wm * 64 + 16 * i + 4 * (lane >> 4) + r;
+        if (row >= a.M) continue;
+        float v = acc[i][j][r] * ep.alpha + bv;
+        if (ep.relu) v = fmaxf(v, 0.f);
+        if (ep.mask && bf2f(ep.mask[(long)row * ep.ldm + col]) <= 0.f) v = 0.f;
+        const long off = (long)row * ep.ldc + col;
+        if (ep.c_f32) {
+          float* c = (float*)ep.c;
+          if (ep.mode == 1) c[off] += v;
+          else c[off] = v;
+        } else {
+          bf16_t* c = (bf16_t*)ep.c;
+          if (ep.mode == 1) v += bf2f(c[off]);
+          c[off] = f2bf(v);
+        }
+      }
+    }
+  }
+}
+
+// Host-side eligibility + launch. Returns false when the shape is not for
+// this core (caller falls back to the register-staged igemm).
+inline int conv_dma_pick_bn(int M, int Ng, int Kd, bool force) {
+  if (force) return Ng % 256 == 0 ? 256 : Ng % 128 == 0 ? 128 : Ng % 64 == 0 ? 64 : 0;
+  // measured (profiles/conv_bench_r1_*.json): BN=64 loses to the igemm (the
+  // 32 KiB A tile per 64 columns is L2-bound); BN>=128 wins even at ~0.6
+  // tiles per CU
+  const int tm = (M + 255) / 256;
+  if (Ng % 256 == 0 && (long)tm * (Ng / 256) >= 96) return 256;
+  if (Ng % 128 == 0 && (long)tm * (Ng / 128) >= 160) return 128;
+  if (Ng % 64 == 0 && Kd >= 1024 && (long)tm * (Ng / 64) >= 512) return 64;
+  return 0;
+}
+
+template <bool FWD>
+inline bool launch_conv_dma(const CDArgs& a, const Epi& ep, hipStream_t s, bool force = false) {
+  if (a.Cs % 64 != 0 || a.Kd % 64 != 0 || a.Kd < 64) return false;
+  if (!FWD && a.stride != 1) return false;
+  if ((long)a.Hs * a.Ws * a.Cs * ((a.M + a.P * a.Q - 1) / (a.P * a.Q)) >= (1L << 31)) return false;
+  if ((long)a.Ng * a.Kd >= (1L << 31)) return false;
+  const int bn = conv_dma_pick_bn(a.M, a.Ng, a.Kd, force);
+  if (!bn) return false;
+  const int tiles = ((a.M + 255) / 256) * (a.Ng / bn);
+  switch (bn) {
+    case 256:
+      hipLaunchKernelGGL((conv_dma_kernel<256, 2, FWD>), dim3(tiles), dim3(512), 0, s, a, ep);
+      break;
+    case 128:
+      hipLaunchKernelGGL((conv_dma_kernel<128, 2, FWD>), dim3(tiles), dim3(512), 0, s, a, ep);
+      break;
+    default:
+      hipLaunchKernelGGL((conv_dma_kernel<64, 1, FWD>), dim3(tiles), dim3(256), 0, s, a, ep);
+      break;
+  }
+  return true;
+}
+
+
+// ===========================================================================
+// LDS-DMA conv weight gradient (split over output pixels, fp32 atomics)
+//
+//   dW[k][(r,s,c)] = sum_m dY[m][k] * X[n, p*st-pad+r, q*st-pad+s, c],  m = (n,p,q)
+//
+// GEMM rows = k (BM), cols = (r,s,c) (BN), reduction = m in 64-pixel steps.
+// BN divides C, so a column tile is ONE tap (r,s) and BN channels: each
+// pixel row of the B tile is one contiguous BN*2-byte segment of X (or the
+// zero row for a padding tap / the pixel tail), each row of the A tile a
+// contiguous BM*2-byte segment of dY. Both images are [64 pixels][cols]
+// (pixel-major), kept as 64 x min(cols,128) sub-images with the MN-major
+// swizzle of igemm.h (applied on the DMA source chunk) and read with
+// ds_read_b64_tr_b16 (read_frag_mn). Each thread advances its rows' (n,p,q)
+// incrementally (no per-step division); the split's blocks accumulate into
+// the fp32 dW with no-return float atomics.
+// ===========================================================================
+struct WGArgs {
+  const bf16_t* dy;    // [Mred][K]
+  const bf16_t* x;     // NHWC [N][H][W][C]
+  float* dw;           // [K][R*S*C]
+  long ldc;            // R*S*C
+  int K, C, H, W, P, Q, S, stride, pad;
+  int Mred;            // N*P*Q
+  int steps_per_split; // 64-pixel steps per blockIdx.z
+  int dn, dp, dq;      // 64 pixels = dn images + dp rows + dq columns
+  int atomic;          // 1: atomic add, 0: plain += (single split)
+};
+
+template <int S>
+__device__ __forceinline__ int wg_swz16(int row) { return mnmaj_swz<S>(row) >> 1; }
+
+template <int BM, int BN, int WM, int WN>
+__global__ void __launch_bounds__(64 * WM * WN, 1) conv_wgrad_dma_kernel(WGArgs a) {
+  constexpr int W = WM * WN, BK = 64;
+  constexpr int SA = BM < 128 ? BM : 128, SB = BN < 128 ? BN : 128;   // sub-image widths
+  constexpr int A_BYTES = BK * BM * 2, B_BYTES = BK * BN * 2, STAGE = A_BYTES + B_BYTES;
+  constexpr int STAGES = 3 * STAGE <= 160 * 1024 ? 3 : 2;
+  constexpr int AI = BM / 8 / W, BI = BN / 8 / W;   // DMA instructions per thread per step
+  constexpr int D = AI + BI;
+  constexpr int TM = BM / WM / 16, TN = BN / WN / 16;
+  static_assert(AI >= 1 && BI >= 1 && BM % (8 * W) == 0 && BN % (8 * W) == 0, "tile/wave split");
+  __shared__ __attribute__((aligned(1024))) char smem[STAGES * STAGE];
+
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int wm = wid % WM, wn = wid / WM;
+  const int tiles_m = (a.K + BM - 1) / BM;
+  const int ncols = (int)a.ldc;
+  const int tiles_n = ncols / BN;
+  const int bid = xcd_remap(blockIdx.x, gridDim.x);
+  const int tm = bid % tiles_m, tn = bid / tiles_m;
+  const int k0 = tm * BM, col0 = tn * BN;
+  (void)tiles_n;
+  // this column tile's tap and channel offset
+  const int rs = col0 / a.C, c0 = col0 % a.C;
+  const int tr = rs / a.S, ts = rs % a.S;
+
+  const int step0 = blockIdx.z * a.steps_per_split;
+  const int nsteps_all = (a.Mred + BK - 1) / BK;
+  const int nk = min(a.steps_per_split, nsteps_all - step0);
+  const int mstart = step0 * BK;
+
+  // ---- A rows (dY): instruction g -> sub-image h, rows RPI*li + lane/(SA/8)
+  constexpr int LPR_A = SA / 8, RPI_A = 64 / LPR_A;
+  const bf16_t* aptr[AI];
+  int arow[AI];
+#pragma unroll
+  for (int j = 0; j < AI; ++j) {
+    const int g = wid + W * j;
+    const int h = g / (SA / 8), li = g % (SA / 8);
+    const int row = RPI_A * li + lane / LPR_A;
+    const int lc = (lane % LPR_A) ^ wg_swz16<SA>(row);
+    int k = k0 + h * SA + 8 * lc;
+    k = k < a.K ? k : a.K - 8;             // clamp: rows of dW past K are never stored
+    arow[j] = row;
+    aptr[j] = a.dy + (long)(mstart + row) * a.K + k;
+  }
+  // ---- B rows (X): per row the pixel (n,p,q) of m = mstart + row, advanced per step
+  constexpr int LPR_B = SB / 8, RPI_B = 64 / LPR_B;
+  int bn_[BI], bp_[BI], bq_[BI], bcol[BI], brow[BI];
+#pragma unroll
+  for (int j = 0; j < BI; ++j) {
+    const int g = wid + W * j;
+    const int h = g / (SB / 8), li = g % (SB / 8);
+    const int row = RPI_B * li + lane / LPR_B;
+    const int lc = (lane % LPR_B) ^ wg_swz16<SB>(row);
+    brow[j] = row;
+    bcol[j] = c0 + h * SB + 8 * lc;
+    const int m = mstart + row;
+    const int q = m % a.Q, t = m / a.Q;
+    bq_[j] = q; bp_[j] = t % a.P; bn_[j] = t / a.P;
+  }
+  const bf16_t* zero = g_cd_zero;
+
+  auto issue = [&](int step, int st) {
+    char* sa = smem + st * STAGE;
+    char* sb = sa + A_BYTES;
+    const int mb = mstart + step * BK;
+#pragma unroll
+    for (int j = 0; j < AI; ++j) {
+      const int g = wid + W * j;
+      const int h = g / (SA / 8), li = g % (SA / 8);
+      const bool ok = mb + arow[j] < a.Mred;
+      const bf16_t* p = ok ? aptr[j] + (long)step * BK * a.K : zero + 8 * (lane % LPR_A);
+      __builtin_amdgcn_global_load_lds((const void*)p,
+                                       (cd_lds_void_t*)(sa + h * (BK * SA * 2) + li * 1024), 16, 0, 0);
+    }
+#pragma unroll
+    for (int j = 0; j < BI; ++j) {
+      const int g = wid + W * j;
+      const int h = g / (SB / 8), li = g % (SB / 8);
+      const int hh = bp_[j] * a.stride - a.pad + tr, ww = bq_[j] * a.stride - a.pad + ts;
+      const bool ok = mb + brow[j] < a.Mred && (unsigned)hh < (unsigned)a.H &&
+                      (unsigned)ww < (unsigned)a.W;
+      const bf16_t* p = ok ? a.x + ((long)(bn_[j] * a.H + hh) * a.W + ww) * a.C + bcol[j]
+                           : zero + 8 * (lane % LPR_B);
+      __builtin_amdgcn_global_load_lds((const void*)p,
+                                       (cd_lds_void_t*)(sb + h * (BK * SB * 2) + li * 1024), 16, 0, 0);
+      // advance this row's pixel by 64
+      int q = bq_[j] + a.dq, pp = bp_[j] + a.dp, n = bn_[j] + a.dn;
+      if (q >= a.Q) { q -= a.Q; ++pp; }
+      if (pp >= a.P) { pp -= a.P; ++n; }
+      bq_[j] = q; bp_[j] = pp; bn_[j] = n;
+    }
+  };
+
+  f32x4_t acc[TM][TN];
+#pragma unroll
+  for (int i = 0; i < TM; ++i)
+#pragma unroll
+    for (int j = 0; j < TN; ++j) acc[i][j] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+
+  if (nk > 0) {
+#pragma unroll
+    for (int t = 0; t < STAGES - 1; ++t)
+      if (t < nk) issue(t, t);
+    for (int t = 0; t < nk; ++t) {
+      if constexpr (STAGES == 3) {
+        if (t + 1 < nk) cd_vm_wait<D>();
+        else cd_vm_wait<0>();
+      } else {
+        cd_vm_wait<0>();
+      }
+      cd_barrier();
+      if (t + STAGES - 1 < nk) issue(t + STAGES - 1, (t + STAGES - 1) % STAGES);
+      const char* ta = smem + (t % STAGES) * STAGE;
+      const char* tb = ta + A_BYTES;
+#pragma unroll
+      for (int kk = 0; kk < BK / 32; ++kk) {
+        s16x8_t fa[TM], fb[TN];
+#pragma unroll
+        for (int i = 0; i < TM; ++i) {
+          const int c = wm * (BM / WM) + 16 * i;
+          fa[i] = read_frag_mn<SA>(ta + (c / SA) * (BK * SA * 2), lane, 32 * kk, c % SA);
+        }
+#pragma unroll
+        for (int j = 0; j < TN; ++j) {
+          const int c = wn * (BN / WN) + 16 * j;
+          fb[j] = read_frag_mn<SB>(tb + (c / SB) * (BK * SB * 2), lane, 32 * kk, c % SB);
+        }
+        __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+        for (int i = 0; i < TM; ++i)
+#pragma unroll
+          for (int j = 0; j < TN; ++j)
+            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(
+                __builtin_bit_cast(bf16x8_t, fa[i]), __builtin_bit_cast(bf16x8_t, fb[j]), acc[i][j],
+                0, 0, 0);
+        __builtin_amdgcn_s_setprio(0);
+      }
+    }
+  }
+
+  // ---- epilogue: row = k, col = (r,s,c); fp32 accumulate into dW
+#pragma unroll
+  for (int j = 0; j < TN; ++j) {
+    const int col = col0 + wn * (BN / WN) + 16 * j + (lane & 15);
+#pragma unroll
+    for (int i = 0; i < TM; ++i) {
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int row = k0 + wm * (BM / WM) + 16 * i + 4 * (lane >> 4) + r;
+        if (row >= a.K) continue;
+        float* c = a.dw + (long)row * a.ldc + col;
+        if (a.atomic) atomicAdd(c, acc[i][j][r]);
+        else *c += acc[i][j][r];
+      }
+    }
+  }
+}
+
+// dw += conv wgrad (mode 1 semantics; mode 0 callers zero dw first)
+inline bool launch_conv_wgrad_dma(const bf16_t* dy, const bf16_t* x, float* dw, const ConvGeom& g,
+                                  int mode, hipStream_t s, bool force = false) {
+  if (g.dil != 1 || g.C % 64 != 0 || g.K % 64 != 0) return false;
+  const long Mred = (long)g.N * g.P * g.Q;
+  if (Mred >= (1L << 31) || (long)g.N * g.H * g.W * g.C >= (1L << 31)) return false;
+  const int ncols = g.R * g.S * g.C;
+  // tile: BN divides C (one tap per column tile); BM over K
+  int bm, bn;
+  if (g.K % 256 == 0 && g.C % 128 == 0) { bm = 256; bn = 128; }
+  else if (g.K % 128 == 0 && g.C % 128 == 0) { bm = 128; bn = 128; }
+  else { bm = 64; bn = 64; }
+  // the 64x64 form beats the igemm only on 1x1 layers (measured)
+  if (!force && bm == 64 && !(g.R == 1 && g.S == 1)) return false;
+  const int tiles = (g.K / bm) * (ncols / bn);
+  const int nsteps = (int)((Mred + 63) / 64);
+  // split the pixel reduction to ~one block per CU, not more: every split
+  // adds |dW| of fp32 atomics (~1.3 TB/s chip-wide), which at 2 blocks/CU
+  // already cost as much as the MFMA work on ResNet-sized layers
+  int splits = 256 / tiles;
+  if (splits > nsteps / 8) splits = nsteps / 8;
+  if (splits < 1) splits = 1;
+  int sps = (nsteps + splits - 1) / splits;
+  splits = (nsteps + sps - 1) / sps;
+  if (mode == 0) TAM_HIP_CHECK(hipMemsetAsync(dw, 0, (size_t)g.K * ncols * sizeof(float), s));
+  const int PQ = g.P * g.Q;
+  WGArgs a{dy, x, dw, ncols, g.K, g.C, g.H, g.W, g.P, g.Q, g.S, g.stride, g.pad, (int)Mred, sps,
+           64 / PQ, (64 % PQ) / g.Q, (64 % PQ) % g.Q, splits > 1 ? 1 : 0};
+  dim3 grid(tiles, 1, splits);
+  if (bm == 256)
+    hipLaunchKernelGGL((conv_wgrad_dma_kernel<256, 128, 4, 2>), grid, dim3(512), 0, s, a);
+  else if (bm == 128)
+    hipLaunchKernelGGL((conv_wgrad_dma_kernel<128, 128, 2, 2>), grid, dim3(256), 0, s, a);
+  else
+    hipLaunchKernelGGL((conv_wgrad_dma_kernel<64, 64, 2, 2>), grid, dim3(256), 0, s, a);
+  return true;
+}
+
+}  // namespace tam

@@ -24,5 +24,6 @@ void conv_dgrad(const bf16_t* dy, const bf16_t* w, const bf16_t* wt, const ConvG
 // dw[K][R*S*C] fp32, ep.mode 0 (overwrite) or 1 (accumulate)
 void conv_wgrad(const bf16_t* dy, const bf16_t* x, const ConvGeom& g, Epi ep, hipStream_t s);
 void conv_weight_t(const bf16_t* w, bf16_t* wt, const ConvGeom& g, hipStream_t s);
+void conv_dma_policy(int p);   // 1: LDS-DMA core where eligible (default), 0: igemm only
 
 }  // namespace tam

@@ -10,8 +10,15 @@
 // 1x1 / stride-1 / pad-0 convolutions go straight to the dense GEMM.
 #include "tam/launch.h"
 #include "tam/tiles.h"
+#include "tam/conv_dma.h"
 
 namespace tam {
+
+// 1 (default): fwd / stride-1 dgrad with C % 64 == 0 go to the LDS-DMA core
+// (conv_dma.h) when the grid fills the chip; 2: LDS-DMA core wherever the
+// shape is eligible (tests); 0: register-staged igemm only (A/B measurements)
+static int g_conv_dma = 1;
+void conv_dma_policy(int p) { g_conv_dma = p; }
 
 template <int BM, int BN>
 static void fwd_tile(const bf16_t* x, const bf16_t* w, const ConvGeom& g, const Epi& ep, int sp,
@@ -31,6 +38,10 @@ void conv_fwd(const bf16_t* x, const bf16_t* w, const ConvGeom& g, Epi ep, hipSt
   if (is_pointwise(g)) {
     gemm(x, g.C, true, w, g.C, true, M, g.K, g.C, ep, false, s);
     return;
+  }
+  if (g_conv_dma && g.dil == 1) {
+    CDArgs a{x, w, M, g.K, Kd, g.H, g.W, g.C, g.P, g.Q, g.S, g.stride, g.pad};
+    if (launch_conv_dma<true>(a, ep, s, g_conv_dma == 2)) return;
   }
   TileChoice t = choose_tiles(M, g.K, Kd, false);
   switch (t.cfg) {
@@ -58,6 +69,11 @@ void conv_dgrad(const bf16_t* dy, const bf16_t* w, const bf16_t* wt, const ConvG
     gemm(dy, g.K, true, w, g.C, false, M, g.C, g.K, ep, false, s);
     return;
   }
+  if (g_conv_dma && g.dil == 1 && g.stride == 1) {
+    // rows = dX pixels over an H x W grid, gathered from dY (P x Q x K), B = Wt [C][R][S][K]
+    CDArgs a{dy, wt, M, g.C, Kd, g.P, g.Q, g.K, g.H, g.W, g.S, 1, g.pad};
+    if (launch_conv_dma<false>(a, ep, s, g_conv_dma == 2)) return;
+  }
   TileChoice t = choose_tiles(M, g.C, Kd, false);
   switch (t.cfg) {
     case 0: dgrad_tile<128, 128>(dy, wt, g, ep, s); break;
@@ -78,6 +94,9 @@ static void wgrad_tile(const bf16_t* dy, const bf16_t* x, const ConvGeom& g, con
 
 void conv_wgrad(const bf16_t* dy, const bf16_t* x, const ConvGeom& g, Epi ep, hipStream_t s) {
   const int Mred = g.N * g.P * g.Q, Nc = g.R * g.S * g.C;
+  if (g_conv_dma && ep.c_f32 && ep.ldc == Nc && ep.mode <= 1 &&
+      launch_conv_wgrad_dma(dy, x, (float*)ep.c, g, ep.mode, s, g_conv_dma == 2))
+    return;
   if (is_pointwise(g)) {
     // dW[k][c] = sum_m dY[m][k] X[m][c]: A(k', m) = dY[m*K + k'], B(m, c) = X[m*C + c]
     gemm(dy, g.K, false, x, g.C, false, g.K, g.C, Mred, ep, true, s);

@@ -182,6 +182,46 @@ def test_conv_fwd_dgrad_wgrad(gpu, cfg):
     assert rel_err(dw, gw.permute(0, 2, 3, 1)) < 1e-4
 
 
+# LDS-DMA conv core (conv_dma.h): every tile width, stride-2 fwd, 1x1 s2, M
+# tails, padding taps, bias+relu epilogue and the relu-masked dgrad
+@pytest.mark.parametrize("cfg", [(2, 12, 12, 64, 64, 3, 1, 1), (3, 9, 11, 128, 128, 3, 1, 1),
+                                 (2, 10, 10, 64, 256, 3, 1, 1), (2, 14, 14, 128, 64, 3, 2, 1),
+                                 (2, 13, 13, 64, 128, 1, 2, 0), (1, 9, 9, 192, 128, 3, 1, 1),
+                                 (4, 16, 16, 128, 256, 3, 1, 1), (2, 7, 7, 256, 128, 1, 1, 0),
+                                 (40, 7, 7, 128, 128, 3, 1, 1)])
+def test_conv_dma_core(gpu, cfg):
+    N, H, W, C, K, R, st, pd = cfg
+    torch.manual_seed(7)
+    T().conv_dma_policy(2)
+    try:
+        x = torch.randn(N, H, W, C, device=gpu).to(BF)
+        w = (torch.randn(K, R, R, C, device=gpu) / math.sqrt(R * R * C)).to(BF)
+        b = torch.randn(K, device=gpu).to(BF)
+        P = (H + 2 * pd - R) // st + 1
+        Q = (W + 2 * pd - R) // st + 1
+        y = torch.empty(N, P, Q, K, device=gpu, dtype=BF)
+        T().conv_fwd(x, w, y, st, pd, 1, b, True)
+        ref = (_ref_conv(x, w, st, pd) + b.float()).clamp_min(0)
+        assert rel_err(y, ref) < 1e-2
+        dy = torch.randn(N, P, Q, K, device=gpu).to(BF)
+        dx = torch.empty_like(x)
+        T().conv_dgrad(dy, w, torch.empty_like(w), dx, st, pd, 1, x)
+        xf = x.float().permute(0, 3, 1, 2).requires_grad_(True)
+        g, = torch.autograd.grad(F.conv2d(xf, w.float().permute(0, 3, 1, 2), stride=st, padding=pd),
+                                 [xf], dy.float().permute(0, 3, 1, 2))
+        assert rel_err(dx, g.permute(0, 2, 3, 1) * (x.float() > 0)) < 1e-2
+        wf = w.float().permute(0, 3, 1, 2).requires_grad_(True)
+        gw, = torch.autograd.grad(F.conv2d(x.float().permute(0, 3, 1, 2), wf, stride=st, padding=pd),
+                                  [wf], dy.float().permute(0, 3, 1, 2))
+        for mode in (0, 1):
+            dw = torch.full((K, R, R, C), 0.5, device=gpu)
+            T().conv_wgrad(dy, x, dw, st, pd, 1, mode)
+            ref = gw.permute(0, 2, 3, 1) + (0.5 if mode == 1 else 0.0)
+            assert rel_err(dw, ref) < 1e-4, (mode, rel_err(dw, ref))
+    finally:
+        T().conv_dma_policy(1)
+
+
 def test_conv_bias_relu_mask(gpu):
     torch.manual_seed(4)
     x = torch.randn(2, 8, 8, 16, device=gpu).to(BF)

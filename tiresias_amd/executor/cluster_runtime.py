@@ -329,8 +329,11 @@ class Worker:
         for a in plan["actions"]:
             op = a["op"]
             if op == "group":
-                pg = dist.new_group(list(a["ranks"]), backend=self.gang_backend)
-                self.groups[tuple(a["ranks"])] = pg
+                # communicators outlive a replay: every rank holds the same
+                # cache (same plans, same order), so skipping is collective-safe
+                if tuple(a["ranks"]) not in self.groups:
+                    pg = dist.new_group(list(a["ranks"]), backend=self.gang_backend)
+                    self.groups[tuple(a["ranks"])] = pg
             elif op == "drop":
                 t = self.trainers.pop(a["job"], None)
                 if t is not None:

@@ -65,9 +65,16 @@ RESNET_CONVS = [  # N,H,C,K,R,stride,pad   (batch 64)
 ]
 
 
-def conv_cases(T, dev):
+VGG_CONVS = [  # batch 32, every distinct VGG-16 conv (first layer: RGB padded to 8 channels)
+    (32, 224, 8, 64, 3, 1, 1), (32, 224, 64, 64, 3, 1, 1), (32, 112, 64, 128, 3, 1, 1),
+    (32, 112, 128, 128, 3, 1, 1), (32, 56, 128, 256, 3, 1, 1), (32, 56, 256, 256, 3, 1, 1),
+    (32, 28, 256, 512, 3, 1, 1), (32, 28, 512, 512, 3, 1, 1), (32, 14, 512, 512, 3, 1, 1),
+]
+
+
+def conv_cases(T, dev, shapes=RESNET_CONVS):
     out = []
-    for (N, H, C, K, R, st, pd) in RESNET_CONVS:
+    for (N, H, C, K, R, st, pd) in shapes:
         x = torch.randn(N, H, H, C, device=dev).to(BF)
         w = (torch.randn(K, R, R, C, device=dev) * 0.05).to(BF)
         P = (H + 2 * pd - R) // st + 1
@@ -124,15 +131,18 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--out", default=None)
     ap.add_argument("--only", default="gemm,conv,attn")
+    ap.add_argument("--conv-dma", type=int, default=1, help="conv_dma_policy (0: igemm only)")
     a = ap.parse_args()
     _lib.load(required=True)
     T = torch.ops.tam
     T.gemm_lib_policy(0)   # measure the MFMA kernels themselves
+    T.conv_dma_policy(a.conv_dma)
     dev = torch.device("cuda", 0)
     torch.manual_seed(0)
     res = []
     for kind in a.only.split(","):
-        fn = {"gemm": gemm_cases, "conv": conv_cases, "attn": attn_cases}[kind]
+        fn = {"gemm": gemm_cases, "conv": conv_cases, "attn": attn_cases,
+              "vggconv": lambda T, d: conv_cases(T, d, VGG_CONVS)}[kind]
         for r in fn(T, dev):
             print(json.dumps(r), flush=True)
             res.append(r)
