@@ -242,12 +242,11 @@ void conv_dgrad_op(const Tensor& dy, const Tensor& w, const Tensor& wt, const Te
   check_bf16(dy, "dy"); check_bf16(w, "w"); check_bf16(dx, "dx");
   check_contig(dy, "dy"); check_contig(w, "w"); check_contig(dx, "dx");
   tam::ConvGeom g = geom(dx, w, dy, stride, pad, dil);
-  const bool pointwise = g.R == 1 && g.S == 1 && g.stride == 1 && g.pad == 0;
-  if (!pointwise) {
-    check_bf16(wt, "wt");
-    TORCH_CHECK(wt.numel() == w.numel(), "tam.conv_dgrad: wt workspace size");
-    tam::conv_weight_t(bp(w), bpm(wt), g, cur_stream(dy));
-  }
+  // wt = W re-laid [C][R][S][K] (the K-major B operand of dgrad; for 1x1
+  // convs the LDS-DMA core reads it, the plain-GEMM fallback does not)
+  check_bf16(wt, "wt");
+  TORCH_CHECK(wt.numel() == w.numel(), "tam.conv_dgrad: wt workspace size");
+  tam::conv_weight_t(bp(w), bpm(wt), g, cur_stream(dy));
   tam::Epi ep;
   ep.c = dx.data_ptr(); ep.ldc = g.C; ep.c_f32 = 0; ep.mode = 0;
   if (mask.has_value() && mask->defined()) {
@@ -255,7 +254,7 @@ void conv_dgrad_op(const Tensor& dy, const Tensor& w, const Tensor& wt, const Te
     TORCH_CHECK(mask->numel() == dx.numel(), "tam.conv_dgrad: mask size");
     ep.mask = bp(*mask); ep.ldm = g.C;
   }
-  tam::conv_dgrad(bp(dy), bp(w), pointwise ? nullptr : bp(wt), g, ep, cur_stream(dy));
+  tam::conv_dgrad(bp(dy), bp(w), bp(wt), g, ep, cur_stream(dy));
 }
 
 void conv_wgrad_op(const Tensor& dy, const Tensor& x, const Tensor& dw, int64_t stride, int64_t pad,

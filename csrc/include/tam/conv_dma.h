@@ -180,8 +180,74 @@ __global__ void __launch_bounds__(256 * WN, 1) conv_dma_kernel(CDArgs a, Epi ep)
     }
   }
 
-  // ---- epilogue: C/D map of 16x16x32: col = lane&15, row = (lane>>4)*4 + r
   const bool add_bias = ep.bias != nullptr;
+  if (!ep.c_f32) {
+    // ---- LDS-staged bf16 epilogue: each wave parks 32 rows of its tile in a
+    // private padded LDS slab (the stage buffers are free after the barrier),
+    // then writes whole 16-B row chunks (and reads the relu mask / the
+    // accumulate operand in the same 16-B units) instead of 2-B scattered
+    // stores from the MFMA C layout.
+    constexpr int LDW = WCOLS + 8;                 // padded slab row (bf16)
+    constexpr int CPR = WCOLS / 8, NCH = 32 * CPR / 64;
+    bf16_t* slab = (bf16_t*)(smem + wid * (32 * LDW * 2));
+    float bv[TN];
+#pragma unroll
+    for (int j = 0; j < TN; ++j)
+      bv[j] = add_bias ? bf2f(ep.bias[n0 + wn * WCOLS + 16 * j + (lane & 15)]) : 0.f;
+    cd_barrier();                                  // every wave is done with the stages
+    const int cbase = n0 + wn * WCOLS;
+#pragma unroll
+    for (int half = 0; half < 2; ++half) {
+#pragma unroll
+      for (int ii = 0; ii < 2; ++ii) {
+        const int i = 2 * half + ii;
+#pragma unroll
+        for (int j = 0; j < TN; ++j)
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            float v = acc[i][j][r] * ep.alpha + bv[j];
+            if (ep.relu) v = fmaxf(v, 0.f);
+            slab[(16 * ii + 4 * (lane >> 4) + r) * LDW + 16 * j + (lane & 15)] = f2bf(v);
+          }
+      }
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+#pragma unroll
+      for (int u = 0; u < NCH; ++u) {
+        const int idx = u * 64 + lane, lr = idx / CPR, ch = idx % CPR;
+        const int row = m0 + wm * 64 + half * 32 + lr;
+        if (row < a.M) {
+          uint4 v = *(const uint4*)(slab + lr * LDW + ch * 8);
+          if (ep.mask) {
+            const uint4 mk = *(const uint4*)(ep.mask + (long)row * ep.ldm + cbase + ch * 8);
+            const uint32_t* mw = (const uint32_t*)&mk;
+            uint32_t* vw = (uint32_t*)&v;
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+              const uint32_t m2 = mw[e];
+              const bool lo = (m2 & 0x8000u) == 0 && (m2 & 0x7fffu) != 0;
+              const bool hi = (m2 & 0x80000000u) == 0 && (m2 & 0x7fff0000u) != 0;
+              vw[e] &= (lo ? 0x0000ffffu : 0u) | (hi ? 0xffff0000u : 0u);
+            }
+          }
+          bf16_t* dst = (bf16_t*)ep.c + (long)row * ep.ldc + cbase + ch * 8;
+          if (ep.mode == 1) {
+            const uint4 o = *(const uint4*)dst;
+            const uint32_t* ow = (const uint32_t*)&o;
+            uint32_t* vw = (uint32_t*)&v;
+#pragma unroll
+            for (int e = 0; e < 4; ++e)
+              vw[e] = pack_bf2(bf2f((bf16_t)(vw[e] & 0xffff)) + bf2f((bf16_t)(ow[e] & 0xffff)),
+                               bf2f((bf16_t)(vw[e] >> 16)) + bf2f((bf16_t)(ow[e] >> 16)));
+          }
+          *(uint4*)dst = v;
+        }
+      }
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    }
+    return;
+  }
+
+  // ---- fp32 output: C/D map of 16x16x32: col = lane&15, row = (lane>>4)*4 + r
 #pragma unroll
   for (int j = 0; j < TN; ++j) {
     const int col = n0 + wn * WCOLS + 16 * j + (lane & 15);
@@ -196,16 +262,9 @@ __global__ void __launch_bounds__(256 * WN, 1) conv_dma_kernel(CDArgs a, Epi ep)
         float v = acc[i][j][r] * ep.alpha + bv;
         if (ep.relu) v = fmaxf(v, 0.f);
         if (ep.mask && bf2f(ep.mask[(long)row * ep.ldm + col]) <= 0.f) v = 0.f;
-        const long off = (long)row * ep.ldc + col;
-        if (ep.c_f32) {
-          float* c = (float*)ep.c;
-          if (ep.mode == 1) c[off] += v;
-          else c[off] = v;
-        } else {
-          bf16_t* c = (bf16_t*)ep.c;
-          if (ep.mode == 1) v += bf2f(c[off]);
-          c[off] = f2bf(v);
-        }
+        float* c = (float*)ep.c + (long)row * ep.ldc + col;
+        if (ep.mode == 1) *c += v;
+        else *c = v;
       }
     }
   }
@@ -227,7 +286,9 @@ inline int conv_dma_pick_bn(int M, int Ng, int Kd, bool force) {
 
 template <bool FWD>
 inline bool launch_conv_dma(const CDArgs& a, const Epi& ep, hipStream_t s, bool force = false) {
-  if (a.Cs % 64 != 0 || a.Kd % 64 != 0 || a.Kd < 64) return false;
+  // Kd >= 256: with fewer than 4 K-tiles the ring never fills (1x1 convs over
+  // 64/128 channels measured slower than the igemm)
+  if (a.Cs % 64 != 0 || a.Kd % 64 != 0 || a.Kd < 256) return false;
   if (!FWD && a.stride != 1) return false;
   if ((long)a.Hs * a.Ws * a.Cs * ((a.M + a.P * a.Q - 1) / (a.P * a.Q)) >= (1L << 31)) return false;
   if ((long)a.Ng * a.Kd >= (1L << 31)) return false;

@@ -346,8 +346,82 @@ igemm_kernel(LA la, LB lb, int M, int N, int K, int ktiles_per_split, Epi ep) {
     }
   }
 
-  // ---- epilogue: C/D map of 16x16x32: col = lane&15, row = (lane>>4)*4 + r
   const bool add_bias = ep.bias != nullptr && blockIdx.z == 0;
+  // ---- bf16 output: LDS-staged epilogue (whole 16-B row chunks instead of
+  // 2-B stores in the MFMA C layout); needs 16-B aligned output rows
+  if (!ep.c_f32 && (ep.ldc & 7) == 0 && (((uintptr_t)ep.c) & 15) == 0 &&
+      (!ep.mask || ((ep.ldm & 7) == 0 && (((uintptr_t)ep.mask) & 15) == 0))) {
+    constexpr int WC = BN / 2, LDW = WC + 8, CPR = WC / 8, NCH = 32 * CPR / 64;
+    bf16_t* slab = (bf16_t*)(smem + wid * (32 * LDW * 2));
+    if (kt0 >= kt1) __syncthreads();   // (the K loop ends with a barrier otherwise)
+    const int cbase = n0 + wc * WC;
+    float bv[TN];
+#pragma unroll
+    for (int j = 0; j < TN; ++j) {
+      const int col = cbase + 16 * j + (lane & 15);
+      bv[j] = (add_bias && col < N) ? bf2f(ep.bias[col]) : 0.f;
+    }
+#pragma unroll
+    for (int h = 0; h < TM / 2; ++h) {
+#pragma unroll
+      for (int ii = 0; ii < 2; ++ii) {
+        const int i = 2 * h + ii;
+#pragma unroll
+        for (int j = 0; j < TN; ++j)
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            float v = acc[i][j][r] * ep.alpha + bv[j];
+            if (ep.relu) v = fmaxf(v, 0.f);
+            slab[(16 * ii + 4 * (lane >> 4) + r) * LDW + 16 * j + (lane & 15)] = f2bf(v);
+          }
+      }
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+#pragma unroll
+      for (int u = 0; u < NCH; ++u) {
+        const int idx = u * 64 + lane, lr = idx / CPR, ch = idx % CPR;
+        const int row = m0 + wr * (BM / 2) + 32 * h + lr;
+        const int col = cbase + ch * 8;
+        if (row >= M || col >= N) continue;
+        bf16_t* dst = (bf16_t*)ep.c + (long)row * ep.ldc + col;
+        const bf16_t* src = slab + lr * LDW + ch * 8;
+        if (col + 8 <= N) {
+          uint4 v = *(const uint4*)src;
+          uint32_t* vw = (uint32_t*)&v;
+          if (ep.mask) {
+            const uint4 mk = *(const uint4*)(ep.mask + (long)row * ep.ldm + col);
+            const uint32_t* mw = (const uint32_t*)&mk;
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+              const uint32_t m2 = mw[e];
+              const bool lo = (m2 & 0x8000u) == 0 && (m2 & 0x7fffu) != 0;
+              const bool hi = (m2 & 0x80000000u) == 0 && (m2 & 0x7fff0000u) != 0;
+              vw[e] &= (lo ? 0x0000ffffu : 0u) | (hi ? 0xffff0000u : 0u);
+            }
+          }
+          if (ep.mode == 1) {
+            const uint4 o = *(const uint4*)dst;
+            const uint32_t* ow = (const uint32_t*)&o;
+#pragma unroll
+            for (int e = 0; e < 4; ++e)
+              vw[e] = pack_bf2(bf2f((bf16_t)(vw[e] & 0xffff)) + bf2f((bf16_t)(ow[e] & 0xffff)),
+                               bf2f((bf16_t)(vw[e] >> 16)) + bf2f((bf16_t)(ow[e] >> 16)));
+          }
+          *(uint4*)dst = v;
+        } else {
+          for (int e = 0; e < 8 && col + e < N; ++e) {
+            float v = bf2f(src[e]);
+            if (ep.mask && bf2f(ep.mask[(long)row * ep.ldm + col + e]) <= 0.f) v = 0.f;
+            if (ep.mode == 1) v += bf2f(dst[e]);
+            dst[e] = f2bf(v);
+          }
+        }
+      }
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    }
+    return;
+  }
+
+  // ---- epilogue: C/D map of 16x16x32: col = lane&15, row = (lane>>4)*4 + r
 #pragma unroll
   for (int j = 0; j < TN; ++j) {
     const int col = n0 + wc * (BN / 2) + 16 * j + (lane & 15);

@@ -26,7 +26,7 @@ inline TileChoice choose_tiles(int M, int N, int K, bool can_split) {
     if (tiles < 512 && ktiles >= 8) {
       int sp = (int)((512 + tiles - 1) / tiles);
       sp = sp < ktiles / 4 ? sp : ktiles / 4;
-      if (sp > 64) sp = 64;
+      if (sp > 256) sp = 256;   // tiny-output reductions (first-layer wgrad: 64x72) need many
       t.splits = sp < 1 ? 1 : sp;
     }
   }

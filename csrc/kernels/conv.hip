@@ -35,13 +35,13 @@ static bool is_pointwise(const ConvGeom& g) {
 
 void conv_fwd(const bf16_t* x, const bf16_t* w, const ConvGeom& g, Epi ep, hipStream_t s) {
   const int M = g.N * g.P * g.Q, Kd = g.R * g.S * g.C;
-  if (is_pointwise(g)) {
-    gemm(x, g.C, true, w, g.C, true, M, g.K, g.C, ep, false, s);
-    return;
-  }
   if (g_conv_dma && g.dil == 1) {
     CDArgs a{x, w, M, g.K, Kd, g.H, g.W, g.C, g.P, g.Q, g.S, g.stride, g.pad};
     if (launch_conv_dma<true>(a, ep, s, g_conv_dma == 2)) return;
+  }
+  if (is_pointwise(g)) {
+    gemm(x, g.C, true, w, g.C, true, M, g.K, g.C, ep, false, s);
+    return;
   }
   TileChoice t = choose_tiles(M, g.K, Kd, false);
   switch (t.cfg) {
@@ -64,15 +64,15 @@ static void dgrad_tile(const bf16_t* dy, const bf16_t* wt, const ConvGeom& g, co
 void conv_dgrad(const bf16_t* dy, const bf16_t* w, const bf16_t* wt, const ConvGeom& g, Epi ep,
                 hipStream_t s) {
   const int M = g.N * g.H * g.W, Kd = g.R * g.S * g.K;
+  if (wt && g_conv_dma && g.dil == 1 && g.stride == 1) {
+    // rows = dX pixels over an H x W grid, gathered from dY (P x Q x K), B = Wt [C][R][S][K]
+    CDArgs a{dy, wt, M, g.C, Kd, g.P, g.Q, g.K, g.H, g.W, g.S, 1, g.pad};
+    if (launch_conv_dma<false>(a, ep, s, g_conv_dma == 2)) return;
+  }
   if (is_pointwise(g)) {
     // dX[m][c] = sum_k dY[m][k] W[k][c]  -> B(k,n) = W[k*C + c], MN-major
     gemm(dy, g.K, true, w, g.C, false, M, g.C, g.K, ep, false, s);
     return;
-  }
-  if (g_conv_dma && g.dil == 1 && g.stride == 1) {
-    // rows = dX pixels over an H x W grid, gathered from dY (P x Q x K), B = Wt [C][R][S][K]
-    CDArgs a{dy, wt, M, g.C, Kd, g.P, g.Q, g.K, g.H, g.W, g.S, 1, g.pad};
-    if (launch_conv_dma<false>(a, ep, s, g_conv_dma == 2)) return;
   }
   TileChoice t = choose_tiles(M, g.C, Kd, false);
   switch (t.cfg) {
