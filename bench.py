@@ -108,7 +108,7 @@ def main():
     ap.add_argument("--baseline-placement", default="yarn")
     ap.add_argument("--no-baseline", action="store_true")
     ap.add_argument("--jobs-per-gpu", type=int, default=16)
-    ap.add_argument("--quantum", type=float, default=0.25)
+    ap.add_argument("--quantum", type=float, default=0.1)
     ap.add_argument("--seed", type=int, default=2019)
     ap.add_argument("--cpu", action="store_true", help="gloo/CPU rehearsal with tiny models")
     ap.add_argument("--no-graph", action="store_true",

@@ -86,7 +86,22 @@ __global__ void __launch_bounds__(256) bn_stats_kernel(const bf16_t* __restrict_
   const long r0 = blockIdx.x * rows_per_block;
   const long r1 = min(M, r0 + rows_per_block);
   if (rl < rpb) {
-    for (long r = r0 + rl; r < r1; r += rpb) {
+    long r = r0 + rl;
+    // 4 independent 16-B loads in flight per thread (latency, not bandwidth,
+    // bounds a one-load-per-iteration loop)
+    for (; r + 3 * rpb < r1; r += 4 * rpb) {
+      uint4 v[4];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) v[u] = *(const uint4*)(x + (r + u * rpb) * C + cg * 8);
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        float f[8];
+        unpack8(v[u], f);
+#pragma unroll
+        for (int i = 0; i < 8; ++i) { s[i] += f[i]; q[i] += f[i] * f[i]; }
+      }
+    }
+    for (; r < r1; r += rpb) {
       float f[8];
       unpack8(*(const uint4*)(x + r * C + cg * 8), f);
 #pragma unroll
@@ -107,6 +122,73 @@ __global__ void __launch_bounds__(256) bn_stats_kernel(const bf16_t* __restrict_
     float* pq = ps + C;
 #pragma unroll
     for (int i = 0; i < 8; ++i) { ps[i] = s[i]; pq[i] = q[i]; }
+  }
+}
+
+// Column reduce of the [nblk][2C] partial rows (fp64) fused with the
+// per-channel finalize: BWD=0 -> mean/rstd, scale/shift, running stats;
+// BWD=1 -> dgamma/dbeta and the k1/k2/k3 coefficients of the apply pass.
+// One launch instead of col_reduce + finalize (each ~5 us of a tiny grid).
+template <int BWD>
+__global__ void __launch_bounds__(256) bn_reduce_finalize_kernel(
+    const float* __restrict__ part, int nblk, long M, int C, float eps, float momentum,
+    const float* __restrict__ gamma, const float* __restrict__ beta_or_rstd,
+    float* __restrict__ o0, float* __restrict__ o1, float* __restrict__ o2,
+    float* __restrict__ o3, float* __restrict__ o4, float* __restrict__ o5) {
+  __shared__ double red[2][16][17];
+  const int cx = threadIdx.x & 15, ly = threadIdx.x >> 4;
+  const int c = blockIdx.x * 16 + cx;
+  const int W = 2 * C;
+  double s = 0.0, q = 0.0;
+  if (c < C) {
+    int b = ly;
+    for (; b + 3 * 16 < nblk; b += 4 * 16) {
+      float v[4], w[4];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        v[u] = part[(long)(b + u * 16) * W + c];
+        w[u] = part[(long)(b + u * 16) * W + C + c];
+      }
+#pragma unroll
+      for (int u = 0; u < 4; ++u) { s += (double)v[u]; q += (double)w[u]; }
+    }
+    for (; b < nblk; b += 16) {
+      s += (double)part[(long)b * W + c];
+      q += (double)part[(long)b * W + C + c];
+    }
+  }
+  red[0][ly][cx] = s;
+  red[1][ly][cx] = q;
+  __syncthreads();
+  if (ly != 0 || c >= C) return;
+  double S = 0.0, Q = 0.0;
+#pragma unroll
+  for (int k = 0; k < 16; ++k) { S += red[0][k][cx]; Q += red[1][k][cx]; }
+  if (BWD == 0) {
+    // o0 mean, o1 rstd, o2 scale, o3 shift, o4 run_mean, o5 run_var
+    const double mean = S / (double)M;
+    double var = Q / (double)M - mean * mean;
+    if (var < 0) var = 0;
+    const float rstd = (float)(1.0 / sqrt(var + (double)eps));
+    o0[c] = (float)mean;
+    o1[c] = rstd;
+    const float sc = gamma[c] * rstd;
+    o2[c] = sc;
+    o3[c] = beta_or_rstd[c] - (float)mean * sc;
+    if (o4) {
+      const double unb = M > 1 ? var * (double)M / (double)(M - 1) : var;
+      o4[c] = (1.f - momentum) * o4[c] + momentum * (float)mean;
+      o5[c] = (1.f - momentum) * o5[c] + momentum * (float)unb;
+    }
+  } else {
+    // o0 dgamma, o1 dbeta (accumulate), o2 k1, o3 k2, o4 k3
+    const float a = (float)S, bb = (float)Q;
+    if (o0) o0[c] += bb;
+    if (o1) o1[c] += a;
+    const float gr = gamma[c] * beta_or_rstd[c];
+    o2[c] = gr;
+    o3[c] = -gr * bb / (float)M;
+    o4[c] = -gr * a / (float)M;
   }
 }
 
@@ -143,8 +225,35 @@ __global__ void __launch_bounds__(256) bn_apply_kernel(const bf16_t* __restrict_
                                                         bf16_t* __restrict__ y, long total8, int C,
                                                         int relu) {
   const int cg8 = C / 8;
-  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < total8;
-       i += (long)gridDim.x * blockDim.x) {
+  const long stride = (long)gridDim.x * blockDim.x;
+  long i = blockIdx.x * (long)blockDim.x + threadIdx.x;
+  // two vectors per thread per iteration: loads of both issued before use
+  for (; i + stride < total8; i += 2 * stride) {
+    const uint4 xa = ((const uint4*)x)[i], xb = ((const uint4*)x)[i + stride];
+    uint4 ra = make_uint4(0, 0, 0, 0), rb = ra;
+    if (res) { ra = ((const uint4*)res)[i]; rb = ((const uint4*)res)[i + stride]; }
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      const long ii = h ? i + stride : i;
+      const int c0 = (int)(ii % cg8) * 8;
+      float f[8], rr[8];
+      unpack8(h ? xb : xa, f);
+      if (res) unpack8(h ? rb : ra, rr);
+      const float4 sa = *(const float4*)(scale + c0), sb = *(const float4*)(scale + c0 + 4);
+      const float4 ha = *(const float4*)(shift + c0), hb = *(const float4*)(shift + c0 + 4);
+      const float sc[8] = {sa.x, sa.y, sa.z, sa.w, sb.x, sb.y, sb.z, sb.w};
+      const float sh[8] = {ha.x, ha.y, ha.z, ha.w, hb.x, hb.y, hb.z, hb.w};
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        float v = f[j] * sc[j] + sh[j];
+        if (res) v += rr[j];
+        if (relu) v = fmaxf(v, 0.f);
+        f[j] = v;
+      }
+      ((uint4*)y)[ii] = pack8(f);
+    }
+  }
+  for (; i < total8; i += stride) {
     const int c0 = (int)(i % cg8) * 8;
     float f[8];
     unpack8(((const uint4*)x)[i], f);
@@ -234,8 +343,37 @@ __global__ void __launch_bounds__(256) bn_bwd_apply_kernel(
     const float* __restrict__ k2, const float* __restrict__ k3, bf16_t* __restrict__ dx,
     bf16_t* __restrict__ dres, long total8, int C, int relu) {
   const int cg8 = C / 8;
-  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < total8;
-       i += (long)gridDim.x * blockDim.x) {
+  const long stride = (long)gridDim.x * blockDim.x;
+  long i = blockIdx.x * (long)blockDim.x + threadIdx.x;
+  for (; i + stride < total8; i += 2 * stride) {
+    const uint4 da = ((const uint4*)dy)[i], db = ((const uint4*)dy)[i + stride];
+    const uint4 xa = ((const uint4*)x)[i], xb = ((const uint4*)x)[i + stride];
+    uint4 ya = make_uint4(0, 0, 0, 0), yb = ya;
+    if (relu) { ya = ((const uint4*)y)[i]; yb = ((const uint4*)y)[i + stride]; }
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      const long ii = h ? i + stride : i;
+      const int c0 = (int)(ii % cg8) * 8;
+      float fd[8], fx[8], fy[8];
+      unpack8(h ? db : da, fd);
+      unpack8(h ? xb : xa, fx);
+      if (relu) {
+        unpack8(h ? yb : ya, fy);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) fd[j] = fy[j] <= 0.f ? 0.f : fd[j];
+      }
+      if (dres) ((uint4*)dres)[ii] = pack8(fd);
+      float o[8];
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const int c = c0 + j;
+        const float xh = (fx[j] - mean[c]) * rstd[c];
+        o[j] = k1[c] * fd[j] + k2[c] * xh + k3[c];
+      }
+      ((uint4*)dx)[ii] = pack8(o);
+    }
+  }
+  for (; i < total8; i += stride) {
     const int c0 = (int)(i % cg8) * 8;
     float fd[8], fx[8], fy[8];
     unpack8(((const uint4*)dy)[i], fd);
@@ -282,10 +420,11 @@ void bn_forward(const bf16_t* x, const bf16_t* res, bf16_t* y, long M, int C, fl
   const int nb = (int)((M + rpb - 1) / rpb);
   double* sums = (double*)(ws_f + 2 * C);
   float* part = ws_f + 6 * C;
+  (void)sums;
   hipLaunchKernelGGL(bn_stats_kernel, dim3(nb), dim3(256), 0, s, x, M, C, rpb, part);
-  col_reduce_f64(part, nb, 2 * C, sums, s);
-  hipLaunchKernelGGL(bn_finalize_kernel, dim3((C + 255) / 256), dim3(256), 0, s, sums, M, C, eps,
-                     momentum, gamma, beta, save_mean, save_rstd, ws_f, ws_f + C, run_mean, run_var);
+  hipLaunchKernelGGL(bn_reduce_finalize_kernel<0>, dim3((C + 15) / 16), dim3(256), 0, s, part, nb, M,
+                     C, eps, momentum, gamma, beta, save_mean, save_rstd, ws_f, ws_f + C, run_mean,
+                     run_var);
   const long total8 = M * C / 8;
   hipLaunchKernelGGL(bn_apply_kernel, dim3(grid_for(total8)), dim3(256), 0, s, x, res, ws_f,
                      ws_f + C, y, total8, C, relu);
@@ -308,9 +447,10 @@ void bn_backward(const bf16_t* dy, const bf16_t* y, const bf16_t* x, const float
   float* part = ws_f + 8 * C;
   hipLaunchKernelGGL(bn_bwd_reduce_kernel, dim3(nb), dim3(256), 0, s, dy, y, x, mean, rstd, M, C,
                      rpb, relu, part);
-  col_reduce_f64(part, nb, 2 * C, sums, s);
-  hipLaunchKernelGGL(bn_bwd_finalize_kernel, dim3((C + 255) / 256), dim3(256), 0, s, sums, M, C,
-                     gamma, rstd, dgamma, dbeta, ws_f, ws_f + C, ws_f + 2 * C);
+  (void)sums;
+  hipLaunchKernelGGL(bn_reduce_finalize_kernel<1>, dim3((C + 15) / 16), dim3(256), 0, s, part, nb, M,
+                     C, 0.f, 0.f, gamma, rstd, dgamma, dbeta, ws_f, ws_f + C, ws_f + 2 * C,
+                     (float*)nullptr);
   const long total8 = M * C / 8;
   hipLaunchKernelGGL(bn_bwd_apply_kernel, dim3(grid_for(total8)), dim3(256), 0, s, dy, y, x, mean,
                      rstd, ws_f, ws_f + C, ws_f + 2 * C, dx, dres, total8, C, relu);

@@ -110,7 +110,8 @@ def build_sched_core(force: bool = False) -> Path:
 
     src = CSRC / "sched_core" / "sched_core.cpp"
     out = PKG / ("_sched_core" + (sysconfig.get_config_var("EXT_SUFFIX") or ".so"))
-    if not force and out.exists() and out.stat().st_mtime >= src.stat().st_mtime:
+    deps = [src, CSRC / "sched_core" / "engine.h"]
+    if not force and out.exists() and out.stat().st_mtime >= max(d.stat().st_mtime for d in deps):
         return out
     cxx = shutil.which("g++") or shutil.which("c++") or _hipcc()
     cmd = [cxx, "-O3", "-std=c++17", "-shared", "-fPIC", f"-I{pybind11.get_include()}",

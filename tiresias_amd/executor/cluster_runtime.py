@@ -43,8 +43,10 @@ from ..metrics.logger import MetricsLogger
 from .trainer import Trainer
 
 # nominal per-iteration seconds on one MI355X (tools/bench_models.py,
-# profiles/model_bench_r1_*.json); refined online from measurements
-NOMINAL_ITER_S = {"resnet50": 0.028, "vgg16": 0.015, "transformer": 0.016, "gnmt": 0.037,
+# profiles/model_bench_r1_v6.json, hipGraph replay); refined online from the
+# workers' measurements. They seed the Gittins prior (service distribution in
+# GPU-seconds) and the first round's iteration count of each job.
+NOMINAL_ITER_S = {"resnet50": 0.0121, "vgg16": 0.0088, "transformer": 0.0075, "gnmt": 0.0155,
                   "resnet_tiny": 0.004, "vgg_tiny": 0.002, "transformer_tiny": 0.006,
                   "gnmt_tiny": 0.01}
 
