@@ -1,3 +1,4 @@
+#include <array>
 // tiresias_amd — torch custom-op registration for the HIP kernel library.
 // Every op validates device / dtype / layout and fails loudly; all launches go
 // to the caller's current HIP stream (so they compose with RCCL side streams
@@ -56,16 +57,21 @@ T* opt_ptr(const optional<Tensor>& t) {
 // small problems always take the MFMA kernel. Policy: -1 measured (default),
 // 0 MFMA only, 1 library whenever eligible.
 using GemmKey = std::tuple<int64_t, int64_t, int64_t, bool, bool, int64_t, bool, bool>;
-std::map<GemmKey, int> g_route;          // 0 = MFMA kernel, 1 = library
-std::map<GemmKey, std::pair<float, float>> g_route_ms;
+std::map<GemmKey, int> g_route;          // 0 = igemm/gemm256, 1 = library, 2 = LDS-DMA GEMM
+std::map<GemmKey, std::array<float, 3>> g_route_ms;   // measured ms per path
 std::mutex g_route_mu;
 int g_lib_policy = -1;
+extern int g_dma_policy;
 bool g_forced = false;   // tile/split forced for tuning: never route to the library
 
 void run_mfma(const Tensor& a, bool ak, const Tensor& b, bool bk, int64_t M, int64_t N, int64_t K,
-              const tam::Epi& ep, bool allow_split) {
-  tam::gemm(bp(a), a.stride(0), ak, bp(b), b.stride(0), bk, (int)M, (int)N, (int)K, ep, allow_split,
-            cur_stream(a));
+              const tam::Epi& ep, bool allow_split, int path = -1) {
+  if (path < 0)
+    tam::gemm(bp(a), a.stride(0), ak, bp(b), b.stride(0), bk, (int)M, (int)N, (int)K, ep,
+              allow_split, cur_stream(a));
+  else
+    tam::gemm_select(bp(a), a.stride(0), ak, bp(b), b.stride(0), bk, (int)M, (int)N, (int)K, ep,
+                     allow_split, cur_stream(a), path);
 }
 
 void run_lib(const Tensor& a, bool ak, const Tensor& b, bool bk, const Tensor& c, int64_t mode,
@@ -146,15 +152,23 @@ void gemm_op(const Tensor& a, bool a_kmajor, const Tensor& b, bool b_kmajor, con
   const bool lib_ok = g_lib_policy != 0 && !g_forced && !relu && ep.mask == nullptr && alpha == 1.0 &&
                       (mode == 0 || (mode == 1 && ep.c_f32)) && !(has_bias && ep.c_f32) &&
                       (double)M * N * K >= (double)(1 << 27) && M >= 16 && N >= 16;
-  if (!lib_ok) {
-    run_mfma(a, a_kmajor, b, b_kmajor, M, N, K, ep, allow_split);
+  // our two kernels are both candidates for every shape the DMA GEMM accepts
+  if (g_dma_policy == 2) {
+    run_mfma(a, a_kmajor, b, b_kmajor, M, N, K, ep, allow_split, 2);
     return;
   }
-  if (g_lib_policy == 1) {
+  const bool dma_ok = g_dma_policy == 1 && !g_forced && K % 64 == 0 &&
+                      (double)M * N * K >= (double)(1 << 24);
+  if (g_lib_policy == 1 && lib_ok) {
     run_lib(a, a_kmajor, b, b_kmajor, c, mode, bias);
     return;
   }
-  const GemmKey key{M, N, K, a_kmajor, b_kmajor, mode, (bool)ep.c_f32, has_bias};
+  if (!lib_ok && !dma_ok) {
+    run_mfma(a, a_kmajor, b, b_kmajor, M, N, K, ep, allow_split);
+    return;
+  }
+  const GemmKey key{M, N, K, a_kmajor, b_kmajor, mode, (bool)ep.c_f32,
+                    has_bias || relu || ep.mask != nullptr};
   int route = -1;
   {
     std::lock_guard<std::mutex> g(g_route_mu);
@@ -169,31 +183,37 @@ void gemm_op(const Tensor& a, bool a_kmajor, const Tensor& b, bool b_kmajor, con
       run_mfma(a, a_kmajor, b, b_kmajor, M, N, K, ep, allow_split);   // never tune in a graph
       return;
     }
-    // time both on scratch output so an accumulating C is untouched
+    // time every candidate on a scratch output so an accumulating C is untouched
     Tensor scratch = at::empty_like(c);
     tam::Epi es = ep;
     es.c = scratch.data_ptr();
     es.ldc = scratch.stride(0);
-    const float t_mfma =
-        time_ms(s, [&] { run_mfma(a, a_kmajor, b, b_kmajor, M, N, K, es, allow_split); });
-    float t_lib = 1e30f;
-    try {
-      t_lib = time_ms(s, [&] { run_lib(a, a_kmajor, b, b_kmajor, scratch, mode, bias); });
-    } catch (const std::exception&) {
-      t_lib = 1e30f;   // library path unsupported for this dtype combo: keep MFMA
+    std::array<float, 3> t{1e30f, 1e30f, 1e30f};
+    t[0] = time_ms(s, [&] { run_mfma(a, a_kmajor, b, b_kmajor, M, N, K, es, allow_split, 0); });
+    if (dma_ok)
+      t[2] = time_ms(s, [&] { run_mfma(a, a_kmajor, b, b_kmajor, M, N, K, es, allow_split, 2); });
+    if (lib_ok) {
+      try {
+        t[1] = time_ms(s, [&] { run_lib(a, a_kmajor, b, b_kmajor, scratch, mode, bias); });
+      } catch (const std::exception&) {
+        t[1] = 1e30f;   // library path unsupported for this dtype combo
+      }
     }
-    route = t_lib < 0.95f * t_mfma ? 1 : 0;
+    // prefer our kernels unless another path is >5% faster
+    route = 0;
+    if (t[2] < 0.95f * t[route]) route = 2;
+    if (t[1] < 0.95f * t[route]) route = 1;
     std::lock_guard<std::mutex> g(g_route_mu);
     g_route[key] = route;
-    g_route_ms[key] = {t_mfma, t_lib};
+    g_route_ms[key] = t;
   }
   if (route == 1) run_lib(a, a_kmajor, b, b_kmajor, c, mode, bias);
-  else run_mfma(a, a_kmajor, b, b_kmajor, M, N, K, ep, allow_split);
+  else run_mfma(a, a_kmajor, b, b_kmajor, M, N, K, ep, allow_split, route);
 }
 
 void gemm_lib_policy_op(int64_t p) { g_lib_policy = (int)p; }
 
-// cached routing decisions: "M N K layout mode f32 bias route t_mfma_ms t_lib_ms" per line
+// cached routing decisions: "M N K layout mode f32 epilogue route t_mfma t_lib t_dma (ms)" per line
 std::string gemm_routes_op() {
   std::lock_guard<std::mutex> g(g_route_mu);
   std::ostringstream o;
@@ -202,8 +222,9 @@ std::string gemm_routes_op() {
     const auto t = g_route_ms[k];
     o << std::get<0>(k) << " " << std::get<1>(k) << " " << std::get<2>(k) << " "
       << (std::get<3>(k) ? "K" : "M") << (std::get<4>(k) ? "K" : "N") << " " << std::get<5>(k)
-      << " " << std::get<6>(k) << " " << std::get<7>(k) << " " << (kv.second ? "lib" : "mfma")
-      << " " << t.first << " " << t.second << "\n";
+      << " " << std::get<6>(k) << " " << std::get<7>(k) << " "
+      << (kv.second == 1 ? "lib" : kv.second == 2 ? "dma" : "mfma") << " " << t[0] << " " << t[1]
+      << " " << t[2] << "\n";
   }
   return o.str();
 }
@@ -380,6 +401,13 @@ void embedding_backward_op(const Tensor& dout, const Tensor& ids, const Tensor& 
 }
 
 void conv_dma_policy_op(int64_t p) { tam::conv_dma_policy((int)p); }
+// 0: never the LDS-DMA GEMM; 1: measured per-shape routing (default);
+// 2: LDS-DMA GEMM wherever eligible, tile cfg forced when >= 0 (tests/sweeps)
+int g_dma_policy = 1;
+void gemm_dma_policy_op(int64_t p, int64_t cfg) {
+  g_dma_policy = (int)p;
+  tam::gemm_dma_policy(p == 2 ? 1 : 0, (int)cfg);
+}
 
 void gemm_force_op(int64_t cfg, int64_t splits) {
   tam::gemm_force((int)cfg, (int)splits);
@@ -538,6 +566,7 @@ TORCH_LIBRARY(tam, m) {
   m.def("gemm_force(int cfg, int splits) -> ()", &gemm_force_op);
   m.def("gemm_lib_policy(int policy) -> ()", &gemm_lib_policy_op);
   m.def("conv_dma_policy(int policy) -> ()", &conv_dma_policy_op);
+  m.def("gemm_dma_policy(int policy, int cfg) -> ()", &gemm_dma_policy_op);
   m.def("gemm_routes() -> str", &gemm_routes_op);
   m.def("relu_backward(Tensor dy, Tensor y, Tensor(a!) dx) -> ()", &relu_backward_op);
   m.def("add(Tensor a, Tensor b, Tensor(a!) y) -> ()", &add_op);

@@ -358,11 +358,14 @@ __global__ void colsum_kernel(const bf16_t* __restrict__ x, float* __restrict__ 
 }
 
 // C % 8 == 0: block = (row lane rl, 8-column group cg) over a <=2048-column
-// chunk, 16 B loads, LDS combine over row lanes; block (x, y) writes its
-// columns of partial row y (no atomics), col_reduce_acc finishes.
+// chunk, 16 B loads, LDS combine over row lanes; block (x, y) either adds its
+// column sums straight into `out` (no-return fp32 atomics, one per column per
+// block: a few hundred blocks never contend measurably) or, with out ==
+// nullptr, writes partial row y for col_reduce_acc.
 __global__ void __launch_bounds__(256) colsum8_kernel(const bf16_t* __restrict__ x,
                                                        float* __restrict__ part, long R, int C,
-                                                       long rows_per_block) {
+                                                       long rows_per_block,
+                                                       float* __restrict__ out) {
   __shared__ float red[256 * 8];
   const int c0 = blockIdx.x * 2048;
   const int cw = min(2048, C - c0);
@@ -392,9 +395,14 @@ __global__ void __launch_bounds__(256) colsum8_kernel(const bf16_t* __restrict__
       for (int j = 1; j < rpp; ++j)
 #pragma unroll
         for (int k = 0; k < 8; ++k) s[k] += red[(j * tpr + cg) * 8 + k];
-      float* pr = part + (long)blockIdx.y * C + c;
-      *(float4*)pr = make_float4(s[0], s[1], s[2], s[3]);
-      *(float4*)(pr + 4) = make_float4(s[4], s[5], s[6], s[7]);
+      if (out) {
+#pragma unroll
+        for (int k = 0; k < 8; ++k) atomicAdd(out + c + k, s[k]);
+      } else {
+        float* pr = part + (long)blockIdx.y * C + c;
+        *(float4*)pr = make_float4(s[0], s[1], s[2], s[3]);
+        *(float4*)(pr + 4) = make_float4(s[4], s[5], s[6], s[7]);
+      }
     }
     __syncthreads();
   }
@@ -409,7 +417,12 @@ void colsum(const bf16_t* x, float* out, float* ws, long R, int C, hipStream_t s
     long rpb = (R + by - 1) / by;
     if (rpb < 32) rpb = 32;
     by = (R + rpb - 1) / rpb;
-    hipLaunchKernelGGL(colsum8_kernel, dim3(bx, by), dim3(256), 0, s, x, ws, R, C, rpb);
+    // partial rows + a column reduce: straight fp32 atomics into `out` (one
+    // per column per block) measured slower — hundreds of blocks adding into
+    // the same few cache lines serialise at the memory side (VGG conv bias,
+    // 64 columns: +20 us per call)
+    hipLaunchKernelGGL(colsum8_kernel, dim3(bx, by), dim3(256), 0, s, x, ws, R, C, rpb,
+                       (float*)nullptr);
     col_reduce_acc(ws, (int)by, C, out, out, C, s);
     return;
   }

@@ -72,6 +72,52 @@ def test_gemm_layouts(gpu, M, N, K, ak, bk):
     assert rel_err(cb, ref) < 1e-2
 
 
+# every tile config of the LDS-DMA GEMM (gemm_dma.h), all majorities, edge
+# tiles, bf16 staged epilogue with bias/relu/mask/accumulate, fp32 split-K
+@pytest.mark.parametrize("cfg", [0, 1, 2, 3])
+@pytest.mark.parametrize("ak,bk", [(True, True), (True, False), (False, True), (False, False)])
+def test_gemm_dma_configs(gpu, cfg, ak, bk):
+    torch.manual_seed(11 + cfg)
+    M, N, K = 328, 200, 384
+    A = torch.randn(M, K, device=gpu).to(BF)
+    B = torch.randn(K, N, device=gpu).to(BF)
+    a = A if ak else A.t().contiguous()
+    b = B.t().contiguous() if bk else B
+    ref = A.float() @ B.float()
+    bias = torch.randn(N, device=gpu).to(BF)
+    mask = torch.randn(M, N, device=gpu).to(BF)
+    T().gemm_dma_policy(2, cfg)
+    try:
+        c = torch.empty(M, N, device=gpu)
+        T().gemm(a, ak, b, bk, c, 0, None, False, None, 1.0, False)
+        assert rel_err(c, ref) < 1e-5
+        acc = torch.full((M, N), 1.5, device=gpu)
+        T().gemm(a, ak, b, bk, acc, 1, None, False, None, 1.0, True)
+        assert rel_err(acc, ref + 1.5) < 1e-5
+        y = torch.empty(M, N, device=gpu, dtype=BF)
+        T().gemm(a, ak, b, bk, y, 0, bias, True, None, 1.0, False)
+        assert rel_err(y, (ref + bias.float()).clamp_min(0)) < 1e-2
+        T().gemm(a, ak, b, bk, y, 0, None, False, mask, 0.5, False)
+        assert rel_err(y, 0.5 * ref * (mask.float() > 0)) < 1e-2
+        y0 = torch.randn(M, N, device=gpu).to(BF)
+        y1 = y0.clone()
+        T().gemm(a, ak, b, bk, y1, 1, None, False, None, 1.0, False)
+        assert rel_err(y1, y0.float() + ref) < 1e-2
+    finally:
+        T().gemm_dma_policy(1, -1)
+
+
+def test_gemm_dma_splitk(gpu):
+    torch.manual_seed(5)
+    M, N, K = 96, 128, 8192
+    A = torch.randn(K, M, device=gpu).to(BF)      # MN-major A (wgrad-like)
+    B = torch.randn(K, N, device=gpu).to(BF)
+    ref = A.float().t() @ B.float()
+    c = torch.full((M, N), 3.0, device=gpu)
+    T().gemm(A, False, B, False, c, 1, None, False, None, 1.0, True)
+    assert rel_err(c, ref + 3.0) < 1e-5
+
+
 def test_gemm_identity_asymmetric(gpu):
     # A = I with an asymmetric B catches a transposed C-write (guide §3)
     n = 128

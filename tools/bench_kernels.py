@@ -35,12 +35,24 @@ def timeit(fn, iters=20, warmup=5):
     return min(ts)
 
 
-def gemm_cases(T, dev):
+BIG_GEMMS = [(4096, 4096, 4096, True, True), (8192, 8192, 8192, True, True),
+             (4096, 4096, 4096, True, False), (4096, 4096, 4096, False, False),
+             (16384, 2048, 512, True, True), (4096, 32000, 512, True, True),
+             (512, 2048, 16384, False, False)]
+# the zoo's small/medium linears: Transformer-base (4096 tokens) fwd KK / dgrad
+# KN / wgrad MN, GNMT LSTM recurrence (batch 64) and its projections
+ZOO_GEMMS = [(4096, 512, 512, True, True), (4096, 1536, 512, True, True),
+             (4096, 2048, 512, True, True), (4096, 512, 2048, True, True),
+             (4096, 512, 512, True, False), (4096, 512, 2048, True, False),
+             (4096, 2048, 512, True, False), (512, 512, 4096, False, False),
+             (2048, 512, 4096, False, False), (512, 2048, 4096, False, False),
+             (64, 4096, 1024, True, True), (64, 1024, 4096, True, False),
+             (3200, 4096, 1024, True, True), (1024, 4096, 3200, False, False)]
+
+
+def gemm_cases(T, dev, shapes=BIG_GEMMS):
     out = []
-    for (M, N, K, ak, bk) in [(4096, 4096, 4096, True, True), (8192, 8192, 8192, True, True),
-                              (4096, 4096, 4096, True, False), (4096, 4096, 4096, False, False),
-                              (16384, 2048, 512, True, True), (4096, 32000, 512, True, True),
-                              (512, 2048, 16384, False, False)]:
+    for (M, N, K, ak, bk) in shapes:
         A = torch.randn(M, K, device=dev).to(BF)
         B = torch.randn(K, N, device=dev).to(BF)
         a = A if ak else A.t().contiguous()
@@ -132,17 +144,21 @@ def main():
     ap.add_argument("--out", default=None)
     ap.add_argument("--only", default="gemm,conv,attn")
     ap.add_argument("--conv-dma", type=int, default=1, help="conv_dma_policy (0: igemm only)")
+    ap.add_argument("--gemm-dma", type=int, default=0,
+                    help="gemm_dma_policy: 0 igemm/gemm256, 2 LDS-DMA GEMM forced, 1 measured routing")
     a = ap.parse_args()
     _lib.load(required=True)
     T = torch.ops.tam
     T.gemm_lib_policy(0)   # measure the MFMA kernels themselves
     T.conv_dma_policy(a.conv_dma)
+    T.gemm_dma_policy(a.gemm_dma, -1)
     dev = torch.device("cuda", 0)
     torch.manual_seed(0)
     res = []
     for kind in a.only.split(","):
         fn = {"gemm": gemm_cases, "conv": conv_cases, "attn": attn_cases,
-              "vggconv": lambda T, d: conv_cases(T, d, VGG_CONVS)}[kind]
+              "vggconv": lambda T, d: conv_cases(T, d, VGG_CONVS),
+              "zoogemm": lambda T, d: gemm_cases(T, d, ZOO_GEMMS)}[kind]
         for r in fn(T, dev):
             print(json.dumps(r), flush=True)
             res.append(r)
