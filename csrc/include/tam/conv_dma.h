@@ -33,15 +33,35 @@ typedef __attribute__((address_space(3))) void cd_lds_void_t;
 // globals are zero-initialised at load; never written)
 static __device__ __attribute__((aligned(256))) bf16_t g_cd_zero[128];
 
+// Every pass is expressed as taps over a row grid:
+//   row m = (n, p, q) over P x Q; its base source pixel (p*stride + base_h,
+//   q*stride + base_w); K-tile kt -> tap t = kt / (Cs/64), channel block
+//   kt % (Cs/64); tap t reads source pixel base + (tap_dh[t], tap_dw[t]) and
+//   B columns tap_kcol[t] + 64*block of the weight rows (row stride ldb).
+//   fwd         : taps (r,s) -> (r, s), kcol (r*S+s)*C, base -pad
+//   dgrad s=1   : taps (r,s) -> (pad-r, pad-s), kcol (r*S+s)*K over Wt, base 0
+//   dgrad s>1   : one launch per output parity (ph,pw) over the parity
+//                 sub-grid, taps r = ph+pad (mod s) -> ((ph+pad-r)/s, ...);
+//                 the epilogue maps row (n,i,j) to pixel (n, i*s+ph, j*s+pw)
 struct CDArgs {
   const bf16_t* src;   // gathered operand, NHWC [.][Hs][Ws][Cs]
-  const bf16_t* wgt;   // B operand, K-major [Ng][Kd]
-  int M, Ng, Kd;       // GEMM dims (Kd = R*S*Cs)
+  const bf16_t* wgt;   // B operand, K-major rows of stride ldb
+  int M, Ng, Kd;       // GEMM dims (Kd = ntaps*Cs)
   int Hs, Ws, Cs;      // gather source geometry
   int P, Q;            // rows m = (n, p, q) over a P x Q grid
-  int S;               // filter width
-  int stride, pad;
+  int stride, base_h, base_w;
+  long ldb;
+  int ntaps;
+  int tap_dh[9], tap_dw[9], tap_kcol[9];
+  // output row map (omap != 0): row (n,p,q) -> pixel (n, p*osh+ooh, q*osw+oow) of oH x oW
+  int omap, oH, oW, osh, osw, ooh, oow;
 };
+
+__device__ __forceinline__ long cd_out_row(const CDArgs& a, int m) {
+  if (!a.omap) return m;
+  const int q = m % a.Q, t = m / a.Q, p = t % a.P, n = t / a.P;
+  return ((long)n * a.oH + p * a.osh + a.ooh) * a.oW + q * a.osw + a.oow;
+}
 
 template <int N>
 __device__ __forceinline__ void cd_vm_wait() {
@@ -54,7 +74,7 @@ __device__ __forceinline__ void cd_barrier() {
   asm volatile("" ::: "memory");
 }
 
-template <int BN, int WN, bool FWD>
+template <int BN, int WN>
 __global__ void __launch_bounds__(256 * WN, 1) conv_dma_kernel(CDArgs a, Epi ep) {
   constexpr int W = 4 * WN;               // waves
   constexpr int BM = 256, BK = 64;
@@ -91,8 +111,8 @@ __global__ void __launch_bounds__(256 * WN, 1) conv_dma_kernel(CDArgs a, Epi ep)
     const int m = m0 + rr;
     if (m < a.M) {
       const int q = m % a.Q, t = m / a.Q, p = t % a.P, n = t / a.P;
-      const int hb = FWD ? p * a.stride - a.pad : p + a.pad;
-      const int wb = FWD ? q * a.stride - a.pad : q + a.pad;
+      const int hb = p * a.stride + a.base_h;
+      const int wb = q * a.stride + a.base_w;
       ah[j] = hb;
       aw[j] = wb;
       abase[j] = ((n * a.Hs + hb) * a.Ws + wb) * a.Cs + c * 8;
@@ -109,7 +129,7 @@ __global__ void __launch_bounds__(256 * WN, 1) conv_dma_kernel(CDArgs a, Epi ep)
     const int c = (lane & 7) ^ ((rr >> 1) & 7);
     int n = n0 + rr;
     n = n < a.Ng ? n : a.Ng - 1;           // clamp: columns past the edge are never stored
-    bptr[j] = a.wgt + (long)n * a.Kd + c * 8;
+    bptr[j] = a.wgt + (long)n * a.ldb + c * 8;
   }
   const int ctiles = a.Cs / BK;
   const int nk = a.Kd / BK;
@@ -117,10 +137,10 @@ __global__ void __launch_bounds__(256 * WN, 1) conv_dma_kernel(CDArgs a, Epi ep)
   auto issue = [&](int kt, int st) {
     char* sa = smem + st * STAGE;
     char* sb = sa + A_BYTES;
-    const int ct = kt % ctiles, rs = kt / ctiles;
-    const int r = rs / a.S, s = rs % a.S;
-    const int dh = FWD ? r : -r, dw = FWD ? s : -s;
+    const int ct = kt % ctiles, tp = kt / ctiles;
+    const int dh = a.tap_dh[tp], dw = a.tap_dw[tp];
     const int toff = (dh * a.Ws + dw) * a.Cs + ct * BK;
+    const int kcol = a.tap_kcol[tp] + ct * BK;
 #pragma unroll
     for (int j = 0; j < AG; ++j) {
       const int h = ah[j] + dh, w = aw[j] + dw;
@@ -133,7 +153,7 @@ __global__ void __launch_bounds__(256 * WN, 1) conv_dma_kernel(CDArgs a, Epi ep)
     }
 #pragma unroll
     for (int j = 0; j < BG; ++j)
-      __builtin_amdgcn_global_load_lds((const void*)(bptr[j] + kt * BK),
+      __builtin_amdgcn_global_load_lds((const void*)(bptr[j] + kcol),
                                        (cd_lds_void_t*)(sb + (wid + W * j) * 1024), 16, 0, 0);
   };
 
@@ -216,9 +236,10 @@ __global__ void __launch_bounds__(256 * WN, 1) conv_dma_kernel(CDArgs a, Epi ep)
         const int idx = u * 64 + lane, lr = idx / CPR, ch = idx % CPR;
         const int row = m0 + wm * 64 + half * 32 + lr;
         if (row < a.M) {
+          const long orow = cd_out_row(a, row);
           uint4 v = *(const uint4*)(slab + lr * LDW + ch * 8);
           if (ep.mask) {
-            const uint4 mk = *(const uint4*)(ep.mask + (long)row * ep.ldm + cbase + ch * 8);
+            const uint4 mk = *(const uint4*)(ep.mask + orow * ep.ldm + cbase + ch * 8);
             const uint32_t* mw = (const uint32_t*)&mk;
             uint32_t* vw = (uint32_t*)&v;
 #pragma unroll
@@ -229,7 +250,7 @@ __global__ void __launch_bounds__(256 * WN, 1) conv_dma_kernel(CDArgs a, Epi ep)
               vw[e] &= (lo ? 0x0000ffffu : 0u) | (hi ? 0xffff0000u : 0u);
             }
           }
-          bf16_t* dst = (bf16_t*)ep.c + (long)row * ep.ldc + cbase + ch * 8;
+          bf16_t* dst = (bf16_t*)ep.c + orow * ep.ldc + cbase + ch * 8;
           if (ep.mode == 1) {
             const uint4 o = *(const uint4*)dst;
             const uint32_t* ow = (const uint32_t*)&o;
@@ -259,10 +280,11 @@ __global__ void __launch_bounds__(256 * WN, 1) conv_dma_kernel(CDArgs a, Epi ep)
       for (int r = 0; r < 4; ++r) {
         const int row = m0 + wm * 64 + 16 * i + 4 * (lane >> 4) + r;
         if (row >= a.M) continue;
+        const long orow = cd_out_row(a, row);
         float v = acc[i][j][r] * ep.alpha + bv;
         if (ep.relu) v = fmaxf(v, 0.f);
-        if (ep.mask && bf2f(ep.mask[(long)row * ep.ldm + col]) <= 0.f) v = 0.f;
-        float* c = (float*)ep.c + (long)row * ep.ldc + col;
+        if (ep.mask && bf2f(ep.mask[orow * ep.ldm + col]) <= 0.f) v = 0.f;
+        float* c = (float*)ep.c + orow * ep.ldc + col;
         if (ep.mode == 1) *c += v;
         else *c = v;
       }
@@ -284,31 +306,79 @@ inline int conv_dma_pick_bn(int M, int Ng, int Kd, bool force) {
   return 0;
 }
 
-template <bool FWD>
 inline bool launch_conv_dma(const CDArgs& a, const Epi& ep, hipStream_t s, bool force = false) {
   // Kd >= 256: with fewer than 4 K-tiles the ring never fills (1x1 convs over
-  // 64/128 channels measured slower than the igemm)
-  if (a.Cs % 64 != 0 || a.Kd % 64 != 0 || a.Kd < 256) return false;
-  if (!FWD && a.stride != 1) return false;
+  // 64/128 channels measured slower than the igemm) — unless forced (tests,
+  // strided-dgrad parity classes, where the igemm alternative is far worse)
+  if (a.Cs % 64 != 0 || a.Kd % 64 != 0 || a.Kd < 64 || (a.Kd < 256 && !force)) return false;
+  if (a.ntaps < 1 || a.ntaps > 9) return false;
   if ((long)a.Hs * a.Ws * a.Cs * ((a.M + a.P * a.Q - 1) / (a.P * a.Q)) >= (1L << 31)) return false;
-  if ((long)a.Ng * a.Kd >= (1L << 31)) return false;
+  if ((long)a.Ng * a.ldb >= (1L << 31)) return false;
   const int bn = conv_dma_pick_bn(a.M, a.Ng, a.Kd, force);
   if (!bn) return false;
   const int tiles = ((a.M + 255) / 256) * (a.Ng / bn);
   switch (bn) {
     case 256:
-      hipLaunchKernelGGL((conv_dma_kernel<256, 2, FWD>), dim3(tiles), dim3(512), 0, s, a, ep);
+      hipLaunchKernelGGL((conv_dma_kernel<256, 2>), dim3(tiles), dim3(512), 0, s, a, ep);
       break;
     case 128:
-      hipLaunchKernelGGL((conv_dma_kernel<128, 2, FWD>), dim3(tiles), dim3(512), 0, s, a, ep);
+      hipLaunchKernelGGL((conv_dma_kernel<128, 2>), dim3(tiles), dim3(512), 0, s, a, ep);
       break;
     default:
-      hipLaunchKernelGGL((conv_dma_kernel<64, 1, FWD>), dim3(tiles), dim3(256), 0, s, a, ep);
+      hipLaunchKernelGGL((conv_dma_kernel<64, 1>), dim3(tiles), dim3(256), 0, s, a, ep);
       break;
   }
   return true;
 }
 
+// argument builders (host)
+inline CDArgs cd_fwd_args(const bf16_t* x, const bf16_t* w, const ConvGeom& g) {
+  CDArgs a{};
+  a.src = x; a.wgt = w;
+  a.M = g.N * g.P * g.Q; a.Ng = g.K; a.Kd = g.R * g.S * g.C;
+  a.Hs = g.H; a.Ws = g.W; a.Cs = g.C; a.P = g.P; a.Q = g.Q;
+  a.stride = g.stride; a.base_h = -g.pad; a.base_w = -g.pad;
+  a.ldb = (long)g.R * g.S * g.C;
+  a.ntaps = g.R * g.S;
+  if (a.ntaps > 9) { a.ntaps = 0; return a; }
+  for (int r = 0; r < g.R; ++r)
+    for (int q = 0; q < g.S; ++q) {
+      const int t = r * g.S + q;
+      a.tap_dh[t] = r; a.tap_dw[t] = q; a.tap_kcol[t] = t * g.C;
+    }
+  return a;
+}
+
+// dgrad over Wt [C][R][S][K]; stride-s layers: parity class (ph, pw)
+inline CDArgs cd_dgrad_args(const bf16_t* dy, const bf16_t* wt, const ConvGeom& g, int ph, int pw) {
+  CDArgs a{};
+  const int st = g.stride;
+  a.src = dy; a.wgt = wt;
+  a.Hs = g.P; a.Ws = g.Q; a.Cs = g.K; a.Ng = g.C;
+  a.ldb = (long)g.R * g.S * g.K;
+  a.stride = 1; a.base_h = 0; a.base_w = 0;
+  a.P = (g.H - ph + st - 1) / st;
+  a.Q = (g.W - pw + st - 1) / st;
+  a.M = g.N * a.P * a.Q;
+  if (st > 1) {
+    a.omap = 1; a.oH = g.H; a.oW = g.W; a.osh = st; a.osw = st; a.ooh = ph; a.oow = pw;
+  }
+  int n = 0;
+  for (int r = 0; r < g.R; ++r) {
+    if (((ph + g.pad - r) % st + st) % st) continue;
+    for (int q = 0; q < g.S; ++q) {
+      if (((pw + g.pad - q) % st + st) % st) continue;
+      if (n == 9) { a.ntaps = 0; return a; }
+      a.tap_dh[n] = (ph + g.pad - r) / st;
+      a.tap_dw[n] = (pw + g.pad - q) / st;
+      a.tap_kcol[n] = (r * g.S + q) * g.K;
+      ++n;
+    }
+  }
+  a.ntaps = n;
+  a.Kd = n * g.K;
+  return a;
+}
 
 // ===========================================================================
 // LDS-DMA conv weight gradient (split over output pixels, fp32 atomics)

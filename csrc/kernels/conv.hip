@@ -36,8 +36,8 @@ static bool is_pointwise(const ConvGeom& g) {
 void conv_fwd(const bf16_t* x, const bf16_t* w, const ConvGeom& g, Epi ep, hipStream_t s) {
   const int M = g.N * g.P * g.Q, Kd = g.R * g.S * g.C;
   if (g_conv_dma && g.dil == 1) {
-    CDArgs a{x, w, M, g.K, Kd, g.H, g.W, g.C, g.P, g.Q, g.S, g.stride, g.pad};
-    if (launch_conv_dma<true>(a, ep, s, g_conv_dma == 2)) return;
+    CDArgs a = cd_fwd_args(x, w, g);
+    if (launch_conv_dma(a, ep, s, g_conv_dma == 2)) return;
   }
   if (is_pointwise(g)) {
     gemm(x, g.C, true, w, g.C, true, M, g.K, g.C, ep, false, s);
@@ -66,8 +66,28 @@ void conv_dgrad(const bf16_t* dy, const bf16_t* w, const bf16_t* wt, const ConvG
   const int M = g.N * g.H * g.W, Kd = g.R * g.S * g.K;
   if (wt && g_conv_dma && g.dil == 1 && g.stride == 1) {
     // rows = dX pixels over an H x W grid, gathered from dY (P x Q x K), B = Wt [C][R][S][K]
-    CDArgs a{dy, wt, M, g.C, Kd, g.P, g.Q, g.K, g.H, g.W, g.S, 1, g.pad};
-    if (launch_conv_dma<false>(a, ep, s, g_conv_dma == 2)) return;
+    CDArgs a = cd_dgrad_args(dy, wt, g, 0, 0);
+    if (launch_conv_dma(a, ep, s, g_conv_dma == 2)) return;
+  }
+  if (wt && g_conv_dma && g.dil == 1 && g.stride > 1 && g.K % 64 == 0 && g.C % 64 == 0 &&
+      ep.mode == 0 && !ep.c_f32 && g.stride * g.stride <= 4) {
+    // strided dgrad = one stride-1 sub-convolution per output parity class
+    // (dX pixels with h % s == ph get only the taps r == ph + pad (mod s));
+    // classes without taps (1x1 stride 2: 3 of 4) are zero
+    CDArgs cls[4];
+    bool ok = true, empty = false;
+    for (int ph = 0, i = 0; ph < g.stride; ++ph)
+      for (int pw = 0; pw < g.stride; ++pw, ++i) {
+        cls[i] = cd_dgrad_args(dy, wt, g, ph, pw);
+        if (cls[i].ntaps == 0) empty = true;
+        else ok = ok && conv_dma_pick_bn(cls[i].M, cls[i].Ng, cls[i].Kd, true) != 0;
+      }
+    if (ok) {
+      if (empty) TAM_HIP_CHECK(hipMemsetAsync(ep.c, 0, (size_t)M * g.C * sizeof(bf16_t), s));
+      for (int i = 0; i < g.stride * g.stride; ++i)
+        if (cls[i].ntaps) launch_conv_dma(cls[i], ep, s, true);
+      return;
+    }
   }
   if (is_pointwise(g)) {
     // dX[m][c] = sum_k dY[m][k] W[k][c]  -> B(k,n) = W[k*C + c], MN-major

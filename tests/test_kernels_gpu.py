@@ -234,7 +234,8 @@ def test_conv_fwd_dgrad_wgrad(gpu, cfg):
                                  (2, 10, 10, 64, 256, 3, 1, 1), (2, 14, 14, 128, 64, 3, 2, 1),
                                  (2, 13, 13, 64, 128, 1, 2, 0), (1, 9, 9, 192, 128, 3, 1, 1),
                                  (4, 16, 16, 128, 256, 3, 1, 1), (2, 7, 7, 256, 128, 1, 1, 0),
-                                 (40, 7, 7, 128, 128, 3, 1, 1)])
+                                 (40, 7, 7, 128, 128, 3, 1, 1), (4, 28, 28, 128, 128, 3, 2, 1),
+                                 (2, 16, 16, 256, 512, 1, 2, 0), (2, 9, 9, 64, 64, 3, 2, 1)])
 def test_conv_dma_core(gpu, cfg):
     N, H, W, C, K, R, st, pd = cfg
     torch.manual_seed(7)
