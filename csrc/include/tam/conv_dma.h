@@ -74,13 +74,14 @@ __device__ __forceinline__ void cd_barrier() {
   asm volatile("" ::: "memory");
 }
 
-template <int BN, int WN>
-__global__ void __launch_bounds__(256 * WN, 1) conv_dma_kernel(CDArgs a, Epi ep) {
-  constexpr int W = 4 * WN;               // waves
-  constexpr int BM = 256, BK = 64;
-  constexpr int STAGES = BN <= 128 ? 3 : 2;
+template <int BN, int WN, int BM = 256>
+__global__ void __launch_bounds__(BM / 64 * 64 * WN, 1) conv_dma_kernel(CDArgs a, Epi ep) {
+  constexpr int WM = BM / 64;             // waves along M (64 rows each)
+  constexpr int W = WM * WN;              // waves
+  constexpr int BK = 64;
   constexpr int A_BYTES = BM * BK * 2, B_BYTES = BN * BK * 2, STAGE = A_BYTES + B_BYTES;
-  constexpr int AG = 32 / W;              // A 8-row groups per wave
+  constexpr int STAGES = 3 * STAGE <= 160 * 1024 ? 3 : 2;
+  constexpr int AG = BM / 8 / W;          // A 8-row groups per wave
   constexpr int BG = BN / 8 / W;          // B 8-row groups per wave
   constexpr int D = AG + BG;              // DMA instructions per thread per K-tile
   constexpr int WCOLS = BN / WN;          // columns per wave
@@ -88,7 +89,7 @@ __global__ void __launch_bounds__(256 * WN, 1) conv_dma_kernel(CDArgs a, Epi ep)
   __shared__ __attribute__((aligned(1024))) char smem[STAGES * STAGE];
 
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
-  const int wm = wid & 3, wn = wid >> 2;
+  const int wm = wid % WM, wn = wid / WM;
 
   const int tiles_m = (a.M + BM - 1) / BM, tiles_n = (a.Ng + BN - 1) / BN;
   const int bid = xcd_remap(blockIdx.x, gridDim.x);
@@ -294,19 +295,29 @@ __global__ void __launch_bounds__(256 * WN, 1) conv_dma_kernel(CDArgs a, Epi ep)
 
 // Host-side eligibility + launch. Returns false when the shape is not for
 // this core (caller falls back to the register-staged igemm).
-inline int conv_dma_pick_bn(int M, int Ng, int Kd, bool force) {
+// returns BN, or BN | 0x1000 for the 128-row tile variant.
+// Cost model (fitted to profiles/conv_bench_r1_dma*.json): time ~ ceil(tiles /
+// 256 CUs) x tile area / efficiency, efficiency 256x256 1.0, 256x128 0.92,
+// 128x128 0.8. BN = 64 only for deep-K gathers (the 32 KiB A tile per 64
+// columns is L2-bound at shallow K and loses to the igemm).
+inline int conv_dma_pick_bn(int M, int Ng, int Kd, int force) {
+  if (force == 2 && Ng % 128 == 0) return 128 | 0x1000;   // tests: the 128-row variant
   if (force) return Ng % 256 == 0 ? 256 : Ng % 128 == 0 ? 128 : Ng % 64 == 0 ? 64 : 0;
-  // measured (profiles/conv_bench_r1_*.json): BN=64 loses to the igemm (the
-  // 32 KiB A tile per 64 columns is L2-bound); BN>=128 wins even at ~0.6
-  // tiles per CU
-  const int tm = (M + 255) / 256;
-  if (Ng % 256 == 0 && (long)tm * (Ng / 256) >= 96) return 256;
-  if (Ng % 128 == 0 && (long)tm * (Ng / 128) >= 160) return 128;
-  if (Ng % 64 == 0 && Kd >= 1024 && (long)tm * (Ng / 64) >= 512) return 64;
-  return 0;
+  const long tm = (M + 255) / 256, tm2 = (M + 127) / 128;
+  double best = 1e30;
+  int pick = 0;
+  auto consider = [&](long tiles, double area, double eff, int code) {
+    const double cost = (double)((tiles + 255) / 256) * area / eff;
+    if (cost < best) { best = cost; pick = code; }
+  };
+  if (Ng % 256 == 0) consider(tm * (Ng / 256), 65536.0, 1.0, 256);
+  if (Ng % 128 == 0) consider(tm * (Ng / 128), 32768.0, 0.92, 128);
+  if (Ng % 128 == 0 && Kd >= 1024) consider(tm2 * (Ng / 128), 16384.0, 0.8, 128 | 0x1000);
+  if (!pick && Ng % 64 == 0 && Kd >= 1024 && tm * (Ng / 64) >= 512) pick = 64;
+  return pick;
 }
 
-inline bool launch_conv_dma(const CDArgs& a, const Epi& ep, hipStream_t s, bool force = false) {
+inline bool launch_conv_dma(const CDArgs& a, const Epi& ep, hipStream_t s, int force = 0) {
   // Kd >= 256: with fewer than 4 K-tiles the ring never fills (1x1 convs over
   // 64/128 channels measured slower than the igemm) — unless forced (tests,
   // strided-dgrad parity classes, where the igemm alternative is far worse)
@@ -314,8 +325,14 @@ inline bool launch_conv_dma(const CDArgs& a, const Epi& ep, hipStream_t s, bool 
   if (a.ntaps < 1 || a.ntaps > 9) return false;
   if ((long)a.Hs * a.Ws * a.Cs * ((a.M + a.P * a.Q - 1) / (a.P * a.Q)) >= (1L << 31)) return false;
   if ((long)a.Ng * a.ldb >= (1L << 31)) return false;
-  const int bn = conv_dma_pick_bn(a.M, a.Ng, a.Kd, force);
-  if (!bn) return false;
+  const int pick = conv_dma_pick_bn(a.M, a.Ng, a.Kd, force);
+  if (!pick) return false;
+  if (pick & 0x1000) {
+    const int tiles = ((a.M + 127) / 128) * (a.Ng / 128);
+    hipLaunchKernelGGL((conv_dma_kernel<128, 2, 128>), dim3(tiles), dim3(256), 0, s, a, ep);
+    return true;
+  }
+  const int bn = pick;
   const int tiles = ((a.M + 255) / 256) * (a.Ng / bn);
   switch (bn) {
     case 256:

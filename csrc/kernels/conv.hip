@@ -16,7 +16,8 @@ namespace tam {
 
 // 1 (default): fwd / stride-1 dgrad with C % 64 == 0 go to the LDS-DMA core
 // (conv_dma.h) when the grid fills the chip; 2: LDS-DMA core wherever the
-// shape is eligible (tests); 0: register-staged igemm only (A/B measurements)
+// shape is eligible (tests); 3: as 2 with the 128-row tile variant (tests);
+// 0: register-staged igemm only (A/B measurements)
 static int g_conv_dma = 1;
 void conv_dma_policy(int p) { g_conv_dma = p; }
 
@@ -37,7 +38,7 @@ void conv_fwd(const bf16_t* x, const bf16_t* w, const ConvGeom& g, Epi ep, hipSt
   const int M = g.N * g.P * g.Q, Kd = g.R * g.S * g.C;
   if (g_conv_dma && g.dil == 1) {
     CDArgs a = cd_fwd_args(x, w, g);
-    if (launch_conv_dma(a, ep, s, g_conv_dma == 2)) return;
+    if (launch_conv_dma(a, ep, s, g_conv_dma >= 2 ? g_conv_dma - 1 : 0)) return;
   }
   if (is_pointwise(g)) {
     gemm(x, g.C, true, w, g.C, true, M, g.K, g.C, ep, false, s);
@@ -67,7 +68,7 @@ void conv_dgrad(const bf16_t* dy, const bf16_t* w, const bf16_t* wt, const ConvG
   if (wt && g_conv_dma && g.dil == 1 && g.stride == 1) {
     // rows = dX pixels over an H x W grid, gathered from dY (P x Q x K), B = Wt [C][R][S][K]
     CDArgs a = cd_dgrad_args(dy, wt, g, 0, 0);
-    if (launch_conv_dma(a, ep, s, g_conv_dma == 2)) return;
+    if (launch_conv_dma(a, ep, s, g_conv_dma >= 2 ? g_conv_dma - 1 : 0)) return;
   }
   if (wt && g_conv_dma && g.dil == 1 && g.stride > 1 && g.K % 64 == 0 && g.C % 64 == 0 &&
       ep.mode == 0 && !ep.c_f32 && g.stride * g.stride <= 4) {
@@ -80,12 +81,12 @@ void conv_dgrad(const bf16_t* dy, const bf16_t* w, const bf16_t* wt, const ConvG
       for (int pw = 0; pw < g.stride; ++pw, ++i) {
         cls[i] = cd_dgrad_args(dy, wt, g, ph, pw);
         if (cls[i].ntaps == 0) empty = true;
-        else ok = ok && conv_dma_pick_bn(cls[i].M, cls[i].Ng, cls[i].Kd, true) != 0;
+        else ok = ok && conv_dma_pick_bn(cls[i].M, cls[i].Ng, cls[i].Kd, 1) != 0;
       }
     if (ok) {
       if (empty) TAM_HIP_CHECK(hipMemsetAsync(ep.c, 0, (size_t)M * g.C * sizeof(bf16_t), s));
       for (int i = 0; i < g.stride * g.stride; ++i)
-        if (cls[i].ntaps) launch_conv_dma(cls[i], ep, s, true);
+        if (cls[i].ntaps) launch_conv_dma(cls[i], ep, s, g_conv_dma == 3 ? 2 : 1);
       return;
     }
   }
@@ -115,7 +116,7 @@ static void wgrad_tile(const bf16_t* dy, const bf16_t* x, const ConvGeom& g, con
 void conv_wgrad(const bf16_t* dy, const bf16_t* x, const ConvGeom& g, Epi ep, hipStream_t s) {
   const int Mred = g.N * g.P * g.Q, Nc = g.R * g.S * g.C;
   if (g_conv_dma && ep.c_f32 && ep.ldc == Nc && ep.mode <= 1 &&
-      launch_conv_wgrad_dma(dy, x, (float*)ep.c, g, ep.mode, s, g_conv_dma == 2))
+      launch_conv_wgrad_dma(dy, x, (float*)ep.c, g, ep.mode, s, g_conv_dma >= 2))
     return;
   if (is_pointwise(g)) {
     // dW[k][c] = sum_m dY[m][k] X[m][c]: A(k', m) = dY[m*K + k'], B(m, c) = X[m*C + c]

@@ -236,10 +236,11 @@ def test_conv_fwd_dgrad_wgrad(gpu, cfg):
                                  (4, 16, 16, 128, 256, 3, 1, 1), (2, 7, 7, 256, 128, 1, 1, 0),
                                  (40, 7, 7, 128, 128, 3, 1, 1), (4, 28, 28, 128, 128, 3, 2, 1),
                                  (2, 16, 16, 256, 512, 1, 2, 0), (2, 9, 9, 64, 64, 3, 2, 1)])
-def test_conv_dma_core(gpu, cfg):
+@pytest.mark.parametrize("policy", [2, 3])
+def test_conv_dma_core(gpu, cfg, policy):
     N, H, W, C, K, R, st, pd = cfg
     torch.manual_seed(7)
-    T().conv_dma_policy(2)
+    T().conv_dma_policy(policy)
     try:
         x = torch.randn(N, H, W, C, device=gpu).to(BF)
         w = (torch.randn(K, R, R, C, device=gpu) / math.sqrt(R * R * C)).to(BF)
