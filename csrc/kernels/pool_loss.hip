@@ -378,7 +378,22 @@ __global__ void __launch_bounds__(256) colsum8_kernel(const bf16_t* __restrict__
     const int c = c0 + cb + cg * 8;
     float s[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
     if (rl < rpp && c < c0 + cw) {
-      for (long r = r0 + rl; r < r1; r += rpp) {
+      long r = r0 + rl;
+      for (; r + 3 * rpp < r1; r += 4 * rpp) {     // 4 independent loads in flight
+        uint4 v[4];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) v[u] = *(const uint4*)(x + (r + u * rpp) * C + c);
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+          const uint32_t w[4] = {v[u].x, v[u].y, v[u].z, v[u].w};
+#pragma unroll
+          for (int k = 0; k < 4; ++k) {
+            s[2 * k] += __uint_as_float(w[k] << 16);
+            s[2 * k + 1] += __uint_as_float(w[k] & 0xffff0000u);
+          }
+        }
+      }
+      for (; r < r1; r += rpp) {
         const uint4 v = *(const uint4*)(x + r * C + c);
         const uint32_t w[4] = {v.x, v.y, v.z, v.w};
 #pragma unroll
@@ -417,10 +432,10 @@ void colsum(const bf16_t* x, float* out, float* ws, long R, int C, hipStream_t s
     long rpb = (R + by - 1) / by;
     if (rpb < 32) rpb = 32;
     by = (R + rpb - 1) / rpb;
-    // partial rows + a column reduce: straight fp32 atomics into `out` (one
-    // per column per block) measured slower — hundreds of blocks adding into
-    // the same few cache lines serialise at the memory side (VGG conv bias,
-    // 64 columns: +20 us per call)
+    // large matrices: partial rows + a column reduce. Straight fp32 atomics
+    // from the hundreds of blocks the bandwidth needs measured slower — they
+    // serialise on the same few cache lines at the memory side (VGG conv
+    // bias, 64 columns: +20 us per call)
     hipLaunchKernelGGL(colsum8_kernel, dim3(bx, by), dim3(256), 0, s, x, ws, R, C, rpb,
                        (float*)nullptr);
     col_reduce_acc(ws, (int)by, C, out, out, C, s);
