@@ -70,7 +70,7 @@ def _move_worker(rank, world, port, outdir):
     w = Worker(rank, world, torch.device("cpu"), dist.group.WORLD)
     base = {"op": "start", "job": "7", "model": "transformer_tiny", "batch": None, "seed": 7}
     # fresh on rank 0, train 2 steps
-    plan = {"actions": [dict(base, ranks=(0,), source="fresh")], "assign": {0: ("7", 2)}}
+    plan = {"actions": [dict(base, ranks=(0,), source="fresh")], "assign": {0: [("7", 2)]}}
     w.apply(plan)
     w.run(plan)
     snap = None
@@ -208,3 +208,31 @@ def test_live_replay_with_host_spill(tmp_path):
     assert s["finished"] == s["jobs"] and s["preemptions"] > 0
     assert r0["spilled"] + r1["spilled"] > 0
     assert r0["restored"] + r1["restored"] > 0
+
+
+def test_live_replay_gpu_sharing_packs_jobs():
+    """GPU sharing in the live runtime (reference --pack / dlas-gpu-pack,
+    SURVEY §2.3): with pack placement several jobs share one rank in a round
+    (run concurrently on per-job streams on a GPU) and every job finishes."""
+    import dataclasses
+
+    import bench
+    from tiresias_amd.executor import cluster_runtime as cr
+
+    jobs = bench.bench_trace(1, 6, seed=9, tiny=True)
+    for j in jobs:
+        j.spec.submit_time = 0.0                 # all queued at once -> contention
+        j.spec.gpu_mem_max = 1000.0
+    cfg = dataclasses.replace(bench.make_cfg("dlas-gpu-pack", "pack", 1, 9), pack=True)
+    seen = []
+    w = cr.Worker(0, 1, torch.device("cpu"))
+    orig = w.run
+
+    def run(plan):
+        seen.append(len(plan["assign"].get(0) or []))
+        return orig(plan)
+
+    w.run = run
+    s = cr.run_replay(cfg, jobs, 0, 1, torch.device("cpu"), worker=w, quantum=0.05)
+    assert s["finished"] == len(jobs) and s["failed"] == 0
+    assert max(seen) >= 2, "no round co-located jobs"

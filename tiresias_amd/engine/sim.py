@@ -175,9 +175,13 @@ class Simulator:
             ordered = pol.order(self.active, self.now)
             chosen = pol.select(ordered, self.cluster.free_gpus(), self.now)
             if chosen is None:
+                # with GPU sharing (pack) a GPU holds up to max_tasks_per_gpu
+                # tasks; whether a job really fits (memory, slots) is the
+                # placement's decision below
+                cap = self.max_gpus * (self.cluster.max_tasks if self.cluster.pack else 1)
                 chosen, used = [], 0
                 for j in ordered:
-                    if used + j.num_gpu <= self.max_gpus:
+                    if used + j.num_gpu <= cap:
                         chosen.append(j)
                         used += j.num_gpu
             cset = set(id(j) for j in chosen)
@@ -193,9 +197,10 @@ class Simulator:
                 if j.is_pending:
                     self._try_place(j)
             # work-conserving back-fill
-            if self.cluster.free_gpus() > 0:
+            if self.cluster.free_gpus() > 0 or self.cluster.pack:
                 for j in ordered:
-                    if j.is_pending and id(j) not in cset and j.num_gpu <= self.cluster.free_gpus():
+                    if j.is_pending and id(j) not in cset and (
+                            self.cluster.pack or j.num_gpu <= self.cluster.free_gpus()):
                         self._try_place(j)
         else:
             ordered = pol.order(self.active, self.now)

@@ -143,20 +143,21 @@ class Controller:
                 d = r["dev"]
                 self.log.device_row(self.now(), r["rank"], d.get("util_pct"), d.get("free_mb"),
                                     d.get("total_mb"), r.get("job"))
-            if not r or r.get("job") is None:
+            if not r:
                 continue
-            jid = r["job"]
-            if jid in seen:
-                continue
-            seen.add(jid)
-            self.done_iters[jid] += r["iters"]
-            rj = self.rjobs[jid]
-            if r["iters"] > 0 and r["run_s"] > 0:
-                k = (rj.model, rj.spec.num_gpu)
-                per = r["run_s"] / r["iters"]
-                self.est[k] = per if k not in self.est else 0.7 * self.est[k] + 0.3 * per
-            j = self.sched.jobs[jid]
-            j.progress = float(min(self.done_iters[jid], rj.iterations))
+            for jr in r.get("jobs") or []:
+                jid = jr["job"]
+                if jid in seen:             # gang members report the same job
+                    continue
+                seen.add(jid)
+                self.done_iters[jid] += jr["iters"]
+                rj = self.rjobs[jid]
+                if jr["iters"] > 0 and jr["run_s"] > 0:
+                    k = (rj.model, rj.spec.num_gpu)
+                    per = jr["run_s"] / jr["iters"]
+                    self.est[k] = per if k not in self.est else 0.7 * self.est[k] + 0.3 * per
+                j = self.sched.jobs[jid]
+                j.progress = float(min(self.done_iters[jid], rj.iterations))
 
     # ---------------------------------------------------------------- submission
     def _poll_spool(self) -> None:
@@ -257,8 +258,9 @@ class Controller:
                     act["old"] = old
                 self.holders[j.job_id] = ranks
                 actions.append(act)
-        # assignments: running jobs -> iterations this round
-        assign: Dict[int, Tuple[str, int]] = {}
+        # assignments: running jobs -> iterations this round; with GPU sharing
+        # (pack placement) a rank can carry several jobs, run concurrently
+        assign: Dict[int, List[Tuple[str, int]]] = {}
         for j in s.active:
             if not j.is_running:
                 continue
@@ -269,7 +271,9 @@ class Controller:
             n = max(1, int(round(self.quantum / self._iter_est(rj.model, j.num_gpu))))
             n = min(n, left)
             for r in gang_ranks(j.allocation, self.gpn):
-                assign[r] = (j.job_id, n)
+                assign.setdefault(r, []).append((j.job_id, n))
+        for r in assign:                      # same order on every rank (gang collectives)
+            assign[r].sort()
         self.round += 1
         stop = not s.active and s.reader.remaining() == 0
         if self.spool is not None:
@@ -293,6 +297,7 @@ class Worker:
         self.device = device
         self.world_pg = world_pg
         self.trainers: Dict[str, Trainer] = {}
+        self.streams: Dict[str, object] = {}     # per-job HIP streams for co-located jobs
         self.groups: Dict[Tuple[int, ...], object] = {}
         self.use_graph = use_graph
         self.spilled_bytes = 0
@@ -337,6 +342,7 @@ class Worker:
                     pg = dist.new_group(list(a["ranks"]), backend=self.gang_backend)
                     self.groups[tuple(a["ranks"])] = pg
             elif op == "drop":
+                self.streams.pop(a["job"], None)
                 t = self.trainers.pop(a["job"], None)
                 if t is not None:
                     t.release()
@@ -400,25 +406,54 @@ class Worker:
         return None
 
     def run(self, plan: dict) -> dict:
-        a = plan["assign"].get(self.rank)
-        if a is None:
-            return {"rank": self.rank, "job": None, "dev": self._dev_sample()}
-        jid, n = a
-        t = self.trainers[jid]
+        """Run this rank's share of the round. One job: its ``n`` steps back
+        to back. Several (GPU sharing): the jobs' steps interleaved in job-id
+        order, each job on its own HIP stream so their kernels overlap on the
+        device; every job is charged the round's wall time (co-location
+        slowdown is real, measured time)."""
+        jobs = plan["assign"].get(self.rank) or []
+        if not jobs:
+            return {"rank": self.rank, "job": None, "jobs": [], "dev": self._dev_sample()}
+        cuda = self.device.type == "cuda"
         t0 = time.perf_counter()
-        for _ in range(n):
-            t.step()
-        if self.device.type == "cuda":
+        if len(jobs) == 1:
+            jid, n = jobs[0]
+            t = self.trainers[jid]
+            for _ in range(n):
+                t.step()
+        else:
+            streams = [self._stream(jid) if cuda else None for jid, _ in jobs]
+            for i in range(max(n for _, n in jobs)):
+                for (jid, n), st in zip(jobs, streams):
+                    if i >= n:
+                        continue
+                    if st is None:
+                        self.trainers[jid].step()
+                    else:
+                        with torch.cuda.stream(st):
+                            self.trainers[jid].step()
+        if cuda:
             torch.cuda.synchronize(self.device)
         dt = time.perf_counter() - t0
-        return {"rank": self.rank, "job": jid, "iters": n, "run_s": dt,
-                "loss": float(t.last_loss) if t.last_loss is not None else None,
-                "dev": self._dev_sample()}
+        reps = []
+        for jid, n in jobs:
+            t = self.trainers[jid]
+            reps.append({"job": jid, "iters": n, "run_s": dt,
+                         "loss": float(t.last_loss) if t.last_loss is not None else None})
+        return {"rank": self.rank, "job": jobs[0][0], "jobs": reps, "dev": self._dev_sample()}
+
+    def _stream(self, jid: str):
+        st = self.streams.get(jid)
+        if st is None:
+            st = torch.cuda.Stream(self.device)
+            self.streams[jid] = st
+        return st
 
     def clear(self):
         for t in self.trainers.values():
             t.release()
         self.trainers.clear()
+        self.streams.clear()
 
 
 class _HostEngine:
