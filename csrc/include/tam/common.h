@@ -83,6 +83,15 @@ __device__ __forceinline__ int xcd_remap(int orig, int nwg) {
 
 __device__ __forceinline__ float sigmoidf_(float x) { return 1.f / (1.f + __expf(-x)); }
 
+// Zero `bytes` at `p` on stream `s` with a kernel (16-B vector stores).
+// Used instead of hipMemsetAsync everywhere on the compute path: memset
+// nodes in replayed hipGraphs were measured to race with the kernel nodes
+// that follow them (ResNet-50 loss diverged only under graph replay with the
+// device idle between steps); a kernel node is ordered like any other.
+void zero_async(void* p, size_t bytes, hipStream_t s);
+// rows x cols fp32 block with row pitch ld (floats)
+void zero_async_2d(float* p, long ld, int cols, int rows, hipStream_t s);
+
 }  // namespace tam
 
 #define TAM_HIP_CHECK(expr)                                                    \

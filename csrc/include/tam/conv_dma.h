@@ -611,7 +611,7 @@ inline bool launch_conv_wgrad_dma(const bf16_t* dy, const bf16_t* x, float* dw, 
   if (splits < 1) splits = 1;
   int sps = (nsteps + splits - 1) / splits;
   splits = (nsteps + sps - 1) / sps;
-  if (mode == 0) TAM_HIP_CHECK(hipMemsetAsync(dw, 0, (size_t)g.K * ncols * sizeof(float), s));
+  if (mode == 0) zero_async(dw, (size_t)g.K * ncols * sizeof(float), s);
   const int PQ = g.P * g.Q;
   WGArgs a{dy, x, dw, ncols, g.K, g.C, g.H, g.W, g.P, g.Q, g.S, g.stride, g.pad, (int)Mred, sps,
            64 / PQ, (64 % PQ) / g.Q, (64 % PQ) % g.Q, splits > 1 ? 1 : 0};

@@ -61,10 +61,9 @@ inline void prepare_split(Epi& ep, int splits, int M, int N, hipStream_t s) {
   if (splits <= 1) return;
   if (ep.mode == 0) {
     if (ep.ldc == N) {
-      TAM_HIP_CHECK(hipMemsetAsync(ep.c, 0, (size_t)M * N * sizeof(float), s));
+      zero_async(ep.c, (size_t)M * N * sizeof(float), s);
     } else {
-      TAM_HIP_CHECK(hipMemset2DAsync(ep.c, (size_t)ep.ldc * sizeof(float), 0,
-                                     (size_t)N * sizeof(float), M, s));
+      zero_async_2d((float*)ep.c, ep.ldc, N, M, s);
     }
   }
   ep.mode = 2;

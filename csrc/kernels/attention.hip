@@ -368,7 +368,7 @@ void attn_backward(const bf16_t* q, const bf16_t* k, const bf16_t* v, const bf16
   hipLaunchKernelGGL(attn_delta_kernel, dim3((rows + 3) / 4), dim3(256), 0, s, o, dout, delta, B, H,
                      Sq, o_stride);
   const long nq = (long)B * Sq * H * AD;
-  TAM_HIP_CHECK(hipMemsetAsync(dq_acc, 0, nq * sizeof(float), s));
+  zero_async(dq_acc, nq * sizeof(float), s);
   dim3 grid((Sk + AT - 1) / AT, B * H);
   hipLaunchKernelGGL(attn_bwd_kernel, grid, dim3(256), 0, s, q, k, v, dout, lse, delta, dk, dv,
                      dq_acc, H, Sq, Sk, q_stride, kv_stride, o_stride, causal, scale, kv_len);

@@ -84,7 +84,7 @@ void conv_dgrad(const bf16_t* dy, const bf16_t* w, const bf16_t* wt, const ConvG
         else ok = ok && conv_dma_pick_bn(cls[i].M, cls[i].Ng, cls[i].Kd, 1) != 0;
       }
     if (ok) {
-      if (empty) TAM_HIP_CHECK(hipMemsetAsync(ep.c, 0, (size_t)M * g.C * sizeof(bf16_t), s));
+      if (empty) zero_async(ep.c, (size_t)M * g.C * sizeof(bf16_t), s);
       for (int i = 0; i < g.stride * g.stride; ++i)
         if (cls[i].ntaps) launch_conv_dma(cls[i], ep, s, g_conv_dma == 3 ? 2 : 1);
       return;

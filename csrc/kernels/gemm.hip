@@ -37,6 +37,49 @@ void gemm_force(int cfg, int splits) { g_force_cfg = cfg; g_force_splits = split
 static int g_dma = 0, g_dma_cfg = -1;
 void gemm_dma_policy(int policy, int cfg) { g_dma = policy; g_dma_cfg = cfg; }
 
+__global__ void __launch_bounds__(256) zero_kernel(uint4* __restrict__ p16, long n16,
+                                                   unsigned char* __restrict__ tail, int ntail) {
+  const long stride = (long)gridDim.x * blockDim.x;
+  for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < n16; i += stride)
+    p16[i] = make_uint4(0u, 0u, 0u, 0u);
+  if (blockIdx.x == 0 && (int)threadIdx.x < ntail) tail[threadIdx.x] = 0;
+}
+
+__global__ void __launch_bounds__(256) zero2d_kernel(float* __restrict__ p, long ld, int cols,
+                                                     long total) {
+  const long stride = (long)gridDim.x * blockDim.x;
+  for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += stride)
+    p[(i / cols) * ld + i % cols] = 0.f;
+}
+
+void zero_async_2d(float* p, long ld, int cols, int rows, hipStream_t s) {
+  const long total = (long)cols * rows;
+  if (total <= 0) return;
+  long blocks = (total + 255) / 256;
+  blocks = blocks > 4096 ? 4096 : blocks;
+  hipLaunchKernelGGL(zero2d_kernel, dim3((unsigned)blocks), dim3(256), 0, s, p, ld, cols, total);
+}
+
+void zero_async(void* p, size_t bytes, hipStream_t s) {
+  if (bytes == 0) return;
+  unsigned char* b = (unsigned char*)p;
+  // unaligned head (never hit by torch allocations) handled as a tail launch
+  const size_t head = (16 - ((uintptr_t)b & 15)) & 15;
+  if (head) {
+    const int h = (int)(head < bytes ? head : bytes);
+    hipLaunchKernelGGL(zero_kernel, dim3(1), dim3(256), 0, s, (uint4*)nullptr, 0L, b, h);
+    b += h;
+    bytes -= h;
+    if (!bytes) return;
+  }
+  const long n16 = (long)(bytes / 16);
+  int ntail = (int)(bytes % 16);
+  long blocks = (n16 + 255) / 256;
+  blocks = blocks < 1 ? 1 : blocks > 4096 ? 4096 : blocks;
+  hipLaunchKernelGGL(zero_kernel, dim3((unsigned)blocks), dim3(256), 0, s, (uint4*)b, n16,
+                     b + n16 * 16, ntail);
+}
+
 void gemm(const bf16_t* A, long lda, bool ak, const bf16_t* B, long ldb, bool bk, int M, int N,
           int K, Epi ep, bool allow_split, hipStream_t s) {
   gemm_select(A, lda, ak, B, ldb, bk, M, N, K, ep, allow_split, s, g_dma ? 2 : 0);
