@@ -89,9 +89,59 @@ def bench_trace(n_gpus: int, jobs_per_gpu: int, seed: int, median_s: float = 0.3
     return jobs
 
 
-def make_cfg(policy: str, scheme: str, n_gpus: int, seed: int) -> SimConfig:
-    return SimConfig(schedule=policy, scheme=scheme, num_queue=2, queue_limits=[1.0], gittins_delta=1.0,
-                     solve_starvation=0.0, seed=seed, ckpt_policy="none",
+def scenario_trace(name: str, n_gpus: int, seed: int, tiny: bool = False):
+    """The other BASELINE.json configs as fixed job sets on the same runtime:
+
+    * ``resnet4``  -- 4 concurrent ResNet-50 DDP jobs, each on n/4 GPUs (1
+      GPU each when n < 4), all submitted at t=0 (config 2);
+    * ``skew``     -- mixed ResNet-50 / VGG-16 multi-GPU gangs arriving
+      together, so placement (consolidated vs spread) matters (config 3);
+    * ``seq``      -- Transformer-base + GNMT jobs with staggered arrivals, for
+      Gittins priority with preemption spilling state to host (config 4).
+    """
+    rng = random.Random(seed)
+    rows = []
+    if name == "resnet4":
+        g = max(1, n_gpus // 4)
+        rows = [("resnet50", g, 0.0, 60) for _ in range(4)]
+    elif name == "skew":
+        sizes = [g for g in (2, 4, 8) if g <= n_gpus] or [1]
+        t = 0.0
+        for i in range(4 * n_gpus):
+            m = "vgg16" if i % 2 else "resnet50"
+            rows.append((m, rng.choice(sizes), round(t, 4), rng.choice((20, 40, 80))))
+            t += rng.expovariate(4.0)
+    elif name == "seq":
+        t = 0.0
+        for i in range(4 * n_gpus):
+            m = "transformer" if i % 2 else "gnmt"
+            g = rng.choice([g for g in (1, 1, 1, 2, 4) if g <= n_gpus])
+            rows.append((m, g, round(t, 4), int(min(400, max(8, rng.lognormvariate(math.log(40), 1.2))))))
+            t += rng.expovariate(3.0)
+    else:
+        raise SystemExit(f"unknown scenario {name}")
+    jobs = []
+    for i, (m, g, t, iters) in enumerate(rows):
+        spec = JobSpec(job_id=str(i), submit_time=t, duration=iters * TRACE_ITER_S[m], num_gpu=g,
+                       model=m, iterations=iters, gpu_util_avg=90.0, gpu_util_max=99.0)
+        jobs.append(ReplayJob(spec=spec, model=TINY[m] if tiny else m, iterations=iters))
+    return jobs
+
+
+# scenario -> (policy, placement, ckpt policy, baseline policy, baseline placement,
+#              2D-LAS queue-0 limit in GPU-seconds; resnet4 is "no preemption")
+SCENARIOS = {
+    "trace": ("dlas-gpu", "tiresias", "none", "fifo", "yarn", 1.0),
+    "resnet4": ("dlas-gpu", "tiresias", "none", "fifo", "yarn", 1e9),
+    "skew": ("dlas-gpu", "tiresias", "none", "dlas-gpu", "random", 1.0),
+    "seq": ("gittins", "tiresias", "host", "fifo", "yarn", 1.0),
+}
+
+
+def make_cfg(policy: str, scheme: str, n_gpus: int, seed: int, ckpt: str = "none",
+             qlimit: float = 1.0) -> SimConfig:
+    return SimConfig(schedule=policy, scheme=scheme, num_queue=2, queue_limits=[qlimit], gittins_delta=1.0,
+                     solve_starvation=0.0, seed=seed, ckpt_policy=ckpt,
                      cluster=ClusterSpec(num_switch=1, num_node_p_switch=1, num_gpu_p_node=n_gpus,
                                          num_cpu_p_node=max(128, 16 * n_gpus),
                                          mem_p_node=max(512, 64 * n_gpus), gpu_memory_mb=288 * 1024))
@@ -102,10 +152,14 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=2)
     ap.add_argument("--warmup", type=int, default=1)
-    ap.add_argument("--policy", default="dlas-gpu")
-    ap.add_argument("--placement", default="tiresias")
-    ap.add_argument("--baseline-policy", default="fifo")
-    ap.add_argument("--baseline-placement", default="yarn")
+    ap.add_argument("--scenario", default="trace", choices=sorted(SCENARIOS),
+                    help="trace: the headline Philly-shaped replay; resnet4 / skew / seq: "
+                         "BASELINE.json configs 2-4 (policy defaults follow the scenario)")
+    ap.add_argument("--policy", default=None)
+    ap.add_argument("--placement", default=None)
+    ap.add_argument("--ckpt", default=None, help="preemption state policy: none (HBM) | host")
+    ap.add_argument("--baseline-policy", default=None)
+    ap.add_argument("--baseline-placement", default=None)
     ap.add_argument("--no-baseline", action="store_true")
     ap.add_argument("--jobs-per-gpu", type=int, default=16)
     ap.add_argument("--quantum", type=float, default=0.1)
@@ -115,6 +169,12 @@ def main():
                     help="disable hipGraph capture of 1-GPU jobs' fwd+bwd (eager launches)")
     ap.add_argument("--out", default=None, help="directory for job.csv / summary.json of the last step")
     a = ap.parse_args()
+    pol, plc, ck, bpol, bplc, qlim = SCENARIOS[a.scenario]
+    a.policy = a.policy or pol
+    a.placement = a.placement or plc
+    a.ckpt = a.ckpt or ck
+    a.baseline_policy = a.baseline_policy or bpol
+    a.baseline_placement = a.baseline_placement or bplc
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
@@ -142,8 +202,11 @@ def main():
 
         _lib.load(required=True)
 
-    jobs = bench_trace(n, a.jobs_per_gpu, a.seed, tiny=not use_cuda)
-    cfg = make_cfg(a.policy, a.placement, n, a.seed)
+    if a.scenario == "trace":
+        jobs = bench_trace(n, a.jobs_per_gpu, a.seed, tiny=not use_cuda)
+    else:
+        jobs = scenario_trace(a.scenario, n, a.seed, tiny=not use_cuda)
+    cfg = make_cfg(a.policy, a.placement, n, a.seed, a.ckpt, qlim)
     worker = Worker(rank, world, device, world_pg, use_graph=use_cuda and not a.no_graph)
 
     def sync():
@@ -173,7 +236,7 @@ def main():
 
     base = None
     if not a.no_baseline:
-        bcfg = make_cfg(a.baseline_policy, a.baseline_placement, n, a.seed)
+        bcfg = make_cfg(a.baseline_policy, a.baseline_placement, n, a.seed, a.ckpt, qlim)
         base = replay(bcfg)
 
     if rank == 0:
@@ -197,6 +260,8 @@ def main():
                 "global_batch": "per job: per-GPU batch x gang size (64 img / 32 img / 32x128 tok / 64x50 tok)",
                 "seq_len": "128 (transformer), 50 (gnmt)",
                 "parallelism": f"dp (gang DDP over RCCL), {n} GPU cluster",
+                "scenario": a.scenario,
+                "ckpt": a.ckpt,
                 "trace_jobs": len(jobs),
                 "hip_graph_1gpu_jobs": bool(use_cuda and not a.no_graph),
                 "jobs_per_gpu": a.jobs_per_gpu,

@@ -138,3 +138,25 @@ def test_comm_profiler_gloo(tmp_path):
     d = torch.load(tmp_path / "comm.pt", weights_only=False)
     assert set(d["res"]) == {"consolidated", "spread"} and len(d["res"]["consolidated"]) == 2
     assert d["cls"]["vgg16"]["consolidated_s"] > d["cls"]["resnet50"]["consolidated_s"]
+
+
+@pytest.mark.parametrize("scenario", ["resnet4", "skew", "seq"])
+@pytest.mark.parametrize("n", [1, 2, 8])
+def test_bench_scenarios_fit_cluster(scenario, n):
+    """bench.py --scenario presets (BASELINE.json configs 2-4): every job fits
+    the n-GPU node, ids are unique, arrivals are ordered, and the resnet4
+    preset disables LAS demotion (no preemption)."""
+    import bench
+
+    jobs = bench.scenario_trace(scenario, n, 2019)
+    assert jobs and all(1 <= j.spec.num_gpu <= n for j in jobs)
+    assert len({j.spec.job_id for j in jobs}) == len(jobs)
+    ts = [j.spec.submit_time for j in jobs]
+    assert ts == sorted(ts)
+    pol, plc, ck, bpol, bplc, qlim = bench.SCENARIOS[scenario]
+    cfg = bench.make_cfg(pol, plc, n, 1, ck, qlim)
+    assert cfg.queue_limits == [qlim]
+    if scenario == "resnet4":
+        assert qlim >= 1e6 and len(jobs) == 4
+    if scenario == "seq":
+        assert pol == "gittins" and ck == "host"
