@@ -1,16 +1,13 @@
 #!/bin/bash
-# Per-model rocprofv3 kernel stats (one run per model; trace CSVs deleted).
-# usage: tools/prof_models.sh <outdir-name> [models...]
-set -u
-ROOT="${GRAFT_REPO_ROOT:-$(cd "$(dirname "$0")/.." && pwd)}"
-name=$1; shift
-cd /tmp && export TMPDIR=/tmp
-for m in "$@"; do
-  out="$ROOT/gpurun_out/$name/$m"
-  mkdir -p "$out"
-  timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$out" -o run -- \
-    python3 "$ROOT/tools/bench_models.py" --models "$m" --steps 10 --warmup 3 > "$out/log.txt" 2>&1
-  rc=$?
-  find "$out" -type f -name "*trace*.csv" -delete
-  if [ $rc -ne 0 ]; then echo "model $m rc=$rc"; exit $rc; fi
+# Per-model rocprofv3 kernel statistics (one run per model, eager steps).
+# Run on the GPU box from the repo root:  bash tools/prof_models.sh [models...]
+set -o pipefail
+export TMPDIR=/tmp
+models="${*:-resnet50 vgg16 transformer gnmt}"
+for m in $models; do
+  timeout -k 10 180 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof_$m -o run -- \
+    python3 tools/bench_models.py --models $m --steps 5 --warmup 2 > gpurun_out/log_prof_$m.txt 2>&1 || { tail -20 gpurun_out/log_prof_$m.txt; exit 1; }
 done
+# keep only the summaries (the full traces exceed what gpurun copies back)
+find gpurun_out -path "*/prof_*" -type f ! -name "*_stats.csv" -delete
+find gpurun_out -name "*kernel_stats.csv"
