@@ -31,3 +31,33 @@ def test_probe_real_gpu(gpu):
         min(x.total_mb for x in devs))
     m = D.DeviceMonitor(period=0.0)
     assert m.sample()[0].index == 0
+
+
+def test_background_monitor_never_blocks(monkeypatch):
+    """Worker-side monitor: the amd-smi probe runs on a daemon thread;
+    sample_own() only reads the cache (a slow CLI cannot stall a round)."""
+    import threading
+    import time
+
+    started = threading.Event()
+
+    def slow_smi():
+        started.set()
+        time.sleep(0.5)
+        return {0: {"util_pct": 50.0, "vram_used_mb": 1.0}}
+
+    monkeypatch.setattr(D, "smi_utilization", slow_smi)
+    m = D.DeviceMonitor(period=10.0, device_index=None).start()
+    assert started.wait(2.0)
+    t0 = time.perf_counter()
+    assert m.sample_own() is None                 # no device index / CPU host
+    assert time.perf_counter() - t0 < 0.05
+    m.stop()
+
+
+@pytest.mark.gpu
+def test_monitor_sample_own_gpu(gpu):
+    m = D.DeviceMonitor(period=5.0, device_index=0).start()
+    d = m.sample_own()
+    assert d is not None and d.index == 0 and 0 < d.free_mb <= d.total_mb
+    m.stop()

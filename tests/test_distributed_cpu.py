@@ -236,3 +236,23 @@ def test_live_replay_gpu_sharing_packs_jobs():
     s = cr.run_replay(cfg, jobs, 0, 1, torch.device("cpu"), worker=w, quantum=0.05)
     assert s["finished"] == len(jobs) and s["failed"] == 0
     assert max(seen) >= 2, "no round co-located jobs"
+
+
+def test_round_ends_at_next_arrival():
+    """A 1-GPU job's round stops at the first step boundary after the next
+    trace arrival (plan["deadline"]) and reports the steps it really ran;
+    without a deadline it runs its full assignment."""
+    import time
+
+    from tiresias_amd.executor import cluster_runtime as cr
+
+    w = cr.Worker(0, 1, torch.device("cpu"))
+    start = {"op": "start", "job": "1", "model": "resnet_tiny", "batch": None, "seed": 1,
+             "ranks": (0,), "source": "fresh"}
+    w.apply({"actions": [start], "assign": {}})
+    r = w.run({"actions": [], "assign": {0: [("1", 5)]}, "deadline": time.perf_counter() - 1.0})
+    assert r["jobs"][0]["iters"] == 1
+    r = w.run({"actions": [], "assign": {0: [("1", 3)]}, "deadline": None})
+    assert r["jobs"][0]["iters"] == 3
+    r = w.run({"actions": [], "assign": {0: [("1", 2)]}, "deadline": time.perf_counter() + 60})
+    assert r["jobs"][0]["iters"] == 2

@@ -22,6 +22,7 @@ from __future__ import annotations
 import json
 import shutil
 import subprocess
+import threading
 import time
 from dataclasses import dataclass
 from typing import Dict, List, Optional
@@ -131,13 +132,24 @@ def probe_cluster_spec(base: Optional[ClusterSpec] = None) -> ClusterSpec:
 
 
 class DeviceMonitor:
-    """Samples the local GPUs at most every ``period`` seconds."""
+    """Samples the local GPUs at most every ``period`` seconds.
 
-    def __init__(self, period: float = 5.0, with_smi: bool = True):
+    ``sample()`` probes synchronously (tools, one-off queries). A training
+    worker instead calls ``start()`` once and then ``sample_own()`` every
+    round: the ``amd-smi`` subprocess (hundreds of ms) runs on a daemon
+    thread and only HIP's mem-info of the worker's OWN device is read inline
+    (microseconds, and no HIP context is created on the other GPUs), so
+    monitoring never stalls the scheduling loop or the GPU."""
+
+    def __init__(self, period: float = 5.0, with_smi: bool = True, device_index: Optional[int] = None):
         self.period = period
         self.with_smi = with_smi
+        self.device_index = device_index
         self._last = 0.0
         self._cache: List[DeviceInfo] = []
+        self._smi: Dict[int, dict] = {}
+        self._thread = None
+        self._stop = threading.Event()
 
     def sample(self, force: bool = False) -> List[DeviceInfo]:
         now = time.monotonic()
@@ -145,3 +157,32 @@ class DeviceMonitor:
             self._cache = probe_devices(self.with_smi)
             self._last = now
         return self._cache
+
+    # ------------------------------------------------ background (workers)
+    def start(self) -> "DeviceMonitor":
+        if self.with_smi and self._thread is None:
+            self._thread = threading.Thread(target=self._loop, name="tam-smi", daemon=True)
+            self._thread.start()
+        return self
+
+    def _loop(self):
+        while not self._stop.is_set():
+            try:
+                self._smi = smi_utilization()
+            except Exception:                     # a missing/broken CLI is not fatal
+                self._smi = {}
+            self._stop.wait(self.period)
+
+    def stop(self):
+        self._stop.set()
+
+    def sample_own(self) -> Optional[DeviceInfo]:
+        import torch
+
+        i = self.device_index
+        if i is None or not torch.cuda.is_available():
+            return None
+        free, total = torch.cuda.mem_get_info(i)
+        s = self._smi.get(i, {})
+        return DeviceInfo(i, "", total / 2 ** 20, free / 2 ** 20, s.get("util_pct"),
+                          s.get("vram_used_mb"))

@@ -285,7 +285,12 @@ class Controller:
         if not assign and not stop:
             # idle cluster: sleep until the next arrival instead of spinning
             wait = max(0.0, min(self.quantum, s.reader.next_time() - self.now()))
-        return {"round": self.round, "actions": actions, "assign": assign, "stop": stop, "wait": wait}
+        # next trace arrival as an absolute host-clock time: 1-GPU jobs end the
+        # round at the first step boundary after it (Worker._run_until)
+        nxt = s.reader.next_time()
+        deadline = self.t0 + nxt if math.isfinite(nxt) else None
+        return {"round": self.round, "actions": actions, "assign": assign, "stop": stop, "wait": wait,
+                "deadline": deadline}
 
 
 class Worker:
@@ -309,7 +314,7 @@ class Worker:
         if device.type == "cuda" and monitor_period > 0:
             from ..cluster.device import DeviceMonitor
 
-            self.monitor = DeviceMonitor(period=monitor_period)
+            self.monitor = DeviceMonitor(period=monitor_period, device_index=device.index).start()
 
     def _ckpt_engine(self):
         if self._engine is None:
@@ -399,11 +404,10 @@ class Worker:
         if now - self._mon_t < self.monitor.period:
             return None
         self._mon_t = now
-        for d in self.monitor.sample(force=True):
-            if d.index == self.device.index:
-                return {"util_pct": d.util_pct, "free_mb": round(d.free_mb, 1),
-                        "total_mb": round(d.total_mb, 1)}
-        return None
+        d = self.monitor.sample_own()
+        if d is None:
+            return None
+        return {"util_pct": d.util_pct, "free_mb": round(d.free_mb, 1), "total_mb": round(d.total_mb, 1)}
 
     def run(self, plan: dict) -> dict:
         """Run this rank's share of the round. One job: its ``n`` steps back
@@ -419,8 +423,14 @@ class Worker:
         if len(jobs) == 1:
             jid, n = jobs[0]
             t = self.trainers[jid]
-            for _ in range(n):
-                t.step()
+            deadline = plan.get("deadline")
+            if deadline is None or t.ddp is not None:
+                # gang members must run the same step count (collectives)
+                for _ in range(n):
+                    t.step()
+            else:
+                n = self._run_until(t, n, deadline, cuda)
+                jobs = [(jid, n)]
         else:
             streams = [self._stream(jid) if cuda else None for jid, _ in jobs]
             for i in range(max(n for _, n in jobs)):
@@ -441,6 +451,25 @@ class Worker:
             reps.append({"job": jid, "iters": n, "run_s": dt,
                          "loss": float(t.last_loss) if t.last_loss is not None else None})
         return {"rank": self.rank, "job": jobs[0][0], "jobs": reps, "dev": self._dev_sample()}
+
+    def _run_until(self, t: Trainer, n: int, deadline: float, cuda: bool) -> int:
+        """Up to ``n`` steps of a 1-GPU job, ending the round at the first step
+        boundary after ``deadline`` (the next trace arrival, host monotonic
+        clock shared by every rank of the node) so the scheduler can react to
+        it within ~one step instead of up to a whole quantum. One step stays
+        queued ahead of the one being waited on, so the GPU never drains."""
+        prev = None
+        for i in range(n):
+            t.step()
+            if cuda:
+                ev = torch.cuda.Event()
+                ev.record()
+                if prev is not None:
+                    prev.synchronize()
+                prev = ev
+            if time.perf_counter() >= deadline and i + 1 < n:
+                return i + 1
+        return n
 
     def _stream(self, jid: str):
         st = self.streams.get(jid)

@@ -120,10 +120,24 @@ class Trainer:
 
     def _graph_step(self) -> torch.Tensor:
         if self._graph is None:
-            # capture fwd+bwd once (capture itself runs no kernels), then replay
+            # capture fwd+bwd once (capture itself runs no kernels), then
+            # replay. Driven directly rather than through torch.cuda.graph(),
+            # whose entry does gc.collect() + empty_cache(): in a long-lived
+            # worker holding many jobs that costs ~20 ms and hands cached
+            # blocks back to the driver, a fixed cost every job would pay
+            # on its first graph step (JCT of short jobs)
+            s = self._side or torch.cuda.Stream(self.device)
+            self._side = s
+            cur = torch.cuda.current_stream(self.device)
+            s.wait_stream(cur)
             g = torch.cuda.CUDAGraph()
-            with torch.cuda.graph(g):
-                self._g_loss = self._fwd_bwd()
+            with torch.cuda.stream(s):
+                g.capture_begin()
+                try:
+                    self._g_loss = self._fwd_bwd()
+                finally:
+                    g.capture_end()
+            cur.wait_stream(s)
             self._graph = g
         self._graph.replay()
         return self._g_loss
