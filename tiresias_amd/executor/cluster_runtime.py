@@ -261,6 +261,7 @@ class Controller:
         # assignments: running jobs -> iterations this round; with GPU sharing
         # (pack placement) a rank can carry several jobs, run concurrently
         assign: Dict[int, List[Tuple[str, int]]] = {}
+        nxt, now = s.reader.next_time(), self.now()
         for j in s.active:
             if not j.is_running:
                 continue
@@ -268,7 +269,13 @@ class Controller:
             left = rj.iterations - self.done_iters[j.job_id]
             if left <= 0:
                 continue
-            n = max(1, int(round(self.quantum / self._iter_est(rj.model, j.num_gpu))))
+            est = self._iter_est(rj.model, j.num_gpu)
+            n = max(1, int(round(self.quantum / est)))
+            if j.num_gpu > 1 and math.isfinite(nxt):
+                # gangs cannot cut a round at the arrival on their own (every
+                # member must run the same step count), so size their share
+                # to end there: the 1-GPU ranks then do not idle waiting
+                n = min(n, max(1, int(math.ceil((nxt - now) / est))))
             n = min(n, left)
             for r in gang_ranks(j.allocation, self.gpn):
                 assign.setdefault(r, []).append((j.job_id, n))
@@ -287,7 +294,6 @@ class Controller:
             wait = max(0.0, min(self.quantum, s.reader.next_time() - self.now()))
         # next trace arrival as an absolute host-clock time: 1-GPU jobs end the
         # round at the first step boundary after it (Worker._run_until)
-        nxt = s.reader.next_time()
         deadline = self.t0 + nxt if math.isfinite(nxt) else None
         return {"round": self.round, "actions": actions, "assign": assign, "stop": stop, "wait": wait,
                 "deadline": deadline}
