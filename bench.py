@@ -129,19 +129,24 @@ def scenario_trace(name: str, n_gpus: int, seed: int, tiny: bool = False):
 
 
 # scenario -> (policy, placement, ckpt policy, baseline policy, baseline placement,
-#              2D-LAS queue-0 limit in GPU-seconds; resnet4 is "no preemption")
+#              2D-LAS queue-0 limit in GPU-seconds (resnet4 is "no preemption"),
+#              GPU sharing when no GPU is free)
 SCENARIOS = {
-    "trace": ("dlas-gpu", "tiresias", "none", "fifo", "yarn", 1.0),
-    "resnet4": ("dlas-gpu", "tiresias", "none", "fifo", "yarn", 1e9),
-    "skew": ("dlas-gpu", "tiresias", "none", "dlas-gpu", "random", 1.0),
-    "seq": ("gittins", "tiresias", "host", "fifo", "yarn", 1.0),
+    "trace": ("dlas-gpu", "tiresias", "none", "fifo", "yarn", 1.0, True),
+    "resnet4": ("dlas-gpu", "tiresias", "none", "fifo", "yarn", 1e9, False),
+    "skew": ("dlas-gpu", "tiresias", "none", "dlas-gpu", "random", 1.0, False),
+    "seq": ("gittins", "tiresias", "host", "fifo", "yarn", 1.0, False),
 }
+# measured in-process co-run throughput of every model pair (tools/measure_stream_sharing.py)
+SHARING_TABLE = os.path.join(ROOT, "profiles", "stream_sharing_mi355x.json")
 
 
 def make_cfg(policy: str, scheme: str, n_gpus: int, seed: int, ckpt: str = "none",
-             qlimit: float = 1.0) -> SimConfig:
+             qlimit: float = 1.0, share: bool = False) -> SimConfig:
     return SimConfig(schedule=policy, scheme=scheme, num_queue=2, queue_limits=[qlimit], gittins_delta=1.0,
-                     solve_starvation=0.0, seed=seed, ckpt_policy=ckpt,
+                     solve_starvation=0.0, seed=seed, ckpt_policy=ckpt, pack=share,
+                     max_tasks_per_gpu=2 if share else 3,
+                     interference_table=SHARING_TABLE if share else "",
                      cluster=ClusterSpec(num_switch=1, num_node_p_switch=1, num_gpu_p_node=n_gpus,
                                          num_cpu_p_node=max(128, 16 * n_gpus),
                                          mem_p_node=max(512, 64 * n_gpus), gpu_memory_mb=288 * 1024))
@@ -161,6 +166,10 @@ def main():
     ap.add_argument("--baseline-policy", default=None)
     ap.add_argument("--baseline-placement", default=None)
     ap.add_argument("--no-baseline", action="store_true")
+    ap.add_argument("--no-share", action="store_true",
+                    help="exclusive GPUs only (no co-location of 1-GPU jobs when the cluster is full)")
+    ap.add_argument("--no-exclusive-ref", action="store_true",
+                    help="skip the untimed exclusive-GPU Tiresias replay reported next to the result")
     ap.add_argument("--jobs-per-gpu", type=int, default=16)
     ap.add_argument("--quantum", type=float, default=0.1)
     ap.add_argument("--seed", type=int, default=2019)
@@ -169,7 +178,8 @@ def main():
                     help="disable hipGraph capture of 1-GPU jobs' fwd+bwd (eager launches)")
     ap.add_argument("--out", default=None, help="directory for job.csv / summary.json of the last step")
     a = ap.parse_args()
-    pol, plc, ck, bpol, bplc, qlim = SCENARIOS[a.scenario]
+    pol, plc, ck, bpol, bplc, qlim, share = SCENARIOS[a.scenario]
+    share = share and not a.no_share
     a.policy = a.policy or pol
     a.placement = a.placement or plc
     a.ckpt = a.ckpt or ck
@@ -206,7 +216,7 @@ def main():
         jobs = bench_trace(n, a.jobs_per_gpu, a.seed, tiny=not use_cuda)
     else:
         jobs = scenario_trace(a.scenario, n, a.seed, tiny=not use_cuda)
-    cfg = make_cfg(a.policy, a.placement, n, a.seed, a.ckpt, qlim)
+    cfg = make_cfg(a.policy, a.placement, n, a.seed, a.ckpt, qlim, share)
     worker = Worker(rank, world, device, world_pg, use_graph=use_cuda and not a.no_graph)
 
     def sync():
@@ -216,8 +226,14 @@ def main():
             torch.cuda.synchronize(device)
 
     def replay(c, out=None):
-        return run_replay(c, jobs, rank, world, device, ctrl_pg=ctrl_pg, world_pg=world_pg,
-                          worker=worker, quantum=a.quantum, out_dir=out)
+        t = time.perf_counter()
+        r = run_replay(c, jobs, rank, world, device, ctrl_pg=ctrl_pg, world_pg=world_pg,
+                       worker=worker, quantum=a.quantum, out_dir=out)
+        if rank == 0:                  # progress on stderr (the JSON line stays alone on stdout)
+            print(f"[bench] {c.schedule}+{c.scheme}{' share' if c.pack else ''}: avg JCT "
+                  f"{r['avg_jct']:.4f} s, makespan {r['makespan']:.3f} s, {r['finished']} jobs, "
+                  f"wall {time.perf_counter() - t:.1f} s", file=sys.stderr, flush=True)
+        return r
 
     for _ in range(a.warmup):
         replay(cfg)
@@ -238,6 +254,10 @@ def main():
     if not a.no_baseline:
         bcfg = make_cfg(a.baseline_policy, a.baseline_placement, n, a.seed, a.ckpt, qlim)
         base = replay(bcfg)
+    excl = None
+    if share and not a.no_exclusive_ref:
+        # the same Tiresias policy without GPU sharing (how much sharing buys)
+        excl = replay(make_cfg(a.policy, a.placement, n, a.seed, a.ckpt, qlim, False))
 
     if rank == 0:
         avg_jct = sum(s["avg_jct"] for s in sums) / len(sums)
@@ -265,7 +285,8 @@ def main():
                 "trace_jobs": len(jobs),
                 "hip_graph_1gpu_jobs": bool(use_cuda and not a.no_graph),
                 "jobs_per_gpu": a.jobs_per_gpu,
-                "policy": f"{a.policy} + {a.placement} placement (Tiresias)",
+                "policy": f"{a.policy} + {a.placement} placement (Tiresias)"
+                          + (" + GPU sharing when full" if share else ""),
                 "baseline": f"{a.baseline_policy} + {a.baseline_placement}",
                 "quantum_s": a.quantum,
             },
@@ -276,6 +297,9 @@ def main():
             "finished_jobs": sums[-1]["finished"],
             "baseline_avg_jct_s": round(base["avg_jct"], 4) if base else None,
             "baseline_makespan_s": round(base["makespan"], 4) if base else None,
+            "tiresias_exclusive_avg_jct_s": round(excl["avg_jct"], 4) if excl else None,
+            "tiresias_exclusive_makespan_s": round(excl["makespan"], 4) if excl else None,
+            "shared_rounds": sums[-1].get("shared_rounds"),
             "gpu_utilization": round(sums[-1]["gpu_utilization"], 4),
             "runtime_breakdown_s": sums[-1].get("runtime_breakdown"),
             "device": torch.cuda.get_device_name(device) if use_cuda else "cpu",

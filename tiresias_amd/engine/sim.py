@@ -70,7 +70,8 @@ class Simulator:
                                headroom_mb=cfg.gpu_mem_headroom_mb, virtual_nodes=cfg.virtual_nodes)
         self.placement = make_placement(scheme, rng=random.Random(cfg.seed + 1),
                                         sensitivity=SensitivityOracle(cfg.skew_threshold),
-                                        cluster_gpus_per_node=self.cluster.spec.num_gpu_p_node)
+                                        cluster_gpus_per_node=self.cluster.spec.num_gpu_p_node,
+                                        pack=pack)
         self.jobs: Dict[str, Job] = {}
         for s in specs:
             if s.job_id in self.jobs:
@@ -82,6 +83,8 @@ class Simulator:
                                   table_path=cfg.ckpt_table if cfg.ckpt_policy == "measured" else "")
         self.interf = (InterferenceModel.load(cfg.interference_table, cfg.interference)
                        if cfg.interference_table else InterferenceModel(cfg.interference))
+        self.placement.model_of = lambda jid: self.jobs[jid].spec.model or ""
+        self.placement.pair_cost = lambda a, b: self.interf.pair(a, b)
         self.now = 0.0
         self.active: List[Job] = []
         self.finished: List[Job] = []
@@ -175,18 +178,27 @@ class Simulator:
             ordered = pol.order(self.active, self.now)
             chosen = pol.select(ordered, self.cluster.free_gpus(), self.now)
             if chosen is None:
-                # with GPU sharing (pack) a GPU holds up to max_tasks_per_gpu
-                # tasks; whether a job really fits (memory, slots) is the
-                # placement's decision below
-                cap = self.max_gpus * (self.cluster.max_tasks if self.cluster.pack else 1)
                 chosen, used = [], 0
                 for j in ordered:
-                    if used + j.num_gpu <= cap:
+                    if used + j.num_gpu <= self.max_gpus:
                         chosen.append(j)
                         used += j.num_gpu
             cset = set(id(j) for j in chosen)
+            # GPU sharing (pack): the priority-ordered exclusive set above
+            # always runs; lower-priority 1-GPU jobs may additionally share
+            # GPUs, but give their slot back whenever a chosen job (e.g. a
+            # gang) cannot be placed because of them
+            extra: List[Job] = []
+            if self.cluster.pack:
+                slots = self.max_gpus * (self.cluster.max_tasks - 1)
+                for j in ordered:
+                    if len(extra) >= slots:
+                        break
+                    if id(j) not in cset and j.num_gpu == 1:
+                        extra.append(j)
+            keep = cset | set(id(j) for j in extra)
             for j in list(self.active):
-                if j.is_running and id(j) not in cset:
+                if j.is_running and id(j) not in keep:
                     self._preempt(j)
             if self.cfg.replace_all:
                 # legacy Tiresias: re-place every runnable job each event
@@ -194,6 +206,13 @@ class Simulator:
                     if j.is_running:
                         self._preempt(j, reason="replace")
             for j in chosen:
+                if j.is_pending and not self._try_place(j):
+                    for x in reversed(extra):
+                        if x.is_running:
+                            self._preempt(x, reason="unshare")
+                            if self._try_place(j):
+                                break
+            for j in extra:
                 if j.is_pending:
                     self._try_place(j)
             # work-conserving back-fill

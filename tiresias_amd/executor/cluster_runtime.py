@@ -43,10 +43,10 @@ from ..metrics.logger import MetricsLogger
 from .trainer import Trainer
 
 # nominal per-iteration seconds on one MI355X (tools/bench_models.py,
-# profiles/model_bench_r1_v6.json, hipGraph replay); refined online from the
+# profiles/model_bench_r1_v7.json, hipGraph replay); refined online from the
 # workers' measurements. They seed the Gittins prior (service distribution in
 # GPU-seconds) and the first round's iteration count of each job.
-NOMINAL_ITER_S = {"resnet50": 0.0121, "vgg16": 0.0088, "transformer": 0.0075, "gnmt": 0.0155,
+NOMINAL_ITER_S = {"resnet50": 0.0113, "vgg16": 0.0080, "transformer": 0.0072, "gnmt": 0.0155,
                   "resnet_tiny": 0.004, "vgg_tiny": 0.002, "transformer_tiny": 0.006,
                   "gnmt_tiny": 0.01}
 
@@ -152,7 +152,9 @@ class Controller:
                 seen.add(jid)
                 self.done_iters[jid] += jr["iters"]
                 rj = self.rjobs[jid]
-                if jr["iters"] > 0 and jr["run_s"] > 0:
+                # co-located rounds measure the pair, not the job: keep the
+                # solo estimate (it sizes rounds and seeds the Gittins prior)
+                if jr["iters"] > 0 and jr["run_s"] > 0 and not jr.get("shared"):
                     k = (rj.model, rj.spec.num_gpu)
                     per = jr["run_s"] / jr["iters"]
                     self.est[k] = per if k not in self.est else 0.7 * self.est[k] + 0.3 * per
@@ -390,6 +392,8 @@ class Worker:
                     # replicas that stay: rebind their DDP bucketer to the new gang
                     if self.rank in ranks and self.rank in old:
                         self.trainers[a["job"]].rebind(self._group(ranks))
+        if any(a["op"] == "drop" for a in plan["actions"]):
+            self.reclaim(64.0)
         if p2p_ops:
             for w in dist.batch_isend_irecv(p2p_ops):
                 w.wait()
@@ -439,6 +443,13 @@ class Worker:
                 jobs = [(jid, n)]
         else:
             streams = [self._stream(jid) if cuda else None for jid, _ in jobs]
+            if cuda:
+                # apply() ran on the default stream: fresh jobs' weight init
+                # and synthetic batch, restores and P2P receives are queued
+                # there; the per-job streams must not run ahead of them
+                cur = torch.cuda.current_stream(self.device)
+                for st in streams:
+                    st.wait_stream(cur)
             for i in range(max(n for _, n in jobs)):
                 for (jid, n), st in zip(jobs, streams):
                     if i >= n:
@@ -454,7 +465,7 @@ class Worker:
         reps = []
         for jid, n in jobs:
             t = self.trainers[jid]
-            reps.append({"job": jid, "iters": n, "run_s": dt,
+            reps.append({"job": jid, "iters": n, "run_s": dt, "shared": len(jobs) > 1,
                          "loss": float(t.last_loss) if t.last_loss is not None else None})
         return {"rank": self.rank, "job": jobs[0][0], "jobs": reps, "dev": self._dev_sample()}
 
@@ -484,11 +495,29 @@ class Worker:
             self.streams[jid] = st
         return st
 
+    def reclaim(self, slack_gb: float) -> bool:
+        """Return cached-but-unused HBM to the driver when more than
+        ``slack_gb`` is held. Finished jobs' hipGraph private pools stay
+        reserved by the caching allocator until empty_cache() (a pool cannot
+        be shared between jobs that may run concurrently on one GPU), so
+        without this every job's pool would accumulate. Called with a small
+        slack when the GPU is idle between arrivals and a large one after
+        drops (a full empty_cache costs milliseconds)."""
+        if self.device.type != "cuda":
+            return False
+        slack = torch.cuda.memory_reserved(self.device) - torch.cuda.memory_allocated(self.device)
+        if slack <= slack_gb * 2 ** 30:
+            return False
+        torch.cuda.synchronize(self.device)
+        torch.cuda.empty_cache()
+        return True
+
     def clear(self):
         for t in self.trainers.values():
             t.release()
         self.trainers.clear()
         self.streams.clear()
+        self.reclaim(0.0)
 
 
 class _HostEngine:
@@ -562,6 +591,7 @@ def run_replay(cfg: SimConfig, jobs: List[ReplayJob], rank: int, world: int, dev
         ctrl.start_clock()
     t_start = time.perf_counter()
     rounds = 0
+    shared = 0                                   # rounds with co-located jobs on a GPU
     # idle_s = sleeping because no job is runnable (arrival gaps), not overhead
     prof = {"plan_s": 0.0, "bcast_s": 0.0, "apply_s": 0.0, "run_s": 0.0, "idle_s": 0.0,
             "gather_s": 0.0}
@@ -576,6 +606,8 @@ def run_replay(cfg: SimConfig, jobs: List[ReplayJob], rank: int, world: int, dev
             break
         if fault and fault.get("rank") == rank and rounds >= fault.get("round", 0):
             os._exit(17)                         # simulated node/rank crash
+        if any(len(v) > 1 for v in plan["assign"].values()):
+            shared += 1
         w.apply(plan)
         td = time.perf_counter()
         rep = w.run(plan)
@@ -585,7 +617,9 @@ def run_replay(cfg: SimConfig, jobs: List[ReplayJob], rank: int, world: int, dev
         prof["apply_s"] += td - tc
         prof["run_s"] += te - td
         if plan.get("wait", 0) > 0 and rep["job"] is None:
-            time.sleep(plan["wait"])
+            tw = time.perf_counter()
+            w.reclaim(4.0)                     # idle GPU: a free moment to return dead pools
+            time.sleep(max(0.0, plan["wait"] - (time.perf_counter() - tw)))
         tf = time.perf_counter()
         prof["idle_s"] += tf - te
         if distributed:
@@ -608,7 +642,7 @@ def run_replay(cfg: SimConfig, jobs: List[ReplayJob], rank: int, world: int, dev
         torch.cuda.synchronize(device)
     if ctrl:
         s = ctrl.sched.summary()
-        s.update(rounds=rounds, replay_wall_s=wall, iter_est={f"{k[0]}x{k[1]}": v for k, v in ctrl.est.items()},
+        s.update(rounds=rounds, shared_rounds=shared, replay_wall_s=wall, iter_est={f"{k[0]}x{k[1]}": v for k, v in ctrl.est.items()},
                  runtime_breakdown={k: round(v, 4) for k, v in prof.items()})
         log.close()
         return s

@@ -59,6 +59,13 @@ class Trainer:
         self._warm = 0           # eager steps done before graph capture
         self._side = None
         self.last_loss: Optional[torch.Tensor] = None
+        # weight init and the synthetic batch were queued on the stream that
+        # built the trainer; a step issued from another stream (GPU sharing
+        # runs each job on its own stream) must wait for them first
+        self._ready = None
+        if self.device.type == "cuda":
+            self._ready = torch.cuda.Event()
+            self._ready.record(torch.cuda.current_stream(self.device))
 
     # ------------------------------------------------------------ one step
     def _fwd_bwd(self) -> torch.Tensor:
@@ -94,6 +101,9 @@ class Trainer:
                 _cpu_opt(self.opt, w, g, self.opt_state, lo, hi, wb, self.lr, wd, gscale, self.step_count)
 
     def step(self) -> torch.Tensor:
+        if self._ready is not None:
+            torch.cuda.current_stream(self.device).wait_event(self._ready)
+            self._ready = None
         if self.use_graph and self._graph is None and self._warm < 2:
             # the first two steps are REAL steps run eagerly on a side stream
             # (allocator pools, library handles/workspaces, GEMM route tuning
@@ -234,6 +244,7 @@ class Trainer:
     def release(self) -> None:
         self._graph = None
         self._g_loss = None
+        self.last_loss = None                    # may alias the graph's output
         self.arena.on_grad_ready = None
 
 

@@ -132,6 +132,11 @@ class Placement:
         self.rng = rng or random.Random(0)
         self.sensitivity = sensitivity
         self.pack = pack
+        # set by the engine when GPU sharing is on: model of a placed job and
+        # the measured co-run slowdown of a model pair (cluster/interference.py)
+        self.model_of: Optional[Callable[[str], str]] = None
+        self.pair_cost: Optional[Callable[[str, str], float]] = None
+        self.share_max_slowdown = float("inf")
 
     def plan(self, cluster: Cluster, job: Job) -> Optional[Plan]:
         raise NotImplementedError
@@ -332,6 +337,53 @@ class TiresiasPlacement(Placement):
     name = "tiresias"
 
     def plan(self, cluster, job):
+        p = self._exclusive(cluster, job)
+        if p is not None or not (self.pack and cluster.pack) or job.num_gpu != 1:
+            return p
+        return self._share(cluster, job)
+
+    def _share(self, cluster, job) -> Optional[Plan]:
+        """Work-conserving GPU sharing (the reference's --pack / Gandiva
+        packing), used only when no GPU is free: a 1-GPU job
+        joins a device that holds only 1-GPU jobs and has memory for it,
+        choosing the partner with the best measured co-run throughput
+        (lowest pair slowdown, profiles/stream_sharing_mi355x.json). The
+        executor runs co-located jobs on separate HIP streams. Gangs never
+        share, so no rank interleaves two jobs' collectives."""
+        t = job.tasks[0]
+        s = _Scratch(cluster)
+        me = job.spec.model or ""
+        best = None
+        for nid, n in cluster.nodes.items():
+            if not s.host_ok(nid, t):
+                continue
+            for d in n.devices:
+                if not d.tasks or not s.dev_ok(nid, d.device_id, t, True):
+                    continue
+                occ = [x.job_id for x in d.tasks.values()]
+                if any(sum(len(dv) for _, dv in cluster.placed.get(o, [("", (0, 0))])) != 1 for o in occ):
+                    continue
+                cost, ok = 0.0, True
+                for o in occ:
+                    other = self.model_of(o) if self.model_of else ""
+                    c = max(self.pair_cost(me, other), self.pair_cost(other, me)) if self.pair_cost else 1.0
+                    # optional cut-off for bad pairs (for two jobs alone, co-running
+                    # at slowdown s beats LAS's run-the-short-one-first iff s < 1.5;
+                    # with queues behind them sharing every measured pair won on
+                    # 12 seeded traces, so the default admits all)
+                    ok = ok and c < self.share_max_slowdown
+                    cost += c
+                if not ok:
+                    continue
+                key = (len(occ), cost, int(nid), d.device_id)
+                if best is None or key < best[0]:
+                    best = (key, nid, d.device_id)
+        if best is None:
+            return None
+        _, nid, dev = best
+        return [(nid, (dev,))]
+
+    def _exclusive(self, cluster, job):
         gpn = max(n.gpu_count for n in cluster.nodes.values())
         sensitive = bool(self.sensitivity and self.sensitivity(job))
         min_nodes = max(1, math.ceil(job.num_gpu / gpn))
