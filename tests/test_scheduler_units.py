@@ -272,3 +272,55 @@ def test_multi_dlas_reserves_per_class():
     chosen = pol.select(pol.order(jobs, 0), 8, 0)
     assert sum(j.num_gpu for j in chosen) <= 8
     assert any(j.num_gpu == 4 for j in chosen) and any(j.num_gpu == 1 for j in chosen)
+
+
+def test_tiresias_shares_only_when_full_and_picks_best_pair():
+    """GPU sharing (pack) in the Tiresias placement: exclusive while a GPU is
+    free; when full, a 1-GPU job joins the device whose 1-GPU occupant pairs
+    best (lowest measured slowdown); never a gang's device; gangs never share."""
+    c = Cluster(ClusterSpec(num_switch=1, num_node_p_switch=1, num_gpu_p_node=3), pack=True,
+                max_tasks_per_gpu=2)
+    pl = make_placement("tiresias", pack=True)
+    models = {"0": "vgg16", "1": "gnmt", "2": "resnet50"}
+    pl.model_of = lambda jid: models[jid]
+    slow = {("gnmt", "gnmt"): 1.38, ("gnmt", "vgg16"): 1.74, ("vgg16", "gnmt"): 1.74}
+    pl.pair_cost = lambda a, b: slow.get((a, b), 1.6)
+    kw = dict(gpu_mem_max=1000.0)
+    a = Job(spec(0, g=1, model="vgg16", **kw))
+    b = Job(spec(1, g=1, model="gnmt", **kw))
+    for j in (a, b):
+        p = pl.plan(c, j)
+        assert c.device(*[(n, d[0]) for n, d in p][0]).is_idle()     # exclusive while free
+        c.commit(j, p)
+    g = Job(spec(2, g=1, model="resnet50", **kw))
+    c.commit(g, pl.plan(c, g))
+    assert c.free_gpus() == 0
+    n = Job(spec(3, g=1, model="gnmt", **kw))
+    p = pl.plan(c, n)
+    assert p == [c.placed["1"][0]]                  # joins the gnmt device (1.38 < 1.74)
+    gang = Job(spec(4, g=2, model="resnet50", **kw))
+    assert pl.plan(c, gang) is None                 # gangs never share
+    # an occupant that is part of a gang is never a sharing partner
+    c2 = Cluster(ClusterSpec(num_switch=1, num_node_p_switch=1, num_gpu_p_node=2), pack=True,
+                 max_tasks_per_gpu=2)
+    c2.commit(Job(spec(5, g=2, **kw)), [("1", (0,)), ("1", (1,))])
+    assert pl.plan(c2, Job(spec(6, g=1, **kw))) is None
+
+
+def test_sharing_yields_to_blocked_gang():
+    """A gang that outranks the 1-GPU jobs sharing its GPUs preempts them
+    (reason "unshare") instead of waiting behind lower-priority sharers."""
+    from tiresias_amd.engine.sim import Simulator
+
+    cfg = SimConfig(schedule="dlas-gpu", scheme="tiresias", num_queue=2, queue_limits=[2.0],
+                    pack=True, max_tasks_per_gpu=2,
+                    cluster=ClusterSpec(num_switch=1, num_node_p_switch=1, num_gpu_p_node=2))
+    jobs = [spec(i, g=1, d=40.0, t=0.0, model="resnet50", gpu_mem_max=1000.0) for i in range(4)]
+    jobs.append(spec(9, g=2, d=5.0, t=5.0, model="resnet50", gpu_mem_max=1000.0))
+    sim = Simulator(cfg, jobs)
+    r = sim.run()
+    assert r["finished"] == 5
+    gang = sim.jobs["9"]
+    # the 1-GPU jobs are demoted (2 GPU-s limit) long before t=5: the new gang
+    # is top priority and starts on arrival although all 4 jobs were co-located
+    assert gang.start_time == pytest.approx(5.0)

@@ -153,8 +153,9 @@ def test_bench_scenarios_fit_cluster(scenario, n):
     assert len({j.spec.job_id for j in jobs}) == len(jobs)
     ts = [j.spec.submit_time for j in jobs]
     assert ts == sorted(ts)
-    pol, plc, ck, bpol, bplc, qlim = bench.SCENARIOS[scenario]
-    cfg = bench.make_cfg(pol, plc, n, 1, ck, qlim)
+    pol, plc, ck, bpol, bplc, qlim, share = bench.SCENARIOS[scenario]
+    cfg = bench.make_cfg(pol, plc, n, 1, ck, qlim, share)
+    assert cfg.pack == share
     assert cfg.queue_limits == [qlim]
     if scenario == "resnet4":
         assert qlim >= 1e6 and len(jobs) == 4
