@@ -282,6 +282,18 @@ class Controller:
             for r in gang_ranks(j.allocation, self.gpn):
                 assign.setdefault(r, []).append((j.job_id, n))
         for r in assign:                      # same order on every rank (gang collectives)
+            if len(assign[r]) > 1:
+                # co-located 1-GPU jobs each progress at 1/s of solo speed:
+                # shrink their shares so the rank still ends near the quantum
+                # (other ranks would otherwise idle at the round barrier)
+                ms = {jid: self.rjobs[jid].model for jid, _ in assign[r]}
+                shr = []
+                for jid, n in assign[r]:
+                    s_ = max(s.interf.pair(ms[jid], ms[o]) for o in ms if o != jid)
+                    left = self.rjobs[jid].iterations - self.done_iters[jid]
+                    est = self._iter_est(ms[jid], 1)
+                    shr.append((jid, max(1, min(left, int(round(self.quantum / (est * s_)))))))
+                assign[r] = shr
             assign[r].sort()
         self.round += 1
         stop = not s.active and s.reader.remaining() == 0
