@@ -44,3 +44,23 @@ def test_graph_capture_matches_eager(gpu):
         lb = float(b.step())
     assert abs(la - lb) < 1e-2 * max(1.0, abs(lb))
     assert rel(a.arena.master, b.arena.master) < 1e-3
+
+
+@pytest.mark.parametrize("model", ["resnet_tiny", "vgg_tiny", "transformer_tiny", "gnmt_tiny"])
+def test_wgrad_stream_overlap_matches(gpu, model):
+    """Weight gradients issued on the side stream (ops/functional.py
+    set_wgrad_stream; tied embedding/projection writers included) give the
+    same gradients as the single-stream backward, eager and under capture."""
+    a = Trainer(model, gpu, seed=4, overlap_wgrad=True)
+    b = Trainer(model, gpu, seed=4, overlap_wgrad=False)
+    b.arena.master.copy_(a.arena.master)
+    b.arena.shadow.copy_(a.arena.shadow)
+    la, lb = a._fwd_bwd(), b._fwd_bwd()
+    torch.cuda.synchronize()
+    assert abs(float(la) - float(lb)) < 1e-3 * max(1.0, abs(float(lb)))
+    assert rel(a.arena.grad, b.arena.grad) < 1e-3
+    g = Trainer(model, gpu, seed=4, overlap_wgrad=True, use_graph=True)
+    e = Trainer(model, gpu, seed=4, overlap_wgrad=False, use_graph=False)
+    for _ in range(4):
+        lg, le = float(g.step()), float(e.step())
+    assert abs(lg - le) < 2e-2 * max(1.0, abs(le))

@@ -23,7 +23,8 @@ from ..parallel.ddp import GradBucketer
 class Trainer:
     def __init__(self, model: str, device, batch: Optional[int] = None, group=None, seed: int = 0,
                  data_seed: Optional[int] = None, use_graph: bool = False, bucket_mb: float = 32.0,
-                 model_kwargs: Optional[dict] = None, lr: Optional[float] = None):
+                 model_kwargs: Optional[dict] = None, lr: Optional[float] = None,
+                 overlap_wgrad: Optional[bool] = None):
         self.model_name = model
         self.spec = MODELS[model]
         self.device = torch.device(device)
@@ -58,6 +59,8 @@ class Trainer:
         self._g_loss = None
         self._warm = 0           # eager steps done before graph capture
         self._side = None
+        self._ws = None                 # weight-gradient stream (1-GPU jobs)
+        self.overlap_wgrad = self.spec.overlap_wgrad if overlap_wgrad is None else overlap_wgrad
         self.last_loss: Optional[torch.Tensor] = None
         # weight init and the synthetic batch were queued on the stream that
         # built the trainer; a step issued from another stream (GPU sharing
@@ -70,15 +73,29 @@ class Trainer:
     # ------------------------------------------------------------ one step
     def _fwd_bwd(self) -> torch.Tensor:
         d = self.data
-        if self.spec.kind == "image":
-            logits = self.model.forward(d["x"])
-        else:
-            logits = self.model.forward(d)
-        labels = d["labels"]
-        rows = labels.numel()
-        loss, dlog = Fx.softmax_xent(logits, labels, smoothing=self.spec.smoothing,
-                                     ignore_index=-100, normalizer=rows)
-        logits.backward(dlog)
+        # 1-GPU jobs: weight gradients on their own stream, concurrent with
+        # the input-gradient chain (ops/functional.py::set_wgrad_stream)
+        ws = None
+        if self.device.type == "cuda" and self.ddp is None and self.overlap_wgrad:
+            if self._ws is None:
+                # (stream priorities were measured: no gain in graph replay)
+                self._ws = torch.cuda.Stream(self.device)
+            ws = self._ws
+        Fx.set_wgrad_stream(ws)
+        try:
+            if self.spec.kind == "image":
+                logits = self.model.forward(d["x"])
+            else:
+                logits = self.model.forward(d)
+            labels = d["labels"]
+            rows = labels.numel()
+            loss, dlog = Fx.softmax_xent(logits, labels, smoothing=self.spec.smoothing,
+                                         ignore_index=-100, normalizer=rows)
+            logits.backward(dlog)
+        finally:
+            Fx.set_wgrad_stream(None)
+        if ws is not None:
+            torch.cuda.current_stream(self.device).wait_stream(ws)   # join before the optimizer
         return loss
 
     def _opt_step(self):

@@ -118,9 +118,10 @@ class _LSTMLayer(Function):
                     Hprev[:-1] = Hs[1:]
                 else:
                     Hprev[1:] = Hs[:-1]
-            _T().gemm(dG2, False, Hprev.view(T * B, Hd), False, w_hh.grad, 1, None, False, None, 1.0, True)
-            _T().gemm(dG2, False, x.reshape(T * B, I), False, w_ih.grad, 1, None, False, None, 1.0, True)
-            _T().colsum(dG2, b.grad)
+            with Fx._OnWgrad(dG2, Hprev, x):     # overlaps the next layer's recurrence
+                _T().gemm(dG2, False, Hprev.view(T * B, Hd), False, w_hh.grad, 1, None, False, None, 1.0, True)
+                _T().gemm(dG2, False, x.reshape(T * B, I), False, w_ih.grad, 1, None, False, None, 1.0, True)
+                _T().colsum(dG2, b.grad)
             dx = None
             if ctx.needs_input_grad[0]:
                 dx = torch.empty(T * B, I, dtype=BF16, device=dev)

@@ -38,6 +38,49 @@ def _cpu_gemm_f32(a: torch.Tensor, b: torch.Tensor) -> torch.Tensor:
     return a.float() @ b.float()
 
 
+# ============================================================ weight-gradient stream
+# Weight gradients (dW = dY^T X, bias colsums, embedding scatter-adds) are off
+# the backward critical path: nothing downstream in the backward pass reads
+# them. When a trainer installs a side stream here, those kernels are issued
+# on it -- forked from the compute stream right after dY exists, BEFORE the
+# input-gradient kernel is launched -- so on the GPU they run concurrently with
+# the dgrad / BN / LSTM-recurrence chain (latency-bound small GEMMs and
+# memory-bound BN kernels fill each other's idle CUs). Inside a hipGraph
+# capture the fork/join becomes parallel graph branches. Every writer of a
+# given grad buffer must then sit on this stream (tied embedding/projection),
+# and the trainer joins it before the optimizer (Trainer._fwd_bwd). Gangs
+# (DDP) leave it unset: their bucket all-reduces follow grad_ready() on the
+# compute stream.
+_WGRAD_STREAM = None
+
+
+def set_wgrad_stream(stream) -> None:
+    global _WGRAD_STREAM
+    _WGRAD_STREAM = stream
+
+
+class _OnWgrad:
+    def __init__(self, *tensors):
+        self.s = _WGRAD_STREAM if tensors[0].is_cuda else None
+        self.ts = tensors
+        self.ctx = None
+
+    def __enter__(self):
+        if self.s is None:
+            return self
+        self.s.wait_stream(torch.cuda.current_stream(self.ts[0].device))
+        for t in self.ts:
+            t.record_stream(self.s)        # not recycled by the compute stream meanwhile
+        self.ctx = torch.cuda.stream(self.s)
+        self.ctx.__enter__()
+        return self
+
+    def __exit__(self, *exc):
+        if self.ctx is not None:
+            self.ctx.__exit__(*exc)
+        return False
+
+
 # ============================================================ Linear
 class _Linear(Function):
     @staticmethod
@@ -72,6 +115,11 @@ class _Linear(Function):
             else:
                 dy = (dy.float() * (y.float() > 0)).to(BF16)
         dx = None
+        if dy.is_cuda:
+            with _OnWgrad(dy, x):
+                _T().gemm(dy, False, x, False, w.grad, 1, None, False, None, 1.0, True)
+                if b is not None:
+                    _T().colsum(dy, b.grad)
         if ctx.needs_input_grad[0]:
             if dy.is_cuda:
                 dx = torch.empty_like(x)
@@ -81,11 +129,7 @@ class _Linear(Function):
                 if ctx.in_relu:
                     dxf = dxf * (x.float() > 0)
                 dx = dxf.to(BF16)
-        if dy.is_cuda:
-            _T().gemm(dy, False, x, False, w.grad, 1, None, False, None, 1.0, True)
-            if b is not None:
-                _T().colsum(dy, b.grad)
-        else:
+        if not dy.is_cuda:
             w.grad += _cpu_gemm_f32(dy.t(), x)
             if b is not None:
                 b.grad += dy.float().sum(0)
@@ -150,13 +194,14 @@ class _Conv(Function):
                 dy = (dy.float() * (y.float() > 0)).to(BF16)
         dx = None
         if dy.is_cuda:
+            with _OnWgrad(dy, x):
+                _T().conv_wgrad(dy, x, w.grad, st, pd, 1, 1)
+                if b is not None:
+                    _T().colsum(dy, b.grad)
             if ctx.needs_input_grad[0]:
                 dx = torch.empty_like(x)
                 wt = torch.empty_like(w.w)
                 _T().conv_dgrad(dy, w.w, wt, dx, st, pd, 1, x if ctx.in_relu else None)
-            _T().conv_wgrad(dy, x, w.grad, st, pd, 1, 1)
-            if b is not None:
-                _T().colsum(dy, b.grad)
         else:
             xf = x.float().permute(0, 3, 1, 2).requires_grad_(ctx.needs_input_grad[0])
             wf = w.w.float().permute(0, 3, 1, 2).requires_grad_(True)
@@ -457,7 +502,8 @@ class _Embed(Function):
         t = ctx.table
         d2 = dout.reshape(-1, t.shape[1]).contiguous()
         if d2.is_cuda:
-            _T().embedding_backward(d2, flat, t.grad, ctx.scale)
+            with _OnWgrad(d2, flat):           # the table may be tied to a projection
+                _T().embedding_backward(d2, flat, t.grad, ctx.scale)
         else:
             t.grad.index_add_(0, flat, d2.float() * ctx.scale)
         t.grad_ready()

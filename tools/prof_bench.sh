@@ -1,17 +1,10 @@
 #!/bin/bash
-# rocprofv3 kernel-trace + stats of one bench replay; keeps only the summary
-# CSVs (the per-dispatch trace is deleted so gpurun_out stays < 64 MiB).
-# usage: tools/prof_bench.sh <outdir-name> [bench args...]
-set -u
-ROOT="${GRAFT_REPO_ROOT:-$(cd "$(dirname "$0")/.." && pwd)}"
-name=$1; shift
-out="$ROOT/gpurun_out/$name"
-mkdir -p "$out"
-cd /tmp && export TMPDIR=/tmp
-timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d "$out" -o run -- \
-  python3 "$ROOT/bench.py" "$@" > "$out/bench.log" 2>&1
-rc=$?
-find "$out" -type f -name "*trace*.csv" -delete
-find "$out" -type f -size +8M -printf "%s %p (deleted)\n" -delete >> "$out/bench.log"
-find "$out" -type f -printf "%s %p\n" >> "$out/bench.log"
-exit $rc
+# rocprofv3 kernel statistics of one headline trace replay (1 GPU).
+# Run on the GPU box from the repo root:  bash tools/prof_bench.sh
+set -o pipefail
+export TMPDIR=/tmp
+timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof_bench -o run -- \
+  python3 bench.py --steps 1 --warmup 0 --no-baseline --no-exclusive-ref > gpurun_out/log_prof_bench.txt 2>&1 \
+  || { tail -20 gpurun_out/log_prof_bench.txt; exit 1; }
+find gpurun_out/prof_bench -type f ! -name "*_stats.csv" -delete
+grep -h metric gpurun_out/log_prof_bench.txt | cut -c 1-200
