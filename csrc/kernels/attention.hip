@@ -184,9 +184,11 @@ __global__ void __launch_bounds__(256) attn_fwd_kernel(const bf16_t* __restrict_
   }
 }
 
-// delta[b,h,q] = sum_d dO * O
+// delta[b,h,q] = sum_d dO * O, and the same wave zeroes that row's fp32 dQ
+// accumulator ([B][Sq][H][64]) -- one launch instead of delta + a memset
 __global__ void attn_delta_kernel(const bf16_t* __restrict__ O, const bf16_t* __restrict__ dO,
-                                  float* __restrict__ delta, int B, int H, int Sq, long os) {
+                                  float* __restrict__ delta, float* __restrict__ dq_acc, int B,
+                                  int H, int Sq, long os) {
   const long row = blockIdx.x * 4L + (threadIdx.x >> 6);
   const int lane = threadIdx.x & 63;
   if (row >= (long)B * H * Sq) return;
@@ -194,6 +196,7 @@ __global__ void attn_delta_kernel(const bf16_t* __restrict__ O, const bf16_t* __
   const long bh = row / Sq;
   const int h = (int)(bh % H), b = (int)(bh / H);
   const long off = ((long)b * Sq + q) * os + h * AD + lane;
+  dq_acc[(((long)b * Sq + q) * H + h) * AD + lane] = 0.f;
   float v = bf2f(O[off]) * bf2f(dO[off]);
   v = wave_sum(v);
   if (lane == 0) delta[row] = v;
@@ -365,10 +368,9 @@ void attn_backward(const bf16_t* q, const bf16_t* k, const bf16_t* v, const bf16
                    long kv_stride, long o_stride, int causal, float scale, const int* kv_len,
                    hipStream_t s) {
   const long rows = (long)B * H * Sq;
-  hipLaunchKernelGGL(attn_delta_kernel, dim3((rows + 3) / 4), dim3(256), 0, s, o, dout, delta, B, H,
-                     Sq, o_stride);
+  hipLaunchKernelGGL(attn_delta_kernel, dim3((rows + 3) / 4), dim3(256), 0, s, o, dout, delta, dq_acc,
+                     B, H, Sq, o_stride);
   const long nq = (long)B * Sq * H * AD;
-  zero_async(dq_acc, nq * sizeof(float), s);
   dim3 grid((Sk + AT - 1) / AT, B * H);
   hipLaunchKernelGGL(attn_bwd_kernel, grid, dim3(256), 0, s, q, k, v, dout, lse, delta, dk, dv,
                      dq_acc, H, Sq, Sk, q_stride, kv_stride, o_stride, causal, scale, kv_len);
