@@ -334,14 +334,21 @@ void ln_forward_op(const Tensor& x, const Tensor& g, const Tensor& b, const Tens
 }
 
 void ln_backward_op(const Tensor& dy, const Tensor& x, const Tensor& g, const Tensor& mean,
-                    const Tensor& rstd, const Tensor& dx, const Tensor& dg, const Tensor& db) {
+                    const Tensor& rstd, const Tensor& dx, const Tensor& dg, const Tensor& db,
+                    const optional<Tensor>& addend) {
   check_bf16(dy, "dy"); check_bf16(x, "x"); check_bf16(dx, "dx");
   check_contig(dy, "dy"); check_contig(x, "x"); check_contig(dx, "dx");
   check_f32(dg, "dg"); check_f32(db, "db");
+  const tam::bf16_t* add = nullptr;
+  if (addend.has_value() && addend->defined()) {
+    check_bf16(*addend, "addend"); check_contig(*addend, "addend");
+    TORCH_CHECK(addend->numel() == x.numel(), "tam.ln_backward: addend size");
+    add = bp(*addend);
+  }
   const int64_t D = x.size(-1);
   Tensor ws = at::empty({(int64_t)tam::LN_MAX_BLOCKS * 2 * D}, x.options().dtype(at::kFloat));
   tam::ln_backward(bp(dy), bp(x), g.data_ptr<float>(), mean.data_ptr<float>(),
-                   rstd.data_ptr<float>(), bpm(dx), dg.data_ptr<float>(), db.data_ptr<float>(),
+                   rstd.data_ptr<float>(), bpm(dx), add, dg.data_ptr<float>(), db.data_ptr<float>(),
                    ws.data_ptr<float>(), x.numel() / D, (int)D, cur_stream(x));
 }
 
@@ -554,7 +561,7 @@ TORCH_LIBRARY(tam, m) {
   m.def("bn_forward(Tensor x, Tensor? res, Tensor(a!) y, Tensor gamma, Tensor beta, Tensor(b!)? run_mean, Tensor(c!)? run_var, Tensor(d!) save_mean, Tensor(e!) save_rstd, float eps, float momentum, bool relu) -> ()", &bn_forward_op);
   m.def("bn_backward(Tensor dy, Tensor? y, Tensor x, Tensor mean, Tensor rstd, Tensor gamma, Tensor(a!) dx, Tensor(b!)? dres, Tensor(c!)? dgamma, Tensor(d!)? dbeta, bool relu) -> ()", &bn_backward_op);
   m.def("ln_forward(Tensor x, Tensor g, Tensor b, Tensor(a!) y, Tensor(b!) mean, Tensor(c!) rstd, float eps) -> ()", &ln_forward_op);
-  m.def("ln_backward(Tensor dy, Tensor x, Tensor g, Tensor mean, Tensor rstd, Tensor(a!) dx, Tensor(b!) dg, Tensor(c!) db) -> ()", &ln_backward_op);
+  m.def("ln_backward(Tensor dy, Tensor x, Tensor g, Tensor mean, Tensor rstd, Tensor(a!) dx, Tensor(b!) dg, Tensor(c!) db, Tensor? addend=None) -> ()", &ln_backward_op);
   m.def("maxpool_forward(Tensor x, Tensor(a!) y, Tensor(b!) idx, int R, int S, int stride, int pad) -> ()", &maxpool_forward_op);
   m.def("maxpool_backward(Tensor dy, Tensor idx, Tensor(a!) dx, int R, int S, int stride, int pad) -> ()", &maxpool_backward_op);
   m.def("avgpool_forward(Tensor x, Tensor(a!) y) -> ()", &avgpool_forward_op);

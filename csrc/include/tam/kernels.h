@@ -29,9 +29,10 @@ void bn_backward(const bf16_t* dy, const bf16_t* y, const bf16_t* x, const float
 // LayerNorm over last dim D (D % 8 == 0, D <= 2048)
 void ln_forward(const bf16_t* x, const float* g, const float* b, bf16_t* y, float* mean,
                 float* rstd, long rows, int D, float eps, hipStream_t s);
+// dx = LN-backward(dy) (+ addend, the fused gradient of a skip connection)
 void ln_backward(const bf16_t* dy, const bf16_t* x, const float* g, const float* mean,
-                 const float* rstd, bf16_t* dx, float* dg, float* db, float* ws, long rows, int D,
-                 hipStream_t s);
+                 const float* rstd, bf16_t* dx, const bf16_t* addend, float* dg, float* db,
+                 float* ws, long rows, int D, hipStream_t s);
 
 // pooling
 void maxpool_forward(const bf16_t* x, bf16_t* y, uint8_t* idx, int N, int H, int W, int C, int P,

@@ -514,6 +514,7 @@ __global__ void __launch_bounds__(256) ln_bwd_kernel(const bf16_t* __restrict__ 
                                                       const float* __restrict__ mean,
                                                       const float* __restrict__ rstd,
                                                       bf16_t* __restrict__ dx,
+                                                      const bf16_t* __restrict__ addend,
                                                       float* __restrict__ part, long rows,
                                                       int D, int rows_per_block) {
   // each wave processes rows_per_block/4 rows, accumulating dgamma/dbeta in
@@ -559,6 +560,12 @@ __global__ void __launch_bounds__(256) ln_bwd_kernel(const bf16_t* __restrict__ 
         float o[8];
 #pragma unroll
         for (int j = 0; j < 8; ++j) o[j] = rs * (fd[v][j] * g[c + j] - s1 - fx[v][j] * s2);
+        if (addend) {                      // + the residual branch's gradient (fused skip)
+          float a[8];
+          unpack8(*(const uint4*)(addend + row * D + c), a);
+#pragma unroll
+          for (int j = 0; j < 8; ++j) o[j] += a[j];
+        }
         *(uint4*)(dx + row * D + c) = pack8(o);
       }
     }
@@ -594,16 +601,16 @@ void ln_forward(const bf16_t* x, const float* g, const float* b, bf16_t* y, floa
 }
 
 void ln_backward(const bf16_t* dy, const bf16_t* x, const float* g, const float* mean,
-                 const float* rstd, bf16_t* dx, float* dg, float* db, float* ws, long rows, int D,
-                 hipStream_t s) {
+                 const float* rstd, bf16_t* dx, const bf16_t* addend, float* dg, float* db,
+                 float* ws, long rows, int D, hipStream_t s) {
   // ws: LN_MAX_BLOCKS * 2 * D floats of per-block partial dgamma / dbeta
   int rpb = (int)((rows + LN_MAX_BLOCKS - 1) / LN_MAX_BLOCKS);
   rpb = ((rpb + 3) / 4) * 4;
   if (rpb < 8) rpb = 8;
   const int blocks = (int)((rows + rpb - 1) / rpb);
-  if (D <= 512) hipLaunchKernelGGL(ln_bwd_kernel<1>, dim3(blocks), dim3(256), 0, s, dy, x, g, mean, rstd, dx, ws, rows, D, rpb);
-  else if (D <= 1024) hipLaunchKernelGGL(ln_bwd_kernel<2>, dim3(blocks), dim3(256), 0, s, dy, x, g, mean, rstd, dx, ws, rows, D, rpb);
-  else hipLaunchKernelGGL(ln_bwd_kernel<4>, dim3(blocks), dim3(256), 0, s, dy, x, g, mean, rstd, dx, ws, rows, D, rpb);
+  if (D <= 512) hipLaunchKernelGGL(ln_bwd_kernel<1>, dim3(blocks), dim3(256), 0, s, dy, x, g, mean, rstd, dx, addend, ws, rows, D, rpb);
+  else if (D <= 1024) hipLaunchKernelGGL(ln_bwd_kernel<2>, dim3(blocks), dim3(256), 0, s, dy, x, g, mean, rstd, dx, addend, ws, rows, D, rpb);
+  else hipLaunchKernelGGL(ln_bwd_kernel<4>, dim3(blocks), dim3(256), 0, s, dy, x, g, mean, rstd, dx, addend, ws, rows, D, rpb);
   col_reduce_acc(ws, blocks, 2 * D, dg, db, D, s);
 }
 

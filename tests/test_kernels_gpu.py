@@ -351,6 +351,11 @@ def test_layernorm(gpu, D, rows):
     gx, gg, gb = torch.autograd.grad(yf, [xf, gf, bf], dy.float())
     assert rel_err(dx, gx) < 2e-2
     assert rel_err(dg, gg) < 1e-2 and rel_err(db, gb) < 1e-2
+    # fused skip gradient (pre-LN residual tap): dx + addend in the epilogue
+    add = torch.randn_like(x)
+    dx2 = torch.empty_like(x)
+    T().ln_backward(dy, x, g, mean, rstd, dx2, torch.zeros(D, device=gpu), torch.zeros(D, device=gpu), add)
+    assert rel_err(dx2, gx + add.float()) < 2e-2
 
 
 # ------------------------------------------------------------------ pooling / loss

@@ -75,7 +75,7 @@ class TransformerBase:
         return Fx.add(x, self.pos[:S].unsqueeze(0).expand_as(x).contiguous())
 
     def _ffn(self, x, L):
-        h = Fx.layernorm(x, *L["ln2" if "q" not in L else "ln3"])
+        x, h = Fx.layernorm_skip(x, *L["ln2" if "q" not in L else "ln3"])
         (w1, b1), (w2, b2) = L["f1"], L["f2"]
         h = Fx.linear(h, w1, b1, relu=True, mask_own_relu=False)
         h = Fx.linear(h, w2, b2, in_relu=True)
@@ -84,7 +84,7 @@ class TransformerBase:
     def encode(self, src):
         x = self._embed(src)
         for L in self.enc:
-            h = Fx.layernorm(x, *L["ln1"])
+            x, h = Fx.layernorm_skip(x, *L["ln1"])
             qkv = Fx.linear(h, *L["qkv"])
             a = Fx.self_attention(qkv, self.h, causal=False)
             x = Fx.add(x, Fx.linear(a, *L["o"]))
@@ -94,10 +94,10 @@ class TransformerBase:
     def decode(self, tgt, mem):
         x = self._embed(tgt)
         for L in self.dec:
-            h = Fx.layernorm(x, *L["ln1"])
+            x, h = Fx.layernorm_skip(x, *L["ln1"])
             a = Fx.self_attention(Fx.linear(h, *L["qkv"]), self.h, causal=True)
             x = Fx.add(x, Fx.linear(a, *L["o"]))
-            h = Fx.layernorm(x, *L["ln2"])
+            x, h = Fx.layernorm_skip(x, *L["ln2"])
             q = Fx.linear(h, *L["q"])
             kv = Fx.linear(mem, *L["kv"])
             a = Fx.cross_attention(q, kv, self.h)

@@ -374,6 +374,44 @@ def layernorm(x: torch.Tensor, g: Param, b: Param, eps: float = 1e-5) -> torch.T
     return _LN.apply(x, g.arena.token, g, b, eps)
 
 
+class _LNSkip(_LN):
+    """Pre-LN residual tap: returns (x, LN(x)). The residual stream leaves
+    through this Function instead of being consumed twice, so autograd does
+    not sum the two incoming gradients with an extra elementwise kernel: the
+    LN backward kernel adds the skip gradient in its epilogue."""
+
+    @staticmethod
+    def forward(ctx, x, token, g: Param, b: Param, eps: float):
+        y = _LN.forward(ctx, x, token, g, b, eps)
+        return x.view_as(x), y
+
+    @staticmethod
+    def backward(ctx, dskip, dy):
+        x, mean, rstd = ctx.saved_tensors
+        g, b = ctx.g, ctx.b
+        if dy is None:
+            return dskip, None, None, None, None
+        dy = dy.contiguous()
+        if dy.is_cuda:
+            dx = torch.empty_like(x)
+            _T().ln_backward(dy, x, g.master, mean, rstd, dx, g.grad, b.grad,
+                             dskip.contiguous() if dskip is not None else None)
+            g.grad_ready()
+            b.grad_ready()
+            return dx, None, None, None, None
+        dx = _LN.backward(ctx, dy)[0]
+        if dskip is not None:
+            dx = (dx.float() + dskip.float()).to(BF16)
+        return dx, None, None, None, None
+
+
+def layernorm_skip(x: torch.Tensor, g: Param, b: Param, eps: float = 1e-5):
+    """(x, layernorm(x)) for ``x + f(layernorm(x))`` blocks; see _LNSkip."""
+    if not x.is_contiguous():
+        x = x.contiguous()
+    return _LNSkip.apply(x, g.arena.token, g, b, eps)
+
+
 # ============================================================ pooling
 class _MaxPool(Function):
     @staticmethod
