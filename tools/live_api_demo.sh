@@ -5,7 +5,7 @@
 #   bash tools/live_api_demo.sh
 set -o pipefail
 SPOOL=$(mktemp -d /tmp/tam_spool.XXXX)
-OUT=gpurun_out/live_api
+OUT=$PWD/gpurun_out/live_api
 mkdir -p $OUT
 timeout -k 10 240 python -u -m tiresias_amd.cli.run_cluster --spool $SPOOL --schedule dlas-gpu \
     --scheme tiresias --quantum 0.1 --log_path $OUT > $OUT/cluster.log 2>&1 &
@@ -25,5 +25,8 @@ python -m tiresias_amd.cli.submit --spool $SPOOL --shutdown
 wait $CL
 rc=$?
 echo "cluster exit $rc"
+for d in accepted rejected; do
+  echo "== $d"; for f in $SPOOL/$d/*; do [ -f "$f" ] && { echo "$(basename $f): $(head -c 300 $f)"; }; done
+done | tee $OUT/spool_outcome.txt
 tail -5 $OUT/cluster.log
 exit $rc
