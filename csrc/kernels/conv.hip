@@ -68,7 +68,11 @@ void conv_dgrad(const bf16_t* dy, const bf16_t* w, const bf16_t* wt, const ConvG
   if (wt && g_conv_dma && g.dil == 1 && g.stride == 1) {
     // rows = dX pixels over an H x W grid, gathered from dY (P x Q x K), B = Wt [C][R][S][K]
     CDArgs a = cd_dgrad_args(dy, wt, g, 0, 0);
-    if (launch_conv_dma(a, ep, s, g_conv_dma >= 2 ? g_conv_dma - 1 : 0)) return;
+    // 64-channel dX over >= 1M pixels (VGG-16's 224x224 layer): the 64-wide
+    // DMA tile beats the igemm although Kd < 1024 (measured 422 -> 364 us);
+    // the cost model's 64-column rule is tuned for ResNet's shallower grids
+    const int force = g_conv_dma >= 2 ? g_conv_dma - 1 : (g.C == 64 && a.M >= (1 << 20) ? 1 : 0);
+    if (launch_conv_dma(a, ep, s, force)) return;
   }
   if (wt && g_conv_dma && g.dil == 1 && g.stride > 1 && g.K % 64 == 0 && g.C % 64 == 0 &&
       ep.mode == 0 && !ep.c_f32 && g.stride * g.stride <= 4) {
@@ -124,6 +128,18 @@ void conv_wgrad(const bf16_t* dy, const bf16_t* x, const ConvGeom& g, Epi ep, hi
     return;
   }
   TileChoice t = choose_tiles(g.K, Nc, Mred, true);
+  if (t.splits > 1 && Nc >= 256) {       // (stem-like Nc = 72 stays on 64x64 tiles)
+    // split-K regime (tiny dW, huge pixel reduction): every N tile re-reads
+    // all of dY, so prefer the widest tile and let split-K fill the CUs
+    // (C=64 3x3 wgrads: 9 -> 5 passes over dY)
+    const int cfg = g.K > 64 ? 0 : 2;
+    const long tiles = (long)cdiv(g.K, cfg == 0 ? 128 : 64) * cdiv(Nc, 128);
+    const int ktiles = cdiv(Mred, IG_BK);
+    int sp = (int)((512 + tiles - 1) / tiles);
+    if (sp > ktiles / 4) sp = ktiles / 4;
+    if (sp > 256) sp = 256;
+    t = TileChoice{cfg, sp < 1 ? 1 : sp};
+  }
   prepare_split(ep, t.splits, g.K, Nc, s);
   switch (t.cfg) {
     case 0: wgrad_tile<128, 128>(dy, x, g, ep, t.splits, s); break;

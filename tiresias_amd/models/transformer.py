@@ -53,9 +53,15 @@ class TransformerBase:
         for i in range(dec_layers):
             p = f"dec{i}"
             self.dec.append(dict(ln1=ln(p + ".ln1"), qkv=lin(p + ".qkv", 3 * d, d), o=lin(p + ".o", d, d),
-                                 ln2=ln(p + ".ln2"), q=lin(p + ".q", d, d), kv=lin(p + ".kv", 2 * d, d),
+                                 ln2=ln(p + ".ln2"), q=lin(p + ".q", d, d),
                                  o2=lin(p + ".o2", d, d), ln3=ln(p + ".ln3"),
                                  f1=lin(p + ".f1", ffn, d), f2=lin(p + ".f2", d, ffn)))
+        # every decoder layer's cross-attention K/V projection of the encoder
+        # memory as ONE [L*2d, d] GEMM (per-layer xavier bound): one fwd GEMM,
+        # one dgrad, one wgrad instead of L each + L-1 gradient sums
+        self.dec_kv = (A.add("dec.kv.w", (dec_layers * 2 * d, d), init="uniform",
+                             std=math.sqrt(6.0 / (3 * d))),
+                       A.add("dec.kv.b", (dec_layers * 2 * d,), init="zeros", decay=False))
         self.dec_ln = ln("dec.ln")
         self.training = True
 
@@ -93,14 +99,17 @@ class TransformerBase:
 
     def decode(self, tgt, mem):
         x = self._embed(tgt)
-        for L in self.dec:
+        n = len(self.dec)
+        kv_all = Fx.linear(mem, *self.dec_kv)          # [B, S, n*2d]
+        hold = {"n": 0}
+        for i, L in enumerate(self.dec):
             x, h = Fx.layernorm_skip(x, *L["ln1"])
             a = Fx.self_attention(Fx.linear(h, *L["qkv"]), self.h, causal=True)
             x = Fx.add(x, Fx.linear(a, *L["o"]))
             x, h = Fx.layernorm_skip(x, *L["ln2"])
             q = Fx.linear(h, *L["q"])
-            kv = Fx.linear(mem, *L["kv"])
-            a = Fx.cross_attention(q, kv, self.h)
+            a = Fx.cross_attention(q, kv_all, self.h, k_slot=2 * i, v_slot=2 * i + 1, nkv=2 * n,
+                                   kv_hold=hold)
             x = Fx.add(x, Fx.linear(a, *L["o2"]))
             x = self._ffn(x, L)
         x = Fx.layernorm(x, *self.dec_ln)

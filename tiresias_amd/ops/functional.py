@@ -578,8 +578,18 @@ class _Attn(Function):
 
     @staticmethod
     def forward(ctx, q_src, kv_src, H: int, q_slot: int, nq: int, k_slot: int, v_slot: int,
-                nkv: int, causal: bool, kv_len):
+                nkv: int, causal: bool, kv_len, kv_hold=None):
         same = q_src is kv_src
+        # kv_hold: several attention calls read different slots of ONE packed
+        # K/V tensor (the decoder's batched cross-attention projection); they
+        # write their slots into one shared gradient buffer and only the call
+        # that ran first (backward runs last) returns it -- no zero-fill, no
+        # autograd sum of per-layer full-size gradients
+        ctx.kv_hold = kv_hold
+        ctx.kv_idx = None
+        if kv_hold is not None:
+            ctx.kv_idx = kv_hold["n"]
+            kv_hold["n"] += 1
         B, Sq, _ = q_src.shape
         Sk = kv_src.shape[1]
         qv = q_src.view(B, Sq, nq, H, 64)[:, :, q_slot]
@@ -606,7 +616,13 @@ class _Attn(Function):
         do = do.contiguous().view(B, Sq, H, 64)
         alloc = torch.empty_like if q_src.is_cuda else torch.zeros_like
         dq_src = alloc(q_src)
-        dkv_src = dq_src if same else alloc(kv_src)
+        hold = ctx.kv_hold
+        if hold is not None:
+            if hold.get("buf") is None:
+                hold["buf"] = alloc(kv_src)
+            dkv_src = hold["buf"]
+        else:
+            dkv_src = dq_src if same else alloc(kv_src)
         qv = q_src.view(B, Sq, nq, H, 64)[:, :, q_slot]
         kvv = kv_src.view(B, Sk, nkv, H, 64)
         dqv = dq_src.view(B, Sq, nq, H, 64)[:, :, q_slot]
@@ -628,21 +644,26 @@ class _Attn(Function):
             dkvv[:, :, k_slot].copy_(gk.to(BF16))
             dkvv[:, :, v_slot].copy_(gv.to(BF16))
         if same:
-            return dq_src, None, None, None, None, None, None, None, None, None
-        return dq_src, dkv_src, None, None, None, None, None, None, None, None
+            return dq_src, None, None, None, None, None, None, None, None, None, None
+        if hold is not None and ctx.kv_idx != 0:
+            dkv_src = None                 # slots written; the first caller returns the buffer
+        return dq_src, dkv_src, None, None, None, None, None, None, None, None, None
 
 
 def self_attention(qkv: torch.Tensor, heads: int, causal: bool = False,
                    kv_len: Optional[torch.Tensor] = None) -> torch.Tensor:
     """qkv: [B,S,3*H*64] packed projection output -> [B,S,H*64]."""
     qkv = qkv.contiguous()
-    return _Attn.apply(qkv, qkv, heads, 0, 3, 1, 2, 3, causal, kv_len)
+    return _Attn.apply(qkv, qkv, heads, 0, 3, 1, 2, 3, causal, kv_len, None)
 
 
 def cross_attention(q: torch.Tensor, kv: torch.Tensor, heads: int,
-                    kv_len: Optional[torch.Tensor] = None) -> torch.Tensor:
-    """q: [B,Sq,H*64], kv: [B,Sk,2*H*64] -> [B,Sq,H*64]."""
-    return _Attn.apply(q, kv, heads, 0, 1, 0, 1, 2, False, kv_len)
+                    kv_len: Optional[torch.Tensor] = None, k_slot: int = 0, v_slot: int = 1,
+                    nkv: int = 2, kv_hold: Optional[dict] = None) -> torch.Tensor:
+    """q: [B,Sq,H*64], kv: [B,Sk,nkv*H*64] (K at slot k_slot, V at v_slot)
+    -> [B,Sq,H*64]. Calls sharing one packed kv pass the same ``kv_hold``
+    dict (``{"n": 0}``, fresh per forward); see _Attn."""
+    return _Attn.apply(q, kv, heads, 0, 1, k_slot, v_slot, nkv, False, kv_len, kv_hold)
 
 
 # ============================================================ residual add
