@@ -64,3 +64,29 @@ def test_wgrad_stream_overlap_matches(gpu, model):
     for _ in range(4):
         lg, le = float(g.step()), float(e.step())
     assert abs(lg - le) < 2e-2 * max(1.0, abs(le))
+
+
+@pytest.mark.parametrize("overlap", [False, True])
+def test_gnmt_branch_streams_match(gpu, overlap):
+    """GNMT's independent recurrences on branch streams (bidirectional
+    halves; first decoder layer alongside the encoder; ops/functional.py
+    on_branch) give the same loss and gradients as the one-stream order,
+    eager and under hipGraph capture, with and without the wgrad stream."""
+    a = Trainer("gnmt_tiny", gpu, seed=6, branches=True, overlap_wgrad=overlap)
+    b = Trainer("gnmt_tiny", gpu, seed=6, branches=False, overlap_wgrad=overlap)
+    b.arena.master.copy_(a.arena.master)
+    b.arena.shadow.copy_(a.arena.shadow)
+    for _ in range(2):
+        la, lb = a._fwd_bwd(), b._fwd_bwd()
+        torch.cuda.synchronize()
+        assert abs(float(la) - float(lb)) < 1e-3 * max(1.0, abs(float(lb)))
+        assert rel(a.arena.grad, b.arena.grad) < 1e-3
+        a.arena.grad.zero_()
+        b.arena.grad.zero_()
+    g = Trainer("gnmt_tiny", gpu, seed=6, branches=True, overlap_wgrad=overlap, use_graph=True)
+    e = Trainer("gnmt_tiny", gpu, seed=6, branches=False, overlap_wgrad=overlap, use_graph=False)
+    for _ in range(5):
+        lg, le = float(g.step()), float(e.step())
+    torch.cuda.synchronize()
+    assert abs(lg - le) < 2e-2 * max(1.0, abs(le))
+    assert rel(g.arena.master, e.arena.master) < 1e-3

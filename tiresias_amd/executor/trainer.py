@@ -24,7 +24,7 @@ class Trainer:
     def __init__(self, model: str, device, batch: Optional[int] = None, group=None, seed: int = 0,
                  data_seed: Optional[int] = None, use_graph: bool = False, bucket_mb: float = 32.0,
                  model_kwargs: Optional[dict] = None, lr: Optional[float] = None,
-                 overlap_wgrad: Optional[bool] = None):
+                 overlap_wgrad: Optional[bool] = None, branches: Optional[bool] = None):
         self.model_name = model
         self.spec = MODELS[model]
         self.device = torch.device(device)
@@ -61,6 +61,9 @@ class Trainer:
         self._side = None
         self._ws = None                 # weight-gradient stream (1-GPU jobs)
         self.overlap_wgrad = self.spec.overlap_wgrad if overlap_wgrad is None else overlap_wgrad
+        # model-declared branch streams (see _fwd_bwd); None = the model's default
+        self.branches = getattr(self.model, "branch_default", False) if branches is None else branches
+        self._bs: List = []
         self.last_loss: Optional[torch.Tensor] = None
         # weight init and the synthetic batch were queued on the stream that
         # built the trainer; a step issued from another stream (GPU sharing
@@ -82,6 +85,13 @@ class Trainer:
                 self._ws = torch.cuda.Stream(self.device)
             ws = self._ws
         Fx.set_wgrad_stream(ws)
+        # independent model branches on their own streams (1-GPU jobs;
+        # ops/functional.py::on_branch), joined before the optimizer
+        nb = getattr(self.model, "branch_streams", 0) if self.branches else 0
+        if self.device.type == "cuda" and self.ddp is None and nb:
+            if len(self._bs) < nb:
+                self._bs = [torch.cuda.Stream(self.device) for _ in range(nb)]
+            Fx.set_branch_streams(self._bs)
         try:
             if self.spec.kind == "image":
                 logits = self.model.forward(d["x"])
@@ -94,8 +104,12 @@ class Trainer:
             logits.backward(dlog)
         finally:
             Fx.set_wgrad_stream(None)
+            Fx.set_branch_streams(None)
         if ws is not None:
             torch.cuda.current_stream(self.device).wait_stream(ws)   # join before the optimizer
+        if self.device.type == "cuda" and self.ddp is None and nb:
+            for s in self._bs:
+                torch.cuda.current_stream(self.device).wait_stream(s)
         return loss
 
     def _opt_step(self):

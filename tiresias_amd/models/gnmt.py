@@ -170,6 +170,12 @@ def lstm(x, p, reverse=False):
 
 class GNMT:
     name = "gnmt"
+    branch_streams = 2          # independent recurrences that CAN be issued concurrently
+    # ...but not by default: each per-timestep split-K recurrence GEMM already
+    # spreads over all 256 CUs, so two co-running recurrences contend (CUs,
+    # 2 x 8 MB of W_hh through the 4 MB per-XCD L2s): measured on MI355X,
+    # hipGraph step 15.5 ms one stream vs 16.3 ms with branches
+    branch_default = False
 
     def __init__(self, arena: Arena, vocab: int = 32000, hidden: int = 1024, enc_layers: int = 4,
                  dec_layers: int = 4, heads: int = 16):
@@ -197,18 +203,27 @@ class GNMT:
     def forward(self, batch):
         src, tgt_in = batch["src"], batch["tgt_in"]       # [B,S] token ids
         # time-major activations [T,B,H]
+        # branch 1: the first decoder layer (+ attention query) reads only the
+        # target embedding, so it runs alongside the whole encoder stack;
+        # branch 0: the reverse half of the bidirectional layer alongside the
+        # forward half (ops/functional.py::on_branch; no-op without streams)
+        tgt_t = tgt_in.t().contiguous()
+        with Fx.on_branch(1, tgt_t):
+            y = Fx.embedding(tgt_t, self.tgt_emb)
+            d0 = lstm(y, self.dec[0])                    # [T,B,H]
+            q = Fx.linear(d0.transpose(0, 1).contiguous(), self.att_q)   # [B,T,H]
         x = Fx.embedding(src.t().contiguous(), self.src_emb)
+        with Fx.on_branch(0, x):
+            bw = lstm(x, self.enc[1], reverse=True)
         fw = lstm(x, self.enc[0])
-        bw = lstm(x, self.enc[1], reverse=True)
+        bw = Fx.join_branch(0, bw)
         h = lstm(torch.cat([fw, bw], 2), self.enc[2])
         for i, p in enumerate(self.enc[3:]):
             o = lstm(h, p)
             h = Fx.add(h, o) if i >= 0 else o          # residual from layer 3 on
         mem = h.transpose(0, 1).contiguous()             # [B,S,H]
-        y = Fx.embedding(tgt_in.t().contiguous(), self.tgt_emb)
-        d0 = lstm(y, self.dec[0])                        # [T,B,H]
-        q = Fx.linear(d0.transpose(0, 1).contiguous(), self.att_q)   # [B,T,H]
         kv = Fx.linear(mem, self.att_kv)                 # [B,S,2H]
+        d0, q = Fx.join_branch(1, d0, q)
         ctxv = Fx.cross_attention(q, kv, self.heads).transpose(0, 1).contiguous()  # [T,B,H]
         h = d0
         for i, p in enumerate(self.dec[1:]):

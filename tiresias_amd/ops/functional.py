@@ -81,6 +81,61 @@ class _OnWgrad:
         return False
 
 
+# ============================================================ branch streams
+# Independent sub-graphs of a model (GNMT: the forward and reverse halves of
+# the bidirectional encoder layer; the first decoder layer, which reads only
+# the target embedding, vs the whole encoder stack) are issued on their own
+# streams. Their per-timestep recurrences are latency-bound (<= 256
+# workgroups per kernel), so two of them co-run on the CUs; inside a hipGraph
+# capture the fork/join become parallel branches. Autograd runs each
+# Function's backward on its forward's stream, so the backward branches
+# overlap too. Every gradient buffer has ONE writer stream, and the trainer
+# joins all branch streams before the optimizer (Trainer._fwd_bwd). Gangs
+# leave them unset: a bucket all-reduce is ordered after the current stream
+# only.
+_BRANCH_STREAMS: list = []
+
+
+def set_branch_streams(streams) -> None:
+    global _BRANCH_STREAMS
+    _BRANCH_STREAMS = list(streams or [])
+
+
+class on_branch:
+    """``with on_branch(i, *inputs):`` issue the block on branch stream ``i``
+    (forked from the current stream; no-op when no branch streams are set)."""
+
+    def __init__(self, i: int, *inputs):
+        self.s = _BRANCH_STREAMS[i] if i < len(_BRANCH_STREAMS) and inputs[0].is_cuda else None
+        self.ts = inputs
+        self.ctx = None
+
+    def __enter__(self):
+        if self.s is None:
+            return self
+        self.s.wait_stream(torch.cuda.current_stream(self.ts[0].device))
+        for t in self.ts:
+            t.record_stream(self.s)        # not recycled by the forking stream meanwhile
+        self.ctx = torch.cuda.stream(self.s)
+        self.ctx.__enter__()
+        return self
+
+    def __exit__(self, *exc):
+        if self.ctx is not None:
+            self.ctx.__exit__(*exc)
+        return False
+
+
+def join_branch(i: int, *outputs):
+    """Order the current stream after branch ``i`` and hand it ``outputs``."""
+    if i < len(_BRANCH_STREAMS) and outputs[0].is_cuda:
+        cur = torch.cuda.current_stream(outputs[0].device)
+        cur.wait_stream(_BRANCH_STREAMS[i])
+        for t in outputs:
+            t.record_stream(cur)
+    return outputs if len(outputs) > 1 else outputs[0]
+
+
 # ============================================================ Linear
 class _Linear(Function):
     @staticmethod

@@ -15,9 +15,10 @@ sys.path.insert(0, __file__.rsplit("/tools/", 1)[0])
 from tiresias_amd.executor.trainer import Trainer  # noqa: E402
 
 
-def bench(model, batch=None, steps=10, warmup=3, graph=False, overlap=None):
+def bench(model, batch=None, steps=10, warmup=3, graph=False, overlap=None, branches=None):
     dev = torch.device("cuda", 0)
-    t = Trainer(model, dev, batch=batch, use_graph=graph, overlap_wgrad=overlap)
+    t = Trainer(model, dev, batch=batch, use_graph=graph, overlap_wgrad=overlap,
+                branches=branches)
     for _ in range(warmup):
         t.step()
     torch.cuda.synchronize()
@@ -26,7 +27,7 @@ def bench(model, batch=None, steps=10, warmup=3, graph=False, overlap=None):
         t.step()
     torch.cuda.synchronize()
     dt = (time.perf_counter() - t0) / steps
-    return dict(model=model, batch=t.batch, graph=graph, overlap_wgrad=t.overlap_wgrad, ms_per_step=dt * 1e3,
+    return dict(model=model, batch=t.batch, graph=graph, overlap_wgrad=t.overlap_wgrad, branches=t.branches, ms_per_step=dt * 1e3,
                 samples_per_s=t.samples_per_step() / dt, loss=float(t.last_loss),
                 params=t.arena.numel, state_mb=t.state_bytes() / 2 ** 20)
 
@@ -40,6 +41,8 @@ def main():
     ap.add_argument("--out", default=None)
     ap.add_argument("--overlap", type=int, default=-1,
                     help="weight gradients on a side stream: -1 per-model default, 0 off, 1 on")
+    ap.add_argument("--branches", type=int, default=-1,
+                    help="model branch streams (GNMT's independent recurrences): -1 model default, 0 off, 1 on")
     ap.add_argument("--lib", type=int, default=-1,
                     help="plain-GEMM routing: -1 measured MFMA/hipBLASLt, 0 MFMA only, 1 library")
     a = ap.parse_args()
@@ -50,7 +53,7 @@ def main():
     res = []
     for m in a.models.split(","):
         r = bench(m, steps=a.steps, warmup=a.warmup, graph=a.graph,
-                  overlap=None if a.overlap < 0 else bool(a.overlap))
+                  overlap=None if a.overlap < 0 else bool(a.overlap), branches=None if a.branches < 0 else bool(a.branches))
         print(json.dumps(r), flush=True)
         res.append(r)
     routes = torch.ops.tam.gemm_routes().strip().splitlines()
