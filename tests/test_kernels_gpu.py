@@ -441,9 +441,11 @@ def test_relu_backward(gpu, n):
 
 
 # ------------------------------------------------------------------ optimizers
-def test_sgd_adam(gpu):
+@pytest.mark.parametrize("n", [4096 + 64, 9 * 2 ** 20 + 64])
+def test_sgd_adam(gpu, n):
+    """Small n: one pass of the grid; 9M+64: grid-stride loop (the grid is
+    capped at 1M float4 groups) with a partial last pass."""
     torch.manual_seed(10)
-    n = 4096 + 64
     w = torch.randn(n, device=gpu); g = torch.randn(n, device=gpu); m = torch.randn(n, device=gpu)
     wb = torch.empty(n, device=gpu, dtype=BF)
     w0, g0, m0 = w.clone(), g.clone(), m.clone()
@@ -453,7 +455,10 @@ def test_sgd_adam(gpu):
     w_ref = w0 - 0.1 * m_ref
     assert torch.allclose(m, m_ref, atol=1e-6) and torch.allclose(w, w_ref, atol=1e-6)
     assert torch.count_nonzero(g) == 0
-    assert torch.equal(wb, w_ref.to(BF))
+    # the shadow is the kernel's own master rounded (the fp32 references
+    # differ by FMA contraction, which moves a few of 9M values across a
+    # bf16 rounding boundary)
+    assert torch.equal(wb, w.to(BF))
     # Adam
     w = torch.randn(n, device=gpu); g = torch.randn(n, device=gpu)
     mm = torch.zeros(n, device=gpu); vv = torch.zeros(n, device=gpu)
