@@ -76,15 +76,16 @@ def _check(gpu, N, shape):
     gx = gx.permute(0, 2, 3, 1)
     if in_relu:
         gx = gx * (x.float() > 0)
-    dx = torch.empty_like(x)
+    finite = []
     if C % 8 == 0 and C > 8:            # stem input (C=8 padded RGB) needs no dgrad
+        dx = torch.empty_like(x)
         T.conv_dgrad(dy, w, torch.empty_like(w), dx, st, pd, 1, x if in_relu else None)
         errs["dgrad"] = _rel(dx, gx)
+        finite.append(dx)               # only tensors a kernel wrote (empty_like may hold NaN bits)
     dw = torch.full((K, R, R, C), 0.25, device=gpu)
     T.conv_wgrad(dy, x, dw, st, pd, 1, 1)
     errs["wgrad"] = _rel(dw, gw.permute(0, 2, 3, 1) + 0.25)
-    errs["finite"] = bool(torch.isfinite(y.float()).all() and torch.isfinite(dw).all()
-                          and torch.isfinite(dx.float()).all())
+    errs["finite"] = all(bool(torch.isfinite(t.float()).all()) for t in [y, dw, *finite])
     return errs
 
 
