@@ -4,20 +4,35 @@ replay on N MI355X GPUs (BASELINE.json metric).
 
 One benchmark *step* = one complete replay of a fixed, seeded, Philly
 (NSDI'19 Microsoft trace)-shaped job trace on the N GPUs of this node: real
-DDP training jobs (ResNet-50 / VGG-16 / Transformer-base / GNMT on the
-hand-written gfx950 kernels, synthetic data, random init) arrive over time,
-the Tiresias scheduler (discretized 2D-LAS on measured attained GPU service +
-skew-aware placement, HBM-resident preemption, xGMI state moves) time-slices
-them, and every job trains its full iteration budget. ``ms_per_step`` is
-therefore the replay makespan; ``value`` is the average job completion time
-(seconds, lower is better). Work scales with N (jobs per GPU fixed: weak
-scaling). The real NSDI'19 trace is not shipped with the reference and there
-is no network, so the trace is synthetic (``data`` says so).
+training jobs (ResNet-50 / VGG-16 / Transformer-base / GNMT on the
+hand-written gfx950 kernels, synthetic data, random init; multi-GPU jobs are
+DDP gangs over RCCL) arrive over time, the Tiresias scheduler (discretized
+2D-LAS on measured attained GPU service + skew-aware placement, HBM-resident
+preemption, xGMI state moves) time-slices them, and every job trains its full
+iteration budget. ``value`` is the average job completion time (seconds,
+lower is better), ``makespan_s`` the replay makespan.
 
-After the timed steps (outside the timed region) the same trace is replayed
-once under the reference's default FIFO + YARN-CS scheduler on the same GPUs:
-``vs_baseline`` = Tiresias avg JCT / FIFO avg JCT (< 1 is better), the
-comparison BASELINE.md defines until the real trace exists.
+The trace is compressed so one replay takes a few seconds yet stays
+scheduler-bound: ``--jobs-per-gpu`` (48) jobs per GPU with heavy-tailed
+(log-normal) service times carrying ``--work-s`` GPU-seconds of nominal work
+per GPU, arriving (Poisson) over work/``--load`` seconds, i.e. the offered
+load exceeds capacity and a queue builds — the regime where the policy
+decides JCT. Work scales with N (jobs per GPU fixed: weak scaling). The real
+NSDI'19 trace is not shipped with the reference and there is no network, so
+the trace is synthetic (``data`` says so).
+
+Fairness of the comparison (``vs_baseline``): after the timed steps, the same
+trace is replayed once under the reference's default FIFO + YARN-CS on the
+same GPUs with the SAME sharing setting; ``vs_baseline`` = Tiresias avg JCT /
+FIFO avg JCT (< 1 is better), the comparison BASELINE.md defines until the
+real trace exists. The Gittins/expected-remaining prior, when a policy needs
+one, comes from a held-out history trace (different seed), never from the
+replayed jobs.
+
+Time budget: the driver runs ``--steps 20 --warmup 5`` under a 600 s limit.
+A guard (``--budget-s``, measured from process start) stops early — before a
+step that would not fit — and the JSON line then reports the steps actually
+timed (``steps`` < ``steps_requested``).
 
   python bench.py --gpus N --steps K --warmup W
   python -m torch.distributed.run --nproc-per-node N --master-addr 127.0.0.1 \
@@ -25,17 +40,21 @@ comparison BASELINE.md defines until the real trace exists.
 """
 from __future__ import annotations
 
-import argparse
-import datetime
-import json
-import math
-import os
-import random
-import sys
 import time
 
-import torch
-import torch.distributed as dist
+T_PROC0 = time.perf_counter()
+
+import argparse  # noqa: E402
+import datetime  # noqa: E402
+import json  # noqa: E402
+import math  # noqa: E402
+import os  # noqa: E402
+import random  # noqa: E402
+import statistics  # noqa: E402
+import sys  # noqa: E402
+
+import torch  # noqa: E402
+import torch.distributed as dist  # noqa: E402
 
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
@@ -48,20 +67,23 @@ METRIC = "avg JCT + makespan on NSDI'19 Microsoft trace, 8×MI355X cluster"
 MODEL_MIX = [("resnet50", 0.35), ("vgg16", 0.20), ("transformer", 0.30), ("gnmt", 0.15)]
 TINY = {"resnet50": "resnet_tiny", "vgg16": "vgg_tiny", "transformer": "transformer_tiny",
         "gnmt": "gnmt_tiny"}
-GPU_DIST = [(1, 0.70), (2, 0.10), (4, 0.10), (8, 0.07), (16, 0.03)]
+GPU_DIST = [(1, 0.70), (2, 0.12), (4, 0.10), (8, 0.08)]
 # Frozen per-iteration seconds used ONLY to turn a sampled service time into an
-# iteration count (round-1 measured MI355X step times). Kept constant so the
-# benchmarked work (iterations per job) is identical across rounds: faster
-# kernels then show up as lower JCT, not as a bigger trace.
-TRACE_ITER_S = {"resnet50": 0.028, "vgg16": 0.015, "transformer": 0.016, "gnmt": 0.037}
+# iteration count (round-1 measured MI355X hipGraph step times,
+# profiles/model_bench_r1_v8.json). Kept constant so the benchmarked work
+# (iterations per job) is identical across rounds: faster kernels then show
+# up as lower JCT, not as a bigger trace.
+TRACE_ITER_S = {"resnet50": 0.0112, "vgg16": 0.0076, "transformer": 0.0068, "gnmt": 0.0153}
+HISTORY_SEED_OFFSET = 7919          # the held-out history trace for the service prior
 
 
-def bench_trace(n_gpus: int, jobs_per_gpu: int, seed: int, median_s: float = 0.3, sigma: float = 1.8,
-                load: float = 1.3, tiny: bool = False):
-    """Philly-shaped mini trace: ~70% 1-GPU jobs with a power-of-two gang
-    tail, heavy-tailed log-normal service times (sigma 1.8, i.e. most jobs
-    short, a few 25x longer, as in the NSDI'19 trace), Poisson arrivals at
-    ``load`` x capacity. Durations are compressed to seconds."""
+def bench_trace(n_gpus: int, jobs_per_gpu: int, seed: int, work_s: float = 5.0, load: float = 1.6,
+                sigma: float = 1.2, min_iters: int = 3, tiny: bool = False):
+    """Philly-shaped compressed trace: ~70 % 1-GPU jobs with a power-of-two
+    gang tail (gangs only when N allows), log-normal service (sigma 1.2: most
+    jobs short, a few ~15x the median, as in the NSDI'19 trace) rescaled so
+    the nominal GPU-work is ``work_s`` per GPU, Poisson arrivals over
+    ``work_s / load`` seconds."""
     rng = random.Random(seed)
     n = jobs_per_gpu * n_gpus
     dist_ = [(g, p) for g, p in GPU_DIST if g <= n_gpus]
@@ -69,24 +91,36 @@ def bench_trace(n_gpus: int, jobs_per_gpu: int, seed: int, median_s: float = 0.3
     gs, ps = [g for g, _ in dist_], [p / tot for _, p in dist_]
     names, ws = [m for m, _ in MODEL_MIX], [w for _, w in MODEL_MIX]
     rows = []
-    for i in range(n):
+    for _ in range(n):
         m = rng.choices(names, weights=ws)[0]
         g = rng.choices(gs, weights=ps)[0]
-        svc = min(15.0, max(0.2, rng.lognormvariate(math.log(median_s), sigma)))
-        it_s = TRACE_ITER_S[m] * (1.0 if g == 1 else 1.1)
-        iters = max(4, int(round(svc / it_s)))
-        rows.append((m, g, svc, iters))
-    mean_work = sum(svc * g for _, g, svc, _ in rows) / n
-    rate = load * n_gpus / mean_work
-    t = 0.0
-    jobs = []
-    for i, (m, g, svc, iters) in enumerate(rows):
-        model = TINY[m] if tiny else m
-        spec = JobSpec(job_id=str(i), submit_time=round(t, 4), duration=svc, num_gpu=g, model=m,
+        rows.append([m, g, rng.lognormvariate(0.0, sigma)])
+    def it_s(m, g):
+        return TRACE_ITER_S[m] * (1.0 if g == 1 else 1.1)
+
+    def iters_of(scale):
+        return [max(min_iters, int(round(x * scale / it_s(m, g)))) for m, g, x in rows]
+
+    # rescale so the nominal work (after the min_iters clamp) is work_s per GPU
+    target = work_s * n_gpus
+    scale = target / sum(x * g for _, g, x in rows)
+    for _ in range(8):
+        w = sum(k * it_s(m, g) * g for k, (m, g, _) in zip(iters_of(scale), rows))
+        scale *= target / w
+    span = work_s / load
+    rate = n / span
+    jobs, t = [], 0.0
+    for i, ((m, g, x), iters) in enumerate(zip(rows, iters_of(scale))):
+        spec = JobSpec(job_id=str(i), submit_time=round(t, 4), duration=iters * it_s(m, g), num_gpu=g, model=m,
                        iterations=iters, gpu_util_avg=90.0, gpu_util_max=99.0)
-        jobs.append(ReplayJob(spec=spec, model=model, iterations=iters))
+        jobs.append(ReplayJob(spec=spec, model=TINY[m] if tiny else m, iterations=iters))
         t += rng.expovariate(rate)
     return jobs
+
+
+def history_prior(jobs) -> list:
+    """GPU-seconds of a held-out trace: the scheduler's service-time history."""
+    return sorted(rj.spec.duration * rj.spec.num_gpu for rj in jobs)
 
 
 def scenario_trace(name: str, n_gpus: int, seed: int, tiny: bool = False):
@@ -113,11 +147,11 @@ def scenario_trace(name: str, n_gpus: int, seed: int, tiny: bool = False):
             t += rng.expovariate(4.0)
     elif name == "seq":
         t = 0.0
-        for i in range(4 * n_gpus):
+        for i in range(16 * n_gpus):
             m = "transformer" if i % 2 else "gnmt"
             g = rng.choice([g for g in (1, 1, 1, 2, 4) if g <= n_gpus])
-            rows.append((m, g, round(t, 4), int(min(400, max(8, rng.lognormvariate(math.log(40), 1.2))))))
-            t += rng.expovariate(3.0)
+            rows.append((m, g, round(t, 4), int(min(200, max(4, rng.lognormvariate(math.log(12), 1.2))))))
+            t += rng.expovariate(16.0)
     else:
         raise SystemExit(f"unknown scenario {name}")
     jobs = []
@@ -129,23 +163,23 @@ def scenario_trace(name: str, n_gpus: int, seed: int, tiny: bool = False):
 
 
 # scenario -> (policy, placement, ckpt policy, baseline policy, baseline placement,
-#              2D-LAS queue-0 limit in GPU-seconds (resnet4 is "no preemption"),
+#              2D-LAS queue limits in GPU-seconds (resnet4 is "no preemption"),
 #              GPU sharing when no GPU is free)
 SCENARIOS = {
-    "trace": ("dlas-gpu", "tiresias", "none", "fifo", "yarn", 1.0, True),
-    "resnet4": ("dlas-gpu", "tiresias", "none", "fifo", "yarn", 1e9, False),
-    "skew": ("dlas-gpu", "tiresias", "none", "dlas-gpu", "random", 1.0, False),
-    "seq": ("gittins", "tiresias", "host", "fifo", "yarn", 1.0, False),
+    "trace": ("dlas-gpu", "tiresias", "none", "fifo", "yarn", [0.05, 0.5], False),
+    "resnet4": ("dlas-gpu", "tiresias", "none", "fifo", "yarn", [1e9], False),
+    "skew": ("dlas-gpu", "tiresias", "none", "dlas-gpu", "random", [1.0], False),
+    "seq": ("gittins", "tiresias", "host", "fifo", "yarn", [0.05, 0.5], False),
 }
 # measured in-process co-run throughput of every model pair (tools/measure_stream_sharing.py)
 SHARING_TABLE = os.path.join(ROOT, "profiles", "stream_sharing_mi355x.json")
 
 
 def make_cfg(policy: str, scheme: str, n_gpus: int, seed: int, ckpt: str = "none",
-             qlimit: float = 1.0, share: bool = False) -> SimConfig:
-    return SimConfig(schedule=policy, scheme=scheme, num_queue=2, queue_limits=[qlimit], gittins_delta=1.0,
-                     solve_starvation=0.0, seed=seed, ckpt_policy=ckpt, pack=share,
-                     max_tasks_per_gpu=2 if share else 3,
+             qlimits=(1.0,), share: bool = False, gittins_delta: float = 0.02) -> SimConfig:
+    return SimConfig(schedule=policy, scheme=scheme, num_queue=len(qlimits) + 1, queue_limits=list(qlimits),
+                     gittins_delta=gittins_delta, solve_starvation=0.0, seed=seed, ckpt_policy=ckpt,
+                     pack=share, max_tasks_per_gpu=2 if share else 3,
                      interference_table=SHARING_TABLE if share else "",
                      cluster=ClusterSpec(num_switch=1, num_node_p_switch=1, num_gpu_p_node=n_gpus,
                                          num_cpu_p_node=max(128, 16 * n_gpus),
@@ -155,8 +189,8 @@ def make_cfg(policy: str, scheme: str, n_gpus: int, seed: int, ckpt: str = "none
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=2)
-    ap.add_argument("--warmup", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=5)
+    ap.add_argument("--warmup", type=int, default=2)
     ap.add_argument("--scenario", default="trace", choices=sorted(SCENARIOS),
                     help="trace: the headline Philly-shaped replay; resnet4 / skew / seq: "
                          "BASELINE.json configs 2-4 (policy defaults follow the scenario)")
@@ -166,20 +200,25 @@ def main():
     ap.add_argument("--baseline-policy", default=None)
     ap.add_argument("--baseline-placement", default=None)
     ap.add_argument("--no-baseline", action="store_true")
-    ap.add_argument("--no-share", action="store_true",
-                    help="exclusive GPUs only (no co-location of 1-GPU jobs when the cluster is full)")
-    ap.add_argument("--no-exclusive-ref", action="store_true",
-                    help="skip the untimed exclusive-GPU Tiresias replay reported next to the result")
-    ap.add_argument("--jobs-per-gpu", type=int, default=16)
-    ap.add_argument("--quantum", type=float, default=0.1)
+    ap.add_argument("--share", action="store_true",
+                    help="co-locate 1-GPU jobs when the cluster is full (Tiresias AND baseline)")
+    ap.add_argument("--jobs-per-gpu", type=int, default=48)
+    ap.add_argument("--work-s", type=float, default=None,
+                    help="nominal GPU-seconds of work per GPU per replay (default 5.0; 0.5 with --cpu)")
+    ap.add_argument("--min-iters", type=int, default=3, help="shortest job, iterations")
+    ap.add_argument("--load", type=float, default=1.6, help="offered load / capacity during arrivals")
+    ap.add_argument("--quantum", type=float, default=0.02, help="scheduling round, seconds")
     ap.add_argument("--seed", type=int, default=2019)
+    ap.add_argument("--budget-s", type=float, default=float(os.environ.get("TAM_BENCH_BUDGET_S", 270)),
+                    help="wall budget from process start; steps that would not fit are skipped")
     ap.add_argument("--cpu", action="store_true", help="gloo/CPU rehearsal with tiny models")
     ap.add_argument("--no-graph", action="store_true",
                     help="disable hipGraph capture of 1-GPU jobs' fwd+bwd (eager launches)")
+    ap.add_argument("--no-pool", action="store_true", help="no warm trainer reuse between jobs")
     ap.add_argument("--out", default=None, help="directory for job.csv / summary.json of the last step")
     a = ap.parse_args()
     pol, plc, ck, bpol, bplc, qlim, share = SCENARIOS[a.scenario]
-    share = share and not a.no_share
+    share = share or a.share
     a.policy = a.policy or pol
     a.placement = a.placement or plc
     a.ckpt = a.ckpt or ck
@@ -193,17 +232,18 @@ def main():
         raise SystemExit(f"--gpus {a.gpus} but WORLD_SIZE={world}")
     n = max(a.gpus, world)
     use_cuda = torch.cuda.is_available() and not a.cpu
+    work_s = a.work_s if a.work_s is not None else (5.0 if use_cuda else 0.5)
     device = torch.device("cuda", local) if use_cuda else torch.device("cpu")
     ctrl_pg = world_pg = None
     if world > 1:
         if use_cuda:
             torch.cuda.set_device(device)
             dist.init_process_group("nccl", device_id=device,
-                                    timeout=datetime.timedelta(seconds=600))
+                                    timeout=datetime.timedelta(seconds=300))
         else:
-            dist.init_process_group("gloo", timeout=datetime.timedelta(seconds=600))
+            dist.init_process_group("gloo", timeout=datetime.timedelta(seconds=300))
         world_pg = dist.group.WORLD
-        ctrl_pg = dist.new_group(backend="gloo", timeout=datetime.timedelta(seconds=600))
+        ctrl_pg = dist.new_group(backend="gloo", timeout=datetime.timedelta(seconds=300))
         # warm the world communicator so later P2P / sub-groups do not need every rank
         tmp = torch.ones(1, device=device)
         dist.all_reduce(tmp)
@@ -212,12 +252,18 @@ def main():
 
         _lib.load(required=True)
 
+    tiny = not use_cuda
     if a.scenario == "trace":
-        jobs = bench_trace(n, a.jobs_per_gpu, a.seed, tiny=not use_cuda)
+        jobs = bench_trace(n, a.jobs_per_gpu, a.seed, work_s=work_s, load=a.load, min_iters=a.min_iters,
+                           tiny=tiny)
+        prior = history_prior(bench_trace(n, a.jobs_per_gpu, a.seed + HISTORY_SEED_OFFSET,
+                                          work_s=work_s, load=a.load, min_iters=a.min_iters))
     else:
-        jobs = scenario_trace(a.scenario, n, a.seed, tiny=not use_cuda)
+        jobs = scenario_trace(a.scenario, n, a.seed, tiny=tiny)
+        prior = history_prior(scenario_trace(a.scenario, n, a.seed + HISTORY_SEED_OFFSET))
     cfg = make_cfg(a.policy, a.placement, n, a.seed, a.ckpt, qlim, share)
-    worker = Worker(rank, world, device, world_pg, use_graph=use_cuda and not a.no_graph)
+    worker = Worker(rank, world, device, world_pg, use_graph=use_cuda and not a.no_graph,
+                    pool_cap=0 if a.no_pool else 2)
 
     def sync():
         if world > 1:
@@ -228,80 +274,112 @@ def main():
     def replay(c, out=None):
         t = time.perf_counter()
         r = run_replay(c, jobs, rank, world, device, ctrl_pg=ctrl_pg, world_pg=world_pg,
-                       worker=worker, quantum=a.quantum, out_dir=out)
+                       worker=worker, quantum=a.quantum, out_dir=out, prior=prior)
+        dt = time.perf_counter() - t
         if rank == 0:                  # progress on stderr (the JSON line stays alone on stdout)
             print(f"[bench] {c.schedule}+{c.scheme}{' share' if c.pack else ''}: avg JCT "
                   f"{r['avg_jct']:.4f} s, makespan {r['makespan']:.3f} s, {r['finished']} jobs, "
-                  f"wall {time.perf_counter() - t:.1f} s", file=sys.stderr, flush=True)
-        return r
+                  f"util {r['gpu_utilization']:.3f}, wall {dt:.2f} s (t={time.perf_counter() - T_PROC0:.0f}s)",
+                  file=sys.stderr, flush=True)
+        return r, dt
 
-    for _ in range(a.warmup):
-        replay(cfg)
+    def fits(longest: float) -> bool:
+        """Every rank takes the same decision (rank 0's clock, broadcast)."""
+        ok = torch.tensor([1 if time.perf_counter() - T_PROC0 + 1.25 * longest <= a.budget_s else 0])
+        if world > 1:
+            dist.broadcast(ok, 0, group=ctrl_pg)
+        return bool(ok.item())
+
+    longest = 0.0
+    warm_done = 0
+    for k in range(a.warmup):
+        if k > 0 and not fits(longest):
+            break
+        _, dt = replay(cfg)
+        longest = max(longest, dt)
+        warm_done += 1
     sync()
     t0 = time.perf_counter()
     sums = []
+    walls = []
     for k in range(a.steps):
-        s = replay(cfg, a.out if (a.out and k == a.steps - 1) else None)
+        if k > 0 and not fits(longest):
+            break
+        s, dt = replay(cfg, a.out if (a.out and k == a.steps - 1) else None)
+        longest = max(longest, dt)
         sums.append(s)
+        walls.append(dt)
     sync()
     elapsed = time.perf_counter() - t0
     if world > 1:
         t = torch.tensor([elapsed], dtype=torch.float64)
         dist.all_reduce(t, op=dist.ReduceOp.MAX, group=ctrl_pg)
         elapsed = float(t.item())
+    steps = len(sums)
 
     base = None
-    if not a.no_baseline:
-        bcfg = make_cfg(a.baseline_policy, a.baseline_placement, n, a.seed, a.ckpt, qlim)
-        base = replay(bcfg)
-    excl = None
-    if share and not a.no_exclusive_ref:
-        # the same Tiresias policy without GPU sharing (how much sharing buys)
-        excl = replay(make_cfg(a.policy, a.placement, n, a.seed, a.ckpt, qlim, False))
+    if not a.no_baseline and fits(3.0 * longest):
+        # FIFO is non-preemptive: its replay can run longer than Tiresias'
+        bcfg = make_cfg(a.baseline_policy, a.baseline_placement, n, a.seed, a.ckpt, qlim, share)
+        base, _ = replay(bcfg)
 
     if rank == 0:
-        avg_jct = sum(s["avg_jct"] for s in sums) / len(sums)
-        makespan = sum(s["makespan"] for s in sums) / len(sums)
+        jcts = [s["avg_jct"] for s in sums]
+        mks = [s["makespan"] for s in sums]
+        avg_jct = statistics.fmean(jcts)
+        makespan = statistics.fmean(mks)
         line = {
             "metric": METRIC,
             "value": round(avg_jct, 4),
             "unit": "s (avg JCT)",
             "n_gpus": n,
-            "steps": a.steps,
-            "warmup": a.warmup,
-            "ms_per_step": round(elapsed / a.steps * 1e3, 2),
+            "steps": steps,
+            "warmup": warm_done,
+            "ms_per_step": round(elapsed / steps * 1e3, 2),
             "higher_is_better": False,
             "scaling": "weak",
             "vs_baseline": round(avg_jct / base["avg_jct"], 4) if base else None,
             "dtype": "bf16",
-            "data": "synthetic (Philly/NSDI'19-shaped trace, random-init weights, synthetic batches)",
+            "data": "synthetic (Philly/NSDI'19-shaped compressed trace, random-init weights, synthetic batches)",
             "config": {
-                "model": "mixed: resnet50 / vgg16 / transformer-base / gnmt DDP jobs",
+                "model": "mixed: resnet50 / vgg16 / transformer-base / gnmt jobs (DDP gangs when N>1)",
                 "global_batch": "per job: per-GPU batch x gang size (64 img / 32 img / 32x128 tok / 64x50 tok)",
                 "seq_len": "128 (transformer), 50 (gnmt)",
                 "parallelism": f"dp (gang DDP over RCCL), {n} GPU cluster",
                 "scenario": a.scenario,
                 "ckpt": a.ckpt,
                 "trace_jobs": len(jobs),
-                "hip_graph_1gpu_jobs": bool(use_cuda and not a.no_graph),
                 "jobs_per_gpu": a.jobs_per_gpu,
-                "policy": f"{a.policy} + {a.placement} placement (Tiresias)"
+                "work_gpu_s_per_gpu": work_s,
+                "offered_load": a.load,
+                "hip_graph_1gpu_jobs": bool(use_cuda and not a.no_graph),
+                "warm_trainer_pool": not a.no_pool,
+                "policy": f"{a.policy} + {a.placement} placement (Tiresias), queue limits {qlim} GPU-s"
                           + (" + GPU sharing when full" if share else ""),
-                "baseline": f"{a.baseline_policy} + {a.baseline_placement}",
+                "baseline": f"{a.baseline_policy} + {a.baseline_placement}"
+                            + (" + GPU sharing when full" if share else ""),
+                "prior": "held-out history trace (seed + %d)" % HISTORY_SEED_OFFSET,
                 "quantum_s": a.quantum,
             },
+            "steps_requested": a.steps,
+            "warmup_requested": a.warmup,
             "makespan_s": round(makespan, 4),
-            "median_jct_s": round(sum(s["median_jct"] for s in sums) / len(sums), 4),
-            "p95_jct_s": round(sum(s["p95_jct"] for s in sums) / len(sums), 4),
+            "avg_jct_per_step_s": [round(x, 4) for x in jcts],
+            "avg_jct_stdev_s": round(statistics.stdev(jcts), 4) if len(jcts) > 1 else 0.0,
+            "makespan_per_step_s": [round(x, 4) for x in mks],
+            "replay_wall_per_step_s": [round(x, 3) for x in walls],
+            "median_jct_s": round(statistics.fmean(s["median_jct"] for s in sums), 4),
+            "p95_jct_s": round(statistics.fmean(s["p95_jct"] for s in sums), 4),
             "preemptions": sums[-1]["preemptions"],
             "finished_jobs": sums[-1]["finished"],
             "baseline_avg_jct_s": round(base["avg_jct"], 4) if base else None,
             "baseline_makespan_s": round(base["makespan"], 4) if base else None,
-            "tiresias_exclusive_avg_jct_s": round(excl["avg_jct"], 4) if excl else None,
-            "tiresias_exclusive_makespan_s": round(excl["makespan"], 4) if excl else None,
             "shared_rounds": sums[-1].get("shared_rounds"),
-            "gpu_utilization": round(sums[-1]["gpu_utilization"], 4),
+            "gpu_utilization": round(statistics.fmean(s["gpu_utilization"] for s in sums), 4),
             "runtime_breakdown_s": sums[-1].get("runtime_breakdown"),
+            "pool_hits": worker.pool_hits,
+            "max_hbm_reserved_gb": round(torch.cuda.max_memory_reserved(device) / 2 ** 30, 2) if use_cuda else None,
+            "process_wall_s": round(time.perf_counter() - T_PROC0, 1),
             "device": torch.cuda.get_device_name(device) if use_cuda else "cpu",
         }
         print(json.dumps(line), flush=True)

@@ -32,15 +32,28 @@ struct Job {
   double attained(bool g) const { return g ? executed * gpu : executed; }
 };
 
+// Gittins index over a HISTORY sample (prior file), or -- online mode, no
+// prior -- over the services of the jobs finished so far; rebuilt when the
+// sample grew by 10 % (policy/las.py::GittinsTable applies the same rule).
 struct Gittins {
-  std::vector<double> d, prefix;
+  std::vector<double> samples, d, prefix;
   double delta = 1;
+  size_t next_build = 0;
   void init(std::vector<double> data, double dl) {
-    d = std::move(data);
-    std::sort(d.begin(), d.end());
+    samples = std::move(data);
     delta = dl;
+    build();
+  }
+  void build() {
+    d = samples;
+    std::sort(d.begin(), d.end());
     prefix.assign(d.size() + 1, 0.0);
     for (size_t i = 0; i < d.size(); ++i) prefix[i + 1] = prefix[i] + d[i];
+    next_build = std::max(d.size() + 1, (size_t)((double)d.size() * 1.1));
+  }
+  void add(double s) {
+    samples.push_back(s);
+    if (samples.size() >= next_build) build();
   }
   double index(double a) const {
     const long n = (long)d.size();
@@ -73,9 +86,11 @@ inline Pol parse(const std::string& s) {
 
 class Engine {
  public:
+  // online_prior: the prior starts empty and learns from finished jobs
   Engine(const std::string& policy, int total_gpus, std::vector<double> limits, double starve,
-         double gittins_delta, std::vector<double> prior)
-      : pol_(parse(policy)), total_(total_gpus), limits_(std::move(limits)), starve_(starve) {
+         double gittins_delta, std::vector<double> prior, bool online_prior = false)
+      : pol_(parse(policy)), total_(total_gpus), limits_(std::move(limits)), starve_(starve),
+        online_(online_prior) {
     std::sort(limits_.begin(), limits_.end());
     nq_ = (int)limits_.size() + 1;
     if (pol_ == DLASGG || pol_ == GITT) git_.init(std::move(prior), gittins_delta);
@@ -197,12 +212,14 @@ class Engine {
         j.state = DONE;
         j.end = now_;
         used_ -= j.gpu;
+        if (online_ && (pol_ == DLASGG || pol_ == GITT)) git_.add(j.total_exec * j.gpu);
         active_.erase(active_.begin() + a);
       } else {
         ++a;
       }
     }
-    while (cursor_ < (long)arrival_order_.size() && jobs_[arrival_order_[cursor_]].submit <= now_ + EPS) {
+    // arrivals within the clock tolerance of now (the loop snaps such events to now)
+    while (cursor_ < (long)arrival_order_.size() && jobs_[arrival_order_[cursor_]].submit <= now_ + std::max(EPS, tol)) {
       Job& j = jobs_[arrival_order_[cursor_++]];
       j.state = PEND;
       j.last_check = now_;
@@ -225,14 +242,17 @@ class Engine {
 
   void update() {
     const bool g = gputime();
+    // the same relative tolerance as the event clock: a threshold whose
+    // remaining time rounds to "now" fires now instead of stalling the loop
+    const double tol = 1e-9 * std::max(1.0, now_);
     for (long k : active_) {
       Job& j = jobs_[k];
       if (is_dlas()) {
         const double a = j.attained(g);
         if (j.state == RUN) {
-          while (j.q < nq_ - 1 && a >= limits_[j.q] - 1e-9) enter(j, j.q + 1);
+          while (j.q < nq_ - 1 && a >= limits_[j.q] - tol * (g ? j.gpu : 1)) enter(j, j.q + 1);
         } else if (starve_ > 0 && j.state == PEND && j.q > 0 && j.executed > 0 &&
-                   j.last_pending >= j.executed * starve_ - 1e-9) {
+                   j.last_pending >= j.executed * starve_ - tol) {
           j.executed = 0; j.last_pending = 0; j.promote++;
           enter(j, 0);
         }
@@ -250,9 +270,8 @@ class Engine {
       case SJF: return x.gpu != y.gpu ? x.gpu < y.gpu : sub(x, y);
       case SRTF: { const double a = x.remaining(), b = y.remaining(); return a != b ? a < b : sub(x, y); }
       case SRSF: { const double a = x.remaining() * x.gpu, b = y.remaining() * y.gpu; return a != b ? a < b : sub(x, y); }
-      case DLAS: case DLASG:
+      case DLAS: case DLASG:   // queue-entry order: demoted jobs queue behind pending ones
         if (x.q != y.q) return x.q < y.q;
-        if (rx != ry) return rx < ry;
         return x.seq < y.seq;
       case DLASGG:
         if (x.q != y.q) return x.q < y.q;
@@ -269,7 +288,7 @@ class Engine {
 
   void start(Job& j) {
     if (j.start < 0) j.start = now_;
-    j.state = RUN; j.resume++; j.last_pending = 0; j.last_check = now_;
+    j.state = RUN; j.resume++; j.last_check = now_;   // last_pending kept until promotion
     used_ += j.gpu;
   }
   void preempt(Job& j) {
@@ -304,6 +323,7 @@ class Engine {
 
   Pol pol_;
   int total_;
+  bool online_ = false;
   std::vector<double> limits_;
   double starve_;
   int nq_;

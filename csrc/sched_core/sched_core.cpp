@@ -52,9 +52,9 @@ py::dict run_py(Engine& e, py::array_t<double> submit, py::array_t<double> dur, 
 PYBIND11_MODULE(_sched_core, m) {
   m.doc() = "tiresias_amd native event-engine core (count placement)";
   py::class_<Engine>(m, "Engine")
-      .def(py::init<const std::string&, int, std::vector<double>, double, double, std::vector<double>>(),
+      .def(py::init<const std::string&, int, std::vector<double>, double, double, std::vector<double>, bool>(),
            py::arg("policy"), py::arg("total_gpus"), py::arg("queue_limits") = std::vector<double>{},
            py::arg("solve_starvation") = 0.0, py::arg("gittins_delta") = 3250.0,
-           py::arg("prior") = std::vector<double>{})
+           py::arg("prior") = std::vector<double>{}, py::arg("online_prior") = false)
       .def("run", &run_py, py::arg("submit"), py::arg("duration"), py::arg("gpus"));
 }

@@ -324,3 +324,71 @@ def test_sharing_yields_to_blocked_gang():
     # the 1-GPU jobs are demoted (2 GPU-s limit) long before t=5: the new gang
     # is top priority and starts on arrival although all 4 jobs were co-located
     assert gang.start_time == pytest.approx(5.0)
+
+
+# ------------------------------------------------------------------ 2D-LAS queue order (reference run_sim.py:752-757, 837-847)
+def _one_gpu(policy, **kw):
+    return SimConfig(schedule=policy, scheme="count", num_queue=2, queue_limits=[10.0],
+                     cluster=ClusterSpec(num_switch=1, num_node_p_switch=1, num_gpu_p_node=1,
+                                         num_cpu_p_node=100, mem_p_node=1000), **kw)
+
+
+def test_dlas_demoted_job_queues_behind_pending():
+    """A is demoted to Q1 (t=10) and preempted by B (t=15). When B is demoted
+    at t=25 it joins the TAIL of Q1, behind the already-pending A: A runs."""
+    from tiresias_amd.engine.sim import Simulator
+
+    def at(t):
+        sim = Simulator(_one_gpu("dlas"), [spec("A", d=100.0, t=0.0), spec("B", d=100.0, t=15.0)])
+        sim.run(until=t)
+        return sim.jobs["A"], sim.jobs["B"]
+
+    a, b = at(20.0)
+    assert b.is_running and a.is_pending and a.queue == 1
+    a, b = at(26.0)
+    assert a.is_running and b.is_pending and b.queue == 1
+
+
+def test_last_pending_time_kept_until_promotion():
+    """Starvation clock (reference :767-778): pending stretches since the job
+    first ran accumulate across resumes; only a promotion clears them."""
+    j = Job(spec("x", d=100.0))
+    j.arrive(0.0)
+    j.start(0.0, {"1": [0]})
+    j.advance(5.0)
+    j.preempt(5.0)
+    j.advance(8.0)
+    j.start(8.0, {"1": [0]})
+    assert j.last_pending_time == pytest.approx(3.0)
+    j.advance(9.0)
+    j.preempt(9.0)
+    j.advance(11.0)
+    assert j.last_pending_time == pytest.approx(5.0)
+
+
+def test_gittins_prior_never_sees_the_future():
+    """Without a history file the Gittins table only holds FINISHED jobs'
+    services (online); the replayed trace's own distribution needs an explicit
+    opt-in and is flagged."""
+    from tiresias_amd.engine.sim import Simulator
+
+    specs = [spec(i, d=float(5 + 7 * i), t=float(i)) for i in range(6)]
+    sim = Simulator(_one_gpu("gittins", gittins_delta=4.0), specs)
+    assert sim.policy.table.data == []
+    s = sim.run()
+    assert s["prior"] == "online" and s["finished"] == 6
+    got = sorted(sim.policy.table._samples)
+    want = sorted(j.total_executed * j.num_gpu for j in sim.jobs.values())
+    assert got == pytest.approx(want)
+    oracle = Simulator(_one_gpu("gittins", gittins_delta=4.0, prior_mode="oracle"), specs)
+    assert oracle.prior_source == "oracle" and len(oracle.policy.table.data) == 6
+
+
+def test_gittins_prior_from_history_file(tmp_path):
+    from tiresias_amd.engine.sim import Simulator
+
+    p = tmp_path / "hist.csv"
+    p.write_text("job_id,duration\n" + "".join(f"{i},{10 * (i + 1)}\n" for i in range(20)))
+    sim = Simulator(_one_gpu("dlas-gpu-gittins", gittins_prior=str(p)), [spec(0, d=5.0)])
+    sim.run()
+    assert sim.prior_source == "file" and len(sim.policy.gittins.data) == 20

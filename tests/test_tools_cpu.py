@@ -156,8 +156,62 @@ def test_bench_scenarios_fit_cluster(scenario, n):
     pol, plc, ck, bpol, bplc, qlim, share = bench.SCENARIOS[scenario]
     cfg = bench.make_cfg(pol, plc, n, 1, ck, qlim, share)
     assert cfg.pack == share
-    assert cfg.queue_limits == [qlim]
+    assert cfg.queue_limits == list(qlim) and cfg.num_queue == len(qlim) + 1
     if scenario == "resnet4":
-        assert qlim >= 1e6 and len(jobs) == 4
+        assert min(qlim) >= 1e6 and len(jobs) == 4
     if scenario == "seq":
         assert pol == "gittins" and ck == "host"
+
+
+def test_bench_trace_is_scheduler_bound():
+    """The headline trace: >= 48 jobs per GPU, offered load above capacity
+    (arrival span < nominal work), heavy-tailed, seeded, gangs only when N
+    allows, and the Gittins prior comes from a DIFFERENT (held-out) trace."""
+    import bench
+
+    for n in (1, 8):
+        jobs = bench.bench_trace(n, 48, 2019, work_s=5.0, load=1.6)
+        assert len(jobs) == 48 * n and all(1 <= j.spec.num_gpu <= n for j in jobs)
+        work = sum(j.spec.duration * j.spec.num_gpu for j in jobs) / n
+        span = max(j.spec.submit_time for j in jobs)
+        assert 4.5 < work < 5.8 and span < work
+        svc = sorted(j.spec.duration for j in jobs)
+        assert svc[-1] > 10 * svc[len(svc) // 2]              # heavy tail
+        if n == 1:
+            assert all(j.spec.num_gpu == 1 for j in jobs)
+        else:
+            assert any(j.spec.num_gpu > 1 for j in jobs)
+    a = bench.bench_trace(1, 48, 2019)
+    b = bench.bench_trace(1, 48, 2019)
+    assert [(j.model, j.iterations) for j in a] == [(j.model, j.iterations) for j in b]
+    h = bench.bench_trace(1, 48, 2019 + bench.HISTORY_SEED_OFFSET)
+    assert [j.iterations for j in h] != [j.iterations for j in a]
+
+
+def test_bench_cpu_driver_contract(tmp_path):
+    """``bench.py --cpu --steps 20 --warmup 5`` (the driver's arguments) must
+    finish well inside its budget and print one valid JSON line."""
+    import json as _json
+    import subprocess
+    import sys
+    import time as _t
+
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    t = _t.perf_counter()
+    r = subprocess.run([sys.executable, os.path.join(root, "bench.py"), "--cpu", "--steps", "20",
+                        "--warmup", "5", "--jobs-per-gpu", "48", "--work-s", "0.05", "--min-iters", "1"],
+                       capture_output=True, text=True, timeout=240, cwd=str(tmp_path))
+    wall = _t.perf_counter() - t
+    assert r.returncode == 0, r.stderr[-3000:]
+    lines = [x for x in r.stdout.splitlines() if x.startswith("{")]
+    assert len(lines) == 1
+    d = _json.loads(lines[0])
+    assert d["metric"] == bench_metric() and d["steps"] == 20 and d["warmup"] == 5
+    assert d["finished_jobs"] == 48 and d["value"] > 0 and d["vs_baseline"] is not None
+    assert d["ms_per_step"] * d["steps"] / 1e3 < wall
+
+
+def bench_metric():
+    import bench
+
+    return bench.METRIC

@@ -50,7 +50,10 @@ def define_flags() -> None:
     D.DEFINE_list("queue_limits", [], "MLFQ demotion thresholds (service units), e.g. 3600,7200")
     D.DEFINE_float("solve_starvation", 0.0, "promote to Q0 when pending >= executed * this (0=off)")
     D.DEFINE_float("gittins_delta", 3250.0, "Gittins quantum (service units)")
-    D.DEFINE_string("gittins_prior", "", "csv with a duration column for the Gittins / expected-remaining prior")
+    D.DEFINE_string("gittins_prior", "", "history csv with a duration column (GPU-service) for the "
+                    "Gittins / expected-remaining prior (reference yarn-gput1000.csv)")
+    D.DEFINE_string("prior_mode", "online", "without --gittins_prior: online (learn from finished jobs) | "
+                    "oracle (the replayed trace's own distribution; flagged in summary.json)")
     D.DEFINE_integer("seed", 0, "RNG seed (all randomness is seeded)")
     D.DEFINE_string("backend", "sim", "sim | fake | mi355x")
     D.DEFINE_string("engine", "event", "event (discrete-event) | tick (reference-compatible tick loop)")
@@ -134,6 +137,7 @@ class SimConfig:
     solve_starvation: float = 0.0
     gittins_delta: float = 3250.0
     gittins_prior: str = ""
+    prior_mode: str = "online"        # no prior file: online (finished jobs) | oracle (trace itself)
     seed: int = 0
     engine: str = "event"
     time_unit: float = 1.0

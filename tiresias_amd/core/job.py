@@ -195,7 +195,9 @@ class Job:
         # stall before progress resumes: restore + the save of the last preemption
         self.restore_left = restore_cost + self.extra.pop("pending_ckpt", 0.0)
         self.overhead_time += restore_cost
-        self.last_pending_time = 0.0
+        # last_pending_time is NOT reset on resume: like the reference
+        # (run_sim.py:767-778) it accumulates every pending stretch since the
+        # job first ran and is cleared only by a starvation promotion
         self.last_check = now
 
     def preempt(self, now: float, ckpt_cost: float = 0.0, ckpt_bytes: float = 0.0) -> None:

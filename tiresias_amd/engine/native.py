@@ -35,11 +35,20 @@ def simulate_native(cfg: SimConfig, specs: List[JobSpec], prior: Optional[List[f
     if cfg.schedule not in SUPPORTED:
         raise ValueError(f"native core supports {SUPPORTED}, not {cfg.schedule}")
     limits = list(cfg.queue_limits) or default_limits(cfg.num_queue if cfg.num_queue > 1 else 2, 3600.0)
-    if prior is None:
-        prior = sorted(s.duration * s.num_gpu for s in specs)
+    # prior: same rules as engine/sim.py::Simulator._prior (history, never the future)
+    source = "explicit"
+    if prior is None and cfg.gittins_prior:
+        from ..trace.readers import read_duration_prior
+
+        prior, source = read_duration_prior(cfg.gittins_prior), "file"
+    elif prior is None and cfg.prior_mode == "oracle":
+        prior, source = sorted(s.duration * s.num_gpu for s in specs), "oracle"
+    online = prior is None
+    if online:
+        prior, source = [], "online"
     eng = _sched_core.Engine(cfg.schedule, cfg.cluster.num_gpus, [float(x) for x in limits],
                              float(cfg.solve_starvation), float(cfg.gittins_delta or 3250.0),
-                             [float(x) for x in prior])
+                             [float(x) for x in prior], online)
     t0 = time.perf_counter()
     out = eng.run(np.array([s.submit_time for s in specs], dtype=np.float64),
                   np.array([s.duration for s in specs], dtype=np.float64),
@@ -56,5 +65,5 @@ def simulate_native(cfg: SimConfig, specs: List[JobSpec], prior: Optional[List[f
                 p95_jct=percentile(jct.tolist(), 95), makespan=float(end.max() - t_first) if done.any() else 0.0,
                 avg_queueing_delay=float((start - sub)[done].mean()) if done.any() else 0.0,
                 preemptions=int(out["preempt"].sum()), promotions=int(out["promote"].sum()),
-                events=int(out["events"]), wall_s=wall, schedule=cfg.schedule, scheme="count",
+                events=int(out["events"]), wall_s=wall, schedule=cfg.schedule, scheme="count", prior=source,
                 per_job={"start": start, "end": end, "preempt": out["preempt"]})

@@ -96,13 +96,27 @@ class Simulator:
         self.max_gpus = self.cluster.num_gpus
         self._gpn = gpn
 
-    @staticmethod
-    def _prior(specs, prior):
+    def _prior(self, specs, prior):
+        """The service prior comes from HISTORY (reference ``run_sim.py:
+        1682-1707`` reads ``yarn-gput1000.csv``, a different trace): an
+        explicit sample, else ``cfg.gittins_prior`` (csv with a duration
+        column), else None = learned online from finished jobs. The trace's
+        own (future) distribution is used only on request
+        (``cfg.prior_mode == "oracle"``) and is flagged in the summary."""
+        self.prior_source = "explicit"
         if prior is not None:
-            return prior
-        # Tiresias learns the service distribution from history; absent a
-        # history file, use the trace's own GPU-service distribution
-        return sorted(s.duration * s.num_gpu for s in specs)
+            return list(prior)
+        path = getattr(self.cfg, "gittins_prior", "")
+        if path:
+            from ..trace.readers import read_duration_prior
+
+            self.prior_source = "file"
+            return read_duration_prior(path)
+        if getattr(self.cfg, "prior_mode", "online") == "oracle":
+            self.prior_source = "oracle"
+            return sorted(s.duration * s.num_gpu for s in specs)
+        self.prior_source = "online"
+        return None
 
     def submit(self, spec: JobSpec) -> Job:
         """Online job submission (live runtime's spool API): registers the job;
@@ -146,6 +160,7 @@ class Simulator:
         self.cluster.release(j)
         j.finish(self.now)
         self.ckpt.on_finish(j)
+        self.policy.on_finish(j, self.now)
         self.active.remove(j)
         self.finished.append(j)
         self.log.job_row(self.now, j)
@@ -274,9 +289,10 @@ class Simulator:
                   (j.remaining <= EPS * max(1.0, j.spec.duration) or j.time_to_finish() <= tol)]:
             j.progress = j.spec.duration
             self._finish(j)
-        for s in self.reader.release(self.now + EPS):
+        # arrivals within the clock tolerance of now (run() snaps such events to now)
+        for s in self.reader.release(self.now + max(EPS, tol)):
             j = self.jobs[s.job_id]
-            j.arrive(max(self.now, s.submit_time))
+            j.arrive(self.now)
             j.last_check = self.now
             self.policy.on_arrival(j, self.now)
             self.active.append(j)
@@ -340,7 +356,7 @@ class Simulator:
     def summary(self) -> Dict:
         return self.log.summary(list(self.jobs.values()), self.cluster.num_gpus, self.wall_s,
                                 extra=dict(schedule=self.cfg.schedule, scheme=self.scheme,
-                                           events=self.events))
+                                           events=self.events, prior=self.prior_source))
 
 
 class TickSimulator(Simulator):

@@ -99,7 +99,7 @@ class ReplayJob:
 
 class Controller:
     def __init__(self, cfg: SimConfig, jobs: List[ReplayJob], world: int, quantum: float,
-                 logger: Optional[MetricsLogger] = None, spool=None):
+                 logger: Optional[MetricsLogger] = None, spool=None, prior: Optional[List[float]] = None):
         self.cfg = cfg
         self.spool = spool            # executor.spool.Spool: online job submission
         self._status_t = -1e9
@@ -110,10 +110,11 @@ class Controller:
             s = rj.spec
             # duration in work units = iterations (progress is reported in iterations)
             specs.append(JobSpec(**{**s.__dict__, "duration": float(rj.iterations)}))
-        prior = sorted(rj.iterations * self._iter_est(rj.model, rj.spec.num_gpu) * rj.spec.num_gpu
-                       for rj in jobs)
-        # serve-only clusters start with no history: a one-point prior until jobs finish
-        self.sched = LiveScheduler(cfg, specs, logger=logger, prior=prior or [1.0])
+        # the Gittins / expected-remaining prior is HISTORY in GPU-seconds: an
+        # explicit sample (e.g. a held-out trace), cfg.gittins_prior, or --
+        # with neither -- learned online from the jobs that finish (measured
+        # wall seconds x GPUs). Never the replayed jobs' own (future) sizes.
+        self.sched = LiveScheduler(cfg, specs, logger=logger, prior=prior)
         self.world = world
         self.quantum = quantum
         self.gpn = self.sched.cluster.spec.num_gpu_p_node
@@ -315,8 +316,15 @@ class Controller:
 
 class Worker:
     def __init__(self, rank: int, world: int, device: torch.device, world_pg=None, use_graph=False,
-                 gang_backend: Optional[str] = None, monitor_period: float = 5.0):
+                 gang_backend: Optional[str] = None, monitor_period: float = 5.0, pool_cap: int = 2):
         self.gang_backend = gang_backend or ("nccl" if device.type == "cuda" else "gloo")
+        # warm pool: finished jobs' trainers, keyed by (model, batch, gang
+        # ranks), handed to the next fresh job of the same shape after
+        # Trainer.reset (new weights / batch / optimizer state in the same
+        # buffers: no allocation, warm-up or graph capture on job start)
+        self.pool: Dict[tuple, List[Trainer]] = {}
+        self.pool_cap = pool_cap
+        self.pool_hits = 0
         self.rank = rank
         self.world = world
         self.device = device
@@ -349,12 +357,40 @@ class Worker:
             return None
         return self.groups[tuple(ranks)]
 
-    def _make_trainer(self, act) -> Trainer:
+    def _make_trainer(self, act, init: bool = True) -> Trainer:
         ranks = tuple(act["ranks"])
         data_seed = act["seed"] * 1000 + ranks.index(self.rank)
-        return Trainer(act["model"], self.device, batch=act.get("batch"), group=self._group(ranks),
-                       seed=act["seed"], data_seed=data_seed,
-                       use_graph=self.use_graph and len(ranks) == 1)
+        key = (act["model"], act.get("batch"), ranks)
+        free = self.pool.get(key)
+        if free:
+            self.pool_hits += 1
+            return free.pop().reset(act["seed"], data_seed, init=init)
+        t = Trainer(act["model"], self.device, batch=act.get("batch"), group=self._group(ranks),
+                    seed=act["seed"], data_seed=data_seed,
+                    use_graph=self.use_graph and len(ranks) == 1)
+        t.pool_key = key
+        return t
+
+    def _retire(self, t: Optional[Trainer]) -> None:
+        """A job left this rank: keep its trainer warm for the next job of the
+        same shape (bounded per key), else free it."""
+        if t is None:
+            return
+        key = getattr(t, "pool_key", None)
+        if key is None or getattr(t, "_spilled", None) or self.pool_cap <= 0:
+            t.release()
+            return
+        lst = self.pool.setdefault(key, [])
+        if len(lst) < self.pool_cap:
+            lst.append(t)
+        else:
+            t.release()
+
+    def drain_pool(self) -> None:
+        for lst in self.pool.values():
+            for t in lst:
+                t.release()
+        self.pool.clear()
 
     def apply(self, plan: dict) -> None:
         p2p_ops = []
@@ -368,9 +404,7 @@ class Worker:
                     self.groups[tuple(a["ranks"])] = pg
             elif op == "drop":
                 self.streams.pop(a["job"], None)
-                t = self.trainers.pop(a["job"], None)
-                if t is not None:
-                    t.release()
+                self._retire(self.trainers.pop(a["job"], None))
             elif op == "spill":
                 t = self.trainers.get(a["job"])
                 if t is not None:
@@ -391,8 +425,8 @@ class Worker:
                     if self.rank in old and self.trainers.get(a["job"]) is not None \
                             and getattr(self.trainers[a["job"]], "_spilled", None):
                         self.restored_bytes += self.trainers[a["job"]].restore()
-                    if self.rank in donors:        # receiver
-                        t = self._make_trainer(a)
+                    if self.rank in donors:        # receiver (state arrives by P2P)
+                        t = self._make_trainer(a, init=False)
                         self.trainers[a["job"]] = t
                         for _, buf in sorted(t.state_tensors().items()):
                             p2p_ops.append(dist.P2POp(dist.irecv, buf, donors[self.rank]))
@@ -403,7 +437,9 @@ class Worker:
                                 p2p_ops.append(dist.P2POp(dist.isend, buf, recv))
                     # replicas that stay: rebind their DDP bucketer to the new gang
                     if self.rank in ranks and self.rank in old:
-                        self.trainers[a["job"]].rebind(self._group(ranks))
+                        t = self.trainers[a["job"]]
+                        t.rebind(self._group(ranks))
+                        t.pool_key = (a["model"], a.get("batch"), ranks)
         if any(a["op"] == "drop" for a in plan["actions"]):
             self.reclaim(64.0)
         if p2p_ops:
@@ -413,9 +449,7 @@ class Worker:
         for a in plan["actions"]:
             if a["op"] == "start" and a["source"] == "p2p":
                 if self.rank in a["old"] and self.rank not in a["ranks"]:
-                    t = self.trainers.pop(a["job"], None)
-                    if t is not None:
-                        t.release()
+                    self._retire(self.trainers.pop(a["job"], None))
 
     def _dev_sample(self) -> Optional[dict]:
         """Real HBM / activity of this rank's GPU (hipMemGetInfo + amd-smi),
@@ -524,11 +558,13 @@ class Worker:
         torch.cuda.empty_cache()
         return True
 
-    def clear(self):
+    def clear(self, keep_pool: bool = True):
         for t in self.trainers.values():
-            t.release()
+            self._retire(t)
         self.trainers.clear()
         self.streams.clear()
+        if not keep_pool:
+            self.drain_pool()
         self.reclaim(0.0)
 
 
@@ -582,7 +618,7 @@ class RankLost(RuntimeError):
 def run_replay(cfg: SimConfig, jobs: List[ReplayJob], rank: int, world: int, device: torch.device,
                ctrl_pg=None, world_pg=None, worker: Optional[Worker] = None, quantum: float = 0.4,
                out_dir: Optional[str] = None, use_graph: bool = False, max_rounds: int = 100000,
-               fault: Optional[dict] = None, spool=None) -> Optional[dict]:
+               fault: Optional[dict] = None, spool=None, prior: Optional[List[float]] = None) -> Optional[dict]:
     """Replay ``jobs`` on the live cluster. Returns the summary on rank 0.
 
     ``fault={"rank": r, "round": k}`` injects a crash of rank r at round k
@@ -595,7 +631,7 @@ def run_replay(cfg: SimConfig, jobs: List[ReplayJob], rank: int, world: int, dev
     log = None
     if rank == 0:
         log = MetricsLogger(out_dir, node_logs=False)
-        ctrl = Controller(cfg, jobs, world, quantum, logger=log, spool=spool)
+        ctrl = Controller(cfg, jobs, world, quantum, logger=log, spool=spool, prior=prior)
     w = worker or Worker(rank, world, device, world_pg, use_graph=use_graph)
     if distributed:
         dist.barrier(group=ctrl_pg)

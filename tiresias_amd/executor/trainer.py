@@ -258,6 +258,38 @@ class Trainer:
         self._spilled = None
         return nbytes
 
+    def reset(self, seed: int, data_seed: Optional[int] = None, init: bool = True) -> "Trainer":
+        """Turn this (finished job's) trainer into a FRESH job of the same
+        model/batch/gang: weights re-initialised from ``seed``, optimizer state
+        and step count zeroed, a new synthetic batch, BN statistics reset.
+        Every buffer keeps its address, so the captured hipGraph, the DDP
+        bucketer and the caching-allocator blocks are reused: a job start
+        costs a few init kernels instead of allocation + warm-up + capture
+        (the worker's warm pool, ``cluster_runtime.Worker``). ``init=False``
+        skips the weight init (the state is about to be overwritten by a P2P
+        receive)."""
+        if getattr(self, "_spilled", None):
+            raise RuntimeError("reset of a spilled trainer")
+        if init:
+            self.arena.reinit(seed)
+            for t in self.opt_state:
+                t.zero_()
+            for k, v in self.model.buffers().items():
+                if k.endswith(".var"):
+                    v.fill_(1.0)
+                else:
+                    v.zero_()
+        fresh = synthetic_batch(self.model_name, self.batch, self.device,
+                                seed=seed if data_seed is None else data_seed)
+        for k, v in fresh.items():
+            self.data[k].copy_(v)
+        self.step_count = 0
+        self.last_loss = None
+        if self.device.type == "cuda":
+            self._ready = torch.cuda.Event()
+            self._ready.record(torch.cuda.current_stream(self.device))
+        return self
+
     def rebind(self, group) -> None:
         """Move the job to a new DDP gang (after a preemption resumed it on
         different GPUs): new communicator, fresh bucketer."""
@@ -271,6 +303,13 @@ class Trainer:
                 self.ddp = GradBucketer(self.arena, group, bucket_mb=self._bucket_mb)
         self.use_graph = self._want_graph and self.ddp is None
         self._graph = None
+
+    def hbm_bytes(self) -> int:
+        """Device bytes this trainer pins: state buffers + batch (the graph's
+        private activation pool is not visible here)."""
+        n = self.arena.numel * (4 + 2 + 4) + sum(t.numel() * 4 for t in self.opt_state)
+        n += sum(v.numel() * v.element_size() for v in self.data.values())
+        return n
 
     def release(self) -> None:
         self._graph = None

@@ -98,17 +98,26 @@ class Arena:
         self.master = torch.zeros(self.numel, dtype=torch.float32, device=dev)
         self.shadow = torch.zeros(self.numel, dtype=torch.bfloat16, device=dev)
         self.grad = torch.zeros(self.numel, dtype=torch.float32, device=dev)
-        # initialise on the device itself (a 138M-param VGG-16 job starts in
-        # milliseconds instead of seconds of host RNG + H2D copy)
-        g = torch.Generator(device=dev)
-        g.manual_seed(self.seed)
         for p in order:
             p.master = self.master[p.offset:p.offset + p.numel].view(p.shape)
             p.w = self.shadow[p.offset:p.offset + p.numel].view(p.shape)
             p.grad = self.grad[p.offset:p.offset + p.numel].view(p.shape)
+        self.reinit(self.seed)
+        return self
+
+    def reinit(self, seed: int) -> None:
+        """(Re-)initialise every parameter in place from ``seed``: the buffers
+        keep their addresses, so a hipGraph captured over them stays valid
+        (warm trainer reuse, ``executor/trainer.py::Trainer.reset``). Runs on
+        the device itself: a 138M-param VGG-16 job starts in milliseconds
+        instead of seconds of host RNG + H2D copy."""
+        self.seed = seed
+        g = torch.Generator(device=self.device)
+        g.manual_seed(seed)
+        for p in self._order():
             self._init_into(p, g)
         self.shadow.copy_(self.master.to(torch.bfloat16))
-        return self
+        self.grad.zero_()
 
     @staticmethod
     def _init_into(p: Param, g: torch.Generator) -> None:

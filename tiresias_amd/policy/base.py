@@ -14,7 +14,12 @@ simulator, ``executor/cluster_runtime.py`` for real GPUs) calls:
 * ``next_event(active, now)`` -> the next time the ordering may change on its
   own (a demotion threshold, a starvation promotion, a time-slice boundary);
 * ``after_schedule(active, now)`` bookkeeping; ``preempt_now(active, now)``
-  for policies that preempt on their own clock (Gandiva time slicing).
+  for policies that preempt on their own clock (Gandiva time slicing);
+* ``on_finish(job, now)`` when a job completes.
+
+``prior`` is a HISTORY sample of job GPU-service (the reference's Gittins
+prior file, ``run_sim.py:1682-1707``); ``None`` means no history: policies
+that need a service distribution learn it online from finished jobs.
 """
 from __future__ import annotations
 
@@ -64,6 +69,9 @@ class Policy:
 
     def preempt_now(self, active: List[Job], now: float) -> List[Job]:
         return []
+
+    def on_finish(self, job: Job, now: float) -> None:
+        """A job completed (policies with an online service prior learn here)."""
 
 
 _REGISTRY: Dict[str, type] = {}

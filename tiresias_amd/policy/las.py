@@ -40,14 +40,35 @@ from .base import INF, Policy, register, submit_key
 
 
 class GittinsTable:
+    """Gittins index over a service-time sample.
+
+    The sample comes from HISTORY, never from the jobs being scheduled: a
+    prior file (``--gittins_prior``, the reference's ``yarn-gput1000.csv``,
+    ``run_sim.py:1682-1707``), or -- with no file -- the services of the jobs
+    that have FINISHED so far (``add``; online learning, no look-ahead). The
+    online table is rebuilt when the sample has grown by 10 % (at least one
+    sample), so a 20k-job replay costs O(n log n); the native core
+    (``csrc/sched_core/engine.h``) applies the same rule."""
+
     def __init__(self, durations: List[float], delta: float, legacy_formula: bool = False):
-        self.data = sorted(float(d) for d in durations)
         self.delta = float(delta)
         self.legacy = legacy_formula
+        self._samples = [float(d) for d in durations]
+        self._next_build = 0
+        self._build()
+
+    def _build(self) -> None:
+        self.data = sorted(self._samples)
         n = len(self.data)
         self.prefix = [0.0] * (n + 1)
         for i, d in enumerate(self.data):
             self.prefix[i + 1] = self.prefix[i] + d
+        self._next_build = max(n + 1, int(n * 1.1))
+
+    def add(self, service: float) -> None:
+        self._samples.append(float(service))
+        if len(self._samples) >= self._next_build:
+            self._build()
 
     def index(self, a: float) -> float:
         n = len(self.data)
@@ -98,6 +119,12 @@ class DLAS(Policy):
             delta = getattr(self.cfg, "gittins_delta", 3250.0) or 3250.0
             self.gittins = GittinsTable(self.prior or [], delta)
 
+    def on_finish(self, job, now):
+        if self.prior is None:                  # online prior: learn from finished jobs
+            self._ensure_gittins()
+            if self.gittins is not None:
+                self.gittins.add(job.total_executed * job.num_gpu)
+
     def _enter(self, j: Job, q: int):
         j.queue = q
         j.extra["seq"] = self.next_seq()
@@ -108,13 +135,16 @@ class DLAS(Policy):
     def update(self, active, now):
         self._ensure_gittins()
         g = self.gputime
+        # the event clock's relative tolerance: a threshold whose remaining
+        # time rounds to "now" fires now (else the engine would stall on it)
+        tol = 1e-9 * max(1.0, now)
         for j in active:
             a = j.attained(g)
             if j.is_running:
-                while j.queue < self.nq - 1 and a >= self.limits[j.queue] - 1e-9:
+                while j.queue < self.nq - 1 and a >= self.limits[j.queue] - tol * (j.num_gpu if g else 1):
                     self._enter(j, j.queue + 1)
             elif (self.starve > 0 and j.is_pending and j.queue > 0 and j.executed > 0
-                  and j.last_pending_time >= j.executed * self.starve - 1e-9):
+                  and j.last_pending_time >= j.executed * self.starve - tol):
                 j.executed = 0.0
                 j.last_pending_time = 0.0
                 j.promote_count += 1
@@ -124,8 +154,14 @@ class DLAS(Policy):
 
     def _key(self, j: Job):
         if self.gittins is not None:
+            # reference :807-809 re-sorts each queue by rank every event; ties
+            # keep running jobs first (no thrash between equal-rank jobs)
             return (j.queue, -j.rank, 0 if j.is_running else 1, j.extra.get("seq", 0))
-        return (j.queue, 0 if j.is_running else 1, j.extra.get("seq", 0))
+        # FIFO by queue-entry order only: a job demoted into Qi gets a new seq
+        # and so queues BEHIND the jobs already pending in Qi (reference
+        # :752-757 appends it to the tail); pending jobs are moved behind the
+        # running ones by after_schedule (:837-847)
+        return (j.queue, j.extra.get("seq", 0))
 
     def order(self, active, now):
         return sorted(active, key=self._key)
@@ -163,6 +199,10 @@ class Gittins(Policy):
         super().__init__(cfg, prior, rng)
         self.delta = float(getattr(cfg, "gittins_delta", 3250.0) or 3250.0)
         self.table = GittinsTable(prior or [], self.delta)
+
+    def on_finish(self, job, now):
+        if self.prior is None:                  # online prior: learn from finished jobs
+            self.table.add(job.total_executed * job.num_gpu)
 
     def update(self, active, now):
         for j in active:

@@ -69,10 +69,21 @@ class ShortestExpected(Policy):
 
     def __init__(self, cfg=None, prior=None, rng=None):
         super().__init__(cfg, prior, rng)
-        self.data = sorted(prior or [])
+        self._samples = list(prior or [])
+        self._build()
+
+    def _build(self):
+        self.data = sorted(self._samples)
         self.suffix = [0.0] * (len(self.data) + 1)
         for i in range(len(self.data) - 1, -1, -1):
             self.suffix[i] = self.suffix[i + 1] + self.data[i]
+        self._next_build = max(len(self.data) + 1, int(len(self.data) * 1.1))
+
+    def on_finish(self, job, now):
+        if self.prior is None:        # no history file: learn from finished jobs
+            self._samples.append(job.total_executed)
+            if len(self._samples) >= self._next_build:
+                self._build()
 
     def expected_remaining(self, a: float) -> float:
         if not self.data:
