@@ -78,10 +78,10 @@ HISTORY_SEED_OFFSET = 7919          # the held-out history trace for the service
 
 
 def bench_trace(n_gpus: int, jobs_per_gpu: int, seed: int, work_s: float = 5.0, load: float = 1.6,
-                sigma: float = 1.2, min_iters: int = 3, tiny: bool = False):
+                sigma: float = 1.6, min_iters: int = 3, tiny: bool = False):
     """Philly-shaped compressed trace: ~70 % 1-GPU jobs with a power-of-two
-    gang tail (gangs only when N allows), log-normal service (sigma 1.2: most
-    jobs short, a few ~15x the median, as in the NSDI'19 trace) rescaled so
+    gang tail (gangs only when N allows), log-normal service (sigma 1.6: most
+    jobs short, a few ~40x the median, as in the NSDI'19 trace) rescaled so
     the nominal GPU-work is ``work_s`` per GPU, Poisson arrivals over
     ``work_s / load`` seconds."""
     rng = random.Random(seed)
@@ -166,7 +166,7 @@ def scenario_trace(name: str, n_gpus: int, seed: int, tiny: bool = False):
 #              2D-LAS queue limits in GPU-seconds (resnet4 is "no preemption"),
 #              GPU sharing when no GPU is free)
 SCENARIOS = {
-    "trace": ("dlas-gpu", "tiresias", "none", "fifo", "yarn", [0.05, 0.5], False),
+    "trace": ("dlas-gpu", "tiresias", "none", "fifo", "yarn", [0.05, 0.25, 1.0], False),
     "resnet4": ("dlas-gpu", "tiresias", "none", "fifo", "yarn", [1e9], False),
     "skew": ("dlas-gpu", "tiresias", "none", "dlas-gpu", "random", [1.0], False),
     "seq": ("gittins", "tiresias", "host", "fifo", "yarn", [0.05, 0.5], False),
