@@ -176,9 +176,11 @@ SHARING_TABLE = os.path.join(ROOT, "profiles", "stream_sharing_mi355x.json")
 
 
 def make_cfg(policy: str, scheme: str, n_gpus: int, seed: int, ckpt: str = "none",
-             qlimits=(1.0,), share: bool = False, gittins_delta: float = 0.02) -> SimConfig:
+             qlimits=(1.0,), share: bool = False, gittins_delta: float = 0.02, virtual_nodes: str = "",
+             skew_profile: str = "") -> SimConfig:
     return SimConfig(schedule=policy, scheme=scheme, num_queue=len(qlimits) + 1, queue_limits=list(qlimits),
                      gittins_delta=gittins_delta, solve_starvation=0.0, seed=seed, ckpt_policy=ckpt,
+                     virtual_nodes=virtual_nodes, skew_profile=skew_profile,
                      pack=share, max_tasks_per_gpu=2 if share else 3,
                      interference_table=SHARING_TABLE if share else "",
                      cluster=ClusterSpec(num_switch=1, num_node_p_switch=1, num_gpu_p_node=n_gpus,
@@ -206,6 +208,12 @@ def main():
     ap.add_argument("--work-s", type=float, default=None,
                     help="nominal GPU-seconds of work per GPU per replay (default 5.0; 0.5 with --cpu)")
     ap.add_argument("--min-iters", type=int, default=3, help="shortest job, iterations")
+    ap.add_argument("--virtual-nodes", default=None,
+                    help="partition the node (e.g. 2x4); default: 2x(N/2) for --scenario skew at N>=4, "
+                         "none otherwise. Spread gangs then pay the emulated inter-node link")
+    ap.add_argument("--nic-gbps", type=float, default=12.5, help="emulated inter-virtual-node link, GB/s")
+    ap.add_argument("--skew-profile", default="",
+                    help="measured consolidated-vs-spread slowdowns (python -m tiresias_amd.profiler.comm)")
     ap.add_argument("--load", type=float, default=1.6, help="offered load / capacity during arrivals")
     ap.add_argument("--quantum", type=float, default=0.02, help="scheduling round, seconds")
     ap.add_argument("--seed", type=int, default=2019)
@@ -261,7 +269,17 @@ def main():
     else:
         jobs = scenario_trace(a.scenario, n, a.seed, tiny=tiny)
         prior = history_prior(scenario_trace(a.scenario, n, a.seed + HISTORY_SEED_OFFSET))
-    cfg = make_cfg(a.policy, a.placement, n, a.seed, a.ckpt, qlim, share)
+    vn = a.virtual_nodes
+    if vn is None:
+        vn = f"2x{n // 2}" if (a.scenario == "skew" and n >= 4) else ""
+
+    def make(policy, scheme):
+        c = make_cfg(policy, scheme, n, a.seed, a.ckpt, qlim, share, virtual_nodes=vn,
+                     skew_profile=a.skew_profile)
+        c.nic_gbps = a.nic_gbps
+        return c
+
+    cfg = make(a.policy, a.placement)
     worker = Worker(rank, world, device, world_pg, use_graph=use_cuda and not a.no_graph,
                     pool_cap=0 if a.no_pool else 2)
 
@@ -320,7 +338,7 @@ def main():
     base = None
     if not a.no_baseline and fits(3.0 * longest):
         # FIFO is non-preemptive: its replay can run longer than Tiresias'
-        bcfg = make_cfg(a.baseline_policy, a.baseline_placement, n, a.seed, a.ckpt, qlim, share)
+        bcfg = make(a.baseline_policy, a.baseline_placement)
         base, _ = replay(bcfg)
 
     if rank == 0:
@@ -360,6 +378,7 @@ def main():
                             + (" + GPU sharing when full" if share else ""),
                 "prior": "held-out history trace (seed + %d)" % HISTORY_SEED_OFFSET,
                 "quantum_s": a.quantum,
+                "virtual_nodes": vn or None,
             },
             "steps_requested": a.steps,
             "warmup_requested": a.warmup,

@@ -107,7 +107,7 @@ def _replay_worker(rank, world, port, q):
     import bench
     from tiresias_amd.executor.cluster_runtime import Worker, run_replay
 
-    jobs = bench.bench_trace(world, 3, seed=5, tiny=True)
+    jobs = bench.bench_trace(world, 3, seed=5, work_s=0.6, tiny=True)
     # force a gang job
     jobs[1].spec.num_gpu = world
     cfg = bench.make_cfg("dlas-gpu", "tiresias", world, 5)
@@ -142,7 +142,7 @@ def _fault_worker(rank, world, port, outdir):
     import bench
     from tiresias_amd.executor.cluster_runtime import Worker, run_replay
 
-    jobs = bench.bench_trace(world, 3, seed=5, tiny=True)
+    jobs = bench.bench_trace(world, 3, seed=5, work_s=0.6, tiny=True)
     cfg = bench.make_cfg("dlas-gpu", "count", world, 5)
     w = Worker(rank, world, torch.device("cpu"), dist.group.WORLD)
     s = run_replay(cfg, jobs, rank, world, torch.device("cpu"), ctrl_pg=ctrl, world_pg=dist.group.WORLD,
@@ -188,7 +188,7 @@ def _spill_replay_worker(rank, world, port, outdir):
     import bench
     from tiresias_amd.executor.cluster_runtime import Worker, run_replay
 
-    jobs = bench.bench_trace(world, 4, seed=9, median_s=0.6, tiny=True)
+    jobs = bench.bench_trace(world, 4, seed=9, work_s=1.2, tiny=True)
     cfg = bench.make_cfg("dlas-gpu", "count", world, 9)
     cfg.ckpt_policy = "host"
     w = Worker(rank, world, torch.device("cpu"), dist.group.WORLD)
@@ -219,7 +219,7 @@ def test_live_replay_gpu_sharing_packs_jobs():
     import bench
     from tiresias_amd.executor import cluster_runtime as cr
 
-    jobs = bench.bench_trace(1, 6, seed=9, tiny=True)
+    jobs = bench.bench_trace(1, 6, seed=9, work_s=0.6, tiny=True)
     for j in jobs:
         j.spec.submit_time = 0.0                 # all queued at once -> contention
         j.spec.gpu_mem_max = 1000.0

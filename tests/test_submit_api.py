@@ -80,3 +80,34 @@ def test_run_cluster_cli_trace(tmp_path):
                           "--quantum", "0.05"])
     assert s["finished"] == 3
     assert (tmp_path / "live" / "job.csv").exists()
+
+
+def test_malformed_requests_are_rejected_not_fatal(tmp_path):
+    """Untrusted spool files: garbage JSON, non-object JSON,
+    non-numeric / negative / boolean fields and absurd batches are moved to
+    rejected/ with a reason; valid jobs in the same poll still run."""
+    sp = Spool(str(tmp_path / "spool"))
+    inc = os.path.join(sp.root, "incoming")
+    bad = {
+        "garbage.json": "{not json",
+        "list.json": json.dumps([1, 2, 3]),
+        "strgpu.json": json.dumps({"job_id": "s", "model": "resnet_tiny", "num_gpu": "two", "iterations": 3}),
+        "neg.json": json.dumps({"job_id": "n", "model": "resnet_tiny", "iterations": -4}),
+        "booliter.json": json.dumps({"job_id": "b", "model": "resnet_tiny", "iterations": True}),
+        "fraciter.json": json.dumps({"job_id": "f", "model": "resnet_tiny", "iterations": 2.5}),
+        "hugebatch.json": json.dumps({"job_id": "h", "model": "resnet_tiny", "iterations": 2, "batch": 10 ** 9}),
+        "nodur.json": json.dumps({"job_id": "d", "model": "resnet_tiny"}),
+        "objid.json": json.dumps({"job_id": {"x": 1}, "model": "resnet_tiny", "iterations": 2}),
+    }
+    for name, text in bad.items():
+        with open(os.path.join(inc, name), "w") as f:
+            f.write(text)
+    sp.submit("resnet_tiny", 1, iterations=2, job_id="ok")
+    sp.shutdown()
+    w = Worker(0, 1, torch.device("cpu"))
+    s = run_replay(_cfg(), [], 0, 1, torch.device("cpu"), worker=w, quantum=0.05, spool=sp)
+    assert s["finished"] == 1
+    rej = set(os.listdir(os.path.join(sp.root, "rejected")))
+    assert set(bad) <= rej
+    assert os.listdir(inc) == []
+    assert "positive integer" in json.load(open(os.path.join(sp.root, "rejected", "strgpu.json")))["reason"]

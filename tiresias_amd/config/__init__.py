@@ -65,6 +65,10 @@ def define_flags() -> None:
     D.DEFINE_string("ckpt_table", "profiles/ckpt_mi355x.json",
                     "measured spill/restore/peer bandwidths for ckpt_policy=measured (python -m tiresias_amd.ckpt)")
     D.DEFINE_string("virtual_nodes", "", "partition the MI355X box, e.g. 2x4 or 4x2")
+    D.DEFINE_float("nic_gbps", 12.5, "inter-virtual-node link rate per GPU, GB/s (spread gangs' "
+                   "host-staged transport, parallel/gang.py)")
+    D.DEFINE_string("skew_profile", "", "JSON of measured consolidated-vs-spread all-reduce slowdowns "
+                    "per model (python -m tiresias_amd.profiler.comm); drives placement sensitivity")
     D.DEFINE_float("interference", 0.2, "co-location slowdown factor (reference infra/interference.py)")
     D.DEFINE_string("interference_table", "", "measured per-model-pair slowdowns (JSON from "
                     "tools/measure_interference.py); overrides the constant factor per pair")
@@ -161,6 +165,8 @@ class SimConfig:
     replace_all: bool = False
     skew_threshold: float = 0.5
     virtual_nodes: str = ""
+    nic_gbps: float = 12.5            # emulated inter-virtual-node link per GPU (GB/s)
+    skew_profile: str = ""            # measured consolidated-vs-spread slowdowns (profiler/comm.py)
     throughput_table: str = ""
     log_path: str = ""
     verbose: bool = False

@@ -69,7 +69,8 @@ class Simulator:
         self.cluster = Cluster(cfg.cluster, pack=pack, max_tasks_per_gpu=cfg.max_tasks_per_gpu,
                                headroom_mb=cfg.gpu_mem_headroom_mb, virtual_nodes=cfg.virtual_nodes)
         self.placement = make_placement(scheme, rng=random.Random(cfg.seed + 1),
-                                        sensitivity=SensitivityOracle(cfg.skew_threshold),
+                                        sensitivity=SensitivityOracle(cfg.skew_threshold,
+                                                                      measured_path=cfg.skew_profile),
                                         cluster_gpus_per_node=self.cluster.spec.num_gpu_p_node,
                                         pack=pack)
         self.jobs: Dict[str, Job] = {}

@@ -40,6 +40,7 @@ from ..config import ClusterSpec, SimConfig
 from ..core.job import Job, JobSpec, JobState
 from ..engine.sim import Simulator
 from ..metrics.logger import MetricsLogger
+from ..parallel.gang import create_gang_comm
 from .trainer import Trainer
 
 # nominal per-iteration seconds on one MI355X (tools/bench_models.py,
@@ -118,6 +119,8 @@ class Controller:
         self.world = world
         self.quantum = quantum
         self.gpn = self.sched.cluster.spec.num_gpu_p_node
+        self.vnode_size = self.gpn if getattr(cfg, "virtual_nodes", "") else 0
+        self.nic_gbps = float(getattr(cfg, "nic_gbps", 12.5))
         self.holders: Dict[str, Tuple[int, ...]] = {}      # job -> ranks holding its state
         self.groups_made: set = set()
         self.est: Dict[Tuple[str, int], float] = {}
@@ -164,28 +167,14 @@ class Controller:
 
     # ---------------------------------------------------------------- submission
     def _poll_spool(self) -> None:
-        from ..models import MODELS
-
         now = self.now()
         for req in self.spool.poll():
-            jid = str(req.get("job_id") or "")
-            model = req.get("model")
-            g = int(req.get("num_gpu") or 1)
-            why = ""
-            if not jid or jid in self.rjobs:
-                why = f"duplicate or empty job id {jid!r}"
-            elif model not in MODELS:
-                why = f"unknown model {model!r} (known: {sorted(MODELS)})"
-            elif not 1 <= g <= self.world:
-                why = f"num_gpu {g} outside 1..{self.world}"
-            iters = req.get("iterations")
-            if not why:
-                if iters is None:
-                    dur = float(req.get("duration") or 0.0)
-                    iters = int(round(dur / self._iter_est(model, g))) if dur > 0 else 0
-                iters = int(iters)
-                if iters <= 0:
-                    why = "iterations/duration must be positive"
+            try:
+                jid, model, g, iters, batch = self._validate(req)
+                why = ""
+            except (ValueError, TypeError, OverflowError) as e:
+                jid = str(req.get("job_id") or "")
+                why = str(e)
             if why:
                 self.spool.resolve(req, False, why)
                 if self.log is not None:
@@ -193,12 +182,49 @@ class Controller:
                 continue
             spec = JobSpec(job_id=jid, submit_time=now, duration=iters * self._iter_est(model, g),
                            num_gpu=g, model=model, iterations=iters)
-            self.rjobs[jid] = ReplayJob(spec=spec, model=model, iterations=iters, batch=req.get("batch"))
+            self.rjobs[jid] = ReplayJob(spec=spec, model=model, iterations=iters, batch=batch)
             self.done_iters[jid] = 0
             self.sched.submit(JobSpec(**{**spec.__dict__, "duration": float(iters)}))
             self.spool.resolve(req, True)
             if self.log is not None:
                 self.log.decision(now, "submit", jid, gpus=g, model=model, iterations=iters)
+
+    def _validate(self, req: dict):
+        """Untrusted spool request -> (job_id, model, num_gpu, iterations,
+        batch); raises ValueError with the rejection reason."""
+        from ..models import MODELS
+
+        jid = req.get("job_id")
+        if not isinstance(jid, (str, int)) or isinstance(jid, bool) or str(jid) == "":
+            raise ValueError(f"job_id must be a non-empty string, got {jid!r}")
+        jid = str(jid)
+        if jid in self.rjobs:
+            raise ValueError(f"duplicate job id {jid!r}")
+        model = req.get("model")
+        if not isinstance(model, str) or model not in MODELS:
+            raise ValueError(f"unknown model {model!r} (known: {sorted(MODELS)})")
+
+        def pos_int(name, v):
+            if isinstance(v, bool) or not isinstance(v, (int, float)) or v != v or int(v) != v or v <= 0:
+                raise ValueError(f"{name} must be a positive integer, got {v!r}")
+            return int(v)
+
+        g = pos_int("num_gpu", req.get("num_gpu", 1) if req.get("num_gpu") is not None else 1)
+        if g > self.world:
+            raise ValueError(f"num_gpu {g} outside 1..{self.world}")
+        batch = req.get("batch")
+        if batch is not None:
+            batch = pos_int("batch", batch)
+            if batch > 4096:
+                raise ValueError(f"batch {batch} too large (max 4096)")
+        iters = req.get("iterations")
+        if iters is None:
+            dur = req.get("duration")
+            if isinstance(dur, bool) or not isinstance(dur, (int, float)) or not dur > 0 or dur == float("inf"):
+                raise ValueError("iterations/duration must be positive")
+            iters = max(1, int(round(float(dur) / self._iter_est(model, g))))
+        iters = pos_int("iterations", iters)
+        return jid, model, g, iters, batch
 
     def status(self) -> dict:
         s = self.sched
@@ -241,7 +267,10 @@ class Controller:
                 ranks = gang_ranks(j.allocation, self.gpn)
                 if len(ranks) > 1 and ranks not in self.groups_made:
                     self.groups_made.add(ranks)
-                    actions.append({"op": "group", "ranks": ranks})
+                    # a gang crossing a virtual-node boundary gets the
+                    # hierarchical transport (parallel/gang.py)
+                    actions.append({"op": "group", "ranks": ranks, "vnode": self.vnode_size,
+                                    "nic_gbps": self.nic_gbps})
                 old = self.holders.get(j.job_id)
                 rj = self.rjobs[j.job_id]
                 act = {"op": "start", "job": j.job_id, "ranks": ranks, "model": rj.model,
@@ -400,8 +429,9 @@ class Worker:
                 # communicators outlive a replay: every rank holds the same
                 # cache (same plans, same order), so skipping is collective-safe
                 if tuple(a["ranks"]) not in self.groups:
-                    pg = dist.new_group(list(a["ranks"]), backend=self.gang_backend)
-                    self.groups[tuple(a["ranks"])] = pg
+                    self.groups[tuple(a["ranks"])] = create_gang_comm(
+                        a["ranks"], self.rank, vnode_size=a.get("vnode", 0), backend=self.gang_backend,
+                        device=self.device, nic_gbps=a.get("nic_gbps", 12.5))
             elif op == "drop":
                 self.streams.pop(a["job"], None)
                 self._retire(self.trainers.pop(a["job"], None))

@@ -71,11 +71,27 @@ class Spool:
             try:
                 with open(path) as f:
                     req = json.load(f)
-            except (OSError, json.JSONDecodeError):
+            except json.JSONDecodeError as e:
+                self._reject_raw(path, f"unparseable JSON: {e}")
+                continue
+            except OSError:
+                continue                     # vanished / unreadable right now: retry next poll
+            if not isinstance(req, dict):
+                self._reject_raw(path, f"request must be a JSON object, got {type(req).__name__}")
                 continue
             req["_path"] = path
             out.append(req)
         return out
+
+    def _reject_raw(self, path: str, reason: str) -> None:
+        """Move a request that cannot even be parsed to rejected/ (it would
+        otherwise be re-read every round)."""
+        dst = os.path.join(self.root, "rejected", os.path.basename(path))
+        try:
+            _atomic_write(dst + ".reason.json", {"reason": reason})
+            os.replace(path, dst)
+        except OSError:
+            pass
 
     def resolve(self, req: Dict, ok: bool, reason: str = "") -> None:
         path = req.pop("_path")

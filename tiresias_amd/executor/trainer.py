@@ -18,6 +18,7 @@ from ..ops import _lib
 from ..ops import functional as Fx
 from ..ops.arena import Arena
 from ..parallel.ddp import GradBucketer
+from ..parallel.gang import comm_size
 
 
 class Trainer:
@@ -48,11 +49,8 @@ class Trainer:
         self.group = group
         self.ddp = None
         self._bucket_mb = bucket_mb
-        if group is not None:
-            import torch.distributed as dist
-
-            if dist.get_world_size(group) > 1:
-                self.ddp = GradBucketer(self.arena, group, bucket_mb=bucket_mb)
+        if group is not None and comm_size(group) > 1:
+            self.ddp = GradBucketer(self.arena, group, bucket_mb=bucket_mb)
         self._want_graph = use_graph and self.device.type == "cuda"
         self.use_graph = self._want_graph and self.ddp is None   # graphs for 1-GPU jobs only
         self._graph = None
@@ -296,11 +294,8 @@ class Trainer:
         self.group = group
         self.arena.on_grad_ready = None
         self.ddp = None
-        if group is not None:
-            import torch.distributed as dist
-
-            if dist.get_world_size(group) > 1:
-                self.ddp = GradBucketer(self.arena, group, bucket_mb=self._bucket_mb)
+        if group is not None and comm_size(group) > 1:
+            self.ddp = GradBucketer(self.arena, group, bucket_mb=self._bucket_mb)
         self.use_graph = self._want_graph and self.ddp is None
         self._graph = None
 

@@ -30,13 +30,19 @@ import torch
 import torch.distributed as dist
 
 from ..ops.arena import Arena, Param
+from .gang import as_comm, comm_size
 
 
 class GradBucketer:
+    """``group``: a gang comm (``parallel/gang.py``: flat RCCL for a
+    consolidated gang, hierarchical intra-node RCCL + throttled host-staged
+    inter-node exchange for a spread one) or a plain process group."""
+
     def __init__(self, arena: Arena, group=None, bucket_mb: float = 32.0, overlap: bool = True):
         self.arena = arena
+        self.comm = as_comm(group) if dist.is_initialized() else None
         self.group = group
-        self.world = dist.get_world_size(group) if dist.is_initialized() else 1
+        self.world = comm_size(self.comm) if self.comm is not None else 1
         self.overlap = overlap
         elems = max(1, int(bucket_mb * (1 << 20) // 4))
         decay = [p for p in arena.params if p.decay]
@@ -84,8 +90,7 @@ class GradBucketer:
         lo, hi = self.ranges[bi]
         view = self.arena.grad[lo:hi]
         if self.world > 1:
-            self._works.append(dist.all_reduce(view, op=dist.ReduceOp.SUM, group=self.group,
-                                               async_op=True))
+            self._works.append(self.comm.start(view))
         self.bytes_reduced += view.numel() * 4
 
     def _on_ready(self, p: Param):
@@ -115,8 +120,8 @@ class GradBucketer:
             self.uses = dict(self._seen)
         for b in range(len(self.buckets)):
             self._launch(b)
-        for w in self._works:
-            w.wait()
+        if self._works:
+            self.comm.finish(self._works)
         self._reset()
 
     @property

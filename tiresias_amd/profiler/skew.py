@@ -93,20 +93,40 @@ class SensitivityOracle:
     """Decides placement sensitivity from measured slowdowns when available,
     else from the static skew."""
 
-    def __init__(self, threshold: float = 0.5, measured_path: str = "", slowdown_threshold: float = 1.1):
+    def __init__(self, threshold: float = 0.5, measured_path: str = "", slowdown_threshold: float = 1.25):
+        """``measured_path``: the JSON ``profiler/comm.py`` writes (per model:
+        iteration-level slowdown when spread over the virtual-node boundary,
+        and the profiler's verdict). Models it covers are classified from the
+        measurement; others (and tiny test models, via their family) fall
+        back to the static skew."""
         self.threshold = threshold
         self.slowdown_threshold = slowdown_threshold
         self.measured: Dict[str, float] = {}
-        if measured_path and os.path.exists(measured_path):
+        self.source = "static-skew"
+        if measured_path:
+            if not os.path.exists(measured_path):
+                raise FileNotFoundError(f"skew profile {measured_path!r} not found "
+                                        "(python -m tiresias_amd.profiler.comm writes it)")
             with open(measured_path) as f:
                 data = json.load(f)
-            self.measured = {k: float(v.get("slowdown", v) if isinstance(v, dict) else v)
-                             for k, v in data.items()}
+            for k, v in data.items():
+                if k.startswith("_"):
+                    continue
+                self.measured[k] = float(v.get("slowdown", 1.0) if isinstance(v, dict) else v)
+            self.source = measured_path
+
+    def slowdown(self, model: str) -> Optional[float]:
+        if model in self.measured:
+            return self.measured[model]
+        from ..cluster.interference import _TINY_BASE
+
+        return self.measured.get(_TINY_BASE.get(model, ""))
 
     def __call__(self, job) -> bool:
         m = job.spec.model
-        if m in self.measured:
-            return self.measured[m] >= self.slowdown_threshold
+        sd = self.slowdown(m)
+        if sd is not None:
+            return sd >= self.slowdown_threshold
         try:
             return model_profile(m).skew >= self.threshold
         except KeyError:
