@@ -176,7 +176,7 @@ SHARING_TABLE = os.path.join(ROOT, "profiles", "stream_sharing_mi355x.json")
 
 
 def make_cfg(policy: str, scheme: str, n_gpus: int, seed: int, ckpt: str = "none",
-             qlimits=(1.0,), share: bool = False, gittins_delta: float = 0.02, virtual_nodes: str = "",
+             qlimits=(1.0,), share: bool = False, gittins_delta: float = 0.05, virtual_nodes: str = "",
              skew_profile: str = "") -> SimConfig:
     return SimConfig(schedule=policy, scheme=scheme, num_queue=len(qlimits) + 1, queue_limits=list(qlimits),
                      gittins_delta=gittins_delta, solve_starvation=0.0, seed=seed, ckpt_policy=ckpt,

@@ -7,6 +7,9 @@ iterations with the measured per-iteration time, compressed by
 ``cli/submit.py``). Outputs: ``<log_path>/{job,cluster,gpu_live}.csv``,
 ``decisions.jsonl``, ``summary.json``.
 
+``--backend fake`` runs the same controller against an in-process virtual-time
+model of the ranks (``executor/fake.py``): no GPUs, no processes.
+
 Launch (one rank per GPU)::
 
     python -m torch.distributed.run --standalone --nproc-per-node 8 \\
@@ -73,12 +76,33 @@ def _trace_jobs(cfg: SimConfig, world: int):
     return jobs
 
 
+def _main_fake(cfg: SimConfig, d: dict):
+    """``--backend fake``: the live controller against an in-process
+    virtual-time model of ``num_gpu_p_node`` ranks (executor/fake.py)."""
+    from ..executor.fake import run_fake
+
+    world = cfg.cluster.num_gpu_p_node
+    cfg.cluster = type(cfg.cluster)(**{**cfg.cluster.__dict__, "num_switch": 1, "num_node_p_switch": 1})
+    jobs = _trace_jobs(cfg, world)
+    if not jobs:
+        raise SystemExit("--backend fake needs --trace_file")
+    log_path = cfg.log_path or ("fake-" + time.strftime("%Y%m%d-%H-%M-%S", time.localtime()))
+    out = log_path if os.path.isabs(log_path) else os.path.join("log", log_path)
+    s = run_fake(cfg, jobs, world, quantum=d["quantum"], out_dir=out)
+    print(json.dumps(s, default=str))
+    return s
+
+
 def main(argv=None):
     define_flags()
     _extra_flags()
     FLAGS.parse(sys.argv[1:] if argv is None else argv)
     cfg = SimConfig.from_flags()
     d = FLAGS.as_dict()
+    if d.get("backend") == "fake":
+        return _main_fake(cfg, d)
+    if d.get("backend") not in ("sim", "mi355x", None):
+        raise SystemExit(f"unknown --backend {d.get('backend')!r} (sim | fake | mi355x)")
     rank = int(os.environ.get("RANK", 0))
     world = int(os.environ.get("WORLD_SIZE", 1))
     local = int(os.environ.get("LOCAL_RANK", 0))

@@ -60,6 +60,14 @@ def main(argv=None) -> dict:
     _extra_flags()
     FLAGS.parse(sys.argv[1:] if argv is None else argv)
     cfg = SimConfig.from_flags()
+    backend = FLAGS.as_dict().get("backend", "sim")
+    if backend == "fake":
+        from . import run_cluster
+
+        return run_cluster.main(sys.argv[1:] if argv is None else argv)
+    if backend != "sim":
+        raise SystemExit(f"--backend {backend}: run_sim drives the event simulator (sim) or the fake "
+                         "executor (fake); real GPUs run through tiresias_amd.cli.run_cluster")
     log_path = cfg.log_path or ("result-" + time.strftime("%Y%m%d-%H-%M-%S", time.localtime()))
     out = log_path if os.path.isabs(log_path) else os.path.join("log", log_path)
     os.makedirs(out, exist_ok=True)

@@ -55,7 +55,8 @@ def define_flags() -> None:
     D.DEFINE_string("prior_mode", "online", "without --gittins_prior: online (learn from finished jobs) | "
                     "oracle (the replayed trace's own distribution; flagged in summary.json)")
     D.DEFINE_integer("seed", 0, "RNG seed (all randomness is seeded)")
-    D.DEFINE_string("backend", "sim", "sim | fake | mi355x")
+    D.DEFINE_string("backend", "sim", "sim: discrete-event simulator | fake: the live controller against "
+                    "a virtual-time executor (executor/fake.py) | mi355x: live GPUs (cli/run_cluster)")
     D.DEFINE_string("engine", "event", "event (discrete-event) | tick (reference-compatible tick loop)")
     D.DEFINE_float("time_unit", 1.0, "seconds per trace time unit")
     D.DEFINE_float("duration_scale", 1.0, "scale applied to trace durations")

@@ -100,8 +100,11 @@ class ReplayJob:
 
 class Controller:
     def __init__(self, cfg: SimConfig, jobs: List[ReplayJob], world: int, quantum: float,
-                 logger: Optional[MetricsLogger] = None, spool=None, prior: Optional[List[float]] = None):
+                 logger: Optional[MetricsLogger] = None, spool=None, prior: Optional[List[float]] = None,
+                 clock=None):
         self.cfg = cfg
+        # seconds clock: host wall clock live, a VirtualClock under the fake backend
+        self.clock = clock or time.perf_counter
         self.spool = spool            # executor.spool.Spool: online job submission
         self._status_t = -1e9
         self.log = logger
@@ -134,10 +137,10 @@ class Controller:
                                              (1.0 if gpus == 1 else 1.08))
 
     def start_clock(self):
-        self.t0 = time.perf_counter()
+        self.t0 = self.clock()
 
     def now(self) -> float:
-        return time.perf_counter() - self.t0
+        return self.clock() - self.t0
 
     # ---------------------------------------------------------------- reports
     def apply_reports(self, reports: List[dict]) -> None:
@@ -329,8 +332,8 @@ class Controller:
         stop = not s.active and s.reader.remaining() == 0
         if self.spool is not None:
             stop = stop and self.spool.shutdown_requested()
-            if time.perf_counter() - self._status_t > 0.5 or stop:
-                self._status_t = time.perf_counter()
+            if self.clock() - self._status_t > 0.5 or stop:
+                self._status_t = self.clock()
                 self.spool.publish(self.status())
         wait = 0.0
         if not assign and not stop:
@@ -681,6 +684,7 @@ def run_replay(cfg: SimConfig, jobs: List[ReplayJob], rank: int, world: int, dev
             plan = _bcast(plan, 0, ctrl_pg)
         tc = time.perf_counter()
         if plan["stop"]:
+            w.apply(plan)                          # the last finished jobs' drops
             break
         if fault and fault.get("rank") == rank and rounds >= fault.get("round", 0):
             os._exit(17)                         # simulated node/rank crash

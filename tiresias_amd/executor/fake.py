@@ -1,0 +1,263 @@
+"""Fake (virtual-time) executor backend: ``--backend fake``.
+
+The live runtime's CONTROLLER (``cluster_runtime.Controller``: the real
+policy / placement / cluster objects, round planning, preemption decisions,
+P2P donor selection, spill decisions) driven against an in-process model of
+the N worker ranks instead of GPU processes (SURVEY §4 test plan item 4):
+
+* every rank of the node lives in this one process; no torch.distributed, no
+  GPU, no training — a round "runs" each rank's assignment by charging
+  per-iteration times (measured MI355X step times, GPU-sharing slowdowns from
+  the interference table, the spread-gang link penalty of
+  ``parallel/gang.py``, state-move / spill / restore costs) to a
+  ``VirtualClock``;
+* it VALIDATES the scheduler<->executor protocol the real ``Worker`` relies
+  on and raises ``ProtocolError`` on any violation: a gang started without
+  its communicator, a "resident" resume on ranks that do not hold the state,
+  P2P donors that hold nothing, a spill of a job that is not resident, a
+  gang sharing a rank with another job (collectives would interleave), gang
+  members assigned different step counts, a rank running a job it does not
+  hold, a drop of an unknown job.
+
+So the scheduler side of the live cluster (and the preemption state
+machine) is testable at world 8+ in milliseconds, and a month-scale trace
+can be replayed through the live controller's code path in virtual time.
+"""
+from __future__ import annotations
+
+import math
+import time
+from typing import Dict, List, Optional, Set, Tuple
+
+from ..config import SimConfig
+from ..metrics.logger import MetricsLogger
+from ..parallel.gang import ring_exchange_bytes, vnode_parts
+from ..profiler.skew import model_profile
+from .cluster_runtime import NOMINAL_ITER_S, Controller, ReplayJob
+
+
+class ProtocolError(AssertionError):
+    pass
+
+
+class VirtualClock:
+    def __init__(self, t0: float = 0.0):
+        self.t = float(t0)
+
+    def __call__(self) -> float:
+        return self.t
+
+    def advance(self, s: float) -> None:
+        if s < 0:
+            raise ValueError("virtual time cannot go backwards")
+        self.t += s
+
+
+def _state_bytes(model: str) -> float:
+    from ..models import MODELS
+
+    try:
+        prof = model_profile(model)
+    except KeyError:
+        return 0.0
+    opt = MODELS[model].opt if model in MODELS else "sgd"
+    return float(prof.state_bytes(opt))
+
+
+class FakeCluster:
+    """N worker ranks in virtual time (see module docstring)."""
+
+    def __init__(self, world: int, iter_s: Optional[Dict[str, float]] = None, interference=None,
+                 vnode_size: int = 0, nic_gbps: float = 12.5, xgmi_gbps: float = 64.0,
+                 host_gbps: float = 50.0, gang_factor: float = 1.08, start_s: float = 0.002):
+        self.world = world
+        self.iter_s = dict(NOMINAL_ITER_S)
+        self.iter_s.update(iter_s or {})
+        self.interf = interference
+        self.vnode_size = vnode_size
+        self.nic = nic_gbps * 1e9
+        self.xgmi = xgmi_gbps * 1e9
+        self.host = host_gbps * 1e9
+        self.gang_factor = gang_factor
+        self.start_s = start_s
+        self.held: Dict[str, Tuple[int, ...]] = {}      # job -> ranks holding its state in HBM
+        self.spilled: Set[str] = set()
+        self.model: Dict[str, str] = {}
+        self.groups: Set[Tuple[int, ...]] = set()
+        self.stats = {"p2p_bytes": 0.0, "spill_bytes": 0.0, "restore_bytes": 0.0, "starts": 0,
+                      "resident_resumes": 0, "rounds": 0}
+
+    # ---------------------------------------------------------------- timing model
+    def step_time(self, model: str, ranks: Tuple[int, ...]) -> float:
+        t = self.iter_s.get(model, 0.03) * (1.0 if len(ranks) == 1 else self.gang_factor)
+        parts = vnode_parts(ranks, self.vnode_size)
+        if len(parts) > 1 and self.nic > 0:
+            # spread gang: the gradient crosses the emulated inter-node link
+            # every step (not hidden behind backward)
+            grad = model_profile(model).params * 4.0
+            t += ring_exchange_bytes(grad, len(parts)) / self.nic
+        return t
+
+    # ---------------------------------------------------------------- protocol
+    def apply(self, plan: dict) -> Dict[int, float]:
+        """Validate and cost the round's actions; returns per-rank seconds."""
+        cost: Dict[int, float] = {}
+
+        def charge(ranks, s):
+            for r in ranks:
+                cost[r] = cost.get(r, 0.0) + s
+
+        for a in plan["actions"]:
+            op, job = a["op"], a.get("job")
+            if op == "group":
+                ranks = tuple(a["ranks"])
+                if len(ranks) < 2 or any(not 0 <= r < self.world for r in ranks):
+                    raise ProtocolError(f"bad gang communicator {ranks}")
+                self.groups.add(ranks)
+            elif op == "drop":
+                if job not in self.held:
+                    raise ProtocolError(f"drop of job {job} that no rank holds")
+                if tuple(a["ranks"]) != self.held[job]:
+                    raise ProtocolError(f"drop of {job} on {a['ranks']} but held on {self.held[job]}")
+                del self.held[job]
+                self.spilled.discard(job)
+            elif op == "spill":
+                if job not in self.held or job in self.spilled:
+                    raise ProtocolError(f"spill of job {job} that is not resident")
+                b = _state_bytes(self.model[job])
+                charge(self.held[job], b / self.host)
+                self.stats["spill_bytes"] += b * len(self.held[job])
+                self.spilled.add(job)
+            elif op == "start":
+                ranks = tuple(a["ranks"])
+                if len(ranks) > 1 and ranks not in self.groups:
+                    raise ProtocolError(f"gang {job} started on {ranks} without a communicator")
+                self.model[job] = a["model"]
+                src = a["source"]
+                b = _state_bytes(a["model"])
+                if src == "fresh":
+                    if job in self.held:
+                        raise ProtocolError(f"fresh start of {job} whose state is still held")
+                    charge(ranks, self.start_s)
+                    self.stats["starts"] += 1
+                elif src == "resident":
+                    if self.held.get(job) != ranks:
+                        raise ProtocolError(f"resident resume of {job} on {ranks}, held on {self.held.get(job)}")
+                    self.stats["resident_resumes"] += 1
+                    if job in self.spilled:
+                        charge(ranks, b / self.host)
+                        self.stats["restore_bytes"] += b * len(ranks)
+                elif src == "p2p":
+                    old = tuple(a["old"])
+                    if self.held.get(job) != old:
+                        raise ProtocolError(f"p2p move of {job} from {old}, held on {self.held.get(job)}")
+                    donors = {int(k): int(v) for k, v in a["donors"].items()}
+                    for recv, donor in donors.items():
+                        if donor not in old or recv in old or recv not in ranks:
+                            raise ProtocolError(f"bad donor {donor}->{recv} for {job}")
+                    if set(ranks) - set(old) != set(donors):
+                        raise ProtocolError(f"new ranks of {job} without a donor")
+                    if job in self.spilled:                  # holders restore first
+                        charge(old, b / self.host)
+                        self.stats["restore_bytes"] += b * len(old)
+                    for recv, donor in donors.items():
+                        charge((recv, donor), b / self.xgmi)
+                        self.stats["p2p_bytes"] += b
+                else:
+                    raise ProtocolError(f"unknown start source {src}")
+                self.held[job] = ranks
+                self.spilled.discard(job)
+            else:
+                raise ProtocolError(f"unknown action {op}")
+        return cost
+
+    def run(self, plan: dict, now_abs: float, action_cost: Dict[int, float]):
+        """One round: per-rank reports and the round's duration (the slowest
+        rank; the real round ends with a gather over all ranks)."""
+        assign = {int(r): list(v) for r, v in plan["assign"].items()}
+        gang_n: Dict[str, int] = {}
+        for r, lst in assign.items():
+            for jid, n in lst:
+                ranks = self.held.get(jid)
+                if ranks is None or r not in ranks:
+                    raise ProtocolError(f"rank {r} assigned job {jid} it does not hold")
+                if jid in self.spilled:
+                    raise ProtocolError(f"job {jid} assigned while spilled")
+                if len(ranks) > 1:
+                    if len(lst) > 1:
+                        raise ProtocolError(f"gang {jid} shares rank {r} (collectives would interleave)")
+                    if gang_n.setdefault(jid, n) != n:
+                        raise ProtocolError(f"gang {jid} members assigned different step counts")
+        deadline = plan.get("deadline")
+        reports, busy = [], {}
+        for r in range(self.world):
+            lst = assign.get(r) or []
+            t0 = action_cost.get(r, 0.0)
+            reps = []
+            if len(lst) == 1:
+                jid, n = lst[0]
+                st = self.step_time(self.model[jid], self.held[jid])
+                if deadline is not None and len(self.held[jid]) == 1:
+                    # 1-GPU job: the round ends at the first step boundary after
+                    # the next arrival (Worker._run_until)
+                    left = deadline - (now_abs + t0)
+                    n = max(1, min(n, int(math.floor(left / st)) + 1)) if left > 0 else 1
+                busy[r] = t0 + n * st
+                reps.append({"job": jid, "iters": n, "run_s": n * st, "shared": False, "loss": None})
+            elif lst:
+                # co-located 1-GPU jobs run concurrently, each slowed by its partner
+                ms = {jid: self.model[jid] for jid, _ in lst}
+                dur = 0.0
+                for jid, n in lst:
+                    s = 1.0
+                    if self.interf is not None:
+                        s = max(self.interf.pair(ms[jid], ms[o]) for o in ms if o != jid)
+                    dur = max(dur, n * self.step_time(ms[jid], (r,)) * s)
+                busy[r] = t0 + dur
+                for jid, n in lst:
+                    reps.append({"job": jid, "iters": n, "run_s": dur, "shared": True, "loss": None})
+            else:
+                busy[r] = t0
+            reports.append({"rank": r, "job": lst[0][0] if lst else None, "jobs": reps, "dev": None})
+        self.stats["rounds"] += 1
+        return reports, max(busy.values()) if busy else 0.0
+
+
+def run_fake(cfg: SimConfig, jobs: List[ReplayJob], world: int, quantum: float = 0.25,
+             out_dir: Optional[str] = None, prior: Optional[List[float]] = None,
+             iter_s: Optional[Dict[str, float]] = None, plan_cost_s: float = 0.0,
+             max_rounds: int = 10 ** 8, fake: Optional[FakeCluster] = None) -> Dict:
+    """Replay ``jobs`` through the live controller against a FakeCluster in
+    virtual time. ``plan_cost_s`` charges each round's scheduling overhead."""
+    from ..cluster.interference import InterferenceModel
+
+    clock = VirtualClock()
+    log = MetricsLogger(out_dir, node_logs=False)
+    ctrl = Controller(cfg, jobs, world, quantum, logger=log, prior=prior, clock=clock)
+    interf = (InterferenceModel.load(cfg.interference_table, cfg.interference)
+              if cfg.interference_table else InterferenceModel(cfg.interference))
+    fc = fake or FakeCluster(world, iter_s=iter_s, interference=interf, vnode_size=ctrl.vnode_size,
+                             nic_gbps=ctrl.nic_gbps)
+    ctrl.start_clock()
+    t_wall = time.perf_counter()
+    rounds = 0
+    while rounds < max_rounds:
+        plan = ctrl.plan_round()
+        cost = fc.apply(plan)
+        if plan["stop"]:
+            break
+        reps, dt = fc.run(plan, clock(), cost)
+        if not any(r["jobs"] for r in reps):
+            dt = max(dt, plan.get("wait", 0.0))
+            if dt <= 0.0:
+                dt = 1e-6
+        clock.advance(dt + plan_cost_s)
+        ctrl.apply_reports(reps)
+        rounds += 1
+    if fc.held:
+        raise ProtocolError(f"replay ended with state still held for {sorted(fc.held)}")
+    s = ctrl.sched.summary()
+    s.update(rounds=rounds, backend="fake", replay_wall_s=time.perf_counter() - t_wall, fake_stats=dict(fc.stats),
+             virtual_s=clock())
+    log.close()
+    return s
