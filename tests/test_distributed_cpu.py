@@ -146,7 +146,7 @@ def _fault_worker(rank, world, port, outdir):
     cfg = bench.make_cfg("dlas-gpu", "count", world, 5)
     w = Worker(rank, world, torch.device("cpu"), dist.group.WORLD)
     s = run_replay(cfg, jobs, rank, world, torch.device("cpu"), ctrl_pg=ctrl, world_pg=dist.group.WORLD,
-                   worker=w, quantum=0.1, fault={"rank": 1, "round": 3})
+                   worker=w, quantum=0.1, fault={"rank": 1, "round": 3}, control="gloo")
     torch.save(s, os.path.join(outdir, f"f{rank}.pt"))
     os._exit(0)
 
@@ -256,3 +256,66 @@ def test_round_ends_at_next_arrival():
     assert r["jobs"][0]["iters"] == 3
     r = w.run({"actions": [], "assign": {0: [("1", 2)]}, "deadline": time.perf_counter() + 60})
     assert r["jobs"][0]["iters"] == 2
+
+
+def _recover_worker(rank, world, port, outdir, fault):
+    import datetime
+
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    os.environ["TAM_GANG_TIMEOUT_S"] = "4"
+    dist.init_process_group("gloo", rank=rank, world_size=world, timeout=datetime.timedelta(seconds=60))
+    torch.set_num_threads(1)
+    ctrl = dist.new_group(backend="gloo", timeout=datetime.timedelta(seconds=60))
+    import bench
+    from tiresias_amd.executor.cluster_runtime import Worker, run_replay
+    from tiresias_amd.parallel import gang
+
+    gang.GANG_TIMEOUT_S = 4.0
+    jobs = bench.bench_trace(world, 4, seed=3, work_s=0.8, min_iters=4, tiny=True)
+    for i in (0, 2, 5):                    # gangs spanning the victim rank
+        jobs[i].spec.num_gpu = 2 if i != 5 else world - 1
+    cfg = bench.make_cfg("dlas-gpu", "count", world, 3, qlimits=[0.05, 0.3])
+    w = Worker(rank, world, torch.device("cpu"), dist.group.WORLD)
+    s = run_replay(cfg, jobs, rank, world, torch.device("cpu"), ctrl_pg=ctrl, world_pg=dist.group.WORLD,
+                   worker=w, quantum=0.05, fault=dict(fault), hb_timeout=1.5, hb_period=0.3)
+    torch.save(s, os.path.join(outdir, f"r{rank}.pt"))
+    os._exit(0)
+
+
+def _run_recover(tmp_path, fault, world=4):
+    port = _free_port()
+    ctx = mp.get_context("spawn")
+    ps = [ctx.Process(target=_recover_worker, args=(r, world, port, str(tmp_path), fault)) for r in range(world)]
+    for p in ps:
+        p.start()
+    for p in ps:
+        p.join(240)
+    for p in ps:
+        if p.is_alive():
+            p.kill()
+    return ps, torch.load(tmp_path / "r0.pt", weights_only=False)
+
+
+@pytest.mark.slow
+def test_rank_loss_is_recovered_in_process(tmp_path):
+    """world 4, rank 3 crashes mid-replay: the store-plane heartbeat detects it
+    within seconds, its GPU leaves the cluster, gangs that spanned it resume
+    from their surviving replicas, and every job that still fits finishes."""
+    ps, s = _run_recover(tmp_path, {"rank": 3, "round": 6, "kind": "crash"})
+    assert ps[3].exitcode == 17 and all(p.exitcode == 0 for p in ps[:3])
+    assert s["lost_ranks"] == [3]
+    assert not s.get("aborted")
+    assert s["finished"] + s["failed"] == s["jobs"]
+    assert s["failed"] <= 1                       # at most the (world-1)-GPU gang... which still fits
+    assert s["recovered_jobs"] or s["restarted_jobs"]
+
+
+@pytest.mark.slow
+def test_delayed_allreduce_is_slow_not_lost(tmp_path):
+    """A straggler (rank 2 stalls 3 s, past the 1.5 s heartbeat timeout,
+    delaying its gang's all-reduce) is NOT declared lost: its heartbeat
+    thread keeps beating; the replay completes with every job."""
+    ps, s = _run_recover(tmp_path, {"rank": 2, "round": 4, "kind": "delay", "seconds": 3.0})
+    assert all(p.exitcode == 0 for p in ps)
+    assert s["lost_ranks"] == [] and s["finished"] == s["jobs"]

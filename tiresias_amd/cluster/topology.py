@@ -34,14 +34,17 @@ class Device:
         self.node_id = node_id
         self.memory = memory_mb
         self.tasks: "OrderedDict[str, Task]" = OrderedDict()
+        self.failed = False          # a lost GPU / rank: never placed on again
 
     def is_idle(self) -> bool:
-        return not self.tasks
+        return not self.tasks and not self.failed
 
     def memory_used(self) -> float:
         return min(self.memory, sum(min(self.memory, t.gpu_mem_max) for t in self.tasks.values()))
 
     def can_fit(self, task: Task, pack: bool, max_tasks: int = 3, headroom_mb: float = 500.0) -> bool:
+        if self.failed:
+            return False
         if self.tasks and not pack:
             return False
         if len(self.tasks) >= max_tasks:
@@ -75,6 +78,9 @@ class Node:
     @property
     def gpu_count(self) -> int:
         return len(self.devices)
+
+    def live_gpus(self) -> int:
+        return sum(1 for d in self.devices if not d.failed)
 
     def free_devices(self) -> List[int]:
         return [d.device_id for d in self.devices if d.is_idle()]
@@ -136,7 +142,16 @@ class Cluster:
     # ------------------------------------------------------------ queries
     @property
     def num_gpus(self) -> int:
-        return sum(n.gpu_count for n in self.nodes.values())
+        """Usable GPUs (failed devices excluded)."""
+        return sum(n.live_gpus() for n in self.nodes.values())
+
+    def fail_device(self, node_id: str, dev: int) -> None:
+        """Take a lost GPU out of the cluster for good. Jobs on it must have
+        been released first (the executor preempts them)."""
+        d = self.nodes[node_id].devices[dev]
+        if d.tasks:
+            raise PlacementError(f"device {node_id}:{dev} still hosts {list(d.tasks)}")
+        d.failed = True
 
     def free_gpus(self) -> int:
         return sum(n.num_free_gpus() for n in self.nodes.values())
@@ -174,6 +189,8 @@ class Cluster:
             for d in devs:
                 if not (0 <= d < self.nodes[nid].gpu_count):
                     return f"bad device {nid}:{d}"
+                if self.nodes[nid].devices[d].failed:
+                    return f"device {nid}:{d} failed"
                 dev_use.setdefault((nid, d), []).append(task)
         for nid, c in cpu.items():
             n = self.nodes[nid]

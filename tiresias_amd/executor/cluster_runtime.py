@@ -131,6 +131,11 @@ class Controller:
         self.round = 0
         self.t0 = None
         self.spill = getattr(cfg, "ckpt_policy", "none") == "host"
+        # failure recovery (rank_lost)
+        self.dead: set = set()
+        self.rebind: set = set()          # jobs whose surviving replicas need a new gang comm
+        self.recovered: set = set()       # resumed from surviving DDP replicas
+        self.restarted: set = set()       # lost their only replica: restarted from scratch
 
     def _iter_est(self, model: str, gpus: int) -> float:
         return getattr(self, "est", {}).get((model, gpus), NOMINAL_ITER_S.get(model, 0.03) *
@@ -144,7 +149,7 @@ class Controller:
 
     # ---------------------------------------------------------------- reports
     def apply_reports(self, reports: List[dict]) -> None:
-        seen = set()
+        per_job: Dict[str, dict] = {}
         for r in reports:
             if r and r.get("dev") and self.log is not None:
                 d = r["dev"]
@@ -153,20 +158,72 @@ class Controller:
             if not r:
                 continue
             for jr in r.get("jobs") or []:
-                jid = jr["job"]
-                if jid in seen:             # gang members report the same job
-                    continue
-                seen.add(jid)
-                self.done_iters[jid] += jr["iters"]
-                rj = self.rjobs[jid]
-                # co-located rounds measure the pair, not the job: keep the
-                # solo estimate (it sizes rounds and seeds the Gittins prior)
-                if jr["iters"] > 0 and jr["run_s"] > 0 and not jr.get("shared"):
-                    k = (rj.model, rj.spec.num_gpu)
-                    per = jr["run_s"] / jr["iters"]
-                    self.est[k] = per if k not in self.est else 0.7 * self.est[k] + 0.3 * per
-                j = self.sched.jobs[jid]
-                j.progress = float(min(self.done_iters[jid], rj.iterations))
+                # gang members report the same job: a step counts once every
+                # member completed it (min), an error from any member marks it
+                agg = per_job.get(jr["job"])
+                if agg is None:
+                    per_job[jr["job"]] = dict(jr)
+                else:
+                    agg["iters"] = min(agg["iters"], jr["iters"])
+                    agg["run_s"] = max(agg["run_s"], jr["run_s"])
+                    agg["error"] = agg.get("error") or jr.get("error")
+        for jid, jr in per_job.items():
+            if jid not in self.rjobs:
+                continue
+            self.done_iters[jid] += jr["iters"]
+            rj = self.rjobs[jid]
+            if jr.get("error") and self.log is not None:
+                self.log.decision(self.now(), "step-error", jid, error=str(jr["error"])[:200])
+            # co-located rounds measure the pair, not the job: keep the
+            # solo estimate (it sizes rounds and seeds the Gittins prior)
+            if jr["iters"] > 0 and jr["run_s"] > 0 and not jr.get("shared") and not jr.get("error"):
+                k = (rj.model, rj.spec.num_gpu)
+                per = jr["run_s"] / jr["iters"]
+                self.est[k] = per if k not in self.est else 0.7 * self.est[k] + 0.3 * per
+            j = self.sched.jobs[jid]
+            j.progress = float(min(self.done_iters[jid], rj.iterations))
+
+    # ---------------------------------------------------------------- failures
+    def rank_lost(self, r: int) -> None:
+        """Rank ``r`` (its GPU / process) is gone: take the GPU out of the
+        cluster, preempt every job running there, and keep each DDP gang's
+        surviving replicas (params + optimizer state are replicated, all at
+        the last completed iteration) as its state holders — the next start
+        moves / rebinds them like any preemption. A job whose only replica
+        lived on ``r`` restarts from scratch."""
+        s = self.sched
+        if r in self.dead:
+            return
+        self.dead.add(r)
+        for j in list(s.active):
+            if j.is_running and r in gang_ranks(j.allocation, self.gpn):
+                s._preempt(j, reason="rank-lost")
+        s.cluster.fail_device(str(r // self.gpn + 1), r % self.gpn)
+        s.max_gpus = s.cluster.num_gpus
+        for j in list(s.active):
+            if j.num_gpu > s.max_gpus:           # can never be placed again
+                if j.is_running:
+                    s._preempt(j, reason="rank-lost")
+                j.state = JobState.FAILED
+                s.active.remove(j)
+                s.finished.append(j)
+                if self.log is not None:
+                    self.log.decision(self.now(), "failed", j.job_id, reason="gang larger than live GPUs")
+        for jid, hold in list(self.holders.items()):
+            if r not in hold:
+                continue
+            left = tuple(x for x in hold if x != r)
+            if left:
+                self.holders[jid] = left
+                self.rebind.add(jid)
+                self.recovered.add(jid)
+            else:
+                self.holders.pop(jid)
+                self.restarted.add(jid)
+                self.done_iters[jid] = 0
+                s.jobs[jid].progress = 0.0
+        if self.log is not None:
+            self.log.decision(self.now(), "rank-lost", str(r), gpus_left=s.cluster.num_gpus)
 
     # ---------------------------------------------------------------- submission
     def _poll_spool(self) -> None:
@@ -280,9 +337,17 @@ class Controller:
                        "batch": rj.batch, "seed": int(j.job_id) if j.job_id.isdigit() else zlib.crc32(j.job_id.encode()) % 100000}
                 if old is None:
                     act["source"] = "fresh"
-                elif old == ranks:
+                elif old == ranks and j.job_id not in self.rebind:
                     act["source"] = "resident"
+                elif old == ranks:
+                    # surviving replicas of a gang that lost a member: same
+                    # ranks, new communicator (the p2p path rebinds, no donors)
+                    act["source"] = "p2p"
+                    act["donors"] = {}
+                    act["old"] = old
+                    self.rebind.discard(j.job_id)
                 else:
+                    self.rebind.discard(j.job_id)
                     # every new rank without a replica receives one from a holder
                     donors = {}
                     for i, r in enumerate(ranks):
@@ -343,7 +408,7 @@ class Controller:
         # round at the first step boundary after it (Worker._run_until)
         deadline = self.t0 + nxt if math.isfinite(nxt) else None
         return {"round": self.round, "actions": actions, "assign": assign, "stop": stop, "wait": wait,
-                "deadline": deadline}
+                "deadline": deadline, "alive": [r for r in range(self.world) if r not in self.dead]}
 
 
 class Worker:
@@ -509,14 +574,22 @@ class Worker:
             return {"rank": self.rank, "job": None, "jobs": [], "dev": self._dev_sample()}
         cuda = self.device.type == "cuda"
         t0 = time.perf_counter()
+        err = None
         if len(jobs) == 1:
             jid, n = jobs[0]
             t = self.trainers[jid]
             deadline = plan.get("deadline")
             if deadline is None or t.ddp is not None:
                 # gang members must run the same step count (collectives)
-                for _ in range(n):
-                    t.step()
+                done = 0
+                try:
+                    for _ in range(n):
+                        t.step()
+                        done += 1
+                except Exception as e:        # a gang peer died mid-collective
+                    err = f"{type(e).__name__}: {e}"
+                    t.broken = True
+                    jobs = [(jid, done)]
             else:
                 n = self._run_until(t, n, deadline, cuda)
                 jobs = [(jid, n)]
@@ -544,8 +617,11 @@ class Worker:
         reps = []
         for jid, n in jobs:
             t = self.trainers[jid]
-            reps.append({"job": jid, "iters": n, "run_s": dt, "shared": len(jobs) > 1,
-                         "loss": float(t.last_loss) if t.last_loss is not None else None})
+            rep = {"job": jid, "iters": n, "run_s": dt, "shared": len(jobs) > 1,
+                   "loss": float(t.last_loss) if (t.last_loss is not None and err is None) else None}
+            if err:
+                rep["error"] = err
+            reps.append(rep)
         return {"rank": self.rank, "job": jobs[0][0], "jobs": reps, "dev": self._dev_sample()}
 
     def _run_until(self, t: Trainer, n: int, deadline: float, cuda: bool) -> int:
@@ -651,13 +727,27 @@ class RankLost(RuntimeError):
 def run_replay(cfg: SimConfig, jobs: List[ReplayJob], rank: int, world: int, device: torch.device,
                ctrl_pg=None, world_pg=None, worker: Optional[Worker] = None, quantum: float = 0.4,
                out_dir: Optional[str] = None, use_graph: bool = False, max_rounds: int = 100000,
-               fault: Optional[dict] = None, spool=None, prior: Optional[List[float]] = None) -> Optional[dict]:
+               fault: Optional[dict] = None, spool=None, prior: Optional[List[float]] = None,
+               control: str = "store", hb_timeout: float = 6.0, hb_period: float = 1.0) -> Optional[dict]:
     """Replay ``jobs`` on the live cluster. Returns the summary on rank 0.
 
-    ``fault={"rank": r, "round": k}`` injects a crash of rank r at round k
-    (failure-detection test): the per-round gather doubles as the heartbeat,
-    so the controller sees the lost rank as a collective error / timeout,
-    marks the jobs that had state on it FAILED and aborts the replay cleanly.
+    ``control``: ``"store"`` (default; executor/control.py::StorePlane —
+    plans and reports through the c10d store, heartbeat threads, a lost rank
+    detected within ``hb_timeout`` seconds and RECOVERED in-process) or
+    ``"gloo"`` (collective plane; a lost rank aborts the replay).
+
+    Fault injection (failure-detection tests):
+      ``{"rank": r, "round": k}`` / ``"kind": "crash"`` -- rank r dies at round k;
+      ``{"rank": r, "round": k, "kind": "delay", "seconds": s}`` -- rank r
+      stalls s seconds before its round-k work (a straggler delaying its
+      gang's all-reduce): detected as slow, NOT as lost.
+
+    Recovery (store plane): the lost GPU leaves the cluster; every job with
+    state on it is preempted. A DDP gang keeps its replicas on the surviving
+    members (data parallelism replicates params + optimizer state) and
+    resumes from them at its last completed iteration, re-placed on live
+    ranks through the normal P2P move / communicator rebind path; a job whose
+    only replica died restarts from scratch (its progress is charged back).
     """
     distributed = world > 1
     ctrl = None
@@ -666,7 +756,16 @@ def run_replay(cfg: SimConfig, jobs: List[ReplayJob], rank: int, world: int, dev
         log = MetricsLogger(out_dir, node_logs=False)
         ctrl = Controller(cfg, jobs, world, quantum, logger=log, spool=spool, prior=prior)
     w = worker or Worker(rank, world, device, world_pg, use_graph=use_graph)
+    plane = None
     if distributed:
+        if control == "store":
+            from .control import StorePlane
+
+            plane = StorePlane(rank, world, hb_period=hb_period, hb_timeout=hb_timeout)
+        else:
+            from .control import GlooPlane
+
+            plane = GlooPlane(ctrl_pg, rank, world)
         dist.barrier(group=ctrl_pg)
     if ctrl:
         ctrl.start_clock()
@@ -676,56 +775,71 @@ def run_replay(cfg: SimConfig, jobs: List[ReplayJob], rank: int, world: int, dev
     # idle_s = sleeping because no job is runnable (arrival gaps), not overhead
     prof = {"plan_s": 0.0, "bcast_s": 0.0, "apply_s": 0.0, "run_s": 0.0, "idle_s": 0.0,
             "gather_s": 0.0}
-    while rounds < max_rounds:
-        ta = time.perf_counter()
-        plan = ctrl.plan_round() if ctrl else None
-        tb = time.perf_counter()
-        if distributed:
-            plan = _bcast(plan, 0, ctrl_pg)
-        tc = time.perf_counter()
-        if plan["stop"]:
-            w.apply(plan)                          # the last finished jobs' drops
-            break
-        if fault and fault.get("rank") == rank and rounds >= fault.get("round", 0):
-            os._exit(17)                         # simulated node/rank crash
-        if any(len(v) > 1 for v in plan["assign"].values()):
-            shared += 1
-        w.apply(plan)
-        td = time.perf_counter()
-        rep = w.run(plan)
-        te = time.perf_counter()
-        prof["plan_s"] += tb - ta
-        prof["bcast_s"] += tc - tb
-        prof["apply_s"] += td - tc
-        prof["run_s"] += te - td
-        if plan.get("wait", 0) > 0 and rep["job"] is None:
-            tw = time.perf_counter()
-            w.reclaim(4.0)                     # idle GPU: a free moment to return dead pools
-            time.sleep(max(0.0, plan["wait"] - (time.perf_counter() - tw)))
-        tf = time.perf_counter()
-        prof["idle_s"] += tf - te
-        if distributed:
-            reps = [None] * world if rank == 0 else None
-            try:
-                dist.gather_object(rep, reps, dst=0, group=ctrl_pg)
-            except Exception as e:                 # heartbeat lost
-                if ctrl:
-                    return _abort(ctrl, log, rounds, f"rank lost during round {rounds}: {e}")
-                raise RankLost(str(e))
-        else:
-            reps = [rep]
-        if ctrl:
-            ctrl.apply_reports(reps)
-        prof["gather_s"] += time.perf_counter() - tf
-        rounds += 1
+    lost_ranks: List[int] = []
+    try:
+        while rounds < max_rounds:
+            ta = time.perf_counter()
+            plan = ctrl.plan_round() if ctrl else None
+            tb = time.perf_counter()
+            if distributed:
+                plan = plane.bcast(plan, rounds)
+            tc = time.perf_counter()
+            if plan["stop"]:
+                w.apply(plan)                          # the last finished jobs' drops
+                break
+            if fault and fault.get("rank") == rank and rounds >= fault.get("round", 0):
+                if fault.get("kind", "crash") == "crash":
+                    os._exit(17)                     # simulated node/rank crash
+                if not fault.get("_done"):
+                    fault["_done"] = True
+                    time.sleep(float(fault.get("seconds", 1.0)))   # straggler
+            if any(len(v) > 1 for v in plan["assign"].values()):
+                shared += 1
+            w.apply(plan)
+            td = time.perf_counter()
+            rep = w.run(plan)
+            te = time.perf_counter()
+            prof["plan_s"] += tb - ta
+            prof["bcast_s"] += tc - tb
+            prof["apply_s"] += td - tc
+            prof["run_s"] += te - td
+            if plan.get("wait", 0) > 0 and rep["job"] is None:
+                tw = time.perf_counter()
+                w.reclaim(4.0)                     # idle GPU: a free moment to return dead pools
+                time.sleep(max(0.0, plan["wait"] - (time.perf_counter() - tw)))
+            tf = time.perf_counter()
+            prof["idle_s"] += tf - te
+            newly: List[int] = []
+            if distributed:
+                try:
+                    reps, newly = plane.gather(rep, rounds, plan.get("alive", range(world)))
+                except Exception as e:                 # gloo plane: heartbeat lost
+                    if ctrl:
+                        return _abort(ctrl, log, rounds, f"rank lost during round {rounds}: {e}")
+                    raise RankLost(str(e))
+            else:
+                reps = [rep]
+            if ctrl:
+                for r in newly:
+                    lost_ranks.append(r)
+                    ctrl.rank_lost(r)
+                ctrl.apply_reports(reps)
+            prof["gather_s"] += time.perf_counter() - tf
+            rounds += 1
+    finally:
+        if plane is not None:
+            plane.close()
     wall = time.perf_counter() - t_start
     w.clear()
     if device.type == "cuda":
         torch.cuda.synchronize(device)
     if ctrl:
         s = ctrl.sched.summary()
-        s.update(rounds=rounds, shared_rounds=shared, replay_wall_s=wall, iter_est={f"{k[0]}x{k[1]}": v for k, v in ctrl.est.items()},
-                 runtime_breakdown={k: round(v, 4) for k, v in prof.items()})
+        s.update(rounds=rounds, shared_rounds=shared, replay_wall_s=wall,
+                 iter_est={f"{k[0]}x{k[1]}": v for k, v in ctrl.est.items()},
+                 runtime_breakdown={k: round(v, 4) for k, v in prof.items()},
+                 lost_ranks=lost_ranks, recovered_jobs=sorted(ctrl.recovered),
+                 restarted_jobs=sorted(ctrl.restarted))
         log.close()
         return s
     return None

@@ -294,6 +294,10 @@ class Trainer:
         self.group = group
         self.arena.on_grad_ready = None
         self.ddp = None
+        # an interrupted step (a peer died mid-collective) may have left
+        # partial gradients: the new gang starts from clean ones
+        self.arena.grad.zero_()
+        self.broken = False
         if group is not None and comm_size(group) > 1:
             self.ddp = GradBucketer(self.arena, group, bucket_mb=self._bucket_mb)
         self.use_graph = self._want_graph and self.ddp is None

@@ -25,8 +25,9 @@ real inter-node transport instead of the free xGMI path:
 The same factory builds the communicators for the training runtime
 (``executor/cluster_runtime.py``) and the skew profiler
 (``profiler/comm.py``), so what the profiler measures is what jobs pay.
-``create_gang_comm`` creates process groups and must therefore be called by
-EVERY rank of the world in the same order (the plan broadcast guarantees it).
+``create_gang_comm`` builds member-only communicators (``GangPG``): only the
+gang's members rendezvous, so gangs form and dissolve freely and a lost rank
+elsewhere does not block anything.
 """
 from __future__ import annotations
 
@@ -68,7 +69,7 @@ class FlatComm:
         self.size = len(self.ranks)
 
     def start(self, view: torch.Tensor):
-        return dist.all_reduce(view, op=dist.ReduceOp.SUM, group=self.pg, async_op=True)
+        return self.pg.all_reduce(view)
 
     def finish(self, handles) -> None:
         for w in handles:
@@ -160,7 +161,7 @@ class HierComm:
                 work.wait()
             host = view
         t0 = time.perf_counter()
-        dist.all_reduce(host, op=dist.ReduceOp.SUM, group=self.leaders_pg)
+        self.leaders_pg.all_reduce(host).wait()
         self.nic.throttle(ring_exchange_bytes(nbytes, self.k), t0)
         if not self._cuda:
             return None
@@ -174,7 +175,7 @@ class HierComm:
     def start(self, view: torch.Tensor):
         w = None
         if self.local_pg is not None:
-            w = dist.reduce(view, dst=self.leader, op=dist.ReduceOp.SUM, group=self.local_pg, async_op=True)
+            w = self.local_pg.reduce(view, self.leader)
         fut = None
         if self.is_leader:
             fut = Future()
@@ -191,7 +192,7 @@ class HierComm:
             elif w is not None:
                 w.wait()
             if self.local_pg is not None:
-                bcasts.append(dist.broadcast(view, src=self.leader, group=self.local_pg, async_op=True))
+                bcasts.append(self.local_pg.broadcast(view, self.leader))
         for b in bcasts:
             b.wait()
 
@@ -201,24 +202,86 @@ class HierComm:
             self._q = None
 
 
+_PGS: Dict[tuple, object] = {}
+GANG_TIMEOUT_S = float(__import__("os").environ.get("TAM_GANG_TIMEOUT_S", "120"))
+
+
+class GangPG:
+    """A communicator over an arbitrary rank set, built directly on a c10d
+    backend (``ProcessGroupNCCL`` = RCCL on ROCm, or ``ProcessGroupGloo``)
+    from the job's key-value store under a per-rank-set prefix: only the
+    members rendezvous (ncclCommInitRank with a unique id exchanged through
+    the store), no world-wide bookkeeping. ``torch.distributed.new_group``
+    would need every rank of the world to take part (or, with local
+    synchronisation, identical group histories on the members) — neither
+    holds once gangs form and dissolve dynamically, or after a rank is lost.
+    Collective calls return Work handles (``wait()`` orders the current
+    stream after them)."""
+
+    def __init__(self, ranks: Sequence[int], my_rank: int, backend: str, timeout_s: float = GANG_TIMEOUT_S):
+        from datetime import timedelta
+
+        self.ranks = tuple(ranks)
+        self.rank = self.ranks.index(my_rank)
+        self.size = len(self.ranks)
+        self.backend = backend
+        base = dist.distributed_c10d._get_default_store()
+        store = dist.PrefixStore(f"tam/pg/{backend}/{'_'.join(map(str, self.ranks))}", base)
+        to = timedelta(seconds=timeout_s)
+        if backend == "nccl":
+            self.pg = dist.ProcessGroupNCCL(store, self.rank, self.size, to)
+        else:
+            self.pg = dist.ProcessGroupGloo(store, self.rank, self.size, to)
+
+    def all_reduce(self, t: torch.Tensor):
+        o = dist.AllreduceOptions()
+        o.reduceOp = dist.ReduceOp.SUM
+        return self.pg.allreduce([t], o)
+
+    def reduce(self, t: torch.Tensor, root_global: int):
+        o = dist.ReduceOptions()
+        o.reduceOp = dist.ReduceOp.SUM
+        o.rootRank = self.ranks.index(root_global)
+        o.rootTensor = 0
+        return self.pg.reduce([t], o)
+
+    def broadcast(self, t: torch.Tensor, root_global: int):
+        o = dist.BroadcastOptions()
+        o.rootRank = self.ranks.index(root_global)
+        o.rootTensor = 0
+        return self.pg.broadcast([t], o)
+
+
+def _pg(ranks: Sequence[int], my_rank: int, backend: str) -> GangPG:
+    """One communicator per (rank set, backend) per process (members create
+    it the first time they need it; the store prefix is the rank set)."""
+    key = (tuple(ranks), backend)
+    if key not in _PGS:
+        _PGS[key] = GangPG(ranks, my_rank, backend)
+    return _PGS[key]
+
+
 def create_gang_comm(ranks: Sequence[int], my_rank: int, vnode_size: int = 0, backend: str = "nccl",
                      device: Optional[torch.device] = None, nic_gbps: float = DEFAULT_NIC_GBPS,
                      nic_latency_s: float = DEFAULT_NIC_LATENCY_S):
-    """Collective over the WORLD: every rank calls it with the same args, in
-    the same order. Returns this rank's comm (None when not a member)."""
+    """Called by every live rank with the same args in the same order (the
+    plan broadcast guarantees it); only members rendezvous. Returns this
+    rank's comm (None when not a member)."""
     ranks = tuple(sorted(int(r) for r in ranks))
     parts = vnode_parts(ranks, vnode_size)
     device = device or torch.device("cpu")
-    if len(parts) <= 1:
-        pg = dist.new_group(list(ranks), backend=backend)
-        return FlatComm(pg, ranks) if my_rank in ranks else None
-    local_pgs = {}
-    for p in parts:
-        if len(p) > 1:
-            local_pgs[p[0]] = dist.new_group(p, backend=backend)
-    leaders_pg = dist.new_group([p[0] for p in parts], backend="gloo")
     if my_rank not in ranks:
         return None
+    if len(parts) <= 1:
+        return FlatComm(_pg(ranks, my_rank, backend), ranks)
+    local_pgs = {}
+    for p in parts:
+        if len(p) > 1 and my_rank in p:
+            local_pgs[p[0]] = _pg(tuple(p), my_rank, backend)
+    leaders_pg = None
+    leaders = tuple(p[0] for p in parts)
+    if my_rank in leaders:
+        leaders_pg = _pg(leaders, my_rank, "gloo")
     return HierComm(ranks, parts, my_rank, local_pgs, leaders_pg, device, nic_gbps, nic_latency_s)
 
 
@@ -231,8 +294,18 @@ def comm_size(group) -> int:
     return dist.get_world_size(group)
 
 
+class _PlainPG:
+    """A torch.distributed process group behind the GangPG interface."""
+
+    def __init__(self, pg):
+        self.pg = pg
+
+    def all_reduce(self, t):
+        return dist.all_reduce(t, op=dist.ReduceOp.SUM, group=self.pg, async_op=True)
+
+
 def as_comm(group):
     """Wrap a plain process group as a FlatComm (legacy callers)."""
     if group is None or isinstance(group, (FlatComm, HierComm)):
         return group
-    return FlatComm(group, tuple(range(dist.get_world_size(group))))
+    return FlatComm(_PlainPG(group), tuple(range(dist.get_world_size(group))))
