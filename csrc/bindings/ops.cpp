@@ -15,6 +15,7 @@
 
 #include "tam/kernels.h"
 #include "tam/launch.h"
+#include "tam/gemm8p.h"
 
 using at::Tensor;
 using c10::optional;
@@ -58,7 +59,7 @@ T* opt_ptr(const optional<Tensor>& t) {
 // 0 MFMA only, 1 library whenever eligible.
 using GemmKey = std::tuple<int64_t, int64_t, int64_t, bool, bool, int64_t, bool, bool>;
 std::map<GemmKey, int> g_route;          // 0 = igemm/gemm256, 1 = library, 2 = LDS-DMA GEMM
-std::map<GemmKey, std::array<float, 3>> g_route_ms;   // measured ms per path
+std::map<GemmKey, std::array<float, 4>> g_route_ms;   // measured ms per path
 std::mutex g_route_mu;
 int g_lib_policy = -1;
 extern int g_dma_policy;
@@ -88,6 +89,20 @@ void run_lib(const Tensor& a, bool ak, const Tensor& b, bool bk, const Tensor& c
   } else {
     at::mm_out(out, Ae, Be);
   }
+}
+
+// 256^2 all-layout kernel; slab split-K (fp32 workspace, one reduce pass,
+// any output dtype) when its tile grid underfills the chip
+void run_p8(const Tensor& a, bool ak, const Tensor& b, bool bk, int64_t M, int64_t N, int64_t K,
+            const tam::Epi& ep, bool allow_split) {
+  const int sp = tam::gemm8p_slab_splits((int)M, (int)N, (int)K);
+  if (sp > 1 && ep.ldc >= N) {
+    Tensor ws = at::empty({sp, M, N}, a.options().dtype(at::kFloat));
+    tam::gemm8p_splitk(bp(a), a.stride(0), ak, bp(b), b.stride(0), bk, (int)M, (int)N, (int)K, ep, sp,
+                       ws.data_ptr<float>(), cur_stream(a));
+    return;
+  }
+  run_mfma(a, ak, b, bk, M, N, K, ep, allow_split, 3);
 }
 
 float time_ms(hipStream_t s, const std::function<void()>& fn) {
@@ -152,6 +167,12 @@ void gemm_op(const Tensor& a, bool a_kmajor, const Tensor& b, bool b_kmajor, con
   const bool lib_ok = g_lib_policy != 0 && !g_forced && !relu && ep.mask == nullptr && alpha == 1.0 &&
                       (mode == 0 || (mode == 1 && ep.c_f32)) && !(has_bias && ep.c_f32) &&
                       (double)M * N * K >= (double)(1 << 27) && M >= 16 && N >= 16;
+  // gemm8p policy 3: the 256^2 kernel with slab split-K wherever eligible (tests)
+  if (tam::gemm8p_policy_mode() == 3 &&
+      tam::gemm8p_ok(a_kmajor, b_kmajor, (int)M, (int)N, (int)K, a.stride(0), b.stride(0))) {
+    run_p8(a, a_kmajor, b, b_kmajor, M, N, K, ep, allow_split);
+    return;
+  }
   // our two kernels are both candidates for every shape the DMA GEMM accepts
   if (g_dma_policy == 2) {
     run_mfma(a, a_kmajor, b, b_kmajor, M, N, K, ep, allow_split, 2);
@@ -159,11 +180,14 @@ void gemm_op(const Tensor& a, bool a_kmajor, const Tensor& b, bool b_kmajor, con
   }
   const bool dma_ok = g_dma_policy == 1 && !g_forced && K % 64 == 0 &&
                       (double)M * N * K >= (double)(1 << 24);
+  const bool p8_ok = !g_forced && tam::gemm8p_policy_mode() == 1 &&
+                     tam::gemm8p_ok(a_kmajor, b_kmajor, (int)M, (int)N, (int)K, a.stride(0), b.stride(0)) &&
+                     (double)M * N * K >= (double)(1 << 27);
   if (g_lib_policy == 1 && lib_ok) {
     run_lib(a, a_kmajor, b, b_kmajor, c, mode, bias);
     return;
   }
-  if (!lib_ok && !dma_ok) {
+  if (!lib_ok && !dma_ok && !p8_ok) {
     run_mfma(a, a_kmajor, b, b_kmajor, M, N, K, ep, allow_split);
     return;
   }
@@ -188,8 +212,10 @@ void gemm_op(const Tensor& a, bool a_kmajor, const Tensor& b, bool b_kmajor, con
     tam::Epi es = ep;
     es.c = scratch.data_ptr();
     es.ldc = scratch.stride(0);
-    std::array<float, 3> t{1e30f, 1e30f, 1e30f};
+    std::array<float, 4> t{1e30f, 1e30f, 1e30f, 1e30f};
     t[0] = time_ms(s, [&] { run_mfma(a, a_kmajor, b, b_kmajor, M, N, K, es, allow_split, 0); });
+    if (p8_ok)
+      t[3] = time_ms(s, [&] { run_p8(a, a_kmajor, b, b_kmajor, M, N, K, es, allow_split); });
     if (dma_ok)
       t[2] = time_ms(s, [&] { run_mfma(a, a_kmajor, b, b_kmajor, M, N, K, es, allow_split, 2); });
     if (lib_ok) {
@@ -202,12 +228,14 @@ void gemm_op(const Tensor& a, bool a_kmajor, const Tensor& b, bool b_kmajor, con
     // prefer our kernels unless another path is >5% faster
     route = 0;
     if (t[2] < 0.95f * t[route]) route = 2;
+    if (t[3] < 0.95f * t[route]) route = 3;
     if (t[1] < 0.95f * t[route]) route = 1;
     std::lock_guard<std::mutex> g(g_route_mu);
     g_route[key] = route;
     g_route_ms[key] = t;
   }
   if (route == 1) run_lib(a, a_kmajor, b, b_kmajor, c, mode, bias);
+  else if (route == 3) run_p8(a, a_kmajor, b, b_kmajor, M, N, K, ep, allow_split);
   else run_mfma(a, a_kmajor, b, b_kmajor, M, N, K, ep, allow_split, route);
 }
 
@@ -223,8 +251,8 @@ std::string gemm_routes_op() {
     o << std::get<0>(k) << " " << std::get<1>(k) << " " << std::get<2>(k) << " "
       << (std::get<3>(k) ? "K" : "M") << (std::get<4>(k) ? "K" : "N") << " " << std::get<5>(k)
       << " " << std::get<6>(k) << " " << std::get<7>(k) << " "
-      << (kv.second == 1 ? "lib" : kv.second == 2 ? "dma" : "mfma") << " " << t[0] << " " << t[1]
-      << " " << t[2] << "\n";
+      << (kv.second == 1 ? "lib" : kv.second == 2 ? "dma" : kv.second == 3 ? "p8" : "mfma") << " " << t[0]
+      << " " << t[1] << " " << t[2] << " " << t[3] << "\n";
   }
   return o.str();
 }
@@ -416,6 +444,8 @@ void gemm_dma_policy_op(int64_t p, int64_t cfg) {
   tam::gemm_dma_policy(p == 2 ? 1 : 0, (int)cfg);
 }
 
+void gemm8p_policy_op(int64_t mode, int64_t stagger) { tam::gemm8p_policy((int)mode, (int)stagger); }
+
 void gemm_force_op(int64_t cfg, int64_t splits) {
   tam::gemm_force((int)cfg, (int)splits);
   g_forced = cfg >= 0 || splits >= 1;
@@ -571,6 +601,7 @@ TORCH_LIBRARY(tam, m) {
   m.def("embedding_backward(Tensor dout, Tensor ids, Tensor(a!) gtable, float scale) -> ()", &embedding_backward_op);
   m.def("colsum(Tensor x, Tensor(a!) out) -> ()", &colsum_op);
   m.def("gemm_force(int cfg, int splits) -> ()", &gemm_force_op);
+  m.def("gemm8p_policy(int mode, int stagger) -> ()", &gemm8p_policy_op);
   m.def("gemm_lib_policy(int policy) -> ()", &gemm_lib_policy_op);
   m.def("conv_dma_policy(int policy) -> ()", &conv_dma_policy_op);
   m.def("gemm_dma_policy(int policy, int cfg) -> ()", &gemm_dma_policy_op);

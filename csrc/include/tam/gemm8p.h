@@ -1,0 +1,403 @@
+// tiresias_amd — 256x256x64 bf16 GEMM, every operand majority, for the big
+// plain GEMMs of the model zoo (vocab projections, FFN / LSTM-gate weight
+// gradients, VGG FC layers): C[M][N] (+)= A . B, fp32 accumulate.
+//
+//   A: K-major [M][K] (AK) or M-major [K][M];  B: K-major [N][K] (BK) or N-major [K][N]
+//
+// MI355X-first structure (cdna_hip_programming.md §5 "The 256^2 8-phase
+// template", T1-T5, T10):
+//  * 512 threads = 8 waves as 2 (M) x 4 (N); each wave owns 128x64 outputs =
+//    8x4 tiles of v_mfma_f32_16x16x32_bf16 (128 fp32 accumulators per lane).
+//  * Both operands are staged HBM/L2 -> LDS by LDS-DMA (global_load_lds_dwordx4,
+//    no VGPR round trip). Each operand tile is split in two half-tiles by the
+//    C-quadrant that reads it (A: the wave's upper / lower 64 rows, B: its
+//    left / right 32 columns); per K-tile a wave runs 4 phases = 4 quadrants
+//    of 16 MFMAs, fragments held in registers between phases.
+//  * K-major half-tile image: [128 rows][64 k] (128-B rows), 16-B chunk c of
+//    row r stored at c ^ ((r>>1)&7): ds_read_b128 fragment reads conflict-free.
+//    MN-major half-tile image: [64 k][128 cols] (256-B rows), 8-B chunk c of
+//    row r at c ^ swz(r) (multiples of 4, so 16-B DMA granules stay whole),
+//    read with the ds_read_b64_tr_b16 hardware transpose (T10). In both the
+//    swizzle is applied to the per-lane SOURCE address (LDS-DMA writes
+//    lane-linear; guide rule 21).
+//  * Two LDS stages (2 x 64 KiB). Each half-tile (2 DMA per thread) is
+//    refilled as EARLY as its buffer allows (>= 2 phases after its last
+//    reader), so every DMA has >= 3 phases of MFMA work to land:
+//        phase:   p1        p2     p3        p4
+//        reads:   AL, BL    BH     AH        -
+//        refill:  AH(t+1)   -      AL(t+2)   BL(t+2), BH(t+2)
+//    and ONE counted `s_waitcnt vmcnt(6)` per K-tile (in p4, before its
+//    first barrier) retires tile t+1 while tile t+2's three half-tiles stay
+//    in flight: the DMA pipeline never drains inside the loop.
+//  * Two raw s_barriers per phase (reads + DMA issue | MFMA cluster), MFMA
+//    clusters bracketed by s_setprio (T5). STAGGER: the upper wave group runs
+//    one barrier behind the lower one, so on every SIMD one wave issues its
+//    MFMA cluster while its partner issues LDS reads / DMA (ping-pong); the
+//    refill / wait placement above stays race-free under that skew (a
+//    refill happens after the partner group's reads have retired; a read
+//    happens after both groups' waits).
+//  * XCD-aware bijective block remap + grouped-M tile order (T1); split-K
+//    over blockIdx.z (fp32 atomic epilogue) when the tile grid underfills
+//    the 256 CUs.
+#pragma once
+#include "tam/igemm.h"
+
+namespace tam {
+
+constexpr int P8_BM = 256, P8_BN = 256, P8_BK = 64, P8_THREADS = 512;
+constexpr int P8_HALF = 128 * 64 * 2;         // 16 KiB half-tile
+constexpr int P8_STAGE = 4 * P8_HALF;          // AL AH BL BH
+constexpr int P8_LDS = 2 * P8_STAGE;           // 128 KiB
+
+typedef __attribute__((address_space(3))) void p8_lds_t;
+
+struct P8Args {
+  const bf16_t* A;
+  long lda;
+  const bf16_t* B;
+  long ldb;
+  int M, N, K;
+  int kps;   // K-tiles per split (blockIdx.z)
+};
+
+// local row lr (0..127) of a half-tile -> global row / column index
+//   A half h: rows wm*128 + h*64 + (lr & 63), wm = lr >> 6
+//   B half h: cols wn*64  + h*32 + (lr & 31), wn = lr >> 5
+template <bool IS_A>
+__device__ __forceinline__ int p8_row(int lr, int h) {
+  if constexpr (IS_A) return ((lr >> 6) << 7) + (h << 6) + (lr & 63);
+  else return ((lr >> 5) << 6) + (h << 5) + (lr & 31);
+}
+
+// Issue one half-tile (2 DMA instructions per thread).
+template <bool IS_A, bool KMAJ>
+__device__ __forceinline__ void p8_issue(const bf16_t* __restrict__ base, long ld, int extent, int o0,
+                                         int k0, char* half, int h, int wid, int lane) {
+#pragma unroll
+  for (int j = 0; j < 2; ++j) {
+    const int g = j * 8 + wid;                 // 1-KiB group 0..15 of the half-tile
+    if constexpr (KMAJ) {
+      // 8 rows x 128 B per group; lane -> row 8g + lane/8, 16-B slot lane%8
+      const int lr = g * 8 + (lane >> 3);
+      const int c = (lane & 7) ^ ((lr >> 1) & 7);
+      int r = o0 + p8_row<IS_A>(lr, h);
+      r = r < extent ? r : extent - 1;         // rows past the edge are never stored
+      const bf16_t* src = base + (long)r * ld + k0 + c * 8;
+      __builtin_amdgcn_global_load_lds((const void*)src, (p8_lds_t*)(half + g * 1024), 16, 0, 0);
+    } else {
+      // 4 k-rows x 256 B per group; lane -> k-row 4g + lane/16, 16-B slot lane%16
+      const int kr = g * 4 + (lane >> 4);
+      const int gran = (lane & 15) ^ (mnmaj_swz<128>(kr) >> 1);   // 8 columns per granule
+      int col = o0 + p8_row<IS_A>(gran * 8, h);
+      col = col + 8 <= extent ? col : extent - 8;                  // extent % 8 == 0
+      const bf16_t* src = base + (long)(k0 + kr) * ld + col;
+      __builtin_amdgcn_global_load_lds((const void*)src, (p8_lds_t*)(half + g * 1024), 16, 0, 0);
+    }
+  }
+}
+
+template <bool KMAJ>
+__device__ __forceinline__ s16x8_t p8_frag(const char* half, int lane, int lbase, int kk) {
+  if constexpr (KMAJ) return read_frag_k(half, lane, lbase, kk);
+  else return read_frag_mn<128>(half, lane, 32 * kk, lbase);
+}
+
+// raw s_barrier fenced for the COMPILER only (LDS reads / DMA issues stay on
+// their side); emits no s_waitcnt, so DMAs stay in flight across it
+__device__ __forceinline__ void p8_barrier() {
+  asm volatile("" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+  asm volatile("" ::: "memory");
+}
+
+template <int I0, int J0>
+__device__ __forceinline__ void p8_mfma(f32x4_t (&acc)[8][4], const s16x8_t (&fa)[4][2],
+                                        const s16x8_t (&fb)[2][2]) {
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  __builtin_amdgcn_sched_barrier(0);
+  __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+  for (int kk = 0; kk < 2; ++kk)
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int j = 0; j < 2; ++j)
+        acc[I0 + i][J0 + j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(
+            __builtin_bit_cast(bf16x8_t, fa[i][kk]), __builtin_bit_cast(bf16x8_t, fb[j][kk]),
+            acc[I0 + i][J0 + j], 0, 0, 0);
+  __builtin_amdgcn_s_setprio(0);
+  __builtin_amdgcn_sched_barrier(0);
+}
+
+// SCHED 0: one barrier per phase (after the MFMA cluster); 1: two barriers
+// per phase (reads | MFMA); 2: two barriers + wave-group stagger
+// ABL (diagnostics only, tools/bench_gemm8p.py --ablate): 1 no DMA refills,
+// 2 no LDS fragment reads, 3 no MFMA
+template <bool AK, bool BK, int SCHED, int ABL = 0>
+__global__ void __launch_bounds__(P8_THREADS, 1) gemm8p_kernel(P8Args a, Epi ep) {
+  constexpr bool STAGGER = SCHED == 2;
+  __shared__ __attribute__((aligned(1024))) char smem[P8_LDS];
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int wm = wid >> 2, wn = wid & 3;
+  // the upper wave group, as a wave-uniform SCALAR condition (a divergent
+  // branch would execute the scalar s_barrier on every wave)
+  const bool upper = __builtin_amdgcn_readfirstlane(tid) >= 256;
+
+  const int tiles_m = (a.M + P8_BM - 1) / P8_BM, tiles_n = (a.N + P8_BN - 1) / P8_BN;
+  const int bid = xcd_remap(blockIdx.x, gridDim.x);
+  constexpr int GROUP = 4;
+  const int per_group = GROUP * tiles_n;
+  const int grp = bid / per_group;
+  const int first_m = grp * GROUP;
+  const int gsize = min(tiles_m - first_m, GROUP);
+  const int tm = first_m + (bid % per_group) % gsize;
+  const int tn = (bid % per_group) / gsize;
+  const int m0 = tm * P8_BM, n0 = tn * P8_BN;
+
+  const int ktiles = a.K / P8_BK;
+  const int kt0 = blockIdx.z * a.kps;
+  const int kt1 = min(ktiles, kt0 + a.kps);
+  const int nk = kt1 - kt0;
+
+  f32x4_t acc[8][4];
+#pragma unroll
+  for (int i = 0; i < 8; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+
+  // stage s: [AL][AH][BL][BH]
+  auto half_ptr = [&](int t, int which) { return smem + (t & 1) * P8_STAGE + which * P8_HALF; };
+  auto issA = [&](int t, int h) {
+    if (ABL == 1 && t > 1) return;
+    p8_issue<true, AK>(a.A, a.lda, a.M, m0, (kt0 + t) * P8_BK, half_ptr(t, h), h, wid, lane);
+  };
+  auto issB = [&](int t, int h) {
+    if (ABL == 1 && t > 1) return;
+    p8_issue<false, BK>(a.B, a.ldb, a.N, n0, (kt0 + t) * P8_BK, half_ptr(t, 2 + h), h, wid, lane);
+  };
+
+  if (nk > 0) {
+    // prologue: tile 0 complete, tile 1's AL / BL / BH in flight
+    issA(0, 0); issB(0, 0); issB(0, 1); issA(0, 1);
+    if (nk > 1) {
+      issA(1, 0); issB(1, 0); issB(1, 1);
+      asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
+    } else {
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+    p8_barrier();
+    if (STAGGER && upper) p8_barrier();
+
+    const int arow = wm * 64, bcol = wn * 32;   // local rows in the half images
+    s16x8_t fa[4][2], fb0[2][2], fb1[2][2];
+    for (int t = 0; t < nk; ++t) {
+      const char* AL = half_ptr(t, 0);
+      const char* AH = half_ptr(t, 1);
+      const char* BL = half_ptr(t, 2);
+      const char* BH = half_ptr(t, 3);
+      const bool n1 = t + 1 < nk, n2 = t + 2 < nk;
+      // ---- p1: quadrant (mh0, nh0)
+#pragma unroll
+      for (int kk = 0; kk < 2; ++kk) {
+        if (ABL != 2 || t == 0)
+#pragma unroll
+        for (int j = 0; j < 2; ++j) fb0[j][kk] = p8_frag<BK>(BL, lane, bcol + 16 * j, kk);
+        if (ABL != 2 || t == 0)
+#pragma unroll
+        for (int i = 0; i < 4; ++i) fa[i][kk] = p8_frag<AK>(AL, lane, arow + 16 * i, kk);
+      }
+      if (n1) issA(t + 1, 1);
+      if constexpr (SCHED > 0) p8_barrier();
+      p8_mfma<0, 0>(acc, fa, fb0);
+      p8_barrier();
+      // ---- p2: quadrant (mh0, nh1)
+#pragma unroll
+      for (int kk = 0; kk < 2; ++kk)
+        if (ABL != 2 || t == 0)
+#pragma unroll
+        for (int j = 0; j < 2; ++j) fb1[j][kk] = p8_frag<BK>(BH, lane, bcol + 16 * j, kk);
+      if constexpr (SCHED > 0) p8_barrier();
+      p8_mfma<0, 2>(acc, fa, fb1);
+      p8_barrier();
+      // ---- p3: quadrant (mh1, nh1)
+#pragma unroll
+      for (int kk = 0; kk < 2; ++kk)
+        if (ABL != 2 || t == 0)
+#pragma unroll
+        for (int i = 0; i < 4; ++i) fa[i][kk] = p8_frag<AK>(AH, lane, arow + 16 * i, kk);
+      if (n2) issA(t + 2, 0);
+      if constexpr (SCHED > 0) p8_barrier();
+      p8_mfma<2 * 2, 2>(acc, fa, fb1);
+      p8_barrier();
+      // ---- p4: quadrant (mh1, nh0); retire tile t+1 (t+2's AL / BL / BH stay in flight)
+      if (n2) {
+        issB(t + 2, 0);
+        issB(t + 2, 1);
+        asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
+      } else {
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      }
+      if constexpr (SCHED > 0) p8_barrier();
+      p8_mfma<2 * 2, 0>(acc, fa, fb0);
+      p8_barrier();
+    }
+    if (STAGGER && !upper) p8_barrier();        // both groups execute the same barrier count
+  }
+  __syncthreads();   // LDS reuse by the epilogue
+
+  const bool add_bias = ep.bias != nullptr && blockIdx.z == 0;
+  const int rbase = m0 + wm * 128, cbase = n0 + wn * 64;
+  // ---- bf16 output, plain store / accumulate: LDS-staged, 16-B row chunks
+  if (!ep.c_f32 && !ep.mask && (ep.ldc & 7) == 0 && (((uintptr_t)ep.c) & 15) == 0) {
+    constexpr int LDW = 64 + 8;
+    bf16_t* slab = (bf16_t*)(smem + wid * (32 * LDW * 2));
+    float bv[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int col = cbase + 16 * j + (lane & 15);
+      bv[j] = (add_bias && col < a.N) ? bf2f(ep.bias[col]) : 0.f;
+    }
+#pragma unroll
+    for (int h = 0; h < 4; ++h) {
+#pragma unroll
+      for (int ii = 0; ii < 2; ++ii)
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            float v = acc[2 * h + ii][j][r] * ep.alpha + bv[j];
+            if (ep.relu) v = fmaxf(v, 0.f);
+            slab[(16 * ii + 4 * (lane >> 4) + r) * LDW + 16 * j + (lane & 15)] = f2bf(v);
+          }
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {              // 32 rows x 8 chunks of 16 B
+        const int idx = u * 64 + lane, lr = idx >> 3, ch = idx & 7;
+        const int row = rbase + 32 * h + lr, col = cbase + ch * 8;
+        if (row >= a.M || col >= a.N) continue;
+        bf16_t* dst = (bf16_t*)ep.c + (long)row * ep.ldc + col;
+        const bf16_t* src = slab + lr * LDW + ch * 8;
+        if (col + 8 <= a.N) {
+          uint4 v = *(const uint4*)src;
+          if (ep.mode == 1) {
+            uint32_t* vw = (uint32_t*)&v;
+            const uint4 o = *(const uint4*)dst;
+            const uint32_t* ow = (const uint32_t*)&o;
+#pragma unroll
+            for (int e = 0; e < 4; ++e)
+              vw[e] = pack_bf2(bf2f((bf16_t)(vw[e] & 0xffff)) + bf2f((bf16_t)(ow[e] & 0xffff)),
+                               bf2f((bf16_t)(vw[e] >> 16)) + bf2f((bf16_t)(ow[e] >> 16)));
+          }
+          *(uint4*)dst = v;
+        } else {
+          for (int e = 0; e < 8 && col + e < a.N; ++e) {
+            float v = bf2f(src[e]);
+            if (ep.mode == 1) v += bf2f(dst[e]);
+            dst[e] = f2bf(v);
+          }
+        }
+      }
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    }
+    return;
+  }
+  // ---- fp32 output, store / accumulate / split-K slab: LDS-staged, 16-B row chunks
+  if (ep.c_f32 && ep.mode != 2 && !ep.mask && (ep.ldc & 3) == 0 && (((uintptr_t)ep.c) & 15) == 0 &&
+      (ep.mode != 3 || (ep.zstride & 3) == 0)) {
+    constexpr int LDF = 64 + 4;
+    float* slab = (float*)(smem + wid * (32 * LDF * 4));
+    float* cz = (float*)ep.c + (ep.mode == 3 ? blockIdx.z * ep.zstride : 0);
+    float bv[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int col = cbase + 16 * j + (lane & 15);
+      bv[j] = (add_bias && col < a.N) ? bf2f(ep.bias[col]) : 0.f;
+    }
+#pragma unroll
+    for (int h = 0; h < 4; ++h) {
+#pragma unroll
+      for (int ii = 0; ii < 2; ++ii)
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            float v = acc[2 * h + ii][j][r] * ep.alpha + bv[j];
+            if (ep.relu) v = fmaxf(v, 0.f);
+            slab[(16 * ii + 4 * (lane >> 4) + r) * LDF + 16 * j + (lane & 15)] = v;
+          }
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+#pragma unroll
+      for (int u = 0; u < 8; ++u) {              // 32 rows x 16 chunks of 16 B
+        const int idx = u * 64 + lane, lr = idx >> 4, ch = idx & 15;
+        const int row = rbase + 32 * h + lr, col = cbase + ch * 4;
+        if (row >= a.M || col >= a.N) continue;
+        float* dst = cz + (long)row * ep.ldc + col;
+        const float* src = slab + lr * LDF + ch * 4;
+        if (col + 4 <= a.N) {
+          float4 v = *(const float4*)src;
+          if (ep.mode == 1) {
+            const float4 o = *(const float4*)dst;
+            v.x += o.x; v.y += o.y; v.z += o.z; v.w += o.w;
+          }
+          *(float4*)dst = v;
+        } else {
+          for (int e = 0; e < 4 && col + e < a.N; ++e) dst[e] = ep.mode == 1 ? dst[e] + src[e] : src[e];
+        }
+      }
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    }
+    return;
+  }
+  // ---- general epilogue (atomics / relu-mask): C/D map of 16x16x32:
+  // col = lane&15, row = (lane>>4)*4 + r
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const int col = cbase + 16 * j + (lane & 15);
+    if (col >= a.N) continue;
+    const float bv = add_bias ? bf2f(ep.bias[col]) : 0.f;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int row = rbase + 16 * i + 4 * (lane >> 4) + r;
+        if (row >= a.M) continue;
+        float v = acc[i][j][r] * ep.alpha + bv;
+        if (ep.relu) v = fmaxf(v, 0.f);
+        if (ep.mask && bf2f(ep.mask[(long)row * ep.ldm + col]) <= 0.f) v = 0.f;
+        const long off = (long)row * ep.ldc + col;
+        if (ep.c_f32) {
+          float* c = (float*)ep.c;
+          if (ep.mode == 3) c[off + blockIdx.z * ep.zstride] = v;
+          else if (ep.mode == 2) atomicAdd(c + off, v);
+          else if (ep.mode == 1) c[off] += v;
+          else c[off] = v;
+        } else {
+          bf16_t* c = (bf16_t*)ep.c;
+          if (ep.mode == 1) v += bf2f(c[off]);
+          c[off] = f2bf(v);
+        }
+      }
+    }
+  }
+}
+
+// shape / layout conditions of the LDS-DMA 256^2 kernel
+inline bool gemm8p_ok(bool ak, bool bk, int M, int N, int K, long lda, long ldb) {
+  if (K % P8_BK != 0 || K < P8_BK || M < 128 || N < 128) return false;
+  if (lda % 8 != 0 || ldb % 8 != 0) return false;
+  if (!ak && M % 8 != 0) return false;       // M-major A: 16-B column granules
+  if (!bk && N % 8 != 0) return false;
+  return true;
+}
+
+void launch_gemm8p(const bf16_t* A, long lda, bool ak, const bf16_t* B, long ldb, bool bk, int M,
+                   int N, int K, const Epi& ep, int splits, hipStream_t s, int sched = 0);
+// split-K without atomics or a zeroing pass, any output dtype / epilogue:
+// every K-slice writes its own fp32 slab of ws[splits][M][N], then one
+// reduce pass sums the slabs and applies ep (bias / relu / mask / alpha /
+// store or accumulate) — deterministic
+void gemm8p_splitk(const bf16_t* A, long lda, bool ak, const bf16_t* B, long ldb, bool bk, int M,
+                   int N, int K, const Epi& ep, int splits, float* ws, hipStream_t s);
+int gemm8p_slab_splits(int M, int N, int K);
+
+}  // namespace tam

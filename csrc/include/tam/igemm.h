@@ -40,6 +40,7 @@ struct Epi {
   const bf16_t* mask = nullptr;  // relu-backward mask: zero where mask<=0
   long ldm = 0;
   float alpha = 1.f;
+  long zstride = 0;         // mode 3: fp32 slab store at c + blockIdx.z * zstride (split-K slabs)
 };
 
 // ---------------------------------------------------------------------------

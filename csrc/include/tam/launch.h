@@ -14,11 +14,14 @@ namespace tam {
 // ep.mode == 0, requires ldc == N).
 void gemm(const bf16_t* A, long lda, bool a_kmajor, const bf16_t* B, long ldb, bool b_kmajor,
           int M, int N, int K, Epi ep, bool allow_split, hipStream_t s);
-// path 0: igemm / gemm256 (heuristic tiles), 2: LDS-DMA GEMM where eligible
+// path 0: heuristic, 2: LDS-DMA GEMM where eligible, 3: gemm8p where eligible
 void gemm_select(const bf16_t* A, long lda, bool a_kmajor, const bf16_t* B, long ldb, bool b_kmajor,
                  int M, int N, int K, Epi ep, bool allow_split, hipStream_t s, int path);
 void gemm_force(int cfg, int splits);   // tuning hook (-1 = heuristic)
 void gemm_dma_policy(int policy, int cfg);   // LDS-DMA GEMM on/off, forced tile cfg (-1 auto)
+// 256^2 all-layout LDS-DMA GEMM: 0 off, 1 auto (big GEMMs), 2 forced where eligible
+void gemm8p_policy(int mode, int sched);
+int gemm8p_policy_mode();
 
 // NHWC convolutions, weights [K][R][S][C] (C, K multiples of 8)
 void conv_fwd(const bf16_t* x, const bf16_t* w, const ConvGeom& g, Epi ep, hipStream_t s);

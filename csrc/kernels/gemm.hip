@@ -3,6 +3,7 @@
 #include "tam/launch.h"
 #include "tam/tiles.h"
 #include "tam/gemm256.h"
+#include "tam/gemm8p.h"
 #include "tam/gemm_dma.h"
 
 namespace tam {
@@ -80,6 +81,110 @@ void zero_async(void* p, size_t bytes, hipStream_t s) {
                      b + n16 * 16, ntail);
 }
 
+// 256x256 all-layout LDS-DMA kernel (gemm8p.h): 0 off (legacy gemm256 for
+// big K-major GEMMs), 1 auto (big GEMMs of every layout), 2 forced wherever
+// eligible (tests / sweeps); stagger = wave-group ping-pong schedule
+static int g_p8 = 1, g_p8_sched = 0, g_p8_abl = 0;
+int gemm8p_policy_mode() { return g_p8; }
+void gemm8p_policy(int mode, int sched) {
+  g_p8 = mode;
+  g_p8_sched = sched % 10;
+  g_p8_abl = sched / 10;      // diagnostics: 10 / 20 = ablation 1 / 2 (KK, schedule 2)
+}
+
+template <bool AK, bool BK>
+static void p8_launch(const P8Args& g, const Epi& ep, dim3 grid, int sched, hipStream_t s) {
+  if (sched == 2) hipLaunchKernelGGL((gemm8p_kernel<AK, BK, 2>), grid, dim3(P8_THREADS), 0, s, g, ep);
+  else if (sched == 1) hipLaunchKernelGGL((gemm8p_kernel<AK, BK, 1>), grid, dim3(P8_THREADS), 0, s, g, ep);
+  else hipLaunchKernelGGL((gemm8p_kernel<AK, BK, 0>), grid, dim3(P8_THREADS), 0, s, g, ep);
+}
+
+void launch_gemm8p(const bf16_t* A, long lda, bool ak, const bf16_t* B, long ldb, bool bk, int M,
+                   int N, int K, const Epi& ep, int splits, hipStream_t s, int stagger) {
+  const int tiles = cdiv(M, P8_BM) * cdiv(N, P8_BN);
+  const int ktiles = K / P8_BK;
+  const int kps = cdiv(ktiles, splits < 1 ? 1 : splits);
+  const int z = cdiv(ktiles, kps);
+  P8Args g{A, lda, B, ldb, M, N, K, kps};
+  const dim3 grid(tiles, 1, z);
+  if (g_p8_abl == 1 && ak && bk)
+    hipLaunchKernelGGL((gemm8p_kernel<true, true, 2, 1>), grid, dim3(P8_THREADS), 0, s, g, ep);
+  else if (g_p8_abl == 2 && ak && bk)
+    hipLaunchKernelGGL((gemm8p_kernel<true, true, 2, 2>), grid, dim3(P8_THREADS), 0, s, g, ep);
+  else if (ak && bk) p8_launch<true, true>(g, ep, grid, stagger, s);
+  else if (ak) p8_launch<true, false>(g, ep, grid, stagger, s);
+  else if (bk) p8_launch<false, true>(g, ep, grid, stagger, s);
+  else p8_launch<false, false>(g, ep, grid, stagger, s);
+}
+
+// ---- slab split-K (gemm8p.h): reduce ws[sp][M][N] -> C with the epilogue
+__global__ void __launch_bounds__(256) p8_slab_reduce_kernel(const float* __restrict__ ws, int sp,
+                                                             int M, int N, Epi ep) {
+  const long mn = (long)M * N;
+  const long n4 = mn >> 2;
+  for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < n4; i += (long)gridDim.x * blockDim.x) {
+    float4 acc = ((const float4*)ws)[i];
+    for (int z = 1; z < sp; ++z) {
+      const float4 v = ((const float4*)(ws + z * mn))[i];
+      acc.x += v.x; acc.y += v.y; acc.z += v.z; acc.w += v.w;
+    }
+    float vv[4] = {acc.x, acc.y, acc.z, acc.w};
+    const long e0 = i << 2;
+    const int row = (int)(e0 / N), col0 = (int)(e0 % N);   // N % 4 == 0: one row per float4
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      const int col = col0 + e;
+      float v = vv[e] * ep.alpha + (ep.bias ? bf2f(ep.bias[col]) : 0.f);
+      if (ep.relu) v = fmaxf(v, 0.f);
+      if (ep.mask && bf2f(ep.mask[(long)row * ep.ldm + col]) <= 0.f) v = 0.f;
+      const long off = (long)row * ep.ldc + col;
+      if (ep.c_f32) {
+        float* c = (float*)ep.c;
+        c[off] = ep.mode == 1 ? c[off] + v : v;
+      } else {
+        bf16_t* c = (bf16_t*)ep.c;
+        c[off] = f2bf(ep.mode == 1 ? v + bf2f(c[off]) : v);
+      }
+    }
+  }
+}
+
+int gemm8p_slab_splits(int M, int N, int K) {
+  const long t = (long)cdiv(M, P8_BM) * cdiv(N, P8_BN);
+  const int kt = K / P8_BK;
+  if (t >= 160 || kt < 16 || N % 4 != 0) return 1;
+  int sp = (int)((256 + t - 1) / t);
+  if (sp > kt / 8) sp = kt / 8;          // >= 8 K-tiles per slice
+  if (sp > 16) sp = 16;
+  return sp < 2 ? 1 : sp;
+}
+
+void gemm8p_splitk(const bf16_t* A, long lda, bool ak, const bf16_t* B, long ldb, bool bk, int M,
+                   int N, int K, const Epi& ep, int splits, float* ws, hipStream_t s) {
+  Epi se;
+  se.c = ws;
+  se.ldc = N;
+  se.c_f32 = 1;
+  se.mode = 3;
+  se.zstride = (long)M * N;
+  launch_gemm8p(A, lda, ak, B, ldb, bk, M, N, K, se, splits, s, g_p8_sched);
+  const int ktiles = K / P8_BK;
+  const int z = cdiv(ktiles, cdiv(ktiles, splits));   // slabs actually written
+  const long n4 = (long)M * N / 4;
+  long blocks = (n4 + 255) / 256;
+  blocks = blocks > 2048 ? 2048 : blocks;
+  hipLaunchKernelGGL(p8_slab_reduce_kernel, dim3((unsigned)blocks), dim3(256), 0, s, ws, z, M, N, ep);
+}
+
+// split count that fills the 256 CUs with 256^2 tiles (>= 4 K-tiles per split)
+static int p8_splits(int M, int N, int K, bool can_split) {
+  const long t = (long)cdiv(M, P8_BM) * cdiv(N, P8_BN);
+  if (!can_split || t >= 192 || K / P8_BK < 8) return 1;
+  int sp = (int)((256 + t - 1) / t);
+  if (sp > K / P8_BK / 4) sp = K / P8_BK / 4;
+  return sp < 1 ? 1 : sp;
+}
+
 void gemm(const bf16_t* A, long lda, bool ak, const bf16_t* B, long ldb, bool bk, int M, int N,
           int K, Epi ep, bool allow_split, hipStream_t s) {
   gemm_select(A, lda, ak, B, ldb, bk, M, N, K, ep, allow_split, s, g_dma ? 2 : 0);
@@ -89,6 +194,17 @@ void gemm_select(const bf16_t* A, long lda, bool ak, const bf16_t* B, long ldb, 
                  int N, int K, Epi ep, bool allow_split, hipStream_t s, int path) {
   if (M <= 0 || N <= 0) return;
   const bool can_split = allow_split && ep.c_f32 && !ep.relu && !ep.mask;
+  if (g_p8 > 0 && g_force_cfg < 0 && gemm8p_ok(ak, bk, M, N, K, lda, ldb)) {
+    const long t8 = (long)cdiv(M, P8_BM) * cdiv(N, P8_BN);
+    const double flop = 2.0 * M * N * K;
+    if (g_p8 >= 2 || path == 3 || (t8 >= 48 && K >= 512 && flop >= 4e9)) {
+      int sp = p8_splits(M, N, K, can_split);
+      if (g_force_splits >= 1) sp = can_split ? g_force_splits : 1;
+      prepare_split(ep, sp, M, N, s);
+      launch_gemm8p(A, lda, ak, B, ldb, bk, M, N, K, ep, sp, s, g_p8_sched);
+      return;
+    }
+  }
   TileChoice t = choose_tiles_gemm(M, N, K, can_split);
   if (g_force_cfg >= 0) t.cfg = g_force_cfg;
   if (g_force_splits >= 1) t.splits = can_split ? g_force_splits : 1;

@@ -107,6 +107,100 @@ def test_gemm_dma_configs(gpu, cfg, ak, bk):
         T().gemm_dma_policy(1, -1)
 
 
+# the 256x256 all-layout LDS-DMA kernel (gemm8p.h), forced: every majority,
+# both schedules (wave-group stagger on / off), edge tiles, K just one tile
+# and many tiles, every epilogue (bf16 staged, bias / relu / mask / alpha /
+# accumulate, fp32 store / accumulate / split-K atomics)
+@pytest.mark.parametrize("stagger", [0, 1, 2])
+@pytest.mark.parametrize("ak,bk", [(True, True), (True, False), (False, True), (False, False)])
+@pytest.mark.parametrize("M,N,K", [(256, 256, 64), (520, 392, 448), (1024, 768, 2048)])
+def test_gemm8p(gpu, stagger, ak, bk, M, N, K):
+    torch.manual_seed(M + N + K + 2 * ak + bk)
+    A = torch.randn(M, K, device=gpu).to(BF)
+    B = torch.randn(K, N, device=gpu).to(BF)
+    a = A if ak else A.t().contiguous()
+    b = B.t().contiguous() if bk else B
+    ref = A.float() @ B.float()
+    bias = torch.randn(N, device=gpu).to(BF)
+    mask = torch.randn(M, N, device=gpu).to(BF)
+    T().gemm8p_policy(2, stagger)
+    try:
+        c = torch.empty(M, N, device=gpu)
+        T().gemm(a, ak, b, bk, c, 0, None, False, None, 1.0, False)
+        assert rel_err(c, ref) < 1e-5
+        acc = torch.full((M, N), 1.5, device=gpu)
+        T().gemm(a, ak, b, bk, acc, 1, None, False, None, 1.0, True)       # split-K atomics
+        assert rel_err(acc, ref + 1.5) < 1e-5
+        y = torch.empty(M, N, device=gpu, dtype=BF)
+        T().gemm(a, ak, b, bk, y, 0, None, False, None, 1.0, False)
+        assert rel_err(y, ref) < 1e-2
+        T().gemm(a, ak, b, bk, y, 0, bias, True, None, 1.0, False)
+        assert rel_err(y, (ref + bias.float()).clamp_min(0)) < 1e-2
+        T().gemm(a, ak, b, bk, y, 0, None, False, mask, 0.5, False)
+        assert rel_err(y, 0.5 * ref * (mask.float() > 0)) < 1e-2
+        y0 = torch.randn(M, N, device=gpu).to(BF)
+        y1 = y0.clone()
+        T().gemm(a, ak, b, bk, y1, 1, None, False, None, 1.0, False)
+        assert rel_err(y1, y0.float() + ref) < 1e-2
+    finally:
+        T().gemm8p_policy(1, 0)
+
+
+@pytest.mark.parametrize("ak,bk", [(True, True), (True, False), (False, True), (False, False)])
+def test_gemm8p_exact_integer_layout(gpu, ak, bk):
+    """Small-integer operands (exact in bf16 and fp32): every output element
+    must match exactly, so a swapped row/col, a mis-swizzled chunk or a
+    stale LDS stage shows as a hard mismatch (guide §3: asymmetric B)."""
+    torch.manual_seed(3)
+    M, N, K = 512, 512, 1024
+    A = torch.randint(-3, 4, (M, K), device=gpu).float()
+    B = torch.randint(-3, 4, (K, N), device=gpu).float()
+    B[:, 0] += torch.arange(K, device=gpu) % 5               # asymmetric
+    a = (A if ak else A.t().contiguous()).to(BF)
+    b = (B.t().contiguous() if bk else B).to(BF)
+    ref = A @ B
+    try:
+        for sched in (0, 1, 2):
+            T().gemm8p_policy(2, sched)
+            c = torch.empty(M, N, device=gpu)
+            T().gemm(a, ak, b, bk, c, 0, None, False, None, 1.0, False)
+            torch.cuda.synchronize()
+            assert torch.equal(c, ref), sched
+    finally:
+        T().gemm8p_policy(1, 0)
+
+
+@pytest.mark.parametrize("ak,bk", [(True, True), (True, False), (False, False)])
+@pytest.mark.parametrize("M,N,K", [(512, 256, 8192), (320, 520, 4096)])
+def test_gemm8p_slab_splitk(gpu, ak, bk, M, N, K):
+    """Few output tiles, long K: K-slices write fp32 slabs, one reduce pass
+    applies the epilogue (bf16 / fp32, bias, relu, mask, alpha, accumulate)."""
+    torch.manual_seed(K + M)
+    A = torch.randn(M, K, device=gpu).to(BF)
+    B = torch.randn(K, N, device=gpu).to(BF)
+    a = A if ak else A.t().contiguous()
+    b = B.t().contiguous() if bk else B
+    ref = A.float() @ B.float()
+    bias = torch.randn(N, device=gpu).to(BF)
+    mask = torch.randn(M, N, device=gpu).to(BF)
+    T().gemm8p_policy(3, 0)
+    try:
+        y = torch.empty(M, N, device=gpu, dtype=BF)
+        T().gemm(a, ak, b, bk, y, 0, bias, True, None, 1.0, False)
+        assert rel_err(y, (ref + bias.float()).clamp_min(0)) < 1e-2
+        T().gemm(a, ak, b, bk, y, 0, None, False, mask, 0.5, False)
+        assert rel_err(y, 0.5 * ref * (mask.float() > 0)) < 1e-2
+        c = torch.full((M, N), 2.0, device=gpu)
+        T().gemm(a, ak, b, bk, c, 1, None, False, None, 1.0, False)
+        assert rel_err(c, ref + 2.0) < 1e-5
+        y0 = torch.randn(M, N, device=gpu).to(BF)
+        y1 = y0.clone()
+        T().gemm(a, ak, b, bk, y1, 1, None, False, None, 1.0, False)
+        assert rel_err(y1, y0.float() + ref) < 1e-2
+    finally:
+        T().gemm8p_policy(1, 0)
+
+
 def test_gemm_dma_splitk(gpu):
     torch.manual_seed(5)
     M, N, K = 96, 128, 8192
