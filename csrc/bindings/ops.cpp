@@ -61,7 +61,10 @@ using GemmKey = std::tuple<int64_t, int64_t, int64_t, bool, bool, int64_t, bool,
 std::map<GemmKey, int> g_route;          // 0 = igemm/gemm256, 1 = library, 2 = LDS-DMA GEMM
 std::map<GemmKey, std::array<float, 4>> g_route_ms;   // measured ms per path
 std::mutex g_route_mu;
-int g_lib_policy = -1;
+// hipBLASLt for plain GEMMs: 0 never (default: every GEMM on our MFMA kernels,
+// profiles/r2/gemm_models.json: -0..7 % model step time vs the measured
+// library routing), -1 measured per-shape routing, 1 always where eligible
+int g_lib_policy = 0;
 extern int g_dma_policy;
 bool g_forced = false;   // tile/split forced for tuning: never route to the library
 
@@ -95,11 +98,12 @@ void run_lib(const Tensor& a, bool ak, const Tensor& b, bool bk, const Tensor& c
 // any output dtype) when its tile grid underfills the chip
 void run_p8(const Tensor& a, bool ak, const Tensor& b, bool bk, int64_t M, int64_t N, int64_t K,
             const tam::Epi& ep, bool allow_split) {
-  const int sp = tam::gemm8p_slab_splits((int)M, (int)N, (int)K);
+  const int tile = tam::gemm8p_tile((int)M, (int)N, (int)K);
+  const int sp = tam::gemm8p_slab_splits((int)M, (int)N, (int)K, tile);
   if (sp > 1 && ep.ldc >= N) {
     Tensor ws = at::empty({sp, M, N}, a.options().dtype(at::kFloat));
     tam::gemm8p_splitk(bp(a), a.stride(0), ak, bp(b), b.stride(0), bk, (int)M, (int)N, (int)K, ep, sp,
-                       ws.data_ptr<float>(), cur_stream(a));
+                       ws.data_ptr<float>(), cur_stream(a), tile);
     return;
   }
   run_mfma(a, ak, b, bk, M, N, K, ep, allow_split, 3);

@@ -1,13 +1,15 @@
-// tiresias_amd — 256x256x64 bf16 GEMM, every operand majority, for the big
-// plain GEMMs of the model zoo (vocab projections, FFN / LSTM-gate weight
-// gradients, VGG FC layers): C[M][N] (+)= A . B, fp32 accumulate.
+// tiresias_amd — LDS-DMA MFMA GEMM for every operand majority, two tile
+// shapes: 256x256 (8 waves, big GEMMs) and 128x128 (4 waves, two blocks per
+// CU, the mid-size GEMMs of the zoo: FFN / LSTM-gate projections and their
+// gradients). C[M][N] (+)= A . B, bf16 in, fp32 accumulate.
 //
 //   A: K-major [M][K] (AK) or M-major [K][M];  B: K-major [N][K] (BK) or N-major [K][N]
 //
 // MI355X-first structure (cdna_hip_programming.md §5 "The 256^2 8-phase
 // template", T1-T5, T10):
-//  * 512 threads = 8 waves as 2 (M) x 4 (N); each wave owns 128x64 outputs =
-//    8x4 tiles of v_mfma_f32_16x16x32_bf16 (128 fp32 accumulators per lane).
+//  * 256^2: 512 threads = 8 waves as 2 (M) x 4 (N), 128x64 outputs per wave
+//    (8x4 tiles of v_mfma_f32_16x16x32_bf16, 128 fp32 accumulators / lane);
+//    128^2: 256 threads = 4 waves as 2 x 2, 64x64 per wave.
 //  * Both operands are staged HBM/L2 -> LDS by LDS-DMA (global_load_lds_dwordx4,
 //    no VGPR round trip). Each operand tile is split in two half-tiles by the
 //    C-quadrant that reads it (A: the wave's upper / lower 64 rows, B: its
@@ -44,10 +46,7 @@
 
 namespace tam {
 
-constexpr int P8_BM = 256, P8_BN = 256, P8_BK = 64, P8_THREADS = 512;
-constexpr int P8_HALF = 128 * 64 * 2;         // 16 KiB half-tile
-constexpr int P8_STAGE = 4 * P8_HALF;          // AL AH BL BH
-constexpr int P8_LDS = 2 * P8_STAGE;           // 128 KiB
+constexpr int P8_BK = 64;
 
 typedef __attribute__((address_space(3))) void p8_lds_t;
 
@@ -60,35 +59,50 @@ struct P8Args {
   int kps;   // K-tiles per split (blockIdx.z)
 };
 
-// local row lr (0..127) of a half-tile -> global row / column index
-//   A half h: rows wm*128 + h*64 + (lr & 63), wm = lr >> 6
-//   B half h: cols wn*64  + h*32 + (lr & 31), wn = lr >> 5
-template <bool IS_A>
+// Tile geometry: BM x BN block, 2 (M) x WNW (N) waves.
+template <int BM, int BN, int WNW>
+struct P8Geo {
+  static constexpr int NW = 2 * WNW, THREADS = 64 * NW;
+  static constexpr int WTM = BM / 2, WTN = BN / WNW;       // wave tile
+  static constexpr int QM = WTM / 2, QN = WTN / 2;         // quadrant (one phase)
+  static constexpr int FI = QM / 16, FJ = QN / 16;         // MFMA tiles per quadrant
+  static constexpr int AROWS = BM / 2, BCOLS = BN / 2;     // rows of an A / B half-tile
+  static constexpr int AHALF = AROWS * P8_BK * 2, BHALF = BCOLS * P8_BK * 2;
+  static constexpr int STAGE = 2 * AHALF + 2 * BHALF;      // AL AH BL BH
+  static constexpr int LDS = 2 * STAGE;
+  static_assert(AHALF == THREADS * 32 && BHALF == THREADS * 32, "2 DMA per thread per half");
+};
+
+// local row lr of a half-tile -> row / column offset in the block tile
+//   A half h: rows wm*WTM + h*QM + (lr % QM), wm = lr / QM
+//   B half h: cols wn*WTN + h*QN + (lr % QN), wn = lr / QN
+template <int Q>
 __device__ __forceinline__ int p8_row(int lr, int h) {
-  if constexpr (IS_A) return ((lr >> 6) << 7) + (h << 6) + (lr & 63);
-  else return ((lr >> 5) << 6) + (h << 5) + (lr & 31);
+  return (lr / Q) * (2 * Q) + h * Q + (lr % Q);
 }
 
-// Issue one half-tile (2 DMA instructions per thread).
-template <bool IS_A, bool KMAJ>
+// Issue one half-tile (2 DMA instructions per thread). EXT = rows of the
+// half-tile (K-major image) or its columns (MN-major image).
+template <int Q, int EXT, int NW, bool KMAJ>
 __device__ __forceinline__ void p8_issue(const bf16_t* __restrict__ base, long ld, int extent, int o0,
                                          int k0, char* half, int h, int wid, int lane) {
 #pragma unroll
   for (int j = 0; j < 2; ++j) {
-    const int g = j * 8 + wid;                 // 1-KiB group 0..15 of the half-tile
+    const int g = j * NW + wid;                // 1-KiB group of the half-tile
     if constexpr (KMAJ) {
       // 8 rows x 128 B per group; lane -> row 8g + lane/8, 16-B slot lane%8
       const int lr = g * 8 + (lane >> 3);
       const int c = (lane & 7) ^ ((lr >> 1) & 7);
-      int r = o0 + p8_row<IS_A>(lr, h);
+      int r = o0 + p8_row<Q>(lr, h);
       r = r < extent ? r : extent - 1;         // rows past the edge are never stored
       const bf16_t* src = base + (long)r * ld + k0 + c * 8;
       __builtin_amdgcn_global_load_lds((const void*)src, (p8_lds_t*)(half + g * 1024), 16, 0, 0);
     } else {
-      // 4 k-rows x 256 B per group; lane -> k-row 4g + lane/16, 16-B slot lane%16
-      const int kr = g * 4 + (lane >> 4);
-      const int gran = (lane & 15) ^ (mnmaj_swz<128>(kr) >> 1);   // 8 columns per granule
-      int col = o0 + p8_row<IS_A>(gran * 8, h);
+      // [64 k][EXT cols] image; RPG k-rows x (EXT*2) B per group
+      constexpr int GPR = EXT / 8, RPG = 64 / GPR;       // 16-B granules per row, rows per group
+      const int kr = g * RPG + lane / GPR;
+      const int gran = (lane % GPR) ^ (mnmaj_swz<EXT>(kr) >> 1);   // 8 columns per granule
+      int col = o0 + p8_row<Q>(gran * 8, h);
       col = col + 8 <= extent ? col : extent - 8;                  // extent % 8 == 0
       const bf16_t* src = base + (long)(k0 + kr) * ld + col;
       __builtin_amdgcn_global_load_lds((const void*)src, (p8_lds_t*)(half + g * 1024), 16, 0, 0);
@@ -96,10 +110,10 @@ __device__ __forceinline__ void p8_issue(const bf16_t* __restrict__ base, long l
   }
 }
 
-template <bool KMAJ>
+template <bool KMAJ, int EXT>
 __device__ __forceinline__ s16x8_t p8_frag(const char* half, int lane, int lbase, int kk) {
   if constexpr (KMAJ) return read_frag_k(half, lane, lbase, kk);
-  else return read_frag_mn<128>(half, lane, 32 * kk, lbase);
+  else return read_frag_mn<EXT>(half, lane, 32 * kk, lbase);
 }
 
 // raw s_barrier fenced for the COMPILER only (LDS reads / DMA issues stay on
@@ -110,18 +124,18 @@ __device__ __forceinline__ void p8_barrier() {
   asm volatile("" ::: "memory");
 }
 
-template <int I0, int J0>
-__device__ __forceinline__ void p8_mfma(f32x4_t (&acc)[8][4], const s16x8_t (&fa)[4][2],
-                                        const s16x8_t (&fb)[2][2]) {
+template <int I0, int J0, int FI, int FJ, int TI, int TJ>
+__device__ __forceinline__ void p8_mfma(f32x4_t (&acc)[TI][TJ], const s16x8_t (&fa)[FI][2],
+                                        const s16x8_t (&fb)[FJ][2]) {
   asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
   __builtin_amdgcn_sched_barrier(0);
   __builtin_amdgcn_s_setprio(1);
 #pragma unroll
   for (int kk = 0; kk < 2; ++kk)
 #pragma unroll
-    for (int i = 0; i < 4; ++i)
+    for (int i = 0; i < FI; ++i)
 #pragma unroll
-      for (int j = 0; j < 2; ++j)
+      for (int j = 0; j < FJ; ++j)
         acc[I0 + i][J0 + j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(
             __builtin_bit_cast(bf16x8_t, fa[i][kk]), __builtin_bit_cast(bf16x8_t, fb[j][kk]),
             acc[I0 + i][J0 + j], 0, 0, 0);
@@ -131,19 +145,20 @@ __device__ __forceinline__ void p8_mfma(f32x4_t (&acc)[8][4], const s16x8_t (&fa
 
 // SCHED 0: one barrier per phase (after the MFMA cluster); 1: two barriers
 // per phase (reads | MFMA); 2: two barriers + wave-group stagger
-// ABL (diagnostics only, tools/bench_gemm8p.py --ablate): 1 no DMA refills,
-// 2 no LDS fragment reads, 3 no MFMA
-template <bool AK, bool BK, int SCHED, int ABL = 0>
-__global__ void __launch_bounds__(P8_THREADS, 1) gemm8p_kernel(P8Args a, Epi ep) {
+template <int BM, int BN, int WNW, bool AK, bool BK, int SCHED>
+__global__ void __launch_bounds__(128 * WNW, (BM == 256 ? 1 : 2))
+gemm8p_kernel(P8Args a, Epi ep) {
+  using G = P8Geo<BM, BN, WNW>;
   constexpr bool STAGGER = SCHED == 2;
-  __shared__ __attribute__((aligned(1024))) char smem[P8_LDS];
+  constexpr int FI = G::FI, FJ = G::FJ, TI = 2 * FI, TJ = 2 * FJ;
+  __shared__ __attribute__((aligned(1024))) char smem[G::LDS];
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
-  const int wm = wid >> 2, wn = wid & 3;
+  const int wm = wid / WNW, wn = wid % WNW;
   // the upper wave group, as a wave-uniform SCALAR condition (a divergent
   // branch would execute the scalar s_barrier on every wave)
-  const bool upper = __builtin_amdgcn_readfirstlane(tid) >= 256;
+  const bool upper = __builtin_amdgcn_readfirstlane(tid) >= G::THREADS / 2;
 
-  const int tiles_m = (a.M + P8_BM - 1) / P8_BM, tiles_n = (a.N + P8_BN - 1) / P8_BN;
+  const int tiles_m = (a.M + BM - 1) / BM, tiles_n = (a.N + BN - 1) / BN;
   const int bid = xcd_remap(blockIdx.x, gridDim.x);
   constexpr int GROUP = 4;
   const int per_group = GROUP * tiles_n;
@@ -152,28 +167,27 @@ __global__ void __launch_bounds__(P8_THREADS, 1) gemm8p_kernel(P8Args a, Epi ep)
   const int gsize = min(tiles_m - first_m, GROUP);
   const int tm = first_m + (bid % per_group) % gsize;
   const int tn = (bid % per_group) / gsize;
-  const int m0 = tm * P8_BM, n0 = tn * P8_BN;
+  const int m0 = tm * BM, n0 = tn * BN;
 
   const int ktiles = a.K / P8_BK;
   const int kt0 = blockIdx.z * a.kps;
   const int kt1 = min(ktiles, kt0 + a.kps);
   const int nk = kt1 - kt0;
 
-  f32x4_t acc[8][4];
+  f32x4_t acc[TI][TJ];
 #pragma unroll
-  for (int i = 0; i < 8; ++i)
+  for (int i = 0; i < TI; ++i)
 #pragma unroll
-    for (int j = 0; j < 4; ++j) acc[i][j] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+    for (int j = 0; j < TJ; ++j) acc[i][j] = f32x4_t{0.f, 0.f, 0.f, 0.f};
 
   // stage s: [AL][AH][BL][BH]
-  auto half_ptr = [&](int t, int which) { return smem + (t & 1) * P8_STAGE + which * P8_HALF; };
+  auto aptr = [&](int t, int h) { return smem + (t & 1) * G::STAGE + h * G::AHALF; };
+  auto bptr = [&](int t, int h) { return smem + (t & 1) * G::STAGE + 2 * G::AHALF + h * G::BHALF; };
   auto issA = [&](int t, int h) {
-    if (ABL == 1 && t > 1) return;
-    p8_issue<true, AK>(a.A, a.lda, a.M, m0, (kt0 + t) * P8_BK, half_ptr(t, h), h, wid, lane);
+    p8_issue<G::QM, G::AROWS, G::NW, AK>(a.A, a.lda, a.M, m0, (kt0 + t) * P8_BK, aptr(t, h), h, wid, lane);
   };
   auto issB = [&](int t, int h) {
-    if (ABL == 1 && t > 1) return;
-    p8_issue<false, BK>(a.B, a.ldb, a.N, n0, (kt0 + t) * P8_BK, half_ptr(t, 2 + h), h, wid, lane);
+    p8_issue<G::QN, G::BCOLS, G::NW, BK>(a.B, a.ldb, a.N, n0, (kt0 + t) * P8_BK, bptr(t, h), h, wid, lane);
   };
 
   if (nk > 0) {
@@ -188,23 +202,21 @@ __global__ void __launch_bounds__(P8_THREADS, 1) gemm8p_kernel(P8Args a, Epi ep)
     p8_barrier();
     if (STAGGER && upper) p8_barrier();
 
-    const int arow = wm * 64, bcol = wn * 32;   // local rows in the half images
-    s16x8_t fa[4][2], fb0[2][2], fb1[2][2];
+    const int arow = wm * G::QM, bcol = wn * G::QN;   // local rows in the half images
+    s16x8_t fa[FI][2], fb0[FJ][2], fb1[FJ][2];
     for (int t = 0; t < nk; ++t) {
-      const char* AL = half_ptr(t, 0);
-      const char* AH = half_ptr(t, 1);
-      const char* BL = half_ptr(t, 2);
-      const char* BH = half_ptr(t, 3);
+      const char* AL = aptr(t, 0);
+      const char* AH = aptr(t, 1);
+      const char* BL = bptr(t, 0);
+      const char* BH = bptr(t, 1);
       const bool n1 = t + 1 < nk, n2 = t + 2 < nk;
       // ---- p1: quadrant (mh0, nh0)
 #pragma unroll
       for (int kk = 0; kk < 2; ++kk) {
-        if (ABL != 2 || t == 0)
 #pragma unroll
-        for (int j = 0; j < 2; ++j) fb0[j][kk] = p8_frag<BK>(BL, lane, bcol + 16 * j, kk);
-        if (ABL != 2 || t == 0)
+        for (int j = 0; j < FJ; ++j) fb0[j][kk] = p8_frag<BK, G::BCOLS>(BL, lane, bcol + 16 * j, kk);
 #pragma unroll
-        for (int i = 0; i < 4; ++i) fa[i][kk] = p8_frag<AK>(AL, lane, arow + 16 * i, kk);
+        for (int i = 0; i < FI; ++i) fa[i][kk] = p8_frag<AK, G::AROWS>(AL, lane, arow + 16 * i, kk);
       }
       if (n1) issA(t + 1, 1);
       if constexpr (SCHED > 0) p8_barrier();
@@ -213,21 +225,19 @@ __global__ void __launch_bounds__(P8_THREADS, 1) gemm8p_kernel(P8Args a, Epi ep)
       // ---- p2: quadrant (mh0, nh1)
 #pragma unroll
       for (int kk = 0; kk < 2; ++kk)
-        if (ABL != 2 || t == 0)
 #pragma unroll
-        for (int j = 0; j < 2; ++j) fb1[j][kk] = p8_frag<BK>(BH, lane, bcol + 16 * j, kk);
+        for (int j = 0; j < FJ; ++j) fb1[j][kk] = p8_frag<BK, G::BCOLS>(BH, lane, bcol + 16 * j, kk);
       if constexpr (SCHED > 0) p8_barrier();
-      p8_mfma<0, 2>(acc, fa, fb1);
+      p8_mfma<0, FJ>(acc, fa, fb1);
       p8_barrier();
       // ---- p3: quadrant (mh1, nh1)
 #pragma unroll
       for (int kk = 0; kk < 2; ++kk)
-        if (ABL != 2 || t == 0)
 #pragma unroll
-        for (int i = 0; i < 4; ++i) fa[i][kk] = p8_frag<AK>(AH, lane, arow + 16 * i, kk);
+        for (int i = 0; i < FI; ++i) fa[i][kk] = p8_frag<AK, G::AROWS>(AH, lane, arow + 16 * i, kk);
       if (n2) issA(t + 2, 0);
       if constexpr (SCHED > 0) p8_barrier();
-      p8_mfma<2 * 2, 2>(acc, fa, fb1);
+      p8_mfma<FI, FJ>(acc, fa, fb1);
       p8_barrier();
       // ---- p4: quadrant (mh1, nh0); retire tile t+1 (t+2's AL / BL / BH stay in flight)
       if (n2) {
@@ -238,7 +248,7 @@ __global__ void __launch_bounds__(P8_THREADS, 1) gemm8p_kernel(P8Args a, Epi ep)
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       }
       if constexpr (SCHED > 0) p8_barrier();
-      p8_mfma<2 * 2, 0>(acc, fa, fb0);
+      p8_mfma<FI, 0>(acc, fa, fb0);
       p8_barrier();
     }
     if (STAGGER && !upper) p8_barrier();        // both groups execute the same barrier count
@@ -246,23 +256,24 @@ __global__ void __launch_bounds__(P8_THREADS, 1) gemm8p_kernel(P8Args a, Epi ep)
   __syncthreads();   // LDS reuse by the epilogue
 
   const bool add_bias = ep.bias != nullptr && blockIdx.z == 0;
-  const int rbase = m0 + wm * 128, cbase = n0 + wn * 64;
+  const int rbase = m0 + wm * G::WTM, cbase = n0 + wn * G::WTN;
+  constexpr int WTN = G::WTN;
+  float bv[TJ];
+#pragma unroll
+  for (int j = 0; j < TJ; ++j) {
+    const int col = cbase + 16 * j + (lane & 15);
+    bv[j] = (add_bias && col < a.N) ? bf2f(ep.bias[col]) : 0.f;
+  }
   // ---- bf16 output, plain store / accumulate: LDS-staged, 16-B row chunks
   if (!ep.c_f32 && !ep.mask && (ep.ldc & 7) == 0 && (((uintptr_t)ep.c) & 15) == 0) {
-    constexpr int LDW = 64 + 8;
+    constexpr int LDW = WTN + 8, CPR = WTN / 8;
     bf16_t* slab = (bf16_t*)(smem + wid * (32 * LDW * 2));
-    float bv[4];
 #pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      const int col = cbase + 16 * j + (lane & 15);
-      bv[j] = (add_bias && col < a.N) ? bf2f(ep.bias[col]) : 0.f;
-    }
-#pragma unroll
-    for (int h = 0; h < 4; ++h) {
+    for (int h = 0; h < TI / 2; ++h) {
 #pragma unroll
       for (int ii = 0; ii < 2; ++ii)
 #pragma unroll
-        for (int j = 0; j < 4; ++j)
+        for (int j = 0; j < TJ; ++j)
 #pragma unroll
           for (int r = 0; r < 4; ++r) {
             float v = acc[2 * h + ii][j][r] * ep.alpha + bv[j];
@@ -271,8 +282,8 @@ __global__ void __launch_bounds__(P8_THREADS, 1) gemm8p_kernel(P8Args a, Epi ep)
           }
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
 #pragma unroll
-      for (int u = 0; u < 4; ++u) {              // 32 rows x 8 chunks of 16 B
-        const int idx = u * 64 + lane, lr = idx >> 3, ch = idx & 7;
+      for (int u = 0; u < 32 * CPR / 64; ++u) {
+        const int idx = u * 64 + lane, lr = idx / CPR, ch = idx % CPR;
         const int row = rbase + 32 * h + lr, col = cbase + ch * 8;
         if (row >= a.M || col >= a.N) continue;
         bf16_t* dst = (bf16_t*)ep.c + (long)row * ep.ldc + col;
@@ -304,21 +315,15 @@ __global__ void __launch_bounds__(P8_THREADS, 1) gemm8p_kernel(P8Args a, Epi ep)
   // ---- fp32 output, store / accumulate / split-K slab: LDS-staged, 16-B row chunks
   if (ep.c_f32 && ep.mode != 2 && !ep.mask && (ep.ldc & 3) == 0 && (((uintptr_t)ep.c) & 15) == 0 &&
       (ep.mode != 3 || (ep.zstride & 3) == 0)) {
-    constexpr int LDF = 64 + 4;
+    constexpr int LDF = WTN + 4, CPR = WTN / 4;
     float* slab = (float*)(smem + wid * (32 * LDF * 4));
     float* cz = (float*)ep.c + (ep.mode == 3 ? blockIdx.z * ep.zstride : 0);
-    float bv[4];
 #pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      const int col = cbase + 16 * j + (lane & 15);
-      bv[j] = (add_bias && col < a.N) ? bf2f(ep.bias[col]) : 0.f;
-    }
-#pragma unroll
-    for (int h = 0; h < 4; ++h) {
+    for (int h = 0; h < TI / 2; ++h) {
 #pragma unroll
       for (int ii = 0; ii < 2; ++ii)
 #pragma unroll
-        for (int j = 0; j < 4; ++j)
+        for (int j = 0; j < TJ; ++j)
 #pragma unroll
           for (int r = 0; r < 4; ++r) {
             float v = acc[2 * h + ii][j][r] * ep.alpha + bv[j];
@@ -327,8 +332,8 @@ __global__ void __launch_bounds__(P8_THREADS, 1) gemm8p_kernel(P8Args a, Epi ep)
           }
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
 #pragma unroll
-      for (int u = 0; u < 8; ++u) {              // 32 rows x 16 chunks of 16 B
-        const int idx = u * 64 + lane, lr = idx >> 4, ch = idx & 15;
+      for (int u = 0; u < 32 * CPR / 64; ++u) {
+        const int idx = u * 64 + lane, lr = idx / CPR, ch = idx % CPR;
         const int row = rbase + 32 * h + lr, col = cbase + ch * 4;
         if (row >= a.M || col >= a.N) continue;
         float* dst = cz + (long)row * ep.ldc + col;
@@ -351,17 +356,16 @@ __global__ void __launch_bounds__(P8_THREADS, 1) gemm8p_kernel(P8Args a, Epi ep)
   // ---- general epilogue (atomics / relu-mask): C/D map of 16x16x32:
   // col = lane&15, row = (lane>>4)*4 + r
 #pragma unroll
-  for (int j = 0; j < 4; ++j) {
+  for (int j = 0; j < TJ; ++j) {
     const int col = cbase + 16 * j + (lane & 15);
     if (col >= a.N) continue;
-    const float bv = add_bias ? bf2f(ep.bias[col]) : 0.f;
 #pragma unroll
-    for (int i = 0; i < 8; ++i) {
+    for (int i = 0; i < TI; ++i) {
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
         const int row = rbase + 16 * i + 4 * (lane >> 4) + r;
         if (row >= a.M) continue;
-        float v = acc[i][j][r] * ep.alpha + bv;
+        float v = acc[i][j][r] * ep.alpha + bv[j];
         if (ep.relu) v = fmaxf(v, 0.f);
         if (ep.mask && bf2f(ep.mask[(long)row * ep.ldm + col]) <= 0.f) v = 0.f;
         const long off = (long)row * ep.ldc + col;
@@ -381,7 +385,7 @@ __global__ void __launch_bounds__(P8_THREADS, 1) gemm8p_kernel(P8Args a, Epi ep)
   }
 }
 
-// shape / layout conditions of the LDS-DMA 256^2 kernel
+// shape / layout conditions of the LDS-DMA kernels (tile >= 128)
 inline bool gemm8p_ok(bool ak, bool bk, int M, int N, int K, long lda, long ldb) {
   if (K % P8_BK != 0 || K < P8_BK || M < 128 || N < 128) return false;
   if (lda % 8 != 0 || ldb % 8 != 0) return false;
@@ -390,14 +394,17 @@ inline bool gemm8p_ok(bool ak, bool bk, int M, int N, int K, long lda, long ldb)
   return true;
 }
 
+// tile: 256 (256x256, 8 waves) or 128 (128x128, 4 waves)
 void launch_gemm8p(const bf16_t* A, long lda, bool ak, const bf16_t* B, long ldb, bool bk, int M,
-                   int N, int K, const Epi& ep, int splits, hipStream_t s, int sched = 0);
+                   int N, int K, const Epi& ep, int splits, hipStream_t s, int sched = 0, int tile = 256);
 // split-K without atomics or a zeroing pass, any output dtype / epilogue:
 // every K-slice writes its own fp32 slab of ws[splits][M][N], then one
 // reduce pass sums the slabs and applies ep (bias / relu / mask / alpha /
 // store or accumulate) — deterministic
 void gemm8p_splitk(const bf16_t* A, long lda, bool ak, const bf16_t* B, long ldb, bool bk, int M,
-                   int N, int K, const Epi& ep, int splits, float* ws, hipStream_t s);
-int gemm8p_slab_splits(int M, int N, int K);
+                   int N, int K, const Epi& ep, int splits, float* ws, hipStream_t s, int tile = 256);
+int gemm8p_slab_splits(int M, int N, int K, int tile = 256);
+// 128 or 256: the tile the auto policy picks for this shape
+int gemm8p_tile(int M, int N, int K);
 
 }  // namespace tam

@@ -81,40 +81,52 @@ void zero_async(void* p, size_t bytes, hipStream_t s) {
                      b + n16 * 16, ntail);
 }
 
-// 256x256 all-layout LDS-DMA kernel (gemm8p.h): 0 off (legacy gemm256 for
-// big K-major GEMMs), 1 auto (big GEMMs of every layout), 2 forced wherever
-// eligible (tests / sweeps); stagger = wave-group ping-pong schedule
-static int g_p8 = 1, g_p8_sched = 0, g_p8_abl = 0;
+// LDS-DMA all-layout kernels (gemm8p.h): 0 off (legacy kernels only),
+// 1 auto (big GEMMs of every layout), 2 forced wherever eligible, 3 forced
+// with slab split-K (the op binding; tests / sweeps). sched: 0 one barrier
+// per phase, 1 two, 2 two + wave-group stagger; tile: 0 auto, 128 / 256 forced
+static int g_p8 = 1, g_p8_sched = 0, g_p8_tile = 0;
 int gemm8p_policy_mode() { return g_p8; }
 void gemm8p_policy(int mode, int sched) {
   g_p8 = mode;
   g_p8_sched = sched % 10;
-  g_p8_abl = sched / 10;      // diagnostics: 10 / 20 = ablation 1 / 2 (KK, schedule 2)
+  g_p8_tile = sched >= 200 ? 256 : sched >= 100 ? 128 : 0;    // tests: sched + 100 / + 200
 }
 
-template <bool AK, bool BK>
-static void p8_launch(const P8Args& g, const Epi& ep, dim3 grid, int sched, hipStream_t s) {
-  if (sched == 2) hipLaunchKernelGGL((gemm8p_kernel<AK, BK, 2>), grid, dim3(P8_THREADS), 0, s, g, ep);
-  else if (sched == 1) hipLaunchKernelGGL((gemm8p_kernel<AK, BK, 1>), grid, dim3(P8_THREADS), 0, s, g, ep);
-  else hipLaunchKernelGGL((gemm8p_kernel<AK, BK, 0>), grid, dim3(P8_THREADS), 0, s, g, ep);
+template <int BM, int BN, int WNW, bool AK, bool BK>
+static void p8_launch_t(const P8Args& g, const Epi& ep, dim3 grid, int sched, hipStream_t s) {
+  constexpr int T = P8Geo<BM, BN, WNW>::THREADS;
+  if (sched == 2) hipLaunchKernelGGL((gemm8p_kernel<BM, BN, WNW, AK, BK, 2>), grid, dim3(T), 0, s, g, ep);
+  else if (sched == 1) hipLaunchKernelGGL((gemm8p_kernel<BM, BN, WNW, AK, BK, 1>), grid, dim3(T), 0, s, g, ep);
+  else hipLaunchKernelGGL((gemm8p_kernel<BM, BN, WNW, AK, BK, 0>), grid, dim3(T), 0, s, g, ep);
+}
+
+template <int BM, int BN, int WNW>
+static void p8_launch_l(bool ak, bool bk, const P8Args& g, const Epi& ep, dim3 grid, int sched, hipStream_t s) {
+  if (ak && bk) p8_launch_t<BM, BN, WNW, true, true>(g, ep, grid, sched, s);
+  else if (ak) p8_launch_t<BM, BN, WNW, true, false>(g, ep, grid, sched, s);
+  else if (bk) p8_launch_t<BM, BN, WNW, false, true>(g, ep, grid, sched, s);
+  else p8_launch_t<BM, BN, WNW, false, false>(g, ep, grid, sched, s);
+}
+
+int gemm8p_tile(int M, int N, int K) {
+  if (g_p8_tile) return g_p8_tile;
+  // 256^2 only when its grid already covers the chip
+  const long t256 = (long)cdiv(M, 256) * cdiv(N, 256);
+  return t256 >= 200 ? 256 : 128;
 }
 
 void launch_gemm8p(const bf16_t* A, long lda, bool ak, const bf16_t* B, long ldb, bool bk, int M,
-                   int N, int K, const Epi& ep, int splits, hipStream_t s, int stagger) {
-  const int tiles = cdiv(M, P8_BM) * cdiv(N, P8_BN);
+                   int N, int K, const Epi& ep, int splits, hipStream_t s, int sched, int tile) {
+  const int T = tile == 128 ? 128 : 256;
+  const int tiles = cdiv(M, T) * cdiv(N, T);
   const int ktiles = K / P8_BK;
   const int kps = cdiv(ktiles, splits < 1 ? 1 : splits);
   const int z = cdiv(ktiles, kps);
   P8Args g{A, lda, B, ldb, M, N, K, kps};
   const dim3 grid(tiles, 1, z);
-  if (g_p8_abl == 1 && ak && bk)
-    hipLaunchKernelGGL((gemm8p_kernel<true, true, 2, 1>), grid, dim3(P8_THREADS), 0, s, g, ep);
-  else if (g_p8_abl == 2 && ak && bk)
-    hipLaunchKernelGGL((gemm8p_kernel<true, true, 2, 2>), grid, dim3(P8_THREADS), 0, s, g, ep);
-  else if (ak && bk) p8_launch<true, true>(g, ep, grid, stagger, s);
-  else if (ak) p8_launch<true, false>(g, ep, grid, stagger, s);
-  else if (bk) p8_launch<false, true>(g, ep, grid, stagger, s);
-  else p8_launch<false, false>(g, ep, grid, stagger, s);
+  if (T == 128) p8_launch_l<128, 128, 2>(ak, bk, g, ep, grid, sched, s);
+  else p8_launch_l<256, 256, 4>(ak, bk, g, ep, grid, sched, s);
 }
 
 // ---- slab split-K (gemm8p.h): reduce ws[sp][M][N] -> C with the epilogue
@@ -149,25 +161,27 @@ __global__ void __launch_bounds__(256) p8_slab_reduce_kernel(const float* __rest
   }
 }
 
-int gemm8p_slab_splits(int M, int N, int K) {
-  const long t = (long)cdiv(M, P8_BM) * cdiv(N, P8_BN);
+int gemm8p_slab_splits(int M, int N, int K, int tile) {
+  const int T = tile == 128 ? 128 : 256;
+  const long t = (long)cdiv(M, T) * cdiv(N, T);
   const int kt = K / P8_BK;
-  if (t >= 160 || kt < 16 || N % 4 != 0) return 1;
-  int sp = (int)((256 + t - 1) / t);
+  const long want = T == 128 ? 448 : 200;     // blocks that fill the chip (128^2: 2 per CU)
+  if (t >= want * 3 / 4 || kt < 16 || N % 4 != 0) return 1;
+  int sp = (int)((want + t - 1) / t);
   if (sp > kt / 8) sp = kt / 8;          // >= 8 K-tiles per slice
   if (sp > 16) sp = 16;
   return sp < 2 ? 1 : sp;
 }
 
 void gemm8p_splitk(const bf16_t* A, long lda, bool ak, const bf16_t* B, long ldb, bool bk, int M,
-                   int N, int K, const Epi& ep, int splits, float* ws, hipStream_t s) {
+                   int N, int K, const Epi& ep, int splits, float* ws, hipStream_t s, int tile) {
   Epi se;
   se.c = ws;
   se.ldc = N;
   se.c_f32 = 1;
   se.mode = 3;
   se.zstride = (long)M * N;
-  launch_gemm8p(A, lda, ak, B, ldb, bk, M, N, K, se, splits, s, g_p8_sched);
+  launch_gemm8p(A, lda, ak, B, ldb, bk, M, N, K, se, splits, s, g_p8_sched, tile);
   const int ktiles = K / P8_BK;
   const int z = cdiv(ktiles, cdiv(ktiles, splits));   // slabs actually written
   const long n4 = (long)M * N / 4;
@@ -176,11 +190,12 @@ void gemm8p_splitk(const bf16_t* A, long lda, bool ak, const bf16_t* B, long ldb
   hipLaunchKernelGGL(p8_slab_reduce_kernel, dim3((unsigned)blocks), dim3(256), 0, s, ws, z, M, N, ep);
 }
 
-// split count that fills the 256 CUs with 256^2 tiles (>= 4 K-tiles per split)
-static int p8_splits(int M, int N, int K, bool can_split) {
-  const long t = (long)cdiv(M, P8_BM) * cdiv(N, P8_BN);
-  if (!can_split || t >= 192 || K / P8_BK < 8) return 1;
-  int sp = (int)((256 + t - 1) / t);
+// atomic split-K count (fp32 outputs) that fills the chip (>= 4 K-tiles per split)
+static int p8_splits(int M, int N, int K, bool can_split, int tile) {
+  const long t = (long)cdiv(M, tile) * cdiv(N, tile);
+  const long want = tile == 128 ? 448 : 200;
+  if (!can_split || t >= want || K / P8_BK < 8) return 1;
+  int sp = (int)((want + t - 1) / t);
   if (sp > K / P8_BK / 4) sp = K / P8_BK / 4;
   return sp < 1 ? 1 : sp;
 }
@@ -195,13 +210,14 @@ void gemm_select(const bf16_t* A, long lda, bool ak, const bf16_t* B, long ldb, 
   if (M <= 0 || N <= 0) return;
   const bool can_split = allow_split && ep.c_f32 && !ep.relu && !ep.mask;
   if (g_p8 > 0 && g_force_cfg < 0 && gemm8p_ok(ak, bk, M, N, K, lda, ldb)) {
-    const long t8 = (long)cdiv(M, P8_BM) * cdiv(N, P8_BN);
+    const long t8 = (long)cdiv(M, 256) * cdiv(N, 256);
     const double flop = 2.0 * M * N * K;
     if (g_p8 >= 2 || path == 3 || (t8 >= 48 && K >= 512 && flop >= 4e9)) {
-      int sp = p8_splits(M, N, K, can_split);
+      const int tile = gemm8p_tile(M, N, K);
+      int sp = p8_splits(M, N, K, can_split, tile);
       if (g_force_splits >= 1) sp = can_split ? g_force_splits : 1;
       prepare_split(ep, sp, M, N, s);
-      launch_gemm8p(A, lda, ak, B, ldb, bk, M, N, K, ep, sp, s, g_p8_sched);
+      launch_gemm8p(A, lda, ak, B, ldb, bk, M, N, K, ep, sp, s, g_p8_sched, tile);
       return;
     }
   }

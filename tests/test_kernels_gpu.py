@@ -27,7 +27,7 @@ def _mfma_only(gpu):
     measured hipBLASLt route of plain GEMMs."""
     T().gemm_lib_policy(0)
     yield
-    T().gemm_lib_policy(-1)
+    T().gemm_lib_policy(0)
 
 
 def test_gemm_routing(gpu):
@@ -39,7 +39,7 @@ def test_gemm_routing(gpu):
     W = torch.randn(N, K, device=gpu).to(BF)
     bias = torch.randn(N, device=gpu).to(BF)
     ref = A.float() @ W.float().t()
-    for pol in (1, -1):
+    for pol in (1, -1, 0):
         T().gemm_lib_policy(pol)
         y = torch.empty(M, N, device=gpu, dtype=BF)
         T().gemm(A, True, W, True, y, 0, bias, False, None, 1.0, False)
@@ -111,7 +111,9 @@ def test_gemm_dma_configs(gpu, cfg, ak, bk):
 # both schedules (wave-group stagger on / off), edge tiles, K just one tile
 # and many tiles, every epilogue (bf16 staged, bias / relu / mask / alpha /
 # accumulate, fp32 store / accumulate / split-K atomics)
-@pytest.mark.parametrize("stagger", [0, 1, 2])
+# sched codes: schedule (0 one barrier / phase, 1 two, 2 two + stagger) +
+# 100: 128x128 tile forced, + 200: 256x256 forced, else the auto tile
+@pytest.mark.parametrize("stagger", [0, 2, 101, 200, 202])
 @pytest.mark.parametrize("ak,bk", [(True, True), (True, False), (False, True), (False, False)])
 @pytest.mark.parametrize("M,N,K", [(256, 256, 64), (520, 392, 448), (1024, 768, 2048)])
 def test_gemm8p(gpu, stagger, ak, bk, M, N, K):
@@ -160,7 +162,7 @@ def test_gemm8p_exact_integer_layout(gpu, ak, bk):
     b = (B.t().contiguous() if bk else B).to(BF)
     ref = A @ B
     try:
-        for sched in (0, 1, 2):
+        for sched in (0, 1, 2, 100, 102, 200, 202):
             T().gemm8p_policy(2, sched)
             c = torch.empty(M, N, device=gpu)
             T().gemm(a, ak, b, bk, c, 0, None, False, None, 1.0, False)

@@ -66,12 +66,13 @@ def main():
         c = torch.empty(M, N, device=dev, dtype=BF)
         fl = 2.0 * M * N * K
         res = {"shape": f"{M}x{N}x{K} {'K' if ak else 'M'}{'K' if bk else 'N'}"}
-        for name, mode, stg in (("p8_1bar", 2, 0), ("p8_stagger", 2, 2), ("p8_slab", 3, 0), ("legacy", 0, 0)):
+        for name, mode, stg in (("p8_256", 2, 200), ("p8_128", 2, 100), ("p8_slab_auto", 3, 0),
+                                ("legacy", 0, 0)):
             T.gemm8p_policy(mode, stg)
             ms = timeit(lambda: T.gemm(a_, ak, b_, bk, c, 0, None, False, None, 1.0, False))
             res[name + "_tflops"] = round(fl / ms / 1e9, 1)
         cf = torch.zeros(M, N, device=dev)
-        for name, mode, stg in (("p8_f32acc", 2, 0), ("p8slab_f32acc", 3, 0)):
+        for name, mode, stg in (("p8_f32acc_auto", 2, 0), ("p8slab_f32acc_auto", 3, 0)):
             T.gemm8p_policy(mode, stg)
             ms = timeit(lambda: T.gemm(a_, ak, b_, bk, cf, 1, None, False, None, 1.0, False))
             res[name + "_tflops"] = round(fl / ms / 1e9, 1)

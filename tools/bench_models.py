@@ -43,7 +43,7 @@ def main():
                     help="weight gradients on a side stream: -1 per-model default, 0 off, 1 on")
     ap.add_argument("--branches", type=int, default=-1,
                     help="model branch streams (GNMT's independent recurrences): -1 model default, 0 off, 1 on")
-    ap.add_argument("--lib", type=int, default=-1,
+    ap.add_argument("--lib", type=int, default=0,
                     help="plain-GEMM routing: -1 measured MFMA/hipBLASLt, 0 MFMA only, 1 library")
     a = ap.parse_args()
     import torch
