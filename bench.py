@@ -169,7 +169,7 @@ SCENARIOS = {
     "trace": ("dlas-gpu", "tiresias", "none", "fifo", "yarn", [0.05, 0.25, 1.0], False),
     "resnet4": ("dlas-gpu", "tiresias", "none", "fifo", "yarn", [1e9], False),
     "skew": ("dlas-gpu", "tiresias", "none", "dlas-gpu", "random", [1.0], False),
-    "seq": ("gittins", "tiresias", "host", "fifo", "yarn", [0.05, 0.5], False),
+    "seq": ("gittins", "tiresias", "pressure", "fifo", "yarn", [0.05, 0.5], False),
 }
 # measured in-process co-run throughput of every model pair (tools/measure_stream_sharing.py)
 SHARING_TABLE = os.path.join(ROOT, "profiles", "stream_sharing_mi355x.json")
@@ -198,7 +198,11 @@ def main():
                          "BASELINE.json configs 2-4 (policy defaults follow the scenario)")
     ap.add_argument("--policy", default=None)
     ap.add_argument("--placement", default=None)
-    ap.add_argument("--ckpt", default=None, help="preemption state policy: none (HBM) | host")
+    ap.add_argument("--ckpt", default=None,
+                    help="preemption state: none (stay in HBM) | pressure (spill to pinned host only when a "
+                         "starting job needs the HBM) | host (always spill)")
+    ap.add_argument("--hbm-budget-gb", type=float, default=None,
+                    help="per-GPU HBM the jobs may use (pressure policy; default: the device's free HBM)")
     ap.add_argument("--baseline-policy", default=None)
     ap.add_argument("--baseline-placement", default=None)
     ap.add_argument("--no-baseline", action="store_true")
@@ -281,7 +285,7 @@ def main():
 
     cfg = make(a.policy, a.placement)
     worker = Worker(rank, world, device, world_pg, use_graph=use_cuda and not a.no_graph,
-                    pool_cap=0 if a.no_pool else 2)
+                    pool_cap=0 if a.no_pool else 2, hbm_budget_gb=a.hbm_budget_gb)
 
     def sync():
         if world > 1:
@@ -397,6 +401,8 @@ def main():
             "gpu_utilization": round(statistics.fmean(s["gpu_utilization"] for s in sums), 4),
             "runtime_breakdown_s": sums[-1].get("runtime_breakdown"),
             "pool_hits": worker.pool_hits,
+            "pressure_spills": worker.pressure_spills,
+            "spilled_gb": round(worker.spilled_bytes / 2 ** 30, 3),
             "max_hbm_reserved_gb": round(torch.cuda.max_memory_reserved(device) / 2 ** 30, 2) if use_cuda else None,
             "process_wall_s": round(time.perf_counter() - T_PROC0, 1),
             "device": torch.cuda.get_device_name(device) if use_cuda else "cpu",

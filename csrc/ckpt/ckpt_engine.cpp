@@ -8,9 +8,10 @@
 // overlaps the next job's compute. Restore is the reverse (H2D on the side
 // stream; the consumer stream waits on an event, never the host).
 //
-// The pinned pool is carved from large hipHostMalloc'd chunks with a
-// first-fit free list (coalescing on free) so spills never call the
-// (synchronising, expensive) pinned allocator on the hot path.
+// The pinned pool (tam/pinned_pool.h, host-only and sanitizer-tested) is
+// carved from large hipHostMalloc'd chunks with a first-fit free list
+// (coalescing on free) so spills never call the (synchronising, expensive)
+// pinned allocator on the hot path.
 #include <ATen/ATen.h>
 #include <c10/hip/HIPStream.h>
 #include <torch/custom_class.h>
@@ -22,80 +23,22 @@
 #include <vector>
 
 #include "tam/common.h"
+#include "tam/pinned_pool.h"
 
 namespace {
 
-struct Block { size_t off, size; };
-
-class PinnedPool {
- public:
-  explicit PinnedPool(size_t chunk) : chunk_(chunk) {}
-  ~PinnedPool() {
-    for (auto& c : chunks_) (void)hipHostFree(c.base);
-  }
-  // returns host pointer; grows by whole chunks (>= request)
-  char* alloc(size_t n) {
-    n = (n + 255) & ~size_t(255);
-    for (auto& c : chunks_) {
-      for (size_t i = 0; i < c.free.size(); ++i) {
-        if (c.free[i].size >= n) {
-          char* p = c.base + c.free[i].off;
-          c.free[i].off += n;
-          c.free[i].size -= n;
-          if (c.free[i].size == 0) c.free.erase(c.free.begin() + i);
-          used_ += n;
-          return p;
-        }
-      }
-    }
-    const size_t sz = n > chunk_ ? n : chunk_;
-    Chunk c;
-    TAM_HIP_CHECK(hipHostMalloc((void**)&c.base, sz, hipHostMallocDefault));
-    c.size = sz;
-    c.free.push_back({n, sz - n});
-    if (c.free.back().size == 0) c.free.pop_back();
-    chunks_.push_back(std::move(c));
-    reserved_ += sz;
-    used_ += n;
-    return chunks_.back().base;
-  }
-  void free(char* p, size_t n) {
-    n = (n + 255) & ~size_t(255);
-    for (auto& c : chunks_) {
-      if (p >= c.base && p < c.base + c.size) {
-        Block b{(size_t)(p - c.base), n};
-        auto it = c.free.begin();
-        while (it != c.free.end() && it->off < b.off) ++it;
-        it = c.free.insert(it, b);
-        // coalesce with next
-        if (it + 1 != c.free.end() && it->off + it->size == (it + 1)->off) {
-          it->size += (it + 1)->size;
-          c.free.erase(it + 1);
-        }
-        // coalesce with prev
-        if (it != c.free.begin() && (it - 1)->off + (it - 1)->size == it->off) {
-          (it - 1)->size += it->size;
-          c.free.erase(it);
-        }
-        used_ -= n;
-        return;
-      }
-    }
-    TORCH_CHECK(false, "PinnedPool: pointer not owned by pool");
-  }
-  size_t reserved() const { return reserved_; }
-  size_t used() const { return used_; }
-
- private:
-  struct Chunk { char* base = nullptr; size_t size = 0; std::vector<Block> free; };
-  size_t chunk_;
-  std::vector<Chunk> chunks_;
-  size_t reserved_ = 0, used_ = 0;
-};
+void* pinned_alloc(size_t n) {
+  void* p = nullptr;
+  TAM_HIP_CHECK(hipHostMalloc(&p, n, hipHostMallocDefault));
+  return p;
+}
+void pinned_free(void* p) { (void)hipHostFree(p); }
+using PinnedPool = tam::PinnedPool<void* (*)(size_t), void (*)(void*)>;
 
 struct Spill {
   char* host = nullptr;
   size_t bytes = 0;
+  hipEvent_t start = nullptr;   // timing events on the side stream (D2H / H2D duration)
   hipEvent_t done = nullptr;
   std::vector<int64_t> shape;
   at::ScalarType dtype;
@@ -103,7 +46,8 @@ struct Spill {
 
 class CkptEngine : public torch::CustomClassHolder {
  public:
-  CkptEngine(int64_t device, int64_t chunk_bytes) : device_((int)device), pool_((size_t)chunk_bytes) {
+  CkptEngine(int64_t device, int64_t chunk_bytes)
+      : device_((int)device), pool_((size_t)chunk_bytes, pinned_alloc, pinned_free) {
     TAM_HIP_CHECK(hipSetDevice(device_));
     int lo = 0, hi = 0;
     TAM_HIP_CHECK(hipDeviceGetStreamPriorityRange(&lo, &hi));
@@ -113,6 +57,7 @@ class CkptEngine : public torch::CustomClassHolder {
   ~CkptEngine() override {
     for (auto& kv : spills_) {
       if (kv.second.done) (void)hipEventDestroy(kv.second.done);
+      if (kv.second.start) (void)hipEventDestroy(kv.second.start);
     }
     (void)hipStreamDestroy(side_);
   }
@@ -132,8 +77,10 @@ class CkptEngine : public torch::CustomClassHolder {
     TAM_HIP_CHECK(hipEventCreateWithFlags(&ready, hipEventDisableTiming));
     TAM_HIP_CHECK(hipEventRecord(ready, prod));
     TAM_HIP_CHECK(hipStreamWaitEvent(side_, ready, 0));
+    TAM_HIP_CHECK(hipEventCreate(&s.start));
+    TAM_HIP_CHECK(hipEventRecord(s.start, side_));
     TAM_HIP_CHECK(hipMemcpyAsync(s.host, src.data_ptr(), s.bytes, hipMemcpyDeviceToHost, side_));
-    TAM_HIP_CHECK(hipEventCreateWithFlags(&s.done, hipEventDisableTiming));
+    TAM_HIP_CHECK(hipEventCreate(&s.done));
     TAM_HIP_CHECK(hipEventRecord(s.done, side_));
     TAM_HIP_CHECK(hipEventDestroy(ready));
     const int64_t h = next_++;
@@ -159,6 +106,7 @@ class CkptEngine : public torch::CustomClassHolder {
     TAM_HIP_CHECK(hipEventRecord(free_ev, cons));
     TAM_HIP_CHECK(hipStreamWaitEvent(side_, free_ev, 0));
     TAM_HIP_CHECK(hipStreamWaitEvent(side_, s.done, 0));
+    TAM_HIP_CHECK(hipEventRecord(s.start, side_));
     TAM_HIP_CHECK(hipMemcpyAsync(dst.data_ptr(), s.host, s.bytes, hipMemcpyHostToDevice, side_));
     TAM_HIP_CHECK(hipEventRecord(s.done, side_));
     TAM_HIP_CHECK(hipStreamWaitEvent(cons, s.done, 0));
@@ -184,6 +132,24 @@ class CkptEngine : public torch::CustomClassHolder {
     TAM_HIP_CHECK(hipEventSynchronize(e));
   }
 
+  // Device time of the last copy of this spill (D2H, or the H2D after a
+  // restore), ms; -1 while it is still in flight. Never blocks.
+  double copy_ms(int64_t h) {
+    std::lock_guard<std::mutex> g(mu_);
+    auto it = spills_.find(h);
+    TORCH_CHECK(it != spills_.end(), "ckpt.copy_ms: unknown handle");
+    if (hipEventQuery(it->second.done) != hipSuccess) return -1.0;
+    float ms = 0.f;
+    TAM_HIP_CHECK(hipEventElapsedTime(&ms, it->second.start, it->second.done));
+    return ms;
+  }
+
+  // The side stream's handle: Python wraps it (torch.cuda.ExternalStream)
+  // to record_stream() a spilled buffer before freeing it, so the caching
+  // allocator defers reusing that HBM until the D2H has drained — the host
+  // never waits for a spill.
+  int64_t stream_handle() { return (int64_t)(uintptr_t)side_; }
+
   // Free the host copy (after restore completes or when the job finished).
   void release(int64_t h) {
     std::lock_guard<std::mutex> g(mu_);
@@ -191,6 +157,7 @@ class CkptEngine : public torch::CustomClassHolder {
     if (it == spills_.end()) return;
     TAM_HIP_CHECK(hipEventSynchronize(it->second.done));
     TAM_HIP_CHECK(hipEventDestroy(it->second.done));
+    TAM_HIP_CHECK(hipEventDestroy(it->second.start));
     pool_.free(it->second.host, it->second.bytes);
     spills_.erase(it);
   }
@@ -231,5 +198,7 @@ TORCH_LIBRARY_FRAGMENT(tam, m) {
       .def("wait", &CkptEngine::wait)
       .def("release", &CkptEngine::release)
       .def("host_view", &CkptEngine::host_view)
+      .def("copy_ms", &CkptEngine::copy_ms)
+      .def("stream_handle", &CkptEngine::stream_handle)
       .def("stats", &CkptEngine::stats);
 }

@@ -319,3 +319,30 @@ def test_delayed_allreduce_is_slow_not_lost(tmp_path):
     ps, s = _run_recover(tmp_path, {"rank": 2, "round": 4, "kind": "delay", "seconds": 3.0})
     assert all(p.exitcode == 0 for p in ps)
     assert s["lost_ranks"] == [] and s["finished"] == s["jobs"]
+
+
+def test_hbm_pressure_spills_only_when_needed(tmp_path):
+    """ckpt policy "pressure": suspended jobs stay resident until a starting
+    job needs the memory; then the least recently run ones spill (and are
+    restored when resumed). A budget large enough for everything spills
+    nothing; job.csv carries the measured bytes."""
+    import csv
+
+    import bench
+    from tiresias_amd.executor import cluster_runtime as cr
+    from tiresias_amd.executor.trainer import Trainer
+
+    one = Trainer("resnet_tiny", "cpu").hbm_bytes()
+    jobs = bench.bench_trace(1, 10, seed=4, work_s=0.4, min_iters=3, tiny=True)
+    for j in jobs:
+        j.model = "resnet_tiny"
+    cfg = bench.make_cfg("dlas-gpu", "count", 1, 4, "pressure", [0.01, 0.05])
+    w = cr.Worker(0, 1, torch.device("cpu"), hbm_budget_gb=2.5 * one / 2 ** 30, pool_cap=0)
+    s = cr.run_replay(cfg, jobs, 0, 1, torch.device("cpu"), worker=w, quantum=0.02, out_dir=str(tmp_path))
+    assert s["finished"] == len(jobs) and s["preemptions"] > 0
+    assert w.pressure_spills > 0 and w.restored_bytes > 0
+    rows = list(csv.DictReader(open(tmp_path / "job.csv")))
+    assert sum(float(r["ckpt_bytes"]) for r in rows) > 0
+    big = cr.Worker(0, 1, torch.device("cpu"), hbm_budget_gb=1000.0, pool_cap=0)
+    s2 = cr.run_replay(cfg, jobs, 0, 1, torch.device("cpu"), worker=big, quantum=0.02)
+    assert s2["finished"] == len(jobs) and big.pressure_spills == 0 and big.spilled_bytes == 0

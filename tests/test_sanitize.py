@@ -17,4 +17,6 @@ def test_sched_core_asan_ubsan(tmp_path):
                        capture_output=True, text=True, env=env, timeout=600)
     assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]
     assert "SANITIZE OK" in r.stdout
+    assert r.stdout.count("POOL OK") == 2                 # ASan+UBSan and TSan runs
+    assert "ThreadSanitizer" not in r.stderr
     assert "runtime error" not in r.stderr and "AddressSanitizer" not in r.stderr

@@ -160,7 +160,7 @@ def test_bench_scenarios_fit_cluster(scenario, n):
     if scenario == "resnet4":
         assert min(qlim) >= 1e6 and len(jobs) == 4
     if scenario == "seq":
-        assert pol == "gittins" and ck == "host"
+        assert pol == "gittins" and ck == "pressure"
 
 
 def test_bench_trace_is_scheduler_bound():

@@ -60,7 +60,8 @@ def define_flags() -> None:
     D.DEFINE_string("engine", "event", "event (discrete-event) | tick (reference-compatible tick loop)")
     D.DEFINE_float("time_unit", 1.0, "seconds per trace time unit")
     D.DEFINE_float("duration_scale", 1.0, "scale applied to trace durations")
-    D.DEFINE_string("ckpt_policy", "none", "none | hbm | host | measured: preemption cost model")
+    D.DEFINE_string("ckpt_policy", "none", "none | hbm | host | measured | pressure: preemption state "
+                    "(pressure: resident in HBM, spilled to pinned host only when a starting job needs the HBM)")
     D.DEFINE_float("ckpt_bw_gbps", 50.0, "spill/restore bandwidth GB/s for ckpt_policy=host")
     D.DEFINE_float("ckpt_hbm_budget_gb", 200.0, "HBM per GPU reserved for suspended jobs")
     D.DEFINE_string("ckpt_table", "profiles/ckpt_mi355x.json",

@@ -11,6 +11,10 @@ Policies:
             xGMI peer copy; over budget it falls back to the host path
   measured  like ``hbm`` but bandwidths from a measured table
             (``profiles/ckpt_*.json``)
+  pressure  the live runtime's policy (``executor/cluster_runtime.Worker``):
+            resident until a starting job needs the HBM, then the least
+            recently run suspended jobs spill asynchronously; modelled like
+            ``hbm`` with the per-GPU budget
 
 Per-GPU state = params x (4 B master + 2 B bf16 shadow + 4/8 B optimizer
 state) of the job's model (each DDP replica holds a full copy).
@@ -59,7 +63,7 @@ class CkptCostModel:
             return 0.0, 0.0
         b = self.state_bytes_per_gpu(job)
         total = b * job.num_gpu
-        if self.policy in ("hbm", "measured") and alloc:
+        if self.policy in ("hbm", "measured", "pressure") and alloc:
             devs = [(nid, d) for nid, ds in alloc.items() for d in ds]
             if all(self.resident.get(k, 0.0) + b <= self.budget for k in devs):
                 for k in devs:

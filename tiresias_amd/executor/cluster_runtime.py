@@ -151,6 +151,12 @@ class Controller:
     def apply_reports(self, reports: List[dict]) -> None:
         per_job: Dict[str, dict] = {}
         for r in reports:
+            for jid, c in ((r or {}).get("ckpt") or {}).items():
+                j = self.sched.jobs.get(jid)
+                if j is not None:
+                    j.ckpt_bytes += c["bytes"]
+                    j.extra["ckpt_save_s"] = j.extra.get("ckpt_save_s", 0.0) + c["save_s"]
+                    j.extra["ckpt_restore_s"] = j.extra.get("ckpt_restore_s", 0.0) + c["restore_s"]
             if r and r.get("dev") and self.log is not None:
                 d = r["dev"]
                 self.log.device_row(self.now(), r["rank"], d.get("util_pct"), d.get("free_mb"),
@@ -408,12 +414,14 @@ class Controller:
         # round at the first step boundary after it (Worker._run_until)
         deadline = self.t0 + nxt if math.isfinite(nxt) else None
         return {"round": self.round, "actions": actions, "assign": assign, "stop": stop, "wait": wait,
-                "deadline": deadline, "alive": [r for r in range(self.world) if r not in self.dead]}
+                "deadline": deadline, "alive": [r for r in range(self.world) if r not in self.dead],
+                "ckpt": getattr(self.cfg, "ckpt_policy", "none")}
 
 
 class Worker:
     def __init__(self, rank: int, world: int, device: torch.device, world_pg=None, use_graph=False,
-                 gang_backend: Optional[str] = None, monitor_period: float = 5.0, pool_cap: int = 2):
+                 gang_backend: Optional[str] = None, monitor_period: float = 5.0, pool_cap: int = 2,
+                 hbm_budget_gb: Optional[float] = None):
         self.gang_backend = gang_backend or ("nccl" if device.type == "cuda" else "gloo")
         # warm pool: finished jobs' trainers, keyed by (model, batch, gang
         # ranks), handed to the next fresh job of the same shape after
@@ -433,6 +441,15 @@ class Worker:
         self.spilled_bytes = 0
         self.restored_bytes = 0
         self._engine = None
+        # HBM-pressure preemption state (ckpt policy "pressure"): suspended
+        # jobs stay resident until a job that is about to start on this rank
+        # needs their HBM; then the least recently run ones spill
+        self.hbm_budget = hbm_budget_gb * 2 ** 30 if hbm_budget_gb else None
+        self._last_run: Dict[str, int] = {}
+        self._round = 0
+        self._need: Dict[str, float] = {}          # model -> measured HBM need of a new job
+        self._ckpt: Dict[str, dict] = {}           # job -> bytes / seconds since the last report
+        self.pressure_spills = 0
         # real-device sampling (HIP mem info + amd-smi) for gpu_live.csv
         self.monitor = None
         self._mon_t = -1e9
@@ -489,7 +506,79 @@ class Worker:
                 t.release()
         self.pool.clear()
 
+    # ------------------------------------------------------------ HBM pressure
+    def _resident_bytes(self) -> float:
+        n = 0.0
+        for t in list(self.trainers.values()) + [t for lst in self.pool.values() for t in lst]:
+            if not getattr(t, "_spilled", None):
+                n += t.hbm_bytes()
+        return n
+
+    def _job_need(self, model: str, batch) -> float:
+        """HBM a new job of ``model`` needs: the measured growth when one was
+        last created here, else 3x its state (weights, optimizer, grads,
+        activations)."""
+        if model in self._need:
+            return self._need[model]
+        from ..profiler.skew import model_profile
+
+        try:
+            st = model_profile(model).state_bytes("adam")
+        except KeyError:
+            st = 1 << 30
+        return 3.0 * st
+
+    def _free_bytes(self) -> float:
+        if self.device.type == "cuda" and self.hbm_budget is None:
+            free, _ = torch.cuda.mem_get_info(self.device)
+            return free + (torch.cuda.memory_reserved(self.device) - torch.cuda.memory_allocated(self.device))
+        budget = self.hbm_budget if self.hbm_budget is not None else float("inf")
+        return budget - self._resident_bytes()
+
+    def _make_room(self, need: float, protect: set) -> None:
+        """Spill least-recently-run suspended jobs of this rank (never one
+        that runs or starts this round) until ``need`` bytes fit, plus a 5 %
+        margin. Spills are asynchronous (Trainer.offload never waits)."""
+        margin = 0.05 * (self.hbm_budget or 0.0)
+        if self._free_bytes() >= need + margin:
+            return
+        victims = sorted((jid for jid, t in self.trainers.items()
+                          if jid not in protect and not getattr(t, "_spilled", None)),
+                         key=lambda j: self._last_run.get(j, -1))
+        for jid in victims:
+            if self._free_bytes() >= need + margin:
+                break
+            self._spill(jid)
+
+    def _spill(self, jid: str) -> None:
+        t = self.trainers[jid]
+        nb = t.offload(self._ckpt_engine())
+        self.spilled_bytes += nb
+        self.pressure_spills += 1
+        c = self._ckpt.setdefault(jid, {"bytes": 0.0, "save_s": 0.0, "restore_s": 0.0})
+        c["bytes"] += nb
+
+    def _restore(self, jid: str) -> None:
+        nb = self.trainers[jid].restore()
+        self.restored_bytes += nb
+        c = self._ckpt.setdefault(jid, {"bytes": 0.0, "save_s": 0.0, "restore_s": 0.0})
+        c["bytes"] += nb
+
     def apply(self, plan: dict) -> None:
+        self._round += 1
+        pressure = plan.get("ckpt") == "pressure"
+        if pressure:
+            # jobs this rank runs or starts this round must stay resident
+            protect = {jid for jid, _ in plan["assign"].get(self.rank) or []}
+            protect |= {a["job"] for a in plan["actions"] if a["op"] == "start"}
+            for a in plan["actions"]:
+                if a["op"] != "start" or self.rank not in a["ranks"]:
+                    continue
+                t = self.trainers.get(a["job"])
+                if t is None:
+                    self._make_room(self._job_need(a["model"], a.get("batch")), protect)
+                elif getattr(t, "_spilled", None):
+                    self._make_room(t.hbm_bytes(), protect)
         p2p_ops = []
         for a in plan["actions"]:
             op = a["op"]
@@ -504,25 +593,30 @@ class Worker:
                 self.streams.pop(a["job"], None)
                 self._retire(self.trainers.pop(a["job"], None))
             elif op == "spill":
-                t = self.trainers.get(a["job"])
-                if t is not None:
-                    self.spilled_bytes += t.offload(self._ckpt_engine())
+                if self.trainers.get(a["job"]) is not None:
+                    self._spill(a["job"])
             elif op == "start":
                 ranks = tuple(a["ranks"])
                 src = a["source"]
                 if src == "fresh":
                     if self.rank in ranks:
+                        before = torch.cuda.memory_allocated(self.device) if self.device.type == "cuda" else 0
                         self.trainers[a["job"]] = self._make_trainer(a)
+                        if self.device.type == "cuda":
+                            grown = torch.cuda.memory_allocated(self.device) - before
+                            if grown > 0:      # a newly built trainer (not a warm-pool reuse)
+                                # activations + graph pool come on top of the state: 2x
+                                self._need[a["model"]] = max(self._need.get(a["model"], 0.0), 2.0 * grown)
                 elif src == "resident":
                     t = self.trainers.get(a["job"])
                     if t is not None and getattr(t, "_spilled", None):
-                        self.restored_bytes += t.restore()
+                        self._restore(a["job"])
                 elif src == "p2p":
                     donors = {int(k): v for k, v in a["donors"].items()}
                     old = tuple(a["old"])
                     if self.rank in old and self.trainers.get(a["job"]) is not None \
                             and getattr(self.trainers[a["job"]], "_spilled", None):
-                        self.restored_bytes += self.trainers[a["job"]].restore()
+                        self._restore(a["job"])
                     if self.rank in donors:        # receiver (state arrives by P2P)
                         t = self._make_trainer(a, init=False)
                         self.trainers[a["job"]] = t
@@ -571,7 +665,10 @@ class Worker:
         slowdown is real, measured time)."""
         jobs = plan["assign"].get(self.rank) or []
         if not jobs:
-            return {"rank": self.rank, "job": None, "jobs": [], "dev": self._dev_sample()}
+            return {"rank": self.rank, "job": None, "jobs": [], "dev": self._dev_sample(),
+                    "ckpt": self._ckpt_report()}
+        for jid, _ in jobs:
+            self._last_run[jid] = self._round
         cuda = self.device.type == "cuda"
         t0 = time.perf_counter()
         err = None
@@ -622,7 +719,23 @@ class Worker:
             if err:
                 rep["error"] = err
             reps.append(rep)
-        return {"rank": self.rank, "job": jobs[0][0], "jobs": reps, "dev": self._dev_sample()}
+        return {"rank": self.rank, "job": jobs[0][0], "jobs": reps, "dev": self._dev_sample(),
+                "ckpt": self._ckpt_report()}
+
+    def _ckpt_report(self) -> Optional[dict]:
+        """Per-job spill / restore bytes and measured device copy seconds since
+        the last report (polls the engine's events: never blocks)."""
+        for jid, t in self.trainers.items():
+            if getattr(t, "_spilled", None) or getattr(t, "_restored", None):
+                got = t.ckpt_poll()
+                if got["save_s"] or got["restore_s"]:
+                    c = self._ckpt.setdefault(jid, {"bytes": 0.0, "save_s": 0.0, "restore_s": 0.0})
+                    c["save_s"] += got["save_s"]
+                    c["restore_s"] += got["restore_s"]
+        if not self._ckpt:
+            return None
+        out, self._ckpt = self._ckpt, {}
+        return out
 
     def _run_until(self, t: Trainer, n: int, deadline: float, cuda: bool) -> int:
         """Up to ``n`` steps of a 1-GPU job, ending the round at the first step

@@ -213,21 +213,31 @@ class Trainer:
 
     def offload(self, engine) -> int:
         """Spill the job's state to pinned host DRAM through the native
-        checkpoint engine (D2H on its low-priority side stream), then release
-        the HBM by shrinking the flat buffers' storages to zero bytes (every
-        parameter view shares those storages, so nothing else changes).
-        The bf16 shadow and the grad buffer are not saved: the shadow is
-        rebuilt from the master on restore, the grad buffer is zero between
-        steps. Returns bytes spilled."""
+        checkpoint engine (D2H on its low-priority side stream, ordered after
+        the work already queued on this stream) and release the HBM by
+        shrinking the flat buffers' storages to zero bytes (every parameter
+        view shares those storages, so nothing else changes). The host NEVER
+        waits for the copy: each spilled buffer is record_stream()-ed on the
+        engine's side stream before it is freed, so the caching allocator
+        reuses that HBM only once the D2H has drained. The bf16 shadow and
+        the grad buffer are not saved (the shadow is rebuilt from the master
+        on restore, the grad buffer is zero between steps). Returns bytes
+        spilled."""
         if getattr(self, "_spilled", None):
             return 0
+        self._release_host_copies()
         self._graph = None
+        self._g_loss = None
+        self.last_loss = None
         handles, nbytes = [], 0
+        self._save_counted = False
         for b in self._spill_buffers():
             handles.append((b, engine.spill(b), b.untyped_storage().nbytes()))
             nbytes += b.numel() * b.element_size()
-        for b, h, _ in handles:
-            engine.wait(h)                       # D2H finished before the HBM is released
+        if self.device.type == "cuda":
+            side = torch.cuda.ExternalStream(engine.stream_handle(), device=self.device)
+            for b, _, _ in handles:
+                b.record_stream(side)
         for b in [self.arena.master, self.arena.shadow, self.arena.grad] + list(self.opt_state):
             b.untyped_storage().resize_(0)
         self._spilled = handles
@@ -251,10 +261,39 @@ class Trainer:
             nbytes += b.numel() * b.element_size()
         A.grad.zero_()
         A.shadow.copy_(A.master.to(torch.bfloat16))
-        for _, h, _ in handles:
-            self._engine.release(h)
+        if hasattr(self._engine, "copy_ms"):
+            self._restored = handles      # host copies released by ckpt_poll once the H2D is done
+        else:
+            for _, h, _ in handles:
+                self._engine.release(h)
         self._spilled = None
+        self._save_counted = False
         return nbytes
+
+    def ckpt_poll(self) -> dict:
+        """Measured device copy seconds of spills / restores completed since
+        the last poll ({"save_s", "restore_s"}); releases the host copies of
+        restores that finished. Never blocks (in-flight copies are picked up
+        by a later poll)."""
+        out = {"save_s": 0.0, "restore_s": 0.0}
+        eng = getattr(self, "_engine", None)
+        if eng is None or not hasattr(eng, "copy_ms"):
+            return out
+        spilled = getattr(self, "_spilled", None) or []
+        if spilled and not getattr(self, "_save_counted", False):
+            ms = [eng.copy_ms(h) for _, h, _ in spilled]
+            if all(m >= 0 for m in ms):
+                out["save_s"] += sum(ms) / 1e3
+                self._save_counted = True
+        restored = getattr(self, "_restored", None) or []
+        if restored:
+            ms = [eng.copy_ms(h) for _, h, _ in restored]
+            if all(m >= 0 for m in ms):
+                out["restore_s"] += sum(ms) / 1e3
+                for _, h, _ in restored:
+                    eng.release(h)
+                self._restored = None
+        return out
 
     def reset(self, seed: int, data_seed: Optional[int] = None, init: bool = True) -> "Trainer":
         """Turn this (finished job's) trainer into a FRESH job of the same
@@ -310,7 +349,15 @@ class Trainer:
         n += sum(v.numel() * v.element_size() for v in self.data.values())
         return n
 
+    def _release_host_copies(self) -> None:
+        eng = getattr(self, "_engine", None)
+        for which in ("_restored", "_spilled"):
+            for _, h, _ in getattr(self, which, None) or []:
+                eng.release(h)
+            setattr(self, which, None)
+
     def release(self) -> None:
+        self._release_host_copies()
         self._graph = None
         self._g_loss = None
         self.last_loss = None                    # may alias the graph's output

@@ -29,7 +29,7 @@ CLUSTER_HEADER = ["delta", "num_idle_nodes", "num_busy_nodes", "num_busy_gpus", 
                   "num_finish_jobs"]
 JOB_HEADER = ["time", "job_id", "num_gpu", "submit_time", "start_time", "end_time", "executed_time",
               "JCT", "duration", "pending_time", "preempt", "resume", "promote", "migration",
-              "queue", "ckpt_overhead", "ckpt_bytes", "model"]
+              "queue", "ckpt_overhead", "ckpt_bytes", "ckpt_save_s", "ckpt_restore_s", "model"]
 
 
 def percentile(xs: List[float], p: float) -> float:
@@ -157,6 +157,9 @@ class MetricsLogger:
                    preempt=j.preempt_count, resume=j.resume_count, promote=j.promote_count,
                    migration=j.migration_count, queue=j.queue,
                    ckpt_overhead=round(j.overhead_time, 6), ckpt_bytes=int(j.ckpt_bytes),
+                   # measured on the live cluster (device copy time of spills / restores)
+                   ckpt_save_s=round(j.extra.get("ckpt_save_s", 0.0), 6),
+                   ckpt_restore_s=round(j.extra.get("ckpt_restore_s", 0.0), 6),
                    model=j.spec.model)
         self.job_rows.append(row)
         if "job" in self._writers:
