@@ -73,6 +73,7 @@ GPU_DIST = [(1, 0.70), (2, 0.12), (4, 0.10), (8, 0.08)]
 # profiles/model_bench_r1_v8.json). Kept constant so the benchmarked work
 # (iterations per job) is identical across rounds: faster kernels then show
 # up as lower JCT, not as a bigger trace.
+SEQ_SCALE = 4
 TRACE_ITER_S = {"resnet50": 0.0112, "vgg16": 0.0076, "transformer": 0.0068, "gnmt": 0.0153}
 HISTORY_SEED_OFFSET = 7919          # the held-out history trace for the service prior
 
@@ -146,12 +147,17 @@ def scenario_trace(name: str, n_gpus: int, seed: int, tiny: bool = False):
             rows.append((m, rng.choice(sizes), round(t, 4), rng.choice((20, 40, 80))))
             t += rng.expovariate(4.0)
     elif name == "seq":
+        # job sizes ~SEQ_SCALE x 12 iterations (0.3-3 s of GPU work): a spill +
+        # restore of a GNMT job costs ~0.1 s of PCIe copies (profiles/r2/
+        # preempt_costs.jsonl), so sub-second jobs would make every preemption
+        # cost as much as the job; arrivals are stretched by the same factor
         t = 0.0
         for i in range(16 * n_gpus):
             m = "transformer" if i % 2 else "gnmt"
             g = rng.choice([g for g in (1, 1, 1, 2, 4) if g <= n_gpus])
-            rows.append((m, g, round(t, 4), int(min(200, max(4, rng.lognormvariate(math.log(12), 1.2))))))
-            t += rng.expovariate(16.0)
+            it = min(200, max(4, rng.lognormvariate(math.log(12), 1.2)))
+            rows.append((m, g, round(t, 4), int(SEQ_SCALE * it)))
+            t += rng.expovariate(16.0 / SEQ_SCALE)
     else:
         raise SystemExit(f"unknown scenario {name}")
     jobs = []
@@ -169,7 +175,7 @@ SCENARIOS = {
     "trace": ("dlas-gpu", "tiresias", "none", "fifo", "yarn", [0.05, 0.25, 1.0], False),
     "resnet4": ("dlas-gpu", "tiresias", "none", "fifo", "yarn", [1e9], False),
     "skew": ("dlas-gpu", "tiresias", "none", "dlas-gpu", "random", [1.0], False),
-    "seq": ("gittins", "tiresias", "pressure", "fifo", "yarn", [0.05, 0.5], False),
+    "seq": ("gittins", "tiresias", "pressure", "fifo", "yarn", [0.2, 2.0], False),
 }
 # measured in-process co-run throughput of every model pair (tools/measure_stream_sharing.py)
 SHARING_TABLE = os.path.join(ROOT, "profiles", "stream_sharing_mi355x.json")
@@ -278,8 +284,11 @@ def main():
         vn = f"2x{n // 2}" if (a.scenario == "skew" and n >= 4) else ""
 
     def make(policy, scheme):
+        # the Gittins quantum scales with the job sizes (a quantum below the
+        # smallest prior job gives every new job index 0: no preemption)
         c = make_cfg(policy, scheme, n, a.seed, a.ckpt, qlim, share, virtual_nodes=vn,
-                     skew_profile=a.skew_profile)
+                     skew_profile=a.skew_profile,
+                     gittins_delta=0.05 * (SEQ_SCALE if a.scenario == "seq" else 1))
         c.nic_gbps = a.nic_gbps
         return c
 
@@ -402,6 +411,8 @@ def main():
             "runtime_breakdown_s": sums[-1].get("runtime_breakdown"),
             "pool_hits": worker.pool_hits,
             "pressure_spills": worker.pressure_spills,
+            "pool_evictions": worker.pool_evictions,
+            "replays": warm_done + steps + (1 if base else 0),
             "spilled_gb": round(worker.spilled_bytes / 2 ** 30, 3),
             "max_hbm_reserved_gb": round(torch.cuda.max_memory_reserved(device) / 2 ** 30, 2) if use_cuda else None,
             "process_wall_s": round(time.perf_counter() - T_PROC0, 1),

@@ -38,8 +38,10 @@ using PinnedPool = tam::PinnedPool<void* (*)(size_t), void (*)(void*)>;
 struct Spill {
   char* host = nullptr;
   size_t bytes = 0;
-  hipEvent_t start = nullptr;   // timing events on the side stream (D2H / H2D duration)
+  hipEvent_t start = nullptr;   // D2H timing events on the side stream
   hipEvent_t done = nullptr;
+  hipEvent_t rstart = nullptr;  // H2D (restore) timing events, created on the first restore
+  hipEvent_t rdone = nullptr;
   std::vector<int64_t> shape;
   at::ScalarType dtype;
 };
@@ -58,6 +60,8 @@ class CkptEngine : public torch::CustomClassHolder {
     for (auto& kv : spills_) {
       if (kv.second.done) (void)hipEventDestroy(kv.second.done);
       if (kv.second.start) (void)hipEventDestroy(kv.second.start);
+      if (kv.second.rstart) (void)hipEventDestroy(kv.second.rstart);
+      if (kv.second.rdone) (void)hipEventDestroy(kv.second.rdone);
     }
     (void)hipStreamDestroy(side_);
   }
@@ -106,10 +110,12 @@ class CkptEngine : public torch::CustomClassHolder {
     TAM_HIP_CHECK(hipEventRecord(free_ev, cons));
     TAM_HIP_CHECK(hipStreamWaitEvent(side_, free_ev, 0));
     TAM_HIP_CHECK(hipStreamWaitEvent(side_, s.done, 0));
-    TAM_HIP_CHECK(hipEventRecord(s.start, side_));
+    if (!s.rstart) TAM_HIP_CHECK(hipEventCreate(&s.rstart));
+    if (!s.rdone) TAM_HIP_CHECK(hipEventCreate(&s.rdone));
+    TAM_HIP_CHECK(hipEventRecord(s.rstart, side_));
     TAM_HIP_CHECK(hipMemcpyAsync(dst.data_ptr(), s.host, s.bytes, hipMemcpyHostToDevice, side_));
-    TAM_HIP_CHECK(hipEventRecord(s.done, side_));
-    TAM_HIP_CHECK(hipStreamWaitEvent(cons, s.done, 0));
+    TAM_HIP_CHECK(hipEventRecord(s.rdone, side_));
+    TAM_HIP_CHECK(hipStreamWaitEvent(cons, s.rdone, 0));
     TAM_HIP_CHECK(hipEventDestroy(free_ev));
     bytes_h2d_ += s.bytes;
   }
@@ -134,13 +140,17 @@ class CkptEngine : public torch::CustomClassHolder {
 
   // Device time of the last copy of this spill (D2H, or the H2D after a
   // restore), ms; -1 while it is still in flight. Never blocks.
-  double copy_ms(int64_t h) {
+  // kind 0: the D2H spill, 1: the latest H2D restore (-2 if never restored)
+  double copy_ms(int64_t h, int64_t kind) {
     std::lock_guard<std::mutex> g(mu_);
     auto it = spills_.find(h);
     TORCH_CHECK(it != spills_.end(), "ckpt.copy_ms: unknown handle");
-    if (hipEventQuery(it->second.done) != hipSuccess) return -1.0;
+    hipEvent_t a = kind ? it->second.rstart : it->second.start;
+    hipEvent_t b = kind ? it->second.rdone : it->second.done;
+    if (!a || !b) return -2.0;
+    if (hipEventQuery(b) != hipSuccess) return -1.0;
     float ms = 0.f;
-    TAM_HIP_CHECK(hipEventElapsedTime(&ms, it->second.start, it->second.done));
+    TAM_HIP_CHECK(hipEventElapsedTime(&ms, a, b));
     return ms;
   }
 
@@ -155,9 +165,11 @@ class CkptEngine : public torch::CustomClassHolder {
     std::lock_guard<std::mutex> g(mu_);
     auto it = spills_.find(h);
     if (it == spills_.end()) return;
-    TAM_HIP_CHECK(hipEventSynchronize(it->second.done));
+    TAM_HIP_CHECK(hipEventSynchronize(it->second.rdone ? it->second.rdone : it->second.done));
     TAM_HIP_CHECK(hipEventDestroy(it->second.done));
     TAM_HIP_CHECK(hipEventDestroy(it->second.start));
+    if (it->second.rstart) TAM_HIP_CHECK(hipEventDestroy(it->second.rstart));
+    if (it->second.rdone) TAM_HIP_CHECK(hipEventDestroy(it->second.rdone));
     pool_.free(it->second.host, it->second.bytes);
     spills_.erase(it);
   }

@@ -693,3 +693,37 @@ def test_ckpt_engine_roundtrip(gpu):
     eng.release(h)
     eng.release(h2)
     assert eng.stats()[1] == 0
+
+
+def test_trainer_async_spill_survives_immediate_reuse(gpu):
+    """Trainer.offload never waits for the D2H: the freed HBM is
+    record_stream()-ed on the engine's side stream, so even when the very
+    next allocations on the compute stream scribble over memory right away,
+    the spilled state restores bit-exact; copy times become known later."""
+    from tiresias_amd.executor.trainer import Trainer
+
+    eng = torch.classes.tam.CkptEngine(0, 64 << 20)
+    t = Trainer("resnet_tiny", gpu, seed=3)
+    for _ in range(3):
+        t.step()
+    torch.cuda.synchronize()
+    master = t.arena.master.clone()
+    mom = t.opt_state[0].clone()
+    nbytes = t.offload(eng)
+    assert nbytes > 0 and t.arena.master.untyped_storage().nbytes() == 0
+    junk = [torch.full((1 << 20,), 7.0, device=gpu) for _ in range(64)]    # reuse the freed blocks now
+    t.restore()
+    del junk
+    torch.cuda.synchronize()
+    assert torch.equal(t.arena.master, master) and torch.equal(t.opt_state[0], mom)
+    got = {"save_s": 0.0, "restore_s": 0.0}
+    for _ in range(100):
+        g = t.ckpt_poll()
+        got = {k: got[k] + g[k] for k in got}
+        if got["restore_s"] > 0:
+            break
+        torch.cuda.synchronize()
+    assert got["save_s"] > 0 and got["restore_s"] > 0
+    t.step()
+    torch.cuda.synchronize()
+    assert eng.stats()[1] == 0          # host copies released after the restore completed

@@ -413,9 +413,18 @@ class Controller:
         # next trace arrival as an absolute host-clock time: 1-GPU jobs end the
         # round at the first step boundary after it (Worker._run_until)
         deadline = self.t0 + nxt if math.isfinite(nxt) else None
-        return {"round": self.round, "actions": actions, "assign": assign, "stop": stop, "wait": wait,
+        plan = {"round": self.round, "actions": actions, "assign": assign, "stop": stop, "wait": wait,
                 "deadline": deadline, "alive": [r for r in range(self.world) if r not in self.dead],
                 "ckpt": getattr(self.cfg, "ckpt_policy", "none")}
+        if plan["ckpt"] == "pressure":
+            # suspended jobs holding state, in the policy's priority order: a
+            # worker under HBM pressure spills from the END (the job the
+            # scheduler will resume last), not merely the least recently run
+            held = [j for j in s.active if j.is_pending and j.job_id in self.holders]
+            if held:
+                rank_of = {j.job_id: i for i, j in enumerate(s.policy.order(list(s.active), s.now))}
+                plan["resume_order"] = sorted((j.job_id for j in held), key=lambda x: rank_of.get(x, 1 << 30))
+        return plan
 
 
 class Worker:
@@ -450,6 +459,7 @@ class Worker:
         self._need: Dict[str, float] = {}          # model -> measured HBM need of a new job
         self._ckpt: Dict[str, dict] = {}           # job -> bytes / seconds since the last report
         self.pressure_spills = 0
+        self.pool_evictions = 0
         # real-device sampling (HIP mem info + amd-smi) for gpu_live.csv
         self.monitor = None
         self._mon_t = -1e9
@@ -515,9 +525,9 @@ class Worker:
         return n
 
     def _job_need(self, model: str, batch) -> float:
-        """HBM a new job of ``model`` needs: the measured growth when one was
-        last created here, else 3x its state (weights, optimizer, grads,
-        activations)."""
+        """HBM a new job of ``model`` needs, in the units the budget counts
+        (Trainer.hbm_bytes: state + batch): the measured growth when one was
+        last created here, else 1.5x its optimizer-inclusive state."""
         if model in self._need:
             return self._need[model]
         from ..profiler.skew import model_profile
@@ -526,7 +536,7 @@ class Worker:
             st = model_profile(model).state_bytes("adam")
         except KeyError:
             st = 1 << 30
-        return 3.0 * st
+        return 1.5 * st
 
     def _free_bytes(self) -> float:
         if self.device.type == "cuda" and self.hbm_budget is None:
@@ -535,16 +545,27 @@ class Worker:
         budget = self.hbm_budget if self.hbm_budget is not None else float("inf")
         return budget - self._resident_bytes()
 
-    def _make_room(self, need: float, protect: set) -> None:
+    def _make_room(self, need: float, protect: set, resume_order=None) -> None:
         """Spill least-recently-run suspended jobs of this rank (never one
         that runs or starts this round) until ``need`` bytes fit, plus a 5 %
         margin. Spills are asynchronous (Trainer.offload never waits)."""
         margin = 0.05 * (self.hbm_budget or 0.0)
         if self._free_bytes() >= need + margin:
             return
+        # idle warm-pool trainers are a cache: they go first, and cost nothing
+        for key in list(self.pool):
+            lst = self.pool[key]
+            while lst and self._free_bytes() < need + margin:
+                lst.pop().release()
+                self.pool_evictions += 1
+            if not lst:
+                del self.pool[key]
+        # victims: lowest scheduler priority first (plan's resume order), then
+        # least recently run
+        order = {jid: i for i, jid in enumerate(resume_order or [])}
         victims = sorted((jid for jid, t in self.trainers.items()
                           if jid not in protect and not getattr(t, "_spilled", None)),
-                         key=lambda j: self._last_run.get(j, -1))
+                         key=lambda j: (-order.get(j, -1), self._last_run.get(j, -1)))
         for jid in victims:
             if self._free_bytes() >= need + margin:
                 break
@@ -571,14 +592,18 @@ class Worker:
             # jobs this rank runs or starts this round must stay resident
             protect = {jid for jid, _ in plan["assign"].get(self.rank) or []}
             protect |= {a["job"] for a in plan["actions"] if a["op"] == "start"}
+            ro = plan.get("resume_order")
             for a in plan["actions"]:
                 if a["op"] != "start" or self.rank not in a["ranks"]:
                     continue
                 t = self.trainers.get(a["job"])
                 if t is None:
-                    self._make_room(self._job_need(a["model"], a.get("batch")), protect)
+                    key = (a["model"], a.get("batch"), tuple(a["ranks"]))
+                    if self.pool.get(key):
+                        continue               # a warm-pool reuse needs no new HBM
+                    self._make_room(self._job_need(a["model"], a.get("batch")), protect, ro)
                 elif getattr(t, "_spilled", None):
-                    self._make_room(t.hbm_bytes(), protect)
+                    self._make_room(t.hbm_bytes(), protect, ro)
         p2p_ops = []
         for a in plan["actions"]:
             op = a["op"]
@@ -605,8 +630,8 @@ class Worker:
                         if self.device.type == "cuda":
                             grown = torch.cuda.memory_allocated(self.device) - before
                             if grown > 0:      # a newly built trainer (not a warm-pool reuse)
-                                # activations + graph pool come on top of the state: 2x
-                                self._need[a["model"]] = max(self._need.get(a["model"], 0.0), 2.0 * grown)
+                                # what _resident_bytes will count for it (state + batch)
+                                self._need[a["model"]] = max(self._need.get(a["model"], 0.0), float(grown))
                 elif src == "resident":
                     t = self.trainers.get(a["job"])
                     if t is not None and getattr(t, "_spilled", None):

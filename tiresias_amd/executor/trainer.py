@@ -267,7 +267,6 @@ class Trainer:
             for _, h, _ in handles:
                 self._engine.release(h)
         self._spilled = None
-        self._save_counted = False
         return nbytes
 
     def ckpt_poll(self) -> dict:
@@ -279,15 +278,16 @@ class Trainer:
         eng = getattr(self, "_engine", None)
         if eng is None or not hasattr(eng, "copy_ms"):
             return out
-        spilled = getattr(self, "_spilled", None) or []
-        if spilled and not getattr(self, "_save_counted", False):
-            ms = [eng.copy_ms(h) for _, h, _ in spilled]
-            if all(m >= 0 for m in ms):
-                out["save_s"] += sum(ms) / 1e3
-                self._save_counted = True
+        for which in ("_spilled", "_restored"):
+            hs = getattr(self, which, None) or []
+            if hs and not getattr(self, "_save_counted", False):
+                ms = [eng.copy_ms(h, 0) for _, h, _ in hs]
+                if all(m >= 0 for m in ms):
+                    out["save_s"] += sum(ms) / 1e3
+                    self._save_counted = True
         restored = getattr(self, "_restored", None) or []
-        if restored:
-            ms = [eng.copy_ms(h) for _, h, _ in restored]
+        if restored and getattr(self, "_save_counted", False):
+            ms = [eng.copy_ms(h, 1) for _, h, _ in restored]
             if all(m >= 0 for m in ms):
                 out["restore_s"] += sum(ms) / 1e3
                 for _, h, _ in restored:
