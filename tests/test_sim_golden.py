@@ -155,3 +155,28 @@ def test_outputs_written(tmp_path):
     s = json.load(open(tmp_path / "summary.json"))
     assert s["finished"] == 2 and s["avg_jct"] > 0
     assert (tmp_path / "decisions.jsonl").read_text().count('"finish"') == 2
+
+
+def test_tick_engine_live_fifo_hand_derived():
+    """The live reference's tick loop (core/scheduling/schedule.py:178-212),
+    derived by reading it: at tick d arrivals with submit <= d are queued, at
+    most ONE job is placed (FIFO head only, schedule_fifo: head-of-line
+    blocking), then d += 1, every running job's processed time += 1
+    (jobs_manager.py:143-147, job.py:53-56) and jobs with processed >=
+    duration are released at tick d (jobs_manager.py:240-246). So a job placed
+    at tick s ends at s + ceil(duration). Trace on one 4-GPU node:
+      A t=0 2 GPU dur 2.5 -> placed 0, ends 3
+      B t=0 1 GPU dur 3   -> placed 1 (one placement per tick), ends 4
+      C t=0 4 GPU dur 1   -> blocked at 2, 3 (3 free after A), placed 4, ends 5
+      D t=1 1 GPU dur 1   -> behind C (FIFO), placed 5, ends 6
+    (Parity with an execution of the reference is unpinned: the reference ships
+    no trace fixture and is not run here.)"""
+    from tiresias_amd.engine.sim import TickSimulator
+
+    c = SimConfig(schedule="fifo", scheme="yarn", engine="tick",
+                  cluster=ClusterSpec(num_switch=1, num_node_p_switch=1, num_gpu_p_node=4))
+    specs = [J("A", 0.0, 2, 2.5), J("B", 0.0, 1, 3.0), J("C", 0.0, 4, 1.0), J("D", 1.0, 1, 1.0)]
+    sim = TickSimulator(c, specs)
+    sim.run()
+    got = {j.job_id: (j.start_time, j.end_time) for j in sim.jobs.values()}
+    assert got == {"A": (0.0, 3.0), "B": (1.0, 4.0), "C": (4.0, 5.0), "D": (5.0, 6.0)}
