@@ -574,6 +574,50 @@ void lstm_step_fwd_op(const Tensor& gx, const Tensor& w_hh, const optional<Tenso
                          act.data_ptr<float>(), (int)B, (int)Hd, cur_stream(gx));
 }
 
+// persistent whole-sequence recurrence; returns false when the shape or
+// co-residency is not supported (caller runs the per-step path).
+// sync: int32 [32 * (B/16 + 1)] = {error flag, per-batch-tile counters on
+// lines of their own (zeroed by the launcher)}
+static void check_sync(const Tensor& sync, int64_t B) {
+  TORCH_CHECK(sync.is_cuda() && sync.scalar_type() == at::kInt && sync.is_contiguous() &&
+              sync.numel() >= 32 * (B / 16 + 1),
+              "tam.lstm_seq: sync must be a contiguous int32 tensor of >= 32 * (B/16 + 1) elements");
+}
+bool lstm_seq_fwd_op(const Tensor& gx, const Tensor& w_hh, const Tensor& hs, const Tensor& cs,
+                     const Tensor& act, bool reverse, const Tensor& sync) {
+  check_f32(gx, "gx"); check_bf16(w_hh, "w_hh"); check_bf16(hs, "hs"); check_f32(cs, "cs");
+  check_f32(act, "act");
+  TORCH_CHECK(hs.dim() == 3 && hs.is_contiguous(), "tam.lstm_seq_forward: hs [T][B][Hd]");
+  const int64_t T = hs.size(0), B = hs.size(1), Hd = hs.size(2);
+  check_sync(sync, B);
+  TORCH_CHECK(w_hh.is_contiguous() && w_hh.size(0) == 4 * Hd && w_hh.size(1) == Hd,
+              "tam.lstm_seq_forward: w_hh [4Hd][Hd]");
+  TORCH_CHECK(gx.is_contiguous() && gx.numel() == T * B * 4 * Hd, "tam.lstm_seq_forward: gx [T][B][4Hd]");
+  TORCH_CHECK(cs.is_contiguous() && cs.numel() == T * B * Hd && act.is_contiguous() &&
+              act.numel() == T * B * 5 * Hd, "tam.lstm_seq_forward: cs / act shapes");
+  int* sp = sync.data_ptr<int>();
+  return tam::lstm_seq_forward(gx.data_ptr<float>(), bp(w_hh), bpm(hs), cs.data_ptr<float>(),
+                               act.data_ptr<float>(), (int)T, (int)B, (int)Hd, reverse ? 1 : 0,
+                               (unsigned*)sp, cur_stream(gx));
+}
+bool lstm_seq_bwd_op(const Tensor& act, const Tensor& cs, const Tensor& dH, const Tensor& w_hh,
+                     const Tensor& dG, bool reverse, const Tensor& sync) {
+  check_f32(act, "act"); check_f32(cs, "cs"); check_f32(dH, "dH"); check_bf16(w_hh, "w_hh");
+  check_bf16(dG, "dG");
+  TORCH_CHECK(cs.dim() == 3 && cs.is_contiguous(), "tam.lstm_seq_backward: cs [T][B][Hd]");
+  const int64_t T = cs.size(0), B = cs.size(1), Hd = cs.size(2);
+  check_sync(sync, B);
+  TORCH_CHECK(w_hh.is_contiguous() && w_hh.size(0) == 4 * Hd && w_hh.size(1) == Hd,
+              "tam.lstm_seq_backward: w_hh [4Hd][Hd]");
+  TORCH_CHECK(act.is_contiguous() && act.numel() == T * B * 5 * Hd && dH.is_contiguous() &&
+              dH.numel() == T * B * Hd && dG.is_contiguous() && dG.numel() == T * B * 4 * Hd,
+              "tam.lstm_seq_backward: act / dH / dG shapes");
+  int* sp = sync.data_ptr<int>();
+  return tam::lstm_seq_backward(act.data_ptr<float>(), cs.data_ptr<float>(), dH.data_ptr<float>(), bp(w_hh),
+                                bpm(dG), (int)T, (int)B, (int)Hd, reverse ? 1 : 0, (unsigned*)sp,
+                                cur_stream(act));
+}
+
 void lstm_bwd_op(const Tensor& act, const optional<Tensor>& c_prev, const optional<Tensor>& dh,
                  const optional<Tensor>& dc_next, const optional<Tensor>& dgates,
                  const optional<Tensor>& dc_prev, const optional<Tensor>& dgates_bf16) {
@@ -618,6 +662,8 @@ TORCH_LIBRARY(tam, m) {
   m.def("attn_forward(Tensor q, Tensor k, Tensor v, Tensor(a!) o, Tensor(b!) lse, bool causal, float scale, Tensor? kv_len) -> ()", &attn_forward_op);
   m.def("attn_backward(Tensor q, Tensor k, Tensor v, Tensor o, Tensor dout, Tensor lse, Tensor(a!) dq, Tensor(b!) dk, Tensor(c!) dv, Tensor(d!) dq_acc, Tensor(e!) delta, bool causal, float scale, Tensor? kv_len) -> ()", &attn_backward_op);
   m.def("lstm_step_forward(Tensor gx, Tensor w_hh, Tensor? h_prev, Tensor? c_prev, Tensor(a!) c_out, Tensor(b!) h_out, Tensor(c!) act) -> ()", &lstm_step_fwd_op);
+  m.def("lstm_seq_forward(Tensor gx, Tensor w_hh, Tensor(a!) hs, Tensor(b!) cs, Tensor(c!) act, bool reverse, Tensor(d!) sync) -> bool", &lstm_seq_fwd_op);
+  m.def("lstm_seq_backward(Tensor act, Tensor cs, Tensor dH, Tensor w_hh, Tensor(a!) dG, bool reverse, Tensor(b!) sync) -> bool", &lstm_seq_bwd_op);
   m.def("lstm_cell_forward(Tensor gates, Tensor? c_prev, Tensor(a!) c_out, Tensor(b!) h_out, Tensor(c!)? h_f32, Tensor(d!) act) -> ()", &lstm_fwd_op);
   m.def("lstm_cell_backward(Tensor act, Tensor? c_prev, Tensor? dh, Tensor? dc_next, Tensor(a!)? dgates, Tensor(b!)? dc_prev, Tensor(c!)? dgates_bf16) -> ()", &lstm_bwd_op);
 }

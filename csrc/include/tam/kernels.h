@@ -83,6 +83,13 @@ void lstm_cell_forward(const float* gates, const float* c_prev, float* c_out, bf
 // fused forward timestep (B % 16 == 0, Hd % 256 == 0): h_out/c_out/act for one t
 void lstm_step_forward(const float* gx, const bf16_t* w_hh, const bf16_t* h_prev, const float* c_prev,
                        float* c_out, bf16_t* h_out, float* act, int B, int Hd, hipStream_t s);
+// persistent whole-sequence recurrence (lstm.hip); false = shape / residency
+// not supported (the caller runs the per-step path). sync: int32 words,
+// [0] error flag, [32 * (bt + 1)] per-batch-tile counters (zeroed here).
+bool lstm_seq_forward(const float* gx, const bf16_t* w_hh, bf16_t* hs, float* cs, float* act, int T,
+                      int B, int Hd, int reverse, unsigned* sync, hipStream_t s);
+bool lstm_seq_backward(const float* act, const float* cs, const float* dH, const bf16_t* w_hh, bf16_t* dG,
+                       int T, int B, int Hd, int reverse, unsigned* sync, hipStream_t s);
 void lstm_cell_backward(const float* act_cache, const float* c_prev, const float* c_out,
                         const float* dh, const float* dc_next, float* dgates, float* dc_prev,
                         bf16_t* dgates_bf16, int B, int Hd, hipStream_t s);

@@ -159,6 +159,303 @@ void lstm_step_forward(const float* gx, const bf16_t* w_hh, const bf16_t* h_prev
                        h_out, act, B, Hd, MT);
 }
 
+// ---------------------------------------------------------------------------
+// Persistent LSTM recurrence: ONE launch per layer-direction per sequence
+// (forward and backward), instead of {recurrent GEMM, cell kernel} per
+// timestep.
+//
+// Workgroup (batch tile of 16 rows, unit tile of 16 hidden units) owns the 64
+// gate rows {i,f,g,o} x 16 units, so the cell update is local. B/16 x Hd/16
+// workgroups (256 for GNMT's B = 64, H = 1024): one per CU. Each of the 8
+// waves keeps its K-slice of those W_hh rows in VGPRs for the whole sequence
+// (forward: Hd/8 of K, 64 VGPRs at H = 1024) and reads only its 16-row slice
+// of h_{t-1} (the batch tile) each step; the cell state stays in a register.
+//
+// Step hand-off (only workgroups of the SAME batch tile depend on each other,
+// so each batch tile has its own arrival counter on a line of its own): the
+// tile's new h (forward) / dG (backward) is staged in LDS, written by ONE wave
+// as 8-B write-through (sc1) stores, drained (vmcnt 0), then one lane adds to
+// the counter (agent atomic). Consumers: one lane polls the counter with
+// relaxed sc1 loads + s_sleep, the workgroup joins at a barrier, and EVERY
+// load of handed-off bytes is a 16-B sc1 buffer load -- no release / acquire fence
+// (guide: Guideline 16 / microarch visibility table, row 1). The spin is
+// bounded: a stuck barrier sets the error word and drains instead of hanging.
+// Co-residency is checked on the host: the launcher refuses (returns false)
+// unless TWO such grids fit at once (two GNMT jobs sharing a GPU).
+// ---------------------------------------------------------------------------
+constexpr int PL_W = 8;          // waves per workgroup
+constexpr unsigned PL_SPIN = 1u << 22;
+typedef __attribute__((address_space(1))) unsigned pl_gu32;
+typedef __attribute__((address_space(1))) unsigned long long pl_gu64;
+#define PL_RLX __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT
+
+// sync layout (int32 words): [0] error flag, [32 * (bt + 1)] arrival counter of batch tile bt
+__device__ __forceinline__ void pl_signal(unsigned* sync, int bt) {
+  // caller: the ONE storing wave, after its sc1 stores
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  if ((threadIdx.x & 63) == 0) __hip_atomic_fetch_add((pl_gu32*)(sync + 32 * (bt + 1)), 1u, PL_RLX);
+}
+
+__device__ __forceinline__ void pl_wait(unsigned* sync, int bt, unsigned target) {
+  if (threadIdx.x == 0) {
+    unsigned polls = 0;
+    while (__hip_atomic_load((pl_gu32*)(sync + 32 * (bt + 1)), PL_RLX) < target) {
+      __builtin_amdgcn_s_sleep(1);
+      if (++polls > PL_SPIN) {
+        __hip_atomic_fetch_or((pl_gu32*)sync, 1u, PL_RLX);
+        break;
+      }
+    }
+  }
+  __syncthreads();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");   // no instruction: keeps loads below
+}
+
+// 16 B of handed-off bf16: one buffer_load_dwordx4 with sc1 (aux 16) through
+// a descriptor built from wave-uniform kernel arguments
+typedef unsigned int pl_u32x4 __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t pl_rsrc(const void* base, long bytes) {
+  return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(base), (short)0, (int)bytes, 0x00020000);
+}
+__device__ __forceinline__ s16x8_t pl_ld16(__amdgpu_buffer_rsrc_t r, unsigned byte_off) {
+  const pl_u32x4 v = __builtin_amdgcn_raw_buffer_load_b128(r, byte_off, 0, 16);
+  return __builtin_bit_cast(s16x8_t, v);
+}
+
+template <int KW>   // k-steps of 32 per wave: Hd / (32 * PL_W)
+__global__ void __launch_bounds__(64 * PL_W, 4) lstm_persist_fwd_kernel(
+    const float* __restrict__ gx, const bf16_t* __restrict__ w, bf16_t* hs, float* __restrict__ cs,
+    float* __restrict__ act, int T, int B, int Hd, int reverse, unsigned* sync) {
+  __shared__ float red[PL_W][16][65];
+  __shared__ __attribute__((aligned(16))) bf16_t hbuf[16][16];
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  const int nbt = B / 16;
+  const int bt = blockIdx.x % nbt, ut = blockIdx.x / nbt;
+  const int b0 = bt * 16, j0 = ut * 16;
+  const int kb = wv * KW * 32 + 8 * (lane >> 4);
+  // W_hh rows of this tile, this wave's K-slice, as MFMA B fragments
+  s16x8_t wf[4][KW];
+#pragma unroll
+  for (int g = 0; g < 4; ++g)
+#pragma unroll
+    for (int ks = 0; ks < KW; ++ks)
+      wf[g][ks] = *(const s16x8_t*)(w + (long)(g * Hd + j0 + (lane & 15)) * Hd + kb + 32 * ks);
+  const __amdgpu_buffer_rsrc_t hrs = pl_rsrc(hs, (long)T * B * Hd * 2);
+  const bool cell = threadIdx.x < 256;
+  const int cr = threadIdx.x >> 4, cu = threadIdx.x & 15;
+  float c_reg = 0.f;
+  for (int s = 0; s < T; ++s) {
+    const int t = reverse ? T - 1 - s : s;
+    float gxv[4] = {0.f, 0.f, 0.f, 0.f};
+    if (cell) {
+      const float* g = gx + ((long)t * B + b0 + cr) * 4 * Hd + j0 + cu;
+#pragma unroll
+      for (int q = 0; q < 4; ++q) gxv[q] = g[(long)q * Hd];
+    }
+    f32x4_t acc[4];
+#pragma unroll
+    for (int g = 0; g < 4; ++g) acc[g] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+    if (s > 0) {
+      const int tp = reverse ? t + 1 : t - 1;
+      const unsigned hoff = (unsigned)((((long)tp * B + b0 + (lane & 15)) * Hd + kb) * 2);
+      s16x8_t ha[KW];
+#pragma unroll
+      for (int ks = 0; ks < KW; ++ks) ha[ks] = pl_ld16(hrs, hoff + 64 * ks);
+#pragma unroll
+      for (int ks = 0; ks < KW; ++ks)
+#pragma unroll
+        for (int g = 0; g < 4; ++g)
+          acc[g] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8_t, ha[ks]),
+                                                           __builtin_bit_cast(bf16x8_t, wf[g][ks]),
+                                                           acc[g], 0, 0, 0);
+    }
+    // C/D map: col = lane & 15 (unit), row = 4*(lane>>4) + r (batch)
+#pragma unroll
+    for (int g = 0; g < 4; ++g)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) red[wv][4 * (lane >> 4) + r][g * 16 + (lane & 15)] = acc[g][r];
+    __syncthreads();
+    if (cell) {
+      float gs[4];
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        float v = gxv[q];
+#pragma unroll
+        for (int k = 0; k < PL_W; ++k) v += red[k][cr][q * 16 + cu];
+        gs[q] = v;
+      }
+      const float i_ = sigmoidf_(gs[0]), f_ = sigmoidf_(gs[1]), g_ = tanhf_(gs[2]), o_ = sigmoidf_(gs[3]);
+      const float cn = f_ * c_reg + i_ * g_;
+      const float tc = tanhf_(cn);
+      const long row = (long)t * B + b0 + cr;
+      const int j = j0 + cu;
+      cs[row * Hd + j] = cn;
+      hbuf[cr][cu] = f2bf(o_ * tc);
+      float* a = act + row * 5 * Hd;
+      a[j] = i_; a[Hd + j] = f_; a[2 * Hd + j] = g_; a[3 * Hd + j] = o_; a[4 * Hd + j] = tc;
+      c_reg = cn;
+    }
+    __syncthreads();
+    if (wv == 0) {
+      // 16 rows x 16 units of h_t: 64 lanes x 8 B, write-through
+      const int r = lane >> 2, q = lane & 3;
+      const unsigned long long v = *(const unsigned long long*)&hbuf[r][4 * q];
+      __hip_atomic_store((pl_gu64*)(hs + ((long)t * B + b0 + r) * Hd + j0 + 4 * q), v, PL_RLX);
+      if (s + 1 < T) pl_signal(sync, bt);
+    }
+    if (s + 1 < T) pl_wait(sync, bt, (unsigned)(s + 1) * (unsigned)(Hd / 16));
+  }
+}
+
+// Backward: dh_t = dH_t + dG_{t+1} W_hh[:, units] (t+1 = the step processed
+// after t in the forward order), then the cell backward; dG_t (bf16) is both
+// the next step's operand and the weight-gradient GEMMs' input. Each wave
+// keeps its K-slice (4Hd/8) of W_hh's 16 unit columns in VGPRs.
+template <int KW>   // k-steps of 32 per wave: 4 Hd / (32 * PL_W)
+__global__ void __launch_bounds__(64 * PL_W, 4) lstm_persist_bwd_kernel(
+    const float* __restrict__ act, const float* __restrict__ cs, const float* __restrict__ dH,
+    const bf16_t* __restrict__ w, bf16_t* dG, int T, int B, int Hd, int reverse, unsigned* sync) {
+  __shared__ float red[PL_W][16][17];
+  __shared__ __attribute__((aligned(16))) bf16_t gbuf[16][64];
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  const int nbt = B / 16;
+  const int bt = blockIdx.x % nbt, ut = blockIdx.x / nbt;
+  const int b0 = bt * 16, j0 = ut * 16;
+  const int kb = wv * KW * 32 + 8 * (lane >> 4);
+  // B fragment (k, n) = W_hh[k][j0 + n]: 8 consecutive k of one column (strided gather, once)
+  s16x8_t wf[KW];
+#pragma unroll
+  for (int ks = 0; ks < KW; ++ks) {
+    const bf16_t* col = w + (long)(kb + 32 * ks) * Hd + j0 + (lane & 15);
+#pragma unroll
+    for (int e = 0; e < 8; ++e) wf[ks][e] = (short)col[(long)e * Hd];
+  }
+  const __amdgpu_buffer_rsrc_t grs = pl_rsrc(dG, (long)T * B * 4 * Hd * 2);
+  const bool cell = threadIdx.x < 256;
+  const int cr = threadIdx.x >> 4, cu = threadIdx.x & 15;
+  float dc_reg = 0.f;
+  for (int s = 0; s < T; ++s) {
+    const int t = reverse ? s : T - 1 - s;             // backward order
+    const int fwd_idx = reverse ? T - 1 - t : t;       // position of t in the forward order
+    const long row = (long)t * B + b0 + cr;
+    const int j = j0 + cu;
+    float dhv = 0.f, av[5] = {0.f, 0.f, 0.f, 0.f, 0.f}, cpv = 0.f;
+    if (cell) {
+      dhv = dH[row * Hd + j];
+      const float* a = act + row * 5 * Hd + j;
+#pragma unroll
+      for (int q = 0; q < 5; ++q) av[q] = a[(long)q * Hd];
+      if (fwd_idx > 0) {
+        const int tp = reverse ? t + 1 : t - 1;
+        cpv = cs[((long)tp * B + b0 + cr) * Hd + j];
+      }
+    }
+    f32x4_t acc = {0.f, 0.f, 0.f, 0.f};
+    if (s > 0) {
+      const int tn = reverse ? t - 1 : t + 1;
+      const unsigned goff = (unsigned)((((long)tn * B + b0 + (lane & 15)) * 4 * Hd + kb) * 2);
+#pragma unroll
+      for (int h = 0; h < KW; h += 4) {
+        s16x8_t ga[4];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) ga[u] = pl_ld16(grs, goff + 64 * (h + u));
+#pragma unroll
+        for (int u = 0; u < 4; ++u)
+          acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8_t, ga[u]),
+                                                        __builtin_bit_cast(bf16x8_t, wf[h + u]), acc, 0,
+                                                        0, 0);
+      }
+    }
+#pragma unroll
+    for (int r = 0; r < 4; ++r) red[wv][4 * (lane >> 4) + r][lane & 15] = acc[r];
+    __syncthreads();
+    if (cell) {
+      float dh = dhv;
+#pragma unroll
+      for (int k = 0; k < PL_W; ++k) dh += red[k][cr][cu];
+      const float i_ = av[0], f_ = av[1], g_ = av[2], o_ = av[3], tc = av[4];
+      const float dc = dh * o_ * (1.f - tc * tc) + dc_reg;
+      gbuf[cr][cu] = f2bf(dc * g_ * i_ * (1.f - i_));
+      gbuf[cr][16 + cu] = f2bf(dc * cpv * f_ * (1.f - f_));
+      gbuf[cr][32 + cu] = f2bf(dc * i_ * (1.f - g_ * g_));
+      gbuf[cr][48 + cu] = f2bf(dh * tc * o_ * (1.f - o_));
+      dc_reg = dc * f_;
+    }
+    __syncthreads();
+    if (wv == 0) {
+      // 16 rows x 4 gates x 16 units of dG_t: 4 x (64 lanes x 8 B), write-through
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        const int idx = u * 64 + lane, r = idx >> 4, g = (idx >> 2) & 3, q = idx & 3;
+        const unsigned long long v = *(const unsigned long long*)&gbuf[r][16 * g + 4 * q];
+        __hip_atomic_store((pl_gu64*)(dG + ((long)t * B + b0 + r) * 4 * Hd + g * Hd + j0 + 4 * q), v,
+                           PL_RLX);
+      }
+      if (s + 1 < T) pl_signal(sync, bt);
+    }
+    if (s + 1 < T) pl_wait(sync, bt, (unsigned)(s + 1) * (unsigned)(Hd / 16));
+  }
+}
+
+template <typename K>
+static bool pl_fits(K kern, int grid) {
+  // TWO grids must be co-resident (GPU sharing can put two GNMT jobs on one
+  // device); the query is cached per kernel
+  static int cap = -1;
+  if (cap < 0) {
+    int per_cu = 0, dev = 0, cus = 0;
+    if (hipGetDevice(&dev) != hipSuccess ||
+        hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess ||
+        hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kern, 64 * PL_W, 0) != hipSuccess)
+      cap = 0;
+    else
+      cap = per_cu * cus;
+  }
+  return 2 * grid <= cap;
+}
+
+bool lstm_seq_forward(const float* gx, const bf16_t* w_hh, bf16_t* hs, float* cs, float* act, int T,
+                      int B, int Hd, int reverse, unsigned* sync, hipStream_t s) {
+  if (T < 1 || B % 16 != 0 || Hd % 256 != 0 || 8 % (B / 16) != 0) return false;
+  const int grid = (B / 16) * (Hd / 16);
+  const int kw = Hd / (32 * PL_W);
+#define PL_FWD(KWV)                                                                        \
+  case KWV:                                                                                \
+    if (!pl_fits(lstm_persist_fwd_kernel<KWV>, grid)) return false;                       \
+    zero_async(sync + 32, (size_t)(B / 16) * 128, s);                                     \
+    hipLaunchKernelGGL(lstm_persist_fwd_kernel<KWV>, dim3(grid), dim3(64 * PL_W), 0, s, gx, w_hh, hs, \
+                       cs, act, T, B, Hd, reverse, sync);                                  \
+    return true;
+  switch (kw) {
+    PL_FWD(1)
+    PL_FWD(2)
+    PL_FWD(4)
+    default: return false;
+  }
+#undef PL_FWD
+}
+
+bool lstm_seq_backward(const float* act, const float* cs, const float* dH, const bf16_t* w_hh, bf16_t* dG,
+                       int T, int B, int Hd, int reverse, unsigned* sync, hipStream_t s) {
+  if (T < 1 || B % 16 != 0 || Hd % 256 != 0 || 8 % (B / 16) != 0) return false;
+  const int grid = (B / 16) * (Hd / 16);
+  const int kw = 4 * Hd / (32 * PL_W);
+#define PL_BWD(KWV)                                                                        \
+  case KWV:                                                                                \
+    if (!pl_fits(lstm_persist_bwd_kernel<KWV>, grid)) return false;                       \
+    zero_async(sync + 32, (size_t)(B / 16) * 128, s);                                     \
+    hipLaunchKernelGGL(lstm_persist_bwd_kernel<KWV>, dim3(grid), dim3(64 * PL_W), 0, s, act, cs, dH, \
+                       w_hh, dG, T, B, Hd, reverse, sync);                                 \
+    return true;
+  switch (kw) {
+    PL_BWD(4)
+    PL_BWD(8)
+    PL_BWD(16)
+    default: return false;
+  }
+#undef PL_BWD
+}
+
 static int lgrid(long n) { long b = (n + 255) / 256; if (b > 2048) b = 2048; return (int)(b < 1 ? 1 : b); }
 
 void lstm_cell_forward(const float* gates, const float* c_prev, float* c_out, bf16_t* h_out,

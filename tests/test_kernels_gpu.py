@@ -676,6 +676,97 @@ def test_lstm_step_fused(gpu, B, Hd, first):
     assert rel_err(act, a_ref) < 1e-4
 
 
+def _lstm_seq_ref(gx, w, reverse):
+    """fp32 recurrence with the kernel's bf16 rounding of h between steps."""
+    T_, B, G4 = gx.shape
+    Hd = G4 // 4
+    wf = w.float()
+    hs = torch.empty(T_, B, Hd, device=gx.device, dtype=BF)
+    cs = torch.empty(T_, B, Hd, device=gx.device)
+    act = torch.empty(T_, B, 5 * Hd, device=gx.device)
+    h = c = None
+    for t in (range(T_ - 1, -1, -1) if reverse else range(T_)):
+        g = gx[t] + (h.float() @ wf.t() if h is not None else 0.0)
+        i, f, gg, o = g.chunk(4, 1)
+        i, f, gg, o = torch.sigmoid(i), torch.sigmoid(f), torch.tanh(gg), torch.sigmoid(o)
+        c = f * (c if c is not None else 0.0) + i * gg
+        tc = torch.tanh(c)
+        h = (o * tc).to(BF)
+        hs[t], cs[t], act[t] = h, c, torch.cat([i, f, gg, o, tc], 1)
+    return hs, cs, act
+
+
+def _lstm_seq_bwd_ref(act, cs, dH, w, reverse):
+    """fp32 cell backward + recurrent dh with dG rounded to bf16 between steps."""
+    T_, B, Hd = cs.shape
+    wf = w.float()
+    dG = torch.empty(T_, B, 4 * Hd, device=cs.device, dtype=BF)
+    order = list(range(T_ - 1, -1, -1) if reverse else range(T_))
+    dc = torch.zeros(B, Hd, device=cs.device)
+    nxt = None
+    for k, t in enumerate(order[::-1]):
+        prev = order[::-1][k + 1] if k + 1 < T_ else None
+        i, f, gg, o, tc = act[t].chunk(5, 1)
+        dh = dH[t] + (nxt.float() @ wf if nxt is not None else 0.0)
+        dcc = dh * o * (1 - tc * tc) + dc
+        cp = cs[prev] if prev is not None else torch.zeros_like(dc)
+        g4 = torch.cat([dcc * gg * i * (1 - i), dcc * cp * f * (1 - f), dcc * i * (1 - gg * gg),
+                        dh * tc * o * (1 - o)], 1)
+        dG[t] = g4.to(BF)
+        nxt = dG[t]
+        dc = dcc * f
+    return dG
+
+
+@pytest.mark.parametrize("T_,B,Hd,reverse", [(12, 64, 1024, False), (12, 64, 1024, True),
+                                              (7, 32, 512, False), (5, 128, 256, True)])
+def test_lstm_persistent_sequence(gpu, T_, B, Hd, reverse):
+    """Persistent whole-sequence recurrence (one launch, grid barrier per
+    timestep) vs an fp32 torch recurrence: forward h/c/activations and the
+    backward gate gradients."""
+    torch.manual_seed(21)
+    gx = torch.randn(T_, B, 4 * Hd, device=gpu)
+    w = (torch.randn(4 * Hd, Hd, device=gpu) / Hd ** 0.5).to(BF)
+    hs = torch.empty(T_, B, Hd, device=gpu, dtype=BF)
+    cs = torch.empty(T_, B, Hd, device=gpu)
+    act = torch.empty(T_, B, 5 * Hd, device=gpu)
+    sync = torch.zeros(32 * (B // 16 + 1), dtype=torch.int32, device=gpu)
+    assert T().lstm_seq_forward(gx, w, hs, cs, act, reverse, sync)
+    torch.cuda.synchronize()
+    assert int(sync[0]) == 0, "grid barrier timed out"
+    h_ref, c_ref, a_ref = _lstm_seq_ref(gx, w, reverse)
+    assert rel_err(cs, c_ref) < 2e-3 and rel_err(hs, h_ref) < 1e-2 and rel_err(act, a_ref) < 2e-3
+    dH = torch.randn(T_, B, Hd, device=gpu)
+    dG = torch.empty(T_, B, 4 * Hd, device=gpu, dtype=BF)
+    sync.zero_()
+    assert T().lstm_seq_backward(act, cs, dH, w, dG, reverse, sync)
+    torch.cuda.synchronize()
+    assert int(sync[0]) == 0, "grid barrier timed out"
+    assert rel_err(dG, _lstm_seq_bwd_ref(act, cs, dH, w, reverse)) < 1e-2
+
+
+def test_gnmt_persistent_matches_per_step(gpu):
+    """The GNMT layer with the persistent kernels vs the per-step path:
+    same loss and gradients (up to summation order)."""
+    from tiresias_amd.models import gnmt as G
+    from tiresias_amd.executor.trainer import Trainer
+
+    grads = []
+    for persist in (True, False):
+        G.PERSIST = persist
+        try:
+            t = Trainer("gnmt", gpu, seed=3, batch=64)
+            loss = t._fwd_bwd()
+            torch.cuda.synchronize()
+            grads.append((float(loss), t.arena.grad.clone()))
+        finally:
+            G.PERSIST = True
+    assert G.persist_errors() == 0
+    (l1, g1), (l2, g2) = grads
+    assert abs(l1 - l2) < 1e-3 * abs(l2)
+    assert rel_err(g1, g2) < 2e-2
+
+
 # ------------------------------------------------------------------ checkpoint engine
 def test_ckpt_engine_roundtrip(gpu):
     eng = torch.classes.tam.CkptEngine(0, 64 << 20)

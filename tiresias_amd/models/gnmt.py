@@ -15,8 +15,9 @@ The LSTM layer is one autograd Function over the whole sequence:
     (GEMM epilogue mode=accumulate) + the fused cell kernel;
   * backward per step: fused cell backward, dh_{t-1} += dG_t W_hh accumulated
     in place; the weight gradients are two large GEMMs over all timesteps.
-The per-step loop is launch-bound, so the job runner captures the whole
-training step into a hipGraph.
+The per-step loop is launch-bound; on MI355X both recurrences run as ONE
+persistent kernel per layer-direction (lstm.hip, grid barrier per timestep,
+W_hh slices resident in VGPRs), the per-step path remaining the fallback.
 """
 from __future__ import annotations
 
@@ -35,6 +36,25 @@ def _T():
 
 
 FUSED_STEP = False
+# whole-sequence persistent recurrence kernels (lstm.hip: lstm_seq_forward /
+# lstm_seq_backward): one launch per layer-direction per pass instead of two
+# per timestep; they decline (return False) for shapes / residency they do not
+# cover and the per-step path runs
+PERSIST = True
+_SYNCS: list = []          # recent barrier/error words (tests read the error flags)
+
+
+def _sync(dev, B: int) -> torch.Tensor:
+    # [0] error flag, [32 * (bt + 1)] arrival counter of batch tile bt (own line each)
+    t = torch.zeros(32 * (B // 16 + 1), dtype=torch.int32, device=dev)
+    _SYNCS.append(t)
+    del _SYNCS[:-64]
+    return t
+
+
+def persist_errors() -> int:
+    """Number of recent persistent launches whose grid barrier timed out."""
+    return sum(int(t[0].item()) for t in _SYNCS)
 
 
 class _LSTMLayer(Function):
@@ -52,6 +72,8 @@ class _LSTMLayer(Function):
         if dev.type == "cuda":
             _T().gemm(x2, True, w_ih.w, True, G, 0, b.w, False, None, 1.0, False)
             Gv = G.view(T, B, 4 * Hd)
+            ran = PERSIST and _T().lstm_seq_forward(Gv, w_hh.w, Hs, Cs, act, reverse, _sync(dev, B))
+            steps = [] if ran else steps
             prev = None
             # the fused per-timestep kernel (lstm_step_forward) ties GEMM + cell +
             # launch boundary on MI355X (12.8 us vs 8.4 + 2.8 us: its 4-units-per-WG
@@ -103,7 +125,8 @@ class _LSTMLayer(Function):
         order = list(range(T - 1, -1, -1) if reverse else range(T))
         rev_order = order[::-1]
         if dev.type == "cuda":
-            for k, t in enumerate(rev_order):
+            ran = PERSIST and _T().lstm_seq_backward(act, Cs, dHf, w_hh.w, dG, reverse, _sync(dev, B))
+            for k, t in enumerate([] if ran else rev_order):
                 prev = rev_order[k + 1] if k + 1 < T else None   # the step that ran before t
                 _T().lstm_cell_backward(act[t], Cs[prev] if prev is not None else None, dHf[t], dc,
                                         None, dc2, dG[t])
