@@ -310,6 +310,43 @@ void conv_dgrad_op(const Tensor& dy, const Tensor& w, const Tensor& wt, const Te
   tam::conv_dgrad(bp(dy), bp(w), bp(wt), g, ep, cur_stream(dy));
 }
 
+// every conv weight of a model re-laid for dgrad in one launch
+void conv_weight_t_batch_op(at::TensorList w, at::TensorList wt) {
+  TORCH_CHECK(w.size() == wt.size(), "tam.conv_weight_t_batch: list sizes differ");
+  if (w.empty()) return;
+  hipStream_t st = cur_stream(w[0]);
+  for (size_t base = 0; base < w.size(); base += tam::WT_MAX) {
+    tam::WTBatch b{};
+    b.n = (int)std::min<size_t>(tam::WT_MAX, w.size() - base);
+    for (int i = 0; i < b.n; ++i) {
+      const Tensor& a = w[base + i];
+      const Tensor& t = wt[base + i];
+      check_bf16(a, "w"); check_bf16(t, "wt"); check_contig(a, "w"); check_contig(t, "wt");
+      TORCH_CHECK(a.dim() == 4 && t.numel() == a.numel(), "tam.conv_weight_t_batch: w must be [K,R,S,C]");
+      b.e[i].w = bp(a); b.e[i].wt = bpm(t);
+      b.e[i].K = (int)a.size(0); b.e[i].RS = (int)(a.size(1) * a.size(2)); b.e[i].C = (int)a.size(3);
+    }
+    tam::conv_weight_t_batch(b, st);
+  }
+}
+
+// dgrad with wt already re-laid (conv_weight_t_batch)
+void conv_dgrad_pre_op(const Tensor& dy, const Tensor& w, const Tensor& wt, const Tensor& dx,
+                       int64_t stride, int64_t pad, int64_t dil, const optional<Tensor>& mask) {
+  check_bf16(dy, "dy"); check_bf16(w, "w"); check_bf16(dx, "dx"); check_bf16(wt, "wt");
+  check_contig(dy, "dy"); check_contig(w, "w"); check_contig(dx, "dx"); check_contig(wt, "wt");
+  TORCH_CHECK(wt.numel() == w.numel(), "tam.conv_dgrad_pre: wt size");
+  tam::ConvGeom g = geom(dx, w, dy, stride, pad, dil);
+  tam::Epi ep;
+  ep.c = dx.data_ptr(); ep.ldc = g.C; ep.c_f32 = 0; ep.mode = 0;
+  if (mask.has_value() && mask->defined()) {
+    check_bf16(*mask, "mask");
+    TORCH_CHECK(mask->numel() == dx.numel(), "tam.conv_dgrad_pre: mask size");
+    ep.mask = bp(*mask); ep.ldm = g.C;
+  }
+  tam::conv_dgrad(bp(dy), bp(w), bp(wt), g, ep, cur_stream(dy));
+}
+
 void conv_wgrad_op(const Tensor& dy, const Tensor& x, const Tensor& dw, int64_t stride, int64_t pad,
                    int64_t dil, int64_t mode) {
   check_bf16(dy, "dy"); check_bf16(x, "x"); check_f32(dw, "dw");
@@ -342,14 +379,18 @@ void bn_forward_op(const Tensor& x, const optional<Tensor>& res, const Tensor& y
 void bn_backward_op(const Tensor& dy, const optional<Tensor>& y, const Tensor& x, const Tensor& mean,
                     const Tensor& rstd, const Tensor& gamma, const Tensor& dx,
                     const optional<Tensor>& dres, const optional<Tensor>& dgamma,
-                    const optional<Tensor>& dbeta, bool relu) {
+                    const optional<Tensor>& dbeta, bool relu, const optional<Tensor>& addend) {
   check_bf16(dy, "dy"); check_bf16(x, "x"); check_bf16(dx, "dx");
   check_contig(dy, "dy"); check_contig(x, "x"); check_contig(dx, "dx");
   const int64_t C = x.size(-1);
   const int64_t M = x.numel() / C;
   TORCH_CHECK(!relu || (y.has_value() && y->defined()), "tam.bn_backward: relu needs y");
+  if (addend.has_value() && addend->defined()) {
+    check_bf16(*addend, "addend"); check_contig(*addend, "addend");
+    TORCH_CHECK(addend->numel() == dy.numel(), "tam.bn_backward: addend size");
+  }
   Tensor ws_f = at::empty({(8 + 2 * tam::BN_MAX_BLOCKS) * C}, x.options().dtype(at::kFloat));
-  tam::bn_backward(bp(dy), opt_ptr<const tam::bf16_t>(y), bp(x), mean.data_ptr<float>(),
+  tam::bn_backward(bp(dy), opt_ptr<const tam::bf16_t>(addend), opt_ptr<const tam::bf16_t>(y), bp(x), mean.data_ptr<float>(),
                    rstd.data_ptr<float>(), gamma.data_ptr<float>(), M, (int)C, relu, bpm(dx),
                    opt_ptr<tam::bf16_t>(dres), opt_ptr<float>(dgamma), opt_ptr<float>(dbeta),
                    ws_f.data_ptr<float>(), cur_stream(x));
@@ -635,9 +676,11 @@ TORCH_LIBRARY(tam, m) {
   m.def("gemm(Tensor a, bool a_kmajor, Tensor b, bool b_kmajor, Tensor(a!) c, int mode, Tensor? bias, bool relu, Tensor? mask, float alpha, bool allow_split) -> ()", &gemm_op);
   m.def("conv_fwd(Tensor x, Tensor w, Tensor(a!) y, int stride, int pad, int dil, Tensor? bias, bool relu) -> ()", &conv_fwd_op);
   m.def("conv_dgrad(Tensor dy, Tensor w, Tensor(a!) wt, Tensor(b!) dx, int stride, int pad, int dil, Tensor? mask) -> ()", &conv_dgrad_op);
+  m.def("conv_weight_t_batch(Tensor[] w, Tensor(a!)[] wt) -> ()", &conv_weight_t_batch_op);
+  m.def("conv_dgrad_pre(Tensor dy, Tensor w, Tensor wt, Tensor(a!) dx, int stride, int pad, int dil, Tensor? mask) -> ()", &conv_dgrad_pre_op);
   m.def("conv_wgrad(Tensor dy, Tensor x, Tensor(a!) dw, int stride, int pad, int dil, int mode) -> ()", &conv_wgrad_op);
   m.def("bn_forward(Tensor x, Tensor? res, Tensor(a!) y, Tensor gamma, Tensor beta, Tensor(b!)? run_mean, Tensor(c!)? run_var, Tensor(d!) save_mean, Tensor(e!) save_rstd, float eps, float momentum, bool relu) -> ()", &bn_forward_op);
-  m.def("bn_backward(Tensor dy, Tensor? y, Tensor x, Tensor mean, Tensor rstd, Tensor gamma, Tensor(a!) dx, Tensor(b!)? dres, Tensor(c!)? dgamma, Tensor(d!)? dbeta, bool relu) -> ()", &bn_backward_op);
+  m.def("bn_backward(Tensor dy, Tensor? y, Tensor x, Tensor mean, Tensor rstd, Tensor gamma, Tensor(a!) dx, Tensor(b!)? dres, Tensor(c!)? dgamma, Tensor(d!)? dbeta, bool relu, Tensor? addend=None) -> ()", &bn_backward_op);
   m.def("ln_forward(Tensor x, Tensor g, Tensor b, Tensor(a!) y, Tensor(b!) mean, Tensor(c!) rstd, float eps) -> ()", &ln_forward_op);
   m.def("ln_backward(Tensor dy, Tensor x, Tensor g, Tensor mean, Tensor rstd, Tensor(a!) dx, Tensor(b!) dg, Tensor(c!) db, Tensor? addend=None) -> ()", &ln_backward_op);
   m.def("maxpool_forward(Tensor x, Tensor(a!) y, Tensor(b!) idx, int R, int S, int stride, int pad) -> ()", &maxpool_forward_op);

@@ -22,7 +22,21 @@ void bn_forward(const bf16_t* x, const bf16_t* res, bf16_t* y, long M, int C, fl
                 hipStream_t s);
 void bn_infer(const bf16_t* x, const bf16_t* res, bf16_t* y, long M, int C, const float* scale,
               const float* shift, int relu, hipStream_t s);
-void bn_backward(const bf16_t* dy, const bf16_t* y, const bf16_t* x, const float* mean,
+// batched conv weight re-layout [K][RS][C] -> [C][RS][K] (one launch)
+struct WTEntry {
+  const bf16_t* w;
+  bf16_t* wt;
+  int K, RS, C, tile0;
+};
+constexpr int WT_MAX = 64;
+struct WTBatch {
+  int n;
+  WTEntry e[WT_MAX];
+};
+void conv_weight_t_batch(WTBatch& b, hipStream_t s);
+// addend (optional): a second upstream gradient of y summed into dy on load
+// (the residual branch's, so autograd never materialises the sum)
+void bn_backward(const bf16_t* dy, const bf16_t* addend, const bf16_t* y, const bf16_t* x, const float* mean,
                  const float* rstd, const float* gamma, long M, int C, int relu, bf16_t* dx,
                  bf16_t* dres, float* dgamma, float* dbeta, float* ws_f, hipStream_t s);
 

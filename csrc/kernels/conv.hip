@@ -11,6 +11,7 @@
 #include "tam/launch.h"
 #include "tam/tiles.h"
 #include "tam/conv_dma.h"
+#include "tam/kernels.h"
 
 namespace tam {
 
@@ -161,6 +162,39 @@ __global__ void conv_weight_t_kernel(const bf16_t* __restrict__ w, bf16_t* __res
     const int c = (int)(t / RS);
     wt[i] = w[((long)k * RS + rs) * C + c];
   }
+}
+
+// Every conv weight of a model re-laid [K][RS][C] -> [C][RS][K] in ONE launch
+// (the dgrad B operand), 64 x 64 (k, c) tiles through LDS so both the read
+// (along c) and the write (along k) are 128-B coalesced rows. Called once per
+// training step after the optimizer's weights are final (model forward).
+__global__ void __launch_bounds__(256) conv_wt_batch_kernel(WTBatch b) {
+  __shared__ bf16_t tile[64][66];
+  int e = 0;
+  while (e + 1 < b.n && (int)blockIdx.x >= b.e[e + 1].tile0) ++e;
+  const WTEntry& en = b.e[e];
+  const int tk = (en.K + 63) / 64, tc = (en.C + 63) / 64;
+  const int local = blockIdx.x - en.tile0;
+  const int rs = local / (tk * tc), r2 = local % (tk * tc);
+  const int k0 = (r2 / tc) * 64, c0 = (r2 % tc) * 64;
+  for (int i = threadIdx.x; i < 64 * 64; i += 256) {
+    const int kk = i >> 6, cc = i & 63, k = k0 + kk, c = c0 + cc;
+    tile[kk][cc] = (k < en.K && c < en.C) ? en.w[((long)k * en.RS + rs) * en.C + c] : (bf16_t)0;
+  }
+  __syncthreads();
+  for (int i = threadIdx.x; i < 64 * 64; i += 256) {
+    const int cc = i >> 6, kk = i & 63, k = k0 + kk, c = c0 + cc;
+    if (k < en.K && c < en.C) en.wt[((long)c * en.RS + rs) * en.K + k] = tile[kk][cc];
+  }
+}
+
+void conv_weight_t_batch(WTBatch& b, hipStream_t s) {
+  int tiles = 0;
+  for (int i = 0; i < b.n; ++i) {
+    b.e[i].tile0 = tiles;
+    tiles += b.e[i].RS * ((b.e[i].K + 63) / 64) * ((b.e[i].C + 63) / 64);
+  }
+  if (tiles > 0) hipLaunchKernelGGL(conv_wt_batch_kernel, dim3(tiles), dim3(256), 0, s, b);
 }
 
 void conv_weight_t(const bf16_t* w, bf16_t* wt, const ConvGeom& g, hipStream_t s) {

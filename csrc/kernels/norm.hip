@@ -277,9 +277,9 @@ __global__ void __launch_bounds__(256) bn_apply_kernel(const bf16_t* __restrict_
 // ---------------------------------------------------------------- BN backward
 // dyr = dy * (y > 0 if relu); accum sum(dyr), sum(dyr * xhat) per channel
 __global__ void __launch_bounds__(256) bn_bwd_reduce_kernel(
-    const bf16_t* __restrict__ dy, const bf16_t* __restrict__ y, const bf16_t* __restrict__ x,
-    const float* __restrict__ mean, const float* __restrict__ rstd, long M, int C,
-    long rows_per_block, int relu, float* __restrict__ part) {
+    const bf16_t* __restrict__ dy, const bf16_t* __restrict__ addend, const bf16_t* __restrict__ y,
+    const bf16_t* __restrict__ x, const float* __restrict__ mean, const float* __restrict__ rstd, long M,
+    int C, long rows_per_block, int relu, float* __restrict__ part) {
   __shared__ float red[256 * 16];
   const int tpr = C / 8, rpb = 256 / tpr;
   const int cg = threadIdx.x % tpr, rl = threadIdx.x / tpr;
@@ -295,6 +295,12 @@ __global__ void __launch_bounds__(256) bn_bwd_reduce_kernel(
       unpack8(*(const uint4*)(dy + off), fd);
       unpack8(*(const uint4*)(x + off), fx);
       if (relu) unpack8(*(const uint4*)(y + off), fy);
+      if (addend) {
+        float fa[8];
+        unpack8(*(const uint4*)(addend + off), fa);
+#pragma unroll
+        for (int i = 0; i < 8; ++i) fd[i] += fa[i];
+      }
 #pragma unroll
       for (int i = 0; i < 8; ++i) {
         const float d = (relu && fy[i] <= 0.f) ? 0.f : fd[i];
@@ -338,7 +344,8 @@ __global__ void bn_bwd_finalize_kernel(const double* __restrict__ sums, long M, 
 }
 
 __global__ void __launch_bounds__(256) bn_bwd_apply_kernel(
-    const bf16_t* __restrict__ dy, const bf16_t* __restrict__ y, const bf16_t* __restrict__ x,
+    const bf16_t* __restrict__ dy, const bf16_t* __restrict__ addend, const bf16_t* __restrict__ y,
+    const bf16_t* __restrict__ x,
     const float* __restrict__ mean, const float* __restrict__ rstd, const float* __restrict__ k1,
     const float* __restrict__ k2, const float* __restrict__ k3, bf16_t* __restrict__ dx,
     bf16_t* __restrict__ dres, long total8, int C, int relu) {
@@ -348,8 +355,9 @@ __global__ void __launch_bounds__(256) bn_bwd_apply_kernel(
   for (; i + stride < total8; i += 2 * stride) {
     const uint4 da = ((const uint4*)dy)[i], db = ((const uint4*)dy)[i + stride];
     const uint4 xa = ((const uint4*)x)[i], xb = ((const uint4*)x)[i + stride];
-    uint4 ya = make_uint4(0, 0, 0, 0), yb = ya;
+    uint4 ya = make_uint4(0, 0, 0, 0), yb = ya, aa = ya, ab = ya;
     if (relu) { ya = ((const uint4*)y)[i]; yb = ((const uint4*)y)[i + stride]; }
+    if (addend) { aa = ((const uint4*)addend)[i]; ab = ((const uint4*)addend)[i + stride]; }
 #pragma unroll
     for (int h = 0; h < 2; ++h) {
       const long ii = h ? i + stride : i;
@@ -357,6 +365,12 @@ __global__ void __launch_bounds__(256) bn_bwd_apply_kernel(
       float fd[8], fx[8], fy[8];
       unpack8(h ? db : da, fd);
       unpack8(h ? xb : xa, fx);
+      if (addend) {
+        float fa[8];
+        unpack8(h ? ab : aa, fa);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) fd[j] += fa[j];
+      }
       if (relu) {
         unpack8(h ? yb : ya, fy);
 #pragma unroll
@@ -378,6 +392,12 @@ __global__ void __launch_bounds__(256) bn_bwd_apply_kernel(
     float fd[8], fx[8], fy[8];
     unpack8(((const uint4*)dy)[i], fd);
     unpack8(((const uint4*)x)[i], fx);
+    if (addend) {
+      float fa[8];
+      unpack8(((const uint4*)addend)[i], fa);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) fd[j] += fa[j];
+    }
     if (relu) {
       unpack8(((const uint4*)y)[i], fy);
 #pragma unroll
@@ -437,23 +457,23 @@ void bn_infer(const bf16_t* x, const bf16_t* res, bf16_t* y, long M, int C, cons
                      shift, y, total8, C, relu);
 }
 
-void bn_backward(const bf16_t* dy, const bf16_t* y, const bf16_t* x, const float* mean,
-                 const float* rstd, const float* gamma, long M, int C, int relu, bf16_t* dx,
-                 bf16_t* dres, float* dgamma, float* dbeta, float* ws_f, hipStream_t s) {
+void bn_backward(const bf16_t* dy, const bf16_t* addend, const bf16_t* y, const bf16_t* x,
+                 const float* mean, const float* rstd, const float* gamma, long M, int C, int relu,
+                 bf16_t* dx, bf16_t* dres, float* dgamma, float* dbeta, float* ws_f, hipStream_t s) {
   // ws_f: 4*C floats k1/k2/k3(+pad) | 2*C doubles column sums | BN_MAX_BLOCKS*2*C partials
   const long rpb = bn_rows_per_block(M, C);
   const int nb = (int)((M + rpb - 1) / rpb);
   double* sums = (double*)(ws_f + 4 * C);
   float* part = ws_f + 8 * C;
-  hipLaunchKernelGGL(bn_bwd_reduce_kernel, dim3(nb), dim3(256), 0, s, dy, y, x, mean, rstd, M, C,
-                     rpb, relu, part);
+  hipLaunchKernelGGL(bn_bwd_reduce_kernel, dim3(nb), dim3(256), 0, s, dy, addend, y, x, mean, rstd, M,
+                     C, rpb, relu, part);
   (void)sums;
   hipLaunchKernelGGL(bn_reduce_finalize_kernel<1>, dim3((C + 15) / 16), dim3(256), 0, s, part, nb, M,
                      C, 0.f, 0.f, gamma, rstd, dgamma, dbeta, ws_f, ws_f + C, ws_f + 2 * C,
                      (float*)nullptr);
   const long total8 = M * C / 8;
-  hipLaunchKernelGGL(bn_bwd_apply_kernel, dim3(grid_for(total8)), dim3(256), 0, s, dy, y, x, mean,
-                     rstd, ws_f, ws_f + C, ws_f + 2 * C, dx, dres, total8, C, relu);
+  hipLaunchKernelGGL(bn_bwd_apply_kernel, dim3(grid_for(total8)), dim3(256), 0, s, dy, addend, y, x,
+                     mean, rstd, ws_f, ws_f + C, ws_f + 2 * C, dx, dres, total8, C, relu);
 }
 
 // ---------------------------------------------------------------- LayerNorm

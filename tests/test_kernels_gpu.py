@@ -426,6 +426,44 @@ def test_batchnorm(gpu, relu, res, shape):
     assert rel_err(rm, 0.1 * xs.mean(0)) < 1e-4
 
 
+@pytest.mark.parametrize("relu", [False, True])
+def test_batchnorm_backward_addend(gpu, relu):
+    """bn_backward(dy, addend=a) == bn_backward(dy + a): the residual branch's
+    gradient summed on load (ResNet residual taps)."""
+    torch.manual_seed(6)
+    N, H, W, C = 16, 14, 14, 256
+    x = (torch.randn(N, H, W, C, device=gpu) * 2).to(BF)
+    g = torch.rand(C, device=gpu) + 0.5
+    b = torch.randn(C, device=gpu)
+    y = torch.empty_like(x)
+    mean = torch.empty(C, device=gpu); rstd = torch.empty(C, device=gpu)
+    r = torch.randn_like(x.float()).to(BF)
+    T().bn_forward(x, r, y, g, b, None, None, mean, rstd, 1e-5, 0.1, relu)
+    dy = torch.randn_like(x.float()).to(BF)
+    a = torch.randn_like(x.float()).to(BF)
+    outs = []
+    for d, add in ((dy, a), ((dy.float() + a.float()).to(BF), None)):
+        dx, dres = torch.empty_like(x), torch.empty_like(x)
+        dg, db = torch.zeros(C, device=gpu), torch.zeros(C, device=gpu)
+        T().bn_backward(d, y, x, mean, rstd, g, dx, dres, dg, db, relu, add)
+        outs.append((dx, dres, dg, db))
+    for u, v in zip(*outs):
+        assert rel_err(u, v) < 1e-2
+
+
+def test_conv_weight_t_batch(gpu):
+    """All conv weights re-laid [K,R,S,C] -> [C,R,S,K] in one launch (odd
+    sizes included) vs torch.permute."""
+    torch.manual_seed(7)
+    shapes = [(64, 7, 7, 8), (256, 1, 1, 64), (64, 3, 3, 64), (2048, 1, 1, 1024), (100, 3, 3, 36)]
+    ws = [torch.randn(*sh, device=gpu).to(BF) for sh in shapes]
+    wts = [torch.empty_like(w) for w in ws]
+    T().conv_weight_t_batch(ws, wts)
+    for w, wt in zip(ws, wts):
+        K, R, S, C = w.shape
+        assert torch.equal(wt.view(C, R, S, K), w.permute(3, 1, 2, 0).contiguous())
+
+
 @pytest.mark.parametrize("D,rows", [(512, 777), (1024, 777), (320, 777), (512, 16384),
                                     (1024, 4100), (2048, 3000)])
 def test_layernorm(gpu, D, rows):

@@ -8,9 +8,11 @@ reference only *models* them: per-tensor gradient sizes in
 * activations NHWC bf16 (channels innermost = the implicit-GEMM K axis);
 * the 3-channel RGB input is zero-padded to 8 channels so every conv keeps
   16-byte channel vectors;
-* ResNet: BN + residual-add + ReLU fused in one kernel; VGG: conv + bias +
-  ReLU fused in the conv epilogue, the ReLU backward fused into the next
-  layer's dgrad epilogue;
+* ResNet: BN + residual-add + ReLU fused in one kernel; the residual
+  branch's gradient is summed inside the producing BN's backward (a tap, no
+  add kernel); VGG: conv + bias + ReLU fused in the conv epilogue, the ReLU
+  backward fused into the next layer's dgrad epilogue;
+* every conv weight is re-laid for dgrad once per step in one launch;
 * all weights live in one flat :class:`Arena` per job.
 """
 from __future__ import annotations
@@ -80,20 +82,29 @@ class ResNet50:
         return Fx.batchnorm(x, p[0], p[1], st.mean, st.var, relu=relu, residual=res,
                             training=self.training)
 
+    def conv_params(self):
+        out = [self.stem]
+        for blk in self.blocks:
+            out += [blk["c1"], blk["c2"], blk["c3"]] + ([blk["down"]] if "down" in blk else [])
+        return out
+
     def forward(self, x: torch.Tensor) -> torch.Tensor:
+        Fx.prepare_conv_wt(self.conv_params())
         y = Fx.conv2d(x, self.stem, stride=2, pad=3)
         y = self._bn(y, self.stem_bn, "stem", relu=True)
         y = Fx.maxpool2d(y, 3, 2, 1)
         for blk in self.blocks:
             pre = blk["pre"]
-            idn = y
+            # the second consumer of y (residual / downsample) goes through a
+            # tap: its gradient is summed inside y's producing BN backward
+            idn = Fx.residual_tap(y) if "down" not in blk else None
             o = Fx.conv2d(y, blk["c1"])
             o = self._bn(o, blk["bn1"], pre + ".bn1", relu=True)
             o = Fx.conv2d(o, blk["c2"], stride=blk["stride"], pad=1)
             o = self._bn(o, blk["bn2"], pre + ".bn2", relu=True)
             o = Fx.conv2d(o, blk["c3"])
             if "down" in blk:
-                idn = Fx.conv2d(y, blk["down"], stride=blk["stride"])
+                idn = Fx.conv2d(Fx.residual_tap(y), blk["down"], stride=blk["stride"])
                 idn = self._bn(idn, blk["down_bn"], pre + ".dbn", relu=False)
             y = self._bn(o, blk["bn3"], pre + ".bn3", relu=True, res=idn)
         y = Fx.global_avgpool(y)
@@ -143,6 +154,7 @@ class VGG16:
         self.training = True
 
     def forward(self, x: torch.Tensor) -> torch.Tensor:
+        Fx.prepare_conv_wt([p[0] for kind, p in self.layers if kind == "conv"])
         y = x
         in_relu = False
         n = len(self.layers)

@@ -18,7 +18,7 @@ reference of the same math (CPU test-suite, gloo rehearsals, numerics refs).
 from __future__ import annotations
 
 import math
-from typing import Optional, Tuple
+from typing import List, Optional, Tuple
 
 import torch
 import torch.nn.functional as F
@@ -255,8 +255,12 @@ class _Conv(Function):
                     _T().colsum(dy, b.grad)
             if ctx.needs_input_grad[0]:
                 dx = torch.empty_like(x)
-                wt = torch.empty_like(w.w)
-                _T().conv_dgrad(dy, w.w, wt, dx, st, pd, 1, x if ctx.in_relu else None)
+                wt = getattr(w, "wt", None)
+                if wt is not None:       # re-laid once per step (prepare_conv_wt)
+                    _T().conv_dgrad_pre(dy, w.w, wt, dx, st, pd, 1, x if ctx.in_relu else None)
+                else:
+                    wt = torch.empty_like(w.w)
+                    _T().conv_dgrad(dy, w.w, wt, dx, st, pd, 1, x if ctx.in_relu else None)
         else:
             xf = x.float().permute(0, 3, 1, 2).requires_grad_(ctx.needs_input_grad[0])
             wf = w.w.float().permute(0, 3, 1, 2).requires_grad_(True)
@@ -278,6 +282,19 @@ class _Conv(Function):
         return dx, None, None, None, None, None, None, None, None
 
 
+def prepare_conv_wt(params: List[Param]) -> None:
+    """Re-lay every conv weight [K,R,S,C] -> [C,R,S,K] (the dgrad operand) in
+    ONE launch per step, into per-parameter buffers kept across steps (the
+    dgrad then skips its own transpose). Call at the start of the forward:
+    the weights are final for the step then. No-op on CPU."""
+    if not params or not params[0].w.is_cuda:
+        return
+    for p in params:
+        if getattr(p, "wt", None) is None or p.wt.device != p.w.device:
+            p.wt = torch.empty_like(p.w)
+    _T().conv_weight_t_batch([p.w for p in params], [p.wt for p in params])
+
+
 def conv2d(x: torch.Tensor, w: Param, b: Optional[Param] = None, stride: int = 1, pad: int = 0,
            relu: bool = False, in_relu: bool = False, mask_own_relu: bool = True) -> torch.Tensor:
     """NHWC conv, weights [K,R,S,C]."""
@@ -287,10 +304,46 @@ def conv2d(x: torch.Tensor, w: Param, b: Optional[Param] = None, stride: int = 1
 
 
 # ============================================================ BatchNorm (NHWC)
+class GradSlot:
+    """A second upstream gradient of a BN output, parked by a residual tap
+    (``residual_tap``) instead of being summed by autograd; the producing
+    BN's backward adds it while loading dy (bn_backward ``addend``), so the
+    residual-branch sum is never materialised (no separate add kernel)."""
+
+    __slots__ = ("stash",)
+
+    def __init__(self):
+        self.stash = None
+
+
+class _Tap(Function):
+    @staticmethod
+    def forward(ctx, y, slot: GradSlot):
+        ctx.slot = slot
+        return y.view_as(y)
+
+    @staticmethod
+    def backward(ctx, g):
+        if ctx.slot.stash is not None:           # a second tap: fall back to autograd's sum
+            return g, None
+        ctx.slot.stash = g.contiguous()
+        return None, None
+
+
+def residual_tap(y: torch.Tensor) -> torch.Tensor:
+    """y for a second consumer (the residual branch / a downsample conv):
+    its gradient goes to y's producing BN as an addend. Plain y when the
+    producer is not such a BN (or on CPU)."""
+    slot = getattr(y, "_tam_slot", None)
+    if slot is None or not y.is_cuda or not torch.is_grad_enabled():
+        return y
+    return _Tap.apply(y, slot)
+
+
 class _BN(Function):
     @staticmethod
     def forward(ctx, x, res, token, g: Param, b: Param, run_mean, run_var, relu: bool, eps: float,
-                momentum: float, training: bool):
+                momentum: float, training: bool, slot: Optional[GradSlot] = None):
         C = x.shape[-1]
         if x.is_cuda:
             y = torch.empty_like(x)
@@ -324,6 +377,7 @@ class _BN(Function):
                 yf = yf.clamp_min(0)
             y = yf.reshape(x.shape).to(BF16)
         ctx.g, ctx.b, ctx.relu, ctx.has_res = g, b, relu, res is not None
+        ctx.slot = slot
         ctx.save_for_backward(x, y if relu else None, mean, rstd)
         return y
 
@@ -333,14 +387,19 @@ class _BN(Function):
         g, b = ctx.g, ctx.b
         dy = dy.contiguous()
         C = x.shape[-1]
+        add = None
+        if ctx.slot is not None:
+            add, ctx.slot.stash = ctx.slot.stash, None
         if dy.is_cuda:
             dx = torch.empty_like(x)
-            dres = torch.empty_like(x) if ctx.has_res and ctx.relu else None
-            _T().bn_backward(dy, y, x, mean, rstd, g.master, dx, dres, g.grad, b.grad, ctx.relu)
-            if ctx.has_res and not ctx.relu:
+            dres = torch.empty_like(x) if ctx.has_res and (ctx.relu or add is not None) else None
+            _T().bn_backward(dy, y, x, mean, rstd, g.master, dx, dres, g.grad, b.grad, ctx.relu, add)
+            if ctx.has_res and dres is None:
                 dres = dy
         else:
             dyf = dy.float().reshape(-1, C)
+            if add is not None:
+                dyf = dyf + add.float().reshape(-1, C)
             if ctx.relu:
                 dyf = dyf * (y.float().reshape(-1, C) > 0)
             xh = (x.float().reshape(-1, C) - mean) * rstd
@@ -354,7 +413,7 @@ class _BN(Function):
             dres = dyf.reshape(x.shape).to(BF16) if ctx.has_res else None
         g.grad_ready()
         b.grad_ready()
-        return dx, dres, None, None, None, None, None, None, None, None, None
+        return dx, dres, None, None, None, None, None, None, None, None, None, None
 
 
 def _bn_infer_gpu(x, res, scale, shift, relu):
@@ -376,8 +435,12 @@ def batchnorm(x: torch.Tensor, g: Param, b: Param, run_mean: Optional[torch.Tens
         x = x.contiguous()
     if residual is not None and not residual.is_contiguous():
         residual = residual.contiguous()
-    return _BN.apply(x, residual, g.arena.token, g, b, run_mean, run_var, relu, eps, momentum,
-                     training)
+    slot = GradSlot() if (x.is_cuda and training and torch.is_grad_enabled()) else None
+    y = _BN.apply(x, residual, g.arena.token, g, b, run_mean, run_var, relu, eps, momentum,
+                  training, slot)
+    if slot is not None:
+        y._tam_slot = slot
+    return y
 
 
 # ============================================================ LayerNorm

@@ -38,6 +38,7 @@ def main():
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--graph", action="store_true")
+    ap.add_argument("--batch", type=int, default=0, help="per-GPU batch override (0: the model default)")
     ap.add_argument("--out", default=None)
     ap.add_argument("--overlap", type=int, default=-1,
                     help="weight gradients on a side stream: -1 per-model default, 0 off, 1 on")
@@ -52,7 +53,7 @@ def main():
     torch.ops.tam.gemm_lib_policy(a.lib)
     res = []
     for m in a.models.split(","):
-        r = bench(m, steps=a.steps, warmup=a.warmup, graph=a.graph,
+        r = bench(m, batch=a.batch or None, steps=a.steps, warmup=a.warmup, graph=a.graph,
                   overlap=None if a.overlap < 0 else bool(a.overlap), branches=None if a.branches < 0 else bool(a.branches))
         print(json.dumps(r), flush=True)
         res.append(r)
