@@ -659,6 +659,8 @@ bool lstm_seq_bwd_op(const Tensor& act, const Tensor& cs, const Tensor& dH, cons
                                 cur_stream(act));
 }
 
+void lstm_seq_policy_op(int64_t ch) { tam::lstm_seq_policy((int)ch); }
+
 void lstm_bwd_op(const Tensor& act, const optional<Tensor>& c_prev, const optional<Tensor>& dh,
                  const optional<Tensor>& dc_next, const optional<Tensor>& dgates,
                  const optional<Tensor>& dc_prev, const optional<Tensor>& dgates_bf16) {
@@ -707,6 +709,7 @@ TORCH_LIBRARY(tam, m) {
   m.def("lstm_step_forward(Tensor gx, Tensor w_hh, Tensor? h_prev, Tensor? c_prev, Tensor(a!) c_out, Tensor(b!) h_out, Tensor(c!) act) -> ()", &lstm_step_fwd_op);
   m.def("lstm_seq_forward(Tensor gx, Tensor w_hh, Tensor(a!) hs, Tensor(b!) cs, Tensor(c!) act, bool reverse, Tensor(d!) sync) -> bool", &lstm_seq_fwd_op);
   m.def("lstm_seq_backward(Tensor act, Tensor cs, Tensor dH, Tensor w_hh, Tensor(a!) dG, bool reverse, Tensor(b!) sync) -> bool", &lstm_seq_bwd_op);
+  m.def("lstm_seq_policy(int ch) -> ()", &lstm_seq_policy_op);
   m.def("lstm_cell_forward(Tensor gates, Tensor? c_prev, Tensor(a!) c_out, Tensor(b!) h_out, Tensor(c!)? h_f32, Tensor(d!) act) -> ()", &lstm_fwd_op);
   m.def("lstm_cell_backward(Tensor act, Tensor? c_prev, Tensor? dh, Tensor? dc_next, Tensor(a!)? dgates, Tensor(b!)? dc_prev, Tensor(c!)? dgates_bf16) -> ()", &lstm_bwd_op);
 }

@@ -104,6 +104,8 @@ bool lstm_seq_forward(const float* gx, const bf16_t* w_hh, bf16_t* hs, float* cs
                       int B, int Hd, int reverse, unsigned* sync, hipStream_t s);
 bool lstm_seq_backward(const float* act, const float* cs, const float* dH, const bf16_t* w_hh, bf16_t* dG,
                        int T, int B, int Hd, int reverse, unsigned* sync, hipStream_t s);
+// unit halves per persistent workgroup: 0 auto, 1 (16 units) or 2 (32 units)
+void lstm_seq_policy(int ch);
 void lstm_cell_backward(const float* act_cache, const float* c_prev, const float* c_out,
                         const float* dh, const float* dc_next, float* dgates, float* dc_prev,
                         bf16_t* dgates_bf16, int B, int Hd, hipStream_t s);

@@ -6,6 +6,9 @@
 #include "tam/common.h"
 #include "tam/kernels.h"
 
+#include <map>
+#include <mutex>
+
 namespace tam {
 
 __device__ __forceinline__ float tanhf_(float x) { return 1.f - 2.f / (__expf(2.f * x) + 1.f); }
@@ -185,6 +188,9 @@ void lstm_step_forward(const float* gx, const bf16_t* w_hh, const bf16_t* h_prev
 // ---------------------------------------------------------------------------
 constexpr int PL_W = 8;          // waves per workgroup
 constexpr unsigned PL_SPIN = 1u << 22;
+#ifndef PL_BCH
+#define PL_BCH 16         // backward: dG fragment loads in flight per chunk
+#endif
 typedef __attribute__((address_space(1))) unsigned pl_gu32;
 typedef __attribute__((address_space(1))) unsigned long long pl_gu64;
 #define PL_RLX __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT
@@ -222,27 +228,33 @@ __device__ __forceinline__ s16x8_t pl_ld16(__amdgpu_buffer_rsrc_t r, unsigned by
   return __builtin_bit_cast(s16x8_t, v);
 }
 
-template <int KW>   // k-steps of 32 per wave: Hd / (32 * PL_W)
-__global__ void __launch_bounds__(64 * PL_W, 4) lstm_persist_fwd_kernel(
+// CH = unit halves per workgroup: 16 * CH hidden units, 8 * CH waves (8 K-
+// slices x CH unit halves). CH = 2 halves the grid (and the per-step h / dG
+// traffic, which every workgroup of a batch tile re-reads) at the same bytes
+// per workgroup.
+template <int KW, int CH>   // KW: k-steps of 32 per wave = Hd / (32 * PL_W)
+__global__ void __launch_bounds__(64 * PL_W * CH, 4) lstm_persist_fwd_kernel(
     const float* __restrict__ gx, const bf16_t* __restrict__ w, bf16_t* hs, float* __restrict__ cs,
     float* __restrict__ act, int T, int B, int Hd, int reverse, unsigned* sync) {
-  __shared__ float red[PL_W][16][65];
-  __shared__ __attribute__((aligned(16))) bf16_t hbuf[16][16];
+  constexpr int U = 16 * CH;                 // units per workgroup
+  __shared__ float red[PL_W][16][4 * U + 1];
+  __shared__ __attribute__((aligned(16))) bf16_t hbuf[16][U];
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  const int ksl = wv % PL_W, half = wv / PL_W;
   const int nbt = B / 16;
   const int bt = blockIdx.x % nbt, ut = blockIdx.x / nbt;
-  const int b0 = bt * 16, j0 = ut * 16;
-  const int kb = wv * KW * 32 + 8 * (lane >> 4);
-  // W_hh rows of this tile, this wave's K-slice, as MFMA B fragments
+  const int b0 = bt * 16, j0 = ut * U;
+  const int kb = ksl * KW * 32 + 8 * (lane >> 4);
+  // W_hh rows {i,f,g,o} x this wave's 16 units, its K-slice, as MFMA B fragments
   s16x8_t wf[4][KW];
 #pragma unroll
   for (int g = 0; g < 4; ++g)
 #pragma unroll
     for (int ks = 0; ks < KW; ++ks)
-      wf[g][ks] = *(const s16x8_t*)(w + (long)(g * Hd + j0 + (lane & 15)) * Hd + kb + 32 * ks);
+      wf[g][ks] = *(const s16x8_t*)(w + (long)(g * Hd + j0 + 16 * half + (lane & 15)) * Hd + kb + 32 * ks);
   const __amdgpu_buffer_rsrc_t hrs = pl_rsrc(hs, (long)T * B * Hd * 2);
-  const bool cell = threadIdx.x < 256;
-  const int cr = threadIdx.x >> 4, cu = threadIdx.x & 15;
+  const bool cell = threadIdx.x < 16 * U;
+  const int cr = threadIdx.x / U, cu = threadIdx.x % U;
   float c_reg = 0.f;
   for (int s = 0; s < T; ++s) {
     const int t = reverse ? T - 1 - s : s;
@@ -273,7 +285,8 @@ __global__ void __launch_bounds__(64 * PL_W, 4) lstm_persist_fwd_kernel(
 #pragma unroll
     for (int g = 0; g < 4; ++g)
 #pragma unroll
-      for (int r = 0; r < 4; ++r) red[wv][4 * (lane >> 4) + r][g * 16 + (lane & 15)] = acc[g][r];
+      for (int r = 0; r < 4; ++r)
+        red[ksl][4 * (lane >> 4) + r][g * U + 16 * half + (lane & 15)] = acc[g][r];
     __syncthreads();
     if (cell) {
       float gs[4];
@@ -281,7 +294,7 @@ __global__ void __launch_bounds__(64 * PL_W, 4) lstm_persist_fwd_kernel(
       for (int q = 0; q < 4; ++q) {
         float v = gxv[q];
 #pragma unroll
-        for (int k = 0; k < PL_W; ++k) v += red[k][cr][q * 16 + cu];
+        for (int k = 0; k < PL_W; ++k) v += red[k][cr][q * U + cu];
         gs[q] = v;
       }
       const float i_ = sigmoidf_(gs[0]), f_ = sigmoidf_(gs[1]), g_ = tanhf_(gs[2]), o_ = sigmoidf_(gs[3]);
@@ -297,48 +310,95 @@ __global__ void __launch_bounds__(64 * PL_W, 4) lstm_persist_fwd_kernel(
     }
     __syncthreads();
     if (wv == 0) {
-      // 16 rows x 16 units of h_t: 64 lanes x 8 B, write-through
-      const int r = lane >> 2, q = lane & 3;
-      const unsigned long long v = *(const unsigned long long*)&hbuf[r][4 * q];
-      __hip_atomic_store((pl_gu64*)(hs + ((long)t * B + b0 + r) * Hd + j0 + 4 * q), v, PL_RLX);
+      // 16 rows x U units of h_t: (64 x CH) x 8 B, write-through
+#pragma unroll
+      for (int u = 0; u < CH; ++u) {
+        const int idx = u * 64 + lane, r = idx / (4 * CH), q = idx % (4 * CH);
+        const unsigned long long v = *(const unsigned long long*)&hbuf[r][4 * q];
+        __hip_atomic_store((pl_gu64*)(hs + ((long)t * B + b0 + r) * Hd + j0 + 4 * q), v, PL_RLX);
+      }
       if (s + 1 < T) pl_signal(sync, bt);
     }
-    if (s + 1 < T) pl_wait(sync, bt, (unsigned)(s + 1) * (unsigned)(Hd / 16));
+    if (s + 1 < T) pl_wait(sync, bt, (unsigned)(s + 1) * (unsigned)(Hd / U));
   }
 }
 
 // Backward: dh_t = dH_t + dG_{t+1} W_hh[:, units] (t+1 = the step processed
 // after t in the forward order), then the cell backward; dG_t (bf16) is both
 // the next step's operand and the weight-gradient GEMMs' input. Each wave
-// keeps its K-slice (4Hd/8) of W_hh's 16 unit columns in VGPRs.
-template <int KW>   // k-steps of 32 per wave: 4 Hd / (32 * PL_W)
-__global__ void __launch_bounds__(64 * PL_W, 4) lstm_persist_bwd_kernel(
+// keeps its K-slice (4Hd/8) of W_hh's 16 columns (its unit half) in VGPRs.
+template <int KW, int CH>   // KW: k-steps of 32 per wave = 4 Hd / (32 * PL_W)
+__global__ void __launch_bounds__(64 * PL_W * CH, 4) lstm_persist_bwd_kernel(
     const float* __restrict__ act, const float* __restrict__ cs, const float* __restrict__ dH,
     const bf16_t* __restrict__ w, bf16_t* dG, int T, int B, int Hd, int reverse, unsigned* sync) {
-  __shared__ float red[PL_W][16][17];
-  __shared__ __attribute__((aligned(16))) bf16_t gbuf[16][64];
+  constexpr int U = 16 * CH;
+  // W fragments: the first KWR k-steps in VGPRs, the rest in LDS (the whole
+  // slice in VGPRs needs > 128 of them and spills; CH = 1 only: 2 blocks/CU
+  // of 8 waves x (KW/2) x 1 KB fit the 160 KB)
+  constexpr int KWL = CH == 1 ? KW / 2 : 0, KWR = KW - KWL;
+  constexpr int RED_BYTES = PL_W * 16 * (U + 1) * 4, STAGE_BYTES = PL_W * CH * 32 * 16 * 2;
+  __shared__ __attribute__((aligned(16))) char misc[RED_BYTES > STAGE_BYTES ? RED_BYTES : STAGE_BYTES];
+  __shared__ __attribute__((aligned(16))) s16x8_t wlds[KWL > 0 ? PL_W * CH : 1][KWL > 0 ? KWL : 1][64];
+  __shared__ __attribute__((aligned(16))) bf16_t gbuf[16][4 * U];
+  auto red = (float(*)[16][U + 1])misc;
+  auto wstage = (bf16_t(*)[32][16])misc;     // prologue only, aliases red
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  const int ksl = wv % PL_W, half = wv / PL_W;
   const int nbt = B / 16;
   const int bt = blockIdx.x % nbt, ut = blockIdx.x / nbt;
-  const int b0 = bt * 16, j0 = ut * 16;
-  const int kb = wv * KW * 32 + 8 * (lane >> 4);
-  // B fragment (k, n) = W_hh[k][j0 + n]: 8 consecutive k of one column (strided gather, once)
-  s16x8_t wf[KW];
+  const int b0 = bt * 16, j0 = ut * U;
+  const int kb = ksl * KW * 32 + 8 * (lane >> 4);
+  // B fragment (k, n) = W_hh[k][j0 + 16 half + n]: 8 consecutive k of one
+  // column, gathered once through a per-wave LDS slab (32 rows x 16 columns
+  // per k-step, 16-B coalesced loads), each lane then picking its 8 k
+  s16x8_t wf[KWR];
+  {
+    const int kw0 = ksl * KW * 32;
+    const bf16_t* wcol = w + j0 + 16 * half;
 #pragma unroll
-  for (int ks = 0; ks < KW; ++ks) {
-    const bf16_t* col = w + (long)(kb + 32 * ks) * Hd + j0 + (lane & 15);
+    for (int ks = 0; ks < KW; ++ks) {
+      const int r = lane >> 1, hh = lane & 1;
+      *(uint4*)&wstage[wv][r][8 * hh] = *(const uint4*)(wcol + (long)(kw0 + 32 * ks + r) * Hd + 8 * hh);
+      asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+      s16x8_t f;
 #pragma unroll
-    for (int e = 0; e < 8; ++e) wf[ks][e] = (short)col[(long)e * Hd];
+      for (int e = 0; e < 8; ++e) f[e] = (short)wstage[wv][8 * (lane >> 4) + e][lane & 15];
+      if (ks < KWR) wf[ks < KWR ? ks : 0] = f;
+      else wlds[wv][ks - KWR][lane] = f;
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    }
   }
+  __syncthreads();                           // wstage (aliases red) retired
   const __amdgpu_buffer_rsrc_t grs = pl_rsrc(dG, (long)T * B * 4 * Hd * 2);
-  const bool cell = threadIdx.x < 256;
-  const int cr = threadIdx.x >> 4, cu = threadIdx.x & 15;
+  const bool cell = threadIdx.x < 16 * U;
+  const int cr = threadIdx.x / U, cu = threadIdx.x % U;
   float dc_reg = 0.f;
   for (int s = 0; s < T; ++s) {
     const int t = reverse ? s : T - 1 - s;             // backward order
     const int fwd_idx = reverse ? T - 1 - t : t;       // position of t in the forward order
     const long row = (long)t * B + b0 + cr;
     const int j = j0 + cu;
+    f32x4_t acc = {0.f, 0.f, 0.f, 0.f};
+    if (s > 0) {
+      const int tn = reverse ? t - 1 : t + 1;
+      const unsigned goff = (unsigned)((((long)tn * B + b0 + (lane & 15)) * 4 * Hd + kb) * 2);
+      constexpr int BCH = PL_BCH < KW ? PL_BCH : KW;
+#pragma unroll
+      for (int h = 0; h < KW; h += BCH) {
+        s16x8_t ga[BCH];
+#pragma unroll
+        for (int u = 0; u < BCH; ++u) ga[u] = pl_ld16(grs, goff + 64 * (h + u));
+#pragma unroll
+        for (int u = 0; u < BCH; ++u) {
+          const int ks = h + u;
+          const s16x8_t b = ks < KWR ? wf[ks < KWR ? ks : 0] : wlds[wv][ks >= KWR ? ks - KWR : 0][lane];
+          acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8_t, ga[u]),
+                                                        __builtin_bit_cast(bf16x8_t, b), acc, 0, 0, 0);
+        }
+      }
+    }
+    // the cell operands are loaded after the MFMA chain (their registers
+    // would otherwise be live across it)
     float dhv = 0.f, av[5] = {0.f, 0.f, 0.f, 0.f, 0.f}, cpv = 0.f;
     if (cell) {
       dhv = dH[row * Hd + j];
@@ -350,24 +410,8 @@ __global__ void __launch_bounds__(64 * PL_W, 4) lstm_persist_bwd_kernel(
         cpv = cs[((long)tp * B + b0 + cr) * Hd + j];
       }
     }
-    f32x4_t acc = {0.f, 0.f, 0.f, 0.f};
-    if (s > 0) {
-      const int tn = reverse ? t - 1 : t + 1;
-      const unsigned goff = (unsigned)((((long)tn * B + b0 + (lane & 15)) * 4 * Hd + kb) * 2);
 #pragma unroll
-      for (int h = 0; h < KW; h += 4) {
-        s16x8_t ga[4];
-#pragma unroll
-        for (int u = 0; u < 4; ++u) ga[u] = pl_ld16(grs, goff + 64 * (h + u));
-#pragma unroll
-        for (int u = 0; u < 4; ++u)
-          acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8_t, ga[u]),
-                                                        __builtin_bit_cast(bf16x8_t, wf[h + u]), acc, 0,
-                                                        0, 0);
-      }
-    }
-#pragma unroll
-    for (int r = 0; r < 4; ++r) red[wv][4 * (lane >> 4) + r][lane & 15] = acc[r];
+    for (int r = 0; r < 4; ++r) red[ksl][4 * (lane >> 4) + r][16 * half + (lane & 15)] = acc[r];
     __syncthreads();
     if (cell) {
       float dh = dhv;
@@ -376,84 +420,110 @@ __global__ void __launch_bounds__(64 * PL_W, 4) lstm_persist_bwd_kernel(
       const float i_ = av[0], f_ = av[1], g_ = av[2], o_ = av[3], tc = av[4];
       const float dc = dh * o_ * (1.f - tc * tc) + dc_reg;
       gbuf[cr][cu] = f2bf(dc * g_ * i_ * (1.f - i_));
-      gbuf[cr][16 + cu] = f2bf(dc * cpv * f_ * (1.f - f_));
-      gbuf[cr][32 + cu] = f2bf(dc * i_ * (1.f - g_ * g_));
-      gbuf[cr][48 + cu] = f2bf(dh * tc * o_ * (1.f - o_));
+      gbuf[cr][U + cu] = f2bf(dc * cpv * f_ * (1.f - f_));
+      gbuf[cr][2 * U + cu] = f2bf(dc * i_ * (1.f - g_ * g_));
+      gbuf[cr][3 * U + cu] = f2bf(dh * tc * o_ * (1.f - o_));
       dc_reg = dc * f_;
     }
     __syncthreads();
     if (wv == 0) {
-      // 16 rows x 4 gates x 16 units of dG_t: 4 x (64 lanes x 8 B), write-through
+      // 16 rows x 4 gates x U units of dG_t: (4 x CH) x (64 lanes x 8 B), write-through
 #pragma unroll
-      for (int u = 0; u < 4; ++u) {
-        const int idx = u * 64 + lane, r = idx >> 4, g = (idx >> 2) & 3, q = idx & 3;
-        const unsigned long long v = *(const unsigned long long*)&gbuf[r][16 * g + 4 * q];
+      for (int u = 0; u < 4 * CH; ++u) {
+        const int idx = u * 64 + lane, r = idx / (16 * CH), rem = idx % (16 * CH);
+        const int g = rem / (4 * CH), q = rem % (4 * CH);
+        const unsigned long long v = *(const unsigned long long*)&gbuf[r][g * U + 4 * q];
         __hip_atomic_store((pl_gu64*)(dG + ((long)t * B + b0 + r) * 4 * Hd + g * Hd + j0 + 4 * q), v,
                            PL_RLX);
       }
       if (s + 1 < T) pl_signal(sync, bt);
     }
-    if (s + 1 < T) pl_wait(sync, bt, (unsigned)(s + 1) * (unsigned)(Hd / 16));
+    if (s + 1 < T) pl_wait(sync, bt, (unsigned)(s + 1) * (unsigned)(Hd / U));
   }
 }
 
-template <typename K>
-static bool pl_fits(K kern, int grid) {
-  // TWO grids must be co-resident (GPU sharing can put two GNMT jobs on one
-  // device); the query is cached per kernel
-  static int cap = -1;
-  if (cap < 0) {
-    int per_cu = 0, dev = 0, cus = 0;
-    if (hipGetDevice(&dev) != hipSuccess ||
-        hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess ||
-        hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kern, 64 * PL_W, 0) != hipSuccess)
-      cap = 0;
-    else
-      cap = per_cu * cus;
+// TWO grids must be co-resident (GPU sharing can put two GNMT jobs on one
+// device); the occupancy query is cached per kernel
+static bool pl_fits(const void* kern, int threads, int grid) {
+  static std::mutex mu;
+  static std::map<const void*, int> cap;
+  std::lock_guard<std::mutex> g(mu);
+  auto it = cap.find(kern);
+  if (it == cap.end()) {
+    int per_cu = 0, dev = 0, cus = 0, c = 0;
+    if (hipGetDevice(&dev) == hipSuccess &&
+        hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess &&
+        hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kern, threads, 0) == hipSuccess)
+      c = per_cu * cus;
+    it = cap.emplace(kern, c).first;
   }
-  return 2 * grid <= cap;
+  return 2 * grid <= it->second;
+}
+
+static int g_pl_ch = 0;   // 0: auto (1), 1 / 2: forced
+void lstm_seq_policy(int ch) { g_pl_ch = ch; }
+
+static int pl_ch(int Hd) {
+  if (g_pl_ch == 1 || g_pl_ch == 2) return g_pl_ch;
+  return 1;   // measured: 2 is slower (latency-bound steps: fwd 220 vs 196, bwd 499 vs 318 us/seq)
+}
+
+template <int KW, int CH>
+static bool pl_fwd(const float* gx, const bf16_t* w_hh, bf16_t* hs, float* cs, float* act, int T, int B,
+                   int Hd, int reverse, unsigned* sync, hipStream_t s) {
+  const int grid = (B / 16) * (Hd / (16 * CH));
+  auto k = lstm_persist_fwd_kernel<KW, CH>;
+  if (!pl_fits((const void*)k, 64 * PL_W * CH, grid)) return false;
+  zero_async(sync + 32, (size_t)(B / 16) * 128, s);
+  hipLaunchKernelGGL(k, dim3(grid), dim3(64 * PL_W * CH), 0, s, gx, w_hh, hs, cs, act, T, B, Hd, reverse,
+                     sync);
+  return true;
+}
+
+template <int KW, int CH>
+static bool pl_bwd(const float* act, const float* cs, const float* dH, const bf16_t* w_hh, bf16_t* dG, int T,
+                   int B, int Hd, int reverse, unsigned* sync, hipStream_t s) {
+  const int grid = (B / 16) * (Hd / (16 * CH));
+  auto k = lstm_persist_bwd_kernel<KW, CH>;
+  if (!pl_fits((const void*)k, 64 * PL_W * CH, grid)) return false;
+  zero_async(sync + 32, (size_t)(B / 16) * 128, s);
+  hipLaunchKernelGGL(k, dim3(grid), dim3(64 * PL_W * CH), 0, s, act, cs, dH, w_hh, dG, T, B, Hd, reverse,
+                     sync);
+  return true;
 }
 
 bool lstm_seq_forward(const float* gx, const bf16_t* w_hh, bf16_t* hs, float* cs, float* act, int T,
                       int B, int Hd, int reverse, unsigned* sync, hipStream_t s) {
   if (T < 1 || B % 16 != 0 || Hd % 256 != 0 || 8 % (B / 16) != 0) return false;
-  const int grid = (B / 16) * (Hd / 16);
-  const int kw = Hd / (32 * PL_W);
-#define PL_FWD(KWV)                                                                        \
-  case KWV:                                                                                \
-    if (!pl_fits(lstm_persist_fwd_kernel<KWV>, grid)) return false;                       \
-    zero_async(sync + 32, (size_t)(B / 16) * 128, s);                                     \
-    hipLaunchKernelGGL(lstm_persist_fwd_kernel<KWV>, dim3(grid), dim3(64 * PL_W), 0, s, gx, w_hh, hs, \
-                       cs, act, T, B, Hd, reverse, sync);                                  \
-    return true;
+  const int kw = Hd / (32 * PL_W), ch = pl_ch(Hd);
+#define PL_F(KWV)                                                                                    \
+  case KWV:                                                                                          \
+    return ch == 2 ? pl_fwd<KWV, 2>(gx, w_hh, hs, cs, act, T, B, Hd, reverse, sync, s)              \
+                   : pl_fwd<KWV, 1>(gx, w_hh, hs, cs, act, T, B, Hd, reverse, sync, s);
   switch (kw) {
-    PL_FWD(1)
-    PL_FWD(2)
-    PL_FWD(4)
+    PL_F(1)
+    PL_F(2)
+    PL_F(4)
     default: return false;
   }
-#undef PL_FWD
+#undef PL_F
 }
 
 bool lstm_seq_backward(const float* act, const float* cs, const float* dH, const bf16_t* w_hh, bf16_t* dG,
                        int T, int B, int Hd, int reverse, unsigned* sync, hipStream_t s) {
   if (T < 1 || B % 16 != 0 || Hd % 256 != 0 || 8 % (B / 16) != 0) return false;
-  const int grid = (B / 16) * (Hd / 16);
-  const int kw = 4 * Hd / (32 * PL_W);
-#define PL_BWD(KWV)                                                                        \
-  case KWV:                                                                                \
-    if (!pl_fits(lstm_persist_bwd_kernel<KWV>, grid)) return false;                       \
-    zero_async(sync + 32, (size_t)(B / 16) * 128, s);                                     \
-    hipLaunchKernelGGL(lstm_persist_bwd_kernel<KWV>, dim3(grid), dim3(64 * PL_W), 0, s, act, cs, dH, \
-                       w_hh, dG, T, B, Hd, reverse, sync);                                 \
-    return true;
+  const int kw = 4 * Hd / (32 * PL_W), ch = pl_ch(Hd);
+#define PL_B(KWV)                                                                                    \
+  case KWV:                                                                                          \
+    return ch == 2 ? pl_bwd<KWV, 2>(act, cs, dH, w_hh, dG, T, B, Hd, reverse, sync, s)              \
+                   : pl_bwd<KWV, 1>(act, cs, dH, w_hh, dG, T, B, Hd, reverse, sync, s);
   switch (kw) {
-    PL_BWD(4)
-    PL_BWD(8)
-    PL_BWD(16)
+    PL_B(4)
+    PL_B(8)
+    PL_B(16)
     default: return false;
   }
-#undef PL_BWD
+#undef PL_B
 }
 
 static int lgrid(long n) { long b = (n + 255) / 256; if (b > 2048) b = 2048; return (int)(b < 1 ? 1 : b); }

@@ -758,11 +758,13 @@ def _lstm_seq_bwd_ref(act, cs, dH, w, reverse):
 
 @pytest.mark.parametrize("T_,B,Hd,reverse", [(12, 64, 1024, False), (12, 64, 1024, True),
                                               (7, 32, 512, False), (5, 128, 256, True)])
-def test_lstm_persistent_sequence(gpu, T_, B, Hd, reverse):
+@pytest.mark.parametrize("ch", [1, 2])
+def test_lstm_persistent_sequence(gpu, T_, B, Hd, reverse, ch):
     """Persistent whole-sequence recurrence (one launch, grid barrier per
     timestep) vs an fp32 torch recurrence: forward h/c/activations and the
     backward gate gradients."""
     torch.manual_seed(21)
+    T().lstm_seq_policy(ch)
     gx = torch.randn(T_, B, 4 * Hd, device=gpu)
     w = (torch.randn(4 * Hd, Hd, device=gpu) / Hd ** 0.5).to(BF)
     hs = torch.empty(T_, B, Hd, device=gpu, dtype=BF)
@@ -781,6 +783,7 @@ def test_lstm_persistent_sequence(gpu, T_, B, Hd, reverse):
     torch.cuda.synchronize()
     assert int(sync[0]) == 0, "grid barrier timed out"
     assert rel_err(dG, _lstm_seq_bwd_ref(act, cs, dH, w, reverse)) < 1e-2
+    T().lstm_seq_policy(0)
 
 
 def test_gnmt_persistent_matches_per_step(gpu):
