@@ -96,18 +96,27 @@ void run_lib(const Tensor& a, bool ak, const Tensor& b, bool bk, const Tensor& c
 
 // 256^2 all-layout kernel; slab split-K (fp32 workspace, one reduce pass,
 // any output dtype) when its tile grid underfills the chip
+// tile / sp < 0: the heuristics (gemm8p_tile, gemm8p_slab_splits); the
+// measured routing passes the (tile, splits) it timed best
 void run_p8(const Tensor& a, bool ak, const Tensor& b, bool bk, int64_t M, int64_t N, int64_t K,
-            const tam::Epi& ep, bool allow_split) {
-  const int tile = tam::gemm8p_tile((int)M, (int)N, (int)K);
-  const int sp = tam::gemm8p_slab_splits((int)M, (int)N, (int)K, tile);
+            const tam::Epi& ep, bool allow_split, int tile = -1, int sp = -1) {
+  const bool explicit_cfg = tile > 0;
+  if (tile < 0) tile = tam::gemm8p_tile((int)M, (int)N, (int)K);
+  if (sp < 0) sp = tam::gemm8p_slab_splits((int)M, (int)N, (int)K, tile);
   if (sp > 1 && ep.ldc >= N) {
     Tensor ws = at::empty({sp, M, N}, a.options().dtype(at::kFloat));
     tam::gemm8p_splitk(bp(a), a.stride(0), ak, bp(b), b.stride(0), bk, (int)M, (int)N, (int)K, ep, sp,
                        ws.data_ptr<float>(), cur_stream(a), tile);
     return;
   }
-  run_mfma(a, ak, b, bk, M, N, K, ep, allow_split, 3);
+  if (explicit_cfg)
+    tam::launch_gemm8p(bp(a), a.stride(0), ak, bp(b), b.stride(0), bk, (int)M, (int)N, (int)K, ep, 1,
+                       cur_stream(a), 0, tile);
+  else
+    run_mfma(a, ak, b, bk, M, N, K, ep, allow_split, 3);
 }
+// measured (tile, splits) of the p8 route per key
+std::map<GemmKey, std::pair<int, int>> g_p8_cfg;
 
 float time_ms(hipStream_t s, const std::function<void()>& fn) {
   fn();   // warm (library heuristics / our first launch)
@@ -218,8 +227,25 @@ void gemm_op(const Tensor& a, bool a_kmajor, const Tensor& b, bool b_kmajor, con
     es.ldc = scratch.stride(0);
     std::array<float, 4> t{1e30f, 1e30f, 1e30f, 1e30f};
     t[0] = time_ms(s, [&] { run_mfma(a, a_kmajor, b, b_kmajor, M, N, K, es, allow_split, 0); });
-    if (p8_ok)
-      t[3] = time_ms(s, [&] { run_p8(a, a_kmajor, b, b_kmajor, M, N, K, es, allow_split); });
+    std::pair<int, int> p8c{-1, -1};
+    if (p8_ok) {
+      // both tiles, each with its slab split (and the 256^2 tile also with
+      // twice that split): the heuristics alone left 3200x2048x32000 on an
+      // unsplit 128^2 grid at ~540 TF/s
+      std::vector<std::pair<int, int>> cands;
+      for (int tl : {256, 128}) {
+        const int sp = tam::gemm8p_slab_splits((int)M, (int)N, (int)K, tl);
+        cands.push_back({tl, sp});
+        if (tl == 256 && sp > 1 && sp * 2 <= 16 && K / 64 / (sp * 2) >= 8) cands.push_back({tl, sp * 2});
+        if (tl == 256 && sp == 1 && (long)((M + 255) / 256) * ((N + 255) / 256) < 150 && K / 64 >= 32)
+          cands.push_back({tl, 2});
+      }
+      for (const auto& c : cands) {
+        const float ms = time_ms(s, [&] { run_p8(a, a_kmajor, b, b_kmajor, M, N, K, es, allow_split, c.first,
+                                                 c.second); });
+        if (ms < t[3]) { t[3] = ms; p8c = c; }
+      }
+    }
     if (dma_ok)
       t[2] = time_ms(s, [&] { run_mfma(a, a_kmajor, b, b_kmajor, M, N, K, es, allow_split, 2); });
     if (lib_ok) {
@@ -237,9 +263,16 @@ void gemm_op(const Tensor& a, bool a_kmajor, const Tensor& b, bool b_kmajor, con
     std::lock_guard<std::mutex> g(g_route_mu);
     g_route[key] = route;
     g_route_ms[key] = t;
+    g_p8_cfg[key] = p8c;
+  }
+  std::pair<int, int> p8c{-1, -1};
+  if (route == 3) {
+    std::lock_guard<std::mutex> g(g_route_mu);
+    auto it = g_p8_cfg.find(key);
+    if (it != g_p8_cfg.end()) p8c = it->second;
   }
   if (route == 1) run_lib(a, a_kmajor, b, b_kmajor, c, mode, bias);
-  else if (route == 3) run_p8(a, a_kmajor, b, b_kmajor, M, N, K, ep, allow_split);
+  else if (route == 3) run_p8(a, a_kmajor, b, b_kmajor, M, N, K, ep, allow_split, p8c.first, p8c.second);
   else run_mfma(a, a_kmajor, b, b_kmajor, M, N, K, ep, allow_split, route);
 }
 

@@ -3,12 +3,14 @@ on one MI355X node, one process per GPU.
 
 Topology (SPMD, ``torch.distributed``):
   * world NCCL (= RCCL over xGMI) group over all N ranks — DDP gangs get
-    sub-communicators (``new_group``, created in the same order on every
-    rank because every rank applies the same broadcast plan), state moves
-    use xGMI P2P (``batch_isend_irecv``);
-  * a gloo control group carries the round plan (broadcast) and the worker
-    reports (gather) — the heartbeat: a rank that stops reporting trips the
-    gloo timeout and the controller aborts the replay (failure detection).
+    member-only communicators (``parallel/gang.py``: c10d backends over a
+    store prefix, hierarchical "spread" transport across virtual nodes),
+    state moves use xGMI P2P (``batch_isend_irecv``);
+  * the control plane (``control.py``) carries the round plan and the worker
+    reports as TCPStore keys, with per-worker heartbeat threads: a rank whose
+    report and heartbeat both stop for ``hb_timeout`` seconds is declared
+    lost and the controller re-plans around it (``Controller.rank_lost``);
+    the gloo-collective plane is kept for comparison.
 
 Rank 0 additionally runs the CONTROLLER: the same Policy / Placement /
 Cluster objects as the simulator (``LiveScheduler`` subclasses the event
@@ -21,8 +23,9 @@ preemption never interrupts an in-flight collective.
 Preemption = suspension in HBM: the job's ``Trainer`` (flat param arena +
 optimizer state, 288 GB per GPU leaves plenty of room) stays resident on its
 ranks; resuming on the same GPUs is a pointer swap, resuming elsewhere moves
-the flat buffers GPU->GPU over xGMI; with ``spill_host`` the state goes to
-pinned host DRAM through the native checkpoint engine instead.
+the flat buffers GPU->GPU over xGMI. ``ckpt_policy=pressure`` spills the
+suspended jobs the scheduler will resume last, asynchronously, only when a
+starting job needs their HBM; ``host`` spills every preempted job.
 """
 from __future__ import annotations
 
