@@ -198,9 +198,12 @@ def test_bench_cpu_driver_contract(tmp_path):
 
     root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
     t = _t.perf_counter()
+    # few host threads: under a parallel test run an oversubscribed torch
+    # thread pool (not the bench) dominates the wall time
+    env = dict(os.environ, OMP_NUM_THREADS="2")
     r = subprocess.run([sys.executable, os.path.join(root, "bench.py"), "--cpu", "--steps", "20",
                         "--warmup", "5", "--jobs-per-gpu", "48", "--work-s", "0.05", "--min-iters", "1"],
-                       capture_output=True, text=True, timeout=240, cwd=str(tmp_path))
+                       capture_output=True, text=True, timeout=240, cwd=str(tmp_path), env=env)
     wall = _t.perf_counter() - t
     assert r.returncode == 0, r.stderr[-3000:]
     lines = [x for x in r.stdout.splitlines() if x.startswith("{")]

@@ -98,20 +98,38 @@ class StorePlane:
         return time.time() - float(self.store.get(k).decode())
 
     # ----------------------------------------------------------- plan / reports
+    def _retry(self, fn, what: str, attempts: int = 3):
+        """Run a store operation; a dropped connection (seen under heavy host
+        load when a peer process dies) reconnects and retries before the
+        controller is declared lost."""
+        for i in range(attempts):
+            try:
+                return fn()
+            except Exception as e:                # DistNetworkError / DistStoreError
+                if i + 1 == attempts:
+                    raise ControllerLost(f"{what}: {e}") from e
+                time.sleep(0.2 * (i + 1))
+                try:
+                    self.store = _store_client(self.plan_timeout)
+                except Exception:
+                    pass
+
     def bcast(self, plan, rnd: int):
         key = f"{self.prefix}/plan/{rnd}"
         if self.rank == 0:
-            self.store.set(key, pickle.dumps(plan))
+            self._retry(lambda: self.store.set(key, pickle.dumps(plan)), f"publish plan {rnd}")
             return plan
-        try:
+
+        def _get():
             self.store.wait([key], timedelta(seconds=self.plan_timeout))
-        except Exception as e:
-            raise ControllerLost(f"no plan for round {rnd}: {e}") from e
-        return pickle.loads(self.store.get(key))
+            return self.store.get(key)
+
+        return pickle.loads(self._retry(_get, f"no plan for round {rnd}"))
 
     def gather(self, rep, rnd: int, alive: Sequence[int]) -> Tuple[Optional[List], List[int]]:
         if self.rank != 0:
-            self.store.set(f"{self.prefix}/rep/{rnd}/{self.rank}", pickle.dumps(rep))
+            data = pickle.dumps(rep)
+            self._retry(lambda: self.store.set(f"{self.prefix}/rep/{rnd}/{self.rank}", data), f"report {rnd}")
             return None, []
         reps: List = [None] * self.world
         reps[0] = rep
