@@ -311,8 +311,10 @@ tam::ConvGeom geom(const Tensor& x, const Tensor& w, const Tensor& y, int64_t st
   return g;
 }
 
-void conv_fwd_op(const Tensor& x, const Tensor& w, const Tensor& y, int64_t stride, int64_t pad,
-                 int64_t dil, const optional<Tensor>& bias, bool relu) {
+// stats (optional, fp32 [>= ceil(M/128)][2K]): BatchNorm partial sums of y
+// from the conv epilogue; returns the rows written (0: none, BN reduces y)
+int64_t conv_fwd_op(const Tensor& x, const Tensor& w, const Tensor& y, int64_t stride, int64_t pad,
+                    int64_t dil, const optional<Tensor>& bias, bool relu, const optional<Tensor>& stats) {
   check_bf16(x, "x"); check_bf16(w, "w"); check_bf16(y, "y");
   check_contig(x, "x"); check_contig(w, "w"); check_contig(y, "y");
   tam::ConvGeom g = geom(x, w, y, stride, pad, dil);
@@ -320,7 +322,14 @@ void conv_fwd_op(const Tensor& x, const Tensor& w, const Tensor& y, int64_t stri
   ep.c = y.data_ptr(); ep.ldc = g.K; ep.c_f32 = 0; ep.mode = 0;
   ep.bias = opt_ptr<const tam::bf16_t>(bias);
   ep.relu = relu;
-  tam::conv_fwd(bp(x), bp(w), g, ep, cur_stream(x));
+  if (stats.has_value() && stats->defined()) {
+    check_f32(*stats, "stats");
+    const int64_t M = (int64_t)g.N * g.P * g.Q;
+    TORCH_CHECK(stats->is_contiguous() && stats->numel() >= (M + 127) / 128 * 2 * g.K,
+                "tam.conv_fwd: stats must hold ceil(M/128) x 2K floats");
+    ep.stats = stats->data_ptr<float>();
+  }
+  return tam::conv_fwd(bp(x), bp(w), g, ep, cur_stream(x));
 }
 
 void conv_dgrad_op(const Tensor& dy, const Tensor& w, const Tensor& wt, const Tensor& dx,
@@ -395,18 +404,26 @@ void conv_wgrad_op(const Tensor& dy, const Tensor& x, const Tensor& dw, int64_t 
 void bn_forward_op(const Tensor& x, const optional<Tensor>& res, const Tensor& y, const Tensor& gamma,
                    const Tensor& beta, const optional<Tensor>& run_mean,
                    const optional<Tensor>& run_var, const Tensor& save_mean,
-                   const Tensor& save_rstd, double eps, double momentum, bool relu) {
+                   const Tensor& save_rstd, double eps, double momentum, bool relu,
+                   const optional<Tensor>& part, int64_t nblk) {
   check_bf16(x, "x"); check_bf16(y, "y"); check_contig(x, "x"); check_contig(y, "y");
   check_f32(gamma, "gamma"); check_f32(beta, "beta");
   const int64_t C = x.size(-1);
   const int64_t M = x.numel() / C;
   TORCH_CHECK(C % 8 == 0 && C <= 2048, "tam.bn: C must be a multiple of 8 and <= 2048");
+  const float* part_in = nullptr;
+  if (part.has_value() && part->defined() && nblk > 0) {
+    check_f32(*part, "part");
+    TORCH_CHECK(part->is_contiguous() && part->numel() >= nblk * 2 * C, "tam.bn_forward: partial rows");
+    part_in = part->data_ptr<float>();
+  }
   Tensor ws_f = at::empty({(6 + 2 * tam::BN_MAX_BLOCKS) * C}, x.options().dtype(at::kFloat));
   if (res.has_value() && res->defined()) { check_bf16(*res, "res"); check_contig(*res, "res"); }
   tam::bn_forward(bp(x), opt_ptr<const tam::bf16_t>(res), bpm(y), M, (int)C, (float)eps,
                   (float)momentum, gamma.data_ptr<float>(), beta.data_ptr<float>(),
                   opt_ptr<float>(run_mean), opt_ptr<float>(run_var), save_mean.data_ptr<float>(),
-                  save_rstd.data_ptr<float>(), ws_f.data_ptr<float>(), relu, cur_stream(x));
+                  save_rstd.data_ptr<float>(), ws_f.data_ptr<float>(), relu, part_in, (int)nblk,
+                  cur_stream(x));
 }
 
 void bn_backward_op(const Tensor& dy, const optional<Tensor>& y, const Tensor& x, const Tensor& mean,
@@ -709,12 +726,12 @@ void lstm_bwd_op(const Tensor& act, const optional<Tensor>& c_prev, const option
 
 TORCH_LIBRARY(tam, m) {
   m.def("gemm(Tensor a, bool a_kmajor, Tensor b, bool b_kmajor, Tensor(a!) c, int mode, Tensor? bias, bool relu, Tensor? mask, float alpha, bool allow_split) -> ()", &gemm_op);
-  m.def("conv_fwd(Tensor x, Tensor w, Tensor(a!) y, int stride, int pad, int dil, Tensor? bias, bool relu) -> ()", &conv_fwd_op);
+  m.def("conv_fwd(Tensor x, Tensor w, Tensor(a!) y, int stride, int pad, int dil, Tensor? bias, bool relu, Tensor(b!)? stats=None) -> int", &conv_fwd_op);
   m.def("conv_dgrad(Tensor dy, Tensor w, Tensor(a!) wt, Tensor(b!) dx, int stride, int pad, int dil, Tensor? mask) -> ()", &conv_dgrad_op);
   m.def("conv_weight_t_batch(Tensor[] w, Tensor(a!)[] wt) -> ()", &conv_weight_t_batch_op);
   m.def("conv_dgrad_pre(Tensor dy, Tensor w, Tensor wt, Tensor(a!) dx, int stride, int pad, int dil, Tensor? mask) -> ()", &conv_dgrad_pre_op);
   m.def("conv_wgrad(Tensor dy, Tensor x, Tensor(a!) dw, int stride, int pad, int dil, int mode) -> ()", &conv_wgrad_op);
-  m.def("bn_forward(Tensor x, Tensor? res, Tensor(a!) y, Tensor gamma, Tensor beta, Tensor(b!)? run_mean, Tensor(c!)? run_var, Tensor(d!) save_mean, Tensor(e!) save_rstd, float eps, float momentum, bool relu) -> ()", &bn_forward_op);
+  m.def("bn_forward(Tensor x, Tensor? res, Tensor(a!) y, Tensor gamma, Tensor beta, Tensor(b!)? run_mean, Tensor(c!)? run_var, Tensor(d!) save_mean, Tensor(e!) save_rstd, float eps, float momentum, bool relu, Tensor? part=None, int nblk=0) -> ()", &bn_forward_op);
   m.def("bn_backward(Tensor dy, Tensor? y, Tensor x, Tensor mean, Tensor rstd, Tensor gamma, Tensor(a!) dx, Tensor(b!)? dres, Tensor(c!)? dgamma, Tensor(d!)? dbeta, bool relu, Tensor? addend=None) -> ()", &bn_backward_op);
   m.def("ln_forward(Tensor x, Tensor g, Tensor b, Tensor(a!) y, Tensor(b!) mean, Tensor(c!) rstd, float eps) -> ()", &ln_forward_op);
   m.def("ln_backward(Tensor dy, Tensor x, Tensor g, Tensor mean, Tensor rstd, Tensor(a!) dx, Tensor(b!) dg, Tensor(c!) db, Tensor? addend=None) -> ()", &ln_backward_op);

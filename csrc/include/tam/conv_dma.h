@@ -210,7 +210,14 @@ __global__ void __launch_bounds__(BM / 64 * 64 * WN, 1) conv_dma_kernel(CDArgs a
     // stores from the MFMA C layout.
     constexpr int LDW = WCOLS + 8;                 // padded slab row (bf16)
     constexpr int CPR = WCOLS / 8, NCH = 32 * CPR / 64;
+    static_assert(64 % CPR == 0, "a lane keeps one 8-channel chunk");
     bf16_t* slab = (bf16_t*)(smem + wid * (32 * LDW * 2));
+    // BN statistics of the stored tile (ep.stats): each lane owns channel
+    // chunk lane % CPR for every row it stores
+    const bool stats = ep.stats != nullptr;
+    float ssum[8], ssq[8];
+#pragma unroll
+    for (int e = 0; e < 8; ++e) ssum[e] = ssq[e] = 0.f;
     float bv[TN];
 #pragma unroll
     for (int j = 0; j < TN; ++j)
@@ -262,9 +269,48 @@ __global__ void __launch_bounds__(BM / 64 * 64 * WN, 1) conv_dma_kernel(CDArgs a
                                bf2f((bf16_t)(vw[e] >> 16)) + bf2f((bf16_t)(ow[e] >> 16)));
           }
           *(uint4*)dst = v;
+          if (stats) {
+            const uint32_t* vw = (const uint32_t*)&v;
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+              const float lo = bf2f((bf16_t)(vw[e] & 0xffff)), hi = bf2f((bf16_t)(vw[e] >> 16));
+              ssum[2 * e] += lo; ssq[2 * e] += lo * lo;
+              ssum[2 * e + 1] += hi; ssq[2 * e + 1] += hi * hi;
+            }
+          }
         }
       }
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    }
+    if (stats) {
+      // lanes sharing a chunk -> the wave's 64 rows; then the WM waves of
+      // one column slice in LDS (past the slabs), one partial row per M-tile
+#pragma unroll
+      for (int o = CPR; o < 64; o <<= 1)
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+          ssum[e] += __shfl_xor(ssum[e], o, 64);
+          ssq[e] += __shfl_xor(ssq[e], o, 64);
+        }
+      float* red = (float*)(smem + W * 32 * LDW * 2);      // [W][2 * WCOLS]
+      if (lane < CPR) {
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+          red[wid * 2 * WCOLS + lane * 8 + e] = ssum[e];
+          red[wid * 2 * WCOLS + WCOLS + lane * 8 + e] = ssq[e];
+        }
+      }
+      __syncthreads();
+      if (wm == 0) {
+        float* prow = ep.stats + (long)tm * 2 * a.Ng;
+        for (int e = lane; e < 2 * WCOLS; e += 64) {
+          float t = 0.f;
+#pragma unroll
+          for (int k = 0; k < WM; ++k) t += red[(k + WM * wn) * 2 * WCOLS + e];
+          if (e < WCOLS) prow[cbase + e] = t;
+          else prow[a.Ng + cbase + (e - WCOLS)] = t;
+        }
+      }
     }
     return;
   }
@@ -317,20 +363,22 @@ inline int conv_dma_pick_bn(int M, int Ng, int Kd, int force) {
   return pick;
 }
 
-inline bool launch_conv_dma(const CDArgs& a, const Epi& ep, hipStream_t s, int force = 0) {
+// returns 0 (not for this core) or the tile height BM of the launch (the
+// number of BN-statistics partial rows is ceil(M / BM))
+inline int launch_conv_dma(const CDArgs& a, const Epi& ep, hipStream_t s, int force = 0) {
   // Kd >= 256: with fewer than 4 K-tiles the ring never fills (1x1 convs over
   // 64/128 channels measured slower than the igemm) — unless forced (tests,
   // strided-dgrad parity classes, where the igemm alternative is far worse)
-  if (a.Cs % 64 != 0 || a.Kd % 64 != 0 || a.Kd < 64 || (a.Kd < 256 && !force)) return false;
-  if (a.ntaps < 1 || a.ntaps > 9) return false;
-  if ((long)a.Hs * a.Ws * a.Cs * ((a.M + a.P * a.Q - 1) / (a.P * a.Q)) >= (1L << 31)) return false;
-  if ((long)a.Ng * a.ldb >= (1L << 31)) return false;
+  if (a.Cs % 64 != 0 || a.Kd % 64 != 0 || a.Kd < 64 || (a.Kd < 256 && !force)) return 0;
+  if (a.ntaps < 1 || a.ntaps > 9) return 0;
+  if ((long)a.Hs * a.Ws * a.Cs * ((a.M + a.P * a.Q - 1) / (a.P * a.Q)) >= (1L << 31)) return 0;
+  if ((long)a.Ng * a.ldb >= (1L << 31)) return 0;
   const int pick = conv_dma_pick_bn(a.M, a.Ng, a.Kd, force);
-  if (!pick) return false;
+  if (!pick) return 0;
   if (pick & 0x1000) {
     const int tiles = ((a.M + 127) / 128) * (a.Ng / 128);
     hipLaunchKernelGGL((conv_dma_kernel<128, 2, 128>), dim3(tiles), dim3(256), 0, s, a, ep);
-    return true;
+    return 128;
   }
   const int bn = pick;
   const int tiles = ((a.M + 255) / 256) * (a.Ng / bn);
@@ -345,7 +393,7 @@ inline bool launch_conv_dma(const CDArgs& a, const Epi& ep, hipStream_t s, int f
       hipLaunchKernelGGL((conv_dma_kernel<64, 1>), dim3(tiles), dim3(256), 0, s, a, ep);
       break;
   }
-  return true;
+  return 256;
 }
 
 // argument builders (host)

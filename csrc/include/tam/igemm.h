@@ -40,7 +40,10 @@ struct Epi {
   const bf16_t* mask = nullptr;  // relu-backward mask: zero where mask<=0
   long ldm = 0;
   float alpha = 1.f;
-  long zstride = 0;         // mode 3: fp32 slab store at c + blockIdx.z * zstride (split-K slabs)
+  long zstride = 0;
+  // conv_dma bf16 epilogue only: per-channel BatchNorm partial sums of the
+  // stored outputs, one row per M-tile: stats[tm][0..N) = sum, [N..2N) = sum sq
+  float* stats = nullptr;         // mode 3: fp32 slab store at c + blockIdx.z * zstride (split-K slabs)
 };
 
 // ---------------------------------------------------------------------------

@@ -19,7 +19,7 @@ void col_reduce_acc(const float* part, int nblk, int W, float* out0, float* out1
 void bn_forward(const bf16_t* x, const bf16_t* res, bf16_t* y, long M, int C, float eps,
                 float momentum, const float* gamma, const float* beta, float* run_mean,
                 float* run_var, float* save_mean, float* save_rstd, float* ws_f, int relu,
-                hipStream_t s);
+                const float* part_in, int nblk_in, hipStream_t s);
 void bn_infer(const bf16_t* x, const bf16_t* res, bf16_t* y, long M, int C, const float* scale,
               const float* shift, int relu, hipStream_t s);
 // batched conv weight re-layout [K][RS][C] -> [C][RS][K] (one launch)

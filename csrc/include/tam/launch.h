@@ -24,7 +24,7 @@ void gemm8p_policy(int mode, int sched);
 int gemm8p_policy_mode();
 
 // NHWC convolutions, weights [K][R][S][C] (C, K multiples of 8)
-void conv_fwd(const bf16_t* x, const bf16_t* w, const ConvGeom& g, Epi ep, hipStream_t s);
+int conv_fwd(const bf16_t* x, const bf16_t* w, const ConvGeom& g, Epi ep, hipStream_t s);
 // dx[N*H*W][C]; wt = conv_weight_t(w) laid out [C][R][S][K] (ignored for 1x1/s1)
 void conv_dgrad(const bf16_t* dy, const bf16_t* w, const bf16_t* wt, const ConvGeom& g, Epi ep,
                 hipStream_t s);

@@ -35,15 +35,19 @@ static bool is_pointwise(const ConvGeom& g) {
   return g.R == 1 && g.S == 1 && g.stride == 1 && g.pad == 0;
 }
 
-void conv_fwd(const bf16_t* x, const bf16_t* w, const ConvGeom& g, Epi ep, hipStream_t s) {
+// returns the number of BN-statistics partial rows written to ep.stats (0:
+// the path taken computes none; the BN then reduces the output itself)
+int conv_fwd(const bf16_t* x, const bf16_t* w, const ConvGeom& g, Epi ep, hipStream_t s) {
   const int M = g.N * g.P * g.Q, Kd = g.R * g.S * g.C;
   if (g_conv_dma && g.dil == 1) {
     CDArgs a = cd_fwd_args(x, w, g);
-    if (launch_conv_dma(a, ep, s, g_conv_dma >= 2 ? g_conv_dma - 1 : 0)) return;
+    const int bm = launch_conv_dma(a, ep, s, g_conv_dma >= 2 ? g_conv_dma - 1 : 0);
+    if (bm) return ep.stats ? (M + bm - 1) / bm : 0;
   }
+  ep.stats = nullptr;
   if (is_pointwise(g)) {
     gemm(x, g.C, true, w, g.C, true, M, g.K, g.C, ep, false, s);
-    return;
+    return 0;
   }
   TileChoice t = choose_tiles(M, g.K, Kd, false);
   switch (t.cfg) {
@@ -52,6 +56,7 @@ void conv_fwd(const bf16_t* x, const bf16_t* w, const ConvGeom& g, Epi ep, hipSt
     case 2: fwd_tile<64, 128>(x, w, g, ep, 1, s); break;
     default: fwd_tile<64, 64>(x, w, g, ep, 1, s); break;
   }
+  return 0;
 }
 
 template <int BM, int BN>

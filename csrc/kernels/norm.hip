@@ -434,14 +434,20 @@ static long bn_rows_per_block(long M, int C) {
 void bn_forward(const bf16_t* x, const bf16_t* res, bf16_t* y, long M, int C, float eps,
                 float momentum, const float* gamma, const float* beta, float* run_mean,
                 float* run_var, float* save_mean, float* save_rstd, float* ws_f, int relu,
-                hipStream_t s) {
+                const float* part_in, int nblk_in, hipStream_t s) {
   // ws_f: 2*C floats scale/shift | 2*C doubles column sums | BN_MAX_BLOCKS*2*C partials
+  // part_in: [nblk_in][2C] partial rows already produced (conv epilogue): no stats pass
   const long rpb = bn_rows_per_block(M, C);
-  const int nb = (int)((M + rpb - 1) / rpb);
+  int nb = (int)((M + rpb - 1) / rpb);
   double* sums = (double*)(ws_f + 2 * C);
-  float* part = ws_f + 6 * C;
+  const float* part = ws_f + 6 * C;
   (void)sums;
-  hipLaunchKernelGGL(bn_stats_kernel, dim3(nb), dim3(256), 0, s, x, M, C, rpb, part);
+  if (part_in && nblk_in > 0) {
+    part = part_in;
+    nb = nblk_in;
+  } else {
+    hipLaunchKernelGGL(bn_stats_kernel, dim3(nb), dim3(256), 0, s, x, M, C, rpb, ws_f + 6 * C);
+  }
   hipLaunchKernelGGL(bn_reduce_finalize_kernel<0>, dim3((C + 15) / 16), dim3(256), 0, s, part, nb, M,
                      C, eps, momentum, gamma, beta, save_mean, save_rstd, ws_f, ws_f + C, run_mean,
                      run_var);

@@ -451,6 +451,45 @@ def test_batchnorm_backward_addend(gpu, relu):
         assert rel_err(u, v) < 1e-2
 
 
+@pytest.mark.parametrize("policy", [1, 3])
+@pytest.mark.parametrize("shape", [(8, 28, 28, 128, 256, 3, 1, 1), (16, 14, 14, 256, 1024, 1, 1, 0),
+                                   (4, 56, 56, 64, 64, 3, 1, 1), (8, 28, 28, 256, 512, 1, 2, 0)])
+def test_conv_fwd_bn_stats(gpu, shape, policy):
+    """BatchNorm partial sums from the conv epilogue == column sums / sums of
+    squares of the stored bf16 output; and bn_forward over those partials ==
+    bn_forward computing its own statistics."""
+    torch.manual_seed(8)
+    N, H, W, C, K, R, st, pd = shape
+    x = torch.randn(N, H, W, C, device=gpu).to(BF)
+    w = (torch.randn(K, R, R, C, device=gpu) / (R * R * C) ** 0.5).to(BF)
+    P = (H + 2 * pd - R) // st + 1
+    y = torch.empty(N, P, P, K, device=gpu, dtype=BF)
+    part = torch.empty((N * P * P + 127) // 128, 2 * K, device=gpu)
+    T().conv_dma_policy(policy)
+    try:
+        nblk = T().conv_fwd(x, w, y, st, pd, 1, None, False, part)
+    finally:
+        T().conv_dma_policy(1)
+    if nblk == 0:
+        pytest.skip("shape not on the LDS-DMA conv core")
+    yf = y.float().reshape(-1, K)
+    s = part[:nblk].sum(0)
+    assert rel_err(s[:K], yf.sum(0)) < 1e-4 and rel_err(s[K:], (yf * yf).sum(0)) < 1e-4
+    g = torch.rand(K, device=gpu) + 0.5
+    b = torch.randn(K, device=gpu)
+    outs = []
+    for use in (True, False):
+        o = torch.empty_like(y)
+        mean, rstd = torch.empty(K, device=gpu), torch.empty(K, device=gpu)
+        if use:
+            T().bn_forward(y, None, o, g, b, None, None, mean, rstd, 1e-5, 0.1, True, part, nblk)
+        else:
+            T().bn_forward(y, None, o, g, b, None, None, mean, rstd, 1e-5, 0.1, True)
+        outs.append((o, mean, rstd))
+    for u, v in zip(*outs):
+        assert rel_err(u, v) < 1e-3
+
+
 def test_conv_weight_t_batch(gpu):
     """All conv weights re-laid [K,R,S,C] -> [C,R,S,K] in one launch (odd
     sizes included) vs torch.permute."""

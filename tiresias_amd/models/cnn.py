@@ -90,7 +90,7 @@ class ResNet50:
 
     def forward(self, x: torch.Tensor) -> torch.Tensor:
         Fx.prepare_conv_wt(self.conv_params())
-        y = Fx.conv2d(x, self.stem, stride=2, pad=3)
+        y = Fx.conv2d(x, self.stem, stride=2, pad=3, bn_stats=True)
         y = self._bn(y, self.stem_bn, "stem", relu=True)
         y = Fx.maxpool2d(y, 3, 2, 1)
         for blk in self.blocks:
@@ -98,13 +98,13 @@ class ResNet50:
             # the second consumer of y (residual / downsample) goes through a
             # tap: its gradient is summed inside y's producing BN backward
             idn = Fx.residual_tap(y) if "down" not in blk else None
-            o = Fx.conv2d(y, blk["c1"])
+            o = Fx.conv2d(y, blk["c1"], bn_stats=True)
             o = self._bn(o, blk["bn1"], pre + ".bn1", relu=True)
-            o = Fx.conv2d(o, blk["c2"], stride=blk["stride"], pad=1)
+            o = Fx.conv2d(o, blk["c2"], stride=blk["stride"], pad=1, bn_stats=True)
             o = self._bn(o, blk["bn2"], pre + ".bn2", relu=True)
-            o = Fx.conv2d(o, blk["c3"])
+            o = Fx.conv2d(o, blk["c3"], bn_stats=True)
             if "down" in blk:
-                idn = Fx.conv2d(Fx.residual_tap(y), blk["down"], stride=blk["stride"])
+                idn = Fx.conv2d(Fx.residual_tap(y), blk["down"], stride=blk["stride"], bn_stats=True)
                 idn = self._bn(idn, blk["down_bn"], pre + ".dbn", relu=False)
             y = self._bn(o, blk["bn3"], pre + ".bn3", relu=True, res=idn)
         y = Fx.global_avgpool(y)

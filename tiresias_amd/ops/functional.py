@@ -218,13 +218,20 @@ def _conv_out(h: int, k: int, s: int, p: int, d: int = 1) -> int:
 class _Conv(Function):
     @staticmethod
     def forward(ctx, x, token, w: Param, b: Optional[Param], stride: int, pad: int, relu: bool,
-                in_relu: bool, mask_own_relu: bool):
+                in_relu: bool, mask_own_relu: bool, bn_stats: bool = False):
         N, H, W, C = x.shape
         K, R, S, _ = w.shape
         P, Q = _conv_out(H, R, stride, pad), _conv_out(W, S, stride, pad)
+        part = None
         if x.is_cuda:
             y = torch.empty(N, P, Q, K, dtype=BF16, device=x.device)
-            _T().conv_fwd(x, w.w, y, stride, pad, 1, b.w if b is not None else None, relu)
+            if bn_stats:
+                # BatchNorm partial sums from the conv epilogue (no stats pass)
+                part = torch.empty((N * P * Q + 127) // 128, 2 * K, dtype=torch.float32, device=x.device)
+                nblk = _T().conv_fwd(x, w.w, y, stride, pad, 1, b.w if b is not None else None, relu, part)
+                part = (part, nblk) if nblk > 0 else None
+            else:
+                _T().conv_fwd(x, w.w, y, stride, pad, 1, b.w if b is not None else None, relu)
         else:
             yf = F.conv2d(x.float().permute(0, 3, 1, 2), w.w.float().permute(0, 3, 1, 2),
                           b.w.float() if b is not None else None, stride=stride, padding=pad)
@@ -233,6 +240,7 @@ class _Conv(Function):
             y = yf.permute(0, 2, 3, 1).contiguous().to(BF16)
         ctx.w, ctx.b, ctx.stride, ctx.pad, ctx.in_relu = w, b, stride, pad, in_relu
         ctx.save_for_backward(x, y if (relu and mask_own_relu) else None)
+        ctx.part = part
         return y
 
     @staticmethod
@@ -279,7 +287,7 @@ class _Conv(Function):
         w.grad_ready()
         if b is not None:
             b.grad_ready()
-        return dx, None, None, None, None, None, None, None, None
+        return dx, None, None, None, None, None, None, None, None, None
 
 
 def prepare_conv_wt(params: List[Param]) -> None:
@@ -296,11 +304,19 @@ def prepare_conv_wt(params: List[Param]) -> None:
 
 
 def conv2d(x: torch.Tensor, w: Param, b: Optional[Param] = None, stride: int = 1, pad: int = 0,
-           relu: bool = False, in_relu: bool = False, mask_own_relu: bool = True) -> torch.Tensor:
-    """NHWC conv, weights [K,R,S,C]."""
+           relu: bool = False, in_relu: bool = False, mask_own_relu: bool = True,
+           bn_stats: bool = False) -> torch.Tensor:
+    """NHWC conv, weights [K,R,S,C]. ``bn_stats``: the output feeds a
+    BatchNorm -- its per-channel partial sums come from the conv epilogue
+    (where the conv path supports it) and ride on the output tensor."""
     if not x.is_contiguous():
         x = x.contiguous()
-    return _Conv.apply(x, w.arena.token, w, b, stride, pad, relu, in_relu, mask_own_relu)
+    y = _Conv.apply(x, w.arena.token, w, b, stride, pad, relu, in_relu, mask_own_relu, bn_stats)
+    if bn_stats and y.is_cuda and y.grad_fn is not None:
+        part = getattr(y.grad_fn, "part", None)
+        if part is not None:
+            y._tam_bnpart = part
+    return y
 
 
 # ============================================================ BatchNorm (NHWC)
@@ -350,8 +366,13 @@ class _BN(Function):
             if training:
                 mean = torch.empty(C, dtype=torch.float32, device=x.device)
                 rstd = torch.empty_like(mean)
-                _T().bn_forward(x, res, y, g.master, b.master, run_mean, run_var, mean, rstd, eps,
-                                momentum, relu)
+                part = getattr(x, "_tam_bnpart", None)
+                if part is not None:
+                    _T().bn_forward(x, res, y, g.master, b.master, run_mean, run_var, mean, rstd, eps,
+                                    momentum, relu, part[0], part[1])
+                else:
+                    _T().bn_forward(x, res, y, g.master, b.master, run_mean, run_var, mean, rstd, eps,
+                                    momentum, relu)
             else:
                 rstd_i = torch.rsqrt(run_var + eps)
                 scale = g.master * rstd_i
