@@ -122,3 +122,35 @@ def test_gnmt_branch_streams_match(gpu, overlap):
     torch.cuda.synchronize()
     assert abs(lg - le) < 2e-2 * max(1.0, abs(le))
     assert rel(g.arena.master, e.arena.master) < 1e-3
+
+
+def test_ddp_bucket_event_timing(gpu, monkeypatch):
+    """GradBucketer records hipEvents around every step's gradient sync and
+    poll_timing() turns finished steps into exposed / span seconds (a
+    stand-in 2-rank comm: the event plumbing, not RCCL, is under test)."""
+    from tiresias_amd.ops.arena import Arena
+    from tiresias_amd.parallel import ddp as D
+
+    class FakeComm:
+        def start(self, view):
+            view.mul_(2.0)
+            return None
+
+        def finish(self, works):
+            pass
+
+    monkeypatch.setattr(D.dist, "is_initialized", lambda: True)
+    monkeypatch.setattr(D, "as_comm", lambda g: g)
+    monkeypatch.setattr(D, "comm_size", lambda c: 2)
+    A = Arena(gpu)
+    p = A.add("w", (4096, 1024))
+    A.materialize()
+    b = D.GradBucketer(A, FakeComm(), bucket_mb=4)
+    for _ in range(3):
+        A.grad.fill_(1.0)
+        p.grad_ready()
+        b.finish()
+    torch.cuda.synchronize()
+    t = b.poll_timing()
+    assert t["steps"] == 3 and t["span_s"] >= t["exposed_s"] >= 0.0
+    assert b.poll_timing()["steps"] == 0

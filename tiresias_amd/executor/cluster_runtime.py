@@ -191,6 +191,13 @@ class Controller:
                 self.est[k] = per if k not in self.est else 0.7 * self.est[k] + 0.3 * per
             j = self.sched.jobs[jid]
             j.progress = float(min(self.done_iters[jid], rj.iterations))
+            for r in reports:
+                for jr in (r or {}).get("jobs") or []:
+                    c = jr.get("comm") if jr.get("job") == jid else None
+                    if c and (r or {}).get("rank") == min(self.holders.get(jid, (r.get("rank"),))):
+                        # one member's view (the gang's lowest rank)
+                        j.extra["comm_exposed_s"] = j.extra.get("comm_exposed_s", 0.0) + c["exposed_s"]
+                        j.extra["comm_span_s"] = j.extra.get("comm_span_s", 0.0) + c["span_s"]
 
     # ---------------------------------------------------------------- failures
     def rank_lost(self, r: int) -> None:
@@ -744,6 +751,11 @@ class Worker:
             t = self.trainers[jid]
             rep = {"job": jid, "iters": n, "run_s": dt, "shared": len(jobs) > 1,
                    "loss": float(t.last_loss) if (t.last_loss is not None and err is None) else None}
+            if t.ddp is not None:
+                # hipEvent-measured gradient sync of the steps finished so far
+                ct = t.ddp.poll_timing()
+                if ct["steps"]:
+                    rep["comm"] = ct
             if err:
                 rep["error"] = err
             reps.append(rep)

@@ -29,7 +29,8 @@ CLUSTER_HEADER = ["delta", "num_idle_nodes", "num_busy_nodes", "num_busy_gpus", 
                   "num_finish_jobs"]
 JOB_HEADER = ["time", "job_id", "num_gpu", "submit_time", "start_time", "end_time", "executed_time",
               "JCT", "duration", "pending_time", "preempt", "resume", "promote", "migration",
-              "queue", "ckpt_overhead", "ckpt_bytes", "ckpt_save_s", "ckpt_restore_s", "model"]
+              "queue", "ckpt_overhead", "ckpt_bytes", "ckpt_save_s", "ckpt_restore_s", "comm_exposed_s",
+              "comm_span_s", "model"]
 
 
 def percentile(xs: List[float], p: float) -> float:
@@ -160,6 +161,8 @@ class MetricsLogger:
                    # measured on the live cluster (device copy time of spills / restores)
                    ckpt_save_s=round(j.extra.get("ckpt_save_s", 0.0), 6),
                    ckpt_restore_s=round(j.extra.get("ckpt_restore_s", 0.0), 6),
+                   comm_exposed_s=round(j.extra.get("comm_exposed_s", 0.0), 6),
+                   comm_span_s=round(j.extra.get("comm_span_s", 0.0), 6),
                    model=j.spec.model)
         self.job_rows.append(row)
         if "job" in self._writers:

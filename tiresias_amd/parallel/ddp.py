@@ -21,6 +21,12 @@ early in backward.
 
 Uses of a param (tied embeddings report twice) are learned on the first
 iteration, which reduces every bucket at the end instead of overlapping.
+
+Timing: on a GPU every step records three hipEvents on the
+compute stream -- first bucket launched, backward done (``finish`` entry),
+all reductions joined -- and ``poll_timing`` turns completed steps into
+``exposed_s`` (the compute stream waiting on communication) and ``span_s``
+(first bucket to last reduction), never blocking the host.
 """
 from __future__ import annotations
 
@@ -73,6 +79,10 @@ class GradBucketer:
         self._launched: List[bool] = []
         self._works = []
         self.bytes_reduced = 0
+        self._timed = self.world > 1 and arena.grad.is_cuda
+        self._ev_first = None
+        self._ev_open: List[tuple] = []          # (first, bwd_done, joined) per step, not yet read
+        self._acc = {"exposed_s": 0.0, "span_s": 0.0, "steps": 0}
         arena.on_grad_ready = self._on_ready
         self._reset()
 
@@ -90,6 +100,9 @@ class GradBucketer:
         lo, hi = self.ranges[bi]
         view = self.arena.grad[lo:hi]
         if self.world > 1:
+            if self._timed and self._ev_first is None:
+                self._ev_first = torch.cuda.Event(enable_timing=True)
+                self._ev_first.record()
             self._works.append(self.comm.start(view))
         self.bytes_reduced += view.numel() * 4
 
@@ -118,11 +131,36 @@ class GradBucketer:
         """Flush unlaunched buckets and order the compute stream after them."""
         if self.uses is None:
             self.uses = dict(self._seen)
+        bwd = None
+        if self._timed:
+            bwd = torch.cuda.Event(enable_timing=True)
+            bwd.record()
         for b in range(len(self.buckets)):
             self._launch(b)
         if self._works:
             self.comm.finish(self._works)
+            if self._timed:
+                done = torch.cuda.Event(enable_timing=True)
+                done.record()
+                self._ev_open.append((self._ev_first if self._ev_first is not None else bwd, bwd, done))
+        self._ev_first = None
         self._reset()
+
+    def poll_timing(self) -> dict:
+        """Measured communication seconds of the steps whose events have
+        completed since the last poll: ``exposed_s`` (backward done -> all
+        reductions joined) and ``span_s`` (first bucket -> joined)."""
+        keep = []
+        for first, bwd, done in self._ev_open:
+            if done.query():
+                self._acc["exposed_s"] += bwd.elapsed_time(done) / 1e3
+                self._acc["span_s"] += first.elapsed_time(done) / 1e3
+                self._acc["steps"] += 1
+            else:
+                keep.append((first, bwd, done))
+        self._ev_open = keep
+        out, self._acc = self._acc, {"exposed_s": 0.0, "span_s": 0.0, "steps": 0}
+        return out
 
     @property
     def grad_scale(self) -> float:
