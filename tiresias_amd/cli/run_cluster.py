@@ -99,6 +99,10 @@ def main(argv=None):
     FLAGS.parse(sys.argv[1:] if argv is None else argv)
     cfg = SimConfig.from_flags()
     d = FLAGS.as_dict()
+    if d.get("debug_kernels"):
+        from ..utils import debug
+
+        debug.enable(d["debug_kernels"])          # before the first HIP call
     if d.get("backend") == "fake":
         return _main_fake(cfg, d)
     if d.get("backend") not in ("sim", "mi355x", None):

@@ -86,6 +86,8 @@ def define_flags() -> None:
     D.DEFINE_float("skew_threshold", 0.5, "placement-sensitivity threshold (largest tensor / total)")
     D.DEFINE_string("throughput_table", "", "json of measured per-model iteration times (MI355X)")
     D.DEFINE_integer("max_jobs", 0, "truncate the trace (0 = all)")
+    D.DEFINE_integer("debug_kernels", 0, "kernel debug mode (utils/debug.py): 1 synchronous launches "
+                     "+ per-op HIP error check, 2 also NaN/Inf checks of every op's outputs")
     D.DEFINE_version("0.1.0")
 
 

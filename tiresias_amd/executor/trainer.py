@@ -51,7 +51,10 @@ class Trainer:
         self._bucket_mb = bucket_mb
         if group is not None and comm_size(group) > 1:
             self.ddp = GradBucketer(self.arena, group, bucket_mb=bucket_mb)
-        self._want_graph = use_graph and self.device.type == "cuda"
+        from ..utils import debug
+
+        # kernel debug mode synchronises after every op: not capturable
+        self._want_graph = use_graph and self.device.type == "cuda" and debug.level() == 0
         self.use_graph = self._want_graph and self.ddp is None   # graphs for 1-GPU jobs only
         self._graph = None
         self._g_loss = None

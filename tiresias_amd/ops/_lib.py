@@ -52,8 +52,12 @@ def load(required: bool | None = None) -> bool:
 
 
 def ops():
+    """``torch.ops.tam`` (or, in kernel debug mode -- ``utils/debug.py``,
+    ``TAM_DEBUG=1`` -- a proxy that synchronises and checks after every op)."""
     load(required=True)
-    return torch.ops.tam
+    from ..utils import debug
+
+    return debug.wrap(torch.ops.tam)
 
 
 def is_loaded() -> bool:
