@@ -1,6 +1,8 @@
 """End-to-end model numerics on the MI355X: one forward+backward of every
 model family through the HIP kernels vs the fp32 PyTorch reference path of
 the same ops (same seed, same synthetic batch), plus a few training steps."""
+import math
+
 import pytest
 import torch
 
@@ -173,5 +175,5 @@ def test_kernel_debug_mode_names_the_op(gpu, monkeypatch):
     with pytest.raises(debug.KernelDebugError, match="tam.gemm"):
         T.gemm(a, True, b, True, c, 0, None, False, None, 1.0, False)
     t = Trainer("resnet_tiny", gpu, seed=1, use_graph=True)
-    assert not t.use_graph
-    assert float(t.step()) == float(t.step()) or True
+    assert not t.use_graph                      # capture + per-op sync do not mix
+    assert math.isfinite(float(t.step()))
