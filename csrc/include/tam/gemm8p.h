@@ -124,11 +124,16 @@ __device__ __forceinline__ void p8_barrier() {
   asm volatile("" ::: "memory");
 }
 
-template <int I0, int J0, int FI, int FJ, int TI, int TJ>
+// FINE: no blanket lgkmcnt(0) in front of the cluster -- the compiler's own
+// per-fragment lgkmcnt waits let the first MFMAs start while later
+// fragment reads are still in flight
+template <int I0, int J0, bool FINE = false, int FI, int FJ, int TI, int TJ>
 __device__ __forceinline__ void p8_mfma(f32x4_t (&acc)[TI][TJ], const s16x8_t (&fa)[FI][2],
                                         const s16x8_t (&fb)[FJ][2]) {
-  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-  __builtin_amdgcn_sched_barrier(0);
+  if constexpr (!FINE) {
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_sched_barrier(0);
+  }
   __builtin_amdgcn_s_setprio(1);
 #pragma unroll
   for (int kk = 0; kk < 2; ++kk)
@@ -144,12 +149,18 @@ __device__ __forceinline__ void p8_mfma(f32x4_t (&acc)[TI][TJ], const s16x8_t (&
 }
 
 // SCHED 0: one barrier per phase (after the MFMA cluster); 1: two barriers
-// per phase (reads | MFMA); 2: two barriers + wave-group stagger
+// per phase (reads | MFMA); 2: two barriers + wave-group stagger; 3: as 0
+// with the B fragments read before the A fragments (pinned order); 4: as 3
+// without the blanket lgkmcnt(0) in front of each MFMA cluster (per-fragment
+// waits); 5: as 4 with 2's two barriers + stagger. Measured in one process,
+// interleaved rounds (tools/ab_gemm8p_sched.py, profiles/r2/gemm8p_sched_ab.json)
 template <int BM, int BN, int WNW, bool AK, bool BK, int SCHED>
 __global__ void __launch_bounds__(128 * WNW, (BM == 256 ? 1 : 2))
 gemm8p_kernel(P8Args a, Epi ep) {
   using G = P8Geo<BM, BN, WNW>;
-  constexpr bool STAGGER = SCHED == 2;
+  constexpr bool STAGGER = SCHED == 2 || SCHED == 5;
+  constexpr bool TWO_BAR = SCHED == 1 || SCHED == 2 || SCHED == 5;
+  constexpr bool FINE = SCHED == 4 || SCHED == 5;
   constexpr int FI = G::FI, FJ = G::FJ, TI = 2 * FI, TJ = 2 * FJ;
   __shared__ __attribute__((aligned(1024))) char smem[G::LDS];
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
@@ -210,25 +221,28 @@ gemm8p_kernel(P8Args a, Epi ep) {
       const char* BL = bptr(t, 0);
       const char* BH = bptr(t, 1);
       const bool n1 = t + 1 < nk, n2 = t + 2 < nk;
-      // ---- p1: quadrant (mh0, nh0)
+      // ---- p1: quadrant (mh0, nh0); B fragments first (SCHED 3: pinned
+      // B-before-A issue order, guide §5 8-phase template)
 #pragma unroll
-      for (int kk = 0; kk < 2; ++kk) {
+      for (int kk = 0; kk < 2; ++kk)
 #pragma unroll
         for (int j = 0; j < FJ; ++j) fb0[j][kk] = p8_frag<BK, G::BCOLS>(BL, lane, bcol + 16 * j, kk);
+      if constexpr (SCHED >= 3) __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+      for (int kk = 0; kk < 2; ++kk)
 #pragma unroll
         for (int i = 0; i < FI; ++i) fa[i][kk] = p8_frag<AK, G::AROWS>(AL, lane, arow + 16 * i, kk);
-      }
       if (n1) issA(t + 1, 1);
-      if constexpr (SCHED > 0) p8_barrier();
-      p8_mfma<0, 0>(acc, fa, fb0);
+      if constexpr (TWO_BAR) p8_barrier();
+      p8_mfma<0, 0, FINE>(acc, fa, fb0);
       p8_barrier();
       // ---- p2: quadrant (mh0, nh1)
 #pragma unroll
       for (int kk = 0; kk < 2; ++kk)
 #pragma unroll
         for (int j = 0; j < FJ; ++j) fb1[j][kk] = p8_frag<BK, G::BCOLS>(BH, lane, bcol + 16 * j, kk);
-      if constexpr (SCHED > 0) p8_barrier();
-      p8_mfma<0, FJ>(acc, fa, fb1);
+      if constexpr (TWO_BAR) p8_barrier();
+      p8_mfma<0, FJ, FINE>(acc, fa, fb1);
       p8_barrier();
       // ---- p3: quadrant (mh1, nh1)
 #pragma unroll
@@ -236,8 +250,8 @@ gemm8p_kernel(P8Args a, Epi ep) {
 #pragma unroll
         for (int i = 0; i < FI; ++i) fa[i][kk] = p8_frag<AK, G::AROWS>(AH, lane, arow + 16 * i, kk);
       if (n2) issA(t + 2, 0);
-      if constexpr (SCHED > 0) p8_barrier();
-      p8_mfma<FI, FJ>(acc, fa, fb1);
+      if constexpr (TWO_BAR) p8_barrier();
+      p8_mfma<FI, FJ, FINE>(acc, fa, fb1);
       p8_barrier();
       // ---- p4: quadrant (mh1, nh0); retire tile t+1 (t+2's AL / BL / BH stay in flight)
       if (n2) {
@@ -247,8 +261,8 @@ gemm8p_kernel(P8Args a, Epi ep) {
       } else {
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       }
-      if constexpr (SCHED > 0) p8_barrier();
-      p8_mfma<FI, 0>(acc, fa, fb0);
+      if constexpr (TWO_BAR) p8_barrier();
+      p8_mfma<FI, 0, FINE>(acc, fa, fb0);
       p8_barrier();
     }
     if (STAGGER && !upper) p8_barrier();        // both groups execute the same barrier count

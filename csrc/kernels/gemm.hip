@@ -85,7 +85,7 @@ void zero_async(void* p, size_t bytes, hipStream_t s) {
 // 1 auto (big GEMMs of every layout), 2 forced wherever eligible, 3 forced
 // with slab split-K (the op binding; tests / sweeps). sched: 0 one barrier
 // per phase, 1 two, 2 two + wave-group stagger; tile: 0 auto, 128 / 256 forced
-static int g_p8 = 1, g_p8_sched = 0, g_p8_tile = 0;
+static int g_p8 = 1, g_p8_sched = 4, g_p8_tile = 0;   // sched 4: profiles/r2/gemm8p_sched_ab.json
 int gemm8p_policy_mode() { return g_p8; }
 void gemm8p_policy(int mode, int sched) {
   g_p8 = mode;
@@ -96,7 +96,10 @@ void gemm8p_policy(int mode, int sched) {
 template <int BM, int BN, int WNW, bool AK, bool BK>
 static void p8_launch_t(const P8Args& g, const Epi& ep, dim3 grid, int sched, hipStream_t s) {
   constexpr int T = P8Geo<BM, BN, WNW>::THREADS;
-  if (sched == 2) hipLaunchKernelGGL((gemm8p_kernel<BM, BN, WNW, AK, BK, 2>), grid, dim3(T), 0, s, g, ep);
+  if (sched == 5) hipLaunchKernelGGL((gemm8p_kernel<BM, BN, WNW, AK, BK, 5>), grid, dim3(T), 0, s, g, ep);
+  else if (sched == 4) hipLaunchKernelGGL((gemm8p_kernel<BM, BN, WNW, AK, BK, 4>), grid, dim3(T), 0, s, g, ep);
+  else if (sched == 3) hipLaunchKernelGGL((gemm8p_kernel<BM, BN, WNW, AK, BK, 3>), grid, dim3(T), 0, s, g, ep);
+  else if (sched == 2) hipLaunchKernelGGL((gemm8p_kernel<BM, BN, WNW, AK, BK, 2>), grid, dim3(T), 0, s, g, ep);
   else if (sched == 1) hipLaunchKernelGGL((gemm8p_kernel<BM, BN, WNW, AK, BK, 1>), grid, dim3(T), 0, s, g, ep);
   else hipLaunchKernelGGL((gemm8p_kernel<BM, BN, WNW, AK, BK, 0>), grid, dim3(T), 0, s, g, ep);
 }
