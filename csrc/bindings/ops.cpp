@@ -540,6 +540,7 @@ void gemm_dma_policy_op(int64_t p, int64_t cfg) {
 }
 
 void gemm8p_policy_op(int64_t mode, int64_t stagger) { tam::gemm8p_policy((int)mode, (int)stagger); }
+void gemm8p_group_op(int64_t g) { tam::gemm8p_group((int)g); }
 
 void gemm_force_op(int64_t cfg, int64_t splits) {
   tam::gemm_force((int)cfg, (int)splits);
@@ -745,6 +746,7 @@ TORCH_LIBRARY(tam, m) {
   m.def("colsum(Tensor x, Tensor(a!) out) -> ()", &colsum_op);
   m.def("gemm_force(int cfg, int splits) -> ()", &gemm_force_op);
   m.def("gemm8p_policy(int mode, int stagger) -> ()", &gemm8p_policy_op);
+  m.def("gemm8p_group(int g) -> ()", &gemm8p_group_op);
   m.def("gemm_lib_policy(int policy) -> ()", &gemm_lib_policy_op);
   m.def("conv_dma_policy(int policy) -> ()", &conv_dma_policy_op);
   m.def("gemm_dma_policy(int policy, int cfg) -> ()", &gemm_dma_policy_op);

@@ -57,6 +57,7 @@ struct P8Args {
   long ldb;
   int M, N, K;
   int kps;   // K-tiles per split (blockIdx.z)
+  int group = 4;   // M-tiles per tile-order group (L2 reuse of B panels)
 };
 
 // Tile geometry: BM x BN block, 2 (M) x WNW (N) waves.
@@ -171,7 +172,7 @@ gemm8p_kernel(P8Args a, Epi ep) {
 
   const int tiles_m = (a.M + BM - 1) / BM, tiles_n = (a.N + BN - 1) / BN;
   const int bid = xcd_remap(blockIdx.x, gridDim.x);
-  constexpr int GROUP = 4;
+  const int GROUP = a.group;
   const int per_group = GROUP * tiles_n;
   const int grp = bid / per_group;
   const int first_m = grp * GROUP;

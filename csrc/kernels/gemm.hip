@@ -85,8 +85,9 @@ void zero_async(void* p, size_t bytes, hipStream_t s) {
 // 1 auto (big GEMMs of every layout), 2 forced wherever eligible, 3 forced
 // with slab split-K (the op binding; tests / sweeps). sched: 0 one barrier
 // per phase, 1 two, 2 two + wave-group stagger; tile: 0 auto, 128 / 256 forced
-static int g_p8 = 1, g_p8_sched = 4, g_p8_tile = 0;   // sched 4: profiles/r2/gemm8p_sched_ab.json
+static int g_p8 = 1, g_p8_sched = 4, g_p8_tile = 0, g_p8_group = 4;   // sched 4: profiles/r2/gemm8p_sched_ab.json
 int gemm8p_policy_mode() { return g_p8; }
+void gemm8p_group(int g) { g_p8_group = g > 0 ? g : 4; }
 void gemm8p_policy(int mode, int sched) {
   g_p8 = mode;
   g_p8_sched = sched % 10;
@@ -126,7 +127,7 @@ void launch_gemm8p(const bf16_t* A, long lda, bool ak, const bf16_t* B, long ldb
   const int ktiles = K / P8_BK;
   const int kps = cdiv(ktiles, splits < 1 ? 1 : splits);
   const int z = cdiv(ktiles, kps);
-  P8Args g{A, lda, B, ldb, M, N, K, kps};
+  P8Args g{A, lda, B, ldb, M, N, K, kps, g_p8_group};
   const dim3 grid(tiles, 1, z);
   if (T == 128) p8_launch_l<128, 128, 2>(ak, bk, g, ep, grid, sched, s);
   else p8_launch_l<256, 256, 4>(ak, bk, g, ep, grid, sched, s);

@@ -13,7 +13,8 @@ from tiresias_amd.ops import _lib  # noqa: E402
 T = _lib.ops()
 T.gemm_lib_policy(0)
 dev = torch.device("cuda", 0)
-variants = [int(v) for v in (sys.argv[1] if len(sys.argv) > 1 else "0,2,3").split(",")]
+# variant "s" = schedule s (group 4); "s:g" = schedule s with tile-order group g
+variants = [v for v in (sys.argv[1] if len(sys.argv) > 1 else "0,2,3").split(",")]
 res = {}
 for (M, N, K) in [(4096, 4096, 4096), (8192, 8192, 8192)]:
     A = (torch.rand(M, K, device=dev) * 2 - 1).to(torch.bfloat16)
@@ -23,7 +24,9 @@ for (M, N, K) in [(4096, 4096, 4096), (8192, 8192, 8192)]:
     times = {v: [] for v in variants}
     for rnd in range(6):
         for v in variants:
-            T.gemm8p_policy(2, 200 + v)          # forced 256^2 tile, schedule v, no split
+            sch, grp = (int(x) for x in (v.split(":") + ["4"])[:2])
+            T.gemm8p_policy(2, 200 + sch)        # forced 256^2 tile, schedule sch, no split
+            T.gemm8p_group(grp)
             for _ in range(2):
                 T.gemm(A, True, B, True, c, 0, None, False, None, 1.0, False)
             e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
@@ -40,5 +43,6 @@ for (M, N, K) in [(4096, 4096, 4096), (8192, 8192, 8192)]:
                 assert err < 1e-3, (v, err)
     res[f"{M}x{N}x{K}"] = {v: {"median_tf": round(statistics.median(t), 1), "best_tf": round(max(t), 1)}
                            for v, t in times.items()}
-T.gemm8p_policy(1, 0)
+T.gemm8p_policy(1, 4)
+T.gemm8p_group(4)
 print(json.dumps(res))
