@@ -412,6 +412,7 @@ def main():
             "pool_hits": worker.pool_hits,
             "pressure_spills": worker.pressure_spills,
             "pool_evictions": worker.pool_evictions,
+            "restore_prefetches": worker.prefetches,
             "replays": warm_done + steps + (1 if base else 0),
             "spilled_gb": round(worker.spilled_bytes / 2 ** 30, 3),
             "max_hbm_reserved_gb": round(torch.cuda.max_memory_reserved(device) / 2 ** 30, 2) if use_cuda else None,

@@ -470,6 +470,7 @@ class Worker:
         self._ckpt: Dict[str, dict] = {}           # job -> bytes / seconds since the last report
         self.pressure_spills = 0
         self.pool_evictions = 0
+        self.prefetches = 0
         # real-device sampling (HIP mem info + amd-smi) for gpu_live.csv
         self.monitor = None
         self._mon_t = -1e9
@@ -677,6 +678,23 @@ class Worker:
             if a["op"] == "start" and a["source"] == "p2p":
                 if self.rank in a["old"] and self.rank not in a["ranks"]:
                     self._retire(self.trainers.pop(a["job"], None))
+        if pressure:
+            self._prefetch(plan.get("resume_order") or [])
+
+    def _prefetch(self, resume_order) -> None:
+        """Restore ahead: the spilled job the scheduler will resume FIRST comes
+        back to HBM now, while this round's jobs compute (the H2D runs on the
+        engine's side stream), when it fits without spilling anything. Its
+        later resume is then a pointer swap instead of an H2D on the critical
+        path."""
+        for jid in resume_order[:1]:
+            t = self.trainers.get(jid)
+            if t is None or not getattr(t, "_spilled", None):
+                continue
+            margin = 0.05 * (self.hbm_budget or 0.0)
+            if self._free_bytes() >= t.hbm_bytes() + margin:
+                self._restore(jid)
+                self.prefetches += 1
 
     def _dev_sample(self) -> Optional[dict]:
         """Real HBM / activity of this rank's GPU (hipMemGetInfo + amd-smi),
