@@ -129,30 +129,34 @@ __global__ void __launch_bounds__(256) bn_stats_kernel(const bf16_t* __restrict_
 // per-channel finalize: BWD=0 -> mean/rstd, scale/shift, running stats;
 // BWD=1 -> dgamma/dbeta and the k1/k2/k3 coefficients of the apply pass.
 // One launch instead of col_reduce + finalize (each ~5 us of a tiny grid).
+// 1024 threads = 16 columns x 64 row lanes, 4 rows in flight per lane: the
+// pass is latency-bound (one dependent kernel per BN), so more lanes per
+// column, not more columns per block
 template <int BWD>
-__global__ void __launch_bounds__(256) bn_reduce_finalize_kernel(
+__global__ void __launch_bounds__(1024) bn_reduce_finalize_kernel(
     const float* __restrict__ part, int nblk, long M, int C, float eps, float momentum,
     const float* __restrict__ gamma, const float* __restrict__ beta_or_rstd,
     float* __restrict__ o0, float* __restrict__ o1, float* __restrict__ o2,
     float* __restrict__ o3, float* __restrict__ o4, float* __restrict__ o5) {
-  __shared__ double red[2][16][17];
+  constexpr int RL = 64;
+  __shared__ double red[2][RL][17];
   const int cx = threadIdx.x & 15, ly = threadIdx.x >> 4;
   const int c = blockIdx.x * 16 + cx;
   const int W = 2 * C;
   double s = 0.0, q = 0.0;
   if (c < C) {
     int b = ly;
-    for (; b + 3 * 16 < nblk; b += 4 * 16) {
+    for (; b + 3 * RL < nblk; b += 4 * RL) {
       float v[4], w[4];
 #pragma unroll
       for (int u = 0; u < 4; ++u) {
-        v[u] = part[(long)(b + u * 16) * W + c];
-        w[u] = part[(long)(b + u * 16) * W + C + c];
+        v[u] = part[(long)(b + u * RL) * W + c];
+        w[u] = part[(long)(b + u * RL) * W + C + c];
       }
 #pragma unroll
       for (int u = 0; u < 4; ++u) { s += (double)v[u]; q += (double)w[u]; }
     }
-    for (; b < nblk; b += 16) {
+    for (; b < nblk; b += RL) {
       s += (double)part[(long)b * W + c];
       q += (double)part[(long)b * W + C + c];
     }
@@ -162,8 +166,8 @@ __global__ void __launch_bounds__(256) bn_reduce_finalize_kernel(
   __syncthreads();
   if (ly != 0 || c >= C) return;
   double S = 0.0, Q = 0.0;
-#pragma unroll
-  for (int k = 0; k < 16; ++k) { S += red[0][k][cx]; Q += red[1][k][cx]; }
+#pragma unroll 8
+  for (int k = 0; k < RL; ++k) { S += red[0][k][cx]; Q += red[1][k][cx]; }
   if (BWD == 0) {
     // o0 mean, o1 rstd, o2 scale, o3 shift, o4 run_mean, o5 run_var
     const double mean = S / (double)M;
@@ -448,7 +452,7 @@ void bn_forward(const bf16_t* x, const bf16_t* res, bf16_t* y, long M, int C, fl
   } else {
     hipLaunchKernelGGL(bn_stats_kernel, dim3(nb), dim3(256), 0, s, x, M, C, rpb, ws_f + 6 * C);
   }
-  hipLaunchKernelGGL(bn_reduce_finalize_kernel<0>, dim3((C + 15) / 16), dim3(256), 0, s, part, nb, M,
+  hipLaunchKernelGGL(bn_reduce_finalize_kernel<0>, dim3((C + 15) / 16), dim3(1024), 0, s, part, nb, M,
                      C, eps, momentum, gamma, beta, save_mean, save_rstd, ws_f, ws_f + C, run_mean,
                      run_var);
   const long total8 = M * C / 8;
@@ -474,7 +478,7 @@ void bn_backward(const bf16_t* dy, const bf16_t* addend, const bf16_t* y, const 
   hipLaunchKernelGGL(bn_bwd_reduce_kernel, dim3(nb), dim3(256), 0, s, dy, addend, y, x, mean, rstd, M,
                      C, rpb, relu, part);
   (void)sums;
-  hipLaunchKernelGGL(bn_reduce_finalize_kernel<1>, dim3((C + 15) / 16), dim3(256), 0, s, part, nb, M,
+  hipLaunchKernelGGL(bn_reduce_finalize_kernel<1>, dim3((C + 15) / 16), dim3(1024), 0, s, part, nb, M,
                      C, 0.f, 0.f, gamma, rstd, dgamma, dbeta, ws_f, ws_f + C, ws_f + 2 * C,
                      (float*)nullptr);
   const long total8 = M * C / 8;
