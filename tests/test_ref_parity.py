@@ -1,0 +1,68 @@
+"""Parity with an EXECUTION of the reference's live simulator.
+
+``tests/fixtures/ref_parity.json`` was produced by ``tools/ref_parity.py``,
+which runs the reference's ``run_sim.py`` (fixed-tick loop,
+core/scheduling/schedule.py:178-212) in a scratch copy on two small
+live-schema traces built so that none of the live-path defects (SURVEY.md §3
+D1, D2, D8) changes the outcome, and records each job's start tick, end tick
+and devices from the reference's own log.
+
+``TickSimulator`` must reproduce every start and end tick for fifo/yarn,
+horus/horus and gandiva/gandiva, and the exact devices for fifo/yarn.
+
+Two documented deviations are configured, not patched over:
+  * the reference never applies its interference slowdown (D6,
+    infra/node.py:201), so the sharing policies (horus, gandiva) are replayed
+    with ``interference=0``;
+  * horus/gandiva device choice is not pinned: the reference's scorer
+    (core/scheduling/horus.py) picks different shared devices than ours; the
+    timing still matches because co-location is free under D6.
+"""
+import json
+import os
+
+import pytest
+
+from tiresias_amd.config import ClusterSpec, SimConfig
+from tiresias_amd.core.job import JobSpec
+from tiresias_amd.engine.sim import TickSimulator
+
+FIXTURE = os.path.join(os.path.dirname(__file__), "fixtures", "ref_parity.json")
+_FX = json.load(open(FIXTURE))
+CASES = [(name, pair) for name, t in sorted(_FX["traces"].items()) for pair in sorted(t["results"])]
+
+
+def _replay(trace: dict, pair: str) -> TickSimulator:
+    schedule, scheme = pair.split("/")
+    # reference job rows: (job_id, arrival tick, used_gpus, gpu_per_container, minutes);
+    # it runs minutes * 0.5 ticks (schedule.py:187 gen_jobs(scale_factor=0.5))
+    specs = [JobSpec(j[0], float(j[1]), j[4] * 0.5, j[2], gpu_per_worker=j[3]) for j in trace["jobs"]]
+    cfg = SimConfig(schedule=schedule, scheme=scheme, engine="tick",
+                    interference=0.0 if schedule != "fifo" else SimConfig.interference,
+                    cluster=ClusterSpec(num_switch=1, num_node_p_switch=trace["nodes"],
+                                        num_gpu_p_node=trace["gpus_per_node"]))
+    sim = TickSimulator(cfg, specs)
+    sim.run()
+    return sim
+
+
+def test_fixture_covers_all_pairs():
+    assert len(CASES) == 6
+    for t in _FX["traces"].values():
+        for res in t["results"].values():
+            assert {j[0] for j in t["jobs"]} == set(res), "reference run did not finish every job"
+
+
+@pytest.mark.parametrize("name,pair", CASES)
+def test_tick_engine_matches_reference_execution(name, pair):
+    trace = _FX["traces"][name]
+    sim = _replay(trace, pair)
+    want = {k: (float(v["start"]), float(v["end"])) for k, v in trace["results"][pair].items()}
+    got = {j.job_id: (j.start_time, j.end_time) for j in sim.jobs.values()}
+    assert got == want
+    if pair == "fifo/yarn":
+        for jid, v in trace["results"][pair].items():
+            j = sim.jobs[jid]
+            alloc = j.allocation or j.allocation_prev
+            ours = sorted([node, d] for node, devs in alloc.items() for d in devs)
+            assert ours == v["devices"], jid

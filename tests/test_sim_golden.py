@@ -169,8 +169,8 @@ def test_tick_engine_live_fifo_hand_derived():
       B t=0 1 GPU dur 3   -> placed 1 (one placement per tick), ends 4
       C t=0 4 GPU dur 1   -> blocked at 2, 3 (3 free after A), placed 4, ends 5
       D t=1 1 GPU dur 1   -> behind C (FIFO), placed 5, ends 6
-    (Parity with an execution of the reference is unpinned: the reference ships
-    no trace fixture and is not run here.)"""
+    (Parity with an EXECUTION of the reference on larger traces is pinned in
+    tests/test_ref_parity.py, fixture from tools/ref_parity.py.)"""
     from tiresias_amd.engine.sim import TickSimulator
 
     c = SimConfig(schedule="fifo", scheme="yarn", engine="tick",

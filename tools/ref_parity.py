@@ -1,0 +1,149 @@
+"""Produce reference-parity fixtures by EXECUTING the reference's live simulator.
+
+Copies the reference tree (``--reference``, read-only) into a scratch
+directory, writes small live-schema traces there, runs the reference's
+``run_sim.py`` (its fixed-tick loop, core/scheduling/schedule.py:178-212) for
+each (schedule, scheme) pair, and parses per-job start/finish ticks and the
+devices each job was placed on from the reference's own log
+(``delta-time: N`` from job_generator.py:202, ``placing task J_worker0 at node
+N - device D`` from infra/node.py:226, ``job J finish`` from schedule.py:156).
+
+The traces are built so none of the reference defects that SURVEY.md §3
+lists for the live path can change the outcome:
+  * D1 (the loop ignores queued jobs): an anchor job runs until every other
+    job has finished, so ``running > 0`` while anything is queued;
+  * D8 (new arrival batches inserted at the queue head): no job arrives while
+    another one is waiting;
+  * D2 (reservation leak) and D6/D7 do not trigger on one node without
+    migration.
+The tool asserts that every job finished in the reference run before it
+writes the fixture; ``tests/test_ref_parity.py`` replays the same traces
+through ``TickSimulator`` and must reproduce every tick.
+
+Usage: python tools/ref_parity.py --reference /root/reference \
+           --out tests/fixtures/ref_parity.json
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import re
+import shutil
+import subprocess
+import sys
+import tempfile
+
+# (job_id, arrival tick, used_gpus, gpu_per_container, minutes); the reference runs minutes*0.5
+# ticks (jobs_manager.py:226 via schedule.py:187 scale_factor=0.5).
+TRACES = {
+    # one 4-GPU node: blocking head, one placement per tick, ceil(0.5*minutes)
+    "node4_blocking": dict(gpus_per_node=4, nodes=1, jobs=[
+        ("0", 0, 1, 1, 60.0),      # anchor (30 ticks)
+        ("1", 1, 2, 2, 5.0),       # placed 1, ends 1+3
+        ("2", 2, 1, 1, 7.0),       # placed 2, ends 2+4
+        ("3", 3, 2, 2, 3.0),       # needs 2, only 0 free -> waits until 1 ends at 4
+        ("4", 8, 3, 3, 4.0),       # 3 free at 8 -> placed 8, ends 10
+        ("5", 12, 3, 3, 9.0),      # placed 12, ends 17
+        ("6", 13, 1, 1, 2.0),      # 0 free until 17 -> placed 17, ends 18
+    ]),
+    # two 4-GPU nodes: multi-worker gangs (workers of gpu_per_container GPUs)
+    "two_node_gang": dict(gpus_per_node=4, nodes=2, jobs=[
+        ("0", 0, 1, 1, 80.0),      # anchor (40 ticks)
+        ("1", 1, 4, 2, 6.0),       # 2 workers x 2 GPUs
+        ("2", 2, 2, 1, 10.0),      # 2 workers x 1 GPU
+        ("3", 3, 4, 4, 4.0),       # whole node: waits for 1
+        ("4", 12, 6, 2, 2.0),      # 3 workers x 2 GPUs across both nodes
+        ("5", 20, 2, 2, 3.0),
+        ("6", 26, 3, 1, 5.0),
+    ]),
+}
+PAIRS = [("fifo", "yarn"), ("horus", "horus"), ("gandiva", "gandiva")]
+
+_DELTA = re.compile(r"delta-time: (\d+)")
+_PLACE = re.compile(r"placing task (\S+?)_worker\d+ at node (\S+) - device (\d+)")
+_FINISH = re.compile(r"\{schedule:\d+\} INFO: job (\S+) finish")
+
+
+def write_trace(path: str, jobs) -> None:
+    with open(path, "w") as f:
+        f.write("job_id,type,normalized_time,minutes,gpu_per_container,used_gpus,"
+                "gpu_utilization_avg,gpu_utilization_max,memory_avg,memory_max,model_name\n")
+        for jid, t, g, gpc, minutes in jobs:
+            f.write(f"{jid},noninteractive,{t * 10000},{minutes},{gpc},{g},50,90,1048576,2097152,resnet50\n")
+
+
+def parse_log(text: str):
+    """Per job: start tick, end tick, sorted [node, device] pairs."""
+    tick = 0
+    out = {}
+    for line in text.splitlines():
+        m = _DELTA.search(line)
+        if m:
+            tick = int(m.group(1))
+            continue
+        m = _PLACE.search(line)
+        if m:
+            r = out.setdefault(m.group(1), {"start": tick, "end": None, "devices": []})
+            r["devices"].append([m.group(2), int(m.group(3))])
+            continue
+        m = _FINISH.search(line)
+        if m:
+            # release_finished_jobs runs after delta_time += 1 (schedule.py:190-192)
+            out[m.group(1)]["end"] = tick + 1
+    for r in out.values():
+        r["devices"].sort()
+    return out
+
+
+def run_reference(ref: str, work: str, name: str, spec: dict, schedule: str, scheme: str) -> dict:
+    write_trace(os.path.join(work, f"{name}.csv"), spec["jobs"])
+    cmd = [sys.executable, "run_sim.py", "--scheme", scheme, "--schedule", schedule,
+           "--trace_file", f"../{name}.csv", "--num_switch", "1",
+           "--num_node_p_switch", str(spec["nodes"]), "--num_gpu_p_node", str(spec["gpus_per_node"]),
+           "--log_path", f"{name}_{schedule}"]
+    p = subprocess.run(cmd, cwd=ref, capture_output=True, text=True, timeout=300)
+    if p.returncode != 0:
+        raise RuntimeError(f"reference failed ({name}, {schedule}):\n{p.stderr[-2000:]}")
+    res = parse_log(p.stderr + p.stdout)
+    want = {j[0] for j in spec["jobs"]}
+    done = {k for k, v in res.items() if v["end"] is not None}
+    if done != want:
+        raise RuntimeError(f"{name}/{schedule}: reference finished {sorted(done)} of {sorted(want)} "
+                           "(a defect triggered; change the trace)")
+    return res
+
+
+def main() -> None:
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--reference", required=True)
+    ap.add_argument("--out", default="tests/fixtures/ref_parity.json")
+    a = ap.parse_args()
+    work = tempfile.mkdtemp(prefix="refparity_")
+    try:
+        ref = os.path.join(work, "ref")
+        shutil.copytree(a.reference, ref, ignore=shutil.ignore_patterns("log", "*.pyc", "__pycache__"))
+        fixture = {"generator": "tools/ref_parity.py (reference run_sim.py executed in a scratch copy)",
+                   "traces": {}}
+        for name, spec in TRACES.items():
+            entry = {"gpus_per_node": spec["gpus_per_node"], "nodes": spec["nodes"],
+                     "jobs": [list(j) for j in spec["jobs"]], "results": {}}
+            for schedule, scheme in PAIRS:
+                try:
+                    entry["results"][f"{schedule}/{scheme}"] = run_reference(ref, work, name, spec,
+                                                                             schedule, scheme)
+                except RuntimeError as e:
+                    print(f"skip {name} {schedule}/{scheme}: {e}", file=sys.stderr)
+            fixture["traces"][name] = entry
+        os.makedirs(os.path.dirname(os.path.abspath(a.out)), exist_ok=True)
+        with open(a.out, "w") as f:
+            json.dump(fixture, f, indent=1, sort_keys=True)
+        print(json.dumps({k: {p: {j: (r["start"], r["end"]) for j, r in v.items()}
+                              for p, v in t["results"].items()}
+                          for k, t in fixture["traces"].items()}, indent=1))
+    finally:
+        shutil.rmtree(work, ignore_errors=True)
+
+
+if __name__ == "__main__":
+    main()
