@@ -35,12 +35,12 @@ def conv_calls(model: str):
     seen = []
     orig = Fx._Conv.apply
 
-    def rec(x, token, w, b, stride, pad, relu, in_relu, mask_own):
+    def rec(x, token, w, b, stride, pad, relu, in_relu, *rest):
         key = (x.shape[1], x.shape[2], x.shape[3], w.shape[0], w.shape[1], stride, pad,
                b is not None, relu, in_relu)
         if key not in seen:
             seen.append(key)
-        return orig(x, token, w, b, stride, pad, relu, in_relu, mask_own)
+        return orig(x, token, w, b, stride, pad, relu, in_relu, *rest)
 
     Fx._Conv.apply = rec
     try:
