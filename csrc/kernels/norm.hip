@@ -230,39 +230,11 @@ __global__ void __launch_bounds__(256) bn_apply_kernel(const bf16_t* __restrict_
                                                         int relu) {
   const int cg8 = C / 8;
   const long stride = (long)gridDim.x * blockDim.x;
-  long i = blockIdx.x * (long)blockDim.x + threadIdx.x;
-  // two vectors per thread per iteration: loads of both issued before use
-  for (; i + stride < total8; i += 2 * stride) {
-    const uint4 xa = ((const uint4*)x)[i], xb = ((const uint4*)x)[i + stride];
-    uint4 ra = make_uint4(0, 0, 0, 0), rb = ra;
-    if (res) { ra = ((const uint4*)res)[i]; rb = ((const uint4*)res)[i + stride]; }
-#pragma unroll
-    for (int h = 0; h < 2; ++h) {
-      const long ii = h ? i + stride : i;
-      const int c0 = (int)(ii % cg8) * 8;
-      float f[8], rr[8];
-      unpack8(h ? xb : xa, f);
-      if (res) unpack8(h ? rb : ra, rr);
-      const float4 sa = *(const float4*)(scale + c0), sb = *(const float4*)(scale + c0 + 4);
-      const float4 ha = *(const float4*)(shift + c0), hb = *(const float4*)(shift + c0 + 4);
-      const float sc[8] = {sa.x, sa.y, sa.z, sa.w, sb.x, sb.y, sb.z, sb.w};
-      const float sh[8] = {ha.x, ha.y, ha.z, ha.w, hb.x, hb.y, hb.z, hb.w};
-#pragma unroll
-      for (int j = 0; j < 8; ++j) {
-        float v = f[j] * sc[j] + sh[j];
-        if (res) v += rr[j];
-        if (relu) v = fmaxf(v, 0.f);
-        f[j] = v;
-      }
-      ((uint4*)y)[ii] = pack8(f);
-    }
-  }
-  for (; i < total8; i += stride) {
-    const int c0 = (int)(i % cg8) * 8;
-    float f[8];
-    unpack8(((const uint4*)x)[i], f);
-    float rr[8];
-    if (res) unpack8(((const uint4*)res)[i], rr);
+  auto one = [&](const long ii, const uint4 vx, const uint4 vr) {
+    const int c0 = (int)(ii % cg8) * 8;
+    float f[8], rr[8];
+    unpack8(vx, f);
+    if (res) unpack8(vr, rr);
     const float4 sa = *(const float4*)(scale + c0), sb = *(const float4*)(scale + c0 + 4);
     const float4 ha = *(const float4*)(shift + c0), hb = *(const float4*)(shift + c0 + 4);
     const float sc[8] = {sa.x, sa.y, sa.z, sa.w, sb.x, sb.y, sb.z, sb.w};
@@ -274,16 +246,34 @@ __global__ void __launch_bounds__(256) bn_apply_kernel(const bf16_t* __restrict_
       if (relu) v = fmaxf(v, 0.f);
       f[j] = v;
     }
-    ((uint4*)y)[i] = pack8(f);
+    ((uint4*)y)[ii] = pack8(f);
+  };
+  const uint4 z = make_uint4(0, 0, 0, 0);
+  long i = blockIdx.x * (long)blockDim.x + threadIdx.x;
+  // 2 vectors' loads in flight per thread before any use
+  constexpr int U = 2;
+  for (; i + (U - 1) * stride < total8; i += U * stride) {
+    uint4 vx[U], vr[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      vx[u] = ((const uint4*)x)[i + u * stride];
+      vr[u] = res ? ((const uint4*)res)[i + u * stride] : z;
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) one(i + u * stride, vx[u], vr[u]);
   }
+  for (; i < total8; i += stride) one(i, ((const uint4*)x)[i], res ? ((const uint4*)res)[i] : z);
 }
 
 // ---------------------------------------------------------------- BN backward
-// dyr = dy * (y > 0 if relu); accum sum(dyr), sum(dyr * xhat) per channel
+// dyr = (dy + addend) * (y > 0 if relu); accum sum(dyr), sum(dyr * xhat) per
+// channel. dp_out (residual BNs): dyr is also stored -- it IS the residual
+// branch's gradient, and the apply pass then reads dyr + x only (no dy,
+// addend, y re-reads, no second dres write: 2 passes of the tensor saved)
 __global__ void __launch_bounds__(256) bn_bwd_reduce_kernel(
     const bf16_t* __restrict__ dy, const bf16_t* __restrict__ addend, const bf16_t* __restrict__ y,
     const bf16_t* __restrict__ x, const float* __restrict__ mean, const float* __restrict__ rstd, long M,
-    int C, long rows_per_block, int relu, float* __restrict__ part) {
+    int C, long rows_per_block, int relu, float* __restrict__ part, bf16_t* __restrict__ dp_out) {
   __shared__ float red[256 * 16];
   const int tpr = C / 8, rpb = 256 / tpr;
   const int cg = threadIdx.x % tpr, rl = threadIdx.x / tpr;
@@ -292,25 +282,53 @@ __global__ void __launch_bounds__(256) bn_bwd_reduce_kernel(
   for (int i = 0; i < 8; ++i) { a[i] = b[i] = 0.f; mu[i] = mean[cg * 8 + i]; rs[i] = rstd[cg * 8 + i]; }
   const long r0 = blockIdx.x * rows_per_block;
   const long r1 = min(M, r0 + rows_per_block);
+  // one row of 8 channels: (dy + addend) masked by y, accumulated; dyr stored
+  auto row = [&](const long off, const uint4 vd, const uint4 vx, const uint4 vy, const uint4 va) {
+    float fd[8], fx[8];
+    unpack8(vd, fd);
+    unpack8(vx, fx);
+    if (addend) {
+      float fa[8];
+      unpack8(va, fa);
+#pragma unroll
+      for (int i = 0; i < 8; ++i) fd[i] += fa[i];
+    }
+    if (relu) {
+      float fy[8];
+      unpack8(vy, fy);
+#pragma unroll
+      for (int i = 0; i < 8; ++i) fd[i] = fy[i] <= 0.f ? 0.f : fd[i];
+    }
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      a[i] += fd[i];
+      b[i] += fd[i] * (fx[i] - mu[i]) * rs[i];
+    }
+    if (dp_out) *(uint4*)(dp_out + off) = pack8(fd);
+  };
   if (rl < rpb) {
-    for (long r = r0 + rl; r < r1; r += rpb) {
+    const uint4 z = make_uint4(0, 0, 0, 0);
+    long r = r0 + rl;
+    // 4 rows' loads in flight per thread before any use (the 2-tensor
+    // non-residual case is otherwise latency-bound)
+    constexpr int U = 4;
+    for (; r + (U - 1) * rpb < r1; r += U * rpb) {
+      uint4 vd[U], vx[U], vy[U], va[U];
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        const long off = (r + u * rpb) * C + cg * 8;
+        vd[u] = *(const uint4*)(dy + off);
+        vx[u] = *(const uint4*)(x + off);
+        vy[u] = relu ? *(const uint4*)(y + off) : z;
+        va[u] = addend ? *(const uint4*)(addend + off) : z;
+      }
+#pragma unroll
+      for (int u = 0; u < U; ++u) row((r + u * rpb) * C + cg * 8, vd[u], vx[u], vy[u], va[u]);
+    }
+    for (; r < r1; r += rpb) {
       const long off = r * C + cg * 8;
-      float fd[8], fx[8], fy[8];
-      unpack8(*(const uint4*)(dy + off), fd);
-      unpack8(*(const uint4*)(x + off), fx);
-      if (relu) unpack8(*(const uint4*)(y + off), fy);
-      if (addend) {
-        float fa[8];
-        unpack8(*(const uint4*)(addend + off), fa);
-#pragma unroll
-        for (int i = 0; i < 8; ++i) fd[i] += fa[i];
-      }
-#pragma unroll
-      for (int i = 0; i < 8; ++i) {
-        const float d = (relu && fy[i] <= 0.f) ? 0.f : fd[i];
-        a[i] += d;
-        b[i] += d * (fx[i] - mu[i]) * rs[i];
-      }
+      row(off, *(const uint4*)(dy + off), *(const uint4*)(x + off),
+          relu ? *(const uint4*)(y + off) : z, addend ? *(const uint4*)(addend + off) : z);
     }
   }
 #pragma unroll
@@ -355,59 +373,24 @@ __global__ void __launch_bounds__(256) bn_bwd_apply_kernel(
     bf16_t* __restrict__ dres, long total8, int C, int relu) {
   const int cg8 = C / 8;
   const long stride = (long)gridDim.x * blockDim.x;
-  long i = blockIdx.x * (long)blockDim.x + threadIdx.x;
-  for (; i + stride < total8; i += 2 * stride) {
-    const uint4 da = ((const uint4*)dy)[i], db = ((const uint4*)dy)[i + stride];
-    const uint4 xa = ((const uint4*)x)[i], xb = ((const uint4*)x)[i + stride];
-    uint4 ya = make_uint4(0, 0, 0, 0), yb = ya, aa = ya, ab = ya;
-    if (relu) { ya = ((const uint4*)y)[i]; yb = ((const uint4*)y)[i + stride]; }
-    if (addend) { aa = ((const uint4*)addend)[i]; ab = ((const uint4*)addend)[i + stride]; }
-#pragma unroll
-    for (int h = 0; h < 2; ++h) {
-      const long ii = h ? i + stride : i;
-      const int c0 = (int)(ii % cg8) * 8;
-      float fd[8], fx[8], fy[8];
-      unpack8(h ? db : da, fd);
-      unpack8(h ? xb : xa, fx);
-      if (addend) {
-        float fa[8];
-        unpack8(h ? ab : aa, fa);
-#pragma unroll
-        for (int j = 0; j < 8; ++j) fd[j] += fa[j];
-      }
-      if (relu) {
-        unpack8(h ? yb : ya, fy);
-#pragma unroll
-        for (int j = 0; j < 8; ++j) fd[j] = fy[j] <= 0.f ? 0.f : fd[j];
-      }
-      if (dres) ((uint4*)dres)[ii] = pack8(fd);
-      float o[8];
-#pragma unroll
-      for (int j = 0; j < 8; ++j) {
-        const int c = c0 + j;
-        const float xh = (fx[j] - mean[c]) * rstd[c];
-        o[j] = k1[c] * fd[j] + k2[c] * xh + k3[c];
-      }
-      ((uint4*)dx)[ii] = pack8(o);
-    }
-  }
-  for (; i < total8; i += stride) {
-    const int c0 = (int)(i % cg8) * 8;
-    float fd[8], fx[8], fy[8];
-    unpack8(((const uint4*)dy)[i], fd);
-    unpack8(((const uint4*)x)[i], fx);
+  auto one = [&](const long ii, const uint4 vd, const uint4 vx, const uint4 vy, const uint4 va) {
+    const int c0 = (int)(ii % cg8) * 8;
+    float fd[8], fx[8];
+    unpack8(vd, fd);
+    unpack8(vx, fx);
     if (addend) {
       float fa[8];
-      unpack8(((const uint4*)addend)[i], fa);
+      unpack8(va, fa);
 #pragma unroll
       for (int j = 0; j < 8; ++j) fd[j] += fa[j];
     }
     if (relu) {
-      unpack8(((const uint4*)y)[i], fy);
+      float fy[8];
+      unpack8(vy, fy);
 #pragma unroll
       for (int j = 0; j < 8; ++j) fd[j] = fy[j] <= 0.f ? 0.f : fd[j];
     }
-    if (dres) ((uint4*)dres)[i] = pack8(fd);
+    if (dres) ((uint4*)dres)[ii] = pack8(fd);
     float o[8];
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
@@ -415,11 +398,33 @@ __global__ void __launch_bounds__(256) bn_bwd_apply_kernel(
       const float xh = (fx[j] - mean[c]) * rstd[c];
       o[j] = k1[c] * fd[j] + k2[c] * xh + k3[c];
     }
-    ((uint4*)dx)[i] = pack8(o);
+    ((uint4*)dx)[ii] = pack8(o);
+  };
+  const uint4 z = make_uint4(0, 0, 0, 0);
+  long i = blockIdx.x * (long)blockDim.x + threadIdx.x;
+  // 2 vectors' loads in flight per thread before any use
+  constexpr int U = 2;
+  for (; i + (U - 1) * stride < total8; i += U * stride) {
+    uint4 vd[U], vx[U], vy[U], va[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const long ii = i + u * stride;
+      vd[u] = ((const uint4*)dy)[ii];
+      vx[u] = ((const uint4*)x)[ii];
+      vy[u] = relu ? ((const uint4*)y)[ii] : z;
+      va[u] = addend ? ((const uint4*)addend)[ii] : z;
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) one(i + u * stride, vd[u], vx[u], vy[u], va[u]);
   }
+  for (; i < total8; i += stride)
+    one(i, ((const uint4*)dy)[i], ((const uint4*)x)[i], relu ? ((const uint4*)y)[i] : z,
+        addend ? ((const uint4*)addend)[i] : z);
 }
 
-static int grid_for(long n, int per_thread_vec = 1) {
+// elementwise grids: one thread per 16-B vector up to 2048 blocks (8 per CU);
+// measured: fewer, 4x-unrolled blocks (n / 1024) were slower on ResNet-50
+static int grid_for(long n) {
   long b = (n + 255) / 256;
   if (b > 2048) b = 2048;
   if (b < 1) b = 1;
@@ -475,8 +480,17 @@ void bn_backward(const bf16_t* dy, const bf16_t* addend, const bf16_t* y, const 
   const int nb = (int)((M + rpb - 1) / rpb);
   double* sums = (double*)(ws_f + 4 * C);
   float* part = ws_f + 8 * C;
+  // residual BN: the reduce pass materialises dyr into dres; the apply pass
+  // then runs on (dres, x) as a plain BN backward
   hipLaunchKernelGGL(bn_bwd_reduce_kernel, dim3(nb), dim3(256), 0, s, dy, addend, y, x, mean, rstd, M,
-                     C, rpb, relu, part);
+                     C, rpb, relu, part, dres);
+  if (dres) {
+    dy = dres;
+    addend = nullptr;
+    y = nullptr;
+    relu = 0;
+    dres = nullptr;
+  }
   (void)sums;
   hipLaunchKernelGGL(bn_reduce_finalize_kernel<1>, dim3((C + 15) / 16), dim3(1024), 0, s, part, nb, M,
                      C, 0.f, 0.f, gamma, rstd, dgamma, dbeta, ws_f, ws_f + C, ws_f + 2 * C,

@@ -10,7 +10,8 @@ reference only *models* them: per-tensor gradient sizes in
   16-byte channel vectors;
 * ResNet: BN + residual-add + ReLU fused in one kernel; the residual
   branch's gradient is summed inside the producing BN's backward (a tap, no
-  add kernel); VGG: conv + bias + ReLU fused in the conv epilogue, the ReLU
+  add kernel); the ReLU backward of bn1/bn2 rides in the next conv's dgrad
+  epilogue; VGG: conv + bias + ReLU fused in the conv epilogue, the ReLU
   backward fused into the next layer's dgrad epilogue;
 * every conv weight is re-laid for dgrad once per step in one launch;
 * all weights live in one flat :class:`Arena` per job.
@@ -77,10 +78,10 @@ class ResNet50:
         self.num_classes = num_classes
         self.in_ch = in_ch
 
-    def _bn(self, x, p, key, relu, res=None):
+    def _bn(self, x, p, key, relu, res=None, consumer_masks=False):
         st = self.bn_state[key]
         return Fx.batchnorm(x, p[0], p[1], st.mean, st.var, relu=relu, residual=res,
-                            training=self.training)
+                            training=self.training, consumer_masks=consumer_masks)
 
     def conv_params(self):
         out = [self.stem]
@@ -98,11 +99,13 @@ class ResNet50:
             # the second consumer of y (residual / downsample) goes through a
             # tap: its gradient is summed inside y's producing BN backward
             idn = Fx.residual_tap(y) if "down" not in blk else None
+            # bn1 / bn2 outputs feed exactly one conv each: that conv's dgrad
+            # epilogue applies their ReLU backward mask (in_relu)
             o = Fx.conv2d(y, blk["c1"], bn_stats=True)
-            o = self._bn(o, blk["bn1"], pre + ".bn1", relu=True)
-            o = Fx.conv2d(o, blk["c2"], stride=blk["stride"], pad=1, bn_stats=True)
-            o = self._bn(o, blk["bn2"], pre + ".bn2", relu=True)
-            o = Fx.conv2d(o, blk["c3"], bn_stats=True)
+            o = self._bn(o, blk["bn1"], pre + ".bn1", relu=True, consumer_masks=True)
+            o = Fx.conv2d(o, blk["c2"], stride=blk["stride"], pad=1, in_relu=True, bn_stats=True)
+            o = self._bn(o, blk["bn2"], pre + ".bn2", relu=True, consumer_masks=True)
+            o = Fx.conv2d(o, blk["c3"], in_relu=True, bn_stats=True)
             if "down" in blk:
                 idn = Fx.conv2d(Fx.residual_tap(y), blk["down"], stride=blk["stride"], bn_stats=True)
                 idn = self._bn(idn, blk["down_bn"], pre + ".dbn", relu=False)

@@ -359,7 +359,8 @@ def residual_tap(y: torch.Tensor) -> torch.Tensor:
 class _BN(Function):
     @staticmethod
     def forward(ctx, x, res, token, g: Param, b: Param, run_mean, run_var, relu: bool, eps: float,
-                momentum: float, training: bool, slot: Optional[GradSlot] = None):
+                momentum: float, training: bool, slot: Optional[GradSlot] = None,
+                consumer_masks: bool = False):
         C = x.shape[-1]
         if x.is_cuda:
             y = torch.empty_like(x)
@@ -397,9 +398,13 @@ class _BN(Function):
             if relu:
                 yf = yf.clamp_min(0)
             y = yf.reshape(x.shape).to(BF16)
-        ctx.g, ctx.b, ctx.relu, ctx.has_res = g, b, relu, res is not None
+        # consumer_masks: the only consumer (a conv with in_relu) already zeroes
+        # the gradient where y <= 0 in its dgrad epilogue -- the backward here
+        # neither re-reads y nor keeps it alive
+        bwd_relu = relu and not consumer_masks
+        ctx.g, ctx.b, ctx.relu, ctx.has_res = g, b, bwd_relu, res is not None
         ctx.slot = slot
-        ctx.save_for_backward(x, y if relu else None, mean, rstd)
+        ctx.save_for_backward(x, y if bwd_relu else None, mean, rstd)
         return y
 
     @staticmethod
@@ -434,7 +439,7 @@ class _BN(Function):
             dres = dyf.reshape(x.shape).to(BF16) if ctx.has_res else None
         g.grad_ready()
         b.grad_ready()
-        return dx, dres, None, None, None, None, None, None, None, None, None, None
+        return dx, dres, None, None, None, None, None, None, None, None, None, None, None
 
 
 def _bn_infer_gpu(x, res, scale, shift, relu):
@@ -450,15 +455,19 @@ def _bn_infer_gpu(x, res, scale, shift, relu):
 def batchnorm(x: torch.Tensor, g: Param, b: Param, run_mean: Optional[torch.Tensor] = None,
               run_var: Optional[torch.Tensor] = None, relu: bool = False,
               residual: Optional[torch.Tensor] = None, eps: float = 1e-5, momentum: float = 0.1,
-              training: bool = True) -> torch.Tensor:
-    """y = relu(BN(x) + residual) over the last (channel) dim of an NHWC tensor."""
+              training: bool = True, consumer_masks: bool = False) -> torch.Tensor:
+    """y = relu(BN(x) + residual) over the last (channel) dim of an NHWC tensor.
+
+    ``consumer_masks``: y has exactly one consumer, a ``conv2d(..., in_relu=True)``
+    whose dgrad applies the ReLU backward mask (reading y once there instead of
+    twice in this BN's backward passes)."""
     if not x.is_contiguous():
         x = x.contiguous()
     if residual is not None and not residual.is_contiguous():
         residual = residual.contiguous()
     slot = GradSlot() if (x.is_cuda and training and torch.is_grad_enabled()) else None
     y = _BN.apply(x, residual, g.arena.token, g, b, run_mean, run_var, relu, eps, momentum,
-                  training, slot)
+                  training, slot, consumer_masks and relu and residual is None)
     if slot is not None:
         y._tam_slot = slot
     return y
