@@ -59,6 +59,11 @@ import torch.distributed as dist  # noqa: E402
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
+if os.environ.get("TAM_STACK_DUMP_S"):         # hang diagnosis: periodic all-thread stacks
+    import faulthandler
+
+    faulthandler.dump_traceback_later(float(os.environ["TAM_STACK_DUMP_S"]), repeat=True)
+
 from tiresias_amd.config import ClusterSpec, SimConfig  # noqa: E402
 from tiresias_amd.core.job import JobSpec  # noqa: E402
 from tiresias_amd.executor.cluster_runtime import ReplayJob, Worker, run_replay  # noqa: E402
@@ -251,10 +256,17 @@ def main():
     n = max(a.gpus, world)
     use_cuda = torch.cuda.is_available() and not a.cpu
     work_s = a.work_s if a.work_s is not None else (5.0 if use_cuda else 0.5)
-    device = torch.device("cuda", local) if use_cuda else torch.device("cpu")
+    # TAM_SHARED_GPU=1: multi-rank rehearsal on a ONE-GPU box -- every rank on
+    # cuda:0, world and gang communicators over gloo (RCCL refuses two ranks
+    # on one device); everything else is the N-GPU code path
+    shared_gpu = use_cuda and world > 1 and os.environ.get("TAM_SHARED_GPU") == "1"
+    device = torch.device("cuda", 0 if shared_gpu else local) if use_cuda else torch.device("cpu")
     ctrl_pg = world_pg = None
     if world > 1:
-        if use_cuda:
+        if shared_gpu:
+            torch.cuda.set_device(device)
+            dist.init_process_group("gloo", timeout=datetime.timedelta(seconds=300))
+        elif use_cuda:
             torch.cuda.set_device(device)
             dist.init_process_group("nccl", device_id=device,
                                     timeout=datetime.timedelta(seconds=300))
@@ -294,6 +306,7 @@ def main():
 
     cfg = make(a.policy, a.placement)
     worker = Worker(rank, world, device, world_pg, use_graph=use_cuda and not a.no_graph,
+                    gang_backend="gloo" if shared_gpu else None,
                     pool_cap=0 if a.no_pool else 2, hbm_budget_gb=a.hbm_budget_gb)
 
     def sync():

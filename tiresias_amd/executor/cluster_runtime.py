@@ -671,8 +671,22 @@ class Worker:
         if any(a["op"] == "drop" for a in plan["actions"]):
             self.reclaim(64.0)
         if p2p_ops:
+            staged = []
+            if self.device.type == "cuda" and dist.get_backend(self.world_pg) == "gloo":
+                # gloo P2P moves host memory only (the one-GPU multi-rank
+                # rehearsal, bench TAM_SHARED_GPU=1): stage through the host
+                torch.cuda.synchronize(self.device)
+                ops = []
+                for o in p2p_ops:
+                    h = o.tensor.cpu() if o.op is dist.isend else torch.empty(o.tensor.shape, dtype=o.tensor.dtype)
+                    ops.append(dist.P2POp(o.op, h, o.peer))
+                    if o.op is dist.irecv:
+                        staged.append((o.tensor, h))
+                p2p_ops = ops
             for w in dist.batch_isend_irecv(p2p_ops):
                 w.wait()
+            for dst, h in staged:
+                dst.copy_(h)
         # holders that are no longer members free their replica after sending
         for a in plan["actions"]:
             if a["op"] == "start" and a["source"] == "p2p":
