@@ -33,3 +33,28 @@ def test_simulator_uses_measured_pairs(tmp_path):
     # b runs at 1/1.25 while sharing; a at 1/2: b ends first at 125 s (a has done 62.5),
     # then a runs alone for 37.5 s more -> 162.5 s
     assert s["makespan"] == pytest.approx(162.5, rel=1e-6)
+
+
+def test_measured_spread_slowdown_drives_progress_rate(tmp_path):
+    """With --enable_network_costs and a measured skew profile, a gang spread
+    over two (virtual) nodes progresses at 1/slowdown measured for its model
+    (profiler/comm.py output), not the analytic ring formula; a model the
+    profile does not cover keeps the analytic rate."""
+    import json
+
+    from tiresias_amd.cluster.network import measured_spread_rate
+    from tiresias_amd.config import ClusterSpec, SimConfig
+    from tiresias_amd.core.job import JobSpec
+    from tiresias_amd.engine.sim import Simulator
+
+    assert measured_spread_rate(1.5, 1) == 1.0
+    assert abs(measured_spread_rate(1.5, 2) - 1 / 1.5) < 1e-12
+    assert measured_spread_rate(1.5, 4) < measured_spread_rate(1.5, 2)      # ring: 2(k-1)/k
+    path = tmp_path / "skew.json"
+    path.write_text(json.dumps({"vgg16": {"slowdown": 1.6, "sensitive": True}}))
+    cfg = SimConfig(schedule="fifo", scheme="yarn", skew_profile=str(path), enable_network_costs=True,
+                    cluster=ClusterSpec(num_switch=1, num_node_p_switch=2, num_gpu_p_node=4))
+    # 6 GPUs cannot fit one 4-GPU node: yarn spreads the gang over both nodes
+    sim = Simulator(cfg, [JobSpec("v", 0.0, 16.0, 6, model="vgg16")])
+    s = sim.run()
+    assert abs(sim.jobs["v"].end_time - 16.0 * 1.6) < 1e-6, s

@@ -37,7 +37,7 @@ import time
 from typing import Dict, List, Optional
 
 from ..cluster.interference import InterferenceModel
-from ..cluster.network import network_rate
+from ..cluster.network import measured_spread_rate, network_rate
 from ..cluster.topology import Cluster, PlacementError
 from ..config import SimConfig
 from ..core.job import Job, JobSpec, JobState
@@ -68,9 +68,9 @@ class Simulator:
         self.scheme = scheme
         self.cluster = Cluster(cfg.cluster, pack=pack, max_tasks_per_gpu=cfg.max_tasks_per_gpu,
                                headroom_mb=cfg.gpu_mem_headroom_mb, virtual_nodes=cfg.virtual_nodes)
+        self.oracle = SensitivityOracle(cfg.skew_threshold, measured_path=cfg.skew_profile)
         self.placement = make_placement(scheme, rng=random.Random(cfg.seed + 1),
-                                        sensitivity=SensitivityOracle(cfg.skew_threshold,
-                                                                      measured_path=cfg.skew_profile),
+                                        sensitivity=self.oracle,
                                         cluster_gpus_per_node=self.cluster.spec.num_gpu_p_node,
                                         pack=pack)
         self.jobs: Dict[str, Job] = {}
@@ -134,8 +134,12 @@ class Simulator:
         r = 1.0
         nodes = self.cluster.nodes_of(j.job_id)
         if self.cfg.enable_network_costs and len(nodes) > 1:
-            r *= network_rate(j, len(nodes), self.cluster.spec.bandwidth_mbps,
-                              self.cluster.spec.internode_latency)
+            sd = self.oracle.slowdown(j.spec.model or "")
+            if sd is not None:
+                r *= measured_spread_rate(sd, len(nodes))
+            else:
+                r *= network_rate(j, len(nodes), self.cluster.spec.bandwidth_mbps,
+                                  self.cluster.spec.internode_latency)
         if self.cluster.pack:
             nb = self.cluster.neighbours(j.job_id)
             if nb:
