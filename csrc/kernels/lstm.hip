@@ -373,11 +373,29 @@ __global__ void __launch_bounds__(64 * PL_W * CH, 4) lstm_persist_bwd_kernel(
   const bool cell = threadIdx.x < 16 * U;
   const int cr = threadIdx.x / U, cu = threadIdx.x % U;
   float dc_reg = 0.f;
-  for (int s = 0; s < T; ++s) {
-    const int t = reverse ? s : T - 1 - s;             // backward order
-    const int fwd_idx = reverse ? T - 1 - t : t;       // position of t in the forward order
+  // cell operands of a step (dH, the 5 saved activations, c_{t-1}) do not
+  // depend on the recurrence: they are loaded one step AHEAD, issued after
+  // the hand-off signal and before the wait, so their HBM latency hides
+  // behind the wait + the next MFMA chain instead of following it
+  float nx_dh = 0.f, nx_a[5] = {0.f, 0.f, 0.f, 0.f, 0.f}, nx_cp = 0.f;
+  auto load_cell = [&](int s) {
+    const int t = reverse ? s : T - 1 - s;
+    const int fwd_idx = reverse ? T - 1 - t : t;
     const long row = (long)t * B + b0 + cr;
     const int j = j0 + cu;
+    nx_dh = dH[row * Hd + j];
+    const float* a = act + row * 5 * Hd + j;
+#pragma unroll
+    for (int q = 0; q < 5; ++q) nx_a[q] = a[(long)q * Hd];
+    nx_cp = 0.f;
+    if (fwd_idx > 0) {
+      const int tp = reverse ? t + 1 : t - 1;
+      nx_cp = cs[((long)tp * B + b0 + cr) * Hd + j];
+    }
+  };
+  if (cell) load_cell(0);
+  for (int s = 0; s < T; ++s) {
+    const int t = reverse ? s : T - 1 - s;             // backward order
     f32x4_t acc = {0.f, 0.f, 0.f, 0.f};
     if (s > 0) {
       const int tn = reverse ? t - 1 : t + 1;
@@ -397,19 +415,10 @@ __global__ void __launch_bounds__(64 * PL_W * CH, 4) lstm_persist_bwd_kernel(
         }
       }
     }
-    // the cell operands are loaded after the MFMA chain (their registers
-    // would otherwise be live across it)
-    float dhv = 0.f, av[5] = {0.f, 0.f, 0.f, 0.f, 0.f}, cpv = 0.f;
-    if (cell) {
-      dhv = dH[row * Hd + j];
-      const float* a = act + row * 5 * Hd + j;
+    const float dhv = nx_dh, cpv = nx_cp;
+    float av[5];
 #pragma unroll
-      for (int q = 0; q < 5; ++q) av[q] = a[(long)q * Hd];
-      if (fwd_idx > 0) {
-        const int tp = reverse ? t + 1 : t - 1;
-        cpv = cs[((long)tp * B + b0 + cr) * Hd + j];
-      }
-    }
+    for (int q = 0; q < 5; ++q) av[q] = nx_a[q];
 #pragma unroll
     for (int r = 0; r < 4; ++r) red[ksl][4 * (lane >> 4) + r][16 * half + (lane & 15)] = acc[r];
     __syncthreads();
@@ -438,6 +447,7 @@ __global__ void __launch_bounds__(64 * PL_W * CH, 4) lstm_persist_bwd_kernel(
       }
       if (s + 1 < T) pl_signal(sync, bt);
     }
+    if (cell && s + 1 < T) load_cell(s + 1);   // after the signal's vmcnt(0) drain
     if (s + 1 < T) pl_wait(sync, bt, (unsigned)(s + 1) * (unsigned)(Hd / U));
   }
 }

@@ -13,7 +13,8 @@ from pathlib import Path
 
 import torch
 
-_LIB = Path(__file__).resolve().parent.parent / "_C.so"
+# TAM_LIB_PATH: an alternative build of the same library (A/B measurements)
+_LIB = Path(os.environ.get("TAM_LIB_PATH") or Path(__file__).resolve().parent.parent / "_C.so")
 _lock = threading.Lock()
 _loaded = False
 
