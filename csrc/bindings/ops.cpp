@@ -668,12 +668,12 @@ void lstm_step_fwd_op(const Tensor& gx, const Tensor& w_hh, const optional<Tenso
 
 // persistent whole-sequence recurrence; returns false when the shape or
 // co-residency is not supported (caller runs the per-step path).
-// sync: int32 [32 * (B/16 + 1)] = {error flag, per-batch-tile counters on
-// lines of their own (zeroed by the launcher)}
+// sync: int32 [32 * (4 * B/16 + 1)] = {error flag, up to 4 arrival counters
+// per batch tile on lines of their own (zeroed by the launcher)}
 static void check_sync(const Tensor& sync, int64_t B) {
   TORCH_CHECK(sync.is_cuda() && sync.scalar_type() == at::kInt && sync.is_contiguous() &&
-              sync.numel() >= 32 * (B / 16 + 1),
-              "tam.lstm_seq: sync must be a contiguous int32 tensor of >= 32 * (B/16 + 1) elements");
+              sync.numel() >= 32 * (4 * (B / 16) + 1),
+              "tam.lstm_seq: sync must be a contiguous int32 tensor of >= 32 * (4 * B/16 + 1) elements");
 }
 bool lstm_seq_fwd_op(const Tensor& gx, const Tensor& w_hh, const Tensor& hs, const Tensor& cs,
                      const Tensor& act, bool reverse, const Tensor& sync) {
@@ -711,6 +711,7 @@ bool lstm_seq_bwd_op(const Tensor& act, const Tensor& cs, const Tensor& dH, cons
 }
 
 void lstm_seq_policy_op(int64_t ch) { tam::lstm_seq_policy((int)ch); }
+void lstm_seq_shards_op(int64_t ns) { tam::lstm_seq_shards((int)ns); }
 
 void lstm_bwd_op(const Tensor& act, const optional<Tensor>& c_prev, const optional<Tensor>& dh,
                  const optional<Tensor>& dc_next, const optional<Tensor>& dgates,
@@ -762,6 +763,7 @@ TORCH_LIBRARY(tam, m) {
   m.def("lstm_seq_forward(Tensor gx, Tensor w_hh, Tensor(a!) hs, Tensor(b!) cs, Tensor(c!) act, bool reverse, Tensor(d!) sync) -> bool", &lstm_seq_fwd_op);
   m.def("lstm_seq_backward(Tensor act, Tensor cs, Tensor dH, Tensor w_hh, Tensor(a!) dG, bool reverse, Tensor(b!) sync) -> bool", &lstm_seq_bwd_op);
   m.def("lstm_seq_policy(int ch) -> ()", &lstm_seq_policy_op);
+  m.def("lstm_seq_shards(int ns) -> ()", &lstm_seq_shards_op);
   m.def("lstm_cell_forward(Tensor gates, Tensor? c_prev, Tensor(a!) c_out, Tensor(b!) h_out, Tensor(c!)? h_f32, Tensor(d!) act) -> ()", &lstm_fwd_op);
   m.def("lstm_cell_backward(Tensor act, Tensor? c_prev, Tensor? dh, Tensor? dc_next, Tensor(a!)? dgates, Tensor(b!)? dc_prev, Tensor(c!)? dgates_bf16) -> ()", &lstm_bwd_op);
 }

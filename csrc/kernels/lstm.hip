@@ -195,17 +195,24 @@ typedef __attribute__((address_space(1))) unsigned pl_gu32;
 typedef __attribute__((address_space(1))) unsigned long long pl_gu64;
 #define PL_RLX __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT
 
-// sync layout (int32 words): [0] error flag, [32 * (bt + 1)] arrival counter of batch tile bt
-__device__ __forceinline__ void pl_signal(unsigned* sync, int bt) {
+// sync layout (int32 words): [0] error flag; [32 * (1 + bt * ns + k)] arrival
+// counter k < ns of batch tile bt, each on a 128-B line of its own. With
+// ns > 1 the Hd/U producers of a batch tile arrive on ns counters (unit tile
+// ut on counter ut % ns): a fan-in of Hd/U atomics on one word serialises at
+// ~12 ns each (MI355X_MICROARCH.md, "fanin"); the consumer's first ns lanes
+// poll one counter each.
+constexpr int PL_NS_MAX = 4;
+__device__ __forceinline__ void pl_signal(unsigned* sync, int line) {
   // caller: the ONE storing wave, after its sc1 stores
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  if ((threadIdx.x & 63) == 0) __hip_atomic_fetch_add((pl_gu32*)(sync + 32 * (bt + 1)), 1u, PL_RLX);
+  if ((threadIdx.x & 63) == 0) __hip_atomic_fetch_add((pl_gu32*)(sync + 32 * (1 + line)), 1u, PL_RLX);
 }
 
-__device__ __forceinline__ void pl_wait(unsigned* sync, int bt, unsigned target) {
-  if (threadIdx.x == 0) {
+// target: arrivals expected on EACH of the ns counters line0 .. line0 + ns - 1
+__device__ __forceinline__ void pl_wait(unsigned* sync, int line0, int ns, unsigned target) {
+  if (threadIdx.x < (unsigned)ns) {
     unsigned polls = 0;
-    while (__hip_atomic_load((pl_gu32*)(sync + 32 * (bt + 1)), PL_RLX) < target) {
+    while (__hip_atomic_load((pl_gu32*)(sync + 32 * (1 + line0 + threadIdx.x)), PL_RLX) < target) {
       __builtin_amdgcn_s_sleep(1);
       if (++polls > PL_SPIN) {
         __hip_atomic_fetch_or((pl_gu32*)sync, 1u, PL_RLX);
@@ -235,7 +242,7 @@ __device__ __forceinline__ s16x8_t pl_ld16(__amdgpu_buffer_rsrc_t r, unsigned by
 template <int KW, int CH>   // KW: k-steps of 32 per wave = Hd / (32 * PL_W)
 __global__ void __launch_bounds__(64 * PL_W * CH, 4) lstm_persist_fwd_kernel(
     const float* __restrict__ gx, const bf16_t* __restrict__ w, bf16_t* hs, float* __restrict__ cs,
-    float* __restrict__ act, int T, int B, int Hd, int reverse, unsigned* sync) {
+    float* __restrict__ act, int T, int B, int Hd, int reverse, unsigned* sync, int ns) {
   constexpr int U = 16 * CH;                 // units per workgroup
   __shared__ float red[PL_W][16][4 * U + 1];
   __shared__ __attribute__((aligned(16))) bf16_t hbuf[16][U];
@@ -317,9 +324,9 @@ __global__ void __launch_bounds__(64 * PL_W * CH, 4) lstm_persist_fwd_kernel(
         const unsigned long long v = *(const unsigned long long*)&hbuf[r][4 * q];
         __hip_atomic_store((pl_gu64*)(hs + ((long)t * B + b0 + r) * Hd + j0 + 4 * q), v, PL_RLX);
       }
-      if (s + 1 < T) pl_signal(sync, bt);
+      if (s + 1 < T) pl_signal(sync, bt * ns + ut % ns);
     }
-    if (s + 1 < T) pl_wait(sync, bt, (unsigned)(s + 1) * (unsigned)(Hd / U));
+    if (s + 1 < T) pl_wait(sync, bt * ns, ns, (unsigned)(s + 1) * (unsigned)(Hd / U / ns));
   }
 }
 
@@ -330,7 +337,7 @@ __global__ void __launch_bounds__(64 * PL_W * CH, 4) lstm_persist_fwd_kernel(
 template <int KW, int CH>   // KW: k-steps of 32 per wave = 4 Hd / (32 * PL_W)
 __global__ void __launch_bounds__(64 * PL_W * CH, 4) lstm_persist_bwd_kernel(
     const float* __restrict__ act, const float* __restrict__ cs, const float* __restrict__ dH,
-    const bf16_t* __restrict__ w, bf16_t* dG, int T, int B, int Hd, int reverse, unsigned* sync) {
+    const bf16_t* __restrict__ w, bf16_t* dG, int T, int B, int Hd, int reverse, unsigned* sync, int ns) {
   constexpr int U = 16 * CH;
   // W fragments: the first KWR k-steps in VGPRs, the rest in LDS (the whole
   // slice in VGPRs needs > 128 of them and spills; CH = 1 only: 2 blocks/CU
@@ -445,10 +452,10 @@ __global__ void __launch_bounds__(64 * PL_W * CH, 4) lstm_persist_bwd_kernel(
         __hip_atomic_store((pl_gu64*)(dG + ((long)t * B + b0 + r) * 4 * Hd + g * Hd + j0 + 4 * q), v,
                            PL_RLX);
       }
-      if (s + 1 < T) pl_signal(sync, bt);
+      if (s + 1 < T) pl_signal(sync, bt * ns + ut % ns);
     }
     if (cell && s + 1 < T) load_cell(s + 1);   // after the signal's vmcnt(0) drain
-    if (s + 1 < T) pl_wait(sync, bt, (unsigned)(s + 1) * (unsigned)(Hd / U));
+    if (s + 1 < T) pl_wait(sync, bt * ns, ns, (unsigned)(s + 1) * (unsigned)(Hd / U / ns));
   }
 }
 
@@ -473,6 +480,13 @@ static bool pl_fits(const void* kern, int threads, int grid) {
 static int g_pl_ch = 0;   // 0: auto (1), 1 / 2: forced
 void lstm_seq_policy(int ch) { g_pl_ch = ch; }
 
+// arrival counters per batch tile (1, 2 or 4). Measured (tools/ab_lstm_shards.py,
+// GNMT hipGraph step, interleaved): 1 -> 10.95 ms, 2 -> 10.71, 4 -> 10.97. With
+// B = 64 (4 batch tiles) a tile's workgroups bt + 4 ut sit on two XCDs under
+// round-robin dispatch, split by ut parity: 2 counters = one per XCD
+static int g_pl_ns = 2;
+void lstm_seq_shards(int ns) { g_pl_ns = (ns == 2 || ns == 4) ? ns : 1; }
+
 static int pl_ch(int Hd) {
   if (g_pl_ch == 1 || g_pl_ch == 2) return g_pl_ch;
   return 1;   // measured: 2 is slower (latency-bound steps: fwd 220 vs 196, bwd 499 vs 318 us/seq)
@@ -484,9 +498,10 @@ static bool pl_fwd(const float* gx, const bf16_t* w_hh, bf16_t* hs, float* cs, f
   const int grid = (B / 16) * (Hd / (16 * CH));
   auto k = lstm_persist_fwd_kernel<KW, CH>;
   if (!pl_fits((const void*)k, 64 * PL_W * CH, grid)) return false;
-  zero_async(sync + 32, (size_t)(B / 16) * 128, s);
+  const int ns = (Hd / (16 * CH)) % g_pl_ns == 0 ? g_pl_ns : 1;
+  zero_async(sync + 32, (size_t)(B / 16) * ns * 128, s);
   hipLaunchKernelGGL(k, dim3(grid), dim3(64 * PL_W * CH), 0, s, gx, w_hh, hs, cs, act, T, B, Hd, reverse,
-                     sync);
+                     sync, ns);
   return true;
 }
 
@@ -496,9 +511,10 @@ static bool pl_bwd(const float* act, const float* cs, const float* dH, const bf1
   const int grid = (B / 16) * (Hd / (16 * CH));
   auto k = lstm_persist_bwd_kernel<KW, CH>;
   if (!pl_fits((const void*)k, 64 * PL_W * CH, grid)) return false;
-  zero_async(sync + 32, (size_t)(B / 16) * 128, s);
+  const int ns = (Hd / (16 * CH)) % g_pl_ns == 0 ? g_pl_ns : 1;
+  zero_async(sync + 32, (size_t)(B / 16) * ns * 128, s);
   hipLaunchKernelGGL(k, dim3(grid), dim3(64 * PL_W * CH), 0, s, act, cs, dH, w_hh, dG, T, B, Hd, reverse,
-                     sync);
+                     sync, ns);
   return true;
 }
 

@@ -809,7 +809,7 @@ def test_lstm_persistent_sequence(gpu, T_, B, Hd, reverse, ch):
     hs = torch.empty(T_, B, Hd, device=gpu, dtype=BF)
     cs = torch.empty(T_, B, Hd, device=gpu)
     act = torch.empty(T_, B, 5 * Hd, device=gpu)
-    sync = torch.zeros(32 * (B // 16 + 1), dtype=torch.int32, device=gpu)
+    sync = torch.zeros(32 * (4 * (B // 16) + 1), dtype=torch.int32, device=gpu)
     assert T().lstm_seq_forward(gx, w, hs, cs, act, reverse, sync)
     torch.cuda.synchronize()
     assert int(sync[0]) == 0, "grid barrier timed out"
@@ -898,3 +898,34 @@ def test_trainer_async_spill_survives_immediate_reuse(gpu):
     t.step()
     torch.cuda.synchronize()
     assert eng.stats()[1] == 0          # host copies released after the restore completed
+
+
+@pytest.mark.parametrize("ns", [2, 4])
+def test_lstm_persistent_sharded_counters_bitwise(gpu, ns):
+    """Arrival counters sharded over ns lines per batch tile (fan-in relief)
+    change only the hand-off bookkeeping: outputs are bit-identical to the
+    single-counter run, and no barrier times out."""
+    T_, B, Hd = 10, 64, 1024
+    torch.manual_seed(5)
+    gx = torch.randn(T_, B, 4 * Hd, device=gpu)
+    w = (torch.randn(4 * Hd, Hd, device=gpu) / Hd ** 0.5).to(BF)
+    dH = torch.randn(T_, B, Hd, device=gpu)
+    outs = []
+    try:
+        for k in (1, ns):
+            T().lstm_seq_shards(k)
+            hs = torch.empty(T_, B, Hd, device=gpu, dtype=BF)
+            cs = torch.empty(T_, B, Hd, device=gpu)
+            act = torch.empty(T_, B, 5 * Hd, device=gpu)
+            dG = torch.empty(T_, B, 4 * Hd, device=gpu, dtype=BF)
+            sync = torch.zeros(32 * (4 * (B // 16) + 1), dtype=torch.int32, device=gpu)
+            assert T().lstm_seq_forward(gx, w, hs, cs, act, False, sync)
+            sync2 = torch.zeros_like(sync)
+            assert T().lstm_seq_backward(act, cs, dH, w, dG, False, sync2)
+            torch.cuda.synchronize()
+            assert int(sync[0]) == 0 and int(sync2[0]) == 0, "grid barrier timed out"
+            outs.append((hs, cs, dG))
+    finally:
+        T().lstm_seq_shards(2)
+    for a, b in zip(*outs):
+        assert torch.equal(a, b)

@@ -45,8 +45,8 @@ _SYNCS: list = []          # recent barrier/error words (tests read the error fl
 
 
 def _sync(dev, B: int) -> torch.Tensor:
-    # [0] error flag, [32 * (bt + 1)] arrival counter of batch tile bt (own line each)
-    t = torch.zeros(32 * (B // 16 + 1), dtype=torch.int32, device=dev)
+    # [0] error flag, up to 4 arrival counters per batch tile (own 128-B line each)
+    t = torch.zeros(32 * (4 * (B // 16) + 1), dtype=torch.int32, device=dev)
     _SYNCS.append(t)
     del _SYNCS[:-64]
     return t

@@ -20,7 +20,7 @@ for (T_, B, Hd, rev) in [(50, 64, 1024, False), (50, 64, 1024, True)]:
     hs = torch.empty(T_, B, Hd, device=gpu, dtype=torch.bfloat16)
     cs = torch.empty(T_, B, Hd, device=gpu)
     act = torch.empty(T_, B, 5 * Hd, device=gpu)
-    sync = torch.zeros(32 * (B // 16 + 1), dtype=torch.int32, device=gpu)
+    sync = torch.zeros(32 * (4 * (B // 16) + 1), dtype=torch.int32, device=gpu)
     assert T.lstm_seq_forward(gx, w, hs, cs, act, rev, sync)
     dH = torch.randn(T_, B, Hd, generator=g).to(gpu)
     dG = torch.empty(T_, B, 4 * Hd, device=gpu, dtype=torch.bfloat16)
