@@ -419,6 +419,7 @@ void launch_gemm8p(const bf16_t* A, long lda, bool ak, const bf16_t* B, long ldb
 void gemm8p_splitk(const bf16_t* A, long lda, bool ak, const bf16_t* B, long ldb, bool bk, int M,
                    int N, int K, const Epi& ep, int splits, float* ws, hipStream_t s, int tile = 256);
 int gemm8p_slab_splits(int M, int N, int K, int tile = 256);
+void gemm8p_slab_force(int sp);   // > 0: forced slab split count (A/B sweeps); 0: heuristic
 // 128 or 256: the tile the auto policy picks for this shape
 int gemm8p_tile(int M, int N, int K);
 

@@ -165,7 +165,11 @@ __global__ void __launch_bounds__(256) p8_slab_reduce_kernel(const float* __rest
   }
 }
 
+static int g_p8_force_sp = 0;   // > 0: slab split count forced (A/B sweeps)
+void gemm8p_slab_force(int sp) { g_p8_force_sp = sp > 0 ? sp : 0; }
+
 int gemm8p_slab_splits(int M, int N, int K, int tile) {
+  if (g_p8_force_sp) return g_p8_force_sp;
   const int T = tile == 128 ? 128 : 256;
   const long t = (long)cdiv(M, T) * cdiv(N, T);
   const int kt = K / P8_BK;
