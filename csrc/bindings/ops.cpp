@@ -680,7 +680,8 @@ void lstm_step_fwd_op(const Tensor& gx, const Tensor& w_hh, const optional<Tenso
 // persistent whole-sequence recurrence; returns false when the shape or
 // co-residency is not supported (caller runs the per-step path).
 // sync: int32 [32 * (4 * B/16 + 1)] = {error flag, up to 4 arrival counters
-// per batch tile on lines of their own (zeroed by the launcher)}
+// per batch tile on lines of their own} -- all zeroed by the launcher (the
+// caller may pass uninitialised memory)
 static void check_sync(const Tensor& sync, int64_t B) {
   TORCH_CHECK(sync.is_cuda() && sync.scalar_type() == at::kInt && sync.is_contiguous() &&
               sync.numel() >= 32 * (4 * (B / 16) + 1),

@@ -499,7 +499,7 @@ static bool pl_fwd(const float* gx, const bf16_t* w_hh, bf16_t* hs, float* cs, f
   auto k = lstm_persist_fwd_kernel<KW, CH>;
   if (!pl_fits((const void*)k, 64 * PL_W * CH, grid)) return false;
   const int ns = (Hd / (16 * CH)) % g_pl_ns == 0 ? g_pl_ns : 1;
-  zero_async(sync + 32, (size_t)(B / 16) * ns * 128, s);
+  zero_async(sync, (size_t)(1 + (B / 16) * ns) * 128, s);   // error flag line + counters
   hipLaunchKernelGGL(k, dim3(grid), dim3(64 * PL_W * CH), 0, s, gx, w_hh, hs, cs, act, T, B, Hd, reverse,
                      sync, ns);
   return true;
@@ -512,7 +512,7 @@ static bool pl_bwd(const float* act, const float* cs, const float* dH, const bf1
   auto k = lstm_persist_bwd_kernel<KW, CH>;
   if (!pl_fits((const void*)k, 64 * PL_W * CH, grid)) return false;
   const int ns = (Hd / (16 * CH)) % g_pl_ns == 0 ? g_pl_ns : 1;
-  zero_async(sync + 32, (size_t)(B / 16) * ns * 128, s);
+  zero_async(sync, (size_t)(1 + (B / 16) * ns) * 128, s);   // error flag line + counters
   hipLaunchKernelGGL(k, dim3(grid), dim3(64 * PL_W * CH), 0, s, act, cs, dH, w_hh, dG, T, B, Hd, reverse,
                      sync, ns);
   return true;

@@ -46,10 +46,16 @@ _SYNCS: list = []          # recent barrier/error words (tests read the error fl
 
 def _sync(dev, B: int) -> torch.Tensor:
     # [0] error flag, up to 4 arrival counters per batch tile (own 128-B line each)
-    t = torch.zeros(32 * (4 * (B // 16) + 1), dtype=torch.int32, device=dev)
-    _SYNCS.append(t)
-    del _SYNCS[:-64]
-    return t
+    # zeroed by the kernel launcher (stream-ordered), no fill kernel here; only
+    # buffers of launches that ran are kept for persist_errors (_ran)
+    return torch.empty(32 * (4 * (B // 16) + 1), dtype=torch.int32, device=dev)
+
+
+def _ran(ok: bool, t: torch.Tensor) -> bool:
+    if ok:
+        _SYNCS.append(t)
+        del _SYNCS[:-64]
+    return ok
 
 
 def persist_errors() -> int:
@@ -72,7 +78,8 @@ class _LSTMLayer(Function):
         if dev.type == "cuda":
             _T().gemm(x2, True, w_ih.w, True, G, 0, b.w, False, None, 1.0, False)
             Gv = G.view(T, B, 4 * Hd)
-            ran = PERSIST and _T().lstm_seq_forward(Gv, w_hh.w, Hs, Cs, act, reverse, _sync(dev, B))
+            sy = _sync(dev, B)
+            ran = PERSIST and _ran(_T().lstm_seq_forward(Gv, w_hh.w, Hs, Cs, act, reverse, sy), sy)
             steps = [] if ran else steps
             prev = None
             # the fused per-timestep kernel (lstm_step_forward) ties GEMM + cell +
@@ -120,12 +127,14 @@ class _LSTMLayer(Function):
         dev = x.device
         dHf = dH.float().contiguous()              # dh accumulator (fp32), updated in place
         dG = torch.empty(T, B, 4 * Hd, dtype=BF16, device=dev)
-        dc = torch.zeros(B, Hd, dtype=torch.float32, device=dev)
-        dc2 = torch.empty_like(dc)
         order = list(range(T - 1, -1, -1) if reverse else range(T))
         rev_order = order[::-1]
         if dev.type == "cuda":
-            ran = PERSIST and _T().lstm_seq_backward(act, Cs, dHf, w_hh.w, dG, reverse, _sync(dev, B))
+            sy = _sync(dev, B)
+            ran = PERSIST and _ran(_T().lstm_seq_backward(act, Cs, dHf, w_hh.w, dG, reverse, sy), sy)
+            if not ran:                            # per-step path: cell-state gradient carry
+                dc = torch.zeros(B, Hd, dtype=torch.float32, device=dev)
+                dc2 = torch.empty_like(dc)
             for k, t in enumerate([] if ran else rev_order):
                 prev = rev_order[k + 1] if k + 1 < T else None   # the step that ran before t
                 _T().lstm_cell_backward(act[t], Cs[prev] if prev is not None else None, dHf[t], dc,
@@ -134,15 +143,16 @@ class _LSTMLayer(Function):
                 if prev is not None:
                     _T().gemm(dG[t], True, w_hh.w, False, dHf[prev], 1, None, False, None, 1.0, True)
             dG2 = dG.view(T * B, 4 * Hd)
-            # h_{t-1} for each t (zero for the first step in processing order)
-            Hprev = torch.zeros_like(Hs)
-            if T > 1:
-                if reverse:
-                    Hprev[:-1] = Hs[1:]
-                else:
-                    Hprev[1:] = Hs[:-1]
-            with Fx._OnWgrad(dG2, Hprev, x):     # overlaps the next layer's recurrence
-                _T().gemm(dG2, False, Hprev.view(T * B, Hd), False, w_hh.grad, 1, None, False, None, 1.0, True)
+            # dW_hh = sum_t dG_t^T h_{t-1} over the steps with a predecessor:
+            # row-shifted views of dG and Hs (no zero-padded h_{t-1} copy)
+            Hs2 = Hs.view(T * B, Hd)
+            if reverse:
+                dGh, Hp = dG2[:(T - 1) * B], Hs2[B:]
+            else:
+                dGh, Hp = dG2[B:], Hs2[:(T - 1) * B]
+            with Fx._OnWgrad(dG2, Hs, x):        # overlaps the next layer's recurrence
+                if T > 1:
+                    _T().gemm(dGh, False, Hp, False, w_hh.grad, 1, None, False, None, 1.0, True)
                 _T().gemm(dG2, False, x.reshape(T * B, I), False, w_ih.grad, 1, None, False, None, 1.0, True)
                 _T().colsum(dG2, b.grad)
             dx = None
@@ -153,6 +163,7 @@ class _LSTMLayer(Function):
         else:
             Whh = w_hh.w.float()
             dGf = torch.empty(T, B, 4 * Hd)
+            dc = torch.zeros(B, Hd, dtype=torch.float32, device=dev)
             for k, t in enumerate(rev_order):
                 prev = rev_order[k + 1] if k + 1 < T else None
                 i, f, gg, o, tc = act[t].chunk(5, 1)
