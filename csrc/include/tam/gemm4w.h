@@ -16,6 +16,12 @@
 // then tile t+1's 16 DMA instructions per thread go out and tile t is computed
 // (2 k-steps x 64 MFMAs per wave). K-major image and swizzle as gemm8p
 // (kmaj_off: 16-B chunk c of row r at c ^ ((r>>1)&7), applied on the SOURCE).
+//
+// Measured (tools/ab_gemm4w.py, profiles/r2/gemm4w_ab.json, interleaved in one
+// process): 4096^3 median 1043 TF/s (PIPE 1) vs gemm8p 1204; 8192^3 1154 vs
+// 1323. One wave per SIMD leaves the barrier / first-fragment latency of every
+// K-tile exposed, which costs more than the LDS traffic saved; not routed --
+// kept as the measured alternative and a numerics-tested kernel.
 #pragma once
 #include "tam/igemm.h"
 
