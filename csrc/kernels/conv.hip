@@ -8,6 +8,8 @@
 //          M = K, N_gemm = R*S*C, Kdim = N*P*Q    (both operands MN-major,
 //          split-K over output pixels with fp32 atomics)
 // 1x1 / stride-1 / pad-0 convolutions go straight to the dense GEMM.
+#include <cstdlib>
+
 #include "tam/launch.h"
 #include "tam/tiles.h"
 #include "tam/conv_dma.h"
@@ -77,7 +79,11 @@ void conv_dgrad(const bf16_t* dy, const bf16_t* w, const bf16_t* wt, const ConvG
     // 64-channel dX over >= 1M pixels (VGG-16's 224x224 layer): the 64-wide
     // DMA tile beats the igemm although Kd < 1024 (measured 422 -> 364 us);
     // the cost model's 64-column rule is tuned for ResNet's shallower grids
-    const int force = g_conv_dma >= 2 ? g_conv_dma - 1 : (g.C == 64 && a.M >= (1 << 20) ? 1 : 0);
+    static const long dg64_min_m = [] {
+      const char* e = getenv("TAM_DGRAD64_MIN_M");     // A/B of the 64-channel rule
+      return e ? atol(e) : (1L << 20);
+    }();
+    const int force = g_conv_dma >= 2 ? g_conv_dma - 1 : (g.C == 64 && a.M >= dg64_min_m ? 1 : 0);
     if (launch_conv_dma(a, ep, s, force)) return;
   }
   if (wt && g_conv_dma && g.dil == 1 && g.stride > 1 && g.K % 64 == 0 && g.C % 64 == 0 &&
