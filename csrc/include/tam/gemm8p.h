@@ -279,8 +279,10 @@ gemm8p_kernel(P8Args a, Epi ep) {
     const int col = cbase + 16 * j + (lane & 15);
     bv[j] = (add_bias && col < a.N) ? bf2f(ep.bias[col]) : 0.f;
   }
-  // ---- bf16 output, plain store / accumulate: LDS-staged, 16-B row chunks
-  if (!ep.c_f32 && !ep.mask && (ep.ldc & 7) == 0 && (((uintptr_t)ep.c) & 15) == 0) {
+  // ---- bf16 output, plain store / accumulate (+ relu-backward mask read in
+  // the same 16-B units): LDS-staged, 16-B row chunks
+  const bool mask16 = ep.mask == nullptr || ((ep.ldm & 7) == 0 && (((uintptr_t)ep.mask) & 15) == 0);
+  if (!ep.c_f32 && mask16 && (ep.ldc & 7) == 0 && (((uintptr_t)ep.c) & 15) == 0) {
     constexpr int LDW = WTN + 8, CPR = WTN / 8;
     bf16_t* slab = (bf16_t*)(smem + wid * (32 * LDW * 2));
 #pragma unroll
@@ -305,6 +307,20 @@ gemm8p_kernel(P8Args a, Epi ep) {
         const bf16_t* src = slab + lr * LDW + ch * 8;
         if (col + 8 <= a.N) {
           uint4 v = *(const uint4*)src;
+          if (ep.mask) {
+            // zero where the mask (a ReLU output) is <= 0: bf16 sign clear and
+            // magnitude non-zero <=> > 0
+            const uint4 mk = *(const uint4*)(ep.mask + (long)row * ep.ldm + col);
+            const uint32_t* mw = (const uint32_t*)&mk;
+            uint32_t* vw = (uint32_t*)&v;
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+              const uint32_t m2 = mw[e];
+              const bool lo = (m2 & 0x8000u) == 0 && (m2 & 0x7fffu) != 0;
+              const bool hi = (m2 & 0x80000000u) == 0 && (m2 & 0x7fff0000u) != 0;
+              vw[e] &= (lo ? 0x0000ffffu : 0u) | (hi ? 0xffff0000u : 0u);
+            }
+          }
           if (ep.mode == 1) {
             uint32_t* vw = (uint32_t*)&v;
             const uint4 o = *(const uint4*)dst;
@@ -318,6 +334,7 @@ gemm8p_kernel(P8Args a, Epi ep) {
         } else {
           for (int e = 0; e < 8 && col + e < a.N; ++e) {
             float v = bf2f(src[e]);
+            if (ep.mask && bf2f(ep.mask[(long)row * ep.ldm + col + e]) <= 0.f) v = 0.f;
             if (ep.mode == 1) v += bf2f(dst[e]);
             dst[e] = f2bf(v);
           }
