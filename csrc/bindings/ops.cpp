@@ -715,7 +715,10 @@ bool lstm_seq_fwd_op(const Tensor& gx, const Tensor& w_hh, const Tensor& hs, con
 }
 bool lstm_seq_bwd_op(const Tensor& act, const Tensor& cs, const Tensor& dH, const Tensor& w_hh,
                      const Tensor& dG, bool reverse, const Tensor& sync) {
-  check_f32(act, "act"); check_f32(cs, "cs"); check_f32(dH, "dH"); check_bf16(w_hh, "w_hh");
+  check_f32(act, "act"); check_f32(cs, "cs"); check_bf16(w_hh, "w_hh");
+  TORCH_CHECK(dH.is_cuda() && (dH.scalar_type() == at::kFloat || dH.scalar_type() == at::kBFloat16),
+              "tam.lstm_seq_backward: dH must be an f32 or bf16 CUDA tensor");
+  const int dh_bf16 = dH.scalar_type() == at::kBFloat16 ? 1 : 0;
   check_bf16(dG, "dG");
   TORCH_CHECK(cs.dim() == 3 && cs.is_contiguous(), "tam.lstm_seq_backward: cs [T][B][Hd]");
   const int64_t T = cs.size(0), B = cs.size(1), Hd = cs.size(2);
@@ -726,9 +729,9 @@ bool lstm_seq_bwd_op(const Tensor& act, const Tensor& cs, const Tensor& dH, cons
               dH.numel() == T * B * Hd && dG.is_contiguous() && dG.numel() == T * B * 4 * Hd,
               "tam.lstm_seq_backward: act / dH / dG shapes");
   int* sp = sync.data_ptr<int>();
-  return tam::lstm_seq_backward(act.data_ptr<float>(), cs.data_ptr<float>(), dH.data_ptr<float>(), bp(w_hh),
-                                bpm(dG), (int)T, (int)B, (int)Hd, reverse ? 1 : 0, (unsigned*)sp,
-                                cur_stream(act));
+  return tam::lstm_seq_backward(act.data_ptr<float>(), cs.data_ptr<float>(), (const float*)dH.data_ptr(),
+                                bp(w_hh), bpm(dG), (int)T, (int)B, (int)Hd, reverse ? 1 : 0, (unsigned*)sp,
+                                dh_bf16, cur_stream(act));
 }
 
 void lstm_seq_policy_op(int64_t ch) { tam::lstm_seq_policy((int)ch); }

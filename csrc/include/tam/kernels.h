@@ -103,7 +103,7 @@ void lstm_step_forward(const float* gx, const bf16_t* w_hh, const bf16_t* h_prev
 bool lstm_seq_forward(const float* gx, const bf16_t* w_hh, bf16_t* hs, float* cs, float* act, int T,
                       int B, int Hd, int reverse, unsigned* sync, hipStream_t s);
 bool lstm_seq_backward(const float* act, const float* cs, const float* dH, const bf16_t* w_hh, bf16_t* dG,
-                       int T, int B, int Hd, int reverse, unsigned* sync, hipStream_t s);
+                       int T, int B, int Hd, int reverse, unsigned* sync, int dh_bf16, hipStream_t s);
 // unit halves per persistent workgroup: 0 auto, 1 (16 units) or 2 (32 units)
 void lstm_seq_policy(int ch);
 void lstm_seq_shards(int ns);   // arrival counters per batch tile (1, 2, 4)

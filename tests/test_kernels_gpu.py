@@ -943,3 +943,26 @@ def test_gemm4w_matches_fp32(gpu, M, N, K, pipe):
     assert T().gemm4w(A, B, c, pipe)
     torch.cuda.synchronize()
     assert rel_err(c, A.float() @ B.float().t()) < 1e-2
+
+
+def test_lstm_persistent_backward_bf16_dh(gpu):
+    """The persistent backward reads a bf16 dH directly (as autograd hands
+    it): bit-identical to feeding the same values as fp32."""
+    T_, B, Hd = 8, 64, 1024
+    torch.manual_seed(9)
+    gx = torch.randn(T_, B, 4 * Hd, device=gpu)
+    w = (torch.randn(4 * Hd, Hd, device=gpu) / Hd ** 0.5).to(BF)
+    hs = torch.empty(T_, B, Hd, device=gpu, dtype=BF)
+    cs = torch.empty(T_, B, Hd, device=gpu)
+    act = torch.empty(T_, B, 5 * Hd, device=gpu)
+    sync = torch.zeros(32 * (4 * (B // 16) + 1), dtype=torch.int32, device=gpu)
+    assert T().lstm_seq_forward(gx, w, hs, cs, act, False, sync)
+    dHb = torch.randn(T_, B, Hd, device=gpu).to(BF)
+    outs = []
+    for dH in (dHb, dHb.float()):
+        dG = torch.empty(T_, B, 4 * Hd, device=gpu, dtype=BF)
+        assert T().lstm_seq_backward(act, cs, dH, w, dG, False, sync)
+        torch.cuda.synchronize()
+        assert int(sync[0]) == 0
+        outs.append(dG)
+    assert torch.equal(outs[0], outs[1])

@@ -125,14 +125,17 @@ class _LSTMLayer(Function):
         T, B, I = x.shape
         Hd = Hs.shape[2]
         dev = x.device
-        dHf = dH.float().contiguous()              # dh accumulator (fp32), updated in place
         dG = torch.empty(T, B, 4 * Hd, dtype=BF16, device=dev)
         order = list(range(T - 1, -1, -1) if reverse else range(T))
         rev_order = order[::-1]
         if dev.type == "cuda":
             sy = _sync(dev, B)
-            ran = PERSIST and _ran(_T().lstm_seq_backward(act, Cs, dHf, w_hh.w, dG, reverse, sy), sy)
+            # the persistent kernel reads dH as it comes (bf16); only the
+            # per-step path needs the fp32 accumulator it updates in place
+            ran = PERSIST and _ran(_T().lstm_seq_backward(act, Cs, dH.contiguous(), w_hh.w, dG, reverse, sy),
+                                   sy)
             if not ran:                            # per-step path: cell-state gradient carry
+                dHf = dH.float().contiguous()
                 dc = torch.zeros(B, Hd, dtype=torch.float32, device=dev)
                 dc2 = torch.empty_like(dc)
             for k, t in enumerate([] if ran else rev_order):
@@ -161,6 +164,7 @@ class _LSTMLayer(Function):
                 _T().gemm(dG2, True, w_ih.w, False, dx, 0, None, False, None, 1.0, False)
                 dx = dx.view(T, B, I)
         else:
+            dHf = dH.float().contiguous()          # dh accumulator (fp32), updated in place
             Whh = w_hh.w.float()
             dGf = torch.empty(T, B, 4 * Hd)
             dc = torch.zeros(B, Hd, dtype=torch.float32, device=dev)
