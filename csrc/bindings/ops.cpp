@@ -383,8 +383,14 @@ void conv_weight_t_batch_op(at::TensorList w, at::TensorList wt) {
 }
 
 // dgrad with wt already re-laid (conv_weight_t_batch)
-void conv_dgrad_pre_op(const Tensor& dy, const Tensor& w, const Tensor& wt, const Tensor& dx,
-                       int64_t stride, int64_t pad, int64_t dil, const optional<Tensor>& mask) {
+// stats / bnx / bnmean / bnrstd (all or none): dx is the gradient of a
+// BatchNorm output whose input was bnx; the dgrad epilogue then writes the
+// BN-backward partial rows into stats and the op returns their count (0:
+// this shape's dgrad path computes none)
+int64_t conv_dgrad_pre_op(const Tensor& dy, const Tensor& w, const Tensor& wt, const Tensor& dx,
+                          int64_t stride, int64_t pad, int64_t dil, const optional<Tensor>& mask,
+                          const optional<Tensor>& stats, const optional<Tensor>& bnx,
+                          const optional<Tensor>& bnmean, const optional<Tensor>& bnrstd) {
   check_bf16(dy, "dy"); check_bf16(w, "w"); check_bf16(dx, "dx"); check_bf16(wt, "wt");
   check_contig(dy, "dy"); check_contig(w, "w"); check_contig(dx, "dx"); check_contig(wt, "wt");
   TORCH_CHECK(wt.numel() == w.numel(), "tam.conv_dgrad_pre: wt size");
@@ -396,7 +402,37 @@ void conv_dgrad_pre_op(const Tensor& dy, const Tensor& w, const Tensor& wt, cons
     TORCH_CHECK(mask->numel() == dx.numel(), "tam.conv_dgrad_pre: mask size");
     ep.mask = bp(*mask); ep.ldm = g.C;
   }
-  tam::conv_dgrad(bp(dy), bp(w), bp(wt), g, ep, cur_stream(dy));
+  if (stats.has_value() && stats->defined()) {
+    TORCH_CHECK(bnx.has_value() && bnmean.has_value() && bnrstd.has_value(),
+                "tam.conv_dgrad_pre: stats needs bnx, bnmean, bnrstd");
+    check_f32(*stats, "stats"); check_bf16(*bnx, "bnx"); check_f32(*bnmean, "bnmean"); check_f32(*bnrstd, "bnrstd");
+    check_contig(*bnx, "bnx");
+    const int64_t rows = (dx.numel() / g.C + 127) / 128;
+    TORCH_CHECK(bnx->numel() == dx.numel() && bnmean->numel() == g.C && bnrstd->numel() == g.C &&
+                stats->is_contiguous() && stats->numel() >= rows * 2 * g.C,
+                "tam.conv_dgrad_pre: BN-backward operand shapes");
+    ep.stats = stats->data_ptr<float>();
+    ep.bnx = bp(*bnx);
+    ep.bnmean = bnmean->data_ptr<float>();
+    ep.bnrstd = bnrstd->data_ptr<float>();
+  }
+  return tam::conv_dgrad(bp(dy), bp(w), bp(wt), g, ep, cur_stream(dy));
+}
+
+void bn_backward_part_op(const Tensor& dy, const Tensor& x, const Tensor& mean, const Tensor& rstd,
+                         const Tensor& gamma, const Tensor& dx, const optional<Tensor>& dgamma,
+                         const optional<Tensor>& dbeta, const Tensor& part, int64_t nblk) {
+  check_bf16(dy, "dy"); check_bf16(x, "x"); check_bf16(dx, "dx"); check_f32(part, "part");
+  check_contig(dy, "dy"); check_contig(x, "x"); check_contig(dx, "dx");
+  const int64_t C = x.size(-1);
+  const int64_t M = x.numel() / C;
+  TORCH_CHECK(dy.numel() == x.numel() && dx.numel() == x.numel() && C % 8 == 0 && nblk > 0 &&
+              part.numel() >= nblk * 2 * C, "tam.bn_backward_part: shapes");
+  Tensor ws_f = at::empty({4 * C}, x.options().dtype(at::kFloat));
+  tam::bn_backward_part(bp(dy), bp(x), mean.data_ptr<float>(), rstd.data_ptr<float>(),
+                        gamma.data_ptr<float>(), M, (int)C, bpm(dx), opt_ptr<float>(dgamma),
+                        opt_ptr<float>(dbeta), part.data_ptr<float>(), (int)nblk, ws_f.data_ptr<float>(),
+                        cur_stream(x));
 }
 
 void conv_wgrad_op(const Tensor& dy, const Tensor& x, const Tensor& dw, int64_t stride, int64_t pad,
@@ -755,7 +791,8 @@ TORCH_LIBRARY(tam, m) {
   m.def("conv_fwd(Tensor x, Tensor w, Tensor(a!) y, int stride, int pad, int dil, Tensor? bias, bool relu, Tensor(b!)? stats=None) -> int", &conv_fwd_op);
   m.def("conv_dgrad(Tensor dy, Tensor w, Tensor(a!) wt, Tensor(b!) dx, int stride, int pad, int dil, Tensor? mask) -> ()", &conv_dgrad_op);
   m.def("conv_weight_t_batch(Tensor[] w, Tensor(a!)[] wt) -> ()", &conv_weight_t_batch_op);
-  m.def("conv_dgrad_pre(Tensor dy, Tensor w, Tensor wt, Tensor(a!) dx, int stride, int pad, int dil, Tensor? mask) -> ()", &conv_dgrad_pre_op);
+  m.def("conv_dgrad_pre(Tensor dy, Tensor w, Tensor wt, Tensor(a!) dx, int stride, int pad, int dil, Tensor? mask, Tensor(b!)? stats=None, Tensor? bnx=None, Tensor? bnmean=None, Tensor? bnrstd=None) -> int", &conv_dgrad_pre_op);
+  m.def("bn_backward_part(Tensor dy, Tensor x, Tensor mean, Tensor rstd, Tensor gamma, Tensor(a!) dx, Tensor(b!)? dgamma, Tensor(c!)? dbeta, Tensor part, int nblk) -> ()", &bn_backward_part_op);
   m.def("conv_wgrad(Tensor dy, Tensor x, Tensor(a!) dw, int stride, int pad, int dil, int mode) -> ()", &conv_wgrad_op);
   m.def("bn_forward(Tensor x, Tensor? res, Tensor(a!) y, Tensor gamma, Tensor beta, Tensor(b!)? run_mean, Tensor(c!)? run_var, Tensor(d!) save_mean, Tensor(e!) save_rstd, float eps, float momentum, bool relu, Tensor? part=None, int nblk=0) -> ()", &bn_forward_op);
   m.def("bn_backward(Tensor dy, Tensor? y, Tensor x, Tensor mean, Tensor rstd, Tensor gamma, Tensor(a!) dx, Tensor(b!)? dres, Tensor(c!)? dgamma, Tensor(d!)? dbeta, bool relu, Tensor? addend=None) -> ()", &bn_backward_op);

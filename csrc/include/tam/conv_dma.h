@@ -215,9 +215,16 @@ __global__ void __launch_bounds__(BM / 64 * 64 * WN, 1) conv_dma_kernel(CDArgs a
     // BN statistics of the stored tile (ep.stats): each lane owns channel
     // chunk lane % CPR for every row it stores
     const bool stats = ep.stats != nullptr;
-    float ssum[8], ssq[8];
+    const bool bnb = stats && ep.bnx != nullptr;   // BN-backward sums (see Epi::bnx)
+    float ssum[8], ssq[8], bmu[8], brs[8];
 #pragma unroll
-    for (int e = 0; e < 8; ++e) ssum[e] = ssq[e] = 0.f;
+    for (int e = 0; e < 8; ++e) ssum[e] = ssq[e] = bmu[e] = brs[e] = 0.f;
+    if (bnb) {
+      // a lane keeps one 8-channel chunk for every row it stores
+      const int c0 = n0 + wn * WCOLS + (lane % CPR) * 8;
+#pragma unroll
+      for (int e = 0; e < 8; ++e) { bmu[e] = ep.bnmean[c0 + e]; brs[e] = ep.bnrstd[c0 + e]; }
+    }
     float bv[TN];
 #pragma unroll
     for (int j = 0; j < TN; ++j)
@@ -269,7 +276,18 @@ __global__ void __launch_bounds__(BM / 64 * 64 * WN, 1) conv_dma_kernel(CDArgs a
                                bf2f((bf16_t)(vw[e] >> 16)) + bf2f((bf16_t)(ow[e] >> 16)));
           }
           *(uint4*)dst = v;
-          if (stats) {
+          if (bnb) {
+            const uint4 xv = *(const uint4*)(ep.bnx + orow * ep.ldc + cbase + ch * 8);
+            const uint32_t* vw = (const uint32_t*)&v;
+            const uint32_t* xw = (const uint32_t*)&xv;
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+              const float lo = bf2f((bf16_t)(vw[e] & 0xffff)), hi = bf2f((bf16_t)(vw[e] >> 16));
+              const float xl = bf2f((bf16_t)(xw[e] & 0xffff)), xh = bf2f((bf16_t)(xw[e] >> 16));
+              ssum[2 * e] += lo; ssq[2 * e] += lo * (xl - bmu[2 * e]) * brs[2 * e];
+              ssum[2 * e + 1] += hi; ssq[2 * e + 1] += hi * (xh - bmu[2 * e + 1]) * brs[2 * e + 1];
+            }
+          } else if (stats) {
             const uint32_t* vw = (const uint32_t*)&v;
 #pragma unroll
             for (int e = 0; e < 4; ++e) {

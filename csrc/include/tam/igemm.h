@@ -44,6 +44,13 @@ struct Epi {
   // conv_dma bf16 epilogue only: per-channel BatchNorm partial sums of the
   // stored outputs, one row per M-tile: stats[tm][0..N) = sum, [N..2N) = sum sq
   float* stats = nullptr;         // mode 3: fp32 slab store at c + blockIdx.z * zstride (split-K slabs)
+  // conv_dma bf16 epilogue only, with stats: the stored tile is the gradient
+  // d of a BatchNorm OUTPUT whose input was bnx (same [rows][N] layout):
+  // the partial sums become sum(d) | sum(d * (bnx - mean) * rstd) -- the
+  // BN-backward reduction, read from the dgrad epilogue instead of a pass
+  const bf16_t* bnx = nullptr;
+  const float* bnmean = nullptr;
+  const float* bnrstd = nullptr;
 };
 
 // ---------------------------------------------------------------------------

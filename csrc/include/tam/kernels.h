@@ -39,6 +39,9 @@ void conv_weight_t_batch(WTBatch& b, hipStream_t s);
 void bn_backward(const bf16_t* dy, const bf16_t* addend, const bf16_t* y, const bf16_t* x, const float* mean,
                  const float* rstd, const float* gamma, long M, int C, int relu, bf16_t* dx,
                  bf16_t* dres, float* dgamma, float* dbeta, float* ws_f, hipStream_t s);
+void bn_backward_part(const bf16_t* dy, const bf16_t* x, const float* mean, const float* rstd,
+                      const float* gamma, long M, int C, bf16_t* dx, float* dgamma, float* dbeta,
+                      const float* part, int nblk, float* ws_f, hipStream_t s);
 
 // LayerNorm over last dim D (D % 8 == 0, D <= 2048)
 void ln_forward(const bf16_t* x, const float* g, const float* b, bf16_t* y, float* mean,

@@ -27,7 +27,7 @@ int gemm8p_policy_mode();
 // NHWC convolutions, weights [K][R][S][C] (C, K multiples of 8)
 int conv_fwd(const bf16_t* x, const bf16_t* w, const ConvGeom& g, Epi ep, hipStream_t s);
 // dx[N*H*W][C]; wt = conv_weight_t(w) laid out [C][R][S][K] (ignored for 1x1/s1)
-void conv_dgrad(const bf16_t* dy, const bf16_t* w, const bf16_t* wt, const ConvGeom& g, Epi ep,
+int conv_dgrad(const bf16_t* dy, const bf16_t* w, const bf16_t* wt, const ConvGeom& g, Epi ep,
                 hipStream_t s);
 // dw[K][R*S*C] fp32, ep.mode 0 (overwrite) or 1 (accumulate)
 void conv_wgrad(const bf16_t* dy, const bf16_t* x, const ConvGeom& g, Epi ep, hipStream_t s);

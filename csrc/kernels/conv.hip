@@ -70,8 +70,11 @@ static void dgrad_tile(const bf16_t* dy, const bf16_t* wt, const ConvGeom& g, co
   launch_igemm<BM, BN>(la, lb, M, g.C, Kd, ep, 1, s);
 }
 
-void conv_dgrad(const bf16_t* dy, const bf16_t* w, const bf16_t* wt, const ConvGeom& g, Epi ep,
-                hipStream_t s) {
+// returns the number of partial rows written to ep.stats (BN-backward sums,
+// Epi::bnx) -- only the single-launch stride-1 LDS-DMA path produces them;
+// every other path clears ep.stats and returns 0
+int conv_dgrad(const bf16_t* dy, const bf16_t* w, const bf16_t* wt, const ConvGeom& g, Epi ep,
+               hipStream_t s) {
   const int M = g.N * g.H * g.W, Kd = g.R * g.S * g.K;
   if (wt && g_conv_dma && g.dil == 1 && g.stride == 1) {
     // rows = dX pixels over an H x W grid, gathered from dY (P x Q x K), B = Wt [C][R][S][K]
@@ -84,8 +87,11 @@ void conv_dgrad(const bf16_t* dy, const bf16_t* w, const bf16_t* wt, const ConvG
       return e ? atol(e) : (1L << 20);
     }();
     const int force = g_conv_dma >= 2 ? g_conv_dma - 1 : (g.C == 64 && a.M >= dg64_min_m ? 1 : 0);
-    if (launch_conv_dma(a, ep, s, force)) return;
+    const int bm = launch_conv_dma(a, ep, s, force);
+    if (bm) return ep.stats ? (M + bm - 1) / bm : 0;
   }
+  ep.stats = nullptr;
+  ep.bnx = nullptr;
   if (wt && g_conv_dma && g.dil == 1 && g.stride > 1 && g.K % 64 == 0 && g.C % 64 == 0 &&
       ep.mode == 0 && !ep.c_f32 && g.stride * g.stride <= 4) {
     // strided dgrad = one stride-1 sub-convolution per output parity class
@@ -103,13 +109,13 @@ void conv_dgrad(const bf16_t* dy, const bf16_t* w, const bf16_t* wt, const ConvG
       if (empty) zero_async(ep.c, (size_t)M * g.C * sizeof(bf16_t), s);
       for (int i = 0; i < g.stride * g.stride; ++i)
         if (cls[i].ntaps) launch_conv_dma(cls[i], ep, s, g_conv_dma == 3 ? 2 : 1);
-      return;
+      return 0;
     }
   }
   if (is_pointwise(g)) {
     // dX[m][c] = sum_k dY[m][k] W[k][c]  -> B(k,n) = W[k*C + c], MN-major
     gemm(dy, g.K, true, w, g.C, false, M, g.C, g.K, ep, false, s);
-    return;
+    return 0;
   }
   TileChoice t = choose_tiles(M, g.C, Kd, false);
   switch (t.cfg) {
@@ -118,6 +124,7 @@ void conv_dgrad(const bf16_t* dy, const bf16_t* w, const bf16_t* wt, const ConvG
     case 2: dgrad_tile<64, 128>(dy, wt, g, ep, s); break;
     default: dgrad_tile<64, 64>(dy, wt, g, ep, s); break;
   }
+  return 0;
 }
 
 template <int BM, int BN>

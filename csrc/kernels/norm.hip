@@ -500,6 +500,21 @@ void bn_backward(const bf16_t* dy, const bf16_t* addend, const bf16_t* y, const 
                      mean, rstd, ws_f, ws_f + C, ws_f + 2 * C, dx, dres, total8, C, relu);
 }
 
+// BN backward whose reduction already happened in the consumer conv's dgrad
+// epilogue (Epi::bnx): part = [nblk][2C] partial rows of sum(d) | sum(d*xhat)
+// over the ReLU-masked output gradient d; finalize + one apply pass
+void bn_backward_part(const bf16_t* dy, const bf16_t* x, const float* mean, const float* rstd,
+                      const float* gamma, long M, int C, bf16_t* dx, float* dgamma, float* dbeta,
+                      const float* part, int nblk, float* ws_f, hipStream_t s) {
+  hipLaunchKernelGGL(bn_reduce_finalize_kernel<1>, dim3((C + 15) / 16), dim3(1024), 0, s, part, nblk, M,
+                     C, 0.f, 0.f, gamma, rstd, dgamma, dbeta, ws_f, ws_f + C, ws_f + 2 * C,
+                     (float*)nullptr);
+  const long total8 = M * C / 8;
+  hipLaunchKernelGGL(bn_bwd_apply_kernel, dim3(grid_for(total8)), dim3(256), 0, s, dy,
+                     (const bf16_t*)nullptr, (const bf16_t*)nullptr, x, mean, rstd, ws_f, ws_f + C,
+                     ws_f + 2 * C, dx, (bf16_t*)nullptr, total8, C, 0);
+}
+
 // ---------------------------------------------------------------- LayerNorm
 // One wave per row; D <= 64*8*ROWVEC. Vectorized 8 bf16 per lane-step.
 template <int VEC>

@@ -177,3 +177,24 @@ def test_kernel_debug_mode_names_the_op(gpu, monkeypatch):
     t = Trainer("resnet_tiny", gpu, seed=1, use_graph=True)
     assert not t.use_graph                      # capture + per-op sync do not mix
     assert math.isfinite(float(t.step()))
+
+
+@pytest.mark.timeout(300)
+def test_resnet50_bn_backward_in_dgrad_epilogue(gpu):
+    """ResNet-50: the bn1/bn2 backward reductions produced by the consumer
+    conv's dgrad epilogue (Epi::bnx) give the same gradients as the separate
+    BN-backward reduce pass (summation order aside)."""
+    from tiresias_amd.ops import functional as Fx
+
+    grads = []
+    try:
+        for fused in (True, False):
+            Fx.BN_DGRAD_FUSION = fused
+            t = Trainer("resnet50", gpu, seed=5, batch=32)
+            t._fwd_bwd()
+            torch.cuda.synchronize()
+            grads.append(t.arena.grad.clone())
+    finally:
+        Fx.BN_DGRAD_FUSION = False
+    e = float((grads[0] - grads[1]).norm() / grads[1].norm())
+    assert e < 2e-3, e

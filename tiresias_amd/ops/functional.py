@@ -215,6 +215,15 @@ def _conv_out(h: int, k: int, s: int, p: int, d: int = 1) -> int:
     return (h + 2 * p - d * (k - 1) - 1) // s + 1
 
 
+# BatchNorm-backward reduction of a consumer_masks BN computed in the consumer
+# conv's dgrad epilogue (Epi::bnx). Measured on ResNet-50 bs 64 (rocprofv3,
+# profiles/r2/resnet50/resnet50_kernel_stats_v3_dgradbn.csv): 23 of 53
+# bn_bwd_reduce launches per step go away (-127 us) but the dgrad convs that
+# now read the BN input in their epilogue get +165 us slower; graph step
+# 10.65 -> 10.66 ms. Off by default; the GPU test keeps the path exact.
+BN_DGRAD_FUSION = False
+
+
 class _Conv(Function):
     @staticmethod
     def forward(ctx, x, token, w: Param, b: Optional[Param], stride: int, pad: int, relu: bool,
@@ -241,6 +250,10 @@ class _Conv(Function):
         ctx.w, ctx.b, ctx.stride, ctx.pad, ctx.in_relu = w, b, stride, pad, in_relu
         ctx.save_for_backward(x, y if (relu and mask_own_relu) else None)
         ctx.part = part
+        # x is the output of a BatchNorm whose ReLU backward this conv applies:
+        # its dgrad epilogue can also produce that BN's backward reduction
+        slot = getattr(x, "_tam_slot", None) if (in_relu and BN_DGRAD_FUSION) else None
+        ctx.bn_slot = slot if (slot is not None and slot.src is not None) else None
         return y
 
     @staticmethod
@@ -264,7 +277,15 @@ class _Conv(Function):
             if ctx.needs_input_grad[0]:
                 dx = torch.empty_like(x)
                 wt = getattr(w, "wt", None)
-                if wt is not None:       # re-laid once per step (prepare_conv_wt)
+                sl = ctx.bn_slot
+                if wt is not None and sl is not None:
+                    bx, bmean, brstd = sl.src
+                    C = x.shape[-1]
+                    part = torch.empty((x.numel() // C + 127) // 128, 2 * C, dtype=torch.float32,
+                                       device=x.device)
+                    nblk = _T().conv_dgrad_pre(dy, w.w, wt, dx, st, pd, 1, x, part, bx, bmean, brstd)
+                    sl.bwd_part = (part, nblk, dx) if nblk > 0 else None
+                elif wt is not None:     # re-laid once per step (prepare_conv_wt)
                     _T().conv_dgrad_pre(dy, w.w, wt, dx, st, pd, 1, x if ctx.in_relu else None)
                 else:
                     wt = torch.empty_like(w.w)
@@ -326,10 +347,14 @@ class GradSlot:
     BN's backward adds it while loading dy (bn_backward ``addend``), so the
     residual-branch sum is never materialised (no separate add kernel)."""
 
-    __slots__ = ("stash",)
+    __slots__ = ("stash", "src", "bwd_part")
 
     def __init__(self):
         self.stash = None
+        # consumer_masks BNs: (x, mean, rstd) for the consumer conv's dgrad
+        # epilogue, which returns the BN-backward partial rows in bwd_part
+        self.src = None
+        self.bwd_part = None
 
 
 class _Tap(Function):
@@ -404,6 +429,8 @@ class _BN(Function):
         bwd_relu = relu and not consumer_masks
         ctx.g, ctx.b, ctx.relu, ctx.has_res = g, b, bwd_relu, res is not None
         ctx.slot = slot
+        if slot is not None and consumer_masks and x.is_cuda and training:
+            slot.src = (x, mean, rstd)
         ctx.save_for_backward(x, y if bwd_relu else None, mean, rstd)
         return y
 
@@ -416,7 +443,17 @@ class _BN(Function):
         add = None
         if ctx.slot is not None:
             add, ctx.slot.stash = ctx.slot.stash, None
-        if dy.is_cuda:
+        part = None
+        if ctx.slot is not None:
+            part, ctx.slot.bwd_part = ctx.slot.bwd_part, None
+        if (dy.is_cuda and part is not None and part[2].data_ptr() == dy.data_ptr() and not ctx.relu
+                and not ctx.has_res and add is None):
+            # the consumer conv's dgrad epilogue already reduced sum(d) and
+            # sum(d * xhat) per channel: finalize + apply only
+            dx = torch.empty_like(x)
+            _T().bn_backward_part(dy, x, mean, rstd, g.master, dx, g.grad, b.grad, part[0], part[1])
+            dres = None
+        elif dy.is_cuda:
             dx = torch.empty_like(x)
             dres = torch.empty_like(x) if ctx.has_res and (ctx.relu or add is not None) else None
             _T().bn_backward(dy, y, x, mean, rstd, g.master, dx, dres, g.grad, b.grad, ctx.relu, add)
