@@ -2,6 +2,7 @@
 all-reduce, gang state moves between ranks (the xGMI P2P path on GPUs), and
 a full scheduler-driven replay with gangs and preemption (SURVEY §4 plan 5)."""
 import os
+import time
 import socket
 
 import pytest
@@ -258,12 +259,12 @@ def test_round_ends_at_next_arrival():
     assert r["jobs"][0]["iters"] == 2
 
 
-def _recover_worker(rank, world, port, outdir, fault):
+def _recover_worker(rank, world, port, outdir, fault, hb_timeout=5.0, gang_timeout=12.0):
     import datetime
 
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
-    os.environ["TAM_GANG_TIMEOUT_S"] = "12"
+    os.environ["TAM_GANG_TIMEOUT_S"] = str(int(gang_timeout))
     dist.init_process_group("gloo", rank=rank, world_size=world, timeout=datetime.timedelta(seconds=60))
     torch.set_num_threads(1)
     ctrl = dist.new_group(backend="gloo", timeout=datetime.timedelta(seconds=60))
@@ -271,26 +272,28 @@ def _recover_worker(rank, world, port, outdir, fault):
     from tiresias_amd.executor.cluster_runtime import Worker, run_replay
     from tiresias_amd.parallel import gang
 
-    gang.GANG_TIMEOUT_S = 12.0
+    gang.GANG_TIMEOUT_S = gang_timeout
     jobs = bench.bench_trace(world, 4, seed=3, work_s=0.8, min_iters=4, tiny=True)
     for i in (0, 2, 5):                    # gangs spanning the victim rank
         jobs[i].spec.num_gpu = 2 if i != 5 else world - 1
     cfg = bench.make_cfg("dlas-gpu", "count", world, 3, qlimits=[0.05, 0.3])
     w = Worker(rank, world, torch.device("cpu"), dist.group.WORLD)
     s = run_replay(cfg, jobs, rank, world, torch.device("cpu"), ctrl_pg=ctrl, world_pg=dist.group.WORLD,
-                   worker=w, quantum=0.05, fault=dict(fault), hb_timeout=5.0, hb_period=0.3)
+                   worker=w, quantum=0.05, fault=dict(fault), hb_timeout=hb_timeout, hb_period=0.3)
     torch.save(s, os.path.join(outdir, f"r{rank}.pt"))
     os._exit(0)
 
 
-def _run_recover(tmp_path, fault, world=4):
+def _run_recover(tmp_path, fault, world=4, hb_timeout=5.0, gang_timeout=12.0):
     port = _free_port()
     ctx = mp.get_context("spawn")
-    ps = [ctx.Process(target=_recover_worker, args=(r, world, port, str(tmp_path), fault)) for r in range(world)]
+    ps = [ctx.Process(target=_recover_worker, args=(r, world, port, str(tmp_path), fault, hb_timeout,
+                                                     gang_timeout)) for r in range(world)]
     for p in ps:
         p.start()
+    deadline = time.time() + 240              # one bound for the whole gang, not per process
     for p in ps:
-        p.join(240)
+        p.join(max(1.0, deadline - time.time()))
     for p in ps:
         if p.is_alive():
             p.kill()
@@ -313,10 +316,11 @@ def test_rank_loss_is_recovered_in_process(tmp_path):
 
 @pytest.mark.slow
 def test_delayed_allreduce_is_slow_not_lost(tmp_path):
-    """A straggler (rank 2 stalls 8 s, past the 5 s heartbeat timeout,
+    """A straggler (rank 2 stalls 5 s, past the 3 s heartbeat timeout,
     delaying its gang's all-reduce) is NOT declared lost: its heartbeat
     thread keeps beating; the replay completes with every job."""
-    ps, s = _run_recover(tmp_path, {"rank": 2, "round": 4, "kind": "delay", "seconds": 8.0})
+    ps, s = _run_recover(tmp_path, {"rank": 2, "round": 4, "kind": "delay", "seconds": 5.0},
+                         hb_timeout=3.0, gang_timeout=8.0)
     assert all(p.exitcode == 0 for p in ps)
     assert s["lost_ranks"] == [] and s["finished"] == s["jobs"]
 
