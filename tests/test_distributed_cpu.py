@@ -278,8 +278,15 @@ def _recover_worker(rank, world, port, outdir, fault, hb_timeout=5.0, gang_timeo
         jobs[i].spec.num_gpu = 2 if i != 5 else world - 1
     cfg = bench.make_cfg("dlas-gpu", "count", world, 3, qlimits=[0.05, 0.3])
     w = Worker(rank, world, torch.device("cpu"), dist.group.WORLD)
-    s = run_replay(cfg, jobs, rank, world, torch.device("cpu"), ctrl_pg=ctrl, world_pg=dist.group.WORLD,
-                   worker=w, quantum=0.05, fault=dict(fault), hb_timeout=hb_timeout, hb_period=0.3)
+    try:
+        s = run_replay(cfg, jobs, rank, world, torch.device("cpu"), ctrl_pg=ctrl, world_pg=dist.group.WORLD,
+                       worker=w, quantum=0.05, fault=dict(fault), hb_timeout=hb_timeout, hb_period=0.3)
+    except BaseException:
+        import traceback
+
+        with open(os.path.join(outdir, f"err{rank}.txt"), "w") as f:
+            f.write(traceback.format_exc())
+        os._exit(3)
     torch.save(s, os.path.join(outdir, f"r{rank}.pt"))
     os._exit(0)
 
@@ -306,7 +313,8 @@ def test_rank_loss_is_recovered_in_process(tmp_path):
     within seconds, its GPU leaves the cluster, gangs that spanned it resume
     from their surviving replicas, and every job that still fits finishes."""
     ps, s = _run_recover(tmp_path, {"rank": 3, "round": 6, "kind": "crash"})
-    assert ps[3].exitcode == 17 and all(p.exitcode == 0 for p in ps[:3])
+    errs = {f.name: f.read_text()[-1500:] for f in tmp_path.glob("err*.txt")}
+    assert ps[3].exitcode == 17 and all(p.exitcode == 0 for p in ps[:3]), ([p.exitcode for p in ps], errs)
     assert s["lost_ranks"] == [3]
     assert not s.get("aborted")
     assert s["finished"] + s["failed"] == s["jobs"]
@@ -321,7 +329,8 @@ def test_delayed_allreduce_is_slow_not_lost(tmp_path):
     thread keeps beating; the replay completes with every job."""
     ps, s = _run_recover(tmp_path, {"rank": 2, "round": 4, "kind": "delay", "seconds": 5.0},
                          hb_timeout=3.0, gang_timeout=8.0)
-    assert all(p.exitcode == 0 for p in ps)
+    errs = {f.name: f.read_text()[-1500:] for f in tmp_path.glob("err*.txt")}
+    assert all(p.exitcode == 0 for p in ps), ([p.exitcode for p in ps], errs)
     assert s["lost_ranks"] == [] and s["finished"] == s["jobs"]
 
 
