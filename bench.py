@@ -192,7 +192,7 @@ def make_cfg(policy: str, scheme: str, n_gpus: int, seed: int, ckpt: str = "none
     return SimConfig(schedule=policy, scheme=scheme, num_queue=len(qlimits) + 1, queue_limits=list(qlimits),
                      gittins_delta=gittins_delta, solve_starvation=0.0, seed=seed, ckpt_policy=ckpt,
                      virtual_nodes=virtual_nodes, skew_profile=skew_profile,
-                     pack=share, max_tasks_per_gpu=2 if share else 3,
+                     pack=share, max_tasks_per_gpu=2 if share else 3, gang_align=True,
                      interference_table=SHARING_TABLE if share else "",
                      cluster=ClusterSpec(num_switch=1, num_node_p_switch=1, num_gpu_p_node=n_gpus,
                                          num_cpu_p_node=max(128, 16 * n_gpus),
@@ -263,6 +263,9 @@ def main():
     device = torch.device("cuda", 0 if shared_gpu else local) if use_cuda else torch.device("cpu")
     ctrl_pg = world_pg = None
     if world > 1:
+        from tiresias_amd.parallel.gang import configure_nccl_env
+
+        configure_nccl_env()          # survivors of a lost rank must not be killed by the watchdog
         if shared_gpu:
             torch.cuda.set_device(device)
             dist.init_process_group("gloo", timeout=datetime.timedelta(seconds=300))
@@ -308,6 +311,19 @@ def main():
     worker = Worker(rank, world, device, world_pg, use_graph=use_cuda and not a.no_graph,
                     gang_backend="gloo" if shared_gpu else None,
                     pool_cap=0 if a.no_pool else 2, hbm_budget_gb=a.hbm_budget_gb)
+    comm_setup_s = 0.0
+    if world > 1:
+        # gang_align placement puts every power-of-two gang on an aligned
+        # buddy block: create (and warm) those communicators now, on every
+        # rank in the same order, so no ncclCommInitRank lands in a replay
+        from tiresias_amd.parallel.gang import canonical_gang_sets
+
+        tc = time.perf_counter()
+        vsz = int(vn.lower().split("x")[1]) if vn else 0
+        worker.precreate_groups(canonical_gang_sets(n, vsz), vnode=vsz, nic_gbps=a.nic_gbps)
+        worker.precreate_pairs()      # state-move communicators (one per rank pair)
+        dist.barrier(group=ctrl_pg)
+        comm_setup_s = time.perf_counter() - tc
 
     def sync():
         if world > 1:
@@ -427,6 +443,9 @@ def main():
             "pool_evictions": worker.pool_evictions,
             "restore_prefetches": worker.prefetches,
             "replays": warm_done + steps + (1 if base else 0),
+            "comm_precreate_s": round(comm_setup_s, 3),
+            "comm_stats": sums[-1].get("comm_stats"),
+            "gang_errors": sum(s_.get("gang_errors", 0) for s_ in sums),
             "spilled_gb": round(worker.spilled_bytes / 2 ** 30, 3),
             "max_hbm_reserved_gb": round(torch.cuda.max_memory_reserved(device) / 2 ** 30, 2) if use_cuda else None,
             "process_wall_s": round(time.perf_counter() - T_PROC0, 1),

@@ -299,11 +299,14 @@ def _run_recover(tmp_path, fault, world=4, hb_timeout=5.0, gang_timeout=12.0):
     for p in ps:
         p.start()
     deadline = time.time() + 240              # one bound for the whole gang, not per process
-    for p in ps:
-        p.join(max(1.0, deadline - time.time()))
+    hung = fault.get("rank") if fault.get("kind") == "hang" else None
+    for r, p in enumerate(ps):
+        if r != hung:
+            p.join(max(1.0, deadline - time.time()))
     for p in ps:
         if p.is_alive():
             p.kill()
+            p.join(10)
     return ps, torch.load(tmp_path / "r0.pt", weights_only=False)
 
 
@@ -324,14 +327,46 @@ def test_rank_loss_is_recovered_in_process(tmp_path):
 
 @pytest.mark.slow
 def test_delayed_allreduce_is_slow_not_lost(tmp_path):
-    """A straggler (rank 2 stalls 5 s, past the 3 s heartbeat timeout,
-    delaying its gang's all-reduce) is NOT declared lost: its heartbeat
-    thread keeps beating; the replay completes with every job."""
-    ps, s = _run_recover(tmp_path, {"rank": 2, "round": 4, "kind": "delay", "seconds": 5.0},
-                         hb_timeout=3.0, gang_timeout=8.0)
+    """A straggler (rank 2 stalls 8 s, past the 5 s heartbeat timeout,
+    delaying its gang's all-reduce, inside the 12 s gang timeout) is NOT
+    declared lost: its heartbeat thread keeps beating; the replay completes
+    with every job. (Round 2 shipped this at 5 s after an 8 s stall wedged a
+    run; the wedge was a gang that kept stepping on a communicator whose
+    collective had timed out -- now recovered, see the next test.)"""
+    ps, s = _run_recover(tmp_path, {"rank": 2, "round": 4, "kind": "delay", "seconds": 8.0},
+                         hb_timeout=5.0, gang_timeout=12.0)
     errs = {f.name: f.read_text()[-1500:] for f in tmp_path.glob("err*.txt")}
     assert all(p.exitcode == 0 for p in ps), ([p.exitcode for p in ps], errs)
     assert s["lost_ranks"] == [] and s["finished"] == s["jobs"]
+
+
+@pytest.mark.slow
+def test_gang_timeout_is_recovered(tmp_path):
+    """A straggler stalling LONGER than the gang communicator timeout (6 s vs
+    2 s) fails its gang's collective. The failure is recovered, not wedged:
+    the controller preempts the job, aborts the communicator (and re-creates
+    it under a new generation), and resumes the gang from ONE replica copied
+    to every member; the rank is not lost and every job finishes."""
+    ps, s = _run_recover(tmp_path, {"rank": 2, "round": 2, "kind": "delay", "seconds": 6.0, "where": "step"},
+                         hb_timeout=5.0, gang_timeout=2.0)
+    errs = {f.name: f.read_text()[-1500:] for f in tmp_path.glob("err*.txt")}
+    assert all(p.exitcode == 0 for p in ps), ([p.exitcode for p in ps], errs)
+    assert s["lost_ranks"] == [] and s["finished"] == s["jobs"] and s["failed"] == 0
+    assert s["gang_errors"] >= 1
+    assert s["comm_stats"]["aborted"] >= 1
+
+
+@pytest.mark.slow
+def test_hung_rank_is_declared_lost(tmp_path):
+    """Rank 3 hangs (no heartbeat, never returns) while gang peers may be
+    blocked in a collective with it: rank 0's monitor thread declares it lost
+    on its own, the survivors' communicators containing it are aborted, and
+    the replay finishes on the remaining ranks."""
+    ps, s = _run_recover(tmp_path, {"rank": 3, "round": 6, "kind": "hang"}, hb_timeout=3.0, gang_timeout=8.0)
+    errs = {f.name: f.read_text()[-1500:] for f in tmp_path.glob("err*.txt")}
+    assert all(p.exitcode == 0 for p in ps[:3]), ([p.exitcode for p in ps], errs)
+    assert s["lost_ranks"] == [3] and not s.get("aborted")
+    assert s["finished"] + s["failed"] == s["jobs"] and s["failed"] <= 1
 
 
 def test_hbm_pressure_spills_only_when_needed(tmp_path):

@@ -260,3 +260,104 @@ def test_torchrun_bench_world8_cpu(tmp_path):
     d = json.loads(lines[0])
     assert d["n_gpus"] == 8 and d["steps"] == 2 and d["finished_jobs"] == 48
     assert d["vs_baseline"] is not None
+
+
+# ------------------------------------------------------------------ world 8: gang churn + rank loss
+def _churn_worker(rank, world, port, outdir, crash_round):
+    import datetime
+
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world, timeout=datetime.timedelta(seconds=120))
+    torch.set_num_threads(1)
+    ctrl = dist.new_group(backend="gloo", timeout=datetime.timedelta(seconds=120))
+    import bench
+    from tiresias_amd.executor.cluster_runtime import Worker, run_replay
+    from tiresias_amd.parallel import gang
+
+    gang.GANG_TIMEOUT_S = 20.0
+    jobs = bench.bench_trace(world, 7, seed=21, work_s=0.5, min_iters=3, tiny=True)
+    sizes = [2, 4, 2, 8, 2, 4]
+    for i, j in enumerate(jobs):
+        if i % 4 != 3:
+            j.spec.num_gpu = sizes[i % len(sizes)]
+        j.model = "resnet_tiny" if i % 2 else "transformer_tiny"
+    cfg = bench.make_cfg("dlas-gpu", "tiresias", world, 21, qlimits=[0.02, 0.1])
+    w = Worker(rank, world, torch.device("cpu"), dist.group.WORLD)
+    w.precreate_groups(gang.canonical_gang_sets(world), vnode=0)
+    stats = {"max_pgs": len(gang.PG_CACHE), "gang_starts": 0, "groups": 0, "aborts": 0,
+             "n8": sum(1 for j in jobs if j.spec.num_gpu == 8)}
+    orig = w.apply
+
+    hist = []
+
+    def apply(plan):
+        hist.append((plan.get("round"), [(a["op"], a.get("job"), a.get("ranks"), a.get("source"), a.get("old"))
+                                          for a in plan["actions"]], sorted(w.trainers),
+                     sorted(plan["assign"].get(rank) or [])))
+        for a in plan["actions"]:
+            if a["op"] == "start" and len(a["ranks"]) > 1:
+                stats["gang_starts"] += 1
+            stats["groups"] += a["op"] == "group"
+            stats["aborts"] += a["op"] == "abort"
+        try:
+            orig(plan)
+        except Exception:
+            with open(os.path.join(outdir, f"plan{rank}.txt"), "w") as f:
+                f.write(repr(plan) + "\n" + repr(sorted(w.trainers)) + "\n" + repr(stats) + "\n")
+                for h in hist:
+                    f.write(repr(h) + "\n")
+            raise
+        stats["max_pgs"] = max(stats["max_pgs"], len(gang.PG_CACHE))
+
+    w.apply = apply
+    try:
+        s = run_replay(cfg, jobs, rank, world, torch.device("cpu"), ctrl_pg=ctrl, world_pg=dist.group.WORLD,
+                       worker=w, quantum=0.05, fault={"rank": 5, "round": crash_round}, out_dir=outdir,
+                       hb_timeout=5.0, hb_period=0.5)
+    except BaseException:
+        import traceback
+
+        with open(os.path.join(outdir, f"err{rank}.txt"), "w") as f:
+            f.write(traceback.format_exc())
+        os._exit(3)
+    torch.save({"s": s, "stats": stats}, os.path.join(outdir, f"w{rank}.pt"))
+    os._exit(0)
+
+
+@pytest.mark.slow
+def test_world8_gang_churn_and_rank_loss(tmp_path):
+    """World 8 (gloo, 8 processes): a trace with >= 40 gang starts of sizes
+    2/4/8 under 2D-LAS with preemption, gang_align placement and the 7
+    canonical communicators pre-created. Every rank holds at most 15 live
+    communicators throughout (the round-2 cache grew without bound), and
+    rank 5 crashing mid-replay -- with gangs containing it in flight -- is
+    recovered: its communicators are aborted on the survivors, and every job
+    that still fits on 7 GPUs finishes."""
+    import time
+
+    world = 8
+    port = _free_port()
+    ctx = mp.get_context("spawn")
+    ps = [ctx.Process(target=_churn_worker, args=(r, world, port, str(tmp_path), 15)) for r in range(world)]
+    for p in ps:
+        p.start()
+    deadline = time.time() + 280
+    for p in ps:
+        p.join(max(1.0, deadline - time.time()))
+    for p in ps:
+        if p.is_alive():
+            p.kill()
+    errs = {f.name: f.read_text()[-1500:] for f in tmp_path.glob("err*.txt")}
+    assert ps[5].exitcode == 17, ([p.exitcode for p in ps], errs)
+    assert all(p.exitcode == 0 for r, p in enumerate(ps) if r != 5), ([p.exitcode for p in ps], errs)
+    res = {r: torch.load(tmp_path / f"w{r}.pt", weights_only=False) for r in range(world) if r != 5}
+    s = res[0]["s"]
+    assert s["lost_ranks"] == [5] and not s.get("aborted")
+    assert s["finished"] + s["failed"] == s["jobs"]
+    n8 = res[0]["stats"]["n8"]
+    assert s["failed"] <= n8                               # only gangs larger than 7 GPUs can fail
+    assert res[0]["stats"]["gang_starts"] >= 40, res[0]["stats"]
+    for r, d in res.items():
+        assert d["stats"]["max_pgs"] <= 15, (r, d["stats"])
+    assert res[0]["stats"]["aborts"] >= 1                  # communicators containing rank 5

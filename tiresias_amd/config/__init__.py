@@ -75,6 +75,8 @@ def define_flags() -> None:
     D.DEFINE_string("interference_table", "", "measured per-model-pair slowdowns (JSON from "
                     "tools/measure_interference.py); overrides the constant factor per pair")
     D.DEFINE_integer("max_tasks_per_gpu", 3, "co-location limit per GPU")
+    D.DEFINE_boolean("gang_align", False, "place power-of-two gangs on aligned buddy device blocks "
+                     "(canonical rank sets: bounded, pre-created RCCL communicators; live runtime)")
     D.DEFINE_float("gpu_mem_headroom_mb", 500.0, "free memory a GPU must keep when packing")
     D.DEFINE_integer("lookahead", 5, "horus/horus+ look-ahead window")
     D.DEFINE_float("timeslice", 100.0, "gandiva time-slice quantum (time units)")
@@ -159,6 +161,7 @@ class SimConfig:
     interference: float = 0.2
     interference_table: str = ""
     max_tasks_per_gpu: int = 3
+    gang_align: bool = False          # canonical (buddy-aligned) gang rank sets
     gpu_mem_headroom_mb: float = 500.0
     lookahead: int = 5
     timeslice: float = 100.0

@@ -42,7 +42,7 @@ from ..cluster.topology import Cluster, PlacementError
 from ..config import SimConfig
 from ..core.job import Job, JobSpec, JobState
 from ..metrics.logger import MetricsLogger
-from ..placement.schemes import make_placement
+from ..placement.schemes import align_plan, make_placement
 from ..policy import make_policy
 from ..profiler.skew import SensitivityOracle
 from ..trace.readers import StreamingReader
@@ -184,6 +184,8 @@ class Simulator:
         if j.num_gpu > self.max_gpus:
             return False
         plan = self.placement.plan(self.cluster, j)
+        if self.cfg.gang_align:
+            plan = align_plan(self.cluster, j, plan)
         if plan is None:
             return False
         try:

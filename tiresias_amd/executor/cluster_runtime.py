@@ -43,7 +43,7 @@ from ..config import ClusterSpec, SimConfig
 from ..core.job import Job, JobSpec, JobState
 from ..engine.sim import Simulator
 from ..metrics.logger import MetricsLogger
-from ..parallel.gang import create_gang_comm
+from ..parallel.gang import GangRegistry, abort_comm, comm_failed, create_gang_comm
 from .trainer import Trainer
 
 # nominal per-iteration seconds on one MI355X (tools/bench_models.py,
@@ -104,7 +104,7 @@ class ReplayJob:
 class Controller:
     def __init__(self, cfg: SimConfig, jobs: List[ReplayJob], world: int, quantum: float,
                  logger: Optional[MetricsLogger] = None, spool=None, prior: Optional[List[float]] = None,
-                 clock=None):
+                 clock=None, comms: Optional[GangRegistry] = None):
         self.cfg = cfg
         # seconds clock: host wall clock live, a VirtualClock under the fake backend
         self.clock = clock or time.perf_counter
@@ -128,7 +128,13 @@ class Controller:
         self.vnode_size = self.gpn if getattr(cfg, "virtual_nodes", "") else 0
         self.nic_gbps = float(getattr(cfg, "nic_gbps", 12.5))
         self.holders: Dict[str, Tuple[int, ...]] = {}      # job -> ranks holding its state
-        self.groups_made: set = set()
+        # gang communicator lifecycle (create / LRU-evict / abort); persists
+        # across replays when the caller passes the rank-0 worker's registry
+        self.comms = comms if comms is not None else GangRegistry()
+        self._pending_acts: List[dict] = []     # aborts decided between plans (rank loss, gang errors)
+        self.resync: set = set()                # gangs whose replicas may disagree (failed step)
+        self.last_old: Dict[str, Tuple[int, ...]] = {}   # job -> holders before its last P2P move
+        self.gang_errors = 0
         self.est: Dict[Tuple[str, int], float] = {}
         self.done_iters: Dict[str, int] = {j: 0 for j in self.rjobs}
         self.round = 0
@@ -176,13 +182,20 @@ class Controller:
                     agg["iters"] = min(agg["iters"], jr["iters"])
                     agg["run_s"] = max(agg["run_s"], jr["run_s"])
                     agg["error"] = agg.get("error") or jr.get("error")
+                    agg["move_failed"] = agg.get("move_failed") or jr.get("move_failed")
         for jid, jr in per_job.items():
             if jid not in self.rjobs:
                 continue
             self.done_iters[jid] += jr["iters"]
             rj = self.rjobs[jid]
-            if jr.get("error") and self.log is not None:
-                self.log.decision(self.now(), "step-error", jid, error=str(jr["error"])[:200])
+            if jr.get("move_failed"):
+                self.move_failed(jid)
+                continue
+            if jr.get("error"):
+                if self.log is not None:
+                    self.log.decision(self.now(), "step-error", jid, error=str(jr["error"])[:200])
+                if jid in self.holders and len(self.holders[jid]) > 1:
+                    self.gang_failed(jid)
             # co-located rounds measure the pair, not the job: keep the
             # solo estimate (it sizes rounds and seeds the Gittins prior)
             if jr["iters"] > 0 and jr["run_s"] > 0 and not jr.get("shared") and not jr.get("error"):
@@ -216,6 +229,10 @@ class Controller:
                 s._preempt(j, reason="rank-lost")
         s.cluster.fail_device(str(r // self.gpn + 1), r % self.gpn)
         s.max_gpus = s.cluster.num_gpus
+        # every communicator that contains the dead rank is aborted on the
+        # survivors (the control plane's watcher already did so asynchronously
+        # to unblock them; the plan action purges the entries in lock-step)
+        self._queue_aborts(self.comms.abort_rank(r))
         for j in list(s.active):
             if j.num_gpu > s.max_gpus:           # can never be placed again
                 if j.is_running:
@@ -240,6 +257,58 @@ class Controller:
                 s.jobs[jid].progress = 0.0
         if self.log is not None:
             self.log.decision(self.now(), "rank-lost", str(r), gpus_left=s.cluster.num_gpus)
+
+    def _queue_aborts(self, acts: List[dict]) -> None:
+        """Abort actions go out with the next plan; held jobs whose gang
+        communicator they destroy get a rebind on resume."""
+        for a in acts:
+            self._pending_acts.append(a)
+            for jid, hold in self.holders.items():
+                if tuple(hold) == tuple(a["ranks"]):
+                    self.rebind.add(jid)
+
+    def gang_failed(self, jid: str) -> None:
+        """A gang step failed (collective timeout, an aborted communicator, a
+        peer error): the step's gradients -- and possibly one member's
+        optimizer update -- are unreliable and the communicator is dead.
+        Preempt the job, abort its communicator (and any sharing one), and
+        resume it from ONE replica: on restart every other member receives
+        the lowest holder's state (``resync``), so the replicas agree again.
+        Without this a broken gang kept stepping on the dead communicator and
+        its members desynchronised (the wedge behind round 2's straggler
+        test)."""
+        s = self.sched
+        j = s.jobs.get(jid)
+        hold = self.holders.get(jid)
+        self.gang_errors += 1
+        if j is not None and j.is_running:
+            s._preempt(j, reason="gang-error")
+        if hold is not None and len(hold) > 1:
+            self._queue_aborts(self.comms.abort_gang(hold))
+            self.resync.add(jid)
+        if self.log is not None:
+            self.log.decision(self.now(), "gang-error", jid, ranks=list(hold or ()))
+
+    def move_failed(self, jid: str) -> None:
+        """A state move did not complete on every participant (a peer died
+        mid-transfer): the valid replicas are on the live OLD holders. Preempt
+        the job there; with no live old holder it restarts from scratch."""
+        s = self.sched
+        j = s.jobs.get(jid)
+        if j is not None and j.is_running:
+            s._preempt(j, reason="move-failed")
+        old = tuple(r for r in self.last_old.get(jid, ()) if r not in self.dead)
+        if old:
+            self.holders[jid] = old
+            self.rebind.add(jid)
+        else:
+            self.holders.pop(jid, None)
+            self.restarted.add(jid)
+            self.done_iters[jid] = 0
+            if j is not None:
+                j.progress = 0.0
+        if self.log is not None:
+            self.log.decision(self.now(), "move-failed", jid, holders=list(old))
 
     # ---------------------------------------------------------------- submission
     def _poll_spool(self) -> None:
@@ -330,7 +399,8 @@ class Controller:
         else:
             s.step(s.now)
         finished = [j for j in s.finished if j.extra.get("reported") is None]
-        actions: List[dict] = []
+        actions: List[dict] = self._pending_acts
+        self._pending_acts = []
         for j in finished:
             j.extra["reported"] = True
             if j.job_id in self.holders:
@@ -341,18 +411,27 @@ class Controller:
                 actions.append({"op": "spill", "job": j.job_id, "ranks": self.holders[j.job_id]})
             if a["op"] == "start" and j.is_running:
                 ranks = gang_ranks(j.allocation, self.gpn)
-                if len(ranks) > 1 and ranks not in self.groups_made:
-                    self.groups_made.add(ranks)
+                if len(ranks) > 1:
                     # a gang crossing a virtual-node boundary gets the
                     # hierarchical transport (parallel/gang.py)
-                    actions.append({"op": "group", "ranks": ranks, "vnode": self.vnode_size,
-                                    "nic_gbps": self.nic_gbps})
+                    actions.extend(self.comms.ensure(ranks, self.vnode_size, self.nic_gbps))
                 old = self.holders.get(j.job_id)
                 rj = self.rjobs[j.job_id]
                 act = {"op": "start", "job": j.job_id, "ranks": ranks, "model": rj.model,
                        "batch": rj.batch, "seed": int(j.job_id) if j.job_id.isdigit() else zlib.crc32(j.job_id.encode()) % 100000}
                 if old is None:
                     act["source"] = "fresh"
+                elif j.job_id in self.resync and len(old) > 1:
+                    # after a failed gang step: every new member except ONE
+                    # holder (the lowest) receives that holder's state
+                    self.resync.discard(j.job_id)
+                    self.rebind.discard(j.job_id)
+                    src = old[0]
+                    act["source"] = "p2p"
+                    act["donors"] = {r: src for r in ranks if r != src}
+                    act["old"] = old
+                    act["resync"] = True
+                    act["step"] = self.done_iters[j.job_id]
                 elif old == ranks and j.job_id not in self.rebind:
                     act["source"] = "resident"
                 elif old == ranks:
@@ -361,6 +440,7 @@ class Controller:
                     act["source"] = "p2p"
                     act["donors"] = {}
                     act["old"] = old
+                    act["step"] = self.done_iters[j.job_id]
                     self.rebind.discard(j.job_id)
                 else:
                     self.rebind.discard(j.job_id)
@@ -372,8 +452,15 @@ class Controller:
                     act["source"] = "p2p"
                     act["donors"] = donors
                     act["old"] = old
+                    # receivers start with the donors' optimizer step count
+                    # (Adam's bias correction), progress = completed steps
+                    act["step"] = self.done_iters[j.job_id]
+                if act["source"] == "p2p":
+                    self.last_old[j.job_id] = tuple(old)
                 self.holders[j.job_id] = ranks
                 actions.append(act)
+        # bounded communicator cache: LRU sets nobody holds state on go away
+        actions.extend(self.comms.evict(set(self.holders.values())))
         # assignments: running jobs -> iterations this round; with GPU sharing
         # (pack placement) a rank can carry several jobs, run concurrently
         assign: Dict[int, List[Tuple[str, int]]] = {}
@@ -455,7 +542,15 @@ class Worker:
         self.world_pg = world_pg
         self.trainers: Dict[str, Trainer] = {}
         self.streams: Dict[str, object] = {}     # per-job HIP streams for co-located jobs
+        # gang comms by rank set (built on the process-wide PGCache); their
+        # lifecycle follows the plan's group / ungroup / abort actions, which
+        # rank 0's controller decides with ``comm_registry`` (kept here so it
+        # persists across replays exactly like this cache)
         self.groups: Dict[Tuple[int, ...], object] = {}
+        self.comm_registry = GangRegistry()
+        self._pairs: Dict[Tuple[int, int], object] = {}    # state-move communicators
+        self._move_failed: set = set()
+        self.plane = None                        # control plane (set by run_replay): move agreement
         self.use_graph = use_graph
         self.spilled_bytes = 0
         self.restored_bytes = 0
@@ -499,12 +594,74 @@ class Worker:
         free = self.pool.get(key)
         if free:
             self.pool_hits += 1
-            return free.pop().reset(act["seed"], data_seed, init=init)
+            t = free.pop().reset(act["seed"], data_seed, init=init)
+            self._bind(t, ranks)
+            return t
         t = Trainer(act["model"], self.device, batch=act.get("batch"), group=self._group(ranks),
                     seed=act["seed"], data_seed=data_seed,
                     use_graph=self.use_graph and len(ranks) == 1)
         t.pool_key = key
         return t
+
+    def _bind(self, t: Trainer, ranks) -> None:
+        """A gang trainer must step on the CURRENT communicator of its rank
+        set (it may have been evicted / aborted and re-created since the
+        trainer last ran): rebind when it is a different object."""
+        if len(ranks) > 1 and t.group is not self.groups.get(tuple(ranks)):
+            t.rebind(self._group(ranks))
+
+    def _drop_pool(self, ranks) -> None:
+        for key in [k for k in self.pool if tuple(k[2]) == tuple(ranks)]:
+            for t in self.pool.pop(key):
+                t.release()
+
+    # ------------------------------------------------------------ communicators
+    def _open_group(self, ranks, vnode: int, nic_gbps: float, pin: bool = False):
+        ranks = tuple(ranks)
+        old = self.groups.pop(ranks, None)
+        if old is not None:
+            old.close()
+        c = create_gang_comm(ranks, self.rank, vnode_size=vnode, backend=self.gang_backend,
+                             device=self.device, nic_gbps=nic_gbps, pin=pin)
+        if c is not None:
+            c.vnode = vnode
+            self.groups[ranks] = c
+        return c
+
+    def _close_group(self, ranks, abort: bool = False, dead: Optional[int] = None, purge=None) -> None:
+        from ..parallel.gang import PG_CACHE
+
+        ranks = tuple(ranks)
+        c = self.groups.pop(ranks, None)
+        if c is not None:
+            if abort:
+                abort_comm(c)
+            c.close(purge=abort)
+        if dead is not None:
+            PG_CACHE.purge([k for k in PG_CACHE.live() if dead in k[0]])
+        if purge:
+            sets = {tuple(x) for x in purge}
+            PG_CACHE.purge([k for k in PG_CACHE.live() if tuple(k[0]) in sets])
+        self._drop_pool(ranks)
+
+    def precreate_groups(self, sets, vnode: int = 0, nic_gbps: float = 12.5) -> int:
+        """Create (and warm: the first collective builds the RCCL
+        communicator) the canonical gang communicators, pinned, on every rank
+        in the same order -- call it collectively outside any timed region.
+        Marks them live in the controller-side registry. Returns how many
+        this rank is a member of."""
+        n = 0
+        for r in sets:
+            r = tuple(r)
+            c = self._open_group(r, vnode, nic_gbps, pin=True)
+            if c is not None:
+                n += 1
+                from ..parallel.gang import _pgs_of
+
+                for pg in _pgs_of(c):
+                    pg.warm(self.device if pg.backend == "nccl" else torch.device("cpu"))
+        self.comm_registry.pin(sets, vnode)
+        return n
 
     def _retire(self, t: Optional[Trainer]) -> None:
         """A job left this rank: keep its trainer warm for the next job of the
@@ -615,16 +772,25 @@ class Worker:
                     self._make_room(self._job_need(a["model"], a.get("batch")), protect, ro)
                 elif getattr(t, "_spilled", None):
                     self._make_room(t.hbm_bytes(), protect, ro)
-        p2p_ops = []
+        moves: Dict[str, tuple] = {}          # job -> ([(send|recv, buffer, peer)], action), plan order
         for a in plan["actions"]:
             op = a["op"]
             if op == "group":
                 # communicators outlive a replay: every rank holds the same
                 # cache (same plans, same order), so skipping is collective-safe
-                if tuple(a["ranks"]) not in self.groups:
-                    self.groups[tuple(a["ranks"])] = create_gang_comm(
-                        a["ranks"], self.rank, vnode_size=a.get("vnode", 0), backend=self.gang_backend,
-                        device=self.device, nic_gbps=a.get("nic_gbps", 12.5))
+                c = self.groups.get(tuple(a["ranks"]))
+                if c is None or getattr(c, "vnode", a.get("vnode", 0)) != a.get("vnode", 0):
+                    if self.rank in a["ranks"]:
+                        try:
+                            self._open_group(a["ranks"], a.get("vnode", 0), a.get("nic_gbps", 12.5))
+                        except Exception as e:      # a member never arrived: the gang's step fails
+                            from ..parallel.gang import FailedComm
+
+                            self.groups[tuple(a["ranks"])] = FailedComm(a["ranks"], f"{type(e).__name__}: {e}")
+            elif op == "ungroup":
+                self._close_group(a["ranks"])
+            elif op == "abort":
+                self._close_group(a["ranks"], abort=True, dead=a.get("dead"), purge=a.get("purge"))
             elif op == "drop":
                 self.streams.pop(a["job"], None)
                 self._retire(self.trainers.pop(a["job"], None))
@@ -647,53 +813,197 @@ class Worker:
                     t = self.trainers.get(a["job"])
                     if t is not None and getattr(t, "_spilled", None):
                         self._restore(a["job"])
+                    if t is not None and self.rank in ranks:
+                        self._bind(t, ranks)
                 elif src == "p2p":
                     donors = {int(k): v for k, v in a["donors"].items()}
                     old = tuple(a["old"])
                     if self.rank in old and self.trainers.get(a["job"]) is not None \
                             and getattr(self.trainers[a["job"]], "_spilled", None):
                         self._restore(a["job"])
+                    if self.rank in old or self.rank in ranks:
+                        # every old holder and new member takes part in the
+                        # move's verdict (a leaving holder frees its replica
+                        # only when the move succeeded everywhere)
+                        moves.setdefault(a["job"], ([], a))
                     if self.rank in donors:        # receiver (state arrives by P2P)
-                        t = self._make_trainer(a, init=False)
-                        self.trainers[a["job"]] = t
+                        t = self.trainers.get(a["job"])
+                        if t is None:
+                            t = self._make_trainer(a, init=False)
+                            self.trainers[a["job"]] = t
+                        # a resync receiver already holds a (possibly diverged) replica
+                        elif t is not None and getattr(t, "_spilled", None):
+                            self._restore(a["job"])
+                        ops = moves.setdefault(a["job"], ([], a))[0]
                         for _, buf in sorted(t.state_tensors().items()):
-                            p2p_ops.append(dist.P2POp(dist.irecv, buf, donors[self.rank]))
+                            ops.append(("recv", buf, donors[self.rank]))
                     for recv, donor in donors.items():
                         if donor == self.rank:
                             t = self.trainers[a["job"]]
+                            ops = moves.setdefault(a["job"], ([], a))[0]
                             for _, buf in sorted(t.state_tensors().items()):
-                                p2p_ops.append(dist.P2POp(dist.isend, buf, recv))
+                                ops.append(("send", buf, recv))
                     # replicas that stay: rebind their DDP bucketer to the new gang
                     if self.rank in ranks and self.rank in old:
                         t = self.trainers[a["job"]]
                         t.rebind(self._group(ranks))
                         t.pool_key = (a["model"], a.get("batch"), ranks)
+                    elif self.rank in ranks:
+                        self._bind(self.trainers[a["job"]], ranks)
+                    if self.rank in ranks and "step" in a:
+                        self.trainers[a["job"]].step_count = int(a["step"])
         if any(a["op"] == "drop" for a in plan["actions"]):
             self.reclaim(64.0)
-        if p2p_ops:
-            staged = []
-            if self.device.type == "cuda" and dist.get_backend(self.world_pg) == "gloo":
-                # gloo P2P moves host memory only (the one-GPU multi-rank
-                # rehearsal, bench TAM_SHARED_GPU=1): stage through the host
-                torch.cuda.synchronize(self.device)
-                ops = []
-                for o in p2p_ops:
-                    h = o.tensor.cpu() if o.op is dist.isend else torch.empty(o.tensor.shape, dtype=o.tensor.dtype)
-                    ops.append(dist.P2POp(o.op, h, o.peer))
-                    if o.op is dist.irecv:
-                        staged.append((o.tensor, h))
-                p2p_ops = ops
-            for w in dist.batch_isend_irecv(p2p_ops):
-                w.wait()
-            for dst, h in staged:
-                dst.copy_(h)
+        failed = self._agree_moves(plan.get("round"), self._do_moves(moves),
+                                   {jid: a for jid, (_, a) in moves.items()}) if moves else set()
+        for jid in failed:
+            # every participant drops the pair communicators this move used
+            # (same verdict everywhere -> same re-creation generation)
+            from ..parallel.gang import PG_CACHE
+
+            for pg in getattr(self, "_move_pgs", {}).get(jid, []):
+                pg.abort()
+                self._pairs.pop(pg.ranks, None)
+                PG_CACHE.purge([pg.key])
+            # the move did not complete everywhere: replicas on the OLD ranks
+            # are the valid ones (the controller re-holds the job there);
+            # whatever a receiver got is discarded, and nobody runs the job
+            # this round (every participant reached the same verdict)
+            a = moves[jid][1]
+            self._move_failed.add(jid)
+            if self.rank not in a["old"]:
+                t = self.trainers.pop(jid, None)
+                if t is not None:
+                    t.release()
         # holders that are no longer members free their replica after sending
         for a in plan["actions"]:
-            if a["op"] == "start" and a["source"] == "p2p":
+            if a["op"] == "start" and a["source"] == "p2p" and a["job"] not in failed:
                 if self.rank in a["old"] and self.rank not in a["ranks"]:
                     self._retire(self.trainers.pop(a["job"], None))
         if pressure:
             self._prefetch(plan.get("resume_order") or [])
+
+    # ------------------------------------------------------------ state moves
+    def _pair_pg(self, peer: int):
+        """State moves run on a dedicated 2-rank communicator per rank pair
+        (``PG_CACHE``, pinned): never the world communicator -- an in-flight
+        move with a rank that dies would poison it for every later move --
+        and abortable by the control plane's watcher like any gang
+        communicator. At most world-1 per rank; the bench pre-creates them."""
+        from ..parallel.gang import PG_CACHE
+
+        pair = (min(self.rank, peer), max(self.rank, peer))
+        pg = self._pairs.get(pair)
+        if pg is None or pg.aborted:
+            pg = PG_CACHE.acquire(pair, self.rank, self.gang_backend, pin=True)
+            self._pairs[pair] = pg
+        return pg
+
+    def precreate_pairs(self) -> None:
+        """Create + warm every pair communicator this rank belongs to, in one
+        global order (no rendezvous cycle); call collectively, untimed."""
+        for a in range(self.world):
+            for b in range(a + 1, self.world):
+                if self.rank in (a, b):
+                    pg = self._pair_pg(b if self.rank == a else a)
+                    pg.warm(self.device if pg.backend == "nccl" else torch.device("cpu"))
+
+    def _do_moves(self, moves) -> Dict[str, bool]:
+        """Run each job's state transfer (plan order, so every pair issues its
+        sends / receives in the same sequence); returns job -> local success
+        (the pair communicators used are kept in ``_move_pgs``)."""
+        ok: Dict[str, bool] = {}
+        cuda = self.device.type == "cuda"
+        stage = cuda and self.gang_backend == "gloo"      # gloo moves host memory (one-GPU rehearsal)
+        if stage:
+            torch.cuda.synchronize(self.device)
+        used: Dict[str, list] = {}
+        for jid, (ops, _) in moves.items():
+            pgs, works, staged = [], [], []
+            try:
+                for kind, buf, peer in ops:
+                    pg = self._pair_pg(peer)
+                    pgs.append(pg)
+                    t = buf
+                    if stage:
+                        t = buf.cpu() if kind == "send" else torch.empty(buf.shape, dtype=buf.dtype)
+                        if kind == "recv":
+                            staged.append((buf, t))
+                    other = pg.ranks.index(peer)
+                    works.append(pg.pg.send([t], other, 0) if kind == "send" else pg.pg.recv([t], other, 0))
+                for w in works:
+                    w.wait()
+                for dst, h in staged:
+                    dst.copy_(h)
+                ok[jid] = True
+            except Exception:
+                ok[jid] = False
+            used[jid] = pgs
+        if cuda and moves:
+            try:
+                torch.cuda.synchronize(self.device)
+            except Exception:
+                pass
+        for jid, pgs in used.items():
+            if any(pg.failed() for pg in pgs):
+                ok[jid] = False
+        self._move_pgs = used
+        return ok
+
+    def _agree_moves(self, rnd, ok: Dict[str, bool], acts: Dict[str, dict]) -> set:
+        """All participants of a job's move (old holders + new members) reach
+        the SAME verdict through the control store before anyone runs the
+        job: each publishes its local outcome; the lowest live participant
+        decides (all published flags good -> ok; a flag that is bad, or whose
+        rank died, or that stays missing past the bound -> failed) and writes
+        the verdict with compare-and-set (first writer wins if a successor
+        took over from a decider that died); everyone adopts the stored
+        verdict. A local timeout per participant would let ranks disagree.
+        Returns the failed jobs."""
+        plane = self.plane
+        if plane is None or rnd is None:
+            return {j for j, v in ok.items() if not v}
+        pre = f"{plane.prefix}/mv/{rnd}"
+        for jid, v in ok.items():
+            plane.store.set(f"{pre}/{jid}/{self.rank}", b"1" if v else b"0")
+        bad = set()
+        bound = max(30.0, 4.0 * plane.hb_timeout)
+        for jid, a in acts.items():
+            parts = sorted(set(a["old"]) | set(a["ranks"]))
+            vkey = f"{pre}/{jid}/verdict"
+            t0 = time.time()
+            verdict = None
+            while verdict is None:
+                if plane.store.check([vkey]):
+                    verdict = plane.store.get(vkey)
+                    break
+                live = [r for r in parts if r not in plane.dead]
+                if live and live[0] == self.rank:
+                    good = True
+                    for r in parts:
+                        k = f"{pre}/{jid}/{r}"
+                        while True:
+                            if r in plane.dead:
+                                good = False
+                                break
+                            if plane.store.check([k]):
+                                good = good and plane.store.get(k) == b"1"
+                                break
+                            if time.time() - t0 > bound:
+                                good = False
+                                break
+                            time.sleep(0.001)
+                        if not good:
+                            break
+                    verdict = plane.store.compare_set(vkey, "", b"1" if good else b"0")
+                    break
+                if time.time() - t0 > 4 * bound:      # decider silent far past its own bound
+                    verdict = plane.store.compare_set(vkey, "", b"0")
+                    break
+                time.sleep(0.001)
+            if verdict != b"1":
+                bad.add(jid)
+        return bad
 
     def _prefetch(self, resume_order) -> None:
         """Restore ahead: the spilled job the scheduler will resume FIRST comes
@@ -731,8 +1041,12 @@ class Worker:
         device; every job is charged the round's wall time (co-location
         slowdown is real, measured time)."""
         jobs = plan["assign"].get(self.rank) or []
+        skipped = [{"job": jid, "iters": 0, "run_s": 0.0, "shared": False, "loss": None, "move_failed": True}
+                   for jid in sorted(self._move_failed)]
+        self._move_failed = set()
+        jobs = [(jid, n) for jid, n in jobs if jid not in {r["job"] for r in skipped}]
         if not jobs:
-            return {"rank": self.rank, "job": None, "jobs": [], "dev": self._dev_sample(),
+            return {"rank": self.rank, "job": None, "jobs": skipped, "dev": self._dev_sample(),
                     "ckpt": self._ckpt_report()}
         for jid, _ in jobs:
             self._last_run[jid] = self._round
@@ -778,6 +1092,16 @@ class Worker:
         if cuda:
             torch.cuda.synchronize(self.device)
         dt = time.perf_counter() - t0
+        if len(jobs) == 1 and err is None:
+            t = self.trainers[jobs[0][0]]
+            if t.ddp is not None and comm_failed(t.group):
+                # the NCCL watchdog (CleanUpOnly) or the control plane's
+                # watcher aborted the communicator under this round's steps
+                err = "gang communicator failed (aborted / watchdog timeout)"
+        if err is not None:
+            t = self.trainers[jobs[0][0]]
+            if t.group is not None:
+                abort_comm(t.group)            # never step on it again
         reps = []
         for jid, n in jobs:
             t = self.trainers[jid]
@@ -791,7 +1115,7 @@ class Worker:
             if err:
                 rep["error"] = err
             reps.append(rep)
-        return {"rank": self.rank, "job": jobs[0][0], "jobs": reps, "dev": self._dev_sample(),
+        return {"rank": self.rank, "job": jobs[0][0], "jobs": reps + skipped, "dev": self._dev_sample(),
                 "ckpt": self._ckpt_report()}
 
     def _ckpt_report(self) -> Optional[dict]:
@@ -925,7 +1249,14 @@ def run_replay(cfg: SimConfig, jobs: List[ReplayJob], rank: int, world: int, dev
       ``{"rank": r, "round": k}`` / ``"kind": "crash"`` -- rank r dies at round k;
       ``{"rank": r, "round": k, "kind": "delay", "seconds": s}`` -- rank r
       stalls s seconds before its round-k work (a straggler delaying its
-      gang's all-reduce): detected as slow, NOT as lost.
+      gang's all-reduce): detected as slow, NOT as lost; a stall longer than
+      the gang communicator timeout fails the gang step (``"where":
+      "step"`` stalls after apply, in the first round the rank runs a gang,
+      so its peers wait inside the collective), which the controller
+      recovers (``Controller.gang_failed``: abort + resync);
+      ``"kind": "hang"`` -- rank r stops heartbeating and blocks forever
+      (a hung GPU / process): declared lost by rank 0's monitor thread while
+      its gang peers may still be blocked in a collective with it.
 
     Recovery (store plane): the lost GPU leaves the cluster; every job with
     state on it is preempted. A DDP gang keeps its replicas on the surviving
@@ -937,16 +1268,24 @@ def run_replay(cfg: SimConfig, jobs: List[ReplayJob], rank: int, world: int, dev
     distributed = world > 1
     ctrl = None
     log = None
+    w = worker or Worker(rank, world, device, world_pg, use_graph=use_graph)
     if rank == 0:
         log = MetricsLogger(out_dir, node_logs=False)
-        ctrl = Controller(cfg, jobs, world, quantum, logger=log, spool=spool, prior=prior)
-    w = worker or Worker(rank, world, device, world_pg, use_graph=use_graph)
+        ctrl = Controller(cfg, jobs, world, quantum, logger=log, spool=spool, prior=prior,
+                          comms=w.comm_registry)
     plane = None
     if distributed:
         if control == "store":
+            from ..parallel.gang import PG_CACHE
             from .control import StorePlane
 
-            plane = StorePlane(rank, world, hb_period=hb_period, hb_timeout=hb_timeout)
+            def _on_dead(r: int) -> None:
+                # watcher / monitor thread: unblock this rank's training
+                # thread if it is inside a collective with the dead rank
+                PG_CACHE.abort_where(lambda k: r in k[0])
+
+            plane = StorePlane(rank, world, hb_period=hb_period, hb_timeout=hb_timeout, on_dead=_on_dead)
+            w.plane = plane
         else:
             from .control import GlooPlane
 
@@ -969,18 +1308,36 @@ def run_replay(cfg: SimConfig, jobs: List[ReplayJob], rank: int, world: int, dev
             if distributed:
                 plan = plane.bcast(plan, rounds)
             tc = time.perf_counter()
+            plan["round"] = rounds
             if plan["stop"]:
                 w.apply(plan)                          # the last finished jobs' drops
+                if plane is not None and hasattr(plane, "finish"):
+                    plane.finish(plan.get("alive", range(world)))
+                break
+            if rank not in plan.get("alive", (rank,)):
+                # declared lost (hung past the control plane's bound): this
+                # rank's GPU has left the cluster -- stop participating
                 break
             if fault and fault.get("rank") == rank and rounds >= fault.get("round", 0):
                 if fault.get("kind", "crash") == "crash":
                     os._exit(17)                     # simulated node/rank crash
-                if not fault.get("_done"):
+                if fault.get("kind") == "hang":
+                    if plane is not None:
+                        plane.close()                # heartbeat stops
+                    while True:
+                        time.sleep(3600)
+                if not fault.get("_done") and fault.get("where", "apply") == "apply":
                     fault["_done"] = True
                     time.sleep(float(fault.get("seconds", 1.0)))   # straggler
             if any(len(v) > 1 for v in plan["assign"].values()):
                 shared += 1
             w.apply(plan)
+            if fault and fault.get("rank") == rank and rounds >= fault.get("round", 0) \
+                    and fault.get("where") == "step" and not fault.get("_done") \
+                    and any(len(w.trainers[j].group.ranks) > 1 if getattr(w.trainers.get(j), "ddp", None) else False
+                            for j, _ in plan["assign"].get(rank) or []):
+                fault["_done"] = True                  # straggler inside a gang step: peers wait in the collective
+                time.sleep(float(fault.get("seconds", 1.0)))
             td = time.perf_counter()
             rep = w.run(plan)
             te = time.perf_counter()
@@ -1014,13 +1371,15 @@ def run_replay(cfg: SimConfig, jobs: List[ReplayJob], rank: int, world: int, dev
     finally:
         if plane is not None:
             plane.close()
+        w.plane = None
     wall = time.perf_counter() - t_start
     w.clear()
     if device.type == "cuda":
         torch.cuda.synchronize(device)
     if ctrl:
         s = ctrl.sched.summary()
-        s.update(rounds=rounds, shared_rounds=shared, replay_wall_s=wall,
+        s.update(rounds=rounds, shared_rounds=shared, replay_wall_s=wall, gang_errors=ctrl.gang_errors,
+                 comm_stats=dict(ctrl.comms.stats, live=len(ctrl.comms.live)),
                  iter_est={f"{k[0]}x{k[1]}": v for k, v in ctrl.est.items()},
                  runtime_breakdown={k: round(v, 4) for k, v in prof.items()},
                  lost_ranks=lost_ranks, recovered_jobs=sorted(ctrl.recovered),

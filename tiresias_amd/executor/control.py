@@ -11,10 +11,19 @@ so a lost rank cannot wedge the surviving ones:
   stamping ``hb/<rank>`` every ``hb_period`` seconds — independent of the
   training thread, so a rank busy in a long step, or stuck in a collective
   with a dead peer, still reads as alive;
-* while gathering, rank 0 polls the report keys; a rank whose report is
-  missing AND whose heartbeat is older than ``hb_timeout`` (5-10 s; never
-  the 10-minute collective timeout) is declared LOST and returned to the
-  controller, which re-plans around it (``Controller.rank_lost``).
+* rank 0 runs a MONITOR thread that checks every heartbeat each period: a
+  rank whose heartbeat is older than ``hb_timeout`` (5-10 s; never the
+  collective timeout) is declared LOST, published under ``<epoch>/dead``,
+  and ``on_dead(r)`` runs at once -- on a separate thread, because rank 0's
+  training thread may itself be stuck in a collective with the dead rank;
+* every other rank's heartbeat thread also WATCHES ``<epoch>/dead`` and
+  runs ``on_dead(r)`` for each newly dead rank: the runtime aborts every
+  communicator containing it, so RCCL kernels spinning on the dead peer
+  exit and the survivors report instead of hanging until the watchdog;
+* while gathering, rank 0 polls the report keys; dead ranks are returned to
+  the controller, which re-plans around them (``Controller.rank_lost``). A
+  rank that is alive but silent is reported (stderr) every ``slow_report_s``
+  and declared lost after ``hung_s`` -- ``gather`` never waits unboundedly.
 
 ``GlooPlane`` is the collective-based plane (``broadcast_object_list`` /
 ``gather_object`` on a gloo group) kept for comparison; a lost rank there
@@ -66,30 +75,85 @@ def _store_client(timeout_s: float):
 
 class StorePlane:
     def __init__(self, rank: int, world: int, hb_period: float = 1.0, hb_timeout: float = 6.0,
-                 plan_timeout: float = 600.0, store=None):
+                 plan_timeout: float = 600.0, store=None, on_dead=None, slow_report_s: float = 30.0,
+                 hung_s: float = 900.0):
         self.rank, self.world = rank, world
         self.hb_period, self.hb_timeout = hb_period, hb_timeout
         self.plan_timeout = plan_timeout
+        self.slow_report_s, self.hung_s = slow_report_s, hung_s
         _EPOCH["n"] += 1                         # every rank replays in the same order
         self.prefix = f"tam/{_EPOCH['n']}"
         self.store = store or _store_client(plan_timeout)
+        self.on_dead = on_dead
         self._stop = threading.Event()
         self._hb: Optional[threading.Thread] = None
+        self._lock = threading.Lock()
         self.dead: set = set()
+        self._reported: set = set()              # dead ranks already returned by gather
         self.last_seen: Dict[int, float] = {}
+        self.t_start = time.time()
         if rank != 0:
             self._hb = threading.Thread(target=self._beat, name=f"hb-{rank}", daemon=True)
-            self._hb.start()
+        else:
+            self._hb = threading.Thread(target=self._monitor, name="hb-monitor", daemon=True)
+        self._hb.start()
 
     # ----------------------------------------------------------- heartbeat
+    def _declare(self, dead_now) -> None:
+        """Record newly dead ranks and run the abort callback (any thread)."""
+        new = []
+        with self._lock:
+            for r in dead_now:
+                if r not in self.dead and r != self.rank:
+                    self.dead.add(r)
+                    new.append(r)
+        for r in new:
+            if self.on_dead is not None:
+                try:
+                    self.on_dead(r)
+                except Exception:
+                    pass
+
     def _beat(self):
         st = _store_client(30.0)
+        dkey = f"{self.prefix}/dead"
+        seen = b""
         while not self._stop.is_set():
             try:
                 st.set(f"tam/hb/{self.rank}", repr(time.time()))
+                if st.check([dkey]):
+                    raw = st.get(dkey)
+                    if raw != seen:
+                        seen = raw
+                        self._declare(pickle.loads(raw))
             except Exception:                    # store gone: controller lost, main thread notices
                 return
             self._stop.wait(self.hb_period)
+
+    def _monitor(self):
+        """Rank 0: declare ranks whose heartbeat stopped, independent of the
+        training thread (which may be blocked in a collective with them)."""
+        st = _store_client(30.0)
+        dkey = f"{self.prefix}/dead"
+        while not self._stop.wait(self.hb_period):
+            if time.time() - self.t_start < self.hb_timeout:
+                continue                         # grace: every heartbeat thread has started
+            try:
+                gone = [r for r in range(1, self.world)
+                        if r not in self.dead and self._age(st, r) > self.hb_timeout]
+                if gone:
+                    self._declare(gone)
+                    with self._lock:
+                        st.set(dkey, pickle.dumps(sorted(self.dead)))
+            except Exception:
+                return
+
+    @staticmethod
+    def _age(st, r: int) -> float:
+        k = f"tam/hb/{r}"
+        if not st.check([k]):
+            return float("inf")
+        return time.time() - float(st.get(k).decode())
 
     def heartbeat_age(self, r: int) -> float:
         k = f"tam/hb/{r}"
@@ -133,13 +197,15 @@ class StorePlane:
             return None, []
         reps: List = [None] * self.world
         reps[0] = rep
-        pending = [r for r in alive if r != 0 and r not in self.dead]
-        newly: List[int] = []
+        pending = [r for r in alive if r != 0]
         t0 = time.time()
+        t_warn = t0
         sleep = 0.0002
         while pending:
             left = []
             for r in pending:
+                if r in self.dead:
+                    continue
                 k = f"{self.prefix}/rep/{rnd}/{r}"
                 if self.store.check([k]):
                     reps[r] = pickle.loads(self.store.get(k))
@@ -149,20 +215,56 @@ class StorePlane:
             pending = left
             if not pending:
                 break
-            if time.time() - t0 > self.hb_timeout:
-                for r in list(pending):
-                    if self.heartbeat_age(r) > self.hb_timeout:
-                        pending.remove(r)
-                        self.dead.add(r)
-                        newly.append(r)
+            now = time.time()
+            if now - t0 > self.hb_timeout:
+                # the monitor thread normally declares first; this covers a
+                # monitor that is itself starved
+                gone = [r for r in pending if self.heartbeat_age(r) > self.hb_timeout]
+                if gone:
+                    self._declare(gone)
+                    self.store.set(f"{self.prefix}/dead", pickle.dumps(sorted(self.dead)))
+            if now - t_warn > self.slow_report_s:
+                t_warn = now
+                import sys
+
+                print(f"[control] round {rnd}: waiting {now - t0:.0f} s for ranks {pending} "
+                      f"(heartbeats alive)", file=sys.stderr, flush=True)
+            if now - t0 > self.hung_s:
+                # alive but silent for longer than any collective may take:
+                # treat as lost rather than wait forever
+                self._declare(pending)
+                self.store.set(f"{self.prefix}/dead", pickle.dumps(sorted(self.dead)))
             time.sleep(sleep)
             sleep = min(0.002, sleep * 1.5)
+        with self._lock:
+            newly = sorted(r for r in self.dead if r not in self._reported)
+            self._reported |= set(newly)
         if rnd > 0:
             try:
                 self.store.delete_key(f"{self.prefix}/plan/{rnd - 1}")
             except Exception:
                 pass
         return reps, newly
+
+    def finish(self, alive: Sequence[int], bound_s: float = 60.0) -> None:
+        """End of replay: workers acknowledge the stop plan; rank 0 returns
+        only once every live worker has (its process may host the store, so
+        exiting early would strand a worker still reading the last plan)."""
+        if self.rank != 0:
+            try:
+                self.store.set(f"{self.prefix}/done/{self.rank}", b"1")
+            except Exception:
+                pass
+            return
+        t0 = time.time()
+        for r in alive:
+            if r == 0:
+                continue
+            k = f"{self.prefix}/done/{r}"
+            while time.time() - t0 < bound_s and r not in self.dead:
+                if self.store.check([k]):
+                    break
+                time.sleep(0.002)
 
     def close(self):
         self._stop.set()

@@ -113,7 +113,18 @@ class FakeCluster:
                 ranks = tuple(a["ranks"])
                 if len(ranks) < 2 or any(not 0 <= r < self.world for r in ranks):
                     raise ProtocolError(f"bad gang communicator {ranks}")
+                if ranks in self.groups:
+                    raise ProtocolError(f"communicator {ranks} created twice without ungroup/abort")
                 self.groups.add(ranks)
+                self.stats["comms_created"] = self.stats.get("comms_created", 0) + 1
+                self.stats["peak_comms"] = max(self.stats.get("peak_comms", 0), len(self.groups))
+            elif op in ("ungroup", "abort"):
+                ranks = tuple(a["ranks"])
+                if ranks not in self.groups:
+                    raise ProtocolError(f"{op} of communicator {ranks} that does not exist")
+                if op == "ungroup" and any(h == ranks for h in self.held.values()):
+                    raise ProtocolError(f"ungroup of {ranks} while a job holds state on it")
+                self.groups.discard(ranks)
             elif op == "drop":
                 if job not in self.held:
                     raise ProtocolError(f"drop of job {job} that no rank holds")
@@ -152,10 +163,14 @@ class FakeCluster:
                     if self.held.get(job) != old:
                         raise ProtocolError(f"p2p move of {job} from {old}, held on {self.held.get(job)}")
                     donors = {int(k): int(v) for k, v in a["donors"].items()}
+                    resync = bool(a.get("resync"))
                     for recv, donor in donors.items():
-                        if donor not in old or recv in old or recv not in ranks:
+                        if donor not in old or recv not in ranks or (recv in old and not resync):
                             raise ProtocolError(f"bad donor {donor}->{recv} for {job}")
-                    if set(ranks) - set(old) != set(donors):
+                    if resync:
+                        if len(set(donors.values())) != 1 or set(ranks) - set(donors) - set(donors.values()):
+                            raise ProtocolError(f"resync of {job} must copy ONE replica to every other member")
+                    elif set(ranks) - set(old) != set(donors):
                         raise ProtocolError(f"new ranks of {job} without a donor")
                     if job in self.spilled:                  # holders restore first
                         charge(old, b / self.host)
@@ -238,6 +253,13 @@ def run_fake(cfg: SimConfig, jobs: List[ReplayJob], world: int, quantum: float =
               if cfg.interference_table else InterferenceModel(cfg.interference))
     fc = fake or FakeCluster(world, iter_s=iter_s, interference=interf, vnode_size=ctrl.vnode_size,
                              nic_gbps=ctrl.nic_gbps)
+    if getattr(cfg, "gang_align", False):
+        # the live bench pre-creates the canonical (buddy) communicators
+        from ..parallel.gang import canonical_gang_sets
+
+        sets = canonical_gang_sets(world, ctrl.vnode_size)
+        ctrl.comms.pin(sets, ctrl.vnode_size)
+        fc.groups.update(tuple(x) for x in sets)
     ctrl.start_clock()
     t_wall = time.perf_counter()
     rounds = 0
@@ -258,6 +280,6 @@ def run_fake(cfg: SimConfig, jobs: List[ReplayJob], world: int, quantum: float =
         raise ProtocolError(f"replay ended with state still held for {sorted(fc.held)}")
     s = ctrl.sched.summary()
     s.update(rounds=rounds, backend="fake", replay_wall_s=time.perf_counter() - t_wall, fake_stats=dict(fc.stats),
-             virtual_s=clock())
+             virtual_s=clock(), comm_stats=dict(ctrl.comms.stats, live=len(ctrl.comms.live)))
     log.close()
     return s

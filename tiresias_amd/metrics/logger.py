@@ -62,7 +62,8 @@ class MetricsLogger:
                 self._open("memory", ["delta", "node", "mem_used", "mem_size"])
                 self._open("network", ["delta", "job_id", "num_nodes", "rate"])
             if decisions:
-                self._dec = open(os.path.join(out_dir, "decisions.jsonl"), "w")
+                # line-buffered: a post-mortem of a wedged / killed run keeps every decision
+                self._dec = open(os.path.join(out_dir, "decisions.jsonl"), "w", buffering=1)
         self.busy_gpu_time = 0.0
         self.last_t = None
         self.last_busy = 0

@@ -31,11 +31,12 @@ elsewhere does not block anything.
 """
 from __future__ import annotations
 
+import os
 import queue
 import threading
 import time
 from concurrent.futures import Future
-from typing import Dict, List, Optional, Sequence
+from typing import Dict, List, Optional, Sequence, Tuple
 
 import torch
 import torch.distributed as dist
@@ -75,8 +76,11 @@ class FlatComm:
         for w in handles:
             w.wait()
 
-    def close(self) -> None:
-        pass
+    def close(self, purge: bool = False) -> None:
+        cache = getattr(self, "_cache", None)
+        if cache is not None and isinstance(self.pg, GangPG):
+            cache.release(self.pg, purge=purge)
+            self._cache = None
 
 
 class _NicLimiter:
@@ -113,6 +117,7 @@ class HierComm:
         self.leader = mine[0]
         self.is_leader = my_rank == self.leader
         self.local_pg = local_pgs.get(mine[0])          # None when the part is a single rank
+        self._local_all = dict(local_pgs)
         self.leaders_pg = leaders_pg
         self.k = len(parts)
         self.nic = _NicLimiter(nic_gbps, nic_latency_s)
@@ -141,18 +146,23 @@ class HierComm:
             item = self._q.get()
             if item is None:
                 return
-            view, work, fut = item
+            view, work, ready, fut = item
             try:
-                fut.set_result(self._exchange(view, work))
+                fut.set_result(self._exchange(view, work, ready))
             except BaseException as e:          # surfaced in finish()
                 fut.set_exception(e)
 
-    def _exchange(self, view: torch.Tensor, work):
+    def _exchange(self, view: torch.Tensor, work, ready):
         nbytes = view.numel() * view.element_size()
         if self._cuda:
             with torch.cuda.stream(self._side):
+                # the D2H must see the finished bucket: order the side stream
+                # after the compute stream that produced it (recorded at
+                # start(), on the issuing thread) AND after the intra-node
+                # reduce when there is one
+                self._side.wait_event(ready)
                 if work is not None:
-                    work.wait()                  # side stream after the intra-node reduce
+                    work.wait()
                 host = self._pinned(view.numel())
                 host.copy_(view, non_blocking=True)
                 self._side.synchronize()         # D2H landed (this thread only)
@@ -178,8 +188,12 @@ class HierComm:
             w = self.local_pg.reduce(view, self.leader)
         fut = None
         if self.is_leader:
+            ready = None
+            if self._cuda:
+                ready = torch.cuda.Event()
+                ready.record(torch.cuda.current_stream(self.device))
             fut = Future()
-            self._q.put((view, w, fut))
+            self._q.put((view, w, ready, fut))
         return (view, w, fut)
 
     def finish(self, handles) -> None:
@@ -196,42 +210,77 @@ class HierComm:
         for b in bcasts:
             b.wait()
 
-    def close(self) -> None:
+    def close(self, purge: bool = False) -> None:
         if self._q is not None:
             self._q.put(None)
             self._q = None
+        cache = getattr(self, "_cache", None)
+        if cache is not None:
+            for pg in _pgs_of(self):
+                cache.release(pg, purge=purge)
+            self._cache = None
 
 
-_PGS: Dict[tuple, object] = {}
-GANG_TIMEOUT_S = float(__import__("os").environ.get("TAM_GANG_TIMEOUT_S", "120"))
+GANG_TIMEOUT_S = float(os.environ.get("TAM_GANG_TIMEOUT_S", "120"))
+# rendezvous of a NEW communicator (gloo connects every pair at construction;
+# RCCL exchanges its unique id through the store): a straggling member only
+# delays it, so it gets a generous bound of its own, not the collective one
+CREATE_TIMEOUT_S = float(os.environ.get("TAM_COMM_CREATE_TIMEOUT_S", "180"))
+
+
+def configure_nccl_env() -> None:
+    """Call BEFORE ``init_process_group`` / the first ``ProcessGroupNCCL``.
+
+    A gang that loses a member must not take its survivors down: their
+    replicas are what the controller resumes the job from
+    (``Controller.rank_lost``). PyTorch's default (``SkipCleanUp``) kills the
+    whole process when a collective times out, so the watchdog is set to
+    ``CleanUpOnly`` -- it aborts the timed-out communicator (the stuck RCCL
+    kernel exits) and records the error, which ``GangPG.failed`` reads after
+    the step; the process lives. The watchdog's own heartbeat monitor (which
+    also kills the process) and the flight-recorder dumps are off: liveness
+    is the control plane's job (``executor/control.py`` heartbeats)."""
+    os.environ.setdefault("TORCH_NCCL_ASYNC_ERROR_HANDLING", "2")
+    os.environ.setdefault("TORCH_NCCL_ENABLE_MONITORING", "0")
+    os.environ.setdefault("TORCH_NCCL_DUMP_ON_TIMEOUT", "0")
 
 
 class GangPG:
     """A communicator over an arbitrary rank set, built directly on a c10d
     backend (``ProcessGroupNCCL`` = RCCL on ROCm, or ``ProcessGroupGloo``)
-    from the job's key-value store under a per-rank-set prefix: only the
-    members rendezvous (ncclCommInitRank with a unique id exchanged through
-    the store), no world-wide bookkeeping. ``torch.distributed.new_group``
-    would need every rank of the world to take part (or, with local
-    synchronisation, identical group histories on the members) — neither
-    holds once gangs form and dissolve dynamically, or after a rank is lost.
-    Collective calls return Work handles (``wait()`` orders the current
-    stream after them)."""
+    from the job's key-value store under a per-(rank set, generation) prefix:
+    only the members rendezvous (ncclCommInitRank with a unique id exchanged
+    through the store), no world-wide bookkeeping. ``torch.distributed.
+    new_group`` would need every rank of the world to take part (or, with
+    local synchronisation, identical group histories on the members) --
+    neither holds once gangs form and dissolve dynamically, or after a rank
+    is lost. The generation makes a re-created communicator (after an abort
+    or an eviction) rendezvous under fresh keys. Collective calls return
+    Work handles (``wait()`` orders the current stream after them)."""
 
-    def __init__(self, ranks: Sequence[int], my_rank: int, backend: str, timeout_s: float = GANG_TIMEOUT_S):
+    def __init__(self, ranks: Sequence[int], my_rank: int, backend: str, timeout_s: Optional[float] = None,
+                 gen: int = 0):
         from datetime import timedelta
 
         self.ranks = tuple(ranks)
         self.rank = self.ranks.index(my_rank)
         self.size = len(self.ranks)
         self.backend = backend
+        self.gen = gen
+        self.aborted = False
         base = dist.distributed_c10d._get_default_store()
-        store = dist.PrefixStore(f"tam/pg/{backend}/{'_'.join(map(str, self.ranks))}", base)
-        to = timedelta(seconds=timeout_s)
+        store = dist.PrefixStore(f"tam/pg/{backend}/{gen}/{'_'.join(map(str, self.ranks))}", base)
+        to = timedelta(seconds=GANG_TIMEOUT_S if timeout_s is None else timeout_s)
+        create = timedelta(seconds=max(CREATE_TIMEOUT_S, to.total_seconds()))
         if backend == "nccl":
             self.pg = dist.ProcessGroupNCCL(store, self.rank, self.size, to)
         else:
-            self.pg = dist.ProcessGroupGloo(store, self.rank, self.size, to)
+            self.pg = dist.ProcessGroupGloo(store, self.rank, self.size, create)
+            self.pg.set_timeout(to)
+
+    @property
+    def key(self) -> tuple:
+        return (self.ranks, self.backend)
 
     def all_reduce(self, t: torch.Tensor):
         o = dist.AllreduceOptions()
@@ -251,38 +300,343 @@ class GangPG:
         o.rootTensor = 0
         return self.pg.broadcast([t], o)
 
+    def warm(self, device: torch.device) -> None:
+        """Force the backend's communicator into existence now (RCCL creates
+        it lazily at the first collective): a one-element all-reduce."""
+        t = torch.zeros(1, device=device)
+        self.all_reduce(t).wait()
+        if device.type == "cuda":
+            torch.cuda.synchronize(device)
 
-def _pg(ranks: Sequence[int], my_rank: int, backend: str) -> GangPG:
-    """One communicator per (rank set, backend) per process (members create
-    it the first time they need it; the store prefix is the rank set)."""
-    key = (tuple(ranks), backend)
-    if key not in _PGS:
-        _PGS[key] = GangPG(ranks, my_rank, backend)
-    return _PGS[key]
+    def failed(self) -> bool:
+        """Aborted here, or the NCCL watchdog recorded an error (a timed-out
+        or aborted collective: its results are garbage)."""
+        if self.aborted:
+            return True
+        if self.backend == "nccl":
+            try:
+                return int(self.pg.get_error()) != 0
+            except Exception:
+                return False
+        return False
+
+    def abort(self) -> None:
+        """Abort the communicator: in-flight RCCL kernels exit, pending works
+        complete with an error. Safe from any thread (the control plane's
+        watcher calls it while the training thread is stuck in a collective
+        with a dead peer) and idempotent."""
+        if self.aborted:
+            return
+        self.aborted = True
+        try:
+            self.pg.abort()
+        except Exception:
+            pass
+
+    def shutdown(self) -> None:
+        """Orderly destruction of an idle communicator (eviction)."""
+        if self.aborted:
+            return
+        try:
+            self.pg.shutdown()
+        except Exception:
+            self.abort()
+        self.aborted = True
+
+
+class PGCache:
+    """This process's member-only communicators, keyed by (rank set, backend),
+    reference-counted by the gang comms built on them (a spread gang's
+    intra-virtual-node part can be the same rank set as a consolidated gang).
+
+    Every change is driven by the round plan (``group`` / ``ungroup`` /
+    ``abort`` actions, identical on every rank), so the members of a rank
+    set create, re-create and destroy its communicator in lock-step -- the
+    per-key generation counter therefore agrees across members without any
+    extra exchange. A communicator nobody references is shut down at once
+    unless it is PINNED (the canonical buddy rank sets pre-created outside
+    the timed region, ``canonical_gang_sets``). The only asynchronous entry
+    is ``abort_where``: the control plane's watcher thread aborts the
+    communicators that contain a dead rank (or that a gang member reported
+    broken) to unblock a training thread stuck in a collective; the entries
+    stay until the plan's ``abort`` action purges them."""
+
+    def __init__(self):
+        self._lock = threading.Lock()
+        self._e: Dict[tuple, list] = {}          # key -> [GangPG, refs, pinned]
+        self._gen: Dict[tuple, int] = {}
+        self.created = 0
+        self.destroyed = 0
+
+    def acquire(self, ranks: Sequence[int], my_rank: int, backend: str, pin: bool = False) -> GangPG:
+        key = (tuple(ranks), backend)
+        with self._lock:
+            e = self._e.get(key)
+            if e is None:
+                gen = self._gen.get(key, 0)
+                self._gen[key] = gen + 1
+                e = [GangPG(key[0], my_rank, backend, gen=gen), 0, False]
+                self._e[key] = e
+                self.created += 1
+            e[1] += 1
+            e[2] = e[2] or pin
+            return e[0]
+
+    def release(self, pg: GangPG, purge: bool = False) -> None:
+        """Drop one reference; ``purge`` removes (and aborts) the entry now
+        regardless of other references or pinning."""
+        with self._lock:
+            e = self._e.get(pg.key)
+            if e is None or e[0] is not pg:
+                return
+            e[1] -= 1
+            if purge or pg.aborted:
+                del self._e[pg.key]
+                self.destroyed += 1
+                pg.abort()
+            elif e[1] <= 0 and not e[2]:
+                del self._e[pg.key]
+                self.destroyed += 1
+                pg.shutdown()
+
+    def purge(self, keys) -> None:
+        with self._lock:
+            for k in keys:
+                k = (tuple(k[0]), k[1])
+                e = self._e.pop(k, None)
+                if e is not None:
+                    self.destroyed += 1
+                    e[0].abort()
+
+    def abort_where(self, pred) -> List[tuple]:
+        with self._lock:
+            hit = [e[0] for k, e in self._e.items() if pred(k) and not e[0].aborted]
+        for pg in hit:
+            pg.abort()
+        return [pg.key for pg in hit]
+
+    def live(self) -> List[tuple]:
+        with self._lock:
+            return sorted(self._e)
+
+    def __len__(self) -> int:
+        return len(self._e)
+
+    def clear(self) -> None:
+        with self._lock:
+            es, self._e = list(self._e.values()), {}
+        for e in es:
+            e[0].shutdown()
+
+
+PG_CACHE = PGCache()
+
+
+class FailedComm:
+    """Stands in for a gang communicator whose creation failed on this rank
+    (a member never arrived): the first bucket raises, so the gang's step
+    reports an error and the controller aborts + re-creates the set
+    (``Controller.gang_failed``) instead of the worker dying."""
+    kind = "failed"
+
+    def __init__(self, ranks, why: str):
+        self.ranks = tuple(ranks)
+        self.size = len(self.ranks)
+        self.why = why
+
+    def start(self, view):
+        raise RuntimeError(f"gang communicator {self.ranks} unavailable: {self.why}")
+
+    def finish(self, handles) -> None:
+        pass
+
+    def close(self, purge: bool = False) -> None:
+        pass
+
+
+def comm_keys(ranks: Sequence[int], vnode_size: int = 0, backend: str = "nccl") -> List[tuple]:
+    """The communicator keys (rank set, backend) a gang over ``ranks`` is
+    built on -- the same rule ``create_gang_comm`` applies, so the controller
+    knows which gangs an abort takes down without asking the workers."""
+    ranks = tuple(sorted(int(r) for r in ranks))
+    parts = vnode_parts(ranks, vnode_size)
+    if len(ranks) <= 1:
+        return []
+    if len(parts) <= 1:
+        return [(ranks, backend)]
+    keys = [(tuple(p), backend) for p in parts if len(p) > 1]
+    keys.append((tuple(p[0] for p in parts), "gloo"))
+    return keys
+
+
+def canonical_gang_sets(world: int, vnode_size: int = 0) -> List[Tuple[int, ...]]:
+    """Aligned power-of-two ("buddy") rank blocks of size >= 2, largest
+    first: {0..7}, {0..3}, {4..7}, {0,1}, ... for world 8 -- 7 sets. With
+    ``gang_align`` placement (``placement/schemes.py::AlignedPlacement``)
+    every power-of-two gang lands on one of them, so the whole replay needs
+    at most these communicators, created once, outside the timed region."""
+    out = []
+    size = 1
+    while size * 2 <= world:
+        size *= 2
+    while size >= 2:
+        for lo in range(0, world - size + 1, size):
+            out.append(tuple(range(lo, lo + size)))
+        size //= 2
+    return out
 
 
 def create_gang_comm(ranks: Sequence[int], my_rank: int, vnode_size: int = 0, backend: str = "nccl",
                      device: Optional[torch.device] = None, nic_gbps: float = DEFAULT_NIC_GBPS,
-                     nic_latency_s: float = DEFAULT_NIC_LATENCY_S):
+                     nic_latency_s: float = DEFAULT_NIC_LATENCY_S, cache: Optional[PGCache] = None,
+                     pin: bool = False):
     """Called by every live rank with the same args in the same order (the
     plan broadcast guarantees it); only members rendezvous. Returns this
-    rank's comm (None when not a member)."""
+    rank's comm (None when not a member). ``close()`` on the comm hands its
+    communicators back to the cache."""
     ranks = tuple(sorted(int(r) for r in ranks))
     parts = vnode_parts(ranks, vnode_size)
     device = device or torch.device("cpu")
+    cache = cache or PG_CACHE
     if my_rank not in ranks:
         return None
     if len(parts) <= 1:
-        return FlatComm(_pg(ranks, my_rank, backend), ranks)
+        c = FlatComm(cache.acquire(ranks, my_rank, backend, pin), ranks)
+        c._cache = cache
+        return c
     local_pgs = {}
     for p in parts:
         if len(p) > 1 and my_rank in p:
-            local_pgs[p[0]] = _pg(tuple(p), my_rank, backend)
+            local_pgs[p[0]] = cache.acquire(tuple(p), my_rank, backend, pin)
     leaders_pg = None
     leaders = tuple(p[0] for p in parts)
     if my_rank in leaders:
-        leaders_pg = _pg(leaders, my_rank, "gloo")
-    return HierComm(ranks, parts, my_rank, local_pgs, leaders_pg, device, nic_gbps, nic_latency_s)
+        leaders_pg = cache.acquire(leaders, my_rank, "gloo", pin)
+    c = HierComm(ranks, parts, my_rank, local_pgs, leaders_pg, device, nic_gbps, nic_latency_s)
+    c._cache = cache
+    return c
+
+
+class GangRegistry:
+    """The controller's (rank 0) view of the live gang communicators, and the
+    only place their lifecycle is decided ("the communicator
+    must be destroyed or aborted and re-created on resume"). It persists
+    across replays with the rank-0 ``Worker`` (as the workers' caches do).
+
+    * ``ensure(ranks)`` -> a ``group`` action the first time a gang needs a
+      rank set (LRU touch otherwise);
+    * ``evict(in_use)`` -> ``ungroup`` actions for the least recently used
+      sets beyond ``cap`` that no job holds state on (pinned canonical sets
+      never count against the cap and are never evicted);
+    * ``abort_rank(r)`` / ``abort_gang(R)`` -> ``abort`` actions for every
+      live set whose communicators include the dead rank / share a
+      communicator with a broken gang, and the sets that now need a rebind.
+
+    Workers apply those actions in plan order, so every member of a rank set
+    sees the same create / destroy sequence (``PGCache``)."""
+
+    def __init__(self, cap: int = 16):
+        from collections import OrderedDict
+
+        self.live: "OrderedDict[Tuple[int, ...], int]" = OrderedDict()   # ranks -> vnode size
+        self.pinned: set = set()
+        self.cap = cap
+        self.stats = {"created": 0, "evicted": 0, "aborted": 0, "peak_live": 0}
+
+    def _note(self):
+        self.stats["peak_live"] = max(self.stats["peak_live"], len(self.live))
+
+    def pin(self, sets, vnode_size: int) -> None:
+        for r in sets:
+            r = tuple(r)
+            self.live[r] = vnode_size
+            self.pinned.add(r)
+        self._note()
+
+    def ensure(self, ranks: Sequence[int], vnode_size: int, nic_gbps: float) -> List[dict]:
+        ranks = tuple(ranks)
+        acts = []
+        if ranks in self.live:
+            if self.live[ranks] == vnode_size:
+                self.live.move_to_end(ranks)
+                return acts
+            del self.live[ranks]                      # transport changed: rebuild
+            self.pinned.discard(ranks)
+            acts.append({"op": "ungroup", "ranks": ranks})
+        self.live[ranks] = vnode_size
+        self.stats["created"] += 1
+        self._note()
+        acts.append({"op": "group", "ranks": ranks, "vnode": vnode_size, "nic_gbps": nic_gbps})
+        return acts
+
+    def evict(self, in_use) -> List[dict]:
+        in_use = {tuple(r) for r in in_use}
+        over = sum(1 for r in self.live if r not in self.pinned) - self.cap
+        acts = []
+        for r in list(self.live):
+            if over <= 0:
+                break
+            if r in self.pinned or r in in_use:
+                continue
+            del self.live[r]
+            over -= 1
+            self.stats["evicted"] += 1
+            acts.append({"op": "ungroup", "ranks": r})
+        return acts
+
+    def _sets(self, r) -> set:
+        return {tuple(k[0]) for k in comm_keys(r, self.live.get(tuple(r), 0))}
+
+    def abort_rank(self, dead: int) -> List[dict]:
+        acts = []
+        for r in list(self.live):
+            if any(dead in ks for ks in self._sets(r)):
+                acts.append(self._abort(r, dead=dead))
+        return acts
+
+    def abort_gang(self, ranks: Sequence[int]) -> List[dict]:
+        ranks = tuple(ranks)
+        if ranks not in self.live:
+            return []
+        broken = self._sets(ranks)
+        acts = [self._abort(ranks, purge=sorted(broken))]
+        for r in list(self.live):
+            if self._sets(r) & broken:                # shares a (now aborted) communicator
+                acts.append(self._abort(r, purge=sorted(broken)))
+        return acts
+
+    def _abort(self, r, dead: Optional[int] = None, purge=None) -> dict:
+        self.live.pop(r, None)
+        self.pinned.discard(r)
+        self.stats["aborted"] += 1
+        a = {"op": "abort", "ranks": r}
+        if dead is not None:
+            a["dead"] = dead
+        if purge is not None:
+            a["purge"] = [tuple(x) for x in purge]
+        return a
+
+
+def _pgs_of(comm) -> List[GangPG]:
+    if isinstance(comm, FlatComm):
+        return [comm.pg] if isinstance(comm.pg, GangPG) else []
+    if isinstance(comm, HierComm):
+        out = [pg for pg in comm._local_all.values()]
+        if comm.leaders_pg is not None:
+            out.append(comm.leaders_pg)
+        return out
+    return []
+
+
+def comm_failed(comm) -> bool:
+    if isinstance(comm, FailedComm):
+        return True
+    return any(pg.failed() for pg in _pgs_of(comm))
+
+
+def abort_comm(comm) -> None:
+    for pg in _pgs_of(comm):
+        pg.abort()
 
 
 def comm_size(group) -> int:

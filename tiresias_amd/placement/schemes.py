@@ -409,6 +409,95 @@ class TiresiasPlacement(Placement):
         return _fill(cluster, job, order)
 
 
+def _next_pow2(n: int) -> int:
+    b = 1
+    while b < n:
+        b *= 2
+    return b
+
+
+def buddy_pick(free: Sequence[bool], count: int) -> Optional[Tuple[int, ...]]:
+    """Best-fit buddy choice on one node: the first ``count`` devices of a
+    fully free ALIGNED block of size next_pow2(count), choosing the block
+    whose enclosing free aligned region is smallest (fill a half-used pair
+    before breaking a free quad), lowest offset on ties. None if no aligned
+    block is free."""
+    n = len(free)
+    b = _next_pow2(max(1, count))
+    if b > n:
+        return None
+    best = None
+    for lo in range(0, n - b + 1, b):
+        if not all(free[lo:lo + b]):
+            continue
+        size = b
+        while size * 2 <= n:
+            plo = lo // (size * 2) * (size * 2)
+            if plo + 2 * size <= n and all(free[plo:plo + 2 * size]):
+                size *= 2
+            else:
+                break
+        key = (size, lo)
+        if best is None or key < best:
+            best = key
+    return None if best is None else tuple(range(best[1], best[1] + count))
+
+
+def align_plan(cluster: Cluster, job: Job, plan: Optional[Plan]) -> Optional[Plan]:
+    """Canonical gang rank sets (``--gang_align``, on for the live MI355X
+    runtime). Keeps the placement's choice of NODES but moves each node's
+    share of the gang onto an aligned buddy block of devices, so every
+    power-of-two gang runs on one of the ``2*gpn - 1 - gpn`` canonical rank
+    sets (``parallel/gang.py::canonical_gang_sets``) whose RCCL
+    communicators are created once, outside the timed region, instead of
+    one communicator per arbitrary device subset (up to 247 on 8 GPUs).
+    1-GPU jobs are best-fit too, which is what keeps aligned blocks free.
+    Shared (packed) placements are left alone. When the chosen node has
+    enough free GPUs but no aligned block, a single-node gang moves to the
+    best-fitting node that has one; otherwise the job waits (None)."""
+    if plan is None:
+        return None
+    for nid, devs in plan:
+        node = cluster.nodes[nid]
+        if any(node.devices[d].tasks for d in devs):
+            return plan                                # GPU sharing: not a gang rank set
+    per_node: Dict[str, int] = {}
+    for nid, devs in plan:
+        per_node[nid] = per_node.get(nid, 0) + len(devs)
+
+    def free_of(nid):
+        return [not d.tasks for d in cluster.nodes[nid].devices]
+
+    blocks = {nid: buddy_pick(free_of(nid), c) for nid, c in per_node.items()}
+    if any(b is None for b in blocks.values()):
+        if len(per_node) != 1:
+            return None
+        c = job.num_gpu
+        s = _Scratch(cluster)
+        best = None
+        for nid in cluster.nodes:
+            if not all(s.host_ok(nid, t) for t in job.tasks):
+                continue
+            fr = free_of(nid)
+            blk = buddy_pick(fr, c)
+            if blk is not None:
+                key = (sum(fr), int(nid))                # fullest node first (best fit)
+                if best is None or key < best[0]:
+                    best = (key, nid, blk)
+        if best is None:
+            return None
+        _, nid, blk = best
+        blocks = {nid: blk}
+        plan = [(nid, devs) for _, devs in plan]
+    out: Plan = []
+    used = {nid: 0 for nid in blocks}
+    for nid, devs in plan:
+        k = used[nid]
+        out.append((nid, tuple(blocks[nid][k:k + len(devs)])))
+        used[nid] = k + len(devs)
+    return out
+
+
 PLACEMENTS = {c.name: c for c in (CountPlacement, YarnPlacement, RandomPlacement, CRandomPlacement,
                                   GreedyPlacement, BalancePlacement, CBalancePlacement, HorusPlacement,
                                   GandivaPlacement, PackPlacement, TiresiasPlacement)}
