@@ -772,6 +772,9 @@ bool lstm_seq_bwd_op(const Tensor& act, const Tensor& cs, const Tensor& dH, cons
 
 void lstm_seq_policy_op(int64_t ch) { tam::lstm_seq_policy((int)ch); }
 void lstm_seq_shards_op(int64_t ns) { tam::lstm_seq_shards((int)ns); }
+void lstm_seq_residency_op(int64_t grids, int64_t rsv) { tam::lstm_seq_residency((int)grids, (int)rsv); }
+int64_t lstm_persist_timeouts_op(bool reset) { return tam::lstm_persist_timeouts(reset); }
+void lstm_seq_spin_limit_op(int64_t polls) { tam::lstm_seq_spin_limit(polls); }
 
 void lstm_bwd_op(const Tensor& act, const optional<Tensor>& c_prev, const optional<Tensor>& dh,
                  const optional<Tensor>& dc_next, const optional<Tensor>& dgates,
@@ -827,6 +830,9 @@ TORCH_LIBRARY(tam, m) {
   m.def("lstm_seq_backward(Tensor act, Tensor cs, Tensor dH, Tensor w_hh, Tensor(a!) dG, bool reverse, Tensor(b!) sync) -> bool", &lstm_seq_bwd_op);
   m.def("lstm_seq_policy(int ch) -> ()", &lstm_seq_policy_op);
   m.def("lstm_seq_shards(int ns) -> ()", &lstm_seq_shards_op);
+  m.def("lstm_seq_residency(int grids, int reserved_cus) -> ()", &lstm_seq_residency_op);
+  m.def("lstm_persist_timeouts(bool reset) -> int", &lstm_persist_timeouts_op);
+  m.def("lstm_seq_spin_limit(int polls) -> ()", &lstm_seq_spin_limit_op);
   m.def("lstm_cell_forward(Tensor gates, Tensor? c_prev, Tensor(a!) c_out, Tensor(b!) h_out, Tensor(c!)? h_f32, Tensor(d!) act) -> ()", &lstm_fwd_op);
   m.def("lstm_cell_backward(Tensor act, Tensor? c_prev, Tensor? dh, Tensor? dc_next, Tensor(a!)? dgates, Tensor(b!)? dc_prev, Tensor(c!)? dgates_bf16) -> ()", &lstm_bwd_op);
 }

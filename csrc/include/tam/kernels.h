@@ -110,6 +110,9 @@ bool lstm_seq_backward(const float* act, const float* cs, const float* dH, const
 // unit halves per persistent workgroup: 0 auto, 1 (16 units) or 2 (32 units)
 void lstm_seq_policy(int ch);
 void lstm_seq_shards(int ns);   // arrival counters per batch tile (1, 2, 4)
+void lstm_seq_residency(int grids, int reserved_cus);   // co-residency rule of the persistent grids
+int64_t lstm_persist_timeouts(bool reset);              // sticky barrier-timeout count (device)
+void lstm_seq_spin_limit(int64_t polls);                // barrier poll bound (<= 0: default)
 void lstm_cell_backward(const float* act_cache, const float* c_prev, const float* c_out,
                         const float* dh, const float* dc_next, float* dgates, float* dc_prev,
                         bf16_t* dgates_bf16, int B, int Hd, hipStream_t s);

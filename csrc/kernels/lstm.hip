@@ -188,6 +188,14 @@ void lstm_step_forward(const float* gx, const bf16_t* w_hh, const bf16_t* h_prev
 // ---------------------------------------------------------------------------
 constexpr int PL_W = 8;          // waves per workgroup
 constexpr unsigned PL_SPIN = 1u << 22;
+// Sticky count of persistent-grid barrier timeouts on this device (every job
+// of the process): the kernels never hang, but a timed-out step computed on
+// h / dG that had not arrived. The host reads it after the round's
+// synchronize (lstm_persist_timeouts) and the trainer raises + falls back to
+// the per-step path (models/gnmt.py). g_pl_spin is the poll bound (tests
+// shrink it to force a timeout).
+__device__ unsigned g_pl_timeouts;
+__device__ unsigned g_pl_spin = PL_SPIN;
 #ifndef PL_BCH
 #define PL_BCH 16         // backward: dG fragment loads in flight per chunk
 #endif
@@ -212,10 +220,12 @@ __device__ __forceinline__ void pl_signal(unsigned* sync, int line) {
 __device__ __forceinline__ void pl_wait(unsigned* sync, int line0, int ns, unsigned target) {
   if (threadIdx.x < (unsigned)ns) {
     unsigned polls = 0;
+    const unsigned spin = g_pl_spin;
     while (__hip_atomic_load((pl_gu32*)(sync + 32 * (1 + line0 + threadIdx.x)), PL_RLX) < target) {
       __builtin_amdgcn_s_sleep(1);
-      if (++polls > PL_SPIN) {
+      if (++polls > spin) {
         __hip_atomic_fetch_or((pl_gu32*)sync, 1u, PL_RLX);
+        __hip_atomic_fetch_add((pl_gu32*)&g_pl_timeouts, 1u, PL_RLX);
         break;
       }
     }
@@ -461,22 +471,49 @@ __global__ void __launch_bounds__(64 * PL_W * CH, 4) lstm_persist_bwd_kernel(
   }
 }
 
-// TWO grids must be co-resident (GPU sharing can put two GNMT jobs on one
-// device); the occupancy query is cached per kernel
+// Co-residency: g_pl_grids such grids must fit at once (GPU sharing can put
+// two GNMT jobs on one device), on the CUs left after g_pl_rsv_cus are set
+// aside for kernels that run concurrently with the recurrence and are not
+// ours -- RCCL's all-reduce of a DDP gang occupies up to one workgroup per
+// channel. Set per job by the trainer (lstm_seq_residency); the occupancy
+// query is cached per kernel.
+static int g_pl_grids = 2, g_pl_rsv_cus = 0;
+void lstm_seq_residency(int grids, int reserved_cus) {
+  g_pl_grids = grids < 1 ? 1 : grids;
+  g_pl_rsv_cus = reserved_cus < 0 ? 0 : reserved_cus;
+}
+
 static bool pl_fits(const void* kern, int threads, int grid) {
   static std::mutex mu;
-  static std::map<const void*, int> cap;
+  static std::map<const void*, std::pair<int, int>> cap;   // kernel -> (per CU, CUs)
   std::lock_guard<std::mutex> g(mu);
   auto it = cap.find(kern);
   if (it == cap.end()) {
-    int per_cu = 0, dev = 0, cus = 0, c = 0;
-    if (hipGetDevice(&dev) == hipSuccess &&
-        hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess &&
-        hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kern, threads, 0) == hipSuccess)
-      c = per_cu * cus;
-    it = cap.emplace(kern, c).first;
+    int per_cu = 0, dev = 0, cus = 0;
+    if (!(hipGetDevice(&dev) == hipSuccess &&
+          hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess &&
+          hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kern, threads, 0) == hipSuccess))
+      per_cu = cus = 0;
+    it = cap.emplace(kern, std::make_pair(per_cu, cus)).first;
   }
-  return 2 * grid <= it->second;
+  const int usable = it->second.first * (it->second.second - g_pl_rsv_cus);
+  return g_pl_grids * grid <= usable;
+}
+
+int64_t lstm_persist_timeouts(bool reset) {
+  unsigned v = 0;
+  if (hipMemcpyFromSymbol(&v, HIP_SYMBOL(g_pl_timeouts), sizeof(v), 0, hipMemcpyDeviceToHost) != hipSuccess)
+    return -1;
+  if (reset && v) {
+    unsigned z = 0;
+    (void)hipMemcpyToSymbol(HIP_SYMBOL(g_pl_timeouts), &z, sizeof(z), 0, hipMemcpyHostToDevice);
+  }
+  return (int64_t)v;
+}
+
+void lstm_seq_spin_limit(int64_t polls) {
+  unsigned v = polls <= 0 ? PL_SPIN : (unsigned)polls;
+  (void)hipMemcpyToSymbol(HIP_SYMBOL(g_pl_spin), &v, sizeof(v), 0, hipMemcpyHostToDevice);
 }
 
 static int g_pl_ch = 0;   // 0: auto (1), 1 / 2: forced

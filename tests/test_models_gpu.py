@@ -198,3 +198,35 @@ def test_resnet50_bn_backward_in_dgrad_epilogue(gpu):
         Fx.BN_DGRAD_FUSION = False
     e = float((grads[0] - grads[1]).norm() / grads[1].norm())
     assert e < 2e-3, e
+
+
+@pytest.mark.timeout(300)
+def test_persist_barrier_timeout_is_loud_and_falls_back(gpu):
+    """A persistent-LSTM grid barrier that times out (forced: poll bound 1)
+    must not pass silently: the worker reads the sticky device counter after
+    the round's synchronize, reports a PersistTimeout error for the job and
+    switches it to the per-step recurrence; the next round runs clean (no
+    timeouts, finite loss, per-step path)."""
+    from tiresias_amd.executor.cluster_runtime import Worker
+    from tiresias_amd.models import gnmt as G
+    from tiresias_amd.ops import _lib
+
+    T = _lib.ops()
+    w = Worker(0, 1, gpu, monitor_period=0)
+    start = {"op": "start", "job": "1", "model": "gnmt", "batch": 16, "seed": 1, "ranks": (0,), "source": "fresh"}
+    w.apply({"actions": [start], "assign": {}})
+    assert w.trainers["1"].uses_persist
+    G.device_timeouts(reset=True)
+    T.lstm_seq_spin_limit(1)
+    try:
+        rep = w.run({"actions": [], "assign": {0: [("1", 1)]}, "deadline": None})
+    finally:
+        T.lstm_seq_spin_limit(0)
+    err = rep["jobs"][0].get("error") or ""
+    assert "PersistTimeout" in err, rep
+    assert not w.trainers["1"].model.persist
+    rep2 = w.run({"actions": [], "assign": {0: [("1", 2)]}, "deadline": None})
+    assert "error" not in rep2["jobs"][0], rep2
+    assert rep2["jobs"][0]["loss"] == rep2["jobs"][0]["loss"]          # finite
+    assert G.device_timeouts(reset=False) == 0
+    w.clear(keep_pool=False)

@@ -102,6 +102,10 @@ def test_malformed_requests_are_rejected_not_fatal(tmp_path):
     for name, text in bad.items():
         with open(os.path.join(inc, name), "w") as f:
             f.write(text)
+    # non-UTF-8 bytes: UnicodeDecodeError is a ValueError, not a JSONDecodeError
+    with open(os.path.join(inc, "latin1.json"), "wb") as f:
+        f.write(b'{"job_id": "\xff\xfe", "model": "resnet_tiny"}')
+    bad["latin1.json"] = None
     sp.submit("resnet_tiny", 1, iterations=2, job_id="ok")
     sp.shutdown()
     w = Worker(0, 1, torch.device("cpu"))
@@ -111,3 +115,5 @@ def test_malformed_requests_are_rejected_not_fatal(tmp_path):
     assert set(bad) <= rej
     assert os.listdir(inc) == []
     assert "positive integer" in json.load(open(os.path.join(sp.root, "rejected", "strgpu.json")))["reason"]
+    why = json.load(open(os.path.join(sp.root, "rejected", "latin1.json.reason.json")))["reason"]
+    assert "UnicodeDecodeError" in why

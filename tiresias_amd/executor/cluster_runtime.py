@@ -1092,13 +1092,26 @@ class Worker:
         if cuda:
             torch.cuda.synchronize(self.device)
         dt = time.perf_counter() - t0
+        if cuda:
+            persist = [jid for jid, _ in jobs if self.trainers[jid].uses_persist]
+            if persist:
+                from ..models.gnmt import device_timeouts
+
+                # the persistent LSTM kernels never hang: a grid barrier that
+                # timed out set a sticky device counter -- read once per round
+                n_to = device_timeouts(reset=True)
+                if n_to:
+                    for jid in persist:
+                        self.trainers[jid].disable_persist()
+                    err = (f"PersistTimeout: {n_to} persistent LSTM barrier timeout(s) this round; "
+                           f"jobs {persist} fall back to the per-step recurrence")
         if len(jobs) == 1 and err is None:
             t = self.trainers[jobs[0][0]]
             if t.ddp is not None and comm_failed(t.group):
                 # the NCCL watchdog (CleanUpOnly) or the control plane's
                 # watcher aborted the communicator under this round's steps
                 err = "gang communicator failed (aborted / watchdog timeout)"
-        if err is not None:
+        if err is not None and len(jobs) == 1 and not err.startswith("PersistTimeout"):
             t = self.trainers[jobs[0][0]]
             if t.group is not None:
                 abort_comm(t.group)            # never step on it again

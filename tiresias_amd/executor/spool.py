@@ -71,8 +71,11 @@ class Spool:
             try:
                 with open(path) as f:
                     req = json.load(f)
-            except json.JSONDecodeError as e:
-                self._reject_raw(path, f"unparseable JSON: {e}")
+            except ValueError as e:
+                # JSONDecodeError, and UnicodeDecodeError for non-UTF-8 bytes
+                # (both ValueErrors): an untrusted file must never reach the
+                # controller (rank 0) as an exception
+                self._reject_raw(path, f"unparseable request: {type(e).__name__}: {e}")
                 continue
             except OSError:
                 continue                     # vanished / unreadable right now: retry next poll

@@ -132,7 +132,26 @@ class Trainer:
             else:
                 _cpu_opt(self.opt, w, g, self.opt_state, lo, hi, wb, self.lr, wd, gscale, self.step_count)
 
+    @property
+    def uses_persist(self) -> bool:
+        """The model runs the persistent-grid LSTM kernels (GNMT)."""
+        return self.device.type == "cuda" and bool(getattr(self.model, "persist", False))
+
+    def disable_persist(self) -> None:
+        """After a persistent-barrier timeout: the per-step recurrence for the
+        rest of the job (a captured graph baked the persistent kernels in, so
+        it is re-captured)."""
+        if hasattr(self.model, "persist"):
+            self.model.persist = False
+        self._graph = None
+        self._g_loss = None
+
     def step(self) -> torch.Tensor:
+        if self.uses_persist:
+            # co-residency rule of the persistent grids (lstm.hip): a DDP
+            # gang's RCCL kernels run next to the recurrence -> keep CUs free
+            # for them; a 1-GPU job may share its GPU with one more grid
+            _lib.ops().lstm_seq_residency(1 if self.ddp is not None else 2, 64 if self.ddp is not None else 0)
         if self._ready is not None:
             torch.cuda.current_stream(self.device).wait_event(self._ready)
             self._ready = None

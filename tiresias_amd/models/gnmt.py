@@ -63,9 +63,23 @@ def persist_errors() -> int:
     return sum(int(t[0].item()) for t in _SYNCS)
 
 
+class PersistTimeout(RuntimeError):
+    """A persistent LSTM grid barrier timed out during the last round's
+    steps: those steps computed on hidden states / gradients that had not
+    arrived. Raised by ``check_device_errors`` after the round's
+    synchronize; the model has already switched to the per-step path."""
+
+
+def device_timeouts(reset: bool = True) -> int:
+    """Sticky device-wide count of persistent-barrier timeouts since the last
+    reset (lstm.hip ``g_pl_timeouts``). Host read: call after a synchronize
+    (the worker does, once per round -- never per step)."""
+    return int(_T().lstm_persist_timeouts(reset))
+
+
 class _LSTMLayer(Function):
     @staticmethod
-    def forward(ctx, x, token, w_ih: Param, w_hh: Param, b: Param, reverse: bool):
+    def forward(ctx, x, token, w_ih: Param, w_hh: Param, b: Param, reverse: bool, persist: bool = True):
         T, B, I = x.shape
         Hd = w_hh.shape[1]
         dev = x.device
@@ -79,7 +93,7 @@ class _LSTMLayer(Function):
             _T().gemm(x2, True, w_ih.w, True, G, 0, b.w, False, None, 1.0, False)
             Gv = G.view(T, B, 4 * Hd)
             sy = _sync(dev, B)
-            ran = PERSIST and _ran(_T().lstm_seq_forward(Gv, w_hh.w, Hs, Cs, act, reverse, sy), sy)
+            ran = PERSIST and persist and _ran(_T().lstm_seq_forward(Gv, w_hh.w, Hs, Cs, act, reverse, sy), sy)
             steps = [] if ran else steps
             prev = None
             # the fused per-timestep kernel (lstm_step_forward) ties GEMM + cell +
@@ -115,13 +129,13 @@ class _LSTMLayer(Function):
                 act[t] = torch.cat([i, f, gg, o, tc], 1)
                 prev = t
         ctx.save_for_backward(x, Hs, Cs, act)
-        ctx.p = (w_ih, w_hh, b, reverse)
+        ctx.p = (w_ih, w_hh, b, reverse, persist)
         return Hs
 
     @staticmethod
     def backward(ctx, dH):
         x, Hs, Cs, act = ctx.saved_tensors
-        w_ih, w_hh, b, reverse = ctx.p
+        w_ih, w_hh, b, reverse, persist = ctx.p
         T, B, I = x.shape
         Hd = Hs.shape[2]
         dev = x.device
@@ -132,8 +146,8 @@ class _LSTMLayer(Function):
             sy = _sync(dev, B)
             # the persistent kernel reads dH as it comes (bf16); only the
             # per-step path needs the fp32 accumulator it updates in place
-            ran = PERSIST and _ran(_T().lstm_seq_backward(act, Cs, dH.contiguous(), w_hh.w, dG, reverse, sy),
-                                   sy)
+            ran = PERSIST and persist and _ran(
+                _T().lstm_seq_backward(act, Cs, dH.contiguous(), w_hh.w, dG, reverse, sy), sy)
             if not ran:                            # per-step path: cell-state gradient carry
                 dHf = dH.float().contiguous()
                 dc = torch.zeros(B, Hd, dtype=torch.float32, device=dev)
@@ -198,12 +212,12 @@ class _LSTMLayer(Function):
         w_ih.grad_ready()
         w_hh.grad_ready()
         b.grad_ready()
-        return dx, None, None, None, None, None
+        return dx, None, None, None, None, None, None
 
 
-def lstm(x, p, reverse=False):
+def lstm(x, p, reverse=False, persist=True):
     """x: [T,B,I] bf16 -> [T,B,H] bf16."""
-    return _LSTMLayer.apply(x.contiguous(), p[0].arena.token, p[0], p[1], p[2], reverse)
+    return _LSTMLayer.apply(x.contiguous(), p[0].arena.token, p[0], p[1], p[2], reverse, persist)
 
 
 class GNMT:
@@ -214,6 +228,9 @@ class GNMT:
     # 2 x 8 MB of W_hh through the 4 MB per-XCD L2s): measured on MI355X,
     # hipGraph step 15.5 ms one stream vs 16.3 ms with branches
     branch_default = False
+    # whole-sequence persistent recurrences; off for the rest of the job
+    # after a barrier timeout (Trainer.check_device_errors)
+    persist = True
 
     def __init__(self, arena: Arena, vocab: int = 32000, hidden: int = 1024, enc_layers: int = 4,
                  dec_layers: int = 4, heads: int = 16):
@@ -248,16 +265,16 @@ class GNMT:
         tgt_t = tgt_in.t().contiguous()
         with Fx.on_branch(1, tgt_t):
             y = Fx.embedding(tgt_t, self.tgt_emb)
-            d0 = lstm(y, self.dec[0])                    # [T,B,H]
+            d0 = lstm(y, self.dec[0], persist=self.persist)                    # [T,B,H]
             q = Fx.linear(d0.transpose(0, 1).contiguous(), self.att_q)   # [B,T,H]
         x = Fx.embedding(src.t().contiguous(), self.src_emb)
         with Fx.on_branch(0, x):
-            bw = lstm(x, self.enc[1], reverse=True)
-        fw = lstm(x, self.enc[0])
+            bw = lstm(x, self.enc[1], reverse=True, persist=self.persist)
+        fw = lstm(x, self.enc[0], persist=self.persist)
         bw = Fx.join_branch(0, bw)
-        h = lstm(torch.cat([fw, bw], 2), self.enc[2])
+        h = lstm(torch.cat([fw, bw], 2), self.enc[2], persist=self.persist)
         for i, p in enumerate(self.enc[3:]):
-            o = lstm(h, p)
+            o = lstm(h, p, persist=self.persist)
             h = Fx.add(h, o) if i >= 0 else o          # residual from layer 3 on
         mem = h.transpose(0, 1).contiguous()             # [B,S,H]
         kv = Fx.linear(mem, self.att_kv)                 # [B,S,2H]
@@ -265,7 +282,7 @@ class GNMT:
         ctxv = Fx.cross_attention(q, kv, self.heads).transpose(0, 1).contiguous()  # [T,B,H]
         h = d0
         for i, p in enumerate(self.dec[1:]):
-            o = lstm(torch.cat([h, ctxv], 2), p)
+            o = lstm(torch.cat([h, ctxv], 2), p, persist=self.persist)
             h = Fx.add(h, o) if i >= 1 else o
         out = torch.cat([h, ctxv], 2).transpose(0, 1).contiguous()   # [B,T,2H]
         return Fx.linear(out, self.cls_w, self.cls_b)
