@@ -627,23 +627,24 @@ void cast_op(const Tensor& x, const Tensor& y) {
 
 // ------------------------------------------------------------------ optimizers
 void sgd_op(const Tensor& w, const Tensor& g, const Tensor& mom, const Tensor& wb, double lr,
-            double momentum, double wd, double gscale, bool nesterov, bool zero_grad) {
+            double momentum, double wd, double gscale, bool nesterov, bool zero_grad, bool lstm_guard) {
   check_f32(w, "w"); check_f32(g, "g"); check_f32(mom, "mom"); check_bf16(wb, "wb");
   TORCH_CHECK(w.numel() % 4 == 0 && g.numel() == w.numel() && mom.numel() == w.numel() &&
                   wb.numel() == w.numel(),
               "tam.sgd: sizes");
   tam::sgd_step(w.data_ptr<float>(), g.data_ptr<float>(), mom.data_ptr<float>(), bpm(wb), w.numel(),
                 (float)lr, (float)momentum, (float)wd, (float)gscale, nesterov, zero_grad,
-                cur_stream(w));
+                cur_stream(w), lstm_guard ? tam::lstm_timeout_word() : nullptr);
 }
 void adam_op(const Tensor& w, const Tensor& g, const Tensor& m, const Tensor& v, const Tensor& wb,
              double lr, double b1, double b2, double eps, double wd, int64_t step, double gscale,
-             bool zero_grad) {
+             bool zero_grad, bool lstm_guard) {
   check_f32(w, "w"); check_f32(g, "g"); check_f32(m, "m"); check_f32(v, "v"); check_bf16(wb, "wb");
   TORCH_CHECK(w.numel() % 4 == 0, "tam.adam: numel % 4");
   tam::adam_step(w.data_ptr<float>(), g.data_ptr<float>(), m.data_ptr<float>(), v.data_ptr<float>(),
                  bpm(wb), w.numel(), (float)lr, (float)b1, (float)b2, (float)eps, (float)wd,
-                 (int)step, (float)gscale, zero_grad, cur_stream(w));
+                 (int)step, (float)gscale, zero_grad, cur_stream(w),
+                 lstm_guard ? tam::lstm_timeout_word() : nullptr);
 }
 
 // ------------------------------------------------------------------ attention
@@ -821,8 +822,8 @@ TORCH_LIBRARY(tam, m) {
   m.def("relu_backward(Tensor dy, Tensor y, Tensor(a!) dx) -> ()", &relu_backward_op);
   m.def("add(Tensor a, Tensor b, Tensor(a!) y) -> ()", &add_op);
   m.def("cast_f32_bf16(Tensor x, Tensor(a!) y) -> ()", &cast_op);
-  m.def("sgd_step(Tensor(a!) w, Tensor(b!) g, Tensor(c!) mom, Tensor(d!) wb, float lr, float momentum, float wd, float gscale, bool nesterov, bool zero_grad) -> ()", &sgd_op);
-  m.def("adam_step(Tensor(a!) w, Tensor(b!) g, Tensor(c!) m, Tensor(d!) v, Tensor(e!) wb, float lr, float b1, float b2, float eps, float wd, int step, float gscale, bool zero_grad) -> ()", &adam_op);
+  m.def("sgd_step(Tensor(a!) w, Tensor(b!) g, Tensor(c!) mom, Tensor(d!) wb, float lr, float momentum, float wd, float gscale, bool nesterov, bool zero_grad, bool lstm_guard=False) -> ()", &sgd_op);
+  m.def("adam_step(Tensor(a!) w, Tensor(b!) g, Tensor(c!) m, Tensor(d!) v, Tensor(e!) wb, float lr, float b1, float b2, float eps, float wd, int step, float gscale, bool zero_grad, bool lstm_guard=False) -> ()", &adam_op);
   m.def("attn_forward(Tensor q, Tensor k, Tensor v, Tensor(a!) o, Tensor(b!) lse, bool causal, float scale, Tensor? kv_len) -> ()", &attn_forward_op);
   m.def("attn_backward(Tensor q, Tensor k, Tensor v, Tensor o, Tensor dout, Tensor lse, Tensor(a!) dq, Tensor(b!) dk, Tensor(c!) dv, Tensor(d!) dq_acc, Tensor(e!) delta, bool causal, float scale, Tensor? kv_len) -> ()", &attn_backward_op);
   m.def("lstm_step_forward(Tensor gx, Tensor w_hh, Tensor? h_prev, Tensor? c_prev, Tensor(a!) c_out, Tensor(b!) h_out, Tensor(c!) act) -> ()", &lstm_step_fwd_op);

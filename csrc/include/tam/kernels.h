@@ -79,10 +79,11 @@ void cast_f32_bf16(const float* x, bf16_t* y, long n, hipStream_t s);
 
 // optimizers over flat arenas (n % 4 == 0)
 void sgd_step(float* w, float* g, float* mom, bf16_t* wb, long n, float lr, float momentum,
-              float wd, float gscale, int nesterov, int zero_grad, hipStream_t s);
+              float wd, float gscale, int nesterov, int zero_grad, hipStream_t s,
+              const unsigned* guard = nullptr);
 void adam_step(float* w, float* g, float* m, float* v, bf16_t* wb, long n, float lr, float b1,
                float b2, float eps, float wd, int step, float gscale, int zero_grad,
-               hipStream_t s);
+               hipStream_t s, const unsigned* guard = nullptr);
 
 // fused attention (bf16, head_dim 64), layout [B][S][H][64] (token-major)
 void attn_forward(const bf16_t* q, const bf16_t* k, const bf16_t* v, bf16_t* o, float* lse, int B,
@@ -113,6 +114,7 @@ void lstm_seq_shards(int ns);   // arrival counters per batch tile (1, 2, 4)
 void lstm_seq_residency(int grids, int reserved_cus);   // co-residency rule of the persistent grids
 int64_t lstm_persist_timeouts(bool reset);              // sticky barrier-timeout count (device)
 void lstm_seq_spin_limit(int64_t polls);                // barrier poll bound (<= 0: default)
+const unsigned* lstm_timeout_word();                     // device address of the timeout counter
 void lstm_cell_backward(const float* act_cache, const float* c_prev, const float* c_out,
                         const float* dh, const float* dc_next, float* dgates, float* dc_prev,
                         bf16_t* dgates_bf16, int B, int Hd, hipStream_t s);

@@ -511,6 +511,12 @@ int64_t lstm_persist_timeouts(bool reset) {
   return (int64_t)v;
 }
 
+const unsigned* lstm_timeout_word() {
+  void* p = nullptr;
+  if (hipGetSymbolAddress(&p, HIP_SYMBOL(g_pl_timeouts)) != hipSuccess) return nullptr;
+  return (const unsigned*)p;
+}
+
 void lstm_seq_spin_limit(int64_t polls) {
   unsigned v = polls <= 0 ? PL_SPIN : (unsigned)polls;
   (void)hipMemcpyToSymbol(HIP_SYMBOL(g_pl_spin), &v, sizeof(v), 0, hipMemcpyHostToDevice);

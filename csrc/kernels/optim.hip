@@ -6,6 +6,13 @@
 // state. One launch updates the whole model: read grad + master + state,
 // write master + state + bf16 shadow, and zero the gradient for the next
 // iteration (saves the separate memset pass). 16 B per lane.
+//
+// ``guard`` (nullable): a device word that, when non-zero, turns the step
+// into a gradient reset only -- no master / state / shadow update. The
+// trainer of a GNMT job passes the persistent-LSTM timeout counter
+// (lstm.hip g_pl_timeouts): a step whose recurrence read h / dG that had not
+// arrived must not reach the weights (the host learns of it at round end and
+// switches the job to the per-step recurrence).
 #include "tam/common.h"
 #include "tam/kernels.h"
 
@@ -15,7 +22,12 @@ __global__ void __launch_bounds__(256) sgd_kernel(float* __restrict__ w, float* 
                                                    float* __restrict__ mom,
                                                    bf16_t* __restrict__ wb, long n4, float lr,
                                                    float momentum, float wd, float gscale,
-                                                   int nesterov, int zero_grad) {
+                                                   int nesterov, int zero_grad, const unsigned* guard) {
+  if (guard != nullptr && *guard != 0u) {
+    for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < n4; i += (long)gridDim.x * blockDim.x)
+      ((float4*)g)[i] = make_float4(0.f, 0.f, 0.f, 0.f);
+    return;
+  }
   for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < n4;
        i += (long)gridDim.x * blockDim.x) {
     float4 wv = ((float4*)w)[i];
@@ -41,7 +53,12 @@ __global__ void __launch_bounds__(256) adam_kernel(float* __restrict__ w, float*
                                                     bf16_t* __restrict__ wb, long n4, float lr,
                                                     float b1, float b2, float eps, float wd,
                                                     float bc1, float bc2, float gscale,
-                                                    int zero_grad) {
+                                                    int zero_grad, const unsigned* guard) {
+  if (guard != nullptr && *guard != 0u) {
+    for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < n4; i += (long)gridDim.x * blockDim.x)
+      ((float4*)g)[i] = make_float4(0.f, 0.f, 0.f, 0.f);
+    return;
+  }
   for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < n4;
        i += (long)gridDim.x * blockDim.x) {
     float4 wv = ((float4*)w)[i], gv = ((float4*)g)[i], mv = ((float4*)m)[i], vv = ((float4*)v)[i];
@@ -67,18 +84,18 @@ static int ogrid(long n4) {
 }
 
 void sgd_step(float* w, float* g, float* mom, bf16_t* wb, long n, float lr, float momentum,
-              float wd, float gscale, int nesterov, int zero_grad, hipStream_t s) {
+              float wd, float gscale, int nesterov, int zero_grad, hipStream_t s, const unsigned* guard) {
   // n % 4 == 0 (arena segments are padded to 64 elements)
   hipLaunchKernelGGL(sgd_kernel, dim3(ogrid(n / 4)), dim3(256), 0, s, w, g, mom, wb, n / 4, lr,
-                     momentum, wd, gscale, nesterov, zero_grad);
+                     momentum, wd, gscale, nesterov, zero_grad, guard);
 }
 
 void adam_step(float* w, float* g, float* m, float* v, bf16_t* wb, long n, float lr, float b1,
                float b2, float eps, float wd, int step, float gscale, int zero_grad,
-               hipStream_t s) {
+               hipStream_t s, const unsigned* guard) {
   const float bc1 = 1.f - powf(b1, (float)step), bc2 = 1.f - powf(b2, (float)step);
   hipLaunchKernelGGL(adam_kernel, dim3(ogrid(n / 4)), dim3(256), 0, s, w, g, m, v, wb, n / 4, lr,
-                     b1, b2, eps, wd, bc1, bc2, gscale, zero_grad);
+                     b1, b2, eps, wd, bc1, bc2, gscale, zero_grad, guard);
 }
 
 }  // namespace tam

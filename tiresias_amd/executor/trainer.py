@@ -124,11 +124,14 @@ class Trainer:
             w, g, wb = A.master[lo:hi], A.grad[lo:hi], A.shadow[lo:hi]
             if self.device.type == "cuda":
                 T = _lib.ops()
+                # GNMT: a step whose persistent recurrence timed out (device
+                # counter) only resets the gradient -- no weight update
+                guard = self.uses_persist
                 if self.opt == "sgd":
-                    T.sgd_step(w, g, self.opt_state[0][lo:hi], wb, self.lr, 0.9, wd, gscale, False, True)
+                    T.sgd_step(w, g, self.opt_state[0][lo:hi], wb, self.lr, 0.9, wd, gscale, False, True, guard)
                 else:
                     T.adam_step(w, g, self.opt_state[0][lo:hi], self.opt_state[1][lo:hi], wb, self.lr,
-                                0.9, 0.98, 1e-9, wd, self.step_count, gscale, True)
+                                0.9, 0.98, 1e-9, wd, self.step_count, gscale, True, guard)
             else:
                 _cpu_opt(self.opt, w, g, self.opt_state, lo, hi, wb, self.lr, wd, gscale, self.step_count)
 

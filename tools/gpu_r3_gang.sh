@@ -5,7 +5,7 @@ set -o pipefail
 # move agreement) -- gloo gang transport because RCCL refuses two ranks/GPU.
 cd $GRAFT_REPO_ROOT
 mkdir -p gpurun_out/r3
-timeout -k 10 120 python -u tools/gpu_rccl_smoke.py > gpurun_out/r3/rccl_smoke.log 2>&1
+PYTHONPATH=. timeout -k 10 120 python -u tools/gpu_rccl_smoke.py > gpurun_out/r3/rccl_smoke.log 2>&1
 rc=$?; echo rccl_rc=$rc; [ $rc -eq 0 ] || exit $rc
 timeout -k 10 300 python -u -m pytest tests/test_models_gpu.py -x -v --timeout 240 --timeout-method thread \
   -k persist_barrier > gpurun_out/r3/persist_timeout.log 2>&1
