@@ -81,6 +81,7 @@ GPU_DIST = [(1, 0.70), (2, 0.12), (4, 0.10), (8, 0.08)]
 SEQ_SCALE = 4
 TRACE_ITER_S = {"resnet50": 0.0112, "vgg16": 0.0076, "transformer": 0.0068, "gnmt": 0.0153}
 HISTORY_SEED_OFFSET = 7919          # the held-out history trace for the service prior
+_routes_loaded = 0
 
 
 def bench_trace(n_gpus: int, jobs_per_gpu: int, seed: int, work_s: float = 5.0, load: float = 1.6,
@@ -238,6 +239,8 @@ def main():
     ap.add_argument("--no-graph", action="store_true",
                     help="disable hipGraph capture of 1-GPU jobs' fwd+bwd (eager launches)")
     ap.add_argument("--no-pool", action="store_true", help="no warm trainer reuse between jobs")
+    ap.add_argument("--no-nopool-replay", action="store_true",
+                    help="skip the extra untimed replay without the warm pool (cold-build JCT)")
     ap.add_argument("--out", default=None, help="directory for job.csv / summary.json of the last step")
     a = ap.parse_args()
     pol, plc, ck, bpol, bplc, qlim, share = SCENARIOS[a.scenario]
@@ -280,10 +283,12 @@ def main():
         # warm the world communicator so later P2P / sub-groups do not need every rank
         tmp = torch.ones(1, device=device)
         dist.all_reduce(tmp)
+    global _routes_loaded
     if use_cuda:
         from tiresias_amd.ops import _lib
 
         _lib.load(required=True)
+        _routes_loaded = len([x for x in torch.ops.tam.gemm_routes().splitlines() if x.strip()])
 
     tiny = not use_cuda
     if a.scenario == "trace":
@@ -352,10 +357,13 @@ def main():
 
     longest = 0.0
     warm_done = 0
+    cold = None
     for k in range(a.warmup):
         if k > 0 and not fits(longest):
             break
-        _, dt = replay(cfg)
+        r_, dt = replay(cfg)
+        if k == 0:
+            cold = r_             # the first replay of a fresh process: every trainer built cold
         longest = max(longest, dt)
         warm_done += 1
     sync()
@@ -382,6 +390,16 @@ def main():
         # FIFO is non-preemptive: its replay can run longer than Tiresias'
         bcfg = make(a.baseline_policy, a.baseline_placement)
         base, _ = replay(bcfg)
+    nopool = None
+    if not a.no_pool and not a.no_nopool_replay and fits(1.5 * longest):
+        # one replay WITHOUT the warm trainer pool: every job builds its own
+        # trainer (allocation, init, eager warm-up, graph capture) inside its
+        # JCT -- what a cluster pays when job shapes do not repeat
+        cap = worker.pool_cap
+        worker.drain_pool()
+        worker.pool_cap = 0
+        nopool, _ = replay(cfg)
+        worker.pool_cap = cap
 
     if rank == 0:
         jcts = [s["avg_jct"] for s in sums]
@@ -434,6 +452,11 @@ def main():
             "preemptions": sums[-1]["preemptions"],
             "finished_jobs": sums[-1]["finished"],
             "baseline_avg_jct_s": round(base["avg_jct"], 4) if base else None,
+            # cold start, both untimed: the first warm-up replay of this fresh
+            # process, and one replay with the warm trainer pool disabled
+            "cold_first_replay_avg_jct_s": round(cold["avg_jct"], 4) if cold else None,
+            "no_pool_replay_avg_jct_s": round(nopool["avg_jct"], 4) if nopool else None,
+            "gemm_routes_preloaded": _routes_loaded,
             "baseline_makespan_s": round(base["makespan"], 4) if base else None,
             "shared_rounds": sums[-1].get("shared_rounds"),
             "gpu_utilization": round(statistics.fmean(s["gpu_utilization"] for s in sums), 4),
@@ -442,10 +465,11 @@ def main():
             "pressure_spills": worker.pressure_spills,
             "pool_evictions": worker.pool_evictions,
             "restore_prefetches": worker.prefetches,
-            "replays": warm_done + steps + (1 if base else 0),
+            "replays": warm_done + steps + (1 if base else 0) + (1 if nopool else 0),
             "comm_precreate_s": round(comm_setup_s, 3),
             "comm_stats": sums[-1].get("comm_stats"),
             "gang_errors": sum(s_.get("gang_errors", 0) for s_ in sums),
+            "step_errors": [e for s_ in sums for e in s_.get("step_errors", [])][:10],
             "spilled_gb": round(worker.spilled_bytes / 2 ** 30, 3),
             "max_hbm_reserved_gb": round(torch.cuda.max_memory_reserved(device) / 2 ** 30, 2) if use_cuda else None,
             "process_wall_s": round(time.perf_counter() - T_PROC0, 1),

@@ -299,9 +299,45 @@ std::string gemm_routes_op() {
       << (std::get<3>(k) ? "K" : "M") << (std::get<4>(k) ? "K" : "N") << " " << std::get<5>(k)
       << " " << std::get<6>(k) << " " << std::get<7>(k) << " "
       << (kv.second == 1 ? "lib" : kv.second == 2 ? "dma" : kv.second == 3 ? "p8" : "mfma") << " " << t[0]
-      << " " << t[1] << " " << t[2] << " " << t[3] << "\n";
+      << " " << t[1] << " " << t[2] << " " << t[3];
+    auto pc = g_p8_cfg.find(k);
+    if (pc != g_p8_cfg.end()) o << " " << pc->second.first << " " << pc->second.second;
+    o << "\n";
   }
   return o.str();
+}
+
+// Pre-load routing decisions (the format gemm_routes() prints): a per-device
+// tuning table shipped with the framework / saved by an earlier process, so
+// a cold process does not time every GEMM shape on its jobs' first steps
+// (like a library's tuned-solution database). Keys already decided in this
+// process are kept. Returns the number of keys loaded.
+int64_t gemm_routes_load_op(const std::string& text) {
+  std::istringstream in(text);
+  std::string line;
+  int64_t n = 0;
+  std::lock_guard<std::mutex> g(g_route_mu);
+  while (std::getline(in, line)) {
+    std::istringstream ls(line);
+    int64_t M, N, K, mode;
+    std::string lay, rt;
+    int f32, epi;
+    std::array<float, 4> t{};
+    if (!(ls >> M >> N >> K >> lay >> mode >> f32 >> epi >> rt >> t[0] >> t[1] >> t[2] >> t[3])) continue;
+    if (lay.size() != 2 || M <= 0 || N <= 0 || K <= 0) continue;
+    const int route = rt == "lib" ? 1 : rt == "dma" ? 2 : rt == "p8" ? 3 : rt == "mfma" ? 0 : -1;
+    if (route < 0) continue;
+    const GemmKey key{M, N, K, lay[0] == 'K', lay[1] == 'K', mode, (bool)f32, (bool)epi};
+    if (g_route.count(key)) continue;
+    int tile = -1, sp = -1;
+    if (route == 3 && !(ls >> tile >> sp)) continue;     // a p8 route needs its measured config
+    if (route == 3 && !((tile == 128 || tile == 256) && sp >= 1 && sp <= 16)) continue;
+    g_route[key] = route;
+    g_route_ms[key] = t;
+    if (route == 3) g_p8_cfg[key] = {tile, sp};
+    ++n;
+  }
+  return n;
 }
 
 // ------------------------------------------------------------------ conv
@@ -831,6 +867,7 @@ TORCH_LIBRARY(tam, m) {
   m.def("lstm_seq_backward(Tensor act, Tensor cs, Tensor dH, Tensor w_hh, Tensor(a!) dG, bool reverse, Tensor(b!) sync) -> bool", &lstm_seq_bwd_op);
   m.def("lstm_seq_policy(int ch) -> ()", &lstm_seq_policy_op);
   m.def("lstm_seq_shards(int ns) -> ()", &lstm_seq_shards_op);
+  m.def("gemm_routes_load(str text) -> int", &gemm_routes_load_op);
   m.def("lstm_seq_residency(int grids, int reserved_cus) -> ()", &lstm_seq_residency_op);
   m.def("lstm_persist_timeouts(bool reset) -> int", &lstm_persist_timeouts_op);
   m.def("lstm_seq_spin_limit(int polls) -> ()", &lstm_seq_spin_limit_op);

@@ -135,6 +135,7 @@ class Controller:
         self.resync: set = set()                # gangs whose replicas may disagree (failed step)
         self.last_old: Dict[str, Tuple[int, ...]] = {}   # job -> holders before its last P2P move
         self.gang_errors = 0
+        self.error_log: List[str] = []          # first step errors (summary)
         self.est: Dict[Tuple[str, int], float] = {}
         self.done_iters: Dict[str, int] = {j: 0 for j in self.rjobs}
         self.round = 0
@@ -194,6 +195,8 @@ class Controller:
             if jr.get("error"):
                 if self.log is not None:
                     self.log.decision(self.now(), "step-error", jid, error=str(jr["error"])[:200])
+                if len(self.error_log) < 20:
+                    self.error_log.append(f"{jid}: {str(jr['error'])[:160]}")
                 if jid in self.holders and len(self.holders[jid]) > 1:
                     self.gang_failed(jid)
             # co-located rounds measure the pair, not the job: keep the
@@ -1392,6 +1395,7 @@ def run_replay(cfg: SimConfig, jobs: List[ReplayJob], rank: int, world: int, dev
     if ctrl:
         s = ctrl.sched.summary()
         s.update(rounds=rounds, shared_rounds=shared, replay_wall_s=wall, gang_errors=ctrl.gang_errors,
+                 step_errors=list(ctrl.error_log),
                  comm_stats=dict(ctrl.comms.stats, live=len(ctrl.comms.live)),
                  iter_est={f"{k[0]}x{k[1]}": v for k, v in ctrl.est.items()},
                  runtime_breakdown={k: round(v, 4) for k, v in prof.items()},

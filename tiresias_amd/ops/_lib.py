@@ -49,7 +49,62 @@ def load(required: bool | None = None) -> bool:
                 return False
         torch.ops.load_library(str(_LIB))
         _loaded = True
+        if torch.cuda.is_available():
+            load_routes()
         return True
+
+
+# Per-device GEMM routing table (measured (path, tile, split-K) per GEMM
+# shape, ``torch.ops.tam.gemm_routes()`` format) shipped with the framework:
+# a cold process starts with the decisions instead of timing every new shape
+# on its first jobs' first steps. TAM_GEMM_ROUTES=<file> overrides, "0"
+# disables. Keyed by device so a table is only used on the hardware it was
+# measured on.
+ROUTES_DIR = Path(__file__).resolve().parent.parent.parent / "profiles"
+
+
+def device_key(index: int = 0) -> str:
+    p = torch.cuda.get_device_properties(index)
+    arch = getattr(p, "gcnArchName", "unknown").split(":")[0]
+    return f"{arch}_{p.multi_processor_count}cu"
+
+
+def routes_file(index: int = 0) -> Path:
+    env = os.environ.get("TAM_GEMM_ROUTES")
+    if env and env != "0":
+        return Path(env)
+    return ROUTES_DIR / f"gemm_routes_{device_key(index)}.txt"
+
+
+def load_routes(index: int = 0) -> int:
+    """Pre-load the routing table for this device (if one exists); returns
+    the number of shapes loaded."""
+    if os.environ.get("TAM_GEMM_ROUTES") == "0":
+        return 0
+    try:
+        f = routes_file(index)
+    except Exception:
+        return 0
+    if not f.exists():
+        return 0
+    return int(torch.ops.tam.gemm_routes_load(f.read_text()))
+
+
+def save_routes(path: str | None = None, index: int = 0) -> str:
+    """Write this process's routing decisions (merged with the file's)."""
+    f = Path(path) if path else routes_file(index)
+    cur = torch.ops.tam.gemm_routes()
+    lines = {}
+    if f.exists():
+        for ln in f.read_text().splitlines():
+            if ln.strip():
+                lines[" ".join(ln.split()[:7])] = ln
+    for ln in cur.splitlines():
+        if ln.strip():
+            lines[" ".join(ln.split()[:7])] = ln
+    f.parent.mkdir(parents=True, exist_ok=True)
+    f.write_text("".join(v + "\n" for _, v in sorted(lines.items())))
+    return str(f)
 
 
 def ops():

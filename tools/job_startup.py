@@ -21,8 +21,11 @@ def timed(fn):
 
 
 def main():
+    # TAM_GEMM_ROUTES=0: cold process WITHOUT the shipped routing table;
+    # --save-routes: write this process's measured routes to the device table
     _lib.load(required=True)
-    models = sys.argv[1].split(",") if len(sys.argv) > 1 else ["resnet50", "vgg16", "transformer", "gnmt"]
+    args = [a for a in sys.argv[1:] if not a.startswith("--")]
+    models = args[0].split(",") if args else ["resnet50", "vgg16", "transformer", "gnmt"]
     out = []
     for rep in range(2):                     # rep 0 = cold process (route tuning etc.), rep 1 = warm
         for m in models:
@@ -38,3 +41,5 @@ def main():
 
 if __name__ == "__main__":
     main()
+    if "--save-routes" in sys.argv:
+        print("routes ->", _lib.save_routes(), flush=True)
