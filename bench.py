@@ -239,6 +239,8 @@ def main():
     ap.add_argument("--no-graph", action="store_true",
                     help="disable hipGraph capture of 1-GPU jobs' fwd+bwd (eager launches)")
     ap.add_argument("--no-pool", action="store_true", help="no warm trainer reuse between jobs")
+    ap.add_argument("--no-prewarm", action="store_true",
+                    help="skip the per-process kernel pre-warm (one eager step per model family)")
     ap.add_argument("--no-nopool-replay", action="store_true",
                     help="skip the extra untimed replay without the warm pool (cold-build JCT)")
     ap.add_argument("--out", default=None, help="directory for job.csv / summary.json of the last step")
@@ -316,6 +318,9 @@ def main():
     worker = Worker(rank, world, device, world_pg, use_graph=use_cuda and not a.no_graph,
                     gang_backend="gloo" if shared_gpu else None,
                     pool_cap=0 if a.no_pool else 2, hbm_budget_gb=a.hbm_budget_gb)
+    # per-process first-launch costs (kernel code objects, library handles),
+    # paid once before the first replay like a cluster daemon's start-up
+    prewarm_s = worker.prewarm(sorted({rj.model for rj in jobs})) if use_cuda and not a.no_prewarm else 0.0
     comm_setup_s = 0.0
     if world > 1:
         # gang_align placement puts every power-of-two gang on an aligned
@@ -467,6 +472,7 @@ def main():
             "restore_prefetches": worker.prefetches,
             "replays": warm_done + steps + (1 if base else 0) + (1 if nopool else 0),
             "comm_precreate_s": round(comm_setup_s, 3),
+            "process_prewarm_s": round(prewarm_s, 3),
             "comm_stats": sums[-1].get("comm_stats"),
             "gang_errors": sum(s_.get("gang_errors", 0) for s_ in sums),
             "step_errors": [e for s_ in sums for e in s_.get("step_errors", [])][:10],
