@@ -259,7 +259,7 @@ def test_round_ends_at_next_arrival():
     assert r["jobs"][0]["iters"] == 2
 
 
-def _recover_worker(rank, world, port, outdir, fault, hb_timeout=5.0, gang_timeout=12.0):
+def _recover_worker(rank, world, port, outdir, fault, hb_timeout=5.0, gang_timeout=12.0, snapshot_s=0.0):
     import datetime
 
     os.environ["MASTER_ADDR"] = "127.0.0.1"
@@ -276,11 +276,16 @@ def _recover_worker(rank, world, port, outdir, fault, hb_timeout=5.0, gang_timeo
     jobs = bench.bench_trace(world, 4, seed=3, work_s=0.8, min_iters=4, tiny=True)
     for i in (0, 2, 5):                    # gangs spanning the victim rank
         jobs[i].spec.num_gpu = 2 if i != 5 else world - 1
+    if snapshot_s > 0:                     # every job a single replica: a loss needs the snapshot
+        for j in jobs:
+            j.spec.num_gpu = 1
     cfg = bench.make_cfg("dlas-gpu", "count", world, 3, qlimits=[0.05, 0.3])
-    w = Worker(rank, world, torch.device("cpu"), dist.group.WORLD)
+    w = Worker(rank, world, torch.device("cpu"), dist.group.WORLD, snapshot_s=snapshot_s,
+               snapshot_dir=os.path.join(outdir, "snap"))
     try:
         s = run_replay(cfg, jobs, rank, world, torch.device("cpu"), ctrl_pg=ctrl, world_pg=dist.group.WORLD,
-                       worker=w, quantum=0.05, fault=dict(fault), hb_timeout=hb_timeout, hb_period=0.3)
+                       worker=w, quantum=0.05, fault=dict(fault), hb_timeout=hb_timeout, hb_period=0.3,
+                       out_dir=outdir if rank == 0 else None)
     except BaseException:
         import traceback
 
@@ -291,11 +296,11 @@ def _recover_worker(rank, world, port, outdir, fault, hb_timeout=5.0, gang_timeo
     os._exit(0)
 
 
-def _run_recover(tmp_path, fault, world=4, hb_timeout=5.0, gang_timeout=12.0):
+def _run_recover(tmp_path, fault, world=4, hb_timeout=5.0, gang_timeout=12.0, snapshot_s=0.0):
     port = _free_port()
     ctx = mp.get_context("spawn")
     ps = [ctx.Process(target=_recover_worker, args=(r, world, port, str(tmp_path), fault, hb_timeout,
-                                                     gang_timeout)) for r in range(world)]
+                                                     gang_timeout, snapshot_s)) for r in range(world)]
     for p in ps:
         p.start()
     deadline = time.time() + 240              # one bound for the whole gang, not per process
@@ -394,3 +399,26 @@ def test_hbm_pressure_spills_only_when_needed(tmp_path):
     big = cr.Worker(0, 1, torch.device("cpu"), hbm_budget_gb=1000.0, pool_cap=0)
     s2 = cr.run_replay(cfg, jobs, 0, 1, torch.device("cpu"), worker=big, quantum=0.02)
     assert s2["finished"] == len(jobs) and big.pressure_spills == 0 and big.spilled_bytes == 0
+
+
+@pytest.mark.slow
+def test_rank_loss_restarts_from_snapshot(tmp_path):
+    """Periodic durable snapshots (ckpt/snapshot.py, every 0.02 s of a job's
+    run time): rank 3 crashes mid-replay; a job whose ONLY replica lived on
+    rank 3 resumes from its last snapshot's iteration (not 0) on another
+    rank, the redone iterations are charged in job.csv (lost_iters), and
+    every job still finishes."""
+    import csv
+    import json
+
+    ps, s = _run_recover(tmp_path, {"rank": 3, "round": 14, "kind": "crash"}, snapshot_s=0.02)
+    errs = {f.name: f.read_text()[-1500:] for f in tmp_path.glob("err*.txt")}
+    assert ps[3].exitcode == 17 and all(p.exitcode == 0 for p in ps[:3]), ([p.exitcode for p in ps], errs)
+    assert s["lost_ranks"] == [3] and s["finished"] + s["failed"] == s["jobs"]
+    assert s["snapshot_restored_jobs"], s
+    dec = [json.loads(x) for x in open(tmp_path / "decisions.jsonl")]
+    rs = [d for d in dec if d["ev"] == "restart" and d["source"] == "snapshot"]
+    assert rs and all(d["from_step"] > 0 for d in rs)
+    rows = {r["job_id"]: r for r in csv.DictReader(open(tmp_path / "job.csv"))}
+    for d in rs:
+        assert int(rows[d["job"]]["lost_iters"]) == d["lost_iters"]

@@ -167,6 +167,9 @@ class Controller:
         self._pending_acts: List[dict] = []     # aborts decided between plans (rank loss, gang errors)
         self.resync: set = set()                # gangs whose replicas may disagree (failed step)
         self.last_old: Dict[str, Tuple[int, ...]] = {}   # job -> holders before its last P2P move
+        self.snapshots: Dict[str, Tuple[int, str]] = {}  # job -> (step, path) of its last durable snapshot
+        self.from_snap: Dict[str, Tuple[int, str]] = {}  # jobs to restart from their snapshot
+        self.snap_restored: set = set()
         self.gang_errors = 0
         self.error_log: List[str] = []          # first step errors (summary)
         self.est: Dict[Tuple[str, int], float] = {}
@@ -194,6 +197,9 @@ class Controller:
     def apply_reports(self, reports: List[dict]) -> None:
         per_job: Dict[str, dict] = {}
         for r in reports:
+            for jid, step, path in (r or {}).get("snap") or []:
+                if jid in self.rjobs and (jid not in self.snapshots or step >= self.snapshots[jid][0]):
+                    self.snapshots[jid] = (int(step), path)
             for jid, c in ((r or {}).get("ckpt") or {}).items():
                 j = self.sched.jobs.get(jid)
                 if j is not None:
@@ -288,11 +294,29 @@ class Controller:
                 self.recovered.add(jid)
             else:
                 self.holders.pop(jid)
-                self.restarted.add(jid)
-                self.done_iters[jid] = 0
-                s.jobs[jid].progress = 0.0
+                self._lost_all_replicas(jid)
         if self.log is not None:
             self.log.decision(self.now(), "rank-lost", str(r), gpus_left=s.cluster.num_gpus)
+
+    def _lost_all_replicas(self, jid: str) -> None:
+        """No live rank holds the job's state: restart it from its last
+        durable snapshot (ckpt/snapshot.py) when there is one, else from
+        scratch; the redone iterations are charged (job.csv lost_iters)."""
+        j = self.sched.jobs[jid]
+        snap = self.snapshots.get(jid)
+        keep = snap[0] if snap is not None else 0
+        lost = max(0, self.done_iters[jid] - keep)
+        j.extra["lost_iters"] = j.extra.get("lost_iters", 0) + lost
+        self.done_iters[jid] = keep
+        j.progress = float(keep)
+        if snap is not None and keep > 0:
+            self.from_snap[jid] = snap
+            self.snap_restored.add(jid)
+        else:
+            self.restarted.add(jid)
+        if self.log is not None:
+            self.log.decision(self.now(), "restart", jid, from_step=keep, lost_iters=lost,
+                              source="snapshot" if keep > 0 else "scratch")
 
     def _queue_aborts(self, acts: List[dict]) -> None:
         """Abort actions go out with the next plan; held jobs whose gang
@@ -339,10 +363,7 @@ class Controller:
             self.rebind.add(jid)
         else:
             self.holders.pop(jid, None)
-            self.restarted.add(jid)
-            self.done_iters[jid] = 0
-            if j is not None:
-                j.progress = 0.0
+            self._lost_all_replicas(jid)
         if self.log is not None:
             self.log.decision(self.now(), "move-failed", jid, holders=list(old))
 
@@ -455,7 +476,12 @@ class Controller:
                 rj = self.rjobs[j.job_id]
                 act = {"op": "start", "job": j.job_id, "ranks": ranks, "model": rj.model,
                        "batch": rj.batch, "seed": int(j.job_id) if j.job_id.isdigit() else zlib.crc32(j.job_id.encode()) % 100000}
-                if old is None:
+                if old is None and j.job_id in self.from_snap:
+                    step, path = self.from_snap.pop(j.job_id)
+                    act["source"] = "snapshot"
+                    act["path"] = path
+                    act["step"] = step
+                elif old is None:
                     act["source"] = "fresh"
                 elif j.job_id in self.resync and len(old) > 1:
                     # after a failed gang step: every new member except ONE
@@ -563,7 +589,7 @@ class Controller:
 class Worker:
     def __init__(self, rank: int, world: int, device: torch.device, world_pg=None, use_graph=False,
                  gang_backend: Optional[str] = None, monitor_period: float = 5.0, pool_cap: int = 2,
-                 hbm_budget_gb: Optional[float] = None):
+                 hbm_budget_gb: Optional[float] = None, snapshot_s: float = 0.0, snapshot_dir: str = ""):
         self.gang_backend = gang_backend or ("nccl" if device.type == "cuda" else "gloo")
         # warm pool: finished jobs' trainers, keyed by (model, batch, gang
         # ranks), handed to the next fresh job of the same shape after
@@ -587,6 +613,16 @@ class Worker:
         self._pairs: Dict[Tuple[int, int], object] = {}    # state-move communicators
         self._move_failed: set = set()
         self.plane = None                        # control plane (set by run_replay): move agreement
+        # periodic durable snapshots (ckpt/snapshot.py): every snapshot_s
+        # seconds of a job's run time, written by the gang's lowest rank
+        self.snapshot_s = snapshot_s
+        self.snap = None
+        if snapshot_s > 0:
+            from ..ckpt.snapshot import SnapshotWriter
+
+            self.snap = SnapshotWriter(snapshot_dir or os.path.join("/tmp", f"tam_snap_{os.getpid()}"), device)
+        self._job_ranks: Dict[str, Tuple[int, ...]] = {}
+        self._snap_acc: Dict[str, float] = {}
         self.use_graph = use_graph
         self.spilled_bytes = 0
         self.restored_bytes = 0
@@ -849,13 +885,31 @@ class Worker:
             elif op == "drop":
                 self.streams.pop(a["job"], None)
                 self._retire(self.trainers.pop(a["job"], None))
+                self._job_ranks.pop(a["job"], None)
+                self._snap_acc.pop(a["job"], None)
+                if self.snap is not None and self.rank == min(a["ranks"]):
+                    self.snap.drop(a["job"])
             elif op == "spill":
                 if self.trainers.get(a["job"]) is not None:
                     self._spill(a["job"])
             elif op == "start":
                 ranks = tuple(a["ranks"])
                 src = a["source"]
-                if src == "fresh":
+                self._job_ranks[a["job"]] = ranks
+                if src == "snapshot":
+                    # the job's only replica died: rebuild from its last
+                    # durable snapshot (every gang member reads the file)
+                    if self.rank in ranks:
+                        from ..ckpt.snapshot import load_snapshot
+
+                        old_t = self.trainers.pop(a["job"], None)
+                        if old_t is not None:
+                            old_t.release()
+                        t = self._make_trainer(a, init=False)
+                        load_snapshot(a["path"], t)
+                        self.trainers[a["job"]] = t
+                        self._snap_acc[a["job"]] = 0.0
+                elif src == "fresh":
                     if self.rank in ranks:
                         before = torch.cuda.memory_allocated(self.device) if self.device.type == "cuda" else 0
                         self.trainers[a["job"]] = self._make_trainer(a)
@@ -1102,7 +1156,7 @@ class Worker:
         jobs = [(jid, n) for jid, n in jobs if jid not in {r["job"] for r in skipped}]
         if not jobs:
             return {"rank": self.rank, "job": None, "jobs": skipped, "dev": self._dev_sample(),
-                    "ckpt": self._ckpt_report()}
+                    "ckpt": self._ckpt_report(), "snap": self.snap.poll() if self.snap else None}
         for jid, _ in jobs:
             self._last_run[jid] = self._round
         cuda = self.device.type == "cuda"
@@ -1170,6 +1224,16 @@ class Worker:
             t = self.trainers[jobs[0][0]]
             if t.group is not None:
                 abort_comm(t.group)            # never step on it again
+        if self.snap is not None and err is None:
+            for jid, n in jobs:
+                ranks = self._job_ranks.get(jid, (self.rank,))
+                if n <= 0 or self.rank != min(ranks):
+                    continue
+                acc = self._snap_acc.get(jid, 0.0) + dt
+                if acc >= self.snapshot_s:
+                    acc = 0.0
+                    self.snap.snapshot(jid, self.trainers[jid])
+                self._snap_acc[jid] = acc
         reps = []
         for jid, n in jobs:
             t = self.trainers[jid]
@@ -1184,7 +1248,7 @@ class Worker:
                 rep["error"] = err
             reps.append(rep)
         return {"rank": self.rank, "job": jobs[0][0], "jobs": reps + skipped, "dev": self._dev_sample(),
-                "ckpt": self._ckpt_report()}
+                "ckpt": self._ckpt_report(), "snap": self.snap.poll() if self.snap else None}
 
     def _ckpt_report(self) -> Optional[dict]:
         """Per-job spill / restore bytes and measured device copy seconds since
@@ -1453,7 +1517,9 @@ def run_replay(cfg: SimConfig, jobs: List[ReplayJob], rank: int, world: int, dev
                  iter_est={f"{k[0]}x{k[1]}": v for k, v in ctrl.est.items()},
                  runtime_breakdown={k: round(v, 4) for k, v in prof.items()},
                  lost_ranks=lost_ranks, recovered_jobs=sorted(ctrl.recovered),
-                 restarted_jobs=sorted(ctrl.restarted))
+                 restarted_jobs=sorted(ctrl.restarted), snapshot_restored_jobs=sorted(ctrl.snap_restored),
+                 lost_iters={j.job_id: j.extra["lost_iters"] for j in ctrl.sched.jobs.values()
+                             if j.extra.get("lost_iters")})
         log.close()
         return s
     return None

@@ -178,6 +178,13 @@ class FakeCluster:
                     for recv, donor in donors.items():
                         charge((recv, donor), b / self.xgmi)
                         self.stats["p2p_bytes"] += b
+                elif src == "snapshot":
+                    # restart of a job whose every replica died: every member
+                    # reads the last durable snapshot from host storage
+                    if job in self.held:
+                        raise ProtocolError(f"snapshot restart of {job} whose state is still held")
+                    charge(ranks, b / self.host)
+                    self.stats["restore_bytes"] += b * len(ranks)
                 else:
                     raise ProtocolError(f"unknown start source {src}")
                 self.held[job] = ranks

@@ -30,7 +30,7 @@ CLUSTER_HEADER = ["delta", "num_idle_nodes", "num_busy_nodes", "num_busy_gpus", 
 JOB_HEADER = ["time", "job_id", "num_gpu", "submit_time", "start_time", "end_time", "executed_time",
               "JCT", "duration", "pending_time", "preempt", "resume", "promote", "migration",
               "queue", "ckpt_overhead", "ckpt_bytes", "ckpt_save_s", "ckpt_restore_s", "comm_exposed_s",
-              "comm_span_s", "model"]
+              "comm_span_s", "model", "lost_iters"]
 
 
 def percentile(xs: List[float], p: float) -> float:
@@ -161,6 +161,9 @@ class MetricsLogger:
                    ckpt_overhead=round(j.overhead_time, 6), ckpt_bytes=int(j.ckpt_bytes),
                    # measured on the live cluster (device copy time of spills / restores)
                    ckpt_save_s=round(j.extra.get("ckpt_save_s", 0.0), 6),
+                   # iterations redone after a failure (restart from the last
+                   # snapshot, or from scratch without one)
+                   lost_iters=int(j.extra.get("lost_iters", 0)),
                    ckpt_restore_s=round(j.extra.get("ckpt_restore_s", 0.0), 6),
                    comm_exposed_s=round(j.extra.get("comm_exposed_s", 0.0), 6),
                    comm_span_s=round(j.extra.get("comm_span_s", 0.0), 6),
