@@ -230,3 +230,31 @@ def test_persist_barrier_timeout_is_loud_and_falls_back(gpu):
     assert rep2["jobs"][0]["loss"] == rep2["jobs"][0]["loss"]          # finite
     assert G.device_timeouts(reset=False) == 0
     w.clear(keep_pool=False)
+
+
+def test_snapshot_roundtrip_on_device(gpu, tmp_path):
+    """ckpt/snapshot.py on the GPU: D2D clone on the compute stream, D2H on
+    the low-priority side stream, atomic file; steps issued right after the
+    snapshot do not leak into it; a fresh trainer restored from the file
+    matches the state (master, optimizer) at the snapshot's step."""
+    from tiresias_amd.ckpt.snapshot import SnapshotWriter, load_snapshot
+
+    t = Trainer("transformer_tiny", gpu, seed=5)
+    for _ in range(3):
+        t.step()
+    want_w = t.arena.master.clone()
+    want_m = t.opt_state[0].clone()
+    w = SnapshotWriter(str(tmp_path), gpu)
+    w.snapshot("7", t)
+    for _ in range(2):                       # keeps training while the copy drains
+        t.step()
+    w.flush()
+    got = w.poll()
+    assert got and got[0][0] == "7" and got[0][1] == 3
+    u = Trainer("transformer_tiny", gpu, seed=9)
+    assert load_snapshot(got[0][2], u) == 3
+    torch.cuda.synchronize()
+    assert torch.equal(u.arena.master, want_w) and torch.equal(u.opt_state[0], want_m)
+    assert not torch.equal(u.arena.master, t.arena.master)
+    assert torch.equal(u.arena.shadow, want_w.to(torch.bfloat16))
+    w.close()
