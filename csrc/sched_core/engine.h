@@ -3,6 +3,7 @@
 // driver (sanitize_main.cpp: ASan + UBSan replay of every policy).
 #pragma once
 #include <algorithm>
+#include <array>
 #include <cmath>
 #include <limits>
 #include <numeric>
@@ -21,6 +22,12 @@ struct Job {
   double submit, dur;
   int gpu;
   long idx;
+  // topology placement (yarn / tiresias): tasks of tgpu GPUs + tcpu / tmem,
+  // placement-sensitivity (tiresias), and the committed plan:
+  // per task [node, dev_0 .. dev_{tgpu-1}]
+  int ntask = 1, tgpu = 1, tcpu = 0, tmem = 0;
+  bool sens = false;
+  std::vector<int> plan;
   double progress = 0, executed = 0, total_exec = 0, pending = 0, last_pending = 0;
   int q = 0;
   long seq = 0;
@@ -70,6 +77,41 @@ struct Gittins {
 };
 
 enum Pol { FIFO, FJF, SJF, SRTF, SRSF, DLAS, DLASG, DLASGG, GITT };
+enum Place { P_COUNT, P_YARN, P_TIRESIAS };
+
+inline Place parse_place(const std::string& s) {
+  if (s == "count" || s.empty()) return P_COUNT;
+  if (s == "yarn") return P_YARN;
+  if (s == "tiresias") return P_TIRESIAS;
+  throw std::invalid_argument("sched_core: unsupported placement " + s);
+}
+
+// Racks x nodes x devices with per-node CPU / memory, the Python Cluster's
+// exclusive (no packing) state: cluster/topology.py. Placement plans are
+// built on a scratch copy and committed atomically, as there.
+struct Topo {
+  int gpn = 0;
+  std::vector<int> rack;                        // node -> rack
+  std::vector<std::vector<int>> rack_nodes;     // rack -> its nodes, in node order
+  std::vector<int> cpu_cap, mem_cap, cpu_used, mem_used;
+  std::vector<std::vector<char>> busy;          // node -> device busy
+  void init(int switches, int nodes_per, int gpus, int cpus, int mem) {
+    gpn = gpus;
+    const int n = switches * nodes_per;
+    rack.assign(n, 0);
+    rack_nodes.assign(switches, {});
+    for (int i = 0; i < n; ++i) { rack[i] = i / nodes_per; rack_nodes[i / nodes_per].push_back(i); }
+    cpu_cap.assign(n, cpus); mem_cap.assign(n, mem);
+    cpu_used.assign(n, 0); mem_used.assign(n, 0);
+    busy.assign(n, std::vector<char>(gpus, 0));
+  }
+  int nodes() const { return (int)busy.size(); }
+  int nfree(int n) const {
+    int c = 0;
+    for (char b : busy[n]) c += !b;
+    return c;
+  }
+};
 
 inline Pol parse(const std::string& s) {
   if (s == "fifo") return FIFO;
@@ -96,6 +138,25 @@ class Engine {
     if (pol_ == DLASGG || pol_ == GITT) git_.init(std::move(prior), gittins_delta);
   }
 
+  // Topology placement (yarn / tiresias) on switches x nodes x gpus with
+  // per-node CPU / memory; per-job task shape and sensitivity are passed to
+  // run_topo. "count" keeps the flat GPU pool.
+  void set_topology(const std::string& placement, int switches, int nodes_per, int gpus, int cpus, int mem) {
+    place_ = parse_place(placement);
+    topo_.init(switches, nodes_per, gpus, cpus, mem);
+    total_ = switches * nodes_per * gpus;
+  }
+
+  void run_topo(const double* submit, const double* dur, const int* gpus, const int* gpw, const int* tcpu,
+                const int* tmem, const unsigned char* sens, long n) {
+    shape_.assign(n, {});
+    for (long i = 0; i < n; ++i) {
+      const int w = std::max(1, gpw[i]);
+      shape_[i] = {std::max(1, gpus[i] / w), w, tcpu[i], tmem[i], (int)sens[i]};
+    }
+    run(submit, dur, gpus, n);
+  }
+
   // Replays n jobs (arrays by job index); results are in jobs() afterwards.
   void run(const double* submit, const double* dur, const int* gpus, long n) {
     jobs_.clear();
@@ -103,7 +164,18 @@ class Engine {
     for (long i = 0; i < n; ++i) {
       Job j;
       j.submit = submit[i]; j.dur = dur[i]; j.gpu = gpus[i]; j.idx = i;
+      if (place_ != P_COUNT) {
+        if ((long)shape_.size() != n) throw std::invalid_argument("sched_core: run_topo needs per-job shapes");
+        j.ntask = shape_[i][0]; j.tgpu = shape_[i][1]; j.tcpu = shape_[i][2]; j.tmem = shape_[i][3];
+        j.sens = shape_[i][4] != 0;
+      }
       jobs_.push_back(j);
+    }
+    if (place_ != P_COUNT) {
+      for (int k = 0; k < topo_.nodes(); ++k) {
+        std::fill(topo_.busy[k].begin(), topo_.busy[k].end(), 0);
+        topo_.cpu_used[k] = 0; topo_.mem_used[k] = 0;
+      }
     }
     std::vector<long> order(n);
     std::iota(order.begin(), order.end(), 0);
@@ -212,6 +284,7 @@ class Engine {
         j.state = DONE;
         j.end = now_;
         used_ -= j.gpu;
+        release(j);
         if (online_ && (pol_ == DLASGG || pol_ == GITT)) git_.add(j.total_exec * j.gpu);
         active_.erase(active_.begin() + a);
       } else {
@@ -294,6 +367,150 @@ class Engine {
   void preempt(Job& j) {
     j.state = PEND; j.preempt++; j.last_check = now_;
     used_ -= j.gpu;
+    release(j);
+  }
+
+  // ------------------------------------------------------------ placement
+  // engine/sim.py::Simulator._try_place -> placement/schemes.py
+  bool try_place(Job& j) {
+    if (j.gpu > total_) return false;
+    if (place_ == P_COUNT) {
+      if (j.gpu > total_ - used_) return false;
+      start(j);
+      return true;
+    }
+    std::vector<int> plan;
+    const bool ok = place_ == P_YARN ? plan_yarn(j, plan) : plan_tiresias(j, plan);
+    if (!ok) return false;
+    commit(j, plan);
+    start(j);
+    return true;
+  }
+
+  void commit(Job& j, const std::vector<int>& plan) {
+    j.plan = plan;
+    size_t p = 0;
+    for (int t = 0; t < j.ntask; ++t) {
+      const int nd = plan[p++];
+      topo_.cpu_used[nd] += j.tcpu;
+      topo_.mem_used[nd] += j.tmem;
+      for (int g = 0; g < j.tgpu; ++g) topo_.busy[nd][plan[p++]] = 1;
+    }
+  }
+
+  void release(Job& j) {
+    if (place_ == P_COUNT || j.plan.empty()) return;
+    size_t p = 0;
+    for (int t = 0; t < j.ntask; ++t) {
+      const int nd = j.plan[p++];
+      topo_.cpu_used[nd] -= j.tcpu;
+      topo_.mem_used[nd] -= j.tmem;
+      for (int g = 0; g < j.tgpu; ++g) topo_.busy[nd][j.plan[p++]] = 0;
+    }
+    j.plan.clear();
+  }
+
+  // placement/schemes.py::_fill on a scratch view: each task on the first
+  // node of ``order`` with the CPU / memory and tgpu free devices (lowest ids)
+  bool fill(const Job& j, const std::vector<int>& order, std::vector<int>& plan) const {
+    plan.clear();
+    std::vector<int> cpu = topo_.cpu_used, mem = topo_.mem_used;
+    std::vector<std::vector<char>> busy;   // copied lazily per touched node
+    std::vector<int> copied(topo_.nodes(), -1);
+    auto dev_busy = [&](int nd, int d) {
+      return copied[nd] >= 0 ? busy[copied[nd]][d] : topo_.busy[nd][d];
+    };
+    for (int t = 0; t < j.ntask; ++t) {
+      bool placed = false;
+      for (int nd : order) {
+        if (topo_.cpu_cap[nd] - cpu[nd] < j.tcpu || topo_.mem_cap[nd] - mem[nd] < j.tmem) continue;
+        int have = 0;
+        for (int d = 0; d < topo_.gpn; ++d) have += !dev_busy(nd, d);
+        if (have < j.tgpu) continue;
+        if (copied[nd] < 0) { copied[nd] = (int)busy.size(); busy.push_back(topo_.busy[nd]); }
+        auto& b = busy[copied[nd]];
+        plan.push_back(nd);
+        int got = 0;
+        for (int d = 0; d < topo_.gpn && got < j.tgpu; ++d)
+          if (!b[d]) { b[d] = 1; plan.push_back(d); ++got; }
+        cpu[nd] += j.tcpu; mem[nd] += j.tmem;
+        placed = true;
+        break;
+      }
+      if (!placed) return false;
+    }
+    return true;
+  }
+
+  bool single_node(const Job& j, const std::vector<int>& order, std::vector<int>& plan) const {
+    for (int nd : order) {
+      if (fill(j, {nd}, plan)) return true;
+    }
+    return false;
+  }
+
+  // placement/schemes.py::YarnPlacement
+  bool plan_yarn(const Job& j, std::vector<int>& plan) const {
+    const int N = topo_.nodes();
+    if (j.gpu <= topo_.gpn) {
+      std::vector<int> order(N);
+      std::iota(order.begin(), order.end(), 0);
+      return single_node(j, order, plan);
+    }
+    auto by_free = [&](std::vector<int> v) {
+      std::stable_sort(v.begin(), v.end(), [&](int a, int b) { return topo_.nfree(a) > topo_.nfree(b); });
+      return v;
+    };
+    for (const auto& rn : topo_.rack_nodes) {
+      std::vector<int> nodes = by_free(rn);
+      int tot = 0;
+      for (int nd : nodes) tot += topo_.nfree(nd);
+      if (tot >= j.gpu && fill(j, nodes, plan)) return true;
+    }
+    std::vector<int> all(N);
+    std::iota(all.begin(), all.end(), 0);
+    return fill(j, by_free(all), plan);
+  }
+
+  // placement/schemes.py::TiresiasPlacement._exclusive (skew-aware)
+  bool plan_tiresias(const Job& j, std::vector<int>& plan) const {
+    const int N = topo_.nodes(), gpn = topo_.gpn;
+    std::vector<int> all(N);
+    std::iota(all.begin(), all.end(), 0);
+    if (j.sens) {
+      if (j.gpu <= gpn) {
+        std::vector<int> order = all;
+        std::stable_sort(order.begin(), order.end(), [&](int a, int b) {
+          const int fa = topo_.nfree(a), fb = topo_.nfree(b);
+          return fa != fb ? fa < fb : a < b;
+        });
+        return single_node(j, order, plan);
+      }
+      std::vector<int> whole;
+      for (int nd : all) if (topo_.nfree(nd) == gpn) whole.push_back(nd);
+      if ((long)whole.size() * gpn < j.gpu) return false;
+      std::vector<int> rk;                         // racks by first appearance in ``whole``
+      std::vector<std::vector<int>> groups;
+      for (int nd : whole) {
+        const int r = topo_.rack[nd];
+        auto it = std::find(rk.begin(), rk.end(), r);
+        if (it == rk.end()) { rk.push_back(r); groups.push_back({nd}); }
+        else groups[it - rk.begin()].push_back(nd);
+      }
+      std::vector<int> gi(groups.size());
+      std::iota(gi.begin(), gi.end(), 0);
+      std::stable_sort(gi.begin(), gi.end(), [&](int a, int b) { return groups[a].size() > groups[b].size(); });
+      for (int g : gi)
+        if ((long)groups[g].size() * gpn >= j.gpu) return fill(j, groups[g], plan);
+      return fill(j, whole, plan);
+    }
+    std::vector<int> order = all;
+    std::stable_sort(order.begin(), order.end(), [&](int a, int b) {
+      const int fa = topo_.nfree(a), fb = topo_.nfree(b);
+      if ((fa == 0) != (fb == 0)) return fa != 0;
+      return fa != fb ? fa < fb : a < b;
+    });
+    return fill(j, order, plan);
   }
 
   void schedule() {
@@ -309,19 +526,22 @@ class Engine {
       long used = 0;
       for (long k : ord) if (used + jobs_[k].gpu <= total_) { chosen[k] = 1; used += jobs_[k].gpu; }
       for (long k : active_) if (jobs_[k].state == RUN && !chosen[k]) preempt(jobs_[k]);
-      for (long k : ord) if (chosen[k] && jobs_[k].state == PEND && jobs_[k].gpu <= total_ - used_) start(jobs_[k]);
-      for (long k : ord)
-        if (!chosen[k] && jobs_[k].state == PEND && jobs_[k].gpu <= total_ - used_) start(jobs_[k]);
+      for (long k : ord) if (chosen[k] && jobs_[k].state == PEND) try_place(jobs_[k]);
+      // work-conserving back-fill (chosen jobs that failed placement are not retried)
+      if (total_ - used_ > 0)
+        for (long k : ord)
+          if (!chosen[k] && jobs_[k].state == PEND && jobs_[k].gpu <= total_ - used_) try_place(jobs_[k]);
     } else {
       for (long k : ord) {
-        Job& j = jobs_[k];
-        if (j.gpu <= total_ - used_) start(j);
-        else if (pol_ == FIFO) break;
+        if (!try_place(jobs_[k]) && pol_ == FIFO) break;
       }
     }
   }
 
   Pol pol_;
+  Place place_ = P_COUNT;
+  Topo topo_;
+  std::vector<std::array<int, 5>> shape_;
   int total_;
   bool online_ = false;
   std::vector<double> limits_;

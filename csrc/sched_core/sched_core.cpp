@@ -20,6 +20,8 @@ using tam_sched::Engine;
 
 namespace {
 
+py::dict collect(Engine& e, long n);
+
 py::dict run_py(Engine& e, py::array_t<double> submit, py::array_t<double> dur, py::array_t<int> gpus) {
   auto s = submit.unchecked<1>();
   auto d = dur.unchecked<1>();
@@ -29,6 +31,10 @@ py::dict run_py(Engine& e, py::array_t<double> submit, py::array_t<double> dur, 
   std::vector<int> gv(n);
   for (long i = 0; i < n; ++i) { sv[i] = s(i); dv[i] = d(i); gv[i] = g(i); }
   e.run(sv.data(), dv.data(), gv.data(), n);
+  return collect(e, n);
+}
+
+py::dict collect(Engine& e, long n) {
   py::array_t<double> st(n), en(n);
   py::array_t<int> pre(n), res(n), pro(n);
   auto ST = st.mutable_unchecked<1>();
@@ -47,14 +53,38 @@ py::dict run_py(Engine& e, py::array_t<double> submit, py::array_t<double> dur, 
   return out;
 }
 
+py::dict run_topo_py(Engine& e, py::array_t<double> submit, py::array_t<double> dur, py::array_t<int> gpus,
+                     py::array_t<int> gpw, py::array_t<int> tcpu, py::array_t<int> tmem,
+                     py::array_t<unsigned char> sens) {
+  const long n = (long)submit.shape(0);
+  if (dur.shape(0) != n || gpus.shape(0) != n || gpw.shape(0) != n || tcpu.shape(0) != n ||
+      tmem.shape(0) != n || sens.shape(0) != n)
+    throw std::invalid_argument("sched_core.run_topo: per-job arrays must have equal length");
+  auto c = [](auto a) { return a.template unchecked<1>(); };
+  auto s = c(submit); auto d = c(dur); auto g = c(gpus); auto w = c(gpw); auto cp = c(tcpu); auto mm = c(tmem);
+  auto se = c(sens);
+  std::vector<double> sv(n), dv(n);
+  std::vector<int> gv(n), wv(n), cv(n), mv(n);
+  std::vector<unsigned char> ev(n);
+  for (long i = 0; i < n; ++i) {
+    sv[i] = s(i); dv[i] = d(i); gv[i] = g(i); wv[i] = w(i); cv[i] = cp(i); mv[i] = mm(i); ev[i] = se(i);
+  }
+  e.run_topo(sv.data(), dv.data(), gv.data(), wv.data(), cv.data(), mv.data(), ev.data(), n);
+  return collect(e, n);
+}
+
 }  // namespace
 
 PYBIND11_MODULE(_sched_core, m) {
-  m.doc() = "tiresias_amd native event-engine core (count placement)";
+  m.doc() = "tiresias_amd native event-engine core (count / yarn / tiresias placement)";
   py::class_<Engine>(m, "Engine")
       .def(py::init<const std::string&, int, std::vector<double>, double, double, std::vector<double>, bool>(),
            py::arg("policy"), py::arg("total_gpus"), py::arg("queue_limits") = std::vector<double>{},
            py::arg("solve_starvation") = 0.0, py::arg("gittins_delta") = 3250.0,
            py::arg("prior") = std::vector<double>{}, py::arg("online_prior") = false)
-      .def("run", &run_py, py::arg("submit"), py::arg("duration"), py::arg("gpus"));
+      .def("run", &run_py, py::arg("submit"), py::arg("duration"), py::arg("gpus"))
+      .def("set_topology", &Engine::set_topology, py::arg("placement"), py::arg("switches"),
+           py::arg("nodes_per_switch"), py::arg("gpus_per_node"), py::arg("cpus"), py::arg("mem"))
+      .def("run_topo", &run_topo_py, py::arg("submit"), py::arg("duration"), py::arg("gpus"),
+           py::arg("gpu_per_worker"), py::arg("cpu_per_task"), py::arg("mem_per_task"), py::arg("sensitive"));
 }

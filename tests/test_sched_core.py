@@ -42,3 +42,33 @@ def test_native_large_trace_fast():
     s = native.simulate_native(_cfg("dlas-gpu", gpus=512), specs)
     assert s["finished"] == 20000
     assert time.perf_counter() - t < 60
+
+
+def _topo_cfg(policy, scheme):
+    # 2 racks x 4 nodes x 8 GPUs, reference-default task shape (12 CPU / 60 GB
+    # per task): cross-node gangs, rack choice and fragmentation all matter
+    return SimConfig(schedule=policy, scheme=scheme, num_queue=3, queue_limits=[2000.0, 20000.0],
+                     gittins_delta=1500.0, solve_starvation=2.0 if policy.startswith("dlas") else 0.0,
+                     cluster=ClusterSpec(num_switch=2, num_node_p_switch=4, num_gpu_p_node=8,
+                                         num_cpu_p_node=128, mem_p_node=512))
+
+
+@pytest.mark.parametrize("scheme", ["yarn", "tiresias"])
+@pytest.mark.parametrize("policy", ["fifo", "shortest", "dlas-gpu", "gittins", "dlas-gpu-gittins"])
+def test_native_topology_placement_matches_python(policy, scheme):
+    """Native yarn / tiresias placement (racks x nodes x devices, per-node
+    CPU / memory, skew-aware consolidation) reproduces the Python engine
+    job-for-job on a 1000-job trace over 64 GPUs with 16/32-GPU gangs."""
+    specs = philly_like_trace(1000, 64, load=1.3, seed=11, median_duration=500)
+    c = _topo_cfg(policy, scheme)
+    prior = sorted(s.duration * s.num_gpu for s in philly_like_trace(1000, 64, load=1.3, seed=99,
+                                                                      median_duration=500))
+    sim = Simulator(c, specs, prior=prior)
+    ps = sim.run()
+    ns = native.simulate_native(c, specs, prior=prior)
+    py_end = np.array([sim.jobs[s.job_id].end_time for s in specs], dtype=float)
+    py_pre = np.array([sim.jobs[s.job_id].preempt_count for s in specs])
+    assert ns["finished"] == ps["finished"] == len(specs)
+    np.testing.assert_allclose(ns["per_job"]["end"], py_end, rtol=1e-9, atol=1e-6)
+    np.testing.assert_array_equal(ns["per_job"]["preempt"], py_pre)
+    assert ns["scheme"] == scheme

@@ -1,8 +1,13 @@
 """Python front-end of the native event core (``csrc/sched_core``).
 
 ``simulate_native(cfg, specs)`` returns the same summary dict as
-``engine.sim.simulate`` for the count placement and the policies the core
-implements; use it for month-scale trace sweeps (10^5 jobs in seconds).
+``engine.sim.simulate`` for the policies the core implements under the
+``count`` (flat GPU pool), ``yarn`` (consolidated, per-node CPU / memory,
+rack-aware cross-node) and ``tiresias`` (skew-aware: sensitive models
+consolidated, insensitive ones on fragments) placements -- the reference's
+sweep configuration (``execute.py:44-53``: 4 switches x 32 nodes, a month
+trace) -- and is cross-checked job-for-job against the Python engine
+(tests/test_sched_core.py). Use it for month-scale trace sweeps.
 """
 from __future__ import annotations
 
@@ -18,6 +23,7 @@ from ..metrics.logger import percentile
 
 SUPPORTED = ("fifo", "fjf", "sjf", "shortest", "shortest-gpu", "dlas", "dlas-gpu", "dlas-gpu-gittins",
              "gittins")
+PLACEMENTS = ("count", "yarn", "tiresias")
 
 
 def available() -> bool:
@@ -34,6 +40,11 @@ def simulate_native(cfg: SimConfig, specs: List[JobSpec], prior: Optional[List[f
 
     if cfg.schedule not in SUPPORTED:
         raise ValueError(f"native core supports {SUPPORTED}, not {cfg.schedule}")
+    scheme = cfg.scheme if cfg.scheme not in ("", "default") else "count"
+    if scheme not in PLACEMENTS:
+        raise ValueError(f"native core placements are {PLACEMENTS}, not {scheme}")
+    if cfg.pack or cfg.virtual_nodes or getattr(cfg, "gang_align", False):
+        raise ValueError("native core: no GPU sharing, virtual nodes or gang alignment (use engine.sim)")
     limits = list(cfg.queue_limits) or default_limits(cfg.num_queue if cfg.num_queue > 1 else 2, 3600.0)
     # prior: same rules as engine/sim.py::Simulator._prior (history, never the future)
     source = "explicit"
@@ -50,9 +61,28 @@ def simulate_native(cfg: SimConfig, specs: List[JobSpec], prior: Optional[List[f
                              float(cfg.solve_starvation), float(cfg.gittins_delta or 3250.0),
                              [float(x) for x in prior], online)
     t0 = time.perf_counter()
-    out = eng.run(np.array([s.submit_time for s in specs], dtype=np.float64),
-                  np.array([s.duration for s in specs], dtype=np.float64),
-                  np.array([s.num_gpu for s in specs], dtype=np.int32))
+    sub_a = np.array([s.submit_time for s in specs], dtype=np.float64)
+    dur_a = np.array([s.duration for s in specs], dtype=np.float64)
+    gpu_a = np.array([s.num_gpu for s in specs], dtype=np.int32)
+    if scheme == "count":
+        out = eng.run(sub_a, dur_a, gpu_a)
+    else:
+        c = cfg.cluster
+        eng.set_topology(scheme, c.num_switch, c.num_node_p_switch, c.num_gpu_p_node, c.num_cpu_p_node,
+                         c.mem_p_node)
+        sens = np.zeros(len(specs), dtype=np.uint8)
+        if scheme == "tiresias":
+            # the same oracle the Python engine consults (measured skew
+            # profile if configured, else the model's largest-tensor ratio)
+            from ..core.job import Job
+            from ..profiler.skew import SensitivityOracle
+
+            oracle = SensitivityOracle(cfg.skew_threshold, measured_path=cfg.skew_profile)
+            sens = np.array([1 if oracle(Job(s)) else 0 for s in specs], dtype=np.uint8)
+        out = eng.run_topo(sub_a, dur_a, gpu_a,
+                           np.array([s.gpu_per_worker for s in specs], dtype=np.int32),
+                           np.array([s.cpu_per_task for s in specs], dtype=np.int32),
+                           np.array([s.mem_per_task for s in specs], dtype=np.int32), sens)
     wall = time.perf_counter() - t0
     sub = np.array([s.submit_time for s in specs])
     end, start = out["end"], out["start"]
@@ -65,5 +95,5 @@ def simulate_native(cfg: SimConfig, specs: List[JobSpec], prior: Optional[List[f
                 p95_jct=percentile(jct.tolist(), 95), makespan=float(end.max() - t_first) if done.any() else 0.0,
                 avg_queueing_delay=float((start - sub)[done].mean()) if done.any() else 0.0,
                 preemptions=int(out["preempt"].sum()), promotions=int(out["promote"].sum()),
-                events=int(out["events"]), wall_s=wall, schedule=cfg.schedule, scheme="count", prior=source,
+                events=int(out["events"]), wall_s=wall, schedule=cfg.schedule, scheme=scheme, prior=source,
                 per_job={"start": start, "end": end, "preempt": out["preempt"]})

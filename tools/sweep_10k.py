@@ -6,8 +6,10 @@ trace (reference ``run_sim.py:1682-1707`` reads ``yarn-gput1000.csv``).
 Two engines:
 * the Python event engine with real placement (``yarn`` consolidated and the
   skew-aware ``tiresias`` scheme) -- the full simulator;
-* the native C++ core (``csrc/sched_core``, count placement) -- same
-  policies, month-scale speed.
+* the native C++ core (``csrc/sched_core``) -- the same policies under the
+  same yarn / tiresias placements (plus count), month-scale speed; every
+  native row with a Python twin is cross-checked (``match``: identical
+  avg JCT, preemptions and finished count).
 
 Writes ``profiles/sweep10k/sweep.csv`` + ``sweep.md`` (table) + the run's
 trace / prior descriptors.
@@ -63,8 +65,7 @@ def _run(args):
     keep = ("avg_jct", "median_jct", "p95_jct", "makespan", "avg_queueing_delay", "preemptions", "finished",
             "jobs", "prior")
     out = {k: s.get(k) for k in keep}
-    out.update(engine=engine, schedule=schedule, scheme=scheme if engine == "event" else "count",
-               wall_s=round(time.perf_counter() - t, 2))
+    out.update(engine=engine, schedule=schedule, scheme=scheme, wall_s=round(time.perf_counter() - t, 2))
     return out
 
 
@@ -75,6 +76,7 @@ def main():
     ap.add_argument("--seed", type=int, default=0)
     ap.add_argument("--workers", type=int, default=6)
     ap.add_argument("--out", default=os.path.join(ROOT, "profiles", "sweep10k"))
+    ap.add_argument("--native-only", action="store_true", help="skip the (slow) Python event engine rows")
     a = ap.parse_args()
     os.makedirs(a.out, exist_ok=True)
     # held-out history: a different seed of the same generator, GPU-service
@@ -87,30 +89,42 @@ def main():
             w.writerow([round(s.duration * s.num_gpu, 3)])
     runs = []
     for sch, sc in POLICIES:
-        runs.append(("event", sch, sc, a.jobs, a.load, a.seed, prior_path))
+        runs.append(("native", sch, sc, a.jobs, a.load, a.seed, prior_path))
     for sch in ("fifo", "shortest", "shortest-gpu", "dlas-gpu", "gittins", "dlas-gpu-gittins"):
         runs.append(("native", sch, "count", a.jobs, a.load, a.seed, prior_path))
+    if not a.native_only:
+        for sch, sc in POLICIES:
+            runs.append(("event", sch, sc, a.jobs, a.load, a.seed, prior_path))
     res = []
     with cf.ProcessPoolExecutor(max_workers=a.workers) as ex:
         for r in ex.map(_run, runs):
             print(json.dumps(r), flush=True)
             res.append(r)
+    twin = {(r["schedule"], r["scheme"]): r for r in res if r["engine"] == "event"}
+    for r in res:
+        t = twin.get((r["schedule"], r["scheme"])) if r["engine"] == "native" else None
+        r["match"] = "" if t is None else (
+            "yes" if (abs(t["avg_jct"] - r["avg_jct"]) <= 1e-6 * max(1.0, t["avg_jct"])
+                      and t["preemptions"] == r["preemptions"] and t["finished"] == r["finished"]) else "NO")
     keys = ["engine", "schedule", "scheme", "avg_jct", "median_jct", "p95_jct", "makespan",
-            "avg_queueing_delay", "preemptions", "finished", "jobs", "prior", "wall_s"]
+            "avg_queueing_delay", "preemptions", "finished", "jobs", "prior", "wall_s", "match"]
     with open(os.path.join(a.out, "sweep.csv"), "w", newline="") as f:
         w = csv.DictWriter(f, keys)
         w.writeheader()
         w.writerows(res)
-    base = {r["engine"]: r["avg_jct"] for r in res if r["schedule"] == "fifo"}
+    base = {(r["engine"], r["scheme"] == "count"): r["avg_jct"] for r in res if r["schedule"] == "fifo"}
     lines = [f"# {a.jobs}-job Philly-shaped trace, 64 GPUs (8x8), load {a.load}, seed {a.seed}",
              "", "Gittins prior: held-out history trace (seed + 7919), GPU-seconds; 2D-LAS threshold 3600 "
              "GPU-s; Gittins quantum 3250 GPU-s.", "",
+             "vs FIFO: against FIFO + yarn of the same engine (count rows: FIFO + count). match: the "
+             "native row reproduces the Python event engine's row (avg JCT, preemptions, finished).", "",
              "| engine | policy | placement | avg JCT (s) | vs FIFO | median JCT | p95 JCT | makespan | "
-             "preemptions | wall (s) |", "|---|---|---|---|---|---|---|---|---|---|"]
+             "preemptions | wall (s) | match |", "|---|---|---|---|---|---|---|---|---|---|---|"]
     for r in res:
+        b = base.get((r["engine"], r["scheme"] == "count"))
         lines.append(f"| {r['engine']} | {r['schedule']} | {r['scheme']} | {r['avg_jct']:.0f} | "
-                     f"{r['avg_jct'] / base[r['engine']]:.3f} | {r['median_jct']:.0f} | {r['p95_jct']:.0f} | "
-                     f"{r['makespan']:.0f} | {r['preemptions']} | {r['wall_s']} |")
+                     f"{(r['avg_jct'] / b) if b else float('nan'):.3f} | {r['median_jct']:.0f} | {r['p95_jct']:.0f} | "
+                     f"{r['makespan']:.0f} | {r['preemptions']} | {r['wall_s']} | {r['match']} |")
     with open(os.path.join(a.out, "sweep.md"), "w") as f:
         f.write("\n".join(lines) + "\n")
     print("\n".join(lines))
