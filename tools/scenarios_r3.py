@@ -1,0 +1,70 @@
+"""BASELINE.json config 3 ("mixed ResNet-50 / VGG-16 jobs with skew-profiled
+placement, consolidated vs spread, over xGMI") at the scale it names, on
+the FAKE backend (``executor/fake.py``): the live controller's code path
+(policy, placement, preemption, P2P moves, gang communicator lifecycle)
+against an in-process model of 8 ranks split into 2 virtual nodes of 4,
+where a spread gang pays the emulated inter-node link on every step. Times
+are VIRTUAL seconds (measured MI355X step times + the link model), not
+wall time on hardware: the 1-GPU box cannot run an 8-rank skew replay.
+
+For each seed: the same job set under Tiresias (skew-aware placement,
+consolidating placement-sensitive VGG-16 gangs) vs random placement vs YARN
+(always consolidate), all under 2D-LAS. Output: mean +- stdev over seeds.
+
+    python tools/scenarios_r3.py [--seeds 12] [--out profiles/r3/skew_fake_world8.json]
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import statistics
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--seeds", type=int, default=12)
+    ap.add_argument("--world", type=int, default=8)
+    ap.add_argument("--nic-gbps", type=float, default=12.5)
+    ap.add_argument("--out", default=os.path.join(ROOT, "profiles", "r3", "skew_fake_world8.json"))
+    a = ap.parse_args()
+    import bench
+    from tiresias_amd.executor.fake import run_fake
+
+    vn = f"2x{a.world // 2}"
+    res = {}
+    for scheme in ("tiresias", "random", "yarn"):
+        res[scheme] = []
+        for seed in range(1, a.seeds + 1):
+            jobs = bench.scenario_trace("skew", a.world, seed)
+            prior = bench.history_prior(bench.scenario_trace("skew", a.world, seed + bench.HISTORY_SEED_OFFSET))
+            cfg = bench.make_cfg("dlas-gpu", scheme, a.world, seed, qlimits=[1.0], virtual_nodes=vn)
+            cfg.nic_gbps = a.nic_gbps
+            s = run_fake(cfg, jobs, a.world, quantum=0.02, prior=prior)
+            res[scheme].append({"seed": seed, "avg_jct": s["avg_jct"], "makespan": s["makespan"],
+                                "preemptions": s["preemptions"], "p2p_gb": s["fake_stats"]["p2p_bytes"] / 1e9})
+    out = {"what": f"fake backend, {a.world} ranks as virtual nodes {vn}, spread-gang link {a.nic_gbps} GB/s, "
+                   "2D-LAS, mixed ResNet-50 / VGG-16 gangs (bench.py scenario 'skew'); VIRTUAL seconds",
+           "seeds": a.seeds, "runs": res, "summary": {}}
+    base = [r["avg_jct"] for r in res["random"]]
+    for scheme, rows in res.items():
+        j = [r["avg_jct"] for r in rows]
+        m = [r["makespan"] for r in rows]
+        ratio = [x / b for x, b in zip(j, base)]
+        out["summary"][scheme] = {"avg_jct_mean": round(statistics.fmean(j), 4),
+                                  "avg_jct_stdev": round(statistics.stdev(j), 4),
+                                  "makespan_mean": round(statistics.fmean(m), 4),
+                                  "vs_random_mean": round(statistics.fmean(ratio), 4),
+                                  "vs_random_stdev": round(statistics.stdev(ratio), 4)}
+    print(json.dumps(out["summary"], indent=1))
+    os.makedirs(os.path.dirname(a.out), exist_ok=True)
+    with open(a.out, "w") as f:
+        json.dump(out, f, indent=1)
+
+
+if __name__ == "__main__":
+    main()
