@@ -8,7 +8,12 @@ D1, D2, D8) changes the outcome, and records each job's start tick, end tick
 and devices from the reference's own log.
 
 ``TickSimulator`` must reproduce every start and end tick for fifo/yarn,
-horus/horus and gandiva/gandiva, and the exact devices for fifo/yarn.
+horus/horus, gandiva/gandiva and horus+/horus+, and the exact devices for
+fifo/yarn. horus+ re-clusters its queue with UNSEEDED k-means in the
+reference (core/jobs/utils.py:36-67); the fixture run seeds numpy / random
+in the launching interpreter (tools/ref_parity.py SEEDED) without touching
+the reference's code, so its outcome is reproducible (on these traces the
+queue never holds more than one job, so the clustering cannot reorder it).
 
 Two documented deviations are configured, not patched over:
   * the reference never applies its interference slowdown (D6,
@@ -47,7 +52,7 @@ def _replay(trace: dict, pair: str) -> TickSimulator:
 
 
 def test_fixture_covers_all_pairs():
-    assert len(CASES) == 6
+    assert len(CASES) == 8
     for t in _FX["traces"].values():
         for res in t["results"].values():
             assert {j[0] for j in t["jobs"]} == set(res), "reference run did not finish every job"

@@ -58,7 +58,13 @@ TRACES = {
         ("6", 26, 3, 1, 5.0),
     ]),
 }
-PAIRS = [("fifo", "yarn"), ("horus", "horus"), ("gandiva", "gandiva")]
+PAIRS = [("fifo", "yarn"), ("horus", "horus"), ("gandiva", "gandiva"), ("horus+", "horus+")]
+# horus+ re-clusters the queue with UNSEEDED k-means (core/jobs/utils.py:36-67,
+# np.random at :39/:62): the reference run is made reproducible by seeding
+# numpy / random in the launching interpreter before run_sim.py executes --
+# the reference's own code is not touched
+SEEDED = "import random, runpy, sys, numpy; numpy.random.seed(0); random.seed(0); " \
+         "sys.argv = ['run_sim.py'] + sys.argv[1:]; runpy.run_path('run_sim.py', run_name='__main__')"
 
 _DELTA = re.compile(r"delta-time: (\d+)")
 _PLACE = re.compile(r"placing task (\S+?)_worker\d+ at node (\S+) - device (\d+)")
@@ -98,7 +104,7 @@ def parse_log(text: str):
 
 def run_reference(ref: str, work: str, name: str, spec: dict, schedule: str, scheme: str) -> dict:
     write_trace(os.path.join(work, f"{name}.csv"), spec["jobs"])
-    cmd = [sys.executable, "run_sim.py", "--scheme", scheme, "--schedule", schedule,
+    cmd = [sys.executable, "-c", SEEDED, "--scheme", scheme, "--schedule", schedule,
            "--trace_file", f"../{name}.csv", "--num_switch", "1",
            "--num_node_p_switch", str(spec["nodes"]), "--num_gpu_p_node", str(spec["gpus_per_node"]),
            "--log_path", f"{name}_{schedule}"]
