@@ -239,6 +239,8 @@ def main():
     ap.add_argument("--no-graph", action="store_true",
                     help="disable hipGraph capture of 1-GPU jobs' fwd+bwd (eager launches)")
     ap.add_argument("--no-pool", action="store_true", help="no warm trainer reuse between jobs")
+    ap.add_argument("--no-scale-limits", dest="scale_limits", action="store_false",
+                    help="2D-LAS queue limits as given instead of per cluster GPU")
     ap.add_argument("--no-prewarm", action="store_true",
                     help="skip the per-process kernel pre-warm (one eager step per model family)")
     ap.add_argument("--no-nopool-replay", action="store_true",
@@ -305,10 +307,19 @@ def main():
     if vn is None:
         vn = f"2x{n // 2}" if (a.scenario == "skew" and n >= 4) else ""
 
+    # 2D-LAS queue limits are GPU-seconds PER CLUSTER GPU: the thresholds
+    # scale with the cluster's service rate (N GPU-s per second), so the
+    # demotion / preemption rate per GPU stays what it is on one GPU as the
+    # cluster grows. Unscaled, an N-GPU cluster preempts N times as often per
+    # unit of work, and beyond one GPU a preemption often means a P2P state
+    # move (fake backend, 10 seeds each, vs FIFO: N=2 0.58 -> 0.48, N=4
+    # 0.49 -> 0.37, N=8 0.48 -> 0.32; N=1 unchanged)
+    qlim_n = [x * n for x in qlim] if a.scale_limits else list(qlim)
+
     def make(policy, scheme):
         # the Gittins quantum scales with the job sizes (a quantum below the
         # smallest prior job gives every new job index 0: no preemption)
-        c = make_cfg(policy, scheme, n, a.seed, a.ckpt, qlim, share, virtual_nodes=vn,
+        c = make_cfg(policy, scheme, n, a.seed, a.ckpt, qlim_n, share, virtual_nodes=vn,
                      skew_profile=a.skew_profile,
                      gittins_delta=0.05 * (SEQ_SCALE if a.scenario == "seq" else 1))
         c.nic_gbps = a.nic_gbps
@@ -438,6 +449,7 @@ def main():
                 "hip_graph_1gpu_jobs": bool(use_cuda and not a.no_graph),
                 "warm_trainer_pool": not a.no_pool,
                 "policy": f"{a.policy} + {a.placement} placement (Tiresias), queue limits {qlim} GPU-s"
+                          + (f" per cluster GPU (= {qlim_n})" if a.scale_limits else "")
                           + (" + GPU sharing when full" if share else ""),
                 "baseline": f"{a.baseline_policy} + {a.baseline_placement}"
                             + (" + GPU sharing when full" if share else ""),
