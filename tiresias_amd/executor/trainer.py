@@ -135,6 +135,18 @@ class Trainer:
             else:
                 _cpu_opt(self.opt, w, g, self.opt_state, lo, hi, wb, self.lr, wd, gscale, self.step_count)
 
+    def enable_graph(self) -> None:
+        """Turn hipGraph capture on for a trainer built without it (a pooled
+        trainer now running a long job): two eager warm steps, then capture."""
+        from ..utils import debug
+
+        if self.device.type != "cuda" or debug.level() != 0 or self.ddp is not None:
+            return
+        self._want_graph = True
+        self.use_graph = True
+        self._graph = None
+        self._warm = 0
+
     @property
     def uses_persist(self) -> bool:
         """The model runs the persistent-grid LSTM kernels (GNMT)."""
