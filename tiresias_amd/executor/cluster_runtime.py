@@ -666,11 +666,13 @@ class Worker:
         data_seed = act["seed"] * 1000 + ranks.index(self.rank)
         key = (act["model"], act.get("batch"), ranks)
         # hipGraph capture (+ instantiation, + a private memory pool per
-        # graph) costs tens of ms per fresh trainer: only jobs long enough
-        # to amortise it capture; a pooled trainer that already holds a
-        # graph uses it for free (measured on MI355X, bench without the warm
-        # pool: every job capturing -> avg JCT 2.38 s, eager 0.25 s)
-        want = self.use_graph and len(ranks) == 1 and int(act.get("iters", 1 << 30)) >= self.graph_min_iters
+        # graph) costs tens of ms per fresh trainer. It pays when the
+        # trainer outlives the job in the warm pool (later jobs of the shape
+        # replay for free) or when the job alone is long enough; otherwise
+        # run eagerly (measured on MI355X, bench without the warm pool:
+        # every job capturing -> avg JCT 2.38 s, eager 0.25 s)
+        long_job = int(act.get("iters", 1 << 30)) >= self.graph_min_iters
+        want = self.use_graph and len(ranks) == 1 and (long_job or self.pool_cap > 0)
         free = self.pool.get(key)
         if free:
             self.pool_hits += 1
