@@ -357,8 +357,9 @@ tam::ConvGeom geom(const Tensor& x, const Tensor& w, const Tensor& y, int64_t st
   return g;
 }
 
-// stats (optional, fp32 [>= ceil(M/128)][2K]): BatchNorm partial sums of y
-// from the conv epilogue; returns the rows written (0: none, BN reduces y)
+// stats (optional, fp64 [2K], zeroed by the caller): BatchNorm sums of y
+// accumulated by the conv epilogue; returns 1 when they were (0: this path
+// computes none, the BN reduces y itself)
 int64_t conv_fwd_op(const Tensor& x, const Tensor& w, const Tensor& y, int64_t stride, int64_t pad,
                     int64_t dil, const optional<Tensor>& bias, bool relu, const optional<Tensor>& stats) {
   check_bf16(x, "x"); check_bf16(w, "w"); check_bf16(y, "y");
@@ -369,11 +370,10 @@ int64_t conv_fwd_op(const Tensor& x, const Tensor& w, const Tensor& y, int64_t s
   ep.bias = opt_ptr<const tam::bf16_t>(bias);
   ep.relu = relu;
   if (stats.has_value() && stats->defined()) {
-    check_f32(*stats, "stats");
-    const int64_t M = (int64_t)g.N * g.P * g.Q;
-    TORCH_CHECK(stats->is_contiguous() && stats->numel() >= (M + 127) / 128 * 2 * g.K,
-                "tam.conv_fwd: stats must hold ceil(M/128) x 2K floats");
-    ep.stats = stats->data_ptr<float>();
+    TORCH_CHECK(stats->is_cuda() && stats->scalar_type() == at::kDouble && stats->is_contiguous() &&
+                stats->numel() == tam::BN_SHARDS * 2 * g.K,
+                "tam.conv_fwd: stats must be a contiguous fp64 [BN_SHARDS * 2K] tensor");
+    ep.stats = stats->data_ptr<double>();
   }
   return tam::conv_fwd(bp(x), bp(w), g, ep, cur_stream(x));
 }
@@ -420,9 +420,9 @@ void conv_weight_t_batch_op(at::TensorList w, at::TensorList wt) {
 
 // dgrad with wt already re-laid (conv_weight_t_batch)
 // stats / bnx / bnmean / bnrstd (all or none): dx is the gradient of a
-// BatchNorm output whose input was bnx; the dgrad epilogue then writes the
-// BN-backward partial rows into stats and the op returns their count (0:
-// this shape's dgrad path computes none)
+// BatchNorm output whose input was bnx; the dgrad epilogue then accumulates
+// the BN-backward sums into stats (fp64 [2C], zeroed by the caller) and the
+// op returns 1 (0: this shape's dgrad path computes none)
 int64_t conv_dgrad_pre_op(const Tensor& dy, const Tensor& w, const Tensor& wt, const Tensor& dx,
                           int64_t stride, int64_t pad, int64_t dil, const optional<Tensor>& mask,
                           const optional<Tensor>& stats, const optional<Tensor>& bnx,
@@ -441,34 +441,17 @@ int64_t conv_dgrad_pre_op(const Tensor& dy, const Tensor& w, const Tensor& wt, c
   if (stats.has_value() && stats->defined()) {
     TORCH_CHECK(bnx.has_value() && bnmean.has_value() && bnrstd.has_value(),
                 "tam.conv_dgrad_pre: stats needs bnx, bnmean, bnrstd");
-    check_f32(*stats, "stats"); check_bf16(*bnx, "bnx"); check_f32(*bnmean, "bnmean"); check_f32(*bnrstd, "bnrstd");
+    check_bf16(*bnx, "bnx"); check_f32(*bnmean, "bnmean"); check_f32(*bnrstd, "bnrstd");
     check_contig(*bnx, "bnx");
-    const int64_t rows = (dx.numel() / g.C + 127) / 128;
-    TORCH_CHECK(bnx->numel() == dx.numel() && bnmean->numel() == g.C && bnrstd->numel() == g.C &&
-                stats->is_contiguous() && stats->numel() >= rows * 2 * g.C,
-                "tam.conv_dgrad_pre: BN-backward operand shapes");
-    ep.stats = stats->data_ptr<float>();
+    TORCH_CHECK(stats->is_cuda() && stats->scalar_type() == at::kDouble && stats->is_contiguous() &&
+                stats->numel() == tam::BN_SHARDS * 2 * g.C && bnx->numel() == dx.numel() && bnmean->numel() == g.C &&
+                bnrstd->numel() == g.C, "tam.conv_dgrad_pre: BN-backward operand shapes");
+    ep.stats = stats->data_ptr<double>();
     ep.bnx = bp(*bnx);
     ep.bnmean = bnmean->data_ptr<float>();
     ep.bnrstd = bnrstd->data_ptr<float>();
   }
   return tam::conv_dgrad(bp(dy), bp(w), bp(wt), g, ep, cur_stream(dy));
-}
-
-void bn_backward_part_op(const Tensor& dy, const Tensor& x, const Tensor& mean, const Tensor& rstd,
-                         const Tensor& gamma, const Tensor& dx, const optional<Tensor>& dgamma,
-                         const optional<Tensor>& dbeta, const Tensor& part, int64_t nblk) {
-  check_bf16(dy, "dy"); check_bf16(x, "x"); check_bf16(dx, "dx"); check_f32(part, "part");
-  check_contig(dy, "dy"); check_contig(x, "x"); check_contig(dx, "dx");
-  const int64_t C = x.size(-1);
-  const int64_t M = x.numel() / C;
-  TORCH_CHECK(dy.numel() == x.numel() && dx.numel() == x.numel() && C % 8 == 0 && nblk > 0 &&
-              part.numel() >= nblk * 2 * C, "tam.bn_backward_part: shapes");
-  Tensor ws_f = at::empty({4 * C}, x.options().dtype(at::kFloat));
-  tam::bn_backward_part(bp(dy), bp(x), mean.data_ptr<float>(), rstd.data_ptr<float>(),
-                        gamma.data_ptr<float>(), M, (int)C, bpm(dx), opt_ptr<float>(dgamma),
-                        opt_ptr<float>(dbeta), part.data_ptr<float>(), (int)nblk, ws_f.data_ptr<float>(),
-                        cur_stream(x));
 }
 
 void conv_wgrad_op(const Tensor& dy, const Tensor& x, const Tensor& dw, int64_t stride, int64_t pad,
@@ -483,49 +466,69 @@ void conv_wgrad_op(const Tensor& dy, const Tensor& x, const Tensor& dw, int64_t 
 }
 
 // ------------------------------------------------------------------ norms
+// sums (optional): fp64 [BN_SHARDS][2C] BN statistics workspace. sums_ready:
+// already accumulated (the producing conv's epilogue); otherwise it must be
+// zeroed and the reduction pass stores into it. Absent: a zeroed temporary.
+static double* bn_sums(const optional<Tensor>& sums, const Tensor& x, int64_t C, Tensor& tmp,
+                       const char* what) {
+  if (sums.has_value() && sums->defined()) {
+    TORCH_CHECK(sums->is_cuda() && sums->scalar_type() == at::kDouble && sums->is_contiguous() &&
+                sums->numel() == tam::BN_SHARDS * 2 * C, what,
+                ": sums must be a contiguous fp64 [BN_SHARDS * 2C] tensor");
+    return sums->data_ptr<double>();
+  }
+  tmp = at::zeros({tam::BN_SHARDS * 2 * C}, x.options().dtype(at::kDouble));
+  return tmp.data_ptr<double>();
+}
+
 void bn_forward_op(const Tensor& x, const optional<Tensor>& res, const Tensor& y, const Tensor& gamma,
                    const Tensor& beta, const optional<Tensor>& run_mean,
                    const optional<Tensor>& run_var, const Tensor& save_mean,
                    const Tensor& save_rstd, double eps, double momentum, bool relu,
-                   const optional<Tensor>& part, int64_t nblk) {
+                   const optional<Tensor>& sums, bool sums_ready) {
   check_bf16(x, "x"); check_bf16(y, "y"); check_contig(x, "x"); check_contig(y, "y");
   check_f32(gamma, "gamma"); check_f32(beta, "beta");
   const int64_t C = x.size(-1);
   const int64_t M = x.numel() / C;
   TORCH_CHECK(C % 8 == 0 && C <= 2048, "tam.bn: C must be a multiple of 8 and <= 2048");
-  const float* part_in = nullptr;
-  if (part.has_value() && part->defined() && nblk > 0) {
-    check_f32(*part, "part");
-    TORCH_CHECK(part->is_contiguous() && part->numel() >= nblk * 2 * C, "tam.bn_forward: partial rows");
-    part_in = part->data_ptr<float>();
-  }
-  Tensor ws_f = at::empty({(6 + 2 * tam::BN_MAX_BLOCKS) * C}, x.options().dtype(at::kFloat));
+  TORCH_CHECK(!sums_ready || (sums.has_value() && sums->defined()), "tam.bn_forward: sums_ready without sums");
   if (res.has_value() && res->defined()) { check_bf16(*res, "res"); check_contig(*res, "res"); }
+  Tensor tmp, part;
+  double* sp = bn_sums(sums, x, C, tmp, "tam.bn_forward");
+  if (!sums_ready) part = at::empty({2 * tam::BN_MAX_BLOCKS * C}, x.options().dtype(at::kFloat));
   tam::bn_forward(bp(x), opt_ptr<const tam::bf16_t>(res), bpm(y), M, (int)C, (float)eps,
                   (float)momentum, gamma.data_ptr<float>(), beta.data_ptr<float>(),
                   opt_ptr<float>(run_mean), opt_ptr<float>(run_var), save_mean.data_ptr<float>(),
-                  save_rstd.data_ptr<float>(), ws_f.data_ptr<float>(), relu, part_in, (int)nblk,
-                  cur_stream(x));
+                  save_rstd.data_ptr<float>(), relu, sp, sums_ready ? 1 : 0,
+                  sums_ready ? nullptr : part.data_ptr<float>(), cur_stream(x));
 }
 
 void bn_backward_op(const Tensor& dy, const optional<Tensor>& y, const Tensor& x, const Tensor& mean,
                     const Tensor& rstd, const Tensor& gamma, const Tensor& dx,
                     const optional<Tensor>& dres, const optional<Tensor>& dgamma,
-                    const optional<Tensor>& dbeta, bool relu, const optional<Tensor>& addend) {
+                    const optional<Tensor>& dbeta, bool relu, const optional<Tensor>& addend,
+                    const optional<Tensor>& sums, bool sums_ready) {
   check_bf16(dy, "dy"); check_bf16(x, "x"); check_bf16(dx, "dx");
   check_contig(dy, "dy"); check_contig(x, "x"); check_contig(dx, "dx");
   const int64_t C = x.size(-1);
   const int64_t M = x.numel() / C;
+  TORCH_CHECK(C % 8 == 0 && C <= 2048, "tam.bn: C must be a multiple of 8 and <= 2048");
   TORCH_CHECK(!relu || (y.has_value() && y->defined()), "tam.bn_backward: relu needs y");
-  if (addend.has_value() && addend->defined()) {
+  const bool has_add = addend.has_value() && addend->defined();
+  if (has_add) {
     check_bf16(*addend, "addend"); check_contig(*addend, "addend");
     TORCH_CHECK(addend->numel() == dy.numel(), "tam.bn_backward: addend size");
   }
-  Tensor ws_f = at::empty({(8 + 2 * tam::BN_MAX_BLOCKS) * C}, x.options().dtype(at::kFloat));
+  TORCH_CHECK(!sums_ready || ((sums.has_value() && sums->defined()) && !relu && !has_add &&
+                              !(dres.has_value() && dres->defined())),
+              "tam.bn_backward: sums_ready takes the already-masked gradient (no relu / addend / dres)");
+  Tensor tmp, part;
+  double* sp = bn_sums(sums, x, C, tmp, "tam.bn_backward");
+  if (!sums_ready) part = at::empty({2 * tam::BN_MAX_BLOCKS * C}, x.options().dtype(at::kFloat));
   tam::bn_backward(bp(dy), opt_ptr<const tam::bf16_t>(addend), opt_ptr<const tam::bf16_t>(y), bp(x), mean.data_ptr<float>(),
                    rstd.data_ptr<float>(), gamma.data_ptr<float>(), M, (int)C, relu, bpm(dx),
                    opt_ptr<tam::bf16_t>(dres), opt_ptr<float>(dgamma), opt_ptr<float>(dbeta),
-                   ws_f.data_ptr<float>(), cur_stream(x));
+                   sp, sums_ready ? 1 : 0, sums_ready ? nullptr : part.data_ptr<float>(), cur_stream(x));
 }
 
 void ln_forward_op(const Tensor& x, const Tensor& g, const Tensor& b, const Tensor& y,
@@ -613,6 +616,11 @@ void embedding_backward_op(const Tensor& dout, const Tensor& ids, const Tensor& 
 }
 
 void conv_dma_policy_op(int64_t p) { tam::conv_dma_policy((int)p); }
+void conv_halo_policy_op(int64_t p) { tam::conv_halo_policy((int)p); }
+// forced (bm, bn, splits) of the LDS-DMA conv wgrad (A/B sweeps; 0 = heuristic)
+void conv_wgrad_force_op(int64_t bm, int64_t bn, int64_t splits, int64_t noatomic) {
+  tam::conv_wgrad_force((int)bm, (int)bn, (int)splits, (int)noatomic);
+}
 // 0: never the LDS-DMA GEMM; 1: measured per-shape routing (default);
 // 2: LDS-DMA GEMM wherever eligible, tile cfg forced when >= 0 (tests/sweeps)
 int g_dma_policy = 1;
@@ -832,10 +840,9 @@ TORCH_LIBRARY(tam, m) {
   m.def("conv_dgrad(Tensor dy, Tensor w, Tensor(a!) wt, Tensor(b!) dx, int stride, int pad, int dil, Tensor? mask) -> ()", &conv_dgrad_op);
   m.def("conv_weight_t_batch(Tensor[] w, Tensor(a!)[] wt) -> ()", &conv_weight_t_batch_op);
   m.def("conv_dgrad_pre(Tensor dy, Tensor w, Tensor wt, Tensor(a!) dx, int stride, int pad, int dil, Tensor? mask, Tensor(b!)? stats=None, Tensor? bnx=None, Tensor? bnmean=None, Tensor? bnrstd=None) -> int", &conv_dgrad_pre_op);
-  m.def("bn_backward_part(Tensor dy, Tensor x, Tensor mean, Tensor rstd, Tensor gamma, Tensor(a!) dx, Tensor(b!)? dgamma, Tensor(c!)? dbeta, Tensor part, int nblk) -> ()", &bn_backward_part_op);
   m.def("conv_wgrad(Tensor dy, Tensor x, Tensor(a!) dw, int stride, int pad, int dil, int mode) -> ()", &conv_wgrad_op);
-  m.def("bn_forward(Tensor x, Tensor? res, Tensor(a!) y, Tensor gamma, Tensor beta, Tensor(b!)? run_mean, Tensor(c!)? run_var, Tensor(d!) save_mean, Tensor(e!) save_rstd, float eps, float momentum, bool relu, Tensor? part=None, int nblk=0) -> ()", &bn_forward_op);
-  m.def("bn_backward(Tensor dy, Tensor? y, Tensor x, Tensor mean, Tensor rstd, Tensor gamma, Tensor(a!) dx, Tensor(b!)? dres, Tensor(c!)? dgamma, Tensor(d!)? dbeta, bool relu, Tensor? addend=None) -> ()", &bn_backward_op);
+  m.def("bn_forward(Tensor x, Tensor? res, Tensor(a!) y, Tensor gamma, Tensor beta, Tensor(b!)? run_mean, Tensor(c!)? run_var, Tensor(d!) save_mean, Tensor(e!) save_rstd, float eps, float momentum, bool relu, Tensor(f!)? sums=None, bool sums_ready=False) -> ()", &bn_forward_op);
+  m.def("bn_backward(Tensor dy, Tensor? y, Tensor x, Tensor mean, Tensor rstd, Tensor gamma, Tensor(a!) dx, Tensor(b!)? dres, Tensor(c!)? dgamma, Tensor(d!)? dbeta, bool relu, Tensor? addend=None, Tensor(e!)? sums=None, bool sums_ready=False) -> ()", &bn_backward_op);
   m.def("ln_forward(Tensor x, Tensor g, Tensor b, Tensor(a!) y, Tensor(b!) mean, Tensor(c!) rstd, float eps) -> ()", &ln_forward_op);
   m.def("ln_backward(Tensor dy, Tensor x, Tensor g, Tensor mean, Tensor rstd, Tensor(a!) dx, Tensor(b!) dg, Tensor(c!) db, Tensor? addend=None) -> ()", &ln_backward_op);
   m.def("maxpool_forward(Tensor x, Tensor(a!) y, Tensor(b!) idx, int R, int S, int stride, int pad) -> ()", &maxpool_forward_op);
@@ -853,6 +860,8 @@ TORCH_LIBRARY(tam, m) {
   m.def("gemm4w(Tensor a, Tensor b, Tensor(a!) c, int pipe=1) -> bool", &gemm4w_op);
   m.def("gemm_lib_policy(int policy) -> ()", &gemm_lib_policy_op);
   m.def("conv_dma_policy(int policy) -> ()", &conv_dma_policy_op);
+  m.def("conv_wgrad_force(int bm, int bn, int splits, int noatomic=0) -> ()", &conv_wgrad_force_op);
+  m.def("conv_halo_policy(int policy) -> ()", &conv_halo_policy_op);
   m.def("gemm_dma_policy(int policy, int cfg) -> ()", &gemm_dma_policy_op);
   m.def("gemm_routes() -> str", &gemm_routes_op);
   m.def("relu_backward(Tensor dy, Tensor y, Tensor(a!) dx) -> ()", &relu_backward_op);

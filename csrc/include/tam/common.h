@@ -17,6 +17,10 @@ typedef float f32x16_t __attribute__((ext_vector_type(16)));
 
 constexpr int kWave = 64;
 
+// shards of a BatchNorm statistics accumulator (fp64 [BN_SHARDS][2C], see
+// norm.hip "BN sums"): conv epilogues spread their atomics over them
+constexpr int BN_SHARDS = 16;
+
 __device__ __forceinline__ float bf2f(bf16_t v) {
   return __uint_as_float(((uint32_t)v) << 16);
 }

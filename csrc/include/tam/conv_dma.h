@@ -74,8 +74,179 @@ __device__ __forceinline__ void cd_barrier() {
   asm volatile("" ::: "memory");
 }
 
-template <int BN, int WN, int BM = 256>
-__global__ void __launch_bounds__(BM / 64 * 64 * WN, 1) conv_dma_kernel(CDArgs a, Epi ep) {
+// Epilogue of the conv cores over one BM x BN accumulator tile (waves WM (M)
+// x WN, each 4 x TN blocks of 16x16 MFMA outputs): bias / ReLU / ReLU-backward
+// mask / accumulate, bf16 (LDS-staged 16-B row chunks) or fp32 stores, and the
+// BatchNorm sums (Epi::stats, Epi::bnx) added into statistics shard `shard`.
+// rmap(tile-local row) -> output row, or -1 for a row that is not stored;
+// Ng = output columns; smem = the kernel's (free) staging LDS.
+template <int BN, int WN, int BM, class RowMap>
+__device__ __forceinline__ void cd_epilogue(f32x4_t (&acc)[4][BN / WN / 16], const Epi& ep, char* smem,
+                                            const int n0, const int Ng, const int shard, RowMap rmap) {
+  constexpr int WM = BM / 64;
+  constexpr int W = WM * WN;
+  constexpr int WCOLS = BN / WN;
+  constexpr int TN = WCOLS / 16, TM = 4;
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int wm = wid % WM, wn = wid / WM;
+  const bool add_bias = ep.bias != nullptr;
+  if (!ep.c_f32) {
+    // ---- LDS-staged bf16 epilogue: each wave parks 32 rows of its tile in a
+    // private padded LDS slab (the stage buffers are free after the barrier),
+    // then writes whole 16-B row chunks (and reads the relu mask / the
+    // accumulate operand in the same 16-B units) instead of 2-B scattered
+    // stores from the MFMA C layout.
+    constexpr int LDW = WCOLS + 8;                 // padded slab row (bf16)
+    constexpr int CPR = WCOLS / 8, NCH = 32 * CPR / 64;
+    static_assert(64 % CPR == 0, "a lane keeps one 8-channel chunk");
+    bf16_t* slab = (bf16_t*)(smem + wid * (32 * LDW * 2));
+    // BN statistics of the stored tile (ep.stats): each lane owns channel
+    // chunk lane % CPR for every row it stores
+    const bool stats = ep.stats != nullptr;
+    const bool bnb = stats && ep.bnx != nullptr;   // BN-backward sums (see Epi::bnx)
+    float ssum[8], ssq[8], bmu[8], brs[8];
+#pragma unroll
+    for (int e = 0; e < 8; ++e) ssum[e] = ssq[e] = bmu[e] = brs[e] = 0.f;
+    if (bnb) {
+      // a lane keeps one 8-channel chunk for every row it stores
+      const int c0 = n0 + wn * WCOLS + (lane % CPR) * 8;
+#pragma unroll
+      for (int e = 0; e < 8; ++e) { bmu[e] = ep.bnmean[c0 + e]; brs[e] = ep.bnrstd[c0 + e]; }
+    }
+    float bv[TN];
+#pragma unroll
+    for (int j = 0; j < TN; ++j)
+      bv[j] = add_bias ? bf2f(ep.bias[n0 + wn * WCOLS + 16 * j + (lane & 15)]) : 0.f;
+    cd_barrier();                                  // every wave is done with the stages
+    const int cbase = n0 + wn * WCOLS;
+#pragma unroll
+    for (int half = 0; half < 2; ++half) {
+#pragma unroll
+      for (int ii = 0; ii < 2; ++ii) {
+        const int i = 2 * half + ii;
+#pragma unroll
+        for (int j = 0; j < TN; ++j)
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            float v = acc[i][j][r] * ep.alpha + bv[j];
+            if (ep.relu) v = fmaxf(v, 0.f);
+            slab[(16 * ii + 4 * (lane >> 4) + r) * LDW + 16 * j + (lane & 15)] = f2bf(v);
+          }
+      }
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+#pragma unroll
+      for (int u = 0; u < NCH; ++u) {
+        const int idx = u * 64 + lane, lr = idx / CPR, ch = idx % CPR;
+        const long orow = rmap(wm * 64 + half * 32 + lr);
+        if (orow >= 0) {
+          uint4 v = *(const uint4*)(slab + lr * LDW + ch * 8);
+          if (ep.mask) {
+            const uint4 mk = *(const uint4*)(ep.mask + orow * ep.ldm + cbase + ch * 8);
+            const uint32_t* mw = (const uint32_t*)&mk;
+            uint32_t* vw = (uint32_t*)&v;
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+              const uint32_t m2 = mw[e];
+              const bool lo = (m2 & 0x8000u) == 0 && (m2 & 0x7fffu) != 0;
+              const bool hi = (m2 & 0x80000000u) == 0 && (m2 & 0x7fff0000u) != 0;
+              vw[e] &= (lo ? 0x0000ffffu : 0u) | (hi ? 0xffff0000u : 0u);
+            }
+          }
+          bf16_t* dst = (bf16_t*)ep.c + orow * ep.ldc + cbase + ch * 8;
+          if (ep.mode == 1) {
+            const uint4 o = *(const uint4*)dst;
+            const uint32_t* ow = (const uint32_t*)&o;
+            uint32_t* vw = (uint32_t*)&v;
+#pragma unroll
+            for (int e = 0; e < 4; ++e)
+              vw[e] = pack_bf2(bf2f((bf16_t)(vw[e] & 0xffff)) + bf2f((bf16_t)(ow[e] & 0xffff)),
+                               bf2f((bf16_t)(vw[e] >> 16)) + bf2f((bf16_t)(ow[e] >> 16)));
+          }
+          *(uint4*)dst = v;
+          if (bnb) {
+            const uint4 xv = *(const uint4*)(ep.bnx + orow * ep.ldc + cbase + ch * 8);
+            const uint32_t* vw = (const uint32_t*)&v;
+            const uint32_t* xw = (const uint32_t*)&xv;
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+              const float lo = bf2f((bf16_t)(vw[e] & 0xffff)), hi = bf2f((bf16_t)(vw[e] >> 16));
+              const float xl = bf2f((bf16_t)(xw[e] & 0xffff)), xh = bf2f((bf16_t)(xw[e] >> 16));
+              ssum[2 * e] += lo; ssq[2 * e] += lo * (xl - bmu[2 * e]) * brs[2 * e];
+              ssum[2 * e + 1] += hi; ssq[2 * e + 1] += hi * (xh - bmu[2 * e + 1]) * brs[2 * e + 1];
+            }
+          } else if (stats) {
+            const uint32_t* vw = (const uint32_t*)&v;
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+              const float lo = bf2f((bf16_t)(vw[e] & 0xffff)), hi = bf2f((bf16_t)(vw[e] >> 16));
+              ssum[2 * e] += lo; ssq[2 * e] += lo * lo;
+              ssum[2 * e + 1] += hi; ssq[2 * e + 1] += hi * hi;
+            }
+          }
+        }
+      }
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    }
+    if (stats) {
+      // lanes sharing a chunk -> the wave's 64 rows; then the WM waves of
+      // one column slice in LDS (past the slabs), one fp64 atomic add per
+      // channel per M-tile
+#pragma unroll
+      for (int o = CPR; o < 64; o <<= 1)
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+          ssum[e] += __shfl_xor(ssum[e], o, 64);
+          ssq[e] += __shfl_xor(ssq[e], o, 64);
+        }
+      float* red = (float*)(smem + W * 32 * LDW * 2);      // [W][2 * WCOLS]
+      if (lane < CPR) {
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+          red[wid * 2 * WCOLS + lane * 8 + e] = ssum[e];
+          red[wid * 2 * WCOLS + WCOLS + lane * 8 + e] = ssq[e];
+        }
+      }
+      __syncthreads();
+      if (wm == 0) {
+        for (int e = lane; e < 2 * WCOLS; e += 64) {
+          float t = 0.f;
+#pragma unroll
+          for (int k = 0; k < WM; ++k) t += red[(k + WM * wn) * 2 * WCOLS + e];
+          unsafeAtomicAdd(ep.stats + (long)shard * 2 * Ng + (e < WCOLS ? cbase + e : Ng + cbase + (e - WCOLS)),
+                          (double)t);
+        }
+      }
+    }
+    return;
+  }
+
+  // ---- fp32 output: C/D map of 16x16x32: col = lane&15, row = (lane>>4)*4 + r
+#pragma unroll
+  for (int j = 0; j < TN; ++j) {
+    const int col = n0 + wn * WCOLS + 16 * j + (lane & 15);
+    if (col >= Ng) continue;
+    const float bv = add_bias ? bf2f(ep.bias[col]) : 0.f;
+#pragma unroll
+    for (int i = 0; i < TM; ++i) {
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const long orow = rmap(wm * 64 + 16 * i + 4 * (lane >> 4) + r);
+        if (orow < 0) continue;
+        float v = acc[i][j][r] * ep.alpha + bv;
+        if (ep.relu) v = fmaxf(v, 0.f);
+        if (ep.mask && bf2f(ep.mask[orow * ep.ldm + col]) <= 0.f) v = 0.f;
+        float* c = (float*)ep.c + orow * ep.ldc + col;
+        if (ep.mode == 1) *c += v;
+        else *c = v;
+      }
+    }
+  }
+}
+
+// one block's tile of one pass; bid = the block's (XCD-remapped) index within
+// the pass's tile grid
+template <int BN, int WN, int BM>
+__device__ __forceinline__ void conv_dma_body(const CDArgs& a, const Epi& ep, const int bid) {
   constexpr int WM = BM / 64;             // waves along M (64 rows each)
   constexpr int W = WM * WN;              // waves
   constexpr int BK = 64;
@@ -92,7 +263,6 @@ __global__ void __launch_bounds__(BM / 64 * 64 * WN, 1) conv_dma_kernel(CDArgs a
   const int wm = wid % WM, wn = wid / WM;
 
   const int tiles_m = (a.M + BM - 1) / BM, tiles_n = (a.Ng + BN - 1) / BN;
-  const int bid = xcd_remap(blockIdx.x, gridDim.x);
   constexpr int GROUP = 8;
   const int per_group = GROUP * tiles_n;
   const int grp = bid / per_group;
@@ -201,160 +371,184 @@ __global__ void __launch_bounds__(BM / 64 * 64 * WN, 1) conv_dma_kernel(CDArgs a
     }
   }
 
-  const bool add_bias = ep.bias != nullptr;
-  if (!ep.c_f32) {
-    // ---- LDS-staged bf16 epilogue: each wave parks 32 rows of its tile in a
-    // private padded LDS slab (the stage buffers are free after the barrier),
-    // then writes whole 16-B row chunks (and reads the relu mask / the
-    // accumulate operand in the same 16-B units) instead of 2-B scattered
-    // stores from the MFMA C layout.
-    constexpr int LDW = WCOLS + 8;                 // padded slab row (bf16)
-    constexpr int CPR = WCOLS / 8, NCH = 32 * CPR / 64;
-    static_assert(64 % CPR == 0, "a lane keeps one 8-channel chunk");
-    bf16_t* slab = (bf16_t*)(smem + wid * (32 * LDW * 2));
-    // BN statistics of the stored tile (ep.stats): each lane owns channel
-    // chunk lane % CPR for every row it stores
-    const bool stats = ep.stats != nullptr;
-    const bool bnb = stats && ep.bnx != nullptr;   // BN-backward sums (see Epi::bnx)
-    float ssum[8], ssq[8], bmu[8], brs[8];
-#pragma unroll
-    for (int e = 0; e < 8; ++e) ssum[e] = ssq[e] = bmu[e] = brs[e] = 0.f;
-    if (bnb) {
-      // a lane keeps one 8-channel chunk for every row it stores
-      const int c0 = n0 + wn * WCOLS + (lane % CPR) * 8;
-#pragma unroll
-      for (int e = 0; e < 8; ++e) { bmu[e] = ep.bnmean[c0 + e]; brs[e] = ep.bnrstd[c0 + e]; }
-    }
-    float bv[TN];
-#pragma unroll
-    for (int j = 0; j < TN; ++j)
-      bv[j] = add_bias ? bf2f(ep.bias[n0 + wn * WCOLS + 16 * j + (lane & 15)]) : 0.f;
-    cd_barrier();                                  // every wave is done with the stages
-    const int cbase = n0 + wn * WCOLS;
-#pragma unroll
-    for (int half = 0; half < 2; ++half) {
-#pragma unroll
-      for (int ii = 0; ii < 2; ++ii) {
-        const int i = 2 * half + ii;
-#pragma unroll
-        for (int j = 0; j < TN; ++j)
-#pragma unroll
-          for (int r = 0; r < 4; ++r) {
-            float v = acc[i][j][r] * ep.alpha + bv[j];
-            if (ep.relu) v = fmaxf(v, 0.f);
-            slab[(16 * ii + 4 * (lane >> 4) + r) * LDW + 16 * j + (lane & 15)] = f2bf(v);
-          }
-      }
-      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-#pragma unroll
-      for (int u = 0; u < NCH; ++u) {
-        const int idx = u * 64 + lane, lr = idx / CPR, ch = idx % CPR;
-        const int row = m0 + wm * 64 + half * 32 + lr;
-        if (row < a.M) {
-          const long orow = cd_out_row(a, row);
-          uint4 v = *(const uint4*)(slab + lr * LDW + ch * 8);
-          if (ep.mask) {
-            const uint4 mk = *(const uint4*)(ep.mask + orow * ep.ldm + cbase + ch * 8);
-            const uint32_t* mw = (const uint32_t*)&mk;
-            uint32_t* vw = (uint32_t*)&v;
-#pragma unroll
-            for (int e = 0; e < 4; ++e) {
-              const uint32_t m2 = mw[e];
-              const bool lo = (m2 & 0x8000u) == 0 && (m2 & 0x7fffu) != 0;
-              const bool hi = (m2 & 0x80000000u) == 0 && (m2 & 0x7fff0000u) != 0;
-              vw[e] &= (lo ? 0x0000ffffu : 0u) | (hi ? 0xffff0000u : 0u);
-            }
-          }
-          bf16_t* dst = (bf16_t*)ep.c + orow * ep.ldc + cbase + ch * 8;
-          if (ep.mode == 1) {
-            const uint4 o = *(const uint4*)dst;
-            const uint32_t* ow = (const uint32_t*)&o;
-            uint32_t* vw = (uint32_t*)&v;
-#pragma unroll
-            for (int e = 0; e < 4; ++e)
-              vw[e] = pack_bf2(bf2f((bf16_t)(vw[e] & 0xffff)) + bf2f((bf16_t)(ow[e] & 0xffff)),
-                               bf2f((bf16_t)(vw[e] >> 16)) + bf2f((bf16_t)(ow[e] >> 16)));
-          }
-          *(uint4*)dst = v;
-          if (bnb) {
-            const uint4 xv = *(const uint4*)(ep.bnx + orow * ep.ldc + cbase + ch * 8);
-            const uint32_t* vw = (const uint32_t*)&v;
-            const uint32_t* xw = (const uint32_t*)&xv;
-#pragma unroll
-            for (int e = 0; e < 4; ++e) {
-              const float lo = bf2f((bf16_t)(vw[e] & 0xffff)), hi = bf2f((bf16_t)(vw[e] >> 16));
-              const float xl = bf2f((bf16_t)(xw[e] & 0xffff)), xh = bf2f((bf16_t)(xw[e] >> 16));
-              ssum[2 * e] += lo; ssq[2 * e] += lo * (xl - bmu[2 * e]) * brs[2 * e];
-              ssum[2 * e + 1] += hi; ssq[2 * e + 1] += hi * (xh - bmu[2 * e + 1]) * brs[2 * e + 1];
-            }
-          } else if (stats) {
-            const uint32_t* vw = (const uint32_t*)&v;
-#pragma unroll
-            for (int e = 0; e < 4; ++e) {
-              const float lo = bf2f((bf16_t)(vw[e] & 0xffff)), hi = bf2f((bf16_t)(vw[e] >> 16));
-              ssum[2 * e] += lo; ssq[2 * e] += lo * lo;
-              ssum[2 * e + 1] += hi; ssq[2 * e + 1] += hi * hi;
-            }
-          }
-        }
-      }
-      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    }
-    if (stats) {
-      // lanes sharing a chunk -> the wave's 64 rows; then the WM waves of
-      // one column slice in LDS (past the slabs), one partial row per M-tile
-#pragma unroll
-      for (int o = CPR; o < 64; o <<= 1)
-#pragma unroll
-        for (int e = 0; e < 8; ++e) {
-          ssum[e] += __shfl_xor(ssum[e], o, 64);
-          ssq[e] += __shfl_xor(ssq[e], o, 64);
-        }
-      float* red = (float*)(smem + W * 32 * LDW * 2);      // [W][2 * WCOLS]
-      if (lane < CPR) {
-#pragma unroll
-        for (int e = 0; e < 8; ++e) {
-          red[wid * 2 * WCOLS + lane * 8 + e] = ssum[e];
-          red[wid * 2 * WCOLS + WCOLS + lane * 8 + e] = ssq[e];
-        }
-      }
-      __syncthreads();
-      if (wm == 0) {
-        float* prow = ep.stats + (long)tm * 2 * a.Ng;
-        for (int e = lane; e < 2 * WCOLS; e += 64) {
-          float t = 0.f;
-#pragma unroll
-          for (int k = 0; k < WM; ++k) t += red[(k + WM * wn) * 2 * WCOLS + e];
-          if (e < WCOLS) prow[cbase + e] = t;
-          else prow[a.Ng + cbase + (e - WCOLS)] = t;
-        }
-      }
-    }
-    return;
-  }
+  cd_epilogue<BN, WN, BM>(acc, ep, smem, n0, a.Ng, tm % BN_SHARDS, [&](int lr) -> long {
+    const int row = m0 + lr;
+    return row < a.M ? cd_out_row(a, row) : -1L;
+  });
+}
 
-  // ---- fp32 output: C/D map of 16x16x32: col = lane&15, row = (lane>>4)*4 + r
+template <int BN, int WN, int BM = 256>
+__global__ void __launch_bounds__(BM / 64 * 64 * WN, 1) conv_dma_kernel(CDArgs a, Epi ep) {
+  conv_dma_body<BN, WN, BM>(a, ep, xcd_remap(blockIdx.x, gridDim.x));
+}
+
+// Several independent passes sharing one epilogue in ONE launch: the parity
+// classes of a strided dgrad (each a stride-1 sub-convolution over a quarter
+// of the dX pixels, 1-4 taps). Launched separately each class is a grid of
+// tens of blocks on 256 CUs (ResNet-50's 7x7 / 14x14 stages); together they
+// fill the chip. Pass c owns blocks [t0[c], t0[c+1]) after the XCD remap.
+constexpr int CD_MULTI = 4;
+struct CDMulti {
+  CDArgs a[CD_MULTI];
+  int t0[CD_MULTI + 1];
+  int n;
+};
+
+template <int BN, int WN, int BM = 256>
+__global__ void __launch_bounds__(BM / 64 * 64 * WN, 1) conv_dma_multi_kernel(CDMulti m, Epi ep) {
+  const int bid = xcd_remap(blockIdx.x, gridDim.x);
+  int c = 0;
+  while (c + 1 < m.n && bid >= m.t0[c + 1]) ++c;
+  conv_dma_body<BN, WN, BM>(m.a[c], ep, bid - m.t0[c]);
+}
+
+// ===========================================================================
+// Halo-tile conv for 64-channel 3x3 stride-1 passes (fwd over X, stride-1
+// dgrad over dY): ResNet-50's 56x56 stage, VGG-16's 224x224 / 112x112 layers.
+//
+// The LDS-DMA core above gathers A per tap, so a 3x3 pass with C = 64 reads
+// its source 9 times through L2 (measured ~5-6 TB/s of tap re-reads: the
+// pass is bound by them, 57-300 TF/s). Here a block owns a 4 x 56 output
+// tile (224 rows of the GEMM, 4 waves of 64 rows, 32 masked) and 64 output
+// channels; its source PATCH -- 6 x 58 pixels x 64 channels incl. the halo
+// and zero padding -- is staged ONCE by LDS-DMA (44 KiB, XOR-swizzled by
+// patch pixel as the K-major tile image), and every tap's A fragment is read
+// from the patch at a per-lane shifted pixel. B (64 x 64 weights of a tap,
+// 8 KiB) streams through a 3-slot ring, tap t+2 issued while tap t computes.
+// 68 KiB of LDS: two blocks per CU, one's patch load under the other's MFMAs.
+// The epilogue is the conv cores' (bias / ReLU / mask / BN sums).
+// ===========================================================================
+constexpr int CH_TR = 4, CH_TQ = 56;                 // output tile
+constexpr int CH_PR = CH_TR + 2, CH_PW = CH_TQ + 2;  // source patch
+constexpr int CH_NP = CH_PR * CH_PW;                 // 348 pixels
+constexpr int CH_GROUPS = (CH_NP + 7) / 8;           // 1-KiB DMA groups (44)
+constexpr int CH_PATCH = CH_GROUPS * 1024;
+constexpr int CH_BSLOT = 64 * 64 * 2;
+
+struct CHArgs {
+  const bf16_t* src;   // [N][P][Q][64]
+  const bf16_t* wgt;   // B rows [Ng][ldb]: a tap's 64 k at column tap_kcol[t]
+  long ldb;
+  int N, P, Q, Ng;     // output grid == source grid (3x3, stride 1, "same")
+  int tap_oh[9], tap_ow[9], tap_kcol[9];   // patch offsets in [0, 2]
+};
+
+__global__ void __launch_bounds__(256, 2) conv_halo_kernel(CHArgs a, Epi ep) {
+  __shared__ __attribute__((aligned(1024))) char smem[CH_PATCH + 3 * CH_BSLOT];
+  char* sp = smem;
+  char* sb = smem + CH_PATCH;
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  // tile (n, p0, q0) x column block tn; tn innermost so both column blocks
+  // of a patch run together (the second patch read hits L2)
+  const int tiles_n = a.Ng / 64, tq = a.Q / CH_TQ, tp = a.P / CH_TR;
+  const int bid = xcd_remap(blockIdx.x, gridDim.x);
+  const int tn = bid % tiles_n;
+  const int sidx = bid / tiles_n;                 // spatial tile
+  const int q0 = (sidx % tq) * CH_TQ;
+  const int p0 = ((sidx / tq) % tp) * CH_TR;
+  const int n = sidx / (tq * tp);
+  const int n0 = tn * 64;
+
+  // ---- patch: group g = wid + 4j holds patch pixels 8g .. 8g+7
 #pragma unroll
-  for (int j = 0; j < TN; ++j) {
-    const int col = n0 + wn * WCOLS + 16 * j + (lane & 15);
-    if (col >= a.Ng) continue;
-    const float bv = add_bias ? bf2f(ep.bias[col]) : 0.f;
-#pragma unroll
-    for (int i = 0; i < TM; ++i) {
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const int row = m0 + wm * 64 + 16 * i + 4 * (lane >> 4) + r;
-        if (row >= a.M) continue;
-        const long orow = cd_out_row(a, row);
-        float v = acc[i][j][r] * ep.alpha + bv;
-        if (ep.relu) v = fmaxf(v, 0.f);
-        if (ep.mask && bf2f(ep.mask[orow * ep.ldm + col]) <= 0.f) v = 0.f;
-        float* c = (float*)ep.c + orow * ep.ldc + col;
-        if (ep.mode == 1) *c += v;
-        else *c = v;
-      }
+  for (int j = 0; j < (CH_GROUPS + 3) / 4; ++j) {
+    const int g = wid + 4 * j;
+    if (g < CH_GROUPS) {
+      const int i = 8 * g + (lane >> 3);
+      const int pr = i / CH_PW, pc = i % CH_PW;
+      const int h = p0 - 1 + pr, w = q0 - 1 + pc;
+      const int c = (lane & 7) ^ ((i >> 1) & 7);
+      const bool ok = i < CH_NP && (unsigned)h < (unsigned)a.P && (unsigned)w < (unsigned)a.Q;
+      const bf16_t* src = ok ? a.src + (((long)n * a.P + h) * a.Q + w) * 64 + c * 8 : g_cd_zero + c * 8;
+      __builtin_amdgcn_global_load_lds((const void*)src, (cd_lds_void_t*)(sp + g * 1024), 16, 0, 0);
     }
   }
+  // ---- B ring: tap t -> slot t % 3; rows rr = (wid + 4j)*8 + lane/8
+  const bf16_t* brow[2];
+#pragma unroll
+  for (int j = 0; j < 2; ++j) {
+    const int rr = (wid + 4 * j) * 8 + (lane >> 3);
+    const int c = (lane & 7) ^ ((rr >> 1) & 7);
+    brow[j] = a.wgt + (long)(n0 + rr) * a.ldb + c * 8;
+  }
+  auto issue_b = [&](int t) {
+    char* dst = sb + (t % 3) * CH_BSLOT;
+#pragma unroll
+    for (int j = 0; j < 2; ++j)
+      __builtin_amdgcn_global_load_lds((const void*)(brow[j] + a.tap_kcol[t]),
+                                       (cd_lds_void_t*)(dst + (wid + 4 * j) * 1024), 16, 0, 0);
+  };
+  issue_b(0);
+  issue_b(1);
+
+  // ---- per-lane patch pixel of each A fragment row (center-less origin)
+  int base[4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    int m = wid * 64 + 16 * i + (lane & 15);
+    m = m < CH_TR * CH_TQ ? m : 0;                // masked rows: any valid pixel
+    base[i] = (m / CH_TQ) * CH_PW + (m % CH_TQ);
+  }
+  f32x4_t acc[4][4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+
+  for (int t = 0; t < 9; ++t) {
+    // retire the patch and B(t); B(t+1) stays in flight
+    if (t + 1 < 9) cd_vm_wait<2>();
+    else cd_vm_wait<0>();
+    cd_barrier();
+    if (t + 2 < 9) issue_b(t + 2);                // slot (t+2)%3 was last read at tap t-1
+    const char* tb = sb + (t % 3) * CH_BSLOT;
+    const int toff = a.tap_oh[t] * CH_PW + a.tap_ow[t];
+#pragma unroll
+    for (int kk = 0; kk < 2; ++kk) {
+      s16x8_t fa[4], fb[4];
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+        fa[i] = *(const s16x8_t*)(sp + kmaj_off(base[i] + toff, 4 * kk + (lane >> 4)));
+#pragma unroll
+      for (int j = 0; j < 4; ++j) fb[j] = read_frag_k(tb, lane, 16 * j, kk);
+      __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(
+              __builtin_bit_cast(bf16x8_t, fa[i]), __builtin_bit_cast(bf16x8_t, fb[j]), acc[i][j], 0, 0, 0);
+      __builtin_amdgcn_s_setprio(0);
+    }
+  }
+  const long rowbase = ((long)n * a.P + p0) * a.Q + q0;
+  cd_epilogue<64, 1, 256>(acc, ep, smem, n0, a.Ng, sidx % BN_SHARDS, [&](int lr) -> long {
+    if (lr >= CH_TR * CH_TQ) return -1L;
+    return rowbase + (long)(lr / CH_TQ) * a.Q + (lr % CH_TQ);
+  });
+}
+
+// 3x3 stride-1 "same" pass over a 64-channel source (fwd: CDArgs of
+// cd_fwd_args; stride-1 dgrad: cd_dgrad_args) -> halo launch; false if the
+// shape is not for this kernel
+inline bool launch_conv_halo(const CDArgs& c, const Epi& ep, hipStream_t s) {
+  if (c.Cs != 64 || c.ntaps != 9 || c.stride != 1 || c.omap || c.Ng % 64 != 0) return false;
+  if (c.P != c.Hs || c.Q != c.Ws || c.P % CH_TR != 0 || c.Q % CH_TQ != 0) return false;
+  const int N = c.M / (c.P * c.Q);
+  if ((long)N * c.P * c.Q != c.M || (long)c.M * 64 >= (1L << 31) || (long)c.Ng * c.ldb >= (1L << 31))
+    return false;
+  CHArgs a{};
+  a.src = c.src; a.wgt = c.wgt; a.ldb = c.ldb;
+  a.N = N; a.P = c.P; a.Q = c.Q; a.Ng = c.Ng;
+  for (int t = 0; t < 9; ++t) {
+    a.tap_oh[t] = c.base_h + c.tap_dh[t] + 1;
+    a.tap_ow[t] = c.base_w + c.tap_dw[t] + 1;
+    a.tap_kcol[t] = c.tap_kcol[t];
+    if (a.tap_oh[t] < 0 || a.tap_oh[t] > 2 || a.tap_ow[t] < 0 || a.tap_ow[t] > 2) return false;
+  }
+  const long blocks = (long)N * (c.P / CH_TR) * (c.Q / CH_TQ) * (c.Ng / 64);
+  hipLaunchKernelGGL(conv_halo_kernel, dim3((unsigned)blocks), dim3(256), 0, s, a, ep);
+  return true;
 }
 
 // Host-side eligibility + launch. Returns false when the shape is not for
@@ -381,8 +575,7 @@ inline int conv_dma_pick_bn(int M, int Ng, int Kd, int force) {
   return pick;
 }
 
-// returns 0 (not for this core) or the tile height BM of the launch (the
-// number of BN-statistics partial rows is ceil(M / BM))
+// returns 0 (not for this core) or the tile height BM of the launch
 inline int launch_conv_dma(const CDArgs& a, const Epi& ep, hipStream_t s, int force = 0) {
   // Kd >= 256: with fewer than 4 K-tiles the ring never fills (1x1 convs over
   // 64/128 channels measured slower than the igemm) — unless forced (tests,
@@ -412,6 +605,45 @@ inline int launch_conv_dma(const CDArgs& a, const Epi& ep, hipStream_t s, int fo
       break;
   }
   return 256;
+}
+
+// One launch over the passes a[0..n) (same Ng, Cs % 64 == 0, 1 <= ntaps <= 9
+// each; the caller checked them): tile by the cost model over the SUM of the
+// passes' tiles. Returns false if no tile fits.
+inline bool launch_conv_dma_multi(const CDArgs* a, int n, const Epi& ep, hipStream_t s) {
+  if (n < 1 || n > CD_MULTI) return false;
+  const int Ng = a[0].Ng;
+  for (int i = 0; i < n; ++i)
+    if (a[i].Ng != Ng || a[i].Cs % 64 || a[i].Kd % 64 || a[i].ntaps < 1 || a[i].ntaps > 9) return false;
+  struct Cand { int bm, bn; double eff; };
+  const Cand cands[3] = {{256, 256, 1.0}, {256, 128, 0.92}, {128, 128, 0.8}};
+  int pick = -1;
+  double best = 1e30;
+  for (int k = 0; k < 3; ++k) {
+    if (Ng % cands[k].bn) continue;
+    long tiles = 0;
+    for (int i = 0; i < n; ++i) tiles += (long)((a[i].M + cands[k].bm - 1) / cands[k].bm) * (Ng / cands[k].bn);
+    const double cost = (double)((tiles + 255) / 256) * cands[k].bm * cands[k].bn / cands[k].eff;
+    if (cost < best) { best = cost; pick = k; }
+  }
+  if (pick < 0) return false;
+  CDMulti m{};
+  m.n = n;
+  int t = 0;
+  for (int i = 0; i < n; ++i) {
+    m.a[i] = a[i];
+    m.t0[i] = t;
+    t += ((a[i].M + cands[pick].bm - 1) / cands[pick].bm) * (Ng / cands[pick].bn);
+  }
+  m.t0[n] = t;
+  for (int i = n + 1; i <= CD_MULTI; ++i) m.t0[i] = t;
+  if (pick == 0)
+    hipLaunchKernelGGL((conv_dma_multi_kernel<256, 2>), dim3(t), dim3(512), 0, s, m, ep);
+  else if (pick == 1)
+    hipLaunchKernelGGL((conv_dma_multi_kernel<128, 2>), dim3(t), dim3(512), 0, s, m, ep);
+  else
+    hipLaunchKernelGGL((conv_dma_multi_kernel<128, 2, 128>), dim3(t), dim3(256), 0, s, m, ep);
+  return true;
 }
 
 // argument builders (host)
@@ -653,6 +885,17 @@ __global__ void __launch_bounds__(64 * WM * WN, 1) conv_wgrad_dma_kernel(WGArgs 
   }
 }
 
+// (bm, bn, splits) forced for A/B sweeps (tools/sweep_wgrad.py); 0 = the
+// heuristic below. [3] != 0: TIMING ONLY -- split blocks add with plain
+// (racy) read-modify-writes instead of atomics, to price the atomic traffic
+inline int g_wgrad_force[4] = {0, 0, 0, 0};
+
+template <int BM, int BN, int WM, int WN>
+inline void wgrad_dma_launch(const WGArgs& a, int tiles, int splits, hipStream_t s) {
+  hipLaunchKernelGGL((conv_wgrad_dma_kernel<BM, BN, WM, WN>), dim3(tiles, 1, splits),
+                     dim3(64 * WM * WN), 0, s, a);
+}
+
 // dw += conv wgrad (mode 1 semantics; mode 0 callers zero dw first)
 inline bool launch_conv_wgrad_dma(const bf16_t* dy, const bf16_t* x, float* dw, const ConvGeom& g,
                                   int mode, hipStream_t s, bool force = false) {
@@ -662,32 +905,39 @@ inline bool launch_conv_wgrad_dma(const bf16_t* dy, const bf16_t* x, float* dw, 
   const int ncols = g.R * g.S * g.C;
   // tile: BN divides C (one tap per column tile); BM over K
   int bm, bn;
-  if (g.K % 256 == 0 && g.C % 128 == 0) { bm = 256; bn = 128; }
-  else if (g.K % 128 == 0 && g.C % 128 == 0) { bm = 128; bn = 128; }
-  else { bm = 64; bn = 64; }
-  // the 64x64 form beats the igemm only on 1x1 layers (measured)
-  if (!force && bm == 64 && !(g.R == 1 && g.S == 1)) return false;
+  const int* fw = g_wgrad_force;
+  if (fw[0] > 0) {
+    bm = fw[0]; bn = fw[1];
+    const bool known = (bm == 256 && (bn == 128 || bn == 64)) || (bm == 128 && (bn == 128 || bn == 64)) ||
+                       (bm == 64 && bn == 64);
+    if (!known || g.K % bm != 0 || g.C % bn != 0) return false;
+  } else {
+    if (g.K % 256 == 0 && g.C % 128 == 0) { bm = 256; bn = 128; }
+    else if (g.K % 128 == 0 && g.C % 128 == 0) { bm = 128; bn = 128; }
+    else { bm = 64; bn = 64; }
+    // the 64x64 form beats the igemm only on 1x1 layers (measured)
+    if (!force && bm == 64 && !(g.R == 1 && g.S == 1)) return false;
+  }
   const int tiles = (g.K / bm) * (ncols / bn);
   const int nsteps = (int)((Mred + 63) / 64);
   // split the pixel reduction to ~one block per CU, not more: every split
   // adds |dW| of fp32 atomics (~1.3 TB/s chip-wide), which at 2 blocks/CU
   // already cost as much as the MFMA work on ResNet-sized layers
-  int splits = 256 / tiles;
-  if (splits > nsteps / 8) splits = nsteps / 8;
+  int splits = fw[2] > 0 ? fw[2] : 256 / tiles;
+  if (fw[2] <= 0 && splits > nsteps / 8) splits = nsteps / 8;
+  if (splits > nsteps) splits = nsteps;
   if (splits < 1) splits = 1;
   int sps = (nsteps + splits - 1) / splits;
   splits = (nsteps + sps - 1) / sps;
   if (mode == 0) zero_async(dw, (size_t)g.K * ncols * sizeof(float), s);
   const int PQ = g.P * g.Q;
   WGArgs a{dy, x, dw, ncols, g.K, g.C, g.H, g.W, g.P, g.Q, g.S, g.stride, g.pad, (int)Mred, sps,
-           64 / PQ, (64 % PQ) / g.Q, (64 % PQ) % g.Q, splits > 1 ? 1 : 0};
-  dim3 grid(tiles, 1, splits);
-  if (bm == 256)
-    hipLaunchKernelGGL((conv_wgrad_dma_kernel<256, 128, 4, 2>), grid, dim3(512), 0, s, a);
-  else if (bm == 128)
-    hipLaunchKernelGGL((conv_wgrad_dma_kernel<128, 128, 2, 2>), grid, dim3(256), 0, s, a);
-  else
-    hipLaunchKernelGGL((conv_wgrad_dma_kernel<64, 64, 2, 2>), grid, dim3(256), 0, s, a);
+           64 / PQ, (64 % PQ) / g.Q, (64 % PQ) % g.Q, splits > 1 && !fw[3] ? 1 : 0};
+  if (bm == 256 && bn == 128) wgrad_dma_launch<256, 128, 4, 2>(a, tiles, splits, s);
+  else if (bm == 256) wgrad_dma_launch<256, 64, 4, 1>(a, tiles, splits, s);
+  else if (bm == 128 && bn == 128) wgrad_dma_launch<128, 128, 2, 2>(a, tiles, splits, s);
+  else if (bm == 128) wgrad_dma_launch<128, 64, 2, 2>(a, tiles, splits, s);
+  else wgrad_dma_launch<64, 64, 2, 2>(a, tiles, splits, s);
   return true;
 }
 

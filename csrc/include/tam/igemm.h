@@ -41,12 +41,13 @@ struct Epi {
   long ldm = 0;
   float alpha = 1.f;
   long zstride = 0;
-  // conv_dma bf16 epilogue only: per-channel BatchNorm partial sums of the
-  // stored outputs, one row per M-tile: stats[tm][0..N) = sum, [N..2N) = sum sq
-  float* stats = nullptr;         // mode 3: fp32 slab store at c + blockIdx.z * zstride (split-K slabs)
+  // conv_dma bf16 epilogue only: per-channel BatchNorm sums of the stored
+  // outputs, fp64 [BN_SHARDS][2N] (sum | sum of squares), accumulated with
+  // device-scope atomics into shard (M-tile % BN_SHARDS); the caller zeroes them
+  double* stats = nullptr;
   // conv_dma bf16 epilogue only, with stats: the stored tile is the gradient
   // d of a BatchNorm OUTPUT whose input was bnx (same [rows][N] layout):
-  // the partial sums become sum(d) | sum(d * (bnx - mean) * rstd) -- the
+  // the sums become sum(d) | sum(d * (bnx - mean) * rstd) -- the
   // BN-backward reduction, read from the dgrad epilogue instead of a pass
   const bf16_t* bnx = nullptr;
   const float* bnmean = nullptr;

@@ -7,7 +7,10 @@
 namespace tam {
 
 // BatchNorm (NHWC rows=M=N*H*W, C channels, C % 8 == 0, C <= 2048).
-// Reductions write per-block partial rows (<= BN_MAX_BLOCKS), no atomics.
+// Statistics: fp64 sums[BN_SHARDS][2C] (norm.hip), zeroed by the caller;
+// sums_ready: the producer (a conv epilogue) already accumulated them -- no
+// reduction pass here. part: BN_MAX_BLOCKS * 2C floats of scratch for the
+// reduction pass's partial rows.
 constexpr int BN_MAX_BLOCKS = 512;
 constexpr int LN_MAX_BLOCKS = 512;
 constexpr int COLSUM_MAX_BLOCKS = 256;
@@ -18,8 +21,8 @@ void col_reduce_acc(const float* part, int nblk, int W, float* out0, float* out1
                     hipStream_t s);
 void bn_forward(const bf16_t* x, const bf16_t* res, bf16_t* y, long M, int C, float eps,
                 float momentum, const float* gamma, const float* beta, float* run_mean,
-                float* run_var, float* save_mean, float* save_rstd, float* ws_f, int relu,
-                const float* part_in, int nblk_in, hipStream_t s);
+                float* run_var, float* save_mean, float* save_rstd, int relu, double* sums,
+                int sums_ready, float* part, hipStream_t s);
 void bn_infer(const bf16_t* x, const bf16_t* res, bf16_t* y, long M, int C, const float* scale,
               const float* shift, int relu, hipStream_t s);
 // batched conv weight re-layout [K][RS][C] -> [C][RS][K] (one launch)
@@ -35,13 +38,14 @@ struct WTBatch {
 };
 void conv_weight_t_batch(WTBatch& b, hipStream_t s);
 // addend (optional): a second upstream gradient of y summed into dy on load
-// (the residual branch's, so autograd never materialises the sum)
+// (the residual branch's, so autograd never materialises the sum).
+// sums: fp64 [BN_SHARDS][2C] sum(d) | sum(d*xhat); sums_ready: accumulated
+// by the consumer conv's dgrad epilogue (Epi::bnx, which also applied the
+// ReLU mask)
 void bn_backward(const bf16_t* dy, const bf16_t* addend, const bf16_t* y, const bf16_t* x, const float* mean,
                  const float* rstd, const float* gamma, long M, int C, int relu, bf16_t* dx,
-                 bf16_t* dres, float* dgamma, float* dbeta, float* ws_f, hipStream_t s);
-void bn_backward_part(const bf16_t* dy, const bf16_t* x, const float* mean, const float* rstd,
-                      const float* gamma, long M, int C, bf16_t* dx, float* dgamma, float* dbeta,
-                      const float* part, int nblk, float* ws_f, hipStream_t s);
+                 bf16_t* dres, float* dgamma, float* dbeta, double* sums, int sums_ready, float* part,
+                 hipStream_t s);
 
 // LayerNorm over last dim D (D % 8 == 0, D <= 2048)
 void ln_forward(const bf16_t* x, const float* g, const float* b, bf16_t* y, float* mean,

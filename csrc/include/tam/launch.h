@@ -33,5 +33,8 @@ int conv_dgrad(const bf16_t* dy, const bf16_t* w, const bf16_t* wt, const ConvGe
 void conv_wgrad(const bf16_t* dy, const bf16_t* x, const ConvGeom& g, Epi ep, hipStream_t s);
 void conv_weight_t(const bf16_t* w, bf16_t* wt, const ConvGeom& g, hipStream_t s);
 void conv_dma_policy(int p);   // 1: LDS-DMA core where eligible (default), 0: igemm only
+// LDS-DMA wgrad tile / split (0: heuristic); noatomic: timing-only racy adds
+void conv_wgrad_force(int bm, int bn, int splits, int noatomic = 0);
+void conv_halo_policy(int p);   // 1: 64-channel 3x3 stride-1 passes on the halo-tile kernel (default)
 
 }  // namespace tam

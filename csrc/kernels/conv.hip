@@ -23,6 +23,16 @@ namespace tam {
 // 0: register-staged igemm only (A/B measurements)
 static int g_conv_dma = 1;
 void conv_dma_policy(int p) { g_conv_dma = p; }
+// 64-channel 3x3 stride-1 passes on the halo-tile kernel (conv_dma.h); 0 for
+// A/B runs against the tap-gather cores
+static int g_conv_halo = [] {
+  const char* e = getenv("TAM_CONV_HALO");
+  return e ? atoi(e) : 1;
+}();
+void conv_halo_policy(int p) { g_conv_halo = p; }
+void conv_wgrad_force(int bm, int bn, int splits, int noatomic) {
+  g_wgrad_force[0] = bm; g_wgrad_force[1] = bn; g_wgrad_force[2] = splits; g_wgrad_force[3] = noatomic;
+}
 
 template <int BM, int BN>
 static void fwd_tile(const bf16_t* x, const bf16_t* w, const ConvGeom& g, const Epi& ep, int sp,
@@ -37,14 +47,15 @@ static bool is_pointwise(const ConvGeom& g) {
   return g.R == 1 && g.S == 1 && g.stride == 1 && g.pad == 0;
 }
 
-// returns the number of BN-statistics partial rows written to ep.stats (0:
-// the path taken computes none; the BN then reduces the output itself)
+// returns 1 when the path taken accumulated the BN statistics into ep.stats
+// (0: none; the BN then reduces the output itself)
 int conv_fwd(const bf16_t* x, const bf16_t* w, const ConvGeom& g, Epi ep, hipStream_t s) {
   const int M = g.N * g.P * g.Q, Kd = g.R * g.S * g.C;
   if (g_conv_dma && g.dil == 1) {
     CDArgs a = cd_fwd_args(x, w, g);
+    if (g_conv_halo && launch_conv_halo(a, ep, s)) return ep.stats ? 1 : 0;
     const int bm = launch_conv_dma(a, ep, s, g_conv_dma >= 2 ? g_conv_dma - 1 : 0);
-    if (bm) return ep.stats ? (M + bm - 1) / bm : 0;
+    if (bm) return ep.stats ? 1 : 0;
   }
   ep.stats = nullptr;
   if (is_pointwise(g)) {
@@ -70,8 +81,8 @@ static void dgrad_tile(const bf16_t* dy, const bf16_t* wt, const ConvGeom& g, co
   launch_igemm<BM, BN>(la, lb, M, g.C, Kd, ep, 1, s);
 }
 
-// returns the number of partial rows written to ep.stats (BN-backward sums,
-// Epi::bnx) -- only the single-launch stride-1 LDS-DMA path produces them;
+// returns 1 when the BN-backward sums (Epi::bnx) were accumulated into
+// ep.stats -- only the single-launch stride-1 LDS-DMA path produces them;
 // every other path clears ep.stats and returns 0
 int conv_dgrad(const bf16_t* dy, const bf16_t* w, const bf16_t* wt, const ConvGeom& g, Epi ep,
                hipStream_t s) {
@@ -79,6 +90,7 @@ int conv_dgrad(const bf16_t* dy, const bf16_t* w, const bf16_t* wt, const ConvGe
   if (wt && g_conv_dma && g.dil == 1 && g.stride == 1) {
     // rows = dX pixels over an H x W grid, gathered from dY (P x Q x K), B = Wt [C][R][S][K]
     CDArgs a = cd_dgrad_args(dy, wt, g, 0, 0);
+    if (g_conv_halo && launch_conv_halo(a, ep, s)) return ep.stats ? 1 : 0;
     // 64-channel dX over >= 1M pixels (VGG-16's 224x224 layer): the 64-wide
     // DMA tile beats the igemm although Kd < 1024 (measured 422 -> 364 us);
     // the cost model's 64-column rule is tuned for ResNet's shallower grids
@@ -88,7 +100,7 @@ int conv_dgrad(const bf16_t* dy, const bf16_t* w, const bf16_t* wt, const ConvGe
     }();
     const int force = g_conv_dma >= 2 ? g_conv_dma - 1 : (g.C == 64 && a.M >= dg64_min_m ? 1 : 0);
     const int bm = launch_conv_dma(a, ep, s, force);
-    if (bm) return ep.stats ? (M + bm - 1) / bm : 0;
+    if (bm) return ep.stats ? 1 : 0;
   }
   ep.stats = nullptr;
   ep.bnx = nullptr;
@@ -107,8 +119,14 @@ int conv_dgrad(const bf16_t* dy, const bf16_t* w, const bf16_t* wt, const ConvGe
       }
     if (ok) {
       if (empty) zero_async(ep.c, (size_t)M * g.C * sizeof(bf16_t), s);
+      // every non-empty class in ONE launch (policy 3, tests: one launch per
+      // class on the 128-row tile)
+      CDArgs live[4];
+      int n = 0;
       for (int i = 0; i < g.stride * g.stride; ++i)
-        if (cls[i].ntaps) launch_conv_dma(cls[i], ep, s, g_conv_dma == 3 ? 2 : 1);
+        if (cls[i].ntaps) live[n++] = cls[i];
+      if (g_conv_dma == 3 || !launch_conv_dma_multi(live, n, ep, s))
+        for (int i = 0; i < n; ++i) launch_conv_dma(live[i], ep, s, g_conv_dma == 3 ? 2 : 1);
       return 0;
     }
   }

@@ -1,11 +1,12 @@
 // tiresias_amd — BatchNorm (NHWC, training) and LayerNorm kernels.
 //
 // BatchNorm is split into a stats pass (per-channel sum / sum-of-squares,
-// fp32 per block -> fp64 global atomics so E[x^2]-E[x]^2 does not cancel at
-// N*H*W ~ 10^5) and a fused apply pass (scale/shift + optional residual add +
-// optional ReLU) reading 16 B per lane. Backward mirrors it: one reduction
-// pass producing dgamma/dbeta (and the two row-means the input gradient
-// needs), one fused pass producing dx (and the residual-branch gradient).
+// fp32 per block -> fp64 atomics, skipped when the producing conv's epilogue
+// already accumulated them) and a fused apply pass (per-channel finalize in
+// its prologue, then scale/shift + optional residual add + optional ReLU, 16 B
+// per lane). Backward mirrors it: one reduction pass (or the consumer conv's
+// dgrad epilogue) accumulating sum(d), sum(d*xhat), and one fused pass
+// producing dx (and the residual-branch gradient) plus dgamma/dbeta.
 #include "tam/common.h"
 #include "tam/kernels.h"
 
@@ -71,7 +72,65 @@ void col_reduce_acc(const float* part, int nblk, int W, float* out0, float* out1
                      (double*)nullptr, out0, out1, split);
 }
 
-// ---------------------------------------------------------------- BN stats
+// ---------------------------------------------------------------- BN sums
+// Per-channel statistics live in fp64 sums[BN_SHARDS][2C] (sum | sum of
+// squares, or sum(d) | sum(d*xhat) in backward); a channel's value is the sum
+// over the shards, taken by the consumer's prologue, which derives mean/rstd
+// (or the backward coefficients) itself -- there is no finalize launch.
+//   * conv epilogues (conv_dma.h, Epi::stats) add each M-tile's column sums
+//     with no-return device-scope atomics into shard tm % BN_SHARDS: tiles
+//     finish spread over the conv, and the shards keep the adders per address
+//     low (same-address fp64 atomics serialise at the memory side: 512
+//     simultaneous adders per address measured +85 us on a 13 us pass);
+//   * this file's reduction passes (all blocks finish together) write per-
+//     block partial rows and one column-reduce launch stores shard 0.
+// fp64 keeps E[x^2] - E[x]^2 from cancelling at N*H*W ~ 10^5-10^6. The
+// caller zeroes sums beforehand (one fill per training step for all of a
+// model's BNs).
+
+// sums[0][c] = sum over nblk partial rows part[b][c] (width W = 2C), fp64;
+// 16 columns x 64 row lanes, 4 rows in flight per lane (latency-bound)
+__global__ void __launch_bounds__(1024) bn_col_sums_kernel(const float* __restrict__ part, int nblk,
+                                                           int W, double* __restrict__ sums) {
+  constexpr int RL = 64;
+  __shared__ double red[RL][17];
+  const int cx = threadIdx.x & 15, ly = threadIdx.x >> 4;
+  const int c = blockIdx.x * 16 + cx;
+  double acc = 0.0;
+  if (c < W) {
+    int b = ly;
+    for (; b + 3 * RL < nblk; b += 4 * RL) {
+      float v[4];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) v[u] = part[(long)(b + u * RL) * W + c];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) acc += (double)v[u];
+    }
+    for (; b < nblk; b += RL) acc += (double)part[(long)b * W + c];
+  }
+  red[ly][cx] = acc;
+  __syncthreads();
+  if (ly != 0 || c >= W) return;
+  double t = 0.0;
+#pragma unroll 8
+  for (int k = 0; k < RL; ++k) t += red[k][cx];
+  sums[c] = t;
+}
+
+// a channel's (S, Q) over the shards
+__device__ __forceinline__ void bn_shard_sum(const double* __restrict__ sums, int C, int c, double& S,
+                                             double& Q) {
+  double s[BN_SHARDS], q[BN_SHARDS];
+#pragma unroll
+  for (int k = 0; k < BN_SHARDS; ++k) {
+    s[k] = sums[(long)k * 2 * C + c];
+    q[k] = sums[(long)k * 2 * C + C + c];
+  }
+  S = 0.0; Q = 0.0;
+#pragma unroll
+  for (int k = 0; k < BN_SHARDS; ++k) { S += s[k]; Q += q[k]; }
+}
+
 // grid.x blocks each own a contiguous row range; thread = (row lane, 8-ch group)
 __global__ void __launch_bounds__(256) bn_stats_kernel(const bf16_t* __restrict__ x, long M, int C,
                                                         long rows_per_block,
@@ -125,151 +184,105 @@ __global__ void __launch_bounds__(256) bn_stats_kernel(const bf16_t* __restrict_
   }
 }
 
-// Column reduce of the [nblk][2C] partial rows (fp64) fused with the
-// per-channel finalize: BWD=0 -> mean/rstd, scale/shift, running stats;
-// BWD=1 -> dgamma/dbeta and the k1/k2/k3 coefficients of the apply pass.
-// One launch instead of col_reduce + finalize (each ~5 us of a tiny grid).
-// 1024 threads = 16 columns x 64 row lanes, 4 rows in flight per lane: the
-// pass is latency-bound (one dependent kernel per BN), so more lanes per
-// column, not more columns per block
-template <int BWD>
-__global__ void __launch_bounds__(1024) bn_reduce_finalize_kernel(
-    const float* __restrict__ part, int nblk, long M, int C, float eps, float momentum,
-    const float* __restrict__ gamma, const float* __restrict__ beta_or_rstd,
-    float* __restrict__ o0, float* __restrict__ o1, float* __restrict__ o2,
-    float* __restrict__ o3, float* __restrict__ o4, float* __restrict__ o5) {
-  constexpr int RL = 64;
-  __shared__ double red[2][RL][17];
-  const int cx = threadIdx.x & 15, ly = threadIdx.x >> 4;
-  const int c = blockIdx.x * 16 + cx;
-  const int W = 2 * C;
-  double s = 0.0, q = 0.0;
-  if (c < C) {
-    int b = ly;
-    for (; b + 3 * RL < nblk; b += 4 * RL) {
-      float v[4], w[4];
-#pragma unroll
-      for (int u = 0; u < 4; ++u) {
-        v[u] = part[(long)(b + u * RL) * W + c];
-        w[u] = part[(long)(b + u * RL) * W + C + c];
-      }
-#pragma unroll
-      for (int u = 0; u < 4; ++u) { s += (double)v[u]; q += (double)w[u]; }
-    }
-    for (; b < nblk; b += RL) {
-      s += (double)part[(long)b * W + c];
-      q += (double)part[(long)b * W + C + c];
-    }
-  }
-  red[0][ly][cx] = s;
-  red[1][ly][cx] = q;
-  __syncthreads();
-  if (ly != 0 || c >= C) return;
-  double S = 0.0, Q = 0.0;
-#pragma unroll 8
-  for (int k = 0; k < RL; ++k) { S += red[0][k][cx]; Q += red[1][k][cx]; }
-  if (BWD == 0) {
-    // o0 mean, o1 rstd, o2 scale, o3 shift, o4 run_mean, o5 run_var
+// Apply passes run over a 2-D grid: blockIdx.y = a slab of <= BN_SLAB
+// channels, blockIdx.x = a contiguous row range. Each block first derives its
+// slab's per-channel coefficients from the fp64 sums into LDS (the old
+// finalize kernel, replicated per block: 2 doubles + 2 floats per channel,
+// L2-resident), then streams rows with 16 B per lane, 2 rows in flight.
+constexpr int BN_SLAB = 256;
+
+struct BnGrid {
+  dim3 grid;
+  long rows_per_block;
+};
+
+static BnGrid bn_apply_grid(long M, int C) {
+  const int slabs = (C + BN_SLAB - 1) / BN_SLAB;
+  const int vs = (C < BN_SLAB ? C : BN_SLAB) / 8;
+  const long rpp = 256 / vs;                              // rows per pass
+  long bx = (2048 + slabs - 1) / slabs;                   // ~8 blocks per CU in all
+  long rpb = (M + bx - 1) / bx;
+  if (rpb < 2 * rpp) rpb = 2 * rpp;
+  rpb = (rpb + rpp - 1) / rpp * rpp;
+  bx = (M + rpb - 1) / rpb;
+  return BnGrid{dim3((unsigned)bx, (unsigned)slabs), rpb};
+}
+
+// y = x*scale + shift (+res) (relu); scale/shift from the sums. Blocks of row
+// range 0 also write save_mean / save_rstd and update the running statistics.
+__global__ void __launch_bounds__(256) bn_apply_kernel(
+    const bf16_t* __restrict__ x, const bf16_t* __restrict__ res, bf16_t* __restrict__ y, long M,
+    int C, long rows_per_block, const double* __restrict__ sums, const float* __restrict__ gamma,
+    const float* __restrict__ beta, float eps, float momentum, float* __restrict__ save_mean,
+    float* __restrict__ save_rstd, float* __restrict__ run_mean, float* __restrict__ run_var,
+    int relu) {
+  __shared__ float s_sc[BN_SLAB], s_sh[BN_SLAB];
+  const int c0 = blockIdx.y * BN_SLAB;
+  const int cs = min(BN_SLAB, C - c0);
+  const int t = threadIdx.x;
+  if (t < cs) {
+    const int c = c0 + t;
+    double S, Q;
+    bn_shard_sum(sums, C, c, S, Q);
     const double mean = S / (double)M;
     double var = Q / (double)M - mean * mean;
     if (var < 0) var = 0;
     const float rstd = (float)(1.0 / sqrt(var + (double)eps));
-    o0[c] = (float)mean;
-    o1[c] = rstd;
     const float sc = gamma[c] * rstd;
-    o2[c] = sc;
-    o3[c] = beta_or_rstd[c] - (float)mean * sc;
-    if (o4) {
-      const double unb = M > 1 ? var * (double)M / (double)(M - 1) : var;
-      o4[c] = (1.f - momentum) * o4[c] + momentum * (float)mean;
-      o5[c] = (1.f - momentum) * o5[c] + momentum * (float)unb;
+    s_sc[t] = sc;
+    s_sh[t] = beta[c] - (float)mean * sc;
+    if (blockIdx.x == 0) {
+      save_mean[c] = (float)mean;
+      save_rstd[c] = rstd;
+      if (run_mean) {
+        const double unb = M > 1 ? var * (double)M / (double)(M - 1) : var;
+        run_mean[c] = (1.f - momentum) * run_mean[c] + momentum * (float)mean;
+        run_var[c] = (1.f - momentum) * run_var[c] + momentum * (float)unb;
+      }
     }
-  } else {
-    // o0 dgamma, o1 dbeta (accumulate), o2 k1, o3 k2, o4 k3
-    const float a = (float)S, bb = (float)Q;
-    if (o0) o0[c] += bb;
-    if (o1) o1[c] += a;
-    const float gr = gamma[c] * beta_or_rstd[c];
-    o2[c] = gr;
-    o3[c] = -gr * bb / (float)M;
-    o4[c] = -gr * a / (float)M;
   }
-}
-
-// mean/rstd + fused scale/shift + running-stat update
-__global__ void bn_finalize_kernel(const double* __restrict__ sums, long M, int C, float eps,
-                                   float momentum,
-                                   const float* __restrict__ gamma, const float* __restrict__ beta,
-                                   float* __restrict__ mean_out, float* __restrict__ rstd_out,
-                                   float* __restrict__ scale, float* __restrict__ shift,
-                                   float* __restrict__ run_mean, float* __restrict__ run_var) {
-  const int c = blockIdx.x * blockDim.x + threadIdx.x;
-  if (c >= C) return;
-  const double mean = sums[c] / (double)M;
-  double var = sums[C + c] / (double)M - mean * mean;
-  if (var < 0) var = 0;
-  const float rstd = (float)(1.0 / sqrt(var + (double)eps));
-  mean_out[c] = (float)mean;
-  rstd_out[c] = rstd;
-  const float sc = gamma[c] * rstd;
-  scale[c] = sc;
-  shift[c] = beta[c] - (float)mean * sc;
-  if (run_mean) {
-    const double unb = M > 1 ? var * (double)M / (double)(M - 1) : var;
-    run_mean[c] = (1.f - momentum) * run_mean[c] + momentum * (float)mean;
-    run_var[c] = (1.f - momentum) * run_var[c] + momentum * (float)unb;
-  }
-}
-
-// y = x*scale + shift (+res) (relu), 8 channels per thread
-__global__ void __launch_bounds__(256) bn_apply_kernel(const bf16_t* __restrict__ x,
-                                                        const bf16_t* __restrict__ res,
-                                                        const float* __restrict__ scale,
-                                                        const float* __restrict__ shift,
-                                                        bf16_t* __restrict__ y, long total8, int C,
-                                                        int relu) {
-  const int cg8 = C / 8;
-  const long stride = (long)gridDim.x * blockDim.x;
-  auto one = [&](const long ii, const uint4 vx, const uint4 vr) {
-    const int c0 = (int)(ii % cg8) * 8;
+  __syncthreads();
+  const int vs = cs / 8, rpp = 256 / vs;
+  const int v = t % vs, rl = t / vs;
+  if (rl >= rpp) return;
+  float sc[8], sh[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) { sc[j] = s_sc[v * 8 + j]; sh[j] = s_sh[v * 8 + j]; }
+  auto one = [&](const long off, const uint4 vx, const uint4 vr) {
     float f[8], rr[8];
     unpack8(vx, f);
     if (res) unpack8(vr, rr);
-    const float4 sa = *(const float4*)(scale + c0), sb = *(const float4*)(scale + c0 + 4);
-    const float4 ha = *(const float4*)(shift + c0), hb = *(const float4*)(shift + c0 + 4);
-    const float sc[8] = {sa.x, sa.y, sa.z, sa.w, sb.x, sb.y, sb.z, sb.w};
-    const float sh[8] = {ha.x, ha.y, ha.z, ha.w, hb.x, hb.y, hb.z, hb.w};
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
-      float v = f[j] * sc[j] + sh[j];
-      if (res) v += rr[j];
-      if (relu) v = fmaxf(v, 0.f);
-      f[j] = v;
+      float o = f[j] * sc[j] + sh[j];
+      if (res) o += rr[j];
+      if (relu) o = fmaxf(o, 0.f);
+      f[j] = o;
     }
-    ((uint4*)y)[ii] = pack8(f);
+    *(uint4*)(y + off) = pack8(f);
   };
   const uint4 z = make_uint4(0, 0, 0, 0);
-  long i = blockIdx.x * (long)blockDim.x + threadIdx.x;
-  // 2 vectors' loads in flight per thread before any use
-  constexpr int U = 2;
-  for (; i + (U - 1) * stride < total8; i += U * stride) {
-    uint4 vx[U], vr[U];
-#pragma unroll
-    for (int u = 0; u < U; ++u) {
-      vx[u] = ((const uint4*)x)[i + u * stride];
-      vr[u] = res ? ((const uint4*)res)[i + u * stride] : z;
-    }
-#pragma unroll
-    for (int u = 0; u < U; ++u) one(i + u * stride, vx[u], vr[u]);
+  const long r0 = blockIdx.x * rows_per_block, r1 = min(M, r0 + rows_per_block);
+  const long col = c0 + v * 8;
+  long r = r0 + rl;
+  for (; r + rpp < r1; r += 2 * rpp) {
+    const long o0 = r * C + col, o1 = (r + rpp) * C + col;
+    const uint4 x0 = *(const uint4*)(x + o0), x1 = *(const uint4*)(x + o1);
+    const uint4 q0 = res ? *(const uint4*)(res + o0) : z, q1 = res ? *(const uint4*)(res + o1) : z;
+    one(o0, x0, q0);
+    one(o1, x1, q1);
   }
-  for (; i < total8; i += stride) one(i, ((const uint4*)x)[i], res ? ((const uint4*)res)[i] : z);
+  if (r < r1) {
+    const long o0 = r * C + col;
+    one(o0, *(const uint4*)(x + o0), res ? *(const uint4*)(res + o0) : z);
+  }
 }
 
 // ---------------------------------------------------------------- BN backward
 // dyr = (dy + addend) * (y > 0 if relu); accum sum(dyr), sum(dyr * xhat) per
-// channel. dp_out (residual BNs): dyr is also stored -- it IS the residual
-// branch's gradient, and the apply pass then reads dyr + x only (no dy,
-// addend, y re-reads, no second dres write: 2 passes of the tensor saved)
+// channel (one partial row per block). dp_out (residual BNs): dyr is also stored -- it IS the
+// residual branch's gradient, and the apply pass then reads dyr + x only (no
+// dy, addend, y re-reads, no second dres write: 2 passes of the tensor saved)
 __global__ void __launch_bounds__(256) bn_bwd_reduce_kernel(
     const bf16_t* __restrict__ dy, const bf16_t* __restrict__ addend, const bf16_t* __restrict__ y,
     const bf16_t* __restrict__ x, const float* __restrict__ mean, const float* __restrict__ rstd, long M,
@@ -347,34 +360,44 @@ __global__ void __launch_bounds__(256) bn_bwd_reduce_kernel(
   }
 }
 
-// dgamma/dbeta accumulate into fp32 grads; coefficient prep for the apply pass
-__global__ void bn_bwd_finalize_kernel(const double* __restrict__ sums, long M, int C,
-                                       const float* __restrict__ gamma,
-                                       const float* __restrict__ rstd, float* __restrict__ dgamma,
-                                       float* __restrict__ dbeta, float* __restrict__ k1,
-                                       float* __restrict__ k2, float* __restrict__ k3) {
-  const int c = blockIdx.x * blockDim.x + threadIdx.x;
-  if (c >= C) return;
-  const float a = (float)sums[c], b = (float)sums[C + c];
-  if (dgamma) dgamma[c] += b;
-  if (dbeta) dbeta[c] += a;
-  // dx = g*rstd*(dyr - a/M - xhat*b/M) = k1*dyr + k2*xhat + k3
-  const float gr = gamma[c] * rstd[c];
-  k1[c] = gr;
-  k2[c] = -gr * b / (float)M;
-  k3[c] = -gr * a / (float)M;
-}
-
+// dx = g*rstd*(dyr - S/M - xhat*Q/M) = k1*dyr + k2*xhat + k3 with S, Q from
+// the sums; blocks of row range 0 accumulate dgamma += Q, dbeta += S
 __global__ void __launch_bounds__(256) bn_bwd_apply_kernel(
     const bf16_t* __restrict__ dy, const bf16_t* __restrict__ addend, const bf16_t* __restrict__ y,
-    const bf16_t* __restrict__ x,
-    const float* __restrict__ mean, const float* __restrict__ rstd, const float* __restrict__ k1,
-    const float* __restrict__ k2, const float* __restrict__ k3, bf16_t* __restrict__ dx,
-    bf16_t* __restrict__ dres, long total8, int C, int relu) {
-  const int cg8 = C / 8;
-  const long stride = (long)gridDim.x * blockDim.x;
-  auto one = [&](const long ii, const uint4 vd, const uint4 vx, const uint4 vy, const uint4 va) {
-    const int c0 = (int)(ii % cg8) * 8;
+    const bf16_t* __restrict__ x, long M, int C, long rows_per_block, const double* __restrict__ sums,
+    const float* __restrict__ mean, const float* __restrict__ rstd, const float* __restrict__ gamma,
+    float* __restrict__ dgamma, float* __restrict__ dbeta, bf16_t* __restrict__ dx,
+    bf16_t* __restrict__ dres, int relu) {
+  __shared__ float s_k[4][BN_SLAB];     // k1, k2, k3, mean
+  const int c0 = blockIdx.y * BN_SLAB;
+  const int cs = min(BN_SLAB, C - c0);
+  const int t = threadIdx.x;
+  if (t < cs) {
+    const int c = c0 + t;
+    double Sd, Qd;
+    bn_shard_sum(sums, C, c, Sd, Qd);
+    const float S = (float)Sd, Q = (float)Qd;
+    const float rs = rstd[c], gr = gamma[c] * rs;
+    // k2 multiplies (x - mean) directly: rstd folded in
+    s_k[0][t] = gr;
+    s_k[1][t] = -gr * Q / (float)M * rs;
+    s_k[2][t] = -gr * S / (float)M;
+    s_k[3][t] = mean[c];
+    if (blockIdx.x == 0) {
+      if (dgamma) dgamma[c] += Q;
+      if (dbeta) dbeta[c] += S;
+    }
+  }
+  __syncthreads();
+  const int vs = cs / 8, rpp = 256 / vs;
+  const int v = t % vs, rl = t / vs;
+  if (rl >= rpp) return;
+  float k1[8], k2[8], k3[8], mu[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    k1[j] = s_k[0][v * 8 + j]; k2[j] = s_k[1][v * 8 + j]; k3[j] = s_k[2][v * 8 + j]; mu[j] = s_k[3][v * 8 + j];
+  }
+  auto one = [&](const long off, const uint4 vd, const uint4 vx, const uint4 vy, const uint4 va) {
     float fd[8], fx[8];
     unpack8(vd, fd);
     unpack8(vx, fx);
@@ -390,49 +413,38 @@ __global__ void __launch_bounds__(256) bn_bwd_apply_kernel(
 #pragma unroll
       for (int j = 0; j < 8; ++j) fd[j] = fy[j] <= 0.f ? 0.f : fd[j];
     }
-    if (dres) ((uint4*)dres)[ii] = pack8(fd);
+    if (dres) *(uint4*)(dres + off) = pack8(fd);
     float o[8];
 #pragma unroll
-    for (int j = 0; j < 8; ++j) {
-      const int c = c0 + j;
-      const float xh = (fx[j] - mean[c]) * rstd[c];
-      o[j] = k1[c] * fd[j] + k2[c] * xh + k3[c];
-    }
-    ((uint4*)dx)[ii] = pack8(o);
+    for (int j = 0; j < 8; ++j) o[j] = k1[j] * fd[j] + k2[j] * (fx[j] - mu[j]) + k3[j];
+    *(uint4*)(dx + off) = pack8(o);
   };
   const uint4 z = make_uint4(0, 0, 0, 0);
-  long i = blockIdx.x * (long)blockDim.x + threadIdx.x;
-  // 2 vectors' loads in flight per thread before any use
-  constexpr int U = 2;
-  for (; i + (U - 1) * stride < total8; i += U * stride) {
-    uint4 vd[U], vx[U], vy[U], va[U];
+  const long r0 = blockIdx.x * rows_per_block, r1 = min(M, r0 + rows_per_block);
+  const long col = c0 + v * 8;
+  long r = r0 + rl;
+  for (; r + rpp < r1; r += 2 * rpp) {
+    uint4 vd[2], vx[2], vy[2], va[2];
 #pragma unroll
-    for (int u = 0; u < U; ++u) {
-      const long ii = i + u * stride;
-      vd[u] = ((const uint4*)dy)[ii];
-      vx[u] = ((const uint4*)x)[ii];
-      vy[u] = relu ? ((const uint4*)y)[ii] : z;
-      va[u] = addend ? ((const uint4*)addend)[ii] : z;
+    for (int u = 0; u < 2; ++u) {
+      const long off = (r + u * rpp) * C + col;
+      vd[u] = *(const uint4*)(dy + off);
+      vx[u] = *(const uint4*)(x + off);
+      vy[u] = relu ? *(const uint4*)(y + off) : z;
+      va[u] = addend ? *(const uint4*)(addend + off) : z;
     }
 #pragma unroll
-    for (int u = 0; u < U; ++u) one(i + u * stride, vd[u], vx[u], vy[u], va[u]);
+    for (int u = 0; u < 2; ++u) one((r + u * rpp) * C + col, vd[u], vx[u], vy[u], va[u]);
   }
-  for (; i < total8; i += stride)
-    one(i, ((const uint4*)dy)[i], ((const uint4*)x)[i], relu ? ((const uint4*)y)[i] : z,
-        addend ? ((const uint4*)addend)[i] : z);
-}
-
-// elementwise grids: one thread per 16-B vector up to 2048 blocks (8 per CU);
-// measured: fewer, 4x-unrolled blocks (n / 1024) were slower on ResNet-50
-static int grid_for(long n) {
-  long b = (n + 255) / 256;
-  if (b > 2048) b = 2048;
-  if (b < 1) b = 1;
-  return (int)b;
+  if (r < r1) {
+    const long off = r * C + col;
+    one(off, *(const uint4*)(dy + off), *(const uint4*)(x + off), relu ? *(const uint4*)(y + off) : z,
+        addend ? *(const uint4*)(addend + off) : z);
+  }
 }
 
 static long bn_rows_per_block(long M, int C) {
-  // <= BN_MAX_BLOCKS partial rows (2 blocks per CU on 256 CUs); each block
+  // <= BN_MAX_BLOCKS reducing blocks (2 per CU on 256 CUs); each block
   // streams >= 4 passes of its thread grid so the loads stay 16 B/lane
   long rpb = (M + BN_MAX_BLOCKS - 1) / BN_MAX_BLOCKS;
   const long minr = 256 / (C / 8) * 4;
@@ -442,77 +454,81 @@ static long bn_rows_per_block(long M, int C) {
 
 void bn_forward(const bf16_t* x, const bf16_t* res, bf16_t* y, long M, int C, float eps,
                 float momentum, const float* gamma, const float* beta, float* run_mean,
-                float* run_var, float* save_mean, float* save_rstd, float* ws_f, int relu,
-                const float* part_in, int nblk_in, hipStream_t s) {
-  // ws_f: 2*C floats scale/shift | 2*C doubles column sums | BN_MAX_BLOCKS*2*C partials
-  // part_in: [nblk_in][2C] partial rows already produced (conv epilogue): no stats pass
-  const long rpb = bn_rows_per_block(M, C);
-  int nb = (int)((M + rpb - 1) / rpb);
-  double* sums = (double*)(ws_f + 2 * C);
-  const float* part = ws_f + 6 * C;
-  (void)sums;
-  if (part_in && nblk_in > 0) {
-    part = part_in;
-    nb = nblk_in;
-  } else {
-    hipLaunchKernelGGL(bn_stats_kernel, dim3(nb), dim3(256), 0, s, x, M, C, rpb, ws_f + 6 * C);
+                float* run_var, float* save_mean, float* save_rstd, int relu, double* sums,
+                int sums_ready, float* part, hipStream_t s) {
+  if (!sums_ready) {
+    const long rpb = bn_rows_per_block(M, C);
+    const int nb = (int)((M + rpb - 1) / rpb);
+    hipLaunchKernelGGL(bn_stats_kernel, dim3(nb), dim3(256), 0, s, x, M, C, rpb, part);
+    hipLaunchKernelGGL(bn_col_sums_kernel, dim3((2 * C + 15) / 16), dim3(1024), 0, s, (const float*)part,
+                       nb, 2 * C, sums);
   }
-  hipLaunchKernelGGL(bn_reduce_finalize_kernel<0>, dim3((C + 15) / 16), dim3(1024), 0, s, part, nb, M,
-                     C, eps, momentum, gamma, beta, save_mean, save_rstd, ws_f, ws_f + C, run_mean,
-                     run_var);
-  const long total8 = M * C / 8;
-  hipLaunchKernelGGL(bn_apply_kernel, dim3(grid_for(total8)), dim3(256), 0, s, x, res, ws_f,
-                     ws_f + C, y, total8, C, relu);
+  const BnGrid g = bn_apply_grid(M, C);
+  hipLaunchKernelGGL(bn_apply_kernel, g.grid, dim3(256), 0, s, x, res, y, M, C, g.rows_per_block,
+                     (const double*)sums, gamma, beta, eps, momentum, save_mean, save_rstd, run_mean,
+                     run_var, relu);
+}
+
+// inference: scale / shift given (no statistics)
+__global__ void __launch_bounds__(256) bn_infer_kernel(const bf16_t* __restrict__ x,
+                                                        const bf16_t* __restrict__ res,
+                                                        const float* __restrict__ scale,
+                                                        const float* __restrict__ shift,
+                                                        bf16_t* __restrict__ y, long total8, int C,
+                                                        int relu) {
+  const int cg8 = C / 8;
+  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < total8;
+       i += (long)gridDim.x * blockDim.x) {
+    const int c0 = (int)(i % cg8) * 8;
+    float f[8], rr[8];
+    unpack8(((const uint4*)x)[i], f);
+    if (res) unpack8(((const uint4*)res)[i], rr);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      float v = f[j] * scale[c0 + j] + shift[c0 + j];
+      if (res) v += rr[j];
+      if (relu) v = fmaxf(v, 0.f);
+      f[j] = v;
+    }
+    ((uint4*)y)[i] = pack8(f);
+  }
 }
 
 void bn_infer(const bf16_t* x, const bf16_t* res, bf16_t* y, long M, int C, const float* scale,
               const float* shift, int relu, hipStream_t s) {
   const long total8 = M * C / 8;
-  hipLaunchKernelGGL(bn_apply_kernel, dim3(grid_for(total8)), dim3(256), 0, s, x, res, scale,
-                     shift, y, total8, C, relu);
+  long b = (total8 + 255) / 256;
+  if (b > 2048) b = 2048;
+  if (b < 1) b = 1;
+  hipLaunchKernelGGL(bn_infer_kernel, dim3((unsigned)b), dim3(256), 0, s, x, res, scale, shift, y,
+                     total8, C, relu);
 }
 
 void bn_backward(const bf16_t* dy, const bf16_t* addend, const bf16_t* y, const bf16_t* x,
                  const float* mean, const float* rstd, const float* gamma, long M, int C, int relu,
-                 bf16_t* dx, bf16_t* dres, float* dgamma, float* dbeta, float* ws_f, hipStream_t s) {
-  // ws_f: 4*C floats k1/k2/k3(+pad) | 2*C doubles column sums | BN_MAX_BLOCKS*2*C partials
-  const long rpb = bn_rows_per_block(M, C);
-  const int nb = (int)((M + rpb - 1) / rpb);
-  double* sums = (double*)(ws_f + 4 * C);
-  float* part = ws_f + 8 * C;
-  // residual BN: the reduce pass materialises dyr into dres; the apply pass
-  // then runs on (dres, x) as a plain BN backward
-  hipLaunchKernelGGL(bn_bwd_reduce_kernel, dim3(nb), dim3(256), 0, s, dy, addend, y, x, mean, rstd, M,
-                     C, rpb, relu, part, dres);
-  if (dres) {
-    dy = dres;
-    addend = nullptr;
-    y = nullptr;
-    relu = 0;
-    dres = nullptr;
+                 bf16_t* dx, bf16_t* dres, float* dgamma, float* dbeta, double* sums,
+                 int sums_ready, float* part, hipStream_t s) {
+  if (!sums_ready) {
+    // residual BN: the reduce pass materialises dyr into dres; the apply pass
+    // then runs on (dres, x) as a plain BN backward
+    const long rpb = bn_rows_per_block(M, C);
+    const int nb = (int)((M + rpb - 1) / rpb);
+    hipLaunchKernelGGL(bn_bwd_reduce_kernel, dim3(nb), dim3(256), 0, s, dy, addend, y, x, mean, rstd, M,
+                       C, rpb, relu, part, dres);
+    hipLaunchKernelGGL(bn_col_sums_kernel, dim3((2 * C + 15) / 16), dim3(1024), 0, s, (const float*)part,
+                       nb, 2 * C, sums);
+    if (dres) {
+      dy = dres;
+      addend = nullptr;
+      y = nullptr;
+      relu = 0;
+      dres = nullptr;
+    }
   }
-  (void)sums;
-  hipLaunchKernelGGL(bn_reduce_finalize_kernel<1>, dim3((C + 15) / 16), dim3(1024), 0, s, part, nb, M,
-                     C, 0.f, 0.f, gamma, rstd, dgamma, dbeta, ws_f, ws_f + C, ws_f + 2 * C,
-                     (float*)nullptr);
-  const long total8 = M * C / 8;
-  hipLaunchKernelGGL(bn_bwd_apply_kernel, dim3(grid_for(total8)), dim3(256), 0, s, dy, addend, y, x,
-                     mean, rstd, ws_f, ws_f + C, ws_f + 2 * C, dx, dres, total8, C, relu);
-}
-
-// BN backward whose reduction already happened in the consumer conv's dgrad
-// epilogue (Epi::bnx): part = [nblk][2C] partial rows of sum(d) | sum(d*xhat)
-// over the ReLU-masked output gradient d; finalize + one apply pass
-void bn_backward_part(const bf16_t* dy, const bf16_t* x, const float* mean, const float* rstd,
-                      const float* gamma, long M, int C, bf16_t* dx, float* dgamma, float* dbeta,
-                      const float* part, int nblk, float* ws_f, hipStream_t s) {
-  hipLaunchKernelGGL(bn_reduce_finalize_kernel<1>, dim3((C + 15) / 16), dim3(1024), 0, s, part, nblk, M,
-                     C, 0.f, 0.f, gamma, rstd, dgamma, dbeta, ws_f, ws_f + C, ws_f + 2 * C,
-                     (float*)nullptr);
-  const long total8 = M * C / 8;
-  hipLaunchKernelGGL(bn_bwd_apply_kernel, dim3(grid_for(total8)), dim3(256), 0, s, dy,
-                     (const bf16_t*)nullptr, (const bf16_t*)nullptr, x, mean, rstd, ws_f, ws_f + C,
-                     ws_f + 2 * C, dx, (bf16_t*)nullptr, total8, C, 0);
+  const BnGrid g = bn_apply_grid(M, C);
+  hipLaunchKernelGGL(bn_bwd_apply_kernel, g.grid, dim3(256), 0, s, dy, addend, y, x, M, C,
+                     g.rows_per_block, (const double*)sums, mean, rstd, gamma, dgamma, dbeta, dx, dres,
+                     relu);
 }
 
 // ---------------------------------------------------------------- LayerNorm

@@ -366,6 +366,83 @@ def test_conv_dma_core(gpu, cfg, policy):
         T().conv_dma_policy(1)
 
 
+# halo-tile kernel (conv_dma.h conv_halo_kernel): 64-channel 3x3 stride-1
+# passes, 4 x 56 output tiles; vs torch fp32 and vs the tap-gather cores
+@pytest.mark.parametrize("cfg", [(2, 56, 56, 64, 64), (1, 8, 112, 64, 128), (1, 4, 224, 64, 64),
+                                 (3, 12, 56, 64, 192)])
+def test_conv_halo(gpu, cfg):
+    from tiresias_amd.ops.functional import BN_SHARDS
+    N, H, W, C, K = cfg
+    torch.manual_seed(11)
+    x = torch.randn(N, H, W, C, device=gpu).to(BF)
+    w = (torch.randn(K, 3, 3, C, device=gpu) / math.sqrt(9 * C)).to(BF)
+    b = torch.randn(K, device=gpu).to(BF)
+    outs = {}
+    try:
+        for halo in (1, 0):
+            T().conv_halo_policy(halo)
+            y = torch.empty(N, H, W, K, device=gpu, dtype=BF)
+            T().conv_fwd(x, w, y, 1, 1, 1, b, True)
+            ys = torch.empty_like(y)
+            sums = torch.zeros(BN_SHARDS * 2 * K, device=gpu, dtype=torch.float64)
+            done = T().conv_fwd(x, w, ys, 1, 1, 1, None, False, sums)
+            # dgrad (halo path when K == 64: a 64-channel dY), masked by x
+            torch.manual_seed(13)
+            dyc = torch.randn(N, H, W, K, device=gpu).to(BF)
+            dx = torch.empty_like(x)
+            T().conv_dgrad(dyc, w, torch.empty_like(w), dx, 1, 1, 1, x)
+            outs[halo] = (y, ys, sums.view(BN_SHARDS, 2 * K).sum(0) if done else None, dx)
+    finally:
+        T().conv_halo_policy(1)
+    y, ys, tot, dx = outs[1]
+    ref = _ref_conv(x, w, 1, 1)
+    assert rel_err(y, (ref + b.float()).clamp_min(0)) < 1e-2
+    assert rel_err(ys, ref) < 1e-2
+    assert tot is not None
+    yf = ys.double().reshape(-1, K)
+    assert rel_err(tot[:K], yf.sum(0)) < 1e-5 and rel_err(tot[K:], (yf * yf).sum(0)) < 1e-5
+    for u, v in zip(outs[1], outs[0]):
+        if u is not None and v is not None:
+            assert rel_err(u, v) < 1e-2
+
+
+def test_conv_halo_dgrad_bnx(gpu):
+    """Halo-path dgrad (64-channel dY) with the ReLU mask and the BN-backward
+    sums of Epi::bnx (conv_dgrad_pre) == the tap-gather core's."""
+    from tiresias_amd.ops.functional import BN_SHARDS
+    torch.manual_seed(12)
+    N, H, W, C, K = 2, 56, 56, 64, 64
+    dy = torch.randn(N, H, W, K, device=gpu).to(BF)
+    w = (torch.randn(K, 3, 3, C, device=gpu) / math.sqrt(9 * C)).to(BF)
+    wt = w.permute(3, 1, 2, 0).contiguous()
+    y = torch.randn(N, H, W, C, device=gpu).to(BF)          # the BN output (mask)
+    bx = torch.randn(N, H, W, C, device=gpu).to(BF)         # the BN input
+    mean = torch.randn(C, device=gpu) * 0.1
+    rstd = torch.rand(C, device=gpu) + 0.5
+    outs = []
+    try:
+        for halo in (1, 0):
+            T().conv_halo_policy(halo)
+            dx = torch.empty(N, H, W, C, device=gpu, dtype=BF)
+            sums = torch.zeros(BN_SHARDS * 2 * C, device=gpu, dtype=torch.float64)
+            done = T().conv_dgrad_pre(dy, w, wt, dx, 1, 1, 1, y, sums, bx, mean, rstd)
+            assert done == 1
+            outs.append((dx, sums.view(BN_SHARDS, 2 * C).sum(0)))
+    finally:
+        T().conv_halo_policy(1)
+    xf = torch.zeros(N, C, H, W, device=gpu, requires_grad=True)
+    g, = torch.autograd.grad(F.conv2d(xf, w.float().permute(0, 3, 1, 2), padding=1), [xf],
+                             dy.float().permute(0, 3, 1, 2))
+    d = g.permute(0, 2, 3, 1) * (y.float() > 0)
+    assert rel_err(outs[0][0], d) < 1e-2
+    dd = outs[0][0].double().reshape(-1, C)
+    xh = (bx.double().reshape(-1, C) - mean.double()) * rstd.double()
+    assert rel_err(outs[0][1][:C], dd.sum(0)) < 1e-4
+    assert rel_err(outs[0][1][C:], (dd * xh).sum(0)) < 1e-4
+    assert rel_err(outs[0][0], outs[1][0]) < 1e-2
+    assert rel_err(outs[0][1], outs[1][1]) < 1e-3
+
+
 def test_conv_bias_relu_mask(gpu):
     torch.manual_seed(4)
     x = torch.randn(2, 8, 8, 16, device=gpu).to(BF)
@@ -387,9 +464,11 @@ def test_conv_bias_relu_mask(gpu):
 
 # ------------------------------------------------------------------ BN / LN
 @pytest.mark.parametrize("shape", [(8, 14, 14, 64), (32, 28, 28, 128), (16, 7, 7, 2048),
-                                   (64, 56, 56, 64)])
+                                   (64, 56, 56, 64), (4, 9, 9, 320), (2, 5, 5, 1000)])
 @pytest.mark.parametrize("relu,res", [(False, False), (True, False), (True, True)])
 def test_batchnorm(gpu, relu, res, shape):
+    """BN forward/backward (fp64-atomic sums, per-block finalize in the apply
+    prologues; channel slabs of 256 incl. a partial last slab) vs torch fp32."""
     torch.manual_seed(5)
     N, H, W, C = shape
     x = (torch.randn(N, H, W, C, device=gpu) * 3 + 1).to(BF)
@@ -455,39 +534,47 @@ def test_batchnorm_backward_addend(gpu, relu):
 @pytest.mark.parametrize("shape", [(8, 28, 28, 128, 256, 3, 1, 1), (16, 14, 14, 256, 1024, 1, 1, 0),
                                    (4, 56, 56, 64, 64, 3, 1, 1), (8, 28, 28, 256, 512, 1, 2, 0)])
 def test_conv_fwd_bn_stats(gpu, shape, policy):
-    """BatchNorm partial sums from the conv epilogue == column sums / sums of
-    squares of the stored bf16 output; and bn_forward over those partials ==
-    bn_forward computing its own statistics."""
+    """BatchNorm sums accumulated by the conv epilogue (fp64 atomics) == column
+    sums / sums of squares of the stored bf16 output; and bn_forward over those
+    sums == bn_forward computing its own statistics (stats pass into a zeroed
+    workspace, and into its own temporary)."""
     torch.manual_seed(8)
     N, H, W, C, K, R, st, pd = shape
     x = torch.randn(N, H, W, C, device=gpu).to(BF)
     w = (torch.randn(K, R, R, C, device=gpu) / (R * R * C) ** 0.5).to(BF)
     P = (H + 2 * pd - R) // st + 1
     y = torch.empty(N, P, P, K, device=gpu, dtype=BF)
-    part = torch.empty((N * P * P + 127) // 128, 2 * K, device=gpu)
+    from tiresias_amd.ops.functional import BN_SHARDS
+    sums = torch.zeros(BN_SHARDS * 2 * K, device=gpu, dtype=torch.float64)
     T().conv_dma_policy(policy)
     try:
-        nblk = T().conv_fwd(x, w, y, st, pd, 1, None, False, part)
+        done = T().conv_fwd(x, w, y, st, pd, 1, None, False, sums)
     finally:
         T().conv_dma_policy(1)
-    if nblk == 0:
+    if done == 0:
+        assert torch.count_nonzero(sums) == 0
         pytest.skip("shape not on the LDS-DMA conv core")
-    yf = y.float().reshape(-1, K)
-    s = part[:nblk].sum(0)
-    assert rel_err(s[:K], yf.sum(0)) < 1e-4 and rel_err(s[K:], (yf * yf).sum(0)) < 1e-4
+    yf = y.double().reshape(-1, K)
+    tot = sums.view(BN_SHARDS, 2 * K).sum(0)
+    assert rel_err(tot[:K], yf.sum(0)) < 1e-5 and rel_err(tot[K:], (yf * yf).sum(0)) < 1e-5
     g = torch.rand(K, device=gpu) + 0.5
     b = torch.randn(K, device=gpu)
     outs = []
-    for use in (True, False):
+    for use in ("conv", "ws", "tmp"):
         o = torch.empty_like(y)
         mean, rstd = torch.empty(K, device=gpu), torch.empty(K, device=gpu)
-        if use:
-            T().bn_forward(y, None, o, g, b, None, None, mean, rstd, 1e-5, 0.1, True, part, nblk)
+        rm, rv = torch.zeros(K, device=gpu), torch.ones(K, device=gpu)
+        if use == "conv":
+            T().bn_forward(y, None, o, g, b, rm, rv, mean, rstd, 1e-5, 0.1, True, sums, True)
+        elif use == "ws":
+            ws = torch.zeros(BN_SHARDS * 2 * K, device=gpu, dtype=torch.float64)
+            T().bn_forward(y, None, o, g, b, rm, rv, mean, rstd, 1e-5, 0.1, True, ws, False)
         else:
-            T().bn_forward(y, None, o, g, b, None, None, mean, rstd, 1e-5, 0.1, True)
-        outs.append((o, mean, rstd))
-    for u, v in zip(*outs):
-        assert rel_err(u, v) < 1e-3
+            T().bn_forward(y, None, o, g, b, rm, rv, mean, rstd, 1e-5, 0.1, True)
+        outs.append((o, mean, rstd, rm, rv))
+    for other in outs[1:]:
+        for u, v in zip(outs[0], other):
+            assert rel_err(u, v) < 1e-3
 
 
 def test_conv_weight_t_batch(gpu):

@@ -14,6 +14,10 @@ reference only *models* them: per-tensor gradient sizes in
   epilogue; VGG: conv + bias + ReLU fused in the conv epilogue, the ReLU
   backward fused into the next layer's dgrad epilogue;
 * every conv weight is re-laid for dgrad once per step in one launch;
+* BN statistics: fp64 sums accumulated by the producing conv's epilogue (or
+  the BN's own pass) into per-layer slices of ONE buffer zeroed once per step;
+  the apply passes finalize per channel in their prologue (no finalize
+  launches);
 * all weights live in one flat :class:`Arena` per job.
 """
 from __future__ import annotations
@@ -73,6 +77,8 @@ class ResNet50:
                 blk["pre"] = pre
                 self.blocks.append(blk)
                 cin = w * 4
+        self.bn_buf, self.bn_ws = Fx.bn_workspaces(
+            {k: st.mean.numel() for k, st in self.bn_state.items()}, dev)
         self.fc_w = A.add("fc.w", (num_classes, cin), init="normal", std=0.01)
         self.fc_b = A.add("fc.b", (num_classes,), init="zeros", decay=False)
         self.num_classes = num_classes
@@ -81,7 +87,13 @@ class ResNet50:
     def _bn(self, x, p, key, relu, res=None, consumer_masks=False):
         st = self.bn_state[key]
         return Fx.batchnorm(x, p[0], p[1], st.mean, st.var, relu=relu, residual=res,
-                            training=self.training, consumer_masks=consumer_masks)
+                            training=self.training, consumer_masks=consumer_masks,
+                            ws=self.bn_ws[key])
+
+    def _st(self, key):
+        # the conv feeding BN `key` accumulates its statistics into the BN's
+        # forward workspace (training on GPU), else the BN reduces itself
+        return self.bn_ws[key].fwd if (self.training and self.bn_buf.is_cuda) else True
 
     def conv_params(self):
         out = [self.stem]
@@ -91,7 +103,9 @@ class ResNet50:
 
     def forward(self, x: torch.Tensor) -> torch.Tensor:
         Fx.prepare_conv_wt(self.conv_params())
-        y = Fx.conv2d(x, self.stem, stride=2, pad=3, bn_stats=True)
+        if self.training:
+            self.bn_buf.zero_()          # every BN accumulator of this step: one memset
+        y = Fx.conv2d(x, self.stem, stride=2, pad=3, bn_stats=self._st("stem"))
         y = self._bn(y, self.stem_bn, "stem", relu=True)
         y = Fx.maxpool2d(y, 3, 2, 1)
         for blk in self.blocks:
@@ -101,13 +115,15 @@ class ResNet50:
             idn = Fx.residual_tap(y) if "down" not in blk else None
             # bn1 / bn2 outputs feed exactly one conv each: that conv's dgrad
             # epilogue applies their ReLU backward mask (in_relu)
-            o = Fx.conv2d(y, blk["c1"], bn_stats=True)
+            o = Fx.conv2d(y, blk["c1"], bn_stats=self._st(pre + ".bn1"))
             o = self._bn(o, blk["bn1"], pre + ".bn1", relu=True, consumer_masks=True)
-            o = Fx.conv2d(o, blk["c2"], stride=blk["stride"], pad=1, in_relu=True, bn_stats=True)
+            o = Fx.conv2d(o, blk["c2"], stride=blk["stride"], pad=1, in_relu=True,
+                          bn_stats=self._st(pre + ".bn2"))
             o = self._bn(o, blk["bn2"], pre + ".bn2", relu=True, consumer_masks=True)
-            o = Fx.conv2d(o, blk["c3"], in_relu=True, bn_stats=True)
+            o = Fx.conv2d(o, blk["c3"], in_relu=True, bn_stats=self._st(pre + ".bn3"))
             if "down" in blk:
-                idn = Fx.conv2d(Fx.residual_tap(y), blk["down"], stride=blk["stride"], bn_stats=True)
+                idn = Fx.conv2d(Fx.residual_tap(y), blk["down"], stride=blk["stride"],
+                                bn_stats=self._st(pre + ".dbn"))
                 idn = self._bn(idn, blk["down_bn"], pre + ".dbn", relu=False)
             y = self._bn(o, blk["bn3"], pre + ".bn3", relu=True, res=idn)
         y = Fx.global_avgpool(y)

@@ -224,21 +224,35 @@ def _conv_out(h: int, k: int, s: int, p: int, d: int = 1) -> int:
 BN_DGRAD_FUSION = False
 
 
+# shards of a BatchNorm statistics accumulator (csrc/include/tam/common.h
+# BN_SHARDS; the ops check the size): fp64 [BN_SHARDS][2C]
+BN_SHARDS = 16
+
+
+def _bn_sums(ws, C: int, device) -> torch.Tensor:
+    """fp64 [BN_SHARDS * 2C] BatchNorm statistics accumulator: the caller's
+    zeroed workspace slice, or a fresh zeroed tensor."""
+    if ws is not None:
+        return ws
+    return torch.zeros(BN_SHARDS * 2 * C, dtype=torch.float64, device=device)
+
+
 class _Conv(Function):
     @staticmethod
     def forward(ctx, x, token, w: Param, b: Optional[Param], stride: int, pad: int, relu: bool,
-                in_relu: bool, mask_own_relu: bool, bn_stats: bool = False):
+                in_relu: bool, mask_own_relu: bool, bn_stats=False):
         N, H, W, C = x.shape
         K, R, S, _ = w.shape
         P, Q = _conv_out(H, R, stride, pad), _conv_out(W, S, stride, pad)
         part = None
         if x.is_cuda:
             y = torch.empty(N, P, Q, K, dtype=BF16, device=x.device)
-            if bn_stats:
-                # BatchNorm partial sums from the conv epilogue (no stats pass)
-                part = torch.empty((N * P * Q + 127) // 128, 2 * K, dtype=torch.float32, device=x.device)
-                nblk = _T().conv_fwd(x, w.w, y, stride, pad, 1, b.w if b is not None else None, relu, part)
-                part = (part, nblk) if nblk > 0 else None
+            if bn_stats is not False and bn_stats is not None:
+                # BatchNorm sums from the conv epilogue (no stats pass): fp64
+                # atomics into the BN's zeroed workspace
+                sums = _bn_sums(bn_stats if isinstance(bn_stats, torch.Tensor) else None, K, x.device)
+                done = _T().conv_fwd(x, w.w, y, stride, pad, 1, b.w if b is not None else None, relu, sums)
+                part = sums if done else None
             else:
                 _T().conv_fwd(x, w.w, y, stride, pad, 1, b.w if b is not None else None, relu)
         else:
@@ -279,12 +293,10 @@ class _Conv(Function):
                 wt = getattr(w, "wt", None)
                 sl = ctx.bn_slot
                 if wt is not None and sl is not None:
-                    bx, bmean, brstd = sl.src
-                    C = x.shape[-1]
-                    part = torch.empty((x.numel() // C + 127) // 128, 2 * C, dtype=torch.float32,
-                                       device=x.device)
-                    nblk = _T().conv_dgrad_pre(dy, w.w, wt, dx, st, pd, 1, x, part, bx, bmean, brstd)
-                    sl.bwd_part = (part, nblk, dx) if nblk > 0 else None
+                    bx, bmean, brstd, bws = sl.src
+                    sums = _bn_sums(bws, x.shape[-1], x.device)
+                    done = _T().conv_dgrad_pre(dy, w.w, wt, dx, st, pd, 1, x, sums, bx, bmean, brstd)
+                    sl.bwd_part = (sums, dx) if done else None
                 elif wt is not None:     # re-laid once per step (prepare_conv_wt)
                     _T().conv_dgrad_pre(dy, w.w, wt, dx, st, pd, 1, x if ctx.in_relu else None)
                 else:
@@ -326,14 +338,15 @@ def prepare_conv_wt(params: List[Param]) -> None:
 
 def conv2d(x: torch.Tensor, w: Param, b: Optional[Param] = None, stride: int = 1, pad: int = 0,
            relu: bool = False, in_relu: bool = False, mask_own_relu: bool = True,
-           bn_stats: bool = False) -> torch.Tensor:
+           bn_stats=False) -> torch.Tensor:
     """NHWC conv, weights [K,R,S,C]. ``bn_stats``: the output feeds a
-    BatchNorm -- its per-channel partial sums come from the conv epilogue
-    (where the conv path supports it) and ride on the output tensor."""
+    BatchNorm -- its per-channel sums come from the conv epilogue (where the
+    conv path supports it) and ride on the output tensor. True, or the BN's
+    zeroed fp64 forward workspace (``BNWorkspace.fwd``) to accumulate into."""
     if not x.is_contiguous():
         x = x.contiguous()
     y = _Conv.apply(x, w.arena.token, w, b, stride, pad, relu, in_relu, mask_own_relu, bn_stats)
-    if bn_stats and y.is_cuda and y.grad_fn is not None:
+    if bn_stats is not False and bn_stats is not None and y.is_cuda and y.grad_fn is not None:
         part = getattr(y.grad_fn, "part", None)
         if part is not None:
             y._tam_bnpart = part
@@ -351,8 +364,9 @@ class GradSlot:
 
     def __init__(self):
         self.stash = None
-        # consumer_masks BNs: (x, mean, rstd) for the consumer conv's dgrad
-        # epilogue, which returns the BN-backward partial rows in bwd_part
+        # consumer_masks BNs: (x, mean, rstd, backward sums workspace) for the
+        # consumer conv's dgrad epilogue, which accumulates the BN-backward
+        # sums and parks (sums, its dx) in bwd_part
         self.src = None
         self.bwd_part = None
 
@@ -385,7 +399,7 @@ class _BN(Function):
     @staticmethod
     def forward(ctx, x, res, token, g: Param, b: Param, run_mean, run_var, relu: bool, eps: float,
                 momentum: float, training: bool, slot: Optional[GradSlot] = None,
-                consumer_masks: bool = False):
+                consumer_masks: bool = False, ws=None):
         C = x.shape[-1]
         if x.is_cuda:
             y = torch.empty_like(x)
@@ -393,12 +407,12 @@ class _BN(Function):
                 mean = torch.empty(C, dtype=torch.float32, device=x.device)
                 rstd = torch.empty_like(mean)
                 part = getattr(x, "_tam_bnpart", None)
-                if part is not None:
+                if part is not None:       # sums accumulated by the producing conv
                     _T().bn_forward(x, res, y, g.master, b.master, run_mean, run_var, mean, rstd, eps,
-                                    momentum, relu, part[0], part[1])
+                                    momentum, relu, part, True)
                 else:
                     _T().bn_forward(x, res, y, g.master, b.master, run_mean, run_var, mean, rstd, eps,
-                                    momentum, relu)
+                                    momentum, relu, ws.fwd if ws is not None else None, False)
             else:
                 rstd_i = torch.rsqrt(run_var + eps)
                 scale = g.master * rstd_i
@@ -429,8 +443,9 @@ class _BN(Function):
         bwd_relu = relu and not consumer_masks
         ctx.g, ctx.b, ctx.relu, ctx.has_res = g, b, bwd_relu, res is not None
         ctx.slot = slot
+        ctx.bws = ws.bwd if ws is not None else None
         if slot is not None and consumer_masks and x.is_cuda and training:
-            slot.src = (x, mean, rstd)
+            slot.src = (x, mean, rstd, ctx.bws)
         ctx.save_for_backward(x, y if bwd_relu else None, mean, rstd)
         return y
 
@@ -446,17 +461,19 @@ class _BN(Function):
         part = None
         if ctx.slot is not None:
             part, ctx.slot.bwd_part = ctx.slot.bwd_part, None
-        if (dy.is_cuda and part is not None and part[2].data_ptr() == dy.data_ptr() and not ctx.relu
+        if (dy.is_cuda and part is not None and part[1].data_ptr() == dy.data_ptr() and not ctx.relu
                 and not ctx.has_res and add is None):
-            # the consumer conv's dgrad epilogue already reduced sum(d) and
-            # sum(d * xhat) per channel: finalize + apply only
+            # the consumer conv's dgrad epilogue already accumulated sum(d) and
+            # sum(d * xhat) per channel: apply only
             dx = torch.empty_like(x)
-            _T().bn_backward_part(dy, x, mean, rstd, g.master, dx, g.grad, b.grad, part[0], part[1])
+            _T().bn_backward(dy, None, x, mean, rstd, g.master, dx, None, g.grad, b.grad, False, None,
+                             part[0], True)
             dres = None
         elif dy.is_cuda:
             dx = torch.empty_like(x)
             dres = torch.empty_like(x) if ctx.has_res and (ctx.relu or add is not None) else None
-            _T().bn_backward(dy, y, x, mean, rstd, g.master, dx, dres, g.grad, b.grad, ctx.relu, add)
+            _T().bn_backward(dy, y, x, mean, rstd, g.master, dx, dres, g.grad, b.grad, ctx.relu, add,
+                             ctx.bws, False)
             if ctx.has_res and dres is None:
                 dres = dy
         else:
@@ -476,7 +493,7 @@ class _BN(Function):
             dres = dyf.reshape(x.shape).to(BF16) if ctx.has_res else None
         g.grad_ready()
         b.grad_ready()
-        return dx, dres, None, None, None, None, None, None, None, None, None, None, None
+        return dx, dres, None, None, None, None, None, None, None, None, None, None, None, None
 
 
 def _bn_infer_gpu(x, res, scale, shift, relu):
@@ -489,22 +506,54 @@ def _bn_infer_gpu(x, res, scale, shift, relu):
     return yf.to(BF16)
 
 
+class BNWorkspace:
+    """fp64 statistics accumulators of one BatchNorm layer: ``fwd``
+    [BN_SHARDS][2C] (sum | sum of squares of x) and ``bwd`` [BN_SHARDS][2C]
+    (sum(d) | sum(d * xhat)),
+    slices of one model-wide buffer that the model zeroes ONCE per training
+    step (``zero_()``, a single memset node in the captured graph). The
+    producing conv's epilogue, or the BN's own reduction pass, accumulates
+    into them with device-scope atomics; the apply passes derive the
+    per-channel coefficients in their prologue (no finalize launches)."""
+
+    def __init__(self, buf: torch.Tensor, off: int, C: int):
+        n = BN_SHARDS * 2 * C
+        self.fwd = buf[off:off + n]
+        self.bwd = buf[off + n:off + 2 * n]
+
+
+def bn_workspaces(channels: dict, device) -> Tuple[torch.Tensor, dict]:
+    """One zero-initialised fp64 buffer for every BN of a model
+    ({key: C} -> (buffer, {key: BNWorkspace}))."""
+    per = {k: 2 * BN_SHARDS * 2 * c for k, c in channels.items()}
+    buf = torch.zeros(max(sum(per.values()), 1), dtype=torch.float64, device=device)
+    out, off = {}, 0
+    for k, c in channels.items():
+        out[k] = BNWorkspace(buf, off, c)
+        off += per[k]
+    return buf, out
+
+
 def batchnorm(x: torch.Tensor, g: Param, b: Param, run_mean: Optional[torch.Tensor] = None,
               run_var: Optional[torch.Tensor] = None, relu: bool = False,
               residual: Optional[torch.Tensor] = None, eps: float = 1e-5, momentum: float = 0.1,
-              training: bool = True, consumer_masks: bool = False) -> torch.Tensor:
+              training: bool = True, consumer_masks: bool = False,
+              ws: Optional[BNWorkspace] = None) -> torch.Tensor:
     """y = relu(BN(x) + residual) over the last (channel) dim of an NHWC tensor.
 
     ``consumer_masks``: y has exactly one consumer, a ``conv2d(..., in_relu=True)``
     whose dgrad applies the ReLU backward mask (reading y once there instead of
-    twice in this BN's backward passes)."""
+    twice in this BN's backward passes).
+    ``ws``: this layer's statistics workspace, zeroed since its last use
+    (None: zeroed temporaries per call)."""
     if not x.is_contiguous():
         x = x.contiguous()
     if residual is not None and not residual.is_contiguous():
         residual = residual.contiguous()
     slot = GradSlot() if (x.is_cuda and training and torch.is_grad_enabled()) else None
     y = _BN.apply(x, residual, g.arena.token, g, b, run_mean, run_var, relu, eps, momentum,
-                  training, slot, consumer_masks and relu and residual is None)
+                  training, slot, consumer_masks and relu and residual is None,
+                  ws if (x.is_cuda and training) else None)
     if slot is not None:
         y._tam_slot = slot
     return y

@@ -46,11 +46,14 @@ def main():
                     help="model branch streams (GNMT's independent recurrences): -1 model default, 0 off, 1 on")
     ap.add_argument("--lib", type=int, default=0,
                     help="plain-GEMM routing: -1 measured MFMA/hipBLASLt, 0 MFMA only, 1 library")
+    ap.add_argument("--conv_policy", type=int, default=1,
+                    help="conv core: 1 LDS-DMA where the cost model picks it, 2 wherever eligible, 0 igemm only")
     a = ap.parse_args()
     import torch
     from tiresias_amd.ops import _lib
     _lib.load(required=True)
     torch.ops.tam.gemm_lib_policy(a.lib)
+    torch.ops.tam.conv_dma_policy(a.conv_policy)
     res = []
     for m in a.models.split(","):
         r = bench(m, batch=a.batch or None, steps=a.steps, warmup=a.warmup, graph=a.graph,
