@@ -433,7 +433,7 @@ struct CHArgs {
   int tap_oh[9], tap_ow[9], tap_kcol[9];   // patch offsets in [0, 2]
 };
 
-__global__ void __launch_bounds__(256, 2) conv_halo_kernel(CHArgs a, Epi ep) {
+static __global__ void __launch_bounds__(256, 2) conv_halo_kernel(CHArgs a, Epi ep) {
   __shared__ __attribute__((aligned(1024))) char smem[CH_PATCH + 3 * CH_BSLOT];
   char* sp = smem;
   char* sb = smem + CH_PATCH;
