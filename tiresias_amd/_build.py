@@ -48,11 +48,27 @@ def _headers():
     return sorted((CSRC / "include").rglob("*.h"))
 
 
+def _deps(obj: Path):
+    """Headers a TU included at its last compile (the -MMD file next to the
+    object), or None when unknown."""
+    d = obj.with_suffix(".d")
+    if not d.exists():
+        return None
+    txt = d.read_text().replace("\\\n", " ")
+    toks = txt.split(":", 1)[1].split() if ":" in txt else []
+    return [Path(t) for t in toks if t.endswith(".h")]
+
+
 def _needs(obj: Path, src: Path, hdr_mtime: float) -> bool:
     if not obj.exists():
         return True
     m = obj.stat().st_mtime
-    return m < src.stat().st_mtime or m < hdr_mtime
+    if m < src.stat().st_mtime:
+        return True
+    deps = _deps(obj)
+    if deps is None:
+        return m < hdr_mtime
+    return any((not h.exists()) or m < h.stat().st_mtime for h in deps)
 
 
 def build(force: bool = False, jobs: int | None = None, verbose: bool = False) -> Path:
@@ -74,7 +90,8 @@ def build(force: bool = False, jobs: int | None = None, verbose: bool = False) -
         if force or _needs(obj, src, hdr_mtime):
             extra = torch_flags if src.suffix == ".cpp" else []
             lang = ["-x", "hip"] if src.suffix == ".cpp" else []
-            cmds.append([hipcc, *common, *extra, *lang, "-c", str(src), "-o", str(obj)])
+            cmds.append([hipcc, *common, *extra, *lang, "-MMD", "-MF", str(obj.with_suffix(".d")), "-c",
+                         str(src), "-o", str(obj)])
     jobs = jobs or min(8, os.cpu_count() or 4)
     if cmds:
         with cf.ThreadPoolExecutor(max_workers=jobs) as ex:

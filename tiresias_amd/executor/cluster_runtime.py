@@ -1084,8 +1084,12 @@ class Worker:
         if plane is None or rnd is None:
             return {j for j, v in ok.items() if not v}
         pre = f"{plane.prefix}/mv/{rnd}"
+        # every store operation goes through the plane's reconnect-and-retry
+        # (a client socket dropped under host load while a peer dies must not
+        # take a surviving rank down with it)
+        rt = plane._retry
         for jid, v in ok.items():
-            plane.store.set(f"{pre}/{jid}/{self.rank}", b"1" if v else b"0")
+            rt(lambda: plane.store.set(f"{pre}/{jid}/{self.rank}", b"1" if v else b"0"), "move flag")
         bad = set()
         bound = max(30.0, 4.0 * plane.hb_timeout)
         for jid, a in acts.items():
@@ -1094,8 +1098,8 @@ class Worker:
             t0 = time.time()
             verdict = None
             while verdict is None:
-                if plane.store.check([vkey]):
-                    verdict = plane.store.get(vkey)
+                if rt(lambda: plane.store.check([vkey]), "move verdict"):
+                    verdict = rt(lambda: plane.store.get(vkey), "move verdict")
                     break
                 live = [r for r in parts if r not in plane.dead]
                 if live and live[0] == self.rank:
@@ -1106,8 +1110,8 @@ class Worker:
                             if r in plane.dead:
                                 good = False
                                 break
-                            if plane.store.check([k]):
-                                good = good and plane.store.get(k) == b"1"
+                            if rt(lambda: plane.store.check([k]), "move flag"):
+                                good = good and rt(lambda: plane.store.get(k), "move flag") == b"1"
                                 break
                             if time.time() - t0 > bound:
                                 good = False
@@ -1115,10 +1119,11 @@ class Worker:
                             time.sleep(0.001)
                         if not good:
                             break
-                    verdict = plane.store.compare_set(vkey, "", b"1" if good else b"0")
+                    verdict = rt(lambda: plane.store.compare_set(vkey, "", b"1" if good else b"0"),
+                                 "move verdict")
                     break
                 if time.time() - t0 > 4 * bound:      # decider silent far past its own bound
-                    verdict = plane.store.compare_set(vkey, "", b"0")
+                    verdict = rt(lambda: plane.store.compare_set(vkey, "", b"0"), "move verdict")
                     break
                 time.sleep(0.001)
             if verdict != b"1":
