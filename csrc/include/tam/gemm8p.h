@@ -417,6 +417,28 @@ gemm8p_kernel(P8Args a, Epi ep) {
   }
 }
 
+// One launcher per kernel variant. Each production variant (SCHED 4) is
+// explicitly instantiated in a translation unit of its own
+// (csrc/kernels/gemm8p_*.hip): co-compiled instantiations of one kernel
+// template share register-allocation context and perturb each other's code
+// (cdna_hip_programming.md §5.4 rule 19); the A/B schedules live together in
+// gemm8p_alt.hip.
+template <int BM, int BN, int WNW, bool AK, bool BK, int SCHED>
+void p8_launch_one(const P8Args& g, const Epi& ep, dim3 grid, hipStream_t s) {
+  hipLaunchKernelGGL((gemm8p_kernel<BM, BN, WNW, AK, BK, SCHED>), grid, dim3(P8Geo<BM, BN, WNW>::THREADS), 0, s,
+                     g, ep);
+}
+
+#define TAM_P8_VARIANTS(X, SCHED)                                                              \
+  X(256, 256, 4, true, true, SCHED) X(256, 256, 4, true, false, SCHED)                           \
+  X(256, 256, 4, false, true, SCHED) X(256, 256, 4, false, false, SCHED)                         \
+  X(128, 128, 2, true, true, SCHED) X(128, 128, 2, true, false, SCHED)                           \
+  X(128, 128, 2, false, true, SCHED) X(128, 128, 2, false, false, SCHED)
+#define TAM_P8_EXTERN(BM, BN, W, AK, BK, S) \
+  extern template void p8_launch_one<BM, BN, W, AK, BK, S>(const P8Args&, const Epi&, dim3, hipStream_t);
+#define TAM_P8_INST(BM, BN, W, AK, BK, S) \
+  template void p8_launch_one<BM, BN, W, AK, BK, S>(const P8Args&, const Epi&, dim3, hipStream_t);
+
 // shape / layout conditions of the LDS-DMA kernels (tile >= 128)
 inline bool gemm8p_ok(bool ak, bool bk, int M, int N, int K, long lda, long ldb) {
   if (K % P8_BK != 0 || K < P8_BK || M < 128 || N < 128) return false;

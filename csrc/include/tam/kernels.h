@@ -9,8 +9,10 @@ namespace tam {
 // BatchNorm (NHWC rows=M=N*H*W, C channels, C % 8 == 0, C <= 2048).
 // Statistics: fp64 sums[BN_SHARDS][2C] (norm.hip), zeroed by the caller;
 // sums_ready: the producer (a conv epilogue) already accumulated them -- no
-// reduction pass here. part: BN_MAX_BLOCKS * 2C floats of scratch for the
-// reduction pass's partial rows.
+// reduction pass here (else one pass adds them with sharded fp64 atomics).
+// ymask (relu BNs): forward stores 1 bit per output (y > 0, byte (r*C+c)/8,
+// bit c%8); backward given ymask (and y == nullptr) masks with the bits
+// instead of re-reading the bf16 y -- 1/16 of the bytes.
 constexpr int BN_MAX_BLOCKS = 512;
 constexpr int LN_MAX_BLOCKS = 512;
 constexpr int COLSUM_MAX_BLOCKS = 256;
@@ -22,7 +24,7 @@ void col_reduce_acc(const float* part, int nblk, int W, float* out0, float* out1
 void bn_forward(const bf16_t* x, const bf16_t* res, bf16_t* y, long M, int C, float eps,
                 float momentum, const float* gamma, const float* beta, float* run_mean,
                 float* run_var, float* save_mean, float* save_rstd, int relu, double* sums,
-                int sums_ready, float* part, hipStream_t s);
+                int sums_ready, uint8_t* ymask, hipStream_t s);
 void bn_infer(const bf16_t* x, const bf16_t* res, bf16_t* y, long M, int C, const float* scale,
               const float* shift, int relu, hipStream_t s);
 // batched conv weight re-layout [K][RS][C] -> [C][RS][K] (one launch)
@@ -44,8 +46,8 @@ void conv_weight_t_batch(WTBatch& b, hipStream_t s);
 // ReLU mask)
 void bn_backward(const bf16_t* dy, const bf16_t* addend, const bf16_t* y, const bf16_t* x, const float* mean,
                  const float* rstd, const float* gamma, long M, int C, int relu, bf16_t* dx,
-                 bf16_t* dres, float* dgamma, float* dbeta, double* sums, int sums_ready, float* part,
-                 hipStream_t s);
+                 bf16_t* dres, float* dgamma, float* dbeta, double* sums, int sums_ready,
+                 const uint8_t* ymask, hipStream_t s);
 
 // LayerNorm over last dim D (D % 8 == 0, D <= 2048)
 void ln_forward(const bf16_t* x, const float* g, const float* b, bf16_t* y, float* mean,
@@ -77,6 +79,7 @@ void embedding_backward(const bf16_t* dout, const long* ids, float* gtable, long
 // misc
 // out[c] += sum_r x[r][c]; ws: COLSUM_MAX_BLOCKS * C floats (C % 8 == 0 path)
 void colsum(const bf16_t* x, float* out, float* ws, long R, int C, hipStream_t s);
+void colsum_policy(int p);   // 0 auto, 1 partial rows + reduce, 2 atomics (A/B)
 void relu_backward(const bf16_t* dy, const bf16_t* y, bf16_t* dx, long n, hipStream_t s);
 void add_bf16(const bf16_t* a, const bf16_t* b, bf16_t* y, long n, hipStream_t s);
 void cast_f32_bf16(const float* x, bf16_t* y, long n, hipStream_t s);

@@ -95,15 +95,21 @@ void gemm8p_policy(int mode, int sched) {
   g_p8_tile = sched >= 200 ? 256 : sched >= 100 ? 128 : 0;    // tests: sched + 100 / + 200
 }
 
+TAM_P8_VARIANTS(TAM_P8_EXTERN, 0)
+TAM_P8_VARIANTS(TAM_P8_EXTERN, 1)
+TAM_P8_VARIANTS(TAM_P8_EXTERN, 2)
+TAM_P8_VARIANTS(TAM_P8_EXTERN, 3)
+TAM_P8_VARIANTS(TAM_P8_EXTERN, 4)
+TAM_P8_VARIANTS(TAM_P8_EXTERN, 5)
+
 template <int BM, int BN, int WNW, bool AK, bool BK>
 static void p8_launch_t(const P8Args& g, const Epi& ep, dim3 grid, int sched, hipStream_t s) {
-  constexpr int T = P8Geo<BM, BN, WNW>::THREADS;
-  if (sched == 5) hipLaunchKernelGGL((gemm8p_kernel<BM, BN, WNW, AK, BK, 5>), grid, dim3(T), 0, s, g, ep);
-  else if (sched == 4) hipLaunchKernelGGL((gemm8p_kernel<BM, BN, WNW, AK, BK, 4>), grid, dim3(T), 0, s, g, ep);
-  else if (sched == 3) hipLaunchKernelGGL((gemm8p_kernel<BM, BN, WNW, AK, BK, 3>), grid, dim3(T), 0, s, g, ep);
-  else if (sched == 2) hipLaunchKernelGGL((gemm8p_kernel<BM, BN, WNW, AK, BK, 2>), grid, dim3(T), 0, s, g, ep);
-  else if (sched == 1) hipLaunchKernelGGL((gemm8p_kernel<BM, BN, WNW, AK, BK, 1>), grid, dim3(T), 0, s, g, ep);
-  else hipLaunchKernelGGL((gemm8p_kernel<BM, BN, WNW, AK, BK, 0>), grid, dim3(T), 0, s, g, ep);
+  if (sched == 5) p8_launch_one<BM, BN, WNW, AK, BK, 5>(g, ep, grid, s);
+  else if (sched == 4) p8_launch_one<BM, BN, WNW, AK, BK, 4>(g, ep, grid, s);
+  else if (sched == 3) p8_launch_one<BM, BN, WNW, AK, BK, 3>(g, ep, grid, s);
+  else if (sched == 2) p8_launch_one<BM, BN, WNW, AK, BK, 2>(g, ep, grid, s);
+  else if (sched == 1) p8_launch_one<BM, BN, WNW, AK, BK, 1>(g, ep, grid, s);
+  else p8_launch_one<BM, BN, WNW, AK, BK, 0>(g, ep, grid, s);
 }
 
 template <int BM, int BN, int WNW>
@@ -218,7 +224,8 @@ void gemm_select(const bf16_t* A, long lda, bool ak, const bf16_t* B, long ldb, 
                  int N, int K, Epi ep, bool allow_split, hipStream_t s, int path) {
   if (M <= 0 || N <= 0) return;
   const bool can_split = allow_split && ep.c_f32 && !ep.relu && !ep.mask;
-  if (g_p8 > 0 && g_force_cfg < 0 && gemm8p_ok(ak, bk, M, N, K, lda, ldb)) {
+  // (Epi::colsum_a is an igemm-only epilogue: no LDS-DMA kernels then)
+  if (g_p8 > 0 && g_force_cfg < 0 && !ep.colsum_a && gemm8p_ok(ak, bk, M, N, K, lda, ldb)) {
     const long t8 = (long)cdiv(M, 256) * cdiv(N, 256);
     const double flop = 2.0 * M * N * K;
     if (g_p8 >= 2 || path == 3 || (t8 >= 48 && K >= 512 && flop >= 4e9)) {
@@ -235,9 +242,9 @@ void gemm_select(const bf16_t* A, long lda, bool ak, const bf16_t* B, long ldb, 
   if (g_force_splits >= 1) t.splits = can_split ? g_force_splits : 1;
   // 256x256 LDS-DMA kernel for large K-major x K-major problems
   const long t256 = (long)cdiv(M, 256) * cdiv(N, 256);
-  const bool big = gemm256_ok(ak, bk, M, N, K, lda, ldb) &&
+  const bool big = !ep.colsum_a && gemm256_ok(ak, bk, M, N, K, lda, ldb) &&
                    (t.cfg == 4 || (g_force_cfg < 0 && t256 >= 192 && K >= 1024));
-  if (!big && path == 2 && g_force_cfg < 0 && gemm_dma_ok(A, lda, ak, B, ldb, bk, M, N, K, ep)) {
+  if (!big && path == 2 && g_force_cfg < 0 && !ep.colsum_a && gemm_dma_ok(A, lda, ak, B, ldb, bk, M, N, K, ep)) {
     GdChoice c = gemm_dma_choose(M, N, K, can_split);
     if (g_dma_cfg >= 0) c.cfg = g_dma_cfg;
     if (g_force_splits >= 1) c.splits = can_split ? g_force_splits : 1;

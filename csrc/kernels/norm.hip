@@ -82,40 +82,12 @@ void col_reduce_acc(const float* part, int nblk, int W, float* out0, float* out1
 //     finish spread over the conv, and the shards keep the adders per address
 //     low (same-address fp64 atomics serialise at the memory side: 512
 //     simultaneous adders per address measured +85 us on a 13 us pass);
-//   * this file's reduction passes (all blocks finish together) write per-
-//     block partial rows and one column-reduce launch stores shard 0.
+//   * this file's reduction passes (<= BN_MAX_BLOCKS blocks) add each
+//     block's column sums the same way into shard blockIdx % BN_SHARDS
+//     (<= 32 adders per address; no partial rows, no column-reduce launch).
 // fp64 keeps E[x^2] - E[x]^2 from cancelling at N*H*W ~ 10^5-10^6. The
 // caller zeroes sums beforehand (one fill per training step for all of a
 // model's BNs).
-
-// sums[0][c] = sum over nblk partial rows part[b][c] (width W = 2C), fp64;
-// 16 columns x 64 row lanes, 4 rows in flight per lane (latency-bound)
-__global__ void __launch_bounds__(1024) bn_col_sums_kernel(const float* __restrict__ part, int nblk,
-                                                           int W, double* __restrict__ sums) {
-  constexpr int RL = 64;
-  __shared__ double red[RL][17];
-  const int cx = threadIdx.x & 15, ly = threadIdx.x >> 4;
-  const int c = blockIdx.x * 16 + cx;
-  double acc = 0.0;
-  if (c < W) {
-    int b = ly;
-    for (; b + 3 * RL < nblk; b += 4 * RL) {
-      float v[4];
-#pragma unroll
-      for (int u = 0; u < 4; ++u) v[u] = part[(long)(b + u * RL) * W + c];
-#pragma unroll
-      for (int u = 0; u < 4; ++u) acc += (double)v[u];
-    }
-    for (; b < nblk; b += RL) acc += (double)part[(long)b * W + c];
-  }
-  red[ly][cx] = acc;
-  __syncthreads();
-  if (ly != 0 || c >= W) return;
-  double t = 0.0;
-#pragma unroll 8
-  for (int k = 0; k < RL; ++k) t += red[k][cx];
-  sums[c] = t;
-}
 
 // a channel's (S, Q) over the shards
 __device__ __forceinline__ void bn_shard_sum(const double* __restrict__ sums, int C, int c, double& S,
@@ -131,10 +103,28 @@ __device__ __forceinline__ void bn_shard_sum(const double* __restrict__ sums, in
   for (int k = 0; k < BN_SHARDS; ++k) { S += s[k]; Q += q[k]; }
 }
 
+// a reducing block's 2C column sums (held by its row-lane-0 threads, 8
+// channels each) -> LDS -> no-return fp64 atomics into shard blockIdx %
+// BN_SHARDS (<= 32 adders per address at BN_MAX_BLOCKS blocks), issued by
+// every thread over CONTIGUOUS addresses (512 B per wave instruction; the
+// per-thread 8-channel strided form measured 1.75x slower on ResNet-50's
+// backward reductions)
+__device__ __forceinline__ void bn_block_atomics(float* red, const float (&s)[8], const float (&q)[8], bool owner,
+                                                 int cg, int C, double* __restrict__ sums) {
+  __syncthreads();                       // red's partial rows are consumed
+  if (owner) {
+#pragma unroll
+    for (int i = 0; i < 8; ++i) { red[cg * 8 + i] = s[i]; red[C + cg * 8 + i] = q[i]; }
+  }
+  __syncthreads();
+  double* sh = sums + (long)(blockIdx.x % BN_SHARDS) * 2 * C;
+  for (int e = threadIdx.x; e < 2 * C; e += blockDim.x) unsafeAtomicAdd(sh + e, (double)red[e]);
+}
+
 // grid.x blocks each own a contiguous row range; thread = (row lane, 8-ch group)
 __global__ void __launch_bounds__(256) bn_stats_kernel(const bf16_t* __restrict__ x, long M, int C,
                                                         long rows_per_block,
-                                                        float* __restrict__ part) {
+                                                        double* __restrict__ sums) {
   __shared__ float red[256 * 16];
   const int tpr = C / 8;                 // threads per row
   const int rpb = 256 / tpr;             // rows per pass (C <= 2048)
@@ -176,12 +166,8 @@ __global__ void __launch_bounds__(256) bn_stats_kernel(const bf16_t* __restrict_
 #pragma unroll
       for (int i = 0; i < 8; ++i) { s[i] += red[t * 16 + i]; q[i] += red[t * 16 + 8 + i]; }
     }
-    // one partial row per block: no atomics, deterministic
-    float* ps = part + (long)blockIdx.x * 2 * C + cg * 8;
-    float* pq = ps + C;
-#pragma unroll
-    for (int i = 0; i < 8; ++i) { ps[i] = s[i]; pq[i] = q[i]; }
   }
+  bn_block_atomics(red, s, q, rl == 0, cg, C, sums);
 }
 
 // Apply passes run over a 2-D grid: blockIdx.y = a slab of <= BN_SLAB
@@ -215,7 +201,7 @@ __global__ void __launch_bounds__(256) bn_apply_kernel(
     int C, long rows_per_block, const double* __restrict__ sums, const float* __restrict__ gamma,
     const float* __restrict__ beta, float eps, float momentum, float* __restrict__ save_mean,
     float* __restrict__ save_rstd, float* __restrict__ run_mean, float* __restrict__ run_var,
-    int relu) {
+    int relu, uint8_t* __restrict__ ymask) {
   __shared__ float s_sc[BN_SLAB], s_sh[BN_SLAB];
   const int c0 = blockIdx.y * BN_SLAB;
   const int cs = min(BN_SLAB, C - c0);
@@ -259,7 +245,20 @@ __global__ void __launch_bounds__(256) bn_apply_kernel(
       if (relu) o = fmaxf(o, 0.f);
       f[j] = o;
     }
-    *(uint4*)(y + off) = pack8(f);
+    const uint4 pk = pack8(f);
+    *(uint4*)(y + off) = pk;
+    if (ymask) {
+      // bit j of byte off/8: the STORED bf16 of channel col+j is > 0 (what a
+      // ReLU backward reading y would test)
+      const uint32_t w[4] = {pk.x, pk.y, pk.z, pk.w};
+      uint32_t bits = 0;
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        bits |= (((w[e] & 0x8000u) == 0 && (w[e] & 0x7fffu) != 0) ? 1u : 0u) << (2 * e);
+        bits |= (((w[e] & 0x80000000u) == 0 && (w[e] & 0x7fff0000u) != 0) ? 1u : 0u) << (2 * e + 1);
+      }
+      ymask[off >> 3] = (uint8_t)bits;
+    }
   };
   const uint4 z = make_uint4(0, 0, 0, 0);
   const long r0 = blockIdx.x * rows_per_block, r1 = min(M, r0 + rows_per_block);
@@ -280,13 +279,14 @@ __global__ void __launch_bounds__(256) bn_apply_kernel(
 
 // ---------------------------------------------------------------- BN backward
 // dyr = (dy + addend) * (y > 0 if relu); accum sum(dyr), sum(dyr * xhat) per
-// channel (one partial row per block). dp_out (residual BNs): dyr is also stored -- it IS the
+// channel (sharded fp64 atomics). dp_out (residual BNs): dyr is also stored -- it IS the
 // residual branch's gradient, and the apply pass then reads dyr + x only (no
 // dy, addend, y re-reads, no second dres write: 2 passes of the tensor saved)
 __global__ void __launch_bounds__(256) bn_bwd_reduce_kernel(
     const bf16_t* __restrict__ dy, const bf16_t* __restrict__ addend, const bf16_t* __restrict__ y,
     const bf16_t* __restrict__ x, const float* __restrict__ mean, const float* __restrict__ rstd, long M,
-    int C, long rows_per_block, int relu, float* __restrict__ part, bf16_t* __restrict__ dp_out) {
+    int C, long rows_per_block, int relu, double* __restrict__ sums, bf16_t* __restrict__ dp_out,
+    const uint8_t* __restrict__ ymask) {
   __shared__ float red[256 * 16];
   const int tpr = C / 8, rpb = 256 / tpr;
   const int cg = threadIdx.x % tpr, rl = threadIdx.x / tpr;
@@ -296,7 +296,8 @@ __global__ void __launch_bounds__(256) bn_bwd_reduce_kernel(
   const long r0 = blockIdx.x * rows_per_block;
   const long r1 = min(M, r0 + rows_per_block);
   // one row of 8 channels: (dy + addend) masked by y, accumulated; dyr stored
-  auto row = [&](const long off, const uint4 vd, const uint4 vx, const uint4 vy, const uint4 va) {
+  auto row = [&](const long off, const uint4 vd, const uint4 vx, const uint4 vy, const uint4 va,
+                 const uint32_t vm) {
     float fd[8], fx[8];
     unpack8(vd, fd);
     unpack8(vx, fx);
@@ -306,7 +307,10 @@ __global__ void __launch_bounds__(256) bn_bwd_reduce_kernel(
 #pragma unroll
       for (int i = 0; i < 8; ++i) fd[i] += fa[i];
     }
-    if (relu) {
+    if (relu && ymask) {
+#pragma unroll
+      for (int i = 0; i < 8; ++i) fd[i] = (vm >> i) & 1u ? fd[i] : 0.f;
+    } else if (relu) {
       float fy[8];
       unpack8(vy, fy);
 #pragma unroll
@@ -327,21 +331,24 @@ __global__ void __launch_bounds__(256) bn_bwd_reduce_kernel(
     constexpr int U = 4;
     for (; r + (U - 1) * rpb < r1; r += U * rpb) {
       uint4 vd[U], vx[U], vy[U], va[U];
+      uint32_t vm[U];
 #pragma unroll
       for (int u = 0; u < U; ++u) {
         const long off = (r + u * rpb) * C + cg * 8;
         vd[u] = *(const uint4*)(dy + off);
         vx[u] = *(const uint4*)(x + off);
-        vy[u] = relu ? *(const uint4*)(y + off) : z;
+        vy[u] = relu && y ? *(const uint4*)(y + off) : z;
         va[u] = addend ? *(const uint4*)(addend + off) : z;
+        vm[u] = relu && ymask ? ymask[off >> 3] : 0u;
       }
 #pragma unroll
-      for (int u = 0; u < U; ++u) row((r + u * rpb) * C + cg * 8, vd[u], vx[u], vy[u], va[u]);
+      for (int u = 0; u < U; ++u) row((r + u * rpb) * C + cg * 8, vd[u], vx[u], vy[u], va[u], vm[u]);
     }
     for (; r < r1; r += rpb) {
       const long off = r * C + cg * 8;
       row(off, *(const uint4*)(dy + off), *(const uint4*)(x + off),
-          relu ? *(const uint4*)(y + off) : z, addend ? *(const uint4*)(addend + off) : z);
+          relu && y ? *(const uint4*)(y + off) : z, addend ? *(const uint4*)(addend + off) : z,
+          relu && ymask ? ymask[off >> 3] : 0u);
     }
   }
 #pragma unroll
@@ -353,11 +360,8 @@ __global__ void __launch_bounds__(256) bn_bwd_reduce_kernel(
 #pragma unroll
       for (int i = 0; i < 8; ++i) { a[i] += red[t * 16 + i]; b[i] += red[t * 16 + 8 + i]; }
     }
-    float* pa = part + (long)blockIdx.x * 2 * C + cg * 8;
-    float* pb = pa + C;
-#pragma unroll
-    for (int i = 0; i < 8; ++i) { pa[i] = a[i]; pb[i] = b[i]; }
   }
+  bn_block_atomics(red, a, b, rl == 0, cg, C, sums);
 }
 
 // dx = g*rstd*(dyr - S/M - xhat*Q/M) = k1*dyr + k2*xhat + k3 with S, Q from
@@ -367,7 +371,7 @@ __global__ void __launch_bounds__(256) bn_bwd_apply_kernel(
     const bf16_t* __restrict__ x, long M, int C, long rows_per_block, const double* __restrict__ sums,
     const float* __restrict__ mean, const float* __restrict__ rstd, const float* __restrict__ gamma,
     float* __restrict__ dgamma, float* __restrict__ dbeta, bf16_t* __restrict__ dx,
-    bf16_t* __restrict__ dres, int relu) {
+    bf16_t* __restrict__ dres, int relu, const uint8_t* __restrict__ ymask) {
   __shared__ float s_k[4][BN_SLAB];     // k1, k2, k3, mean
   const int c0 = blockIdx.y * BN_SLAB;
   const int cs = min(BN_SLAB, C - c0);
@@ -397,7 +401,8 @@ __global__ void __launch_bounds__(256) bn_bwd_apply_kernel(
   for (int j = 0; j < 8; ++j) {
     k1[j] = s_k[0][v * 8 + j]; k2[j] = s_k[1][v * 8 + j]; k3[j] = s_k[2][v * 8 + j]; mu[j] = s_k[3][v * 8 + j];
   }
-  auto one = [&](const long off, const uint4 vd, const uint4 vx, const uint4 vy, const uint4 va) {
+  auto one = [&](const long off, const uint4 vd, const uint4 vx, const uint4 vy, const uint4 va,
+                 const uint32_t vm) {
     float fd[8], fx[8];
     unpack8(vd, fd);
     unpack8(vx, fx);
@@ -407,7 +412,10 @@ __global__ void __launch_bounds__(256) bn_bwd_apply_kernel(
 #pragma unroll
       for (int j = 0; j < 8; ++j) fd[j] += fa[j];
     }
-    if (relu) {
+    if (relu && ymask) {
+#pragma unroll
+      for (int j = 0; j < 8; ++j) fd[j] = (vm >> j) & 1u ? fd[j] : 0.f;
+    } else if (relu) {
       float fy[8];
       unpack8(vy, fy);
 #pragma unroll
@@ -425,21 +433,23 @@ __global__ void __launch_bounds__(256) bn_bwd_apply_kernel(
   long r = r0 + rl;
   for (; r + rpp < r1; r += 2 * rpp) {
     uint4 vd[2], vx[2], vy[2], va[2];
+    uint32_t vm[2];
 #pragma unroll
     for (int u = 0; u < 2; ++u) {
       const long off = (r + u * rpp) * C + col;
       vd[u] = *(const uint4*)(dy + off);
       vx[u] = *(const uint4*)(x + off);
-      vy[u] = relu ? *(const uint4*)(y + off) : z;
+      vy[u] = relu && y ? *(const uint4*)(y + off) : z;
       va[u] = addend ? *(const uint4*)(addend + off) : z;
+      vm[u] = relu && ymask ? ymask[off >> 3] : 0u;
     }
 #pragma unroll
-    for (int u = 0; u < 2; ++u) one((r + u * rpp) * C + col, vd[u], vx[u], vy[u], va[u]);
+    for (int u = 0; u < 2; ++u) one((r + u * rpp) * C + col, vd[u], vx[u], vy[u], va[u], vm[u]);
   }
   if (r < r1) {
     const long off = r * C + col;
-    one(off, *(const uint4*)(dy + off), *(const uint4*)(x + off), relu ? *(const uint4*)(y + off) : z,
-        addend ? *(const uint4*)(addend + off) : z);
+    one(off, *(const uint4*)(dy + off), *(const uint4*)(x + off), relu && y ? *(const uint4*)(y + off) : z,
+        addend ? *(const uint4*)(addend + off) : z, relu && ymask ? ymask[off >> 3] : 0u);
   }
 }
 
@@ -455,18 +465,16 @@ static long bn_rows_per_block(long M, int C) {
 void bn_forward(const bf16_t* x, const bf16_t* res, bf16_t* y, long M, int C, float eps,
                 float momentum, const float* gamma, const float* beta, float* run_mean,
                 float* run_var, float* save_mean, float* save_rstd, int relu, double* sums,
-                int sums_ready, float* part, hipStream_t s) {
+                int sums_ready, uint8_t* ymask, hipStream_t s) {
   if (!sums_ready) {
     const long rpb = bn_rows_per_block(M, C);
     const int nb = (int)((M + rpb - 1) / rpb);
-    hipLaunchKernelGGL(bn_stats_kernel, dim3(nb), dim3(256), 0, s, x, M, C, rpb, part);
-    hipLaunchKernelGGL(bn_col_sums_kernel, dim3((2 * C + 15) / 16), dim3(1024), 0, s, (const float*)part,
-                       nb, 2 * C, sums);
+    hipLaunchKernelGGL(bn_stats_kernel, dim3(nb), dim3(256), 0, s, x, M, C, rpb, sums);
   }
   const BnGrid g = bn_apply_grid(M, C);
   hipLaunchKernelGGL(bn_apply_kernel, g.grid, dim3(256), 0, s, x, res, y, M, C, g.rows_per_block,
                      (const double*)sums, gamma, beta, eps, momentum, save_mean, save_rstd, run_mean,
-                     run_var, relu);
+                     run_var, relu, ymask);
 }
 
 // inference: scale / shift given (no statistics)
@@ -507,20 +515,19 @@ void bn_infer(const bf16_t* x, const bf16_t* res, bf16_t* y, long M, int C, cons
 void bn_backward(const bf16_t* dy, const bf16_t* addend, const bf16_t* y, const bf16_t* x,
                  const float* mean, const float* rstd, const float* gamma, long M, int C, int relu,
                  bf16_t* dx, bf16_t* dres, float* dgamma, float* dbeta, double* sums,
-                 int sums_ready, float* part, hipStream_t s) {
+                 int sums_ready, const uint8_t* ymask, hipStream_t s) {
   if (!sums_ready) {
     // residual BN: the reduce pass materialises dyr into dres; the apply pass
     // then runs on (dres, x) as a plain BN backward
     const long rpb = bn_rows_per_block(M, C);
     const int nb = (int)((M + rpb - 1) / rpb);
     hipLaunchKernelGGL(bn_bwd_reduce_kernel, dim3(nb), dim3(256), 0, s, dy, addend, y, x, mean, rstd, M,
-                       C, rpb, relu, part, dres);
-    hipLaunchKernelGGL(bn_col_sums_kernel, dim3((2 * C + 15) / 16), dim3(1024), 0, s, (const float*)part,
-                       nb, 2 * C, sums);
+                       C, rpb, relu, sums, dres, ymask);
     if (dres) {
       dy = dres;
       addend = nullptr;
       y = nullptr;
+      ymask = nullptr;
       relu = 0;
       dres = nullptr;
     }
@@ -528,7 +535,7 @@ void bn_backward(const bf16_t* dy, const bf16_t* addend, const bf16_t* y, const 
   const BnGrid g = bn_apply_grid(M, C);
   hipLaunchKernelGGL(bn_bwd_apply_kernel, g.grid, dim3(256), 0, s, dy, addend, y, x, M, C,
                      g.rows_per_block, (const double*)sums, mean, rstd, gamma, dgamma, dbeta, dx, dres,
-                     relu);
+                     relu, ymask);
 }
 
 // ---------------------------------------------------------------- LayerNorm

@@ -423,9 +423,29 @@ __global__ void __launch_bounds__(256) colsum8_kernel(const bf16_t* __restrict__
   }
 }
 
+// 0 (default): tiny matrices (R*C <= COLSUM_ATOMIC_MAX) in ONE launch --
+// <= 64 row blocks add their column sums straight into out (fp32 atomics),
+// the rest as partial rows + column reduce; 1: always partial rows; 2:
+// always atomics. Measured (tools/ab_colsum.py, profiles/r3/s3/ab_colsum.json):
+// atomics 3.4 vs 5.1 us at 64x1000 but 15 vs 5 us at 4096x512 and 2-3x
+// slower on every larger shape
+static int g_colsum = [] {
+  const char* e = getenv("TAM_COLSUM");
+  return e ? atoi(e) : 0;
+}();
+void colsum_policy(int p) { g_colsum = p; }
+constexpr long COLSUM_ATOMIC_MAX = 1L << 17;
+
 void colsum(const bf16_t* x, float* out, float* ws, long R, int C, hipStream_t s) {
   if (C % 8 == 0) {
     const int bx = (C + 2047) / 2048;
+    if (g_colsum == 2 || (g_colsum == 0 && R * C <= COLSUM_ATOMIC_MAX)) {
+      long rpb = (R + 63) / 64;
+      if (rpb < 32) rpb = 32;
+      const long by = (R + rpb - 1) / rpb;
+      hipLaunchKernelGGL(colsum8_kernel, dim3(bx, by), dim3(256), 0, s, x, (float*)nullptr, R, C, rpb, out);
+      return;
+    }
     // >= ~512 blocks in flight, >= 32 rows each, <= COLSUM_MAX_BLOCKS partial rows
     long by = (512 + bx - 1) / bx;
     if (by > COLSUM_MAX_BLOCKS) by = COLSUM_MAX_BLOCKS;
