@@ -134,10 +134,23 @@ float time_ms(hipStream_t s, const std::function<void()>& fn) {
   return ms / 3.f;
 }
 
+// routing (tuned per shape) + launch of one GEMM whose epilogue is set up
+void gemm_dispatch(const Tensor& a, bool a_kmajor, const Tensor& b, bool b_kmajor, const Tensor& c,
+                   int64_t mode, const optional<Tensor>& bias, bool relu, double alpha, bool allow_split,
+                   int64_t M, int64_t N, int64_t K, const tam::Epi& ep);
+
+// the bias-gradient fusion (Epi::colsum_a) runs on the register-staged igemm
+// only: fuse when that is the routed path, or when it is at most this much
+// slower than the routed one (a separate column-sum pass costs ~5-9 us on the
+// Transformer's shapes, profiles/r3/s3/ab_colsum.json)
+constexpr float COLSUM_FUSE_SLACK_MS = 0.005f;
+
 // a: (M,K) if a_kmajor else (K,M); b: (N,K) if b_kmajor else (K,N); c: (M,N)
+// colsum (M-major A only): colsum[m] += sum_k A[k][m] (fp32) -- the bias
+// gradient of a Linear layer whose weight gradient this GEMM computes
 void gemm_op(const Tensor& a, bool a_kmajor, const Tensor& b, bool b_kmajor, const Tensor& c,
              int64_t mode, const optional<Tensor>& bias, bool relu, const optional<Tensor>& mask,
-             double alpha, bool allow_split) {
+             double alpha, bool allow_split, const optional<Tensor>& colsum) {
   check_bf16(a, "a");
   check_bf16(b, "b");
   check_dev(c, "c");
@@ -176,6 +189,45 @@ void gemm_op(const Tensor& a, bool a_kmajor, const Tensor& b, bool b_kmajor, con
     ep.ldm = mask->stride(0);
   }
   ep.alpha = (float)alpha;
+  if (colsum.has_value() && colsum->defined()) {
+    TORCH_CHECK(!a_kmajor, "tam.gemm: colsum needs an M-major A");
+    check_f32(*colsum, "colsum");
+    TORCH_CHECK(colsum->numel() == M && colsum->is_contiguous(), "tam.gemm: colsum size");
+    const GemmKey key{M, N, K, a_kmajor, b_kmajor, mode, (bool)ep.c_f32, bias.has_value() && bias->defined()};
+    bool fuse = false;
+    {
+      std::lock_guard<std::mutex> g(g_route_mu);
+      auto it = g_route.find(key);
+      if (it != g_route.end()) {
+        const auto t = g_route_ms[key];
+        fuse = it->second == 0 || t[0] <= t[it->second] + COLSUM_FUSE_SLACK_MS;
+      }
+    }
+    // shapes gemm_dispatch never tunes go straight to the igemm anyway
+    const double mnk = (double)M * N * K;
+    const bool tuned = (g_lib_policy != 0 && mnk >= (double)(1 << 27)) ||
+                       (g_dma_policy == 1 && K % 64 == 0 && mnk >= (double)(1 << 24)) ||
+                       (tam::gemm8p_policy_mode() == 1 && mnk >= (double)(1 << 27) &&
+                        tam::gemm8p_ok(a_kmajor, b_kmajor, (int)M, (int)N, (int)K, a.stride(0), b.stride(0)));
+    if (!tuned) fuse = true;
+    if (fuse && !g_forced && tam::gemm8p_policy_mode() != 3 && g_dma_policy != 2) {
+      ep.colsum_a = colsum->data_ptr<float>();
+      run_mfma(a, a_kmajor, b, b_kmajor, M, N, K, ep, allow_split, 0);
+      return;
+    }
+    // not fused (first, tuning call of a shape, or a faster non-igemm route):
+    // the GEMM as routed, then the column sums as their own pass over A
+    gemm_dispatch(a, a_kmajor, b, b_kmajor, c, mode, bias, relu, alpha, allow_split, M, N, K, ep);
+    Tensor ws = at::empty({M % 8 == 0 ? (int64_t)tam::COLSUM_MAX_BLOCKS * M : 1}, a.options().dtype(at::kFloat));
+    tam::colsum(bp(a), colsum->data_ptr<float>(), ws.data_ptr<float>(), K, (int)M, cur_stream(a));
+    return;
+  }
+  gemm_dispatch(a, a_kmajor, b, b_kmajor, c, mode, bias, relu, alpha, allow_split, M, N, K, ep);
+}
+
+void gemm_dispatch(const Tensor& a, bool a_kmajor, const Tensor& b, bool b_kmajor, const Tensor& c,
+                   int64_t mode, const optional<Tensor>& bias, bool relu, double alpha, bool allow_split,
+                   int64_t M, int64_t N, int64_t K, const tam::Epi& ep) {
   const bool has_bias = ep.bias != nullptr;
   const bool lib_ok = g_lib_policy != 0 && !g_forced && !relu && ep.mask == nullptr && alpha == 1.0 &&
                       (mode == 0 || (mode == 1 && ep.c_f32)) && !(has_bias && ep.c_f32) &&
@@ -485,7 +537,7 @@ void bn_forward_op(const Tensor& x, const optional<Tensor>& res, const Tensor& y
                    const Tensor& beta, const optional<Tensor>& run_mean,
                    const optional<Tensor>& run_var, const Tensor& save_mean,
                    const Tensor& save_rstd, double eps, double momentum, bool relu,
-                   const optional<Tensor>& sums, bool sums_ready) {
+                   const optional<Tensor>& sums, bool sums_ready, const optional<Tensor>& ymask) {
   check_bf16(x, "x"); check_bf16(y, "y"); check_contig(x, "x"); check_contig(y, "y");
   check_f32(gamma, "gamma"); check_f32(beta, "beta");
   const int64_t C = x.size(-1);
@@ -493,27 +545,36 @@ void bn_forward_op(const Tensor& x, const optional<Tensor>& res, const Tensor& y
   TORCH_CHECK(C % 8 == 0 && C <= 2048, "tam.bn: C must be a multiple of 8 and <= 2048");
   TORCH_CHECK(!sums_ready || (sums.has_value() && sums->defined()), "tam.bn_forward: sums_ready without sums");
   if (res.has_value() && res->defined()) { check_bf16(*res, "res"); check_contig(*res, "res"); }
-  Tensor tmp, part;
+  Tensor tmp;
   double* sp = bn_sums(sums, x, C, tmp, "tam.bn_forward");
-  if (!sums_ready) part = at::empty({2 * tam::BN_MAX_BLOCKS * C}, x.options().dtype(at::kFloat));
+  uint8_t* mp = nullptr;
+  if (ymask.has_value() && ymask->defined()) {
+    TORCH_CHECK(relu && ymask->is_cuda() && ymask->scalar_type() == at::kByte && ymask->is_contiguous() &&
+                ymask->numel() == x.numel() / 8, "tam.bn_forward: ymask must be uint8 [numel/8] (relu only)");
+    mp = ymask->data_ptr<uint8_t>();
+  }
   tam::bn_forward(bp(x), opt_ptr<const tam::bf16_t>(res), bpm(y), M, (int)C, (float)eps,
                   (float)momentum, gamma.data_ptr<float>(), beta.data_ptr<float>(),
                   opt_ptr<float>(run_mean), opt_ptr<float>(run_var), save_mean.data_ptr<float>(),
-                  save_rstd.data_ptr<float>(), relu, sp, sums_ready ? 1 : 0,
-                  sums_ready ? nullptr : part.data_ptr<float>(), cur_stream(x));
+                  save_rstd.data_ptr<float>(), relu, sp, sums_ready ? 1 : 0, mp, cur_stream(x));
 }
 
 void bn_backward_op(const Tensor& dy, const optional<Tensor>& y, const Tensor& x, const Tensor& mean,
                     const Tensor& rstd, const Tensor& gamma, const Tensor& dx,
                     const optional<Tensor>& dres, const optional<Tensor>& dgamma,
                     const optional<Tensor>& dbeta, bool relu, const optional<Tensor>& addend,
-                    const optional<Tensor>& sums, bool sums_ready) {
+                    const optional<Tensor>& sums, bool sums_ready, const optional<Tensor>& ymask) {
   check_bf16(dy, "dy"); check_bf16(x, "x"); check_bf16(dx, "dx");
   check_contig(dy, "dy"); check_contig(x, "x"); check_contig(dx, "dx");
   const int64_t C = x.size(-1);
   const int64_t M = x.numel() / C;
   TORCH_CHECK(C % 8 == 0 && C <= 2048, "tam.bn: C must be a multiple of 8 and <= 2048");
-  TORCH_CHECK(!relu || (y.has_value() && y->defined()), "tam.bn_backward: relu needs y");
+  const bool has_mask = ymask.has_value() && ymask->defined();
+  TORCH_CHECK(!relu || (y.has_value() && y->defined()) || has_mask, "tam.bn_backward: relu needs y or ymask");
+  if (has_mask)
+    TORCH_CHECK(ymask->is_cuda() && ymask->scalar_type() == at::kByte && ymask->is_contiguous() &&
+                ymask->numel() == x.numel() / 8, "tam.bn_backward: ymask must be uint8 [numel/8]");
+  const tam::bf16_t* yp = has_mask ? nullptr : opt_ptr<const tam::bf16_t>(y);
   const bool has_add = addend.has_value() && addend->defined();
   if (has_add) {
     check_bf16(*addend, "addend"); check_contig(*addend, "addend");
@@ -522,13 +583,12 @@ void bn_backward_op(const Tensor& dy, const optional<Tensor>& y, const Tensor& x
   TORCH_CHECK(!sums_ready || ((sums.has_value() && sums->defined()) && !relu && !has_add &&
                               !(dres.has_value() && dres->defined())),
               "tam.bn_backward: sums_ready takes the already-masked gradient (no relu / addend / dres)");
-  Tensor tmp, part;
+  Tensor tmp;
   double* sp = bn_sums(sums, x, C, tmp, "tam.bn_backward");
-  if (!sums_ready) part = at::empty({2 * tam::BN_MAX_BLOCKS * C}, x.options().dtype(at::kFloat));
-  tam::bn_backward(bp(dy), opt_ptr<const tam::bf16_t>(addend), opt_ptr<const tam::bf16_t>(y), bp(x), mean.data_ptr<float>(),
+  tam::bn_backward(bp(dy), opt_ptr<const tam::bf16_t>(addend), yp, bp(x), mean.data_ptr<float>(),
                    rstd.data_ptr<float>(), gamma.data_ptr<float>(), M, (int)C, relu, bpm(dx),
                    opt_ptr<tam::bf16_t>(dres), opt_ptr<float>(dgamma), opt_ptr<float>(dbeta),
-                   sp, sums_ready ? 1 : 0, sums_ready ? nullptr : part.data_ptr<float>(), cur_stream(x));
+                   sp, sums_ready ? 1 : 0, has_mask ? ymask->data_ptr<uint8_t>() : nullptr, cur_stream(x));
 }
 
 void ln_forward_op(const Tensor& x, const Tensor& g, const Tensor& b, const Tensor& y,
@@ -617,6 +677,8 @@ void embedding_backward_op(const Tensor& dout, const Tensor& ids, const Tensor& 
 
 void conv_dma_policy_op(int64_t p) { tam::conv_dma_policy((int)p); }
 void conv_halo_policy_op(int64_t p) { tam::conv_halo_policy((int)p); }
+void colsum_policy_op(int64_t p) { tam::colsum_policy((int)p); }
+void attn_short_policy_op(int64_t p) { tam::attn_short_policy((int)p); }
 // forced (bm, bn, splits) of the LDS-DMA conv wgrad (A/B sweeps; 0 = heuristic)
 void conv_wgrad_force_op(int64_t bm, int64_t bn, int64_t splits, int64_t noatomic) {
   tam::conv_wgrad_force((int)bm, (int)bn, (int)splits, (int)noatomic);
@@ -835,14 +897,14 @@ void lstm_bwd_op(const Tensor& act, const optional<Tensor>& c_prev, const option
 }  // namespace
 
 TORCH_LIBRARY(tam, m) {
-  m.def("gemm(Tensor a, bool a_kmajor, Tensor b, bool b_kmajor, Tensor(a!) c, int mode, Tensor? bias, bool relu, Tensor? mask, float alpha, bool allow_split) -> ()", &gemm_op);
+  m.def("gemm(Tensor a, bool a_kmajor, Tensor b, bool b_kmajor, Tensor(a!) c, int mode, Tensor? bias, bool relu, Tensor? mask, float alpha, bool allow_split, Tensor(b!)? colsum=None) -> ()", &gemm_op);
   m.def("conv_fwd(Tensor x, Tensor w, Tensor(a!) y, int stride, int pad, int dil, Tensor? bias, bool relu, Tensor(b!)? stats=None) -> int", &conv_fwd_op);
   m.def("conv_dgrad(Tensor dy, Tensor w, Tensor(a!) wt, Tensor(b!) dx, int stride, int pad, int dil, Tensor? mask) -> ()", &conv_dgrad_op);
   m.def("conv_weight_t_batch(Tensor[] w, Tensor(a!)[] wt) -> ()", &conv_weight_t_batch_op);
   m.def("conv_dgrad_pre(Tensor dy, Tensor w, Tensor wt, Tensor(a!) dx, int stride, int pad, int dil, Tensor? mask, Tensor(b!)? stats=None, Tensor? bnx=None, Tensor? bnmean=None, Tensor? bnrstd=None) -> int", &conv_dgrad_pre_op);
   m.def("conv_wgrad(Tensor dy, Tensor x, Tensor(a!) dw, int stride, int pad, int dil, int mode) -> ()", &conv_wgrad_op);
-  m.def("bn_forward(Tensor x, Tensor? res, Tensor(a!) y, Tensor gamma, Tensor beta, Tensor(b!)? run_mean, Tensor(c!)? run_var, Tensor(d!) save_mean, Tensor(e!) save_rstd, float eps, float momentum, bool relu, Tensor(f!)? sums=None, bool sums_ready=False) -> ()", &bn_forward_op);
-  m.def("bn_backward(Tensor dy, Tensor? y, Tensor x, Tensor mean, Tensor rstd, Tensor gamma, Tensor(a!) dx, Tensor(b!)? dres, Tensor(c!)? dgamma, Tensor(d!)? dbeta, bool relu, Tensor? addend=None, Tensor(e!)? sums=None, bool sums_ready=False) -> ()", &bn_backward_op);
+  m.def("bn_forward(Tensor x, Tensor? res, Tensor(a!) y, Tensor gamma, Tensor beta, Tensor(b!)? run_mean, Tensor(c!)? run_var, Tensor(d!) save_mean, Tensor(e!) save_rstd, float eps, float momentum, bool relu, Tensor(f!)? sums=None, bool sums_ready=False, Tensor(g!)? ymask=None) -> ()", &bn_forward_op);
+  m.def("bn_backward(Tensor dy, Tensor? y, Tensor x, Tensor mean, Tensor rstd, Tensor gamma, Tensor(a!) dx, Tensor(b!)? dres, Tensor(c!)? dgamma, Tensor(d!)? dbeta, bool relu, Tensor? addend=None, Tensor(e!)? sums=None, bool sums_ready=False, Tensor? ymask=None) -> ()", &bn_backward_op);
   m.def("ln_forward(Tensor x, Tensor g, Tensor b, Tensor(a!) y, Tensor(b!) mean, Tensor(c!) rstd, float eps) -> ()", &ln_forward_op);
   m.def("ln_backward(Tensor dy, Tensor x, Tensor g, Tensor mean, Tensor rstd, Tensor(a!) dx, Tensor(b!) dg, Tensor(c!) db, Tensor? addend=None) -> ()", &ln_backward_op);
   m.def("maxpool_forward(Tensor x, Tensor(a!) y, Tensor(b!) idx, int R, int S, int stride, int pad) -> ()", &maxpool_forward_op);
@@ -862,6 +924,8 @@ TORCH_LIBRARY(tam, m) {
   m.def("conv_dma_policy(int policy) -> ()", &conv_dma_policy_op);
   m.def("conv_wgrad_force(int bm, int bn, int splits, int noatomic=0) -> ()", &conv_wgrad_force_op);
   m.def("conv_halo_policy(int policy) -> ()", &conv_halo_policy_op);
+  m.def("colsum_policy(int policy) -> ()", &colsum_policy_op);
+  m.def("attn_short_policy(int policy) -> ()", &attn_short_policy_op);
   m.def("gemm_dma_policy(int policy, int cfg) -> ()", &gemm_dma_policy_op);
   m.def("gemm_routes() -> str", &gemm_routes_op);
   m.def("relu_backward(Tensor dy, Tensor y, Tensor(a!) dx) -> ()", &relu_backward_op);

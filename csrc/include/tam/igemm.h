@@ -52,6 +52,10 @@ struct Epi {
   const bf16_t* bnx = nullptr;
   const float* bnmean = nullptr;
   const float* bnrstd = nullptr;
+  // igemm with an M-major A only: colsum_a[m] += sum_k A[k][m] (fp32 no-return
+  // atomics, one per column per K-split) -- a Linear layer's bias gradient
+  // from the weight-gradient GEMM's own A loads (dW = dY^T X, db = colsum(dY))
+  float* colsum_a = nullptr;
 };
 
 // ---------------------------------------------------------------------------
@@ -313,6 +317,26 @@ igemm_kernel(LA la, LB lb, int M, int N, int K, int ktiles_per_split, Epi ep) {
   using SA = Stager<LA, BM>;
   using SB = Stager<LB, BN>;
   uint4 ra[SA::P], rb[SB::P];
+  // fused A column sums (Epi::colsum_a): the column-0 blocks add up the A
+  // values they stage (each thread: 8 columns of its own K rows)
+  bool csum = false;
+  float cs[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+  if constexpr (!LA::kKMajor) csum = ep.colsum_a != nullptr && tn == 0;
+  auto acc_cols = [&]() {
+    if constexpr (!LA::kKMajor) {
+      if (csum) {
+#pragma unroll
+        for (int i = 0; i < SA::P; ++i) {
+          const uint32_t w[4] = {ra[i].x, ra[i].y, ra[i].z, ra[i].w};
+#pragma unroll
+          for (int e = 0; e < 4; ++e) {
+            cs[2 * e] += __uint_as_float(w[e] << 16);
+            cs[2 * e + 1] += __uint_as_float(w[e] & 0xffff0000u);
+          }
+        }
+      }
+    }
+  };
 
   f32x4_t acc[TM][TN];
 #pragma unroll
@@ -325,6 +349,7 @@ igemm_kernel(LA la, LB lb, int M, int N, int K, int ktiles_per_split, Epi ep) {
     SB::fetch(lb, rb, kt0 * BK, tid);
     SA::store(smem, ra, tid);
     SB::store(smem + 2 * A_BYTES, rb, tid);
+    acc_cols();
     __syncthreads();
     for (int kt = kt0; kt < kt1; ++kt) {
       const int cur = (kt - kt0) & 1;
@@ -353,6 +378,33 @@ igemm_kernel(LA la, LB lb, int M, int N, int K, int ktiles_per_split, Epi ep) {
       if (more) {
         SA::store(smem + (cur ^ 1) * A_BYTES, ra, tid);
         SB::store(smem + 2 * A_BYTES + (cur ^ 1) * B_BYTES, rb, tid);
+        acc_cols();
+      }
+      __syncthreads();
+    }
+  }
+  if constexpr (!LA::kKMajor) {
+    if (csum) {
+      // threads t and t' = t + CPR*j hold the same 8 columns: combine in LDS
+      // (the stages are free after the loop's last barrier), then one atomic
+      // per column
+      constexpr int CPR = BM / 8, RPP = IG_THREADS / CPR;
+      float* red = (float*)smem;
+      if (kt0 >= kt1) __syncthreads();
+#pragma unroll
+      for (int e = 0; e < 8; ++e) red[tid * 8 + e] = cs[e];
+      __syncthreads();
+      if (tid < CPR) {
+        float t8[8];
+#pragma unroll
+        for (int e = 0; e < 8; ++e) t8[e] = 0.f;
+        for (int r = 0; r < RPP; ++r)
+#pragma unroll
+          for (int e = 0; e < 8; ++e) t8[e] += red[(r * CPR + tid) * 8 + e];
+        const int col = m0 + tid * 8;
+#pragma unroll
+        for (int e = 0; e < 8; ++e)
+          if (col + e < M) atomicAdd(ep.colsum_a + col + e, t8[e]);
       }
       __syncthreads();
     }

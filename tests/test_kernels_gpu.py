@@ -51,6 +51,27 @@ def test_gemm_routing(gpu):
     assert "1024 2048 1024 KK 0 0 1" in routes and "1024 2048 1024 MK 1 1 0" in routes
 
 
+@pytest.mark.parametrize("M,N,K", [(512, 512, 4096), (2048, 512, 4096), (512, 2048, 4096), (6144, 512, 4096),
+                                   (200, 136, 72), (1000, 64, 520)])
+def test_gemm_colsum_fused(gpu, M, N, K):
+    """Linear weight gradient with the bias gradient fused (Epi::colsum_a):
+    C += A^T B and colsum += sum_k A[k][:] vs fp32 torch; the first (tuning)
+    call takes the separate column-sum path, later ones the fused igemm
+    where it is routed -- both must give the same numbers."""
+    torch.manual_seed(21)
+    dy = torch.randn(K, M, device=gpu).to(BF)           # A, M-major: [K][M]
+    x = torch.randn(K, N, device=gpu).to(BF)            # B, N-major: [K][N]
+    ref = dy.float().t() @ x.float()
+    ref_b = dy.float().sum(0)
+    for call in range(3):
+        c = torch.full((M, N), 1.0, device=gpu)
+        db = torch.full((M,), 0.5, device=gpu)
+        T().gemm(dy, False, x, False, c, 1, None, False, None, 1.0, True, db)
+        torch.cuda.synchronize()
+        assert rel_err(c, ref + 1.0) < 1e-4, call
+        assert rel_err(db, ref_b + 0.5) < 1e-4, call
+
+
 # ------------------------------------------------------------------ GEMM
 @pytest.mark.parametrize("M,N,K", [(256, 256, 256), (200, 136, 72), (1000, 64, 520), (64, 1000, 64),
                                    (4096, 1024, 512), (33, 40, 8)])
@@ -534,6 +555,44 @@ def test_batchnorm_backward_addend(gpu, relu):
         assert rel_err(u, v) < 1e-2
 
 
+@pytest.mark.parametrize("res,add", [(False, False), (True, False), (True, True)])
+@pytest.mark.parametrize("shape", [(16, 14, 14, 256), (4, 9, 9, 320), (8, 7, 7, 2048)])
+def test_batchnorm_relu_bitmask(gpu, res, add, shape):
+    """The forward's 1-bit ReLU mask (ymask) gives the same backward as
+    re-reading the bf16 output y: bits set exactly where y > 0, and dx /
+    dres / dgamma / dbeta equal to the y-read path's."""
+    torch.manual_seed(9)
+    N, H, W, C = shape
+    x = (torch.randn(N, H, W, C, device=gpu) * 2).to(BF)
+    r = torch.randn_like(x.float()).to(BF) if res else None
+    g = torch.rand(C, device=gpu) + 0.5
+    b = torch.randn(C, device=gpu)
+    y = torch.empty_like(x)
+    mean = torch.empty(C, device=gpu); rstd = torch.empty(C, device=gpu)
+    ym = torch.full((x.numel() // 8,), 0xA5, dtype=torch.uint8, device=gpu)
+    T().bn_forward(x, r, y, g, b, None, None, mean, rstd, 1e-5, 0.1, True, None, False, ym)
+    bits = ((ym[:, None].int() >> torch.arange(8, device=gpu)) & 1).reshape(-1).bool()
+    assert torch.equal(bits, (y.float() > 0).reshape(-1))
+    dy = torch.randn_like(x.float()).to(BF)
+    a = torch.randn_like(x.float()).to(BF) if add else None
+    outs = []
+    for use_mask in (False, True):
+        dx = torch.empty_like(x)
+        dres = torch.empty_like(x) if res else None
+        dg, db = torch.zeros(C, device=gpu), torch.zeros(C, device=gpu)
+        if use_mask:
+            T().bn_backward(dy, None, x, mean, rstd, g, dx, dres, dg, db, True, a, None, False, ym)
+        else:
+            T().bn_backward(dy, y, x, mean, rstd, g, dx, dres, dg, db, True, a)
+        outs.append((dx, dres, dg, db))
+    # dres does not depend on the statistics: identical; the rest only up to
+    # the fp64 atomic summation order of the per-channel sums
+    (dx0, dr0, dg0, db0), (dx1, dr1, dg1, db1) = outs
+    if res:
+        assert torch.equal(dr0, dr1)
+    assert rel_err(dx0, dx1) < 1e-3 and rel_err(dg0, dg1) < 1e-5 and rel_err(db0, db1) < 1e-5
+
+
 @pytest.mark.parametrize("policy", [1, 3])
 @pytest.mark.parametrize("shape", [(8, 28, 28, 128, 256, 3, 1, 1), (16, 14, 14, 256, 1024, 1, 1, 0),
                                    (4, 56, 56, 64, 64, 3, 1, 1), (8, 28, 28, 256, 512, 1, 2, 0)])
@@ -752,10 +811,15 @@ def _attn_ref(q, k, v, causal, kv_len=None):
 
 @pytest.mark.parametrize("B,H,Sq,Sk,causal", [(2, 4, 128, 128, False), (2, 8, 128, 128, True),
                                               (3, 2, 100, 77, False), (1, 4, 65, 65, True),
-                                              (2, 8, 256, 200, False)])
-def test_attention(gpu, B, H, Sq, Sk, causal):
+                                              (2, 8, 256, 200, False), (2, 4, 192, 128, False)])
+@pytest.mark.parametrize("short", [1, 0])
+def test_attention(gpu, B, H, Sq, Sk, causal, short):
+    """Forward and backward vs fp32 torch; short=1: key ranges <= 128 take
+    the one-launch (b, h)-per-workgroup backward, 0: the key-blocked kernels
+    with fp32 dQ atomics."""
     if causal and Sq != Sk:
         pytest.skip()
+    T().attn_short_policy(short)
     torch.manual_seed(11)
     qkv = torch.randn(B, Sq, 3, H, 64, device=gpu).to(BF) if Sq == Sk else None
     if qkv is not None:
@@ -782,10 +846,34 @@ def test_attention(gpu, B, H, Sq, Sk, causal):
     T().attn_backward(q, k, v, o, do, lse, dq, dk, dv,
                       torch.empty(B, Sq, H, 64, device=gpu), torch.empty(B, H, Sq, device=gpu),
                       causal, 0.125, None)
+    T().attn_short_policy(1)
     gq, gk, gv = torch.autograd.grad(of, [qf, kf, vf], do.float())
     assert rel_err(dq, gq) < 2e-2
     assert rel_err(dk, gk) < 2e-2
     assert rel_err(dv, gv) < 2e-2
+
+
+@pytest.mark.parametrize("short", [1, 0])
+def test_attention_kvlen_backward(gpu, short):
+    """Padded key ranges (kv_len) in the backward of both kernel families."""
+    torch.manual_seed(14)
+    B, H, S = 3, 2, 96
+    q, k, v = (torch.randn(B, S, H, 64, device=gpu).to(BF) for _ in range(3))
+    kl = torch.tensor([96, 50, 7], device=gpu, dtype=torch.int32)
+    o = torch.empty_like(q); lse = torch.empty(B, H, S, device=gpu)
+    T().attn_forward(q, k, v, o, lse, False, 0.125, kl)
+    qf, kf, vf = (t.float().requires_grad_(True) for t in (q, k, v))
+    of, _ = _attn_ref(qf, kf, vf, False, kl.long())
+    do = torch.randn_like(o)
+    dq, dk, dv = torch.empty_like(q), torch.empty_like(k), torch.empty_like(v)
+    T().attn_short_policy(short)
+    try:
+        T().attn_backward(q, k, v, o, do, lse, dq, dk, dv, torch.empty(B, S, H, 64, device=gpu),
+                          torch.empty(B, H, S, device=gpu), False, 0.125, kl)
+    finally:
+        T().attn_short_policy(1)
+    gq, gk, gv = torch.autograd.grad(of, [qf, kf, vf], do.float())
+    assert rel_err(dq, gq) < 2e-2 and rel_err(dk, gk) < 2e-2 and rel_err(dv, gv) < 2e-2
 
 
 def test_attention_kvlen(gpu):

@@ -172,9 +172,10 @@ class _Linear(Function):
         dx = None
         if dy.is_cuda:
             with _OnWgrad(dy, x):
-                _T().gemm(dy, False, x, False, w.grad, 1, None, False, None, 1.0, True)
-                if b is not None:
-                    _T().colsum(dy, b.grad)
+                # the bias gradient colsum(dy) rides on the weight-gradient
+                # GEMM's own A loads (fused on the igemm route, else a pass)
+                _T().gemm(dy, False, x, False, w.grad, 1, None, False, None, 1.0, True,
+                          b.grad if b is not None else None)
         if ctx.needs_input_grad[0]:
             if dy.is_cuda:
                 dx = torch.empty_like(x)
@@ -223,6 +224,10 @@ def _conv_out(h: int, k: int, s: int, p: int, d: int = 1) -> int:
 # 10.65 -> 10.66 ms. Off by default; the GPU test keeps the path exact.
 BN_DGRAD_FUSION = False
 
+
+# relu BNs whose backward applies the ReLU mask itself keep it as 1 bit per
+# output (bn_forward ymask) instead of re-reading the bf16 output
+BN_RELU_BITMASK = True
 
 # shards of a BatchNorm statistics accumulator (csrc/include/tam/common.h
 # BN_SHARDS; the ops check the size): fp64 [BN_SHARDS][2C]
@@ -401,18 +406,26 @@ class _BN(Function):
                 momentum: float, training: bool, slot: Optional[GradSlot] = None,
                 consumer_masks: bool = False, ws=None):
         C = x.shape[-1]
+        # consumer_masks: the only consumer (a conv with in_relu) already zeroes
+        # the gradient where y <= 0 in its dgrad epilogue -- the backward here
+        # neither re-reads y nor keeps it alive
+        bwd_relu = relu and not consumer_masks
+        ymask = None
         if x.is_cuda:
             y = torch.empty_like(x)
             if training:
                 mean = torch.empty(C, dtype=torch.float32, device=x.device)
                 rstd = torch.empty_like(mean)
+                if bwd_relu and BN_RELU_BITMASK:
+                    # the backward's ReLU mask as 1 bit per output (1/16 of y's bytes)
+                    ymask = torch.empty(x.numel() // 8, dtype=torch.uint8, device=x.device)
                 part = getattr(x, "_tam_bnpart", None)
                 if part is not None:       # sums accumulated by the producing conv
                     _T().bn_forward(x, res, y, g.master, b.master, run_mean, run_var, mean, rstd, eps,
-                                    momentum, relu, part, True)
+                                    momentum, relu, part, True, ymask)
                 else:
                     _T().bn_forward(x, res, y, g.master, b.master, run_mean, run_var, mean, rstd, eps,
-                                    momentum, relu, ws.fwd if ws is not None else None, False)
+                                    momentum, relu, ws.fwd if ws is not None else None, False, ymask)
             else:
                 rstd_i = torch.rsqrt(run_var + eps)
                 scale = g.master * rstd_i
@@ -437,16 +450,13 @@ class _BN(Function):
             if relu:
                 yf = yf.clamp_min(0)
             y = yf.reshape(x.shape).to(BF16)
-        # consumer_masks: the only consumer (a conv with in_relu) already zeroes
-        # the gradient where y <= 0 in its dgrad epilogue -- the backward here
-        # neither re-reads y nor keeps it alive
-        bwd_relu = relu and not consumer_masks
         ctx.g, ctx.b, ctx.relu, ctx.has_res = g, b, bwd_relu, res is not None
+        ctx.bitmask = ymask is not None
         ctx.slot = slot
         ctx.bws = ws.bwd if ws is not None else None
         if slot is not None and consumer_masks and x.is_cuda and training:
             slot.src = (x, mean, rstd, ctx.bws)
-        ctx.save_for_backward(x, y if bwd_relu else None, mean, rstd)
+        ctx.save_for_backward(x, (ymask if ymask is not None else y) if bwd_relu else None, mean, rstd)
         return y
 
     @staticmethod
@@ -472,8 +482,12 @@ class _BN(Function):
         elif dy.is_cuda:
             dx = torch.empty_like(x)
             dres = torch.empty_like(x) if ctx.has_res and (ctx.relu or add is not None) else None
-            _T().bn_backward(dy, y, x, mean, rstd, g.master, dx, dres, g.grad, b.grad, ctx.relu, add,
-                             ctx.bws, False)
+            if ctx.bitmask:
+                _T().bn_backward(dy, None, x, mean, rstd, g.master, dx, dres, g.grad, b.grad, ctx.relu, add,
+                                 ctx.bws, False, y)
+            else:
+                _T().bn_backward(dy, y, x, mean, rstd, g.master, dx, dres, g.grad, b.grad, ctx.relu, add,
+                                 ctx.bws, False)
             if ctx.has_res and dres is None:
                 dres = dy
         else:
