@@ -679,6 +679,7 @@ void conv_dma_policy_op(int64_t p) { tam::conv_dma_policy((int)p); }
 void conv_halo_policy_op(int64_t p) { tam::conv_halo_policy((int)p); }
 void colsum_policy_op(int64_t p) { tam::colsum_policy((int)p); }
 void attn_short_policy_op(int64_t p) { tam::attn_short_policy((int)p); }
+void gemm_igemm_depth_op(int64_t d) { tam::gemm_igemm_depth((int)d); }
 // forced (bm, bn, splits) of the LDS-DMA conv wgrad (A/B sweeps; 0 = heuristic)
 void conv_wgrad_force_op(int64_t bm, int64_t bn, int64_t splits, int64_t noatomic) {
   tam::conv_wgrad_force((int)bm, (int)bn, (int)splits, (int)noatomic);
@@ -926,6 +927,7 @@ TORCH_LIBRARY(tam, m) {
   m.def("conv_halo_policy(int policy) -> ()", &conv_halo_policy_op);
   m.def("colsum_policy(int policy) -> ()", &colsum_policy_op);
   m.def("attn_short_policy(int policy) -> ()", &attn_short_policy_op);
+  m.def("gemm_igemm_depth(int depth) -> ()", &gemm_igemm_depth_op);
   m.def("gemm_dma_policy(int policy, int cfg) -> ()", &gemm_dma_policy_op);
   m.def("gemm_routes() -> str", &gemm_routes_op);
   m.def("relu_backward(Tensor dy, Tensor y, Tensor(a!) dx) -> ()", &relu_backward_op);

@@ -96,6 +96,7 @@ void adam_step(float* w, float* g, float* m, float* v, bf16_t* wb, long n, float
 void attn_forward(const bf16_t* q, const bf16_t* k, const bf16_t* v, bf16_t* o, float* lse, int B,
                   int H, int Sq, int Sk, long q_stride, long kv_stride, long o_stride, int causal,
                   float scale, const int* kv_len, hipStream_t s);
+void attn_short_policy(int p);   // 1: Sk <= 128 backward in one fused launch (default)
 void attn_backward(const bf16_t* q, const bf16_t* k, const bf16_t* v, const bf16_t* o,
                    const bf16_t* dout, const float* lse, bf16_t* dq, bf16_t* dk, bf16_t* dv,
                    float* dq_acc, float* delta, int B, int H, int Sq, int Sk, long q_stride,

@@ -344,6 +344,181 @@ __global__ void __launch_bounds__(256) attn_bwd_kernel(
   }
 }
 
+// ============================================================== backward, Sk <= 128
+// Short key ranges (the Transformer's 128-token sequences): ONE workgroup of
+// 8 waves per (b, h) owns every key (waves 0-3: keys 0-63, 4-7: keys 64-127,
+// 16 per wave, dK^T / dV^T in registers as in attn_bwd_kernel) and sweeps the
+// query tiles. With all keys in the block, a query tile's dQ = dS K over the
+// 128 keys is finished in-block (dS [kv][q] and K [kv][d] LDS images) and
+// stored as bf16 directly; delta = rowsum(dO * O) is formed in-block from the
+// dO and O tile images. One launch instead of delta+zero / backward /
+// fp32-dQ cast, and no dQ atomics.
+constexpr int ATS_K = 128;
+__global__ void __launch_bounds__(512) attn_bwd_short_kernel(
+    const bf16_t* __restrict__ Q, const bf16_t* __restrict__ K, const bf16_t* __restrict__ V,
+    const bf16_t* __restrict__ O, const bf16_t* __restrict__ dO, const float* __restrict__ LSE,
+    bf16_t* __restrict__ dQ, bf16_t* __restrict__ dK, bf16_t* __restrict__ dV, int H, int Sq, int Sk,
+    long qs, long kvs, long os, int causal, float scale, const int* __restrict__ kv_len) {
+  // LDS: Q row image, Q^T image (rho), dO row image, dO^T image (rho), O row
+  //      image (delta), K [kv][d] image (128 rows), dS [kv][q] image (128 rows),
+  //      lse[64], delta[64]
+  constexpr int T = AT * AD * 2;     // one 64x64 bf16 image
+  __shared__ __attribute__((aligned(16))) char smem[5 * T + 2 * 2 * T + 2 * AT * 4];
+  char* q_k = smem;
+  char* q_mn = smem + 1 * T;
+  char* do_k = smem + 2 * T;
+  char* do_mn = smem + 3 * T;
+  char* o_k = smem + 4 * T;
+  char* k_mn = smem + 5 * T;          // [128 kv][64 d]
+  char* ds_mn = smem + 7 * T;         // [128 kv][64 q]
+  float* s_lse = (float*)(smem + 9 * T);
+  float* s_del = s_lse + AT;
+
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, g = lane >> 4;
+  const int half = tid >> 8, ht = tid & 255;          // 256-thread halves
+  const int bh = blockIdx.x, b = bh / H, h = bh % H;
+  const int klen = kv_len ? min(Sk, kv_len[b]) : Sk;
+  const int kvw = 16 * w + (lane & 15);               // this lane's key (0..127)
+
+  const bf16_t* Qb = Q + (long)b * Sq * qs + h * AD;
+  const bf16_t* dOb = dO + (long)b * Sq * os + h * AD;
+  const bf16_t* Ob = O + (long)b * Sq * os + h * AD;
+  const bf16_t* Kb = K + (long)b * Sk * kvs + h * AD;
+  const bf16_t* Vb = V + (long)b * Sk * kvs + h * AD;
+  const float* lse_b = LSE + ((long)b * H + h) * Sq;
+
+  s16x8_t kf[2], vf[2];
+#pragma unroll
+  for (int ks = 0; ks < 2; ++ks) {
+    const bool ok = kvw < klen;
+    kf[ks] = ok ? *(const s16x8_t*)(Kb + (long)kvw * kvs + 32 * ks + 8 * g) : s16x8_t{0, 0, 0, 0, 0, 0, 0, 0};
+    vf[ks] = ok ? *(const s16x8_t*)(Vb + (long)kvw * kvs + 32 * ks + 8 * g) : s16x8_t{0, 0, 0, 0, 0, 0, 0, 0};
+  }
+  {  // K image: half 0 keys 0-63, half 1 keys 64-127 (rows 64*half + r)
+    uint4 rk[2];
+    tile_fetch(Kb, kvs, 64 * half, klen, rk, ht);
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      const int row = 64 * half + (ht >> 3) + 32 * i;
+      *(uint4*)(k_mn + mnmaj_off<64>(row, 2 * (ht & 7))) = rk[i];
+    }
+  }
+  f32x4_t dvt[4], dkt[4];
+#pragma unroll
+  for (int mt = 0; mt < 4; ++mt) dvt[mt] = dkt[mt] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+  const float sl2 = scale * kLog2e;
+
+  for (int q0 = 0; q0 < Sq; q0 += AT) {
+    // half 0 stages Q, half 1 stages dO and O
+    uint4 ra[2], rb[2];
+    if (half == 0) {
+      tile_fetch(Qb, qs, q0, Sq, ra, ht);
+    } else {
+      tile_fetch(dOb, os, q0, Sq, ra, ht);
+      tile_fetch(Ob, os, q0, Sq, rb, ht);
+    }
+    __syncthreads();   // previous iteration done with all images
+    if (half == 0) {
+      tile_store_k(q_k, ra, ht, false);
+      tile_store_mn(q_mn, ra, ht, true);
+      if (ht < AT) s_lse[ht] = q0 + ht < Sq ? lse_b[q0 + ht] * kLog2e : 0.f;
+    } else {
+      tile_store_k(do_k, ra, ht, false);
+      tile_store_mn(do_mn, ra, ht, true);
+      tile_store_k(o_k, rb, ht, false);
+    }
+    __syncthreads();
+    {  // delta[q] = sum_d dO[q][d] O[q][d]: 8 threads per row, 8 d each
+      const int row = tid >> 3, c = tid & 7;
+      const uint4 a = *(const uint4*)(do_k + kmaj_off(row, c));
+      const uint4 o = *(const uint4*)(o_k + kmaj_off(row, c));
+      const uint32_t aw[4] = {a.x, a.y, a.z, a.w}, ow[4] = {o.x, o.y, o.z, o.w};
+      float d = 0.f;
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        d += __uint_as_float(aw[e] << 16) * __uint_as_float(ow[e] << 16);
+        d += __uint_as_float(aw[e] & 0xffff0000u) * __uint_as_float(ow[e] & 0xffff0000u);
+      }
+      d += __shfl_xor(d, 1, 64);
+      d += __shfl_xor(d, 2, 64);
+      d += __shfl_xor(d, 4, 64);
+      if (c == 0) s_del[row] = d;
+    }
+    __syncthreads();
+    // S[q][kv], dP[q][kv] for this wave's 16 keys: q = 16t + 4g + r
+    f32x4_t sp[4], dp[4];
+#pragma unroll
+    for (int t = 0; t < 4; ++t) {
+      sp[t] = dp[t] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int ks = 0; ks < 2; ++ks) {
+        sp[t] = mfma(read_frag_k(q_k, lane, 16 * t, ks), kf[ks], sp[t]);
+        dp[t] = mfma(read_frag_k(do_k, lane, 16 * t, ks), vf[ks], dp[t]);
+      }
+    }
+#pragma unroll
+    for (int t = 0; t < 4; ++t)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int ql = 16 * t + 4 * g + r;
+        const int q = q0 + ql;
+        float p = exp2f(sp[t][r] * sl2 - s_lse[ql]);
+        if (q >= Sq || kvw >= klen || (causal && kvw > q)) p = 0.f;
+        sp[t][r] = p;
+        dp[t][r] = p * (dp[t][r] - s_del[ql]);
+      }
+#pragma unroll
+    for (int s = 0; s < 2; ++s) {
+      const s16x8_t pb = pack_frag(sp[2 * s], sp[2 * s + 1]);
+      const s16x8_t sb = pack_frag(dp[2 * s], dp[2 * s + 1]);
+#pragma unroll
+      for (int mt = 0; mt < 4; ++mt) {
+        dvt[mt] = mfma(read_frag_mn<64>(do_mn, lane, 32 * s, 16 * mt), pb, dvt[mt]);
+        dkt[mt] = mfma(read_frag_mn<64>(q_mn, lane, 32 * s, 16 * mt), sb, dkt[mt]);
+      }
+    }
+    // dS -> LDS [kv][q]
+#pragma unroll
+    for (int t = 0; t < 4; ++t) {
+      const int c8 = (16 * t + 4 * g) >> 2;
+      *(uint2*)(ds_mn + mnmaj_off<64>(kvw, c8)) =
+          make_uint2(pack_bf2(dp[t][0], dp[t][1]), pack_bf2(dp[t][2], dp[t][3]));
+    }
+    __syncthreads();
+    // dQ[q][d] over all 128 keys: wave w -> q rows 16*(w&3), d columns 32*(w>>2) + {0, 16}
+    f32x4_t dq[2];
+    dq[0] = dq[1] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int s = 0; s < ATS_K / 32; ++s) {
+      const s16x8_t a = read_frag_mn<64>(ds_mn, lane, 32 * s, 16 * (w & 3));
+#pragma unroll
+      for (int nt = 0; nt < 2; ++nt)
+        dq[nt] = mfma(a, read_frag_mn<64>(k_mn, lane, 32 * s, 32 * (w >> 2) + 16 * nt), dq[nt]);
+    }
+#pragma unroll
+    for (int nt = 0; nt < 2; ++nt)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int q = q0 + 16 * (w & 3) + 4 * g + r;
+        if (q < Sq) {
+          const int d = 32 * (w >> 2) + 16 * nt + (lane & 15);
+          dQ[((long)b * Sq + q) * qs + h * AD + d] = f2bf(dq[nt][r] * scale);
+        }
+      }
+  }
+  if (kvw < Sk) {
+    bf16_t* dKb = dK + ((long)b * Sk + kvw) * kvs + h * AD;
+    bf16_t* dVb = dV + ((long)b * Sk + kvw) * kvs + h * AD;
+#pragma unroll
+    for (int mt = 0; mt < 4; ++mt) {
+      const int d = 16 * mt + 4 * g;
+      *(uint2*)(dKb + d) = make_uint2(pack_bf2(dkt[mt][0] * scale, dkt[mt][1] * scale),
+                                      pack_bf2(dkt[mt][2] * scale, dkt[mt][3] * scale));
+      *(uint2*)(dVb + d) = make_uint2(pack_bf2(dvt[mt][0], dvt[mt][1]), pack_bf2(dvt[mt][2], dvt[mt][3]));
+    }
+  }
+}
+
 // dq (bf16, strided like Q) = dq_acc (fp32, packed [B][Sq][H][64])
 __global__ void attn_dq_cast_kernel(const float* __restrict__ acc, bf16_t* __restrict__ dq, long n,
                                     int HD, long qs) {
@@ -362,11 +537,21 @@ void attn_forward(const bf16_t* q, const bf16_t* k, const bf16_t* v, bf16_t* o, 
                      kv_stride, o_stride, causal, scale, kv_len);
 }
 
+// 1 (default): key ranges <= 128 take the one-launch short-sequence backward;
+// 0: always the key-blocked kernels (tests / A/B)
+static int g_attn_short = 1;
+void attn_short_policy(int p) { g_attn_short = p; }
+
 void attn_backward(const bf16_t* q, const bf16_t* k, const bf16_t* v, const bf16_t* o,
                    const bf16_t* dout, const float* lse, bf16_t* dq, bf16_t* dk, bf16_t* dv,
                    float* dq_acc, float* delta, int B, int H, int Sq, int Sk, long q_stride,
                    long kv_stride, long o_stride, int causal, float scale, const int* kv_len,
                    hipStream_t s) {
+  if (Sk <= ATS_K && g_attn_short) {
+    hipLaunchKernelGGL(attn_bwd_short_kernel, dim3(B * H), dim3(512), 0, s, q, k, v, o, dout, lse, dq, dk, dv,
+                       H, Sq, Sk, q_stride, kv_stride, o_stride, causal, scale, kv_len);
+    return;
+  }
   const long rows = (long)B * H * Sq;
   hipLaunchKernelGGL(attn_delta_kernel, dim3((rows + 3) / 4), dim3(256), 0, s, o, dout, delta, dq_acc,
                      B, H, Sq, o_stride);
