@@ -210,6 +210,10 @@ void gemm_op(const Tensor& a, bool a_kmajor, const Tensor& b, bool b_kmajor, con
                        (tam::gemm8p_policy_mode() == 1 && mnk >= (double)(1 << 27) &&
                         tam::gemm8p_ok(a_kmajor, b_kmajor, (int)M, (int)N, (int)K, a.stride(0), b.stride(0)));
     if (!tuned) fuse = true;
+    // route 0 of a big shape IS the LDS-DMA kernel (gemm_select's size rule),
+    // which the fusion would trade for the igemm: never worth it
+    if (tam::gemm_select_big_p8(a_kmajor, b_kmajor, (int)M, (int)N, (int)K, a.stride(0), b.stride(0)))
+      fuse = false;
     if (fuse && !g_forced && tam::gemm8p_policy_mode() != 3 && g_dma_policy != 2) {
       ep.colsum_a = colsum->data_ptr<float>();
       run_mfma(a, a_kmajor, b, b_kmajor, M, N, K, ep, allow_split, 0);
@@ -679,7 +683,6 @@ void conv_dma_policy_op(int64_t p) { tam::conv_dma_policy((int)p); }
 void conv_halo_policy_op(int64_t p) { tam::conv_halo_policy((int)p); }
 void colsum_policy_op(int64_t p) { tam::colsum_policy((int)p); }
 void attn_short_policy_op(int64_t p) { tam::attn_short_policy((int)p); }
-void gemm_igemm_depth_op(int64_t d) { tam::gemm_igemm_depth((int)d); }
 // forced (bm, bn, splits) of the LDS-DMA conv wgrad (A/B sweeps; 0 = heuristic)
 void conv_wgrad_force_op(int64_t bm, int64_t bn, int64_t splits, int64_t noatomic) {
   tam::conv_wgrad_force((int)bm, (int)bn, (int)splits, (int)noatomic);
@@ -927,7 +930,6 @@ TORCH_LIBRARY(tam, m) {
   m.def("conv_halo_policy(int policy) -> ()", &conv_halo_policy_op);
   m.def("colsum_policy(int policy) -> ()", &colsum_policy_op);
   m.def("attn_short_policy(int policy) -> ()", &attn_short_policy_op);
-  m.def("gemm_igemm_depth(int depth) -> ()", &gemm_igemm_depth_op);
   m.def("gemm_dma_policy(int policy, int cfg) -> ()", &gemm_dma_policy_op);
   m.def("gemm_routes() -> str", &gemm_routes_op);
   m.def("relu_backward(Tensor dy, Tensor y, Tensor(a!) dx) -> ()", &relu_backward_op);

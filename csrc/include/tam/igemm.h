@@ -285,7 +285,13 @@ struct Stager {
   }
 };
 
-template <int BM, int BN, class LA, class LB>
+// NPF: register-staged K-tiles in flight. 1: the next tile's loads have ONE
+// K-tile of MFMA work to land (the conv loaders, whose address math is
+// heavier); NPF > 1: tiles t+1 .. t+NPF are in flight while tile t computes
+// (NPF register sets, the loop unrolled by NPF so every set index is a
+// compile-time constant) -- the plain small-tile GEMMs with deep K (weight
+// gradients: 64 K-tiles of 8 MFMAs per wave) are load-latency bound at NPF 1.
+template <int BM, int BN, class LA, class LB, int NPF = 1>
 __global__ void __launch_bounds__(IG_THREADS, 2)
 igemm_kernel(LA la, LB lb, int M, int N, int K, int ktiles_per_split, Epi ep) {
   constexpr int BK = IG_BK;
@@ -316,18 +322,18 @@ igemm_kernel(LA la, LB lb, int M, int N, int K, int ktiles_per_split, Epi ep) {
 
   using SA = Stager<LA, BM>;
   using SB = Stager<LB, BN>;
-  uint4 ra[SA::P], rb[SB::P];
+  uint4 ra[NPF][SA::P], rb[NPF][SB::P];
   // fused A column sums (Epi::colsum_a): the column-0 blocks add up the A
   // values they stage (each thread: 8 columns of its own K rows)
   bool csum = false;
   float cs[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
   if constexpr (!LA::kKMajor) csum = ep.colsum_a != nullptr && tn == 0;
-  auto acc_cols = [&]() {
+  auto acc_cols = [&](const uint4 (&rs)[SA::P]) {
     if constexpr (!LA::kKMajor) {
       if (csum) {
 #pragma unroll
         for (int i = 0; i < SA::P; ++i) {
-          const uint32_t w[4] = {ra[i].x, ra[i].y, ra[i].z, ra[i].w};
+          const uint32_t w[4] = {rs[i].x, rs[i].y, rs[i].z, rs[i].w};
 #pragma unroll
           for (int e = 0; e < 4; ++e) {
             cs[2 * e] += __uint_as_float(w[e] << 16);
@@ -344,43 +350,58 @@ igemm_kernel(LA la, LB lb, int M, int N, int K, int ktiles_per_split, Epi ep) {
 #pragma unroll
     for (int j = 0; j < TN; ++j) acc[i][j] = f32x4_t{0.f, 0.f, 0.f, 0.f};
 
+  auto compute = [&](const char* ta, const char* tb) {
+#pragma unroll
+    for (int kk = 0; kk < BK / 32; ++kk) {
+      s16x8_t fa[TM], fb[TN];
+#pragma unroll
+      for (int i = 0; i < TM; ++i) fa[i] = SA::frag(ta, lane, wr * (BM / 2) + 16 * i, kk);
+#pragma unroll
+      for (int j = 0; j < TN; ++j) fb[j] = SB::frag(tb, lane, wc * (BN / 2) + 16 * j, kk);
+#pragma unroll
+      for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int j = 0; j < TN; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(
+              __builtin_bit_cast(bf16x8_t, fa[i]), __builtin_bit_cast(bf16x8_t, fb[j]),
+              acc[i][j], 0, 0, 0);
+    }
+  };
   if (kt0 < kt1) {
-    SA::fetch(la, ra, kt0 * BK, tid);
-    SB::fetch(lb, rb, kt0 * BK, tid);
-    SA::store(smem, ra, tid);
-    SB::store(smem + 2 * A_BYTES, rb, tid);
-    acc_cols();
+    // tile kt0 -> LDS stage 0 (through set 0), then tiles kt0+1 .. kt0+NPF
+    // into sets 0 .. NPF-1
+    SA::fetch(la, ra[0], kt0 * BK, tid);
+    SB::fetch(lb, rb[0], kt0 * BK, tid);
+    SA::store(smem, ra[0], tid);
+    SB::store(smem + 2 * A_BYTES, rb[0], tid);
+    acc_cols(ra[0]);
+#pragma unroll
+    for (int u = 0; u < NPF; ++u) {
+      if (kt0 + 1 + u < kt1) {
+        SA::fetch(la, ra[u], (kt0 + 1 + u) * BK, tid);
+        SB::fetch(lb, rb[u], (kt0 + 1 + u) * BK, tid);
+      }
+    }
     __syncthreads();
-    for (int kt = kt0; kt < kt1; ++kt) {
-      const int cur = (kt - kt0) & 1;
-      const bool more = kt + 1 < kt1;
-      if (more) {
-        SA::fetch(la, ra, (kt + 1) * BK, tid);
-        SB::fetch(lb, rb, (kt + 1) * BK, tid);
+    for (int kb = kt0; kb < kt1; kb += NPF) {
+#pragma unroll
+      for (int u = 0; u < NPF; ++u) {
+        const int kt = kb + u;            // tile kt + 1 is in set u
+        if (kt < kt1) {
+          const int cur = (kt - kt0) & 1;
+          compute(smem + cur * A_BYTES, smem + 2 * A_BYTES + cur * B_BYTES);
+          if (kt + 1 < kt1) {
+            SA::store(smem + (cur ^ 1) * A_BYTES, ra[u], tid);
+            SB::store(smem + 2 * A_BYTES + (cur ^ 1) * B_BYTES, rb[u], tid);
+            acc_cols(ra[u]);
+            if (kt + 1 + NPF < kt1) {
+              SA::fetch(la, ra[u], (kt + 1 + NPF) * BK, tid);
+              SB::fetch(lb, rb[u], (kt + 1 + NPF) * BK, tid);
+            }
+          }
+          __syncthreads();
+        }
       }
-      const char* ta = smem + cur * A_BYTES;
-      const char* tb = smem + 2 * A_BYTES + cur * B_BYTES;
-#pragma unroll
-      for (int kk = 0; kk < BK / 32; ++kk) {
-        s16x8_t fa[TM], fb[TN];
-#pragma unroll
-        for (int i = 0; i < TM; ++i) fa[i] = SA::frag(ta, lane, wr * (BM / 2) + 16 * i, kk);
-#pragma unroll
-        for (int j = 0; j < TN; ++j) fb[j] = SB::frag(tb, lane, wc * (BN / 2) + 16 * j, kk);
-#pragma unroll
-        for (int i = 0; i < TM; ++i)
-#pragma unroll
-          for (int j = 0; j < TN; ++j)
-            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(
-                __builtin_bit_cast(bf16x8_t, fa[i]), __builtin_bit_cast(bf16x8_t, fb[j]),
-                acc[i][j], 0, 0, 0);
-      }
-      if (more) {
-        SA::store(smem + (cur ^ 1) * A_BYTES, ra, tid);
-        SB::store(smem + 2 * A_BYTES + (cur ^ 1) * B_BYTES, rb, tid);
-        acc_cols();
-      }
-      __syncthreads();
     }
   }
   if constexpr (!LA::kKMajor) {

@@ -36,5 +36,6 @@ void conv_dma_policy(int p);   // 1: LDS-DMA core where eligible (default), 0: i
 // LDS-DMA wgrad tile / split (0: heuristic); noatomic: timing-only racy adds
 void conv_wgrad_force(int bm, int bn, int splits, int noatomic = 0);
 void conv_halo_policy(int p);   // 1: 64-channel 3x3 stride-1 passes on the halo-tile kernel (default)
+bool gemm_select_big_p8(bool ak, bool bk, int M, int N, int K, long lda, long ldb);   // plain-GEMM igemm K-tiles in flight (1..3)
 
 }  // namespace tam

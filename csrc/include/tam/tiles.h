@@ -69,7 +69,7 @@ inline void prepare_split(Epi& ep, int splits, int M, int N, hipStream_t s) {
   ep.mode = 2;
 }
 
-template <int BM, int BN, class LA, class LB>
+template <int BM, int BN, int NPF = 1, class LA, class LB>
 inline void launch_igemm(const LA& la, const LB& lb, int M, int N, int K, const Epi& ep, int splits,
                          hipStream_t s) {
   const int tiles = cdiv(M, BM) * cdiv(N, BN);
@@ -78,7 +78,7 @@ inline void launch_igemm(const LA& la, const LB& lb, int M, int N, int K, const 
   if (kps < 1) kps = 1;
   const int z = cdiv(ktiles, kps) < 1 ? 1 : cdiv(ktiles, kps);
   dim3 grid(tiles, 1, z);
-  hipLaunchKernelGGL((igemm_kernel<BM, BN, LA, LB>), grid, dim3(IG_THREADS), 0, s, la, lb, M, N, K,
+  hipLaunchKernelGGL((igemm_kernel<BM, BN, LA, LB, NPF>), grid, dim3(IG_THREADS), 0, s, la, lb, M, N, K,
                      kps, ep);
 }
 

@@ -9,22 +9,30 @@
 
 namespace tam {
 
+template <int BM, int BN, int NPF>
+static void gemm_tile_p(const bf16_t* A, long lda, bool ak, const bf16_t* B, long ldb, bool bk,
+                        int M, int N, int K, Epi ep, int splits, hipStream_t s) {
+  if (ak && bk) {
+    LdKMajor<BM> la{A, lda, M, K}; LdKMajor<BN> lb{B, ldb, N, K};
+    launch_igemm<BM, BN, NPF>(la, lb, M, N, K, ep, splits, s);
+  } else if (ak && !bk) {
+    LdKMajor<BM> la{A, lda, M, K}; LdMNMajor<BN> lb{B, ldb, N, K};
+    launch_igemm<BM, BN, NPF>(la, lb, M, N, K, ep, splits, s);
+  } else if (!ak && bk) {
+    LdMNMajor<BM> la{A, lda, M, K}; LdKMajor<BN> lb{B, ldb, N, K};
+    launch_igemm<BM, BN, NPF>(la, lb, M, N, K, ep, splits, s);
+  } else {
+    LdMNMajor<BM> la{A, lda, M, K}; LdMNMajor<BN> lb{B, ldb, N, K};
+    launch_igemm<BM, BN, NPF>(la, lb, M, N, K, ep, splits, s);
+  }
+}
+
 template <int BM, int BN>
 static void gemm_tile(const bf16_t* A, long lda, bool ak, const bf16_t* B, long ldb, bool bk,
                       int M, int N, int K, Epi ep, int splits, hipStream_t s) {
-  if (ak && bk) {
-    LdKMajor<BM> la{A, lda, M, K}; LdKMajor<BN> lb{B, ldb, N, K};
-    launch_igemm<BM, BN>(la, lb, M, N, K, ep, splits, s);
-  } else if (ak && !bk) {
-    LdKMajor<BM> la{A, lda, M, K}; LdMNMajor<BN> lb{B, ldb, N, K};
-    launch_igemm<BM, BN>(la, lb, M, N, K, ep, splits, s);
-  } else if (!ak && bk) {
-    LdMNMajor<BM> la{A, lda, M, K}; LdKMajor<BN> lb{B, ldb, N, K};
-    launch_igemm<BM, BN>(la, lb, M, N, K, ep, splits, s);
-  } else {
-    LdMNMajor<BM> la{A, lda, M, K}; LdMNMajor<BN> lb{B, ldb, N, K};
-    launch_igemm<BM, BN>(la, lb, M, N, K, ep, splits, s);
-  }
+  // register prefetch depth 1: depths 2 / 3 (igemm_kernel NPF) measured equal
+  // on the Transformer / GNMT igemm shapes (profiles/r3/s3/ab_igemm_prefetch_depth.json)
+  gemm_tile_p<BM, BN, 1>(A, lda, ak, B, ldb, bk, M, N, K, ep, splits, s);
 }
 
 // tuning hook: force tile config / split count (-1 = heuristic); used by
@@ -218,6 +226,16 @@ static int p8_splits(int M, int N, int K, bool can_split, int tile) {
 void gemm(const bf16_t* A, long lda, bool ak, const bf16_t* B, long ldb, bool bk, int M, int N,
           int K, Epi ep, bool allow_split, hipStream_t s) {
   gemm_select(A, lda, ak, B, ldb, bk, M, N, K, ep, allow_split, s, g_dma ? 2 : 0);
+}
+
+// would gemm_select's own size rule put this shape on the 256^2/128^2
+// LDS-DMA kernel (path 0 / 1 calls)? The bias-gradient fusion (colsum_a, an
+// igemm-only epilogue) is then not worth the igemm fallback
+bool gemm_select_big_p8(bool ak, bool bk, int M, int N, int K, long lda, long ldb) {
+  if (!(g_p8 > 0 && g_force_cfg < 0 && gemm8p_ok(ak, bk, M, N, K, lda, ldb))) return false;
+  const long t8 = (long)cdiv(M, 256) * cdiv(N, 256);
+  const double flop = 2.0 * M * N * K;
+  return g_p8 >= 2 || (t8 >= 48 && K >= 512 && flop >= 4e9);
 }
 
 void gemm_select(const bf16_t* A, long lda, bool ak, const bf16_t* B, long ldb, bool bk, int M,
