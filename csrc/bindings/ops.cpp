@@ -595,14 +595,24 @@ void bn_backward_op(const Tensor& dy, const optional<Tensor>& y, const Tensor& x
                    sp, sums_ready ? 1 : 0, has_mask ? ymask->data_ptr<uint8_t>() : nullptr, cur_stream(x));
 }
 
+// addend / sum_out (both or neither): y = LN(x + addend), sum_out = x + addend
 void ln_forward_op(const Tensor& x, const Tensor& g, const Tensor& b, const Tensor& y,
-                   const Tensor& mean, const Tensor& rstd, double eps) {
+                   const Tensor& mean, const Tensor& rstd, double eps, const optional<Tensor>& addend,
+                   const optional<Tensor>& sum_out) {
   check_bf16(x, "x"); check_bf16(y, "y"); check_contig(x, "x"); check_contig(y, "y");
   check_f32(g, "g"); check_f32(b, "b");
   const int64_t D = x.size(-1);
   TORCH_CHECK(D % 8 == 0 && D <= 2048, "tam.ln: D must be a multiple of 8 and <= 2048");
+  const bool add = addend.has_value() && addend->defined();
+  TORCH_CHECK(add == (sum_out.has_value() && sum_out->defined()), "tam.ln_forward: addend needs sum_out");
+  if (add) {
+    check_bf16(*addend, "addend"); check_contig(*addend, "addend");
+    check_bf16(*sum_out, "sum_out"); check_contig(*sum_out, "sum_out");
+    TORCH_CHECK(addend->numel() == x.numel() && sum_out->numel() == x.numel(), "tam.ln_forward: addend size");
+  }
   tam::ln_forward(bp(x), g.data_ptr<float>(), b.data_ptr<float>(), bpm(y), mean.data_ptr<float>(),
-                  rstd.data_ptr<float>(), x.numel() / D, (int)D, (float)eps, cur_stream(x));
+                  rstd.data_ptr<float>(), x.numel() / D, (int)D, (float)eps, cur_stream(x),
+                  add ? bp(*addend) : nullptr, add ? bpm(*sum_out) : nullptr);
 }
 
 void ln_backward_op(const Tensor& dy, const Tensor& x, const Tensor& g, const Tensor& mean,
@@ -909,7 +919,7 @@ TORCH_LIBRARY(tam, m) {
   m.def("conv_wgrad(Tensor dy, Tensor x, Tensor(a!) dw, int stride, int pad, int dil, int mode) -> ()", &conv_wgrad_op);
   m.def("bn_forward(Tensor x, Tensor? res, Tensor(a!) y, Tensor gamma, Tensor beta, Tensor(b!)? run_mean, Tensor(c!)? run_var, Tensor(d!) save_mean, Tensor(e!) save_rstd, float eps, float momentum, bool relu, Tensor(f!)? sums=None, bool sums_ready=False, Tensor(g!)? ymask=None) -> ()", &bn_forward_op);
   m.def("bn_backward(Tensor dy, Tensor? y, Tensor x, Tensor mean, Tensor rstd, Tensor gamma, Tensor(a!) dx, Tensor(b!)? dres, Tensor(c!)? dgamma, Tensor(d!)? dbeta, bool relu, Tensor? addend=None, Tensor(e!)? sums=None, bool sums_ready=False, Tensor? ymask=None) -> ()", &bn_backward_op);
-  m.def("ln_forward(Tensor x, Tensor g, Tensor b, Tensor(a!) y, Tensor(b!) mean, Tensor(c!) rstd, float eps) -> ()", &ln_forward_op);
+  m.def("ln_forward(Tensor x, Tensor g, Tensor b, Tensor(a!) y, Tensor(b!) mean, Tensor(c!) rstd, float eps, Tensor? addend=None, Tensor(d!)? sum_out=None) -> ()", &ln_forward_op);
   m.def("ln_backward(Tensor dy, Tensor x, Tensor g, Tensor mean, Tensor rstd, Tensor(a!) dx, Tensor(b!) dg, Tensor(c!) db, Tensor? addend=None) -> ()", &ln_backward_op);
   m.def("maxpool_forward(Tensor x, Tensor(a!) y, Tensor(b!) idx, int R, int S, int stride, int pad) -> ()", &maxpool_forward_op);
   m.def("maxpool_backward(Tensor dy, Tensor idx, Tensor(a!) dx, int R, int S, int stride, int pad) -> ()", &maxpool_backward_op);

@@ -50,8 +50,11 @@ void bn_backward(const bf16_t* dy, const bf16_t* addend, const bf16_t* y, const 
                  const uint8_t* ymask, hipStream_t s);
 
 // LayerNorm over last dim D (D % 8 == 0, D <= 2048)
+// addend (optional): LN of (x + addend), the bf16 sum also stored to sum_out
+// (a residual add fused into the next pre-LN)
 void ln_forward(const bf16_t* x, const float* g, const float* b, bf16_t* y, float* mean,
-                float* rstd, long rows, int D, float eps, hipStream_t s);
+                float* rstd, long rows, int D, float eps, hipStream_t s, const bf16_t* addend = nullptr,
+                bf16_t* sum_out = nullptr);
 // dx = LN-backward(dy) (+ addend, the fused gradient of a skip connection)
 void ln_backward(const bf16_t* dy, const bf16_t* x, const float* g, const float* mean,
                  const float* rstd, bf16_t* dx, const bf16_t* addend, float* dg, float* db,

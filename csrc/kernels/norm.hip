@@ -547,7 +547,8 @@ __global__ void __launch_bounds__(256) ln_fwd_kernel(const bf16_t* __restrict__ 
                                                       bf16_t* __restrict__ y,
                                                       float* __restrict__ mean_o,
                                                       float* __restrict__ rstd_o, long rows, int D,
-                                                      float eps) {
+                                                      float eps, const bf16_t* __restrict__ addend,
+                                                      bf16_t* __restrict__ sum_out) {
   const int lane = threadIdx.x & 63;
   const long row = blockIdx.x * 4L + (threadIdx.x >> 6);
   if (row >= rows) return;
@@ -557,8 +558,20 @@ __global__ void __launch_bounds__(256) ln_fwd_kernel(const bf16_t* __restrict__ 
 #pragma unroll
   for (int v = 0; v < VEC; ++v) {
     const int c = (v * 64 + lane) * 8;
-    if (c < D) unpack8(*(const uint4*)(xr + c), f[v]);
-    else {
+    if (c < D) {
+      unpack8(*(const uint4*)(xr + c), f[v]);
+      if (addend) {
+        // fused residual add: the bf16-rounded sum is both stored (the
+        // residual stream) and normalised -- as an add pass + LN would see it
+        float a[8];
+        unpack8(*(const uint4*)(addend + row * D + c), a);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) f[v][j] += a[j];
+        const uint4 pk = pack8(f[v]);
+        *(uint4*)(sum_out + row * D + c) = pk;
+        unpack8(pk, f[v]);
+      }
+    } else {
 #pragma unroll
       for (int j = 0; j < 8; ++j) f[v][j] = 0.f;
     }
@@ -675,11 +688,12 @@ __global__ void __launch_bounds__(256) ln_bwd_kernel(const bf16_t* __restrict__ 
 
 
 void ln_forward(const bf16_t* x, const float* g, const float* b, bf16_t* y, float* mean,
-                float* rstd, long rows, int D, float eps, hipStream_t s) {
+                float* rstd, long rows, int D, float eps, hipStream_t s, const bf16_t* addend,
+                bf16_t* sum_out) {
   const int blocks = (int)((rows + 3) / 4);
-  if (D <= 512) hipLaunchKernelGGL(ln_fwd_kernel<1>, dim3(blocks), dim3(256), 0, s, x, g, b, y, mean, rstd, rows, D, eps);
-  else if (D <= 1024) hipLaunchKernelGGL(ln_fwd_kernel<2>, dim3(blocks), dim3(256), 0, s, x, g, b, y, mean, rstd, rows, D, eps);
-  else hipLaunchKernelGGL(ln_fwd_kernel<4>, dim3(blocks), dim3(256), 0, s, x, g, b, y, mean, rstd, rows, D, eps);
+  if (D <= 512) hipLaunchKernelGGL(ln_fwd_kernel<1>, dim3(blocks), dim3(256), 0, s, x, g, b, y, mean, rstd, rows, D, eps, addend, sum_out);
+  else if (D <= 1024) hipLaunchKernelGGL(ln_fwd_kernel<2>, dim3(blocks), dim3(256), 0, s, x, g, b, y, mean, rstd, rows, D, eps, addend, sum_out);
+  else hipLaunchKernelGGL(ln_fwd_kernel<4>, dim3(blocks), dim3(256), 0, s, x, g, b, y, mean, rstd, rows, D, eps, addend, sum_out);
 }
 
 void ln_backward(const bf16_t* dy, const bf16_t* x, const float* g, const float* mean,

@@ -679,6 +679,13 @@ def test_layernorm(gpu, D, rows):
     dx2 = torch.empty_like(x)
     T().ln_backward(dy, x, g, mean, rstd, dx2, torch.zeros(D, device=gpu), torch.zeros(D, device=gpu), add)
     assert rel_err(dx2, gx + add.float()) < 2e-2
+    # fused residual add in the forward: LN(x + r) and the stored bf16 sum
+    r = torch.randn_like(x.float()).to(BF)
+    sm, y2 = torch.empty_like(x), torch.empty_like(x)
+    m2 = torch.empty(rows, device=gpu); r2 = torch.empty(rows, device=gpu)
+    T().ln_forward(x, g, b, y2, m2, r2, 1e-5, r, sm)
+    assert torch.equal(sm, (x.float() + r.float()).to(BF))
+    assert rel_err(y2, F.layer_norm(sm.float(), (D,), g, b, 1e-5)) < 1e-2
 
 
 # ------------------------------------------------------------------ pooling / loss

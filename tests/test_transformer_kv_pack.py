@@ -26,3 +26,21 @@ def test_packed_cross_attention_kv_matches_sliced(monkeypatch):
     gb = b.arena.grad.clone()
     assert abs(la - lb) < 1e-6
     assert ((ga - gb).norm() / gb.norm()).item() < 1e-6
+
+
+def test_fused_residual_layernorm_matches_add_then_layernorm(monkeypatch):
+    """add_layernorm_skip (the residual add fused into the next pre-LN) gives
+    the same loss and gradients as a separate add + layernorm_skip."""
+    a = Trainer("transformer_tiny", "cpu", seed=4)
+    la = float(a._fwd_bwd())
+    ga = a.arena.grad.clone()
+
+    def unfused(x, r, g, b, eps=1e-5):
+        return Fx.layernorm_skip(Fx.add(x, r), g, b, eps)
+
+    monkeypatch.setattr(Fx, "add_layernorm_skip", unfused)
+    b = Trainer("transformer_tiny", "cpu", seed=4)
+    lb = float(b._fwd_bwd())
+    gb = b.arena.grad.clone()
+    assert abs(la - lb) < 1e-6
+    assert ((ga - gb).norm() / gb.norm()).item() < 1e-6

@@ -660,6 +660,47 @@ def layernorm_skip(x: torch.Tensor, g: Param, b: Param, eps: float = 1e-5):
     return _LNSkip.apply(x, g.arena.token, g, b, eps)
 
 
+class _AddLNSkip(Function):
+    """(s, LN(s)) with s = x + r: the residual add of a pre-LN block fused
+    into the next LayerNorm's forward (one kernel writes s and LN(s)); the
+    backward is _LNSkip's (dskip summed in the LN backward kernel) and hands
+    ds to both addends."""
+
+    @staticmethod
+    def forward(ctx, x, r, token, g: Param, b: Param, eps: float):
+        D = x.shape[-1]
+        rows = x.numel() // D
+        if x.is_cuda:
+            sm = torch.empty_like(x)
+            y = torch.empty_like(x)
+            mean = torch.empty(rows, dtype=torch.float32, device=x.device)
+            rstd = torch.empty_like(mean)
+            _T().ln_forward(x, g.master, b.master, y, mean, rstd, eps, r, sm)
+        else:
+            sm = (x.float() + r.float()).to(BF16)
+            sf = sm.float().reshape(rows, D)
+            mean = sf.mean(1)
+            rstd = torch.rsqrt(sf.var(1, unbiased=False) + eps)
+            y = (((sf - mean[:, None]) * rstd[:, None]) * g.master + b.master).reshape(x.shape).to(BF16)
+        ctx.g, ctx.b = g, b
+        ctx.save_for_backward(sm, mean, rstd)
+        return sm, y
+
+    @staticmethod
+    def backward(ctx, dskip, dy):
+        ds = _LNSkip.backward(ctx, dskip, dy)[0]
+        return ds, ds, None, None, None, None
+
+
+def add_layernorm_skip(x: torch.Tensor, r: torch.Tensor, g: Param, b: Param, eps: float = 1e-5):
+    """(x + r, layernorm(x + r)) in one kernel: ``layernorm_skip(add(x, r))``."""
+    if not x.is_contiguous():
+        x = x.contiguous()
+    if not r.is_contiguous():
+        r = r.contiguous()
+    return _AddLNSkip.apply(x, r, g.arena.token, g, b, eps)
+
+
 # ============================================================ pooling
 class _MaxPool(Function):
     @staticmethod
