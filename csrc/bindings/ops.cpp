@@ -694,6 +694,7 @@ void conv_halo_policy_op(int64_t p) { tam::conv_halo_policy((int)p); }
 void colsum_policy_op(int64_t p) { tam::colsum_policy((int)p); }
 void attn_short_policy_op(int64_t p) { tam::attn_short_policy((int)p); }
 // forced (bm, bn, splits) of the LDS-DMA conv wgrad (A/B sweeps; 0 = heuristic)
+void conv_wgrad_c64_policy_op(int64_t p) { tam::conv_wgrad_c64_policy((int)p); }
 void conv_wgrad_force_op(int64_t bm, int64_t bn, int64_t splits, int64_t noatomic) {
   tam::conv_wgrad_force((int)bm, (int)bn, (int)splits, (int)noatomic);
 }
@@ -937,6 +938,7 @@ TORCH_LIBRARY(tam, m) {
   m.def("gemm_lib_policy(int policy) -> ()", &gemm_lib_policy_op);
   m.def("conv_dma_policy(int policy) -> ()", &conv_dma_policy_op);
   m.def("conv_wgrad_force(int bm, int bn, int splits, int noatomic=0) -> ()", &conv_wgrad_force_op);
+  m.def("conv_wgrad_c64_policy(int policy) -> ()", &conv_wgrad_c64_policy_op);
   m.def("conv_halo_policy(int policy) -> ()", &conv_halo_policy_op);
   m.def("colsum_policy(int policy) -> ()", &colsum_policy_op);
   m.def("attn_short_policy(int policy) -> ()", &attn_short_policy_op);

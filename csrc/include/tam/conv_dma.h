@@ -885,6 +885,173 @@ __global__ void __launch_bounds__(64 * WM * WN, 1) conv_wgrad_dma_kernel(WGArgs 
   }
 }
 
+// ===========================================================================
+// Weight gradient of a 3x3 stride-1 "same" conv, per 64-channel input slice
+// (VGG-16's 224x224 / 112x112 layers, ResNet-50's 56x56 stage): dW is only
+// K x 576 but the pixel reduction is 0.2-1.6 M long, and the tap-gather
+// cores re-read X nine times through L2 (202 TF/s on VGG's first wgrad).
+// Here a block owns a 64-channel k-slice x 64-channel input slice (grid y,
+// z) and sweeps 112-pixel tiles (half a
+// 224 row, a 112 row, or two 56 rows): per tile the dY rows (128-row image,
+// 112 live) and the X PATCH with its halo ((rows+2) x (cols+2) pixels x 64
+// channels, zero padded) are staged ONCE by LDS-DMA, and every tap's B
+// fragment is a per-lane-group shifted read of the patch (8-pixel groups
+// never straddle an image row). Wave w owns N-tiles 9w..9w+8 of the 36
+// (tap, 16-channel) tiles and all four 16-k tiles: 144 fp32 accumulators per
+// lane, one dY fragment per k-tile reused across its 9 B fragments. At the
+// end every accumulator is added into the fp32 dW (no-return atomics).
+// ===========================================================================
+constexpr int WC_TP = 112;                    // live pixels per tile
+constexpr int WC_ROWS = 128;                  // dY image rows (4 chunks of 32)
+// patch rows, largest tile shape (3 x 114 = 342) rounded up to the 8-row
+// (1 KiB) DMA granule: the last DMA group of a patch writes whole 1-KiB
+// blocks, which at 342 rows spilled into the other buffer's dY image
+constexpr int WC_MAXP = 344;
+
+struct WCArgs {
+  const bf16_t* dy;    // [N][H][W][K]
+  const bf16_t* x;     // [N][H][W][C]
+  float* dw;           // [K][3][3][C]
+  int N, H, W, K, C;   // C % 64 == 0: blockIdx.z = 64-channel input slice
+  int tw, tr;          // tile: tr image rows x tw columns (tr * tw == 112)
+  int ntiles;
+};
+
+// MN-major transposed fragment read whose 8 rows for this lane group start
+// at `rbase` (a per-group base instead of kbase + 8g; read_frag_mn's layout)
+__device__ __forceinline__ s16x8_t wc_frag(const char* tile, int lane, int rbase, int colbase) {
+  const int t = lane & 15, q = t >> 2, p = t & 3;
+  const int c8 = (colbase >> 2) + p;
+  s16x4_t lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(tile + mnmaj_off<64>(rbase + q, c8)));
+  s16x4_t hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(tile + mnmaj_off<64>(rbase + q + 4, c8)));
+  s16x8_t r;
+  r[0] = lo[0]; r[1] = lo[1]; r[2] = lo[2]; r[3] = lo[3];
+  r[4] = hi[0]; r[5] = hi[1]; r[6] = hi[2]; r[7] = hi[3];
+  return r;
+}
+
+static __global__ void __launch_bounds__(256, 1) conv_wgrad_c64_kernel(WCArgs a) {
+  // two buffers of [dY image | X patch]: tile t+grid's DMA lands while tile t computes
+  constexpr int BUF = WC_ROWS * 128 + WC_MAXP * 128;
+  __shared__ __attribute__((aligned(1024))) char smem[2 * BUF];
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, g = lane >> 4;
+  const int kb = blockIdx.y * 64, cb = blockIdx.z * 64;
+  const int pw = a.tw + 2, npat = (a.tr + 2) * pw;
+  const int tq = a.W / a.tw, th = a.H / a.tr;
+  f32x4_t acc[4][9];
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 9; ++j) acc[i][j] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+
+  auto stage = [&](int tile, char* buf) {
+    char* dyi = buf;
+    char* pat = buf + WC_ROWS * 128;
+    const int qb = tile % tq, rest = tile / tq;
+    const int hb = rest % th, n = rest / th;
+    const int h0 = hb * a.tr, q0 = qb * a.tw;
+    // dY image: row i = tile pixel i (rows >= 112 zero); the granule for
+    // LDS slot `slot` of row i is source granule slot ^ swz(i) (the DMA
+    // writes lane-linear: the swizzle goes on the source)
+#pragma unroll
+    for (int j = 0; j < WC_ROWS * 8 / 256; ++j) {
+      const int gi = j * 256 + tid;
+      const int row = gi >> 3, slot = gi & 7;
+      const int c = slot ^ (mnmaj_swz<64>(row) >> 1);
+      const bf16_t* src = g_cd_zero + 8 * c;
+      if (row < WC_TP) {
+        const int hh = h0 + row / a.tw, qq = q0 + row % a.tw;
+        src = a.dy + (((long)n * a.H + hh) * a.W + qq) * a.K + kb + 8 * c;
+      }
+      __builtin_amdgcn_global_load_lds((const void*)src, (cd_lds_void_t*)(dyi + (gi >> 6) * 1024), 16, 0, 0);
+    }
+    // X patch: row r = pixel (h0 - 1 + r / pw, q0 - 1 + r % pw), zero outside
+    for (int gi = tid; gi < ((npat * 8 + 63) & ~63); gi += 256) {
+      const int row = gi >> 3, slot = gi & 7;
+      const int c = slot ^ (mnmaj_swz<64>(row) >> 1);
+      const bf16_t* src = g_cd_zero + 8 * c;
+      if (row < npat) {
+        const int hh = h0 - 1 + row / pw, qq = q0 - 1 + row % pw;
+        if ((unsigned)hh < (unsigned)a.H && (unsigned)qq < (unsigned)a.W)
+          src = a.x + (((long)n * a.H + hh) * a.W + qq) * a.C + cb + 8 * c;
+      }
+      __builtin_amdgcn_global_load_lds((const void*)src, (cd_lds_void_t*)(pat + (gi >> 6) * 1024), 16, 0, 0);
+    }
+  };
+
+  if (blockIdx.x < a.ntiles) stage(blockIdx.x, smem);
+  int it = 0;
+  for (int tile = blockIdx.x; tile < a.ntiles; tile += gridDim.x, ++it) {
+    char* buf = smem + (it & 1) * BUF;
+    cd_vm_wait<0>();                 // this tile's DMA (issued one iteration ago) landed ...
+    cd_barrier();                    // ... for every wave; and all are done with the other buffer
+    if (tile + (int)gridDim.x < a.ntiles) stage(tile + gridDim.x, smem + ((it + 1) & 1) * BUF);
+    const char* dyi = buf;
+    const char* pat = buf + WC_ROWS * 128;
+#pragma unroll
+    for (int ch = 0; ch < WC_ROWS / 32; ++ch) {
+      // this lane group's 8 pixels: tile pixel i0 = 32ch + 8g (clamped past 112;
+      // their dY rows are zero)
+      int i0 = 32 * ch + 8 * g;
+      i0 = i0 < WC_TP ? i0 : 0;
+      const int pbase = (i0 / a.tw) * pw + (i0 % a.tw);   // patch row at tap (0, 0)
+      s16x8_t fa[4];
+#pragma unroll
+      for (int kt = 0; kt < 4; ++kt) fa[kt] = read_frag_mn<64>(dyi, lane, 32 * ch, 16 * kt);
+#pragma unroll
+      for (int nn = 0; nn < 9; ++nn) {
+        const int nt = 9 * w + nn, tap = nt >> 2, ct = nt & 3;
+        const int dh = tap / 3, dwc = tap % 3;
+        const s16x8_t fb = wc_frag(pat, lane, pbase + dh * pw + dwc, 16 * ct);
+        __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+        for (int kt = 0; kt < 4; ++kt)
+          acc[kt][nn] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8_t, fa[kt]),
+                                                                __builtin_bit_cast(bf16x8_t, fb), acc[kt][nn], 0, 0, 0);
+        __builtin_amdgcn_s_setprio(0);
+      }
+    }
+  }
+  // ---- dW[kb + 16kt + 4g' + r][tap][16ct + (lane&15)] += acc
+#pragma unroll
+  for (int kt = 0; kt < 4; ++kt)
+#pragma unroll
+    for (int nn = 0; nn < 9; ++nn) {
+      const int nt = 9 * w + nn, tap = nt >> 2, ct = nt & 3;
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int k = kb + 16 * kt + 4 * (lane >> 4) + r;
+        unsafeAtomicAdd(a.dw + (long)k * 9 * a.C + tap * a.C + cb + 16 * ct + (lane & 15), acc[kt][nn][r]);
+      }
+    }
+}
+
+// dW (+)= wgrad of a 3x3 / stride 1 / pad 1 conv over a 64-channel input on
+// conv_wgrad_c64_kernel; false when the shape is not for it
+// force_small: also the 56-wide grids (two-row tiles), measured slower than
+// the tap-gather path on ResNet-50's stage 1 (tests / A/B only)
+inline bool launch_conv_wgrad_c64(const bf16_t* dy, const bf16_t* x, float* dw, const ConvGeom& g, int mode,
+                                  int blocks_per_kslice, hipStream_t s, bool force_small = false) {
+  if (g.C % 64 != 0 || g.R != 3 || g.S != 3 || g.stride != 1 || g.pad != 1 || g.dil != 1 || g.K % 64 != 0)
+    return false;
+  if (g.P != g.H || g.Q != g.W) return false;
+  int tw, tr;
+  if (g.W % 112 == 0) { tw = 112; tr = 1; }
+  else if (g.W == 56 && force_small) { tw = 56; tr = 2; }   // (ResNet's 56x56: 74 vs 61 us on the tap-gather path)
+  else return false;
+  if (g.H % tr != 0 || (long)g.N * g.H * g.W * (g.K > g.C ? g.K : g.C) >= (1L << 31)) return false;
+  if ((((tr + 2) * (tw + 2) + 7) & ~7) > WC_MAXP) return false;   // patch DMA groups must fit the buffer
+  const int ntiles = g.N * (g.H / tr) * (g.W / tw);
+  if (mode == 0) zero_async(dw, (size_t)g.K * 9 * g.C * sizeof(float), s);
+  WCArgs a{dy, x, dw, g.N, g.H, g.W, g.K, g.C, tw, tr, ntiles};
+  const int slices = (g.K / 64) * (g.C / 64);
+  int bx = blocks_per_kslice > 0 ? blocks_per_kslice : 256 / slices;   // one block per CU
+  if (bx < 1) bx = 1;
+  if (bx > ntiles) bx = ntiles;
+  hipLaunchKernelGGL(conv_wgrad_c64_kernel, dim3(bx, g.K / 64, g.C / 64), dim3(256), 0, s, a);
+  return true;
+}
+
 // (bm, bn, splits) forced for A/B sweeps (tools/sweep_wgrad.py); 0 = the
 // heuristic below. [3] != 0: TIMING ONLY -- split blocks add with plain
 // (racy) read-modify-writes instead of atomics, to price the atomic traffic

@@ -35,6 +35,7 @@ void conv_weight_t(const bf16_t* w, bf16_t* wt, const ConvGeom& g, hipStream_t s
 void conv_dma_policy(int p);   // 1: LDS-DMA core where eligible (default), 0: igemm only
 // LDS-DMA wgrad tile / split (0: heuristic); noatomic: timing-only racy adds
 void conv_wgrad_force(int bm, int bn, int splits, int noatomic = 0);
+void conv_wgrad_c64_policy(int p);   // 64-channel 3x3 wgrad kernel: 1 on (default), 0 off, >= 2 blocks per k-slice
 void conv_halo_policy(int p);   // 1: 64-channel 3x3 stride-1 passes on the halo-tile kernel (default)
 bool gemm_select_big_p8(bool ak, bool bk, int M, int N, int K, long lda, long ldb);   // plain-GEMM igemm K-tiles in flight (1..3)
 

@@ -154,8 +154,19 @@ static void wgrad_tile(const bf16_t* dy, const bf16_t* x, const ConvGeom& g, con
   launch_igemm<BM, BN>(la, lb, g.K, Nc, Mred, ep, sp, s);
 }
 
+// 64-channel 3x3 stride-1 weight gradients on the patch-staged kernel
+// (conv_dma.h conv_wgrad_c64_kernel): 1 (default) on with its own grid, 0
+// off (A/B against the tap-gather cores), >= 2: that many blocks per
+// 64-channel k-slice (grid sweeps)
+static int g_wgrad_c64 = 1;
+void conv_wgrad_c64_policy(int p) { g_wgrad_c64 = p; }
+
 void conv_wgrad(const bf16_t* dy, const bf16_t* x, const ConvGeom& g, Epi ep, hipStream_t s) {
   const int Mred = g.N * g.P * g.Q, Nc = g.R * g.S * g.C;
+  if (g_conv_dma && g_wgrad_c64 && ep.c_f32 && ep.ldc == Nc && ep.mode <= 1 &&
+      launch_conv_wgrad_c64(dy, x, (float*)ep.c, g, ep.mode, g_wgrad_c64 >= 2 ? g_wgrad_c64 : 0, s,
+                            g_conv_dma >= 2 || g_wgrad_c64 >= 2))
+    return;
   if (g_conv_dma && ep.c_f32 && ep.ldc == Nc && ep.mode <= 1 &&
       launch_conv_wgrad_dma(dy, x, (float*)ep.c, g, ep.mode, s, g_conv_dma >= 2))
     return;

@@ -320,6 +320,38 @@ def _ref_conv(x, w, stride, pad):
                     padding=pad).permute(0, 2, 3, 1)
 
 
+@pytest.mark.parametrize("cfg", [(2, 8, 56, 64, 64), (1, 4, 224, 64, 64), (2, 6, 112, 128, 64),
+                                 (3, 14, 56, 192, 64), (1, 2, 112, 64, 64), (2, 4, 112, 128, 128),
+                                 (1, 4, 56, 64, 192)])
+@pytest.mark.parametrize("mode", [0, 1])
+def test_conv_wgrad_c64(gpu, cfg, mode):
+    """3x3 stride-1 weight gradient on the patch-staged kernel (halo rows /
+    columns zero-padded, 112-pixel tiles incl. two-row tiles at W=56, several
+    64-channel k- and input-channel slices, accumulate mode) vs fp32 torch,
+    and vs the tap-gather path."""
+    N, H, W, K, C = cfg
+    torch.manual_seed(17)
+    x = torch.randn(N, H, W, C, device=gpu).to(BF)
+    dy = torch.randn(N, H, W, K, device=gpu).to(BF)
+    xf = x.float().permute(0, 3, 1, 2)
+    wf = torch.zeros(K, C, 3, 3, device=gpu, requires_grad=True)
+    gw, = torch.autograd.grad(F.conv2d(xf, wf, padding=1), [wf], dy.float().permute(0, 3, 1, 2))
+    ref = gw.permute(0, 2, 3, 1)
+    outs = []
+    try:
+        # kernel default grid / tap-gather path / 2 and 7 blocks per slice (many
+        # tiles per block: both LDS buffers recycled several times)
+        for pol in (1, 0, 2, 7):
+            T().conv_wgrad_c64_policy(pol)
+            dw = torch.full((K, 3, 3, C), 0.25, device=gpu)
+            T().conv_wgrad(dy, x, dw, 1, 1, 1, mode)
+            outs.append(dw - (0.25 if mode == 1 else 0.0))
+    finally:
+        T().conv_wgrad_c64_policy(1)
+    for o in outs:
+        assert rel_err(o, ref) < 1e-3
+
+
 @pytest.mark.parametrize("cfg", CONVS)
 def test_conv_fwd_dgrad_wgrad(gpu, cfg):
     N, H, W, C, K, R, st, pd = cfg

@@ -56,6 +56,9 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--models", default="resnet50,vgg16")
     ap.add_argument("--out", default=None)
+    ap.add_argument("--c64_ab", action="store_true",
+                    help="3x3 stride-1 layers with C, K % 64 == 0 only: the patch-staged kernel (default grid; "
+                         "64 / 256 blocks per slice) vs the tap-gather path, interleaved rounds, numerics")
     ap.add_argument("--atomic_ab", action="store_true",
                     help="only time the heuristic with atomics vs racy plain adds (prices the atomics)")
     a = ap.parse_args()
@@ -75,6 +78,24 @@ def main():
         dw.zero_(); run(); torch.cuda.synchronize(); ref = dw.clone()
         row = {"model": model, "shape": [N, H, W, C, K, R, st, pd], "calls": calls,
                "auto_us": round(_time(run), 2)}
+        if a.c64_ab:
+            if not (C % 64 == 0 and K % 64 == 0 and R == 3 and st == 1):
+                continue
+            best = {}
+            for _ in range(2):
+                for pol in (0, 1, 64, 256):
+                    T.conv_wgrad_c64_policy(pol)
+                    best[pol] = min(best.get(pol, 1e9), _time(run))
+            T.conv_wgrad_c64_policy(0)
+            dw.zero_(); run(); torch.cuda.synchronize(); r0 = dw.clone()
+            T.conv_wgrad_c64_policy(1)
+            dw.zero_(); run(); torch.cuda.synchronize()
+            row.update({"gather_us": round(best[0], 2), "c64_us": round(best[1], 2), "c64_g64_us": round(best[64], 2),
+                        "c64_g256_us": round(best[256], 2),
+                        "rel_diff": float((dw - r0).norm() / r0.norm().clamp_min(1e-30))})
+            out.append(row)
+            print(json.dumps(row), flush=True)
+            continue
         if a.atomic_ab:
             T.conv_wgrad_force(0, 0, 0, 1)
             row["noatomic_us"] = round(_time(run), 2)
