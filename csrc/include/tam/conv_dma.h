@@ -1034,6 +1034,7 @@ inline bool launch_conv_wgrad_c64(const bf16_t* dy, const bf16_t* x, float* dw, 
                                   int blocks_per_kslice, hipStream_t s, bool force_small = false) {
   if (g.C % 64 != 0 || g.R != 3 || g.S != 3 || g.stride != 1 || g.pad != 1 || g.dil != 1 || g.K % 64 != 0)
     return false;
+  if (g.C != 64 && !force_small) return false;   // wider inputs (channel slices): tests / A/B until measured
   if (g.P != g.H || g.Q != g.W) return false;
   int tw, tr;
   if (g.W % 112 == 0) { tw = 112; tr = 1; }
