@@ -155,10 +155,14 @@ static void wgrad_tile(const bf16_t* dy, const bf16_t* x, const ConvGeom& g, con
 }
 
 // 64-channel 3x3 stride-1 weight gradients on the patch-staged kernel
-// (conv_dma.h conv_wgrad_c64_kernel): 1 (default) on with its own grid, 0
-// off (A/B against the tap-gather cores), >= 2: that many blocks per
-// 64-channel k-slice (grid sweeps)
-static int g_wgrad_c64 = 1;
+// (conv_dma.h conv_wgrad_c64_kernel): 1 on with its own grid, 0 (default)
+// off, >= 2: that many blocks per 64-channel k-slice (grid sweeps). Off by
+// default: 2x faster in isolation (VGG-16 224x224: 585 -> 302 us) but its
+// 120 KB of LDS per CU starves the main-stream kernels it co-runs with when
+// the weight gradients are on the side stream (VGG-16 graph step 7.42 ->
+// 7.52 ms, tools/ab_vgg_c64.py); the side-stream-aware routing is on branch
+// work pending GPU validation
+static int g_wgrad_c64 = 0;
 void conv_wgrad_c64_policy(int p) { g_wgrad_c64 = p; }
 
 void conv_wgrad(const bf16_t* dy, const bf16_t* x, const ConvGeom& g, Epi ep, hipStream_t s) {

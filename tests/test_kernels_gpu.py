@@ -347,7 +347,7 @@ def test_conv_wgrad_c64(gpu, cfg, mode):
             T().conv_wgrad(dy, x, dw, 1, 1, 1, mode)
             outs.append(dw - (0.25 if mode == 1 else 0.0))
     finally:
-        T().conv_wgrad_c64_policy(1)
+        T().conv_wgrad_c64_policy(0)
     for o in outs:
         assert rel_err(o, ref) < 1e-3
 
