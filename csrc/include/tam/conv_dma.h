@@ -721,6 +721,7 @@ struct WGArgs {
   int steps_per_split; // 64-pixel steps per blockIdx.z
   int dn, dp, dq;      // 64 pixels = dn images + dp rows + dq columns
   int atomic;          // 1: atomic add, 0: plain += (single split)
+  float* dbias;        // optional: dbias[k] += sum_m dY[m][k] (the conv's bias gradient)
 };
 
 template <int S>
@@ -825,6 +826,12 @@ __global__ void __launch_bounds__(64 * WM * WN, 1) conv_wgrad_dma_kernel(WGArgs 
   for (int i = 0; i < TM; ++i)
 #pragma unroll
     for (int j = 0; j < TN; ++j) acc[i][j] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+  // fused bias gradient: the column-tile-0 blocks' wn == 0 waves add up the
+  // dY fragments they already read (lane: 8 pixels of channel 16i + lane%16)
+  const bool bsum_on = a.dbias != nullptr && tn == 0 && wn == 0;
+  float bsum[TM];
+#pragma unroll
+  for (int i = 0; i < TM; ++i) bsum[i] = 0.f;
 
   if (nk > 0) {
 #pragma unroll
@@ -849,6 +856,12 @@ __global__ void __launch_bounds__(64 * WM * WN, 1) conv_wgrad_dma_kernel(WGArgs 
           const int c = wm * (BM / WM) + 16 * i;
           fa[i] = read_frag_mn<SA>(ta + (c / SA) * (BK * SA * 2), lane, 32 * kk, c % SA);
         }
+        if (bsum_on) {
+#pragma unroll
+          for (int i = 0; i < TM; ++i)
+#pragma unroll
+            for (int e = 0; e < 8; ++e) bsum[i] += __uint_as_float((uint32_t)(uint16_t)fa[i][e] << 16);
+        }
 #pragma unroll
         for (int j = 0; j < TN; ++j) {
           const int c = wn * (BN / WN) + 16 * j;
@@ -867,6 +880,16 @@ __global__ void __launch_bounds__(64 * WM * WN, 1) conv_wgrad_dma_kernel(WGArgs 
     }
   }
 
+  if (bsum_on) {
+#pragma unroll
+    for (int i = 0; i < TM; ++i) {
+      float v = bsum[i];
+      v += __shfl_xor(v, 16, 64);
+      v += __shfl_xor(v, 32, 64);
+      const int k = k0 + wm * (BM / WM) + 16 * i + lane;
+      if (lane < 16 && k < a.K) atomicAdd(a.dbias + k, v);
+    }
+  }
   // ---- epilogue: row = k, col = (r,s,c); fp32 accumulate into dW
 #pragma unroll
   for (int j = 0; j < TN; ++j) {
@@ -915,6 +938,7 @@ struct WCArgs {
   int N, H, W, K, C;   // C % 64 == 0: blockIdx.z = 64-channel input slice
   int tw, tr;          // tile: tr image rows x tw columns (tr * tw == 112)
   int ntiles;
+  float* dbias;        // optional: dbias[k] += sum dY[.][k] (input slice 0, wave 0)
 };
 
 // MN-major transposed fragment read whose 8 rows for this lane group start
@@ -943,6 +967,9 @@ static __global__ void __launch_bounds__(256, 1) conv_wgrad_c64_kernel(WCArgs a)
   for (int i = 0; i < 4; ++i)
 #pragma unroll
     for (int j = 0; j < 9; ++j) acc[i][j] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+  // fused bias gradient from the dY fragments wave 0 of input slice 0 reads
+  const bool bsum_on = a.dbias != nullptr && blockIdx.z == 0 && w == 0;
+  float bsum[4] = {0.f, 0.f, 0.f, 0.f};
 
   auto stage = [&](int tile, char* buf) {
     char* dyi = buf;
@@ -998,6 +1025,12 @@ static __global__ void __launch_bounds__(256, 1) conv_wgrad_c64_kernel(WCArgs a)
       s16x8_t fa[4];
 #pragma unroll
       for (int kt = 0; kt < 4; ++kt) fa[kt] = read_frag_mn<64>(dyi, lane, 32 * ch, 16 * kt);
+      if (bsum_on) {
+#pragma unroll
+        for (int kt = 0; kt < 4; ++kt)
+#pragma unroll
+          for (int e = 0; e < 8; ++e) bsum[kt] += __uint_as_float((uint32_t)(uint16_t)fa[kt][e] << 16);
+      }
 #pragma unroll
       for (int nn = 0; nn < 9; ++nn) {
         const int nt = 9 * w + nn, tap = nt >> 2, ct = nt & 3;
@@ -1010,6 +1043,15 @@ static __global__ void __launch_bounds__(256, 1) conv_wgrad_c64_kernel(WCArgs a)
                                                                 __builtin_bit_cast(bf16x8_t, fb), acc[kt][nn], 0, 0, 0);
         __builtin_amdgcn_s_setprio(0);
       }
+    }
+  }
+  if (bsum_on) {
+#pragma unroll
+    for (int kt = 0; kt < 4; ++kt) {
+      float v = bsum[kt];
+      v += __shfl_xor(v, 16, 64);
+      v += __shfl_xor(v, 32, 64);
+      if (lane < 16) atomicAdd(a.dbias + kb + 16 * kt + lane, v);
     }
   }
   // ---- dW[kb + 16kt + 4g' + r][tap][16ct + (lane&15)] += acc
@@ -1031,7 +1073,8 @@ static __global__ void __launch_bounds__(256, 1) conv_wgrad_c64_kernel(WCArgs a)
 // force_small: also the 56-wide grids (two-row tiles), measured slower than
 // the tap-gather path on ResNet-50's stage 1 (tests / A/B only)
 inline bool launch_conv_wgrad_c64(const bf16_t* dy, const bf16_t* x, float* dw, const ConvGeom& g, int mode,
-                                  int blocks_per_kslice, hipStream_t s, bool force_small = false) {
+                                  int blocks_per_kslice, hipStream_t s, bool force_small = false,
+                                  float* dbias = nullptr) {
   if (g.C % 64 != 0 || g.R != 3 || g.S != 3 || g.stride != 1 || g.pad != 1 || g.dil != 1 || g.K % 64 != 0)
     return false;
   if (g.C != 64 && !force_small) return false;   // wider inputs (channel slices): tests / A/B until measured
@@ -1044,7 +1087,7 @@ inline bool launch_conv_wgrad_c64(const bf16_t* dy, const bf16_t* x, float* dw, 
   if ((((tr + 2) * (tw + 2) + 7) & ~7) > WC_MAXP) return false;   // patch DMA groups must fit the buffer
   const int ntiles = g.N * (g.H / tr) * (g.W / tw);
   if (mode == 0) zero_async(dw, (size_t)g.K * 9 * g.C * sizeof(float), s);
-  WCArgs a{dy, x, dw, g.N, g.H, g.W, g.K, g.C, tw, tr, ntiles};
+  WCArgs a{dy, x, dw, g.N, g.H, g.W, g.K, g.C, tw, tr, ntiles, dbias};
   const int slices = (g.K / 64) * (g.C / 64);
   int bx = blocks_per_kslice > 0 ? blocks_per_kslice : 256 / slices;   // one block per CU
   if (bx < 1) bx = 1;
@@ -1066,7 +1109,7 @@ inline void wgrad_dma_launch(const WGArgs& a, int tiles, int splits, hipStream_t
 
 // dw += conv wgrad (mode 1 semantics; mode 0 callers zero dw first)
 inline bool launch_conv_wgrad_dma(const bf16_t* dy, const bf16_t* x, float* dw, const ConvGeom& g,
-                                  int mode, hipStream_t s, bool force = false) {
+                                  int mode, hipStream_t s, bool force = false, float* dbias = nullptr) {
   if (g.dil != 1 || g.C % 64 != 0 || g.K % 64 != 0) return false;
   const long Mred = (long)g.N * g.P * g.Q;
   if (Mred >= (1L << 31) || (long)g.N * g.H * g.W * g.C >= (1L << 31)) return false;
@@ -1100,7 +1143,7 @@ inline bool launch_conv_wgrad_dma(const bf16_t* dy, const bf16_t* x, float* dw, 
   if (mode == 0) zero_async(dw, (size_t)g.K * ncols * sizeof(float), s);
   const int PQ = g.P * g.Q;
   WGArgs a{dy, x, dw, ncols, g.K, g.C, g.H, g.W, g.P, g.Q, g.S, g.stride, g.pad, (int)Mred, sps,
-           64 / PQ, (64 % PQ) / g.Q, (64 % PQ) % g.Q, splits > 1 && !fw[3] ? 1 : 0};
+           64 / PQ, (64 % PQ) / g.Q, (64 % PQ) % g.Q, splits > 1 && !fw[3] ? 1 : 0, dbias};
   if (bm == 256 && bn == 128) wgrad_dma_launch<256, 128, 4, 2>(a, tiles, splits, s);
   else if (bm == 256) wgrad_dma_launch<256, 64, 4, 1>(a, tiles, splits, s);
   else if (bm == 128 && bn == 128) wgrad_dma_launch<128, 128, 2, 2>(a, tiles, splits, s);

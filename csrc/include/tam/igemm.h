@@ -506,6 +506,59 @@ igemm_kernel(LA la, LB lb, int M, int N, int K, int ktiles_per_split, Epi ep) {
     return;
   }
 
+  // ---- fp32 store / accumulate (no atomics): LDS-staged, 16-B row chunks.
+  // A rank-k update with tiny K (VGG's classifier weight gradients, K = the
+  // batch) is bound by the read-modify-write of C: whole 16-B chunks of
+  // consecutive columns per lane instead of the MFMA layout's 4-B stores
+  if (ep.c_f32 && (ep.mode == 0 || ep.mode == 1) && !ep.mask && (ep.ldc & 3) == 0 &&
+      (((uintptr_t)ep.c) & 15) == 0) {
+    constexpr int WR = BM / 2, WC = BN / 2, HR = WR < 32 ? WR : 32, LDF = WC + 4, CPR = WC / 4;
+    static_assert(4 * HR * LDF * 4 <= 2 * (A_BYTES + B_BYTES), "fp32 staging exceeds the igemm LDS");
+    float* slab = (float*)smem + wid * (HR * LDF);
+    if (kt0 >= kt1) __syncthreads();   // (the K loop ends with a barrier otherwise)
+    const int cbase = n0 + wc * WC;
+    float bv[TN];
+#pragma unroll
+    for (int j = 0; j < TN; ++j) {
+      const int col = cbase + 16 * j + (lane & 15);
+      bv[j] = (add_bias && col < N) ? bf2f(ep.bias[col]) : 0.f;
+    }
+#pragma unroll
+    for (int h = 0; h < WR / HR; ++h) {
+#pragma unroll
+      for (int ii = 0; ii < HR / 16; ++ii)
+#pragma unroll
+        for (int j = 0; j < TN; ++j)
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            float v = acc[h * (HR / 16) + ii][j][r] * ep.alpha + bv[j];
+            if (ep.relu) v = fmaxf(v, 0.f);
+            slab[(16 * ii + 4 * (lane >> 4) + r) * LDF + 16 * j + (lane & 15)] = v;
+          }
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+#pragma unroll
+      for (int u = 0; u < (HR * CPR + 63) / 64; ++u) {
+        const int idx = u * 64 + lane, lr = idx / CPR, ch = idx % CPR;
+        const int row = m0 + wr * WR + h * HR + lr, col = cbase + ch * 4;
+        if (lr >= HR || row >= M || col >= N) continue;
+        float* dst = (float*)ep.c + (long)row * ep.ldc + col;
+        const float* src = slab + lr * LDF + ch * 4;
+        if (col + 4 <= N) {
+          float4 v = *(const float4*)src;
+          if (ep.mode == 1) {
+            const float4 o = *(const float4*)dst;
+            v.x += o.x; v.y += o.y; v.z += o.z; v.w += o.w;
+          }
+          *(float4*)dst = v;
+        } else {
+          for (int e = 0; e < 4 && col + e < N; ++e) dst[e] = ep.mode == 1 ? dst[e] + src[e] : src[e];
+        }
+      }
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    }
+    return;
+  }
+
   // ---- epilogue: C/D map of 16x16x32: col = lane&15, row = (lane>>4)*4 + r
 #pragma unroll
   for (int j = 0; j < TN; ++j) {

@@ -165,20 +165,27 @@ static void wgrad_tile(const bf16_t* dy, const bf16_t* x, const ConvGeom& g, con
 static int g_wgrad_c64 = 0;
 void conv_wgrad_c64_policy(int p) { g_wgrad_c64 = p; }
 
-void conv_wgrad(const bf16_t* dy, const bf16_t* x, const ConvGeom& g, Epi ep, hipStream_t s) {
+// dbias (optional, fp32 [K]): += the bias gradient sum_m dY[m][k], fused
+// into whichever wgrad kernel runs (each reads dY anyway); returns 1 when
+// fused, 0 when the caller must add it itself (the LDS-DMA GEMM route of a
+// pointwise wgrad has no such epilogue)
+int conv_wgrad(const bf16_t* dy, const bf16_t* x, const ConvGeom& g, Epi ep, hipStream_t s, float* dbias) {
   const int Mred = g.N * g.P * g.Q, Nc = g.R * g.S * g.C;
   if (g_conv_dma && g_wgrad_c64 && ep.c_f32 && ep.ldc == Nc && ep.mode <= 1 &&
       launch_conv_wgrad_c64(dy, x, (float*)ep.c, g, ep.mode, g_wgrad_c64 >= 2 ? g_wgrad_c64 : 0, s,
-                            g_conv_dma >= 2 || g_wgrad_c64 >= 2))
-    return;
+                            g_conv_dma >= 2 || g_wgrad_c64 >= 2, dbias))
+    return dbias ? 1 : 0;
   if (g_conv_dma && ep.c_f32 && ep.ldc == Nc && ep.mode <= 1 &&
-      launch_conv_wgrad_dma(dy, x, (float*)ep.c, g, ep.mode, s, g_conv_dma >= 2))
-    return;
+      launch_conv_wgrad_dma(dy, x, (float*)ep.c, g, ep.mode, s, g_conv_dma >= 2, dbias))
+    return dbias ? 1 : 0;
   if (is_pointwise(g)) {
     // dW[k][c] = sum_m dY[m][k] X[m][c]: A(k', m) = dY[m*K + k'], B(m, c) = X[m*C + c]
+    const bool big = gemm_select_big_p8(false, false, g.K, g.C, Mred, g.K, g.C);
+    if (!big) ep.colsum_a = dbias;
     gemm(dy, g.K, false, x, g.C, false, g.K, g.C, Mred, ep, true, s);
-    return;
+    return (dbias && !big) ? 1 : 0;
   }
+  ep.colsum_a = dbias;                    // the gather igemm: A = dY, M-major
   TileChoice t = choose_tiles(g.K, Nc, Mred, true);
   if (t.splits > 1 && Nc >= 256) {       // (stem-like Nc = 72 stays on 64x64 tiles)
     // split-K regime (tiny dW, huge pixel reduction): every N tile re-reads
@@ -199,6 +206,7 @@ void conv_wgrad(const bf16_t* dy, const bf16_t* x, const ConvGeom& g, Epi ep, hi
     case 2: wgrad_tile<64, 128>(dy, x, g, ep, t.splits, s); break;
     default: wgrad_tile<64, 64>(dy, x, g, ep, t.splits, s); break;
   }
+  return dbias ? 1 : 0;
 }
 
 // wt[c][(r*S+s)*K + k] = w[k][(r*S+s)*C + c]

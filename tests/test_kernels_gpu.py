@@ -344,12 +344,15 @@ def test_conv_wgrad_c64(gpu, cfg, mode):
         for pol in (1, 0, 2, 7):
             T().conv_wgrad_c64_policy(pol)
             dw = torch.full((K, 3, 3, C), 0.25, device=gpu)
-            T().conv_wgrad(dy, x, dw, 1, 1, 1, mode)
-            outs.append(dw - (0.25 if mode == 1 else 0.0))
+            db = torch.full((K,), 0.5, device=gpu)       # fused bias gradient (+=)
+            T().conv_wgrad(dy, x, dw, 1, 1, 1, mode, db)
+            outs.append((dw - (0.25 if mode == 1 else 0.0), db - 0.5))
     finally:
         T().conv_wgrad_c64_policy(0)
-    for o in outs:
+    ref_b = dy.float().sum((0, 1, 2))
+    for o, b in outs:
         assert rel_err(o, ref) < 1e-3
+        assert rel_err(b, ref_b) < 1e-4
 
 
 @pytest.mark.parametrize("cfg", CONVS)
@@ -373,7 +376,9 @@ def test_conv_fwd_dgrad_wgrad(gpu, cfg):
     T().conv_dgrad(dy, w, wt, dx, st, pd, 1, None)
     assert rel_err(dx, gx.permute(0, 2, 3, 1)) < 1e-2
     dw = torch.zeros(K, R, R, C, device=gpu)
-    T().conv_wgrad(dy, x, dw, st, pd, 1, 0)
+    db = torch.zeros(K, device=gpu)
+    T().conv_wgrad(dy, x, dw, st, pd, 1, 0, db)
+    assert rel_err(db, dy.float().sum((0, 1, 2))) < 1e-4
     assert rel_err(dw, gw.permute(0, 2, 3, 1)) < 1e-4
 
 

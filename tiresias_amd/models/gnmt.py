@@ -170,8 +170,10 @@ class _LSTMLayer(Function):
             with Fx._OnWgrad(dG2, Hs, x):        # overlaps the next layer's recurrence
                 if T > 1:
                     _T().gemm(dGh, False, Hp, False, w_hh.grad, 1, None, False, None, 1.0, True)
-                _T().gemm(dG2, False, x.reshape(T * B, I), False, w_ih.grad, 1, None, False, None, 1.0, True)
-                _T().colsum(dG2, b.grad)
+                # bias gradient colsum(dG) fused into the weight-gradient GEMM
+                # where it runs on the igemm, else a pass inside the op
+                _T().gemm(dG2, False, x.reshape(T * B, I), False, w_ih.grad, 1, None, False, None, 1.0, True,
+                          b.grad)
             dx = None
             if ctx.needs_input_grad[0]:
                 dx = torch.empty(T * B, I, dtype=BF16, device=dev)

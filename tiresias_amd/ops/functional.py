@@ -290,9 +290,8 @@ class _Conv(Function):
         dx = None
         if dy.is_cuda:
             with _OnWgrad(dy, x):
-                _T().conv_wgrad(dy, x, w.grad, st, pd, 1, 1)
-                if b is not None:
-                    _T().colsum(dy, b.grad)
+                # the bias gradient colsum(dy) rides on the wgrad kernel's dY reads
+                _T().conv_wgrad(dy, x, w.grad, st, pd, 1, 1, b.grad if b is not None else None)
             if ctx.needs_input_grad[0]:
                 dx = torch.empty_like(x)
                 wt = getattr(w, "wt", None)
