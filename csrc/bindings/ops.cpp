@@ -513,7 +513,7 @@ int64_t conv_dgrad_pre_op(const Tensor& dy, const Tensor& w, const Tensor& wt, c
 // dbias (optional, fp32 [K]): += the bias gradient colsum(dY), fused into the
 // wgrad kernel where it has the epilogue, else a column-sum pass
 void conv_wgrad_op(const Tensor& dy, const Tensor& x, const Tensor& dw, int64_t stride, int64_t pad,
-                   int64_t dil, int64_t mode, const optional<Tensor>& dbias) {
+                   int64_t dil, int64_t mode, const optional<Tensor>& dbias, bool patch) {
   check_bf16(dy, "dy"); check_bf16(x, "x"); check_f32(dw, "dw");
   check_contig(dy, "dy"); check_contig(x, "x"); check_contig(dw, "dw");
   TORCH_CHECK(dw.dim() == 4, "tam.conv_wgrad: dw must be [K,R,S,C]");
@@ -526,7 +526,7 @@ void conv_wgrad_op(const Tensor& dy, const Tensor& x, const Tensor& dw, int64_t 
     TORCH_CHECK(dbias->numel() == g.K && dbias->is_contiguous(), "tam.conv_wgrad: dbias size");
     db = dbias->data_ptr<float>();
   }
-  const int fused = tam::conv_wgrad(bp(dy), bp(x), g, ep, cur_stream(dy), db);
+  const int fused = tam::conv_wgrad(bp(dy), bp(x), g, ep, cur_stream(dy), db, patch);
   if (db && !fused) {
     const long R = (long)g.N * g.P * g.Q;
     Tensor ws = at::empty({g.K % 8 == 0 ? (int64_t)tam::COLSUM_MAX_BLOCKS * g.K : 1}, dy.options().dtype(at::kFloat));
@@ -930,7 +930,7 @@ TORCH_LIBRARY(tam, m) {
   m.def("conv_dgrad(Tensor dy, Tensor w, Tensor(a!) wt, Tensor(b!) dx, int stride, int pad, int dil, Tensor? mask) -> ()", &conv_dgrad_op);
   m.def("conv_weight_t_batch(Tensor[] w, Tensor(a!)[] wt) -> ()", &conv_weight_t_batch_op);
   m.def("conv_dgrad_pre(Tensor dy, Tensor w, Tensor wt, Tensor(a!) dx, int stride, int pad, int dil, Tensor? mask, Tensor(b!)? stats=None, Tensor? bnx=None, Tensor? bnmean=None, Tensor? bnrstd=None) -> int", &conv_dgrad_pre_op);
-  m.def("conv_wgrad(Tensor dy, Tensor x, Tensor(a!) dw, int stride, int pad, int dil, int mode, Tensor(b!)? dbias=None) -> ()", &conv_wgrad_op);
+  m.def("conv_wgrad(Tensor dy, Tensor x, Tensor(a!) dw, int stride, int pad, int dil, int mode, Tensor(b!)? dbias=None, bool patch=True) -> ()", &conv_wgrad_op);
   m.def("bn_forward(Tensor x, Tensor? res, Tensor(a!) y, Tensor gamma, Tensor beta, Tensor(b!)? run_mean, Tensor(c!)? run_var, Tensor(d!) save_mean, Tensor(e!) save_rstd, float eps, float momentum, bool relu, Tensor(f!)? sums=None, bool sums_ready=False, Tensor(g!)? ymask=None) -> ()", &bn_forward_op);
   m.def("bn_backward(Tensor dy, Tensor? y, Tensor x, Tensor mean, Tensor rstd, Tensor gamma, Tensor(a!) dx, Tensor(b!)? dres, Tensor(c!)? dgamma, Tensor(d!)? dbeta, bool relu, Tensor? addend=None, Tensor(e!)? sums=None, bool sums_ready=False, Tensor? ymask=None) -> ()", &bn_backward_op);
   m.def("ln_forward(Tensor x, Tensor g, Tensor b, Tensor(a!) y, Tensor(b!) mean, Tensor(c!) rstd, float eps, Tensor? addend=None, Tensor(d!)? sum_out=None) -> ()", &ln_forward_op);

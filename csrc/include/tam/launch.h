@@ -31,7 +31,7 @@ int conv_dgrad(const bf16_t* dy, const bf16_t* w, const bf16_t* wt, const ConvGe
                 hipStream_t s);
 // dw[K][R*S*C] fp32, ep.mode 0 (overwrite) or 1 (accumulate)
 int conv_wgrad(const bf16_t* dy, const bf16_t* x, const ConvGeom& g, Epi ep, hipStream_t s,
-               float* dbias = nullptr);
+               float* dbias = nullptr, bool allow_patch = true);
 void conv_weight_t(const bf16_t* w, bf16_t* wt, const ConvGeom& g, hipStream_t s);
 void conv_dma_policy(int p);   // 1: LDS-DMA core where eligible (default), 0: igemm only
 // LDS-DMA wgrad tile / split (0: heuristic); noatomic: timing-only racy adds

@@ -169,9 +169,14 @@ void conv_wgrad_c64_policy(int p) { g_wgrad_c64 = p; }
 // into whichever wgrad kernel runs (each reads dY anyway); returns 1 when
 // fused, 0 when the caller must add it itself (the LDS-DMA GEMM route of a
 // pointwise wgrad has no such epilogue)
-int conv_wgrad(const bf16_t* dy, const bf16_t* x, const ConvGeom& g, Epi ep, hipStream_t s, float* dbias) {
+// allow_patch: the caller's stream does not run beside the main compute
+// stream (the patch kernel holds 120 KB of LDS per CU for its whole run and
+// starves co-running kernels: VGG-16's graph step with the weight gradients
+// on the side stream measured 7.42 -> 7.52 ms with it)
+int conv_wgrad(const bf16_t* dy, const bf16_t* x, const ConvGeom& g, Epi ep, hipStream_t s, float* dbias,
+               bool allow_patch) {
   const int Mred = g.N * g.P * g.Q, Nc = g.R * g.S * g.C;
-  if (g_conv_dma && g_wgrad_c64 && ep.c_f32 && ep.ldc == Nc && ep.mode <= 1 &&
+  if (g_conv_dma && g_wgrad_c64 && (allow_patch || g_wgrad_c64 >= 2) && ep.c_f32 && ep.ldc == Nc && ep.mode <= 1 &&
       launch_conv_wgrad_c64(dy, x, (float*)ep.c, g, ep.mode, g_wgrad_c64 >= 2 ? g_wgrad_c64 : 0, s,
                             g_conv_dma >= 2 || g_wgrad_c64 >= 2, dbias))
     return dbias ? 1 : 0;

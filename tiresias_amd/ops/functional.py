@@ -289,9 +289,10 @@ class _Conv(Function):
                 dy = (dy.float() * (y.float() > 0)).to(BF16)
         dx = None
         if dy.is_cuda:
-            with _OnWgrad(dy, x):
-                # the bias gradient colsum(dy) rides on the wgrad kernel's dY reads
-                _T().conv_wgrad(dy, x, w.grad, st, pd, 1, 1, b.grad if b is not None else None)
+            with _OnWgrad(dy, x) as ow:
+                # the bias gradient colsum(dy) rides on the wgrad kernel's dY reads;
+                # the LDS-heavy patch-staged wgrad only off the side stream
+                _T().conv_wgrad(dy, x, w.grad, st, pd, 1, 1, b.grad if b is not None else None, ow.s is None)
             if ctx.needs_input_grad[0]:
                 dx = torch.empty_like(x)
                 wt = getattr(w, "wt", None)
