@@ -155,14 +155,14 @@ static void wgrad_tile(const bf16_t* dy, const bf16_t* x, const ConvGeom& g, con
 }
 
 // 64-channel 3x3 stride-1 weight gradients on the patch-staged kernel
-// (conv_dma.h conv_wgrad_c64_kernel): 1 on with its own grid, 0 (default)
-// off, >= 2: that many blocks per 64-channel k-slice (grid sweeps). Off by
-// default: 2x faster in isolation (VGG-16 224x224: 585 -> 302 us) but its
-// 120 KB of LDS per CU starves the main-stream kernels it co-runs with when
-// the weight gradients are on the side stream (VGG-16 graph step 7.42 ->
-// 7.52 ms, tools/ab_vgg_c64.py); the side-stream-aware routing is on branch
-// work pending GPU validation
-static int g_wgrad_c64 = 0;
+// (conv_dma.h conv_wgrad_c64_kernel): 1 (default) on wherever the caller's
+// stream does not run beside the main stream (conv_wgrad allow_patch), 0
+// off, >= 2: forced with that many blocks per 64-channel k-slice (tests,
+// grid sweeps). VGG-16 (tools/ab_vgg_c64.py): eager gang path without the
+// weight-gradient side stream 7.71 -> 7.41 ms; hipGraph with the side stream
+// unchanged (the kernel's 120 KB of LDS per CU starves co-running kernels
+// there, so it is routed around: 7.42 -> 7.52 ms when it was not)
+static int g_wgrad_c64 = 1;
 void conv_wgrad_c64_policy(int p) { g_wgrad_c64 = p; }
 
 // dbias (optional, fp32 [K]): += the bias gradient sum_m dY[m][k], fused

@@ -348,7 +348,7 @@ def test_conv_wgrad_c64(gpu, cfg, mode):
             T().conv_wgrad(dy, x, dw, 1, 1, 1, mode, db)
             outs.append((dw - (0.25 if mode == 1 else 0.0), db - 0.5))
     finally:
-        T().conv_wgrad_c64_policy(0)
+        T().conv_wgrad_c64_policy(1)
     ref_b = dy.float().sum((0, 1, 2))
     for o, b in outs:
         assert rel_err(o, ref) < 1e-3

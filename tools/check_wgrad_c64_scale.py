@@ -32,7 +32,7 @@ for N, H, C, K in ((32, 224, 64, 64), (32, 112, 64, 128), (64, 56, 64, 64), (32,
         if e > 1e-3:
             d = (dw - ref).abs()
             row[("c64" if pol else "gather") + "_worst"] = [list(map(int, divmod(int(d.argmax()), 9 * C))), float(d.max())]
-    T.conv_wgrad_c64_policy(0)
+    T.conv_wgrad_c64_policy(1)
     print(json.dumps(row), flush=True)
     del x, dy, wf, gw, ref
     torch.cuda.empty_cache()
