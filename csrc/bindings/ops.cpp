@@ -12,6 +12,7 @@
 #include <mutex>
 #include <sstream>
 #include <tuple>
+#include <vector>
 
 #include "tam/kernels.h"
 #include "tam/launch.h"
@@ -452,6 +453,46 @@ void conv_dgrad_op(const Tensor& dy, const Tensor& w, const Tensor& wt, const Te
     ep.mask = bp(*mask); ep.ldm = g.C;
   }
   tam::conv_dgrad(bp(dy), bp(w), bp(wt), g, ep, cur_stream(dy));
+}
+
+// deferred weight gradients of many Linear layers in one grouped launch:
+// dw[i] (fp32 [M][N]) += dy[i]^T x[i] (dy [T][M], x [T][N] bf16), db[i] (fp32
+// [M], or an empty tensor for none) += colsum(dy[i])
+void gemm_wgrad_grouped_op(at::TensorList dy, at::TensorList x, at::TensorList dw, at::TensorList db) {
+  TORCH_CHECK(dy.size() == x.size() && dy.size() == dw.size() && dy.size() == db.size(),
+              "tam.gemm_wgrad_grouped: list sizes differ");
+  if (dy.empty()) return;
+  std::vector<tam::GGProblem> probs(dy.size());
+  for (size_t i = 0; i < dy.size(); ++i) {
+    const Tensor& a = dy[i];
+    const Tensor& b = x[i];
+    const Tensor& c = dw[i];
+    check_bf16(a, "dy"); check_bf16(b, "x"); check_f32(c, "dw");
+    check_contig(a, "dy"); check_contig(b, "x"); check_contig(c, "dw");
+    TORCH_CHECK(a.dim() == 2 && b.dim() == 2 && c.dim() == 2 && a.size(0) == b.size(0) &&
+                    c.size(0) == a.size(1) && c.size(1) == b.size(1),
+                "tam.gemm_wgrad_grouped: shapes dy [T,M], x [T,N], dw [M,N] expected");
+    TORCH_CHECK(a.device() == dy[0].device() && b.device() == a.device() && c.device() == a.device(),
+                "tam.gemm_wgrad_grouped: all operands on one device");
+    const int M = (int)a.size(1), N = (int)b.size(1), K = (int)a.size(0);
+    TORCH_CHECK(tam::gemm_wgrad_grouped_ok(M, N, K, M, N),
+                "tam.gemm_wgrad_grouped: problem ", i, " (", M, "x", N, "x", K,
+                ") not eligible (K % 64, M/N >= 128 and % 8)");
+    float* bias = nullptr;
+    if (db[i].defined() && db[i].numel() > 0) {
+      check_f32(db[i], "db");
+      TORCH_CHECK(db[i].numel() == M && db[i].is_contiguous(), "tam.gemm_wgrad_grouped: db must be [M]");
+      bias = db[i].data_ptr<float>();
+    }
+    probs[i] = tam::GGProblem{bp(a), bp(b), c.data_ptr<float>(), bias, M, N, K, M, N};
+  }
+  tam::gemm_wgrad_grouped(probs.data(), (int)probs.size(), cur_stream(dy[0]));
+}
+
+void gemm_grouped_tile_op(int64_t t) { tam::gemm_grouped_tile((int)t); }
+
+bool gemm_wgrad_grouped_ok_op(int64_t M, int64_t N, int64_t K) {
+  return tam::gemm_wgrad_grouped_ok((int)M, (int)N, (int)K, M, N);
 }
 
 // every conv weight of a model re-laid for dgrad in one launch
@@ -929,6 +970,9 @@ TORCH_LIBRARY(tam, m) {
   m.def("conv_fwd(Tensor x, Tensor w, Tensor(a!) y, int stride, int pad, int dil, Tensor? bias, bool relu, Tensor(b!)? stats=None) -> int", &conv_fwd_op);
   m.def("conv_dgrad(Tensor dy, Tensor w, Tensor(a!) wt, Tensor(b!) dx, int stride, int pad, int dil, Tensor? mask) -> ()", &conv_dgrad_op);
   m.def("conv_weight_t_batch(Tensor[] w, Tensor(a!)[] wt) -> ()", &conv_weight_t_batch_op);
+  m.def("gemm_wgrad_grouped(Tensor[] dy, Tensor[] x, Tensor(a!)[] dw, Tensor(b!)[] db) -> ()", &gemm_wgrad_grouped_op);
+  m.def("gemm_wgrad_grouped_ok(int M, int N, int K) -> bool", &gemm_wgrad_grouped_ok_op);
+  m.def("gemm_grouped_tile(int tile) -> ()", &gemm_grouped_tile_op);
   m.def("conv_dgrad_pre(Tensor dy, Tensor w, Tensor wt, Tensor(a!) dx, int stride, int pad, int dil, Tensor? mask, Tensor(b!)? stats=None, Tensor? bnx=None, Tensor? bnmean=None, Tensor? bnrstd=None) -> int", &conv_dgrad_pre_op);
   m.def("conv_wgrad(Tensor dy, Tensor x, Tensor(a!) dw, int stride, int pad, int dil, int mode, Tensor(b!)? dbias=None, bool patch=True) -> ()", &conv_wgrad_op);
   m.def("bn_forward(Tensor x, Tensor? res, Tensor(a!) y, Tensor gamma, Tensor beta, Tensor(b!)? run_mean, Tensor(c!)? run_var, Tensor(d!) save_mean, Tensor(e!) save_rstd, float eps, float momentum, bool relu, Tensor(f!)? sums=None, bool sums_ready=False, Tensor(g!)? ymask=None) -> ()", &bn_forward_op);

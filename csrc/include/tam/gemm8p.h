@@ -155,9 +155,11 @@ __device__ __forceinline__ void p8_mfma(f32x4_t (&acc)[TI][TJ], const s16x8_t (&
 // without the blanket lgkmcnt(0) in front of each MFMA cluster (per-fragment
 // waits); 5: as 4 with 2's two barriers + stagger. Measured in one process,
 // interleaved rounds (tools/ab_gemm8p_sched.py, profiles/r2/gemm8p_sched_ab.json)
+// The kernel body over one tile: bid = the (XCD-remapped) tile index within
+// the M x N tile grid, kz = the K-split slice. Shared by gemm8p_kernel and the
+// grouped launch (gemm8p_grouped_kernel: many independent problems, one grid).
 template <int BM, int BN, int WNW, bool AK, bool BK, int SCHED>
-__global__ void __launch_bounds__(128 * WNW, (BM == 256 ? 1 : 2))
-gemm8p_kernel(P8Args a, Epi ep) {
+__device__ __forceinline__ void gemm8p_body(const P8Args& a, const Epi& ep, const int bid, const int kz) {
   using G = P8Geo<BM, BN, WNW>;
   constexpr bool STAGGER = SCHED == 2 || SCHED == 5;
   constexpr bool TWO_BAR = SCHED == 1 || SCHED == 2 || SCHED == 5;
@@ -171,7 +173,6 @@ gemm8p_kernel(P8Args a, Epi ep) {
   const bool upper = __builtin_amdgcn_readfirstlane(tid) >= G::THREADS / 2;
 
   const int tiles_m = (a.M + BM - 1) / BM, tiles_n = (a.N + BN - 1) / BN;
-  const int bid = xcd_remap(blockIdx.x, gridDim.x);
   const int GROUP = a.group;
   const int per_group = GROUP * tiles_n;
   const int grp = bid / per_group;
@@ -182,7 +183,7 @@ gemm8p_kernel(P8Args a, Epi ep) {
   const int m0 = tm * BM, n0 = tn * BN;
 
   const int ktiles = a.K / P8_BK;
-  const int kt0 = blockIdx.z * a.kps;
+  const int kt0 = kz * a.kps;
   const int kt1 = min(ktiles, kt0 + a.kps);
   const int nk = kt1 - kt0;
 
@@ -270,7 +271,7 @@ gemm8p_kernel(P8Args a, Epi ep) {
   }
   __syncthreads();   // LDS reuse by the epilogue
 
-  const bool add_bias = ep.bias != nullptr && blockIdx.z == 0;
+  const bool add_bias = ep.bias != nullptr && kz == 0;
   const int rbase = m0 + wm * G::WTM, cbase = n0 + wn * G::WTN;
   constexpr int WTN = G::WTN;
   float bv[TJ];
@@ -349,7 +350,7 @@ gemm8p_kernel(P8Args a, Epi ep) {
       (ep.mode != 3 || (ep.zstride & 3) == 0)) {
     constexpr int LDF = WTN + 4, CPR = WTN / 4;
     float* slab = (float*)(smem + wid * (32 * LDF * 4));
-    float* cz = (float*)ep.c + (ep.mode == 3 ? blockIdx.z * ep.zstride : 0);
+    float* cz = (float*)ep.c + (ep.mode == 3 ? kz * ep.zstride : 0);
 #pragma unroll
     for (int h = 0; h < TI / 2; ++h) {
 #pragma unroll
@@ -403,7 +404,7 @@ gemm8p_kernel(P8Args a, Epi ep) {
         const long off = (long)row * ep.ldc + col;
         if (ep.c_f32) {
           float* c = (float*)ep.c;
-          if (ep.mode == 3) c[off + blockIdx.z * ep.zstride] = v;
+          if (ep.mode == 3) c[off + kz * ep.zstride] = v;
           else if (ep.mode == 2) atomicAdd(c + off, v);
           else if (ep.mode == 1) c[off] += v;
           else c[off] = v;
@@ -415,6 +416,12 @@ gemm8p_kernel(P8Args a, Epi ep) {
       }
     }
   }
+}
+
+template <int BM, int BN, int WNW, bool AK, bool BK, int SCHED>
+__global__ void __launch_bounds__(128 * WNW, (BM == 256 ? 1 : 2))
+gemm8p_kernel(P8Args a, Epi ep) {
+  gemm8p_body<BM, BN, WNW, AK, BK, SCHED>(a, ep, xcd_remap(blockIdx.x, gridDim.x), blockIdx.z);
 }
 
 // One launcher per kernel variant. Each production variant (SCHED 4) is

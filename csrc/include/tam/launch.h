@@ -24,6 +24,21 @@ void gemm8p_policy(int mode, int sched);
 void gemm8p_group(int g);   // M-tiles per tile-order group of gemm8p (default 4)
 int gemm8p_policy_mode();
 
+// Grouped weight-gradient GEMM (gemm_grouped.hip): for every problem p,
+//   C_p[M][N] += A_p^T B_p  (A_p [K][lda] M-major, B_p [K][ldb] N-major, fp32 C row stride N)
+//   bias_p[M] += column sums of A_p (when bias_p != null)
+// in ONE launch per P8G_MAX problems (gemm8p 128^2 tiles + column-sum blocks).
+struct GGProblem {
+  const bf16_t* A;
+  const bf16_t* B;
+  float* C;
+  float* bias;
+  int M, N, K, lda, ldb;
+};
+void gemm_wgrad_grouped(const GGProblem* probs, int n, hipStream_t s);
+bool gemm_wgrad_grouped_ok(int M, int N, int K, long lda, long ldb);
+void gemm_grouped_tile(int t);   // 128 (default) or 256
+
 // NHWC convolutions, weights [K][R][S][C] (C, K multiples of 8)
 int conv_fwd(const bf16_t* x, const bf16_t* w, const ConvGeom& g, Epi ep, hipStream_t s);
 // dx[N*H*W][C]; wt = conv_weight_t(w) laid out [C][R][S][K] (ignored for 1x1/s1)

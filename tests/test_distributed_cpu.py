@@ -422,3 +422,69 @@ def test_rank_loss_restarts_from_snapshot(tmp_path):
     rows = {r["job_id"]: r for r in csv.DictReader(open(tmp_path / "job.csv"))}
     for d in rs:
         assert int(rows[d["job"]]["lost_iters"]) == d["lost_iters"]
+
+
+@pytest.mark.slow
+def test_unreadable_snapshot_restarts_from_scratch(tmp_path):
+    """Rank 3 crashes AND tears the shared snapshot store (every snapshot
+    file truncated): the ranks that restart a job from its snapshot fail to
+    read it, agree on that verdict (nobody runs it on garbage state), and the
+    controller restarts the job from scratch, charging every iteration the
+    snapshot held (lost_iters) -- the replay still finishes every job."""
+    import csv
+    import json
+
+    ps, s = _run_recover(tmp_path, {"rank": 3, "round": 14, "kind": "crash", "corrupt_snapshots": True},
+                         snapshot_s=0.02)
+    errs = {f.name: f.read_text()[-1500:] for f in tmp_path.glob("err*.txt")}
+    assert ps[3].exitcode == 17 and all(p.exitcode == 0 for p in ps[:3]), ([p.exitcode for p in ps], errs)
+    assert s["lost_ranks"] == [3] and s["finished"] + s["failed"] == s["jobs"]
+    dec = [json.loads(x) for x in open(tmp_path / "decisions.jsonl")]
+    bad = [d for d in dec if d["ev"] == "restart" and d.get("reason") == "snapshot unreadable"]
+    tried = [d for d in dec if d["ev"] == "restart" and d["source"] == "snapshot"]
+    assert tried, "no job needed its snapshot"
+    assert {d["job"] for d in bad} == {d["job"] for d in tried}
+    rows = {r["job_id"]: r for r in csv.DictReader(open(tmp_path / "job.csv"))}
+    for d in tried:
+        # the iterations redone before the crash and the ones the snapshot held
+        assert int(rows[d["job"]]["lost_iters"]) == d["lost_iters"] + d["from_step"]
+
+
+def test_snapshot_needs_shared_dir():
+    from tiresias_amd.executor.cluster_runtime import Worker
+
+    with pytest.raises(ValueError, match="snapshot_dir"):
+        Worker(0, 1, torch.device("cpu"), snapshot_s=1.0)
+
+
+def test_heartbeat_liveness_ignores_wall_clock(monkeypatch):
+    """Liveness is a heartbeat COUNTER timed on rank 0's monotonic clock
+    (executor/control.py): with the wall clock unusable (skewed hosts; here
+    time.time raises) a beating rank stays alive, and a rank whose counter
+    stops is declared lost within about hb_timeout."""
+    from tiresias_amd.executor import control
+
+    port = _free_port()
+    master = dist.TCPStore("127.0.0.1", port, is_master=True, wait_for_workers=False)
+    monkeypatch.setenv("MASTER_ADDR", "127.0.0.1")
+    monkeypatch.setenv("MASTER_PORT", str(port))
+
+    def _no_wall_clock():
+        raise AssertionError("liveness must not read the wall clock")
+
+    monkeypatch.setattr(control.time, "time", _no_wall_clock)
+    dead = []
+    p1 = control.StorePlane(1, 2, hb_period=0.1, hb_timeout=0.8, store=master)
+    p0 = control.StorePlane(0, 2, hb_period=0.1, hb_timeout=0.8, store=master, on_dead=dead.append)
+    try:
+        time.sleep(2.5)
+        assert dead == [] and p0.heartbeat_age(1) < 0.5
+        p1.close()                                    # the rank stops beating
+        t0 = time.monotonic()
+        while not dead and time.monotonic() - t0 < 5.0:
+            time.sleep(0.05)
+        assert dead == [1]
+        assert time.monotonic() - t0 < 0.8 + 1.0
+    finally:
+        p0.close()
+        p1.close()

@@ -72,6 +72,45 @@ def test_gemm_colsum_fused(gpu, M, N, K):
         assert rel_err(db, ref_b + 0.5) < 1e-4, call
 
 
+@pytest.mark.parametrize("tile", [256, 128])
+def test_gemm_wgrad_grouped(gpu, tile):
+    """Grouped weight-gradient launch over a RAGGED group (different M, N, K
+    per problem, some with a bias gradient, some without) vs fp32 torch,
+    under both tile variants, and more problems than one launch holds."""
+    torch.manual_seed(31)
+    shapes = [(512, 512, 4096, True), (1536, 512, 4096, True), (2048, 512, 4096, False),
+              (512, 2048, 4096, True), (128, 136, 64, True), (6144, 512, 1024, False),
+              (264, 384, 192, True)]
+    dys, xs, dws, dbs, refs = [], [], [], [], []
+    for M, N, K, bias in shapes:
+        dy = torch.randn(K, M, device=gpu).to(BF)
+        x = torch.randn(K, N, device=gpu).to(BF)
+        dys.append(dy)
+        xs.append(x)
+        dws.append(torch.full((M, N), 0.25, device=gpu))
+        dbs.append(torch.full((M,), -1.0, device=gpu) if bias else torch.empty(0, device=gpu))
+        refs.append((dy.float().t() @ x.float() + 0.25, dy.float().sum(0) - 1.0 if bias else None))
+    assert all(T().gemm_wgrad_grouped_ok(M, N, K) for M, N, K, _ in shapes)
+    T().gemm_grouped_tile(tile)
+    assert not T().gemm_wgrad_grouped_ok(512, 512, 100)
+    T().gemm_wgrad_grouped(dys, xs, dws, dbs)
+    torch.cuda.synchronize()
+    for i, (rw, rb) in enumerate(refs):
+        assert rel_err(dws[i], rw) < 1e-4, i
+        if rb is not None:
+            assert rel_err(dbs[i], rb) < 1e-5, i
+    # 70 problems -> two launches (64 + 6); every result accumulated once
+    many = [(dys[i % 2], xs[i % 2]) for i in range(70)]
+    outs = [torch.zeros(shapes[i % 2][0], shapes[i % 2][1], device=gpu) for i in range(70)]
+    bs = [torch.zeros(shapes[i % 2][0], device=gpu) for i in range(70)]
+    T().gemm_wgrad_grouped([m[0] for m in many], [m[1] for m in many], outs, bs)
+    torch.cuda.synchronize()
+    T().gemm_grouped_tile(256)
+    for i in range(70):
+        assert rel_err(outs[i], refs[i % 2][0] - 0.25) < 1e-4, i
+        assert rel_err(bs[i], refs[i % 2][1] + 1.0) < 1e-5, i
+
+
 # ------------------------------------------------------------------ GEMM
 @pytest.mark.parametrize("M,N,K", [(256, 256, 256), (200, 136, 72), (1000, 64, 520), (64, 1000, 64),
                                    (4096, 1024, 512), (33, 40, 8)])

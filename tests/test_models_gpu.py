@@ -100,6 +100,46 @@ def test_wgrad_stream_overlap_matches(gpu, model):
     assert abs(lg - le) < 2e-2 * max(1.0, abs(le))
 
 
+@pytest.mark.parametrize("overlap", [True, False])
+def test_grouped_wgrad_matches(gpu, overlap, monkeypatch):
+    """Transformer (full width, 2+2 layers) with every Linear weight gradient
+    deferred into the grouped launch gives the gradients of the per-layer
+    path, eager and under hipGraph capture, with and without the weight-
+    gradient stream, and with a mid-backward chunked flush."""
+    from tiresias_amd.ops import functional as Fx
+
+    kw = dict(enc_layers=2, dec_layers=2)
+    a = Trainer("transformer", gpu, seed=4, batch=4, model_kwargs=kw, overlap_wgrad=overlap)
+    b = Trainer("transformer", gpu, seed=4, batch=4, model_kwargs=kw, overlap_wgrad=overlap)
+    assert a.group_wgrad
+    b.group_wgrad = False
+    b.arena.master.copy_(a.arena.master)
+    b.arena.shadow.copy_(a.arena.shadow)
+    calls = []
+    real = Fx.flush_wgrad
+    monkeypatch.setattr(Fx, "flush_wgrad", lambda: calls.append(real()) or calls[-1])
+    la, lb = a._fwd_bwd(), b._fwd_bwd()
+    torch.cuda.synchronize()
+    assert calls and calls[0] >= 20, calls         # the Linear layers went through the group
+    assert abs(float(la) - float(lb)) < 1e-3 * max(1.0, abs(float(lb)))
+    assert rel(a.arena.grad, b.arena.grad) < 2e-3
+    monkeypatch.setattr(Fx, "_DEFER_CHUNK", 5)     # flushes every 5 deferred layers
+    a.arena.grad.zero_()
+    a._fwd_bwd()
+    torch.cuda.synchronize()
+    assert rel(a.arena.grad, b.arena.grad) < 2e-3
+    monkeypatch.setattr(Fx, "_DEFER_CHUNK", 0)
+    g = Trainer("transformer", gpu, seed=4, batch=4, model_kwargs=kw, overlap_wgrad=overlap, use_graph=True)
+    e = Trainer("transformer", gpu, seed=4, batch=4, model_kwargs=kw, overlap_wgrad=overlap)
+    e.group_wgrad = False
+    e.arena.master.copy_(g.arena.master)
+    e.arena.shadow.copy_(g.arena.shadow)
+    for _ in range(4):
+        lg, le = float(g.step()), float(e.step())
+    assert abs(lg - le) < 2e-2 * max(1.0, abs(le))
+    assert rel(g.arena.master, e.arena.master) < 1e-3
+
+
 @pytest.mark.parametrize("overlap", [False, True])
 def test_gnmt_branch_streams_match(gpu, overlap):
     """GNMT's independent recurrences on branch streams (bidirectional

@@ -49,6 +49,7 @@ class SnapshotWriter:
         self._lock = threading.Lock()
         self._done: List[Tuple[str, int, str]] = []
         self._dropped: set = set()
+        self._jobs: set = set()                 # every job this writer snapshotted
         self.written = 0
         self.bytes = 0
         self._th = threading.Thread(target=self._loop, name="snapshot-writer", daemon=True)
@@ -62,6 +63,7 @@ class SnapshotWriter:
         step = int(trainer.step_count)
         with self._lock:
             self._dropped.discard(jid)
+            self._jobs.add(jid)
         if self._cuda:
             cur = torch.cuda.current_stream(self.device)
             clones = {k: v.clone() for k, v in state.items()}           # D2D, compute stream
@@ -116,10 +118,17 @@ class SnapshotWriter:
             out, self._done = self._done, []
         return out
 
+    def wrote(self, jid: str) -> bool:
+        """This writer snapshotted the job at some point (it must also drop it)."""
+        with self._lock:
+            return jid in self._jobs
+
     def drop(self, jid: str) -> None:
-        """The job finished: its snapshot is no longer needed."""
+        """The job finished: its snapshot is no longer needed (any queued
+        write of it is discarded)."""
         with self._lock:
             self._dropped.add(jid)
+            self._jobs.discard(jid)
         _unlink(self.path_of(jid))
 
     def flush(self, timeout: float = 60.0) -> None:

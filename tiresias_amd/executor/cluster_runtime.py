@@ -31,6 +31,7 @@ from __future__ import annotations
 
 import math
 import os
+import sys
 import time
 import zlib
 from dataclasses import dataclass, field
@@ -223,11 +224,15 @@ class Controller:
                     agg["run_s"] = max(agg["run_s"], jr["run_s"])
                     agg["error"] = agg.get("error") or jr.get("error")
                     agg["move_failed"] = agg.get("move_failed") or jr.get("move_failed")
+                    agg["snap_failed"] = agg.get("snap_failed") or jr.get("snap_failed")
         for jid, jr in per_job.items():
             if jid not in self.rjobs:
                 continue
             self.done_iters[jid] += jr["iters"]
             rj = self.rjobs[jid]
+            if jr.get("snap_failed"):
+                self.snapshot_failed(jid)
+                continue
             if jr.get("move_failed"):
                 self.move_failed(jid)
                 continue
@@ -348,6 +353,32 @@ class Controller:
             self.resync.add(jid)
         if self.log is not None:
             self.log.decision(self.now(), "gang-error", jid, ranks=list(hold or ()))
+
+    def snapshot_failed(self, jid: str) -> None:
+        """A restart from the job's durable snapshot failed on some member (the
+        file is missing, truncated or unreadable there; the members agreed
+        and none ran it): restart the job from scratch instead, charging the
+        iterations the snapshot held (job.csv lost_iters)."""
+        s = self.sched
+        j = s.jobs.get(jid)
+        if j is None:
+            return
+        if j.is_running:
+            s._preempt(j, reason="snapshot-failed")
+        self.snapshots.pop(jid, None)
+        self.from_snap.pop(jid, None)
+        self.snap_restored.discard(jid)
+        self.holders.pop(jid, None)
+        self.last_old.pop(jid, None)
+        lost = self.done_iters.get(jid, 0)
+        j.extra["lost_iters"] = j.extra.get("lost_iters", 0) + lost
+        j.extra["snapshot_failures"] = j.extra.get("snapshot_failures", 0) + 1
+        self.done_iters[jid] = 0
+        j.progress = 0.0
+        self.restarted.add(jid)
+        if self.log is not None:
+            self.log.decision(self.now(), "restart", jid, from_step=0, lost_iters=lost,
+                              source="scratch", reason="snapshot unreadable")
 
     def move_failed(self, jid: str) -> None:
         """A state move did not complete on every participant (a peer died
@@ -622,7 +653,13 @@ class Worker:
         if snapshot_s > 0:
             from ..ckpt.snapshot import SnapshotWriter
 
-            self.snap = SnapshotWriter(snapshot_dir or os.path.join("/tmp", f"tam_snap_{os.getpid()}"), device)
+            # a snapshot must outlive its writer AND be readable by whichever
+            # ranks restart the job: only a directory shared by every rank
+            # (never a per-process /tmp default) serves both
+            if not snapshot_dir:
+                raise ValueError("snapshot_s > 0 needs a snapshot_dir shared by every rank")
+            self.snap = SnapshotWriter(snapshot_dir, device)
+        self._snap_failed: set = set()          # jobs whose snapshot load failed (this round)
         self._job_ranks: Dict[str, Tuple[int, ...]] = {}
         self._snap_acc: Dict[str, float] = {}
         self.use_graph = use_graph
@@ -875,6 +912,7 @@ class Worker:
                 elif getattr(t, "_spilled", None):
                     self._make_room(t.hbm_bytes(), protect, ro)
         moves: Dict[str, tuple] = {}          # job -> ([(send|recv, buffer, peer)], action), plan order
+        snap_loads: Dict[str, tuple] = {}     # job -> (local load ok, action): restarts from snapshots
         for a in plan["actions"]:
             op = a["op"]
             if op == "group":
@@ -898,7 +936,10 @@ class Worker:
                 self._retire(self.trainers.pop(a["job"], None))
                 self._job_ranks.pop(a["job"], None)
                 self._snap_acc.pop(a["job"], None)
-                if self.snap is not None and self.rank == min(a["ranks"]):
+                # the holder's lowest rank deletes the (shared) file, and so
+                # does every rank whose writer ever snapshotted the job -- an
+                # earlier holder's queued write must not re-create it later
+                if self.snap is not None and (self.rank == min(a["ranks"]) or self.snap.wrote(a["job"])):
                     self.snap.drop(a["job"])
             elif op == "spill":
                 if self.trainers.get(a["job"]) is not None:
@@ -909,7 +950,9 @@ class Worker:
                 self._job_ranks[a["job"]] = ranks
                 if src == "snapshot":
                     # the job's only replica died: rebuild from its last
-                    # durable snapshot (every gang member reads the file)
+                    # durable snapshot (every gang member reads the file); a
+                    # missing / truncated / unreadable file fails the load on
+                    # that member, and the members agree on the verdict below
                     if self.rank in ranks:
                         from ..ckpt.snapshot import load_snapshot
 
@@ -917,9 +960,17 @@ class Worker:
                         if old_t is not None:
                             old_t.release()
                         t = self._make_trainer(a, init=False)
-                        load_snapshot(a["path"], t)
+                        ok = True
+                        try:
+                            load_snapshot(a["path"], t)
+                        except Exception as e:
+                            ok = False
+                            print(f"[worker {self.rank}] job {a['job']}: snapshot {a['path']} unreadable "
+                                  f"({type(e).__name__}: {e}); restarting it from scratch",
+                                  file=sys.stderr, flush=True)
                         self.trainers[a["job"]] = t
                         self._snap_acc[a["job"]] = 0.0
+                        snap_loads[a["job"]] = (ok, {**a, "old": []})
                 elif src == "fresh":
                     if self.rank in ranks:
                         before = torch.cuda.memory_allocated(self.device) if self.device.type == "cuda" else 0
@@ -974,8 +1025,22 @@ class Worker:
                         self.trainers[a["job"]].step_count = int(a["step"])
         if any(a["op"] == "drop" for a in plan["actions"]):
             self.reclaim(64.0)
-        failed = self._agree_moves(plan.get("round"), self._do_moves(moves),
-                                   {jid: a for jid, (_, a) in moves.items()}) if moves else set()
+        failed = set()
+        if moves or snap_loads:
+            ok = self._do_moves(moves) if moves else {}
+            ok.update({jid: v for jid, (v, _) in snap_loads.items()})
+            acts = {jid: a for jid, (_, a) in moves.items()}
+            acts.update({jid: a for jid, (_, a) in snap_loads.items()})
+            failed = self._agree_moves(plan.get("round"), ok, acts)
+        for jid in [j for j in failed if j in snap_loads]:
+            # some member could not read the snapshot: no member runs the job
+            # on it (replicas would disagree); the controller restarts it
+            # from scratch and charges the iterations the snapshot held
+            failed.discard(jid)
+            self._snap_failed.add(jid)
+            t = self.trainers.pop(jid, None)
+            if t is not None:
+                t.release()
         for jid in failed:
             # every participant drops the pair communicators this move used
             # (same verdict everywhere -> same re-creation generation)
@@ -1168,7 +1233,10 @@ class Worker:
         jobs = plan["assign"].get(self.rank) or []
         skipped = [{"job": jid, "iters": 0, "run_s": 0.0, "shared": False, "loss": None, "move_failed": True}
                    for jid in sorted(self._move_failed)]
+        skipped += [{"job": jid, "iters": 0, "run_s": 0.0, "shared": False, "loss": None, "snap_failed": True}
+                    for jid in sorted(self._snap_failed)]
         self._move_failed = set()
+        self._snap_failed = set()
         jobs = [(jid, n) for jid, n in jobs if jid not in {r["job"] for r in skipped}]
         if not jobs:
             return {"rank": self.rank, "job": None, "jobs": skipped, "dev": self._dev_sample(),
@@ -1468,6 +1536,14 @@ def run_replay(cfg: SimConfig, jobs: List[ReplayJob], rank: int, world: int, dev
                 break
             if fault and fault.get("rank") == rank and rounds >= fault.get("round", 0):
                 if fault.get("kind", "crash") == "crash":
+                    if fault.get("corrupt_snapshots") and worker.snap is not None:
+                        # the crash also tears the shared snapshot store:
+                        # every snapshot file is truncated
+                        worker.snap.flush(10.0)
+                        for f in os.listdir(worker.snap.dir):
+                            if f.endswith(".pt"):
+                                with open(os.path.join(worker.snap.dir, f), "r+b") as fh:
+                                    fh.truncate(16)
                     os._exit(17)                     # simulated node/rank crash
                 if fault.get("kind") == "hang":
                     if plane is not None:

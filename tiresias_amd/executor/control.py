@@ -8,12 +8,15 @@ so a lost rank cannot wedge the surviving ones:
 * rank 0 publishes ``plan/<epoch>/<round>``; workers block on it
   (``store.wait``), run, and publish ``rep/<epoch>/<round>/<rank>``;
 * every worker also runs a HEARTBEAT thread on its own store connection,
-  stamping ``hb/<rank>`` every ``hb_period`` seconds — independent of the
-  training thread, so a rank busy in a long step, or stuck in a collective
-  with a dead peer, still reads as alive;
-* rank 0 runs a MONITOR thread that checks every heartbeat each period: a
-  rank whose heartbeat is older than ``hb_timeout`` (5-10 s; never the
-  collective timeout) is declared LOST, published under ``<epoch>/dead``,
+  bumping an increasing COUNTER under ``hb/<rank>`` every ``hb_period``
+  seconds — independent of the training thread, so a rank busy in a long
+  step, or stuck in a collective with a dead peer, still reads as alive;
+* rank 0 runs a MONITOR thread that reads every counter each period and
+  times, on its OWN monotonic clock, how long each one has gone without
+  changing (no wall-clock timestamps cross hosts, so clock skew between
+  hosts cannot make a healthy rank look dead): a rank whose counter is
+  stale for ``hb_timeout`` (5-10 s; never the collective timeout) is
+  declared LOST, published under ``<epoch>/dead``,
   and ``on_dead(r)`` runs at once -- on a separate thread, because rank 0's
   training thread may itself be stuck in a collective with the dead rank;
 * every other rank's heartbeat thread also WATCHES ``<epoch>/dead`` and
@@ -90,8 +93,9 @@ class StorePlane:
         self._lock = threading.Lock()
         self.dead: set = set()
         self._reported: set = set()              # dead ranks already returned by gather
-        self.last_seen: Dict[int, float] = {}
-        self.t_start = time.time()
+        # rank -> (last heartbeat counter seen, monotonic time it changed)
+        self._hb_seen: Dict[int, Tuple[Optional[bytes], float]] = {}
+        self.t_start = time.monotonic()
         if rank != 0:
             self._hb = threading.Thread(target=self._beat, name=f"hb-{rank}", daemon=True)
         else:
@@ -118,9 +122,11 @@ class StorePlane:
         st = _store_client(30.0)
         dkey = f"{self.prefix}/dead"
         seen = b""
+        beat = 0
         while not self._stop.is_set():
             try:
-                st.set(f"tam/hb/{self.rank}", repr(time.time()))
+                beat += 1
+                st.set(f"tam/hb/{self.rank}", str(beat))
                 if st.check([dkey]):
                     raw = st.get(dkey)
                     if raw != seen:
@@ -136,7 +142,7 @@ class StorePlane:
         st = _store_client(30.0)
         dkey = f"{self.prefix}/dead"
         while not self._stop.wait(self.hb_period):
-            if time.time() - self.t_start < self.hb_timeout:
+            if time.monotonic() - self.t_start < self.hb_timeout:
                 continue                         # grace: every heartbeat thread has started
             try:
                 gone = [r for r in range(1, self.world)
@@ -148,18 +154,21 @@ class StorePlane:
             except Exception:
                 return
 
-    @staticmethod
-    def _age(st, r: int) -> float:
+    def _age(self, st, r: int) -> float:
+        """Seconds (rank 0's monotonic clock) since rank r's heartbeat counter
+        last changed; a rank that never beat counts from this plane's start."""
         k = f"tam/hb/{r}"
-        if not st.check([k]):
-            return float("inf")
-        return time.time() - float(st.get(k).decode())
+        val = st.get(k) if st.check([k]) else None
+        now = time.monotonic()
+        with self._lock:
+            last = self._hb_seen.get(r)
+            if last is None or (val is not None and val != last[0]):
+                last = (val, now if (last is not None or val is not None) else self.t_start)
+                self._hb_seen[r] = last
+            return now - last[1]
 
     def heartbeat_age(self, r: int) -> float:
-        k = f"tam/hb/{r}"
-        if not self.store.check([k]):
-            return float("inf")
-        return time.time() - float(self.store.get(k).decode())
+        return self._age(self.store, r)
 
     # ----------------------------------------------------------- plan / reports
     def _retry(self, fn, what: str, attempts: int = 3):
@@ -198,7 +207,7 @@ class StorePlane:
         reps: List = [None] * self.world
         reps[0] = rep
         pending = [r for r in alive if r != 0]
-        t0 = time.time()
+        t0 = time.monotonic()
         t_warn = t0
         sleep = 0.0002
         while pending:
@@ -215,7 +224,7 @@ class StorePlane:
             pending = left
             if not pending:
                 break
-            now = time.time()
+            now = time.monotonic()
             if now - t0 > self.hb_timeout:
                 # the monitor thread normally declares first; this covers a
                 # monitor that is itself starved
@@ -256,12 +265,12 @@ class StorePlane:
             except Exception:
                 pass
             return
-        t0 = time.time()
+        t0 = time.monotonic()
         for r in alive:
             if r == 0:
                 continue
             k = f"{self.prefix}/done/{r}"
-            while time.time() - t0 < bound_s and r not in self.dead:
+            while time.monotonic() - t0 < bound_s and r not in self.dead:
                 if self.store.check([k]):
                     break
                 time.sleep(0.002)

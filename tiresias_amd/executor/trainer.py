@@ -8,6 +8,7 @@ four flat buffers a preemption checkpoints, ``release()`` frees HBM.
 """
 from __future__ import annotations
 
+import os
 import time
 from typing import Dict, List, Optional
 
@@ -62,6 +63,8 @@ class Trainer:
         self._side = None
         self._ws = None                 # weight-gradient stream (1-GPU jobs)
         self.overlap_wgrad = self.spec.overlap_wgrad if overlap_wgrad is None else overlap_wgrad
+        # grouped weight gradients (TAM_GROUP_WGRAD=0 turns them off for A/B runs)
+        self.group_wgrad = self.spec.group_wgrad and os.environ.get("TAM_GROUP_WGRAD", "1") != "0"
         # model-declared branch streams (see _fwd_bwd); None = the model's default
         self.branches = getattr(self.model, "branch_default", False) if branches is None else branches
         self._bs: List = []
@@ -93,6 +96,9 @@ class Trainer:
             if len(self._bs) < nb:
                 self._bs = [torch.cuda.Stream(self.device) for _ in range(nb)]
             Fx.set_branch_streams(self._bs)
+        group = (self.device.type == "cuda" and self.ddp is None and self.group_wgrad)
+        if group:
+            Fx.defer_wgrad(True)
         try:
             if self.spec.kind == "image":
                 logits = self.model.forward(d["x"])
@@ -103,7 +109,11 @@ class Trainer:
             loss, dlog = Fx.softmax_xent(logits, labels, smoothing=self.spec.smoothing,
                                          ignore_index=-100, normalizer=rows)
             logits.backward(dlog)
+            if group:
+                Fx.flush_wgrad()
         finally:
+            if group:
+                Fx.defer_wgrad(False, discard=True)
             Fx.set_wgrad_stream(None)
             Fx.set_branch_streams(None)
         if ws is not None:

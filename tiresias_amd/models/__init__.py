@@ -37,6 +37,9 @@ class ModelSpec:
     # +3 %, Transformer +2 %, GNMT +20 %: big wgrad GEMMs starve the
     # latency-bound recurrence / small-GEMM chains of CUs)
     overlap_wgrad: bool = False
+    # Linear weight gradients deferred and issued as ONE grouped launch per
+    # backward (ops/functional.py defer_wgrad; 1-GPU jobs)
+    group_wgrad: bool = False
 
 
 MODELS: Dict[str, ModelSpec] = {
@@ -46,7 +49,7 @@ MODELS: Dict[str, ModelSpec] = {
     # hipGraph steps): Transformer 7.28 -> 7.14 ms on; ResNet-50 10.65 -> 11.01
     # and GNMT 10.87 -> 11.93 (the persistent recurrence loses its CUs) off
     "transformer": ModelSpec(TransformerBase, "seq2seq", 32, "adam", 5e-4, 0.0, seq=128,
-                             smoothing=0.1, overlap_wgrad=True),
+                             smoothing=0.1, overlap_wgrad=True, group_wgrad=True),
     "gnmt": ModelSpec(GNMT, "seq2seq", 64, "adam", 1e-3, 0.0, seq=50),
     # tiny variants (CPU tests / gloo rehearsals / smoke)
     "resnet_tiny": ModelSpec(ResNet50, "image", 4, "sgd", 0.1, 1e-4,

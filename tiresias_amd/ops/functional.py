@@ -18,6 +18,7 @@ reference of the same math (CPU test-suite, gloo rehearsals, numerics refs).
 from __future__ import annotations
 
 import math
+import os
 from typing import List, Optional, Tuple
 
 import torch
@@ -79,6 +80,59 @@ class _OnWgrad:
         if self.ctx is not None:
             self.ctx.__exit__(*exc)
         return False
+
+
+# ============================================================ grouped weight gradients
+# A trainer may DEFER every eligible Linear weight gradient of a backward pass
+# (dW = dY^T X, db = colsum(dY)) and issue them together as ONE grouped
+# launch (csrc/kernels/gemm_grouped.hip): the per-layer dW GEMMs of
+# Transformer-base (512..2048 x 512 x 4096) each underfill the 256 CUs, while
+# the ~60 of a step fill it as one grid. dY / X stay alive until the flush
+# (a few MB each). ``TAM_WGRAD_GROUP_CHUNK`` = n > 0 flushes every n deferred
+# layers instead of once at the end (A/B of overlap vs. fill).
+_DEFER_WGRAD: Optional[list] = None
+_DEFER_CHUNK = int(os.environ.get("TAM_WGRAD_GROUP_CHUNK", "0") or 0)
+_GROUP_OK: dict = {}
+
+
+def defer_wgrad(on: bool, discard: bool = False) -> None:
+    """Start (True) or stop (False) deferring Linear weight gradients; stopping
+    with problems still pending is a programming error (flush first) unless
+    ``discard`` (an aborted step)."""
+    global _DEFER_WGRAD
+    if not on and _DEFER_WGRAD and not discard:
+        raise RuntimeError("defer_wgrad(False) with unflushed weight gradients")
+    _DEFER_WGRAD = [] if on else None
+
+
+def _group_ok(M: int, N: int, K: int) -> bool:
+    key = (M, N, K)
+    ok = _GROUP_OK.get(key)
+    if ok is None:
+        ok = bool(_T().gemm_wgrad_grouped_ok(M, N, K))
+        _GROUP_OK[key] = ok
+    return ok
+
+
+def flush_wgrad() -> int:
+    """Issue every deferred weight gradient as one grouped launch (on the
+    weight-gradient stream when one is installed), then signal grad_ready.
+    Returns the number of problems flushed."""
+    pend = _DEFER_WGRAD
+    if not pend:
+        return 0
+    items = list(pend)
+    pend.clear()
+    dys = [it[0] for it in items]
+    with _OnWgrad(*dys, *[it[1] for it in items]):
+        empty = torch.empty(0, dtype=torch.float32, device=dys[0].device)
+        _T().gemm_wgrad_grouped(dys, [it[1] for it in items], [it[2].grad for it in items],
+                                [it[3].grad if it[3] is not None else empty for it in items])
+    for _, _, w, b in items:
+        w.grad_ready()
+        if b is not None:
+            b.grad_ready()
+    return len(items)
 
 
 # ============================================================ branch streams
@@ -170,12 +224,18 @@ class _Linear(Function):
             else:
                 dy = (dy.float() * (y.float() > 0)).to(BF16)
         dx = None
+        deferred = False
         if dy.is_cuda:
-            with _OnWgrad(dy, x):
-                # the bias gradient colsum(dy) rides on the weight-gradient
-                # GEMM's own A loads (fused on the igemm route, else a pass)
-                _T().gemm(dy, False, x, False, w.grad, 1, None, False, None, 1.0, True,
-                          b.grad if b is not None else None)
+            if (_DEFER_WGRAD is not None and x.dim() == 2 and w.grad.is_contiguous()
+                    and _group_ok(w.shape[0], w.shape[1], x.shape[0])):
+                _DEFER_WGRAD.append((dy, x, w, b))      # issued by flush_wgrad
+                deferred = True
+            else:
+                with _OnWgrad(dy, x):
+                    # the bias gradient colsum(dy) rides on the weight-gradient
+                    # GEMM's own A loads (fused on the igemm route, else a pass)
+                    _T().gemm(dy, False, x, False, w.grad, 1, None, False, None, 1.0, True,
+                              b.grad if b is not None else None)
         if ctx.needs_input_grad[0]:
             if dy.is_cuda:
                 dx = torch.empty_like(x)
@@ -189,9 +249,13 @@ class _Linear(Function):
             w.grad += _cpu_gemm_f32(dy.t(), x)
             if b is not None:
                 b.grad += dy.float().sum(0)
-        w.grad_ready()
-        if b is not None:
-            b.grad_ready()
+        if deferred:
+            if _DEFER_CHUNK and len(_DEFER_WGRAD) >= _DEFER_CHUNK:
+                flush_wgrad()
+        else:
+            w.grad_ready()
+            if b is not None:
+                b.grad_ready()
         return dx, None, None, None, None, None, None
 
 
