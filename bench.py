@@ -46,6 +46,7 @@ T_PROC0 = time.perf_counter()
 
 import argparse  # noqa: E402
 import datetime  # noqa: E402
+import gc  # noqa: E402
 import json  # noqa: E402
 import math  # noqa: E402
 import os  # noqa: E402
@@ -246,6 +247,8 @@ def main():
     ap.add_argument("--no-nopool-replay", action="store_true",
                     help="skip the extra untimed replay without the warm pool (cold-build JCT)")
     ap.add_argument("--out", default=None, help="directory for job.csv / summary.json of the last step")
+    ap.add_argument("--preflight-s", type=float, default=120.0,
+                    help="N > 1: bound of the communicator pre-flight (world + every canonical gang)")
     a = ap.parse_args()
     pol, plc, ck, bpol, bplc, qlim, share = SCENARIOS[a.scenario]
     share = share or a.share
@@ -316,10 +319,11 @@ def main():
     # 0.49 -> 0.37, N=8 0.48 -> 0.32; N=1 unchanged)
     qlim_n = [x * n for x in qlim] if a.scale_limits else list(qlim)
 
-    def make(policy, scheme):
+    def make(policy, scheme, limits=None):
         # the Gittins quantum scales with the job sizes (a quantum below the
         # smallest prior job gives every new job index 0: no preemption)
-        c = make_cfg(policy, scheme, n, a.seed, a.ckpt, qlim_n, share, virtual_nodes=vn,
+        c = make_cfg(policy, scheme, n, a.seed, a.ckpt, qlim_n if limits is None else limits, share,
+                     virtual_nodes=vn,
                      skew_profile=a.skew_profile,
                      gittins_delta=0.05 * (SEQ_SCALE if a.scenario == "seq" else 1))
         c.nic_gbps = a.nic_gbps
@@ -345,6 +349,18 @@ def main():
         worker.precreate_pairs()      # state-move communicators (one per rank pair)
         dist.barrier(group=ctrl_pg)
         comm_setup_s = time.perf_counter() - tc
+        # pre-flight: known values all-reduced on the world communicator and
+        # every canonical gang, checked exactly; any failure (wrong sum,
+        # creation error, a member that never joins) stops EVERY rank with
+        # the rank sets named, before anything is timed
+        from tiresias_amd.parallel.gang import preflight
+
+        errs = preflight(worker.groups, rank, device, world_pg, ctrl_pg, timeout_s=a.preflight_s)
+        if errs:
+            if rank == 0:
+                for e in errs:
+                    print(f"[bench] PREFLIGHT FAILED: {e}", file=sys.stderr, flush=True)
+            os._exit(3)
 
     def sync():
         if world > 1:
@@ -352,11 +368,43 @@ def main():
         if use_cuda:
             torch.cuda.synchronize(device)
 
+    # Python's cyclic GC stays out of the replays: a gen-2 collection inside
+    # one paused the controller for ~0.1 s (round 3's 0.2547 s outlier replay:
+    # makespan +0.1 s with no eviction / spill / route change). Collected
+    # between replays instead (untimed for the JCTs), with every long-lived
+    # object frozen after the warm-up so those collections stay cheap; the
+    # pause time of any collection that still happens is recorded per replay.
+    gc_ms = [0.0]
+    gc_t = [0.0]
+
+    def _gc_cb(phase, info):
+        if phase == "start":
+            gc_t[0] = time.perf_counter()
+        else:
+            gc_ms[0] += (time.perf_counter() - gc_t[0]) * 1e3
+
+    gc.callbacks.append(_gc_cb)
+    replay_diag = []
+
     def replay(c, out=None):
+        gc.collect()
+        gc.disable()
+        gc_ms[0] = 0.0
+        ev0 = (worker.pool_evictions, worker.pressure_spills, worker.pool_hits)
         t = time.perf_counter()
-        r = run_replay(c, jobs, rank, world, device, ctrl_pg=ctrl_pg, world_pg=world_pg,
-                       worker=worker, quantum=a.quantum, out_dir=out, prior=prior)
+        try:
+            r = run_replay(c, jobs, rank, world, device, ctrl_pg=ctrl_pg, world_pg=world_pg,
+                           worker=worker, quantum=a.quantum, out_dir=out, prior=prior)
+        finally:
+            gc.enable()
         dt = time.perf_counter() - t
+        replay_diag.append({"policy": f"{c.schedule}+{c.scheme}", "avg_jct": round(r["avg_jct"], 4),
+                            "makespan": round(r["makespan"], 4), "wall_s": round(dt, 3),
+                            "gc_ms": round(gc_ms[0], 2),
+                            "pool_evictions": worker.pool_evictions - ev0[0],
+                            "pressure_spills": worker.pressure_spills - ev0[1],
+                            "pool_hits": worker.pool_hits - ev0[2],
+                            "breakdown": r.get("runtime_breakdown")})
         if rank == 0:                  # progress on stderr (the JSON line stays alone on stdout)
             print(f"[bench] {c.schedule}+{c.scheme}{' share' if c.pack else ''}: avg JCT "
                   f"{r['avg_jct']:.4f} s, makespan {r['makespan']:.3f} s, {r['finished']} jobs, "
@@ -382,6 +430,8 @@ def main():
             cold = r_             # the first replay of a fresh process: every trainer built cold
         longest = max(longest, dt)
         warm_done += 1
+    gc.collect()
+    gc.freeze()                       # warm-up state is long-lived: out of every later collection
     sync()
     t0 = time.perf_counter()
     sums = []
@@ -406,6 +456,13 @@ def main():
         # FIFO is non-preemptive: its replay can run longer than Tiresias'
         bcfg = make(a.baseline_policy, a.baseline_placement)
         base, _ = replay(bcfg)
+    # the reference treats 2D-LAS queue limits as absolute GPU-seconds
+    # (run_sim.py dlas_sim_jobs): one untimed replay with the UNSCALED limits
+    # reports that reference-faithful number next to the headline (at N = 1
+    # the two configurations are the same)
+    unscaled = None
+    if a.scale_limits and n > 1 and fits(1.5 * longest):
+        unscaled, _ = replay(make(a.policy, a.placement, limits=list(qlim)))
     nopool = None
     if not a.no_pool and not a.no_nopool_replay and fits(1.5 * longest):
         # one replay WITHOUT the warm trainer pool: every job builds its own
@@ -462,6 +519,11 @@ def main():
             "makespan_s": round(makespan, 4),
             "avg_jct_per_step_s": [round(x, 4) for x in jcts],
             "avg_jct_stdev_s": round(statistics.stdev(jcts), 4) if len(jcts) > 1 else 0.0,
+            "avg_jct_max_s": round(max(jcts), 4),
+            "avg_jct_p95_s": round(sorted(jcts)[min(len(jcts) - 1, int(math.ceil(0.95 * len(jcts))) - 1)], 4),
+            # per timed replay: GC pause inside it, pool / spill activity, and
+            # the controller's runtime breakdown (outlier attribution)
+            "replay_diag": replay_diag[warm_done:warm_done + steps],
             "makespan_per_step_s": [round(x, 4) for x in mks],
             "replay_wall_per_step_s": [round(x, 3) for x in walls],
             "median_jct_s": round(statistics.fmean(s["median_jct"] for s in sums), 4),
@@ -469,6 +531,10 @@ def main():
             "preemptions": sums[-1]["preemptions"],
             "finished_jobs": sums[-1]["finished"],
             "baseline_avg_jct_s": round(base["avg_jct"], 4) if base else None,
+            "unscaled_limits_avg_jct_s": (round(unscaled["avg_jct"], 4) if unscaled else
+                                          (round(avg_jct, 4) if (n == 1 or not a.scale_limits) else None)),
+            "unscaled_limits_vs_baseline": (round((unscaled["avg_jct"] if unscaled else avg_jct) / base["avg_jct"], 4)
+                                            if base and (unscaled or n == 1 or not a.scale_limits) else None),
             # cold start, both untimed: the first warm-up replay of this fresh
             # process, and one replay with the warm trainer pool disabled
             "cold_first_replay_avg_jct_s": round(cold["avg_jct"], 4) if cold else None,
@@ -482,7 +548,7 @@ def main():
             "pressure_spills": worker.pressure_spills,
             "pool_evictions": worker.pool_evictions,
             "restore_prefetches": worker.prefetches,
-            "replays": warm_done + steps + (1 if base else 0) + (1 if nopool else 0),
+            "replays": warm_done + steps + (1 if base else 0) + (1 if nopool else 0) + (1 if unscaled else 0),
             "comm_precreate_s": round(comm_setup_s, 3),
             "process_prewarm_s": round(prewarm_s, 3),
             "comm_stats": sums[-1].get("comm_stats"),

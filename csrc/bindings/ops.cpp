@@ -801,25 +801,38 @@ void cast_op(const Tensor& x, const Tensor& y) {
 }
 
 // ------------------------------------------------------------------ optimizers
+// guard (optional int32 [2], the job's persistent-LSTM error words): a
+// non-zero guard[0] turns the step into a gradient reset (optim.hip)
+static const unsigned* guard_ptr(const optional<Tensor>& guard, const Tensor& like) {
+  if (!(guard.has_value() && guard->defined())) return nullptr;
+  TORCH_CHECK(guard->scalar_type() == at::kInt && guard->numel() >= 2 && guard->device() == like.device(),
+              "tam: guard must be an int32 [2] tensor on the parameters' device");
+  return (const unsigned*)guard->data_ptr<int>();
+}
 void sgd_op(const Tensor& w, const Tensor& g, const Tensor& mom, const Tensor& wb, double lr,
-            double momentum, double wd, double gscale, bool nesterov, bool zero_grad, bool lstm_guard) {
+            double momentum, double wd, double gscale, bool nesterov, bool zero_grad,
+            const optional<Tensor>& guard) {
   check_f32(w, "w"); check_f32(g, "g"); check_f32(mom, "mom"); check_bf16(wb, "wb");
   TORCH_CHECK(w.numel() % 4 == 0 && g.numel() == w.numel() && mom.numel() == w.numel() &&
                   wb.numel() == w.numel(),
               "tam.sgd: sizes");
   tam::sgd_step(w.data_ptr<float>(), g.data_ptr<float>(), mom.data_ptr<float>(), bpm(wb), w.numel(),
                 (float)lr, (float)momentum, (float)wd, (float)gscale, nesterov, zero_grad,
-                cur_stream(w), lstm_guard ? tam::lstm_timeout_word() : nullptr);
+                cur_stream(w), guard_ptr(guard, w));
 }
 void adam_op(const Tensor& w, const Tensor& g, const Tensor& m, const Tensor& v, const Tensor& wb,
              double lr, double b1, double b2, double eps, double wd, int64_t step, double gscale,
-             bool zero_grad, bool lstm_guard) {
+             bool zero_grad, const optional<Tensor>& guard) {
   check_f32(w, "w"); check_f32(g, "g"); check_f32(m, "m"); check_f32(v, "v"); check_bf16(wb, "wb");
   TORCH_CHECK(w.numel() % 4 == 0, "tam.adam: numel % 4");
   tam::adam_step(w.data_ptr<float>(), g.data_ptr<float>(), m.data_ptr<float>(), v.data_ptr<float>(),
                  bpm(wb), w.numel(), (float)lr, (float)b1, (float)b2, (float)eps, (float)wd,
-                 (int)step, (float)gscale, zero_grad, cur_stream(w),
-                 lstm_guard ? tam::lstm_timeout_word() : nullptr);
+                 (int)step, (float)gscale, zero_grad, cur_stream(w), guard_ptr(guard, w));
+}
+void lstm_guard_step_op(const Tensor& err) {
+  TORCH_CHECK(err.is_cuda() && err.scalar_type() == at::kInt && err.numel() >= 2,
+              "tam.lstm_guard_step: err must be an int32 [2] GPU tensor");
+  tam::lstm_guard_step((unsigned*)err.data_ptr<int>(), cur_stream(err));
 }
 
 // ------------------------------------------------------------------ attention
@@ -908,8 +921,21 @@ static void check_sync(const Tensor& sync, int64_t B) {
               sync.numel() >= 32 * (4 * (B / 16) + 1),
               "tam.lstm_seq: sync must be a contiguous int32 tensor of >= 32 * (4 * B/16 + 1) elements");
 }
+// per-launch co-residency rule + the job's timeout word (see tam::PLOpts)
+static tam::PLOpts pl_opts(const optional<Tensor>& job_err, int64_t grids, int64_t rsv) {
+  tam::PLOpts o;
+  o.grids = (int)grids;
+  o.rsv = (int)rsv;
+  if (job_err.has_value() && job_err->defined()) {
+    TORCH_CHECK(job_err->is_cuda() && job_err->scalar_type() == at::kInt && job_err->numel() >= 2,
+                "tam.lstm_seq: job_err must be an int32 [2] GPU tensor");
+    o.job_err = (unsigned*)job_err->data_ptr<int>();
+  }
+  return o;
+}
 bool lstm_seq_fwd_op(const Tensor& gx, const Tensor& w_hh, const Tensor& hs, const Tensor& cs,
-                     const Tensor& act, bool reverse, const Tensor& sync) {
+                     const Tensor& act, bool reverse, const Tensor& sync, const optional<Tensor>& job_err,
+                     int64_t grids, int64_t rsv) {
   check_f32(gx, "gx"); check_bf16(w_hh, "w_hh"); check_bf16(hs, "hs"); check_f32(cs, "cs");
   check_f32(act, "act");
   TORCH_CHECK(hs.dim() == 3 && hs.is_contiguous(), "tam.lstm_seq_forward: hs [T][B][Hd]");
@@ -923,10 +949,11 @@ bool lstm_seq_fwd_op(const Tensor& gx, const Tensor& w_hh, const Tensor& hs, con
   int* sp = sync.data_ptr<int>();
   return tam::lstm_seq_forward(gx.data_ptr<float>(), bp(w_hh), bpm(hs), cs.data_ptr<float>(),
                                act.data_ptr<float>(), (int)T, (int)B, (int)Hd, reverse ? 1 : 0,
-                               (unsigned*)sp, cur_stream(gx));
+                               (unsigned*)sp, cur_stream(gx), pl_opts(job_err, grids, rsv));
 }
 bool lstm_seq_bwd_op(const Tensor& act, const Tensor& cs, const Tensor& dH, const Tensor& w_hh,
-                     const Tensor& dG, bool reverse, const Tensor& sync) {
+                     const Tensor& dG, bool reverse, const Tensor& sync, const optional<Tensor>& job_err,
+                     int64_t grids, int64_t rsv) {
   check_f32(act, "act"); check_f32(cs, "cs"); check_bf16(w_hh, "w_hh");
   TORCH_CHECK(dH.is_cuda() && (dH.scalar_type() == at::kFloat || dH.scalar_type() == at::kBFloat16),
               "tam.lstm_seq_backward: dH must be an f32 or bf16 CUDA tensor");
@@ -943,7 +970,7 @@ bool lstm_seq_bwd_op(const Tensor& act, const Tensor& cs, const Tensor& dH, cons
   int* sp = sync.data_ptr<int>();
   return tam::lstm_seq_backward(act.data_ptr<float>(), cs.data_ptr<float>(), (const float*)dH.data_ptr(),
                                 bp(w_hh), bpm(dG), (int)T, (int)B, (int)Hd, reverse ? 1 : 0, (unsigned*)sp,
-                                dh_bf16, cur_stream(act));
+                                dh_bf16, cur_stream(act), pl_opts(job_err, grids, rsv));
 }
 
 void lstm_seq_policy_op(int64_t ch) { tam::lstm_seq_policy((int)ch); }
@@ -1004,13 +1031,14 @@ TORCH_LIBRARY(tam, m) {
   m.def("relu_backward(Tensor dy, Tensor y, Tensor(a!) dx) -> ()", &relu_backward_op);
   m.def("add(Tensor a, Tensor b, Tensor(a!) y) -> ()", &add_op);
   m.def("cast_f32_bf16(Tensor x, Tensor(a!) y) -> ()", &cast_op);
-  m.def("sgd_step(Tensor(a!) w, Tensor(b!) g, Tensor(c!) mom, Tensor(d!) wb, float lr, float momentum, float wd, float gscale, bool nesterov, bool zero_grad, bool lstm_guard=False) -> ()", &sgd_op);
-  m.def("adam_step(Tensor(a!) w, Tensor(b!) g, Tensor(c!) m, Tensor(d!) v, Tensor(e!) wb, float lr, float b1, float b2, float eps, float wd, int step, float gscale, bool zero_grad, bool lstm_guard=False) -> ()", &adam_op);
+  m.def("sgd_step(Tensor(a!) w, Tensor(b!) g, Tensor(c!) mom, Tensor(d!) wb, float lr, float momentum, float wd, float gscale, bool nesterov, bool zero_grad, Tensor? guard=None) -> ()", &sgd_op);
+  m.def("adam_step(Tensor(a!) w, Tensor(b!) g, Tensor(c!) m, Tensor(d!) v, Tensor(e!) wb, float lr, float b1, float b2, float eps, float wd, int step, float gscale, bool zero_grad, Tensor? guard=None) -> ()", &adam_op);
+  m.def("lstm_guard_step(Tensor(a!) err) -> ()", &lstm_guard_step_op);
   m.def("attn_forward(Tensor q, Tensor k, Tensor v, Tensor(a!) o, Tensor(b!) lse, bool causal, float scale, Tensor? kv_len) -> ()", &attn_forward_op);
   m.def("attn_backward(Tensor q, Tensor k, Tensor v, Tensor o, Tensor dout, Tensor lse, Tensor(a!) dq, Tensor(b!) dk, Tensor(c!) dv, Tensor(d!) dq_acc, Tensor(e!) delta, bool causal, float scale, Tensor? kv_len) -> ()", &attn_backward_op);
   m.def("lstm_step_forward(Tensor gx, Tensor w_hh, Tensor? h_prev, Tensor? c_prev, Tensor(a!) c_out, Tensor(b!) h_out, Tensor(c!) act) -> ()", &lstm_step_fwd_op);
-  m.def("lstm_seq_forward(Tensor gx, Tensor w_hh, Tensor(a!) hs, Tensor(b!) cs, Tensor(c!) act, bool reverse, Tensor(d!) sync) -> bool", &lstm_seq_fwd_op);
-  m.def("lstm_seq_backward(Tensor act, Tensor cs, Tensor dH, Tensor w_hh, Tensor(a!) dG, bool reverse, Tensor(b!) sync) -> bool", &lstm_seq_bwd_op);
+  m.def("lstm_seq_forward(Tensor gx, Tensor w_hh, Tensor(a!) hs, Tensor(b!) cs, Tensor(c!) act, bool reverse, Tensor(d!) sync, Tensor(e!)? job_err=None, int grids=-1, int reserved_cus=0) -> bool", &lstm_seq_fwd_op);
+  m.def("lstm_seq_backward(Tensor act, Tensor cs, Tensor dH, Tensor w_hh, Tensor(a!) dG, bool reverse, Tensor(b!) sync, Tensor(c!)? job_err=None, int grids=-1, int reserved_cus=0) -> bool", &lstm_seq_bwd_op);
   m.def("lstm_seq_policy(int ch) -> ()", &lstm_seq_policy_op);
   m.def("lstm_seq_shards(int ns) -> ()", &lstm_seq_shards_op);
   m.def("gemm_routes_load(str text) -> int", &gemm_routes_load_op);

@@ -115,10 +115,21 @@ void lstm_step_forward(const float* gx, const bf16_t* w_hh, const bf16_t* h_prev
 // persistent whole-sequence recurrence (lstm.hip); false = shape / residency
 // not supported (the caller runs the per-step path). sync: int32 words,
 // [0] error flag, [32 * (bt + 1)] per-batch-tile counters (zeroed here).
+// PLOpts: per-launch co-residency rule (grids that must fit at once, CUs
+// reserved for foreign kernels; grids < 0: the lstm_seq_residency default)
+// and the launching job's own timeout word (nullable).
+struct PLOpts {
+  int grids = -1, rsv = 0;
+  unsigned* job_err = nullptr;
+};
 bool lstm_seq_forward(const float* gx, const bf16_t* w_hh, bf16_t* hs, float* cs, float* act, int T,
-                      int B, int Hd, int reverse, unsigned* sync, hipStream_t s);
+                      int B, int Hd, int reverse, unsigned* sync, hipStream_t s, const PLOpts& o = PLOpts());
 bool lstm_seq_backward(const float* act, const float* cs, const float* dH, const bf16_t* w_hh, bf16_t* dG,
-                       int T, int B, int Hd, int reverse, unsigned* sync, int dh_bf16, hipStream_t s);
+                       int T, int B, int Hd, int reverse, unsigned* sync, int dh_bf16, hipStream_t s,
+                       const PLOpts& o = PLOpts());
+// the job's guard word after its optimizer step: err[0] != 0 (a timed-out
+// barrier this step; the optimizer skipped the update) -> err[1] += 1, err[0] = 0
+void lstm_guard_step(unsigned* err, hipStream_t s);
 // unit halves per persistent workgroup: 0 auto, 1 (16 units) or 2 (32 units)
 void lstm_seq_policy(int ch);
 void lstm_seq_shards(int ns);   // arrival counters per batch tile (1, 2, 4)

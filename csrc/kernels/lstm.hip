@@ -217,7 +217,9 @@ __device__ __forceinline__ void pl_signal(unsigned* sync, int line) {
 }
 
 // target: arrivals expected on EACH of the ns counters line0 .. line0 + ns - 1
-__device__ __forceinline__ void pl_wait(unsigned* sync, int line0, int ns, unsigned target) {
+// job_err (nullable): the launching JOB's own timeout word (models/gnmt.py
+// GNMT.err[0]), so one job's timeout guards only that job's optimizer step
+__device__ __forceinline__ void pl_wait(unsigned* sync, int line0, int ns, unsigned target, unsigned* job_err) {
   if (threadIdx.x < (unsigned)ns) {
     unsigned polls = 0;
     const unsigned spin = g_pl_spin;
@@ -226,6 +228,7 @@ __device__ __forceinline__ void pl_wait(unsigned* sync, int line0, int ns, unsig
       if (++polls > spin) {
         __hip_atomic_fetch_or((pl_gu32*)sync, 1u, PL_RLX);
         __hip_atomic_fetch_add((pl_gu32*)&g_pl_timeouts, 1u, PL_RLX);
+        if (job_err != nullptr) __hip_atomic_fetch_add((pl_gu32*)job_err, 1u, PL_RLX);
         break;
       }
     }
@@ -252,7 +255,7 @@ __device__ __forceinline__ s16x8_t pl_ld16(__amdgpu_buffer_rsrc_t r, unsigned by
 template <int KW, int CH>   // KW: k-steps of 32 per wave = Hd / (32 * PL_W)
 __global__ void __launch_bounds__(64 * PL_W * CH, 4) lstm_persist_fwd_kernel(
     const float* __restrict__ gx, const bf16_t* __restrict__ w, bf16_t* hs, float* __restrict__ cs,
-    float* __restrict__ act, int T, int B, int Hd, int reverse, unsigned* sync, int ns) {
+    float* __restrict__ act, int T, int B, int Hd, int reverse, unsigned* sync, int ns, unsigned* job_err) {
   constexpr int U = 16 * CH;                 // units per workgroup
   __shared__ float red[PL_W][16][4 * U + 1];
   __shared__ __attribute__((aligned(16))) bf16_t hbuf[16][U];
@@ -336,7 +339,7 @@ __global__ void __launch_bounds__(64 * PL_W * CH, 4) lstm_persist_fwd_kernel(
       }
       if (s + 1 < T) pl_signal(sync, bt * ns + ut % ns);
     }
-    if (s + 1 < T) pl_wait(sync, bt * ns, ns, (unsigned)(s + 1) * (unsigned)(Hd / U / ns));
+    if (s + 1 < T) pl_wait(sync, bt * ns, ns, (unsigned)(s + 1) * (unsigned)(Hd / U / ns), job_err);
   }
 }
 
@@ -348,7 +351,7 @@ template <int KW, int CH>   // KW: k-steps of 32 per wave = 4 Hd / (32 * PL_W)
 __global__ void __launch_bounds__(64 * PL_W * CH, 4) lstm_persist_bwd_kernel(
     const float* __restrict__ act, const float* __restrict__ cs, const float* __restrict__ dH,
     const bf16_t* __restrict__ w, bf16_t* dG, int T, int B, int Hd, int reverse, unsigned* sync, int ns,
-    int dh_bf16) {
+    int dh_bf16, unsigned* job_err) {
   constexpr int U = 16 * CH;
   // W fragments: the first KWR k-steps in VGPRs, the rest in LDS (the whole
   // slice in VGPRs needs > 128 of them and spills; CH = 1 only: 2 blocks/CU
@@ -467,25 +470,31 @@ __global__ void __launch_bounds__(64 * PL_W * CH, 4) lstm_persist_bwd_kernel(
       if (s + 1 < T) pl_signal(sync, bt * ns + ut % ns);
     }
     if (cell && s + 1 < T) load_cell(s + 1);   // after the signal's vmcnt(0) drain
-    if (s + 1 < T) pl_wait(sync, bt * ns, ns, (unsigned)(s + 1) * (unsigned)(Hd / U / ns));
+    if (s + 1 < T) pl_wait(sync, bt * ns, ns, (unsigned)(s + 1) * (unsigned)(Hd / U / ns), job_err);
   }
 }
 
-// Co-residency: g_pl_grids such grids must fit at once (GPU sharing can put
-// two GNMT jobs on one device), on the CUs left after g_pl_rsv_cus are set
-// aside for kernels that run concurrently with the recurrence and are not
-// ours -- RCCL's all-reduce of a DDP gang occupies up to one workgroup per
-// channel. Set per job by the trainer (lstm_seq_residency); the occupancy
-// query is cached per kernel.
+// Co-residency: `grids` such grids must fit at once (GPU sharing can put
+// two GNMT jobs on one device), on the CUs left after `rsv` are set aside
+// for kernels that run concurrently with the recurrence and are not ours --
+// RCCL's all-reduce of a DDP gang occupies up to one workgroup per channel.
+// Passed with every launch by the job's model (GNMT.residency; a process-
+// wide setting would let two jobs sharing a device overwrite each other's);
+// lstm_seq_residency only sets the default for callers that pass none
+// (grids < 0). The occupancy query is cached per kernel.
 static int g_pl_grids = 2, g_pl_rsv_cus = 0;
 void lstm_seq_residency(int grids, int reserved_cus) {
   g_pl_grids = grids < 1 ? 1 : grids;
   g_pl_rsv_cus = reserved_cus < 0 ? 0 : reserved_cus;
 }
 
-static bool pl_fits(const void* kern, int threads, int grid) {
+static bool pl_fits(const void* kern, int threads, int grid, int grids, int rsv) {
   static std::mutex mu;
   static std::map<const void*, std::pair<int, int>> cap;   // kernel -> (per CU, CUs)
+  if (grids < 1) {
+    grids = g_pl_grids;
+    rsv = g_pl_rsv_cus;
+  }
   std::lock_guard<std::mutex> g(mu);
   auto it = cap.find(kern);
   if (it == cap.end()) {
@@ -496,8 +505,8 @@ static bool pl_fits(const void* kern, int threads, int grid) {
       per_cu = cus = 0;
     it = cap.emplace(kern, std::make_pair(per_cu, cus)).first;
   }
-  const int usable = it->second.first * (it->second.second - g_pl_rsv_cus);
-  return g_pl_grids * grid <= usable;
+  const int usable = it->second.first * (it->second.second - (rsv < 0 ? 0 : rsv));
+  return grids * grid <= usable;
 }
 
 int64_t lstm_persist_timeouts(bool reset) {
@@ -539,38 +548,38 @@ static int pl_ch(int Hd) {
 
 template <int KW, int CH>
 static bool pl_fwd(const float* gx, const bf16_t* w_hh, bf16_t* hs, float* cs, float* act, int T, int B,
-                   int Hd, int reverse, unsigned* sync, hipStream_t s) {
+                   int Hd, int reverse, unsigned* sync, const PLOpts& o, hipStream_t s) {
   const int grid = (B / 16) * (Hd / (16 * CH));
   auto k = lstm_persist_fwd_kernel<KW, CH>;
-  if (!pl_fits((const void*)k, 64 * PL_W * CH, grid)) return false;
+  if (!pl_fits((const void*)k, 64 * PL_W * CH, grid, o.grids, o.rsv)) return false;
   const int ns = (Hd / (16 * CH)) % g_pl_ns == 0 ? g_pl_ns : 1;
   zero_async(sync, (size_t)(1 + (B / 16) * ns) * 128, s);   // error flag line + counters
   hipLaunchKernelGGL(k, dim3(grid), dim3(64 * PL_W * CH), 0, s, gx, w_hh, hs, cs, act, T, B, Hd, reverse,
-                     sync, ns);
+                     sync, ns, o.job_err);
   return true;
 }
 
 template <int KW, int CH>
 static bool pl_bwd(const float* act, const float* cs, const float* dH, const bf16_t* w_hh, bf16_t* dG, int T,
-                   int B, int Hd, int reverse, unsigned* sync, int dh_bf16, hipStream_t s) {
+                   int B, int Hd, int reverse, unsigned* sync, int dh_bf16, const PLOpts& o, hipStream_t s) {
   const int grid = (B / 16) * (Hd / (16 * CH));
   auto k = lstm_persist_bwd_kernel<KW, CH>;
-  if (!pl_fits((const void*)k, 64 * PL_W * CH, grid)) return false;
+  if (!pl_fits((const void*)k, 64 * PL_W * CH, grid, o.grids, o.rsv)) return false;
   const int ns = (Hd / (16 * CH)) % g_pl_ns == 0 ? g_pl_ns : 1;
   zero_async(sync, (size_t)(1 + (B / 16) * ns) * 128, s);   // error flag line + counters
   hipLaunchKernelGGL(k, dim3(grid), dim3(64 * PL_W * CH), 0, s, act, cs, dH, w_hh, dG, T, B, Hd, reverse,
-                     sync, ns, dh_bf16);
+                     sync, ns, dh_bf16, o.job_err);
   return true;
 }
 
 bool lstm_seq_forward(const float* gx, const bf16_t* w_hh, bf16_t* hs, float* cs, float* act, int T,
-                      int B, int Hd, int reverse, unsigned* sync, hipStream_t s) {
+                      int B, int Hd, int reverse, unsigned* sync, hipStream_t s, const PLOpts& o) {
   if (T < 1 || B % 16 != 0 || Hd % 256 != 0 || 8 % (B / 16) != 0) return false;
   const int kw = Hd / (32 * PL_W), ch = pl_ch(Hd);
 #define PL_F(KWV)                                                                                    \
   case KWV:                                                                                          \
-    return ch == 2 ? pl_fwd<KWV, 2>(gx, w_hh, hs, cs, act, T, B, Hd, reverse, sync, s)              \
-                   : pl_fwd<KWV, 1>(gx, w_hh, hs, cs, act, T, B, Hd, reverse, sync, s);
+    return ch == 2 ? pl_fwd<KWV, 2>(gx, w_hh, hs, cs, act, T, B, Hd, reverse, sync, o, s)           \
+                   : pl_fwd<KWV, 1>(gx, w_hh, hs, cs, act, T, B, Hd, reverse, sync, o, s);
   switch (kw) {
     PL_F(1)
     PL_F(2)
@@ -581,13 +590,14 @@ bool lstm_seq_forward(const float* gx, const bf16_t* w_hh, bf16_t* hs, float* cs
 }
 
 bool lstm_seq_backward(const float* act, const float* cs, const float* dH, const bf16_t* w_hh, bf16_t* dG,
-                       int T, int B, int Hd, int reverse, unsigned* sync, int dh_bf16, hipStream_t s) {
+                       int T, int B, int Hd, int reverse, unsigned* sync, int dh_bf16, hipStream_t s,
+                       const PLOpts& o) {
   if (T < 1 || B % 16 != 0 || Hd % 256 != 0 || 8 % (B / 16) != 0) return false;
   const int kw = 4 * Hd / (32 * PL_W), ch = pl_ch(Hd);
 #define PL_B(KWV)                                                                                    \
   case KWV:                                                                                          \
-    return ch == 2 ? pl_bwd<KWV, 2>(act, cs, dH, w_hh, dG, T, B, Hd, reverse, sync, dh_bf16, s)     \
-                   : pl_bwd<KWV, 1>(act, cs, dH, w_hh, dG, T, B, Hd, reverse, sync, dh_bf16, s);
+    return ch == 2 ? pl_bwd<KWV, 2>(act, cs, dH, w_hh, dG, T, B, Hd, reverse, sync, dh_bf16, o, s)  \
+                   : pl_bwd<KWV, 1>(act, cs, dH, w_hh, dG, T, B, Hd, reverse, sync, dh_bf16, o, s);
   switch (kw) {
     PL_B(4)
     PL_B(8)

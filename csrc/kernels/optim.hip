@@ -9,10 +9,12 @@
 //
 // ``guard`` (nullable): a device word that, when non-zero, turns the step
 // into a gradient reset only -- no master / state / shadow update. The
-// trainer of a GNMT job passes the persistent-LSTM timeout counter
-// (lstm.hip g_pl_timeouts): a step whose recurrence read h / dG that had not
-// arrived must not reach the weights (the host learns of it at round end and
-// switches the job to the per-step recurrence).
+// trainer of a GNMT job passes ITS OWN persistent-LSTM timeout word
+// (models/gnmt.py GNMT.err[0], bumped by a timed-out grid barrier of that
+// job only): a step whose recurrence read h / dG that had not arrived must
+// not reach the weights. lstm_guard_step then moves the word into the job's
+// skipped-step count (err[1]), which the worker subtracts from the round's
+// progress and uses to switch the job to the per-step recurrence.
 #include "tam/common.h"
 #include "tam/kernels.h"
 
@@ -96,6 +98,17 @@ void adam_step(float* w, float* g, float* m, float* v, bf16_t* wb, long n, float
   const float bc1 = 1.f - powf(b1, (float)step), bc2 = 1.f - powf(b2, (float)step);
   hipLaunchKernelGGL(adam_kernel, dim3(ogrid(n / 4)), dim3(256), 0, s, w, g, m, v, wb, n / 4, lr,
                      b1, b2, eps, wd, bc1, bc2, gscale, zero_grad, guard);
+}
+
+__global__ void lstm_guard_step_kernel(unsigned* err) {
+  if (threadIdx.x == 0 && err[0] != 0u) {
+    err[1] += 1u;
+    err[0] = 0u;
+  }
+}
+
+void lstm_guard_step(unsigned* err, hipStream_t s) {
+  hipLaunchKernelGGL(lstm_guard_step_kernel, dim3(1), dim3(64), 0, s, err);
 }
 
 }  // namespace tam

@@ -6,6 +6,7 @@
 #include <array>
 #include <cmath>
 #include <limits>
+#include <map>
 #include <numeric>
 #include <stdexcept>
 #include <string>
@@ -35,7 +36,14 @@ struct Job {
   int state = SUB;
   double start = -1, end = -1, last_check = 0;
   int preempt = 0, resume = 0, promote = 0;
+  // priced replays (Engine::set_costs): progress rate of the current
+  // placement (spread gangs < 1), the restore / save stall still ahead of
+  // the next resume, and what checkpointing cost so far -- core/job.py
+  double rate = 1.0, restore_left = 0.0, pending_ckpt = 0.0, overhead = 0.0, ckpt_bytes = 0.0;
+  int where = 0;                       // suspended state: 0 none, 1 resident in HBM, 2 on the host
+  std::vector<std::pair<int, int>> where_devs;   // (node, device) holding it when resident
   double remaining() const { return std::max(0.0, dur - progress); }
+  double time_to_finish() const { return rate <= 0 ? INF : restore_left + remaining() / rate; }
   double attained(bool g) const { return g ? executed * gpu : executed; }
 };
 
@@ -77,14 +85,37 @@ struct Gittins {
 };
 
 enum Pol { FIFO, FJF, SJF, SRTF, SRSF, DLAS, DLASG, DLASGG, GITT };
-enum Place { P_COUNT, P_YARN, P_TIRESIAS };
+// P_COUNT: flat GPU pool; P_FILL: "count" on the topology (placement/
+// schemes.py::CountPlacement: tasks filled node by node in id order) -- used
+// when costs need the nodes / devices a job landed on
+enum Place { P_COUNT, P_YARN, P_TIRESIAS, P_FILL };
 
 inline Place parse_place(const std::string& s) {
-  if (s == "count" || s.empty()) return P_COUNT;
+  if (s.empty()) return P_COUNT;
+  if (s == "count") return P_FILL;
   if (s == "yarn") return P_YARN;
   if (s == "tiresias") return P_TIRESIAS;
   throw std::invalid_argument("sched_core: unsupported placement " + s);
 }
+
+// The Python engine's cost terms (engine/sim.py::Simulator._rate and
+// engine/ckpt_model.py::CkptCostModel), evaluated from per-job parameters the
+// front-end derives once (engine/native.py):
+//  * network: a gang spread over k > 1 nodes progresses at
+//    1 / (1 + (sd - 1) * 2(k-1)/k) from its MEASURED 2-node slowdown sd
+//    (cluster/network.py::measured_spread_rate), else c / (c + allreduce(k))
+//    with per-iteration time c and the analytic ring all-reduce over the
+//    link bandwidth / latency (network_rate);
+//  * checkpoints: 0 none; 1 host (every preemption spills, every resume
+//    restores: bytes / bandwidth); 2 hbm / measured / pressure (suspended
+//    state stays resident within a per-GPU budget: resume on the same GPUs
+//    free, elsewhere an xGMI copy; over budget the host path).
+struct Costs {
+  bool net = false;
+  double bw_mbps = 1250.0, latency = 0.015;
+  int ckpt = 0;
+  double host_gbps = 50.0, h2d_gbps = 50.0, xgmi_gbps = 64.0, budget = 200e9;
+};
 
 // Racks x nodes x devices with per-node CPU / memory, the Python Cluster's
 // exclusive (no packing) state: cluster/topology.py. Placement plans are
@@ -147,6 +178,18 @@ class Engine {
     total_ = switches * nodes_per * gpus;
   }
 
+  // Cost terms (see Costs) and their per-job parameters: state bytes per GPU
+  // (ckpt_b), measured 2-node slowdown (net_sd, < 0: none -> analytic with
+  // per-iteration seconds net_c and all-reduce bytes net_bytes). Arrays of
+  // the next run's length; costs need a topology placement.
+  void set_costs(const Costs& c, std::vector<double> ckpt_b, std::vector<double> net_sd,
+                 std::vector<double> net_c, std::vector<double> net_bytes) {
+    costs_ = c;
+    ckpt_b_ = std::move(ckpt_b); net_sd_ = std::move(net_sd);
+    net_c_ = std::move(net_c); net_bytes_ = std::move(net_bytes);
+  }
+  bool priced() const { return costs_.net || costs_.ckpt != 0; }
+
   void run_topo(const double* submit, const double* dur, const int* gpus, const int* gpw, const int* tcpu,
                 const int* tmem, const unsigned char* sens, long n) {
     shape_.assign(n, {});
@@ -171,6 +214,13 @@ class Engine {
       }
       jobs_.push_back(j);
     }
+    if (priced()) {
+      if (place_ == P_COUNT) throw std::invalid_argument("sched_core: costs need a topology placement");
+      if ((long)ckpt_b_.size() != n || (long)net_sd_.size() != n || (long)net_c_.size() != n ||
+          (long)net_bytes_.size() != n)
+        throw std::invalid_argument("sched_core: set_costs arrays must match the run's job count");
+    }
+    resident_.clear();
     if (place_ != P_COUNT) {
       for (int k = 0; k < topo_.nodes(); ++k) {
         std::fill(topo_.busy[k].begin(), topo_.busy[k].end(), 0);
@@ -199,7 +249,7 @@ class Engine {
       }
       if (t <= now_ + 1e-9 * std::max(1.0, now_)) {
         t = now_;
-        if (++stall > 10000) throw std::runtime_error("sched_core: no progress");
+        if (++stall > 10000) throw std::runtime_error("sched_core: no progress (" + stall_info() + ")");
       } else {
         stall = 0;
       }
@@ -225,9 +275,33 @@ class Engine {
     double t = next_arrival();
     for (long k : active_) {
       const Job& j = jobs_[k];
-      if (j.state == RUN) t = std::min(t, now_ + j.remaining());
+      if (j.state == RUN) t = std::min(t, now_ + j.time_to_finish());
     }
     return std::min(t, policy_next());
+  }
+
+  // wall seconds to the job's next Gittins quantum boundary; one closer than
+  // the clock tolerance counts as reached (policy/las.py::_quantum_wait)
+  double quantum_wait(const Job& j) const {
+    const double dl = git_.delta;
+    const double a = j.attained(true);
+    double w = ((std::floor(a / dl + 1e-6) + 1) * dl - a) / j.gpu;
+    if (w <= 1e-9 * std::max(1.0, now_)) w += dl / j.gpu;
+    return w;
+  }
+
+  // what keeps requesting events at now (the stall diagnostic)
+  std::string stall_info() {
+    std::string out = "t=" + std::to_string(now_);
+    for (long k : active_) {
+      const Job& j = jobs_[k];
+      if (j.state == RUN && now_ + j.time_to_finish() <= now_ + 1e-9 * std::max(1.0, now_))
+        out += " finish:job" + std::to_string(j.idx) + " ttf=" + std::to_string(j.time_to_finish()) +
+               " rem=" + std::to_string(j.remaining()) + " rate=" + std::to_string(j.rate);
+    }
+    const double p = policy_next();
+    out += " policy_next-now=" + std::to_string(p - now_);
+    return out;
   }
 
   double policy_next() {
@@ -244,12 +318,7 @@ class Engine {
           if (left > 0) t = std::min(t, now_ + left);
         }
       }
-      if ((pol_ == DLASGG || pol_ == GITT) && j.state == RUN) {
-        const double dl = git_.delta;
-        const double a = j.attained(true);
-        const double nxt = (std::floor(a / dl + 1e-6) + 1) * dl;
-        t = std::min(t, now_ + (nxt - a) / j.gpu);
-      }
+      if ((pol_ == DLASGG || pol_ == GITT) && j.state == RUN) t = std::min(t, now_ + quantum_wait(j));
     }
     return t;
   }
@@ -262,7 +331,13 @@ class Engine {
       if (j.state == RUN) {
         j.total_exec += dt;
         j.executed += dt;
-        j.progress = std::min(j.dur, j.progress + dt);
+        double work = dt;
+        if (j.restore_left > 0) {                 // stalled on a restore / the last save
+          const double r = std::min(j.restore_left, dt);
+          j.restore_left -= r;
+          work -= r;
+        }
+        j.progress = std::min(j.dur, j.progress + work * j.rate);
       } else if (j.state == PEND) {
         j.pending += dt;
         if (j.executed > 0) j.last_pending += dt;
@@ -279,12 +354,13 @@ class Engine {
     const double tol = 1e-9 * std::max(1.0, now_);
     for (size_t a = 0; a < active_.size();) {
       Job& j = jobs_[active_[a]];
-      if (j.state == RUN && (j.remaining() <= EPS * std::max(1.0, j.dur) || j.remaining() <= tol)) {
+      if (j.state == RUN && (j.remaining() <= EPS * std::max(1.0, j.dur) || j.time_to_finish() <= tol)) {
         j.progress = j.dur;
         j.state = DONE;
         j.end = now_;
         used_ -= j.gpu;
         release(j);
+        ckpt_finish(j);
         if (online_ && (pol_ == DLASGG || pol_ == GITT)) git_.add(j.total_exec * j.gpu);
         active_.erase(active_.begin() + a);
       } else {
@@ -301,6 +377,7 @@ class Engine {
     }
     update();
     schedule();
+    if (costs_.net) refresh_rates();
     if (is_dlas()) {
       std::vector<long> pend;
       for (long k : active_) if (jobs_[k].state == PEND) pend.push_back(k);
@@ -363,11 +440,113 @@ class Engine {
     if (j.start < 0) j.start = now_;
     j.state = RUN; j.resume++; j.last_check = now_;   // last_pending kept until promotion
     used_ += j.gpu;
+    if (priced()) {
+      // stall before progress resumes: this restore + the last preemption's save
+      const double restore = ckpt_resume(j);
+      j.restore_left = restore + j.pending_ckpt;
+      j.pending_ckpt = 0;
+      j.overhead += restore;
+      j.rate = 1.0;                                  // refresh_rates after the round
+    }
   }
   void preempt(Job& j) {
+    if (priced()) {
+      const double save = ckpt_preempt(j);          // on the allocation it ran on
+      j.restore_left = 0;
+      j.pending_ckpt += save;
+      j.overhead += save;
+    }
     j.state = PEND; j.preempt++; j.last_check = now_;
     used_ -= j.gpu;
     release(j);
+  }
+
+  // ------------------------------------------------------------ cost terms
+  std::vector<std::pair<int, int>> devs_of(const Job& j) const {
+    std::vector<std::pair<int, int>> v;
+    size_t p = 0;
+    for (int t = 0; t < j.ntask && p < j.plan.size(); ++t) {
+      const int nd = j.plan[p++];
+      for (int g = 0; g < j.tgpu; ++g) v.emplace_back(nd, j.plan[p++]);
+    }
+    std::sort(v.begin(), v.end());
+    return v;
+  }
+  int nodes_of(const Job& j) const {
+    std::vector<int> nd;
+    size_t p = 0;
+    for (int t = 0; t < j.ntask && p < j.plan.size(); ++t) {
+      nd.push_back(j.plan[p]);
+      p += 1 + j.tgpu;
+    }
+    std::sort(nd.begin(), nd.end());
+    return (int)(std::unique(nd.begin(), nd.end()) - nd.begin());
+  }
+  double spread_rate(const Job& j, int k) const {
+    if (k <= 1) return 1.0;
+    const double sd = net_sd_[j.idx];
+    if (sd >= 0) return 1.0 / (1.0 + std::max(0.0, sd - 1.0) * 2.0 * (k - 1) / k);
+    const double c = net_c_[j.idx];
+    const double comm = 2.0 * (k - 1) / k * (net_bytes_[j.idx] / 1048576.0) / costs_.bw_mbps +
+                        2.0 * (k - 1) * costs_.latency;
+    return c > 0 ? c / (c + comm) : 1.0;
+  }
+  void refresh_rates() {
+    for (long k : active_) {
+      Job& j = jobs_[k];
+      if (j.state == RUN) j.rate = spread_rate(j, nodes_of(j));
+    }
+  }
+  // engine/ckpt_model.py::CkptCostModel.on_preempt -> save seconds
+  double ckpt_preempt(Job& j) {
+    j.where = 0;
+    if (costs_.ckpt == 0) return 0.0;
+    const double b = ckpt_b_[j.idx];
+    if (costs_.ckpt == 2 && !j.plan.empty()) {
+      const auto devs = devs_of(j);
+      bool fits = true;
+      for (const auto& d : devs) {
+        auto it = resident_.find(d);
+        if ((it == resident_.end() ? 0.0 : it->second) + b > costs_.budget) { fits = false; break; }
+      }
+      if (fits) {
+        for (const auto& d : devs) resident_[d] += b;
+        j.where = 1;
+        j.where_devs = devs;
+        return 0.0;
+      }
+    }
+    j.where = 2;
+    j.where_devs.clear();
+    j.ckpt_bytes += b * j.gpu;
+    return b / (costs_.host_gbps * 1e9);
+  }
+  void unreside(Job& j, double b) {
+    for (const auto& d : j.where_devs) {
+      double& r = resident_[d];
+      r = std::max(0.0, r - b);
+    }
+    j.where_devs.clear();
+  }
+  // on_resume -> restore seconds (the job's new plan is committed)
+  double ckpt_resume(Job& j) {
+    const int w = j.where;
+    j.where = 0;
+    if (w == 0 || costs_.ckpt == 0) return 0.0;
+    const double b = ckpt_b_[j.idx];
+    if (w == 1) {
+      const bool same = j.where_devs == devs_of(j);
+      unreside(j, b);
+      if (same) return 0.0;
+      j.ckpt_bytes += b * j.gpu;
+      return b / (costs_.xgmi_gbps * 1e9);
+    }
+    j.ckpt_bytes += b * j.gpu;
+    return b / (costs_.h2d_gbps * 1e9);
+  }
+  void ckpt_finish(Job& j) {
+    if (j.where == 1) unreside(j, ckpt_b_.empty() ? 0.0 : ckpt_b_[j.idx]);
+    j.where = 0;
   }
 
   // ------------------------------------------------------------ placement
@@ -380,7 +559,14 @@ class Engine {
       return true;
     }
     std::vector<int> plan;
-    const bool ok = place_ == P_YARN ? plan_yarn(j, plan) : plan_tiresias(j, plan);
+    bool ok;
+    if (place_ == P_FILL) {
+      std::vector<int> all(topo_.nodes());
+      std::iota(all.begin(), all.end(), 0);
+      ok = fill(j, all, plan);
+    } else {
+      ok = place_ == P_YARN ? plan_yarn(j, plan) : plan_tiresias(j, plan);
+    }
     if (!ok) return false;
     commit(j, plan);
     start(j);
@@ -540,6 +726,9 @@ class Engine {
 
   Pol pol_;
   Place place_ = P_COUNT;
+  Costs costs_;
+  std::vector<double> ckpt_b_, net_sd_, net_c_, net_bytes_;
+  std::map<std::pair<int, int>, double> resident_;   // (node, device) -> suspended state bytes
   Topo topo_;
   std::vector<std::array<int, 5>> shape_;
   int total_;

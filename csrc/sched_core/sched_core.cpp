@@ -4,11 +4,13 @@
 // placements, packing, interference, network, checkpoints, live runtime);
 // it is O(active jobs) Python per event. Replaying the month-long NSDI'19
 // trace (~10^5 jobs) across a policy sweep needs a native loop. This core
-// implements the same event semantics for the resource-counting placement
-// ("count") with the preemptive / non-preemptive policy family Tiresias is
+// implements the same event semantics for the count / yarn / tiresias
+// placements with the preemptive / non-preemptive policy family Tiresias is
 // evaluated on — fifo, fjf, sjf, shortest, shortest-gpu, dlas, dlas-gpu,
-// dlas-gpu-gittins, gittins — and is cross-checked job-for-job against the
-// Python engine in tests/test_sched_core.py.
+// dlas-gpu-gittins, gittins — optionally PRICED like the Python engine
+// (spread-gang network rate, checkpoint save / restore stalls: set_costs),
+// and is cross-checked job-for-job against the Python engine in
+// tests/test_sched_core.py.
 #include <pybind11/numpy.h>
 #include <pybind11/pybind11.h>
 #include <pybind11/stl.h>
@@ -73,6 +75,28 @@ py::dict run_topo_py(Engine& e, py::array_t<double> submit, py::array_t<double> 
   return collect(e, n);
 }
 
+void set_costs_py(Engine& e, bool net, double bw_mbps, double latency, int ckpt, double host_gbps,
+                  double h2d_gbps, double xgmi_gbps, double budget_bytes, std::vector<double> ckpt_b,
+                  std::vector<double> net_sd, std::vector<double> net_c, std::vector<double> net_bytes) {
+  tam_sched::Costs c;
+  c.net = net; c.bw_mbps = bw_mbps; c.latency = latency; c.ckpt = ckpt;
+  c.host_gbps = host_gbps; c.h2d_gbps = h2d_gbps; c.xgmi_gbps = xgmi_gbps; c.budget = budget_bytes;
+  if (ckpt < 0 || ckpt > 2) throw std::invalid_argument("sched_core.set_costs: ckpt must be 0, 1 or 2");
+  e.set_costs(c, std::move(ckpt_b), std::move(net_sd), std::move(net_c), std::move(net_bytes));
+}
+
+py::dict costs_py(Engine& e) {
+  const auto& jobs = e.jobs();
+  const long n = (long)jobs.size();
+  py::array_t<double> ov(n), by(n);
+  auto O = ov.mutable_unchecked<1>();
+  auto B = by.mutable_unchecked<1>();
+  for (long i = 0; i < n; ++i) { O(i) = jobs[i].overhead; B(i) = jobs[i].ckpt_bytes; }
+  py::dict out;
+  out["overhead"] = ov; out["ckpt_bytes"] = by;
+  return out;
+}
+
 }  // namespace
 
 PYBIND11_MODULE(_sched_core, m) {
@@ -85,6 +109,11 @@ PYBIND11_MODULE(_sched_core, m) {
       .def("run", &run_py, py::arg("submit"), py::arg("duration"), py::arg("gpus"))
       .def("set_topology", &Engine::set_topology, py::arg("placement"), py::arg("switches"),
            py::arg("nodes_per_switch"), py::arg("gpus_per_node"), py::arg("cpus"), py::arg("mem"))
+      .def("set_costs", &set_costs_py, py::arg("network"), py::arg("bw_mbps"), py::arg("latency"),
+           py::arg("ckpt"), py::arg("host_gbps"), py::arg("h2d_gbps"), py::arg("xgmi_gbps"),
+           py::arg("budget_bytes"), py::arg("ckpt_bytes"), py::arg("net_slowdown"), py::arg("net_iter_s"),
+           py::arg("net_bytes"))
+      .def("costs", &costs_py)
       .def("run_topo", &run_topo_py, py::arg("submit"), py::arg("duration"), py::arg("gpus"),
            py::arg("gpu_per_worker"), py::arg("cpu_per_task"), py::arg("mem_per_task"), py::arg("sensitive"));
 }

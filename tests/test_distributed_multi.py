@@ -244,6 +244,52 @@ def test_gang_protocol_world4(tmp_path):
     assert torch.equal(r[3]["after_move"], r[2]["before_move"])
 
 
+# ------------------------------------------------------------------ communicator pre-flight
+def _preflight_worker(rank, world, port, q):
+    from tiresias_amd.parallel import gang as G
+
+    _init(rank, world, port)
+    ctrl = dist.new_group(backend="gloo")
+    sets = G.canonical_gang_sets(world)
+    groups = {s: G.create_gang_comm(s, rank, backend="gloo") for s in sets}
+    out = {"clean": G.preflight(groups, rank, torch.device("cpu"), dist.group.WORLD, ctrl, timeout_s=30)}
+    # a member that corrupts its contribution on gang (2, 3)
+    c = groups.get((2, 3))
+    if c is not None and rank == 2:
+        real = c.start
+        c.start = lambda t, real=real: real(t.add_(1.0))
+    out["corrupt"] = G.preflight(groups, rank, torch.device("cpu"), None, ctrl, timeout_s=30)
+    if c is not None and rank == 2:
+        c.start = real
+    # a member that never joins gang (0, 1, 2, 3): its peers time out
+    g2 = {k: v for k, v in groups.items() if not (rank == 3 and k == (0, 1, 2, 3))}
+    out["missing"] = G.preflight(g2, rank, torch.device("cpu"), None, ctrl, timeout_s=4)
+    q.put((rank, out))
+    dist.barrier(group=ctrl)
+    os._exit(0)
+
+
+def test_preflight_names_broken_gangs():
+    """bench.py's N > 1 pre-flight (parallel/gang.py preflight) on gloo world
+    4: clean communicators pass; a corrupted contribution and a member that
+    never joins are both caught, named by rank set, and reported to EVERY
+    rank (so all of them stop together)."""
+    world = 4
+    q = mp.get_context("spawn").SimpleQueue()
+    ctx = mp.get_context("spawn")
+    port = _free_port()
+    ps = [ctx.Process(target=_preflight_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in ps:
+        p.start()
+    res = dict(q.get() for _ in range(world))
+    for p in ps:
+        p.join(60)
+    for r in range(world):
+        assert res[r]["clean"] == [], res[r]
+        assert res[r]["corrupt"] and all("(2, 3)" in e for e in res[r]["corrupt"]), res[r]
+        assert any("timed out" in e and "(0, 1, 2, 3)" in e for e in res[r]["missing"]), res[r]
+
+
 # ------------------------------------------------------------------ torchrun, 8 ranks
 @pytest.mark.slow
 def test_torchrun_bench_world8_cpu(tmp_path):

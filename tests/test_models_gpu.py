@@ -264,11 +264,16 @@ def test_persist_barrier_timeout_is_loud_and_falls_back(gpu):
         T.lstm_seq_spin_limit(0)
     err = rep["jobs"][0].get("error") or ""
     assert "PersistTimeout" in err, rep
+    assert rep["jobs"][0]["iters"] == 0, rep        # the guarded step is not progress
     assert not w.trainers["1"].model.persist
+    assert int(w.trainers["1"].model.err.sum()) == 0      # read and reset by the worker
+    assert G.device_timeouts(reset=True) > 0              # the device-wide counter saw them too
     rep2 = w.run({"actions": [], "assign": {0: [("1", 2)]}, "deadline": None})
     assert "error" not in rep2["jobs"][0], rep2
+    assert rep2["jobs"][0]["iters"] == 2
     assert rep2["jobs"][0]["loss"] == rep2["jobs"][0]["loss"]          # finite
     assert G.device_timeouts(reset=False) == 0
+    assert w.trainers["1"].persist_skipped(reset=False) == 0
     w.clear(keep_pool=False)
 
 
@@ -298,3 +303,33 @@ def test_snapshot_roundtrip_on_device(gpu, tmp_path):
     assert not torch.equal(u.arena.master, t.arena.master)
     assert torch.equal(u.arena.shadow, want_w.to(torch.bfloat16))
     w.close()
+
+
+def test_optimizer_guard_is_per_job(gpu):
+    """The persistent-LSTM guard is the JOB's own word: a set guard turns
+    that job's optimizer step into a gradient reset and lstm_guard_step
+    moves it into the job's skipped-step count; a job with a clear word
+    (sharing the device) updates normally."""
+    from tiresias_amd.ops import _lib
+
+    T = _lib.ops()
+    n = 4096
+    for opt in ("sgd", "adam"):
+        outs = []
+        for bad in (1, 0):
+            w = torch.randn(n, device=gpu)
+            w0 = w.clone()
+            g = torch.randn(n, device=gpu)
+            m, v = torch.zeros(n, device=gpu), torch.zeros(n, device=gpu)
+            wb = torch.empty(n, device=gpu, dtype=torch.bfloat16)
+            err = torch.tensor([bad, 0], dtype=torch.int32, device=gpu)
+            if opt == "sgd":
+                T.sgd_step(w, g, m, wb, 0.1, 0.9, 0.0, 1.0, False, True, err)
+            else:
+                T.adam_step(w, g, m, v, wb, 0.1, 0.9, 0.98, 1e-9, 0.0, 1, 1.0, True, err)
+            T.lstm_guard_step(err)
+            torch.cuda.synchronize()
+            assert float(g.abs().sum()) == 0.0                  # gradient reset either way
+            outs.append((torch.equal(w, w0), err.tolist()))
+        assert outs[0] == (True, [0, 1]), (opt, outs)           # guarded: no update, counted
+        assert outs[1] == (False, [0, 0]), (opt, outs)          # the other job updates

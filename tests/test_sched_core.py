@@ -72,3 +72,41 @@ def test_native_topology_placement_matches_python(policy, scheme):
     np.testing.assert_allclose(ns["per_job"]["end"], py_end, rtol=1e-9, atol=1e-6)
     np.testing.assert_array_equal(ns["per_job"]["preempt"], py_pre)
     assert ns["scheme"] == scheme
+
+
+@pytest.mark.parametrize("ckpt,net", [("host", False), ("measured", False), ("none", True), ("measured", True),
+                                      ("hbm", True)])
+@pytest.mark.parametrize("scheme,policy", [("yarn", "dlas-gpu"), ("tiresias", "gittins"),
+                                           ("count", "dlas-gpu"), ("yarn", "fifo")])
+def test_native_priced_matches_python(ckpt, net, scheme, policy, tmp_path):
+    """PRICED replays (BASELINE config 1 with costs): checkpoint save /
+    restore stalls (host path, HBM residency with xGMI moves, the measured
+    MI355X bandwidth table) and the spread-gang network rate (measured
+    slowdowns for the profiled models, analytic all-reduce for the rest)
+    give the Python engine's per-job end times, preemption counts and
+    checkpoint overheads."""
+    specs = philly_like_trace(600, 64, load=1.3, seed=5, median_duration=500)
+    c = _topo_cfg(policy, scheme)
+    c.ckpt_policy = ckpt
+    c.enable_network_costs = net
+    c.ckpt_hbm_budget_gb = 2.0                 # small budget: both the resident and the host path
+    # measured 2-node slowdowns for two families; every other model takes
+    # the analytic all-reduce
+    prof = tmp_path / "skew.json"
+    prof.write_text('{"vgg16": {"slowdown": 1.7}, "resnet50": {"slowdown": 1.04}}')
+    c.skew_profile = str(prof)
+    prior = sorted(s.duration * s.num_gpu for s in philly_like_trace(600, 64, load=1.3, seed=98,
+                                                                     median_duration=500))
+    sim = Simulator(c, specs, prior=prior)
+    ps = sim.run()
+    ns = native.simulate_native(c, specs, prior=prior)
+    assert ns["priced"]
+    py_end = np.array([sim.jobs[s.job_id].end_time for s in specs], dtype=float)
+    py_pre = np.array([sim.jobs[s.job_id].preempt_count for s in specs])
+    py_ov = np.array([sim.jobs[s.job_id].overhead_time for s in specs], dtype=float)
+    assert ns["finished"] == ps["finished"]
+    np.testing.assert_array_equal(ns["per_job"]["preempt"], py_pre)
+    np.testing.assert_allclose(ns["per_job"]["end"], py_end, rtol=1e-9, atol=1e-6)
+    np.testing.assert_allclose(ns["per_job"]["overhead"], py_ov, rtol=1e-9, atol=1e-9)
+    if ckpt != "none" and policy != "fifo":
+        assert ns["ckpt_overhead_s"] > 0

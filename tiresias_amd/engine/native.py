@@ -43,7 +43,7 @@ def simulate_native(cfg: SimConfig, specs: List[JobSpec], prior: Optional[List[f
     scheme = cfg.scheme if cfg.scheme not in ("", "default") else "count"
     if scheme not in PLACEMENTS:
         raise ValueError(f"native core placements are {PLACEMENTS}, not {scheme}")
-    if cfg.pack or cfg.virtual_nodes or getattr(cfg, "gang_align", False):
+    if cfg.pack or cfg.virtual_nodes or getattr(cfg, "gang_align", False) or cfg.enable_migration:
         raise ValueError("native core: no GPU sharing, virtual nodes or gang alignment (use engine.sim)")
     limits = list(cfg.queue_limits) or default_limits(cfg.num_queue if cfg.num_queue > 1 else 2, 3600.0)
     # prior: same rules as engine/sim.py::Simulator._prior (history, never the future)
@@ -60,11 +60,12 @@ def simulate_native(cfg: SimConfig, specs: List[JobSpec], prior: Optional[List[f
     eng = _sched_core.Engine(cfg.schedule, cfg.cluster.num_gpus, [float(x) for x in limits],
                              float(cfg.solve_starvation), float(cfg.gittins_delta or 3250.0),
                              [float(x) for x in prior], online)
+    priced = _set_costs(eng, cfg, specs)
     t0 = time.perf_counter()
     sub_a = np.array([s.submit_time for s in specs], dtype=np.float64)
     dur_a = np.array([s.duration for s in specs], dtype=np.float64)
     gpu_a = np.array([s.num_gpu for s in specs], dtype=np.int32)
-    if scheme == "count":
+    if scheme == "count" and not priced:
         out = eng.run(sub_a, dur_a, gpu_a)
     else:
         c = cfg.cluster
@@ -84,6 +85,7 @@ def simulate_native(cfg: SimConfig, specs: List[JobSpec], prior: Optional[List[f
                            np.array([s.cpu_per_task for s in specs], dtype=np.int32),
                            np.array([s.mem_per_task for s in specs], dtype=np.int32), sens)
     wall = time.perf_counter() - t0
+    cost = eng.costs() if priced else None
     sub = np.array([s.submit_time for s in specs])
     end, start = out["end"], out["start"]
     done = end >= 0
@@ -96,4 +98,51 @@ def simulate_native(cfg: SimConfig, specs: List[JobSpec], prior: Optional[List[f
                 avg_queueing_delay=float((start - sub)[done].mean()) if done.any() else 0.0,
                 preemptions=int(out["preempt"].sum()), promotions=int(out["promote"].sum()),
                 events=int(out["events"]), wall_s=wall, schedule=cfg.schedule, scheme=scheme, prior=source,
-                per_job={"start": start, "end": end, "preempt": out["preempt"]})
+                priced=priced,
+                ckpt_overhead_s=float(cost["overhead"].sum()) if cost is not None else 0.0,
+                ckpt_gb=float(cost["ckpt_bytes"].sum() / 1e9) if cost is not None else 0.0,
+                per_job={"start": start, "end": end, "preempt": out["preempt"],
+                         **({"overhead": cost["overhead"], "ckpt_bytes": cost["ckpt_bytes"]}
+                            if cost is not None else {})})
+
+
+CKPT_MODE = {"none": 0, "host": 1, "hbm": 2, "measured": 2, "pressure": 2}
+
+
+def _set_costs(eng, cfg: SimConfig, specs: List[JobSpec]) -> bool:
+    """Price the replay like the Python engine: the per-job parameters of
+    engine/sim.py::Simulator._rate (measured 2-node slowdown, else the
+    analytic all-reduce over the link) and engine/ckpt_model.py (state bytes
+    per GPU, bandwidths -- the measured table for ckpt_policy=measured).
+    Returns whether any cost is on."""
+    net = bool(cfg.enable_network_costs)
+    mode = CKPT_MODE.get(cfg.ckpt_policy)
+    if mode is None:
+        raise ValueError(f"native core: unsupported ckpt_policy {cfg.ckpt_policy}")
+    if not net and mode == 0:
+        return False
+    from ..core.job import Job
+    from ..profiler.skew import SensitivityOracle, model_profile
+    from .ckpt_model import CkptCostModel
+
+    ck = CkptCostModel(cfg.ckpt_policy, cfg.ckpt_bw_gbps, cfg.ckpt_hbm_budget_gb,
+                       table_path=cfg.ckpt_table if cfg.ckpt_policy == "measured" else "")
+    oracle = SensitivityOracle(cfg.skew_threshold, measured_path=cfg.skew_profile)
+    ckpt_b, sd, it_s, nbytes = [], [], [], []
+    for s in specs:
+        j = Job(s)
+        ckpt_b.append(float(ck.state_bytes_per_gpu(j)))
+        m = s.model or ""
+        v = oracle.slowdown(m)
+        sd.append(float(v) if v is not None else -1.0)
+        # cluster/network.py::network_rate's inputs
+        try:
+            mb = model_profile(m).total_mb if m else 100.0
+        except KeyError:
+            mb = 100.0
+        it_s.append(s.duration / s.iterations if s.iterations and s.iterations > 0 else 0.25)
+        nbytes.append(mb * 2 ** 20)
+    c = cfg.cluster
+    eng.set_costs(net, float(c.bandwidth_mbps), float(c.internode_latency), mode, float(ck.host_gbps),
+                  float(ck.h2d_gbps), float(ck.xgmi_gbps), float(ck.budget), ckpt_b, sd, it_s, nbytes)
+    return True

@@ -1285,19 +1285,24 @@ class Worker:
         if cuda:
             torch.cuda.synchronize(self.device)
         dt = time.perf_counter() - t0
+        persist_err: Dict[str, str] = {}
         if cuda:
-            persist = [jid for jid, _ in jobs if self.trainers[jid].uses_persist]
-            if persist:
-                from ..models.gnmt import device_timeouts
-
-                # the persistent LSTM kernels never hang: a grid barrier that
-                # timed out set a sticky device counter -- read once per round
-                n_to = device_timeouts(reset=True)
-                if n_to:
-                    for jid in persist:
-                        self.trainers[jid].disable_persist()
-                    err = (f"PersistTimeout: {n_to} persistent LSTM barrier timeout(s) this round; "
-                           f"jobs {persist} fall back to the per-step recurrence")
+            # the persistent LSTM kernels never hang: a grid barrier that timed
+            # out bumped the JOB's own timeout word, its optimizer skipped that
+            # step's update and counted it -- read once per round, per job: the
+            # skipped steps are not progress, and only that job falls back to
+            # the per-step recurrence
+            fixed = []
+            for jid, n in jobs:
+                t = self.trainers[jid]
+                sk = t.persist_skipped(reset=True) if t.uses_persist else 0
+                if sk:
+                    t.disable_persist()
+                    persist_err[jid] = (f"PersistTimeout: {sk} step(s) of job {jid} hit a persistent LSTM "
+                                        f"barrier timeout (update skipped); it falls back to the per-step "
+                                        f"recurrence")
+                fixed.append((jid, max(0, n - sk)))
+            jobs = fixed
         if len(jobs) == 1 and err is None:
             t = self.trainers[jobs[0][0]]
             if t.ddp is not None and comm_failed(t.group):
@@ -1328,8 +1333,8 @@ class Worker:
                 ct = t.ddp.poll_timing()
                 if ct["steps"]:
                     rep["comm"] = ct
-            if err:
-                rep["error"] = err
+            if err or jid in persist_err:
+                rep["error"] = err or persist_err[jid]
             reps.append(rep)
         return {"rank": self.rank, "job": jobs[0][0], "jobs": reps + skipped, "dev": self._dev_sample(),
                 "ckpt": self._ckpt_report(), "snap": self.snap.poll() if self.snap else None}

@@ -134,9 +134,9 @@ class Trainer:
             w, g, wb = A.master[lo:hi], A.grad[lo:hi], A.shadow[lo:hi]
             if self.device.type == "cuda":
                 T = _lib.ops()
-                # GNMT: a step whose persistent recurrence timed out (device
-                # counter) only resets the gradient -- no weight update
-                guard = self.uses_persist
+                # GNMT: a step whose persistent recurrence timed out (this
+                # job's own timeout word) only resets the gradient
+                guard = self.model.err if self.uses_persist else None
                 if self.opt == "sgd":
                     T.sgd_step(w, g, self.opt_state[0][lo:hi], wb, self.lr, 0.9, wd, gscale, False, True, guard)
                 else:
@@ -144,6 +144,9 @@ class Trainer:
                                 0.9, 0.98, 1e-9, wd, self.step_count, gscale, True, guard)
             else:
                 _cpu_opt(self.opt, w, g, self.opt_state, lo, hi, wb, self.lr, wd, gscale, self.step_count)
+        if self.uses_persist:
+            # a guarded step -> the job's skipped-step count (persist_skipped)
+            _lib.ops().lstm_guard_step(self.model.err)
 
     def enable_graph(self) -> None:
         """Turn hipGraph capture on for a trainer built without it (a pooled
@@ -162,6 +165,17 @@ class Trainer:
         """The model runs the persistent-grid LSTM kernels (GNMT)."""
         return self.device.type == "cuda" and bool(getattr(self.model, "persist", False))
 
+    def persist_skipped(self, reset: bool = True) -> int:
+        """Steps of THIS job whose persistent recurrence timed out since the
+        last reset (their weight update was skipped; they are not progress).
+        A host read: call after the round's synchronize."""
+        if not self.uses_persist:
+            return 0
+        n = int(self.model.err[1].item())
+        if reset and n:
+            self.model.err.zero_()
+        return n
+
     def disable_persist(self) -> None:
         """After a persistent-barrier timeout: the per-step recurrence for the
         rest of the job (a captured graph baked the persistent kernels in, so
@@ -173,10 +187,11 @@ class Trainer:
 
     def step(self) -> torch.Tensor:
         if self.uses_persist:
-            # co-residency rule of the persistent grids (lstm.hip): a DDP
-            # gang's RCCL kernels run next to the recurrence -> keep CUs free
-            # for them; a 1-GPU job may share its GPU with one more grid
-            _lib.ops().lstm_seq_residency(1 if self.ddp is not None else 2, 64 if self.ddp is not None else 0)
+            # co-residency rule of THIS job's persistent grids (lstm.hip,
+            # passed with every launch): a DDP gang's RCCL kernels run next to
+            # the recurrence -> keep CUs free for them; a 1-GPU job may share
+            # its GPU with one more grid
+            self.model.residency = (1, 64) if self.ddp is not None else (2, 0)
         if self._ready is not None:
             torch.cuda.current_stream(self.device).wait_event(self._ready)
             self._ready = None

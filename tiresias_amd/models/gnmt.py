@@ -79,7 +79,11 @@ def device_timeouts(reset: bool = True) -> int:
 
 class _LSTMLayer(Function):
     @staticmethod
-    def forward(ctx, x, token, w_ih: Param, w_hh: Param, b: Param, reverse: bool, persist: bool = True):
+    def forward(ctx, x, token, w_ih: Param, w_hh: Param, b: Param, reverse: bool, m=None):
+        # m: the owning model (GNMT) -- its persist flag, its own timeout
+        # word (err) and its co-residency rule (residency) go with every
+        # persistent launch; None: persistent with the process defaults
+        persist = m.persist if m is not None else True
         T, B, I = x.shape
         Hd = w_hh.shape[1]
         dev = x.device
@@ -93,7 +97,8 @@ class _LSTMLayer(Function):
             _T().gemm(x2, True, w_ih.w, True, G, 0, b.w, False, None, 1.0, False)
             Gv = G.view(T, B, 4 * Hd)
             sy = _sync(dev, B)
-            ran = PERSIST and persist and _ran(_T().lstm_seq_forward(Gv, w_hh.w, Hs, Cs, act, reverse, sy), sy)
+            ran = PERSIST and persist and _ran(_T().lstm_seq_forward(Gv, w_hh.w, Hs, Cs, act, reverse, sy,
+                                                                     *_pl_args(m)), sy)
             steps = [] if ran else steps
             prev = None
             # the fused per-timestep kernel (lstm_step_forward) ties GEMM + cell +
@@ -129,13 +134,14 @@ class _LSTMLayer(Function):
                 act[t] = torch.cat([i, f, gg, o, tc], 1)
                 prev = t
         ctx.save_for_backward(x, Hs, Cs, act)
-        ctx.p = (w_ih, w_hh, b, reverse, persist)
+        ctx.p = (w_ih, w_hh, b, reverse, m)
         return Hs
 
     @staticmethod
     def backward(ctx, dH):
         x, Hs, Cs, act = ctx.saved_tensors
-        w_ih, w_hh, b, reverse, persist = ctx.p
+        w_ih, w_hh, b, reverse, m = ctx.p
+        persist = m.persist if m is not None else True
         T, B, I = x.shape
         Hd = Hs.shape[2]
         dev = x.device
@@ -147,7 +153,7 @@ class _LSTMLayer(Function):
             # the persistent kernel reads dH as it comes (bf16); only the
             # per-step path needs the fp32 accumulator it updates in place
             ran = PERSIST and persist and _ran(
-                _T().lstm_seq_backward(act, Cs, dH.contiguous(), w_hh.w, dG, reverse, sy), sy)
+                _T().lstm_seq_backward(act, Cs, dH.contiguous(), w_hh.w, dG, reverse, sy, *_pl_args(m)), sy)
             if not ran:                            # per-step path: cell-state gradient carry
                 dHf = dH.float().contiguous()
                 dc = torch.zeros(B, Hd, dtype=torch.float32, device=dev)
@@ -217,9 +223,17 @@ class _LSTMLayer(Function):
         return dx, None, None, None, None, None, None
 
 
-def lstm(x, p, reverse=False, persist=True):
+def _pl_args(m):
+    """(job_err, grids, reserved_cus) of a persistent launch for model m."""
+    if m is None:
+        return (None, -1, 0)
+    g, r = m.residency
+    return (m.err if (m.err is not None and m.err.is_cuda) else None, g, r)
+
+
+def lstm(x, p, reverse=False, model=None):
     """x: [T,B,I] bf16 -> [T,B,H] bf16."""
-    return _LSTMLayer.apply(x.contiguous(), p[0].arena.token, p[0], p[1], p[2], reverse, persist)
+    return _LSTMLayer.apply(x.contiguous(), p[0].arena.token, p[0], p[1], p[2], reverse, model)
 
 
 class GNMT:
@@ -231,7 +245,7 @@ class GNMT:
     # hipGraph step 15.5 ms one stream vs 16.3 ms with branches
     branch_default = False
     # whole-sequence persistent recurrences; off for the rest of the job
-    # after a barrier timeout (Trainer.check_device_errors)
+    # after a barrier timeout (Worker.run reads the job's own err words)
     persist = True
 
     def __init__(self, arena: Arena, vocab: int = 32000, hidden: int = 1024, enc_layers: int = 4,
@@ -256,6 +270,12 @@ class GNMT:
         self.cls_w = A.add("cls.w", (vocab, 2 * H), init="uniform", std=0.1)
         self.cls_b = A.add("cls.b", (vocab,), init="zeros", decay=False)
         self.training = True
+        # this job's persistent-LSTM words: [0] barrier timeouts of the current
+        # step (the optimizer's guard), [1] steps whose update was skipped
+        self.err = torch.zeros(2, dtype=torch.int32, device=arena.device)
+        # co-residency rule of this job's persistent grids (grids that must
+        # fit at once, CUs reserved for RCCL): set by the trainer per job
+        self.residency = (2, 0)
 
     def forward(self, batch):
         src, tgt_in = batch["src"], batch["tgt_in"]       # [B,S] token ids
@@ -267,16 +287,16 @@ class GNMT:
         tgt_t = tgt_in.t().contiguous()
         with Fx.on_branch(1, tgt_t):
             y = Fx.embedding(tgt_t, self.tgt_emb)
-            d0 = lstm(y, self.dec[0], persist=self.persist)                    # [T,B,H]
+            d0 = lstm(y, self.dec[0], model=self)                    # [T,B,H]
             q = Fx.linear(d0.transpose(0, 1).contiguous(), self.att_q)   # [B,T,H]
         x = Fx.embedding(src.t().contiguous(), self.src_emb)
         with Fx.on_branch(0, x):
-            bw = lstm(x, self.enc[1], reverse=True, persist=self.persist)
-        fw = lstm(x, self.enc[0], persist=self.persist)
+            bw = lstm(x, self.enc[1], reverse=True, model=self)
+        fw = lstm(x, self.enc[0], model=self)
         bw = Fx.join_branch(0, bw)
-        h = lstm(torch.cat([fw, bw], 2), self.enc[2], persist=self.persist)
+        h = lstm(torch.cat([fw, bw], 2), self.enc[2], model=self)
         for i, p in enumerate(self.enc[3:]):
-            o = lstm(h, p, persist=self.persist)
+            o = lstm(h, p, model=self)
             h = Fx.add(h, o) if i >= 0 else o          # residual from layer 3 on
         mem = h.transpose(0, 1).contiguous()             # [B,S,H]
         kv = Fx.linear(mem, self.att_kv)                 # [B,S,2H]
@@ -284,7 +304,7 @@ class GNMT:
         ctxv = Fx.cross_attention(q, kv, self.heads).transpose(0, 1).contiguous()  # [T,B,H]
         h = d0
         for i, p in enumerate(self.dec[1:]):
-            o = lstm(torch.cat([h, ctxv], 2), p, persist=self.persist)
+            o = lstm(torch.cat([h, ctxv], 2), p, model=self)
             h = Fx.add(h, o) if i >= 1 else o
         out = torch.cat([h, ctxv], 2).transpose(0, 1).contiguous()   # [B,T,2H]
         return Fx.linear(out, self.cls_w, self.cls_b)

@@ -663,3 +663,63 @@ def as_comm(group):
     if group is None or isinstance(group, (FlatComm, HierComm)):
         return group
     return FlatComm(_PlainPG(group), tuple(range(dist.get_world_size(group))))
+
+
+def preflight(groups: Dict[Tuple[int, ...], object], my_rank: int, device: torch.device, world_pg=None,
+              ctrl_pg=None, timeout_s: float = 60.0, numel: int = 1 << 16) -> List[str]:
+    """Communicator pre-flight before a timed run (bench.py at N > 1): an
+    all-reduce of KNOWN values (rank r contributes r + 1 everywhere) on the
+    world communicator and on every gang communicator this rank belongs to
+    (``groups``: rank set -> FlatComm / HierComm, e.g. the pre-created
+    canonical gangs), each result checked exactly, the whole pass bounded by
+    ``timeout_s`` (a member that never joins reads as a timeout, not a
+    hang). Every rank learns every rank's verdict over ``ctrl_pg`` (gloo:
+    host-only, independent of the communicators under test). Returns the
+    failures (empty: all good), each naming its rank set."""
+    errs: List[str] = []
+    done = threading.Event()
+
+    def _check(name, ranks, run):
+        t = torch.full((numel,), float(my_rank + 1), dtype=torch.float32, device=device)
+        run(t)
+        want = float(sum(r + 1 for r in ranks))
+        got = t.cpu()
+        if not bool(torch.all(got == want)):
+            bad = got[got != want]
+            errs.append(f"{name} {tuple(ranks)}: expected {want}, got {float(bad[0])} "
+                        f"({bad.numel()} of {numel} elements wrong)")
+
+    def _body():
+        try:
+            if world_pg is not None:
+                n = dist.get_world_size(world_pg)
+                _check("world", range(n), lambda t: dist.all_reduce(t, group=world_pg))
+            for ranks in sorted(groups):
+                c = groups[ranks]
+                if c is None or my_rank not in ranks or isinstance(c, FailedComm):
+                    if isinstance(c, FailedComm):
+                        errs.append(f"gang {tuple(ranks)}: communicator creation failed ({c.why})")
+                    continue
+
+                def run(t, c=c):
+                    c.finish([c.start(t)])
+                    if t.is_cuda:
+                        torch.cuda.synchronize(t.device)
+
+                _check("gang", ranks, run)
+        except Exception as e:                       # a collective error names its set
+            errs.append(f"preflight error: {type(e).__name__}: {e}")
+        finally:
+            done.set()
+
+    th = threading.Thread(target=_body, name="tam-preflight", daemon=True)
+    th.start()
+    if not done.wait(timeout_s):
+        errs.append(f"rank {my_rank}: preflight timed out after {timeout_s:.0f} s "
+                    f"(world / gangs {sorted(r for r in groups if my_rank in r)})")
+    if ctrl_pg is not None:
+        # every rank's verdict to every rank (so all of them stop, or none)
+        out: List[Optional[List[str]]] = [None] * dist.get_world_size(ctrl_pg)
+        dist.all_gather_object(out, [f"rank {my_rank}: {e}" for e in errs], group=ctrl_pg)
+        errs = [e for lst in out for e in (lst or [])]
+    return errs

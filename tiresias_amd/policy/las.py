@@ -183,11 +183,21 @@ class DLAS(Policy):
                 if left > 0:
                     t = min(t, now + left)
             if self.gittins is not None and j.is_running:
-                d = self.gittins.delta
-                a = j.attained(g)
-                nxt = (math.floor(a / d + 1e-6) + 1) * d
-                t = min(t, now + (nxt - a) / (j.num_gpu if g else 1))
+                t = min(t, now + _quantum_wait(j.attained(g), self.gittins.delta, j.num_gpu if g else 1, now))
         return t
+
+
+def _quantum_wait(a: float, d: float, div: float, now: float) -> float:
+    """Wall seconds until attained service ``a`` (accruing at ``div`` per
+    second) reaches the next Gittins quantum boundary. A boundary closer than
+    the event clock's tolerance (1e-9 x now: the engine snaps such events to
+    now, where no service accrues) counts as reached -- else a long replay
+    with a wide gang stalls on it (csrc/sched_core/engine.h::quantum_wait is
+    the same rule)."""
+    w = ((math.floor(a / d + 1e-6) + 1) * d - a) / div
+    if w <= 1e-9 * max(1.0, now):
+        w += d / div
+    return w
 
 
 @register("gittins")
@@ -215,9 +225,7 @@ class Gittins(Policy):
         t = INF
         for j in active:
             if j.is_running:
-                a = j.attained(True)
-                nxt = (math.floor(a / self.delta + 1e-6) + 1) * self.delta
-                t = min(t, now + (nxt - a) / j.num_gpu)
+                t = min(t, now + _quantum_wait(j.attained(True), self.delta, j.num_gpu, now))
         return t
 
 
