@@ -398,13 +398,14 @@ def main():
         finally:
             gc.enable()
         dt = time.perf_counter() - t
-        replay_diag.append({"policy": f"{c.schedule}+{c.scheme}", "avg_jct": round(r["avg_jct"], 4),
-                            "makespan": round(r["makespan"], 4), "wall_s": round(dt, 3),
-                            "gc_ms": round(gc_ms[0], 2),
-                            "pool_evictions": worker.pool_evictions - ev0[0],
-                            "pressure_spills": worker.pressure_spills - ev0[1],
-                            "pool_hits": worker.pool_hits - ev0[2],
-                            "breakdown": r.get("runtime_breakdown")})
+        if r is not None:              # (the controller's summary lives on rank 0)
+            replay_diag.append({"policy": f"{c.schedule}+{c.scheme}", "avg_jct": round(r["avg_jct"], 4),
+                                "makespan": round(r["makespan"], 4), "wall_s": round(dt, 3),
+                                "gc_ms": round(gc_ms[0], 2),
+                                "pool_evictions": worker.pool_evictions - ev0[0],
+                                "pressure_spills": worker.pressure_spills - ev0[1],
+                                "pool_hits": worker.pool_hits - ev0[2],
+                                "breakdown": r.get("runtime_breakdown")})
         if rank == 0:                  # progress on stderr (the JSON line stays alone on stdout)
             print(f"[bench] {c.schedule}+{c.scheme}{' share' if c.pack else ''}: avg JCT "
                   f"{r['avg_jct']:.4f} s, makespan {r['makespan']:.3f} s, {r['finished']} jobs, "

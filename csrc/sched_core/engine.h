@@ -84,6 +84,36 @@ struct Gittins {
   }
 };
 
+// E[remaining service | attained a] over a service sample (GPU-seconds):
+// engine/spread.py::ServiceEstimate (same rebuild rule when learned online)
+struct ServiceEst {
+  std::vector<double> raw, d, pre{0.0};
+  size_t next = 0;
+  void init(const std::vector<double>& s) {
+    raw = s;
+    if (!raw.empty()) build();
+  }
+  void build() {
+    d = raw;
+    std::sort(d.begin(), d.end());
+    pre.assign(1, 0.0);
+    for (double x : d) pre.push_back(pre.back() + x);
+    next = std::max(d.size() + 1, (size_t)((double)d.size() * 1.1));
+  }
+  void add(double s) {
+    raw.push_back(s);
+    if (raw.size() >= next) build();
+  }
+  bool empty() const { return d.empty(); }
+  double remaining(double a) const {
+    const size_t n = d.size();
+    const size_t i = std::upper_bound(d.begin(), d.end(), a) - d.begin();
+    const size_t alive = n - i;
+    if (alive == 0) return std::max(a, pre[n] / (double)n);
+    return (pre[n] - pre[i]) / (double)alive - a;
+  }
+};
+
 enum Pol { FIFO, FJF, SJF, SRTF, SRSF, DLAS, DLASG, DLASGG, GITT };
 // P_COUNT: flat GPU pool; P_FILL: "count" on the topology (placement/
 // schemes.py::CountPlacement: tasks filled node by node in id order) -- used
@@ -166,8 +196,16 @@ class Engine {
         online_(online_prior) {
     std::sort(limits_.begin(), limits_.end());
     nq_ = (int)limits_.size() + 1;
+    svc_online_ = prior.empty();
+    svc_init_ = prior;
     if (pol_ == DLASGG || pol_ == GITT) git_.init(std::move(prior), gittins_delta);
   }
+
+  // tiresias placement, insensitive gangs: false = fragments first (spread
+  // whenever no consolidated block is free), true = wait-vs-spread
+  // (engine/spread.py; needs set_costs' per-job spread parameters)
+  void set_spread_wait(bool on) { spread_wait_ = on; }
+  long spread_decisions(bool spread) const { return spread ? n_spread_ : n_wait_; }
 
   // Topology placement (yarn / tiresias) on switches x nodes x gpus with
   // per-node CPU / memory; per-job task shape and sensitivity are passed to
@@ -221,6 +259,11 @@ class Engine {
         throw std::invalid_argument("sched_core: set_costs arrays must match the run's job count");
     }
     resident_.clear();
+    svc_ = ServiceEst();
+    svc_.init(svc_init_);
+    n_spread_ = n_wait_ = 0;
+    if (spread_wait_ && place_ == P_TIRESIAS && (long)net_sd_.size() != n)
+      throw std::invalid_argument("sched_core: the wait spread rule needs set_costs' per-job arrays");
     if (place_ != P_COUNT) {
       for (int k = 0; k < topo_.nodes(); ++k) {
         std::fill(topo_.busy[k].begin(), topo_.busy[k].end(), 0);
@@ -361,6 +404,7 @@ class Engine {
         used_ -= j.gpu;
         release(j);
         ckpt_finish(j);
+        if (svc_online_) svc_.add(j.total_exec * j.gpu);
         if (online_ && (pol_ == DLASGG || pol_ == GITT)) git_.add(j.total_exec * j.gpu);
         active_.erase(active_.begin() + a);
       } else {
@@ -696,7 +740,88 @@ class Engine {
       if ((fa == 0) != (fb == 0)) return fa != 0;
       return fa != fb ? fa < fb : a < b;
     });
-    return fill(j, order, plan);
+    if (!spread_wait_) return fill(j, order, plan);
+    // wait-vs-spread (placement/schemes.py::TiresiasPlacement._exclusive)
+    if (j.gpu <= gpn) {
+      std::vector<int> best = all;
+      std::stable_sort(best.begin(), best.end(), [&](int a, int b) {
+        const int fa = topo_.nfree(a), fb = topo_.nfree(b);
+        return fa != fb ? fa < fb : a < b;
+      });
+      if (single_node(j, best, plan)) return true;
+    }
+    if (!fill(j, order, plan)) return false;
+    std::vector<int> nd;
+    for (size_t p = 0; p < plan.size(); p += 1 + j.tgpu) nd.push_back(plan[p]);
+    std::sort(nd.begin(), nd.end());
+    const int k = (int)(std::unique(nd.begin(), nd.end()) - nd.begin());
+    const int min_nodes = std::max(1, (j.gpu + gpn - 1) / gpn);
+    if (k <= min_nodes || should_spread(j, k, min_nodes)) return true;
+    plan.clear();
+    return false;
+  }
+
+  // engine/spread.py::SpreadAdvisor (the engine's remaining-wall / rate rules)
+  bool remaining_wall(const Job& j, double& out) const {
+    if (svc_.empty()) return false;
+    const double rem = svc_.remaining(j.attained(true));
+    const double r = (j.state == RUN && j.rate > 0) ? j.rate : 1.0;
+    out = rem / std::max(1, j.gpu) / r + (j.state == RUN ? j.restore_left : 0.0);
+    return true;
+  }
+  double wait_for_block(const Job& j, int min_nodes) const {
+    const int N = topo_.nodes(), gpn = topo_.gpn;
+    std::vector<std::vector<std::pair<double, int>>> per(N);
+    for (long k : active_) {
+      const Job& r = jobs_[k];
+      if (r.state != RUN || r.plan.empty()) continue;
+      double rem = 0;
+      remaining_wall(r, rem);
+      std::vector<int> cnt(N, 0);
+      size_t p = 0;
+      for (int t = 0; t < r.ntask; ++t) { cnt[r.plan[p]] += r.tgpu; p += 1 + r.tgpu; }
+      for (int nd = 0; nd < N; ++nd) if (cnt[nd]) per[nd].emplace_back(rem, cnt[nd]);
+    }
+    const bool whole = j.gpu > gpn;
+    std::vector<double> times;
+    for (int nd = 0; nd < N; ++nd) {
+      if (whole) {
+        double m = 0.0;
+        for (const auto& e : per[nd]) m = std::max(m, e.first);
+        times.push_back(m);
+        continue;
+      }
+      if (gpn < j.gpu) continue;
+      int free = topo_.nfree(nd);
+      double t = 0.0;
+      std::sort(per[nd].begin(), per[nd].end());
+      for (const auto& e : per[nd]) {
+        if (free >= j.gpu) break;
+        free += e.second;
+        t = e.first;
+      }
+      if (free >= j.gpu) times.push_back(t);
+    }
+    if (whole) {
+      std::sort(times.begin(), times.end());
+      return (int)times.size() >= min_nodes ? times[min_nodes - 1] : INF;
+    }
+    double m = INF;
+    for (double t : times) m = std::min(m, t);
+    return m;
+  }
+  bool should_spread(const Job& j, int k, int min_nodes) const {
+    const double r_k = spread_rate(j, k), r_min = spread_rate(j, min_nodes);
+    double rem = 0;
+    bool ok;
+    if (!remaining_wall(j, rem) || r_k <= 0) {
+      ok = true;
+    } else {
+      const double penalty = (1.0 / r_k - 1.0 / std::max(r_min, 1e-9)) * rem;
+      ok = wait_for_block(j, min_nodes) > penalty;
+    }
+    ++(ok ? n_spread_ : n_wait_);
+    return ok;
   }
 
   void schedule() {
@@ -727,6 +852,10 @@ class Engine {
   Pol pol_;
   Place place_ = P_COUNT;
   Costs costs_;
+  bool spread_wait_ = false, svc_online_ = true;
+  std::vector<double> svc_init_;
+  ServiceEst svc_;
+  mutable long n_spread_ = 0, n_wait_ = 0;
   std::vector<double> ckpt_b_, net_sd_, net_c_, net_bytes_;
   std::map<std::pair<int, int>, double> resident_;   // (node, device) -> suspended state bytes
   Topo topo_;

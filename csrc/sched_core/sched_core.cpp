@@ -114,6 +114,8 @@ PYBIND11_MODULE(_sched_core, m) {
            py::arg("budget_bytes"), py::arg("ckpt_bytes"), py::arg("net_slowdown"), py::arg("net_iter_s"),
            py::arg("net_bytes"))
       .def("costs", &costs_py)
+      .def("set_spread_wait", &Engine::set_spread_wait, py::arg("on"))
+      .def("spread_decisions", &Engine::spread_decisions, py::arg("spread"))
       .def("run_topo", &run_topo_py, py::arg("submit"), py::arg("duration"), py::arg("gpus"),
            py::arg("gpu_per_worker"), py::arg("cpu_per_task"), py::arg("mem_per_task"), py::arg("sensitive"));
 }

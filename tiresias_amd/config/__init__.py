@@ -86,6 +86,9 @@ def define_flags() -> None:
     D.DEFINE_string("gandiva_mem_util", "one", "gandiva-ns job slot size: one|legacy|measured")
     D.DEFINE_boolean("replace_all", False, "re-place every runnable job at each event (legacy Tiresias)")
     D.DEFINE_float("skew_threshold", 0.5, "placement-sensitivity threshold (largest tensor / total)")
+    D.DEFINE_string("spread_rule", "wait", "tiresias placement, insensitive gangs: fragments (spread "
+                    "whenever no consolidated block is free) | wait (spread only when the expected wait "
+                    "for a block exceeds the spread penalty, engine/spread.py)")
     D.DEFINE_string("throughput_table", "", "json of measured per-model iteration times (MI355X)")
     D.DEFINE_integer("max_jobs", 0, "truncate the trace (0 = all)")
     D.DEFINE_integer("debug_kernels", 0, "kernel debug mode (utils/debug.py): 1 synchronous launches "
@@ -171,6 +174,7 @@ class SimConfig:
     gandiva_mem_util: str = "one"
     replace_all: bool = False
     skew_threshold: float = 0.5
+    spread_rule: str = "wait"          # tiresias placement: wait | fragments (engine/spread.py)
     virtual_nodes: str = ""
     nic_gbps: float = 12.5            # emulated inter-virtual-node link per GPU (GB/s)
     skew_profile: str = ""            # measured consolidated-vs-spread slowdowns (profiler/comm.py)

@@ -60,7 +60,9 @@ def simulate_native(cfg: SimConfig, specs: List[JobSpec], prior: Optional[List[f
     eng = _sched_core.Engine(cfg.schedule, cfg.cluster.num_gpus, [float(x) for x in limits],
                              float(cfg.solve_starvation), float(cfg.gittins_delta or 3250.0),
                              [float(x) for x in prior], online)
-    priced = _set_costs(eng, cfg, specs)
+    wait_rule = scheme == "tiresias" and getattr(cfg, "spread_rule", "wait") == "wait"
+    priced = _set_costs(eng, cfg, specs, force=wait_rule)
+    eng.set_spread_wait(wait_rule)
     t0 = time.perf_counter()
     sub_a = np.array([s.submit_time for s in specs], dtype=np.float64)
     dur_a = np.array([s.duration for s in specs], dtype=np.float64)
@@ -109,17 +111,19 @@ def simulate_native(cfg: SimConfig, specs: List[JobSpec], prior: Optional[List[f
 CKPT_MODE = {"none": 0, "host": 1, "hbm": 2, "measured": 2, "pressure": 2}
 
 
-def _set_costs(eng, cfg: SimConfig, specs: List[JobSpec]) -> bool:
+def _set_costs(eng, cfg: SimConfig, specs: List[JobSpec], force: bool = False) -> bool:
     """Price the replay like the Python engine: the per-job parameters of
     engine/sim.py::Simulator._rate (measured 2-node slowdown, else the
     analytic all-reduce over the link) and engine/ckpt_model.py (state bytes
     per GPU, bandwidths -- the measured table for ckpt_policy=measured).
+    ``force``: hand over the per-job spread parameters even when nothing is
+    charged (the wait-vs-spread placement rule estimates with them).
     Returns whether any cost is on."""
     net = bool(cfg.enable_network_costs)
     mode = CKPT_MODE.get(cfg.ckpt_policy)
     if mode is None:
         raise ValueError(f"native core: unsupported ckpt_policy {cfg.ckpt_policy}")
-    if not net and mode == 0:
+    if not net and mode == 0 and not force:
         return False
     from ..core.job import Job
     from ..profiler.skew import SensitivityOracle, model_profile
@@ -145,4 +149,4 @@ def _set_costs(eng, cfg: SimConfig, specs: List[JobSpec]) -> bool:
     c = cfg.cluster
     eng.set_costs(net, float(c.bandwidth_mbps), float(c.internode_latency), mode, float(ck.host_gbps),
                   float(ck.h2d_gbps), float(ck.xgmi_gbps), float(ck.budget), ckpt_b, sd, it_s, nbytes)
-    return True
+    return net or mode != 0

@@ -37,16 +37,17 @@ import time
 from typing import Dict, List, Optional
 
 from ..cluster.interference import InterferenceModel
-from ..cluster.network import measured_spread_rate, network_rate
+from ..cluster.network import allreduce_seconds, measured_spread_rate, network_rate
 from ..cluster.topology import Cluster, PlacementError
 from ..config import SimConfig
 from ..core.job import Job, JobSpec, JobState
 from ..metrics.logger import MetricsLogger
 from ..placement.schemes import align_plan, make_placement
 from ..policy import make_policy
-from ..profiler.skew import SensitivityOracle
+from ..profiler.skew import SensitivityOracle, model_profile
 from ..trace.readers import StreamingReader
 from .ckpt_model import CkptCostModel
+from .spread import ServiceEstimate, SpreadAdvisor
 
 EPS = 1e-9
 PACK_SCHEMES = {"horus", "horus+", "gandiva", "pack"}
@@ -86,6 +87,18 @@ class Simulator:
                        if cfg.interference_table else InterferenceModel(cfg.interference))
         self.placement.model_of = lambda jid: self.jobs[jid].spec.model or ""
         self.placement.pair_cost = lambda a, b: self.interf.pair(a, b)
+        # service-time history for non-clairvoyant remaining-time estimates
+        # (the Gittins prior; learned from finished jobs when there is none)
+        prior_s = self._prior(specs, prior)
+        self._svc = ServiceEstimate(prior_s)
+        self._svc_online = not prior_s
+        # per-iteration seconds of a job (the live controller overrides it:
+        # its job durations are iteration counts)
+        self.iter_s_of = lambda j: (j.spec.duration / j.spec.iterations
+                                    if j.spec.iterations and j.spec.iterations > 0 else 0.25)
+        if scheme == "tiresias" and getattr(cfg, "spread_rule", "wait") == "wait":
+            self.placement.advisor = SpreadAdvisor(self._remaining_wall, self._spread_rate)
+            self.placement.jobs_by_id = self.jobs
         self.now = 0.0
         self.active: List[Job] = []
         self.finished: List[Job] = []
@@ -130,6 +143,37 @@ class Simulator:
         return j
 
     # ------------------------------------------------------------------ helpers
+    def _remaining_wall(self, j: Job) -> Optional[float]:
+        """Expected wall seconds job j still needs (engine/spread.py)."""
+        rem = self._svc.remaining(j.attained(True))
+        if rem is None:
+            return None
+        r = j.rate if (j.is_running and j.rate > 0) else 1.0
+        return rem / max(1, j.num_gpu) / r + (j.restore_left if j.is_running else 0.0)
+
+    def _spread_rate(self, j: Job, k: int) -> float:
+        """Progress rate of job j as a gang over k nodes: the measured 2-node
+        slowdown ring-scaled to k, else the analytic all-reduce over the
+        inter-node link (the emulated NIC with virtual nodes)."""
+        if k <= 1:
+            return 1.0
+        sd = self.oracle.slowdown(j.spec.model or "")
+        if sd is not None:
+            return measured_spread_rate(sd, k)
+        if self.cfg.virtual_nodes:           # the emulated NIC between virtual nodes
+            from ..parallel.gang import DEFAULT_NIC_LATENCY_S
+
+            bw, lat = getattr(self.cfg, "nic_gbps", 12.5) * 1000.0, DEFAULT_NIC_LATENCY_S
+        else:
+            bw, lat = self.cluster.spec.bandwidth_mbps, self.cluster.spec.internode_latency
+        try:
+            mb = model_profile(j.spec.model).total_mb if j.spec.model else 100.0
+        except KeyError:
+            mb = 100.0
+        c = self.iter_s_of(j)
+        comm = allreduce_seconds(mb * 2 ** 20, k, bw, lat)
+        return c / (c + comm) if c > 0 else 1.0
+
     def _rate(self, j: Job) -> float:
         r = 1.0
         nodes = self.cluster.nodes_of(j.job_id)
@@ -164,6 +208,8 @@ class Simulator:
     def _finish(self, j: Job) -> None:
         self.cluster.release(j)
         j.finish(self.now)
+        if self._svc_online:
+            self._svc.add(j.total_executed * j.num_gpu)
         self.ckpt.on_finish(j)
         self.policy.on_finish(j, self.now)
         self.active.remove(j)

@@ -155,6 +155,9 @@ class Controller:
         # with neither -- learned online from the jobs that finish (measured
         # wall seconds x GPUs). Never the replayed jobs' own (future) sizes.
         self.sched = LiveScheduler(cfg, specs, logger=logger, prior=prior)
+        # job durations here are iteration counts: the spread advisor needs
+        # seconds per iteration (measured, else nominal)
+        self.sched.iter_s_of = lambda j: self._iter_est(j.spec.model or "", j.num_gpu)
         self.sched.holders_of = lambda jid: self.holders.get(jid)
         self.world = world
         self.quantum = quantum

@@ -137,6 +137,10 @@ class Placement:
         self.model_of: Optional[Callable[[str], str]] = None
         self.pair_cost: Optional[Callable[[str, str], float]] = None
         self.share_max_slowdown = float("inf")
+        # set by the engine (engine/spread.py): wait-vs-spread advice for
+        # insensitive gangs, and the engine's job table it consults
+        self.advisor = None
+        self.jobs_by_id: Optional[Dict[str, Job]] = None
 
     def plan(self, cluster: Cluster, job: Job) -> Optional[Plan]:
         raise NotImplementedError
@@ -406,7 +410,24 @@ class TiresiasPlacement(Placement):
         # insensitive: fill fragments first (fewest free GPUs first), keep whole nodes
         order = sorted(cluster.nodes, key=lambda nid: (cluster.nodes[nid].num_free_gpus() == 0,
                                                       cluster.nodes[nid].num_free_gpus(), int(nid)))
-        return _fill(cluster, job, order)
+        if self.advisor is None:
+            return _fill(cluster, job, order)
+        # with wait-vs-spread advice (engine/spread.py): a gang that fits one
+        # node takes the best-fit node when one is free (no link time at
+        # all); otherwise the fragments, but only when the expected wait for
+        # a consolidated block exceeds what spreading costs it
+        if job.num_gpu <= gpn:
+            best = sorted(cluster.nodes, key=lambda nid: (cluster.nodes[nid].num_free_gpus(), int(nid)))
+            p = _single_node(cluster, job, best)
+            if p is not None:
+                return p
+        p = _fill(cluster, job, order)
+        if p is None:
+            return None
+        k = len({nid for nid, _ in p})
+        if k <= min_nodes or self.advisor.should_spread(cluster, job, self.jobs_by_id or {}, k, gpn, min_nodes):
+            return p
+        return None
 
 
 def _next_pow2(n: int) -> int:

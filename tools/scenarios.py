@@ -8,10 +8,12 @@ are VIRTUAL seconds (measured MI355X step times + the link model), not
 wall time on hardware: the 1-GPU box cannot run an 8-rank skew replay.
 
 For each seed: the same job set under Tiresias (skew-aware placement,
-consolidating placement-sensitive VGG-16 gangs) vs random placement vs YARN
-(always consolidate), all under 2D-LAS. Output: mean +- stdev over seeds.
+consolidating placement-sensitive VGG-16 gangs; ``tiresias+wait``: the
+same with the wait-vs-spread rule of engine/spread.py) vs random placement
+vs YARN (always consolidate), all under 2D-LAS. Output: mean +- stdev over
+seeds and the per-seed ratios.
 
-    python tools/scenarios_r3.py [--seeds 12] [--out profiles/r3/skew_fake_world8.json]
+    python tools/scenarios.py [--seeds 12] [--out profiles/r4/skew_fake_world8.json]
 """
 from __future__ import annotations
 
@@ -30,36 +32,45 @@ def main():
     ap.add_argument("--seeds", type=int, default=12)
     ap.add_argument("--world", type=int, default=8)
     ap.add_argument("--nic-gbps", type=float, default=12.5)
-    ap.add_argument("--out", default=os.path.join(ROOT, "profiles", "r3", "skew_fake_world8.json"))
+    ap.add_argument("--out", default=os.path.join(ROOT, "profiles", "r4", "skew_fake_world8.json"))
+    ap.add_argument("--schemes", default="tiresias+wait,tiresias,random,yarn")
     a = ap.parse_args()
     import bench
     from tiresias_amd.executor.fake import run_fake
 
     vn = f"2x{a.world // 2}"
     res = {}
-    for scheme in ("tiresias", "random", "yarn"):
-        res[scheme] = []
+    for name in a.schemes.split(","):
+        scheme, _, rule = name.partition("+")
+        res[name] = []
         for seed in range(1, a.seeds + 1):
             jobs = bench.scenario_trace("skew", a.world, seed)
             prior = bench.history_prior(bench.scenario_trace("skew", a.world, seed + bench.HISTORY_SEED_OFFSET))
             cfg = bench.make_cfg("dlas-gpu", scheme, a.world, seed, qlimits=[1.0], virtual_nodes=vn)
             cfg.nic_gbps = a.nic_gbps
+            cfg.spread_rule = rule or "fragments"
             s = run_fake(cfg, jobs, a.world, quantum=0.02, prior=prior)
-            res[scheme].append({"seed": seed, "avg_jct": s["avg_jct"], "makespan": s["makespan"],
+            res[name].append({"seed": seed, "avg_jct": s["avg_jct"], "makespan": s["makespan"],
                                 "preemptions": s["preemptions"], "p2p_gb": s["fake_stats"]["p2p_bytes"] / 1e9})
     out = {"what": f"fake backend, {a.world} ranks as virtual nodes {vn}, spread-gang link {a.nic_gbps} GB/s, "
                    "2D-LAS, mixed ResNet-50 / VGG-16 gangs (bench.py scenario 'skew'); VIRTUAL seconds",
            "seeds": a.seeds, "runs": res, "summary": {}}
-    base = [r["avg_jct"] for r in res["random"]]
+    base = [r["avg_jct"] for r in res["random"]] if "random" in res else None
     for scheme, rows in res.items():
         j = [r["avg_jct"] for r in rows]
         m = [r["makespan"] for r in rows]
-        ratio = [x / b for x, b in zip(j, base)]
+        ratio = [x / b for x, b in zip(j, base)] if base else [0.0, 0.0]
         out["summary"][scheme] = {"avg_jct_mean": round(statistics.fmean(j), 4),
                                   "avg_jct_stdev": round(statistics.stdev(j), 4),
                                   "makespan_mean": round(statistics.fmean(m), 4),
                                   "vs_random_mean": round(statistics.fmean(ratio), 4),
                                   "vs_random_stdev": round(statistics.stdev(ratio), 4)}
+    if "yarn" in res:
+        y = [r["avg_jct"] for r in res["yarn"]]
+        for scheme, rows in res.items():
+            per = [r["avg_jct"] / b for r, b in zip(rows, y)]
+            out["summary"][scheme]["vs_yarn_per_seed"] = [round(x, 4) for x in per]
+            out["summary"][scheme]["vs_yarn_mean"] = round(statistics.fmean(per), 4)
     print(json.dumps(out["summary"], indent=1))
     os.makedirs(os.path.dirname(a.out), exist_ok=True)
     with open(a.out, "w") as f:
