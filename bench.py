@@ -247,6 +247,10 @@ def main():
     ap.add_argument("--no-nopool-replay", action="store_true",
                     help="skip the extra untimed replay without the warm pool (cold-build JCT)")
     ap.add_argument("--out", default=None, help="directory for job.csv / summary.json of the last step")
+    ap.add_argument("--ddp-shard", action="store_true",
+                    help="gangs: reduce-scatter + sharded optimizer + bf16 shadow all-gather (parallel/ddp.py)")
+    ap.add_argument("--ddp-wire", default="fp32", choices=["fp32", "bf16"],
+                    help="sharded gangs: reduce-scatter wire dtype")
     ap.add_argument("--preflight-s", type=float, default=120.0,
                     help="N > 1: bound of the communicator pre-flight (world + every canonical gang)")
     a = ap.parse_args()
@@ -327,12 +331,14 @@ def main():
                      skew_profile=a.skew_profile,
                      gittins_delta=0.05 * (SEQ_SCALE if a.scenario == "seq" else 1))
         c.nic_gbps = a.nic_gbps
+        c.ddp_shard, c.ddp_wire = a.ddp_shard, a.ddp_wire
         return c
 
     cfg = make(a.policy, a.placement)
     worker = Worker(rank, world, device, world_pg, use_graph=use_cuda and not a.no_graph,
                     gang_backend="gloo" if shared_gpu else None,
-                    pool_cap=0 if a.no_pool else 2, hbm_budget_gb=a.hbm_budget_gb)
+                    pool_cap=0 if a.no_pool else 2, hbm_budget_gb=a.hbm_budget_gb,
+                    ddp_shard=a.ddp_shard, ddp_wire=a.ddp_wire)
     # per-process first-launch costs (kernel code objects, library handles),
     # paid once before the first replay like a cluster daemon's start-up
     prewarm_s = worker.prewarm(sorted({rj.model for rj in jobs})) if use_cuda and not a.no_prewarm else 0.0

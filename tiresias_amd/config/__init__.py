@@ -89,6 +89,9 @@ def define_flags() -> None:
     D.DEFINE_string("spread_rule", "wait", "tiresias placement, insensitive gangs: fragments (spread "
                     "whenever no consolidated block is free) | wait (spread only when the expected wait "
                     "for a block exceeds the spread penalty, engine/spread.py)")
+    D.DEFINE_boolean("ddp_shard", False, "live gangs: reduce-scatter + sharded optimizer + bf16 all-gather "
+                     "(consolidated on suspension)")
+    D.DEFINE_string("ddp_wire", "fp32", "sharded gangs: reduce-scatter wire dtype fp32 | bf16")
     D.DEFINE_string("throughput_table", "", "json of measured per-model iteration times (MI355X)")
     D.DEFINE_integer("max_jobs", 0, "truncate the trace (0 = all)")
     D.DEFINE_integer("debug_kernels", 0, "kernel debug mode (utils/debug.py): 1 synchronous launches "
@@ -175,6 +178,8 @@ class SimConfig:
     replace_all: bool = False
     skew_threshold: float = 0.5
     spread_rule: str = "wait"          # tiresias placement: wait | fragments (engine/spread.py)
+    ddp_shard: bool = False            # live gangs: sharded data parallelism (parallel/ddp.py)
+    ddp_wire: str = "fp32"             # sharded gangs: reduce-scatter dtype fp32 | bf16
     virtual_nodes: str = ""
     nic_gbps: float = 12.5            # emulated inter-virtual-node link per GPU (GB/s)
     skew_profile: str = ""            # measured consolidated-vs-spread slowdowns (profiler/comm.py)

@@ -44,7 +44,7 @@ from ..config import ClusterSpec, SimConfig
 from ..core.job import Job, JobSpec, JobState
 from ..engine.sim import Simulator
 from ..metrics.logger import MetricsLogger
-from ..parallel.gang import GangRegistry, abort_comm, comm_failed, create_gang_comm
+from ..parallel.gang import GangRegistry, abort_comm, comm_failed, create_gang_comm, vnode_parts
 from .trainer import Trainer
 
 # nominal per-iteration seconds on one MI355X (tools/bench_models.py,
@@ -174,6 +174,12 @@ class Controller:
         self.snapshots: Dict[str, Tuple[int, str]] = {}  # job -> (step, path) of its last durable snapshot
         self.from_snap: Dict[str, Tuple[int, str]] = {}  # jobs to restart from their snapshot
         self.snap_restored: set = set()
+        # sharded data parallelism (cfg.ddp_shard): gangs whose master /
+        # optimizer state is currently sharded across their members (from
+        # their start until the consolidate action of their suspension)
+        self.ddp_shard = bool(getattr(cfg, "ddp_shard", False))
+        self.sharded: set = set()
+        self.consolidations = 0
         self.gang_errors = 0
         self.error_log: List[str] = []          # first step errors (summary)
         self.est: Dict[Tuple[str, int], float] = {}
@@ -228,6 +234,7 @@ class Controller:
                     agg["error"] = agg.get("error") or jr.get("error")
                     agg["move_failed"] = agg.get("move_failed") or jr.get("move_failed")
                     agg["snap_failed"] = agg.get("snap_failed") or jr.get("snap_failed")
+                    agg["consolidate_failed"] = agg.get("consolidate_failed") or jr.get("consolidate_failed")
         for jid, jr in per_job.items():
             if jid not in self.rjobs:
                 continue
@@ -235,6 +242,13 @@ class Controller:
             rj = self.rjobs[jid]
             if jr.get("snap_failed"):
                 self.snapshot_failed(jid)
+                continue
+            if jr.get("consolidate_failed"):
+                # a member of the suspended sharded gang died before its state
+                # was gathered: restart from the last snapshot / scratch
+                if jid in self.holders:
+                    self.holders.pop(jid)
+                    self._lost_all_replicas(jid)
                 continue
             if jr.get("move_failed"):
                 self.move_failed(jid)
@@ -261,6 +275,9 @@ class Controller:
                         # one member's view (the gang's lowest rank)
                         j.extra["comm_exposed_s"] = j.extra.get("comm_exposed_s", 0.0) + c["exposed_s"]
                         j.extra["comm_span_s"] = j.extra.get("comm_span_s", 0.0) + c["span_s"]
+                        # bytes this member put on the wire per step (the gang's wire format)
+                        j.extra["comm_bytes"] = j.extra.get("comm_bytes", 0.0) + c.get("bytes", 0.0)
+                        j.extra["comm_steps"] = j.extra.get("comm_steps", 0) + c.get("bytes_steps", 0)
 
     # ---------------------------------------------------------------- failures
     def rank_lost(self, r: int) -> None:
@@ -296,6 +313,12 @@ class Controller:
             if r not in hold:
                 continue
             left = tuple(x for x in hold if x != r)
+            if left and jid in self.sharded:
+                # sharded state: the dead member's slices are gone with it
+                self.sharded.discard(jid)
+                self.holders.pop(jid)
+                self._lost_all_replicas(jid)
+                continue
             if left:
                 self.holders[jid] = left
                 self.rebind.add(jid)
@@ -353,7 +376,13 @@ class Controller:
             s._preempt(j, reason="gang-error")
         if hold is not None and len(hold) > 1:
             self._queue_aborts(self.comms.abort_gang(hold))
-            self.resync.add(jid)
+            if jid in self.sharded:
+                # no member holds the whole (consistent) state to resync from
+                self.sharded.discard(jid)
+                self.holders.pop(jid, None)
+                self._lost_all_replicas(jid)
+            else:
+                self.resync.add(jid)
         if self.log is not None:
             self.log.decision(self.now(), "gang-error", jid, ranks=list(hold or ()))
 
@@ -498,6 +527,17 @@ class Controller:
                 actions.append({"op": "drop", "job": j.job_id, "ranks": self.holders.pop(j.job_id)})
         for a in s.actions:
             j = s.jobs[a["job"]]
+            if a["op"] == "suspend" and j.job_id in self.sharded and j.job_id in self.holders \
+                    and any(r in self.dead for r in self.holders[j.job_id]):
+                self.sharded.discard(j.job_id)
+                self.holders.pop(j.job_id)
+                self._lost_all_replicas(j.job_id)
+            if a["op"] == "suspend" and j.job_id in self.sharded and j.job_id in self.holders:
+                # a suspended sharded gang gathers its full state on every
+                # member first: moves, spills and snapshots read whole buffers
+                actions.insert(0, {"op": "consolidate", "job": j.job_id, "ranks": self.holders[j.job_id]})
+                self.sharded.discard(j.job_id)
+                self.consolidations += 1
             if a["op"] == "suspend" and self.spill and j.is_pending and j.job_id in self.holders:
                 actions.append({"op": "spill", "job": j.job_id, "ranks": self.holders[j.job_id]})
             if a["op"] == "start" and j.is_running:
@@ -555,6 +595,8 @@ class Controller:
                 if act["source"] == "p2p":
                     self.last_old[j.job_id] = tuple(old)
                 self.holders[j.job_id] = ranks
+                if self.ddp_shard and len(ranks) > 1 and len(vnode_parts(ranks, self.vnode_size)) <= 1:
+                    self.sharded.add(j.job_id)     # steps shard the state from now on
                 actions.append(act)
         # bounded communicator cache: LRU sets nobody holds state on go away
         actions.extend(self.comms.evict(set(self.holders.values())))
@@ -624,8 +666,11 @@ class Controller:
 class Worker:
     def __init__(self, rank: int, world: int, device: torch.device, world_pg=None, use_graph=False,
                  gang_backend: Optional[str] = None, monitor_period: float = 5.0, pool_cap: int = 2,
-                 hbm_budget_gb: Optional[float] = None, snapshot_s: float = 0.0, snapshot_dir: str = ""):
+                 hbm_budget_gb: Optional[float] = None, snapshot_s: float = 0.0, snapshot_dir: str = "",
+                 ddp_shard: bool = False, ddp_wire: str = "fp32"):
         self.gang_backend = gang_backend or ("nccl" if device.type == "cuda" else "gloo")
+        self.ddp_shard, self.ddp_wire = ddp_shard, ddp_wire
+        self.consolidated_bytes = 0
         # warm pool: finished jobs' trainers, keyed by (model, batch, gang
         # ranks), handed to the next fresh job of the same shape after
         # Trainer.reset (new weights / batch / optimizer state in the same
@@ -663,6 +708,7 @@ class Worker:
                 raise ValueError("snapshot_s > 0 needs a snapshot_dir shared by every rank")
             self.snap = SnapshotWriter(snapshot_dir, device)
         self._snap_failed: set = set()          # jobs whose snapshot load failed (this round)
+        self._consolidate_failed: set = set()   # sharded gangs whose consolidation failed
         self._job_ranks: Dict[str, Tuple[int, ...]] = {}
         self._snap_acc: Dict[str, float] = {}
         self.use_graph = use_graph
@@ -722,7 +768,8 @@ class Worker:
                 t.enable_graph()
             return t
         t = Trainer(act["model"], self.device, batch=act.get("batch"), group=self._group(ranks),
-                    seed=act["seed"], data_seed=data_seed, use_graph=want)
+                    seed=act["seed"], data_seed=data_seed, use_graph=want, ddp_shard=self.ddp_shard,
+                    ddp_wire=self.ddp_wire)
         t.pool_key = key
         return t
 
@@ -930,6 +977,18 @@ class Worker:
                             from ..parallel.gang import FailedComm
 
                             self.groups[tuple(a["ranks"])] = FailedComm(a["ranks"], f"{type(e).__name__}: {e}")
+            elif op == "consolidate":
+                t = self.trainers.get(a["job"])
+                if t is not None and self.rank in a["ranks"]:
+                    try:
+                        self.consolidated_bytes += t.consolidate()
+                    except Exception as e:           # a member died: no one holds the whole state
+                        print(f"[worker {self.rank}] job {a['job']}: consolidate over {a['ranks']} failed "
+                              f"({type(e).__name__}: {e})", file=sys.stderr, flush=True)
+                        abort_comm(t.group)
+                        self.trainers.pop(a["job"], None)
+                        t.release()
+                        self._consolidate_failed.add(a["job"])
             elif op == "ungroup":
                 self._close_group(a["ranks"])
             elif op == "abort":
@@ -1238,8 +1297,11 @@ class Worker:
                    for jid in sorted(self._move_failed)]
         skipped += [{"job": jid, "iters": 0, "run_s": 0.0, "shared": False, "loss": None, "snap_failed": True}
                     for jid in sorted(self._snap_failed)]
+        skipped += [{"job": jid, "iters": 0, "run_s": 0.0, "shared": False, "loss": None,
+                     "consolidate_failed": True} for jid in sorted(self._consolidate_failed)]
         self._move_failed = set()
         self._snap_failed = set()
+        self._consolidate_failed = set()
         jobs = [(jid, n) for jid, n in jobs if jid not in {r["job"] for r in skipped}]
         if not jobs:
             return {"rank": self.rank, "job": None, "jobs": skipped, "dev": self._dev_sample(),
@@ -1319,8 +1381,8 @@ class Worker:
         if self.snap is not None and err is None:
             for jid, n in jobs:
                 ranks = self._job_ranks.get(jid, (self.rank,))
-                if n <= 0 or self.rank != min(ranks):
-                    continue
+                if n <= 0 or self.rank != min(ranks) or self.trainers[jid].state_sharded:
+                    continue                         # (sharded gangs: state consolidated on suspension)
                 acc = self._snap_acc.get(jid, 0.0) + dt
                 if acc >= self.snapshot_s:
                     acc = 0.0
@@ -1334,7 +1396,7 @@ class Worker:
             if t.ddp is not None:
                 # hipEvent-measured gradient sync of the steps finished so far
                 ct = t.ddp.poll_timing()
-                if ct["steps"]:
+                if ct["steps"] or ct.get("bytes_steps"):
                     rep["comm"] = ct
             if err or jid in persist_err:
                 rep["error"] = err or persist_err[jid]
@@ -1618,6 +1680,7 @@ def run_replay(cfg: SimConfig, jobs: List[ReplayJob], rank: int, world: int, dev
                  runtime_breakdown={k: round(v, 4) for k, v in prof.items()},
                  lost_ranks=lost_ranks, recovered_jobs=sorted(ctrl.recovered),
                  restarted_jobs=sorted(ctrl.restarted), snapshot_restored_jobs=sorted(ctrl.snap_restored),
+                 ddp_shard=ctrl.ddp_shard, consolidations=ctrl.consolidations,
                  lost_iters={j.job_id: j.extra["lost_iters"] for j in ctrl.sched.jobs.values()
                              if j.extra.get("lost_iters")})
         log.close()

@@ -132,6 +132,18 @@ class FakeCluster:
                     raise ProtocolError(f"drop of {job} on {a['ranks']} but held on {self.held[job]}")
                 del self.held[job]
                 self.spilled.discard(job)
+            elif op == "consolidate":
+                # a suspended sharded gang all-gathers its master / optimizer
+                # slices over xGMI (parallel/ddp.py GradBucketer.consolidate)
+                ranks = tuple(a["ranks"])
+                if self.held.get(job) != ranks:
+                    raise ProtocolError(f"consolidate of {job} on {ranks}, held on {self.held.get(job)}")
+                if job in self.spilled:
+                    raise ProtocolError(f"consolidate of {job} after its spill")
+                w = len(ranks)
+                b = _state_bytes(self.model[job]) * (w - 1) / w
+                charge(ranks, b / self.xgmi)
+                self.stats["consolidate_bytes"] = self.stats.get("consolidate_bytes", 0.0) + b * w
             elif op == "spill":
                 if job not in self.held or job in self.spilled:
                     raise ProtocolError(f"spill of job {job} that is not resident")

@@ -26,7 +26,8 @@ class Trainer:
     def __init__(self, model: str, device, batch: Optional[int] = None, group=None, seed: int = 0,
                  data_seed: Optional[int] = None, use_graph: bool = False, bucket_mb: float = 32.0,
                  model_kwargs: Optional[dict] = None, lr: Optional[float] = None,
-                 overlap_wgrad: Optional[bool] = None, branches: Optional[bool] = None):
+                 overlap_wgrad: Optional[bool] = None, branches: Optional[bool] = None,
+                 ddp_shard: bool = False, ddp_wire: str = "fp32"):
         self.model_name = model
         self.spec = MODELS[model]
         self.device = torch.device(device)
@@ -50,8 +51,12 @@ class Trainer:
         self.group = group
         self.ddp = None
         self._bucket_mb = bucket_mb
+        # sharded data parallelism (parallel/ddp.py): reduce-scatter + 1/N
+        # optimizer + bf16 shadow all-gather; master / optimizer state sharded
+        # until consolidate()
+        self.ddp_shard, self.ddp_wire = ddp_shard, ddp_wire
         if group is not None and comm_size(group) > 1:
-            self.ddp = GradBucketer(self.arena, group, bucket_mb=bucket_mb)
+            self.ddp = GradBucketer(self.arena, group, bucket_mb=bucket_mb, shard=ddp_shard, wire=ddp_wire)
         from ..utils import debug
 
         # kernel debug mode synchronises after every op: not capturable
@@ -127,7 +132,18 @@ class Trainer:
         A = self.arena
         gscale = self.ddp.grad_scale if self.ddp is not None else 1.0
         self.step_count += 1
-        regions = [(0, A.n_decay, self.spec.wd), (A.n_decay, A.numel, 0.0)]
+        sharded = self.ddp is not None and self.ddp.shard
+        if sharded:
+            # this member's slices (+ replicated tails), split at the
+            # decay / no-decay boundary; the gradient is reset as a whole below
+            regions = []
+            for a, b in self.ddp.owned_ranges():
+                if a < A.n_decay:
+                    regions.append((a, min(b, A.n_decay), self.spec.wd))
+                if b > A.n_decay:
+                    regions.append((max(a, A.n_decay), b, 0.0))
+        else:
+            regions = [(0, A.n_decay, self.spec.wd), (A.n_decay, A.numel, 0.0)]
         for lo, hi, wd in regions:
             if hi <= lo:
                 continue
@@ -138,12 +154,15 @@ class Trainer:
                 # job's own timeout word) only resets the gradient
                 guard = self.model.err if self.uses_persist else None
                 if self.opt == "sgd":
-                    T.sgd_step(w, g, self.opt_state[0][lo:hi], wb, self.lr, 0.9, wd, gscale, False, True, guard)
+                    T.sgd_step(w, g, self.opt_state[0][lo:hi], wb, self.lr, 0.9, wd, gscale, False, not sharded, guard)
                 else:
                     T.adam_step(w, g, self.opt_state[0][lo:hi], self.opt_state[1][lo:hi], wb, self.lr,
-                                0.9, 0.98, 1e-9, wd, self.step_count, gscale, True, guard)
+                                0.9, 0.98, 1e-9, wd, self.step_count, gscale, not sharded, guard)
             else:
                 _cpu_opt(self.opt, w, g, self.opt_state, lo, hi, wb, self.lr, wd, gscale, self.step_count)
+        if sharded:
+            A.grad.zero_()                 # the slices of the other members held local partials
+            self.ddp.gather_shadow()
         if self.uses_persist:
             # a guarded step -> the job's skipped-step count (persist_skipped)
             _lib.ops().lstm_guard_step(self.model.err)
@@ -256,7 +275,21 @@ class Trainer:
         return samples_per_batch(self.model_name, self.batch)
 
     # ------------------------------------------------------------ state
+    def consolidate(self) -> int:
+        """Sharded data parallelism: all-gather the master / optimizer-state
+        slices so this member holds the job's full state (collective over
+        the gang; every member calls it). Returns bytes gathered."""
+        if self.ddp is None or not self.ddp.shard:
+            return 0
+        return self.ddp.consolidate([self.arena.master] + list(self.opt_state))
+
+    @property
+    def state_sharded(self) -> bool:
+        return self.ddp is not None and self.ddp.shard and self.ddp.dirty
+
     def state_tensors(self) -> Dict[str, torch.Tensor]:
+        if self.state_sharded:
+            raise RuntimeError("trainer state is sharded across its gang: consolidate() first")
         st = {"master": self.arena.master, "shadow": self.arena.shadow}
         for i, t in enumerate(self.opt_state):
             st[f"opt{i}"] = t
@@ -369,6 +402,10 @@ class Trainer:
         receive)."""
         if getattr(self, "_spilled", None):
             raise RuntimeError("reset of a spilled trainer")
+        if self.ddp is not None:
+            # fresh state (re-initialised identically on every member, or
+            # about to be overwritten whole by a P2P receive)
+            self.ddp.dirty = False
         if init:
             self.arena.reinit(seed)
             for t in self.opt_state:
@@ -392,6 +429,14 @@ class Trainer:
     def rebind(self, group) -> None:
         """Move the job to a new DDP gang (after a preemption resumed it on
         different GPUs): new communicator, fresh bucketer."""
+        # sharded state survives only a re-created communicator over the SAME
+        # rank set (same member positions); anything else needs consolidate()
+        dirty = self.state_sharded
+        old_ranks = tuple(getattr(self.ddp.comm, "ranks", ())) if self.ddp is not None else ()
+        new_ranks = tuple(getattr(group, "ranks", ())) if group is not None else ()
+        if dirty and old_ranks != new_ranks:
+            raise RuntimeError(f"sharded trainer state on {old_ranks} cannot move to {new_ranks}: "
+                               "consolidate() first")
         self.group = group
         self.arena.on_grad_ready = None
         self.ddp = None
@@ -400,7 +445,9 @@ class Trainer:
         self.arena.grad.zero_()
         self.broken = False
         if group is not None and comm_size(group) > 1:
-            self.ddp = GradBucketer(self.arena, group, bucket_mb=self._bucket_mb)
+            self.ddp = GradBucketer(self.arena, group, bucket_mb=self._bucket_mb, shard=self.ddp_shard,
+                                    wire=self.ddp_wire)
+            self.ddp.dirty = dirty and self.ddp.shard
         self.use_graph = self._want_graph and self.ddp is None
         self._graph = None
 

@@ -22,6 +22,24 @@ early in backward.
 Uses of a param (tied embeddings report twice) are learned on the first
 iteration, which reduces every bucket at the end instead of overlapping.
 
+Sharded mode (``shard=True``, ZeRO-1/2 style; consolidated gangs only --
+a spread gang's hierarchical transport keeps the all-reduce): each bucket's
+main part (a multiple of ``world`` x 16 elements) is REDUCE-SCATTERED in
+place instead of all-reduced, so member ``p`` (its position in the gang)
+holds the summed gradient of slice ``p`` of every bucket; the few tail
+elements past the last full slice, and the buckets of norm parameters the
+kernels read in fp32, are all-reduced (replicated). The optimizer then runs
+on the member's slices (+ the replicated tails) only -- 1/world of the
+arena's optimizer traffic per member -- and the updated bf16 shadow slices
+are ALL-GATHERED back into every member's compute copy. Per parameter and
+step a member sends (W-1)/W x (4 + 2) bytes instead of 2(W-1)/W x 4 (25 %
+fewer; ``wire="bf16"`` also reduce-scatters in bf16: (W-1)/W x 4, half).
+The fp32 master and the optimizer state are then SHARDED: only this
+member's slices are current. ``consolidate()`` all-gathers them so every
+member holds the full state again -- required before anything reads the
+job's state (a preemption's P2P move or spill, a snapshot); the live
+runtime issues it as a plan action when it suspends such a gang.
+
 Timing: on a GPU every step records three hipEvents on the
 compute stream -- first bucket launched, backward done (``finish`` entry),
 all reductions joined -- and ``poll_timing`` turns completed steps into
@@ -44,12 +62,20 @@ class GradBucketer:
     consolidated gang, hierarchical intra-node RCCL + throttled host-staged
     inter-node exchange for a spread one) or a plain process group."""
 
-    def __init__(self, arena: Arena, group=None, bucket_mb: float = 32.0, overlap: bool = True):
+    def __init__(self, arena: Arena, group=None, bucket_mb: float = 32.0, overlap: bool = True,
+                 shard: bool = False, wire: str = "fp32"):
         self.arena = arena
         self.comm = as_comm(group) if dist.is_initialized() else None
         self.group = group
         self.world = comm_size(self.comm) if self.comm is not None else 1
         self.overlap = overlap
+        # sharded data parallelism only over a flat (consolidated) gang
+        self.shard = bool(shard and self.world > 1 and getattr(self.comm, "sharding", False))
+        if wire not in ("fp32", "bf16"):
+            raise ValueError(f"wire must be fp32 or bf16, not {wire!r}")
+        self.wire = wire if self.shard else "fp32"
+        self.position = self.comm.position if self.shard else 0
+        self.dirty = False                       # sharded master / optimizer state (consolidate())
         elems = max(1, int(bucket_mb * (1 << 20) // 4))
         decay = [p for p in arena.params if p.decay]
         nodecay = [p for p in arena.params if not p.decay]
@@ -66,27 +92,39 @@ class GradBucketer:
                 self.buckets.append(cur)
         self.bucket_of: Dict[int, int] = {}
         self.ranges = []
+        self.slices = []          # sharded: per bucket (slice length s, main-part end lo + W*s)
         for bi, ps in enumerate(self.buckets):
             lo = min(p.offset for p in ps)
             hi = max(p.offset + p.numel for p in ps)
             hi = min(arena.numel, (hi + 63) // 64 * 64)
             self.ranges.append((lo, hi))
+            # buckets holding params the kernels read in fp32 (norm params:
+            # Param.fp32_compute) stay replicated -- every member needs their
+            # updated master, and they are tiny
+            sl = ((hi - lo) // self.world) // 16 * 16 if (self.shard and not any(p.fp32_compute for p in ps)) else 0
+            self.slices.append((sl, lo + self.world * sl))
             for p in ps:
                 self.bucket_of[id(p)] = bi
+        self._wbufs: List[Optional[torch.Tensor]] = []     # bf16 wire staging, per bucket
         self.uses: Optional[Dict[int, int]] = None
         self._seen: Dict[int, int] = {}
         self._pending: List[int] = []
         self._launched: List[bool] = []
         self._works = []
         self.bytes_reduced = 0
+        # bytes this member SENDS (ring algorithms): all-reduce 2(W-1)/W x n,
+        # reduce-scatter / all-gather (W-1)/W x n each
+        self.wire_bytes = 0.0
         self._timed = self.world > 1 and arena.grad.is_cuda
         self._ev_first = None
         self._ev_open: List[tuple] = []          # (first, bwd_done, joined) per step, not yet read
         self._acc = {"exposed_s": 0.0, "span_s": 0.0, "steps": 0}
+        self._bytes_acc = [0.0, 0]               # wire bytes / steps since the last poll
         arena.on_grad_ready = self._on_ready
         self._reset()
 
     def _reset(self):
+        self._step_w0 = self.wire_bytes
         self._seen = {}
         self._launched = [False] * len(self.buckets)
         self._works = []
@@ -103,8 +141,46 @@ class GradBucketer:
             if self._timed and self._ev_first is None:
                 self._ev_first = torch.cuda.Event(enable_timing=True)
                 self._ev_first.record()
+            if self.shard:
+                self._launch_shard(bi, lo, hi)
+                return
             self._works.append(self.comm.start(view))
+            self.wire_bytes += 2.0 * (self.world - 1) / self.world * view.numel() * 4
         self.bytes_reduced += view.numel() * 4
+
+    def _launch_shard(self, bi: int, lo: int, hi: int) -> None:
+        sl, mid = self.slices[bi]
+        W, p = self.world, self.position
+        g = self.arena.grad
+        if sl > 0:
+            if self.wire == "bf16":
+                # bf16 on the wire: cast the main part, reduce-scatter it,
+                # widen this member's summed slice back into the fp32 grad
+                # (after finish(), see _widen)
+                buf = self._wire_buf(bi, mid - lo)
+                buf.copy_(g[lo:mid])
+                self._works.append(self.comm.reduce_scatter(buf[p * sl:(p + 1) * sl], buf))
+                self.bytes_reduced += (mid - lo) * 2
+                self.wire_bytes += (W - 1) / W * (mid - lo) * 2
+            else:
+                self._works.append(self.comm.reduce_scatter(g[lo + p * sl:lo + (p + 1) * sl], g[lo:mid]))
+                self.bytes_reduced += (mid - lo) * 4
+                self.wire_bytes += (W - 1) / W * (mid - lo) * 4
+        if hi > mid:                                  # tail: replicated
+            self._works.append(self.comm.start(g[mid:hi]))
+            self.bytes_reduced += (hi - mid) * 4
+            self.wire_bytes += 2.0 * (W - 1) / W * (hi - mid) * 4
+
+    def _wire_buf(self, bi: int, n: int) -> torch.Tensor:
+        # one bf16 staging buffer per in-flight bucket (distinct memory: the
+        # reduce-scatters of several buckets are in flight together)
+        while len(self._wbufs) <= bi:
+            self._wbufs.append(None)
+        b = self._wbufs[bi]
+        if b is None or b.numel() < n:
+            b = torch.empty(n, dtype=torch.bfloat16, device=self.arena.grad.device)
+            self._wbufs[bi] = b
+        return b[:n]
 
     def _on_ready(self, p: Param):
         k = id(p)
@@ -139,11 +215,20 @@ class GradBucketer:
             self._launch(b)
         if self._works:
             self.comm.finish(self._works)
+            if self.shard and self.wire == "bf16":
+                g, p = self.arena.grad, self.position
+                for bi, (sl, _) in enumerate(self.slices):
+                    if sl > 0:
+                        lo = self.ranges[bi][0]
+                        g[lo + p * sl:lo + (p + 1) * sl].copy_(self._wbufs[bi][p * sl:(p + 1) * sl])
             if self._timed:
                 done = torch.cuda.Event(enable_timing=True)
                 done.record()
                 self._ev_open.append((self._ev_first if self._ev_first is not None else bwd, bwd, done))
         self._ev_first = None
+        if self.world > 1:
+            self._bytes_acc[0] += self.wire_bytes - self._step_w0
+            self._bytes_acc[1] += 1
         self._reset()
 
     def poll_timing(self) -> dict:
@@ -160,8 +245,53 @@ class GradBucketer:
                 keep.append((first, bwd, done))
         self._ev_open = keep
         out, self._acc = self._acc, {"exposed_s": 0.0, "span_s": 0.0, "steps": 0}
+        # wire bytes of the steps finished since the last poll (the sharded
+        # all-gather of a step counts with the NEXT step's finish)
+        out["bytes"], out["bytes_steps"] = self._bytes_acc
+        self._bytes_acc = [0.0, 0]
         return out
 
     @property
     def grad_scale(self) -> float:
         return 1.0 / self.world
+
+    # ------------------------------------------------------------ sharded mode
+    def owned_ranges(self) -> List[tuple]:
+        """Arena ranges whose summed gradient this member holds after
+        finish(): its slice of every bucket plus every (replicated) tail."""
+        out = []
+        for (lo, hi), (sl, mid) in zip(self.ranges, self.slices):
+            if sl > 0:
+                a = lo + self.position * sl
+                out.append((a, a + sl))
+            if hi > mid:
+                out.append((mid, hi))
+        return sorted(out)
+
+    def gather_shadow(self) -> None:
+        """After the sharded optimizer step: every member's updated bf16
+        slices into every member's compute copy (all-gather per bucket)."""
+        sh, p = self.arena.shadow, self.position
+        works = []
+        for (lo, _), (sl, mid) in zip(self.ranges, self.slices):
+            if sl > 0:
+                works.append(self.comm.all_gather(sh[lo:mid], sh[lo + p * sl:lo + (p + 1) * sl]))
+                self.wire_bytes += (self.world - 1) / self.world * (mid - lo) * 2
+        self.comm.finish(works)
+        self.dirty = True
+
+    def consolidate(self, state: List[torch.Tensor]) -> int:
+        """All-gather the sharded fp32 buffers (master + optimizer state) so
+        every member holds the full job state again; collective over the
+        gang. Returns bytes gathered per member."""
+        if not self.dirty:
+            return 0
+        p, works, nb = self.position, [], 0
+        for buf in state:
+            for (lo, _), (sl, mid) in zip(self.ranges, self.slices):
+                if sl > 0:
+                    works.append(self.comm.all_gather(buf[lo:mid], buf[lo + p * sl:lo + (p + 1) * sl]))
+                    nb += (mid - lo - sl) * buf.element_size()
+        self.comm.finish(works)
+        self.dirty = False
+        return nb

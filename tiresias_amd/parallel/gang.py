@@ -72,6 +72,22 @@ class FlatComm:
     def start(self, view: torch.Tensor):
         return self.pg.all_reduce(view)
 
+    # sharded data parallelism (parallel/ddp.py GradBucketer(shard=True)):
+    # in-place reduce-scatter (out is this member's slice of inp) and
+    # all-gather (inp is this member's slice of out), SUM / concatenation in
+    # the comm's rank order
+    sharding = True
+
+    def reduce_scatter(self, out: torch.Tensor, inp: torch.Tensor):
+        return self.pg.reduce_scatter(out, inp)
+
+    def all_gather(self, out: torch.Tensor, inp: torch.Tensor):
+        return self.pg.all_gather(out, inp)
+
+    @property
+    def position(self) -> int:
+        return self.pg.position
+
     def finish(self, handles) -> None:
         for w in handles:
             w.wait()
@@ -245,6 +261,13 @@ def configure_nccl_env() -> None:
     os.environ.setdefault("TORCH_NCCL_DUMP_ON_TIMEOUT", "0")
 
 
+class _Done:
+    """A completed collective (host-staged gloo path)."""
+
+    def wait(self):
+        return True
+
+
 class GangPG:
     """A communicator over an arbitrary rank set, built directly on a c10d
     backend (``ProcessGroupNCCL`` = RCCL on ROCm, or ``ProcessGroupGloo``)
@@ -286,6 +309,34 @@ class GangPG:
         o = dist.AllreduceOptions()
         o.reduceOp = dist.ReduceOp.SUM
         return self.pg.allreduce([t], o)
+
+    def reduce_scatter(self, out: torch.Tensor, inp: torch.Tensor):
+        o = dist.ReduceScatterOptions()
+        o.reduceOp = dist.ReduceOp.SUM
+        if self.backend != "nccl" and inp.is_cuda:
+            # gloo gangs on device tensors (the one-GPU multi-rank
+            # rehearsal): staged through host memory, synchronously
+            off = (out.data_ptr() - inp.data_ptr()) // inp.element_size()
+            h = inp.cpu()
+            ho = h[off:off + out.numel()]
+            self.pg._reduce_scatter_base(ho, h, o).wait()
+            out.copy_(ho)
+            return _Done()
+        return self.pg._reduce_scatter_base(out, inp, o)
+
+    def all_gather(self, out: torch.Tensor, inp: torch.Tensor):
+        if self.backend != "nccl":
+            if inp.is_cuda:
+                ho = torch.empty(out.shape, dtype=out.dtype)
+                self.pg._allgather_base(ho, inp.cpu()).wait()
+                out.copy_(ho)
+                return _Done()
+            inp = inp.clone()                 # gloo: no aliasing of in / out
+        return self.pg._allgather_base(out, inp)
+
+    @property
+    def position(self) -> int:
+        return self.rank
 
     def reduce(self, t: torch.Tensor, root_global: int):
         o = dist.ReduceOptions()
@@ -656,6 +707,18 @@ class _PlainPG:
 
     def all_reduce(self, t):
         return dist.all_reduce(t, op=dist.ReduceOp.SUM, group=self.pg, async_op=True)
+
+    def reduce_scatter(self, out, inp):
+        return dist.reduce_scatter_tensor(out, inp, op=dist.ReduceOp.SUM, group=self.pg, async_op=True)
+
+    def all_gather(self, out, inp):
+        if dist.get_backend(self.pg) != "nccl":
+            inp = inp.clone()
+        return dist.all_gather_into_tensor(out, inp, group=self.pg, async_op=True)
+
+    @property
+    def position(self) -> int:
+        return dist.get_rank(self.pg)
 
 
 def as_comm(group):
