@@ -764,14 +764,6 @@ void gemm8p_policy_op(int64_t mode, int64_t stagger) { tam::gemm8p_policy((int)m
 void gemm8p_group_op(int64_t g) { tam::gemm8p_group((int)g); }
 void gemm8p_slab_force_op(int64_t sp) { tam::gemm8p_slab_force((int)sp); }
 // C[M][N] = A[M][K] . B[N][K]^T through the 4-wave 256^2 kernel (A/B and tests)
-bool gemm4w_op(const Tensor& a, const Tensor& b, const Tensor& c, int64_t pipe) {
-  check_bf16(a, "a"); check_bf16(b, "b"); check_bf16(c, "c");
-  TORCH_CHECK(a.dim() == 2 && b.dim() == 2 && c.dim() == 2 && a.stride(1) == 1 && b.stride(1) == 1 &&
-              c.stride(1) == 1, "tam.gemm4w: 2-D row-major operands");
-  TORCH_CHECK(a.size(1) == b.size(1) && c.size(0) == a.size(0) && c.size(1) == b.size(0), "tam.gemm4w: shapes");
-  return tam::gemm4w(bp(a), a.stride(0), bp(b), b.stride(0), bpm(c), c.stride(0), (int)a.size(0),
-                     (int)b.size(0), (int)a.size(1), (int)pipe, cur_stream(a));
-}
 
 void gemm_force_op(int64_t cfg, int64_t splits) {
   tam::gemm_force((int)cfg, (int)splits);
@@ -1018,7 +1010,6 @@ TORCH_LIBRARY(tam, m) {
   m.def("gemm8p_policy(int mode, int stagger) -> ()", &gemm8p_policy_op);
   m.def("gemm8p_group(int g) -> ()", &gemm8p_group_op);
   m.def("gemm8p_slab_force(int sp) -> ()", &gemm8p_slab_force_op);
-  m.def("gemm4w(Tensor a, Tensor b, Tensor(a!) c, int pipe=1) -> bool", &gemm4w_op);
   m.def("gemm_lib_policy(int policy) -> ()", &gemm_lib_policy_op);
   m.def("conv_dma_policy(int policy) -> ()", &conv_dma_policy_op);
   m.def("conv_wgrad_force(int bm, int bn, int splits, int noatomic=0) -> ()", &conv_wgrad_force_op);

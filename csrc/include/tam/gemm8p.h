@@ -466,9 +466,6 @@ void gemm8p_splitk(const bf16_t* A, long lda, bool ak, const bf16_t* B, long ldb
                    int N, int K, const Epi& ep, int splits, float* ws, hipStream_t s, int tile = 256);
 int gemm8p_slab_splits(int M, int N, int K, int tile = 256);
 void gemm8p_slab_force(int sp);   // > 0: forced slab split count (A/B sweeps); 0: heuristic
-// 4-wave 256^2 variant (gemm4w.h): K-major A and B, bf16 C; false if ineligible
-bool gemm4w(const bf16_t* A, long lda, const bf16_t* B, long ldb, bf16_t* C, long ldc, int M, int N, int K,
-            int pipe, hipStream_t s);
 // 128 or 256: the tile the auto policy picks for this shape
 int gemm8p_tile(int M, int N, int K);
 

@@ -5,7 +5,6 @@
 #include "tam/gemm256.h"
 #include "tam/gemm8p.h"
 #include "tam/gemm_dma.h"
-#include "tam/gemm4w.h"
 
 namespace tam {
 
@@ -290,15 +289,6 @@ void gemm_select(const bf16_t* A, long lda, bool ak, const bf16_t* B, long ldb, 
     case 2: gemm_tile<64, 128>(A, lda, ak, B, ldb, bk, M, N, K, ep, t.splits, s); break;
     default: gemm_tile<64, 64>(A, lda, ak, B, ldb, bk, M, N, K, ep, t.splits, s); break;
   }
-}
-
-// 4-wave 256^2 GEMM (gemm4w.h), K-major x K-major, bf16 out; false when the
-// shape / strides are not for it
-bool gemm4w(const bf16_t* A, long lda, const bf16_t* B, long ldb, bf16_t* C, long ldc, int M, int N, int K,
-            int pipe, hipStream_t s) {
-  if (!gemm4w_ok(M, N, K, lda, ldb, ldc)) return false;
-  launch_gemm4w(A, lda, B, ldb, C, ldc, M, N, K, g_p8_group, pipe, s);
-  return true;
 }
 
 }  // namespace tam

@@ -1193,20 +1193,6 @@ def test_lstm_persistent_sharded_counters_bitwise(gpu, ns):
         assert torch.equal(a, b)
 
 
-@pytest.mark.parametrize("M,N,K", [(512, 512, 256), (3000, 1000, 640), (256, 264, 64)])
-@pytest.mark.parametrize("pipe", [0, 1])
-def test_gemm4w_matches_fp32(gpu, M, N, K, pipe):
-    """4-wave 256^2 GEMM (K-major x K-major, bf16 out) vs fp32 torch, edge
-    tiles included (rows / columns past M, N are loaded clamped, never stored)."""
-    torch.manual_seed(7)
-    A = (torch.rand(M, K, device=gpu) * 2 - 1).to(BF)
-    B = (torch.rand(N, K, device=gpu) * 2 - 1).to(BF)
-    c = torch.full((M, N), 7.0, device=gpu, dtype=BF)
-    assert T().gemm4w(A, B, c, pipe)
-    torch.cuda.synchronize()
-    assert rel_err(c, A.float() @ B.float().t()) < 1e-2
-
-
 def test_lstm_persistent_backward_bf16_dh(gpu):
     """The persistent backward reads a bf16 dH directly (as autograd hands
     it): bit-identical to feeding the same values as fp32."""

@@ -1612,8 +1612,11 @@ def run_replay(cfg: SimConfig, jobs: List[ReplayJob], rank: int, world: int, dev
                         worker.snap.flush(10.0)
                         for f in os.listdir(worker.snap.dir):
                             if f.endswith(".pt"):
-                                with open(os.path.join(worker.snap.dir, f), "r+b") as fh:
-                                    fh.truncate(16)
+                                try:             # another rank's writer may drop it meanwhile
+                                    with open(os.path.join(worker.snap.dir, f), "r+b") as fh:
+                                        fh.truncate(16)
+                                except FileNotFoundError:
+                                    pass
                     os._exit(17)                     # simulated node/rank crash
                 if fault.get("kind") == "hang":
                     if plane is not None:
