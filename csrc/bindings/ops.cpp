@@ -99,8 +99,19 @@ void run_lib(const Tensor& a, bool ak, const Tensor& b, bool bk, const Tensor& c
 // any output dtype) when its tile grid underfills the chip
 // tile / sp < 0: the heuristics (gemm8p_tile, gemm8p_slab_splits); the
 // measured routing passes the (tile, splits) it timed best
+// sp == 0 (tile 256): the stream-K schedule; g_sk_force: the heuristic
+// configuration becomes stream-K wherever eligible (tests)
+bool g_sk_force = false;
 void run_p8(const Tensor& a, bool ak, const Tensor& b, bool bk, int64_t M, int64_t N, int64_t K,
             const tam::Epi& ep, bool allow_split, int tile = -1, int sp = -1) {
+  if ((sp == 0 || (g_sk_force && tile < 0)) &&
+      tam::gemm8p_sk_ok(ak, bk, (int)M, (int)N, (int)K, a.stride(0), b.stride(0))) {
+    Tensor ws = at::empty({tam::gemm8p_sk_ws_floats((int)M, (int)N, (int)K)}, a.options().dtype(at::kFloat));
+    tam::gemm8p_streamk(bp(a), a.stride(0), ak, bp(b), b.stride(0), bk, (int)M, (int)N, (int)K, ep,
+                        ws.data_ptr<float>(), cur_stream(a));
+    return;
+  }
+  if (sp == 0) sp = -1;
   const bool explicit_cfg = tile > 0;
   if (tile < 0) tile = tam::gemm8p_tile((int)M, (int)N, (int)K);
   if (sp < 0) sp = tam::gemm8p_slab_splits((int)M, (int)N, (int)K, tile);
@@ -115,6 +126,13 @@ void run_p8(const Tensor& a, bool ak, const Tensor& b, bool bk, int64_t M, int64
                        cur_stream(a), 0, tile);
   else
     run_mfma(a, ak, b, bk, M, N, K, ep, allow_split, 3);
+}
+void run_skinny(const Tensor& a, const Tensor& b, bool bk, int64_t M, int64_t N, int64_t K, const tam::Epi& ep) {
+  const int sp = tam::gemm_skinny_splits((int)M, (int)N, (int)K);
+  Tensor ws;
+  if (sp > 1) ws = at::empty({sp, M, N}, a.options().dtype(at::kFloat));
+  tam::gemm_skinny(bp(a), a.stride(0), bp(b), b.stride(0), bk, (int)M, (int)N, (int)K, ep, sp,
+                   sp > 1 ? ws.data_ptr<float>() : nullptr, cur_stream(a));
 }
 // measured (tile, splits) of the p8 route per key
 std::map<GemmKey, std::pair<int, int>> g_p8_cfg;
@@ -243,6 +261,13 @@ void gemm_dispatch(const Tensor& a, bool a_kmajor, const Tensor& b, bool b_kmajo
     run_p8(a, a_kmajor, b, b_kmajor, M, N, K, ep, allow_split);
     return;
   }
+  // skinny M (<= 64, a batch-sized activation times a weight of >= 1 Mi
+  // elements): the weight-streaming kernel, split-K over every CU
+  if (!g_forced && mode != 2 && (double)N * K >= (double)(1 << 20) &&
+      tam::gemm_skinny_ok(a_kmajor, b_kmajor, (int)M, (int)N, (int)K, a.stride(0), b.stride(0))) {
+    run_skinny(a, b, b_kmajor, M, N, K, ep);
+    return;
+  }
   // our two kernels are both candidates for every shape the DMA GEMM accepts
   if (g_dma_policy == 2) {
     run_mfma(a, a_kmajor, b, b_kmajor, M, N, K, ep, allow_split, 2);
@@ -301,6 +326,8 @@ void gemm_dispatch(const Tensor& a, bool a_kmajor, const Tensor& b, bool b_kmajo
           cands.push_back({tl, one_wave > 16 ? 16 : one_wave});
         if (tl == 256 && sp == 1 && t256 < 150 && K / 64 >= 32 && one_wave != 2) cands.push_back({tl, 2});
       }
+      if (tam::gemm8p_sk_ok(a_kmajor, b_kmajor, (int)M, (int)N, (int)K, a.stride(0), b.stride(0)))
+        cands.push_back({256, 0});   // stream-K
     }
     // two interleaved rounds, best of each: a single timing taken while other
     // streams still drain work (the first eager steps) can be off by 40 %
@@ -388,7 +415,7 @@ int64_t gemm_routes_load_op(const std::string& text) {
     if (g_route.count(key)) continue;
     int tile = -1, sp = -1;
     if (route == 3 && !(ls >> tile >> sp)) continue;     // a p8 route needs its measured config
-    if (route == 3 && !((tile == 128 || tile == 256) && sp >= 1 && sp <= 16)) continue;
+    if (route == 3 && !((tile == 128 || tile == 256) && sp >= (tile == 256 ? 0 : 1) && sp <= 16)) continue;
     g_route[key] = route;
     g_route_ms[key] = t;
     if (route == 3) g_p8_cfg[key] = {tile, sp};
@@ -432,7 +459,10 @@ int64_t conv_fwd_op(const Tensor& x, const Tensor& w, const Tensor& y, int64_t s
                 "tam.conv_fwd: stats must be a contiguous fp64 [BN_SHARDS * 2K] tensor");
     ep.stats = stats->data_ptr<double>();
   }
-  return tam::conv_fwd(bp(x), bp(w), g, ep, cur_stream(x));
+  const long wsf = tam::conv_fwd_split_ws(g);
+  Tensor ws;
+  if (wsf > 0) ws = at::empty({wsf}, x.options().dtype(at::kFloat));
+  return tam::conv_fwd(bp(x), bp(w), g, ep, cur_stream(x), wsf > 0 ? ws.data_ptr<float>() : nullptr, wsf);
 }
 
 void conv_dgrad_op(const Tensor& dy, const Tensor& w, const Tensor& wt, const Tensor& dx,
@@ -452,7 +482,10 @@ void conv_dgrad_op(const Tensor& dy, const Tensor& w, const Tensor& wt, const Te
     TORCH_CHECK(mask->numel() == dx.numel(), "tam.conv_dgrad: mask size");
     ep.mask = bp(*mask); ep.ldm = g.C;
   }
-  tam::conv_dgrad(bp(dy), bp(w), bp(wt), g, ep, cur_stream(dy));
+  const long wsf = tam::conv_dgrad_split_ws(g);
+  Tensor ws;
+  if (wsf > 0) ws = at::empty({wsf}, dy.options().dtype(at::kFloat));
+  tam::conv_dgrad(bp(dy), bp(w), bp(wt), g, ep, cur_stream(dy), wsf > 0 ? ws.data_ptr<float>() : nullptr, wsf);
 }
 
 // deferred weight gradients of many Linear layers in one grouped launch:
@@ -548,7 +581,11 @@ int64_t conv_dgrad_pre_op(const Tensor& dy, const Tensor& w, const Tensor& wt, c
     ep.bnmean = bnmean->data_ptr<float>();
     ep.bnrstd = bnrstd->data_ptr<float>();
   }
-  return tam::conv_dgrad(bp(dy), bp(w), bp(wt), g, ep, cur_stream(dy));
+  const long wsf = ep.bnx ? 0 : tam::conv_dgrad_split_ws(g);
+  Tensor ws;
+  if (wsf > 0) ws = at::empty({wsf}, dy.options().dtype(at::kFloat));
+  return tam::conv_dgrad(bp(dy), bp(w), bp(wt), g, ep, cur_stream(dy), wsf > 0 ? ws.data_ptr<float>() : nullptr,
+                         wsf);
 }
 
 // dbias (optional, fp32 [K]): += the bias gradient colsum(dY), fused into the
@@ -763,6 +800,11 @@ void gemm_dma_policy_op(int64_t p, int64_t cfg) {
 void gemm8p_policy_op(int64_t mode, int64_t stagger) { tam::gemm8p_policy((int)mode, (int)stagger); }
 void gemm8p_group_op(int64_t g) { tam::gemm8p_group((int)g); }
 void gemm8p_slab_force_op(int64_t sp) { tam::gemm8p_slab_force((int)sp); }
+void gemm8p_sk_force_op(int64_t on) { g_sk_force = on != 0; }
+void conv_split_policy_op(int64_t p) { tam::conv_split_policy((int)p); }
+void gemm_skinny_policy_op(int64_t on, int64_t sp, int64_t nst) {
+  tam::gemm_skinny_policy((int)on, (int)sp, (int)nst);
+}
 // C[M][N] = A[M][K] . B[N][K]^T through the 4-wave 256^2 kernel (A/B and tests)
 
 void gemm_force_op(int64_t cfg, int64_t splits) {
@@ -1010,6 +1052,9 @@ TORCH_LIBRARY(tam, m) {
   m.def("gemm8p_policy(int mode, int stagger) -> ()", &gemm8p_policy_op);
   m.def("gemm8p_group(int g) -> ()", &gemm8p_group_op);
   m.def("gemm8p_slab_force(int sp) -> ()", &gemm8p_slab_force_op);
+  m.def("gemm_skinny_policy(int on, int force_splits, int nst) -> ()", &gemm_skinny_policy_op);
+  m.def("gemm8p_sk_force(int on) -> ()", &gemm8p_sk_force_op);
+  m.def("conv_split_policy(int p) -> ()", &conv_split_policy_op);
   m.def("gemm_lib_policy(int policy) -> ()", &gemm_lib_policy_op);
   m.def("conv_dma_policy(int policy) -> ()", &conv_dma_policy_op);
   m.def("conv_wgrad_force(int bm, int bn, int splits, int noatomic=0) -> ()", &conv_wgrad_force_op);

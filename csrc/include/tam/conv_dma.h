@@ -245,8 +245,12 @@ __device__ __forceinline__ void cd_epilogue(f32x4_t (&acc)[4][BN / WN / 16], con
 
 // one block's tile of one pass; bid = the block's (XCD-remapped) index within
 // the pass's tile grid
+// kt_hi >= 0: only K-tiles [kt_lo, kt_hi) (split-K slice); slab != null:
+// the raw fp32 accumulators go to slab[m][Ng] (tile rows m, no row map, no
+// epilogue) for cd_slab_reduce_kernel
 template <int BN, int WN, int BM>
-__device__ __forceinline__ void conv_dma_body(const CDArgs& a, const Epi& ep, const int bid) {
+__device__ __forceinline__ void conv_dma_body(const CDArgs& a, const Epi& ep, const int bid, const int kt_lo = 0,
+                                              const int kt_hi = -1, float* __restrict__ slab = nullptr) {
   constexpr int WM = BM / 64;             // waves along M (64 rows each)
   constexpr int W = WM * WN;              // waves
   constexpr int BK = 64;
@@ -303,11 +307,12 @@ __device__ __forceinline__ void conv_dma_body(const CDArgs& a, const Epi& ep, co
     bptr[j] = a.wgt + (long)n * a.ldb + c * 8;
   }
   const int ctiles = a.Cs / BK;
-  const int nk = a.Kd / BK;
+  const int nk = (kt_hi < 0 ? a.Kd / BK : kt_hi) - kt_lo;
 
-  auto issue = [&](int kt, int st) {
+  auto issue = [&](int t, int st) {
     char* sa = smem + st * STAGE;
     char* sb = sa + A_BYTES;
+    const int kt = kt_lo + t;
     const int ct = kt % ctiles, tp = kt / ctiles;
     const int dh = a.tap_dh[tp], dw = a.tap_dw[tp];
     const int toff = (dh * a.Ws + dw) * a.Cs + ct * BK;
@@ -371,10 +376,109 @@ __device__ __forceinline__ void conv_dma_body(const CDArgs& a, const Epi& ep, co
     }
   }
 
+  if (slab) {
+    // C/D map of 16x16x32: col = lane&15, row = (lane>>4)*4 + r
+#pragma unroll
+    for (int j = 0; j < TN; ++j) {
+      const int col = n0 + wn * WCOLS + 16 * j + (lane & 15);
+#pragma unroll
+      for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int row = m0 + wm * 64 + 16 * i + 4 * (lane >> 4) + r;
+          if (row < a.M) slab[(long)row * a.Ng + col] = acc[i][j][r];
+        }
+    }
+    return;
+  }
   cd_epilogue<BN, WN, BM>(acc, ep, smem, n0, a.Ng, tm % BN_SHARDS, [&](int lr) -> long {
     const int row = m0 + lr;
     return row < a.M ? cd_out_row(a, row) : -1L;
   });
+}
+
+// split-K over blockIdx.y: slice kz owns K-tiles [kz * kps, (kz+1) * kps) and
+// writes its partial sums to ws[kz][M][Ng]
+template <int BN, int WN, int BM = 256>
+__global__ void __launch_bounds__(BM / 64 * 64 * WN, 1) conv_dma_split_kernel(CDArgs a, float* ws, int kps) {
+  const int nk = a.Kd / 64;
+  const int lo = blockIdx.y * kps;
+  conv_dma_body<BN, WN, BM>(a, Epi{}, xcd_remap(blockIdx.x, gridDim.x), lo, min(nk, lo + kps),
+                            ws + (long)blockIdx.y * a.M * a.Ng);
+}
+
+// C = epilogue(sum_z ws[z]) for the split conv: bf16 output rows through the
+// pass's row map, bias / relu / relu-mask / accumulate, and the BatchNorm sums
+// of the stored values (Epi::stats, sharded fp64 atomics) -- what cd_epilogue
+// does for an unsplit tile. Block = (Ng/8 channel groups) x row lanes over a
+// contiguous row range.
+static __global__ void __launch_bounds__(256) cd_slab_reduce_kernel(const float* __restrict__ ws, int sp, CDArgs a,
+                                                             Epi ep, int rows_per_block) {
+  __shared__ float red[2 * 2048];
+  const int vs = a.Ng / 8, rpp = 256 / vs;
+  const int cg = threadIdx.x % vs, rl = threadIdx.x / vs;
+  const int c = cg * 8;
+  float ssum[8], ssq[8];
+#pragma unroll
+  for (int e = 0; e < 8; ++e) ssum[e] = ssq[e] = 0.f;
+  const long plane = (long)a.M * a.Ng;
+  if (rl < rpp) {
+    float bv[8];
+#pragma unroll
+    for (int e = 0; e < 8; ++e) bv[e] = ep.bias ? bf2f(ep.bias[c + e]) : 0.f;
+    const int r0 = blockIdx.x * rows_per_block, r1 = min(a.M, r0 + rows_per_block);
+    for (int m = r0 + rl; m < r1; m += rpp) {
+      const float* src = ws + (long)m * a.Ng + c;
+      float4 lo = *(const float4*)src, hi = *(const float4*)(src + 4);
+      for (int z = 1; z < sp; ++z) {
+        const float4 l2 = *(const float4*)(src + z * plane), h2 = *(const float4*)(src + z * plane + 4);
+        lo.x += l2.x; lo.y += l2.y; lo.z += l2.z; lo.w += l2.w;
+        hi.x += h2.x; hi.y += h2.y; hi.z += h2.z; hi.w += h2.w;
+      }
+      float v[8] = {lo.x, lo.y, lo.z, lo.w, hi.x, hi.y, hi.z, hi.w};
+      const long orow = cd_out_row(a, m);
+      bf16_t* dst = (bf16_t*)ep.c + orow * ep.ldc + c;
+      uint4 mk = make_uint4(0u, 0u, 0u, 0u), old = make_uint4(0u, 0u, 0u, 0u);
+      if (ep.mask) mk = *(const uint4*)(ep.mask + orow * ep.ldm + c);
+      if (ep.mode == 1) old = *(const uint4*)dst;
+      const uint32_t* mw = (const uint32_t*)&mk;
+      const uint32_t* ow = (const uint32_t*)&old;
+      uint32_t out[4];
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        float t = v[e] * ep.alpha + bv[e];
+        if (ep.relu) t = fmaxf(t, 0.f);
+        if (ep.mask) {
+          const uint32_t mb = (mw[e >> 1] >> (16 * (e & 1))) & 0xffffu;
+          if ((mb & 0x8000u) || !(mb & 0x7fffu)) t = 0.f;     // mask <= 0
+        }
+        if (ep.mode == 1) t = bf2f(f2bf(t)) + bf2f((bf16_t)((ow[e >> 1] >> (16 * (e & 1))) & 0xffffu));
+        v[e] = bf2f(f2bf(t));                                 // the stored value
+      }
+#pragma unroll
+      for (int e = 0; e < 4; ++e) out[e] = pack_bf2(v[2 * e], v[2 * e + 1]);
+      *(uint4*)dst = make_uint4(out[0], out[1], out[2], out[3]);
+      if (ep.stats) {
+#pragma unroll
+        for (int e = 0; e < 8; ++e) { ssum[e] += v[e]; ssq[e] += v[e] * v[e]; }
+      }
+    }
+  }
+  if (!ep.stats) return;
+  // row lanes of one channel group -> LDS (float atomics) -> one fp64
+  // atomic per channel per block into shard blockIdx % BN_SHARDS
+  for (int e = threadIdx.x; e < 2 * a.Ng; e += 256) red[e] = 0.f;
+  __syncthreads();
+  if (rl < rpp) {
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      atomicAdd(&red[c + e], ssum[e]);
+      atomicAdd(&red[a.Ng + c + e], ssq[e]);
+    }
+  }
+  __syncthreads();
+  double* sh = ep.stats + (long)(blockIdx.x % BN_SHARDS) * 2 * a.Ng;
+  for (int e = threadIdx.x; e < 2 * a.Ng; e += 256) unsafeAtomicAdd(sh + e, (double)red[e]);
 }
 
 template <int BN, int WN, int BM = 256>
@@ -575,17 +679,98 @@ inline int conv_dma_pick_bn(int M, int Ng, int Kd, int force) {
   return pick;
 }
 
-// returns 0 (not for this core) or the tile height BM of the launch
-inline int launch_conv_dma(const CDArgs& a, const Epi& ep, hipStream_t s, int force = 0) {
+// Split-K for a pass whose tile grid covers a fraction of the 256 CUs (the
+// 7x7 / 14x14 stages of ResNet-50 at batch 64: 26-196 tiles). Every conv_dma
+// tile runs one block per CU (the 3-stage rings are 96-192 KiB of LDS), so a
+// launch costs ceil(blocks / CUs) block times; a split adds the fp32 slab
+// round trip ((sp + 1) M Ng 4 B) and a reduce launch. Time model (us), per-CU
+// rates as the pick model's efficiencies x ~2.4 TF/s (the measured 128-row
+// 7x7 rate); returns the pick (tile code) and slices of the cheapest plan
+// with >= 8 K-tiles per slice and <= 64 MiB of slabs.
+struct CdSplit { int pick, sp; };
+inline CdSplit cd_split_plan(const CDArgs& a, int pick0, int cus) {
+  CdSplit best{pick0, 1};
+  const int nk = a.Kd / 64;
+  if (nk < 16) return best;
+  double tbest = 1e30;
+  const int codes[3] = {256, 128, 128 | 0x1000};
+  const double eff[3] = {1.0, 0.92, 0.8};
+  for (int c = 0; c < 3; ++c) {
+    const int code = codes[c], bm = (code & 0x1000) ? 128 : 256, bn = code & 0xfff;
+    if (a.Ng % bn) continue;
+    if ((code & 0x1000) && a.Kd < 1024) continue;
+    const long tiles = (long)((a.M + bm - 1) / bm) * (a.Ng / bn);
+    for (int sp = 1; sp <= 8; ++sp) {
+      if (sp > 1 && (nk / sp < 8 || (long)sp * a.M * a.Ng > (16L << 20))) break;
+      const double block_us = 2.0 * bm * bn * (double)a.Kd / sp / (eff[c] * 2.4e6);
+      const double waves = (double)((tiles * sp + cus - 1) / cus);
+      double t = waves * block_us;
+      if (sp > 1) t += (double)(sp + 1) * a.M * a.Ng * 4 / 4.0e6 + 3.0;
+      if (t < tbest * 0.97) { tbest = t; best = CdSplit{code, sp}; }
+    }
+  }
+  return best;
+}
+
+inline int cd_cus() {
+  static int n = 0;
+  if (!n) {
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess ||
+        hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || n < 1)
+      n = 256;
+  }
+  return n;
+}
+
+inline bool cd_base_ok(const CDArgs& a, int force) {
   // Kd >= 256: with fewer than 4 K-tiles the ring never fills (1x1 convs over
   // 64/128 channels measured slower than the igemm) — unless forced (tests,
   // strided-dgrad parity classes, where the igemm alternative is far worse)
-  if (a.Cs % 64 != 0 || a.Kd % 64 != 0 || a.Kd < 64 || (a.Kd < 256 && !force)) return 0;
-  if (a.ntaps < 1 || a.ntaps > 9) return 0;
-  if ((long)a.Hs * a.Ws * a.Cs * ((a.M + a.P * a.Q - 1) / (a.P * a.Q)) >= (1L << 31)) return 0;
-  if ((long)a.Ng * a.ldb >= (1L << 31)) return 0;
+  if (a.Cs % 64 != 0 || a.Kd % 64 != 0 || a.Kd < 64 || (a.Kd < 256 && !force)) return false;
+  if (a.ntaps < 1 || a.ntaps > 9) return false;
+  if ((long)a.Hs * a.Ws * a.Cs * ((a.M + a.P * a.Q - 1) / (a.P * a.Q)) >= (1L << 31)) return false;
+  if ((long)a.Ng * a.ldb >= (1L << 31)) return false;
+  return true;
+}
+
+// fp32 workspace (floats) a split launch of this pass would use; 0: unsplit
+inline long conv_dma_split_ws(const CDArgs& a, int force = 0) {
+  if (!cd_base_ok(a, force)) return 0;
+  const int pick = conv_dma_pick_bn(a.M, a.Ng, a.Kd, force);
+  if (!pick || force || (a.Ng / 8) > 256) return 0;
+  const CdSplit p = cd_split_plan(a, pick, cd_cus());
+  return p.sp > 1 ? (long)p.sp * a.M * a.Ng : 0;
+}
+
+// returns 0 (not for this core) or the tile height BM of the launch. ws /
+// ws_floats: scratch for split-K (conv_dma_split_ws floats; none -> unsplit)
+inline int launch_conv_dma(const CDArgs& a, const Epi& ep, hipStream_t s, int force = 0, float* ws = nullptr,
+                           long ws_floats = 0) {
+  if (!cd_base_ok(a, force)) return 0;
   const int pick = conv_dma_pick_bn(a.M, a.Ng, a.Kd, force);
   if (!pick) return 0;
+  if (ws && !force && !ep.c_f32 && ep.mode != 2 && !ep.bnx && a.Ng / 8 <= 256) {
+    const CdSplit p = cd_split_plan(a, pick, cd_cus());
+    const int sp = p.sp;
+    if (sp > 1 && (long)sp * a.M * a.Ng <= ws_floats) {
+      const int nk = a.Kd / 64, kps = (nk + sp - 1) / sp, z = (nk + kps - 1) / kps;
+      const bool t128 = (p.pick & 0x1000) != 0;
+      const int bm = t128 ? 128 : 256, bn = p.pick & 0xfff;
+      const dim3 grid((unsigned)(((a.M + bm - 1) / bm) * (a.Ng / bn)), (unsigned)z);
+      if (t128) hipLaunchKernelGGL((conv_dma_split_kernel<128, 2, 128>), grid, dim3(256), 0, s, a, ws, kps);
+      else if (bn == 256) hipLaunchKernelGGL((conv_dma_split_kernel<256, 2>), grid, dim3(512), 0, s, a, ws, kps);
+      else if (bn == 128) hipLaunchKernelGGL((conv_dma_split_kernel<128, 2>), grid, dim3(512), 0, s, a, ws, kps);
+      else hipLaunchKernelGGL((conv_dma_split_kernel<64, 1>), grid, dim3(256), 0, s, a, ws, kps);
+      const int rpp = 256 / (a.Ng / 8);
+      int rpb = (a.M + 511) / 512;                       // ~512 reducing blocks
+      rpb = (rpb + rpp - 1) / rpp * rpp;
+      if (rpb < rpp) rpb = rpp;
+      hipLaunchKernelGGL(cd_slab_reduce_kernel, dim3((unsigned)((a.M + rpb - 1) / rpb)), dim3(256), 0, s, ws, z,
+                         a, ep, rpb);
+      return bm;
+    }
+  }
   if (pick & 0x1000) {
     const int tiles = ((a.M + 127) / 128) * (a.Ng / 128);
     hipLaunchKernelGGL((conv_dma_kernel<128, 2, 128>), dim3(tiles), dim3(256), 0, s, a, ep);

@@ -158,8 +158,25 @@ __device__ __forceinline__ void p8_mfma(f32x4_t (&acc)[TI][TJ], const s16x8_t (&
 // The kernel body over one tile: bid = the (XCD-remapped) tile index within
 // the M x N tile grid, kz = the K-split slice. Shared by gemm8p_kernel and the
 // grouped launch (gemm8p_grouped_kernel: many independent problems, one grid).
+// tile index -> (m0, n0): grouped-M order (a.group M-tiles per group) so
+// consecutive tiles share B panels in L2
+template <int BM, int BN>
+__device__ __forceinline__ void p8_tile_origin(const P8Args& a, const int bid, int& m0, int& n0) {
+  const int tiles_m = (a.M + BM - 1) / BM, tiles_n = (a.N + BN - 1) / BN;
+  const int GROUP = a.group;
+  const int per_group = GROUP * tiles_n;
+  const int grp = bid / per_group;
+  const int first_m = grp * GROUP;
+  const int gsize = min(tiles_m - first_m, GROUP);
+  m0 = (first_m + (bid % per_group) % gsize) * BM;
+  n0 = ((bid % per_group) / gsize) * BN;
+}
+
+// kt_lo / kt_hi >= 0: an explicit K-tile range (stream-K segments); else
+// slice kz of a.kps K-tiles
 template <int BM, int BN, int WNW, bool AK, bool BK, int SCHED>
-__device__ __forceinline__ void gemm8p_body(const P8Args& a, const Epi& ep, const int bid, const int kz) {
+__device__ __forceinline__ void gemm8p_body(const P8Args& a, const Epi& ep, const int bid, const int kz,
+                                            const int kt_lo = -1, const int kt_hi = -1) {
   using G = P8Geo<BM, BN, WNW>;
   constexpr bool STAGGER = SCHED == 2 || SCHED == 5;
   constexpr bool TWO_BAR = SCHED == 1 || SCHED == 2 || SCHED == 5;
@@ -172,19 +189,12 @@ __device__ __forceinline__ void gemm8p_body(const P8Args& a, const Epi& ep, cons
   // branch would execute the scalar s_barrier on every wave)
   const bool upper = __builtin_amdgcn_readfirstlane(tid) >= G::THREADS / 2;
 
-  const int tiles_m = (a.M + BM - 1) / BM, tiles_n = (a.N + BN - 1) / BN;
-  const int GROUP = a.group;
-  const int per_group = GROUP * tiles_n;
-  const int grp = bid / per_group;
-  const int first_m = grp * GROUP;
-  const int gsize = min(tiles_m - first_m, GROUP);
-  const int tm = first_m + (bid % per_group) % gsize;
-  const int tn = (bid % per_group) / gsize;
-  const int m0 = tm * BM, n0 = tn * BN;
+  int m0, n0;
+  p8_tile_origin<BM, BN>(a, bid, m0, n0);
 
   const int ktiles = a.K / P8_BK;
-  const int kt0 = kz * a.kps;
-  const int kt1 = min(ktiles, kt0 + a.kps);
+  const int kt0 = kt_lo >= 0 ? kt_lo : kz * a.kps;
+  const int kt1 = kt_lo >= 0 ? kt_hi : min(ktiles, kt0 + a.kps);
   const int nk = kt1 - kt0;
 
   f32x4_t acc[TI][TJ];
@@ -468,5 +478,12 @@ int gemm8p_slab_splits(int M, int N, int K, int tile = 256);
 void gemm8p_slab_force(int sp);   // > 0: forced slab split count (A/B sweeps); 0: heuristic
 // 128 or 256: the tile the auto policy picks for this shape
 int gemm8p_tile(int M, int N, int K);
+// stream-K schedule of the 256^2 kernel (gemm8p_sk.hip): one persistent
+// block per CU over the flattened (tile, K-tile) space, fp32 partial tiles in
+// ws (gemm8p_sk_ws_floats floats), one fixup pass applies ep
+bool gemm8p_sk_ok(bool ak, bool bk, int M, int N, int K, long lda, long ldb);
+long gemm8p_sk_ws_floats(int M, int N, int K);
+void gemm8p_streamk(const bf16_t* A, long lda, bool ak, const bf16_t* B, long ldb, bool bk, int M, int N, int K,
+                    const Epi& ep, float* ws, hipStream_t s);
 
 }  // namespace tam

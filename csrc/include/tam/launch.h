@@ -39,11 +39,29 @@ void gemm_wgrad_grouped(const GGProblem* probs, int n, hipStream_t s);
 bool gemm_wgrad_grouped_ok(int M, int N, int K, long lda, long ldb);
 void gemm_grouped_tile(int t);   // 128 (default) or 256
 
+// split-K slab reduce: C (op)= epilogue(sum_z ws[z][M][N]) -- N % 4 == 0
+void gemm_slab_reduce(const float* ws, int sp, int M, int N, const Epi& ep, hipStream_t s);
+
+// Skinny-M weight-streaming GEMM (gemm_skinny.hip): A K-major [M][K] with
+// M <= 64, B K-major or N-major, K % 64 == 0. sp K-slices (gemm_skinny_splits);
+// sp > 1 needs ws = fp32 [sp][M][N] and N % 4 == 0.
+bool gemm_skinny_ok(bool ak, bool bk, int M, int N, int K, long lda, long ldb);
+int gemm_skinny_splits(int M, int N, int K);
+void gemm_skinny(const bf16_t* A, long lda, const bf16_t* B, long ldb, bool bk, int M, int N, int K,
+                 const Epi& ep, int sp, float* ws, hipStream_t s);
+// on: 0 off / 1 on; force_splits > 0 forces the K-slice count; nst: LDS ring depth 3 or 4
+void gemm_skinny_policy(int on, int force_splits, int nst);
+
 // NHWC convolutions, weights [K][R][S][C] (C, K multiples of 8)
-int conv_fwd(const bf16_t* x, const bf16_t* w, const ConvGeom& g, Epi ep, hipStream_t s);
+// ws / ws_floats: split-K scratch of conv_*_split_ws(g) floats (none: unsplit)
+int conv_fwd(const bf16_t* x, const bf16_t* w, const ConvGeom& g, Epi ep, hipStream_t s, float* ws = nullptr,
+             long ws_floats = 0);
+long conv_fwd_split_ws(const ConvGeom& g);
+long conv_dgrad_split_ws(const ConvGeom& g);
+void conv_split_policy(int p);   // 1: split-K of under-filled LDS-DMA passes (default), 0: off
 // dx[N*H*W][C]; wt = conv_weight_t(w) laid out [C][R][S][K] (ignored for 1x1/s1)
 int conv_dgrad(const bf16_t* dy, const bf16_t* w, const bf16_t* wt, const ConvGeom& g, Epi ep,
-                hipStream_t s);
+               hipStream_t s, float* ws = nullptr, long ws_floats = 0);
 // dw[K][R*S*C] fp32, ep.mode 0 (overwrite) or 1 (accumulate)
 int conv_wgrad(const bf16_t* dy, const bf16_t* x, const ConvGeom& g, Epi ep, hipStream_t s,
                float* dbias = nullptr, bool allow_patch = true);

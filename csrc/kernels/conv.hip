@@ -23,6 +23,9 @@ namespace tam {
 // 0: register-staged igemm only (A/B measurements)
 static int g_conv_dma = 1;
 void conv_dma_policy(int p) { g_conv_dma = p; }
+// split-K of under-filled LDS-DMA conv passes (cd_split_plan): 1 on, 0 off (A/B)
+static int g_conv_split = 1;
+void conv_split_policy(int p) { g_conv_split = p; }
 // 64-channel 3x3 stride-1 passes on the halo-tile kernel (conv_dma.h); 0 for
 // A/B runs against the tap-gather cores
 static int g_conv_halo = [] {
@@ -49,12 +52,26 @@ static bool is_pointwise(const ConvGeom& g) {
 
 // returns 1 when the path taken accumulated the BN statistics into ep.stats
 // (0: none; the BN then reduces the output itself)
-int conv_fwd(const bf16_t* x, const bf16_t* w, const ConvGeom& g, Epi ep, hipStream_t s) {
+// split-K scratch (floats) conv_fwd / conv_dgrad would use on the LDS-DMA
+// core for this geometry (0: the pass runs unsplit); the caller allocates it
+long conv_fwd_split_ws(const ConvGeom& g) {
+  if (!g_conv_dma || g.dil != 1 || !g_conv_split) return 0;
+  return conv_dma_split_ws(cd_fwd_args(nullptr, nullptr, g), g_conv_dma >= 2 ? g_conv_dma - 1 : 0);
+}
+long conv_dgrad_split_ws(const ConvGeom& g) {
+  if (!g_conv_dma || g.dil != 1 || g.stride != 1 || !g_conv_split) return 0;
+  CDArgs a = cd_dgrad_args(nullptr, nullptr, g, 0, 0);
+  const int force = g_conv_dma >= 2 ? g_conv_dma - 1 : (g.C == 64 && a.M >= (1L << 20) ? 1 : 0);
+  return conv_dma_split_ws(a, force);
+}
+
+int conv_fwd(const bf16_t* x, const bf16_t* w, const ConvGeom& g, Epi ep, hipStream_t s, float* ws,
+             long ws_floats) {
   const int M = g.N * g.P * g.Q, Kd = g.R * g.S * g.C;
   if (g_conv_dma && g.dil == 1) {
     CDArgs a = cd_fwd_args(x, w, g);
     if (g_conv_halo && launch_conv_halo(a, ep, s)) return ep.stats ? 1 : 0;
-    const int bm = launch_conv_dma(a, ep, s, g_conv_dma >= 2 ? g_conv_dma - 1 : 0);
+    const int bm = launch_conv_dma(a, ep, s, g_conv_dma >= 2 ? g_conv_dma - 1 : 0, ws, ws_floats);
     if (bm) return ep.stats ? 1 : 0;
   }
   ep.stats = nullptr;
@@ -85,7 +102,7 @@ static void dgrad_tile(const bf16_t* dy, const bf16_t* wt, const ConvGeom& g, co
 // ep.stats -- only the single-launch stride-1 LDS-DMA path produces them;
 // every other path clears ep.stats and returns 0
 int conv_dgrad(const bf16_t* dy, const bf16_t* w, const bf16_t* wt, const ConvGeom& g, Epi ep,
-               hipStream_t s) {
+               hipStream_t s, float* ws, long ws_floats) {
   const int M = g.N * g.H * g.W, Kd = g.R * g.S * g.K;
   if (wt && g_conv_dma && g.dil == 1 && g.stride == 1) {
     // rows = dX pixels over an H x W grid, gathered from dY (P x Q x K), B = Wt [C][R][S][K]
@@ -99,7 +116,7 @@ int conv_dgrad(const bf16_t* dy, const bf16_t* w, const bf16_t* wt, const ConvGe
       return e ? atol(e) : (1L << 20);
     }();
     const int force = g_conv_dma >= 2 ? g_conv_dma - 1 : (g.C == 64 && a.M >= dg64_min_m ? 1 : 0);
-    const int bm = launch_conv_dma(a, ep, s, force);
+    const int bm = launch_conv_dma(a, ep, s, force, ws, ws_floats);
     if (bm) return ep.stats ? 1 : 0;
   }
   ep.stats = nullptr;

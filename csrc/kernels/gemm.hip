@@ -206,10 +206,14 @@ void gemm8p_splitk(const bf16_t* A, long lda, bool ak, const bf16_t* B, long ldb
   launch_gemm8p(A, lda, ak, B, ldb, bk, M, N, K, se, splits, s, g_p8_sched, tile);
   const int ktiles = K / P8_BK;
   const int z = cdiv(ktiles, cdiv(ktiles, splits));   // slabs actually written
+  gemm_slab_reduce(ws, z, M, N, ep, s);
+}
+
+void gemm_slab_reduce(const float* ws, int sp, int M, int N, const Epi& ep, hipStream_t s) {
   const long n4 = (long)M * N / 4;
   long blocks = (n4 + 255) / 256;
   blocks = blocks > 2048 ? 2048 : blocks;
-  hipLaunchKernelGGL(p8_slab_reduce_kernel, dim3((unsigned)blocks), dim3(256), 0, s, ws, z, M, N, ep);
+  hipLaunchKernelGGL(p8_slab_reduce_kernel, dim3((unsigned)blocks), dim3(256), 0, s, ws, sp, M, N, ep);
 }
 
 // atomic split-K count (fp32 outputs) that fills the chip (>= 4 K-tiles per split)

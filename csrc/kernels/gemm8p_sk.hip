@@ -1,0 +1,139 @@
+// tiresias_amd — stream-K schedule of the 256^2 gemm8p kernel for GEMMs
+// whose tile grid is a fraction of the chip but whose K is long: the GNMT
+// vocab projections 3200x2048x32000 (104 tiles of 500 K-tiles on 256 CUs)
+// and kin. Uniform split-K cannot balance those (104 x sp is never close
+// to a multiple of 256 without tiny slices: 2 slabs = 81 % of the CUs,
+// VERDICT r3 item 7b); stream-K gives every CU the same number of
+// K-iterations of the flattened (tile, K-tile) space (Osama et al.,
+// "Stream-K", PPoPP'23 -- the decomposition, not any code):
+//  * one persistent block per CU (256^2 tiles run one per CU), block b owns
+//    iterations [b W / P, (b+1) W / P) with W = tiles x K-tiles; its range
+//    crosses at most a few tile boundaries -> one segment per tile touched,
+//    each run by the unchanged gemm8p body over an explicit K range.
+//  * every segment writes its raw fp32 partial tile to a compact slab
+//    ws[b + t][256][256] (slot b + t is unique per (block, tile) pair);
+//    a fixup pass (4 blocks per tile) sums a tile's segments in block order
+//    -- deterministic -- and applies the real epilogue (alpha / bias / relu
+//    / mask / store or accumulate, bf16 or fp32).
+//  * used only where every tile is shared (W / P < K-tiles), so no segment
+//    ever needs the epilogue in the main kernel; picked per shape by the
+//    measured routing (ops.cpp gemm_dispatch), next to uniform split-K.
+#include "tam/launch.h"
+#include "tam/tiles.h"
+#include "tam/gemm8p.h"
+
+namespace tam {
+
+constexpr int SK_T = 256;
+
+template <bool AK, bool BK>
+__global__ void __launch_bounds__(512, 1) gemm8p_sk_kernel(P8Args a, float* ws, long W, int nblk) {
+  const int b = xcd_remap(blockIdx.x, gridDim.x);   // neighbouring ranges on one XCD
+  const int kt = a.K / P8_BK;
+  long i0 = (long)b * W / nblk;
+  const long i1 = (long)(b + 1) * W / nblk;
+  while (i0 < i1) {                                  // block-uniform
+    const int t = (int)(i0 / kt);
+    const int k0 = (int)(i0 % kt);
+    const int k1 = (int)min((long)kt, (long)k0 + (i1 - i0));
+    int m0, n0;
+    p8_tile_origin<SK_T, SK_T>(a, t, m0, n0);
+    Epi e;
+    // compact slab: element (row, col) of the tile at (row - m0) * 256 + col - n0
+    e.c = (void*)((uintptr_t)(ws + (long)(b + t) * SK_T * SK_T) - ((uintptr_t)m0 * SK_T + n0) * sizeof(float));
+    e.ldc = SK_T;
+    e.c_f32 = 1;
+    e.mode = 0;
+    gemm8p_body<SK_T, SK_T, 4, AK, BK, 4>(a, e, t, 0, k0, k1);
+    __syncthreads();                                 // epilogue LDS reads before the next prologue's DMA
+    i0 += k1 - k0;
+  }
+}
+
+// 4 blocks per tile (64 rows each); thread -> 4 columns x 16 rows
+__global__ void __launch_bounds__(256) gemm8p_sk_fixup(const float* __restrict__ ws, P8Args a, Epi ep, long W,
+                                                       int nblk) {
+  const int t = blockIdx.x >> 2, quarter = blockIdx.x & 3;
+  const int kt = a.K / P8_BK;
+  const long i0 = (long)t * kt, i1 = i0 + kt;
+  int b = (int)(i0 * nblk / W);
+  while (b > 0 && (long)b * W / nblk > i0) --b;
+  while ((long)(b + 1) * W / nblk <= i0) ++b;
+  int m0, n0;
+  p8_tile_origin<SK_T, SK_T>(a, t, m0, n0);
+  const int c4 = threadIdx.x & 63, r0 = quarter * 64 + (threadIdx.x >> 6);
+  float4 acc[16];
+#pragma unroll
+  for (int j = 0; j < 16; ++j) acc[j] = make_float4(0.f, 0.f, 0.f, 0.f);
+  for (int bb = b; bb < nblk && (long)bb * W / nblk < i1; ++bb) {
+    const float* slab = ws + (long)(bb + t) * SK_T * SK_T;
+#pragma unroll
+    for (int j = 0; j < 16; ++j) {
+      const float4 v = *(const float4*)(slab + (r0 + 4 * j) * SK_T + 4 * c4);
+      acc[j].x += v.x; acc[j].y += v.y; acc[j].z += v.z; acc[j].w += v.w;
+    }
+  }
+#pragma unroll
+  for (int j = 0; j < 16; ++j) {
+    const int row = m0 + r0 + 4 * j;
+    if (row >= a.M) continue;
+    const float vv[4] = {acc[j].x, acc[j].y, acc[j].z, acc[j].w};
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      const int col = n0 + 4 * c4 + e;
+      if (col >= a.N) continue;
+      float v = vv[e] * ep.alpha + (ep.bias ? bf2f(ep.bias[col]) : 0.f);
+      if (ep.relu) v = fmaxf(v, 0.f);
+      if (ep.mask && bf2f(ep.mask[(long)row * ep.ldm + col]) <= 0.f) v = 0.f;
+      const long off = (long)row * ep.ldc + col;
+      if (ep.c_f32) {
+        float* c = (float*)ep.c;
+        if (ep.mode == 2) atomicAdd(c + off, v);
+        else c[off] = ep.mode == 1 ? c[off] + v : v;
+      } else {
+        bf16_t* c = (bf16_t*)ep.c;
+        c[off] = f2bf(ep.mode == 1 ? v + bf2f(c[off]) : v);
+      }
+    }
+  }
+}
+
+static int sk_blocks() {
+  static int n = 0;
+  if (!n) {
+    int dev = 0;
+    TAM_HIP_CHECK(hipGetDevice(&dev));
+    TAM_HIP_CHECK(hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev));
+    if (n < 1) n = 256;
+  }
+  return n;
+}
+
+long gemm8p_sk_ws_floats(int M, int N, int K) {
+  const long tiles = (long)cdiv(M, SK_T) * cdiv(N, SK_T);
+  return (tiles + sk_blocks()) * SK_T * SK_T;
+}
+
+bool gemm8p_sk_ok(bool ak, bool bk, int M, int N, int K, long lda, long ldb) {
+  if (!gemm8p_ok(ak, bk, M, N, K, lda, ldb)) return false;
+  const long tiles = (long)cdiv(M, SK_T) * cdiv(N, SK_T);
+  const long kt = K / P8_BK, P = sk_blocks();
+  const long per = tiles * kt / P;
+  return tiles < P && per < kt && per >= 8;     // every tile shared; >= 8 K-tiles per block
+}
+
+void gemm8p_streamk(const bf16_t* A, long lda, bool ak, const bf16_t* B, long ldb, bool bk, int M, int N, int K,
+                    const Epi& ep, float* ws, hipStream_t s) {
+  const int P = sk_blocks();
+  const int tiles = cdiv(M, SK_T) * cdiv(N, SK_T);
+  const long W = (long)tiles * (K / P8_BK);
+  P8Args g{A, lda, B, ldb, M, N, K, K / P8_BK, 4};
+  const dim3 grid(P), blk(512);
+  if (ak && bk) hipLaunchKernelGGL((gemm8p_sk_kernel<true, true>), grid, blk, 0, s, g, ws, W, P);
+  else if (ak) hipLaunchKernelGGL((gemm8p_sk_kernel<true, false>), grid, blk, 0, s, g, ws, W, P);
+  else if (bk) hipLaunchKernelGGL((gemm8p_sk_kernel<false, true>), grid, blk, 0, s, g, ws, W, P);
+  else hipLaunchKernelGGL((gemm8p_sk_kernel<false, false>), grid, blk, 0, s, g, ws, W, P);
+  hipLaunchKernelGGL(gemm8p_sk_fixup, dim3(tiles * 4), dim3(256), 0, s, ws, g, ep, W, P);
+}
+
+}  // namespace tam

@@ -132,6 +132,82 @@ def test_gemm_layouts(gpu, M, N, K, ak, bk):
     assert rel_err(cb, ref) < 1e-2
 
 
+@pytest.mark.parametrize("M,N,K", [(32, 4096, 25088), (32, 25088, 4096), (32, 1000, 4096), (1, 1024, 1024),
+                                   (17, 1032, 2048), (48, 2048, 1536), (64, 4096, 4096)])
+@pytest.mark.parametrize("bk", [True, False])
+@pytest.mark.parametrize("nst,sp", [(3, 0), (4, 0), (3, 1)])
+def test_gemm_skinny(gpu, M, N, K, bk, nst, sp):
+    """Skinny-M weight-streaming GEMM (gemm_skinny.hip; the VGG classifier
+    shapes and ragged M / N edges): exact on small-integer operands (any
+    layout / swizzle / slice bookkeeping bug shows), then random operands
+    with every epilogue (bias + relu, relu mask, accumulate, fp32 out) vs
+    fp32 torch, split-K on the slab reduce and unsplit."""
+    if not bk and N % 8:
+        pytest.skip("N-major W needs N % 8 == 0")
+    T().gemm_skinny_policy(1, sp, nst)
+    try:
+        torch.manual_seed(M + N + K)
+        A = torch.randint(-2, 3, (M, K), device=gpu).to(BF)
+        W = torch.randint(-2, 3, (N, K), device=gpu).to(BF)
+        b = W if bk else W.t().contiguous()
+        c = torch.empty(M, N, device=gpu)
+        T().gemm(A, True, b, bk, c, 0, None, False, None, 1.0, False)
+        ref = A.float() @ W.float().t()
+        assert torch.equal(c, ref)
+        A = torch.randn(M, K, device=gpu).to(BF)
+        W = (torch.randn(N, K, device=gpu) / 8).to(BF)
+        b = W if bk else W.t().contiguous()
+        bias = torch.randn(N, device=gpu).to(BF)
+        ref = A.float() @ W.float().t()
+        y = torch.empty(M, N, device=gpu, dtype=BF)
+        T().gemm(A, True, b, bk, y, 0, bias, True, None, 1.0, False)
+        assert rel_err(y, torch.relu(ref + bias.float())) < 1e-2
+        mask = torch.randn(M, N, device=gpu).to(BF)
+        y = torch.empty(M, N, device=gpu, dtype=BF)
+        T().gemm(A, True, b, bk, y, 0, None, False, mask, 1.0, False)
+        assert rel_err(y, ref * (mask.float() > 0)) < 1e-2
+        acc = torch.full((M, N), 0.5, device=gpu)
+        T().gemm(A, True, b, bk, acc, 1, None, False, None, 2.0, False)
+        assert rel_err(acc, 2 * ref + 0.5) < 1e-5
+    finally:
+        T().gemm_skinny_policy(1, 0, 3)
+
+
+@pytest.mark.parametrize("ak,bk", [(True, True), (True, False), (False, True), (False, False)])
+@pytest.mark.parametrize("M,N,K", [(520, 392, 22016), (3200, 2048, 32000)])
+def test_gemm8p_streamk(gpu, ak, bk, M, N, K):
+    """Stream-K schedule of the 256^2 kernel (gemm8p_sk.hip): segments of
+    the flattened (tile, K-tile) space, partial tiles + fixup. Exact on
+    small-integer operands (segment bookkeeping), then bf16 bias + relu and
+    fp32 accumulate epilogues vs fp32 torch."""
+    T().gemm8p_policy(3, 4)
+    T().gemm8p_sk_force(1)
+    try:
+        torch.manual_seed(M)
+        A = torch.randint(-2, 3, (M, K), device=gpu).to(BF)
+        B = torch.randint(-2, 3, (K, N), device=gpu).to(BF)
+        a = A if ak else A.t().contiguous()
+        b = B.t().contiguous() if bk else B
+        c = torch.empty(M, N, device=gpu)
+        T().gemm(a, ak, b, bk, c, 0, None, False, None, 1.0, False)
+        assert torch.equal(c, A.float() @ B.float())
+        A = torch.randn(M, K, device=gpu).to(BF)
+        B = (torch.randn(K, N, device=gpu) / 16).to(BF)
+        a = A if ak else A.t().contiguous()
+        b = B.t().contiguous() if bk else B
+        ref = A.float() @ B.float()
+        bias = torch.randn(N, device=gpu).to(BF)
+        y = torch.empty(M, N, device=gpu, dtype=BF)
+        T().gemm(a, ak, b, bk, y, 0, bias, True, None, 1.0, False)
+        assert rel_err(y, torch.relu(ref + bias.float())) < 1e-2
+        acc = torch.full((M, N), 0.5, device=gpu)
+        T().gemm(a, ak, b, bk, acc, 1, None, False, None, 1.0, False)
+        assert rel_err(acc, ref + 0.5) < 1e-5
+    finally:
+        T().gemm8p_sk_force(0)
+        T().gemm8p_policy(1, 4)
+
+
 # every tile config of the LDS-DMA GEMM (gemm_dma.h), all majorities, edge
 # tiles, bf16 staged epilogue with bias/relu/mask/accumulate, fp32 split-K
 @pytest.mark.parametrize("cfg", [0, 1, 2, 3])
@@ -419,6 +495,60 @@ def test_conv_fwd_dgrad_wgrad(gpu, cfg):
     T().conv_wgrad(dy, x, dw, st, pd, 1, 0, db)
     assert rel_err(db, dy.float().sum((0, 1, 2))) < 1e-4
     assert rel_err(dw, gw.permute(0, 2, 3, 1)) < 1e-4
+
+
+@pytest.mark.parametrize("cfg", [(8, 7, 7, 512, 512, 3, 1, 1), (16, 14, 14, 256, 256, 3, 1, 1),
+                                 (8, 7, 7, 2048, 512, 1, 1, 0), (8, 7, 7, 512, 2048, 1, 1, 0),
+                                 (5, 9, 7, 256, 384, 3, 1, 1)])
+def test_conv_split_k(gpu, cfg):
+    """Split-K of under-filled LDS-DMA conv passes (ResNet-50's 7x7 / 14x14
+    stages, ragged M): fwd with bias + relu and with the BatchNorm sums of
+    the stored output, dgrad with the relu-backward mask (both the re-laying
+    and the pre-laid entry points), each vs fp32 torch and vs the unsplit
+    launch (conv_split_policy 0)."""
+    N, H, W, C, K, R, st, pd = cfg
+    torch.manual_seed(5)
+    x = torch.randn(N, H, W, C, device=gpu).to(BF)
+    w = (torch.randn(K, R, R, C, device=gpu) / math.sqrt(R * R * C)).to(BF)
+    bias = torch.randn(K, device=gpu).to(BF)
+    P = (H + 2 * pd - R) // st + 1
+    Q = (W + 2 * pd - R) // st + 1
+    xf = x.float().permute(0, 3, 1, 2).requires_grad_(True)
+    wf = w.float().permute(0, 3, 1, 2).requires_grad_(True)
+    yf = F.conv2d(xf, wf, stride=st, padding=pd)
+    ref_y = yf.permute(0, 2, 3, 1)
+    dy = torch.randn(N, P, Q, K, device=gpu).to(BF)
+    gx, = torch.autograd.grad(yf, [xf], dy.float().permute(0, 3, 1, 2))
+    mask = torch.randn(N, H, W, C, device=gpu).to(BF)
+    ref_dx = gx.permute(0, 2, 3, 1) * (mask.float() > 0)
+    from tiresias_amd.ops.functional import BN_SHARDS
+    outs = {}
+    try:
+        for pol in (1, 0):
+            T().conv_split_policy(pol)
+            y = torch.empty(N, P, Q, K, device=gpu, dtype=BF)
+            T().conv_fwd(x, w, y, st, pd, 1, bias, True)
+            assert rel_err(y, torch.relu(ref_y + bias.float())) < 1e-2, pol
+            ys = torch.empty_like(y)
+            sums = torch.zeros(BN_SHARDS * 2 * K, device=gpu, dtype=torch.float64)
+            done = T().conv_fwd(x, w, ys, st, pd, 1, None, False, sums)
+            assert rel_err(ys, ref_y) < 1e-2, pol
+            if done:
+                yd = ys.double().reshape(-1, K)
+                tot = sums.view(BN_SHARDS, 2 * K).sum(0)
+                assert rel_err(tot[:K], yd.sum(0)) < 1e-5 and rel_err(tot[K:], (yd * yd).sum(0)) < 1e-5, pol
+            dx = torch.empty_like(x)
+            wt = torch.empty_like(w)
+            T().conv_dgrad(dy, w, wt, dx, st, pd, 1, mask)
+            assert rel_err(dx, ref_dx) < 1e-2, pol
+            dx2 = torch.empty_like(x)
+            T().conv_dgrad_pre(dy, w, wt, dx2, st, pd, 1, mask)
+            assert torch.equal(dx, dx2), pol
+            outs[pol] = (y, ys, dx)
+    finally:
+        T().conv_split_policy(1)
+    for a_, b_ in zip(outs[1], outs[0]):
+        assert rel_err(a_, b_) < 1e-2
 
 
 # LDS-DMA conv core (conv_dma.h): every tile width, stride-2 fwd, 1x1 s2, M

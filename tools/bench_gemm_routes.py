@@ -41,6 +41,8 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--out", default=None)
     ap.add_argument("--min-mflop", type=float, default=100.0, help="skip tiny GEMMs")
+    ap.add_argument("--save", default=None, help="write this process's routing decisions here (run with "
+                    "TAM_GEMM_ROUTES=0 to re-tune every shape instead of loading the shipped table)")
     a = ap.parse_args()
     T = _lib.ops()
     dev = torch.device("cuda", 0)
@@ -81,6 +83,9 @@ def main():
     if a.out:
         with open(a.out, "w") as f:
             json.dump(rows, f, indent=1)
+    if a.save:
+        with open(a.save, "w") as f:
+            f.write(T.gemm_routes())
 
 
 if __name__ == "__main__":

@@ -48,12 +48,15 @@ def main():
                     help="plain-GEMM routing: -1 measured MFMA/hipBLASLt, 0 MFMA only, 1 library")
     ap.add_argument("--conv_policy", type=int, default=1,
                     help="conv core: 1 LDS-DMA where the cost model picks it, 2 wherever eligible, 0 igemm only")
+    ap.add_argument("--conv_split", type=int, default=1,
+                    help="split-K of under-filled LDS-DMA conv passes: 1 on (default), 0 off")
     a = ap.parse_args()
     import torch
     from tiresias_amd.ops import _lib
     _lib.load(required=True)
     torch.ops.tam.gemm_lib_policy(a.lib)
     torch.ops.tam.conv_dma_policy(a.conv_policy)
+    torch.ops.tam.conv_split_policy(a.conv_split)
     res = []
     for m in a.models.split(","):
         r = bench(m, batch=a.batch or None, steps=a.steps, warmup=a.warmup, graph=a.graph,
@@ -64,7 +67,7 @@ def main():
     print(f"gemm routes ({sum('lib' in r for r in routes)} of {len(routes)} plain-GEMM shapes -> hipBLASLt):")
     print("\n".join(routes))
     if a.out:
-        json.dump({"models": res, "lib_policy": a.lib, "gemm_routes": routes}, open(a.out, "w"), indent=1)
+        json.dump({"models": res, "lib_policy": a.lib, "conv_split": a.conv_split, "gemm_routes": routes}, open(a.out, "w"), indent=1)
 
 
 if __name__ == "__main__":
