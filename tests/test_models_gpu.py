@@ -166,6 +166,27 @@ def test_gnmt_branch_streams_match(gpu, overlap):
     assert rel(g.arena.master, e.arena.master) < 1e-3
 
 
+@pytest.mark.parametrize("model", ["vgg_tiny", "gnmt_tiny"])
+@pytest.mark.parametrize("graph", [False, True])
+def test_store_grad_matches_accumulate(gpu, model, graph, monkeypatch):
+    """store_grad weights (first gradient write of a step stores, the
+    optimizer skips zeroing them; ops/functional.py grad_mode) train exactly
+    like the zero-then-accumulate path over several optimizer steps, eager
+    and under hipGraph replay."""
+    import tiresias_amd.ops.functional as Fx
+    runs = []
+    for store in (True, False):
+        monkeypatch.setattr(Fx, "STORE_GRAD", store)
+        t = Trainer(model, gpu, seed=7, use_graph=graph)
+        assert any(p.store_grad for p in t.arena.params) and t.arena.n_store > 0
+        losses = [float(t.step()) for _ in range(5)]
+        torch.cuda.synchronize()
+        runs.append((losses, t.arena.master.clone()))
+    (la, ma), (lb, mb) = runs
+    assert all(abs(x - y) < 1e-3 * max(1.0, abs(y)) for x, y in zip(la, lb)), (la, lb)
+    assert rel(ma, mb) < 1e-4
+
+
 def test_ddp_bucket_event_timing(gpu, monkeypatch):
     """GradBucketer records hipEvents around every step's gradient sync and
     poll_timing() turns finished steps into exposed / span seconds (a

@@ -64,6 +64,7 @@ class Trainer:
         self.use_graph = self._want_graph and self.ddp is None   # graphs for 1-GPU jobs only
         self._graph = None
         self._g_loss = None
+        self._g_written = []     # store_grad params the captured backward writes
         self._warm = 0           # eager steps done before graph capture
         self._side = None
         self._ws = None                 # weight-gradient stream (1-GPU jobs)
@@ -142,9 +143,21 @@ class Trainer:
                     regions.append((a, min(b, A.n_decay), self.spec.wd))
                 if b > A.n_decay:
                     regions.append((max(a, A.n_decay), b, 0.0))
+        elif self.device.type == "cuda":
+            # store_grad params: every step's first gradient write stores
+            # (Fx.grad_mode), so their region is not zeroed -- except a param
+            # nothing wrote this step (its buffer holds an older gradient)
+            for p in A.params:
+                if p.store_grad and p.gw_epoch != A.grad_epoch:
+                    p.grad.zero_()
+            regions = [(0, A.n_store, self.spec.wd, not Fx.STORE_GRAD), (A.n_store, A.n_decay, self.spec.wd, True),
+                       (A.n_decay, A.numel, 0.0, True)]
         else:
             regions = [(0, A.n_decay, self.spec.wd), (A.n_decay, A.numel, 0.0)]
-        for lo, hi, wd in regions:
+        A.grad_epoch += 1
+        for reg in regions:
+            lo, hi, wd = reg[:3]
+            zero = (reg[3] if len(reg) > 3 else True) and not sharded
             if hi <= lo:
                 continue
             w, g, wb = A.master[lo:hi], A.grad[lo:hi], A.shadow[lo:hi]
@@ -154,10 +167,10 @@ class Trainer:
                 # job's own timeout word) only resets the gradient
                 guard = self.model.err if self.uses_persist else None
                 if self.opt == "sgd":
-                    T.sgd_step(w, g, self.opt_state[0][lo:hi], wb, self.lr, 0.9, wd, gscale, False, not sharded, guard)
+                    T.sgd_step(w, g, self.opt_state[0][lo:hi], wb, self.lr, 0.9, wd, gscale, False, zero, guard)
                 else:
                     T.adam_step(w, g, self.opt_state[0][lo:hi], self.opt_state[1][lo:hi], wb, self.lr,
-                                0.9, 0.98, 1e-9, wd, self.step_count, gscale, not sharded, guard)
+                                0.9, 0.98, 1e-9, wd, self.step_count, gscale, zero, guard)
             else:
                 _cpu_opt(self.opt, w, g, self.opt_state, lo, hi, wb, self.lr, wd, gscale, self.step_count)
         if sharded:
@@ -259,7 +272,13 @@ class Trainer:
                     g.capture_end()
             cur.wait_stream(s)
             self._graph = g
+            # the gradient writes baked into the graph (store-mode firsts
+            # included) happen on every replay: _opt_step must see them
+            A = self.arena
+            self._g_written = [p for p in A.params if p.store_grad and p.gw_epoch == A.grad_epoch]
         self._graph.replay()
+        for p in self._g_written:
+            p.gw_epoch = self.arena.grad_epoch
         return self._g_loss
 
     def run(self, iters: int) -> float:

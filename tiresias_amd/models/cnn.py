@@ -165,9 +165,13 @@ class VGG16:
                 cin = v
                 ci += 1
         self.flat = cin * spatial * spatial
-        self.fc = [(A.add("fc0.w", (fc, self.flat), init="normal", std=0.005), A.add("fc0.b", (fc,), init="zeros", decay=False)),
-                   (A.add("fc1.w", (fc, fc), init="normal", std=0.005), A.add("fc1.b", (fc,), init="zeros", decay=False)),
-                   (A.add("fc2.w", (num_classes, fc), init="normal", std=0.005), A.add("fc2.b", (num_classes,), init="zeros", decay=False))]
+        # classifier weights: one dW GEMM per step each (store_grad)
+        self.fc = [(A.add("fc0.w", (fc, self.flat), init="normal", std=0.005, store_grad=True),
+                    A.add("fc0.b", (fc,), init="zeros", decay=False)),
+                   (A.add("fc1.w", (fc, fc), init="normal", std=0.005, store_grad=True),
+                    A.add("fc1.b", (fc,), init="zeros", decay=False)),
+                   (A.add("fc2.w", (num_classes, fc), init="normal", std=0.005, store_grad=True),
+                    A.add("fc2.b", (num_classes,), init="zeros", decay=False))]
         self.num_classes = num_classes
         self.in_ch = in_ch
         self.training = True

@@ -175,11 +175,11 @@ class _LSTMLayer(Function):
                 dGh, Hp = dG2[B:], Hs2[:(T - 1) * B]
             with Fx._OnWgrad(dG2, Hs, x):        # overlaps the next layer's recurrence
                 if T > 1:
-                    _T().gemm(dGh, False, Hp, False, w_hh.grad, 1, None, False, None, 1.0, True)
+                    _T().gemm(dGh, False, Hp, False, w_hh.grad, Fx.grad_mode(w_hh), None, False, None, 1.0, True)
                 # bias gradient colsum(dG) fused into the weight-gradient GEMM
                 # where it runs on the igemm, else a pass inside the op
-                _T().gemm(dG2, False, x.reshape(T * B, I), False, w_ih.grad, 1, None, False, None, 1.0, True,
-                          b.grad)
+                _T().gemm(dG2, False, x.reshape(T * B, I), False, w_ih.grad, Fx.grad_mode(w_ih), None, False, None,
+                          1.0, True, b.grad)
             dx = None
             if ctx.needs_input_grad[0]:
                 dx = torch.empty(T * B, I, dtype=BF16, device=dev)
@@ -258,16 +258,18 @@ class GNMT:
         self.tgt_emb = A.add("tgt_emb", (vocab, H), init="uniform", std=0.1)
 
         def lstm_p(n, i):
-            return (A.add(n + ".w_ih", (4 * H, i), init="uniform", std=0.1),
-                    A.add(n + ".w_hh", (4 * H, H), init="uniform", std=0.1),
+            return (A.add(n + ".w_ih", (4 * H, i), init="uniform", std=0.1, store_grad=True),
+                    A.add(n + ".w_hh", (4 * H, H), init="uniform", std=0.1, store_grad=True),
                     A.add(n + ".b", (4 * H,), init="zeros", decay=False))
 
         self.enc = [lstm_p("enc0.fw", H), lstm_p("enc0.bw", H), lstm_p("enc1", 2 * H)]
         self.enc += [lstm_p(f"enc{i}", H) for i in range(2, enc_layers)]
         self.dec = [lstm_p("dec0", H)] + [lstm_p(f"dec{i}", 2 * H) for i in range(1, dec_layers)]
-        self.att_q = A.add("att.q", (H, H), init="xavier")
-        self.att_kv = A.add("att.kv", (2 * H, H), init="xavier")
-        self.cls_w = A.add("cls.w", (vocab, 2 * H), init="uniform", std=0.1)
+        # weights whose gradient is one GEMM per step (store_grad: stored, not
+        # accumulated into a zeroed buffer)
+        self.att_q = A.add("att.q", (H, H), init="xavier", store_grad=True)
+        self.att_kv = A.add("att.kv", (2 * H, H), init="xavier", store_grad=True)
+        self.cls_w = A.add("cls.w", (vocab, 2 * H), init="uniform", std=0.1, store_grad=True)
         self.cls_b = A.add("cls.b", (vocab,), init="zeros", decay=False)
         self.training = True
         # this job's persistent-LSTM words: [0] barrier timeouts of the current

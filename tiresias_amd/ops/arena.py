@@ -6,16 +6,19 @@ Every job owns exactly four device buffers::
     shadow  bf16 [N]   compute copy every kernel reads (rewritten by the fused
                        optimizer step, never by a separate cast pass)
     grad    fp32 [N]   backward kernels ACCUMULATE straight into it (conv wgrad
-                       split-K atomics, GEMM epilogues, BN/LN reductions); the
-                       bucketed all-reduce reduces it in place; the optimizer
-                       step zeroes it
+                       split-K atomics, GEMM epilogues, BN/LN reductions) --
+                       except a GEMM that writes a weight's gradient FIRST in a
+                       step, which stores; the bucketed all-reduce reduces it in
+                       place; the optimizer step zeroes it (not the leading
+                       store_grad params, whose first write always stores)
     state   fp32 [k*N] optimizer state (momentum / Adam m,v)
 
 so a checkpoint is four memcpys, a preemption spill is one contiguous D2H per
 buffer, a DDP bucket is a contiguous slice, and the optimizer is one launch.
 
-Layout: weight-decayed params first (in registration = forward order), then
-the no-decay params (norm scales/shifts, biases). Every param is padded to
+Layout: weight-decayed params first (in registration = forward order; the
+store_grad ones leading), then the no-decay params (norm scales/shifts,
+biases). Every param is padded to
 64 elements so each view starts 256-B aligned (16-B vector loads).
 """
 from __future__ import annotations
@@ -37,6 +40,11 @@ class Param:
     std: float = 0.02
     decay: bool = True
     fp32_compute: bool = False     # kernels read the fp32 master (norm params)
+    # every step's FIRST write of the gradient is a full-tensor store (a GEMM
+    # in store mode, ops/functional.py::grad_mode): the optimizer step then
+    # skips zeroing it (Arena layout: these params lead the decay region)
+    store_grad: bool = False
+    gw_epoch: int = -1             # Arena.grad_epoch of the last gradient write
     offset: int = 0
     numel: int = 0
     # views (set by Arena.materialize)
@@ -67,6 +75,8 @@ class Arena:
         self.master = self.shadow = self.grad = None
         self.numel = 0
         self.n_decay = 0
+        self.n_store = 0          # [0, n_store): the store_grad params
+        self.grad_epoch = 0       # optimizer steps taken (ops/functional.py::grad_mode)
         self.on_grad_ready: Optional[Callable[[Param], None]] = None
         # autograd anchor: every param-consuming op takes it as an input so
         # outputs require grad even when the data input does not.
@@ -74,16 +84,17 @@ class Arena:
 
     # ----------------------------------------------------------------- build
     def add(self, name: str, shape: Sequence[int], init: str = "normal", std: float = 0.02,
-            decay: bool = True, fp32_compute: bool = False) -> Param:
+            decay: bool = True, fp32_compute: bool = False, store_grad: bool = False) -> Param:
         p = Param(name=name, shape=tuple(int(s) for s in shape), init=init, std=std, decay=decay,
-                  fp32_compute=fp32_compute)
+                  fp32_compute=fp32_compute, store_grad=store_grad and decay)
         p.numel = int(math.prod(p.shape))
         p.arena = self
         self.params.append(p)
         return p
 
     def _order(self) -> List[Param]:
-        return [p for p in self.params if p.decay] + [p for p in self.params if not p.decay]
+        return ([p for p in self.params if p.store_grad] + [p for p in self.params if p.decay and not p.store_grad]
+                + [p for p in self.params if not p.decay])
 
     def materialize(self) -> "Arena":
         off = 0
@@ -93,6 +104,8 @@ class Arena:
             off += _padded(p.numel)
             if p.decay:
                 self.n_decay = off
+            if p.store_grad:
+                self.n_store = off
         self.numel = max(off, _ALIGN)
         dev = self.device
         self.master = torch.zeros(self.numel, dtype=torch.float32, device=dev)

@@ -191,6 +191,26 @@ def join_branch(i: int, *outputs):
 
 
 # ============================================================ Linear
+# first gradient write of a step stores (grad_mode); 0: always accumulate
+# into the optimizer-zeroed buffer (A/B and the equivalence test)
+STORE_GRAD = os.environ.get("TAM_STORE_GRAD", "1") != "0"
+
+
+def grad_mode(p: Param) -> int:
+    """Epilogue mode of a GEMM that writes p's whole gradient: 0 (store) for
+    the first write since the last optimizer step (the buffer's content is
+    dead: zeroed, or a store_grad param's stale gradient), 1 (accumulate)
+    after it. The store skips the fp32 read of C (4 B per weight) and lets the
+    optimizer skip zeroing store_grad params (another 4 B). Only the writers
+    that call this may write such a param's gradient (a bias / BN / conv
+    accumulation into it would be lost); under hipGraph capture the decision
+    is taken once, at capture, like every other host-side choice."""
+    A = p.arena
+    first = p.gw_epoch != A.grad_epoch
+    p.gw_epoch = A.grad_epoch
+    return 0 if (first and STORE_GRAD) else 1
+
+
 class _Linear(Function):
     @staticmethod
     def forward(ctx, x, token, w: Param, b: Optional[Param], relu: bool, in_relu: bool,
@@ -226,15 +246,16 @@ class _Linear(Function):
         dx = None
         deferred = False
         if dy.is_cuda:
-            if (_DEFER_WGRAD is not None and x.dim() == 2 and w.grad.is_contiguous()
+            if (_DEFER_WGRAD is not None and x.dim() == 2 and w.grad.is_contiguous() and not w.store_grad
                     and _group_ok(w.shape[0], w.shape[1], x.shape[0])):
-                _DEFER_WGRAD.append((dy, x, w, b))      # issued by flush_wgrad
+                _DEFER_WGRAD.append((dy, x, w, b))      # issued by flush_wgrad (accumulates)
+                w.gw_epoch = w.arena.grad_epoch
                 deferred = True
             else:
                 with _OnWgrad(dy, x):
                     # the bias gradient colsum(dy) rides on the weight-gradient
                     # GEMM's own A loads (fused on the igemm route, else a pass)
-                    _T().gemm(dy, False, x, False, w.grad, 1, None, False, None, 1.0, True,
+                    _T().gemm(dy, False, x, False, w.grad, grad_mode(w), None, False, None, 1.0, True,
                               b.grad if b is not None else None)
         if ctx.needs_input_grad[0]:
             if dy.is_cuda:

@@ -58,7 +58,7 @@ class _ShapeArena:
         self.shapes = []
         self.token = None
 
-    def add(self, name, shape, init="normal", std=0.02, decay=True, fp32_compute=False):
+    def add(self, name, shape, init="normal", std=0.02, decay=True, fp32_compute=False, store_grad=False):
         from ..ops.arena import Param
 
         p = Param(name=name, shape=tuple(shape))

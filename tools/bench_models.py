@@ -48,6 +48,8 @@ def main():
                     help="plain-GEMM routing: -1 measured MFMA/hipBLASLt, 0 MFMA only, 1 library")
     ap.add_argument("--conv_policy", type=int, default=1,
                     help="conv core: 1 LDS-DMA where the cost model picks it, 2 wherever eligible, 0 igemm only")
+    ap.add_argument("--save_routes", default=None,
+                    help="write the routing table (shipped decisions + the shapes tuned in this run) here")
     ap.add_argument("--conv_split", type=int, default=1,
                     help="split-K of under-filled LDS-DMA conv passes: 1 on (default), 0 off")
     a = ap.parse_args()
@@ -66,6 +68,8 @@ def main():
     routes = torch.ops.tam.gemm_routes().strip().splitlines()
     print(f"gemm routes ({sum('lib' in r for r in routes)} of {len(routes)} plain-GEMM shapes -> hipBLASLt):")
     print("\n".join(routes))
+    if a.save_routes:
+        print("routes ->", _lib.save_routes(a.save_routes), flush=True)
     if a.out:
         json.dump({"models": res, "lib_policy": a.lib, "conv_split": a.conv_split, "gemm_routes": routes}, open(a.out, "w"), indent=1)
 
