@@ -91,6 +91,7 @@ void cast_f32_bf16(const float* x, bf16_t* y, long n, hipStream_t s);
 void sgd_step(float* w, float* g, float* mom, bf16_t* wb, long n, float lr, float momentum,
               float wd, float gscale, int nesterov, int zero_grad, hipStream_t s,
               const unsigned* guard = nullptr);
+void optim_variant(int v);   // streaming optimizer variants (optim.hip), 0 = baseline
 void adam_step(float* w, float* g, float* m, float* v, bf16_t* wb, long n, float lr, float b1,
                float b2, float eps, float wd, int step, float gscale, int zero_grad,
                hipStream_t s, const unsigned* guard = nullptr);

@@ -79,6 +79,125 @@ __global__ void __launch_bounds__(256) adam_kernel(float* __restrict__ w, float*
   }
 }
 
+// Streaming variants (optim_variant): U float4 groups per thread per
+// iteration, all loads issued before any math (U x 4 x 16 B in flight per
+// lane), NT: non-temporal loads / stores (every byte is touched once per
+// step; keeps the step from evicting the next forward's L2 / MALL working
+// set). Tail groups (n4 % U) are handled with the same body at U = 1.
+typedef unsigned u32x2_t __attribute__((ext_vector_type(2)));
+template <int U, bool NT>
+__device__ __forceinline__ float4 ld4(const float* p, long i) {
+  if constexpr (NT) {
+    const f32x4_t r = __builtin_nontemporal_load((const f32x4_t*)p + i);
+    return make_float4(r[0], r[1], r[2], r[3]);
+  } else {
+    return ((const float4*)p)[i];
+  }
+}
+template <bool NT>
+__device__ __forceinline__ void st4(float* p, long i, float4 v) {
+  if constexpr (NT) __builtin_nontemporal_store(f32x4_t{v.x, v.y, v.z, v.w}, (f32x4_t*)p + i);
+  else ((float4*)p)[i] = v;
+}
+template <bool NT>
+__device__ __forceinline__ void st2(bf16_t* p, long i, uint2 v) {
+  if constexpr (NT) __builtin_nontemporal_store(u32x2_t{v.x, v.y}, (u32x2_t*)p + i);
+  else ((uint2*)p)[i] = v;
+}
+
+template <int U, bool NT>
+__global__ void __launch_bounds__(256) adam_stream_kernel(float* __restrict__ w, float* __restrict__ g,
+                                                           float* __restrict__ m, float* __restrict__ v,
+                                                           bf16_t* __restrict__ wb, long n4, float lr, float b1,
+                                                           float b2, float eps, float wd, float bc1, float bc2,
+                                                           float gscale, int zero_grad, const unsigned* guard) {
+  const long stride = (long)gridDim.x * blockDim.x;
+  if (guard != nullptr && *guard != 0u) {
+    for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < n4; i += stride)
+      st4<NT>(g, i, make_float4(0.f, 0.f, 0.f, 0.f));
+    return;
+  }
+  const float ib1 = 1.f / bc1, ib2 = 1.f / bc2;
+  auto body = [&](long i, float4 wv, float4 gv, float4 mv, float4 vv) {
+    float* wp = (float*)&wv; float* gp = (float*)&gv; float* mp = (float*)&mv; float* vp = (float*)&vv;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      const float gr = gp[k] * gscale;
+      mp[k] = b1 * mp[k] + (1.f - b1) * gr;
+      vp[k] = b2 * vp[k] + (1.f - b2) * gr * gr;
+      const float mh = mp[k] * ib1, vh = vp[k] * ib2;
+      wp[k] -= lr * (mh / (sqrtf(vh) + eps) + wd * wp[k]);   // decoupled (AdamW)
+    }
+    st4<NT>(w, i, wv); st4<NT>(m, i, mv); st4<NT>(v, i, vv);
+    if (zero_grad) st4<NT>(g, i, make_float4(0.f, 0.f, 0.f, 0.f));
+    st2<NT>(wb, i, make_uint2(pack_bf2(wp[0], wp[1]), pack_bf2(wp[2], wp[3])));
+  };
+  const long t = blockIdx.x * (long)blockDim.x + threadIdx.x;
+  const long full = n4 / (U * stride) * (U * stride);
+  for (long base = t; base < full; base += U * stride) {
+    float4 wv[U], gv[U], mv[U], vv[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const long i = base + u * stride;
+      wv[u] = ld4<U, NT>(w, i); gv[u] = ld4<U, NT>(g, i); mv[u] = ld4<U, NT>(m, i); vv[u] = ld4<U, NT>(v, i);
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) body(base + u * stride, wv[u], gv[u], mv[u], vv[u]);
+  }
+  for (long i = full + t; i < n4; i += stride)
+    body(i, ld4<1, NT>(w, i), ld4<1, NT>(g, i), ld4<1, NT>(m, i), ld4<1, NT>(v, i));
+}
+
+template <int U, bool NT>
+__global__ void __launch_bounds__(256) sgd_stream_kernel(float* __restrict__ w, float* __restrict__ g,
+                                                          float* __restrict__ mom, bf16_t* __restrict__ wb, long n4,
+                                                          float lr, float momentum, float wd, float gscale,
+                                                          int nesterov, int zero_grad, const unsigned* guard) {
+  const long stride = (long)gridDim.x * blockDim.x;
+  if (guard != nullptr && *guard != 0u) {
+    for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < n4; i += stride)
+      st4<NT>(g, i, make_float4(0.f, 0.f, 0.f, 0.f));
+    return;
+  }
+  auto body = [&](long i, float4 wv, float4 gv, float4 mv) {
+    float* wp = (float*)&wv; float* gp = (float*)&gv; float* mp = (float*)&mv;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      float d = gp[k] * gscale + wd * wp[k];
+      mp[k] = momentum * mp[k] + d;
+      d = nesterov ? d + momentum * mp[k] : mp[k];
+      wp[k] -= lr * d;
+    }
+    st4<NT>(w, i, wv); st4<NT>(mom, i, mv);
+    if (zero_grad) st4<NT>(g, i, make_float4(0.f, 0.f, 0.f, 0.f));
+    st2<NT>(wb, i, make_uint2(pack_bf2(wp[0], wp[1]), pack_bf2(wp[2], wp[3])));
+  };
+  const long t = blockIdx.x * (long)blockDim.x + threadIdx.x;
+  const long full = n4 / (U * stride) * (U * stride);
+  for (long base = t; base < full; base += U * stride) {
+    float4 wv[U], gv[U], mv[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const long i = base + u * stride;
+      wv[u] = ld4<U, NT>(w, i); gv[u] = ld4<U, NT>(g, i); mv[u] = ld4<U, NT>(mom, i);
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) body(base + u * stride, wv[u], gv[u], mv[u]);
+  }
+  for (long i = full + t; i < n4; i += stride) body(i, ld4<1, NT>(w, i), ld4<1, NT>(g, i), ld4<1, NT>(mom, i));
+}
+
+// 0: adam_kernel / sgd_kernel (one group per thread per iteration); 1: U=2;
+// 2: U=2 + NT; 3: U=4 + NT; -1 (default): 3 for arrays of >= 64M params, else
+// 0 -- measured: VGG-16's 138M-param SGD step 868 -> 743 us, GNMT's 227M Adam
+// 1.73 -> 1.67 ms, the 26M / 61M arrays equal or slower with the streaming
+// forms (tools/bench_optim.py, profiles/r4/optim_variants.json)
+static int g_optim_variant = -1;
+void optim_variant(int v) { g_optim_variant = v; }
+static int optim_pick(long n4) {
+  return g_optim_variant >= 0 ? g_optim_variant : (n4 >= (16L << 20) ? 3 : 0);
+}
+
 static int ogrid(long n4) {
   long b = (n4 + 255) / 256;
   if (b > 4096) b = 4096;
@@ -88,16 +207,48 @@ static int ogrid(long n4) {
 void sgd_step(float* w, float* g, float* mom, bf16_t* wb, long n, float lr, float momentum,
               float wd, float gscale, int nesterov, int zero_grad, hipStream_t s, const unsigned* guard) {
   // n % 4 == 0 (arena segments are padded to 64 elements)
-  hipLaunchKernelGGL(sgd_kernel, dim3(ogrid(n / 4)), dim3(256), 0, s, w, g, mom, wb, n / 4, lr,
-                     momentum, wd, gscale, nesterov, zero_grad, guard);
+  const dim3 grid(ogrid(n / 4));
+  switch (optim_pick(n / 4)) {
+    case 1:
+      hipLaunchKernelGGL((sgd_stream_kernel<2, false>), grid, dim3(256), 0, s, w, g, mom, wb, n / 4, lr, momentum, wd,
+                         gscale, nesterov, zero_grad, guard);
+      break;
+    case 2:
+      hipLaunchKernelGGL((sgd_stream_kernel<2, true>), grid, dim3(256), 0, s, w, g, mom, wb, n / 4, lr, momentum, wd,
+                         gscale, nesterov, zero_grad, guard);
+      break;
+    case 3:
+      hipLaunchKernelGGL((sgd_stream_kernel<4, true>), grid, dim3(256), 0, s, w, g, mom, wb, n / 4, lr, momentum, wd,
+                         gscale, nesterov, zero_grad, guard);
+      break;
+    default:
+      hipLaunchKernelGGL(sgd_kernel, grid, dim3(256), 0, s, w, g, mom, wb, n / 4, lr, momentum, wd, gscale, nesterov,
+                         zero_grad, guard);
+  }
 }
 
 void adam_step(float* w, float* g, float* m, float* v, bf16_t* wb, long n, float lr, float b1,
                float b2, float eps, float wd, int step, float gscale, int zero_grad,
                hipStream_t s, const unsigned* guard) {
   const float bc1 = 1.f - powf(b1, (float)step), bc2 = 1.f - powf(b2, (float)step);
-  hipLaunchKernelGGL(adam_kernel, dim3(ogrid(n / 4)), dim3(256), 0, s, w, g, m, v, wb, n / 4, lr,
-                     b1, b2, eps, wd, bc1, bc2, gscale, zero_grad, guard);
+  const dim3 grid(ogrid(n / 4));
+  switch (optim_pick(n / 4)) {
+    case 1:
+      hipLaunchKernelGGL((adam_stream_kernel<2, false>), grid, dim3(256), 0, s, w, g, m, v, wb, n / 4, lr, b1, b2, eps,
+                         wd, bc1, bc2, gscale, zero_grad, guard);
+      break;
+    case 2:
+      hipLaunchKernelGGL((adam_stream_kernel<2, true>), grid, dim3(256), 0, s, w, g, m, v, wb, n / 4, lr, b1, b2, eps,
+                         wd, bc1, bc2, gscale, zero_grad, guard);
+      break;
+    case 3:
+      hipLaunchKernelGGL((adam_stream_kernel<4, true>), grid, dim3(256), 0, s, w, g, m, v, wb, n / 4, lr, b1, b2, eps,
+                         wd, bc1, bc2, gscale, zero_grad, guard);
+      break;
+    default:
+      hipLaunchKernelGGL(adam_kernel, grid, dim3(256), 0, s, w, g, m, v, wb, n / 4, lr, b1, b2, eps, wd, bc1, bc2,
+                         gscale, zero_grad, guard);
+  }
 }
 
 __global__ void lstm_guard_step_kernel(unsigned* err) {

@@ -977,10 +977,20 @@ def test_relu_backward(gpu, n):
 
 
 # ------------------------------------------------------------------ optimizers
+@pytest.mark.parametrize("variant", [0, 1, 2, 3])
 @pytest.mark.parametrize("n", [4096 + 64, 9 * 2 ** 20 + 64])
-def test_sgd_adam(gpu, n):
+def test_sgd_adam(gpu, n, variant):
     """Small n: one pass of the grid; 9M+64: grid-stride loop (the grid is
-    capped at 1M float4 groups) with a partial last pass."""
+    capped at 1M float4 groups) with a partial last pass; every streaming
+    variant (optim.hip optim_variant: unrolled, non-temporal)."""
+    T().optim_variant(variant)
+    try:
+        _sgd_adam_check(gpu, n)
+    finally:
+        T().optim_variant(-1)
+
+
+def _sgd_adam_check(gpu, n):
     torch.manual_seed(10)
     w = torch.randn(n, device=gpu); g = torch.randn(n, device=gpu); m = torch.randn(n, device=gpu)
     wb = torch.empty(n, device=gpu, dtype=BF)
