@@ -491,9 +491,11 @@ void conv_dgrad_op(const Tensor& dy, const Tensor& w, const Tensor& wt, const Te
 // deferred weight gradients of many Linear layers in one grouped launch:
 // dw[i] (fp32 [M][N]) += dy[i]^T x[i] (dy [T][M], x [T][N] bf16), db[i] (fp32
 // [M], or an empty tensor for none) += colsum(dy[i])
-void gemm_wgrad_grouped_op(at::TensorList dy, at::TensorList x, at::TensorList dw, at::TensorList db) {
+void gemm_wgrad_grouped_op(at::TensorList dy, at::TensorList x, at::TensorList dw, at::TensorList db,
+                           at::OptionalIntArrayRef modes) {
   TORCH_CHECK(dy.size() == x.size() && dy.size() == dw.size() && dy.size() == db.size(),
               "tam.gemm_wgrad_grouped: list sizes differ");
+  TORCH_CHECK(!modes.has_value() || modes->size() == dy.size(), "tam.gemm_wgrad_grouped: modes size");
   if (dy.empty()) return;
   std::vector<tam::GGProblem> probs(dy.size());
   for (size_t i = 0; i < dy.size(); ++i) {
@@ -517,7 +519,9 @@ void gemm_wgrad_grouped_op(at::TensorList dy, at::TensorList x, at::TensorList d
       TORCH_CHECK(db[i].numel() == M && db[i].is_contiguous(), "tam.gemm_wgrad_grouped: db must be [M]");
       bias = db[i].data_ptr<float>();
     }
-    probs[i] = tam::GGProblem{bp(a), bp(b), c.data_ptr<float>(), bias, M, N, K, M, N};
+    const int mode = modes.has_value() ? (int)(*modes)[i] : 1;
+    TORCH_CHECK(mode == 0 || mode == 1, "tam.gemm_wgrad_grouped: mode must be 0 (store) or 1 (accumulate)");
+    probs[i] = tam::GGProblem{bp(a), bp(b), c.data_ptr<float>(), bias, M, N, K, M, N, mode};
   }
   tam::gemm_wgrad_grouped(probs.data(), (int)probs.size(), cur_stream(dy[0]));
 }
@@ -771,13 +775,16 @@ void embedding_forward_op(const Tensor& table, const Tensor& ids, const Tensor& 
   TORCH_CHECK(ids.scalar_type() == at::kLong && ids.is_contiguous(), "tam.embedding: ids");
   const int64_t D = table.size(1);
   TORCH_CHECK(D % 8 == 0, "tam.embedding: D % 8");
+  TORCH_CHECK(out.numel() == ids.numel() * D, "tam.embedding: out size");
   tam::embedding_forward(bp(table), ids.data_ptr<int64_t>(), bpm(out), ids.numel(), (int)D,
-                         (float)scale, cur_stream(table));
+                         (float)scale, cur_stream(table), table.size(0));
 }
 void embedding_backward_op(const Tensor& dout, const Tensor& ids, const Tensor& gtable, double scale) {
   check_bf16(dout, "dout"); check_f32(gtable, "gtable"); check_contig(dout, "dout");
+  TORCH_CHECK(ids.scalar_type() == at::kLong && ids.is_contiguous() && gtable.dim() == 2 &&
+                  dout.numel() == ids.numel() * gtable.size(1), "tam.embedding_backward: shapes");
   tam::embedding_backward(bp(dout), ids.data_ptr<int64_t>(), gtable.data_ptr<float>(), ids.numel(),
-                          (int)gtable.size(1), (float)scale, cur_stream(dout));
+                          (int)gtable.size(1), (float)scale, cur_stream(dout), gtable.size(0));
 }
 
 void conv_dma_policy_op(int64_t p) { tam::conv_dma_policy((int)p); }
@@ -1032,7 +1039,7 @@ TORCH_LIBRARY(tam, m) {
   m.def("conv_fwd(Tensor x, Tensor w, Tensor(a!) y, int stride, int pad, int dil, Tensor? bias, bool relu, Tensor(b!)? stats=None) -> int", &conv_fwd_op);
   m.def("conv_dgrad(Tensor dy, Tensor w, Tensor(a!) wt, Tensor(b!) dx, int stride, int pad, int dil, Tensor? mask) -> ()", &conv_dgrad_op);
   m.def("conv_weight_t_batch(Tensor[] w, Tensor(a!)[] wt) -> ()", &conv_weight_t_batch_op);
-  m.def("gemm_wgrad_grouped(Tensor[] dy, Tensor[] x, Tensor(a!)[] dw, Tensor(b!)[] db) -> ()", &gemm_wgrad_grouped_op);
+  m.def("gemm_wgrad_grouped(Tensor[] dy, Tensor[] x, Tensor(a!)[] dw, Tensor(b!)[] db, int[]? modes=None) -> ()", &gemm_wgrad_grouped_op);
   m.def("gemm_wgrad_grouped_ok(int M, int N, int K) -> bool", &gemm_wgrad_grouped_ok_op);
   m.def("gemm_grouped_tile(int tile) -> ()", &gemm_grouped_tile_op);
   m.def("conv_dgrad_pre(Tensor dy, Tensor w, Tensor wt, Tensor(a!) dx, int stride, int pad, int dil, Tensor? mask, Tensor(b!)? stats=None, Tensor? bnx=None, Tensor? bnmean=None, Tensor? bnrstd=None) -> int", &conv_dgrad_pre_op);

@@ -74,10 +74,11 @@ void softmax_xent(const bf16_t* logits, const long* labels, bf16_t* dlogits, flo
                   hipStream_t s);
 
 // embedding
+// V = table rows: ids outside [0, V) read zero rows / take no gradient
 void embedding_forward(const bf16_t* table, const long* ids, bf16_t* out, long T, int D,
-                       float scale, hipStream_t s);
+                       float scale, hipStream_t s, long V);
 void embedding_backward(const bf16_t* dout, const long* ids, float* gtable, long T, int D,
-                        float scale, hipStream_t s);
+                        float scale, hipStream_t s, long V);
 
 // misc
 // out[c] += sum_r x[r][c]; ws: COLSUM_MAX_BLOCKS * C floats (C % 8 == 0 path)

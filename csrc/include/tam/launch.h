@@ -25,7 +25,7 @@ void gemm8p_group(int g);   // M-tiles per tile-order group of gemm8p (default 4
 int gemm8p_policy_mode();
 
 // Grouped weight-gradient GEMM (gemm_grouped.hip): for every problem p,
-//   C_p[M][N] += A_p^T B_p  (A_p [K][lda] M-major, B_p [K][ldb] N-major, fp32 C row stride N)
+//   C_p[M][N] (+)= A_p^T B_p  (A_p [K][lda] M-major, B_p [K][ldb] N-major, fp32 C row stride N)
 //   bias_p[M] += column sums of A_p (when bias_p != null)
 // in ONE launch per P8G_MAX problems (gemm8p 128^2 tiles + column-sum blocks).
 struct GGProblem {
@@ -34,6 +34,7 @@ struct GGProblem {
   float* C;
   float* bias;
   int M, N, K, lda, ldb;
+  int mode = 1;      // 0: C = A^T B (store), 1: C += A^T B
 };
 void gemm_wgrad_grouped(const GGProblem* probs, int n, hipStream_t s);
 bool gemm_wgrad_grouped_ok(int M, int N, int K, long lda, long ldb);

@@ -25,16 +25,17 @@
 
 namespace tam {
 
-constexpr int P8G_MAX = 64;   // problems per launch (kernel-argument budget: 64 x 56 B)
+constexpr int P8G_MAX = 64;   // problems per launch (kernel-argument budget: 64 x 64 B)
 
 struct P8GProb {
   const bf16_t* A;   // [K][M] M-major (dY), contiguous
   const bf16_t* B;   // [K][N] N-major (X), contiguous
-  float* C;          // [M][N] fp32, accumulated
+  float* C;          // [M][N] fp32, stored (mode 0) or accumulated (mode 1)
   float* bias;       // optional: [M] += column sums of A
   int M, N, K;
   int t0;            // first GEMM tile (relative to the GEMM part of the grid)
   int c0;            // first column-sum block
+  int mode;          // 0: C = A^T B (a weight's first gradient write of the step), 1: C +=
 };
 
 struct P8Group {
@@ -109,7 +110,7 @@ __global__ void __launch_bounds__(64 * 2 * WNW, (BM == 256 ? 1 : 2)) gemm8p_grou
   ep.c = pr.C;
   ep.ldc = pr.N;
   ep.c_f32 = 1;
-  ep.mode = 1;
+  ep.mode = pr.mode;
   gemm8p_body<BM, BN, WNW, false, false, 4>(a, ep, t - pr.t0, 0);
 }
 
@@ -123,7 +124,7 @@ static int g_gg_tile = [] {
 }();
 void gemm_grouped_tile(int t) { g_gg_tile = t == 256 ? 256 : 128; }
 
-// problems: A [K][lda] (M-major), B [K][ldb] (N-major), C [M][N] fp32 +=,
+// problems: A [K][lda] (M-major), B [K][ldb] (N-major), C [M][N] fp32 = or +=,
 // bias [M] += colsum(A) or null. Host checks the gemm8p conditions (K % 64,
 // M, N >= 128 and % 8, lda / ldb % 8) -- the caller routes anything else to
 // the per-problem gemm(). Launches ceil(n / P8G_MAX) grids.
@@ -138,6 +139,7 @@ void gemm_wgrad_grouped(const GGProblem* probs, int n, hipStream_t s) {
       P8GProb& p = g.p[i];
       p.A = q.A; p.B = q.B; p.C = q.C; p.bias = q.bias;
       p.M = q.M; p.N = q.N; p.K = q.K;
+      p.mode = q.mode;
       p.t0 = tiles;
       p.c0 = cs;
       tiles += cdiv(q.M, T) * cdiv(q.N, T);

@@ -300,15 +300,19 @@ void softmax_xent(const bf16_t* logits, const long* labels, bf16_t* dlogits, flo
 
 // ------------------------------------------------------------------ embedding
 // out[t][:] = table[ids[t]][:] * scale  (D % 8 == 0), 16 B per lane
+// ids outside [0, V) (a batch built for another vocabulary) read as zero
+// rows and take no gradient, instead of faulting the device
 __global__ void embed_fwd_kernel(const bf16_t* __restrict__ table, const long* __restrict__ ids,
-                                 bf16_t* __restrict__ out, long T, int D, float scale) {
+                                 bf16_t* __restrict__ out, long T, int D, float scale, long V) {
   const int d8 = D / 8;
   const long total = T * d8;
   for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < total;
        i += (long)gridDim.x * blockDim.x) {
     const long t = i / d8;
     const int c = (int)(i % d8) * 8;
-    const uint4 u = *(const uint4*)(table + ids[t] * D + c);
+    const long id = ids[t];
+    const uint4 u = (unsigned long)id < (unsigned long)V ? *(const uint4*)(table + id * D + c)
+                                                          : make_uint4(0u, 0u, 0u, 0u);
     if (scale == 1.f) {
       *(uint4*)(out + t * D + c) = u;
     } else {
@@ -323,24 +327,25 @@ __global__ void embed_fwd_kernel(const bf16_t* __restrict__ table, const long* _
 }
 // grad_table[ids[t]] += dout[t] * scale  (fp32 atomics; rows of D contiguous)
 __global__ void embed_bwd_kernel(const bf16_t* __restrict__ dout, const long* __restrict__ ids,
-                                 float* __restrict__ gtable, long T, int D, float scale) {
+                                 float* __restrict__ gtable, long T, int D, float scale, long V) {
   const long total = T * D;
   for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < total;
        i += (long)gridDim.x * blockDim.x) {
     const long t = i / D;
     const int c = (int)(i % D);
-    atomicAdd(gtable + ids[t] * D + c, bf2f(dout[i]) * scale);
+    const long id = ids[t];
+    if ((unsigned long)id < (unsigned long)V) atomicAdd(gtable + id * D + c, bf2f(dout[i]) * scale);
   }
 }
 void embedding_forward(const bf16_t* table, const long* ids, bf16_t* out, long T, int D,
-                       float scale, hipStream_t s) {
+                       float scale, hipStream_t s, long V) {
   hipLaunchKernelGGL(embed_fwd_kernel, dim3(grid_cap(T * D / 8)), dim3(256), 0, s, table, ids, out,
-                     T, D, scale);
+                     T, D, scale, V);
 }
 void embedding_backward(const bf16_t* dout, const long* ids, float* gtable, long T, int D,
-                        float scale, hipStream_t s) {
+                        float scale, hipStream_t s, long V) {
   hipLaunchKernelGGL(embed_bwd_kernel, dim3(grid_cap(T * D)), dim3(256), 0, s, dout, ids, gtable, T,
-                     D, scale);
+                     D, scale, V);
 }
 
 // ------------------------------------------------------------- column sums

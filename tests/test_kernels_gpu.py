@@ -953,6 +953,20 @@ def test_embedding(gpu):
     T().embedding_backward(dout, ids.reshape(-1), g, 2.0)
     ref = torch.zeros(1000, 64, device=gpu).index_add_(0, ids.reshape(-1), dout.float() * 2)
     assert rel_err(g, ref) < 1e-5
+    # ids outside the table (a batch of another vocabulary): zero rows, no
+    # gradient, no device fault
+    bad = ids.reshape(-1).clone()
+    bad[::5] = 1000 + bad[::5]
+    bad[1::7] = -1
+    ok = (bad >= 0) & (bad < 1000)
+    out2 = torch.empty_like(out)
+    T().embedding_forward(table, bad, out2, 2.0)
+    torch.cuda.synchronize()
+    assert torch.equal(out2[ok], out[ok]) and torch.count_nonzero(out2[~ok]) == 0
+    g2 = torch.zeros(1000, 64, device=gpu)
+    T().embedding_backward(dout, bad, g2, 2.0)
+    ref2 = torch.zeros(1000, 64, device=gpu).index_add_(0, bad[ok], dout.float()[ok] * 2)
+    assert rel_err(g2, ref2) < 1e-5
 
 
 @pytest.mark.parametrize("R,C", [(4096, 2048), (3200, 32000), (100, 24), (777, 512), (64, 4096),

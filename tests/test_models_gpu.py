@@ -140,6 +140,31 @@ def test_grouped_wgrad_matches(gpu, overlap, monkeypatch):
     assert rel(g.arena.master, e.arena.master) < 1e-3
 
 
+def test_gnmt_lstm_grouped_wgrad_matches(gpu, monkeypatch):
+    """GNMT's per-layer LSTM weight gradients (dW_hh, dW_ih + the bias column
+    sums) as one grouped launch (models/gnmt.py LSTM_GROUPED_WGRAD, store-
+    mode first writes) give the gradients and the training trajectory of the
+    per-GEMM path (batch 64, so every layer's problems are grouped)."""
+    import tiresias_amd.models.gnmt as G
+    kw = dict(hidden=256, enc_layers=3, dec_layers=2, heads=4)      # the batch's 32000-token vocabulary
+    runs = []
+    for grouped in (True, False):
+        monkeypatch.setattr(G, "LSTM_GROUPED_WGRAD", grouped)
+        t = Trainer("gnmt", gpu, seed=8, batch=64, model_kwargs=kw)
+        loss = float(t._fwd_bwd())
+        torch.cuda.synchronize()
+        grad = t.arena.grad.clone()
+        t.arena.grad.zero_()
+        losses = [float(t.step()) for _ in range(3)]
+        torch.cuda.synchronize()
+        runs.append((loss, grad, losses, t.arena.master.clone()))
+    (la, ga, lsa, ma), (lb, gb, lsb, mb) = runs
+    assert abs(la - lb) < 1e-4 * max(1.0, abs(lb))
+    assert rel(ga, gb) < 2e-3
+    assert all(abs(x - y) < 1e-2 * max(1.0, abs(y)) for x, y in zip(lsa, lsb)), (lsa, lsb)
+    assert rel(ma, mb) < 1e-3
+
+
 @pytest.mark.parametrize("overlap", [False, True])
 def test_gnmt_branch_streams_match(gpu, overlap):
     """GNMT's independent recurrences on branch streams (bidirectional
@@ -166,7 +191,7 @@ def test_gnmt_branch_streams_match(gpu, overlap):
     assert rel(g.arena.master, e.arena.master) < 1e-3
 
 
-@pytest.mark.parametrize("model", ["vgg_tiny", "gnmt_tiny"])
+@pytest.mark.parametrize("model", ["vgg_tiny", "gnmt_tiny", "transformer"])
 @pytest.mark.parametrize("graph", [False, True])
 def test_store_grad_matches_accumulate(gpu, model, graph, monkeypatch):
     """store_grad weights (first gradient write of a step stores, the
@@ -177,7 +202,9 @@ def test_store_grad_matches_accumulate(gpu, model, graph, monkeypatch):
     runs = []
     for store in (True, False):
         monkeypatch.setattr(Fx, "STORE_GRAD", store)
-        t = Trainer(model, gpu, seed=7, use_graph=graph)
+        kw = dict(enc_layers=2, dec_layers=2) if model == "transformer" else None
+        t = Trainer(model, gpu, seed=7, use_graph=graph, batch=4 if model == "transformer" else None,
+                    model_kwargs=kw)
         assert any(p.store_grad for p in t.arena.params) and t.arena.n_store > 0
         losses = [float(t.step()) for _ in range(5)]
         torch.cuda.synchronize()

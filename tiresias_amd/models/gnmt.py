@@ -21,6 +21,8 @@ W_hh slices resident in VGPRs), the per-step path remaining the fallback.
 """
 from __future__ import annotations
 
+import os
+
 import torch
 from torch.autograd import Function
 
@@ -41,6 +43,10 @@ FUSED_STEP = False
 # per timestep; they decline (return False) for shapes / residency they do not
 # cover and the per-step path runs
 PERSIST = True
+# LSTM weight gradients (dW_hh, dW_ih, the bias column sums) of a layer as
+# one grouped launch (csrc/kernels/gemm_grouped.hip) instead of two routed
+# GEMMs with split-K slab reduces + a column-sum pass; 0: the per-GEMM path
+LSTM_GROUPED_WGRAD = os.environ.get("TAM_LSTM_GROUPED", "1") != "0"
 _SYNCS: list = []          # recent barrier/error words (tests read the error flags)
 
 
@@ -173,13 +179,23 @@ class _LSTMLayer(Function):
                 dGh, Hp = dG2[:(T - 1) * B], Hs2[B:]
             else:
                 dGh, Hp = dG2[B:], Hs2[:(T - 1) * B]
+            x2 = x.reshape(T * B, I)
+            grouped = (LSTM_GROUPED_WGRAD and T > 1 and x2.is_contiguous() and Fx._group_ok(4 * Hd, Hd, (T - 1) * B)
+                       and Fx._group_ok(4 * Hd, I, T * B))
             with Fx._OnWgrad(dG2, Hs, x):        # overlaps the next layer's recurrence
-                if T > 1:
-                    _T().gemm(dGh, False, Hp, False, w_hh.grad, Fx.grad_mode(w_hh), None, False, None, 1.0, True)
-                # bias gradient colsum(dG) fused into the weight-gradient GEMM
-                # where it runs on the igemm, else a pass inside the op
-                _T().gemm(dG2, False, x.reshape(T * B, I), False, w_ih.grad, Fx.grad_mode(w_ih), None, False, None,
-                          1.0, True, b.grad)
+                if grouped:
+                    # dW_hh, dW_ih and the bias colsum in ONE launch (no split-K
+                    # slabs, no separate column-sum passes)
+                    empty = torch.empty(0, dtype=torch.float32, device=dev)
+                    _T().gemm_wgrad_grouped([dGh, dG2], [Hp, x2], [w_hh.grad, w_ih.grad], [empty, b.grad],
+                                            [Fx.grad_mode(w_hh), Fx.grad_mode(w_ih)])
+                else:
+                    if T > 1:
+                        _T().gemm(dGh, False, Hp, False, w_hh.grad, Fx.grad_mode(w_hh), None, False, None, 1.0, True)
+                    # bias gradient colsum(dG) fused into the weight-gradient GEMM
+                    # where it runs on the igemm, else a pass inside the op
+                    _T().gemm(dG2, False, x2, False, w_ih.grad, Fx.grad_mode(w_ih), None, False, None, 1.0, True,
+                              b.grad)
             dx = None
             if ctx.needs_input_grad[0]:
                 dx = torch.empty(T * B, I, dtype=BF16, device=dev)

@@ -40,7 +40,8 @@ class TransformerBase:
                     A.add(n + ".b", (d,), init="zeros", decay=False, fp32_compute=True))
 
         def lin(n, o, i, bias=True):
-            w = A.add(n + ".w", (o, i), init="xavier")
+            # one dW GEMM per step each (grouped launch, store mode): store_grad
+            w = A.add(n + ".w", (o, i), init="xavier", store_grad=True)
             b = A.add(n + ".b", (o,), init="zeros", decay=False) if bias else None
             return (w, b)
 
@@ -61,7 +62,7 @@ class TransformerBase:
         # memory as ONE [L*2d, d] GEMM (per-layer xavier bound): one fwd GEMM,
         # one dgrad, one wgrad instead of L each + L-1 gradient sums
         self.dec_kv = (A.add("dec.kv.w", (dec_layers * 2 * d, d), init="uniform",
-                             std=math.sqrt(6.0 / (3 * d))),
+                             std=math.sqrt(6.0 / (3 * d)), store_grad=True),
                        A.add("dec.kv.b", (dec_layers * 2 * d,), init="zeros", decay=False))
         self.dec_ln = ln("dec.ln")
         self.training = True

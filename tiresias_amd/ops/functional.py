@@ -102,6 +102,9 @@ def defer_wgrad(on: bool, discard: bool = False) -> None:
     global _DEFER_WGRAD
     if not on and _DEFER_WGRAD and not discard:
         raise RuntimeError("defer_wgrad(False) with unflushed weight gradients")
+    if not on and _DEFER_WGRAD:
+        for it in _DEFER_WGRAD:            # dropped writes: the next one must store (grad_mode)
+            it[2].gw_epoch = -1
     _DEFER_WGRAD = [] if on else None
 
 
@@ -127,8 +130,9 @@ def flush_wgrad() -> int:
     with _OnWgrad(*dys, *[it[1] for it in items]):
         empty = torch.empty(0, dtype=torch.float32, device=dys[0].device)
         _T().gemm_wgrad_grouped(dys, [it[1] for it in items], [it[2].grad for it in items],
-                                [it[3].grad if it[3] is not None else empty for it in items])
-    for _, _, w, b in items:
+                                [it[3].grad if it[3] is not None else empty for it in items],
+                                [it[4] for it in items])
+    for _, _, w, b, _ in items:
         w.grad_ready()
         if b is not None:
             b.grad_ready()
@@ -246,10 +250,19 @@ class _Linear(Function):
         dx = None
         deferred = False
         if dy.is_cuda:
-            if (_DEFER_WGRAD is not None and x.dim() == 2 and w.grad.is_contiguous() and not w.store_grad
+            if (_DEFER_WGRAD is not None and x.dim() == 2 and w.grad.is_contiguous()
                     and _group_ok(w.shape[0], w.shape[1], x.shape[0])):
-                _DEFER_WGRAD.append((dy, x, w, b))      # issued by flush_wgrad (accumulates)
-                w.gw_epoch = w.arena.grad_epoch
+                if any(it[2] is w for it in _DEFER_WGRAD):
+                    flush_wgrad()      # a second use of w: its pending write goes first
+                # issued by flush_wgrad, AFTER writers that run in between
+                # (a tied embedding's scatter-add): only a store_grad weight,
+                # which nothing else writes, may store there
+                if w.store_grad:
+                    mode = grad_mode(w)
+                else:
+                    w.gw_epoch = w.arena.grad_epoch
+                    mode = 1
+                _DEFER_WGRAD.append((dy, x, w, b, mode))
                 deferred = True
             else:
                 with _OnWgrad(dy, x):
@@ -913,6 +926,7 @@ class _Embed(Function):
         (flat,) = ctx.saved_tensors
         t = ctx.table
         d2 = dout.reshape(-1, t.shape[1]).contiguous()
+        t.gw_epoch = t.arena.grad_epoch       # written (accumulated) this step: see grad_mode
         if d2.is_cuda:
             with _OnWgrad(d2, flat):           # the table may be tied to a projection
                 _T().embedding_backward(d2, flat, t.grad, ctx.scale)
