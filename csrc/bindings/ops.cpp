@@ -964,10 +964,11 @@ static void check_sync(const Tensor& sync, int64_t B) {
               "tam.lstm_seq: sync must be a contiguous int32 tensor of >= 32 * (4 * B/16 + 1) elements");
 }
 // per-launch co-residency rule + the job's timeout word (see tam::PLOpts)
-static tam::PLOpts pl_opts(const optional<Tensor>& job_err, int64_t grids, int64_t rsv) {
+static tam::PLOpts pl_opts(const optional<Tensor>& job_err, int64_t grids, int64_t rsv, bool zeroed) {
   tam::PLOpts o;
   o.grids = (int)grids;
   o.rsv = (int)rsv;
+  o.zeroed = zeroed ? 1 : 0;
   if (job_err.has_value() && job_err->defined()) {
     TORCH_CHECK(job_err->is_cuda() && job_err->scalar_type() == at::kInt && job_err->numel() >= 2,
                 "tam.lstm_seq: job_err must be an int32 [2] GPU tensor");
@@ -977,7 +978,7 @@ static tam::PLOpts pl_opts(const optional<Tensor>& job_err, int64_t grids, int64
 }
 bool lstm_seq_fwd_op(const Tensor& gx, const Tensor& w_hh, const Tensor& hs, const Tensor& cs,
                      const Tensor& act, bool reverse, const Tensor& sync, const optional<Tensor>& job_err,
-                     int64_t grids, int64_t rsv) {
+                     int64_t grids, int64_t rsv, bool zeroed) {
   check_f32(gx, "gx"); check_bf16(w_hh, "w_hh"); check_bf16(hs, "hs"); check_f32(cs, "cs");
   check_f32(act, "act");
   TORCH_CHECK(hs.dim() == 3 && hs.is_contiguous(), "tam.lstm_seq_forward: hs [T][B][Hd]");
@@ -991,11 +992,11 @@ bool lstm_seq_fwd_op(const Tensor& gx, const Tensor& w_hh, const Tensor& hs, con
   int* sp = sync.data_ptr<int>();
   return tam::lstm_seq_forward(gx.data_ptr<float>(), bp(w_hh), bpm(hs), cs.data_ptr<float>(),
                                act.data_ptr<float>(), (int)T, (int)B, (int)Hd, reverse ? 1 : 0,
-                               (unsigned*)sp, cur_stream(gx), pl_opts(job_err, grids, rsv));
+                               (unsigned*)sp, cur_stream(gx), pl_opts(job_err, grids, rsv, zeroed));
 }
 bool lstm_seq_bwd_op(const Tensor& act, const Tensor& cs, const Tensor& dH, const Tensor& w_hh,
                      const Tensor& dG, bool reverse, const Tensor& sync, const optional<Tensor>& job_err,
-                     int64_t grids, int64_t rsv) {
+                     int64_t grids, int64_t rsv, bool zeroed) {
   check_f32(act, "act"); check_f32(cs, "cs"); check_bf16(w_hh, "w_hh");
   TORCH_CHECK(dH.is_cuda() && (dH.scalar_type() == at::kFloat || dH.scalar_type() == at::kBFloat16),
               "tam.lstm_seq_backward: dH must be an f32 or bf16 CUDA tensor");
@@ -1012,7 +1013,7 @@ bool lstm_seq_bwd_op(const Tensor& act, const Tensor& cs, const Tensor& dH, cons
   int* sp = sync.data_ptr<int>();
   return tam::lstm_seq_backward(act.data_ptr<float>(), cs.data_ptr<float>(), (const float*)dH.data_ptr(),
                                 bp(w_hh), bpm(dG), (int)T, (int)B, (int)Hd, reverse ? 1 : 0, (unsigned*)sp,
-                                dh_bf16, cur_stream(act), pl_opts(job_err, grids, rsv));
+                                dh_bf16, cur_stream(act), pl_opts(job_err, grids, rsv, zeroed));
 }
 
 void lstm_seq_policy_op(int64_t ch) { tam::lstm_seq_policy((int)ch); }
@@ -1082,8 +1083,8 @@ TORCH_LIBRARY(tam, m) {
   m.def("attn_forward(Tensor q, Tensor k, Tensor v, Tensor(a!) o, Tensor(b!) lse, bool causal, float scale, Tensor? kv_len) -> ()", &attn_forward_op);
   m.def("attn_backward(Tensor q, Tensor k, Tensor v, Tensor o, Tensor dout, Tensor lse, Tensor(a!) dq, Tensor(b!) dk, Tensor(c!) dv, Tensor(d!) dq_acc, Tensor(e!) delta, bool causal, float scale, Tensor? kv_len) -> ()", &attn_backward_op);
   m.def("lstm_step_forward(Tensor gx, Tensor w_hh, Tensor? h_prev, Tensor? c_prev, Tensor(a!) c_out, Tensor(b!) h_out, Tensor(c!) act) -> ()", &lstm_step_fwd_op);
-  m.def("lstm_seq_forward(Tensor gx, Tensor w_hh, Tensor(a!) hs, Tensor(b!) cs, Tensor(c!) act, bool reverse, Tensor(d!) sync, Tensor(e!)? job_err=None, int grids=-1, int reserved_cus=0) -> bool", &lstm_seq_fwd_op);
-  m.def("lstm_seq_backward(Tensor act, Tensor cs, Tensor dH, Tensor w_hh, Tensor(a!) dG, bool reverse, Tensor(b!) sync, Tensor(c!)? job_err=None, int grids=-1, int reserved_cus=0) -> bool", &lstm_seq_bwd_op);
+  m.def("lstm_seq_forward(Tensor gx, Tensor w_hh, Tensor(a!) hs, Tensor(b!) cs, Tensor(c!) act, bool reverse, Tensor(d!) sync, Tensor(e!)? job_err=None, int grids=-1, int reserved_cus=0, bool zeroed=False) -> bool", &lstm_seq_fwd_op);
+  m.def("lstm_seq_backward(Tensor act, Tensor cs, Tensor dH, Tensor w_hh, Tensor(a!) dG, bool reverse, Tensor(b!) sync, Tensor(c!)? job_err=None, int grids=-1, int reserved_cus=0, bool zeroed=False) -> bool", &lstm_seq_bwd_op);
   m.def("lstm_seq_policy(int ch) -> ()", &lstm_seq_policy_op);
   m.def("lstm_seq_shards(int ns) -> ()", &lstm_seq_shards_op);
   m.def("gemm_routes_load(str text) -> int", &gemm_routes_load_op);

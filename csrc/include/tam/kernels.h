@@ -123,6 +123,7 @@ void lstm_step_forward(const float* gx, const bf16_t* w_hh, const bf16_t* h_prev
 struct PLOpts {
   int grids = -1, rsv = 0;
   unsigned* job_err = nullptr;
+  int zeroed = 0;    // 1: the caller zeroed the sync words (one fill for a whole step's launches)
 };
 bool lstm_seq_forward(const float* gx, const bf16_t* w_hh, bf16_t* hs, float* cs, float* act, int T,
                       int B, int Hd, int reverse, unsigned* sync, hipStream_t s, const PLOpts& o = PLOpts());

@@ -553,7 +553,7 @@ static bool pl_fwd(const float* gx, const bf16_t* w_hh, bf16_t* hs, float* cs, f
   auto k = lstm_persist_fwd_kernel<KW, CH>;
   if (!pl_fits((const void*)k, 64 * PL_W * CH, grid, o.grids, o.rsv)) return false;
   const int ns = (Hd / (16 * CH)) % g_pl_ns == 0 ? g_pl_ns : 1;
-  zero_async(sync, (size_t)(1 + (B / 16) * ns) * 128, s);   // error flag line + counters
+  if (!o.zeroed) zero_async(sync, (size_t)(1 + (B / 16) * ns) * 128, s);   // error flag line + counters
   hipLaunchKernelGGL(k, dim3(grid), dim3(64 * PL_W * CH), 0, s, gx, w_hh, hs, cs, act, T, B, Hd, reverse,
                      sync, ns, o.job_err);
   return true;
@@ -566,7 +566,7 @@ static bool pl_bwd(const float* act, const float* cs, const float* dH, const bf1
   auto k = lstm_persist_bwd_kernel<KW, CH>;
   if (!pl_fits((const void*)k, 64 * PL_W * CH, grid, o.grids, o.rsv)) return false;
   const int ns = (Hd / (16 * CH)) % g_pl_ns == 0 ? g_pl_ns : 1;
-  zero_async(sync, (size_t)(1 + (B / 16) * ns) * 128, s);   // error flag line + counters
+  if (!o.zeroed) zero_async(sync, (size_t)(1 + (B / 16) * ns) * 128, s);   // error flag line + counters
   hipLaunchKernelGGL(k, dim3(grid), dim3(64 * PL_W * CH), 0, s, act, cs, dH, w_hh, dG, T, B, Hd, reverse,
                      sync, ns, dh_bf16, o.job_err);
   return true;

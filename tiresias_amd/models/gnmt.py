@@ -50,11 +50,24 @@ LSTM_GROUPED_WGRAD = os.environ.get("TAM_LSTM_GROUPED", "1") != "0"
 _SYNCS: list = []          # recent barrier/error words (tests read the error flags)
 
 
-def _sync(dev, B: int) -> torch.Tensor:
-    # [0] error flag, up to 4 arrival counters per batch tile (own 128-B line each)
-    # zeroed by the kernel launcher (stream-ordered), no fill kernel here; only
-    # buffers of launches that ran are kept for persist_errors (_ran)
-    return torch.empty(32 * (4 * (B // 16) + 1), dtype=torch.int32, device=dev)
+def _sync_words(B: int) -> int:
+    return 32 * (4 * (B // 16) + 1)
+
+
+def _sync(dev, B: int, m=None):
+    """(sync words, zeroed) of one persistent launch: [0] error flag, up to 4
+    arrival counters per batch tile (own 128-B line each). A slice of the
+    model's per-step pool (zeroed by ONE fill at the start of the forward,
+    GNMT.forward) when one is left, else a fresh buffer the kernel launcher
+    zeroes (stream-ordered). Only buffers of launches that ran are kept for
+    persist_errors (_ran)."""
+    pool = getattr(m, "_sync_pool", None)
+    n = _sync_words(B)
+    if pool is not None and m._sync_next + n <= pool.numel() and m._sync_B == B:
+        t = pool[m._sync_next:m._sync_next + n]
+        m._sync_next += n
+        return t, True
+    return torch.empty(n, dtype=torch.int32, device=dev), False
 
 
 def _ran(ok: bool, t: torch.Tensor) -> bool:
@@ -102,9 +115,9 @@ class _LSTMLayer(Function):
         if dev.type == "cuda":
             _T().gemm(x2, True, w_ih.w, True, G, 0, b.w, False, None, 1.0, False)
             Gv = G.view(T, B, 4 * Hd)
-            sy = _sync(dev, B)
+            sy, zeroed = _sync(dev, B, m)
             ran = PERSIST and persist and _ran(_T().lstm_seq_forward(Gv, w_hh.w, Hs, Cs, act, reverse, sy,
-                                                                     *_pl_args(m)), sy)
+                                                                     *_pl_args(m), zeroed), sy)
             steps = [] if ran else steps
             prev = None
             # the fused per-timestep kernel (lstm_step_forward) ties GEMM + cell +
@@ -155,11 +168,12 @@ class _LSTMLayer(Function):
         order = list(range(T - 1, -1, -1) if reverse else range(T))
         rev_order = order[::-1]
         if dev.type == "cuda":
-            sy = _sync(dev, B)
+            sy, zeroed = _sync(dev, B, m)
             # the persistent kernel reads dH as it comes (bf16); only the
             # per-step path needs the fp32 accumulator it updates in place
             ran = PERSIST and persist and _ran(
-                _T().lstm_seq_backward(act, Cs, dH.contiguous(), w_hh.w, dG, reverse, sy, *_pl_args(m)), sy)
+                _T().lstm_seq_backward(act, Cs, dH.contiguous(), w_hh.w, dG, reverse, sy, *_pl_args(m), zeroed),
+                sy)
             if not ran:                            # per-step path: cell-state gradient carry
                 dHf = dH.float().contiguous()
                 dc = torch.zeros(B, Hd, dtype=torch.float32, device=dev)
@@ -297,6 +311,14 @@ class GNMT:
 
     def forward(self, batch):
         src, tgt_in = batch["src"], batch["tgt_in"]       # [B,S] token ids
+        if src.is_cuda and PERSIST and self.persist:
+            # the sync words of every persistent launch of this step (forward
+            # and backward of each layer-direction) zeroed by one fill instead
+            # of one zeroing kernel per launch
+            B = src.shape[0]
+            n = 2 * (len(self.enc) + len(self.dec)) * _sync_words(B)
+            self._sync_pool = torch.zeros(n, dtype=torch.int32, device=src.device)
+            self._sync_next, self._sync_B = 0, B
         # time-major activations [T,B,H]
         # branch 1: the first decoder layer (+ attention query) reads only the
         # target embedding, so it runs alongside the whole encoder stack;
