@@ -15,6 +15,8 @@
 // not reach the weights. lstm_guard_step then moves the word into the job's
 // skipped-step count (err[1]), which the worker subtracts from the round's
 // progress and uses to switch the job to the per-step recurrence.
+#include <cstdlib>
+
 #include "tam/common.h"
 #include "tam/kernels.h"
 
@@ -188,14 +190,22 @@ __global__ void __launch_bounds__(256) sgd_stream_kernel(float* __restrict__ w, 
 }
 
 // 0: adam_kernel / sgd_kernel (one group per thread per iteration); 1: U=2;
-// 2: U=2 + NT; 3: U=4 + NT; -1 (default): 3 for arrays of >= 64M params, else
-// 0 -- measured: VGG-16's 138M-param SGD step 868 -> 743 us, GNMT's 227M Adam
-// 1.73 -> 1.67 ms, the 26M / 61M arrays equal or slower with the streaming
-// forms (tools/bench_optim.py, profiles/r4/optim_variants.json)
-static int g_optim_variant = -1;
+// 2: U=2 + NT; 3: U=4 + NT; -1 (default): optim_pick -- isolated: VGG-16's
+// 138M-param SGD step 868 -> 743 us, GNMT's 227M Adam 1.73 -> 1.67 ms, the
+// 26M / 61M arrays equal or slower with the streaming forms
+// (tools/bench_optim.py, profiles/r4/optim_variants.json)
+static int g_optim_variant = [] {
+  const char* e = getenv("TAM_OPTIM_VARIANT");   // A/B runs
+  return e ? atoi(e) : -1;
+}();
 void optim_variant(int v) { g_optim_variant = v; }
-static int optim_pick(long n4) {
-  return g_optim_variant >= 0 ? g_optim_variant : (n4 >= (16L << 20) ? 3 : 0);
+// auto: SGD on >= 64M params takes the streaming form (VGG-16 graph step
+// 6.94 -> 6.88 ms); Adam stays on the baseline kernel -- its isolated gain
+// (GNMT 1.73 -> 1.67 ms) did not survive inside the graph step (10.20 vs
+// 10.23 ms, two A/B rounds, profiles/r4/optim_variants_step_ab.log)
+static int optim_pick(long n4, bool adam) {
+  if (g_optim_variant >= 0) return g_optim_variant;
+  return (!adam && n4 >= (16L << 20)) ? 3 : 0;
 }
 
 static int ogrid(long n4) {
@@ -208,7 +218,7 @@ void sgd_step(float* w, float* g, float* mom, bf16_t* wb, long n, float lr, floa
               float wd, float gscale, int nesterov, int zero_grad, hipStream_t s, const unsigned* guard) {
   // n % 4 == 0 (arena segments are padded to 64 elements)
   const dim3 grid(ogrid(n / 4));
-  switch (optim_pick(n / 4)) {
+  switch (optim_pick(n / 4, false)) {
     case 1:
       hipLaunchKernelGGL((sgd_stream_kernel<2, false>), grid, dim3(256), 0, s, w, g, mom, wb, n / 4, lr, momentum, wd,
                          gscale, nesterov, zero_grad, guard);
@@ -232,7 +242,7 @@ void adam_step(float* w, float* g, float* m, float* v, bf16_t* wb, long n, float
                hipStream_t s, const unsigned* guard) {
   const float bc1 = 1.f - powf(b1, (float)step), bc2 = 1.f - powf(b2, (float)step);
   const dim3 grid(ogrid(n / 4));
-  switch (optim_pick(n / 4)) {
+  switch (optim_pick(n / 4, true)) {
     case 1:
       hipLaunchKernelGGL((adam_stream_kernel<2, false>), grid, dim3(256), 0, s, w, g, m, v, wb, n / 4, lr, b1, b2, eps,
                          wd, bc1, bc2, gscale, zero_grad, guard);
