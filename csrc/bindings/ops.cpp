@@ -325,6 +325,20 @@ void gemm_dispatch(const Tensor& a, bool a_kmajor, const Tensor& b, bool b_kmajo
             K / 64 / one_wave >= 8)
           cands.push_back({tl, one_wave > 16 ? 16 : one_wave});
         if (tl == 256 && sp == 1 && t256 < 150 && K / 64 >= 32 && one_wave != 2) cands.push_back({tl, 2});
+        // deep K over few tiles: the slice count whose block total lands just
+        // under a whole number of waves (3200x2048x32000: 104 tiles x 7 = 728
+        // blocks = 0.95 of 3 waves, 522 vs 538 us at 2 slices,
+        // profiles/r4/streamk_vs_splitk.json)
+        if (tl == 256 && t256 < 150 && K / 64 >= 256) {
+          int best_sp = 0;
+          double best_fill = 0.0;
+          for (int q = 3; q <= 16 && K / 64 / q >= 16; ++q) {
+            const long blocks = t256 * q;
+            const double fill = (double)blocks / (double)(((blocks + 255) / 256) * 256);
+            if (fill > best_fill + 1e-9) { best_fill = fill; best_sp = q; }
+          }
+          if (best_sp && best_sp != sp && best_sp != 2 * sp) cands.push_back({tl, best_sp});
+        }
       }
       if (tam::gemm8p_sk_ok(a_kmajor, b_kmajor, (int)M, (int)N, (int)K, a.stride(0), b.stride(0)))
         cands.push_back({256, 0});   // stream-K

@@ -23,6 +23,7 @@
 //     t-1 used, then tile t is computed;
 //   * XCD-aware bijective workgroup remap, grouped-M tile order.
 #pragma once
+#include <cstdlib>
 #include "tam/igemm.h"
 
 namespace tam {
@@ -248,14 +249,14 @@ __device__ __forceinline__ void cd_epilogue(f32x4_t (&acc)[4][BN / WN / 16], con
 // kt_hi >= 0: only K-tiles [kt_lo, kt_hi) (split-K slice); slab != null:
 // the raw fp32 accumulators go to slab[m][Ng] (tile rows m, no row map, no
 // epilogue) for cd_slab_reduce_kernel
-template <int BN, int WN, int BM>
+template <int BN, int WN, int BM, int NST = 0>   // NST: LDS ring depth (0: 3 if it fits, else 2)
 __device__ __forceinline__ void conv_dma_body(const CDArgs& a, const Epi& ep, const int bid, const int kt_lo = 0,
                                               const int kt_hi = -1, float* __restrict__ slab = nullptr) {
   constexpr int WM = BM / 64;             // waves along M (64 rows each)
   constexpr int W = WM * WN;              // waves
   constexpr int BK = 64;
   constexpr int A_BYTES = BM * BK * 2, B_BYTES = BN * BK * 2, STAGE = A_BYTES + B_BYTES;
-  constexpr int STAGES = 3 * STAGE <= 160 * 1024 ? 3 : 2;
+  constexpr int STAGES = NST ? NST : (3 * STAGE <= 160 * 1024 ? 3 : 2);
   constexpr int AG = BM / 8 / W;          // A 8-row groups per wave
   constexpr int BG = BN / 8 / W;          // B 8-row groups per wave
   constexpr int D = AG + BG;              // DMA instructions per thread per K-tile
@@ -399,12 +400,13 @@ __device__ __forceinline__ void conv_dma_body(const CDArgs& a, const Epi& ep, co
 
 // split-K over blockIdx.y: slice kz owns K-tiles [kz * kps, (kz+1) * kps) and
 // writes its partial sums to ws[kz][M][Ng]
-template <int BN, int WN, int BM = 256>
-__global__ void __launch_bounds__(BM / 64 * 64 * WN, 1) conv_dma_split_kernel(CDArgs a, float* ws, int kps) {
+template <int BN, int WN, int BM = 256, int NST = 0>
+__global__ void __launch_bounds__(BM / 64 * 64 * WN, NST == 2 ? 2 : 1) conv_dma_split_kernel(CDArgs a, float* ws,
+                                                                                            int kps) {
   const int nk = a.Kd / 64;
   const int lo = blockIdx.y * kps;
-  conv_dma_body<BN, WN, BM>(a, Epi{}, xcd_remap(blockIdx.x, gridDim.x), lo, min(nk, lo + kps),
-                            ws + (long)blockIdx.y * a.M * a.Ng);
+  conv_dma_body<BN, WN, BM, NST>(a, Epi{}, xcd_remap(blockIdx.x, gridDim.x), lo, min(nk, lo + kps),
+                                 ws + (long)blockIdx.y * a.M * a.Ng);
 }
 
 // C = epilogue(sum_z ws[z]) for the split conv: bf16 output rows through the
@@ -481,9 +483,10 @@ static __global__ void __launch_bounds__(256) cd_slab_reduce_kernel(const float*
   for (int e = threadIdx.x; e < 2 * a.Ng; e += 256) unsafeAtomicAdd(sh + e, (double)red[e]);
 }
 
-template <int BN, int WN, int BM = 256>
-__global__ void __launch_bounds__(BM / 64 * 64 * WN, 1) conv_dma_kernel(CDArgs a, Epi ep) {
-  conv_dma_body<BN, WN, BM>(a, ep, xcd_remap(blockIdx.x, gridDim.x));
+// NST = 2 (128-row tile only): a 64 KiB two-stage ring, two blocks per CU
+template <int BN, int WN, int BM = 256, int NST = 0>
+__global__ void __launch_bounds__(BM / 64 * 64 * WN, NST == 2 ? 2 : 1) conv_dma_kernel(CDArgs a, Epi ep) {
+  conv_dma_body<BN, WN, BM, NST>(a, ep, xcd_remap(blockIdx.x, gridDim.x));
 }
 
 // Several independent passes sharing one epilogue in ONE launch: the parity
@@ -687,6 +690,16 @@ inline int conv_dma_pick_bn(int M, int Ng, int Kd, int force) {
 // rates as the pick model's efficiencies x ~2.4 TF/s (the measured 128-row
 // 7x7 rate); returns the pick (tile code) and slices of the cheapest plan
 // with >= 8 K-tiles per slice and <= 64 MiB of slabs.
+// 128-row tiles on the two-stage ring (two blocks per CU): A/B knob
+// (TAM_CONV128_NST2=1), off by default
+inline bool cd_nst2() {
+  static const int v = [] {
+    const char* e = getenv("TAM_CONV128_NST2");
+    return e ? atoi(e) : 0;
+  }();
+  return v != 0;
+}
+
 struct CdSplit { int pick, sp; };
 inline CdSplit cd_split_plan(const CDArgs& a, int pick0, int cus) {
   CdSplit best{pick0, 1};
@@ -700,10 +713,14 @@ inline CdSplit cd_split_plan(const CDArgs& a, int pick0, int cus) {
     if (a.Ng % bn) continue;
     if ((code & 0x1000) && a.Kd < 1024) continue;
     const long tiles = (long)((a.M + bm - 1) / bm) * (a.Ng / bn);
+    // the two-stage 128-row variant holds two blocks per CU; each then runs
+    // at ~0.7x the single-block rate (cd_nst2)
+    const bool two = (code & 0x1000) && cd_nst2();
+    const long slots = two ? 2L * cus : cus;
     for (int sp = 1; sp <= 8; ++sp) {
       if (sp > 1 && (nk / sp < 8 || (long)sp * a.M * a.Ng > (16L << 20))) break;
-      const double block_us = 2.0 * bm * bn * (double)a.Kd / sp / (eff[c] * 2.4e6);
-      const double waves = (double)((tiles * sp + cus - 1) / cus);
+      const double block_us = 2.0 * bm * bn * (double)a.Kd / sp / (eff[c] * 2.4e6) * (two ? 1.4 : 1.0);
+      const double waves = (double)((tiles * sp + slots - 1) / slots);
       double t = waves * block_us;
       if (sp > 1) t += (double)(sp + 1) * a.M * a.Ng * 4 / 4.0e6 + 3.0;
       if (t < tbest * 0.97) { tbest = t; best = CdSplit{code, sp}; }
@@ -758,7 +775,8 @@ inline int launch_conv_dma(const CDArgs& a, const Epi& ep, hipStream_t s, int fo
       const bool t128 = (p.pick & 0x1000) != 0;
       const int bm = t128 ? 128 : 256, bn = p.pick & 0xfff;
       const dim3 grid((unsigned)(((a.M + bm - 1) / bm) * (a.Ng / bn)), (unsigned)z);
-      if (t128) hipLaunchKernelGGL((conv_dma_split_kernel<128, 2, 128>), grid, dim3(256), 0, s, a, ws, kps);
+      if (t128 && cd_nst2()) hipLaunchKernelGGL((conv_dma_split_kernel<128, 2, 128, 2>), grid, dim3(256), 0, s, a, ws, kps);
+      else if (t128) hipLaunchKernelGGL((conv_dma_split_kernel<128, 2, 128>), grid, dim3(256), 0, s, a, ws, kps);
       else if (bn == 256) hipLaunchKernelGGL((conv_dma_split_kernel<256, 2>), grid, dim3(512), 0, s, a, ws, kps);
       else if (bn == 128) hipLaunchKernelGGL((conv_dma_split_kernel<128, 2>), grid, dim3(512), 0, s, a, ws, kps);
       else hipLaunchKernelGGL((conv_dma_split_kernel<64, 1>), grid, dim3(256), 0, s, a, ws, kps);
@@ -773,7 +791,8 @@ inline int launch_conv_dma(const CDArgs& a, const Epi& ep, hipStream_t s, int fo
   }
   if (pick & 0x1000) {
     const int tiles = ((a.M + 127) / 128) * (a.Ng / 128);
-    hipLaunchKernelGGL((conv_dma_kernel<128, 2, 128>), dim3(tiles), dim3(256), 0, s, a, ep);
+    if (cd_nst2()) hipLaunchKernelGGL((conv_dma_kernel<128, 2, 128, 2>), dim3(tiles), dim3(256), 0, s, a, ep);
+    else hipLaunchKernelGGL((conv_dma_kernel<128, 2, 128>), dim3(tiles), dim3(256), 0, s, a, ep);
     return 128;
   }
   const int bn = pick;
