@@ -219,3 +219,33 @@ def bench_metric():
     import bench
 
     return bench.METRIC
+
+
+def test_store_grad_arena_layout_and_grad_mode():
+    """store_grad params lead the decay region (the optimizer skips zeroing
+    [0, n_store)); grad_mode stores the first write of a step and
+    accumulates after it; a new optimizer step (grad_epoch) re-arms it."""
+    from tiresias_amd.ops import functional as Fx
+    from tiresias_amd.ops.arena import Arena
+
+    A = Arena("cpu")
+    a = A.add("a", (4, 8))
+    s1 = A.add("s1", (16, 8), store_grad=True)
+    b = A.add("b", (8,), decay=False, store_grad=True)        # no-decay: never store_grad
+    s2 = A.add("s2", (3, 5), store_grad=True)
+    A.materialize()
+    assert not b.store_grad
+    assert [p.name for p in A._order()] == ["s1", "s2", "a", "b"]
+    assert s1.offset == 0 and A.n_store == s2.offset + 64 and a.offset == A.n_store
+    assert A.n_store <= A.n_decay <= b.offset
+    assert Fx.grad_mode(s1) == 0 and Fx.grad_mode(s1) == 1      # first write stores, then accumulate
+    assert Fx.grad_mode(a) == 0                                   # (a zeroed param: store == accumulate)
+    A.grad_epoch += 1                                             # an optimizer step
+    assert Fx.grad_mode(s1) == 0
+    old = Fx.STORE_GRAD
+    try:
+        Fx.STORE_GRAD = False
+        A.grad_epoch += 1
+        assert Fx.grad_mode(s2) == 1                              # A/B switch: always accumulate
+    finally:
+        Fx.STORE_GRAD = old
