@@ -483,7 +483,8 @@ static __global__ void __launch_bounds__(256) cd_slab_reduce_kernel(const float*
   for (int e = threadIdx.x; e < 2 * a.Ng; e += 256) unsafeAtomicAdd(sh + e, (double)red[e]);
 }
 
-// NST = 2 (128-row tile only): a 64 KiB two-stage ring, two blocks per CU
+// NST = 2 on the 128-row tile (a 64 KiB ring, two blocks per CU) measured
+// ResNet-50 9.72 -> 9.76 ms (profiles/r4/conv128_nst2_ab.log): not launched
 template <int BN, int WN, int BM = 256, int NST = 0>
 __global__ void __launch_bounds__(BM / 64 * 64 * WN, NST == 2 ? 2 : 1) conv_dma_kernel(CDArgs a, Epi ep) {
   conv_dma_body<BN, WN, BM, NST>(a, ep, xcd_remap(blockIdx.x, gridDim.x));
@@ -690,16 +691,6 @@ inline int conv_dma_pick_bn(int M, int Ng, int Kd, int force) {
 // rates as the pick model's efficiencies x ~2.4 TF/s (the measured 128-row
 // 7x7 rate); returns the pick (tile code) and slices of the cheapest plan
 // with >= 8 K-tiles per slice and <= 64 MiB of slabs.
-// 128-row tiles on the two-stage ring (two blocks per CU): A/B knob
-// (TAM_CONV128_NST2=1), off by default
-inline bool cd_nst2() {
-  static const int v = [] {
-    const char* e = getenv("TAM_CONV128_NST2");
-    return e ? atoi(e) : 0;
-  }();
-  return v != 0;
-}
-
 struct CdSplit { int pick, sp; };
 inline CdSplit cd_split_plan(const CDArgs& a, int pick0, int cus) {
   CdSplit best{pick0, 1};
@@ -713,13 +704,10 @@ inline CdSplit cd_split_plan(const CDArgs& a, int pick0, int cus) {
     if (a.Ng % bn) continue;
     if ((code & 0x1000) && a.Kd < 1024) continue;
     const long tiles = (long)((a.M + bm - 1) / bm) * (a.Ng / bn);
-    // the two-stage 128-row variant holds two blocks per CU; each then runs
-    // at ~0.7x the single-block rate (cd_nst2)
-    const bool two = (code & 0x1000) && cd_nst2();
-    const long slots = two ? 2L * cus : cus;
+    const long slots = cus;
     for (int sp = 1; sp <= 8; ++sp) {
       if (sp > 1 && (nk / sp < 8 || (long)sp * a.M * a.Ng > (16L << 20))) break;
-      const double block_us = 2.0 * bm * bn * (double)a.Kd / sp / (eff[c] * 2.4e6) * (two ? 1.4 : 1.0);
+      const double block_us = 2.0 * bm * bn * (double)a.Kd / sp / (eff[c] * 2.4e6);
       const double waves = (double)((tiles * sp + slots - 1) / slots);
       double t = waves * block_us;
       if (sp > 1) t += (double)(sp + 1) * a.M * a.Ng * 4 / 4.0e6 + 3.0;
@@ -775,8 +763,7 @@ inline int launch_conv_dma(const CDArgs& a, const Epi& ep, hipStream_t s, int fo
       const bool t128 = (p.pick & 0x1000) != 0;
       const int bm = t128 ? 128 : 256, bn = p.pick & 0xfff;
       const dim3 grid((unsigned)(((a.M + bm - 1) / bm) * (a.Ng / bn)), (unsigned)z);
-      if (t128 && cd_nst2()) hipLaunchKernelGGL((conv_dma_split_kernel<128, 2, 128, 2>), grid, dim3(256), 0, s, a, ws, kps);
-      else if (t128) hipLaunchKernelGGL((conv_dma_split_kernel<128, 2, 128>), grid, dim3(256), 0, s, a, ws, kps);
+      if (t128) hipLaunchKernelGGL((conv_dma_split_kernel<128, 2, 128>), grid, dim3(256), 0, s, a, ws, kps);
       else if (bn == 256) hipLaunchKernelGGL((conv_dma_split_kernel<256, 2>), grid, dim3(512), 0, s, a, ws, kps);
       else if (bn == 128) hipLaunchKernelGGL((conv_dma_split_kernel<128, 2>), grid, dim3(512), 0, s, a, ws, kps);
       else hipLaunchKernelGGL((conv_dma_split_kernel<64, 1>), grid, dim3(256), 0, s, a, ws, kps);
@@ -791,8 +778,7 @@ inline int launch_conv_dma(const CDArgs& a, const Epi& ep, hipStream_t s, int fo
   }
   if (pick & 0x1000) {
     const int tiles = ((a.M + 127) / 128) * (a.Ng / 128);
-    if (cd_nst2()) hipLaunchKernelGGL((conv_dma_kernel<128, 2, 128, 2>), dim3(tiles), dim3(256), 0, s, a, ep);
-    else hipLaunchKernelGGL((conv_dma_kernel<128, 2, 128>), dim3(tiles), dim3(256), 0, s, a, ep);
+    hipLaunchKernelGGL((conv_dma_kernel<128, 2, 128>), dim3(tiles), dim3(256), 0, s, a, ep);
     return 128;
   }
   const int bn = pick;

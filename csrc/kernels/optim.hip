@@ -189,8 +189,9 @@ __global__ void __launch_bounds__(256) sgd_stream_kernel(float* __restrict__ w, 
   for (long i = full + t; i < n4; i += stride) body(i, ld4<1, NT>(w, i), ld4<1, NT>(g, i), ld4<1, NT>(mom, i));
 }
 
-// 0: adam_kernel / sgd_kernel (one group per thread per iteration); 1: U=2;
-// 2: U=2 + NT; 3: U=4 + NT; -1 (default): optim_pick -- isolated: VGG-16's
+// 0: adam_kernel / sgd_kernel (one group per thread per iteration); 3: U=4
+// + NT (1 / 2, U=2 with / without NT, measured between the two and were
+// dropped); -1 (default): optim_pick -- isolated: VGG-16's
 // 138M-param SGD step 868 -> 743 us, GNMT's 227M Adam 1.73 -> 1.67 ms, the
 // 26M / 61M arrays equal or slower with the streaming forms
 // (tools/bench_optim.py, profiles/r4/optim_variants.json)
@@ -219,14 +220,6 @@ void sgd_step(float* w, float* g, float* mom, bf16_t* wb, long n, float lr, floa
   // n % 4 == 0 (arena segments are padded to 64 elements)
   const dim3 grid(ogrid(n / 4));
   switch (optim_pick(n / 4, false)) {
-    case 1:
-      hipLaunchKernelGGL((sgd_stream_kernel<2, false>), grid, dim3(256), 0, s, w, g, mom, wb, n / 4, lr, momentum, wd,
-                         gscale, nesterov, zero_grad, guard);
-      break;
-    case 2:
-      hipLaunchKernelGGL((sgd_stream_kernel<2, true>), grid, dim3(256), 0, s, w, g, mom, wb, n / 4, lr, momentum, wd,
-                         gscale, nesterov, zero_grad, guard);
-      break;
     case 3:
       hipLaunchKernelGGL((sgd_stream_kernel<4, true>), grid, dim3(256), 0, s, w, g, mom, wb, n / 4, lr, momentum, wd,
                          gscale, nesterov, zero_grad, guard);
@@ -243,14 +236,6 @@ void adam_step(float* w, float* g, float* m, float* v, bf16_t* wb, long n, float
   const float bc1 = 1.f - powf(b1, (float)step), bc2 = 1.f - powf(b2, (float)step);
   const dim3 grid(ogrid(n / 4));
   switch (optim_pick(n / 4, true)) {
-    case 1:
-      hipLaunchKernelGGL((adam_stream_kernel<2, false>), grid, dim3(256), 0, s, w, g, m, v, wb, n / 4, lr, b1, b2, eps,
-                         wd, bc1, bc2, gscale, zero_grad, guard);
-      break;
-    case 2:
-      hipLaunchKernelGGL((adam_stream_kernel<2, true>), grid, dim3(256), 0, s, w, g, m, v, wb, n / 4, lr, b1, b2, eps,
-                         wd, bc1, bc2, gscale, zero_grad, guard);
-      break;
     case 3:
       hipLaunchKernelGGL((adam_stream_kernel<4, true>), grid, dim3(256), 0, s, w, g, m, v, wb, n / 4, lr, b1, b2, eps,
                          wd, bc1, bc2, gscale, zero_grad, guard);
