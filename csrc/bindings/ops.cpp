@@ -622,7 +622,11 @@ void conv_wgrad_op(const Tensor& dy, const Tensor& x, const Tensor& dw, int64_t 
     TORCH_CHECK(dbias->numel() == g.K && dbias->is_contiguous(), "tam.conv_wgrad: dbias size");
     db = dbias->data_ptr<float>();
   }
-  const int fused = tam::conv_wgrad(bp(dy), bp(x), g, ep, cur_stream(dy), db, patch);
+  const long wsf = tam::conv_wgrad_split_ws(g);
+  Tensor wsl;
+  if (wsf > 0) wsl = at::empty({wsf}, dy.options().dtype(at::kFloat));
+  const int fused = tam::conv_wgrad(bp(dy), bp(x), g, ep, cur_stream(dy), db, patch,
+                                    wsf > 0 ? wsl.data_ptr<float>() : nullptr, wsf);
   if (db && !fused) {
     const long R = (long)g.N * g.P * g.Q;
     Tensor ws = at::empty({g.K % 8 == 0 ? (int64_t)tam::COLSUM_MAX_BLOCKS * g.K : 1}, dy.options().dtype(at::kFloat));
@@ -807,6 +811,8 @@ void colsum_policy_op(int64_t p) { tam::colsum_policy((int)p); }
 void attn_short_policy_op(int64_t p) { tam::attn_short_policy((int)p); }
 // forced (bm, bn, splits) of the LDS-DMA conv wgrad (A/B sweeps; 0 = heuristic)
 void conv_wgrad_c64_policy_op(int64_t p) { tam::conv_wgrad_c64_policy((int)p); }
+void conv_wgrad_order_op(int64_t p) { tam::conv_wgrad_order((int)p); }
+void conv_wgrad_slab_policy_op(int64_t p) { tam::conv_wgrad_slab_policy((int)p); }
 void conv_wgrad_force_op(int64_t bm, int64_t bn, int64_t splits, int64_t noatomic) {
   tam::conv_wgrad_force((int)bm, (int)bn, (int)splits, (int)noatomic);
 }
@@ -1083,6 +1089,8 @@ TORCH_LIBRARY(tam, m) {
   m.def("conv_dma_policy(int policy) -> ()", &conv_dma_policy_op);
   m.def("conv_wgrad_force(int bm, int bn, int splits, int noatomic=0) -> ()", &conv_wgrad_force_op);
   m.def("conv_wgrad_c64_policy(int policy) -> ()", &conv_wgrad_c64_policy_op);
+  m.def("conv_wgrad_order(int flat) -> ()", &conv_wgrad_order_op);
+  m.def("conv_wgrad_slab_policy(int policy) -> ()", &conv_wgrad_slab_policy_op);
   m.def("conv_halo_policy(int policy) -> ()", &conv_halo_policy_op);
   m.def("colsum_policy(int policy) -> ()", &colsum_policy_op);
   m.def("attn_short_policy(int policy) -> ()", &attn_short_policy_op);

@@ -912,6 +912,9 @@ struct WGArgs {
   int dn, dp, dq;      // 64 pixels = dn images + dp rows + dq columns
   int atomic;          // 1: atomic add, 0: plain += (single split)
   float* dbias;        // optional: dbias[k] += sum_m dY[m][k] (the conv's bias gradient)
+  int tiles;           // output tiles per split
+  int flat;            // 1: 1-D grid of tiles x splits, split-major per XCD (see below)
+  float* slab;         // split-K partials [splits][K][ldc], plain stores (nullptr: atomics into dw)
 };
 
 template <int S>
@@ -934,7 +937,20 @@ __global__ void __launch_bounds__(64 * WM * WN, 1) conv_wgrad_dma_kernel(WGArgs 
   const int tiles_m = (a.K + BM - 1) / BM;
   const int ncols = (int)a.ldc;
   const int tiles_n = ncols / BN;
-  const int bid = xcd_remap(blockIdx.x, gridDim.x);
+  // Block -> (tile, split). The hardware deals workgroups round-robin over
+  // the 8 XCDs by LINEAR id; a (tiles, 1, splits) grid remapped on x alone
+  // spreads every split's pixel rows over all 8 L2s, and each XCD's working
+  // set is the whole dY + X (12.8 MB at 14x14x256, 4 MB of L2). The flat
+  // form remaps the linear id so each XCD owns a run of consecutive splits
+  // with all their tiles: one split's dY rows are fetched into one L2 and
+  // shared by every column tile, its X rows by every row tile.
+  int bid, split;
+  if (a.flat) {
+    const int f = xcd_remap(blockIdx.x, gridDim.x);
+    bid = f % a.tiles; split = f / a.tiles;
+  } else {
+    bid = xcd_remap(blockIdx.x, gridDim.x); split = blockIdx.z;
+  }
   const int tm = bid % tiles_m, tn = bid / tiles_m;
   const int k0 = tm * BM, col0 = tn * BN;
   (void)tiles_n;
@@ -942,7 +958,7 @@ __global__ void __launch_bounds__(64 * WM * WN, 1) conv_wgrad_dma_kernel(WGArgs 
   const int rs = col0 / a.C, c0 = col0 % a.C;
   const int tr = rs / a.S, ts = rs % a.S;
 
-  const int step0 = blockIdx.z * a.steps_per_split;
+  const int step0 = split * a.steps_per_split;
   const int nsteps_all = (a.Mred + BK - 1) / BK;
   const int nk = min(a.steps_per_split, nsteps_all - step0);
   const int mstart = step0 * BK;
@@ -1080,7 +1096,9 @@ __global__ void __launch_bounds__(64 * WM * WN, 1) conv_wgrad_dma_kernel(WGArgs 
       if (lane < 16 && k < a.K) atomicAdd(a.dbias + k, v);
     }
   }
-  // ---- epilogue: row = k, col = (r,s,c); fp32 accumulate into dW
+  // ---- epilogue: row = k, col = (r,s,c); fp32 accumulate into dW, or store
+  // this split's partial tile into its slab (reduced by gemm_slab_reduce)
+  float* slab = a.slab ? a.slab + (long)split * a.K * a.ldc : nullptr;
 #pragma unroll
   for (int j = 0; j < TN; ++j) {
     const int col = col0 + wn * (BN / WN) + 16 * j + (lane & 15);
@@ -1090,9 +1108,10 @@ __global__ void __launch_bounds__(64 * WM * WN, 1) conv_wgrad_dma_kernel(WGArgs 
       for (int r = 0; r < 4; ++r) {
         const int row = k0 + wm * (BM / WM) + 16 * i + 4 * (lane >> 4) + r;
         if (row >= a.K) continue;
-        float* c = a.dw + (long)row * a.ldc + col;
-        if (a.atomic) atomicAdd(c, acc[i][j][r]);
-        else *c += acc[i][j][r];
+        const long off = (long)row * a.ldc + col;
+        if (slab) slab[off] = acc[i][j][r];
+        else if (a.atomic) atomicAdd(a.dw + off, acc[i][j][r]);
+        else a.dw[off] += acc[i][j][r];
       }
     }
   }
@@ -1290,55 +1309,134 @@ inline bool launch_conv_wgrad_c64(const bf16_t* dy, const bf16_t* x, float* dw, 
 // heuristic below. [3] != 0: TIMING ONLY -- split blocks add with plain
 // (racy) read-modify-writes instead of atomics, to price the atomic traffic
 inline int g_wgrad_force[4] = {0, 0, 0, 0};
+// block order of the DMA wgrad kernel: 1 split-major flat XCD remap
+// (default), 0 the (tiles, 1, splits) grid (A/B: conv_wgrad_order)
+inline int g_wgrad_flat = 1;
 
 template <int BM, int BN, int WM, int WN>
 inline void wgrad_dma_launch(const WGArgs& a, int tiles, int splits, hipStream_t s) {
-  hipLaunchKernelGGL((conv_wgrad_dma_kernel<BM, BN, WM, WN>), dim3(tiles, 1, splits),
-                     dim3(64 * WM * WN), 0, s, a);
+  const dim3 grid = a.flat ? dim3(tiles * splits) : dim3(tiles, 1, splits);
+  hipLaunchKernelGGL((conv_wgrad_dma_kernel<BM, BN, WM, WN>), grid, dim3(64 * WM * WN), 0, s, a);
 }
 
-// dw += conv wgrad (mode 1 semantics; mode 0 callers zero dw first)
-inline bool launch_conv_wgrad_dma(const bf16_t* dy, const bf16_t* x, float* dw, const ConvGeom& g,
-                                  int mode, hipStream_t s, bool force = false, float* dbias = nullptr) {
-  if (g.dil != 1 || g.C % 64 != 0 || g.K % 64 != 0) return false;
+// slab split-K for the DMA wgrad: 1 (default) split passes store fp32
+// partials and one reduce pass adds them into dw (store mode needs no zero
+// pass); 0: every split adds into dw with fp32 atomics (A/B). The atomics /
+// read-modify-writes of the split epilogues run at ~1.2 TB/s chip-wide
+// (32 MB of them at 256 blocks of 256x128: ~27 us on ResNet-50's 14x14
+// layers), the slab's plain stores + one streaming reduce at HBM rate.
+inline int g_wgrad_slab = 1;
+
+struct WGPlan {
+  int bm = 0, bn = 0, tiles = 0, splits = 0, sps = 0;
+  bool ok = false;
+};
+
+inline WGPlan wgrad_dma_plan(const ConvGeom& g, bool force) {
+  WGPlan p;
+  if (g.dil != 1 || g.C % 64 != 0 || g.K % 64 != 0) return p;
   const long Mred = (long)g.N * g.P * g.Q;
-  if (Mred >= (1L << 31) || (long)g.N * g.H * g.W * g.C >= (1L << 31)) return false;
+  if (Mred >= (1L << 31) || (long)g.N * g.H * g.W * g.C >= (1L << 31)) return p;
   const int ncols = g.R * g.S * g.C;
   // tile: BN divides C (one tap per column tile); BM over K
-  int bm, bn;
   const int* fw = g_wgrad_force;
   if (fw[0] > 0) {
-    bm = fw[0]; bn = fw[1];
-    const bool known = (bm == 256 && (bn == 128 || bn == 64)) || (bm == 128 && (bn == 128 || bn == 64)) ||
-                       (bm == 64 && bn == 64);
-    if (!known || g.K % bm != 0 || g.C % bn != 0) return false;
+    p.bm = fw[0]; p.bn = fw[1];
+    const bool known = (p.bm == 256 && (p.bn == 128 || p.bn == 64)) || (p.bm == 128 && (p.bn == 128 || p.bn == 64)) ||
+                       (p.bm == 64 && p.bn == 64);
+    if (!known || g.K % p.bm != 0 || g.C % p.bn != 0) return p;
   } else {
-    if (g.K % 256 == 0 && g.C % 128 == 0) { bm = 256; bn = 128; }
-    else if (g.K % 128 == 0 && g.C % 128 == 0) { bm = 128; bn = 128; }
-    else { bm = 64; bn = 64; }
+    if (g.K % 256 == 0 && g.C % 128 == 0) { p.bm = 256; p.bn = 128; }
+    else if (g.K % 128 == 0 && g.C % 128 == 0) { p.bm = 128; p.bn = 128; }
+    else { p.bm = 64; p.bn = 64; }
     // the 64x64 form beats the igemm only on 1x1 layers (measured)
-    if (!force && bm == 64 && !(g.R == 1 && g.S == 1)) return false;
+    if (!force && p.bm == 64 && !(g.R == 1 && g.S == 1)) return p;
   }
-  const int tiles = (g.K / bm) * (ncols / bn);
+  p.tiles = (g.K / p.bm) * (ncols / p.bn);
   const int nsteps = (int)((Mred + 63) / 64);
   // split the pixel reduction to ~one block per CU, not more: every split
-  // adds |dW| of fp32 atomics (~1.3 TB/s chip-wide), which at 2 blocks/CU
-  // already cost as much as the MFMA work on ResNet-sized layers
-  int splits = fw[2] > 0 ? fw[2] : 256 / tiles;
+  // adds |dW| of fp32 partials to write and reduce
+  int splits = fw[2] > 0 ? fw[2] : 256 / p.tiles;
   if (fw[2] <= 0 && splits > nsteps / 8) splits = nsteps / 8;
   if (splits > nsteps) splits = nsteps;
   if (splits < 1) splits = 1;
-  int sps = (nsteps + splits - 1) / splits;
-  splits = (nsteps + sps - 1) / sps;
-  if (mode == 0) zero_async(dw, (size_t)g.K * ncols * sizeof(float), s);
+  p.sps = (nsteps + splits - 1) / splits;
+  p.splits = (nsteps + p.sps - 1) / p.sps;
+  p.ok = true;
+  return p;
+}
+
+// fp32 slab floats launch_conv_wgrad_dma would use for this geometry (0: none)
+inline long wgrad_dma_slab_floats(const ConvGeom& g, bool force) {
+  if (!g_wgrad_slab || g_wgrad_force[3]) return 0;
+  const WGPlan p = wgrad_dma_plan(g, force);
+  if (!p.ok || p.splits < 2) return 0;
+  return (long)p.splits * g.K * g.R * g.S * g.C;
+}
+
+// dw[i] = (mode ? dw[i] : 0) + sum_z ws[z][i] over mn contiguous floats (mn % 4
+// == 0). A block is (256 / L) float4 columns x L split lanes: every thread
+// sums a strided subset of the slabs with independent loads, the lanes meet
+// in LDS. L grows with the split count so no thread walks a long dependent
+// chain of slab loads (a one-thread-per-element reduce over 98 slabs of a
+// 64K-float dW measured 12 us slower than the atomics it replaced).
+static __global__ void __launch_bounds__(256) wg_slab_reduce_kernel(const float* __restrict__ ws, int sp, long mn,
+                                                                    float* __restrict__ dw, int mode, int L) {
+  __shared__ f32x4_t red[256];
+  const int cols = 256 / L;
+  const int cx = threadIdx.x % cols, zy = threadIdx.x / cols;
+  const long n4 = mn >> 2;
+  const long i = (long)blockIdx.x * cols + cx;
+  f32x4_t acc = {0.f, 0.f, 0.f, 0.f};
+  if (i < n4) {
+    const f32x4_t* w4 = (const f32x4_t*)ws + i;
+    const long zs = n4 * L;
+    int z = zy;
+    for (; z + 3 * L < sp; z += 4 * L) {
+      const f32x4_t v0 = w4[z * n4], v1 = w4[z * n4 + zs], v2 = w4[z * n4 + 2 * zs], v3 = w4[z * n4 + 3 * zs];
+      acc += (v0 + v1) + (v2 + v3);
+    }
+    for (; z < sp; z += L) acc += w4[z * n4];
+  }
+  red[threadIdx.x] = acc;
+  __syncthreads();
+  if (zy == 0 && i < n4) {
+    for (int k = 1; k < L; ++k) acc += red[k * cols + cx];
+    f32x4_t* o = (f32x4_t*)dw + i;
+    *o = mode ? *o + acc : acc;
+  }
+}
+
+inline void wgrad_slab_reduce(const float* ws, int sp, long mn, float* dw, int mode, hipStream_t s) {
+  int L = 1;
+  while (L < 64 && (sp + L - 1) / L > 8) L *= 2;   // <= 8 slab loads per thread
+  const int cols = 256 / L;
+  const long blocks = ((mn >> 2) + cols - 1) / cols;
+  hipLaunchKernelGGL(wg_slab_reduce_kernel, dim3((unsigned)blocks), dim3(256), 0, s, ws, sp, mn, dw, mode, L);
+}
+
+// dw = (mode ? dw : 0) + conv wgrad
+// ws / ws_floats: slab scratch of wgrad_dma_slab_floats(g) floats (else atomics)
+inline bool launch_conv_wgrad_dma(const bf16_t* dy, const bf16_t* x, float* dw, const ConvGeom& g,
+                                  int mode, hipStream_t s, bool force = false, float* dbias = nullptr,
+                                  float* ws = nullptr, long ws_floats = 0) {
+  const WGPlan p = wgrad_dma_plan(g, force);
+  if (!p.ok) return false;
+  const int ncols = g.R * g.S * g.C;
+  const bool slab = p.splits > 1 && ws != nullptr && ws_floats >= wgrad_dma_slab_floats(g, force) &&
+                    wgrad_dma_slab_floats(g, force) > 0;
+  if (mode == 0 && !slab) zero_async(dw, (size_t)g.K * ncols * sizeof(float), s);
   const int PQ = g.P * g.Q;
-  WGArgs a{dy, x, dw, ncols, g.K, g.C, g.H, g.W, g.P, g.Q, g.S, g.stride, g.pad, (int)Mred, sps,
-           64 / PQ, (64 % PQ) / g.Q, (64 % PQ) % g.Q, splits > 1 && !fw[3] ? 1 : 0, dbias};
-  if (bm == 256 && bn == 128) wgrad_dma_launch<256, 128, 4, 2>(a, tiles, splits, s);
-  else if (bm == 256) wgrad_dma_launch<256, 64, 4, 1>(a, tiles, splits, s);
-  else if (bm == 128 && bn == 128) wgrad_dma_launch<128, 128, 2, 2>(a, tiles, splits, s);
-  else if (bm == 128) wgrad_dma_launch<128, 64, 2, 2>(a, tiles, splits, s);
-  else wgrad_dma_launch<64, 64, 2, 2>(a, tiles, splits, s);
+  WGArgs a{dy, x, dw, ncols, g.K, g.C, g.H, g.W, g.P, g.Q, g.S, g.stride, g.pad, g.N * g.P * g.Q, p.sps,
+           64 / PQ, (64 % PQ) / g.Q, (64 % PQ) % g.Q, p.splits > 1 && !g_wgrad_force[3] ? 1 : 0, dbias,
+           p.tiles, g_wgrad_flat, slab ? ws : nullptr};
+  const int bm = p.bm, bn = p.bn;
+  if (bm == 256 && bn == 128) wgrad_dma_launch<256, 128, 4, 2>(a, p.tiles, p.splits, s);
+  else if (bm == 256) wgrad_dma_launch<256, 64, 4, 1>(a, p.tiles, p.splits, s);
+  else if (bm == 128 && bn == 128) wgrad_dma_launch<128, 128, 2, 2>(a, p.tiles, p.splits, s);
+  else if (bm == 128) wgrad_dma_launch<128, 64, 2, 2>(a, p.tiles, p.splits, s);
+  else wgrad_dma_launch<64, 64, 2, 2>(a, p.tiles, p.splits, s);
+  if (slab) wgrad_slab_reduce(ws, p.splits, (long)g.K * ncols, dw, mode, s);
   return true;
 }
 

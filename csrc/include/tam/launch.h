@@ -64,12 +64,16 @@ void conv_split_policy(int p);   // 1: split-K of under-filled LDS-DMA passes (d
 int conv_dgrad(const bf16_t* dy, const bf16_t* w, const bf16_t* wt, const ConvGeom& g, Epi ep,
                hipStream_t s, float* ws = nullptr, long ws_floats = 0);
 // dw[K][R*S*C] fp32, ep.mode 0 (overwrite) or 1 (accumulate)
+// ws / ws_floats: slab split-K scratch of conv_wgrad_split_ws(g) floats (none: atomics)
 int conv_wgrad(const bf16_t* dy, const bf16_t* x, const ConvGeom& g, Epi ep, hipStream_t s,
-               float* dbias = nullptr, bool allow_patch = true);
+               float* dbias = nullptr, bool allow_patch = true, float* ws = nullptr, long ws_floats = 0);
+long conv_wgrad_split_ws(const ConvGeom& g);
+void conv_wgrad_slab_policy(int p);   // 1: slab split-K for the DMA wgrad (default), 0: fp32 atomics
 void conv_weight_t(const bf16_t* w, bf16_t* wt, const ConvGeom& g, hipStream_t s);
 void conv_dma_policy(int p);   // 1: LDS-DMA core where eligible (default), 0: igemm only
 // LDS-DMA wgrad tile / split (0: heuristic); noatomic: timing-only racy adds
 void conv_wgrad_force(int bm, int bn, int splits, int noatomic = 0);
+void conv_wgrad_order(int flat);    // DMA wgrad block order: 1 split-major XCD remap (default), 0 3-D grid
 void conv_wgrad_c64_policy(int p);   // 64-channel 3x3 wgrad kernel: 1 on (default), 0 off, >= 2 blocks per k-slice
 void conv_halo_policy(int p);   // 1: 64-channel 3x3 stride-1 passes on the halo-tile kernel (default)
 bool gemm_select_big_p8(bool ak, bool bk, int M, int N, int K, long lda, long ldb);   // plain-GEMM igemm K-tiles in flight (1..3)

@@ -181,6 +181,12 @@ static void wgrad_tile(const bf16_t* dy, const bf16_t* x, const ConvGeom& g, con
 // there, so it is routed around: 7.42 -> 7.52 ms when it was not)
 static int g_wgrad_c64 = 1;
 void conv_wgrad_c64_policy(int p) { g_wgrad_c64 = p; }
+void conv_wgrad_order(int flat) { g_wgrad_flat = flat; }
+void conv_wgrad_slab_policy(int p) { g_wgrad_slab = p; }
+long conv_wgrad_split_ws(const ConvGeom& g) {
+  if (!g_conv_dma || (is_pointwise(g) && (long)g.N * g.P * g.Q < 100352 && g_conv_dma < 2)) return 0;
+  return wgrad_dma_slab_floats(g, g_conv_dma >= 2);
+}
 
 // dbias (optional, fp32 [K]): += the bias gradient sum_m dY[m][k], fused
 // into whichever wgrad kernel runs (each reads dY anyway); returns 1 when
@@ -191,14 +197,20 @@ void conv_wgrad_c64_policy(int p) { g_wgrad_c64 = p; }
 // starves co-running kernels: VGG-16's graph step with the weight gradients
 // on the side stream measured 7.42 -> 7.52 ms with it)
 int conv_wgrad(const bf16_t* dy, const bf16_t* x, const ConvGeom& g, Epi ep, hipStream_t s, float* dbias,
-               bool allow_patch) {
+               bool allow_patch, float* ws, long ws_floats) {
   const int Mred = g.N * g.P * g.Q, Nc = g.R * g.S * g.C;
   if (g_conv_dma && g_wgrad_c64 && (allow_patch || g_wgrad_c64 >= 2) && ep.c_f32 && ep.ldc == Nc && ep.mode <= 1 &&
       launch_conv_wgrad_c64(dy, x, (float*)ep.c, g, ep.mode, g_wgrad_c64 >= 2 ? g_wgrad_c64 : 0, s,
                             g_conv_dma >= 2 || g_wgrad_c64 >= 2, dbias))
     return dbias ? 1 : 0;
-  if (g_conv_dma && ep.c_f32 && ep.ldc == Nc && ep.mode <= 1 &&
-      launch_conv_wgrad_dma(dy, x, (float*)ep.c, g, ep.mode, s, g_conv_dma >= 2, dbias))
+  // pointwise wgrads with a short pixel reduction (ResNet-50 stages 2-4,
+  // <= 28x28 at batch 64) are plain dY^T X GEMMs that the routed GEMM runs
+  // faster (14x14 256->1024: 24.0 vs 30.7 us, 7x7 512->2048: 22.9 vs 29.5;
+  // tools/sweep_wgrad.py, profiles/r4/wgrad_sweep_*.json); the 56x56 ones
+  // stay on the DMA kernel (19.6 vs 57 us at 64->64)
+  const bool pw_gemm = is_pointwise(g) && Mred < 100352 && g_conv_dma < 2;
+  if (g_conv_dma && !pw_gemm && ep.c_f32 && ep.ldc == Nc && ep.mode <= 1 &&
+      launch_conv_wgrad_dma(dy, x, (float*)ep.c, g, ep.mode, s, g_conv_dma >= 2, dbias, ws, ws_floats))
     return dbias ? 1 : 0;
   if (is_pointwise(g)) {
     // dW[k][c] = sum_m dY[m][k] X[m][c]: A(k', m) = dY[m*K + k'], B(m, c) = X[m*C + c]

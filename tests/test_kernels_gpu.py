@@ -551,6 +551,44 @@ def test_conv_split_k(gpu, cfg):
         assert rel_err(a_, b_) < 1e-2
 
 
+@pytest.mark.parametrize("cfg", [(16, 14, 14, 256, 256, 3, 1, 1), (16, 56, 56, 64, 256, 1, 1, 0),
+                                 (8, 28, 28, 256, 256, 3, 2, 1), (4, 7, 7, 512, 512, 3, 1, 1),
+                                 (3, 13, 11, 128, 128, 3, 1, 1)])
+def test_conv_wgrad_slab_order(gpu, cfg):
+    """LDS-DMA weight gradient (conv_dma.h): split partials stored to fp32
+    slabs + split-parallel reduce vs the fp32-atomic epilogue, under both
+    block orders (split-major flat XCD remap / 3-D grid), store and
+    accumulate modes, each vs fp32 torch; the 56x56 case has ~100 splits."""
+    N, H, W, C, K, R, st, pd = cfg
+    torch.manual_seed(9)
+    x = torch.randn(N, H, W, C, device=gpu).to(BF)
+    P = (H + 2 * pd - R) // st + 1
+    Q = (W + 2 * pd - R) // st + 1
+    dy = torch.randn(N, P, Q, K, device=gpu).to(BF)
+    wf = torch.zeros(K, C, R, R, device=gpu, requires_grad=True)
+    gw, = torch.autograd.grad(F.conv2d(x.float().permute(0, 3, 1, 2), wf, stride=st, padding=pd),
+                              [wf], dy.float().permute(0, 3, 1, 2))
+    ref = gw.permute(0, 2, 3, 1)
+    db_ref = dy.float().sum((0, 1, 2))
+    T().conv_dma_policy(2)
+    try:
+        for slab in (1, 0):
+            for order in (1, 0):
+                T().conv_wgrad_slab_policy(slab)
+                T().conv_wgrad_order(order)
+                for mode in (0, 1):
+                    dw = torch.full((K, R, R, C), 0.25, device=gpu)
+                    db = torch.zeros(K, device=gpu)
+                    T().conv_wgrad(dy, x, dw, st, pd, 1, mode, db)
+                    want = ref + (0.25 if mode == 1 else 0.0)
+                    assert rel_err(dw, want) < 1e-4, (slab, order, mode, rel_err(dw, want))
+                    assert rel_err(db, db_ref) < 1e-4, (slab, order, mode)
+    finally:
+        T().conv_dma_policy(1)
+        T().conv_wgrad_slab_policy(1)
+        T().conv_wgrad_order(1)
+
+
 # LDS-DMA conv core (conv_dma.h): every tile width, stride-2 fwd, 1x1 s2, M
 # tails, padding taps, bias+relu epilogue and the relu-masked dgrad
 @pytest.mark.parametrize("cfg", [(2, 12, 12, 64, 64, 3, 1, 1), (3, 9, 11, 128, 128, 3, 1, 1),

@@ -390,7 +390,9 @@ class _Conv(Function):
             with _OnWgrad(dy, x) as ow:
                 # the bias gradient colsum(dy) rides on the wgrad kernel's dY reads;
                 # the LDS-heavy patch-staged wgrad only off the side stream
-                _T().conv_wgrad(dy, x, w.grad, st, pd, 1, 1, b.grad if b is not None else None, ow.s is None)
+                # the weight's only gradient writer in a step: the first write stores
+                _T().conv_wgrad(dy, x, w.grad, st, pd, 1, grad_mode(w), b.grad if b is not None else None,
+                                ow.s is None)
             if ctx.needs_input_grad[0]:
                 dx = torch.empty_like(x)
                 wt = getattr(w, "wt", None)

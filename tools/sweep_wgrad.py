@@ -61,9 +61,16 @@ def main():
                          "64 / 256 blocks per slice) vs the tap-gather path, interleaved rounds, numerics")
     ap.add_argument("--atomic_ab", action="store_true",
                     help="only time the heuristic with atomics vs racy plain adds (prices the atomics)")
+    ap.add_argument("--order_ab", action="store_true",
+                    help="heuristic config, 3-D grid vs split-major flat XCD order (conv_wgrad_order), interleaved")
+    ap.add_argument("--slab_ab", action="store_true",
+                    help="heuristic config, fp32-atomic split epilogue vs slab partials + reduce "
+                         "(conv_wgrad_slab_policy), interleaved, both store and accumulate modes")
+    ap.add_argument("--slab", type=int, default=1, help="slab policy for the other modes")
     a = ap.parse_args()
     _lib.load(required=True)
     T = torch.ops.tam
+    T.conv_wgrad_slab_policy(a.slab)
     dev = torch.device("cuda", 0)
     shapes = [("resnet50",) + s for s in RN50] * ("resnet50" in a.models) + \
              [("vgg16",) + s for s in VGG] * ("vgg16" in a.models)
@@ -95,6 +102,45 @@ def main():
                         "rel_diff": float((dw - r0).norm() / r0.norm().clamp_min(1e-30))})
             out.append(row)
             print(json.dumps(row), flush=True)
+            continue
+        if a.slab_ab:
+            best = {}
+            run0 = lambda: T.conv_wgrad(dy, x, dw, st, pd, 1, 0)  # noqa: E731  (store mode)
+            for _ in range(3):
+                for o in (0, 1):
+                    T.conv_wgrad_slab_policy(o)
+                    best[o] = min(best.get(o, 1e9), _time(run))
+                    best[o + 2] = min(best.get(o + 2, 1e9), _time(run0))
+            T.conv_wgrad_slab_policy(0)
+            dw.normal_(); run0(); torch.cuda.synchronize(); r0 = dw.clone()
+            T.conv_wgrad_slab_policy(1)
+            dw.normal_(); run0(); torch.cuda.synchronize()
+            d0 = float((dw - r0).norm() / r0.norm().clamp_min(1e-30))
+            dw.copy_(r0); run(); torch.cuda.synchronize()
+            d1 = float((dw - 2 * r0).norm() / (2 * r0).norm().clamp_min(1e-30))
+            T.conv_wgrad_slab_policy(a.slab)
+            row.update({"atomic_us": round(best[0], 2), "slab_us": round(best[1], 2),
+                        "atomic_store_us": round(best[2], 2), "slab_store_us": round(best[3], 2),
+                        "rel_diff_store": d0, "rel_diff_acc": d1})
+            out.append(row)
+            print(f"{model:8s} {str(row['shape']):38s} x{calls} acc: atomic {best[0]:7.2f} slab {best[1]:7.2f} | "
+                  f"store: atomic {best[2]:7.2f} slab {best[3]:7.2f} | diff {d0:.1e} {d1:.1e}", flush=True)
+            continue
+        if a.order_ab:
+            best = {}
+            for _ in range(3):
+                for o in (0, 1):
+                    T.conv_wgrad_order(o)
+                    best[o] = min(best.get(o, 1e9), _time(run))
+            T.conv_wgrad_order(0)
+            dw.zero_(); run(); torch.cuda.synchronize(); r0 = dw.clone()
+            T.conv_wgrad_order(1)
+            dw.zero_(); run(); torch.cuda.synchronize()
+            row.update({"grid3d_us": round(best[0], 2), "flat_us": round(best[1], 2),
+                        "rel_diff": float((dw - r0).norm() / r0.norm().clamp_min(1e-30))})
+            out.append(row)
+            print(f"{model:8s} {str(row['shape']):38s} x{calls} 3d {row['grid3d_us']:7.2f} "
+                  f"flat {row['flat_us']:7.2f} diff {row['rel_diff']:.1e}", flush=True)
             continue
         if a.atomic_ab:
             T.conv_wgrad_force(0, 0, 0, 1)
@@ -133,7 +179,8 @@ def main():
               f"best {best} {row['best_us']}", flush=True)
         del x, dy, dw, ref
     tot = {k: sum(r[k] * r["calls"] for r in out if r.get(k))
-           for k in ("auto_us", "igemm_us", "best_us", "noatomic_us")}
+           for k in ("auto_us", "igemm_us", "best_us", "noatomic_us", "grid3d_us", "flat_us",
+                     "atomic_us", "slab_us", "atomic_store_us", "slab_store_us")}
     print("per-step totals (us):", {k: round(v, 1) for k, v in tot.items()})
     if a.out:
         with open(a.out, "w") as f:
