@@ -1338,13 +1338,20 @@ inline WGPlan wgrad_dma_plan(const ConvGeom& g, bool force) {
   const long Mred = (long)g.N * g.P * g.Q;
   if (Mred >= (1L << 31) || (long)g.N * g.H * g.W * g.C >= (1L << 31)) return p;
   const int ncols = g.R * g.S * g.C;
-  // tile: BN divides C (one tap per column tile); BM over K
+  // tile: BN divides C (one tap per column tile); BM over K.
+  // 1x1 wgrads over >= 100K pixels (ResNet-50's 56x56 stage) stream dY and X
+  // from HBM: small tiles at two blocks per CU hide more latency than big
+  // tiles at one (64->256: 47 -> 32 us, 256->64: 49 -> 34 us, 256->128:
+  // 51 -> 45 us; profiles/r4/wgrad_sweep_56.json)
+  const bool stream = g.R == 1 && g.S == 1 && Mred >= 100352;
   const int* fw = g_wgrad_force;
   if (fw[0] > 0) {
     p.bm = fw[0]; p.bn = fw[1];
     const bool known = (p.bm == 256 && (p.bn == 128 || p.bn == 64)) || (p.bm == 128 && (p.bn == 128 || p.bn == 64)) ||
                        (p.bm == 64 && p.bn == 64);
     if (!known || g.K % p.bm != 0 || g.C % p.bn != 0) return p;
+  } else if (stream) {
+    p.bm = g.K % 128 == 0 ? 128 : 64; p.bn = 64;
   } else {
     if (g.K % 256 == 0 && g.C % 128 == 0) { p.bm = 256; p.bn = 128; }
     else if (g.K % 128 == 0 && g.C % 128 == 0) { p.bm = 128; p.bn = 128; }
@@ -1354,9 +1361,10 @@ inline WGPlan wgrad_dma_plan(const ConvGeom& g, bool force) {
   }
   p.tiles = (g.K / p.bm) * (ncols / p.bn);
   const int nsteps = (int)((Mred + 63) / 64);
-  // split the pixel reduction to ~one block per CU, not more: every split
-  // adds |dW| of fp32 partials to write and reduce
-  int splits = fw[2] > 0 ? fw[2] : 256 / p.tiles;
+  // split the pixel reduction to ~one block per CU (two for the streaming
+  // 1x1 passes, whose small tiles leave room for a second block), not
+  // more: every split adds |dW| of fp32 partials to write and reduce
+  int splits = fw[2] > 0 ? fw[2] : (stream ? 512 : 256) / p.tiles;
   if (fw[2] <= 0 && splits > nsteps / 8) splits = nsteps / 8;
   if (splits > nsteps) splits = nsteps;
   if (splits < 1) splits = 1;

@@ -47,7 +47,7 @@ class ResNet50:
         dev = arena.device
         self.training = True
         A = arena
-        self.stem = A.add("stem.conv", (width, 7, 7, in_ch), init="kaiming", store_grad=True)
+        self.stem = A.add("stem.conv", (width, 7, 7, in_ch), init="kaiming")
         self.stem_bn = (A.add("stem.bn.g", (width,), init="ones", decay=False, fp32_compute=True),
                         A.add("stem.bn.b", (width,), init="zeros", decay=False, fp32_compute=True))
         self.bn_state = {"stem": _BNState(width, dev)}
@@ -59,9 +59,9 @@ class ResNet50:
                 pre = f"s{si}.b{bi}"
                 blk = {
                     "stride": stride,
-                    "c1": A.add(pre + ".c1", (w, 1, 1, cin), init="kaiming", store_grad=True),
-                    "c2": A.add(pre + ".c2", (w, 3, 3, w), init="kaiming", store_grad=True),
-                    "c3": A.add(pre + ".c3", (w * 4, 1, 1, w), init="kaiming", store_grad=True),
+                    "c1": A.add(pre + ".c1", (w, 1, 1, cin), init="kaiming"),
+                    "c2": A.add(pre + ".c2", (w, 3, 3, w), init="kaiming"),
+                    "c3": A.add(pre + ".c3", (w * 4, 1, 1, w), init="kaiming"),
                 }
                 for k, c in (("bn1", w), ("bn2", w), ("bn3", w * 4)):
                     # zero-init the last BN gamma of each block (standard trick)
@@ -70,7 +70,7 @@ class ResNet50:
                               A.add(f"{pre}.{k}.b", (c,), init="zeros", decay=False, fp32_compute=True))
                     self.bn_state[f"{pre}.{k}"] = _BNState(c, dev)
                 if bi == 0:
-                    blk["down"] = A.add(pre + ".down", (w * 4, 1, 1, cin), init="kaiming", store_grad=True)
+                    blk["down"] = A.add(pre + ".down", (w * 4, 1, 1, cin), init="kaiming")
                     blk["down_bn"] = (A.add(pre + ".dbn.g", (w * 4,), init="ones", decay=False, fp32_compute=True),
                                       A.add(pre + ".dbn.b", (w * 4,), init="zeros", decay=False, fp32_compute=True))
                     self.bn_state[pre + ".dbn"] = _BNState(w * 4, dev)
@@ -159,7 +159,7 @@ class VGG16:
                 self.layers.append(("pool", None))
                 spatial //= 2
             else:
-                w = A.add(f"conv{ci}.w", (v, 3, 3, cin), init="kaiming", store_grad=True)
+                w = A.add(f"conv{ci}.w", (v, 3, 3, cin), init="kaiming")
                 b = A.add(f"conv{ci}.b", (v,), init="zeros", decay=False)
                 self.layers.append(("conv", (w, b)))
                 cin = v

@@ -390,9 +390,11 @@ class _Conv(Function):
             with _OnWgrad(dy, x) as ow:
                 # the bias gradient colsum(dy) rides on the wgrad kernel's dY reads;
                 # the LDS-heavy patch-staged wgrad only off the side stream
-                # the weight's only gradient writer in a step: the first write stores
-                _T().conv_wgrad(dy, x, w.grad, st, pd, 1, grad_mode(w), b.grad if b is not None else None,
-                                ow.s is None)
+                # accumulate into the optimizer-zeroed buffer: a store-mode first
+                # write costs a zero pass of dW on the fp32-atomic split paths
+                # (ResNet-50: 29 more zero launches per step when conv weights
+                # were store_grad), the optimizer's bulk zeroing does not
+                _T().conv_wgrad(dy, x, w.grad, st, pd, 1, 1, b.grad if b is not None else None, ow.s is None)
             if ctx.needs_input_grad[0]:
                 dx = torch.empty_like(x)
                 wt = getattr(w, "wt", None)

@@ -67,6 +67,8 @@ def main():
                     help="heuristic config, fp32-atomic split epilogue vs slab partials + reduce "
                          "(conv_wgrad_slab_policy), interleaved, both store and accumulate modes")
     ap.add_argument("--slab", type=int, default=1, help="slab policy for the other modes")
+    ap.add_argument("--min_hw", type=int, default=0, help="only shapes with H >= this")
+    ap.add_argument("--splits", default="1,2,4,8,16,32,64,128", help="forced split counts to sweep")
     a = ap.parse_args()
     _lib.load(required=True)
     T = torch.ops.tam
@@ -76,6 +78,8 @@ def main():
              [("vgg16",) + s for s in VGG] * ("vgg16" in a.models)
     out = []
     for model, N, H, W, C, K, R, st, pd, calls in shapes:
+        if H < a.min_hw:
+            continue
         P = (H + 2 * pd - R) // st + 1
         x = torch.randn(N, H, W, C, device=dev).to(torch.bfloat16)
         dy = torch.randn(N, P, P, K, device=dev).to(torch.bfloat16)
@@ -158,7 +162,7 @@ def main():
         for bm, bn in ((256, 128), (256, 64), (128, 128), (128, 64), (64, 64)):
             if K % bm or C % bn:
                 continue
-            for sp in (1, 2, 4, 8, 16, 32, 64, 128):
+            for sp in [int(v) for v in a.splits.split(",")]:
                 if sp > max(1, nsteps // 2):
                     continue
                 T.conv_wgrad_force(bm, bn, sp)
