@@ -756,6 +756,7 @@ void maxpool_forward_op(const Tensor& x, const Tensor& y, const Tensor& idx, int
                        (int)x.size(2), (int)x.size(3), (int)y.size(1), (int)y.size(2), (int)R,
                        (int)S, (int)st, (int)pad, cur_stream(x));
 }
+void maxpool_k3s2_policy_op(int64_t p) { tam::maxpool_k3s2_policy((int)p); }
 void maxpool_backward_op(const Tensor& dy, const Tensor& idx, const Tensor& dx, int64_t R, int64_t S,
                          int64_t st, int64_t pad) {
   check_bf16(dy, "dy"); check_bf16(dx, "dx");
@@ -812,6 +813,7 @@ void attn_short_policy_op(int64_t p) { tam::attn_short_policy((int)p); }
 // forced (bm, bn, splits) of the LDS-DMA conv wgrad (A/B sweeps; 0 = heuristic)
 void conv_wgrad_c64_policy_op(int64_t p) { tam::conv_wgrad_c64_policy((int)p); }
 void conv_wgrad_order_op(int64_t p) { tam::conv_wgrad_order((int)p); }
+void conv_stem_policy_op(int64_t p) { tam::conv_stem_policy((int)p); }
 void conv_wgrad_slab_policy_op(int64_t p) { tam::conv_wgrad_slab_policy((int)p); }
 void conv_wgrad_force_op(int64_t bm, int64_t bn, int64_t splits, int64_t noatomic) {
   tam::conv_wgrad_force((int)bm, (int)bn, (int)splits, (int)noatomic);
@@ -1071,6 +1073,7 @@ TORCH_LIBRARY(tam, m) {
   m.def("ln_backward(Tensor dy, Tensor x, Tensor g, Tensor mean, Tensor rstd, Tensor(a!) dx, Tensor(b!) dg, Tensor(c!) db, Tensor? addend=None) -> ()", &ln_backward_op);
   m.def("maxpool_forward(Tensor x, Tensor(a!) y, Tensor(b!) idx, int R, int S, int stride, int pad) -> ()", &maxpool_forward_op);
   m.def("maxpool_backward(Tensor dy, Tensor idx, Tensor(a!) dx, int R, int S, int stride, int pad) -> ()", &maxpool_backward_op);
+  m.def("maxpool_k3s2_policy(int policy) -> ()", &maxpool_k3s2_policy_op);
   m.def("avgpool_forward(Tensor x, Tensor(a!) y) -> ()", &avgpool_forward_op);
   m.def("avgpool_backward(Tensor dy, Tensor(a!) dx) -> ()", &avgpool_backward_op);
   m.def("softmax_xent(Tensor logits, Tensor labels, Tensor(a!)? dlogits, Tensor(b!) loss_rows, float smoothing, float grad_scale, int ignore_index) -> ()", &softmax_xent_op);
@@ -1090,6 +1093,7 @@ TORCH_LIBRARY(tam, m) {
   m.def("conv_wgrad_force(int bm, int bn, int splits, int noatomic=0) -> ()", &conv_wgrad_force_op);
   m.def("conv_wgrad_c64_policy(int policy) -> ()", &conv_wgrad_c64_policy_op);
   m.def("conv_wgrad_order(int flat) -> ()", &conv_wgrad_order_op);
+  m.def("conv_stem_policy(int policy) -> ()", &conv_stem_policy_op);
   m.def("conv_wgrad_slab_policy(int policy) -> ()", &conv_wgrad_slab_policy_op);
   m.def("conv_halo_policy(int policy) -> ()", &conv_halo_policy_op);
   m.def("colsum_policy(int policy) -> ()", &colsum_policy_op);

@@ -63,6 +63,7 @@ void ln_backward(const bf16_t* dy, const bf16_t* x, const float* g, const float*
 // pooling
 void maxpool_forward(const bf16_t* x, bf16_t* y, uint8_t* idx, int N, int H, int W, int C, int P,
                      int Q, int R, int S, int st, int pad, hipStream_t s);
+void maxpool_k3s2_policy(int p);   // 1: 3x3/s2/p1 backward kernel (default), 0: generic
 void maxpool_backward(const bf16_t* dy, const uint8_t* idx, bf16_t* dx, int N, int H, int W, int C,
                       int P, int Q, int R, int S, int st, int pad, hipStream_t s);
 void avgpool_forward(const bf16_t* x, bf16_t* y, int N, int HW, int C, hipStream_t s);

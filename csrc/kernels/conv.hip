@@ -68,6 +68,7 @@ long conv_dgrad_split_ws(const ConvGeom& g) {
 int conv_fwd(const bf16_t* x, const bf16_t* w, const ConvGeom& g, Epi ep, hipStream_t s, float* ws,
              long ws_floats) {
   const int M = g.N * g.P * g.Q, Kd = g.R * g.S * g.C;
+  if (conv_stem_fwd(x, w, g, ep, s)) return ep.stats ? 1 : 0;   // 7x7/s2 8->64 stem (conv_stem.hip)
   if (g_conv_dma && g.dil == 1) {
     CDArgs a = cd_fwd_args(x, w, g);
     if (g_conv_halo && launch_conv_halo(a, ep, s)) return ep.stats ? 1 : 0;

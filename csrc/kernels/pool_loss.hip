@@ -156,6 +156,64 @@ __global__ void maxpool_bwd8_kernel(const bf16_t* __restrict__ dy, const uint8_t
   }
 }
 
+// 3x3 / stride 2 / pad 1 (the ResNet stem pool): an input pixel lies in 1, 2
+// or 4 windows, found from the parities of h and w with no tap loop and no
+// runtime division (the generic kernel above spends its time in the 9-tap
+// loop's integer div / mod: 83 us for the 112x112x64 batch-64 stem, ~3x
+// its bytes at HBM rate)
+__global__ void __launch_bounds__(256) maxpool_bwd8_k3s2_kernel(const bf16_t* __restrict__ dy,
+                                                                 const uint8_t* __restrict__ idx,
+                                                                 bf16_t* __restrict__ dx, int N, int H, int W,
+                                                                 int C8, int P, int Q) {
+  const long total = (long)N * H * W * C8;
+  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < total; i += (long)gridDim.x * blockDim.x) {
+    const int c = (int)(i % C8) * 8;
+    const long t = i / C8;
+    const int w = (int)(t % W);
+    const long t2 = t / W;
+    const int h = (int)(t2 % H);
+    const int n = (int)(t2 / H);
+    // windows p with h = 2p - 1 + r, r in [0, 3): odd h -> p = (h+1)/2 (r=0)
+    // and (h-1)/2 (r=2); even h -> p = h/2 (r=1)
+    int ps[2], rs[2], np = 0;
+    if (h & 1) {
+      if ((h + 1) / 2 < P) { ps[np] = (h + 1) / 2; rs[np] = 0; ++np; }
+      ps[np] = (h - 1) / 2; rs[np] = 2; ++np;
+    } else {
+      if (h / 2 < P) { ps[np] = h / 2; rs[np] = 1; ++np; }
+    }
+    int qs[2], ss[2], nq = 0;
+    if (w & 1) {
+      if ((w + 1) / 2 < Q) { qs[nq] = (w + 1) / 2; ss[nq] = 0; ++nq; }
+      qs[nq] = (w - 1) / 2; ss[nq] = 2; ++nq;
+    } else {
+      if (w / 2 < Q) { qs[nq] = w / 2; ss[nq] = 1; ++nq; }
+    }
+    float acc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+    for (int a = 0; a < np; ++a)
+      for (int b = 0; b < nq; ++b) {
+        const long o = (((long)n * P + ps[a]) * Q + qs[b]) * (C8 * 8) + c;
+        const uint2 ix = *(const uint2*)(idx + o);
+        const uint4 d = *(const uint4*)(dy + o);
+        const uint32_t wd[4] = {d.x, d.y, d.z, d.w};
+        const uint32_t tap = (uint32_t)(rs[a] * 3 + ss[b]);
+#pragma unroll
+        for (int k = 0; k < 8; ++k) {
+          const uint32_t bb = ((k < 4 ? ix.x : ix.y) >> (8 * (k & 3))) & 0xffu;
+          const uint32_t wk = wd[k >> 1];
+          const float g = __uint_as_float((k & 1) ? (wk & 0xffff0000u) : (wk << 16));
+          if (bb == tap) acc[k] += g;
+        }
+      }
+    *(uint4*)(dx + i * 8) = make_uint4(pack_bf2(acc[0], acc[1]), pack_bf2(acc[2], acc[3]),
+                                       pack_bf2(acc[4], acc[5]), pack_bf2(acc[6], acc[7]));
+  }
+}
+
+// policy: 1 (default) the 3x3/s2/p1 kernel where it applies, 0 generic (A/B, tests)
+static int g_pool_k3s2 = 1;
+void maxpool_k3s2_policy(int p) { g_pool_k3s2 = p; }
+
 void maxpool_forward(const bf16_t* x, bf16_t* y, uint8_t* idx, int N, int H, int W, int C, int P,
                      int Q, int R, int S, int st, int pad, hipStream_t s) {
   if (C % 8 == 0) {
@@ -168,6 +226,12 @@ void maxpool_forward(const bf16_t* x, bf16_t* y, uint8_t* idx, int N, int H, int
 }
 void maxpool_backward(const bf16_t* dy, const uint8_t* idx, bf16_t* dx, int N, int H, int W, int C,
                       int P, int Q, int R, int S, int st, int pad, hipStream_t s) {
+  if (C % 8 == 0 && g_pool_k3s2 && R == 3 && S == 3 && st == 2 && pad == 1 && P == (H - 1) / 2 + 1 &&
+      Q == (W - 1) / 2 + 1) {
+    hipLaunchKernelGGL(maxpool_bwd8_k3s2_kernel, dim3(grid_cap((long)N * H * W * (C / 8))), dim3(256), 0, s, dy,
+                       idx, dx, N, H, W, C / 8, P, Q);
+    return;
+  }
   if (C % 8 == 0) {
     hipLaunchKernelGGL(maxpool_bwd8_kernel, dim3(grid_cap((long)N * H * W * (C / 8))), dim3(256), 0,
                        s, dy, idx, dx, N, H, W, C, P, Q, R, S, st, pad);

@@ -589,6 +589,43 @@ def test_conv_wgrad_slab_order(gpu, cfg):
         T().conv_wgrad_order(1)
 
 
+@pytest.mark.parametrize("shape", [(2, 224, 224), (3, 37, 29), (1, 16, 18)])
+def test_conv_stem(gpu, shape):
+    """ResNet stem forward kernel (conv_stem.hip: 7x7 / s2 / p3, 8 -> 64) vs
+    fp32 torch and vs the generic path: plain, bias + ReLU, and the BatchNorm
+    sums of the stored output (sharded fp64) -- tails in both P and Q."""
+    from tiresias_amd.ops.functional import BN_SHARDS
+    N, H, W = shape
+    torch.manual_seed(13)
+    x = torch.randn(N, H, W, 8, device=gpu).to(BF)
+    w = (torch.randn(64, 7, 7, 8, device=gpu) / math.sqrt(392)).to(BF)
+    b = torch.randn(64, device=gpu).to(BF)
+    P, Q = (H - 1) // 2 + 1, (W - 1) // 2 + 1
+    ref = _ref_conv(x, w, 2, 3)
+    outs = {}
+    try:
+        for pol in (1, 0):
+            T().conv_stem_policy(pol)
+            y = torch.empty(N, P, Q, 64, device=gpu, dtype=BF)
+            sums = torch.zeros(BN_SHARDS * 2 * 64, device=gpu, dtype=torch.float64)
+            done = T().conv_fwd(x, w, y, 2, 3, 1, None, False, sums)
+            assert rel_err(y, ref) < 1e-2, pol
+            if pol == 1:
+                assert done
+            if done:
+                yd = y.double().reshape(-1, 64)
+                tot = sums.view(BN_SHARDS, 128).sum(0)
+                assert rel_err(tot[:64], yd.sum(0)) < 1e-5 and rel_err(tot[64:], (yd * yd).sum(0)) < 1e-5, pol
+            yb = torch.empty_like(y)
+            T().conv_fwd(x, w, yb, 2, 3, 1, b, True)
+            assert rel_err(yb, (ref + b.float()).clamp_min(0)) < 1e-2, pol
+            outs[pol] = (y, yb)
+    finally:
+        T().conv_stem_policy(1)
+    for a_, b_ in zip(outs[1], outs[0]):
+        assert rel_err(a_, b_) < 1e-2
+
+
 # LDS-DMA conv core (conv_dma.h): every tile width, stride-2 fwd, 1x1 s2, M
 # tails, padding taps, bias+relu epilogue and the relu-masked dgrad
 @pytest.mark.parametrize("cfg", [(2, 12, 12, 64, 64, 3, 1, 1), (3, 9, 11, 128, 128, 3, 1, 1),
@@ -934,10 +971,14 @@ def test_layernorm(gpu, D, rows):
 
 # ------------------------------------------------------------------ pooling / loss
 @pytest.mark.parametrize("C", [16, 64, 5])
-def test_maxpool(gpu, C):
+@pytest.mark.parametrize("hw", [(17, 18), (16, 15)])
+def test_maxpool(gpu, C, hw):
+    """3x3 / s2 / p1 max pool vs torch; the backward on the parity-indexed
+    k3s2 kernel (C % 8 == 0) and on the generic tap loop, equal bit for bit."""
     torch.manual_seed(7)
-    x = torch.randn(2, 17, 18, C, device=gpu).to(BF)
-    P = (17 + 2 - 3) // 2 + 1; Q = (18 + 2 - 3) // 2 + 1
+    H, W = hw
+    x = torch.randn(2, H, W, C, device=gpu).to(BF)
+    P = (H + 2 - 3) // 2 + 1; Q = (W + 2 - 3) // 2 + 1
     y = torch.empty(2, P, Q, C, device=gpu, dtype=BF)
     idx = torch.empty(2, P, Q, C, device=gpu, dtype=torch.uint8)
     T().maxpool_forward(x, y, idx, 3, 3, 2, 1)
@@ -949,6 +990,13 @@ def test_maxpool(gpu, C):
     T().maxpool_backward(dy, idx, dx, 3, 3, 2, 1)
     g, = torch.autograd.grad(yf, [xf], dy.float().permute(0, 3, 1, 2))
     assert rel_err(dx, g.permute(0, 2, 3, 1)) < 1e-2
+    dx0 = torch.empty_like(x)
+    T().maxpool_k3s2_policy(0)
+    try:
+        T().maxpool_backward(dy, idx, dx0, 3, 3, 2, 1)
+    finally:
+        T().maxpool_k3s2_policy(1)
+    assert torch.equal(dx, dx0)
 
 
 def test_avgpool(gpu):

@@ -50,6 +50,9 @@ def main():
                     help="conv core: 1 LDS-DMA where the cost model picks it, 2 wherever eligible, 0 igemm only")
     ap.add_argument("--save_routes", default=None,
                     help="write the routing table (shipped decisions + the shapes tuned in this run) here")
+    ap.add_argument("--policy", action="append", default=[],
+                    help="name=value: call torch.ops.tam.<name>(value) before the runs (A/B switches, "
+                         "e.g. conv_stem_policy=0); repeatable")
     ap.add_argument("--conv_split", type=int, default=1,
                     help="split-K of under-filled LDS-DMA conv passes: 1 on (default), 0 off")
     a = ap.parse_args()
@@ -59,6 +62,9 @@ def main():
     torch.ops.tam.gemm_lib_policy(a.lib)
     torch.ops.tam.conv_dma_policy(a.conv_policy)
     torch.ops.tam.conv_split_policy(a.conv_split)
+    for kv in a.policy:
+        k, v = kv.split("=")
+        getattr(torch.ops.tam, k)(int(v))
     res = []
     for m in a.models.split(","):
         r = bench(m, batch=a.batch or None, steps=a.steps, warmup=a.warmup, graph=a.graph,
