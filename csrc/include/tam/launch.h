@@ -60,7 +60,11 @@ int conv_fwd(const bf16_t* x, const bf16_t* w, const ConvGeom& g, Epi ep, hipStr
 long conv_fwd_split_ws(const ConvGeom& g);
 // ResNet stem (7x7 / s2 / p3, C 8 -> K 64) forward kernel; false: not its shape
 bool conv_stem_fwd(const bf16_t* x, const bf16_t* w, const ConvGeom& g, const Epi& ep, hipStream_t s);
-void conv_stem_policy(int p);   // 1: stem kernel where it applies (default), 0: generic paths
+void conv_stem_policy(int p);   // 1: stem kernels where they apply (default), 0: generic paths
+// stem weight gradient (per-CU fp32 partial slabs + reduce); ws: conv_stem_wgrad_ws(g) floats
+long conv_stem_wgrad_ws(const ConvGeom& g);
+bool conv_stem_wgrad(const bf16_t* dy, const bf16_t* x, const ConvGeom& g, float* dw, int mode, float* ws,
+                     long ws_floats, hipStream_t s);
 long conv_dgrad_split_ws(const ConvGeom& g);
 void conv_split_policy(int p);   // 1: split-K of under-filled LDS-DMA passes (default), 0: off
 // dx[N*H*W][C]; wt = conv_weight_t(w) laid out [C][R][S][K] (ignored for 1x1/s1)

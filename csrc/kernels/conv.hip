@@ -185,6 +185,8 @@ void conv_wgrad_c64_policy(int p) { g_wgrad_c64 = p; }
 void conv_wgrad_order(int flat) { g_wgrad_flat = flat; }
 void conv_wgrad_slab_policy(int p) { g_wgrad_slab = p; }
 long conv_wgrad_split_ws(const ConvGeom& g) {
+  const long stem = conv_stem_wgrad_ws(g);     // the stem kernel's per-CU partial slabs
+  if (stem > 0) return stem;
   if (!g_conv_dma || (is_pointwise(g) && (long)g.N * g.P * g.Q < 100352 && g_conv_dma < 2)) return 0;
   return wgrad_dma_slab_floats(g, g_conv_dma >= 2);
 }
@@ -200,6 +202,9 @@ long conv_wgrad_split_ws(const ConvGeom& g) {
 int conv_wgrad(const bf16_t* dy, const bf16_t* x, const ConvGeom& g, Epi ep, hipStream_t s, float* dbias,
                bool allow_patch, float* ws, long ws_floats) {
   const int Mred = g.N * g.P * g.Q, Nc = g.R * g.S * g.C;
+  if (!dbias && ep.c_f32 && ep.ldc == Nc && ep.mode <= 1 &&
+      conv_stem_wgrad(dy, x, g, (float*)ep.c, ep.mode, ws, ws_floats, s))   // 7x7/s2 8->64 stem
+    return 0;
   if (g_conv_dma && g_wgrad_c64 && (allow_patch || g_wgrad_c64 >= 2) && ep.c_f32 && ep.ldc == Nc && ep.mode <= 1 &&
       launch_conv_wgrad_c64(dy, x, (float*)ep.c, g, ep.mode, g_wgrad_c64 >= 2 ? g_wgrad_c64 : 0, s,
                             g_conv_dma >= 2 || g_wgrad_c64 >= 2, dbias))

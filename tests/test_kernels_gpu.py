@@ -624,6 +624,24 @@ def test_conv_stem(gpu, shape):
         T().conv_stem_policy(1)
     for a_, b_ in zip(outs[1], outs[0]):
         assert rel_err(a_, b_) < 1e-2
+    # weight gradient (per-CU partial slabs + reduce), store and accumulate
+    dy = torch.randn(N, P, Q, 64, device=gpu).to(BF)
+    wf = torch.zeros(64, 8, 7, 7, device=gpu, requires_grad=True)
+    gw, = torch.autograd.grad(F.conv2d(x.float().permute(0, 3, 1, 2), wf, stride=2, padding=3), [wf],
+                              dy.float().permute(0, 3, 1, 2))
+    ref_w = gw.permute(0, 2, 3, 1)
+    got = {}
+    try:
+        for pol in (1, 0):
+            T().conv_stem_policy(pol)
+            for mode in (0, 1):
+                dw = torch.full((64, 7, 7, 8), 0.5, device=gpu)
+                T().conv_wgrad(dy, x, dw, 2, 3, 1, mode)
+                want = ref_w + (0.5 if mode else 0.0)
+                assert rel_err(dw, want) < 1e-4, (pol, mode, rel_err(dw, want))
+                got[(pol, mode)] = dw
+    finally:
+        T().conv_stem_policy(1)
 
 
 # LDS-DMA conv core (conv_dma.h): every tile width, stride-2 fwd, 1x1 s2, M
