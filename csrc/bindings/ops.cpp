@@ -905,8 +905,9 @@ void check_attn_view(const Tensor& t, const char* name) {
   check_bf16(t, name);
   TORCH_CHECK(t.dim() == 4 && t.size(3) == 64 && t.stride(3) == 1 && t.stride(2) == 64,
               "tam.attn: ", name, " must be a [B,S,H,64] view with packed heads");
-  TORCH_CHECK(t.stride(0) == t.size(1) * t.stride(1), "tam.attn: ", name, " batch stride");
-  TORCH_CHECK(t.stride(1) % 8 == 0, "tam.attn: ", name, " token stride alignment");
+  // any batch / token strides (batch-major [B,S,.] or a time-major [S,B,.]
+  // tensor viewed transposed), 16-byte aligned rows
+  TORCH_CHECK(t.stride(1) % 8 == 0 && t.stride(0) % 8 == 0, "tam.attn: ", name, " stride alignment");
 }
 void attn_forward_op(const Tensor& q, const Tensor& k, const Tensor& v, const Tensor& o,
                      const Tensor& lse, bool causal, double scale, const optional<Tensor>& kv_len) {
@@ -915,9 +916,10 @@ void attn_forward_op(const Tensor& q, const Tensor& k, const Tensor& v, const Te
   check_f32(lse, "lse");
   const int B = (int)q.size(0), Sq = (int)q.size(1), H = (int)q.size(2), Sk = (int)k.size(1);
   TORCH_CHECK(lse.numel() == (int64_t)B * H * Sq, "tam.attn: lse size");
+  TORCH_CHECK(k.stride(0) == v.stride(0), "tam.attn: k/v batch strides differ");
   tam::attn_forward(bp(q), bp(k), bp(v), bpm(o), lse.data_ptr<float>(), B, H, Sq, Sk, q.stride(1),
-                    k.stride(1), o.stride(1), causal, (float)scale, opt_ptr<const int>(kv_len),
-                    cur_stream(q));
+                    k.stride(1), o.stride(1), q.stride(0), k.stride(0), o.stride(0), causal, (float)scale,
+                    opt_ptr<const int>(kv_len), cur_stream(q));
 }
 void attn_backward_op(const Tensor& q, const Tensor& k, const Tensor& v, const Tensor& o,
                       const Tensor& dout, const Tensor& lse, const Tensor& dq, const Tensor& dk,
@@ -926,8 +928,10 @@ void attn_backward_op(const Tensor& q, const Tensor& k, const Tensor& v, const T
   check_attn_view(q, "q"); check_attn_view(k, "k"); check_attn_view(v, "v"); check_attn_view(o, "o");
   check_attn_view(dout, "dout"); check_attn_view(dq, "dq"); check_attn_view(dk, "dk");
   check_attn_view(dv, "dv");
-  TORCH_CHECK(dout.stride(1) == o.stride(1), "tam.attn_bwd: dout must match o layout");
-  TORCH_CHECK(dq.stride(1) == q.stride(1) && dk.stride(1) == k.stride(1) && dv.stride(1) == k.stride(1),
+  TORCH_CHECK(dout.stride(1) == o.stride(1) && dout.stride(0) == o.stride(0), "tam.attn_bwd: dout must match o layout");
+  TORCH_CHECK(dq.stride(1) == q.stride(1) && dk.stride(1) == k.stride(1) && dv.stride(1) == k.stride(1) &&
+                  dq.stride(0) == q.stride(0) && dk.stride(0) == k.stride(0) && dv.stride(0) == k.stride(0) &&
+                  v.stride(0) == k.stride(0) && v.stride(1) == k.stride(1),
               "tam.attn_bwd: grads must match input layouts");
   const int B = (int)q.size(0), Sq = (int)q.size(1), H = (int)q.size(2), Sk = (int)k.size(1);
   check_f32(dq_acc, "dq_acc"); check_f32(delta, "delta");
@@ -935,7 +939,8 @@ void attn_backward_op(const Tensor& q, const Tensor& k, const Tensor& v, const T
               "tam.attn_bwd: workspace sizes");
   tam::attn_backward(bp(q), bp(k), bp(v), bp(o), bp(dout), lse.data_ptr<float>(), bpm(dq), bpm(dk),
                      bpm(dv), dq_acc.data_ptr<float>(), delta.data_ptr<float>(), B, H, Sq, Sk,
-                     q.stride(1), k.stride(1), o.stride(1), causal, (float)scale,
+                     q.stride(1), k.stride(1), o.stride(1), q.stride(0), k.stride(0), o.stride(0), causal,
+                     (float)scale,
                      opt_ptr<const int>(kv_len), cur_stream(q));
 }
 

@@ -1344,7 +1344,10 @@ inline WGPlan wgrad_dma_plan(const ConvGeom& g, bool force) {
   // from HBM: small tiles at two blocks per CU hide more latency than big
   // tiles at one (64->256: 47 -> 32 us, 256->64: 49 -> 34 us, 256->128:
   // 51 -> 45 us; profiles/r4/wgrad_sweep_56.json)
-  const bool stream = g.R == 1 && g.S == 1 && Mred >= 100352;
+  // The same holds for 3x3 wgrads over >= 256K pixels with K % 128 == 0
+  // (VGG-16's 112x112 128->128: 322 -> 264 us at 128x64 / 28 splits;
+  // profiles/r4/wgrad_sweep_vgg.json); the 56x56 VGG layers stay on 256x128.
+  const bool stream = (g.R == 1 && g.S == 1 && Mred >= 100352) || (Mred >= 262144 && g.K % 128 == 0);
   const int* fw = g_wgrad_force;
   if (fw[0] > 0) {
     p.bm = fw[0]; p.bn = fw[1];

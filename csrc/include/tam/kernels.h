@@ -98,16 +98,18 @@ void adam_step(float* w, float* g, float* m, float* v, bf16_t* wb, long n, float
                float b2, float eps, float wd, int step, float gscale, int zero_grad,
                hipStream_t s, const unsigned* guard = nullptr);
 
-// fused attention (bf16, head_dim 64), layout [B][S][H][64] (token-major)
+// fused attention (bf16, head_dim 64): element (b, s, h, d) at b * *_bstride +
+// s * *_stride + 64 h + d (batch-major [B][S][H][64], or a time-major
+// [S][B][H][64] tensor with bstride = H*64 per batch row)
 void attn_forward(const bf16_t* q, const bf16_t* k, const bf16_t* v, bf16_t* o, float* lse, int B,
-                  int H, int Sq, int Sk, long q_stride, long kv_stride, long o_stride, int causal,
-                  float scale, const int* kv_len, hipStream_t s);
+                  int H, int Sq, int Sk, long q_stride, long kv_stride, long o_stride, long q_bstride,
+                  long kv_bstride, long o_bstride, int causal, float scale, const int* kv_len, hipStream_t s);
 void attn_short_policy(int p);   // 1: Sk <= 128 backward in one fused launch (default)
 void attn_backward(const bf16_t* q, const bf16_t* k, const bf16_t* v, const bf16_t* o,
                    const bf16_t* dout, const float* lse, bf16_t* dq, bf16_t* dk, bf16_t* dv,
                    float* dq_acc, float* delta, int B, int H, int Sq, int Sk, long q_stride,
-                   long kv_stride, long o_stride, int causal, float scale, const int* kv_len,
-                   hipStream_t s);
+                   long kv_stride, long o_stride, long q_bstride, long kv_bstride, long o_bstride, int causal,
+                   float scale, const int* kv_len, hipStream_t s);
 
 // LSTM cell pointwise (gates = x W_ih^T + h W_hh^T + b precomputed, fp32)
 void lstm_cell_forward(const float* gates, const float* c_prev, float* c_out, bf16_t* h_out,

@@ -85,6 +85,7 @@ __global__ void __launch_bounds__(256) attn_fwd_kernel(const bf16_t* __restrict_
                                                         bf16_t* __restrict__ O,
                                                         float* __restrict__ LSE, int H, int Sq,
                                                         int Sk, long qs, long kvs, long os,
+                                                        long qb, long kvb, long ob,
                                                         int causal, float scale,
                                                         const int* __restrict__ kv_len) {
   __shared__ __attribute__((aligned(16))) char smem[2 * AT * AD * 2];
@@ -96,9 +97,9 @@ __global__ void __launch_bounds__(256) attn_fwd_kernel(const bf16_t* __restrict_
   const int qw = q0 + 16 * w + (lane & 15);   // this lane's query
   const int klen = kv_len ? min(Sk, kv_len[b]) : Sk;
 
-  const bf16_t* Qb = Q + (long)b * Sq * qs + h * AD;
-  const bf16_t* Kb = K + (long)b * Sk * kvs + h * AD;
-  const bf16_t* Vb = V + (long)b * Sk * kvs + h * AD;
+  const bf16_t* Qb = Q + (long)b * qb + h * AD;
+  const bf16_t* Kb = K + (long)b * kvb + h * AD;
+  const bf16_t* Vb = V + (long)b * kvb + h * AD;
 
   // Q^T fragments as the B operand: lane holds Q[q = lane&15][d = 8g + j + 32ks]
   s16x8_t qf[2];
@@ -172,7 +173,7 @@ __global__ void __launch_bounds__(256) attn_fwd_kernel(const bf16_t* __restrict_
   }
   if (qw < Sq) {
     const float inv = l > 0.f ? 1.f / l : 0.f;
-    bf16_t* Ob = O + ((long)b * Sq + qw) * os + h * AD;
+    bf16_t* Ob = O + (long)b * ob + (long)qw * os + h * AD;
 #pragma unroll
     for (int mt = 0; mt < 4; ++mt) {
       const int d = 16 * mt + 4 * g;
@@ -188,14 +189,14 @@ __global__ void __launch_bounds__(256) attn_fwd_kernel(const bf16_t* __restrict_
 // accumulator ([B][Sq][H][64]) -- one launch instead of delta + a memset
 __global__ void attn_delta_kernel(const bf16_t* __restrict__ O, const bf16_t* __restrict__ dO,
                                   float* __restrict__ delta, float* __restrict__ dq_acc, int B,
-                                  int H, int Sq, long os) {
+                                  int H, int Sq, long os, long ob) {
   const long row = blockIdx.x * 4L + (threadIdx.x >> 6);
   const int lane = threadIdx.x & 63;
   if (row >= (long)B * H * Sq) return;
   const int q = (int)(row % Sq);
   const long bh = row / Sq;
   const int h = (int)(bh % H), b = (int)(bh / H);
-  const long off = ((long)b * Sq + q) * os + h * AD + lane;
+  const long off = (long)b * ob + (long)q * os + h * AD + lane;
   dq_acc[(((long)b * Sq + q) * H + h) * AD + lane] = 0.f;
   float v = bf2f(O[off]) * bf2f(dO[off]);
   v = wave_sum(v);
@@ -207,7 +208,8 @@ __global__ void __launch_bounds__(256) attn_bwd_kernel(
     const bf16_t* __restrict__ Q, const bf16_t* __restrict__ K, const bf16_t* __restrict__ V,
     const bf16_t* __restrict__ dO, const float* __restrict__ LSE, const float* __restrict__ DELTA,
     bf16_t* __restrict__ dK, bf16_t* __restrict__ dV, float* __restrict__ dQacc, int H, int Sq,
-    int Sk, long qs, long kvs, long os, int causal, float scale, const int* __restrict__ kv_len) {
+    int Sk, long qs, long kvs, long os, long qb, long kvb, long ob, int causal, float scale,
+    const int* __restrict__ kv_len) {
   // LDS: Q row image, Q^T image (rho), dO row image, dO^T image (rho), K^T image, dS image,
   //      lse[64], delta[64]
   __shared__ __attribute__((aligned(16))) char smem[6 * AT * AD * 2 + 2 * AT * 4];
@@ -226,10 +228,10 @@ __global__ void __launch_bounds__(256) attn_bwd_kernel(
   const int klen = kv_len ? min(Sk, kv_len[b]) : Sk;
   const int kvw = k0 + 16 * w + (lane & 15);   // this lane's key (column of S)
 
-  const bf16_t* Qb = Q + (long)b * Sq * qs + h * AD;
-  const bf16_t* dOb = dO + (long)b * Sq * os + h * AD;
-  const bf16_t* Kb = K + (long)b * Sk * kvs + h * AD;
-  const bf16_t* Vb = V + (long)b * Sk * kvs + h * AD;
+  const bf16_t* Qb = Q + (long)b * qb + h * AD;
+  const bf16_t* dOb = dO + (long)b * ob + h * AD;
+  const bf16_t* Kb = K + (long)b * kvb + h * AD;
+  const bf16_t* Vb = V + (long)b * kvb + h * AD;
   const float* lse_b = LSE + ((long)b * H + h) * Sq;
   const float* del_b = DELTA + ((long)b * H + h) * Sq;
 
@@ -332,8 +334,8 @@ __global__ void __launch_bounds__(256) attn_bwd_kernel(
       }
   }
   if (kvw < Sk) {
-    bf16_t* dKb = dK + ((long)b * Sk + kvw) * kvs + h * AD;
-    bf16_t* dVb = dV + ((long)b * Sk + kvw) * kvs + h * AD;
+    bf16_t* dKb = dK + (long)b * kvb + (long)kvw * kvs + h * AD;
+    bf16_t* dVb = dV + (long)b * kvb + (long)kvw * kvs + h * AD;
 #pragma unroll
     for (int mt = 0; mt < 4; ++mt) {
       const int d = 16 * mt + 4 * g;
@@ -358,7 +360,8 @@ __global__ void __launch_bounds__(512) attn_bwd_short_kernel(
     const bf16_t* __restrict__ Q, const bf16_t* __restrict__ K, const bf16_t* __restrict__ V,
     const bf16_t* __restrict__ O, const bf16_t* __restrict__ dO, const float* __restrict__ LSE,
     bf16_t* __restrict__ dQ, bf16_t* __restrict__ dK, bf16_t* __restrict__ dV, int H, int Sq, int Sk,
-    long qs, long kvs, long os, int causal, float scale, const int* __restrict__ kv_len) {
+    long qs, long kvs, long os, long qb, long kvb, long ob, int causal, float scale,
+    const int* __restrict__ kv_len) {
   // LDS: Q row image, Q^T image (rho), dO row image, dO^T image (rho), O row
   //      image (delta), K [kv][d] image (128 rows), dS [kv][q] image (128 rows),
   //      lse[64], delta[64]
@@ -380,11 +383,11 @@ __global__ void __launch_bounds__(512) attn_bwd_short_kernel(
   const int klen = kv_len ? min(Sk, kv_len[b]) : Sk;
   const int kvw = 16 * w + (lane & 15);               // this lane's key (0..127)
 
-  const bf16_t* Qb = Q + (long)b * Sq * qs + h * AD;
-  const bf16_t* dOb = dO + (long)b * Sq * os + h * AD;
-  const bf16_t* Ob = O + (long)b * Sq * os + h * AD;
-  const bf16_t* Kb = K + (long)b * Sk * kvs + h * AD;
-  const bf16_t* Vb = V + (long)b * Sk * kvs + h * AD;
+  const bf16_t* Qb = Q + (long)b * qb + h * AD;
+  const bf16_t* dOb = dO + (long)b * ob + h * AD;
+  const bf16_t* Ob = O + (long)b * ob + h * AD;
+  const bf16_t* Kb = K + (long)b * kvb + h * AD;
+  const bf16_t* Vb = V + (long)b * kvb + h * AD;
   const float* lse_b = LSE + ((long)b * H + h) * Sq;
 
   s16x8_t kf[2], vf[2];
@@ -502,13 +505,13 @@ __global__ void __launch_bounds__(512) attn_bwd_short_kernel(
         const int q = q0 + 16 * (w & 3) + 4 * g + r;
         if (q < Sq) {
           const int d = 32 * (w >> 2) + 16 * nt + (lane & 15);
-          dQ[((long)b * Sq + q) * qs + h * AD + d] = f2bf(dq[nt][r] * scale);
+          dQ[(long)b * qb + (long)q * qs + h * AD + d] = f2bf(dq[nt][r] * scale);
         }
       }
   }
   if (kvw < Sk) {
-    bf16_t* dKb = dK + ((long)b * Sk + kvw) * kvs + h * AD;
-    bf16_t* dVb = dV + ((long)b * Sk + kvw) * kvs + h * AD;
+    bf16_t* dKb = dK + (long)b * kvb + (long)kvw * kvs + h * AD;
+    bf16_t* dVb = dV + (long)b * kvb + (long)kvw * kvs + h * AD;
 #pragma unroll
     for (int mt = 0; mt < 4; ++mt) {
       const int d = 16 * mt + 4 * g;
@@ -521,20 +524,20 @@ __global__ void __launch_bounds__(512) attn_bwd_short_kernel(
 
 // dq (bf16, strided like Q) = dq_acc (fp32, packed [B][Sq][H][64])
 __global__ void attn_dq_cast_kernel(const float* __restrict__ acc, bf16_t* __restrict__ dq, long n,
-                                    int HD, long qs) {
+                                    int HD, int Sq, long qs, long qb) {
   for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < n; i += (long)gridDim.x * blockDim.x) {
     const long tok = i / HD;
     const int c = (int)(i % HD);
-    dq[tok * qs + c] = f2bf(acc[i]);
+    dq[(tok / Sq) * qb + (tok % Sq) * qs + c] = f2bf(acc[i]);
   }
 }
 
 void attn_forward(const bf16_t* q, const bf16_t* k, const bf16_t* v, bf16_t* o, float* lse, int B,
-                  int H, int Sq, int Sk, long q_stride, long kv_stride, long o_stride, int causal,
-                  float scale, const int* kv_len, hipStream_t s) {
+                  int H, int Sq, int Sk, long q_stride, long kv_stride, long o_stride, long q_bstride,
+                  long kv_bstride, long o_bstride, int causal, float scale, const int* kv_len, hipStream_t s) {
   dim3 grid((Sq + AT - 1) / AT, B * H);
   hipLaunchKernelGGL(attn_fwd_kernel, grid, dim3(256), 0, s, q, k, v, o, lse, H, Sq, Sk, q_stride,
-                     kv_stride, o_stride, causal, scale, kv_len);
+                     kv_stride, o_stride, q_bstride, kv_bstride, o_bstride, causal, scale, kv_len);
 }
 
 // 1 (default): key ranges <= 128 take the one-launch short-sequence backward;
@@ -545,24 +548,26 @@ void attn_short_policy(int p) { g_attn_short = p; }
 void attn_backward(const bf16_t* q, const bf16_t* k, const bf16_t* v, const bf16_t* o,
                    const bf16_t* dout, const float* lse, bf16_t* dq, bf16_t* dk, bf16_t* dv,
                    float* dq_acc, float* delta, int B, int H, int Sq, int Sk, long q_stride,
-                   long kv_stride, long o_stride, int causal, float scale, const int* kv_len,
-                   hipStream_t s) {
+                   long kv_stride, long o_stride, long q_bstride, long kv_bstride, long o_bstride, int causal,
+                   float scale, const int* kv_len, hipStream_t s) {
   if (Sk <= ATS_K && g_attn_short) {
     hipLaunchKernelGGL(attn_bwd_short_kernel, dim3(B * H), dim3(512), 0, s, q, k, v, o, dout, lse, dq, dk, dv,
-                       H, Sq, Sk, q_stride, kv_stride, o_stride, causal, scale, kv_len);
+                       H, Sq, Sk, q_stride, kv_stride, o_stride, q_bstride, kv_bstride, o_bstride, causal, scale,
+                       kv_len);
     return;
   }
   const long rows = (long)B * H * Sq;
   hipLaunchKernelGGL(attn_delta_kernel, dim3((rows + 3) / 4), dim3(256), 0, s, o, dout, delta, dq_acc,
-                     B, H, Sq, o_stride);
+                     B, H, Sq, o_stride, o_bstride);
   const long nq = (long)B * Sq * H * AD;
   dim3 grid((Sk + AT - 1) / AT, B * H);
   hipLaunchKernelGGL(attn_bwd_kernel, grid, dim3(256), 0, s, q, k, v, dout, lse, delta, dk, dv,
-                     dq_acc, H, Sq, Sk, q_stride, kv_stride, o_stride, causal, scale, kv_len);
+                     dq_acc, H, Sq, Sk, q_stride, kv_stride, o_stride, q_bstride, kv_bstride, o_bstride, causal,
+                     scale, kv_len);
   long blocks = (nq + 255) / 256;
   if (blocks > 4096) blocks = 4096;
-  hipLaunchKernelGGL(attn_dq_cast_kernel, dim3(blocks), dim3(256), 0, s, dq_acc, dq, nq, H * AD,
-                     q_stride);
+  hipLaunchKernelGGL(attn_dq_cast_kernel, dim3(blocks), dim3(256), 0, s, dq_acc, dq, nq, H * AD, Sq,
+                     q_stride, q_bstride);
 }
 
 }  // namespace tam

@@ -1194,6 +1194,35 @@ def test_attention(gpu, B, H, Sq, Sk, causal, short):
     assert rel_err(dv, gv) < 2e-2
 
 
+@pytest.mark.parametrize("Sq,Sk", [(50, 50), (37, 160)])
+@pytest.mark.parametrize("short", [1, 0])
+def test_cross_attention_time_major(gpu, Sq, Sk, short):
+    """Time-major cross attention (GNMT: q [Sq,B,H*64], kv [Sk,B,2*H*64],
+    output [Sq,B,H*64]; the kernels run on transposed [B,S,H,64] views via
+    batch / token strides) equals the batch-major call on the transposed
+    copies, forward and both backward kernel families."""
+    import tiresias_amd.ops.functional as Fx
+    B, H = 3, 4
+    torch.manual_seed(17)
+    T().attn_short_policy(short)
+    try:
+        q = torch.randn(Sq, B, H * 64, device=gpu).to(BF).requires_grad_(True)
+        kv = torch.randn(Sk, B, 2 * H * 64, device=gpu).to(BF).requires_grad_(True)
+        o = Fx.cross_attention(q, kv, H, time_major=True)
+        assert o.shape == (Sq, B, H * 64)
+        qb = q.detach().transpose(0, 1).contiguous().requires_grad_(True)
+        kvb = kv.detach().transpose(0, 1).contiguous().requires_grad_(True)
+        ob = Fx.cross_attention(qb, kvb, H)
+        assert torch.equal(o.detach(), ob.detach().transpose(0, 1))
+        do = torch.randn_like(o)
+        gq, gkv = torch.autograd.grad(o, [q, kv], do)
+        gqb, gkvb = torch.autograd.grad(ob, [qb, kvb], do.transpose(0, 1).contiguous())
+        assert rel_err(gq, gqb.transpose(0, 1)) < 1e-3
+        assert rel_err(gkv, gkvb.transpose(0, 1)) < 1e-3
+    finally:
+        T().attn_short_policy(1)
+
+
 @pytest.mark.parametrize("short", [1, 0])
 def test_attention_kvlen_backward(gpu, short):
     """Padded key ranges (kv_len) in the backward of both kernel families."""

@@ -111,6 +111,8 @@ class Trainer:
             else:
                 logits = self.model.forward(d)
             labels = d["labels"]
+            if getattr(self.model, "logits_time_major", False):
+                labels = labels.t()                  # [B,T] -> the logits' [T,B] row order
             rows = labels.numel()
             loss, dlog = Fx.softmax_xent(logits, labels, smoothing=self.spec.smoothing,
                                          ignore_index=-100, normalizer=rows)

@@ -274,6 +274,8 @@ class GNMT:
     # 2 x 8 MB of W_hh through the 4 MB per-XCD L2s): measured on MI355X,
     # hipGraph step 15.5 ms one stream vs 16.3 ms with branches
     branch_default = False
+    # forward returns [T,B,V]; the trainer transposes the [B,T] labels to match
+    logits_time_major = True
     # whole-sequence persistent recurrences; off for the rest of the job
     # after a barrier timeout (Worker.run reads the job's own err words)
     persist = True
@@ -324,11 +326,15 @@ class GNMT:
         # target embedding, so it runs alongside the whole encoder stack;
         # branch 0: the reverse half of the bidirectional layer alongside the
         # forward half (ops/functional.py::on_branch; no-op without streams)
+        # everything stays time-major [T,B,.]: the attention kernels take
+        # batch / token strides and the logits come out [T,B,V] with the
+        # labels transposed to match (logits_time_major), so no activation
+        # or gradient is ever re-laid between the recurrences and attention
         tgt_t = tgt_in.t().contiguous()
         with Fx.on_branch(1, tgt_t):
             y = Fx.embedding(tgt_t, self.tgt_emb)
             d0 = lstm(y, self.dec[0], model=self)                    # [T,B,H]
-            q = Fx.linear(d0.transpose(0, 1).contiguous(), self.att_q)   # [B,T,H]
+            q = Fx.linear(d0, self.att_q)                            # [T,B,H]
         x = Fx.embedding(src.t().contiguous(), self.src_emb)
         with Fx.on_branch(0, x):
             bw = lstm(x, self.enc[1], reverse=True, model=self)
@@ -338,16 +344,15 @@ class GNMT:
         for i, p in enumerate(self.enc[3:]):
             o = lstm(h, p, model=self)
             h = Fx.add(h, o) if i >= 0 else o          # residual from layer 3 on
-        mem = h.transpose(0, 1).contiguous()             # [B,S,H]
-        kv = Fx.linear(mem, self.att_kv)                 # [B,S,2H]
+        kv = Fx.linear(h, self.att_kv)                   # [S,B,2H]
         d0, q = Fx.join_branch(1, d0, q)
-        ctxv = Fx.cross_attention(q, kv, self.heads).transpose(0, 1).contiguous()  # [T,B,H]
+        ctxv = Fx.cross_attention(q, kv, self.heads, time_major=True)   # [T,B,H]
         h = d0
         for i, p in enumerate(self.dec[1:]):
             o = lstm(torch.cat([h, ctxv], 2), p, model=self)
             h = Fx.add(h, o) if i >= 1 else o
-        out = torch.cat([h, ctxv], 2).transpose(0, 1).contiguous()   # [B,T,2H]
-        return Fx.linear(out, self.cls_w, self.cls_b)
+        out = torch.cat([h, ctxv], 2)                    # [T,B,2H]
+        return Fx.linear(out, self.cls_w, self.cls_b)    # [T,B,V] (logits_time_major)
 
     def buffers(self):
         return {}

@@ -970,8 +970,12 @@ class _Attn(Function):
 
     @staticmethod
     def forward(ctx, q_src, kv_src, H: int, q_slot: int, nq: int, k_slot: int, v_slot: int,
-                nkv: int, causal: bool, kv_len, kv_hold=None):
+                nkv: int, causal: bool, kv_len, kv_hold=None, tm: bool = False):
+        # tm: q_src / kv_src / the output are time-major [S,B,.] (GNMT's
+        # recurrent layout); the kernels take batch and token strides, so the
+        # [B,S,H,64] views are transposes and no layout copy is made
         same = q_src is kv_src
+        ctx.tm = tm
         # kv_hold: several attention calls read different slots of ONE packed
         # K/V tensor (the decoder's batched cross-attention projection); they
         # write their slots into one shared gradient buffer and only the call
@@ -982,30 +986,33 @@ class _Attn(Function):
         if kv_hold is not None:
             ctx.kv_idx = kv_hold["n"]
             kv_hold["n"] += 1
-        B, Sq, _ = q_src.shape
-        Sk = kv_src.shape[1]
-        qv = q_src.view(B, Sq, nq, H, 64)[:, :, q_slot]
-        kvv = kv_src.view(B, Sk, nkv, H, 64)
+        qv, kvv, B, Sq, Sk = _attn_views(q_src, kv_src, H, nq, nkv, q_slot, tm)
         kv_, vv = kvv[:, :, k_slot], kvv[:, :, v_slot]
         scale = 1.0 / math.sqrt(64)
         if q_src.is_cuda:
-            o = torch.empty(B, Sq, H, 64, dtype=BF16, device=q_src.device)
+            ob = torch.empty((Sq, B, H, 64) if tm else (B, Sq, H, 64), dtype=BF16, device=q_src.device)
+            o = ob.transpose(0, 1) if tm else ob
             lse = torch.empty(B, H, Sq, dtype=torch.float32, device=q_src.device)
             _T().attn_forward(qv, kv_, vv, o, lse, causal, scale, kv_len)
         else:
             of, lse = _attn_ref(qv, kv_, vv, causal, scale, kv_len)
-            o = of.to(BF16).contiguous()
+            ob = (of.transpose(0, 1) if tm else of).to(BF16).contiguous()
         ctx.cfg = (same, H, q_slot, nq, k_slot, v_slot, nkv, causal, scale)
-        ctx.save_for_backward(q_src, kv_src, o, lse, kv_len)
-        return o.view(B, Sq, H * 64)
+        ctx.save_for_backward(q_src, kv_src, ob, lse, kv_len)
+        return ob.view(Sq, B, H * 64) if tm else ob.view(B, Sq, H * 64)
 
     @staticmethod
     def backward(ctx, do):
-        q_src, kv_src, o, lse, kv_len = ctx.saved_tensors
+        q_src, kv_src, ob, lse, kv_len = ctx.saved_tensors
         same, H, q_slot, nq, k_slot, v_slot, nkv, causal, scale = ctx.cfg
-        B, Sq, _ = q_src.shape
-        Sk = kv_src.shape[1]
-        do = do.contiguous().view(B, Sq, H, 64)
+        tm = ctx.tm
+        qv, kvv, B, Sq, Sk = _attn_views(q_src, kv_src, H, nq, nkv, q_slot, tm)
+        if tm:
+            o = ob.transpose(0, 1)
+            do = do.contiguous().view(Sq, B, H, 64).transpose(0, 1)
+        else:
+            o = ob
+            do = do.contiguous().view(B, Sq, H, 64)
         alloc = torch.empty_like if q_src.is_cuda else torch.zeros_like
         dq_src = alloc(q_src)
         hold = ctx.kv_hold
@@ -1015,10 +1022,7 @@ class _Attn(Function):
             dkv_src = hold["buf"]
         else:
             dkv_src = dq_src if same else alloc(kv_src)
-        qv = q_src.view(B, Sq, nq, H, 64)[:, :, q_slot]
-        kvv = kv_src.view(B, Sk, nkv, H, 64)
-        dqv = dq_src.view(B, Sq, nq, H, 64)[:, :, q_slot]
-        dkvv = dkv_src.view(B, Sk, nkv, H, 64)
+        dqv, dkvv, _, _, _ = _attn_views(dq_src, dkv_src, H, nq, nkv, q_slot, tm)
         if q_src.is_cuda:
             dq_acc = torch.empty(B, Sq, H, 64, dtype=torch.float32, device=q_src.device)
             delta = torch.empty(B, H, Sq, dtype=torch.float32, device=q_src.device)
@@ -1036,10 +1040,26 @@ class _Attn(Function):
             dkvv[:, :, k_slot].copy_(gk.to(BF16))
             dkvv[:, :, v_slot].copy_(gv.to(BF16))
         if same:
-            return dq_src, None, None, None, None, None, None, None, None, None, None
+            return dq_src, None, None, None, None, None, None, None, None, None, None, None
         if hold is not None and ctx.kv_idx != 0:
             dkv_src = None                 # slots written; the first caller returns the buffer
-        return dq_src, dkv_src, None, None, None, None, None, None, None, None, None
+        return dq_src, dkv_src, None, None, None, None, None, None, None, None, None, None
+
+
+def _attn_views(q_src, kv_src, H, nq, nkv, q_slot, tm):
+    """[B,S,H,64] views of the packed q / kv sources (transposes of the
+    time-major tensors when tm) and (B, Sq, Sk)."""
+    if tm:
+        Sq, B, _ = q_src.shape
+        Sk = kv_src.shape[0]
+        qv = q_src.view(Sq, B, nq, H, 64)[:, :, q_slot].transpose(0, 1)
+        kvv = kv_src.view(Sk, B, nkv, H, 64).transpose(0, 1)
+    else:
+        B, Sq, _ = q_src.shape
+        Sk = kv_src.shape[1]
+        qv = q_src.view(B, Sq, nq, H, 64)[:, :, q_slot]
+        kvv = kv_src.view(B, Sk, nkv, H, 64)
+    return qv, kvv, B, Sq, Sk
 
 
 def self_attention(qkv: torch.Tensor, heads: int, causal: bool = False,
@@ -1051,11 +1071,14 @@ def self_attention(qkv: torch.Tensor, heads: int, causal: bool = False,
 
 def cross_attention(q: torch.Tensor, kv: torch.Tensor, heads: int,
                     kv_len: Optional[torch.Tensor] = None, k_slot: int = 0, v_slot: int = 1,
-                    nkv: int = 2, kv_hold: Optional[dict] = None) -> torch.Tensor:
+                    nkv: int = 2, kv_hold: Optional[dict] = None, time_major: bool = False) -> torch.Tensor:
     """q: [B,Sq,H*64], kv: [B,Sk,nkv*H*64] (K at slot k_slot, V at v_slot)
-    -> [B,Sq,H*64]. Calls sharing one packed kv pass the same ``kv_hold``
+    -> [B,Sq,H*64]; time_major: q [Sq,B,.], kv [Sk,B,.] -> [Sq,B,H*64] with
+    no layout copies. Calls sharing one packed kv pass the same ``kv_hold``
     dict (``{"n": 0}``, fresh per forward); see _Attn."""
-    return _Attn.apply(q, kv, heads, 0, 1, k_slot, v_slot, nkv, False, kv_len, kv_hold)
+    if time_major:
+        q, kv = q.contiguous(), kv.contiguous()
+    return _Attn.apply(q, kv, heads, 0, 1, k_slot, v_slot, nkv, False, kv_len, kv_hold, time_major)
 
 
 # ============================================================ residual add
