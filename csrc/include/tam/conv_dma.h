@@ -1347,7 +1347,12 @@ inline WGPlan wgrad_dma_plan(const ConvGeom& g, bool force) {
   // The same holds for 3x3 wgrads over >= 256K pixels with K % 128 == 0
   // (VGG-16's 112x112 128->128: 322 -> 264 us at 128x64 / 28 splits;
   // profiles/r4/wgrad_sweep_vgg.json); the 56x56 VGG layers stay on 256x128.
-  const bool stream = (g.R == 1 && g.S == 1 && Mred >= 100352) || (Mred >= 262144 && g.K % 128 == 0);
+  // 64->64 3x3 over >= 1M pixels (VGG-16's 224x224 layer when it runs on
+  // the weight-gradient side stream, where the patch kernel is not used):
+  // 64x64 tiles at 256 splits, 580 (igemm) -> 343 us
+  // (profiles/r4/wgrad_sweep_vgg224.json).
+  const bool stream = (g.R == 1 && g.S == 1 && Mred >= 100352) || (Mred >= 262144 && g.K % 128 == 0) ||
+                      (Mred >= (1L << 20) && g.K == 64);
   const int* fw = g_wgrad_force;
   if (fw[0] > 0) {
     p.bm = fw[0]; p.bn = fw[1];
@@ -1368,7 +1373,8 @@ inline WGPlan wgrad_dma_plan(const ConvGeom& g, bool force) {
   // split the pixel reduction to ~one block per CU (two for the streaming
   // 1x1 passes, whose small tiles leave room for a second block), not
   // more: every split adds |dW| of fp32 partials to write and reduce
-  int splits = fw[2] > 0 ? fw[2] : (stream ? 512 : 256) / p.tiles;
+  const int target = !stream ? 256 : (p.bm == 64 && !(g.R == 1 && g.S == 1) ? 2304 : 512);
+  int splits = fw[2] > 0 ? fw[2] : target / p.tiles;
   if (fw[2] <= 0 && splits > nsteps / 8) splits = nsteps / 8;
   if (splits > nsteps) splits = nsteps;
   if (splits < 1) splits = 1;

@@ -205,7 +205,11 @@ int conv_wgrad(const bf16_t* dy, const bf16_t* x, const ConvGeom& g, Epi ep, hip
   if (!dbias && ep.c_f32 && ep.ldc == Nc && ep.mode <= 1 &&
       conv_stem_wgrad(dy, x, g, (float*)ep.c, ep.mode, ws, ws_floats, s))   // 7x7/s2 8->64 stem
     return 0;
-  if (g_conv_dma && g_wgrad_c64 && (allow_patch || g_wgrad_c64 >= 2) && ep.c_f32 && ep.ldc == Nc && ep.mode <= 1 &&
+  // the patch kernel only for 64 -> 64 (VGG-16's 224x224 layer: 313 vs 343 us
+  // on the DMA kernel); 64 -> 128 at 112x112 runs 172 us on it vs 136 us on
+  // the DMA kernel's streaming tiles (profiles/r4/wgrad_sweep_vgg224.json)
+  if (g_conv_dma && g_wgrad_c64 && (allow_patch || g_wgrad_c64 >= 2) && (g.K == 64 || g_wgrad_c64 >= 2) &&
+      ep.c_f32 && ep.ldc == Nc && ep.mode <= 1 &&
       launch_conv_wgrad_c64(dy, x, (float*)ep.c, g, ep.mode, g_wgrad_c64 >= 2 ? g_wgrad_c64 : 0, s,
                             g_conv_dma >= 2 || g_wgrad_c64 >= 2, dbias))
     return dbias ? 1 : 0;

@@ -68,11 +68,15 @@ def main():
                          "(conv_wgrad_slab_policy), interleaved, both store and accumulate modes")
     ap.add_argument("--slab", type=int, default=1, help="slab policy for the other modes")
     ap.add_argument("--min_hw", type=int, default=0, help="only shapes with H >= this")
+    ap.add_argument("--no_c64", action="store_true",
+                    help="patch-staged 64-channel kernel off (the path a side-stream wgrad takes)")
     ap.add_argument("--splits", default="1,2,4,8,16,32,64,128", help="forced split counts to sweep")
     a = ap.parse_args()
     _lib.load(required=True)
     T = torch.ops.tam
     T.conv_wgrad_slab_policy(a.slab)
+    if a.no_c64:
+        T.conv_wgrad_c64_policy(0)
     dev = torch.device("cuda", 0)
     shapes = [("resnet50",) + s for s in RN50] * ("resnet50" in a.models) + \
              [("vgg16",) + s for s in VGG] * ("vgg16" in a.models)
