@@ -44,12 +44,17 @@ class ModelSpec:
 
 MODELS: Dict[str, ModelSpec] = {
     "resnet50": ModelSpec(ResNet50, "image", 64, "sgd", 0.1, 1e-4),
-    "vgg16": ModelSpec(VGG16, "image", 32, "sgd", 0.01, 5e-4, overlap_wgrad=True),
+    "vgg16": ModelSpec(VGG16, "image", 32, "sgd", 0.01, 5e-4),
     # weight-gradient side stream: measured per model (profiles/r2/ab_overlap.txt,
     # hipGraph steps): Transformer 7.28 -> 7.14 ms on; ResNet-50 10.65 -> 11.01
-    # and GNMT 10.87 -> 11.93 (the persistent recurrence loses its CUs) off
+    # and GNMT 10.87 -> 11.93 (the persistent recurrence loses its CUs) off.
+    # Re-measured at the end of round 4 with the slab-split weight gradients
+    # (profiles/r4/*_overlap_ab.log): VGG-16 6.71 on vs 6.62 off (off: the
+    # patch-staged 224x224 wgrad runs again), ResNet-50 9.63 on vs 9.19 off
+    # (Transformer re-measured too: 5.38 on vs 5.21 off -- the deferred weight
+    # gradients are one grouped launch at the end of the backward now)
     "transformer": ModelSpec(TransformerBase, "seq2seq", 32, "adam", 5e-4, 0.0, seq=128,
-                             smoothing=0.1, overlap_wgrad=True, group_wgrad=True),
+                             smoothing=0.1, group_wgrad=True),
     "gnmt": ModelSpec(GNMT, "seq2seq", 64, "adam", 1e-3, 0.0, seq=50),
     # tiny variants (CPU tests / gloo rehearsals / smoke)
     "resnet_tiny": ModelSpec(ResNet50, "image", 4, "sgd", 0.1, 1e-4,
