@@ -161,7 +161,12 @@ def test_rank_failure_is_detected(tmp_path):
         p.start()
     for p in ps:
         p.join(120)
+    alive = [p.pid for p in ps if p.is_alive()]
+    for p in ps:
+        if p.is_alive():
+            p.kill()
     assert ps[1].exitcode == 17
+    assert (tmp_path / "f0.pt").exists(), f"rank 0 wrote no result: exitcode {ps[0].exitcode}, still running {alive}"
     s = torch.load(tmp_path / "f0.pt", weights_only=False)
     assert s["aborted"] and "rank lost" in s["reason"]
 
