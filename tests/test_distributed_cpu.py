@@ -493,3 +493,129 @@ def test_heartbeat_liveness_ignores_wall_clock(monkeypatch):
     finally:
         p0.close()
         p1.close()
+
+
+# ------------------------------------------------------------------ DDP bucket layout
+@pytest.mark.parametrize("model", ["resnet50", "vgg16", "transformer", "gnmt", "transformer_tiny", "gnmt_tiny"])
+@pytest.mark.parametrize("bucket_mb", [32.0, 0.1, 0.2])
+def test_ddp_bucket_ranges_are_disjoint(model, bucket_mb):
+    """Every DDP bucket is ONE contiguous arena range, buckets never overlap,
+    and every param is in exactly one bucket whose range holds it. (Full-size
+    Transformer-base at the default 32 MB used to get a bucket spanning the
+    store_grad region: its Linear gradients were all-reduced twice.)"""
+    from tiresias_amd.models import make_model
+    from tiresias_amd.ops.arena import Arena
+    from tiresias_amd.parallel.ddp import GradBucketer
+
+    a = Arena("cpu")
+    make_model(model, a)
+    a.layout()                                     # offsets only, no allocation
+    a.grad = torch.empty(0, device="meta")
+    b = GradBucketer(a, None, bucket_mb=bucket_mb)
+    rs = sorted(b.ranges)
+    for (lo0, hi0), (lo1, _) in zip(rs, rs[1:]):
+        assert hi0 <= lo1
+    seen = set()
+    for bi, ps in enumerate(b.buckets):
+        lo, hi = b.ranges[bi]
+        for p in ps:
+            assert lo <= p.offset and p.offset + p.numel <= hi
+            assert id(p) not in seen
+            seen.add(id(p))
+        # contiguous: the bucket's params tile its range (64-element padding)
+        assert sum((p.numel + 63) // 64 * 64 for p in ps) >= (hi - lo) - 64
+    assert len(seen) == len(a.params)
+
+
+def _ddp_adam_worker(rank, world, port, q, model, bucket_mb):
+    _init(rank, world, port)
+    from tiresias_amd.executor.trainer import Trainer
+
+    t = Trainer(model, "cpu", seed=3, data_seed=40 + rank, group=dist.group.WORLD, bucket_mb=bucket_mb)
+    # single-process reference: local gradients, averaged by hand, same Adam
+    loc = Trainer(model, "cpu", seed=3, data_seed=40 + rank)
+    for _ in range(3):
+        t.step()
+        loc._fwd_bwd()
+        dist.all_reduce(loc.arena.grad)
+        loc.arena.grad /= world
+        loc._opt_step()
+        loc.arena.grad.zero_()
+    err = float((t.arena.master - loc.arena.master).norm() / loc.arena.master.norm())
+    q.put((rank, err, t.ddp.bytes_reduced, t.arena.numel))
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("model,bucket_mb", [("transformer_tiny", 0.1), ("gnmt_tiny", 0.2)])
+def test_ddp_adam_matches_single_process(model, bucket_mb):
+    """World-2 bucketed DDP + Adam matches one process averaging the same
+    gradients by hand, at bucket sizes whose buckets used to overlap; every
+    gradient element is reduced exactly once per step."""
+    world = 2
+    q = mp.get_context("spawn").SimpleQueue()
+    mp.spawn(_ddp_adam_worker, args=(world, _free_port(), q, model, bucket_mb), nprocs=world, join=True)
+    for _ in range(world):
+        rank, err, nbytes, numel = q.get()
+        assert err < 1e-5, (rank, err)
+        assert nbytes <= 3 * numel * 4, (nbytes, numel)
+
+
+def _shard_pressure_worker(rank, world, port, outdir):
+    _init(rank, world, port)
+    ctrl = dist.new_group(backend="gloo")
+    import bench
+    from tiresias_amd.executor.cluster_runtime import Worker, run_replay
+    from tiresias_amd.executor.trainer import Trainer
+
+    one = Trainer("transformer_tiny", "cpu").hbm_bytes()
+    jobs = bench.bench_trace(world, 5, seed=13, work_s=0.6, min_iters=3, tiny=True)
+    for j in jobs:
+        j.model = "transformer_tiny"
+        j.spec.num_gpu = world                     # every job a 2-rank sharded gang
+    cfg = bench.make_cfg("dlas-gpu", "count", world, 13, "pressure", [0.01, 0.05])
+    cfg.ddp_shard = True
+    w = Worker(rank, world, torch.device("cpu"), dist.group.WORLD, ddp_shard=True,
+               hbm_budget_gb=2.5 * one / 2 ** 30, pool_cap=0)
+    refused = []
+    orig = w._spill
+
+    def spill(jid):
+        # a pressure victim must never be a member still holding only its slices
+        if w.trainers[jid].state_sharded:
+            refused.append(jid)
+        orig(jid)
+
+    w._spill = spill
+    s = run_replay(cfg, jobs, rank, world, torch.device("cpu"), ctrl_pg=ctrl,
+                   world_pg=dist.group.WORLD, worker=w, quantum=0.05)
+    torch.save({"s": s, "spills": w.pressure_spills, "refused": refused}, os.path.join(outdir, f"p{rank}.pt"))
+    dist.destroy_process_group()
+
+
+@pytest.mark.slow
+def test_sharded_gangs_under_hbm_pressure(tmp_path):
+    """Sharded data parallelism + ckpt policy "pressure" (world 2, gloo):
+    preempted gangs are consolidated before any pressure spill can pick them,
+    suspended gangs DO get spilled (and restored), and every job finishes."""
+    world = 2
+    mp.spawn(_shard_pressure_worker, args=(world, _free_port(), str(tmp_path)), nprocs=world, join=True)
+    res = [torch.load(tmp_path / f"p{r}.pt", weights_only=False) for r in range(world)]
+    s = res[0]["s"]
+    assert s["finished"] == s["jobs"] and s["preemptions"] > 0, s
+    assert s["ddp_shard"] and s["consolidations"] > 0, s
+    assert sum(r["spills"] for r in res) > 0
+    assert all(not r["refused"] for r in res)
+
+
+def test_offload_refuses_sharded_state():
+    from tiresias_amd.executor.cluster_runtime import _HostEngine
+    from tiresias_amd.executor.trainer import Trainer
+
+    t = Trainer("resnet_tiny", "cpu")
+
+    class _D:
+        shard, dirty = True, True
+
+    t.ddp = _D()
+    with pytest.raises(RuntimeError, match="consolidate"):
+        t.offload(_HostEngine())

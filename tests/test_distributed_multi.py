@@ -431,7 +431,6 @@ def _shard_worker(rank, world, port, q, wire):
         assert sh.ddp.shard and len(sh.ddp.buckets) > 2
         for _ in range(3):
             ref.step()
-            ref.ddp.finish() if False else None
             sh.step()
         # the compute copy (bf16 shadow) is complete on every member after
         # every step; the master / optimizer state only after consolidate()
@@ -453,7 +452,7 @@ def _shard_worker(rank, world, port, q, wire):
     dist.barrier()
 
 
-@pytest.mark.parametrize("world,wire", [(2, "fp32"), (4, "fp32"), (4, "bf16"), (8, "fp32")])
+@pytest.mark.parametrize("world,wire", [(2, "fp32"), (4, "fp32"), (4, "bf16"), (8, "fp32"), (8, "bf16")])
 def test_sharded_ddp_matches_allreduce(world, wire):
     """Sharded data parallelism (reduce-scatter -> 1/N optimizer -> bf16
     shadow all-gather) on gloo world 2/4/8: the compute copy every member
@@ -463,7 +462,7 @@ def test_sharded_ddp_matches_allreduce(world, wire):
     q = mp.get_context("spawn").SimpleQueue()
     _spawn(_shard_worker, world, q, wire)
     res = dict(q.get() for _ in range(world))
-    tol = 2e-3 if wire == "fp32" else 2e-2
+    tol = 2e-3 if wire == "fp32" else 1e-2
     for model in ("vgg_tiny", "transformer_tiny"):
         sums = {res[r][model]["master_sum"] for r in range(world)}
         assert len(sums) == 1, sums                         # every member holds the same full state

@@ -920,8 +920,11 @@ class Worker:
         # victims: lowest scheduler priority first (plan's resume order), then
         # least recently run
         order = {jid: i for i, jid in enumerate(resume_order or [])}
+        # a sharded gang member holds only its slices of the job's state until
+        # the plan's 'consolidate' action has run: never a pressure victim
         victims = sorted((jid for jid, t in self.trainers.items()
-                          if jid not in protect and not getattr(t, "_spilled", None)),
+                          if jid not in protect and not getattr(t, "_spilled", None)
+                          and not t.state_sharded),
                          key=lambda j: (-order.get(j, -1), self._last_run.get(j, -1)))
         for jid in victims:
             if self._free_bytes() >= need + margin:

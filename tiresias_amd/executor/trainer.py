@@ -341,6 +341,10 @@ class Trainer:
         spilled."""
         if getattr(self, "_spilled", None):
             return 0
+        if self.state_sharded:
+            # only this member's slices of master / optimizer state are
+            # current: spilling them would lose the job (consolidate() first)
+            raise RuntimeError("trainer state is sharded across its gang: consolidate() before offload()")
         self._release_host_copies()
         self._graph = None
         self._g_loss = None

@@ -96,7 +96,9 @@ class Arena:
         return ([p for p in self.params if p.store_grad] + [p for p in self.params if p.decay and not p.store_grad]
                 + [p for p in self.params if not p.decay])
 
-    def materialize(self) -> "Arena":
+    def layout(self) -> List[Param]:
+        """Assign every param its arena offset (no allocation); returns the
+        params in arena order."""
         off = 0
         order = self._order()
         for p in order:
@@ -107,6 +109,10 @@ class Arena:
             if p.store_grad:
                 self.n_store = off
         self.numel = max(off, _ALIGN)
+        return order
+
+    def materialize(self) -> "Arena":
+        order = self.layout()
         dev = self.device
         self.master = torch.zeros(self.numel, dtype=torch.float32, device=dev)
         self.shadow = torch.zeros(self.numel, dtype=torch.bfloat16, device=dev)

@@ -33,7 +33,9 @@ on the member's slices (+ the replicated tails) only -- 1/world of the
 arena's optimizer traffic per member -- and the updated bf16 shadow slices
 are ALL-GATHERED back into every member's compute copy. Per parameter and
 step a member sends (W-1)/W x (4 + 2) bytes instead of 2(W-1)/W x 4 (25 %
-fewer; ``wire="bf16"`` also reduce-scatters in bf16: (W-1)/W x 4, half).
+fewer; ``wire="bf16"`` exchanges the gradient in bf16 -- an all-to-all of
+bf16 slices summed in fp32 by the owning member, so no partial sum is
+rounded to bf16 -- (W-1)/W x 4, half).
 The fp32 master and the optimizer state are then SHARDED: only this
 member's slices are current. ``consolidate()`` all-gathers them so every
 member holds the full state again -- required before anything reads the
@@ -57,6 +59,16 @@ from ..ops.arena import Arena, Param
 from .gang import as_comm, comm_size
 
 
+def check_disjoint(ranges: List[tuple]) -> None:
+    """Bucket ranges must not overlap: an element in two buckets is reduced
+    twice (W x the mean) and, sharded, updated by two owners."""
+    last = -1
+    for lo, hi in sorted(ranges):
+        if lo < last:
+            raise AssertionError(f"overlapping DDP bucket ranges at {lo} (< {last}): {sorted(ranges)}")
+        last = hi
+
+
 class GradBucketer:
     """``group``: a gang comm (``parallel/gang.py``: flat RCCL for a
     consolidated gang, hierarchical intra-node RCCL + throttled host-staged
@@ -77,12 +89,20 @@ class GradBucketer:
         self.position = self.comm.position if self.shard else 0
         self.dirty = False                       # sharded master / optimizer state (consolidate())
         elems = max(1, int(bucket_mb * (1 << 20) // 4))
-        decay = [p for p in arena.params if p.decay]
-        nodecay = [p for p in arena.params if not p.decay]
+        # A bucket must be ONE contiguous arena range. The arena is laid out
+        # as [store_grad | other decay | no-decay] (ops/arena.py::Arena._order),
+        # each region in registration order, so buckets are cut per region,
+        # walking it from its highest offset down (backward produces the
+        # last-registered params' gradients first). Walking all decay params
+        # in registration order instead would let one bucket's [min, max)
+        # span the other region and reduce those gradients twice.
+        regions = ([p for p in arena.params if p.store_grad],
+                   [p for p in arena.params if p.decay and not p.store_grad],
+                   [p for p in arena.params if not p.decay])
         self.buckets: List[List[Param]] = []
-        for plist in (list(reversed(decay)), list(reversed(nodecay))):
+        for plist in regions:
             cur, size = [], 0
-            for p in plist:
+            for p in sorted(plist, key=lambda q: q.offset, reverse=True):
                 cur.append(p)
                 size += p.numel
                 if size >= elems:
@@ -105,7 +125,9 @@ class GradBucketer:
             self.slices.append((sl, lo + self.world * sl))
             for p in ps:
                 self.bucket_of[id(p)] = bi
+        check_disjoint(self.ranges)
         self._wbufs: List[Optional[torch.Tensor]] = []     # bf16 wire staging, per bucket
+        self._rbufs: List[Optional[torch.Tensor]] = []     # bf16 all-to-all receive, per bucket
         self.uses: Optional[Dict[int, int]] = None
         self._seen: Dict[int, int] = {}
         self._pending: List[int] = []
@@ -154,12 +176,16 @@ class GradBucketer:
         g = self.arena.grad
         if sl > 0:
             if self.wire == "bf16":
-                # bf16 on the wire: cast the main part, reduce-scatter it,
-                # widen this member's summed slice back into the fp32 grad
-                # (after finish(), see _widen)
-                buf = self._wire_buf(bi, mid - lo)
+                # bf16 on the wire, fp32 accumulation: cast the main part and
+                # ALL-TO-ALL it (member j receives every member's copy of
+                # slice j: the same (W-1)/W x n x 2 bytes as a bf16
+                # reduce-scatter), then finish() sums the W received copies
+                # in fp32 into this member's slice of the fp32 grad. A bf16
+                # reduce-scatter would round every partial sum to bf16.
+                buf = self._wire_buf(self._wbufs, bi, mid - lo)
                 buf.copy_(g[lo:mid])
-                self._works.append(self.comm.reduce_scatter(buf[p * sl:(p + 1) * sl], buf))
+                recv = self._wire_buf(self._rbufs, bi, mid - lo)
+                self._works.append(self.comm.all_to_all(recv, buf))
                 self.bytes_reduced += (mid - lo) * 2
                 self.wire_bytes += (W - 1) / W * (mid - lo) * 2
             else:
@@ -171,15 +197,15 @@ class GradBucketer:
             self.bytes_reduced += (hi - mid) * 4
             self.wire_bytes += 2.0 * (W - 1) / W * (hi - mid) * 4
 
-    def _wire_buf(self, bi: int, n: int) -> torch.Tensor:
+    def _wire_buf(self, pool: List[Optional[torch.Tensor]], bi: int, n: int) -> torch.Tensor:
         # one bf16 staging buffer per in-flight bucket (distinct memory: the
-        # reduce-scatters of several buckets are in flight together)
-        while len(self._wbufs) <= bi:
-            self._wbufs.append(None)
-        b = self._wbufs[bi]
+        # exchanges of several buckets are in flight together)
+        while len(pool) <= bi:
+            pool.append(None)
+        b = pool[bi]
         if b is None or b.numel() < n:
             b = torch.empty(n, dtype=torch.bfloat16, device=self.arena.grad.device)
-            self._wbufs[bi] = b
+            pool[bi] = b
         return b[:n]
 
     def _on_ready(self, p: Param):
@@ -216,11 +242,12 @@ class GradBucketer:
         if self._works:
             self.comm.finish(self._works)
             if self.shard and self.wire == "bf16":
-                g, p = self.arena.grad, self.position
+                g, p, W = self.arena.grad, self.position, self.world
                 for bi, (sl, _) in enumerate(self.slices):
                     if sl > 0:
                         lo = self.ranges[bi][0]
-                        g[lo + p * sl:lo + (p + 1) * sl].copy_(self._wbufs[bi][p * sl:(p + 1) * sl])
+                        copies = self._rbufs[bi][:W * sl].view(W, sl)
+                        torch.sum(copies, dim=0, dtype=torch.float32, out=g[lo + p * sl:lo + (p + 1) * sl])
             if self._timed:
                 done = torch.cuda.Event(enable_timing=True)
                 done.record()

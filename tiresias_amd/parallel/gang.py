@@ -84,6 +84,11 @@ class FlatComm:
     def all_gather(self, out: torch.Tensor, inp: torch.Tensor):
         return self.pg.all_gather(out, inp)
 
+    def all_to_all(self, out: torch.Tensor, inp: torch.Tensor):
+        """Equal-split all-to-all: chunk j of ``inp`` goes to member j, chunk
+        i of ``out`` comes from member i (out and inp must not alias)."""
+        return self.pg.all_to_all(out, inp)
+
     @property
     def position(self) -> int:
         return self.pg.position
@@ -333,6 +338,14 @@ class GangPG:
                 return _Done()
             inp = inp.clone()                 # gloo: no aliasing of in / out
         return self.pg._allgather_base(out, inp)
+
+    def all_to_all(self, out: torch.Tensor, inp: torch.Tensor):
+        if self.backend != "nccl" and inp.is_cuda:
+            ho = torch.empty(out.shape, dtype=out.dtype)
+            self.pg.alltoall_base(ho, inp.cpu(), [], [], dist.AllToAllOptions()).wait()
+            out.copy_(ho)
+            return _Done()
+        return self.pg.alltoall_base(out, inp, [], [], dist.AllToAllOptions())
 
     @property
     def position(self) -> int:
@@ -715,6 +728,9 @@ class _PlainPG:
         if dist.get_backend(self.pg) != "nccl":
             inp = inp.clone()
         return dist.all_gather_into_tensor(out, inp, group=self.pg, async_op=True)
+
+    def all_to_all(self, out, inp):
+        return dist.all_to_all_single(out, inp, group=self.pg, async_op=True)
 
     @property
     def position(self) -> int:
