@@ -67,7 +67,8 @@ std::mutex g_route_mu;
 // library routing), -1 measured per-shape routing, 1 always where eligible
 int g_lib_policy = 0;
 extern int g_dma_policy;
-bool g_forced = false;   // tile/split forced for tuning: never route to the library
+int g_forced = 0;   // tile/split forced for tuning: never route to the library
+TAM_KNOB(g_lib_policy) TAM_KNOB(g_forced)
 
 void run_mfma(const Tensor& a, bool ak, const Tensor& b, bool bk, int64_t M, int64_t N, int64_t K,
               const tam::Epi& ep, bool allow_split, int path = -1) {
@@ -101,7 +102,8 @@ void run_lib(const Tensor& a, bool ak, const Tensor& b, bool bk, const Tensor& c
 // measured routing passes the (tile, splits) it timed best
 // sp == 0 (tile 256): the stream-K schedule; g_sk_force: the heuristic
 // configuration becomes stream-K wherever eligible (tests)
-bool g_sk_force = false;
+int g_sk_force = 0;
+TAM_KNOB(g_sk_force)
 void run_p8(const Tensor& a, bool ak, const Tensor& b, bool bk, int64_t M, int64_t N, int64_t K,
             const tam::Epi& ep, bool allow_split, int tile = -1, int sp = -1) {
   if ((sp == 0 || (g_sk_force && tile < 0)) &&
@@ -123,7 +125,7 @@ void run_p8(const Tensor& a, bool ak, const Tensor& b, bool bk, int64_t M, int64
   }
   if (explicit_cfg)
     tam::launch_gemm8p(bp(a), a.stride(0), ak, bp(b), b.stride(0), bk, (int)M, (int)N, (int)K, ep, 1,
-                       cur_stream(a), 0, tile);
+                       cur_stream(a), tile);
   else
     run_mfma(a, ak, b, bk, M, N, K, ep, allow_split, 3);
 }
@@ -821,12 +823,34 @@ void conv_wgrad_force_op(int64_t bm, int64_t bn, int64_t splits, int64_t noatomi
 // 0: never the LDS-DMA GEMM; 1: measured per-shape routing (default);
 // 2: LDS-DMA GEMM wherever eligible, tile cfg forced when >= 0 (tests/sweeps)
 int g_dma_policy = 1;
+TAM_KNOB(g_dma_policy)
 void gemm_dma_policy_op(int64_t p, int64_t cfg) {
   g_dma_policy = (int)p;
   tam::gemm_dma_policy(p == 2 ? 1 : 0, (int)cfg);
 }
 
-void gemm8p_policy_op(int64_t mode, int64_t stagger) { tam::gemm8p_policy((int)mode, (int)stagger); }
+void gemm8p_policy_op(int64_t mode, int64_t tile) { tam::gemm8p_policy((int)mode, (int)tile); }
+
+// every registered tuning knob (common.h TAM_KNOB): names (comma-joined, in
+// registration order), current values, and a bulk restore
+std::string policy_names_op() {
+  std::string out;
+  for (const auto& k : tam::knob_registry()) {
+    if (!out.empty()) out += ",";
+    out += k.name;
+  }
+  return out;
+}
+std::vector<int64_t> policy_state_op() {
+  std::vector<int64_t> v;
+  for (const auto& k : tam::knob_registry()) v.push_back(*k.p);
+  return v;
+}
+void policy_load_op(std::vector<int64_t> v) {
+  auto& reg = tam::knob_registry();
+  TORCH_CHECK(v.size() == reg.size(), "policy_load: ", v.size(), " values for ", reg.size(), " knobs");
+  for (size_t i = 0; i < reg.size(); ++i) *reg[i].p = (int)v[i];
+}
 void gemm8p_group_op(int64_t g) { tam::gemm8p_group((int)g); }
 void gemm8p_slab_force_op(int64_t sp) { tam::gemm8p_slab_force((int)sp); }
 void gemm8p_sk_force_op(int64_t on) { g_sk_force = on != 0; }
@@ -1086,7 +1110,10 @@ TORCH_LIBRARY(tam, m) {
   m.def("embedding_backward(Tensor dout, Tensor ids, Tensor(a!) gtable, float scale) -> ()", &embedding_backward_op);
   m.def("colsum(Tensor x, Tensor(a!) out) -> ()", &colsum_op);
   m.def("gemm_force(int cfg, int splits) -> ()", &gemm_force_op);
-  m.def("gemm8p_policy(int mode, int stagger) -> ()", &gemm8p_policy_op);
+  m.def("gemm8p_policy(int mode, int tile) -> ()", &gemm8p_policy_op);
+  m.def("policy_names() -> str", &policy_names_op);
+  m.def("policy_state() -> int[]", &policy_state_op);
+  m.def("policy_load(int[] v) -> ()", &policy_load_op);
   m.def("gemm8p_group(int g) -> ()", &gemm8p_group_op);
   m.def("gemm8p_slab_force(int sp) -> ()", &gemm8p_slab_force_op);
   m.def("gemm_skinny_policy(int on, int force_splits, int nst) -> ()", &gemm_skinny_policy_op);

@@ -6,6 +6,8 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include <vector>
+
 namespace tam {
 
 typedef unsigned short bf16_t;  // raw bf16 bits in memory
@@ -95,6 +97,23 @@ __device__ __forceinline__ float sigmoidf_(float x) { return 1.f / (1.f + __expf
 void zero_async(void* p, size_t bytes, hipStream_t s);
 // rows x cols fp32 block with row pitch ld (floats)
 void zero_async_2d(float* p, long ld, int cols, int rows, hipStream_t s);
+
+// ---- host-side registry of the library's tuning knobs (every *_policy /
+// *_force setting): tests snapshot it at load and restore it after each test
+// (ops.cpp policy_state / policy_load), so no test leaves a non-production
+// configuration behind for the next one
+struct KnobRef {
+  const char* name;
+  int* p;
+};
+inline std::vector<KnobRef>& knob_registry() {
+  static std::vector<KnobRef> v;
+  return v;
+}
+struct KnobReg {
+  KnobReg(const char* n, int* p) { knob_registry().push_back({n, p}); }
+};
+#define TAM_KNOB(var) static ::tam::KnobReg var##_knob_reg_(#var, &var);
 
 }  // namespace tam
 

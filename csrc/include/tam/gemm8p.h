@@ -31,13 +31,9 @@
 //    and ONE counted `s_waitcnt vmcnt(6)` per K-tile (in p4, before its
 //    first barrier) retires tile t+1 while tile t+2's three half-tiles stay
 //    in flight: the DMA pipeline never drains inside the loop.
-//  * Two raw s_barriers per phase (reads + DMA issue | MFMA cluster), MFMA
-//    clusters bracketed by s_setprio (T5). STAGGER: the upper wave group runs
-//    one barrier behind the lower one, so on every SIMD one wave issues its
-//    MFMA cluster while its partner issues LDS reads / DMA (ping-pong); the
-//    refill / wait placement above stays race-free under that skew (a
-//    refill happens after the partner group's reads have retired; a read
-//    happens after both groups' waits).
+//  * One raw s_barrier per phase (after its MFMA cluster), MFMA clusters
+//    bracketed by s_setprio (T5); fragment reads wait per fragment, so a
+//    cluster's first MFMAs start while its later reads are in flight.
 //  * XCD-aware bijective block remap + grouped-M tile order (T1); split-K
 //    over blockIdx.z (fp32 atomic epilogue) when the tile grid underfills
 //    the 256 CUs.
@@ -149,12 +145,10 @@ __device__ __forceinline__ void p8_mfma(f32x4_t (&acc)[TI][TJ], const s16x8_t (&
   __builtin_amdgcn_sched_barrier(0);
 }
 
-// SCHED 0: one barrier per phase (after the MFMA cluster); 1: two barriers
-// per phase (reads | MFMA); 2: two barriers + wave-group stagger; 3: as 0
-// with the B fragments read before the A fragments (pinned order); 4: as 3
-// without the blanket lgkmcnt(0) in front of each MFMA cluster (per-fragment
-// waits); 5: as 4 with 2's two barriers + stagger. Measured in one process,
-// interleaved rounds (tools/ab_gemm8p_sched.py, profiles/r2/gemm8p_sched_ab.json)
+// One schedule (measured best of six in round 2, profiles/r2/gemm8p_sched_ab.json;
+// the other five were deleted in round 5): one barrier per phase, B fragments
+// read before A (pinned order), and per-fragment lgkmcnt waits instead of a
+// blanket lgkmcnt(0) in front of each MFMA cluster.
 // The kernel body over one tile: bid = the (XCD-remapped) tile index within
 // the M x N tile grid, kz = the K-split slice. Shared by gemm8p_kernel and the
 // grouped launch (gemm8p_grouped_kernel: many independent problems, one grid).
@@ -174,20 +168,15 @@ __device__ __forceinline__ void p8_tile_origin(const P8Args& a, const int bid, i
 
 // kt_lo / kt_hi >= 0: an explicit K-tile range (stream-K segments); else
 // slice kz of a.kps K-tiles
-template <int BM, int BN, int WNW, bool AK, bool BK, int SCHED>
+template <int BM, int BN, int WNW, bool AK, bool BK>
 __device__ __forceinline__ void gemm8p_body(const P8Args& a, const Epi& ep, const int bid, const int kz,
                                             const int kt_lo = -1, const int kt_hi = -1) {
   using G = P8Geo<BM, BN, WNW>;
-  constexpr bool STAGGER = SCHED == 2 || SCHED == 5;
-  constexpr bool TWO_BAR = SCHED == 1 || SCHED == 2 || SCHED == 5;
-  constexpr bool FINE = SCHED == 4 || SCHED == 5;
+  constexpr bool FINE = true;
   constexpr int FI = G::FI, FJ = G::FJ, TI = 2 * FI, TJ = 2 * FJ;
   __shared__ __attribute__((aligned(1024))) char smem[G::LDS];
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const int wm = wid / WNW, wn = wid % WNW;
-  // the upper wave group, as a wave-uniform SCALAR condition (a divergent
-  // branch would execute the scalar s_barrier on every wave)
-  const bool upper = __builtin_amdgcn_readfirstlane(tid) >= G::THREADS / 2;
 
   int m0, n0;
   p8_tile_origin<BM, BN>(a, bid, m0, n0);
@@ -223,7 +212,6 @@ __device__ __forceinline__ void gemm8p_body(const P8Args& a, const Epi& ep, cons
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     }
     p8_barrier();
-    if (STAGGER && upper) p8_barrier();
 
     const int arow = wm * G::QM, bcol = wn * G::QN;   // local rows in the half images
     s16x8_t fa[FI][2], fb0[FJ][2], fb1[FJ][2];
@@ -233,19 +221,18 @@ __device__ __forceinline__ void gemm8p_body(const P8Args& a, const Epi& ep, cons
       const char* BL = bptr(t, 0);
       const char* BH = bptr(t, 1);
       const bool n1 = t + 1 < nk, n2 = t + 2 < nk;
-      // ---- p1: quadrant (mh0, nh0); B fragments first (SCHED 3: pinned
+      // ---- p1: quadrant (mh0, nh0); B fragments first (pinned
       // B-before-A issue order, guide §5 8-phase template)
 #pragma unroll
       for (int kk = 0; kk < 2; ++kk)
 #pragma unroll
         for (int j = 0; j < FJ; ++j) fb0[j][kk] = p8_frag<BK, G::BCOLS>(BL, lane, bcol + 16 * j, kk);
-      if constexpr (SCHED >= 3) __builtin_amdgcn_sched_barrier(0);
+      __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
       for (int kk = 0; kk < 2; ++kk)
 #pragma unroll
         for (int i = 0; i < FI; ++i) fa[i][kk] = p8_frag<AK, G::AROWS>(AL, lane, arow + 16 * i, kk);
       if (n1) issA(t + 1, 1);
-      if constexpr (TWO_BAR) p8_barrier();
       p8_mfma<0, 0, FINE>(acc, fa, fb0);
       p8_barrier();
       // ---- p2: quadrant (mh0, nh1)
@@ -253,7 +240,6 @@ __device__ __forceinline__ void gemm8p_body(const P8Args& a, const Epi& ep, cons
       for (int kk = 0; kk < 2; ++kk)
 #pragma unroll
         for (int j = 0; j < FJ; ++j) fb1[j][kk] = p8_frag<BK, G::BCOLS>(BH, lane, bcol + 16 * j, kk);
-      if constexpr (TWO_BAR) p8_barrier();
       p8_mfma<0, FJ, FINE>(acc, fa, fb1);
       p8_barrier();
       // ---- p3: quadrant (mh1, nh1)
@@ -262,7 +248,6 @@ __device__ __forceinline__ void gemm8p_body(const P8Args& a, const Epi& ep, cons
 #pragma unroll
         for (int i = 0; i < FI; ++i) fa[i][kk] = p8_frag<AK, G::AROWS>(AH, lane, arow + 16 * i, kk);
       if (n2) issA(t + 2, 0);
-      if constexpr (TWO_BAR) p8_barrier();
       p8_mfma<FI, FJ, FINE>(acc, fa, fb1);
       p8_barrier();
       // ---- p4: quadrant (mh1, nh0); retire tile t+1 (t+2's AL / BL / BH stay in flight)
@@ -273,11 +258,9 @@ __device__ __forceinline__ void gemm8p_body(const P8Args& a, const Epi& ep, cons
       } else {
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       }
-      if constexpr (TWO_BAR) p8_barrier();
       p8_mfma<FI, 0, FINE>(acc, fa, fb0);
       p8_barrier();
     }
-    if (STAGGER && !upper) p8_barrier();        // both groups execute the same barrier count
   }
   __syncthreads();   // LDS reuse by the epilogue
 
@@ -428,33 +411,31 @@ __device__ __forceinline__ void gemm8p_body(const P8Args& a, const Epi& ep, cons
   }
 }
 
-template <int BM, int BN, int WNW, bool AK, bool BK, int SCHED>
+template <int BM, int BN, int WNW, bool AK, bool BK>
 __global__ void __launch_bounds__(128 * WNW, (BM == 256 ? 1 : 2))
 gemm8p_kernel(P8Args a, Epi ep) {
-  gemm8p_body<BM, BN, WNW, AK, BK, SCHED>(a, ep, xcd_remap(blockIdx.x, gridDim.x), blockIdx.z);
+  gemm8p_body<BM, BN, WNW, AK, BK>(a, ep, xcd_remap(blockIdx.x, gridDim.x), blockIdx.z);
 }
 
-// One launcher per kernel variant. Each production variant (SCHED 4) is
-// explicitly instantiated in a translation unit of its own
-// (csrc/kernels/gemm8p_*.hip): co-compiled instantiations of one kernel
-// template share register-allocation context and perturb each other's code
-// (cdna_hip_programming.md §5.4 rule 19); the A/B schedules live together in
-// gemm8p_alt.hip.
-template <int BM, int BN, int WNW, bool AK, bool BK, int SCHED>
+// One launcher per kernel variant. Each variant is explicitly instantiated
+// in a translation unit of its own (csrc/kernels/gemm8p_*.hip): co-compiled
+// instantiations of one kernel template share register-allocation context
+// and perturb each other's code (cdna_hip_programming.md §5.4 rule 19).
+template <int BM, int BN, int WNW, bool AK, bool BK>
 void p8_launch_one(const P8Args& g, const Epi& ep, dim3 grid, hipStream_t s) {
-  hipLaunchKernelGGL((gemm8p_kernel<BM, BN, WNW, AK, BK, SCHED>), grid, dim3(P8Geo<BM, BN, WNW>::THREADS), 0, s,
+  hipLaunchKernelGGL((gemm8p_kernel<BM, BN, WNW, AK, BK>), grid, dim3(P8Geo<BM, BN, WNW>::THREADS), 0, s,
                      g, ep);
 }
 
-#define TAM_P8_VARIANTS(X, SCHED)                                                              \
-  X(256, 256, 4, true, true, SCHED) X(256, 256, 4, true, false, SCHED)                           \
-  X(256, 256, 4, false, true, SCHED) X(256, 256, 4, false, false, SCHED)                         \
-  X(128, 128, 2, true, true, SCHED) X(128, 128, 2, true, false, SCHED)                           \
-  X(128, 128, 2, false, true, SCHED) X(128, 128, 2, false, false, SCHED)
-#define TAM_P8_EXTERN(BM, BN, W, AK, BK, S) \
-  extern template void p8_launch_one<BM, BN, W, AK, BK, S>(const P8Args&, const Epi&, dim3, hipStream_t);
-#define TAM_P8_INST(BM, BN, W, AK, BK, S) \
-  template void p8_launch_one<BM, BN, W, AK, BK, S>(const P8Args&, const Epi&, dim3, hipStream_t);
+#define TAM_P8_VARIANTS(X)                                                                     \
+  X(256, 256, 4, true, true) X(256, 256, 4, true, false)                                       \
+  X(256, 256, 4, false, true) X(256, 256, 4, false, false)                                     \
+  X(128, 128, 2, true, true) X(128, 128, 2, true, false)                                       \
+  X(128, 128, 2, false, true) X(128, 128, 2, false, false)
+#define TAM_P8_EXTERN(BM, BN, W, AK, BK) \
+  extern template void p8_launch_one<BM, BN, W, AK, BK>(const P8Args&, const Epi&, dim3, hipStream_t);
+#define TAM_P8_INST(BM, BN, W, AK, BK) \
+  template void p8_launch_one<BM, BN, W, AK, BK>(const P8Args&, const Epi&, dim3, hipStream_t);
 
 // shape / layout conditions of the LDS-DMA kernels (tile >= 128)
 inline bool gemm8p_ok(bool ak, bool bk, int M, int N, int K, long lda, long ldb) {
@@ -467,7 +448,7 @@ inline bool gemm8p_ok(bool ak, bool bk, int M, int N, int K, long lda, long ldb)
 
 // tile: 256 (256x256, 8 waves) or 128 (128x128, 4 waves)
 void launch_gemm8p(const bf16_t* A, long lda, bool ak, const bf16_t* B, long ldb, bool bk, int M,
-                   int N, int K, const Epi& ep, int splits, hipStream_t s, int sched = 0, int tile = 256);
+                   int N, int K, const Epi& ep, int splits, hipStream_t s, int tile = 256);
 // split-K without atomics or a zeroing pass, any output dtype / epilogue:
 // every K-slice writes its own fp32 slab of ws[splits][M][N], then one
 // reduce pass sums the slabs and applies ep (bias / relu / mask / alpha /

@@ -20,7 +20,7 @@ void gemm_select(const bf16_t* A, long lda, bool a_kmajor, const bf16_t* B, long
 void gemm_force(int cfg, int splits);   // tuning hook (-1 = heuristic)
 void gemm_dma_policy(int policy, int cfg);   // LDS-DMA GEMM on/off, forced tile cfg (-1 auto)
 // 256^2 all-layout LDS-DMA GEMM: 0 off, 1 auto (big GEMMs), 2 forced where eligible
-void gemm8p_policy(int mode, int sched);
+void gemm8p_policy(int mode, int tile);   // tile 128 / 256: forced (tests), else auto
 void gemm8p_group(int g);   // M-tiles per tile-order group of gemm8p (default 4)
 int gemm8p_policy_mode();
 

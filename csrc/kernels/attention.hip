@@ -543,6 +543,7 @@ void attn_forward(const bf16_t* q, const bf16_t* k, const bf16_t* v, bf16_t* o, 
 // 1 (default): key ranges <= 128 take the one-launch short-sequence backward;
 // 0: always the key-blocked kernels (tests / A/B)
 static int g_attn_short = 1;
+TAM_KNOB(g_attn_short)
 void attn_short_policy(int p) { g_attn_short = p; }
 
 void attn_backward(const bf16_t* q, const bf16_t* k, const bf16_t* v, const bf16_t* o,

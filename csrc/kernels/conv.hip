@@ -22,9 +22,11 @@ namespace tam {
 // shape is eligible (tests); 3: as 2 with the 128-row tile variant (tests);
 // 0: register-staged igemm only (A/B measurements)
 static int g_conv_dma = 1;
+TAM_KNOB(g_conv_dma)
 void conv_dma_policy(int p) { g_conv_dma = p; }
 // split-K of under-filled LDS-DMA conv passes (cd_split_plan): 1 on, 0 off (A/B)
 static int g_conv_split = 1;
+TAM_KNOB(g_conv_split)
 void conv_split_policy(int p) { g_conv_split = p; }
 // 64-channel 3x3 stride-1 passes on the halo-tile kernel (conv_dma.h); 0 for
 // A/B runs against the tap-gather cores
@@ -32,7 +34,10 @@ static int g_conv_halo = [] {
   const char* e = getenv("TAM_CONV_HALO");
   return e ? atoi(e) : 1;
 }();
+TAM_KNOB(g_conv_halo)
 void conv_halo_policy(int p) { g_conv_halo = p; }
+static ::tam::KnobReg g_wgrad_force_knobs_[4] = {{"g_wgrad_force0", &g_wgrad_force[0]}, {"g_wgrad_force1", &g_wgrad_force[1]},
+                                                  {"g_wgrad_force2", &g_wgrad_force[2]}, {"g_wgrad_force3", &g_wgrad_force[3]}};
 void conv_wgrad_force(int bm, int bn, int splits, int noatomic) {
   g_wgrad_force[0] = bm; g_wgrad_force[1] = bn; g_wgrad_force[2] = splits; g_wgrad_force[3] = noatomic;
 }
@@ -181,6 +186,7 @@ static void wgrad_tile(const bf16_t* dy, const bf16_t* x, const ConvGeom& g, con
 // unchanged (the kernel's 120 KB of LDS per CU starves co-running kernels
 // there, so it is routed around: 7.42 -> 7.52 ms when it was not)
 static int g_wgrad_c64 = 1;
+TAM_KNOB(g_wgrad_c64) TAM_KNOB(g_wgrad_slab)
 void conv_wgrad_c64_policy(int p) { g_wgrad_c64 = p; }
 void conv_wgrad_order(int flat) { g_wgrad_flat = flat; }
 void conv_wgrad_slab_policy(int p) { g_wgrad_slab = p; }

@@ -190,6 +190,7 @@ constexpr int ST_WBUF = ST_WPENT + ST_WDYENT;    // entries per buffer
 constexpr int ST_NCOL = 392, ST_NT = 25;         // dW columns, 16-column tiles
 
 static int g_conv_stem_v = 1;
+TAM_KNOB(g_conv_stem_v)
 static int g_conv_stem_ref() { return g_conv_stem_v; }
 
 struct StemWArgs {

@@ -37,6 +37,7 @@ static void gemm_tile(const bf16_t* A, long lda, bool ak, const bf16_t* B, long 
 // tuning hook: force tile config / split count (-1 = heuristic); used by
 // tools/sweep_gemm.py to measure the policy, never set in training
 static int g_force_cfg = -1, g_force_splits = -1;
+TAM_KNOB(g_force_cfg) TAM_KNOB(g_force_splits)
 void gemm_force(int cfg, int splits) { g_force_cfg = cfg; g_force_splits = splits; }
 // LDS-DMA pipelined GEMM (gemm_dma.h) for plain gemm() calls: policy 1 = on
 // where eligible, 0 = off (default: measured slower than the igemm on most
@@ -44,6 +45,7 @@ void gemm_force(int cfg, int splits) { g_force_cfg = cfg; g_force_splits = split
 // by measurement instead, gemm_select(path=2)); cfg >= 0 forces its tile
 // config (tests / sweeps)
 static int g_dma = 0, g_dma_cfg = -1;
+TAM_KNOB(g_dma) TAM_KNOB(g_dma_cfg)
 void gemm_dma_policy(int policy, int cfg) { g_dma = policy; g_dma_cfg = cfg; }
 
 __global__ void __launch_bounds__(256) zero_kernel(uint4* __restrict__ p16, long n16,
@@ -91,40 +93,26 @@ void zero_async(void* p, size_t bytes, hipStream_t s) {
 
 // LDS-DMA all-layout kernels (gemm8p.h): 0 off (legacy kernels only),
 // 1 auto (big GEMMs of every layout), 2 forced wherever eligible, 3 forced
-// with slab split-K (the op binding; tests / sweeps). sched: 0 one barrier
-// per phase, 1 two, 2 two + wave-group stagger; tile: 0 auto, 128 / 256 forced
-static int g_p8 = 1, g_p8_sched = 4, g_p8_tile = 0, g_p8_group = 4;   // sched 4: profiles/r2/gemm8p_sched_ab.json
+// with slab split-K (the op binding; tests / sweeps). tile: 0 auto,
+// 128 / 256 forced (tests / sweeps)
+static int g_p8 = 1, g_p8_tile = 0, g_p8_group = 4;
+TAM_KNOB(g_p8) TAM_KNOB(g_p8_tile) TAM_KNOB(g_p8_group)
 int gemm8p_policy_mode() { return g_p8; }
+int gemm8p_policy_tile() { return g_p8_tile; }
 void gemm8p_group(int g) { g_p8_group = g > 0 ? g : 4; }
-void gemm8p_policy(int mode, int sched) {
+void gemm8p_policy(int mode, int tile) {
   g_p8 = mode;
-  g_p8_sched = sched % 10;
-  g_p8_tile = sched >= 200 ? 256 : sched >= 100 ? 128 : 0;    // tests: sched + 100 / + 200
+  g_p8_tile = tile == 128 || tile == 256 ? tile : 0;
 }
 
-TAM_P8_VARIANTS(TAM_P8_EXTERN, 0)
-TAM_P8_VARIANTS(TAM_P8_EXTERN, 1)
-TAM_P8_VARIANTS(TAM_P8_EXTERN, 2)
-TAM_P8_VARIANTS(TAM_P8_EXTERN, 3)
-TAM_P8_VARIANTS(TAM_P8_EXTERN, 4)
-TAM_P8_VARIANTS(TAM_P8_EXTERN, 5)
-
-template <int BM, int BN, int WNW, bool AK, bool BK>
-static void p8_launch_t(const P8Args& g, const Epi& ep, dim3 grid, int sched, hipStream_t s) {
-  if (sched == 5) p8_launch_one<BM, BN, WNW, AK, BK, 5>(g, ep, grid, s);
-  else if (sched == 4) p8_launch_one<BM, BN, WNW, AK, BK, 4>(g, ep, grid, s);
-  else if (sched == 3) p8_launch_one<BM, BN, WNW, AK, BK, 3>(g, ep, grid, s);
-  else if (sched == 2) p8_launch_one<BM, BN, WNW, AK, BK, 2>(g, ep, grid, s);
-  else if (sched == 1) p8_launch_one<BM, BN, WNW, AK, BK, 1>(g, ep, grid, s);
-  else p8_launch_one<BM, BN, WNW, AK, BK, 0>(g, ep, grid, s);
-}
+TAM_P8_VARIANTS(TAM_P8_EXTERN)
 
 template <int BM, int BN, int WNW>
-static void p8_launch_l(bool ak, bool bk, const P8Args& g, const Epi& ep, dim3 grid, int sched, hipStream_t s) {
-  if (ak && bk) p8_launch_t<BM, BN, WNW, true, true>(g, ep, grid, sched, s);
-  else if (ak) p8_launch_t<BM, BN, WNW, true, false>(g, ep, grid, sched, s);
-  else if (bk) p8_launch_t<BM, BN, WNW, false, true>(g, ep, grid, sched, s);
-  else p8_launch_t<BM, BN, WNW, false, false>(g, ep, grid, sched, s);
+static void p8_launch_l(bool ak, bool bk, const P8Args& g, const Epi& ep, dim3 grid, hipStream_t s) {
+  if (ak && bk) p8_launch_one<BM, BN, WNW, true, true>(g, ep, grid, s);
+  else if (ak) p8_launch_one<BM, BN, WNW, true, false>(g, ep, grid, s);
+  else if (bk) p8_launch_one<BM, BN, WNW, false, true>(g, ep, grid, s);
+  else p8_launch_one<BM, BN, WNW, false, false>(g, ep, grid, s);
 }
 
 int gemm8p_tile(int M, int N, int K) {
@@ -135,7 +123,7 @@ int gemm8p_tile(int M, int N, int K) {
 }
 
 void launch_gemm8p(const bf16_t* A, long lda, bool ak, const bf16_t* B, long ldb, bool bk, int M,
-                   int N, int K, const Epi& ep, int splits, hipStream_t s, int sched, int tile) {
+                   int N, int K, const Epi& ep, int splits, hipStream_t s, int tile) {
   const int T = tile == 128 ? 128 : 256;
   const int tiles = cdiv(M, T) * cdiv(N, T);
   const int ktiles = K / P8_BK;
@@ -143,8 +131,8 @@ void launch_gemm8p(const bf16_t* A, long lda, bool ak, const bf16_t* B, long ldb
   const int z = cdiv(ktiles, kps);
   P8Args g{A, lda, B, ldb, M, N, K, kps, g_p8_group};
   const dim3 grid(tiles, 1, z);
-  if (T == 128) p8_launch_l<128, 128, 2>(ak, bk, g, ep, grid, sched, s);
-  else p8_launch_l<256, 256, 4>(ak, bk, g, ep, grid, sched, s);
+  if (T == 128) p8_launch_l<128, 128, 2>(ak, bk, g, ep, grid, s);
+  else p8_launch_l<256, 256, 4>(ak, bk, g, ep, grid, s);
 }
 
 // ---- slab split-K (gemm8p.h): reduce ws[sp][M][N] -> C with the epilogue
@@ -180,6 +168,7 @@ __global__ void __launch_bounds__(256) p8_slab_reduce_kernel(const float* __rest
 }
 
 static int g_p8_force_sp = 0;   // > 0: slab split count forced (A/B sweeps)
+TAM_KNOB(g_p8_force_sp)
 void gemm8p_slab_force(int sp) { g_p8_force_sp = sp > 0 ? sp : 0; }
 
 int gemm8p_slab_splits(int M, int N, int K, int tile) {
@@ -203,7 +192,7 @@ void gemm8p_splitk(const bf16_t* A, long lda, bool ak, const bf16_t* B, long ldb
   se.c_f32 = 1;
   se.mode = 3;
   se.zstride = (long)M * N;
-  launch_gemm8p(A, lda, ak, B, ldb, bk, M, N, K, se, splits, s, g_p8_sched, tile);
+  launch_gemm8p(A, lda, ak, B, ldb, bk, M, N, K, se, splits, s, tile);
   const int ktiles = K / P8_BK;
   const int z = cdiv(ktiles, cdiv(ktiles, splits));   // slabs actually written
   gemm_slab_reduce(ws, z, M, N, ep, s);
@@ -254,7 +243,7 @@ void gemm_select(const bf16_t* A, long lda, bool ak, const bf16_t* B, long ldb, 
       int sp = p8_splits(M, N, K, can_split, tile);
       if (g_force_splits >= 1) sp = can_split ? g_force_splits : 1;
       prepare_split(ep, sp, M, N, s);
-      launch_gemm8p(A, lda, ak, B, ldb, bk, M, N, K, ep, sp, s, g_p8_sched, tile);
+      launch_gemm8p(A, lda, ak, B, ldb, bk, M, N, K, ep, sp, s, tile);
       return;
     }
   }

@@ -2,5 +2,5 @@
 #include "tam/gemm8p.h"
 
 namespace tam {
-TAM_P8_INST(128, 128, 2, false, true, 4)
+TAM_P8_INST(128, 128, 2, false, true)
 }  // namespace tam

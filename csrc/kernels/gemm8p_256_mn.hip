@@ -2,5 +2,5 @@
 #include "tam/gemm8p.h"
 
 namespace tam {
-TAM_P8_INST(256, 256, 4, false, false, 4)
+TAM_P8_INST(256, 256, 4, false, false)
 }  // namespace tam

@@ -44,7 +44,7 @@ __global__ void __launch_bounds__(512, 1) gemm8p_sk_kernel(P8Args a, float* ws, 
     e.ldc = SK_T;
     e.c_f32 = 1;
     e.mode = 0;
-    gemm8p_body<SK_T, SK_T, 4, AK, BK, 4>(a, e, t, 0, k0, k1);
+    gemm8p_body<SK_T, SK_T, 4, AK, BK>(a, e, t, 0, k0, k1);
     __syncthreads();                                 // epilogue LDS reads before the next prologue's DMA
     i0 += k1 - k0;
   }

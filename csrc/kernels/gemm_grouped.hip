@@ -111,7 +111,7 @@ __global__ void __launch_bounds__(64 * 2 * WNW, (BM == 256 ? 1 : 2)) gemm8p_grou
   ep.ldc = pr.N;
   ep.c_f32 = 1;
   ep.mode = pr.mode;
-  gemm8p_body<BM, BN, WNW, false, false, 4>(a, ep, t - pr.t0, 0);
+  gemm8p_body<BM, BN, WNW, false, false>(a, ep, t - pr.t0, 0);
 }
 
 // tile of the grouped launch: 128 (128^2, 4 waves, 2 blocks / CU; default)
@@ -122,6 +122,7 @@ static int g_gg_tile = [] {
   const char* e = getenv("TAM_GROUPED_TILE");
   return e ? atoi(e) : 128;
 }();
+TAM_KNOB(g_gg_tile)
 void gemm_grouped_tile(int t) { g_gg_tile = t == 256 ? 256 : 128; }
 
 // problems: A [K][lda] (M-major), B [K][ldb] (N-major), C [M][N] fp32 = or +=,

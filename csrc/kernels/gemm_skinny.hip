@@ -173,6 +173,7 @@ __global__ void __launch_bounds__(256, 2) gemm_skinny_kernel(SkArgs a, Epi ep) {
 }
 
 static int g_sk_policy = 1, g_sk_force_sp = 0, g_sk_nst = 3;
+TAM_KNOB(g_sk_policy) TAM_KNOB(g_sk_force_sp) TAM_KNOB(g_sk_nst)
 void gemm_skinny_policy(int on, int force_splits, int nst) {
   g_sk_policy = on;
   g_sk_force_sp = force_splits > 0 ? force_splits : 0;

@@ -483,6 +483,7 @@ __global__ void __launch_bounds__(64 * PL_W * CH, 4) lstm_persist_bwd_kernel(
 // lstm_seq_residency only sets the default for callers that pass none
 // (grids < 0). The occupancy query is cached per kernel.
 static int g_pl_grids = 2, g_pl_rsv_cus = 0;
+TAM_KNOB(g_pl_grids) TAM_KNOB(g_pl_rsv_cus)
 void lstm_seq_residency(int grids, int reserved_cus) {
   g_pl_grids = grids < 1 ? 1 : grids;
   g_pl_rsv_cus = reserved_cus < 0 ? 0 : reserved_cus;
@@ -539,6 +540,8 @@ void lstm_seq_policy(int ch) { g_pl_ch = ch; }
 // B = 64 (4 batch tiles) a tile's workgroups bt + 4 ut sit on two XCDs under
 // round-robin dispatch, split by ut parity: 2 counters = one per XCD
 static int g_pl_ns = 2;
+TAM_KNOB(g_pl_ns)
+TAM_KNOB(g_pl_ch)
 void lstm_seq_shards(int ns) { g_pl_ns = (ns == 2 || ns == 4) ? ns : 1; }
 
 static int pl_ch(int Hd) {

@@ -199,6 +199,7 @@ static int g_optim_variant = [] {
   const char* e = getenv("TAM_OPTIM_VARIANT");   // A/B runs
   return e ? atoi(e) : -1;
 }();
+TAM_KNOB(g_optim_variant)
 void optim_variant(int v) { g_optim_variant = v; }
 // auto: SGD on >= 64M params takes the streaming form (VGG-16 graph step
 // 6.94 -> 6.88 ms); Adam stays on the baseline kernel -- its isolated gain

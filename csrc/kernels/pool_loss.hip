@@ -212,6 +212,7 @@ __global__ void __launch_bounds__(256) maxpool_bwd8_k3s2_kernel(const bf16_t* __
 
 // policy: 1 (default) the 3x3/s2/p1 kernel where it applies, 0 generic (A/B, tests)
 static int g_pool_k3s2 = 1;
+TAM_KNOB(g_pool_k3s2)
 void maxpool_k3s2_policy(int p) { g_pool_k3s2 = p; }
 
 void maxpool_forward(const bf16_t* x, bf16_t* y, uint8_t* idx, int N, int H, int W, int C, int P,
@@ -502,6 +503,7 @@ static int g_colsum = [] {
   const char* e = getenv("TAM_COLSUM");
   return e ? atoi(e) : 0;
 }();
+TAM_KNOB(g_colsum)
 void colsum_policy(int p) { g_colsum = p; }
 constexpr long COLSUM_ATOMIC_MAX = 1L << 17;
 

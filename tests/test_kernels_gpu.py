@@ -180,32 +180,28 @@ def test_gemm8p_streamk(gpu, ak, bk, M, N, K):
     the flattened (tile, K-tile) space, partial tiles + fixup. Exact on
     small-integer operands (segment bookkeeping), then bf16 bias + relu and
     fp32 accumulate epilogues vs fp32 torch."""
-    T().gemm8p_policy(3, 4)
+    T().gemm8p_policy(3, 0)
     T().gemm8p_sk_force(1)
-    try:
-        torch.manual_seed(M)
-        A = torch.randint(-2, 3, (M, K), device=gpu).to(BF)
-        B = torch.randint(-2, 3, (K, N), device=gpu).to(BF)
-        a = A if ak else A.t().contiguous()
-        b = B.t().contiguous() if bk else B
-        c = torch.empty(M, N, device=gpu)
-        T().gemm(a, ak, b, bk, c, 0, None, False, None, 1.0, False)
-        assert torch.equal(c, A.float() @ B.float())
-        A = torch.randn(M, K, device=gpu).to(BF)
-        B = (torch.randn(K, N, device=gpu) / 16).to(BF)
-        a = A if ak else A.t().contiguous()
-        b = B.t().contiguous() if bk else B
-        ref = A.float() @ B.float()
-        bias = torch.randn(N, device=gpu).to(BF)
-        y = torch.empty(M, N, device=gpu, dtype=BF)
-        T().gemm(a, ak, b, bk, y, 0, bias, True, None, 1.0, False)
-        assert rel_err(y, torch.relu(ref + bias.float())) < 1e-2
-        acc = torch.full((M, N), 0.5, device=gpu)
-        T().gemm(a, ak, b, bk, acc, 1, None, False, None, 1.0, False)
-        assert rel_err(acc, ref + 0.5) < 1e-5
-    finally:
-        T().gemm8p_sk_force(0)
-        T().gemm8p_policy(1, 4)
+    torch.manual_seed(M)
+    A = torch.randint(-2, 3, (M, K), device=gpu).to(BF)
+    B = torch.randint(-2, 3, (K, N), device=gpu).to(BF)
+    a = A if ak else A.t().contiguous()
+    b = B.t().contiguous() if bk else B
+    c = torch.empty(M, N, device=gpu)
+    T().gemm(a, ak, b, bk, c, 0, None, False, None, 1.0, False)
+    assert torch.equal(c, A.float() @ B.float())
+    A = torch.randn(M, K, device=gpu).to(BF)
+    B = (torch.randn(K, N, device=gpu) / 16).to(BF)
+    a = A if ak else A.t().contiguous()
+    b = B.t().contiguous() if bk else B
+    ref = A.float() @ B.float()
+    bias = torch.randn(N, device=gpu).to(BF)
+    y = torch.empty(M, N, device=gpu, dtype=BF)
+    T().gemm(a, ak, b, bk, y, 0, bias, True, None, 1.0, False)
+    assert rel_err(y, torch.relu(ref + bias.float())) < 1e-2
+    acc = torch.full((M, N), 0.5, device=gpu)
+    T().gemm(a, ak, b, bk, acc, 1, None, False, None, 1.0, False)
+    assert rel_err(acc, ref + 0.5) < 1e-5
 
 
 # every tile config of the LDS-DMA GEMM (gemm_dma.h), all majorities, edge
@@ -243,16 +239,15 @@ def test_gemm_dma_configs(gpu, cfg, ak, bk):
         T().gemm_dma_policy(1, -1)
 
 
-# the 256x256 all-layout LDS-DMA kernel (gemm8p.h), forced: every majority,
-# both schedules (wave-group stagger on / off), edge tiles, K just one tile
-# and many tiles, every epilogue (bf16 staged, bias / relu / mask / alpha /
-# accumulate, fp32 store / accumulate / split-K atomics)
-# sched codes: schedule (0 one barrier / phase, 1 two, 2 two + stagger) +
-# 100: 128x128 tile forced, + 200: 256x256 forced, else the auto tile
-@pytest.mark.parametrize("stagger", [0, 2, 101, 200, 202])
+# the all-layout LDS-DMA kernel (gemm8p.h, the production schedule -- the
+# only one built), forced: every majority, both tiles (128x128 / 256x256
+# forced, 0 = the auto tile), edge tiles, K just one tile and many tiles,
+# every epilogue (bf16 staged, bias / relu / mask / alpha / accumulate, fp32
+# store / accumulate / split-K atomics)
+@pytest.mark.parametrize("tile", [0, 128, 256])
 @pytest.mark.parametrize("ak,bk", [(True, True), (True, False), (False, True), (False, False)])
 @pytest.mark.parametrize("M,N,K", [(256, 256, 64), (520, 392, 448), (1024, 768, 2048)])
-def test_gemm8p(gpu, stagger, ak, bk, M, N, K):
+def test_gemm8p(gpu, tile, ak, bk, M, N, K):
     torch.manual_seed(M + N + K + 2 * ak + bk)
     A = torch.randn(M, K, device=gpu).to(BF)
     B = torch.randn(K, N, device=gpu).to(BF)
@@ -261,27 +256,24 @@ def test_gemm8p(gpu, stagger, ak, bk, M, N, K):
     ref = A.float() @ B.float()
     bias = torch.randn(N, device=gpu).to(BF)
     mask = torch.randn(M, N, device=gpu).to(BF)
-    T().gemm8p_policy(2, stagger)
-    try:
-        c = torch.empty(M, N, device=gpu)
-        T().gemm(a, ak, b, bk, c, 0, None, False, None, 1.0, False)
-        assert rel_err(c, ref) < 1e-5
-        acc = torch.full((M, N), 1.5, device=gpu)
-        T().gemm(a, ak, b, bk, acc, 1, None, False, None, 1.0, True)       # split-K atomics
-        assert rel_err(acc, ref + 1.5) < 1e-5
-        y = torch.empty(M, N, device=gpu, dtype=BF)
-        T().gemm(a, ak, b, bk, y, 0, None, False, None, 1.0, False)
-        assert rel_err(y, ref) < 1e-2
-        T().gemm(a, ak, b, bk, y, 0, bias, True, None, 1.0, False)
-        assert rel_err(y, (ref + bias.float()).clamp_min(0)) < 1e-2
-        T().gemm(a, ak, b, bk, y, 0, None, False, mask, 0.5, False)
-        assert rel_err(y, 0.5 * ref * (mask.float() > 0)) < 1e-2
-        y0 = torch.randn(M, N, device=gpu).to(BF)
-        y1 = y0.clone()
-        T().gemm(a, ak, b, bk, y1, 1, None, False, None, 1.0, False)
-        assert rel_err(y1, y0.float() + ref) < 1e-2
-    finally:
-        T().gemm8p_policy(1, 0)
+    T().gemm8p_policy(2, tile)
+    c = torch.empty(M, N, device=gpu)
+    T().gemm(a, ak, b, bk, c, 0, None, False, None, 1.0, False)
+    assert rel_err(c, ref) < 1e-5
+    acc = torch.full((M, N), 1.5, device=gpu)
+    T().gemm(a, ak, b, bk, acc, 1, None, False, None, 1.0, True)       # split-K atomics
+    assert rel_err(acc, ref + 1.5) < 1e-5
+    y = torch.empty(M, N, device=gpu, dtype=BF)
+    T().gemm(a, ak, b, bk, y, 0, None, False, None, 1.0, False)
+    assert rel_err(y, ref) < 1e-2
+    T().gemm(a, ak, b, bk, y, 0, bias, True, None, 1.0, False)
+    assert rel_err(y, (ref + bias.float()).clamp_min(0)) < 1e-2
+    T().gemm(a, ak, b, bk, y, 0, None, False, mask, 0.5, False)
+    assert rel_err(y, 0.5 * ref * (mask.float() > 0)) < 1e-2
+    y0 = torch.randn(M, N, device=gpu).to(BF)
+    y1 = y0.clone()
+    T().gemm(a, ak, b, bk, y1, 1, None, False, None, 1.0, False)
+    assert rel_err(y1, y0.float() + ref) < 1e-2
 
 
 @pytest.mark.parametrize("ak,bk", [(True, True), (True, False), (False, True), (False, False)])
@@ -297,15 +289,20 @@ def test_gemm8p_exact_integer_layout(gpu, ak, bk):
     a = (A if ak else A.t().contiguous()).to(BF)
     b = (B.t().contiguous() if bk else B).to(BF)
     ref = A @ B
-    try:
-        for sched in (0, 1, 2, 100, 102, 200, 202):
-            T().gemm8p_policy(2, sched)
-            c = torch.empty(M, N, device=gpu)
-            T().gemm(a, ak, b, bk, c, 0, None, False, None, 1.0, False)
-            torch.cuda.synchronize()
-            assert torch.equal(c, ref), sched
-    finally:
-        T().gemm8p_policy(1, 0)
+    for tile in (0, 128, 256):
+        T().gemm8p_policy(2, tile)
+        c = torch.empty(M, N, device=gpu)
+        T().gemm(a, ak, b, bk, c, 0, None, False, None, 1.0, False)
+        torch.cuda.synchronize()
+        assert torch.equal(c, ref), tile
+        # slab split-K (fp32 slabs + reduce) of the same tiles: still exact
+        T().gemm8p_policy(3, tile)
+        T().gemm8p_slab_force(4)
+        c = torch.empty(M, N, device=gpu)
+        T().gemm(a, ak, b, bk, c, 0, None, False, None, 1.0, False)
+        torch.cuda.synchronize()
+        T().gemm8p_slab_force(0)
+        assert torch.equal(c, ref), ("slab", tile)
 
 
 @pytest.mark.parametrize("ak,bk", [(True, True), (True, False), (False, False)])
@@ -322,21 +319,18 @@ def test_gemm8p_slab_splitk(gpu, ak, bk, M, N, K):
     bias = torch.randn(N, device=gpu).to(BF)
     mask = torch.randn(M, N, device=gpu).to(BF)
     T().gemm8p_policy(3, 0)
-    try:
-        y = torch.empty(M, N, device=gpu, dtype=BF)
-        T().gemm(a, ak, b, bk, y, 0, bias, True, None, 1.0, False)
-        assert rel_err(y, (ref + bias.float()).clamp_min(0)) < 1e-2
-        T().gemm(a, ak, b, bk, y, 0, None, False, mask, 0.5, False)
-        assert rel_err(y, 0.5 * ref * (mask.float() > 0)) < 1e-2
-        c = torch.full((M, N), 2.0, device=gpu)
-        T().gemm(a, ak, b, bk, c, 1, None, False, None, 1.0, False)
-        assert rel_err(c, ref + 2.0) < 1e-5
-        y0 = torch.randn(M, N, device=gpu).to(BF)
-        y1 = y0.clone()
-        T().gemm(a, ak, b, bk, y1, 1, None, False, None, 1.0, False)
-        assert rel_err(y1, y0.float() + ref) < 1e-2
-    finally:
-        T().gemm8p_policy(1, 0)
+    y = torch.empty(M, N, device=gpu, dtype=BF)
+    T().gemm(a, ak, b, bk, y, 0, bias, True, None, 1.0, False)
+    assert rel_err(y, (ref + bias.float()).clamp_min(0)) < 1e-2
+    T().gemm(a, ak, b, bk, y, 0, None, False, mask, 0.5, False)
+    assert rel_err(y, 0.5 * ref * (mask.float() > 0)) < 1e-2
+    c = torch.full((M, N), 2.0, device=gpu)
+    T().gemm(a, ak, b, bk, c, 1, None, False, None, 1.0, False)
+    assert rel_err(c, ref + 2.0) < 1e-5
+    y0 = torch.randn(M, N, device=gpu).to(BF)
+    y1 = y0.clone()
+    T().gemm(a, ak, b, bk, y1, 1, None, False, None, 1.0, False)
+    assert rel_err(y1, y0.float() + ref) < 1e-2
 
 
 def test_gemm_dma_splitk(gpu):

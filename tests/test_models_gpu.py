@@ -15,6 +15,19 @@ def rel(a, b):
     return ((a.float() - b.float()).norm() / (b.float().norm() + 1e-12)).item()
 
 
+@pytest.fixture(autouse=True)
+def _production_policies(gpu):
+    """Model-level parity is claimed for the configuration production runs:
+    every kernel policy must hold its load-time (production) value here,
+    whatever kernel tests ran before (conftest restores them after each)."""
+    import conftest
+
+    names = str(torch.ops.tam.policy_names()).split(",")
+    state = conftest.policy_state()
+    diff = {n: (v, p) for n, v, p in zip(names, state, conftest.PRODUCTION_POLICIES) if v != p}
+    assert not diff, f"non-production kernel policies at model test start: {diff}"
+
+
 @pytest.mark.parametrize("model", ["resnet_tiny", "vgg_tiny", "transformer_tiny", "gnmt_tiny"])
 def test_model_grads_match_reference(gpu, model):
     tg = Trainer(model, gpu, seed=3)

@@ -222,7 +222,20 @@ class Controller:
                                     d.get("total_mb"), r.get("job"))
             if not r:
                 continue
+            # one rank's entries per job first: a fill carry (steps finished
+            # after the last plan snapshot) adds to the round's own entry
+            mine: Dict[str, dict] = {}
             for jr in r.get("jobs") or []:
+                m = mine.get(jr["job"])
+                if m is None:
+                    mine[jr["job"]] = dict(jr)
+                else:
+                    m["iters"] += jr["iters"]
+                    m["run_s"] += jr["run_s"]
+                    m["fill"] = m.get("fill") and jr.get("fill")
+                    for f in ("error", "move_failed", "snap_failed", "consolidate_failed"):
+                        m[f] = m.get(f) or jr.get(f)
+            for jr in mine.values():
                 # gang members report the same job: a step counts once every
                 # member completed it (min), an error from any member marks it
                 agg = per_job.get(jr["job"])
@@ -278,6 +291,19 @@ class Controller:
                         # bytes this member put on the wire per step (the gang's wire format)
                         j.extra["comm_bytes"] = j.extra.get("comm_bytes", 0.0) + c.get("bytes", 0.0)
                         j.extra["comm_steps"] = j.extra.get("comm_steps", 0) + c.get("bytes_steps", 0)
+
+    def apply_fill(self, counts: Dict[str, int]) -> None:
+        """Fill-mode progress read at plan time (``Worker.fill``): steps a
+        rank took on its job after finishing its round's share, while the
+        round's slowest rank was still running. Counted as progress now (a
+        job that completes in fill finishes in this plan); steps completed
+        after this snapshot arrive as carry in the next reports."""
+        for jid, n in counts.items():
+            if jid not in self.rjobs or n <= 0:
+                continue
+            self.done_iters[jid] += int(n)
+            j = self.sched.jobs[jid]
+            j.progress = float(min(self.done_iters[jid], self.rjobs[jid].iterations))
 
     # ---------------------------------------------------------------- failures
     def rank_lost(self, r: int) -> None:
@@ -621,6 +647,10 @@ class Controller:
             n = min(n, left)
             for r in gang_ranks(j.allocation, self.gpn):
                 assign.setdefault(r, []).append((j.job_id, n))
+        # iterations each assigned job has left after this round's share
+        # (bounds fill-mode steps, Worker.fill)
+        left = {jid: self.rjobs[jid].iterations - self.done_iters[jid] - n
+                for r in assign for jid, n in assign[r]}
         for r in assign:                      # same order on every rank (gang collectives)
             if len(assign[r]) > 1:
                 # co-located 1-GPU jobs each progress at 1/s of solo speed:
@@ -649,7 +679,7 @@ class Controller:
         # next trace arrival as an absolute host-clock time: 1-GPU jobs end the
         # round at the first step boundary after it (Worker._run_until)
         deadline = self.t0 + nxt if math.isfinite(nxt) else None
-        plan = {"round": self.round, "actions": actions, "assign": assign, "stop": stop, "wait": wait,
+        plan = {"round": self.round, "actions": actions, "assign": assign, "left": left, "stop": stop, "wait": wait,
                 "deadline": deadline, "alive": [r for r in range(self.world) if r not in self.dead],
                 "ckpt": getattr(self.cfg, "ckpt_policy", "none")}
         if plan["ckpt"] == "pressure":

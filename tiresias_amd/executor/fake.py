@@ -69,7 +69,8 @@ class FakeCluster:
 
     def __init__(self, world: int, iter_s: Optional[Dict[str, float]] = None, interference=None,
                  vnode_size: int = 0, nic_gbps: float = 12.5, xgmi_gbps: float = 64.0,
-                 host_gbps: float = 50.0, gang_factor: float = 1.08, start_s: float = 0.002):
+                 host_gbps: float = 50.0, gang_factor: float = 1.08, start_s: float = 0.002,
+                 fill: bool = True, vote_s: float = 60e-6):
         self.world = world
         self.iter_s = dict(NOMINAL_ITER_S)
         self.iter_s.update(iter_s or {})
@@ -86,6 +87,18 @@ class FakeCluster:
         self.groups: Set[Tuple[int, ...]] = set()
         self.stats = {"p2p_bytes": 0.0, "spill_bytes": 0.0, "restore_bytes": 0.0, "starts": 0,
                       "resident_resumes": 0, "rounds": 0}
+        # fill mode (cluster_runtime.Worker.fill): a rank that finished its
+        # round's share keeps stepping its job until the next plan arrives;
+        # a gang agrees on every extra step with a one-element all-reduce
+        # (vote_s). fill_seen: the fill steps the controller saw at plan time;
+        # carry: steps completed after that (in flight when the plan came),
+        # reported with the next round; late: how far into the next round a
+        # rank's in-flight fill step runs
+        self.fill = fill
+        self.vote_s = vote_s
+        self.fill_seen: Dict[str, int] = {}
+        self.carry: Dict[int, Dict[str, Tuple[int, float]]] = {}
+        self.late: Dict[int, float] = {}
 
     # ---------------------------------------------------------------- timing model
     def step_time(self, model: str, ranks: Tuple[int, ...]) -> float:
@@ -224,19 +237,30 @@ class FakeCluster:
                         raise ProtocolError(f"gang {jid} members assigned different step counts")
         deadline = plan.get("deadline")
         reports, busy = [], {}
+        steps: Dict[int, float] = {}              # rank -> step seconds of its single job
+        late = self.late
+        self.late = {}
+
+        def ready(x):
+            return action_cost.get(x, 0.0) + late.get(x, 0.0)
+
         for r in range(self.world):
             lst = assign.get(r) or []
-            t0 = action_cost.get(r, 0.0)
+            t0 = ready(r)
             reps = []
             if len(lst) == 1:
                 jid, n = lst[0]
                 st = self.step_time(self.model[jid], self.held[jid])
+                if len(self.held[jid]) > 1:
+                    # a gang steps together: its members start when the last one is ready
+                    t0 = max(ready(x) for x in self.held[jid])
                 if deadline is not None and len(self.held[jid]) == 1:
                     # 1-GPU job: the round ends at the first step boundary after
                     # the next arrival (Worker._run_until)
                     left = deadline - (now_abs + t0)
                     n = max(1, min(n, int(math.floor(left / st)) + 1)) if left > 0 else 1
                 busy[r] = t0 + n * st
+                steps[r] = st
                 reps.append({"job": jid, "iters": n, "run_s": n * st, "shared": False, "loss": None})
             elif lst:
                 # co-located 1-GPU jobs run concurrently, each slowed by its partner
@@ -252,9 +276,62 @@ class FakeCluster:
                     reps.append({"job": jid, "iters": n, "run_s": dur, "shared": True, "loss": None})
             else:
                 busy[r] = t0
+            # fill steps completed after the last plan snapshot, in flight then
+            for jid, (k, sec) in (self.carry.pop(r, None) or {}).items():
+                reps.append({"job": jid, "iters": k, "run_s": sec, "shared": False, "loss": None, "fill": True})
             reports.append({"rank": r, "job": lst[0][0] if lst else None, "jobs": reps, "dev": None})
         self.stats["rounds"] += 1
-        return reports, max(busy.values()) if busy else 0.0
+        dur = max(busy.values()) if busy else 0.0
+        # fill: ranks whose single job has iterations left keep stepping it
+        # until the plan (at dur); a gang by agreement (vote per extra step)
+        self.fill_seen = {}
+        left_of = plan.get("left") or {}
+        filled: Dict[int, float] = {}
+        if self.fill:
+            done_g: Dict[str, Tuple[int, int, float]] = {}
+            for r in sorted(steps):
+                jid, n = assign[r][0]
+                ranks = self.held[jid]
+                left = int(left_of.get(jid, 0))
+                if left <= 0:
+                    continue
+                if len(ranks) > 1:
+                    if jid not in done_g:
+                        st = steps[r] + self.vote_s
+                        b = max(busy[x] for x in ranks)
+                        gap = dur - b
+                        k = min(left, int(math.floor(gap / st))) if gap > 0 else 0
+                        fl = 1 if (k < left and gap > 0) else 0       # the step in flight at the plan
+                        done_g[jid] = (k, fl, st)
+                    k, fl, st = done_g[jid]
+                    b = max(busy[x] for x in ranks)
+                else:
+                    st = steps[r]
+                    b = busy[r]
+                    gap = dur - b
+                    k = min(left, int(math.floor(gap / st))) if gap > 0 else 0
+                    fl = 1 if (k < left and gap > 0) else 0
+                if k:
+                    self.fill_seen[jid] = k
+                filled[r] = k * st
+                if fl:
+                    self.carry.setdefault(r, {})[jid] = (1, st)
+                    self.late[r] = b + (k + 1) * st - dur
+                    filled[r] = dur - b
+        # barrier idle: a rank that had work this round but finished before
+        # the slowest rank waits at the round's gather (bulk-synchronous
+        # rounds) unless it fills; GPU time = what ranks with work were busy
+        for r in assign:
+            if assign[r]:
+                self.stats["busy_s"] = self.stats.get("busy_s", 0.0) + busy[r] + filled.get(r, 0.0)
+                idle = dur - busy[r] - min(filled.get(r, 0.0), dur - busy[r])
+                self.stats["barrier_idle_s"] = self.stats.get("barrier_idle_s", 0.0) + idle
+                jid = assign[r][0][0]
+                why = ("shared" if len(assign[r]) > 1 else "job_done" if int(left_of.get(jid, 0)) <= 0
+                       else "gang" if len(self.held[jid]) > 1 else "one_gpu")
+                self.stats["idle_" + why] = self.stats.get("idle_" + why, 0.0) + idle
+                self.stats["fill_s"] = self.stats.get("fill_s", 0.0) + filled.get(r, 0.0)
+        return reports, dur
 
 
 def run_fake(cfg: SimConfig, jobs: List[ReplayJob], world: int, quantum: float = 0.25,
@@ -294,6 +371,8 @@ def run_fake(cfg: SimConfig, jobs: List[ReplayJob], world: int, quantum: float =
                 dt = 1e-6
         clock.advance(dt + plan_cost_s)
         ctrl.apply_reports(reps)
+        if fc.fill_seen:
+            ctrl.apply_fill(fc.fill_seen)     # read at plan time (live: the fill keys)
         rounds += 1
     if fc.held:
         raise ProtocolError(f"replay ended with state still held for {sorted(fc.held)}")

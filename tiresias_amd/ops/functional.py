@@ -265,6 +265,11 @@ class _Linear(Function):
                 _DEFER_WGRAD.append((dy, x, w, b, mode))
                 deferred = True
             else:
+                if _DEFER_WGRAD is not None and any(it[2] is w for it in _DEFER_WGRAD):
+                    # w also has a deferred (possibly store-mode) write pending:
+                    # issue it first, or its later store would overwrite this
+                    # accumulation
+                    flush_wgrad()
                 with _OnWgrad(dy, x):
                     # the bias gradient colsum(dy) rides on the weight-gradient
                     # GEMM's own A loads (fused on the igemm route, else a pass)

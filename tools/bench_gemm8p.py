@@ -52,8 +52,8 @@ def main():
         A = (torch.rand(M, K, device=dev) * 2 - 1).to(BF)
         B = (torch.rand(N, K, device=dev) * 2 - 1).to(BF)
         c = torch.empty(M, N, device=dev, dtype=BF)
-        for name, sched in (("stagger", 2), ("no_dma", 12), ("no_lds_read", 22), ("1bar", 0)):
-            T.gemm8p_policy(2, sched)
+        for name, tile in (("p8_256", 256), ("p8_128", 128)):
+            T.gemm8p_policy(2, tile)
             ms = timeit(lambda: T.gemm(A, True, B, True, c, 0, None, False, None, 1.0, False))
             print(json.dumps({"ablation": name, "tflops": round(2.0 * M * N * K / ms / 1e9, 1)}), flush=True)
         T.gemm8p_policy(1, 0)
@@ -66,7 +66,7 @@ def main():
         c = torch.empty(M, N, device=dev, dtype=BF)
         fl = 2.0 * M * N * K
         res = {"shape": f"{M}x{N}x{K} {'K' if ak else 'M'}{'K' if bk else 'N'}"}
-        for name, mode, stg in (("p8_256", 2, 200), ("p8_128", 2, 100), ("p8_slab_auto", 3, 0),
+        for name, mode, stg in (("p8_256", 2, 256), ("p8_128", 2, 128), ("p8_slab_auto", 3, 0),
                                 ("legacy", 0, 0)):
             T.gemm8p_policy(mode, stg)
             ms = timeit(lambda: T.gemm(a_, ak, b_, bk, c, 0, None, False, None, 1.0, False))

@@ -56,7 +56,7 @@ def main():
         mode = 1 if f32 else 0
         fn = lambda: T.gemm(a_, ak, b_, bk, c, mode, None, False, None, 1.0, True)  # noqa: E731
         r = {"shape": f"{M}x{N}x{K} {lay}", "f32_acc": f32}
-        T.gemm8p_policy(3, 4)
+        T.gemm8p_policy(3, 0)
         T.gemm8p_sk_force(1)
         r["streamk_us"] = round(timeit(fn), 2)
         T.gemm8p_sk_force(0)
@@ -64,11 +64,11 @@ def main():
             for sp in (1, 2, 3, 4, 5, 7, 8):
                 if K // 64 // sp < 8:
                     continue
-                T.gemm8p_policy(3, 4 + (200 if tile == 256 else 100))
+                T.gemm8p_policy(3, tile)
                 T.gemm8p_slab_force(sp)
                 r[f"p8_{tile}_sp{sp}_us"] = round(timeit(fn), 2)
         T.gemm8p_slab_force(0)
-        T.gemm8p_policy(1, 4)
+        T.gemm8p_policy(1, 0)
         Ae, Be = A, B
         if f32:
             # store-only fp32 (what bench_gemm_routes times) and accumulate into C (what ours does)

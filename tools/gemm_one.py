@@ -20,7 +20,7 @@ def main():
     a_ = A if ak else A.t().contiguous()
     b_ = B.t().contiguous() if bk else B
     c = torch.empty(M, N, device=dev, dtype=torch.bfloat16)
-    T.gemm8p_policy(2, 200)          # force the 256^2 p8 kernel, no split
+    T.gemm8p_policy(2, 256)          # force the 256^2 p8 kernel, no split
     for _ in range(iters):
         T.gemm(a_, ak, b_, bk, c, 0, None, False, None, 1.0, False)
     torch.cuda.synchronize()
