@@ -60,9 +60,13 @@ import torch.distributed as dist  # noqa: E402
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
-if os.environ.get("TAM_STACK_DUMP_S"):         # hang diagnosis: periodic all-thread stacks
-    import faulthandler
+import faulthandler  # noqa: E402
 
+# every rank: a fatal signal (SIGSEGV / SIGABRT / SIGBUS / SIGFPE) leaves all
+# threads' Python stacks on stderr (round 4 recorded an undiagnosed rank-0
+# SIGSEGV in the shared-GPU rehearsal)
+faulthandler.enable(all_threads=True)
+if os.environ.get("TAM_STACK_DUMP_S"):         # hang diagnosis: periodic all-thread stacks
     faulthandler.dump_traceback_later(float(os.environ["TAM_STACK_DUMP_S"]), repeat=True)
 
 from tiresias_amd.config import ClusterSpec, SimConfig  # noqa: E402
@@ -481,6 +485,15 @@ def main():
         nopool, _ = replay(cfg)
         worker.pool_cap = cap
 
+    # every rank's plan-application seconds by action kind over the whole
+    # process (all replays), and its fill-mode steps: where N>1 time goes
+    ap_all = [{"rank": rank, "apply_s": {k: round(v, 4) for k, v in sorted(worker.apply_prof.items())},
+               "apply_n": dict(sorted(worker.apply_count.items())),
+               "fill_s": round(worker.fill_s_total, 4), "fill_steps": worker.fill_steps_total}]
+    if world > 1:
+        got = [None] * world
+        dist.all_gather_object(got, ap_all[0], group=ctrl_pg)
+        ap_all = got
     if rank == 0:
         jcts = [s["avg_jct"] for s in sums]
         mks = [s["makespan"] for s in sums]
@@ -551,6 +564,10 @@ def main():
             "shared_rounds": sums[-1].get("shared_rounds"),
             "gpu_utilization": round(statistics.fmean(s["gpu_utilization"] for s in sums), 4),
             "runtime_breakdown_s": sums[-1].get("runtime_breakdown"),
+            "apply_breakdown_last_replay_rank0_s": sums[-1].get("apply_breakdown_rank0"),
+            "apply_counts_last_replay_rank0": sums[-1].get("apply_counts_rank0"),
+            "per_rank_process_totals": ap_all,
+            "fill_mode": bool(worker.fill_enabled and world > 1),
             "pool_hits": worker.pool_hits,
             "pressure_spills": worker.pressure_spills,
             "pool_evictions": worker.pool_evictions,

@@ -278,6 +278,11 @@ def _recover_worker(rank, world, port, outdir, fault, hb_timeout=5.0, gang_timeo
     from tiresias_amd.parallel import gang
 
     gang.GANG_TIMEOUT_S = gang_timeout
+    import faulthandler
+
+    # a rank still running after 60 s leaves every thread's stack behind
+    stacks = open(os.path.join(outdir, f"stacks{rank}.txt"), "w")
+    faulthandler.dump_traceback_later(60.0, repeat=True, file=stacks)
     jobs = bench.bench_trace(world, 4, seed=3, work_s=0.8, min_iters=4, tiny=True)
     for i in (0, 2, 5):                    # gangs spanning the victim rank
         jobs[i].spec.num_gpu = 2 if i != 5 else world - 1
@@ -416,7 +421,8 @@ def test_rank_loss_restarts_from_snapshot(tmp_path):
     import csv
     import json
 
-    ps, s = _run_recover(tmp_path, {"rank": 3, "round": 14, "kind": "crash"}, snapshot_s=0.02)
+    ps, s = _run_recover(tmp_path, {"rank": 3, "round": 3, "kind": "crash", "when": "snapshotted"},
+                         snapshot_s=0.02)
     errs = {f.name: f.read_text()[-1500:] for f in tmp_path.glob("err*.txt")}
     assert ps[3].exitcode == 17 and all(p.exitcode == 0 for p in ps[:3]), ([p.exitcode for p in ps], errs)
     assert s["lost_ranks"] == [3] and s["finished"] + s["failed"] == s["jobs"]
@@ -439,8 +445,8 @@ def test_unreadable_snapshot_restarts_from_scratch(tmp_path):
     import csv
     import json
 
-    ps, s = _run_recover(tmp_path, {"rank": 3, "round": 14, "kind": "crash", "corrupt_snapshots": True},
-                         snapshot_s=0.02)
+    ps, s = _run_recover(tmp_path, {"rank": 3, "round": 3, "kind": "crash", "corrupt_snapshots": True,
+                                    "when": "snapshotted"}, snapshot_s=0.02)
     errs = {f.name: f.read_text()[-1500:] for f in tmp_path.glob("err*.txt")}
     assert ps[3].exitcode == 17 and all(p.exitcode == 0 for p in ps[:3]), ([p.exitcode for p in ps], errs)
     assert s["lost_ranks"] == [3] and s["finished"] + s["failed"] == s["jobs"]

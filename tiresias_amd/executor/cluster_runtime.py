@@ -184,6 +184,7 @@ class Controller:
         self.error_log: List[str] = []          # first step errors (summary)
         self.est: Dict[Tuple[str, int], float] = {}
         self.done_iters: Dict[str, int] = {j: 0 for j in self.rjobs}
+        self.plan_fill: Dict[str, int] = {}     # fill steps credited for the next plan (echoed to workers)
         self.round = 0
         self.t0 = None
         self.spill = getattr(cfg, "ckpt_policy", "none") == "host"
@@ -291,6 +292,17 @@ class Controller:
                         # bytes this member put on the wire per step (the gang's wire format)
                         j.extra["comm_bytes"] = j.extra.get("comm_bytes", 0.0) + c.get("bytes", 0.0)
                         j.extra["comm_steps"] = j.extra.get("comm_steps", 0) + c.get("bytes_steps", 0)
+
+    def credit_fill(self, counts: Dict[int, Dict[str, int]]) -> Dict[str, int]:
+        """Per-rank fill counts -> the steps credited per job (a gang's step
+        counts once every member finished it: the min over its holders)."""
+        per: Dict[str, int] = {}
+        for jid, hold in self.holders.items():
+            vals = [int((counts.get(r) or {}).get(jid, 0)) for r in hold]
+            if vals and min(vals) > 0:
+                per[jid] = min(vals)
+        self.apply_fill(per)
+        return per
 
     def apply_fill(self, counts: Dict[str, int]) -> None:
         """Fill-mode progress read at plan time (``Worker.fill``): steps a
@@ -679,7 +691,9 @@ class Controller:
         # next trace arrival as an absolute host-clock time: 1-GPU jobs end the
         # round at the first step boundary after it (Worker._run_until)
         deadline = self.t0 + nxt if math.isfinite(nxt) else None
-        plan = {"round": self.round, "actions": actions, "assign": assign, "left": left, "stop": stop, "wait": wait,
+        seen, self.plan_fill = self.plan_fill, {}
+        plan = {"round": self.round, "actions": actions, "assign": assign, "left": left, "fill_seen": seen,
+                "stop": stop, "wait": wait,
                 "deadline": deadline, "alive": [r for r in range(self.world) if r not in self.dead],
                 "ckpt": getattr(self.cfg, "ckpt_policy", "none")}
         if plan["ckpt"] == "pressure":
@@ -737,7 +751,22 @@ class Worker:
             if not snapshot_dir:
                 raise ValueError("snapshot_s > 0 needs a snapshot_dir shared by every rank")
             self.snap = SnapshotWriter(snapshot_dir, device)
+        # fill mode (fill_step): the job this rank keeps stepping after its
+        # round's share while slower ranks finish, steps taken, and the
+        # steps the controller's snapshot did not see (reported next round)
+        self._fill: Optional[dict] = None
+        self._carry: List[dict] = []
+        self.fill_enabled = os.environ.get("TAM_FILL", "1") != "0"
+        self.fill_s_total = 0.0
+        self.fill_steps_total = 0
+        # host seconds of plan application per action kind (start_fresh_build /
+        # _pool, start_p2p / _resident / _snapshot, p2p_transfer, move_agree,
+        # group, consolidate, drop, spill, pressure_room, reclaim, prefetch)
+        # and the hipGraph captures of fresh trainers' first steps
+        self.apply_prof: Dict[str, float] = {}
+        self.apply_count: Dict[str, int] = {}
         self._snap_failed: set = set()          # jobs whose snapshot load failed (this round)
+        self.snap_reported: set = set()         # jobs with a durable snapshot the controller was told of
         self._consolidate_failed: set = set()   # sharded gangs whose consolidation failed
         self._job_ranks: Dict[str, Tuple[int, ...]] = {}
         self._snap_acc: Dict[str, float] = {}
@@ -975,8 +1004,16 @@ class Worker:
         c = self._ckpt.setdefault(jid, {"bytes": 0.0, "save_s": 0.0, "restore_s": 0.0})
         c["bytes"] += nb
 
+    def _ap(self, key: str, t0: float) -> float:
+        """Charge the host seconds since ``t0`` to apply-breakdown ``key``."""
+        t = time.perf_counter()
+        self.apply_prof[key] = self.apply_prof.get(key, 0.0) + (t - t0)
+        self.apply_count[key] = self.apply_count.get(key, 0) + 1
+        return t
+
     def apply(self, plan: dict) -> None:
         self._round += 1
+        ta = time.perf_counter()
         pressure = plan.get("ckpt") == "pressure"
         if pressure:
             # jobs this rank runs or starts this round must stay resident
@@ -994,139 +1031,158 @@ class Worker:
                     self._make_room(self._job_need(a["model"], a.get("batch")), protect, ro)
                 elif getattr(t, "_spilled", None):
                     self._make_room(t.hbm_bytes(), protect, ro)
+            ta = self._ap("pressure_room", ta)
         moves: Dict[str, tuple] = {}          # job -> ([(send|recv, buffer, peer)], action), plan order
         snap_loads: Dict[str, tuple] = {}     # job -> (local load ok, action): restarts from snapshots
         for a in plan["actions"]:
             op = a["op"]
-            if op == "group":
-                # communicators outlive a replay: every rank holds the same
-                # cache (same plans, same order), so skipping is collective-safe
-                c = self.groups.get(tuple(a["ranks"]))
-                if c is None or getattr(c, "vnode", a.get("vnode", 0)) != a.get("vnode", 0):
-                    if self.rank in a["ranks"]:
-                        try:
-                            self._open_group(a["ranks"], a.get("vnode", 0), a.get("nic_gbps", 12.5))
-                        except Exception as e:      # a member never arrived: the gang's step fails
-                            from ..parallel.gang import FailedComm
+            if op != "start":
+                key = op
+            elif a["source"] == "fresh" and self.rank in a["ranks"]:
+                key = "start_fresh_pool" if self.pool.get((a["model"], a.get("batch"), tuple(a["ranks"]))) \
+                    else "start_fresh_build"
+            else:
+                key = "start_" + a["source"]
+            ta = self._apply_one(a, op, moves, snap_loads, ta, key)
+        ta = self._finish_apply(plan, moves, snap_loads, pressure, ta)
 
-                            self.groups[tuple(a["ranks"])] = FailedComm(a["ranks"], f"{type(e).__name__}: {e}")
-            elif op == "consolidate":
-                t = self.trainers.get(a["job"])
-                if t is not None and self.rank in a["ranks"]:
+    def _apply_one(self, a, op, moves, snap_loads, ta, key) -> float:
+        """One plan action (timed into apply_prof[key])."""
+        if op == "group":
+            # communicators outlive a replay: every rank holds the same
+            # cache (same plans, same order), so skipping is collective-safe
+            c = self.groups.get(tuple(a["ranks"]))
+            if c is None or getattr(c, "vnode", a.get("vnode", 0)) != a.get("vnode", 0):
+                if self.rank in a["ranks"]:
                     try:
-                        self.consolidated_bytes += t.consolidate()
-                    except Exception as e:           # a member died: no one holds the whole state
-                        print(f"[worker {self.rank}] job {a['job']}: consolidate over {a['ranks']} failed "
-                              f"({type(e).__name__}: {e})", file=sys.stderr, flush=True)
-                        abort_comm(t.group)
-                        self.trainers.pop(a["job"], None)
-                        t.release()
-                        self._consolidate_failed.add(a["job"])
-            elif op == "ungroup":
-                self._close_group(a["ranks"])
-            elif op == "abort":
-                self._close_group(a["ranks"], abort=True, dead=a.get("dead"), purge=a.get("purge"))
-            elif op == "drop":
-                self.streams.pop(a["job"], None)
-                self._retire(self.trainers.pop(a["job"], None))
-                self._job_ranks.pop(a["job"], None)
-                self._snap_acc.pop(a["job"], None)
-                # the holder's lowest rank deletes the (shared) file, and so
-                # does every rank whose writer ever snapshotted the job -- an
-                # earlier holder's queued write must not re-create it later
-                if self.snap is not None and (self.rank == min(a["ranks"]) or self.snap.wrote(a["job"])):
-                    self.snap.drop(a["job"])
-            elif op == "spill":
-                if self.trainers.get(a["job"]) is not None:
-                    self._spill(a["job"])
-            elif op == "start":
-                ranks = tuple(a["ranks"])
-                src = a["source"]
-                self._job_ranks[a["job"]] = ranks
-                if src == "snapshot":
-                    # the job's only replica died: rebuild from its last
-                    # durable snapshot (every gang member reads the file); a
-                    # missing / truncated / unreadable file fails the load on
-                    # that member, and the members agree on the verdict below
-                    if self.rank in ranks:
-                        from ..ckpt.snapshot import load_snapshot
+                        self._open_group(a["ranks"], a.get("vnode", 0), a.get("nic_gbps", 12.5))
+                    except Exception as e:      # a member never arrived: the gang's step fails
+                        from ..parallel.gang import FailedComm
 
-                        old_t = self.trainers.pop(a["job"], None)
-                        if old_t is not None:
-                            old_t.release()
-                        t = self._make_trainer(a, init=False)
-                        ok = True
-                        try:
-                            load_snapshot(a["path"], t)
-                        except Exception as e:
-                            ok = False
-                            print(f"[worker {self.rank}] job {a['job']}: snapshot {a['path']} unreadable "
-                                  f"({type(e).__name__}: {e}); restarting it from scratch",
-                                  file=sys.stderr, flush=True)
-                        self.trainers[a["job"]] = t
-                        self._snap_acc[a["job"]] = 0.0
-                        snap_loads[a["job"]] = (ok, {**a, "old": []})
-                elif src == "fresh":
-                    if self.rank in ranks:
-                        before = torch.cuda.memory_allocated(self.device) if self.device.type == "cuda" else 0
-                        self.trainers[a["job"]] = self._make_trainer(a)
-                        if self.device.type == "cuda":
-                            grown = torch.cuda.memory_allocated(self.device) - before
-                            if grown > 0:      # a newly built trainer (not a warm-pool reuse)
-                                # what _resident_bytes will count for it (state + batch)
-                                self._need[a["model"]] = max(self._need.get(a["model"], 0.0), float(grown))
-                elif src == "resident":
+                        self.groups[tuple(a["ranks"])] = FailedComm(a["ranks"], f"{type(e).__name__}: {e}")
+        elif op == "consolidate":
+            t = self.trainers.get(a["job"])
+            if t is not None and self.rank in a["ranks"]:
+                try:
+                    self.consolidated_bytes += t.consolidate()
+                except Exception as e:           # a member died: no one holds the whole state
+                    print(f"[worker {self.rank}] job {a['job']}: consolidate over {a['ranks']} failed "
+                          f"({type(e).__name__}: {e})", file=sys.stderr, flush=True)
+                    abort_comm(t.group)
+                    self.trainers.pop(a["job"], None)
+                    t.release()
+                    self._consolidate_failed.add(a["job"])
+        elif op == "ungroup":
+            self._close_group(a["ranks"])
+        elif op == "abort":
+            self._close_group(a["ranks"], abort=True, dead=a.get("dead"), purge=a.get("purge"))
+        elif op == "drop":
+            self.streams.pop(a["job"], None)
+            self._retire(self.trainers.pop(a["job"], None))
+            self._job_ranks.pop(a["job"], None)
+            self._snap_acc.pop(a["job"], None)
+            # the holder's lowest rank deletes the (shared) file, and so
+            # does every rank whose writer ever snapshotted the job -- an
+            # earlier holder's queued write must not re-create it later
+            if self.snap is not None and (self.rank == min(a["ranks"]) or self.snap.wrote(a["job"])):
+                self.snap.drop(a["job"])
+        elif op == "spill":
+            if self.trainers.get(a["job"]) is not None:
+                self._spill(a["job"])
+        elif op == "start":
+            ranks = tuple(a["ranks"])
+            src = a["source"]
+            self._job_ranks[a["job"]] = ranks
+            if src == "snapshot":
+                # the job's only replica died: rebuild from its last
+                # durable snapshot (every gang member reads the file); a
+                # missing / truncated / unreadable file fails the load on
+                # that member, and the members agree on the verdict below
+                if self.rank in ranks:
+                    from ..ckpt.snapshot import load_snapshot
+
+                    old_t = self.trainers.pop(a["job"], None)
+                    if old_t is not None:
+                        old_t.release()
+                    t = self._make_trainer(a, init=False)
+                    ok = True
+                    try:
+                        load_snapshot(a["path"], t)
+                    except Exception as e:
+                        ok = False
+                        print(f"[worker {self.rank}] job {a['job']}: snapshot {a['path']} unreadable "
+                              f"({type(e).__name__}: {e}); restarting it from scratch",
+                              file=sys.stderr, flush=True)
+                    self.trainers[a["job"]] = t
+                    self._snap_acc[a["job"]] = 0.0
+                    snap_loads[a["job"]] = (ok, {**a, "old": []})
+            elif src == "fresh":
+                if self.rank in ranks:
+                    before = torch.cuda.memory_allocated(self.device) if self.device.type == "cuda" else 0
+                    self.trainers[a["job"]] = self._make_trainer(a)
+                    if self.device.type == "cuda":
+                        grown = torch.cuda.memory_allocated(self.device) - before
+                        if grown > 0:      # a newly built trainer (not a warm-pool reuse)
+                            # what _resident_bytes will count for it (state + batch)
+                            self._need[a["model"]] = max(self._need.get(a["model"], 0.0), float(grown))
+            elif src == "resident":
+                t = self.trainers.get(a["job"])
+                if t is not None and getattr(t, "_spilled", None):
+                    self._restore(a["job"])
+                if t is not None and self.rank in ranks:
+                    self._bind(t, ranks)
+            elif src == "p2p":
+                donors = {int(k): v for k, v in a["donors"].items()}
+                old = tuple(a["old"])
+                if self.rank in old and self.trainers.get(a["job"]) is not None \
+                        and getattr(self.trainers[a["job"]], "_spilled", None):
+                    self._restore(a["job"])
+                if self.rank in old or self.rank in ranks:
+                    # every old holder and new member takes part in the
+                    # move's verdict (a leaving holder frees its replica
+                    # only when the move succeeded everywhere)
+                    moves.setdefault(a["job"], ([], a))
+                if self.rank in donors:        # receiver (state arrives by P2P)
                     t = self.trainers.get(a["job"])
-                    if t is not None and getattr(t, "_spilled", None):
+                    if t is None:
+                        t = self._make_trainer(a, init=False)
+                        self.trainers[a["job"]] = t
+                    # a resync receiver already holds a (possibly diverged) replica
+                    elif t is not None and getattr(t, "_spilled", None):
                         self._restore(a["job"])
-                    if t is not None and self.rank in ranks:
-                        self._bind(t, ranks)
-                elif src == "p2p":
-                    donors = {int(k): v for k, v in a["donors"].items()}
-                    old = tuple(a["old"])
-                    if self.rank in old and self.trainers.get(a["job"]) is not None \
-                            and getattr(self.trainers[a["job"]], "_spilled", None):
-                        self._restore(a["job"])
-                    if self.rank in old or self.rank in ranks:
-                        # every old holder and new member takes part in the
-                        # move's verdict (a leaving holder frees its replica
-                        # only when the move succeeded everywhere)
-                        moves.setdefault(a["job"], ([], a))
-                    if self.rank in donors:        # receiver (state arrives by P2P)
-                        t = self.trainers.get(a["job"])
-                        if t is None:
-                            t = self._make_trainer(a, init=False)
-                            self.trainers[a["job"]] = t
-                        # a resync receiver already holds a (possibly diverged) replica
-                        elif t is not None and getattr(t, "_spilled", None):
-                            self._restore(a["job"])
+                    ops = moves.setdefault(a["job"], ([], a))[0]
+                    for _, buf in sorted(t.state_tensors().items()):
+                        ops.append(("recv", buf, donors[self.rank]))
+                for recv, donor in donors.items():
+                    if donor == self.rank:
+                        t = self.trainers[a["job"]]
                         ops = moves.setdefault(a["job"], ([], a))[0]
                         for _, buf in sorted(t.state_tensors().items()):
-                            ops.append(("recv", buf, donors[self.rank]))
-                    for recv, donor in donors.items():
-                        if donor == self.rank:
-                            t = self.trainers[a["job"]]
-                            ops = moves.setdefault(a["job"], ([], a))[0]
-                            for _, buf in sorted(t.state_tensors().items()):
-                                ops.append(("send", buf, recv))
-                    # replicas that stay: rebind their DDP bucketer to the new gang
-                    if self.rank in ranks and self.rank in old:
-                        t = self.trainers[a["job"]]
-                        t.rebind(self._group(ranks))
-                        t.pool_key = (a["model"], a.get("batch"), ranks)
-                    elif self.rank in ranks:
-                        self._bind(self.trainers[a["job"]], ranks)
-                    if self.rank in ranks and "step" in a:
-                        self.trainers[a["job"]].step_count = int(a["step"])
+                            ops.append(("send", buf, recv))
+                # replicas that stay: rebind their DDP bucketer to the new gang
+                if self.rank in ranks and self.rank in old:
+                    t = self.trainers[a["job"]]
+                    t.rebind(self._group(ranks))
+                    t.pool_key = (a["model"], a.get("batch"), ranks)
+                elif self.rank in ranks:
+                    self._bind(self.trainers[a["job"]], ranks)
+                if self.rank in ranks and "step" in a:
+                    self.trainers[a["job"]].step_count = int(a["step"])
+        return self._ap(key, ta)
+
+    def _finish_apply(self, plan, moves, snap_loads, pressure, ta) -> float:
         if any(a["op"] == "drop" for a in plan["actions"]):
             self.reclaim(64.0)
+            ta = self._ap("reclaim", ta)
         failed = set()
         if moves or snap_loads:
             ok = self._do_moves(moves) if moves else {}
+            ta = self._ap("p2p_transfer", ta)
             ok.update({jid: v for jid, (v, _) in snap_loads.items()})
             acts = {jid: a for jid, (_, a) in moves.items()}
             acts.update({jid: a for jid, (_, a) in snap_loads.items()})
             failed = self._agree_moves(plan.get("round"), ok, acts)
+            ta = self._ap("move_agree", ta)
         for jid in [j for j in failed if j in snap_loads]:
             # some member could not read the snapshot: no member runs the job
             # on it (replicas would disagree); the controller restarts it
@@ -1162,6 +1218,8 @@ class Worker:
                     self._retire(self.trainers.pop(a["job"], None))
         if pressure:
             self._prefetch(plan.get("resume_order") or [])
+            ta = self._ap("prefetch", ta)
+        return ta
 
     # ------------------------------------------------------------ state moves
     def _pair_pg(self, peer: int):
@@ -1175,7 +1233,11 @@ class Worker:
         pair = (min(self.rank, peer), max(self.rank, peer))
         pg = self._pairs.get(pair)
         if pg is None or pg.aborted:
-            pg = PG_CACHE.acquire(pair, self.rank, self.gang_backend, pin=True)
+            # a move can meet a peer that dies in the same round: bound the
+            # rendezvous by the control plane's loss detection, not 180 s
+            hb = getattr(self.plane, "hb_timeout", None)
+            pg = PG_CACHE.acquire(pair, self.rank, self.gang_backend, pin=True,
+                                  create_s=max(15.0, 3.0 * hb) if hb else None)
             self._pairs[pair] = pg
         return pg
 
@@ -1335,10 +1397,13 @@ class Worker:
         self._move_failed = set()
         self._snap_failed = set()
         self._consolidate_failed = set()
-        jobs = [(jid, n) for jid, n in jobs if jid not in {r["job"] for r in skipped}]
+        # fill-mode steps the last plan's snapshot did not count
+        skipped += self._carry
+        self._carry = []
+        jobs = [(jid, n) for jid, n in jobs if jid not in {r["job"] for r in skipped if not r.get("fill")}]
         if not jobs:
             return {"rank": self.rank, "job": None, "jobs": skipped, "dev": self._dev_sample(),
-                    "ckpt": self._ckpt_report(), "snap": self.snap.poll() if self.snap else None}
+                    "ckpt": self._ckpt_report(), "snap": self._snap_poll()}
         for jid, _ in jobs:
             self._last_run[jid] = self._round
         cuda = self.device.type == "cuda"
@@ -1383,6 +1448,13 @@ class Worker:
         if cuda:
             torch.cuda.synchronize(self.device)
         dt = time.perf_counter() - t0
+        for jid, _ in jobs:
+            # hipGraph captures of fresh trainers ran inside these steps
+            t = self.trainers.get(jid)
+            if t is not None and t.capture_s > getattr(t, "_cap_seen", 0.0):
+                self.apply_prof["graph_capture_in_run"] = self.apply_prof.get("graph_capture_in_run", 0.0) + \
+                    t.capture_s - getattr(t, "_cap_seen", 0.0)
+                t._cap_seen = t.capture_s
         persist_err: Dict[str, str] = {}
         if cuda:
             # the persistent LSTM kernels never hang: a grid barrier that timed
@@ -1435,7 +1507,119 @@ class Worker:
                 rep["error"] = err or persist_err[jid]
             reps.append(rep)
         return {"rank": self.rank, "job": jobs[0][0], "jobs": reps + skipped, "dev": self._dev_sample(),
-                "ckpt": self._ckpt_report(), "snap": self.snap.poll() if self.snap else None}
+                "ckpt": self._ckpt_report(), "snap": self._snap_poll()}
+
+    def _snap_poll(self):
+        if self.snap is None:
+            return None
+        got = self.snap.poll()
+        self.snap_reported.update(jid for jid, _, _ in got)
+        return got
+
+    # ------------------------------------------------------------ fill mode
+    def fill_begin(self, plan: dict, rep: dict) -> None:
+        """After this rank's share of the round: keep stepping its (single,
+        exclusive) job until the next plan is out, instead of idling at the
+        round barrier while slower ranks finish (fake backend, headline
+        trace, N=8: barrier idle 20 % -> 4 % of GPU time). Bounded by the
+        job's iterations left; a gang agrees on every extra step (vote)."""
+        self._fill = None
+        if not self.fill_enabled:
+            return
+        mine = plan["assign"].get(self.rank) or []
+        if len(mine) != 1:
+            return
+        jid = mine[0][0]
+        left = int((plan.get("left") or {}).get(jid, 0))
+        t = self.trainers.get(jid)
+        if left <= 0 or t is None or getattr(t, "broken", False) or getattr(t, "_spilled", None):
+            return
+        if any(r.get("error") for r in rep.get("jobs") or [] if r.get("job") == jid):
+            return
+        gang = t.ddp is not None and len(self._job_ranks.get(jid, (self.rank,))) > 1
+        if gang and (comm_failed(t.group) or t.ddp.comm is None):
+            return
+        self._fill = {"job": jid, "left": left, "n": 0, "sec": 0.0, "gang": gang, "done": False,
+                      "prev": None, "err": None, "t": t}
+
+    def _vote(self, t: Trainer, stop: bool) -> bool:
+        """One-element SUM all-reduce over the job's gang: does ANY member
+        want to stop? Every member takes the same decision, so the gang runs
+        the same number of fill steps on every member (its collectives
+        match)."""
+        v = getattr(t, "_vote_buf", None)
+        if v is None:
+            v = torch.zeros(1, dtype=torch.float32, device=self.device)
+            t._vote_buf = v
+        v.fill_(1.0 if stop else 0.0)
+        c = t.ddp.comm
+        c.finish([c.start(v)])
+        return float(v.item()) > 0.0
+
+    def fill_step(self, ready: bool) -> bool:
+        """One fill step when the round's next plan is not out yet
+        (``ready`` False); returns False once this rank's fill is over."""
+        f = self._fill
+        if f is None or f["done"]:
+            return False
+        t = f["t"]
+        cuda = self.device.type == "cuda"
+        try:
+            if f["gang"]:
+                if self._vote(t, ready or f["n"] >= f["left"]):
+                    f["done"] = True
+                    return False
+            elif ready or f["n"] >= f["left"]:
+                f["done"] = True
+                if f["prev"] is not None:
+                    f["prev"].synchronize()
+                return False
+            t0 = time.perf_counter()
+            t.step()
+            if cuda and not f["gang"]:
+                # keep one step queued ahead of the one waited on (the GPU
+                # never drains between fill steps)
+                ev = torch.cuda.Event()
+                ev.record()
+                if f["prev"] is not None:
+                    f["prev"].synchronize()
+                f["prev"] = ev
+            elif cuda:
+                torch.cuda.current_stream(self.device).synchronize()
+            f["n"] += 1
+            dt = time.perf_counter() - t0
+            f["sec"] += dt
+            self.fill_s_total += dt
+            self.fill_steps_total += 1
+            return True
+        except Exception as e:                    # a gang peer died mid-collective
+            f["err"] = f"{type(e).__name__}: {e}"
+            f["done"] = True
+            t.broken = True
+            if t.group is not None:
+                abort_comm(t.group)
+            return False
+
+    def fill_counts(self) -> Dict[str, int]:
+        f = self._fill
+        return {f["job"]: f["n"]} if f is not None and f["n"] else {}
+
+    def fill_end(self, seen: Dict[str, int]) -> None:
+        """The next plan is here: the fill steps its snapshot did not count
+        (``seen``: the controller's credited count per job) are reported with
+        the next round."""
+        f, self._fill = self._fill, None
+        if f is None:
+            return
+        if f["prev"] is not None and not f["done"]:
+            f["prev"].synchronize()
+        extra = f["n"] - int(seen.get(f["job"], 0))
+        if extra > 0 or f["err"]:
+            e = {"job": f["job"], "iters": max(0, extra), "run_s": f["sec"] * max(0, extra) / max(1, f["n"]),
+                 "shared": False, "loss": None, "fill": True}
+            if f["err"]:
+                e["error"] = f["err"]
+            self._carry.append(e)
 
     def _ckpt_report(self) -> Optional[dict]:
         """Per-job spill / restore bytes and measured device copy seconds since
@@ -1595,12 +1779,14 @@ def run_replay(cfg: SimConfig, jobs: List[ReplayJob], rank: int, world: int, dev
     plane = None
     if distributed:
         if control == "store":
-            from ..parallel.gang import PG_CACHE
+            from ..parallel.gang import PG_CACHE, note_dead
             from .control import StorePlane
 
             def _on_dead(r: int) -> None:
                 # watcher / monitor thread: unblock this rank's training
-                # thread if it is inside a collective with the dead rank
+                # thread if it is inside a collective with the dead rank, or
+                # inside a communicator rendezvous that includes it
+                note_dead(r)
                 PG_CACHE.abort_where(lambda k: r in k[0])
 
             plane = StorePlane(rank, world, hb_period=hb_period, hb_timeout=hb_timeout, on_dead=_on_dead)
@@ -1617,15 +1803,27 @@ def run_replay(cfg: SimConfig, jobs: List[ReplayJob], rank: int, world: int, dev
     shared = 0                                   # rounds with co-located jobs on a GPU
     # idle_s = sleeping because no job is runnable (arrival gaps), not overhead
     prof = {"plan_s": 0.0, "bcast_s": 0.0, "apply_s": 0.0, "run_s": 0.0, "idle_s": 0.0,
-            "gather_s": 0.0}
+            "gather_s": 0.0, "fill_s": 0.0}
+    ctrl_alive = list(range(world))
+    fill0 = (w.fill_s_total, w.fill_steps_total)
+    ap0, apc0 = dict(w.apply_prof), dict(w.apply_count)
     lost_ranks: List[int] = []
     try:
+        fill = distributed and control == "store" and w.fill_enabled
         while rounds < max_rounds:
             ta = time.perf_counter()
+            if ctrl and fill and rounds > 0:
+                # fill-mode steps every rank took since its last report (the
+                # snapshot this plan counts; later ones come as carry)
+                counts = plane.read_fill(rounds - 1, ctrl_alive)
+                counts[0] = w.fill_counts()
+                ctrl.plan_fill = ctrl.credit_fill(counts)
             plan = ctrl.plan_round() if ctrl else None
             tb = time.perf_counter()
             if distributed:
                 plan = plane.bcast(plan, rounds)
+            if fill:
+                w.fill_end(plan.get("fill_seen") or {})
             tc = time.perf_counter()
             plan["round"] = rounds
             if plan["stop"]:
@@ -1637,7 +1835,12 @@ def run_replay(cfg: SimConfig, jobs: List[ReplayJob], rank: int, world: int, dev
                 # declared lost (hung past the control plane's bound): this
                 # rank's GPU has left the cluster -- stop participating
                 break
-            if fault and fault.get("rank") == rank and rounds >= fault.get("round", 0):
+            if fault and fault.get("rank") == rank and rounds >= fault.get("round", 0) and (
+                    fault.get("when") != "snapshotted" or any(
+                        jid in w.snap_reported and w._job_ranks.get(jid) == (rank,)
+                        and jid in {j for j, _ in plan["assign"].get(rank) or []} for jid in w.trainers)):
+                # ("when": "snapshotted" -- only once this rank holds the ONLY
+                # replica of a job whose snapshot the controller knows of)
                 if fault.get("kind", "crash") == "crash":
                     if fault.get("corrupt_snapshots") and worker.snap is not None:
                         # the crash also tears the shared snapshot store:
@@ -1683,8 +1886,27 @@ def run_replay(cfg: SimConfig, jobs: List[ReplayJob], rank: int, world: int, dev
             prof["idle_s"] += tf - te
             newly: List[int] = []
             if distributed:
+                if fill:
+                    w.fill_begin(plan, rep)
                 try:
-                    reps, newly = plane.gather(rep, rounds, plan.get("alive", range(world)))
+                    if fill and rank == 0:
+                        ctrl_alive = list(plan.get("alive", range(world)))
+                        reps, newly = plane.gather(rep, rounds, ctrl_alive, fill=w.fill_step)
+                    else:
+                        reps, newly = plane.gather(rep, rounds, plan.get("alive", range(world)))
+                    if fill and rank != 0:
+                        # keep stepping this rank's job until the next plan is out
+                        tw = time.perf_counter()
+                        nxt = rounds + 1
+                        while True:
+                            ready = plane.plan_ready(nxt)
+                            if w.fill_step(ready):
+                                plane.publish_fill(rounds, w.fill_counts())
+                                continue
+                            if ready:
+                                break
+                            time.sleep(0.0003)
+                        prof["fill_s"] += time.perf_counter() - tw
                 except Exception as e:                 # gloo plane: heartbeat lost
                     if ctrl:
                         return _abort(ctrl, log, rounds, f"rank lost during round {rounds}: {e}")
@@ -1713,7 +1935,11 @@ def run_replay(cfg: SimConfig, jobs: List[ReplayJob], rank: int, world: int, dev
                  step_errors=list(ctrl.error_log),
                  comm_stats=dict(ctrl.comms.stats, live=len(ctrl.comms.live)),
                  iter_est={f"{k[0]}x{k[1]}": v for k, v in ctrl.est.items()},
-                 runtime_breakdown={k: round(v, 4) for k, v in prof.items()},
+                 runtime_breakdown={**{k: round(v, 4) for k, v in prof.items()},
+                                    "fill_s": round(w.fill_s_total - fill0[0], 4)},
+                 fill_steps_rank0=w.fill_steps_total - fill0[1],
+                 apply_breakdown_rank0={k: round(v - ap0.get(k, 0.0), 4) for k, v in w.apply_prof.items()},
+                 apply_counts_rank0={k: v - apc0.get(k, 0) for k, v in w.apply_count.items()},
                  lost_ranks=lost_ranks, recovered_jobs=sorted(ctrl.recovered),
                  restarted_jobs=sorted(ctrl.restarted), snapshot_restored_jobs=sorted(ctrl.snap_restored),
                  ddp_shard=ctrl.ddp_shard, consolidations=ctrl.consolidations,

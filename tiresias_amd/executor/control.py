@@ -199,7 +199,42 @@ class StorePlane:
 
         return pickle.loads(self._retry(_get, f"no plan for round {rnd}"))
 
-    def gather(self, rep, rnd: int, alive: Sequence[int]) -> Tuple[Optional[List], List[int]]:
+    # ----------------------------------------------------------- fill mode
+    # (cluster_runtime.Worker.fill_step): a rank that finished its round's
+    # share keeps stepping its job until the next plan is published and
+    # posts its running step count under fill/<round>/<rank>; rank 0 reads
+    # every count once, when it plans (the snapshot the plan echoes)
+    def plan_ready(self, rnd: int) -> bool:
+        return bool(self._retry(lambda: self.store.check([f"{self.prefix}/plan/{rnd}"]), f"plan {rnd} check"))
+
+    def publish_fill(self, rnd: int, counts: Dict[str, int]) -> None:
+        data = pickle.dumps(counts)
+        self._retry(lambda: self.store.set(f"{self.prefix}/fill/{rnd}/{self.rank}", data), f"fill {rnd}")
+
+    def read_fill(self, rnd: int, alive: Sequence[int]) -> Dict[int, Dict[str, int]]:
+        out: Dict[int, Dict[str, int]] = {}
+        for r in alive:
+            if r == 0 or r in self.dead:
+                continue
+            k = f"{self.prefix}/fill/{rnd}/{r}"
+            if self.store.check([k]):
+                out[r] = pickle.loads(self.store.get(k))
+        if rnd > 0:
+            # every worker has seen plan rnd (it reported round rnd): none
+            # writes fill/<rnd - 1> any more
+            for r in alive:
+                try:
+                    self.store.delete_key(f"{self.prefix}/fill/{rnd - 1}/{r}")
+                except Exception:
+                    pass
+        return out
+
+    def gather(self, rep, rnd: int, alive: Sequence[int], fill=None) -> Tuple[Optional[List], List[int]]:
+        """Rank 0: every live rank's report of round ``rnd``. ``fill(ready)``
+        (Worker.fill_step) runs between polls -- rank 0 keeps stepping its
+        own job while the slower ranks finish -- and is called with
+        ready=True once every report is in, until it returns False (a gang
+        agrees on stopping)."""
         if self.rank != 0:
             data = pickle.dumps(rep)
             self._retry(lambda: self.store.set(f"{self.prefix}/rep/{rnd}/{self.rank}", data), f"report {rnd}")
@@ -210,7 +245,11 @@ class StorePlane:
         t0 = time.monotonic()
         t_warn = t0
         sleep = 0.0002
-        while pending:
+        while True:
+            if not pending:
+                if fill is not None and fill(True):
+                    continue
+                break
             left = []
             for r in pending:
                 if r in self.dead:
@@ -223,7 +262,9 @@ class StorePlane:
                     left.append(r)
             pending = left
             if not pending:
-                break
+                continue
+            # a step of rank 0's own job instead of sleeping
+            stepped = fill is not None and fill(False)
             now = time.monotonic()
             if now - t0 > self.hb_timeout:
                 # the monitor thread normally declares first; this covers a
@@ -243,8 +284,9 @@ class StorePlane:
                 # treat as lost rather than wait forever
                 self._declare(pending)
                 self.store.set(f"{self.prefix}/dead", pickle.dumps(sorted(self.dead)))
-            time.sleep(sleep)
-            sleep = min(0.002, sleep * 1.5)
+            if not stepped:
+                time.sleep(sleep)
+                sleep = min(0.002, sleep * 1.5)
         with self._lock:
             newly = sorted(r for r in self.dead if r not in self._reported)
             self._reported |= set(newly)

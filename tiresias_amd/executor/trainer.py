@@ -66,6 +66,7 @@ class Trainer:
         self._g_loss = None
         self._g_written = []     # store_grad params the captured backward writes
         self._warm = 0           # eager steps done before graph capture
+        self.capture_s = 0.0     # host seconds spent capturing the hipGraph
         self._side = None
         self._ws = None                 # weight-gradient stream (1-GPU jobs)
         self.overlap_wgrad = self.spec.overlap_wgrad if overlap_wgrad is None else overlap_wgrad
@@ -265,6 +266,7 @@ class Trainer:
             self._side = s
             cur = torch.cuda.current_stream(self.device)
             s.wait_stream(cur)
+            tc = time.perf_counter()
             g = torch.cuda.CUDAGraph()
             with torch.cuda.stream(s):
                 g.capture_begin()
@@ -274,6 +276,7 @@ class Trainer:
                     g.capture_end()
             cur.wait_stream(s)
             self._graph = g
+            self.capture_s += time.perf_counter() - tc
             # the gradient writes baked into the graph (store-mode firsts
             # included) happen on every replay: _opt_step must see them
             A = self.arena

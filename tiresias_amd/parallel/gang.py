@@ -287,7 +287,7 @@ class GangPG:
     Work handles (``wait()`` orders the current stream after them)."""
 
     def __init__(self, ranks: Sequence[int], my_rank: int, backend: str, timeout_s: Optional[float] = None,
-                 gen: int = 0):
+                 gen: int = 0, create_timeout_s: Optional[float] = None):
         from datetime import timedelta
 
         self.ranks = tuple(ranks)
@@ -299,7 +299,8 @@ class GangPG:
         base = dist.distributed_c10d._get_default_store()
         store = dist.PrefixStore(f"tam/pg/{backend}/{gen}/{'_'.join(map(str, self.ranks))}", base)
         to = timedelta(seconds=GANG_TIMEOUT_S if timeout_s is None else timeout_s)
-        create = timedelta(seconds=max(CREATE_TIMEOUT_S, to.total_seconds()))
+        create = timedelta(seconds=create_timeout_s if create_timeout_s else
+                           max(CREATE_TIMEOUT_S, to.total_seconds()))
         if backend == "nccl":
             self.pg = dist.ProcessGroupNCCL(store, self.rank, self.size, to)
         else:
@@ -408,6 +409,49 @@ class GangPG:
         self.aborted = True
 
 
+# ranks the control plane declared lost (run_replay's on_dead hook): a
+# communicator rendezvous that includes one of them is abandoned at once
+DEAD_RANKS: set = set()
+
+
+def note_dead(r: int) -> None:
+    DEAD_RANKS.add(int(r))
+
+
+def _create_pg(ranks: Tuple[int, ...], my_rank: int, backend: str, gen: int,
+               create_s: Optional[float] = None) -> "GangPG":
+    """GangPG construction that gives up as soon as a member is declared
+    dead. A gloo rendezvous blocks (up to CREATE_TIMEOUT_S) until every
+    member connects; it runs on a helper thread while this one watches
+    DEAD_RANKS (an abandoned attempt times out on its own). ProcessGroupNCCL
+    creates its communicator lazily, at the first collective, where the
+    watcher's abort_where() reaches it. Gloo serialises rendezvous in the
+    process: an abandoned one holds up the next until it times out, so
+    callers that can meet a dying peer pass a short ``create_s``."""
+    if any(r in DEAD_RANKS for r in ranks if r != my_rank):
+        raise RuntimeError(f"communicator {ranks}: member {sorted(DEAD_RANKS & set(ranks))} is lost")
+    if backend == "nccl":
+        return GangPG(ranks, my_rank, backend, gen=gen)
+    box: Dict[str, object] = {}
+
+    def _run():
+        try:
+            box["pg"] = GangPG(ranks, my_rank, backend, gen=gen, create_timeout_s=create_s)
+        except BaseException as e:           # surfaced below
+            box["err"] = e
+
+    th = threading.Thread(target=_run, name=f"pg-create-{'_'.join(map(str, ranks))}", daemon=True)
+    th.start()
+    while th.is_alive():
+        th.join(0.05)
+        dead = DEAD_RANKS & set(r for r in ranks if r != my_rank)
+        if dead and th.is_alive():
+            raise RuntimeError(f"communicator {ranks}: member {sorted(dead)} lost during its rendezvous")
+    if "err" in box:
+        raise box["err"]
+    return box["pg"]
+
+
 class PGCache:
     """This process's member-only communicators, keyed by (rank set, backend),
     reference-counted by the gang comms built on them (a spread gang's
@@ -432,16 +476,24 @@ class PGCache:
         self.created = 0
         self.destroyed = 0
 
-    def acquire(self, ranks: Sequence[int], my_rank: int, backend: str, pin: bool = False) -> GangPG:
+    def acquire(self, ranks: Sequence[int], my_rank: int, backend: str, pin: bool = False,
+                create_s: Optional[float] = None) -> GangPG:
         key = (tuple(ranks), backend)
         with self._lock:
             e = self._e.get(key)
             if e is None:
                 gen = self._gen.get(key, 0)
                 self._gen[key] = gen + 1
-                e = [GangPG(key[0], my_rank, backend, gen=gen), 0, False]
+        if e is None:
+            # built OUTSIDE the lock: a gloo rendezvous blocks until every
+            # member connects, and the control plane's watcher must still be
+            # able to abort_where() meanwhile (only the training thread
+            # acquires, so no second creation of the key can race this one)
+            e = [_create_pg(key[0], my_rank, backend, gen, create_s), 0, False]
+            with self._lock:
                 self._e[key] = e
                 self.created += 1
+        with self._lock:
             e[1] += 1
             e[2] = e[2] or pin
             return e[0]
