@@ -433,6 +433,7 @@ class TickSimulator(Simulator):
                 placed += 1
             elif pol.blocking:
                 break
+        pol.after_schedule(self.active, self.now)
 
     def run(self, until: float = math.inf, max_events: int = 50_000_000) -> Dict:
         t0 = time.perf_counter()

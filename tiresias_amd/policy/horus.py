@@ -20,6 +20,7 @@
 """
 from __future__ import annotations
 
+import heapq
 import random
 from statistics import median
 from typing import List, Optional, Sequence
@@ -62,17 +63,59 @@ def kmeans_jobs(jobs: List[Job], k: int, rng: random.Random, max_iter: int = 100
     return cent, assign, loss
 
 
+class _RefItem:
+    """A queued job as the reference's heap sees it
+    (``core/jobs/base_factory.py:2-14`` CompareAbleByUtilization): lower
+    average utilisation first, and ``<`` is False between equal (or zero)
+    utilisations -- so heapq's sift, not arrival order, decides among ties."""
+    __slots__ = ("job",)
+
+    def __init__(self, job: Job):
+        self.job = job
+
+    def __lt__(self, other: "_RefItem") -> bool:
+        a = self.job.spec.gpu_util_avg
+        return bool(a) and a < other.job.spec.gpu_util_avg
+
+
 @register("horus")
 class Horus(Policy):
+    """Event engine: pending jobs in (utilisation, arrival) order. Under the
+    reference-compatible tick engine (``cfg.engine == "tick"``) the queue is
+    the reference's own heap operation for operation (``schedule_horus``,
+    ``algorithm.py:204-238``): every tick pops min(k, queued) jobs, the
+    engine places the first that fits, and the rest are pushed back in
+    look-ahead order -- which reorders equal-utilisation jobs exactly as the
+    reference does (pinned by tests/test_ref_parity.py's hplus_queue trace)."""
     default_placement = "horus"
 
     def __init__(self, cfg=None, prior=None, rng=None):
         super().__init__(cfg, prior, rng)
         self.lookahead = int(getattr(cfg, "lookahead", 5) or 5)
+        self.ref_heap = getattr(cfg, "engine", "event") == "tick"
+        self._heap: List[_RefItem] = []
+        self._look: List[Job] = []
+
+    def on_arrival(self, job, now):
+        super().on_arrival(job, now)
+        if self.ref_heap:
+            heapq.heappush(self._heap, _RefItem(job))
 
     def order(self, active, now):
+        if self.ref_heap:
+            n = min(self.lookahead, len(self._heap))
+            self._look = [heapq.heappop(self._heap).job for _ in range(n)]
+            return list(self._look)
         return sorted((j for j in active if j.is_pending),
                       key=lambda j: (j.spec.gpu_util_avg, submit_key(j)))
+
+    def after_schedule(self, active, now):
+        if self.ref_heap:
+            # the look-ahead jobs that did not start go back (jobs_manager.insert)
+            for j in self._look:
+                if j.is_pending:
+                    heapq.heappush(self._heap, _RefItem(j))
+            self._look = []
 
 
 @register("horus+")
@@ -83,6 +126,8 @@ class HorusPlus(Horus):
         self.rng = rng or random.Random(getattr(cfg, "seed", 0) or 0)
         self._key = None
         self._assign = {}
+        self._queues: List[List[_RefItem]] = [[] for _ in range(self.k)]
+        self._batch: List[Job] = []
 
     def credits(self, queues: List[List[Job]]) -> List[float]:
         out = []
@@ -94,7 +139,45 @@ class HorusPlus(Horus):
             out.append(len(q) if m < 1 else m * len(q))
         return out
 
+    # ---- reference-compatible tick engine: num_queue heaps; every tick's
+    # insert (gen_jobs -> jobs_manager.insert, with or without arrivals) pops
+    # ALL queued jobs (heap order, queue by queue) and re-inserts them + the
+    # batch at their k-means queue (jobs_manager.py:115-140); each
+    # of the tick's look-ahead pops takes the queue with the highest credit
+    # (schedule_horus_plus, algorithm.py:240-288); non-starters go back to
+    # their queue
+    def on_arrival(self, job, now):
+        Policy.on_arrival(self, job, now)
+        if self.ref_heap:
+            self._batch.append(job)
+
+    def _ref_insert_batch(self) -> None:
+        # every tick, even with no arrival: gen_jobs always calls insert(),
+        # which for horus+ pops and re-clusters the whole queue
+        queued = []
+        for q in self._queues:
+            while q:
+                queued.append(heapq.heappop(q).job)
+        jobs = queued + self._batch
+        self._batch = []
+        _, assign, _ = kmeans_jobs(jobs, self.k, self.rng)
+        for j, qi in zip(jobs, assign):
+            heapq.heappush(self._queues[qi], _RefItem(j))
+            j.queue = qi
+
+    def _ref_credits(self) -> List[float]:
+        return self.credits([[it.job for it in q] for q in self._queues])
+
     def order(self, active, now):
+        if self.ref_heap:
+            self._ref_insert_batch()
+            n = min(self.lookahead, sum(len(q) for q in self._queues))
+            self._look = []
+            for _ in range(n):
+                cr = self._ref_credits()
+                qi = max(range(self.k), key=lambda i: (cr[i], -i))     # np.argmax: first maximum
+                self._look.append((heapq.heappop(self._queues[qi]).job, qi))
+            return [j for j, _ in self._look]
         pend = sorted((j for j in active if j.is_pending), key=submit_key)
         key = tuple(j.job_id for j in pend)
         if key != self._key:
@@ -112,6 +195,13 @@ class HorusPlus(Horus):
             qi = max(range(self.k), key=lambda i: (cr[i], -i))
             out.append(queues[qi].pop(0))
         return out
+
+    def after_schedule(self, active, now):
+        if self.ref_heap:
+            for j, qi in self._look:
+                if j.is_pending:
+                    heapq.heappush(self._queues[qi], _RefItem(j))
+            self._look = []
 
 
 @register("gandiva")

@@ -66,7 +66,7 @@ TRACES = {
     # 50 %-utilisation jobs per GPU, so whole-node (4-GPU) jobs queue behind
     # the anchor + one running job. Horus policies only: under FIFO this trace
     # would trigger D8 (arrivals while jobs wait).
-    "hplus_queue": dict(gpus_per_node=4, nodes=1, pairs=[("horus+", "horus+"), ("horus", "horus")], jobs=[
+    "hplus_queue": dict(gpus_per_node=4, nodes=1, pairs=[("horus+", "horus+"), ("horus", "horus")], d2fix=True, jobs=[
         ("0", 0, 1, 1, 90.0),      # anchor (45 ticks)
         ("1", 1, 4, 4, 10.0),      # 1-3 share the node (packing)
         ("2", 2, 4, 4, 8.0),
@@ -86,8 +86,31 @@ PAIRS = [("fifo", "yarn"), ("horus", "horus"), ("gandiva", "gandiva"), ("horus+"
 SEEDED = "import random, runpy, sys, numpy; numpy.random.seed(0); random.seed(0); " \
          "sys.argv = ['run_sim.py'] + sys.argv[1:]; runpy.run_path('run_sim.py', run_name='__main__')"
 
+# SEEDED with the reservation leak (infra/node.py:212-233) removed
+# at run time: a task that does not fit on every device it needs leaves no
+# device entry or cpu / mem reservation behind. The reference's files are
+# not touched; the patch is applied in the launching interpreter.
+D2FIX = "import infra.node as N\n" \
+        "def _atomic(self, task, pack=False, _orig=N.Node.try_reserve_and_placed_task):\n" \
+        "    before = {d: dict(dev.running_tasks) for d, dev in self.device_cache.items()}\n" \
+        "    cpu, mem = self.cpu_used, self.mem_used\n" \
+        "    ok = _orig(self, task, pack=pack)\n" \
+        "    if not ok:\n" \
+        "        for d, dev in self.device_cache.items():\n" \
+        "            dev.running_tasks.clear(); dev.running_tasks.update(before[d])\n" \
+        "        self.cpu_used, self.mem_used = cpu, mem\n" \
+        "    return ok\n" \
+        "N.Node.try_reserve_and_placed_task = _atomic\n"
+SEEDED_D2FIX = "import random, runpy, sys, numpy; numpy.random.seed(0); random.seed(0); " \
+               "sys.argv = ['run_sim.py'] + sys.argv[1:]; sys.path.insert(0, '.'); exec(%r); " \
+               "runpy.run_path('run_sim.py', run_name='__main__')" % D2FIX
+
 _DELTA = re.compile(r"delta-time: (\d+)")
 _PLACE = re.compile(r"placing task (\S+?)_worker\d+ at node (\S+) - device (\d+)")
+# horus / gandiva placement logs trial reservations (placing ... lines, also
+# for trials that fail) before its commit, "placed task J_workerK at node N"
+# (core/scheduling/algorithm.py:170): a job starts at its commit tick
+_COMMIT = re.compile(r"\{algorithm:\d+\} INFO: placed task (\S+?)_worker\d+ at node (\S+)$")
 _FINISH = re.compile(r"\{schedule:\d+\} INFO: job (\S+) finish")
 
 
@@ -100,7 +123,10 @@ def write_trace(path: str, jobs) -> None:
 
 
 def parse_log(text: str):
-    """Per job: start tick, end tick, sorted [node, device] pairs."""
+    """Per job: start tick (the placement commit; the first reservation for
+    yarn, which logs no trials), end tick, sorted [node, device] pairs of
+    its reservations, and ``trial_ticks``: ticks with reservation lines but
+    no commit (failed horus trials -- where the D2 leak happens)."""
     tick = 0
     out = {}
     for line in text.splitlines():
@@ -110,8 +136,16 @@ def parse_log(text: str):
             continue
         m = _PLACE.search(line)
         if m:
-            r = out.setdefault(m.group(1), {"start": tick, "end": None, "devices": []})
+            r = out.setdefault(m.group(1), {"start": None, "end": None, "devices": [], "resv": []})
             r["devices"].append([m.group(2), int(m.group(3))])
+            r["resv"].append(tick)
+            continue
+        m = _COMMIT.search(line)
+        if m:
+            r = out[m.group(1)]
+            if r["start"] is None or r.get("commit") is None:
+                r["start"] = tick
+            r["commit"] = tick
             continue
         m = _FINISH.search(line)
         if m:
@@ -119,12 +153,19 @@ def parse_log(text: str):
             out[m.group(1)]["end"] = tick + 1
     for r in out.values():
         r["devices"].sort()
+        if r["start"] is None:                 # yarn: reservations are the placement
+            r["start"] = r["resv"][0]
+        trials = sorted(set(t for t in r.pop("resv") if t != r.get("commit", r["start"])))
+        r.pop("commit", None)
+        if trials:
+            r["trial_ticks"] = trials
     return out
 
 
-def run_reference(ref: str, work: str, name: str, spec: dict, schedule: str, scheme: str) -> dict:
+def run_reference(ref: str, work: str, name: str, spec: dict, schedule: str, scheme: str,
+                  d2fix: bool = False) -> dict:
     write_trace(os.path.join(work, f"{name}.csv"), spec["jobs"])
-    cmd = [sys.executable, "-c", SEEDED, "--scheme", scheme, "--schedule", schedule,
+    cmd = [sys.executable, "-c", SEEDED_D2FIX if d2fix else SEEDED, "--scheme", scheme, "--schedule", schedule,
            "--trace_file", f"../{name}.csv", "--num_switch", "1",
            "--num_node_p_switch", str(spec["nodes"]), "--num_gpu_p_node", str(spec["gpus_per_node"]),
            "--log_path", f"{name}_{schedule}"]
@@ -160,6 +201,10 @@ def main() -> None:
                                                                              schedule, scheme)
                 except RuntimeError as e:
                     print(f"skip {name} {schedule}/{scheme}: {e}", file=sys.stderr)
+                if spec.get("d2fix"):
+                    # the same reference with only D2 removed (attribution run)
+                    entry.setdefault("results_d2fix", {})[f"{schedule}/{scheme}"] = run_reference(
+                        ref, work, name, spec, schedule, scheme, d2fix=True)
             fixture["traces"][name] = entry
         os.makedirs(os.path.dirname(os.path.abspath(a.out)), exist_ok=True)
         with open(a.out, "w") as f:
