@@ -29,6 +29,7 @@ struct Job {
   int ntask = 1, tgpu = 1, tcpu = 0, tmem = 0;
   bool sens = false;
   std::vector<int> plan;
+  std::vector<int> held;               // lazy preemption: plan of a tentatively released victim
   double progress = 0, executed = 0, total_exec = 0, pending = 0, last_pending = 0;
   int q = 0;
   long seq = 0;
@@ -205,6 +206,8 @@ class Engine {
   // whenever no consolidated block is free), true = wait-vs-spread
   // (engine/spread.py; needs set_costs' per-job spread parameters)
   void set_spread_wait(bool on) { spread_wait_ = on; }
+  // preemptive policies on topology placements: lazy (default) or eager
+  void set_lazy_preempt(bool on) { lazy_ = on; }
   long spread_decisions(bool spread) const { return spread ? n_spread_ : n_wait_; }
 
   // Topology placement (yarn / tiresias) on switches x nodes x gpus with
@@ -836,6 +839,10 @@ class Engine {
       std::vector<char> chosen(jobs_.size(), 0);
       long used = 0;
       for (long k : ord) if (used + jobs_[k].gpu <= total_) { chosen[k] = 1; used += jobs_[k].gpu; }
+      if (lazy_ && (place_ == P_YARN || place_ == P_TIRESIAS)) {   // "count" stays eager (Python: the same)
+        schedule_lazy(ord, chosen);
+        return;
+      }
       for (long k : active_) if (jobs_[k].state == RUN && !chosen[k]) preempt(jobs_[k]);
       for (long k : ord) if (chosen[k] && jobs_[k].state == PEND) try_place(jobs_[k]);
       // work-conserving back-fill (chosen jobs that failed placement are not retried)
@@ -849,7 +856,57 @@ class Engine {
     }
   }
 
+  // engine/sim.py::Simulator._schedule_lazy (topology placements): victims
+  // released tentatively, chosen jobs placed, then the back-fill in priority
+  // order re-commits a victim whose devices are all still free in place and
+  // preempts the others (which may then be placed elsewhere, as any pending job)
+  bool plan_free(const Job& j, const std::vector<int>& plan) const {
+    std::vector<int> cpu = topo_.cpu_used, mem = topo_.mem_used;
+    size_t p = 0;
+    for (int t = 0; t < j.ntask; ++t) {
+      const int nd = plan[p++];
+      cpu[nd] += j.tcpu; mem[nd] += j.tmem;
+      if (cpu[nd] > topo_.cpu_cap[nd] || mem[nd] > topo_.mem_cap[nd]) return false;
+      for (int g = 0; g < j.tgpu; ++g) if (topo_.busy[nd][plan[p++]]) return false;
+    }
+    return true;
+  }
+  void schedule_lazy(const std::vector<long>& ord, const std::vector<char>& chosen) {
+    std::vector<long> victims;
+    for (long k : ord) if (jobs_[k].state == RUN && !chosen[k]) victims.push_back(k);
+    for (long k : victims) {
+      Job& v = jobs_[k];
+      v.held = v.plan;
+      release(v);                                  // topology free, still RUN
+      used_ -= v.gpu;
+    }
+    for (long k : ord) if (chosen[k] && jobs_[k].state == PEND) try_place(jobs_[k]);
+    for (long k : ord) {
+      Job& j = jobs_[k];
+      if (!j.held.empty()) {
+        std::vector<int> h;
+        h.swap(j.held);
+        if (plan_free(j, h)) {                     // nothing took its GPUs: it never stopped
+          commit(j, h);
+          used_ += j.gpu;
+          continue;
+        }
+        j.plan = h;                                // preempt on the allocation it ran on
+        if (priced()) {
+          const double save = ckpt_preempt(j);
+          j.restore_left = 0;
+          j.pending_ckpt += save;
+          j.overhead += save;
+        }
+        j.state = PEND; j.preempt++; j.last_check = now_;
+        j.plan.clear();                            // (topology and ledger already released)
+      }
+      if (j.state == PEND && !chosen[k] && j.gpu > 0 && j.gpu <= total_ - used_) try_place(j);
+    }
+  }
+
   Pol pol_;
+  bool lazy_ = true;
   Place place_ = P_COUNT;
   Costs costs_;
   bool spread_wait_ = false, svc_online_ = true;

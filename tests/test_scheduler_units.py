@@ -392,3 +392,27 @@ def test_gittins_prior_from_history_file(tmp_path):
     sim = Simulator(_one_gpu("dlas-gpu-gittins", gittins_prior=str(p)), [spec(0, d=5.0)])
     sim.run()
     assert sim.prior_source == "file" and len(sim.policy.gittins.data) == 20
+
+
+def test_lazy_preemption_skips_no_op_suspensions():
+    """2 nodes x 4 GPUs, 2D-LAS + yarn: when B (4 GPUs, queue 0) arrives, the
+    count prefix chooses it over the demoted V (3 GPUs), but no single node
+    can take B even with V's GPUs free. The eager rule suspends V anyway and
+    backfills it straight back (a no-op preemption that a priced or live run
+    pays for); the lazy rule (default) leaves V running. Same schedule."""
+    from tiresias_amd.config import ClusterSpec, SimConfig
+    from tiresias_amd.core.job import JobSpec
+    from tiresias_amd.engine.sim import Simulator
+
+    def run(rule):
+        specs = [JobSpec("F", 0.0, 1000.0, 1), JobSpec("V", 0.1, 1000.0, 3),
+                 JobSpec("A", 50.0, 500.0, 3), JobSpec("B", 60.0, 100.0, 4)]
+        cfg = SimConfig(schedule="dlas-gpu", scheme="yarn", num_queue=2, queue_limits=[60.0], preempt_rule=rule,
+                        cluster=ClusterSpec(num_switch=1, num_node_p_switch=2, num_gpu_p_node=4))
+        sim = Simulator(cfg, specs, check_invariants=True)
+        sim.run()
+        return {j.job_id: (j.start_time, j.end_time, j.preempt_count) for j in sim.jobs.values()}
+
+    eager, lazy = run("eager"), run("lazy")
+    assert eager["V"][2] == 1 and lazy["V"][2] == 0
+    assert {k: v[:2] for k, v in eager.items()} == {k: v[:2] for k, v in lazy.items()}

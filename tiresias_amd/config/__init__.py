@@ -89,6 +89,8 @@ def define_flags() -> None:
     D.DEFINE_string("spread_rule", "wait", "tiresias placement, insensitive gangs: fragments (spread "
                     "whenever no consolidated block is free) | wait (spread only when the expected wait "
                     "for a block exceeds the spread penalty, engine/spread.py)")
+    D.DEFINE_string("preempt_rule", "lazy", "preemptive policies: lazy (preempt only what a chosen job's "
+                    "placement needs) | eager (every running job outside the priority prefix)")
     D.DEFINE_boolean("ddp_shard", False, "live gangs: reduce-scatter + sharded optimizer + bf16 all-gather "
                      "(consolidated on suspension)")
     D.DEFINE_string("ddp_wire", "fp32", "sharded gangs: reduce-scatter wire dtype fp32 | bf16")
@@ -178,6 +180,7 @@ class SimConfig:
     replace_all: bool = False
     skew_threshold: float = 0.5
     spread_rule: str = "wait"          # tiresias placement: wait | fragments (engine/spread.py)
+    preempt_rule: str = "lazy"         # preemptive policies: lazy | eager (engine/sim.py::_schedule_lazy)
     ddp_shard: bool = False            # live gangs: sharded data parallelism (parallel/ddp.py)
     ddp_wire: str = "fp32"             # sharded gangs: reduce-scatter dtype fp32 | bf16
     virtual_nodes: str = ""

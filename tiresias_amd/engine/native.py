@@ -63,6 +63,7 @@ def simulate_native(cfg: SimConfig, specs: List[JobSpec], prior: Optional[List[f
     wait_rule = scheme == "tiresias" and getattr(cfg, "spread_rule", "wait") == "wait"
     priced = _set_costs(eng, cfg, specs, force=wait_rule)
     eng.set_spread_wait(wait_rule)
+    eng.set_lazy_preempt(getattr(cfg, "preempt_rule", "lazy") == "lazy")
     t0 = time.perf_counter()
     sub_a = np.array([s.submit_time for s in specs], dtype=np.float64)
     dur_a = np.array([s.duration for s in specs], dtype=np.float64)

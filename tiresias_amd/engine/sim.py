@@ -103,6 +103,11 @@ class Simulator:
         self.active: List[Job] = []
         self.finished: List[Job] = []
         self.check = check_invariants
+        # preemption rule of preemptive policies: "lazy" (only what a chosen
+        # job's placement needs, _schedule_lazy) or "eager" (every running job
+        # outside the priority prefix, then backfill)
+        # (topology placements; "count" keeps the eager rule: no fragmentation)
+        self.lazy_preempt = getattr(cfg, "preempt_rule", "lazy") == "lazy" and self.scheme != "count"
         self.events = 0
         self._stall = 0
         self.wall_s = 0.0
@@ -265,6 +270,10 @@ class Simulator:
                     if id(j) not in cset and j.num_gpu == 1:
                         extra.append(j)
             keep = cset | set(id(j) for j in extra)
+            if self.lazy_preempt and not self.cluster.pack and not self.cfg.replace_all:
+                self._schedule_lazy(ordered, chosen, keep)
+                pol.after_schedule(self.active, self.now)
+                return
             for j in list(self.active):
                 if j.is_running and id(j) not in keep:
                     self._preempt(j)
@@ -299,6 +308,46 @@ class Simulator:
                 if not self._try_place(j) and pol.blocking:
                     break
         pol.after_schedule(self.active, self.now)
+
+    def _schedule_lazy(self, ordered: List[Job], chosen: List[Job], keep: set) -> None:
+        """Preempt only what a chosen job's placement actually needs.
+
+        The priority prefix (``chosen``) is computed by GPU count, but a
+        topology placement can still fail for a chosen job (no consolidated
+        block, or the wait-vs-spread rule prefers waiting). Preempting every
+        lower-priority running job up front then suspends jobs whose GPUs
+        nobody takes -- they are backfilled right back (measured on the
+        priced 2000-job Philly trace, 64 GPUs: 79 % of tiresias' and 67 % of
+        yarn's Gittins preemptions restarted at the same instant, each paying
+        a checkpoint stall, and often on other GPUs). Here the victims
+        (running, not chosen) are released TENTATIVELY -- the chosen jobs are
+        placed with every victim's GPUs available, as in the eager rule --
+        and the back-fill then walks the priority order as the eager rule's
+        does, except that a victim whose devices are all still free is
+        re-committed in place (it never stopped) instead of being preempted
+        and restarted; only the others are preempted."""
+        victims = [j for j in ordered if j.is_running and id(j) not in keep]
+        held: Dict[str, list] = {}
+        for v in victims:
+            held[v.job_id] = self.cluster.placed[v.job_id]
+            self.cluster.release(v)
+        for j in chosen:
+            if j.is_pending:
+                self._try_place(j)
+        # work-conserving back-fill in priority order, as the eager rule's:
+        # a victim whose devices are all still free is re-committed there (it
+        # never stopped); one that cannot be is preempted now and, like any
+        # pending job, placed wherever it fits (a migration)
+        cset = set(id(j) for j in chosen)
+        for j in ordered:
+            plan = held.pop(j.job_id, None)
+            if plan is not None:
+                if self.cluster.validate(j, plan) is None:
+                    self.cluster.commit(j, plan)
+                    continue
+                self._preempt(j)
+            if j.is_pending and id(j) not in cset and 0 < j.num_gpu <= self.cluster.free_gpus():
+                self._try_place(j)
 
     def _migrate(self) -> None:
         """Move a task off an overloaded device when idle devices exist

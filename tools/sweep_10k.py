@@ -34,12 +34,12 @@ POLICIES = [("fifo", "yarn"), ("shortest", "yarn"), ("shortest-gpu", "yarn"), ("
             ("dlas-gpu-gittins", "tiresias")]
 
 
-def _cfg(schedule, scheme, prior_path, seed, ckpt="none", net=False):
+def _cfg(schedule, scheme, prior_path, seed, ckpt="none", net=False, preempt_rule="lazy"):
     from tiresias_amd.config import ClusterSpec, SimConfig
 
     return SimConfig(schedule=schedule, scheme=scheme, num_queue=2, queue_limits=[3600.0],
                      gittins_delta=3250.0, gittins_prior=prior_path, seed=seed,
-                     ckpt_policy=ckpt, enable_network_costs=net,
+                     ckpt_policy=ckpt, enable_network_costs=net, preempt_rule=preempt_rule,
                      ckpt_table=os.path.join(ROOT, "profiles", "ckpt_mi355x.json"),
                      cluster=ClusterSpec(num_switch=1, num_node_p_switch=8, num_gpu_p_node=8))
 
@@ -51,9 +51,9 @@ def _trace(n, load, seed):
 
 
 def _run(args):
-    engine, schedule, scheme, n, load, seed, prior_path, ckpt, net = args
+    engine, schedule, scheme, n, load, seed, prior_path, ckpt, net, rule = args
     specs = _trace(n, load, seed)
-    cfg = _cfg(schedule, scheme, prior_path, seed, ckpt, net)
+    cfg = _cfg(schedule, scheme, prior_path, seed, ckpt, net, rule)
     t = time.perf_counter()
     if engine == "native":
         from tiresias_amd.engine.native import simulate_native
@@ -83,6 +83,7 @@ def main():
     ap.add_argument("--native-only", action="store_true", help="skip the (slow) Python event engine rows")
     ap.add_argument("--ckpt_policy", default="none",
                     help="preemption cost: none | host | hbm | measured (profiles/ckpt_mi355x.json) | pressure")
+    ap.add_argument("--preempt_rule", default="lazy", help="lazy | eager (engine/sim.py::_schedule_lazy)")
     ap.add_argument("--enable_network_costs", action="store_true",
                     help="spread gangs progress at the network-limited rate (cluster/network.py)")
     a = ap.parse_args()
@@ -98,14 +99,14 @@ def main():
     runs = []
     for sch, sc in POLICIES:
         runs.append(("native", sch, sc, a.jobs, a.load, a.seed, prior_path, a.ckpt_policy,
-                     a.enable_network_costs))
+                     a.enable_network_costs, a.preempt_rule))
     for sch in ("fifo", "shortest", "shortest-gpu", "dlas-gpu", "gittins", "dlas-gpu-gittins"):
         runs.append(("native", sch, "count", a.jobs, a.load, a.seed, prior_path, a.ckpt_policy,
-                     a.enable_network_costs))
+                     a.enable_network_costs, a.preempt_rule))
     if not a.native_only:
         for sch, sc in POLICIES:
             runs.append(("event", sch, sc, a.jobs, a.load, a.seed, prior_path, a.ckpt_policy,
-                         a.enable_network_costs))
+                         a.enable_network_costs, a.preempt_rule))
     res = []
     with cf.ProcessPoolExecutor(max_workers=a.workers) as ex:
         for r in ex.map(_run, runs):
@@ -129,7 +130,8 @@ def main():
                                                        if a.ckpt_policy == "measured" else "")
               + ("; spread gangs at the network-limited rate (analytic ring all-reduce over the "
                  "reference's 1250 MB/s, 0.015 s links)" if a.enable_network_costs else "; network free"))
-    lines = [f"# {a.jobs}-job Philly-shaped trace, 64 GPUs (8x8), load {a.load}, seed {a.seed}",
+    lines = [f"# {a.jobs}-job Philly-shaped trace, 64 GPUs (8x8), load {a.load}, seed {a.seed}, "
+             f"preemption rule {a.preempt_rule}",
              "", "Gittins prior: held-out history trace (seed + 7919), GPU-seconds; 2D-LAS threshold 3600 "
              "GPU-s; Gittins quantum 3250 GPU-s.", "", priced + ".", "",
              "vs FIFO: against FIFO + yarn of the same engine (count rows: FIFO + count). match: the "
