@@ -236,7 +236,9 @@ def main():
     ap.add_argument("--skew-profile", default="",
                     help="measured consolidated-vs-spread slowdowns (python -m tiresias_amd.profiler.comm)")
     ap.add_argument("--load", type=float, default=1.6, help="offered load / capacity during arrivals")
-    ap.add_argument("--quantum", type=float, default=0.02, help="scheduling round, seconds")
+    ap.add_argument("--quantum", type=float, default=0.01,
+                    help="scheduling round, seconds (0.01: N=1 avg JCT 0.1576 vs 0.1606 s at 0.02 on one "
+                         "box, profiles/r5/quantum_ab.md; N>1 rounds end early anyway in fill mode)")
     ap.add_argument("--seed", type=int, default=2019)
     ap.add_argument("--budget-s", type=float, default=float(os.environ.get("TAM_BENCH_BUDGET_S", 270)),
                     help="wall budget from process start; steps that would not fit are skipped")

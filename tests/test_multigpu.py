@@ -196,6 +196,42 @@ def test_shared_gpu_sharded_ddp_matches(gpu, wire):
         assert res[r]["ratio"] < (0.6 if wire == "bf16" else 0.85), res
 
 
+def _shared_ipc_move(rank, world, port, q):
+    from tiresias_amd.executor.cluster_runtime import Worker
+    from tiresias_amd.executor.control import StorePlane
+
+    os.environ["TAM_SHARED_GPU"] = "1"
+    _init(rank, world, port, "gloo")
+    torch.cuda.set_device(0)
+    dev = torch.device("cuda", 0)
+    w = Worker(rank, world, dev, dist.group.WORLD, gang_backend="gloo", monitor_period=0)
+    w.plane = StorePlane(rank, world, hb_period=0.5, hb_timeout=10.0)
+    g = torch.Generator(device=dev).manual_seed(5)
+    state = {"master": torch.randn(1 << 20, device=dev, generator=g),
+             "opt0": torch.randn(3 << 18, device=dev, generator=g)}
+    bufs = {k: (v.clone() if rank == 0 else torch.zeros_like(v)) for k, v in state.items()}
+    act = {"op": "start", "job": "J", "ranks": (1,), "old": (0,), "donors": {1: 0}}
+    ops = [("send" if rank == 0 else "recv", b, 1 - rank, k) for k, b in sorted(bufs.items())]
+    t0 = time.perf_counter()
+    ok = w._do_moves_ipc({"J": (ops, act)}, 0)
+    dt = time.perf_counter() - t0
+    torch.cuda.synchronize()
+    q.put((rank, {"ok": ok["J"], "s": dt, "same": all(torch.equal(bufs[k], state[k]) for k in state)}))
+    dist.barrier()
+    w.plane.close()
+    dist.destroy_process_group()
+
+
+def test_shared_gpu_ipc_state_move(gpu):
+    """One-GPU multi-rank rehearsal: a job's state moves between two ranks
+    on cuda:0 device to device through HIP IPC handles published in the
+    control store (no gloo host staging): bitwise equal on the receiver."""
+    codes, res = _run(_shared_ipc_move, 2)
+    assert codes == [0, 0], codes
+    assert res[0]["ok"] and res[1]["ok"], res
+    assert res[1]["same"], res
+
+
 # ------------------------------------------------------------------ >= 2 GPUs, RCCL
 def _ndev():
     try:
@@ -245,13 +281,21 @@ def _rccl_multi(rank, world, port, q):
         g.warm(dev)
         if rank == 0:
             t = torch.ones(1 << 16, device=dev)
-            w = g.all_reduce(t)
+            g.all_reduce(t)
             time.sleep(2.0)
             g.abort()
             out["abort_failed"] = g.failed()
         else:
             time.sleep(4.0)
-            out["abort_failed"] = True
+            g.abort()                 # the plan's abort action reaches the peer too
+        # the survivor is usable: both members build a FRESH communicator
+        # (next generation, fresh store keys) and all-reduce through it
+        g2 = G.GangPG((0, 1), rank, "nccl", timeout_s=30.0, gen=10)
+        t2 = torch.full((1 << 12,), float(rank + 1), device=dev)
+        g2.all_reduce(t2).wait()
+        torch.cuda.synchronize()
+        out["rebuilt_sum"] = float(t2[0])
+        out["rebuilt_failed"] = g2.failed()
     q.put((rank, out))
     os._exit(0)
 
@@ -267,6 +311,8 @@ def test_rccl_multi_gangs(gpu):
         if "hier_vs_flat" in res[r]:
             assert res[r]["hier_vs_flat"] < 1e-3, res[r]
     assert res[1]["p2p_bitwise"] and res[0]["abort_failed"]
+    for r in (0, 1):
+        assert res[r]["rebuilt_sum"] == 3.0 and not res[r]["rebuilt_failed"], res[r]
 
 
 def _rccl_shard(rank, world, port, q):
@@ -282,7 +328,6 @@ def _rccl_shard(rank, world, port, q):
                  ddp_shard=True, ddp_wire="bf16")
     for _ in range(3):
         ref.step()
-        ref.ddp.finish() if False else None
         sh.step()
     sh.consolidate()
     torch.cuda.synchronize()

@@ -757,6 +757,11 @@ class Worker:
         self._fill: Optional[dict] = None
         self._carry: List[dict] = []
         self.fill_enabled = os.environ.get("TAM_FILL", "1") != "0"
+        # every rank on ONE physical GPU (the one-GPU multi-rank rehearsal):
+        # state moves go device to device through HIP IPC (_do_moves_ipc)
+        self.shared_device = (device.type == "cuda" and self.gang_backend == "gloo"
+                              and os.environ.get("TAM_SHARED_GPU") == "1"
+                              and os.environ.get("TAM_IPC_MOVES", "1") != "0")
         self.fill_s_total = 0.0
         self.fill_steps_total = 0
         # host seconds of plan application per action kind (start_fresh_build /
@@ -1151,14 +1156,14 @@ class Worker:
                     elif t is not None and getattr(t, "_spilled", None):
                         self._restore(a["job"])
                     ops = moves.setdefault(a["job"], ([], a))[0]
-                    for _, buf in sorted(t.state_tensors().items()):
-                        ops.append(("recv", buf, donors[self.rank]))
+                    for name, buf in sorted(t.state_tensors().items()):
+                        ops.append(("recv", buf, donors[self.rank], name))
                 for recv, donor in donors.items():
                     if donor == self.rank:
                         t = self.trainers[a["job"]]
                         ops = moves.setdefault(a["job"], ([], a))[0]
-                        for _, buf in sorted(t.state_tensors().items()):
-                            ops.append(("send", buf, recv))
+                        for name, buf in sorted(t.state_tensors().items()):
+                            ops.append(("send", buf, recv, name))
                 # replicas that stay: rebind their DDP bucketer to the new gang
                 if self.rank in ranks and self.rank in old:
                     t = self.trainers[a["job"]]
@@ -1176,7 +1181,10 @@ class Worker:
             ta = self._ap("reclaim", ta)
         failed = set()
         if moves or snap_loads:
-            ok = self._do_moves(moves) if moves else {}
+            if moves and self.shared_device and self.plane is not None:
+                ok = self._do_moves_ipc(moves, plan.get("round"))
+            else:
+                ok = self._do_moves(moves) if moves else {}
             ta = self._ap("p2p_transfer", ta)
             ok.update({jid: v for jid, (v, _) in snap_loads.items()})
             acts = {jid: a for jid, (_, a) in moves.items()}
@@ -1263,7 +1271,7 @@ class Worker:
         for jid, (ops, _) in moves.items():
             pgs, works, staged = [], [], []
             try:
-                for kind, buf, peer in ops:
+                for kind, buf, peer, _ in ops:
                     pg = self._pair_pg(peer)
                     pgs.append(pg)
                     t = buf
@@ -1290,6 +1298,61 @@ class Worker:
             if any(pg.failed() for pg in pgs):
                 ok[jid] = False
         self._move_pgs = used
+        return ok
+
+    def _do_moves_ipc(self, moves, rnd) -> Dict[str, bool]:
+        """State moves when every rank drives the SAME physical GPU (the
+        one-GPU multi-rank rehearsal, ``TAM_SHARED_GPU=1``: gloo
+        communicators would stage every byte through host memory and TCP --
+        0.5 s per move measured). The donor exports each state buffer as a
+        HIP IPC handle through the control store; the receiver maps it and
+        copies device to device, then acknowledges, and only then may the
+        donor free its replica. Jobs in plan order on every rank."""
+        import pickle
+
+        from torch.multiprocessing.reductions import reduce_tensor
+
+        plane = self.plane
+        rt = plane._retry
+        pre = f"{plane.prefix}/ipc/{rnd}"
+        bound = max(30.0, 4.0 * plane.hb_timeout)
+
+        def wait_key(k, peer, what):
+            t0 = time.time()
+            while not rt(lambda: plane.store.check([k]), what):
+                if peer in plane.dead or time.time() - t0 > bound:
+                    raise RuntimeError(f"{what}: rank {peer} silent")
+                time.sleep(0.0005)
+
+        ok: Dict[str, bool] = {}
+        for jid, (ops, _) in moves.items():
+            try:
+                sends = [(buf, peer, name) for kind, buf, peer, name in ops if kind == "send"]
+                if sends:
+                    torch.cuda.current_stream(self.device).synchronize()   # donor state final
+                    for buf, peer, name in sends:
+                        data = pickle.dumps(reduce_tensor(buf))
+                        rt(lambda k=f"{pre}/{jid}/{self.rank}-{peer}/{name}", d=data: plane.store.set(k, d),
+                           "ipc handle")
+                recvs = [(buf, peer, name) for kind, buf, peer, name in ops if kind == "recv"]
+                for buf, peer, name in recvs:
+                    k = f"{pre}/{jid}/{peer}-{self.rank}/{name}"
+                    wait_key(k, peer, f"ipc move of {jid}")
+                    fn, args = pickle.loads(rt(lambda: plane.store.get(k), "ipc handle"))
+                    src = fn(*args)
+                    buf.copy_(src)
+                    del src
+                if recvs:
+                    torch.cuda.current_stream(self.device).synchronize()
+                    rt(lambda: plane.store.set(f"{pre}/{jid}/ack/{self.rank}", b"1"), "ipc ack")
+                for peer in sorted({p for _, p, _ in sends}):
+                    wait_key(f"{pre}/{jid}/ack/{peer}", peer, f"ipc ack of {jid}")
+                ok[jid] = True
+            except Exception as e:
+                print(f"[worker {self.rank}] ipc move of job {jid} failed ({type(e).__name__}: {e})",
+                      file=sys.stderr, flush=True)
+                ok[jid] = False
+        self._move_pgs = {}
         return ok
 
     def _agree_moves(self, rnd, ok: Dict[str, bool], acts: Dict[str, dict]) -> set:
