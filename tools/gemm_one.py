@@ -12,6 +12,7 @@ def main():
     M, N, K = (int(x) for x in sys.argv[1:4])
     lay = sys.argv[4]
     iters = int(sys.argv[5]) if len(sys.argv) > 5 else 20
+    tile = int(sys.argv[6]) if len(sys.argv) > 6 else 256
     ak, bk = lay[0] == "K", lay[1] == "K"
     T = _lib.ops()
     dev = torch.device("cuda", 0)
@@ -20,7 +21,7 @@ def main():
     a_ = A if ak else A.t().contiguous()
     b_ = B.t().contiguous() if bk else B
     c = torch.empty(M, N, device=dev, dtype=torch.bfloat16)
-    T.gemm8p_policy(2, 256)          # force the 256^2 p8 kernel, no split
+    T.gemm8p_policy(2, tile)         # force the 256^2 (or 128^2) p8 kernel, no split
     for _ in range(iters):
         T.gemm(a_, ak, b_, bk, c, 0, None, False, None, 1.0, False)
     torch.cuda.synchronize()
