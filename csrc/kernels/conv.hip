@@ -70,6 +70,17 @@ long conv_dgrad_split_ws(const ConvGeom& g) {
   return conv_dma_split_ws(a, force);
 }
 
+// 1: a shallow (Kd 64 / 128) pointwise conv whose BatchNorm statistics are
+// requested runs on the LDS-DMA core anyway (its epilogue accumulates the
+// statistics; the igemm fallback needs a separate bn_stats pass over the
+// output). 0: the cost model alone decides (A/B, TAM_CONV_STATS_FORCE)
+static int g_conv_stats_force = [] {
+  const char* e = getenv("TAM_CONV_STATS_FORCE");
+  return e ? atoi(e) : 0;
+}();
+TAM_KNOB(g_conv_stats_force)
+void conv_stats_force(int p) { g_conv_stats_force = p; }
+
 int conv_fwd(const bf16_t* x, const bf16_t* w, const ConvGeom& g, Epi ep, hipStream_t s, float* ws,
              long ws_floats) {
   const int M = g.N * g.P * g.Q, Kd = g.R * g.S * g.C;
@@ -77,7 +88,9 @@ int conv_fwd(const bf16_t* x, const bf16_t* w, const ConvGeom& g, Epi ep, hipStr
   if (g_conv_dma && g.dil == 1) {
     CDArgs a = cd_fwd_args(x, w, g);
     if (g_conv_halo && launch_conv_halo(a, ep, s)) return ep.stats ? 1 : 0;
-    const int bm = launch_conv_dma(a, ep, s, g_conv_dma >= 2 ? g_conv_dma - 1 : 0, ws, ws_floats);
+    int force = g_conv_dma >= 2 ? g_conv_dma - 1 : 0;
+    if (!force && g_conv_stats_force && ep.stats && is_pointwise(g) && Kd < 256 && Kd % 64 == 0) force = 1;
+    const int bm = launch_conv_dma(a, ep, s, force, ws, ws_floats);
     if (bm) return ep.stats ? 1 : 0;
   }
   ep.stats = nullptr;

@@ -36,6 +36,8 @@ struct P8GProb {
   int t0;            // first GEMM tile (relative to the GEMM part of the grid)
   int c0;            // first column-sum block
   int mode;          // 0: C = A^T B (a weight's first gradient write of the step), 1: C +=
+  int ntiles;        // output tiles
+  int kps;           // K-tiles per slice; slices = (tiles owned) / ntiles
 };
 
 struct P8Group {
@@ -105,13 +107,19 @@ __global__ void __launch_bounds__(64 * 2 * WNW, (BM == 256 ? 1 : 2)) gemm8p_grou
   int c = 0;
   while (c + 1 < g.n && t >= g.p[c + 1].t0) ++c;
   const P8GProb& pr = g.p[c];
-  P8Args a{pr.A, (long)pr.M, pr.B, (long)pr.N, pr.M, pr.N, pr.K, pr.K / P8_BK, 4};
+  // a long-K problem is split over K: slice-major unit order, so the
+  // consecutive blocks of one XCD (xcd_remap) are tiles of ONE K-slice and
+  // share its A / B panels in L2; the slices meet in fp32 atomics (mode 2)
+  const int u = t - pr.t0;
+  const int tile = u % pr.ntiles, kz = u / pr.ntiles;
+  const bool split = pr.kps < pr.K / P8_BK;
+  P8Args a{pr.A, (long)pr.M, pr.B, (long)pr.N, pr.M, pr.N, pr.K, pr.kps, 4};
   Epi ep;
   ep.c = pr.C;
   ep.ldc = pr.N;
   ep.c_f32 = 1;
-  ep.mode = pr.mode;
-  gemm8p_body<BM, BN, WNW, false, false>(a, ep, t - pr.t0, 0);
+  ep.mode = split ? 2 : pr.mode;
+  gemm8p_body<BM, BN, WNW, false, false>(a, ep, tile, kz);
 }
 
 // tile of the grouped launch: 128 (128^2, 4 waves, 2 blocks / CU; default)
@@ -124,6 +132,27 @@ static int g_gg_tile = [] {
 }();
 TAM_KNOB(g_gg_tile)
 void gemm_grouped_tile(int t) { g_gg_tile = t == 256 ? 256 : 128; }
+
+// K-split of long-K problems: a problem of more than 2x this many K-tiles
+// (64 deep each) is cut into slices of about this many (<= 32 slices) whose
+// partial tiles meet in fp32 atomics -- accumulate-mode (1) problems only.
+// ResNet-50's 1x1-conv weight gradients are 128..2048 x 128..2048 GEMMs
+// over K = 3136..200704 output pixels: unsplit, a 4-tile problem would run
+// ~800 K-tiles on 4 CUs. 0: never split. The Transformer / GNMT problems
+// (K = 3136..4096) stay whole.
+static int g_gg_split_kt = [] {
+  const char* e = getenv("TAM_GROUPED_SPLIT_KT");
+  return e ? atoi(e) : 64;
+}();
+TAM_KNOB(g_gg_split_kt)
+
+static int gg_kps(int K, int mode) {
+  const int kt = K / P8_BK;
+  if (g_gg_split_kt <= 0 || mode != 1 || kt <= 2 * g_gg_split_kt) return kt;
+  int sk = cdiv(kt, g_gg_split_kt);
+  if (sk > 32) sk = 32;
+  return cdiv(kt, sk);
+}
 
 // problems: A [K][lda] (M-major), B [K][ldb] (N-major), C [M][N] fp32 = or +=,
 // bias [M] += colsum(A) or null. Host checks the gemm8p conditions (K % 64,
@@ -143,7 +172,9 @@ void gemm_wgrad_grouped(const GGProblem* probs, int n, hipStream_t s) {
       p.mode = q.mode;
       p.t0 = tiles;
       p.c0 = cs;
-      tiles += cdiv(q.M, T) * cdiv(q.N, T);
+      p.ntiles = cdiv(q.M, T) * cdiv(q.N, T);
+      p.kps = gg_kps(q.K, q.mode);
+      tiles += p.ntiles * cdiv(q.K / P8_BK, p.kps);
       if (q.bias) cs += cdiv(q.M, 64);
     }
     // (a bias-less problem owns no column-sum blocks: its c0 equals the next

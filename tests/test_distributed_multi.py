@@ -432,8 +432,13 @@ def _shard_worker(rank, world, port, q, wire):
         for _ in range(3):
             ref.step()
             sh.step()
+        # the shadow all-gathers of the last step are deferred to the next
+        # forward's first parameter reads (Param.w joins its bucket only)
+        pending = len(sh.ddp._gathers)
+        hooked = sh.arena.on_param_use is not None
+        sh.ddp.join_gather()
         # the compute copy (bf16 shadow) is complete on every member after
-        # every step; the master / optimizer state only after consolidate()
+        # the join; the master / optimizer state only after consolidate()
         e_shadow = float((sh.arena.shadow.float() - ref.arena.shadow.float()).norm() /
                          ref.arena.shadow.float().norm())
         assert sh.state_sharded
@@ -446,6 +451,7 @@ def _shard_worker(rank, world, port, q, wire):
         e_master = float((sh.arena.master - ref.arena.master).norm() / ref.arena.master.norm())
         e_opt = float((sh.opt_state[0] - ref.opt_state[0]).norm() / (ref.opt_state[0].norm() + 1e-12))
         out[model] = dict(e_shadow=e_shadow, e_master=e_master, e_opt=e_opt, raised=raised, nb=nb,
+                          pending=pending, hooked=hooked, joined=sh.arena.on_param_use is None,
                           bytes_sh=sh.ddp.wire_bytes, bytes_ref=ref.ddp.wire_bytes,
                           master_sum=float(sh.arena.master.double().sum()))
     q.put((rank, out))
@@ -469,6 +475,7 @@ def test_sharded_ddp_matches_allreduce(world, wire):
         for r in range(world):
             o = res[r][model]
             assert o["raised"] and o["nb"] > 0
+            assert o["pending"] > 0 and o["hooked"] and o["joined"], (model, r, o)
             assert o["e_shadow"] < tol and o["e_master"] < tol and o["e_opt"] < 5 * tol, (model, r, o)
             # per-member wire bytes: bf16 reduce-scatter + bf16 all-gather is
             # half of the fp32 all-reduce, fp32 reduce-scatter ~3/4 (the

@@ -111,6 +111,30 @@ def test_gemm_wgrad_grouped(gpu, tile):
         assert rel_err(bs[i], refs[i % 2][1] + 1.0) < 1e-5, i
 
 
+@pytest.mark.parametrize("tile", [128, 256])
+def test_gemm_wgrad_grouped_ksplit(gpu, tile):
+    """Long-K problems (ResNet-50's 1x1-conv weight gradients: K = output
+    pixels) are K-split inside the grouped launch (fp32 atomics between the
+    slices, accumulate mode only): vs fp32 torch, next to a store-mode
+    long-K problem (never split) and a short-K one."""
+    torch.manual_seed(37)
+    shapes = [(128, 512, 50176, 1), (256, 1024, 12544, 1), (2048, 512, 3136, 1), (512, 256, 16384, 0),
+              (384, 128, 4096, 1)]
+    dys, xs, dws, refs = [], [], [], []
+    for M, N, K, mode in shapes:
+        dy = (torch.randn(K, M, device=gpu) * 0.5).to(BF)
+        x = (torch.randn(K, N, device=gpu) * 0.5).to(BF)
+        dys.append(dy)
+        xs.append(x)
+        dws.append(torch.full((M, N), 0.5, device=gpu))
+        refs.append(dy.float().t() @ x.float() + (0.5 if mode == 1 else 0.0))
+    T().gemm_grouped_tile(tile)
+    T().gemm_wgrad_grouped(dys, xs, dws, [torch.empty(0, device=gpu)] * len(shapes), [s[3] for s in shapes])
+    torch.cuda.synchronize()
+    for i, r in enumerate(refs):
+        assert rel_err(dws[i], r) < 1e-4, (i, shapes[i])
+
+
 # ------------------------------------------------------------------ GEMM
 @pytest.mark.parametrize("M,N,K", [(256, 256, 256), (200, 136, 72), (1000, 64, 520), (64, 1000, 64),
                                    (4096, 1024, 512), (33, 40, 8)])

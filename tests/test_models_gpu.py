@@ -153,6 +153,49 @@ def test_grouped_wgrad_matches(gpu, overlap, monkeypatch):
     assert rel(g.arena.master, e.arena.master) < 1e-3
 
 
+@pytest.mark.timeout(300)
+def test_resnet50_grouped_conv_wgrad_matches(gpu, monkeypatch):
+    """ResNet-50 (full size, batch 32): the 1x1 stride-1 conv weight
+    gradients deferred into the grouped launch (K-split over the output
+    pixels, fp32 atomics between slices) give the per-conv path's gradients,
+    eager and under hipGraph replay."""
+    from tiresias_amd.ops import functional as Fx
+
+    a = Trainer("resnet50", gpu, seed=6, batch=32)
+    b = Trainer("resnet50", gpu, seed=6, batch=32)
+    assert a.group_wgrad
+    b.group_wgrad = False
+    b.arena.master.copy_(a.arena.master)
+    b.arena.shadow.copy_(a.arena.shadow)
+    calls = []
+    real = Fx.flush_wgrad
+    monkeypatch.setattr(Fx, "flush_wgrad", lambda: calls.append(real()) or calls[-1])
+    la, lb = a._fwd_bwd(), b._fwd_bwd()
+    torch.cuda.synchronize()
+    assert calls and calls[0] >= 20, calls          # the 1x1 convs of stages 1-3 went through the group
+    assert abs(float(la) - float(lb)) < 1e-3 * max(1.0, abs(float(lb)))
+    assert rel(a.arena.grad, b.arena.grad) < 2e-3
+    # second backward: the early flush (side stream, issued at the n-th
+    # deferred problem of the previous step) gives the same gradients
+    assert a._defer_n == calls[0]
+    monkeypatch.setattr(a.spec, "group_early", True)
+    a.arena.grad.zero_()
+    a._fwd_bwd()
+    torch.cuda.synchronize()
+    assert a._gs is not None and len(calls) == 3 and calls[1] == a._defer_n and calls[2] == 0, calls
+    assert rel(a.arena.grad, b.arena.grad) < 2e-3
+    monkeypatch.setattr(Fx, "flush_wgrad", real)
+    g = Trainer("resnet50", gpu, seed=6, batch=32, use_graph=True)
+    e = Trainer("resnet50", gpu, seed=6, batch=32)
+    e.group_wgrad = False
+    e.arena.master.copy_(g.arena.master)
+    e.arena.shadow.copy_(g.arena.shadow)
+    for _ in range(4):
+        lg, le = float(g.step()), float(e.step())
+    assert abs(lg - le) < 2e-2 * max(1.0, abs(le))
+    assert rel(g.arena.master, e.arena.master) < 1e-3
+
+
 def test_gnmt_lstm_grouped_wgrad_matches(gpu, monkeypatch):
     """GNMT's per-layer LSTM weight gradients (dW_hh, dW_ih + the bias column
     sums) as one grouped launch (models/gnmt.py LSTM_GROUPED_WGRAD, store-

@@ -69,6 +69,8 @@ class Trainer:
         self.capture_s = 0.0     # host seconds spent capturing the hipGraph
         self._side = None
         self._ws = None                 # weight-gradient stream (1-GPU jobs)
+        self._gs = None                 # grouped weight-gradient stream (early flush)
+        self._defer_n = 0               # problems the last backward deferred
         self.overlap_wgrad = self.spec.overlap_wgrad if overlap_wgrad is None else overlap_wgrad
         # grouped weight gradients (TAM_GROUP_WGRAD=0 turns them off for A/B runs)
         self.group_wgrad = self.spec.group_wgrad and os.environ.get("TAM_GROUP_WGRAD", "1") != "0"
@@ -104,8 +106,15 @@ class Trainer:
                 self._bs = [torch.cuda.Stream(self.device) for _ in range(nb)]
             Fx.set_branch_streams(self._bs)
         group = (self.device.type == "cuda" and self.ddp is None and self.group_wgrad)
+        gs = None
         if group:
-            Fx.defer_wgrad(True)
+            # early flush on a side stream (ops/functional.py defer_wgrad):
+            # the expected count is the previous backward's
+            if self.spec.group_early and self._defer_n:
+                if self._gs is None:
+                    self._gs = torch.cuda.Stream(self.device)
+                gs = self._gs
+            Fx.defer_wgrad(True, expect=self._defer_n if gs is not None else 0, stream=gs)
         try:
             if self.spec.kind == "image":
                 logits = self.model.forward(d["x"])
@@ -120,6 +129,7 @@ class Trainer:
             logits.backward(dlog)
             if group:
                 Fx.flush_wgrad()
+                self._defer_n = Fx.deferred_count()
         finally:
             if group:
                 Fx.defer_wgrad(False, discard=True)
@@ -127,6 +137,8 @@ class Trainer:
             Fx.set_branch_streams(None)
         if ws is not None:
             torch.cuda.current_stream(self.device).wait_stream(ws)   # join before the optimizer
+        if gs is not None:
+            torch.cuda.current_stream(self.device).wait_stream(gs)
         if self.device.type == "cuda" and self.ddp is None and nb:
             for s in self._bs:
                 torch.cuda.current_stream(self.device).wait_stream(s)
@@ -465,8 +477,15 @@ class Trainer:
         if dirty and old_ranks != new_ranks:
             raise RuntimeError(f"sharded trainer state on {old_ranks} cannot move to {new_ranks}: "
                                "consolidate() first")
+        # shadow all-gathers still pending on the old communicator (deferred
+        # to the next forward) are abandoned: a broken gang may never finish
+        # them; the new bucketer re-gathers below
+        regather = self.ddp is not None and bool(self.ddp._gathers)
+        if self.ddp is not None:
+            self.ddp._gathers = {}
         self.group = group
         self.arena.on_grad_ready = None
+        self.arena.on_param_use = None
         self.ddp = None
         # an interrupted step (a peer died mid-collective) may have left
         # partial gradients: the new gang starts from clean ones
@@ -476,6 +495,10 @@ class Trainer:
             self.ddp = GradBucketer(self.arena, group, bucket_mb=self._bucket_mb, shard=self.ddp_shard,
                                     wire=self.ddp_wire)
             self.ddp.dirty = dirty and self.ddp.shard
+            if regather and self.ddp.dirty:
+                # every member's own shadow slices are current (its optimizer
+                # wrote them); rebuild the rest over the new communicator
+                self.ddp.gather_shadow(defer=False)
         self.use_graph = self._want_graph and self.ddp is None
         self._graph = None
 

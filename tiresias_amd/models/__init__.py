@@ -8,6 +8,8 @@ and ``model/model_factory.py:19-55`` (sizes only).
 """
 from __future__ import annotations
 
+import os
+
 from dataclasses import dataclass, field
 from typing import Any, Callable, Dict
 
@@ -40,10 +42,18 @@ class ModelSpec:
     # Linear weight gradients deferred and issued as ONE grouped launch per
     # backward (ops/functional.py defer_wgrad; 1-GPU jobs)
     group_wgrad: bool = False
+    # ...issued early on a side stream, beside the rest of the backward, once
+    # the previous step's count of deferred problems is reached. Off: measured
+    # slower on MI355X (hipGraph steps, two runs each: ResNet-50 9.07 vs 8.89
+    # ms, Transformer 5.41 vs 5.30 -- the grouped launch and the memory-bound
+    # tail of the backward contend for the same CUs); TAM_GROUP_EARLY=1 for A/B
+    group_early: bool = bool(int(os.environ.get("TAM_GROUP_EARLY", "0")))
 
 
 MODELS: Dict[str, ModelSpec] = {
-    "resnet50": ModelSpec(ResNet50, "image", 64, "sgd", 0.1, 1e-4),
+    # the 1x1 / stride-1 conv weight gradients (stages 1-3) as one K-split
+    # grouped launch at the end of the backward (ops/functional.py _Conv)
+    "resnet50": ModelSpec(ResNet50, "image", 64, "sgd", 0.1, 1e-4, group_wgrad=True),
     "vgg16": ModelSpec(VGG16, "image", 32, "sgd", 0.01, 5e-4),
     # weight-gradient side stream: measured per model (profiles/r2/ab_overlap.txt,
     # hipGraph steps): Transformer 7.28 -> 7.14 ms on; ResNet-50 10.65 -> 11.01

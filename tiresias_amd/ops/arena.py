@@ -47,11 +47,27 @@ class Param:
     gw_epoch: int = -1             # Arena.grad_epoch of the last gradient write
     offset: int = 0
     numel: int = 0
-    # views (set by Arena.materialize)
-    w: Optional[torch.Tensor] = None        # bf16 shadow view
+    # views (set by Arena.materialize); the bf16 shadow view is ``w`` (a
+    # property: a first read may first join a pending all-gather of it)
+    _w: Optional[torch.Tensor] = field(default=None, repr=False)
     master: Optional[torch.Tensor] = None   # fp32 master view
     grad: Optional[torch.Tensor] = None     # fp32 grad view
     arena: Optional["Arena"] = field(default=None, repr=False)
+
+    @property
+    def w(self) -> Optional[torch.Tensor]:
+        """bf16 shadow view. While a sharded gang's shadow all-gather is in
+        flight (parallel/ddp.py GradBucketer.gather_shadow) the arena's
+        ``on_param_use`` hook orders this read after the gather of THIS
+        parameter's bucket only (the next forward overlaps the rest)."""
+        a = self.arena
+        if a is not None and a.on_param_use is not None:
+            a.on_param_use(self)
+        return self._w
+
+    @w.setter
+    def w(self, t: Optional[torch.Tensor]) -> None:
+        self._w = t
 
     @property
     def value(self) -> torch.Tensor:
@@ -78,6 +94,8 @@ class Arena:
         self.n_store = 0          # [0, n_store): the store_grad params
         self.grad_epoch = 0       # optimizer steps taken (ops/functional.py::grad_mode)
         self.on_grad_ready: Optional[Callable[[Param], None]] = None
+        # set while a deferred shadow all-gather is pending (Param.w)
+        self.on_param_use: Optional[Callable[[Param], None]] = None
         # autograd anchor: every param-consuming op takes it as an input so
         # outputs require grad even when the data input does not.
         self.token = torch.zeros(1, device=self.device, requires_grad=True)

@@ -61,8 +61,8 @@ def set_wgrad_stream(stream) -> None:
 
 
 class _OnWgrad:
-    def __init__(self, *tensors):
-        self.s = _WGRAD_STREAM if tensors[0].is_cuda else None
+    def __init__(self, *tensors, stream=None):
+        self.s = (stream or _WGRAD_STREAM) if tensors[0].is_cuda else None
         self.ts = tensors
         self.ctx = None
 
@@ -93,13 +93,24 @@ class _OnWgrad:
 _DEFER_WGRAD: Optional[list] = None
 _DEFER_CHUNK = int(os.environ.get("TAM_WGRAD_GROUP_CHUNK", "0") or 0)
 _GROUP_OK: dict = {}
+# early flush (``defer_wgrad(True, expect=n, stream=s)``): the trainer knows
+# from its previous step how many problems a backward defers; the grouped
+# launch is issued on side stream s as soon as the n-th is deferred, so it
+# runs beside the rest of the backward (ResNet-50: the stage-0 / stem
+# backward, memory-bound, after the last deferred 1x1 conv of stage 1)
+_DEFER_EXPECT = 0
+_DEFER_COUNT = 0
+_GROUP_STREAM = None
 
 
-def defer_wgrad(on: bool, discard: bool = False) -> None:
+def defer_wgrad(on: bool, discard: bool = False, expect: int = 0, stream=None) -> None:
     """Start (True) or stop (False) deferring Linear weight gradients; stopping
     with problems still pending is a programming error (flush first) unless
-    ``discard`` (an aborted step)."""
-    global _DEFER_WGRAD
+    ``discard`` (an aborted step). ``expect`` / ``stream``: the early flush
+    (above); the caller joins ``stream`` before reading the gradients."""
+    global _DEFER_WGRAD, _DEFER_EXPECT, _DEFER_COUNT, _GROUP_STREAM
+    _DEFER_EXPECT, _DEFER_COUNT = (expect, 0) if on else (0, 0)
+    _GROUP_STREAM = stream if on else None
     if not on and _DEFER_WGRAD and not discard:
         raise RuntimeError("defer_wgrad(False) with unflushed weight gradients")
     if not on and _DEFER_WGRAD:
@@ -117,6 +128,22 @@ def _group_ok(M: int, N: int, K: int) -> bool:
     return ok
 
 
+def deferred_count() -> int:
+    """Problems deferred so far in this backward (flushed or not)."""
+    return _DEFER_COUNT
+
+
+def _deferred(pending_flush: bool = True) -> None:
+    """After appending one deferred problem: count it; flush when the
+    expected total is reached (early flush) or a chunk is full."""
+    global _DEFER_COUNT
+    _DEFER_COUNT += 1
+    if _DEFER_EXPECT and _DEFER_COUNT == _DEFER_EXPECT:
+        flush_wgrad()
+    elif _DEFER_CHUNK and len(_DEFER_WGRAD) >= _DEFER_CHUNK:
+        flush_wgrad()
+
+
 def flush_wgrad() -> int:
     """Issue every deferred weight gradient as one grouped launch (on the
     weight-gradient stream when one is installed), then signal grad_ready.
@@ -127,15 +154,16 @@ def flush_wgrad() -> int:
     items = list(pend)
     pend.clear()
     dys = [it[0] for it in items]
-    with _OnWgrad(*dys, *[it[1] for it in items]):
+    with _OnWgrad(*dys, *[it[1] for it in items], stream=_GROUP_STREAM):
         empty = torch.empty(0, dtype=torch.float32, device=dys[0].device)
-        _T().gemm_wgrad_grouped(dys, [it[1] for it in items], [it[2].grad for it in items],
+        # it[5] (when present): the 2-D view of a conv weight's gradient
+        _T().gemm_wgrad_grouped(dys, [it[1] for it in items], [it[5] if len(it) > 5 else it[2].grad for it in items],
                                 [it[3].grad if it[3] is not None else empty for it in items],
                                 [it[4] for it in items])
-    for _, _, w, b, _ in items:
-        w.grad_ready()
-        if b is not None:
-            b.grad_ready()
+    for it in items:
+        it[2].grad_ready()
+        if it[3] is not None:
+            it[3].grad_ready()
     return len(items)
 
 
@@ -289,8 +317,7 @@ class _Linear(Function):
             if b is not None:
                 b.grad += dy.float().sum(0)
         if deferred:
-            if _DEFER_CHUNK and len(_DEFER_WGRAD) >= _DEFER_CHUNK:
-                flush_wgrad()
+            _deferred()
         else:
             w.grad_ready()
             if b is not None:
@@ -391,15 +418,29 @@ class _Conv(Function):
             else:
                 dy = (dy.float() * (y.float() > 0)).to(BF16)
         dx = None
+        deferred = False
         if dy.is_cuda:
-            with _OnWgrad(dy, x) as ow:
-                # the bias gradient colsum(dy) rides on the wgrad kernel's dY reads;
-                # the LDS-heavy patch-staged wgrad only off the side stream
-                # accumulate into the optimizer-zeroed buffer: a store-mode first
-                # write costs a zero pass of dW on the fp32-atomic split paths
-                # (ResNet-50: 29 more zero launches per step when conv weights
-                # were store_grad), the optimizer's bulk zeroing does not
-                _T().conv_wgrad(dy, x, w.grad, st, pd, 1, 1, b.grad if b is not None else None, ow.s is None)
+            K, R, S, C = w.shape
+            Mr = dy.numel() // K
+            if (_DEFER_WGRAD is not None and R == 1 and S == 1 and st == 1 and pd == 0 and b is None
+                    and w.grad.is_contiguous() and not any(it[2] is w for it in _DEFER_WGRAD)
+                    and _group_ok(K, C, Mr)):
+                # a 1x1 / stride-1 conv's dW = dY^T X is a plain GEMM over the
+                # output pixels: deferred into the backward's grouped launch
+                # (K-split there: ResNet-50's are 128..2048 x 128..2048 x
+                # 3136..200704), accumulating into the optimizer-zeroed buffer
+                w.gw_epoch = w.arena.grad_epoch
+                _DEFER_WGRAD.append((dy.view(Mr, K), x.view(Mr, C), w, None, 1, w.grad.view(K, C)))
+                deferred = True
+            else:
+                with _OnWgrad(dy, x) as ow:
+                    # the bias gradient colsum(dy) rides on the wgrad kernel's dY reads;
+                    # the LDS-heavy patch-staged wgrad only off the side stream
+                    # accumulate into the optimizer-zeroed buffer: a store-mode first
+                    # write costs a zero pass of dW on the fp32-atomic split paths
+                    # (ResNet-50: 29 more zero launches per step when conv weights
+                    # were store_grad), the optimizer's bulk zeroing does not
+                    _T().conv_wgrad(dy, x, w.grad, st, pd, 1, 1, b.grad if b is not None else None, ow.s is None)
             if ctx.needs_input_grad[0]:
                 dx = torch.empty_like(x)
                 wt = getattr(w, "wt", None)
@@ -429,9 +470,12 @@ class _Conv(Function):
             w.grad += grads[-1].permute(0, 2, 3, 1)
             if b is not None:
                 b.grad += dy.float().sum((0, 1, 2))
-        w.grad_ready()
-        if b is not None:
-            b.grad_ready()
+        if deferred:
+            _deferred()
+        else:
+            w.grad_ready()
+            if b is not None:
+                b.grad_ready()
         return dx, None, None, None, None, None, None, None, None, None
 
 

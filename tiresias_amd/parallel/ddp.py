@@ -142,6 +142,13 @@ class GradBucketer:
         self._ev_open: List[tuple] = []          # (first, bwd_done, joined) per step, not yet read
         self._acc = {"exposed_s": 0.0, "span_s": 0.0, "steps": 0}
         self._bytes_acc = [0.0, 0]               # wire bytes / steps since the last poll
+        # deferred shadow all-gathers (sharded): bucket -> work, joined at the
+        # bucket's first parameter read in the next forward
+        self._gathers: Dict[int, object] = {}
+        self._gather_ev = None                   # [issued, last joined] on the compute stream
+        self._gather_waits: List[tuple] = []     # (before, after) each join's wait
+        self._gather_open: List[tuple] = []
+        self._gacc = {"gather_exposed_s": 0.0, "gather_window_s": 0.0, "gather_steps": 0}
         arena.on_grad_ready = self._on_ready
         self._reset()
 
@@ -271,7 +278,18 @@ class GradBucketer:
             else:
                 keep.append((first, bwd, done))
         self._ev_open = keep
+        gkeep = []
+        for (iss, end), waits in self._gather_open:
+            if end.query():
+                self._gacc["gather_window_s"] += iss.elapsed_time(end) / 1e3
+                self._gacc["gather_exposed_s"] += sum(a.elapsed_time(b) for a, b in waits) / 1e3
+                self._gacc["gather_steps"] += 1
+            else:
+                gkeep.append(((iss, end), waits))
+        self._gather_open = gkeep
         out, self._acc = self._acc, {"exposed_s": 0.0, "span_s": 0.0, "steps": 0}
+        out.update(self._gacc)
+        self._gacc = {"gather_exposed_s": 0.0, "gather_window_s": 0.0, "gather_steps": 0}
         # wire bytes of the steps finished since the last poll (the sharded
         # all-gather of a step counts with the NEXT step's finish)
         out["bytes"], out["bytes_steps"] = self._bytes_acc
@@ -295,22 +313,79 @@ class GradBucketer:
                 out.append((mid, hi))
         return sorted(out)
 
-    def gather_shadow(self) -> None:
+    def gather_shadow(self, defer: bool = True) -> None:
         """After the sharded optimizer step: every member's updated bf16
-        slices into every member's compute copy (all-gather per bucket)."""
+        slices into every member's compute copy (all-gather per bucket).
+
+        ``defer`` (default): the gathers are issued in FORWARD order (the
+        buckets were cut walking backward order, so reversed) and not
+        joined here: the next forward's first read of a parameter
+        (``Param.w``) joins only that parameter's bucket, so the later
+        buckets' gathers overlap the forward's first layers.
+        ``join_gather()`` joins whatever is still pending (before anything
+        else reads the shadow: consolidate, a move, a snapshot)."""
+        self.join_gather()
         sh, p = self.arena.shadow, self.position
-        works = []
-        for (lo, _), (sl, mid) in zip(self.ranges, self.slices):
+        works: Dict[int, object] = {}
+        for bi in reversed(range(len(self.ranges))):
+            lo = self.ranges[bi][0]
+            sl, mid = self.slices[bi]
             if sl > 0:
-                works.append(self.comm.all_gather(sh[lo:mid], sh[lo + p * sl:lo + (p + 1) * sl]))
+                works[bi] = self.comm.all_gather(sh[lo:mid], sh[lo + p * sl:lo + (p + 1) * sl])
                 self.wire_bytes += (self.world - 1) / self.world * (mid - lo) * 2
-        self.comm.finish(works)
         self.dirty = True
+        if not works:
+            return
+        if not defer:
+            self.comm.finish(list(works.values()))
+            return
+        self._gathers = works
+        if self._timed:
+            ev = torch.cuda.Event(enable_timing=True)
+            ev.record()
+            self._gather_ev = [ev, None]
+        self.arena.on_param_use = self._before_use
+
+    def _before_use(self, p: Param) -> None:
+        bi = self.bucket_of.get(id(p))
+        w = self._gathers.pop(bi, None) if bi is not None else None
+        if w is not None:
+            a = None
+            if self._timed:
+                a = torch.cuda.Event(enable_timing=True)
+                a.record()
+            self.comm.finish([w])
+            if a is not None:
+                b = torch.cuda.Event(enable_timing=True)
+                b.record()
+                self._gather_waits.append((a, b))
+        if not self._gathers:
+            self._close_gather()
+
+    def _close_gather(self) -> None:
+        self.arena.on_param_use = None
+        if self._timed and self._gather_ev is not None:
+            # issue -> last join on the compute stream: the forward work the
+            # gathers overlapped with, plus their exposed waits
+            end = torch.cuda.Event(enable_timing=True)
+            end.record()
+            self._gather_ev[1] = end
+            self._gather_open.append((self._gather_ev, self._gather_waits))
+        self._gather_ev, self._gather_waits = None, []
+
+    def join_gather(self) -> None:
+        """Join every pending shadow all-gather (compute stream waits)."""
+        if self._gathers:
+            works = list(self._gathers.values())
+            self._gathers = {}
+            self.comm.finish(works)
+            self._close_gather()
 
     def consolidate(self, state: List[torch.Tensor]) -> int:
         """All-gather the sharded fp32 buffers (master + optimizer state) so
         every member holds the full job state again; collective over the
         gang. Returns bytes gathered per member."""
+        self.join_gather()
         if not self.dirty:
             return 0
         p, works, nb = self.position, [], 0
