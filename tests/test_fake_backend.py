@@ -111,3 +111,25 @@ def test_backend_fake_cli(tmp_path):
                       "--quantum", "0.05"])
     assert s["backend"] == "fake" and s["finished"] == 12
     assert (tmp_path / "f" / "job.csv").exists()
+
+
+def test_fill_mode_keeps_barrier_idle_low_at_world8():
+    """Bulk-synchronous rounds with fill mode (ranks keep stepping their job
+    until the next plan) and finishing rounds (a round in which a job ends
+    gives every other single-job rank a share of 0 steps, so the freed GPU
+    is re-planned as soon as its job is done): on the headline trace at
+    N = 8 the barrier idle stays under 3 % of GPU time, and each mechanism
+    lowers it (executor/fake.py barrier accounting)."""
+    def idle(fill, fill_rounds):
+        jobs = bench.bench_trace(8, 24, 5)
+        fc = FakeCluster(8, iter_s=dict(bench.TRACE_ITER_S), fill=fill)
+        s = run_fake(_cfg(), jobs, 8, quantum=0.01, iter_s=dict(bench.TRACE_ITER_S), fake=fc,
+                     prior=bench.history_prior(bench.bench_trace(8, 24, 5 + bench.HISTORY_SEED_OFFSET)),
+                     fill_rounds=fill_rounds)
+        st = s["fake_stats"]
+        assert s["finished"] == len(jobs)
+        return st["barrier_idle_s"] / (st["barrier_idle_s"] + st["busy_s"])
+
+    off, fill, both = idle(False, False), idle(True, False), idle(True, True)
+    assert off > fill > both, (off, fill, both)
+    assert both < 0.03, both

@@ -254,7 +254,7 @@ class FakeCluster:
                 if len(self.held[jid]) > 1:
                     # a gang steps together: its members start when the last one is ready
                     t0 = max(ready(x) for x in self.held[jid])
-                if deadline is not None and len(self.held[jid]) == 1:
+                if deadline is not None and len(self.held[jid]) == 1 and n > 0:
                     # 1-GPU job: the round ends at the first step boundary after
                     # the next arrival (Worker._run_until)
                     left = deadline - (now_abs + t0)
@@ -337,7 +337,8 @@ class FakeCluster:
 def run_fake(cfg: SimConfig, jobs: List[ReplayJob], world: int, quantum: float = 0.25,
              out_dir: Optional[str] = None, prior: Optional[List[float]] = None,
              iter_s: Optional[Dict[str, float]] = None, plan_cost_s: float = 0.0,
-             max_rounds: int = 10 ** 8, fake: Optional[FakeCluster] = None) -> Dict:
+             max_rounds: int = 10 ** 8, fake: Optional[FakeCluster] = None,
+             fill_rounds: bool = True) -> Dict:
     """Replay ``jobs`` through the live controller against a FakeCluster in
     virtual time. ``plan_cost_s`` charges each round's scheduling overhead."""
     from ..cluster.interference import InterferenceModel
@@ -349,6 +350,7 @@ def run_fake(cfg: SimConfig, jobs: List[ReplayJob], world: int, quantum: float =
               if cfg.interference_table else InterferenceModel(cfg.interference))
     fc = fake or FakeCluster(world, iter_s=iter_s, interference=interf, vnode_size=ctrl.vnode_size,
                              nic_gbps=ctrl.nic_gbps)
+    ctrl.fill_rounds = fc.fill and fill_rounds
     if getattr(cfg, "gang_align", False):
         # the live bench pre-creates the canonical (buddy) communicators
         from ..parallel.gang import canonical_gang_sets

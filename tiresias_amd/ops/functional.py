@@ -352,7 +352,7 @@ def _conv_out(h: int, k: int, s: int, p: int, d: int = 1) -> int:
 # bn_bwd_reduce launches per step go away (-127 us) but the dgrad convs that
 # now read the BN input in their epilogue get +165 us slower; graph step
 # 10.65 -> 10.66 ms. Off by default; the GPU test keeps the path exact.
-BN_DGRAD_FUSION = False
+BN_DGRAD_FUSION = os.environ.get("TAM_BN_DGRAD_FUSION", "0") == "1"
 
 
 # relu BNs whose backward applies the ReLU mask itself keep it as 1 bit per
@@ -444,6 +444,8 @@ class _Conv(Function):
             if ctx.needs_input_grad[0]:
                 dx = torch.empty_like(x)
                 wt = getattr(w, "wt", None)
+                if wt is not None:
+                    _wt_join(dx.device)
                 sl = ctx.bn_slot
                 if wt is not None and sl is not None:
                     bx, bmean, brstd, bws = sl.src
@@ -479,17 +481,48 @@ class _Conv(Function):
         return dx, None, None, None, None, None, None, None, None, None
 
 
+# the re-laid weights are first read by the backward's dgrad: the re-lay runs
+# on a side stream beside the forward, and the first dgrad waits for it
+_WT_STREAMS: dict = {}     # compute stream -> its side stream (GPU-shared jobs stay independent)
+_WT_READY = None
+WT_SIDE = os.environ.get("TAM_WT_SIDE", "1") != "0"
+
+
 def prepare_conv_wt(params: List[Param]) -> None:
     """Re-lay every conv weight [K,R,S,C] -> [C,R,S,K] (the dgrad operand) in
     ONE launch per step, into per-parameter buffers kept across steps (the
     dgrad then skips its own transpose). Call at the start of the forward:
-    the weights are final for the step then. No-op on CPU."""
+    the weights are final for the step then. The launch goes on a side stream
+    (forked here, joined by the first dgrad: _wt_join), so it overlaps the
+    forward. No-op on CPU."""
+    global _WT_READY
     if not params or not params[0].w.is_cuda:
         return
     for p in params:
         if getattr(p, "wt", None) is None or p.wt.device != p.w.device:
             p.wt = torch.empty_like(p.w)
-    _T().conv_weight_t_batch([p.w for p in params], [p.wt for p in params])
+    if not WT_SIDE:
+        _T().conv_weight_t_batch([p.w for p in params], [p.wt for p in params])
+        return
+    dev = params[0].w.device
+    cur = torch.cuda.current_stream(dev)
+    side = _WT_STREAMS.get(cur.cuda_stream)
+    if side is None:
+        side = _WT_STREAMS[cur.cuda_stream] = torch.cuda.Stream(dev)
+    side.wait_stream(cur)
+    with torch.cuda.stream(side):
+        _T().conv_weight_t_batch([p.w for p in params], [p.wt for p in params])
+    ev = torch.cuda.Event()
+    ev.record(side)
+    _WT_READY = ev
+
+
+def _wt_join(dev) -> None:
+    """Order the current stream after the side-stream weight re-lay (once)."""
+    global _WT_READY
+    if _WT_READY is not None:
+        torch.cuda.current_stream(dev).wait_event(_WT_READY)
+        _WT_READY = None
 
 
 def conv2d(x: torch.Tensor, w: Param, b: Optional[Param] = None, stride: int = 1, pad: int = 0,
