@@ -570,6 +570,7 @@ def main():
             "apply_counts_last_replay_rank0": sums[-1].get("apply_counts_rank0"),
             "per_rank_process_totals": ap_all,
             "fill_mode": bool(worker.fill_enabled and world > 1),
+            "comm_totals_last_replay_s": sums[-1].get("comm_totals_s"),
             "pool_hits": worker.pool_hits,
             "pressure_spills": worker.pressure_spills,
             "pool_evictions": worker.pool_evictions,

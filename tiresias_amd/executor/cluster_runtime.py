@@ -301,6 +301,12 @@ class Controller:
                         # bytes this member put on the wire per step (the gang's wire format)
                         j.extra["comm_bytes"] = j.extra.get("comm_bytes", 0.0) + c.get("bytes", 0.0)
                         j.extra["comm_steps"] = j.extra.get("comm_steps", 0) + c.get("bytes_steps", 0)
+                        # sharded gangs: the deferred shadow all-gather's joins
+                        # (compute-stream waits) and the window it overlapped
+                        j.extra["gather_exposed_s"] = j.extra.get("gather_exposed_s", 0.0) + \
+                            c.get("gather_exposed_s", 0.0)
+                        j.extra["gather_window_s"] = j.extra.get("gather_window_s", 0.0) + \
+                            c.get("gather_window_s", 0.0)
 
     def credit_fill(self, counts: Dict[int, Dict[str, int]]) -> Dict[str, int]:
         """Per-rank fill counts -> the steps credited per job (a gang's step
@@ -2023,6 +2029,12 @@ def run_replay(cfg: SimConfig, jobs: List[ReplayJob], rank: int, world: int, dev
                  lost_ranks=lost_ranks, recovered_jobs=sorted(ctrl.recovered),
                  restarted_jobs=sorted(ctrl.restarted), snapshot_restored_jobs=sorted(ctrl.snap_restored),
                  ddp_shard=ctrl.ddp_shard, consolidations=ctrl.consolidations,
+                 # measured on the gangs' compute streams (hipEvents, lowest
+                 # member): DDP reductions exposed after backward, and the
+                 # deferred sharded shadow all-gather's exposed joins vs the
+                 # forward window it overlapped
+                 comm_totals_s={k: round(sum(j.extra.get(k, 0.0) for j in ctrl.sched.jobs.values()), 6)
+                                for k in ("comm_exposed_s", "comm_span_s", "gather_exposed_s", "gather_window_s")},
                  lost_iters={j.job_id: j.extra["lost_iters"] for j in ctrl.sched.jobs.values()
                              if j.extra.get("lost_iters")})
         log.close()

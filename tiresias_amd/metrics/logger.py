@@ -30,7 +30,7 @@ CLUSTER_HEADER = ["delta", "num_idle_nodes", "num_busy_nodes", "num_busy_gpus", 
 JOB_HEADER = ["time", "job_id", "num_gpu", "submit_time", "start_time", "end_time", "executed_time",
               "JCT", "duration", "pending_time", "preempt", "resume", "promote", "migration",
               "queue", "ckpt_overhead", "ckpt_bytes", "ckpt_save_s", "ckpt_restore_s", "comm_exposed_s",
-              "comm_span_s", "comm_bytes_per_step", "model", "lost_iters"]
+              "comm_span_s", "comm_bytes_per_step", "gather_exposed_s", "gather_window_s", "model", "lost_iters"]
 
 
 def percentile(xs: List[float], p: float) -> float:
@@ -169,6 +169,8 @@ class MetricsLogger:
                    comm_span_s=round(j.extra.get("comm_span_s", 0.0), 6),
                    comm_bytes_per_step=(int(j.extra["comm_bytes"] / j.extra["comm_steps"])
                                         if j.extra.get("comm_steps") else 0),
+                   gather_exposed_s=round(j.extra.get("gather_exposed_s", 0.0), 6),
+                   gather_window_s=round(j.extra.get("gather_window_s", 0.0), 6),
                    model=j.spec.model)
         self.job_rows.append(row)
         if "job" in self._writers:
