@@ -749,6 +749,39 @@ void ln_backward_op(const Tensor& dy, const Tensor& x, const Tensor& g, const Te
                    ws.data_ptr<float>(), x.numel() / D, (int)D, cur_stream(x));
 }
 
+// LN backward without its column reduce: per-block partials into ws (fp32,
+// >= LN_MAX_BLOCKS * 2D); returns the partial-row count for col_reduce_acc
+int64_t ln_backward_split_op(const Tensor& dy, const Tensor& x, const Tensor& g, const Tensor& mean,
+                             const Tensor& rstd, const Tensor& dx, const Tensor& ws,
+                             const optional<Tensor>& addend) {
+  check_bf16(dy, "dy"); check_bf16(x, "x"); check_bf16(dx, "dx");
+  check_contig(dy, "dy"); check_contig(x, "x"); check_contig(dx, "dx");
+  check_f32(ws, "ws");
+  const int64_t D = x.size(-1);
+  TORCH_CHECK(ws.is_contiguous() && ws.numel() >= (int64_t)tam::LN_MAX_BLOCKS * 2 * D,
+              "tam.ln_backward_split: ws must hold LN_MAX_BLOCKS * 2D floats");
+  const tam::bf16_t* add = nullptr;
+  if (addend.has_value() && addend->defined()) {
+    check_bf16(*addend, "addend"); check_contig(*addend, "addend");
+    TORCH_CHECK(addend->numel() == x.numel(), "tam.ln_backward_split: addend size");
+    add = bp(*addend);
+  }
+  return tam::ln_backward_partial(bp(dy), bp(x), g.data_ptr<float>(), mean.data_ptr<float>(),
+                                  rstd.data_ptr<float>(), bpm(dx), add, ws.data_ptr<float>(), x.numel() / D,
+                                  (int)D, cur_stream(x));
+}
+
+// out0[c] += sum_b part[b][c] (c < split), out1[c - split] += ... (c >= split)
+void col_reduce_acc_op(const Tensor& part, int64_t nblk, int64_t W, const Tensor& out0, const Tensor& out1,
+                       int64_t split) {
+  check_f32(part, "part"); check_f32(out0, "out0"); check_f32(out1, "out1");
+  TORCH_CHECK(part.is_contiguous() && part.numel() >= nblk * W && out0.numel() == split &&
+                  out1.numel() == W - split && out0.is_contiguous() && out1.is_contiguous(),
+              "tam.col_reduce_acc: shapes");
+  tam::col_reduce_acc(part.data_ptr<float>(), (int)nblk, (int)W, out0.data_ptr<float>(), out1.data_ptr<float>(),
+                      (int)split, cur_stream(part));
+}
+
 // ------------------------------------------------------------------ pooling
 void maxpool_forward_op(const Tensor& x, const Tensor& y, const Tensor& idx, int64_t R, int64_t S,
                         int64_t st, int64_t pad) {
@@ -811,6 +844,7 @@ void embedding_backward_op(const Tensor& dout, const Tensor& ids, const Tensor& 
 void conv_dma_policy_op(int64_t p) { tam::conv_dma_policy((int)p); }
 void conv_halo_policy_op(int64_t p) { tam::conv_halo_policy((int)p); }
 void conv_stats_force_op(int64_t p) { tam::conv_stats_force((int)p); }
+void conv_igemm_stats_op(int64_t p) { tam::conv_igemm_stats((int)p); }
 void colsum_policy_op(int64_t p) { tam::colsum_policy((int)p); }
 void attn_short_policy_op(int64_t p) { tam::attn_short_policy((int)p); }
 // forced (bm, bn, splits) of the LDS-DMA conv wgrad (A/B sweeps; 0 = heuristic)
@@ -1101,6 +1135,8 @@ TORCH_LIBRARY(tam, m) {
   m.def("bn_backward(Tensor dy, Tensor? y, Tensor x, Tensor mean, Tensor rstd, Tensor gamma, Tensor(a!) dx, Tensor(b!)? dres, Tensor(c!)? dgamma, Tensor(d!)? dbeta, bool relu, Tensor? addend=None, Tensor(e!)? sums=None, bool sums_ready=False, Tensor? ymask=None) -> ()", &bn_backward_op);
   m.def("ln_forward(Tensor x, Tensor g, Tensor b, Tensor(a!) y, Tensor(b!) mean, Tensor(c!) rstd, float eps, Tensor? addend=None, Tensor(d!)? sum_out=None) -> ()", &ln_forward_op);
   m.def("ln_backward(Tensor dy, Tensor x, Tensor g, Tensor mean, Tensor rstd, Tensor(a!) dx, Tensor(b!) dg, Tensor(c!) db, Tensor? addend=None) -> ()", &ln_backward_op);
+  m.def("ln_backward_split(Tensor dy, Tensor x, Tensor g, Tensor mean, Tensor rstd, Tensor(a!) dx, Tensor(b!) ws, Tensor? addend=None) -> int", &ln_backward_split_op);
+  m.def("col_reduce_acc(Tensor part, int nblk, int W, Tensor(a!) out0, Tensor(b!) out1, int split) -> ()", &col_reduce_acc_op);
   m.def("maxpool_forward(Tensor x, Tensor(a!) y, Tensor(b!) idx, int R, int S, int stride, int pad) -> ()", &maxpool_forward_op);
   m.def("maxpool_backward(Tensor dy, Tensor idx, Tensor(a!) dx, int R, int S, int stride, int pad) -> ()", &maxpool_backward_op);
   m.def("maxpool_k3s2_policy(int policy) -> ()", &maxpool_k3s2_policy_op);
@@ -1121,6 +1157,7 @@ TORCH_LIBRARY(tam, m) {
   m.def("gemm8p_sk_force(int on) -> ()", &gemm8p_sk_force_op);
   m.def("conv_split_policy(int p) -> ()", &conv_split_policy_op);
   m.def("conv_stats_force(int p) -> ()", &conv_stats_force_op);
+  m.def("conv_igemm_stats(int p) -> ()", &conv_igemm_stats_op);
   m.def("optim_variant(int v) -> ()", &optim_variant_op);
   m.def("gemm_lib_policy(int policy) -> ()", &gemm_lib_policy_op);
   m.def("conv_dma_policy(int policy) -> ()", &conv_dma_policy_op);

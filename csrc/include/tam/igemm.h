@@ -440,6 +440,13 @@ igemm_kernel(LA la, LB lb, int M, int N, int K, int ktiles_per_split, Epi ep) {
     bf16_t* slab = (bf16_t*)(smem + wid * (32 * LDW * 2));
     if (kt0 >= kt1) __syncthreads();   // (the K loop ends with a barrier otherwise)
     const int cbase = n0 + wc * WC;
+    // BatchNorm statistics of the STORED values (Epi::stats; a pointwise
+    // conv's output feeding a BN): a lane keeps one 8-column chunk (ch =
+    // lane % CPR for every u) over all its rows
+    const bool stats = ep.stats != nullptr;
+    float ssum[8], ssq[8];
+#pragma unroll
+    for (int e = 0; e < 8; ++e) ssum[e] = ssq[e] = 0.f;
     float bv[TN];
 #pragma unroll
     for (int j = 0; j < TN; ++j) {
@@ -492,16 +499,57 @@ igemm_kernel(LA la, LB lb, int M, int N, int K, int ktiles_per_split, Epi ep) {
                                bf2f((bf16_t)(vw[e] >> 16)) + bf2f((bf16_t)(ow[e] >> 16)));
           }
           *(uint4*)dst = v;
+          if (stats) {
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+              const float lo = bf2f((bf16_t)(vw[e] & 0xffff)), hi = bf2f((bf16_t)(vw[e] >> 16));
+              ssum[2 * e] += lo; ssq[2 * e] += lo * lo;
+              ssum[2 * e + 1] += hi; ssq[2 * e + 1] += hi * hi;
+            }
+          }
         } else {
           for (int e = 0; e < 8 && col + e < N; ++e) {
             float v = bf2f(src[e]);
             if (ep.mask && bf2f(ep.mask[(long)row * ep.ldm + col + e]) <= 0.f) v = 0.f;
             if (ep.mode == 1) v += bf2f(dst[e]);
-            dst[e] = f2bf(v);
+            const bf16_t o = f2bf(v);
+            dst[e] = o;
+            if (stats) { const float f = bf2f(o); ssum[e] += f; ssq[e] += f * f; }
           }
         }
       }
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    }
+    if (stats) {
+      // lanes of one chunk -> the wave's rows; the two row-waves of a column
+      // half through LDS (the slabs are retired); one fp64 atomic per
+      // channel and sum into statistics shard (M-tile % BN_SHARDS)
+#pragma unroll
+      for (int o = CPR; o < 64; o <<= 1)
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+          ssum[e] += __shfl_xor(ssum[e], o, 64);
+          ssq[e] += __shfl_xor(ssq[e], o, 64);
+        }
+      __syncthreads();
+      float* red = (float*)smem;                   // [wr][wc][sum | sq][WC]
+      if (lane < CPR) {
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+          red[((wr * 2 + wc) * 2 + 0) * WC + lane * 8 + e] = ssum[e];
+          red[((wr * 2 + wc) * 2 + 1) * WC + lane * 8 + e] = ssq[e];
+        }
+      }
+      __syncthreads();
+      if (wr == 0) {
+        double* sh = ep.stats + (long)((m0 / BM) % BN_SHARDS) * 2 * N;
+        for (int e = lane; e < 2 * WC; e += 64) {
+          const int q = e / WC, c = e % WC, col = cbase + c;
+          if (col < N)
+            unsafeAtomicAdd(sh + q * N + col, (double)(red[((0 * 2 + wc) * 2 + q) * WC + c] +
+                                                       red[((1 * 2 + wc) * 2 + q) * WC + c]));
+        }
+      }
     }
     return;
   }

@@ -59,6 +59,11 @@ void ln_forward(const bf16_t* x, const float* g, const float* b, bf16_t* y, floa
 void ln_backward(const bf16_t* dy, const bf16_t* x, const float* g, const float* mean,
                  const float* rstd, bf16_t* dx, const bf16_t* addend, float* dg, float* db,
                  float* ws, long rows, int D, hipStream_t s);
+// the same without the column reduce: per-block partial dgamma | dbeta rows
+// in ws; returns their count (col_reduce_acc finishes, e.g. on a side stream)
+int ln_backward_partial(const bf16_t* dy, const bf16_t* x, const float* g, const float* mean,
+                        const float* rstd, bf16_t* dx, const bf16_t* addend, float* ws, long rows, int D,
+                        hipStream_t s);
 
 // pooling
 void maxpool_forward(const bf16_t* x, bf16_t* y, uint8_t* idx, int N, int H, int W, int C, int P,

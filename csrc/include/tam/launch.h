@@ -12,6 +12,9 @@ namespace tam {
 //   B(k,n) = b_kmajor ? B[n*ldb+k] : B[k*ldb+n]
 // allow_split: permit split-K (fp32 atomic output; C is zeroed first when
 // ep.mode == 0, requires ldc == N).
+// the heuristic-tile igemm, unsplit (Epi::stats honoured in its bf16 epilogue)
+void gemm_igemm(const bf16_t* A, long lda, bool a_kmajor, const bf16_t* B, long ldb, bool b_kmajor, int M,
+                int N, int K, const Epi& ep, hipStream_t s);
 void gemm(const bf16_t* A, long lda, bool a_kmajor, const bf16_t* B, long ldb, bool b_kmajor,
           int M, int N, int K, Epi ep, bool allow_split, hipStream_t s);
 // path 0: heuristic, 2: LDS-DMA GEMM where eligible, 3: gemm8p where eligible
@@ -82,6 +85,7 @@ void conv_dma_policy(int p);   // 1: LDS-DMA core where eligible (default), 0: i
 void conv_wgrad_force(int bm, int bn, int splits, int noatomic = 0);
 void conv_wgrad_order(int flat);    // DMA wgrad block order: 1 split-major XCD remap (default), 0 3-D grid
 void conv_wgrad_c64_policy(int p);   // 64-channel 3x3 wgrad kernel: 1 on (default), 0 off, >= 2 blocks per k-slice
+void conv_igemm_stats(int p);   // 1: shallow pointwise convs on the igemm produce BN stats in its epilogue
 void conv_stats_force(int p);   // 1: shallow pointwise convs with BN stats on the LDS-DMA core
 void conv_halo_policy(int p);   // 1: 64-channel 3x3 stride-1 passes on the halo-tile kernel (default)
 bool gemm_select_big_p8(bool ak, bool bk, int M, int N, int K, long lda, long ldb);   // plain-GEMM igemm K-tiles in flight (1..3)

@@ -215,6 +215,21 @@ static int p8_splits(int M, int N, int K, bool can_split, int tile) {
   return sp < 1 ? 1 : sp;
 }
 
+// the register-staged igemm with the heuristic tile, never split -- the
+// route gemm_select takes for shallow-K shapes; its bf16 epilogue honours
+// Epi::stats (BatchNorm sums of a pointwise conv's output)
+void gemm_igemm(const bf16_t* A, long lda, bool ak, const bf16_t* B, long ldb, bool bk, int M, int N,
+                int K, const Epi& ep, hipStream_t s) {
+  if (M <= 0 || N <= 0) return;
+  TileChoice t = choose_tiles_gemm(M, N, K, false);
+  switch (t.cfg > 3 ? 0 : t.cfg) {
+    case 0: gemm_tile<128, 128>(A, lda, ak, B, ldb, bk, M, N, K, ep, 1, s); break;
+    case 1: gemm_tile<128, 64>(A, lda, ak, B, ldb, bk, M, N, K, ep, 1, s); break;
+    case 2: gemm_tile<64, 128>(A, lda, ak, B, ldb, bk, M, N, K, ep, 1, s); break;
+    default: gemm_tile<64, 64>(A, lda, ak, B, ldb, bk, M, N, K, ep, 1, s); break;
+  }
+}
+
 void gemm(const bf16_t* A, long lda, bool ak, const bf16_t* B, long ldb, bool bk, int M, int N,
           int K, Epi ep, bool allow_split, hipStream_t s) {
   gemm_select(A, lda, ak, B, ldb, bk, M, N, K, ep, allow_split, s, g_dma ? 2 : 0);

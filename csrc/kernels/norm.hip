@@ -553,17 +553,6 @@ __global__ void __launch_bounds__(256) ln_fwd_kernel(const bf16_t* __restrict__ 
   const long row = blockIdx.x * 4L + (threadIdx.x >> 6);
   if (row >= rows) return;
   const bf16_t* xr = x + row * D;
-  // gamma / beta issued with the row's loads (one memory round trip, not
-  // two: the kernel is a few us of latency at Transformer sizes)
-  float4 gq[VEC][2], bq[VEC][2];
-#pragma unroll
-  for (int v = 0; v < VEC; ++v) {
-    const int c = (v * 64 + lane) * 8;
-    if (c < D) {
-      gq[v][0] = *(const float4*)(g + c); gq[v][1] = *(const float4*)(g + c + 4);
-      bq[v][0] = *(const float4*)(b + c); bq[v][1] = *(const float4*)(b + c + 4);
-    }
-  }
   float f[VEC][8];
   float s = 0.f;
 #pragma unroll
@@ -605,13 +594,9 @@ __global__ void __launch_bounds__(256) ln_fwd_kernel(const bf16_t* __restrict__ 
   for (int v = 0; v < VEC; ++v) {
     const int c = (v * 64 + lane) * 8;
     if (c < D) {
-      const float gg[8] = {gq[v][0].x, gq[v][0].y, gq[v][0].z, gq[v][0].w,
-                           gq[v][1].x, gq[v][1].y, gq[v][1].z, gq[v][1].w};
-      const float bb[8] = {bq[v][0].x, bq[v][0].y, bq[v][0].z, bq[v][0].w,
-                           bq[v][1].x, bq[v][1].y, bq[v][1].z, bq[v][1].w};
       float o[8];
 #pragma unroll
-      for (int j = 0; j < 8; ++j) o[j] = (f[v][j] - mu) * rstd * gg[j] + bb[j];
+      for (int j = 0; j < 8; ++j) o[j] = (f[v][j] - mu) * rstd * g[c + j] + b[c + j];
       *(uint4*)(y + row * D + c) = pack8(o);
     }
   }
@@ -639,50 +624,21 @@ __global__ void __launch_bounds__(256) ln_bwd_kernel(const bf16_t* __restrict__ 
 #pragma unroll
     for (int j = 0; j < 8; ++j) dgacc[v][j] = dbacc[v][j] = 0.f;
   const long r0 = (long)blockIdx.x * rows_per_block;
-  const long rend = min(rows, r0 + rows_per_block);
-  // gamma once per lane; each row's x / dy / mean / rstd are issued one row
-  // AHEAD (the wave walks its rows serially: without the prefetch every row
-  // is a full memory round trip)
-  float gl[VEC][8];
-#pragma unroll
-  for (int v = 0; v < VEC; ++v) {
-    const int c = (v * 64 + lane) * 8;
-#pragma unroll
-    for (int j = 0; j < 8; ++j) gl[v][j] = c < D ? g[c + j] : 0.f;
-  }
-  const uint4 z4 = make_uint4(0, 0, 0, 0);
-  uint4 nx[VEC], nd[VEC];
-  float nmu = 0.f, nrs = 0.f;
-  auto fetch = [&](long r) {
-#pragma unroll
-    for (int v = 0; v < VEC; ++v) {
-      const int c = (v * 64 + lane) * 8;
-      nx[v] = c < D ? *(const uint4*)(x + r * D + c) : z4;
-      nd[v] = c < D ? *(const uint4*)(dy + r * D + c) : z4;
-    }
-    nmu = mean[r];
-    nrs = rstd[r];
-  };
-  if (r0 + w < rend) fetch(r0 + w);
-  for (long row = r0 + w; row < rend; row += 4) {
-    const float mu = nmu, rs = nrs;
-    uint4 cx[VEC], cd[VEC];
-#pragma unroll
-    for (int v = 0; v < VEC; ++v) { cx[v] = nx[v]; cd[v] = nd[v]; }
-    if (row + 4 < rend) fetch(row + 4);
+  for (long row = r0 + w; row < min(rows, r0 + rows_per_block); row += 4) {
+    const float mu = mean[row], rs = rstd[row];
     float fx[VEC][8], fd[VEC][8];
     float s1 = 0.f, s2 = 0.f;
 #pragma unroll
     for (int v = 0; v < VEC; ++v) {
       const int c = (v * 64 + lane) * 8;
       if (c < D) {
-        unpack8(cx[v], fx[v]);
-        unpack8(cd[v], fd[v]);
+        unpack8(*(const uint4*)(x + row * D + c), fx[v]);
+        unpack8(*(const uint4*)(dy + row * D + c), fd[v]);
 #pragma unroll
         for (int j = 0; j < 8; ++j) {
           const float xh = (fx[v][j] - mu) * rs;
           fx[v][j] = xh;
-          const float gd = fd[v][j] * gl[v][j];
+          const float gd = fd[v][j] * g[c + j];
           s1 += gd;
           s2 += gd * xh;
           dgacc[v][j] += fd[v][j] * xh;
@@ -698,7 +654,7 @@ __global__ void __launch_bounds__(256) ln_bwd_kernel(const bf16_t* __restrict__ 
       if (c < D) {
         float o[8];
 #pragma unroll
-        for (int j = 0; j < 8; ++j) o[j] = rs * (fd[v][j] * gl[v][j] - s1 - fx[v][j] * s2);
+        for (int j = 0; j < 8; ++j) o[j] = rs * (fd[v][j] * g[c + j] - s1 - fx[v][j] * s2);
         if (addend) {                      // + the residual branch's gradient (fused skip)
           float a[8];
           unpack8(*(const uint4*)(addend + row * D + c), a);
@@ -740,9 +696,9 @@ void ln_forward(const bf16_t* x, const float* g, const float* b, bf16_t* y, floa
   else hipLaunchKernelGGL(ln_fwd_kernel<4>, dim3(blocks), dim3(256), 0, s, x, g, b, y, mean, rstd, rows, D, eps, addend, sum_out);
 }
 
-void ln_backward(const bf16_t* dy, const bf16_t* x, const float* g, const float* mean,
-                 const float* rstd, bf16_t* dx, const bf16_t* addend, float* dg, float* db,
-                 float* ws, long rows, int D, hipStream_t s) {
+int ln_backward_partial(const bf16_t* dy, const bf16_t* x, const float* g, const float* mean,
+                        const float* rstd, bf16_t* dx, const bf16_t* addend, float* ws, long rows, int D,
+                        hipStream_t s) {
   // ws: LN_MAX_BLOCKS * 2 * D floats of per-block partial dgamma / dbeta
   int rpb = (int)((rows + LN_MAX_BLOCKS - 1) / LN_MAX_BLOCKS);
   rpb = ((rpb + 3) / 4) * 4;
@@ -751,6 +707,13 @@ void ln_backward(const bf16_t* dy, const bf16_t* x, const float* g, const float*
   if (D <= 512) hipLaunchKernelGGL(ln_bwd_kernel<1>, dim3(blocks), dim3(256), 0, s, dy, x, g, mean, rstd, dx, addend, ws, rows, D, rpb);
   else if (D <= 1024) hipLaunchKernelGGL(ln_bwd_kernel<2>, dim3(blocks), dim3(256), 0, s, dy, x, g, mean, rstd, dx, addend, ws, rows, D, rpb);
   else hipLaunchKernelGGL(ln_bwd_kernel<4>, dim3(blocks), dim3(256), 0, s, dy, x, g, mean, rstd, dx, addend, ws, rows, D, rpb);
+  return blocks;
+}
+
+void ln_backward(const bf16_t* dy, const bf16_t* x, const float* g, const float* mean,
+                 const float* rstd, bf16_t* dx, const bf16_t* addend, float* dg, float* db,
+                 float* ws, long rows, int D, hipStream_t s) {
+  const int blocks = ln_backward_partial(dy, x, g, mean, rstd, dx, addend, ws, rows, D, s);
   col_reduce_acc(ws, blocks, 2 * D, dg, db, D, s);
 }
 

@@ -204,8 +204,11 @@ def test_gnmt_lstm_grouped_wgrad_matches(gpu, monkeypatch):
     import tiresias_amd.models.gnmt as G
     kw = dict(hidden=256, enc_layers=3, dec_layers=2, heads=4)      # the batch's 32000-token vocabulary
     runs = []
-    for grouped in (True, False):
+    # (grouped, deferred into the backward's one launch): deferred (the
+    # production path), one grouped launch per layer, per-GEMM (reference)
+    for grouped, defer in ((True, True), (True, False), (False, False)):
         monkeypatch.setattr(G, "LSTM_GROUPED_WGRAD", grouped)
+        monkeypatch.setattr(G, "LSTM_DEFER_WGRAD", defer)
         t = Trainer("gnmt", gpu, seed=8, batch=64, model_kwargs=kw)
         loss = float(t._fwd_bwd())
         torch.cuda.synchronize()
@@ -214,11 +217,12 @@ def test_gnmt_lstm_grouped_wgrad_matches(gpu, monkeypatch):
         losses = [float(t.step()) for _ in range(3)]
         torch.cuda.synchronize()
         runs.append((loss, grad, losses, t.arena.master.clone()))
-    (la, ga, lsa, ma), (lb, gb, lsb, mb) = runs
-    assert abs(la - lb) < 1e-4 * max(1.0, abs(lb))
-    assert rel(ga, gb) < 2e-3
-    assert all(abs(x - y) < 1e-2 * max(1.0, abs(y)) for x, y in zip(lsa, lsb)), (lsa, lsb)
-    assert rel(ma, mb) < 1e-3
+    lb, gb, lsb, mb = runs[-1]
+    for la, ga, lsa, ma in runs[:-1]:
+        assert abs(la - lb) < 1e-4 * max(1.0, abs(lb))
+        assert rel(ga, gb) < 2e-3
+        assert all(abs(x - y) < 1e-2 * max(1.0, abs(y)) for x, y in zip(lsa, lsb)), (lsa, lsb)
+        assert rel(ma, mb) < 1e-3
 
 
 @pytest.mark.parametrize("overlap", [False, True])

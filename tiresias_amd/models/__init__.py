@@ -65,7 +65,9 @@ MODELS: Dict[str, ModelSpec] = {
     # gradients are one grouped launch at the end of the backward now)
     "transformer": ModelSpec(TransformerBase, "seq2seq", 32, "adam", 5e-4, 0.0, seq=128,
                              smoothing=0.1, group_wgrad=True),
-    "gnmt": ModelSpec(GNMT, "seq2seq", 64, "adam", 1e-3, 0.0, seq=50),
+    # LSTM dW_hh / dW_ih (+ bias column sums) and the attention projections'
+    # weight gradients as one grouped launch per backward (models/gnmt.py)
+    "gnmt": ModelSpec(GNMT, "seq2seq", 64, "adam", 1e-3, 0.0, seq=50, group_wgrad=True),
     # tiny variants (CPU tests / gloo rehearsals / smoke)
     "resnet_tiny": ModelSpec(ResNet50, "image", 4, "sgd", 0.1, 1e-4,
                              dict(layers=(1, 1, 1, 1), width=8, num_classes=16), image=32, classes=16),

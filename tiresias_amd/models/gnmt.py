@@ -47,6 +47,10 @@ PERSIST = True
 # one grouped launch (csrc/kernels/gemm_grouped.hip) instead of two routed
 # GEMMs with split-K slab reduces + a column-sum pass; 0: the per-GEMM path
 LSTM_GROUPED_WGRAD = os.environ.get("TAM_LSTM_GROUPED", "1") != "0"
+# ...and, when the trainer defers weight gradients (ModelSpec.group_wgrad),
+# every layer's problems join the backward's ONE grouped launch instead of
+# one launch per layer (TAM_LSTM_DEFER=0: per-layer launches, A/B)
+LSTM_DEFER_WGRAD = os.environ.get("TAM_LSTM_DEFER", "1") != "0"
 _SYNCS: list = []          # recent barrier/error words (tests read the error flags)
 
 
@@ -196,8 +200,15 @@ class _LSTMLayer(Function):
             x2 = x.reshape(T * B, I)
             grouped = (LSTM_GROUPED_WGRAD and T > 1 and x2.is_contiguous() and Fx._group_ok(4 * Hd, Hd, (T - 1) * B)
                        and Fx._group_ok(4 * Hd, I, T * B))
+            if grouped and LSTM_DEFER_WGRAD and Fx.defer_problems(
+                    [(dGh, Hp, w_hh, None, Fx.grad_mode(w_hh)), (dG2, x2, w_ih, b, Fx.grad_mode(w_ih))]):
+                # into the backward's ONE grouped launch (trainer group_wgrad):
+                # grad_ready() is signalled by the flush
+                grouped = None
             with Fx._OnWgrad(dG2, Hs, x):        # overlaps the next layer's recurrence
-                if grouped:
+                if grouped is None:
+                    pass
+                elif grouped:
                     # dW_hh, dW_ih and the bias colsum in ONE launch (no split-K
                     # slabs, no separate column-sum passes)
                     empty = torch.empty(0, dtype=torch.float32, device=dev)
@@ -247,9 +258,10 @@ class _LSTMLayer(Function):
             w_ih.grad += dG2.t() @ x.reshape(T * B, I).float()
             b.grad += dG2.sum(0)
             dx = (dG2 @ w_ih.w.float()).to(BF16).view(T, B, I) if ctx.needs_input_grad[0] else None
-        w_ih.grad_ready()
-        w_hh.grad_ready()
-        b.grad_ready()
+        if not (dev.type == "cuda" and grouped is None):
+            w_ih.grad_ready()
+            w_hh.grad_ready()
+            b.grad_ready()
         return dx, None, None, None, None, None, None
 
 

@@ -119,13 +119,35 @@ def defer_wgrad(on: bool, discard: bool = False, expect: int = 0, stream=None) -
     _DEFER_WGRAD = [] if on else None
 
 
+# a weight gradient this big fills the chip on its own, on the 256^2 route
+# (~770-880 TF/s) -- inside the grouped launch (128^2 tiles, ~460 TF/s) it
+# would run slower: the vocab-sized classifier gradients stay per-layer
+GROUP_MAX_MNK = float(os.environ.get("TAM_GROUP_MAX_MNK", str(float(1 << 35))))
+
+
 def _group_ok(M: int, N: int, K: int) -> bool:
     key = (M, N, K)
     ok = _GROUP_OK.get(key)
     if ok is None:
-        ok = bool(_T().gemm_wgrad_grouped_ok(M, N, K))
+        ok = bool(_T().gemm_wgrad_grouped_ok(M, N, K)) and float(M) * N * K <= GROUP_MAX_MNK
         _GROUP_OK[key] = ok
     return ok
+
+
+def defer_problems(probs) -> bool:
+    """Defer a layer's weight-gradient problems [(dY, X, w, b, mode), ...]
+    into the backward's grouped launch when deferral is on (a model's own
+    grouped call, e.g. the LSTM's dW_hh / dW_ih); False: issue them now."""
+    if _DEFER_WGRAD is None:
+        return False
+    for it in probs:
+        if any(p[2] is it[2] for p in _DEFER_WGRAD):
+            flush_wgrad()            # a second write of the same weight: the pending one first
+            break
+    for it in probs:
+        _DEFER_WGRAD.append(tuple(it))
+        _deferred()
+    return True
 
 
 def deferred_count() -> int:
@@ -758,6 +780,32 @@ def batchnorm(x: torch.Tensor, g: Param, b: Param, run_mean: Optional[torch.Tens
 
 
 # ============================================================ LayerNorm
+# 1-GPU jobs: the LN weight-gradient column reduce runs on this side stream
+# (installed by the trainer, joined before the optimizer), beside the next
+# input-gradient GEMM instead of in front of it
+_AUX_STREAM = None
+LN_AUX = os.environ.get("TAM_LN_AUX", "1") != "0"
+
+
+def set_aux_stream(stream) -> None:
+    global _AUX_STREAM
+    _AUX_STREAM = stream
+
+
+def _ln_backward(dy, x, g: Param, b: Param, mean, rstd, dx, addend=None) -> None:
+    if _AUX_STREAM is None or not LN_AUX:
+        _T().ln_backward(dy, x, g.master, mean, rstd, dx, g.grad, b.grad, addend)
+        return
+    D = x.shape[-1]
+    ws = torch.empty(_LN_MAX_BLOCKS * 2 * D, dtype=torch.float32, device=x.device)
+    nblk = _T().ln_backward_split(dy, x, g.master, mean, rstd, dx, ws, addend)
+    with _OnWgrad(ws, stream=_AUX_STREAM):
+        _T().col_reduce_acc(ws, nblk, 2 * D, g.grad, b.grad, D)
+
+
+_LN_MAX_BLOCKS = 512        # csrc/include/tam/kernels.h LN_MAX_BLOCKS
+
+
 class _LN(Function):
     @staticmethod
     def forward(ctx, x, token, g: Param, b: Param, eps: float):
@@ -785,7 +833,7 @@ class _LN(Function):
         D = x.shape[-1]
         if dy.is_cuda:
             dx = torch.empty_like(x)
-            _T().ln_backward(dy, x, g.master, mean, rstd, dx, g.grad, b.grad)
+            _ln_backward(dy, x, g, b, mean, rstd, dx)
         else:
             rows = x.numel() // D
             xh = (x.float().reshape(rows, D) - mean[:, None]) * rstd[:, None]
@@ -826,8 +874,7 @@ class _LNSkip(_LN):
         dy = dy.contiguous()
         if dy.is_cuda:
             dx = torch.empty_like(x)
-            _T().ln_backward(dy, x, g.master, mean, rstd, dx, g.grad, b.grad,
-                             dskip.contiguous() if dskip is not None else None)
+            _ln_backward(dy, x, g, b, mean, rstd, dx, dskip.contiguous() if dskip is not None else None)
             g.grad_ready()
             b.grad_ready()
             return dx, None, None, None, None
