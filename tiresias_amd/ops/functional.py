@@ -780,11 +780,13 @@ def batchnorm(x: torch.Tensor, g: Param, b: Param, run_mean: Optional[torch.Tens
 
 
 # ============================================================ LayerNorm
-# 1-GPU jobs: the LN weight-gradient column reduce runs on this side stream
-# (installed by the trainer, joined before the optimizer), beside the next
-# input-gradient GEMM instead of in front of it
+# 1-GPU jobs: the LN weight-gradient column reduce CAN run on this side
+# stream (installed by the trainer, joined before the optimizer), beside the
+# next input-gradient GEMM. Off: measured much slower in hipGraph replay
+# (Transformer 5.49-5.57 vs 5.18 ms, same box: 32 fork / join pairs per
+# step); TAM_LN_AUX=1 for A/B
 _AUX_STREAM = None
-LN_AUX = os.environ.get("TAM_LN_AUX", "1") != "0"
+LN_AUX = os.environ.get("TAM_LN_AUX", "0") != "0"
 
 
 def set_aux_stream(stream) -> None:
