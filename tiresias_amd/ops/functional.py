@@ -503,11 +503,14 @@ class _Conv(Function):
         return dx, None, None, None, None, None, None, None, None, None
 
 
-# the re-laid weights are first read by the backward's dgrad: the re-lay runs
-# on a side stream beside the forward, and the first dgrad waits for it
+# the re-laid weights are first read by the backward's dgrad: the re-lay CAN
+# run on a side stream beside the forward, the first dgrad waiting for it.
+# Off: slower in hipGraph replay (same box, two runs each: ResNet-50 9.02-9.03
+# vs 8.88 ms, VGG-16 6.65 vs 6.61-6.62 ms -- a fork / join costs more than
+# the 60 us launch it hides); TAM_WT_SIDE=1 for A/B
 _WT_STREAMS: dict = {}     # compute stream -> its side stream (GPU-shared jobs stay independent)
 _WT_READY = None
-WT_SIDE = os.environ.get("TAM_WT_SIDE", "1") != "0"
+WT_SIDE = os.environ.get("TAM_WT_SIDE", "0") != "0"
 
 
 def prepare_conv_wt(params: List[Param]) -> None:
