@@ -782,6 +782,32 @@ void col_reduce_acc_op(const Tensor& part, int64_t nblk, int64_t W, const Tensor
                       (int)split, cur_stream(part));
 }
 
+// many col_reduce_acc in one launch: parts[i] [nblk[i]][W[i]] fp32 partial
+// rows; out0[i][c] += sum (c < split[i]), out1[i][c - split[i]] += sum
+void col_reduce_acc_batch_op(at::TensorList parts, at::IntArrayRef nblk, at::TensorList out0,
+                             at::TensorList out1) {
+  const size_t n = parts.size();
+  TORCH_CHECK(nblk.size() == n && out0.size() == n && out1.size() == n, "tam.col_reduce_acc_batch: list sizes");
+  if (n == 0) return;
+  std::vector<const float*> pp(n);
+  std::vector<float*> o0(n), o1(n);
+  std::vector<int> nb(n), W(n), sp(n);
+  for (size_t i = 0; i < n; ++i) {
+    check_f32(parts[i], "part"); check_f32(out0[i], "out0"); check_f32(out1[i], "out1");
+    sp[i] = (int)out0[i].numel();
+    W[i] = sp[i] + (int)out1[i].numel();
+    nb[i] = (int)nblk[i];
+    TORCH_CHECK(parts[i].is_contiguous() && parts[i].numel() >= (int64_t)nb[i] * W[i] &&
+                    out0[i].is_contiguous() && out1[i].is_contiguous() && parts[i].device() == parts[0].device(),
+                "tam.col_reduce_acc_batch: entry ", i);
+    pp[i] = parts[i].data_ptr<float>();
+    o0[i] = out0[i].data_ptr<float>();
+    o1[i] = out1[i].data_ptr<float>();
+  }
+  tam::col_reduce_acc_batch(pp.data(), nb.data(), W.data(), o0.data(), o1.data(), sp.data(), (int)n,
+                            cur_stream(parts[0]));
+}
+
 // ------------------------------------------------------------------ pooling
 void maxpool_forward_op(const Tensor& x, const Tensor& y, const Tensor& idx, int64_t R, int64_t S,
                         int64_t st, int64_t pad) {
@@ -1137,6 +1163,7 @@ TORCH_LIBRARY(tam, m) {
   m.def("ln_backward(Tensor dy, Tensor x, Tensor g, Tensor mean, Tensor rstd, Tensor(a!) dx, Tensor(b!) dg, Tensor(c!) db, Tensor? addend=None) -> ()", &ln_backward_op);
   m.def("ln_backward_split(Tensor dy, Tensor x, Tensor g, Tensor mean, Tensor rstd, Tensor(a!) dx, Tensor(b!) ws, Tensor? addend=None) -> int", &ln_backward_split_op);
   m.def("col_reduce_acc(Tensor part, int nblk, int W, Tensor(a!) out0, Tensor(b!) out1, int split) -> ()", &col_reduce_acc_op);
+  m.def("col_reduce_acc_batch(Tensor[] parts, int[] nblk, Tensor(a!)[] out0, Tensor(b!)[] out1) -> ()", &col_reduce_acc_batch_op);
   m.def("maxpool_forward(Tensor x, Tensor(a!) y, Tensor(b!) idx, int R, int S, int stride, int pad) -> ()", &maxpool_forward_op);
   m.def("maxpool_backward(Tensor dy, Tensor idx, Tensor(a!) dx, int R, int S, int stride, int pad) -> ()", &maxpool_backward_op);
   m.def("maxpool_k3s2_policy(int policy) -> ()", &maxpool_k3s2_policy_op);

@@ -19,6 +19,10 @@ constexpr int COLSUM_MAX_BLOCKS = 256;
 // out[c] = sum over nblk partial rows part[b][c] (width W): fp64 store, or fp32
 // accumulate into out0[c] (c < split) / out1[c - split]
 void col_reduce_f64(const float* part, int nblk, int W, double* out, hipStream_t s);
+constexpr int CR_BATCH_MAX = 48;   // column reduces per batched launch (kernel-argument budget)
+// col_reduce_acc over n (part, nblk, W, out0, out1, split) entries in one launch per 48
+void col_reduce_acc_batch(const float* const* part, const int* nblk, const int* W, float* const* out0,
+                          float* const* out1, const int* split, int n, hipStream_t s);
 void col_reduce_acc(const float* part, int nblk, int W, float* out0, float* out1, int split,
                     hipStream_t s);
 void bn_forward(const bf16_t* x, const bf16_t* res, bf16_t* y, long M, int C, float eps,

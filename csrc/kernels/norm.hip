@@ -62,6 +62,67 @@ __global__ void __launch_bounds__(256) col_reduce_kernel(const float* __restrict
   }
 }
 
+// Many column reduces in ONE launch (the deferred LayerNorm weight-gradient
+// reductions of a backward, ops/functional.py flush_wgrad): blocks
+// [c0_e, c0_{e+1}) serve entry e, 16 columns each, exactly as
+// col_reduce_kernel<1> would for that entry alone.
+struct ColRedBatch {
+  const float* part[CR_BATCH_MAX];
+  float* out0[CR_BATCH_MAX];
+  float* out1[CR_BATCH_MAX];
+  int nblk[CR_BATCH_MAX], W[CR_BATCH_MAX], split[CR_BATCH_MAX], c0[CR_BATCH_MAX + 1];
+  int n;
+};
+
+__global__ void __launch_bounds__(256) col_reduce_batch_kernel(ColRedBatch b) {
+  __shared__ double red[16][17];
+  int e = 0;
+  while (e + 1 < b.n && (int)blockIdx.x >= b.c0[e + 1]) ++e;
+  const float* __restrict__ part = b.part[e];
+  const int nblk = b.nblk[e], W = b.W[e], split = b.split[e];
+  const int cx = threadIdx.x & 15, ly = threadIdx.x >> 4;
+  const int c = ((int)blockIdx.x - b.c0[e]) * 16 + cx;
+  double s = 0.0;
+  if (c < W) {
+    int k = ly;
+    for (; k + 7 * 16 < nblk; k += 8 * 16) {
+      float v[8];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) v[u] = part[(long)(k + u * 16) * W + c];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) s += (double)v[u];
+    }
+    for (; k < nblk; k += 16) s += (double)part[(long)k * W + c];
+  }
+  red[ly][cx] = s;
+  __syncthreads();
+  if (ly == 0 && c < W) {
+    double t = 0.0;
+#pragma unroll
+    for (int k = 0; k < 16; ++k) t += red[k][cx];
+    if (c < split) b.out0[e][c] += (float)t;
+    else b.out1[e][c - split] += (float)t;
+  }
+}
+
+void col_reduce_acc_batch(const float* const* part, const int* nblk, const int* W, float* const* out0,
+                          float* const* out1, const int* split, int n, hipStream_t s) {
+  for (int base = 0; base < n; base += CR_BATCH_MAX) {
+    ColRedBatch b{};
+    const int m = n - base < CR_BATCH_MAX ? n - base : CR_BATCH_MAX;
+    int blocks = 0;
+    for (int i = 0; i < m; ++i) {
+      b.part[i] = part[base + i]; b.out0[i] = out0[base + i]; b.out1[i] = out1[base + i];
+      b.nblk[i] = nblk[base + i]; b.W[i] = W[base + i]; b.split[i] = split[base + i];
+      b.c0[i] = blocks;
+      blocks += (W[base + i] + 15) / 16;
+    }
+    b.c0[m] = blocks;
+    b.n = m;
+    if (blocks) hipLaunchKernelGGL(col_reduce_batch_kernel, dim3((unsigned)blocks), dim3(256), 0, s, b);
+  }
+}
+
 void col_reduce_f64(const float* part, int nblk, int W, double* out, hipStream_t s) {
   hipLaunchKernelGGL(col_reduce_kernel<0>, dim3((W + 15) / 16), dim3(256), 0, s, part, nblk, W, out,
                      (float*)nullptr, (float*)nullptr, W);

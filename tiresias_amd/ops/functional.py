@@ -113,6 +113,8 @@ def defer_wgrad(on: bool, discard: bool = False, expect: int = 0, stream=None) -
     _GROUP_STREAM = stream if on else None
     if not on and _DEFER_WGRAD and not discard:
         raise RuntimeError("defer_wgrad(False) with unflushed weight gradients")
+    if not on:
+        _DEFER_LNRED.clear()               # (an aborted step: its partial rows are dropped)
     if not on and _DEFER_WGRAD:
         for it in _DEFER_WGRAD:            # dropped writes: the next one must store (grad_mode)
             it[2].gw_epoch = -1
@@ -170,6 +172,14 @@ def flush_wgrad() -> int:
     """Issue every deferred weight gradient as one grouped launch (on the
     weight-gradient stream when one is installed), then signal grad_ready.
     Returns the number of problems flushed."""
+    if _DEFER_LNRED:
+        lnr = list(_DEFER_LNRED)
+        _DEFER_LNRED.clear()
+        _T().col_reduce_acc_batch([e[0] for e in lnr], [e[1] for e in lnr], [e[2].grad for e in lnr],
+                                  [e[3].grad for e in lnr])
+        for _, _, g, b in lnr:
+            g.grad_ready()
+            b.grad_ready()
     pend = _DEFER_WGRAD
     if not pend:
         return 0
@@ -797,15 +807,30 @@ def set_aux_stream(stream) -> None:
     _AUX_STREAM = stream
 
 
-def _ln_backward(dy, x, g: Param, b: Param, mean, rstd, dx, addend=None) -> None:
-    if _AUX_STREAM is None or not LN_AUX:
+# while weight gradients are deferred (trainer group_wgrad), a LayerNorm's
+# dgamma / dbeta column reduce is deferred too and every one of the backward
+# runs in ONE batched launch at the flush (Transformer-base: 32 reduce
+# launches per step -> 1); TAM_LN_DEFER=0 for A/B
+LN_DEFER = os.environ.get("TAM_LN_DEFER", "1") != "0"
+_DEFER_LNRED: list = []
+
+
+def _ln_backward(dy, x, g: Param, b: Param, mean, rstd, dx, addend=None) -> bool:
+    """LN backward; returns True when dgamma / dbeta were deferred to the
+    flush (their grad_ready() then comes from flush_wgrad)."""
+    deferred = _DEFER_WGRAD is not None and LN_DEFER
+    if not deferred and (_AUX_STREAM is None or not LN_AUX):
         _T().ln_backward(dy, x, g.master, mean, rstd, dx, g.grad, b.grad, addend)
-        return
+        return False
     D = x.shape[-1]
     ws = torch.empty(_LN_MAX_BLOCKS * 2 * D, dtype=torch.float32, device=x.device)
     nblk = _T().ln_backward_split(dy, x, g.master, mean, rstd, dx, ws, addend)
+    if deferred:
+        _DEFER_LNRED.append((ws, nblk, g, b))
+        return True
     with _OnWgrad(ws, stream=_AUX_STREAM):
         _T().col_reduce_acc(ws, nblk, 2 * D, g.grad, b.grad, D)
+    return False
 
 
 _LN_MAX_BLOCKS = 512        # csrc/include/tam/kernels.h LN_MAX_BLOCKS
@@ -838,7 +863,8 @@ class _LN(Function):
         D = x.shape[-1]
         if dy.is_cuda:
             dx = torch.empty_like(x)
-            _ln_backward(dy, x, g, b, mean, rstd, dx)
+            if _ln_backward(dy, x, g, b, mean, rstd, dx):
+                return dx, None, None, None, None
         else:
             rows = x.numel() // D
             xh = (x.float().reshape(rows, D) - mean[:, None]) * rstd[:, None]
@@ -879,9 +905,9 @@ class _LNSkip(_LN):
         dy = dy.contiguous()
         if dy.is_cuda:
             dx = torch.empty_like(x)
-            _ln_backward(dy, x, g, b, mean, rstd, dx, dskip.contiguous() if dskip is not None else None)
-            g.grad_ready()
-            b.grad_ready()
+            if not _ln_backward(dy, x, g, b, mean, rstd, dx, dskip.contiguous() if dskip is not None else None):
+                g.grad_ready()
+                b.grad_ready()
             return dx, None, None, None, None
         dx = _LN.backward(ctx, dy)[0]
         if dskip is not None:
