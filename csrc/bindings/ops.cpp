@@ -610,6 +610,60 @@ int64_t conv_dgrad_pre_op(const Tensor& dy, const Tensor& w, const Tensor& wt, c
 
 // dbias (optional, fp32 [K]): += the bias gradient colsum(dY), fused into the
 // wgrad kernel where it has the epilogue, else a column-sum pass
+// conv_wgrad_deferred: as conv_wgrad, but a slab-split pass leaves its
+// reduce to the caller: returns (slabs, sp) -- sp > 0: dw is NOT written yet;
+// wgrad_slab_reduce_many([slabs], [sp], [dw], [mode]) finishes it (batched
+// over a backward). sp == 0: dw is complete (slabs is empty)
+std::tuple<Tensor, int64_t> conv_wgrad_deferred_op(const Tensor& dy, const Tensor& x, const Tensor& dw,
+                                                   int64_t stride, int64_t pad, int64_t dil, int64_t mode,
+                                                   const optional<Tensor>& dbias, bool patch) {
+  check_bf16(dy, "dy"); check_bf16(x, "x"); check_f32(dw, "dw");
+  check_contig(dy, "dy"); check_contig(x, "x"); check_contig(dw, "dw");
+  TORCH_CHECK(dw.dim() == 4, "tam.conv_wgrad_deferred: dw must be [K,R,S,C]");
+  tam::ConvGeom g = geom(x, dw, dy, stride, pad, dil);
+  tam::Epi ep;
+  ep.c = dw.data_ptr(); ep.ldc = g.R * g.S * g.C; ep.c_f32 = 1; ep.mode = (int)mode;
+  float* db = nullptr;
+  if (dbias.has_value() && dbias->defined()) {
+    check_f32(*dbias, "dbias");
+    TORCH_CHECK(dbias->numel() == g.K && dbias->is_contiguous(), "tam.conv_wgrad_deferred: dbias size");
+    db = dbias->data_ptr<float>();
+  }
+  const long wsf = tam::conv_wgrad_split_ws(g);
+  Tensor wsl = at::empty({wsf > 0 ? wsf : 0}, dy.options().dtype(at::kFloat));
+  int sp = 0;
+  const int fused = tam::conv_wgrad(bp(dy), bp(x), g, ep, cur_stream(dy), db, patch,
+                                    wsf > 0 ? wsl.data_ptr<float>() : nullptr, wsf, &sp);
+  if (db && !fused) {
+    const long R = (long)g.N * g.P * g.Q;
+    Tensor ws = at::empty({g.K % 8 == 0 ? (int64_t)tam::COLSUM_MAX_BLOCKS * g.K : 1}, dy.options().dtype(at::kFloat));
+    tam::colsum(bp(dy), db, ws.data_ptr<float>(), R, g.K, cur_stream(dy));
+  }
+  return {sp > 0 ? wsl : at::empty({0}, dy.options().dtype(at::kFloat)), (int64_t)sp};
+}
+
+void wgrad_slab_reduce_many_op(at::TensorList slabs, at::IntArrayRef sp, at::TensorList dw, at::IntArrayRef mode) {
+  const size_t n = slabs.size();
+  TORCH_CHECK(sp.size() == n && dw.size() == n && mode.size() == n, "tam.wgrad_slab_reduce_many: list sizes");
+  if (n == 0) return;
+  std::vector<const float*> ws(n);
+  std::vector<float*> out(n);
+  std::vector<int> s(n), md(n);
+  std::vector<long> mn(n);
+  for (size_t i = 0; i < n; ++i) {
+    check_f32(slabs[i], "slab"); check_f32(dw[i], "dw");
+    TORCH_CHECK(dw[i].is_contiguous() && dw[i].numel() % 4 == 0 && sp[i] > 0 &&
+                    slabs[i].numel() >= sp[i] * dw[i].numel(),
+                "tam.wgrad_slab_reduce_many: entry ", i);
+    ws[i] = slabs[i].data_ptr<float>();
+    out[i] = dw[i].data_ptr<float>();
+    s[i] = (int)sp[i];
+    md[i] = (int)mode[i];
+    mn[i] = (long)dw[i].numel();
+  }
+  tam::wgrad_slab_reduce_many(ws.data(), s.data(), mn.data(), out.data(), md.data(), (int)n, cur_stream(dw[0]));
+}
+
 void conv_wgrad_op(const Tensor& dy, const Tensor& x, const Tensor& dw, int64_t stride, int64_t pad,
                    int64_t dil, int64_t mode, const optional<Tensor>& dbias, bool patch) {
   check_bf16(dy, "dy"); check_bf16(x, "x"); check_f32(dw, "dw");
@@ -1157,6 +1211,8 @@ TORCH_LIBRARY(tam, m) {
   m.def("gemm_grouped_tile(int tile) -> ()", &gemm_grouped_tile_op);
   m.def("conv_dgrad_pre(Tensor dy, Tensor w, Tensor wt, Tensor(a!) dx, int stride, int pad, int dil, Tensor? mask, Tensor(b!)? stats=None, Tensor? bnx=None, Tensor? bnmean=None, Tensor? bnrstd=None) -> int", &conv_dgrad_pre_op);
   m.def("conv_wgrad(Tensor dy, Tensor x, Tensor(a!) dw, int stride, int pad, int dil, int mode, Tensor(b!)? dbias=None, bool patch=True) -> ()", &conv_wgrad_op);
+  m.def("conv_wgrad_deferred(Tensor dy, Tensor x, Tensor(a!) dw, int stride, int pad, int dil, int mode, Tensor(b!)? dbias, bool patch) -> (Tensor, int)", &conv_wgrad_deferred_op);
+  m.def("wgrad_slab_reduce_many(Tensor[] slabs, int[] sp, Tensor(a!)[] dw, int[] mode) -> ()", &wgrad_slab_reduce_many_op);
   m.def("bn_forward(Tensor x, Tensor? res, Tensor(a!) y, Tensor gamma, Tensor beta, Tensor(b!)? run_mean, Tensor(c!)? run_var, Tensor(d!) save_mean, Tensor(e!) save_rstd, float eps, float momentum, bool relu, Tensor(f!)? sums=None, bool sums_ready=False, Tensor(g!)? ymask=None) -> ()", &bn_forward_op);
   m.def("bn_backward(Tensor dy, Tensor? y, Tensor x, Tensor mean, Tensor rstd, Tensor gamma, Tensor(a!) dx, Tensor(b!)? dres, Tensor(c!)? dgamma, Tensor(d!)? dbeta, bool relu, Tensor? addend=None, Tensor(e!)? sums=None, bool sums_ready=False, Tensor? ymask=None) -> ()", &bn_backward_op);
   m.def("ln_forward(Tensor x, Tensor g, Tensor b, Tensor(a!) y, Tensor(b!) mean, Tensor(c!) rstd, float eps, Tensor? addend=None, Tensor(d!)? sum_out=None) -> ()", &ln_forward_op);

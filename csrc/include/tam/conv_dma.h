@@ -1394,9 +1394,11 @@ inline long wgrad_dma_slab_floats(const ConvGeom& g, bool force) {
 
 // dw = (mode ? dw : 0) + conv wgrad
 // ws / ws_floats: slab scratch of wgrad_dma_slab_floats(g) floats (else atomics)
+// slab_defer (non-null): a slab launch leaves the reduce to the caller and
+// reports its slab count there (*slab_defer = splits; 0: nothing deferred)
 inline bool launch_conv_wgrad_dma(const bf16_t* dy, const bf16_t* x, float* dw, const ConvGeom& g,
                                   int mode, hipStream_t s, bool force = false, float* dbias = nullptr,
-                                  float* ws = nullptr, long ws_floats = 0) {
+                                  float* ws = nullptr, long ws_floats = 0, int* slab_defer = nullptr) {
   const WGPlan p = wgrad_dma_plan(g, force);
   if (!p.ok) return false;
   const int ncols = g.R * g.S * g.C;
@@ -1413,7 +1415,8 @@ inline bool launch_conv_wgrad_dma(const bf16_t* dy, const bf16_t* x, float* dw, 
   else if (bm == 128 && bn == 128) wgrad_dma_launch<128, 128, 2, 2>(a, p.tiles, p.splits, s);
   else if (bm == 128) wgrad_dma_launch<128, 64, 2, 2>(a, p.tiles, p.splits, s);
   else wgrad_dma_launch<64, 64, 2, 2>(a, p.tiles, p.splits, s);
-  if (slab) wgrad_slab_reduce(ws, p.splits, (long)g.K * ncols, dw, mode, s);
+  if (slab && slab_defer) *slab_defer = p.splits;
+  else if (slab) wgrad_slab_reduce(ws, p.splits, (long)g.K * ncols, dw, mode, s);
   return true;
 }
 

@@ -40,6 +40,10 @@ struct GGProblem {
   int mode = 1;      // 0: C = A^T B (store), 1: C += A^T B
 };
 void gemm_wgrad_grouped(const GGProblem* probs, int n, hipStream_t s);
+// deferred conv weight-gradient slab reduces, one launch per 40:
+// dw[e] = (mode[e] ? dw[e] : 0) + sum_z ws[e][z][:mn[e]]
+void wgrad_slab_reduce_many(const float* const* ws, const int* sp, const long* mn, float* const* dw,
+                            const int* mode, int n, hipStream_t s);
 bool gemm_wgrad_grouped_ok(int M, int N, int K, long lda, long ldb);
 void gemm_grouped_tile(int t);   // 128 (default) or 256
 
@@ -76,7 +80,8 @@ int conv_dgrad(const bf16_t* dy, const bf16_t* w, const bf16_t* wt, const ConvGe
 // dw[K][R*S*C] fp32, ep.mode 0 (overwrite) or 1 (accumulate)
 // ws / ws_floats: slab split-K scratch of conv_wgrad_split_ws(g) floats (none: atomics)
 int conv_wgrad(const bf16_t* dy, const bf16_t* x, const ConvGeom& g, Epi ep, hipStream_t s,
-               float* dbias = nullptr, bool allow_patch = true, float* ws = nullptr, long ws_floats = 0);
+               float* dbias = nullptr, bool allow_patch = true, float* ws = nullptr, long ws_floats = 0,
+               int* slab_defer = nullptr);
 long conv_wgrad_split_ws(const ConvGeom& g);
 void conv_wgrad_slab_policy(int p);   // 1: slab split-K for the DMA wgrad (default), 0: fp32 atomics
 void conv_weight_t(const bf16_t* w, bf16_t* wt, const ConvGeom& g, hipStream_t s);

@@ -239,7 +239,8 @@ long conv_wgrad_split_ws(const ConvGeom& g) {
 // starves co-running kernels: VGG-16's graph step with the weight gradients
 // on the side stream measured 7.42 -> 7.52 ms with it)
 int conv_wgrad(const bf16_t* dy, const bf16_t* x, const ConvGeom& g, Epi ep, hipStream_t s, float* dbias,
-               bool allow_patch, float* ws, long ws_floats) {
+               bool allow_patch, float* ws, long ws_floats, int* slab_defer) {
+  if (slab_defer) *slab_defer = 0;
   const int Mred = g.N * g.P * g.Q, Nc = g.R * g.S * g.C;
   if (!dbias && ep.c_f32 && ep.ldc == Nc && ep.mode <= 1 &&
       conv_stem_wgrad(dy, x, g, (float*)ep.c, ep.mode, ws, ws_floats, s))   // 7x7/s2 8->64 stem
@@ -259,7 +260,8 @@ int conv_wgrad(const bf16_t* dy, const bf16_t* x, const ConvGeom& g, Epi ep, hip
   // stay on the DMA kernel (19.6 vs 57 us at 64->64)
   const bool pw_gemm = is_pointwise(g) && Mred < 100352 && g_conv_dma < 2;
   if (g_conv_dma && !pw_gemm && ep.c_f32 && ep.ldc == Nc && ep.mode <= 1 &&
-      launch_conv_wgrad_dma(dy, x, (float*)ep.c, g, ep.mode, s, g_conv_dma >= 2, dbias, ws, ws_floats))
+      launch_conv_wgrad_dma(dy, x, (float*)ep.c, g, ep.mode, s, g_conv_dma >= 2, dbias, ws, ws_floats,
+                            slab_defer))
     return dbias ? 1 : 0;
   if (is_pointwise(g)) {
     // dW[k][c] = sum_m dY[m][k] X[m][c]: A(k', m) = dY[m*K + k'], B(m, c) = X[m*C + c]
@@ -290,6 +292,11 @@ int conv_wgrad(const bf16_t* dy, const bf16_t* x, const ConvGeom& g, Epi ep, hip
     default: wgrad_tile<64, 64>(dy, x, g, ep, t.splits, s); break;
   }
   return dbias ? 1 : 0;
+}
+
+void wgrad_slab_reduce_many(const float* const* ws, const int* sp, const long* mn, float* const* dw,
+                            const int* mode, int n, hipStream_t s) {
+  wgrad_slab_reduce_batch(ws, sp, mn, dw, mode, n, s);
 }
 
 // wt[c][(r*S+s)*K + k] = w[k][(r*S+s)*C + c]

@@ -54,7 +54,9 @@ MODELS: Dict[str, ModelSpec] = {
     # the 1x1 / stride-1 conv weight gradients (stages 1-3) as one K-split
     # grouped launch at the end of the backward (ops/functional.py _Conv)
     "resnet50": ModelSpec(ResNet50, "image", 64, "sgd", 0.1, 1e-4, group_wgrad=True),
-    "vgg16": ModelSpec(VGG16, "image", 32, "sgd", 0.01, 5e-4),
+    # (no layer of VGG-16 is grouped-eligible; deferral here batches the
+    # slab-split conv weight-gradient reduces into one launch per backward)
+    "vgg16": ModelSpec(VGG16, "image", 32, "sgd", 0.01, 5e-4, group_wgrad=True),
     # weight-gradient side stream: measured per model (profiles/r2/ab_overlap.txt,
     # hipGraph steps): Transformer 7.28 -> 7.14 ms on; ResNet-50 10.65 -> 11.01
     # and GNMT 10.87 -> 11.93 (the persistent recurrence loses its CUs) off.

@@ -115,6 +115,7 @@ def defer_wgrad(on: bool, discard: bool = False, expect: int = 0, stream=None) -
         raise RuntimeError("defer_wgrad(False) with unflushed weight gradients")
     if not on:
         _DEFER_LNRED.clear()               # (an aborted step: its partial rows are dropped)
+        _DEFER_SLABS.clear()
     if not on and _DEFER_WGRAD:
         for it in _DEFER_WGRAD:            # dropped writes: the next one must store (grad_mode)
             it[2].gw_epoch = -1
@@ -172,6 +173,13 @@ def flush_wgrad() -> int:
     """Issue every deferred weight gradient as one grouped launch (on the
     weight-gradient stream when one is installed), then signal grad_ready.
     Returns the number of problems flushed."""
+    if _DEFER_SLABS:
+        sl = list(_DEFER_SLABS)
+        _DEFER_SLABS.clear()
+        _T().wgrad_slab_reduce_many([e[0] for e in sl], [e[1] for e in sl], [e[2].grad for e in sl],
+                                    [1] * len(sl))
+        for e in sl:
+            e[2].grad_ready()
     if _DEFER_LNRED:
         lnr = list(_DEFER_LNRED)
         _DEFER_LNRED.clear()
@@ -451,6 +459,7 @@ class _Conv(Function):
                 dy = (dy.float() * (y.float() > 0)).to(BF16)
         dx = None
         deferred = False
+        slab_deferred = False
         if dy.is_cuda:
             K, R, S, C = w.shape
             Mr = dy.numel() // K
@@ -472,7 +481,16 @@ class _Conv(Function):
                     # write costs a zero pass of dW on the fp32-atomic split paths
                     # (ResNet-50: 29 more zero launches per step when conv weights
                     # were store_grad), the optimizer's bulk zeroing does not
-                    _T().conv_wgrad(dy, x, w.grad, st, pd, 1, 1, b.grad if b is not None else None, ow.s is None)
+                    if _DEFER_WGRAD is not None and SLAB_DEFER and ow.s is None:
+                        slabs, sp = _T().conv_wgrad_deferred(dy, x, w.grad, st, pd, 1, 1,
+                                                             b.grad if b is not None else None, True)
+                        if sp > 0:
+                            # dW itself is written by the batched reduce at the flush
+                            _DEFER_SLABS.append((slabs, sp, w))
+                            slab_deferred = True
+                    else:
+                        _T().conv_wgrad(dy, x, w.grad, st, pd, 1, 1, b.grad if b is not None else None,
+                                        ow.s is None)
             if ctx.needs_input_grad[0]:
                 dx = torch.empty_like(x)
                 wt = getattr(w, "wt", None)
@@ -504,7 +522,10 @@ class _Conv(Function):
             w.grad += grads[-1].permute(0, 2, 3, 1)
             if b is not None:
                 b.grad += dy.float().sum((0, 1, 2))
-        if deferred:
+        if slab_deferred:
+            if b is not None:                  # the bias gradient is complete now
+                b.grad_ready()
+        elif deferred:
             _deferred()
         else:
             w.grad_ready()
@@ -813,6 +834,10 @@ def set_aux_stream(stream) -> None:
 # launches per step -> 1); TAM_LN_DEFER=0 for A/B
 LN_DEFER = os.environ.get("TAM_LN_DEFER", "1") != "0"
 _DEFER_LNRED: list = []
+# ...and a slab-split conv weight gradient's slab reduce likewise (ResNet-50:
+# 24 reduce launches per step -> 1); TAM_SLAB_DEFER=0 for A/B
+SLAB_DEFER = os.environ.get("TAM_SLAB_DEFER", "1") != "0"
+_DEFER_SLABS: list = []
 
 
 def _ln_backward(dy, x, g: Param, b: Param, mean, rstd, dx, addend=None) -> bool:
