@@ -206,6 +206,10 @@ class Engine {
   // whenever no consolidated block is free), true = wait-vs-spread
   // (engine/spread.py; needs set_costs' per-job spread parameters)
   void set_spread_wait(bool on) { spread_wait_ = on; }
+  // spread_rule "node": a gang that fits one node is never fragmented across
+  // nodes (it waits for a free node; the wait-vs-spread rule decides only
+  // for gangs wider than a node)
+  void set_spread_node(bool on) { spread_node_ = on; }
   // preemptive policies on topology placements: lazy (default) or eager
   void set_lazy_preempt(bool on) { lazy_ = on; }
   long spread_decisions(bool spread) const { return spread ? n_spread_ : n_wait_; }
@@ -752,6 +756,7 @@ class Engine {
         return fa != fb ? fa < fb : a < b;
       });
       if (single_node(j, best, plan)) return true;
+      if (spread_node_) return false;
     }
     if (!fill(j, order, plan)) return false;
     std::vector<int> nd;
@@ -909,7 +914,7 @@ class Engine {
   bool lazy_ = true;
   Place place_ = P_COUNT;
   Costs costs_;
-  bool spread_wait_ = false, svc_online_ = true;
+  bool spread_wait_ = false, spread_node_ = false, svc_online_ = true;
   std::vector<double> svc_init_;
   ServiceEst svc_;
   mutable long n_spread_ = 0, n_wait_ = 0;

@@ -86,9 +86,10 @@ def define_flags() -> None:
     D.DEFINE_string("gandiva_mem_util", "one", "gandiva-ns job slot size: one|legacy|measured")
     D.DEFINE_boolean("replace_all", False, "re-place every runnable job at each event (legacy Tiresias)")
     D.DEFINE_float("skew_threshold", 0.5, "placement-sensitivity threshold (largest tensor / total)")
-    D.DEFINE_string("spread_rule", "wait", "tiresias placement, insensitive gangs: fragments (spread "
+    D.DEFINE_string("spread_rule", "node", "tiresias placement, insensitive gangs: fragments (spread "
                     "whenever no consolidated block is free) | wait (spread only when the expected wait "
-                    "for a block exceeds the spread penalty, engine/spread.py)")
+                    "for a block exceeds the spread penalty, engine/spread.py) | node (as wait, but a gang "
+                    "that fits one node is never fragmented)")
     D.DEFINE_string("preempt_rule", "lazy", "preemptive policies: lazy (preempt only what a chosen job's "
                     "placement needs) | eager (every running job outside the priority prefix)")
     D.DEFINE_boolean("ddp_shard", False, "live gangs: reduce-scatter + sharded optimizer + bf16 all-gather "
@@ -179,7 +180,7 @@ class SimConfig:
     gandiva_mem_util: str = "one"
     replace_all: bool = False
     skew_threshold: float = 0.5
-    spread_rule: str = "wait"          # tiresias placement: wait | fragments (engine/spread.py)
+    spread_rule: str = "node"          # tiresias placement: node | wait | fragments (engine/spread.py)
     preempt_rule: str = "lazy"         # preemptive policies: lazy | eager (engine/sim.py::_schedule_lazy)
     ddp_shard: bool = False            # live gangs: sharded data parallelism (parallel/ddp.py)
     ddp_wire: str = "fp32"             # sharded gangs: reduce-scatter dtype fp32 | bf16

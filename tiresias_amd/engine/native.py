@@ -60,9 +60,11 @@ def simulate_native(cfg: SimConfig, specs: List[JobSpec], prior: Optional[List[f
     eng = _sched_core.Engine(cfg.schedule, cfg.cluster.num_gpus, [float(x) for x in limits],
                              float(cfg.solve_starvation), float(cfg.gittins_delta or 3250.0),
                              [float(x) for x in prior], online)
-    wait_rule = scheme == "tiresias" and getattr(cfg, "spread_rule", "wait") == "wait"
+    rule = getattr(cfg, "spread_rule", "node")
+    wait_rule = scheme == "tiresias" and rule in ("wait", "node")
     priced = _set_costs(eng, cfg, specs, force=wait_rule)
     eng.set_spread_wait(wait_rule)
+    eng.set_spread_node(scheme == "tiresias" and rule == "node")
     eng.set_lazy_preempt(getattr(cfg, "preempt_rule", "lazy") == "lazy")
     t0 = time.perf_counter()
     sub_a = np.array([s.submit_time for s in specs], dtype=np.float64)

@@ -96,9 +96,11 @@ class Simulator:
         # its job durations are iteration counts)
         self.iter_s_of = lambda j: (j.spec.duration / j.spec.iterations
                                     if j.spec.iterations and j.spec.iterations > 0 else 0.25)
-        if scheme == "tiresias" and getattr(cfg, "spread_rule", "wait") == "wait":
+        rule = getattr(cfg, "spread_rule", "node")
+        if scheme == "tiresias" and rule in ("wait", "node"):
             self.placement.advisor = SpreadAdvisor(self._remaining_wall, self._spread_rate)
             self.placement.jobs_by_id = self.jobs
+            self.placement.spread_node_gangs = rule != "node"
         self.now = 0.0
         self.active: List[Job] = []
         self.finished: List[Job] = []

@@ -141,6 +141,9 @@ class Placement:
         # insensitive gangs, and the engine's job table it consults
         self.advisor = None
         self.jobs_by_id: Optional[Dict[str, Job]] = None
+        # with the advisor: may a gang that fits one node be fragmented?
+        # (spread_rule "wait": yes, when the rule says so; "node": never)
+        self.spread_node_gangs = True
 
     def plan(self, cluster: Cluster, job: Job) -> Optional[Plan]:
         raise NotImplementedError
@@ -421,6 +424,12 @@ class TiresiasPlacement(Placement):
             p = _single_node(cluster, job, best)
             if p is not None:
                 return p
+            if not self.spread_node_gangs:
+                # spread_rule "node": a gang that fits one node waits for one
+                # (spreading it trades a short wait for a slower rate over its
+                # whole run AND fragments the nodes the gangs queued behind it
+                # need; priced 10k sweep, profiles/r5/spread_node_rule.md)
+                return None
         p = _fill(cluster, job, order)
         if p is None:
             return None
