@@ -757,6 +757,11 @@ class Engine {
       });
       if (single_node(j, best, plan)) return true;
       if (spread_node_) return false;
+    } else if (spread_node_) {   // wider than a node: fullest-free nodes first
+      std::stable_sort(order.begin(), order.end(), [&](int a, int b) {
+        const int fa = topo_.nfree(a), fb = topo_.nfree(b);
+        return fa != fb ? fa > fb : a < b;
+      });
     }
     if (!fill(j, order, plan)) return false;
     std::vector<int> nd;

@@ -215,16 +215,24 @@ def test_tiresias_node_rule_never_fragments_node_sized_gangs():
     assert len({nid for nid, _ in pl.plan(c, r2)}) == 1
     c8 = _cluster(nodes=3, gpn=4)
     c8.commit(Job(spec(7, g=2)), [("1", (0,)), ("1", (1,))])
-    r8 = Job(spec(3, g=8, model="resnet50"))                      # wider than a node: the advisor decides
+    r8 = Job(spec(3, g=8, model="resnet50"))                      # wider than a node: fullest-free first
+    assert sorted({nid for nid, _ in pl.plan(c8, r8)}) == ["2", "3"]
+    pl.spread_node_gangs = True                                   # rule "wait": fragments first
     assert len({nid for nid, _ in pl.plan(c8, r8)}) == 3
+    pl.spread_node_gangs = False
+    c8.commit(Job(spec(6, g=1)), [("2", (0,))])                   # no 2 whole nodes left: the advisor decides
+    n0 = Always.decisions["spread"]
+    assert len({nid for nid, _ in pl.plan(c8, r8)}) == 3
+    assert Always.decisions["spread"] == n0 + 1
 
 
 def test_priced_node_rule_vs_wait_rule_and_yarn():
     """Priced replay (measured checkpoint stalls, spread gangs at the
     network-limited rate), lazy preemption, Gittins, 3000 Philly-shaped jobs
-    on 64 GPUs, 3 seeds: the node rule (a node-sized gang never fragments)
-    beats the wait rule on avg JCT on every seed and stays within 3 % of
-    consolidate-always on average (wait: +11-19 %); the native core matches
+    on 64 GPUs, 3 seeds: the node rule (a node-sized gang never fragments, a
+    wider one packs the fullest-free nodes) beats both yarn's
+    consolidate-always placement (measured 0.93-0.97x) and the round-4 wait
+    rule (1.11-1.19x yarn) on avg JCT on every seed; the native core matches
     the Python engine on the node-rule replay (profiles/r5/spread_node_rule.md)."""
     import dataclasses
     import os
@@ -258,7 +266,7 @@ def test_priced_node_rule_vs_wait_rule_and_yarn():
         os.remove(prior)
         assert jct[("tiresias", "node")] < jct[("tiresias", "wait")], (seed, jct)
         ratios.append(jct[("tiresias", "node")] / jct[("yarn", "node")])
-    assert sum(ratios) / len(ratios) < 1.03, ratios
+    assert max(ratios) < 0.99, ratios
 
 
 def test_horus_prefers_low_cost_and_colocates():

@@ -430,6 +430,10 @@ class TiresiasPlacement(Placement):
                 # whole run AND fragments the nodes the gangs queued behind it
                 # need; priced 10k sweep, profiles/r5/spread_node_rule.md)
                 return None
+        elif not self.spread_node_gangs:
+            # ... and a gang wider than a node packs the fullest-free nodes
+            # first (fewest nodes, no fragment of a busy node unless needed)
+            order = sorted(cluster.nodes, key=lambda nid: (-cluster.nodes[nid].num_free_gpus(), int(nid)))
         p = _fill(cluster, job, order)
         if p is None:
             return None
