@@ -184,6 +184,24 @@ def test_resnet50_grouped_conv_wgrad_matches(gpu, monkeypatch):
     torch.cuda.synchronize()
     assert a._gs is not None and len(calls) == 3 and calls[1] == a._defer_n and calls[2] == 0, calls
     assert rel(a.arena.grad, b.arena.grad) < 2e-3
+    # third backward: slab-split 3x3 conv weight gradients' reduces deferred
+    # into the flush's one batched launch (TAM_SLAB_DEFER, off by default)
+    monkeypatch.setattr(a.spec, "group_early", False)
+    monkeypatch.setattr(Fx, "SLAB_DEFER", True)
+
+    class Seen(list):
+        n = 0
+
+        def append(self, x):
+            Seen.n += 1
+            super().append(x)
+    monkeypatch.setattr(Fx, "_DEFER_SLABS", Seen())
+    a.arena.grad.zero_()
+    a._fwd_bwd()
+    torch.cuda.synchronize()
+    assert Seen.n >= 4 and not Fx._DEFER_SLABS, Seen.n
+    assert rel(a.arena.grad, b.arena.grad) < 2e-3
+    monkeypatch.setattr(Fx, "SLAB_DEFER", False)
     monkeypatch.setattr(Fx, "flush_wgrad", real)
     g = Trainer("resnet50", gpu, seed=6, batch=32, use_graph=True)
     e = Trainer("resnet50", gpu, seed=6, batch=32)

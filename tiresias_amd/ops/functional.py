@@ -835,8 +835,11 @@ def set_aux_stream(stream) -> None:
 LN_DEFER = os.environ.get("TAM_LN_DEFER", "1") != "0"
 _DEFER_LNRED: list = []
 # ...and a slab-split conv weight gradient's slab reduce likewise (ResNet-50:
-# 24 reduce launches per step -> 1); TAM_SLAB_DEFER=0 for A/B
-SLAB_DEFER = os.environ.get("TAM_SLAB_DEFER", "1") != "0"
+# 24 reduce launches per step -> 1). Measured neutral in graph replay
+# (ResNet-50 8.92-8.94 vs 8.91-8.93 ms, VGG-16 6.67-6.68 vs 6.62-6.67, same
+# box) while it holds every slab conv's gradient back to the flush, which
+# delays the DDP buckets: off by default, TAM_SLAB_DEFER=1 to enable
+SLAB_DEFER = os.environ.get("TAM_SLAB_DEFER", "0") != "0"
 _DEFER_SLABS: list = []
 
 
