@@ -1173,13 +1173,18 @@ bool lstm_seq_bwd_op(const Tensor& act, const Tensor& cs, const Tensor& dH, cons
   check_sync(sync, B);
   TORCH_CHECK(w_hh.is_contiguous() && w_hh.size(0) == 4 * Hd && w_hh.size(1) == Hd,
               "tam.lstm_seq_backward: w_hh [4Hd][Hd]");
-  TORCH_CHECK(act.is_contiguous() && act.numel() == T * B * 5 * Hd && dH.is_contiguous() &&
-              dH.numel() == T * B * Hd && dG.is_contiguous() && dG.numel() == T * B * 4 * Hd,
-              "tam.lstm_seq_backward: act / dH / dG shapes");
+  // dH: contiguous [T][B][Hd], or a [T][B][Hd] column slice of a wider row
+  // (row pitch ldh = stride(1), stride(0) = B * ldh): read in place
+  TORCH_CHECK(dH.dim() == 3 && dH.size(0) == T && dH.size(1) == B && dH.size(2) == Hd && dH.stride(2) == 1 &&
+                  dH.stride(1) >= Hd && dH.stride(0) == B * dH.stride(1),
+              "tam.lstm_seq_backward: dH [T][B][Hd] with unit column stride and uniform row pitch");
+  TORCH_CHECK(act.is_contiguous() && act.numel() == T * B * 5 * Hd && dG.is_contiguous() &&
+                  dG.numel() == T * B * 4 * Hd,
+              "tam.lstm_seq_backward: act / dG shapes");
   int* sp = sync.data_ptr<int>();
   return tam::lstm_seq_backward(act.data_ptr<float>(), cs.data_ptr<float>(), (const float*)dH.data_ptr(),
                                 bp(w_hh), bpm(dG), (int)T, (int)B, (int)Hd, reverse ? 1 : 0, (unsigned*)sp,
-                                dh_bf16, cur_stream(act), pl_opts(job_err, grids, rsv, zeroed));
+                                dh_bf16, (int)dH.stride(1), cur_stream(act), pl_opts(job_err, grids, rsv, zeroed));
 }
 
 void lstm_seq_policy_op(int64_t ch) { tam::lstm_seq_policy((int)ch); }

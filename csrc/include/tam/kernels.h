@@ -139,8 +139,9 @@ struct PLOpts {
 };
 bool lstm_seq_forward(const float* gx, const bf16_t* w_hh, bf16_t* hs, float* cs, float* act, int T,
                       int B, int Hd, int reverse, unsigned* sync, hipStream_t s, const PLOpts& o = PLOpts());
+// dH: [T][B] rows of Hd values at row pitch ldh (>= Hd; elements)
 bool lstm_seq_backward(const float* act, const float* cs, const float* dH, const bf16_t* w_hh, bf16_t* dG,
-                       int T, int B, int Hd, int reverse, unsigned* sync, int dh_bf16, hipStream_t s,
+                       int T, int B, int Hd, int reverse, unsigned* sync, int dh_bf16, int ldh, hipStream_t s,
                        const PLOpts& o = PLOpts());
 // the job's guard word after its optimizer step: err[0] != 0 (a timed-out
 // barrier this step; the optimizer skipped the update) -> err[1] += 1, err[0] = 0

@@ -351,7 +351,7 @@ template <int KW, int CH>   // KW: k-steps of 32 per wave = 4 Hd / (32 * PL_W)
 __global__ void __launch_bounds__(64 * PL_W * CH, 4) lstm_persist_bwd_kernel(
     const float* __restrict__ act, const float* __restrict__ cs, const float* __restrict__ dH,
     const bf16_t* __restrict__ w, bf16_t* dG, int T, int B, int Hd, int reverse, unsigned* sync, int ns,
-    int dh_bf16, unsigned* job_err) {
+    int dh_bf16, int ldh, unsigned* job_err) {
   constexpr int U = 16 * CH;
   // W fragments: the first KWR k-steps in VGPRs, the rest in LDS (the whole
   // slice in VGPRs needs > 128 of them and spills; CH = 1 only: 2 blocks/CU
@@ -404,8 +404,10 @@ __global__ void __launch_bounds__(64 * PL_W * CH, 4) lstm_persist_bwd_kernel(
     const int fwd_idx = reverse ? T - 1 - t : t;
     const long row = (long)t * B + b0 + cr;
     const int j = j0 + cu;
-    // dH is the layer output's gradient as autograd hands it (bf16), or fp32
-    nx_dh = dh_bf16 ? bf2f(((const bf16_t*)dH)[row * Hd + j]) : dH[row * Hd + j];
+    // dH is the layer output's gradient as autograd hands it (bf16), or fp32;
+    // row pitch ldh >= Hd: a column slice of a wider gradient (the backward
+    // of a feature concat) is read in place, with no gather copy
+    nx_dh = dh_bf16 ? bf2f(((const bf16_t*)dH)[row * ldh + j]) : dH[row * ldh + j];
     const float* a = act + row * 5 * Hd + j;
 #pragma unroll
     for (int q = 0; q < 5; ++q) nx_a[q] = a[(long)q * Hd];
@@ -564,14 +566,15 @@ static bool pl_fwd(const float* gx, const bf16_t* w_hh, bf16_t* hs, float* cs, f
 
 template <int KW, int CH>
 static bool pl_bwd(const float* act, const float* cs, const float* dH, const bf16_t* w_hh, bf16_t* dG, int T,
-                   int B, int Hd, int reverse, unsigned* sync, int dh_bf16, const PLOpts& o, hipStream_t s) {
+                   int B, int Hd, int reverse, unsigned* sync, int dh_bf16, int ldh, const PLOpts& o,
+                   hipStream_t s) {
   const int grid = (B / 16) * (Hd / (16 * CH));
   auto k = lstm_persist_bwd_kernel<KW, CH>;
   if (!pl_fits((const void*)k, 64 * PL_W * CH, grid, o.grids, o.rsv)) return false;
   const int ns = (Hd / (16 * CH)) % g_pl_ns == 0 ? g_pl_ns : 1;
   if (!o.zeroed) zero_async(sync, (size_t)(1 + (B / 16) * ns) * 128, s);   // error flag line + counters
   hipLaunchKernelGGL(k, dim3(grid), dim3(64 * PL_W * CH), 0, s, act, cs, dH, w_hh, dG, T, B, Hd, reverse,
-                     sync, ns, dh_bf16, o.job_err);
+                     sync, ns, dh_bf16, ldh, o.job_err);
   return true;
 }
 
@@ -593,14 +596,14 @@ bool lstm_seq_forward(const float* gx, const bf16_t* w_hh, bf16_t* hs, float* cs
 }
 
 bool lstm_seq_backward(const float* act, const float* cs, const float* dH, const bf16_t* w_hh, bf16_t* dG,
-                       int T, int B, int Hd, int reverse, unsigned* sync, int dh_bf16, hipStream_t s,
+                       int T, int B, int Hd, int reverse, unsigned* sync, int dh_bf16, int ldh, hipStream_t s,
                        const PLOpts& o) {
-  if (T < 1 || B % 16 != 0 || Hd % 256 != 0 || 8 % (B / 16) != 0) return false;
+  if (T < 1 || B % 16 != 0 || Hd % 256 != 0 || 8 % (B / 16) != 0 || ldh < Hd) return false;
   const int kw = 4 * Hd / (32 * PL_W), ch = pl_ch(Hd);
 #define PL_B(KWV)                                                                                    \
   case KWV:                                                                                          \
-    return ch == 2 ? pl_bwd<KWV, 2>(act, cs, dH, w_hh, dG, T, B, Hd, reverse, sync, dh_bf16, o, s)  \
-                   : pl_bwd<KWV, 1>(act, cs, dH, w_hh, dG, T, B, Hd, reverse, sync, dh_bf16, o, s);
+    return ch == 2 ? pl_bwd<KWV, 2>(act, cs, dH, w_hh, dG, T, B, Hd, reverse, sync, dh_bf16, ldh, o, s)  \
+                   : pl_bwd<KWV, 1>(act, cs, dH, w_hh, dG, T, B, Hd, reverse, sync, dh_bf16, ldh, o, s);
   switch (kw) {
     PL_B(4)
     PL_B(8)

@@ -150,6 +150,8 @@ void col_reduce_acc(const float* part, int nblk, int W, float* out0, float* out1
 // caller zeroes sums beforehand (one fill per training step for all of a
 // model's BNs).
 
+constexpr int BN_SLAB = 256;
+
 // a channel's (S, Q) over the shards
 __device__ __forceinline__ void bn_shard_sum(const double* __restrict__ sums, int C, int c, double& S,
                                              double& Q) {
@@ -171,25 +173,67 @@ __device__ __forceinline__ void bn_shard_sum(const double* __restrict__ sums, in
 // per-thread 8-channel strided form measured 1.75x slower on ResNet-50's
 // backward reductions)
 __device__ __forceinline__ void bn_block_atomics(float* red, const float (&s)[8], const float (&q)[8], bool owner,
-                                                 int cg, int C, double* __restrict__ sums) {
+                                                 int cg, int cs, int c0, int C, double* __restrict__ sums) {
   __syncthreads();                       // red's partial rows are consumed
   if (owner) {
 #pragma unroll
-    for (int i = 0; i < 8; ++i) { red[cg * 8 + i] = s[i]; red[C + cg * 8 + i] = q[i]; }
+    for (int i = 0; i < 8; ++i) { red[cg * 8 + i] = s[i]; red[cs + cg * 8 + i] = q[i]; }
   }
   __syncthreads();
-  double* sh = sums + (long)(blockIdx.x % BN_SHARDS) * 2 * C;
-  for (int e = threadIdx.x; e < 2 * C; e += blockDim.x) unsafeAtomicAdd(sh + e, (double)red[e]);
+  double* sh = sums + (long)(blockIdx.x % BN_SHARDS) * 2 * C + c0;
+  for (int e = threadIdx.x; e < 2 * cs; e += blockDim.x) {
+    const int hi = e >= cs;
+    unsafeAtomicAdd(sh + hi * C + (e - hi * cs), (double)red[e]);
+  }
+}
+
+// Reduction passes run over a 2-D grid: blockIdx.y = a slab of <= sw
+// channels (sw = BN_SLAB, or C itself with g_bn_red_slab = 0), blockIdx.x a
+// contiguous row range. Each block adds 2 * sw fp64 atomics, so slabbing a
+// wide BN (C = 1024 / 2048 on ResNet-50's 14x14 / 7x7 layers) lets each block
+// cover more rows for the same grid: the full-width form issued 1-1.8 M
+// atomics per pass there against 262 K now.
+static int g_bn_red_slab = [] {
+  const char* e = getenv("TAM_BN_RED_SLAB");
+  return e ? atoi(e) : 1;
+}();
+TAM_KNOB(g_bn_red_slab)
+static int g_bn_red_blocks = [] {
+  const char* e = getenv("TAM_BN_RED_BLOCKS");
+  return e ? atoi(e) : BN_MAX_BLOCKS;
+}();
+TAM_KNOB(g_bn_red_blocks)
+
+struct BnRed {
+  dim3 grid;
+  long rows_per_block;
+  int sw;
+};
+
+static BnRed bn_reduce_grid(long M, int C) {
+  const int sw = g_bn_red_slab && C > BN_SLAB ? BN_SLAB : C;
+  const int slabs = (C + sw - 1) / sw;
+  const int nbmax = g_bn_red_blocks > 0 ? g_bn_red_blocks : BN_MAX_BLOCKS;
+  long rx = nbmax / slabs;
+  if (rx < 1) rx = 1;
+  // each block streams >= 4 passes of its thread grid so the loads stay 16 B/lane
+  long rpb = (M + rx - 1) / rx;
+  const long minr = 256 / (sw / 8) * 4;
+  if (rpb < minr) rpb = minr;
+  return BnRed{dim3((unsigned)((M + rpb - 1) / rpb), (unsigned)slabs), rpb, sw};
 }
 
 // grid.x blocks each own a contiguous row range; thread = (row lane, 8-ch group)
 __global__ void __launch_bounds__(256) bn_stats_kernel(const bf16_t* __restrict__ x, long M, int C,
-                                                        long rows_per_block,
+                                                        long rows_per_block, int sw,
                                                         double* __restrict__ sums) {
   __shared__ float red[256 * 16];
-  const int tpr = C / 8;                 // threads per row
-  const int rpb = 256 / tpr;             // rows per pass (C <= 2048)
+  const int c0 = blockIdx.y * sw;
+  const int cs = min(sw, C - c0);
+  const int tpr = cs / 8;                // threads per row
+  const int rpb = 256 / tpr;             // rows per pass (cs <= 2048)
   const int cg = threadIdx.x % tpr, rl = threadIdx.x / tpr;
+  x += c0;
   float s[8], q[8];
 #pragma unroll
   for (int i = 0; i < 8; ++i) s[i] = q[i] = 0.f;
@@ -228,7 +272,7 @@ __global__ void __launch_bounds__(256) bn_stats_kernel(const bf16_t* __restrict_
       for (int i = 0; i < 8; ++i) { s[i] += red[t * 16 + i]; q[i] += red[t * 16 + 8 + i]; }
     }
   }
-  bn_block_atomics(red, s, q, rl == 0, cg, C, sums);
+  bn_block_atomics(red, s, q, rl == 0, cg, cs, c0, C, sums);
 }
 
 // Apply passes run over a 2-D grid: blockIdx.y = a slab of <= BN_SLAB
@@ -236,18 +280,29 @@ __global__ void __launch_bounds__(256) bn_stats_kernel(const bf16_t* __restrict_
 // slab's per-channel coefficients from the fp64 sums into LDS (the old
 // finalize kernel, replicated per block: 2 doubles + 2 floats per channel,
 // L2-resident), then streams rows with 16 B per lane, 2 rows in flight.
-constexpr int BN_SLAB = 256;
-
 struct BnGrid {
   dim3 grid;
   long rows_per_block;
 };
 
+// g_bn_apply_blocks: the grid's block target; 0 (default) = 1024 blocks for
+// tensors of >= 32 M elements, 512 below. Each block also reads its slab's 16
+// statistics shards (64 KB at 256 channels) from L2, so fewer, longer blocks
+// pay: ResNet-50's 53 BN layers, forward + backward apply, 2802 -> 2683 us
+// against a flat 2048 (tools/bench_bn.py, same box; flat 1024: 2735, flat
+// 512: 2710 -- the 51 M-element stage-1 / stem tensors prefer 1024)
+static int g_bn_apply_blocks = [] {
+  const char* e = getenv("TAM_BN_APPLY_BLOCKS");
+  return e ? atoi(e) : 0;
+}();
+TAM_KNOB(g_bn_apply_blocks)
+
 static BnGrid bn_apply_grid(long M, int C) {
   const int slabs = (C + BN_SLAB - 1) / BN_SLAB;
   const int vs = (C < BN_SLAB ? C : BN_SLAB) / 8;
   const long rpp = 256 / vs;                              // rows per pass
-  long bx = (2048 + slabs - 1) / slabs;                   // ~8 blocks per CU in all
+  const long target = g_bn_apply_blocks > 0 ? g_bn_apply_blocks : (M * C >= (32L << 20) ? 1024 : 512);
+  long bx = (target + slabs - 1) / slabs;
   long rpb = (M + bx - 1) / bx;
   if (rpb < 2 * rpp) rpb = 2 * rpp;
   rpb = (rpb + rpp - 1) / rpp * rpp;
@@ -346,14 +401,16 @@ __global__ void __launch_bounds__(256) bn_apply_kernel(
 __global__ void __launch_bounds__(256) bn_bwd_reduce_kernel(
     const bf16_t* __restrict__ dy, const bf16_t* __restrict__ addend, const bf16_t* __restrict__ y,
     const bf16_t* __restrict__ x, const float* __restrict__ mean, const float* __restrict__ rstd, long M,
-    int C, long rows_per_block, int relu, double* __restrict__ sums, bf16_t* __restrict__ dp_out,
+    int C, long rows_per_block, int sw, int relu, double* __restrict__ sums, bf16_t* __restrict__ dp_out,
     const uint8_t* __restrict__ ymask) {
   __shared__ float red[256 * 16];
-  const int tpr = C / 8, rpb = 256 / tpr;
+  const int c0 = blockIdx.y * sw;
+  const int cs = min(sw, C - c0);
+  const int tpr = cs / 8, rpb = 256 / tpr;
   const int cg = threadIdx.x % tpr, rl = threadIdx.x / tpr;
   float a[8], b[8], mu[8], rs[8];
 #pragma unroll
-  for (int i = 0; i < 8; ++i) { a[i] = b[i] = 0.f; mu[i] = mean[cg * 8 + i]; rs[i] = rstd[cg * 8 + i]; }
+  for (int i = 0; i < 8; ++i) { a[i] = b[i] = 0.f; mu[i] = mean[c0 + cg * 8 + i]; rs[i] = rstd[c0 + cg * 8 + i]; }
   const long r0 = blockIdx.x * rows_per_block;
   const long r1 = min(M, r0 + rows_per_block);
   // one row of 8 channels: (dy + addend) masked by y, accumulated; dyr stored
@@ -395,7 +452,7 @@ __global__ void __launch_bounds__(256) bn_bwd_reduce_kernel(
       uint32_t vm[U];
 #pragma unroll
       for (int u = 0; u < U; ++u) {
-        const long off = (r + u * rpb) * C + cg * 8;
+        const long off = (r + u * rpb) * C + c0 + cg * 8;
         vd[u] = *(const uint4*)(dy + off);
         vx[u] = *(const uint4*)(x + off);
         vy[u] = relu && y ? *(const uint4*)(y + off) : z;
@@ -403,10 +460,10 @@ __global__ void __launch_bounds__(256) bn_bwd_reduce_kernel(
         vm[u] = relu && ymask ? ymask[off >> 3] : 0u;
       }
 #pragma unroll
-      for (int u = 0; u < U; ++u) row((r + u * rpb) * C + cg * 8, vd[u], vx[u], vy[u], va[u], vm[u]);
+      for (int u = 0; u < U; ++u) row((r + u * rpb) * C + c0 + cg * 8, vd[u], vx[u], vy[u], va[u], vm[u]);
     }
     for (; r < r1; r += rpb) {
-      const long off = r * C + cg * 8;
+      const long off = r * C + c0 + cg * 8;
       row(off, *(const uint4*)(dy + off), *(const uint4*)(x + off),
           relu && y ? *(const uint4*)(y + off) : z, addend ? *(const uint4*)(addend + off) : z,
           relu && ymask ? ymask[off >> 3] : 0u);
@@ -422,7 +479,7 @@ __global__ void __launch_bounds__(256) bn_bwd_reduce_kernel(
       for (int i = 0; i < 8; ++i) { a[i] += red[t * 16 + i]; b[i] += red[t * 16 + 8 + i]; }
     }
   }
-  bn_block_atomics(red, a, b, rl == 0, cg, C, sums);
+  bn_block_atomics(red, a, b, rl == 0, cg, cs, c0, C, sums);
 }
 
 // dx = g*rstd*(dyr - S/M - xhat*Q/M) = k1*dyr + k2*xhat + k3 with S, Q from
@@ -514,23 +571,13 @@ __global__ void __launch_bounds__(256) bn_bwd_apply_kernel(
   }
 }
 
-static long bn_rows_per_block(long M, int C) {
-  // <= BN_MAX_BLOCKS reducing blocks (2 per CU on 256 CUs); each block
-  // streams >= 4 passes of its thread grid so the loads stay 16 B/lane
-  long rpb = (M + BN_MAX_BLOCKS - 1) / BN_MAX_BLOCKS;
-  const long minr = 256 / (C / 8) * 4;
-  if (rpb < minr) rpb = minr;
-  return rpb;
-}
-
 void bn_forward(const bf16_t* x, const bf16_t* res, bf16_t* y, long M, int C, float eps,
                 float momentum, const float* gamma, const float* beta, float* run_mean,
                 float* run_var, float* save_mean, float* save_rstd, int relu, double* sums,
                 int sums_ready, uint8_t* ymask, hipStream_t s) {
   if (!sums_ready) {
-    const long rpb = bn_rows_per_block(M, C);
-    const int nb = (int)((M + rpb - 1) / rpb);
-    hipLaunchKernelGGL(bn_stats_kernel, dim3(nb), dim3(256), 0, s, x, M, C, rpb, sums);
+    const BnRed g = bn_reduce_grid(M, C);
+    hipLaunchKernelGGL(bn_stats_kernel, g.grid, dim3(256), 0, s, x, M, C, g.rows_per_block, g.sw, sums);
   }
   const BnGrid g = bn_apply_grid(M, C);
   hipLaunchKernelGGL(bn_apply_kernel, g.grid, dim3(256), 0, s, x, res, y, M, C, g.rows_per_block,
@@ -580,10 +627,9 @@ void bn_backward(const bf16_t* dy, const bf16_t* addend, const bf16_t* y, const 
   if (!sums_ready) {
     // residual BN: the reduce pass materialises dyr into dres; the apply pass
     // then runs on (dres, x) as a plain BN backward
-    const long rpb = bn_rows_per_block(M, C);
-    const int nb = (int)((M + rpb - 1) / rpb);
-    hipLaunchKernelGGL(bn_bwd_reduce_kernel, dim3(nb), dim3(256), 0, s, dy, addend, y, x, mean, rstd, M,
-                       C, rpb, relu, sums, dres, ymask);
+    const BnRed g = bn_reduce_grid(M, C);
+    hipLaunchKernelGGL(bn_bwd_reduce_kernel, g.grid, dim3(256), 0, s, dy, addend, y, x, mean, rstd, M,
+                       C, g.rows_per_block, g.sw, relu, sums, dres, ymask);
     if (dres) {
       dy = dres;
       addend = nullptr;

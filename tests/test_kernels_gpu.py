@@ -1393,7 +1393,18 @@ def test_lstm_persistent_sequence(gpu, T_, B, Hd, reverse, ch):
     assert T().lstm_seq_backward(act, cs, dH, w, dG, reverse, sync)
     torch.cuda.synchronize()
     assert int(sync[0]) == 0, "grid barrier timed out"
-    assert rel_err(dG, _lstm_seq_bwd_ref(act, cs, dH, w, reverse)) < 1e-2
+    ref = _lstm_seq_bwd_ref(act, cs, dH, w, reverse)
+    assert rel_err(dG, ref) < 1e-2
+    # dH as a column slice of a wider bf16 gradient (the backward of a
+    # feature concat), read in place at its row pitch
+    wide = torch.randn(T_, B, 2 * Hd + 64, device=gpu).to(BF)
+    wide[:, :, 64:64 + Hd] = dH.to(BF)
+    dGs = torch.empty_like(dG)
+    sync.zero_()
+    assert T().lstm_seq_backward(act, cs, wide[:, :, 64:64 + Hd], w, dGs, reverse, sync)
+    torch.cuda.synchronize()
+    assert int(sync[0]) == 0, "grid barrier timed out"
+    assert rel_err(dGs, _lstm_seq_bwd_ref(act, cs, wide[:, :, 64:64 + Hd].float(), w, reverse)) < 1e-2
     T().lstm_seq_policy(0)
 
 

@@ -176,7 +176,7 @@ class _LSTMLayer(Function):
             # the persistent kernel reads dH as it comes (bf16); only the
             # per-step path needs the fp32 accumulator it updates in place
             ran = PERSIST and persist and _ran(
-                _T().lstm_seq_backward(act, Cs, dH.contiguous(), w_hh.w, dG, reverse, sy, *_pl_args(m), zeroed),
+                _T().lstm_seq_backward(act, Cs, _pitched(dH), w_hh.w, dG, reverse, sy, *_pl_args(m), zeroed),
                 sy)
             if not ran:                            # per-step path: cell-state gradient carry
                 dHf = dH.float().contiguous()
@@ -263,6 +263,21 @@ class _LSTMLayer(Function):
             w_hh.grad_ready()
             b.grad_ready()
         return dx, None, None, None, None, None, None
+
+
+# TAM_LSTM_PITCHED=0: gather every non-contiguous dH (A/B)
+LSTM_PITCHED_DH = os.environ.get("TAM_LSTM_PITCHED", "1") != "0"
+
+
+def _pitched(dH: torch.Tensor) -> torch.Tensor:
+    """dH as the persistent backward reads it: a [T,B,H] column slice of a
+    wider gradient (the backward of the decoder / encoder feature concats
+    hands the layer output's gradient as such a view) is read in place at
+    its row pitch; anything else is made contiguous."""
+    T, B, H = dH.shape
+    if LSTM_PITCHED_DH and dH.stride(2) == 1 and dH.stride(1) >= H and dH.stride(0) == B * dH.stride(1):
+        return dH
+    return dH.contiguous()
 
 
 def _pl_args(m):
