@@ -625,3 +625,46 @@ def test_offload_refuses_sharded_state():
     t.ddp = _D()
     with pytest.raises(RuntimeError, match="consolidate"):
         t.offload(_HostEngine())
+
+
+def test_gang_fill_votes_match_when_one_member_cannot_step():
+    """Fill-mode eligibility is partly local (this rank's trainer state and
+    its own report): a gang member that cannot step still joins the first
+    vote and votes stop, so a peer that could step never waits in a vote the
+    member would not join; a lone job with a local error does not fill."""
+    from types import SimpleNamespace
+    from tiresias_amd.executor.cluster_runtime import Worker
+
+    votes = []
+
+    class Comm:
+        def start(self, v):
+            votes.append(float(v.item()))
+            return v
+
+        def finish(self, hs):
+            pass
+
+    def worker(rank, trainer, job_ranks):
+        w = Worker.__new__(Worker)
+        w.fill_enabled, w.rank, w.device = True, rank, torch.device("cpu")
+        w.trainers = {"j": trainer}
+        w._job_ranks = {"j": job_ranks}
+        w.fill_s_total, w.fill_steps_total = 0.0, 0
+        return w
+
+    steps = []
+    t = SimpleNamespace(ddp=SimpleNamespace(comm=Comm()), group=None, broken=False, _spilled=None,
+                        step=lambda: steps.append(1))
+    plan = {"assign": {0: [("j", 0)]}, "left": {"j": 5}}
+    bad_rep = {"jobs": [{"job": "j", "error": "RuntimeError: oom"}]}
+    w = worker(0, t, (0, 1))
+    w.fill_begin(plan, bad_rep)
+    assert w._fill is not None and w._fill["left"] == 0
+    assert w.fill_step(False) is False and votes == [1.0] and not steps   # one vote: stop
+    votes.clear()
+    w.fill_begin(plan, {"jobs": []})                      # healthy member: steps until a vote stops
+    assert w.fill_step(False) is True and votes == [0.0] and steps == [1]
+    solo = worker(0, SimpleNamespace(ddp=None, group=None, broken=False, _spilled=None, step=None), (0,))
+    solo.fill_begin(plan, bad_rep)
+    assert solo._fill is None

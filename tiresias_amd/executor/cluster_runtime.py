@@ -1616,16 +1616,25 @@ class Worker:
             return
         jid = mine[0][0]
         left = int((plan.get("left") or {}).get(jid, 0))
-        t = self.trainers.get(jid)
-        if left <= 0 or t is None or getattr(t, "broken", False) or getattr(t, "_spilled", None):
+        if left <= 0:                              # plan-level: the same on every gang member
             return
-        if any(r.get("error") for r in rep.get("jobs") or [] if r.get("job") == jid):
+        t = self.trainers.get(jid)
+        if t is None:
             return
         gang = t.ddp is not None and len(self._job_ranks.get(jid, (self.rank,))) > 1
-        if gang and (comm_failed(t.group) or t.ddp.comm is None):
+        comm_ok = not gang or (t.ddp.comm is not None and not comm_failed(t.group))
+        if not comm_ok:
+            return                                 # peers' votes fail on the same communicator
+        local_bad = (getattr(t, "broken", False) or getattr(t, "_spilled", None) or
+                     any(r.get("error") for r in rep.get("jobs") or [] if r.get("job") == jid))
+        if local_bad and not gang:
             return
-        self._fill = {"job": jid, "left": left, "n": 0, "sec": 0.0, "gang": gang, "done": False,
-                      "prev": None, "err": None, "t": t}
+        # a gang member that cannot step still takes part in the FIRST vote
+        # (and votes stop), so peers that can step never wait in a vote it
+        # would not join: eligibility here is partly local (this rank's
+        # trainer state and report), the votes must match on every member
+        self._fill = {"job": jid, "left": 0 if local_bad else left, "n": 0, "sec": 0.0, "gang": gang,
+                      "done": False, "prev": None, "err": None, "t": t}
 
     def _vote(self, t: Trainer, stop: bool) -> bool:
         """One-element SUM all-reduce over the job's gang: does ANY member
