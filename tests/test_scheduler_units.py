@@ -497,3 +497,19 @@ def test_lazy_preemption_skips_no_op_suspensions():
     eager, lazy = run("eager"), run("lazy")
     assert eager["V"][2] == 1 and lazy["V"][2] == 0
     assert {k: v[:2] for k, v in eager.items()} == {k: v[:2] for k, v in lazy.items()}
+
+
+def test_spread_rule_is_validated():
+    """An unknown --spread_rule is an error in both engines, not a silent
+    fallback to fragments-first."""
+    import dataclasses
+    from tiresias_amd.config import SimConfig
+    from tiresias_amd.engine.native import simulate_native
+    from tiresias_amd.engine.sim import simulate
+
+    cfg = dataclasses.replace(SimConfig(schedule="dlas-gpu", scheme="tiresias"), spread_rule="nodes")
+    specs = [spec(0, g=1)]
+    with pytest.raises(ValueError, match="spread_rule"):
+        simulate(cfg, specs)
+    with pytest.raises(ValueError, match="spread_rule"):
+        simulate_native(cfg, specs)

@@ -89,7 +89,8 @@ def define_flags() -> None:
     D.DEFINE_string("spread_rule", "node", "tiresias placement, insensitive gangs: fragments (spread "
                     "whenever no consolidated block is free) | wait (spread only when the expected wait "
                     "for a block exceeds the spread penalty, engine/spread.py) | node (as wait, but a gang "
-                    "that fits one node is never fragmented)")
+                    "that fits one node is never fragmented and a wider gang fills the fullest-free "
+                    "nodes first)")
     D.DEFINE_string("preempt_rule", "lazy", "preemptive policies: lazy (preempt only what a chosen job's "
                     "placement needs) | eager (every running job outside the priority prefix)")
     D.DEFINE_boolean("ddp_shard", False, "live gangs: reduce-scatter + sharded optimizer + bf16 all-gather "

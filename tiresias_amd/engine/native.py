@@ -61,6 +61,8 @@ def simulate_native(cfg: SimConfig, specs: List[JobSpec], prior: Optional[List[f
                              float(cfg.solve_starvation), float(cfg.gittins_delta or 3250.0),
                              [float(x) for x in prior], online)
     rule = getattr(cfg, "spread_rule", "node")
+    if rule not in ("node", "wait", "fragments"):
+        raise ValueError(f"spread_rule must be node | wait | fragments, got {rule!r}")
     wait_rule = scheme == "tiresias" and rule in ("wait", "node")
     priced = _set_costs(eng, cfg, specs, force=wait_rule)
     eng.set_spread_wait(wait_rule)
