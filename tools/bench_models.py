@@ -44,8 +44,9 @@ def main():
                     help="weight gradients on a side stream: -1 per-model default, 0 off, 1 on")
     ap.add_argument("--branches", type=int, default=-1,
                     help="model branch streams (GNMT's independent recurrences): -1 model default, 0 off, 1 on")
-    ap.add_argument("--lib", type=int, default=0,
-                    help="plain-GEMM routing: -1 measured MFMA/hipBLASLt, 0 MFMA only, 1 library")
+    ap.add_argument("--lib", type=int, default=None,
+                    help="plain-GEMM routing: -1 measured MFMA/hipBLASLt (production default), 0 MFMA only, "
+                         "1 library; unset: the library default")
     ap.add_argument("--conv_policy", type=int, default=1,
                     help="conv core: 1 LDS-DMA where the cost model picks it, 2 wherever eligible, 0 igemm only")
     ap.add_argument("--save_routes", default=None,
@@ -59,7 +60,8 @@ def main():
     import torch
     from tiresias_amd.ops import _lib
     _lib.load(required=True)
-    torch.ops.tam.gemm_lib_policy(a.lib)
+    if a.lib is not None:
+        torch.ops.tam.gemm_lib_policy(a.lib)
     torch.ops.tam.conv_dma_policy(a.conv_policy)
     torch.ops.tam.conv_split_policy(a.conv_split)
     for kv in a.policy:
