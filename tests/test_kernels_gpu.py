@@ -51,6 +51,26 @@ def test_gemm_routing(gpu):
     assert "1024 2048 1024 KK 0 0 1" in routes and "1024 2048 1024 MK 1 1 0" in routes
 
 
+def test_gemm_routes_lib_decision_respects_policy(gpu):
+    """A shipped "lib" routing decision (with the p8 config it was timed
+    against) runs the library under the default measured routing and falls
+    back to our fastest recorded kernel under policy 0 -- same numbers both
+    ways; a line with an unknown route is skipped."""
+    torch.manual_seed(13)
+    M, N, K = 1536, 1792, 2048          # a shape no other test routes
+    A = torch.randn(M, K, device=gpu).to(BF)
+    W = torch.randn(N, K, device=gpu).to(BF)
+    ref = A.float() @ W.float().t()
+    line = f"{M} {N} {K} KK 0 0 0 lib 0.05 0.04 0.06 0.045 128 2\n{M} {N} {K + 64} KK 0 0 0 bogus 1 1 1 1\n"
+    assert T().gemm_routes_load(line) == 1
+    assert f"{M} {N} {K} KK 0 0 0 lib" in T().gemm_routes()
+    for pol in (-1, 0):
+        T().gemm_lib_policy(pol)
+        y = torch.empty(M, N, device=gpu, dtype=BF)
+        T().gemm(A, True, W, True, y, 0, None, False, None, 1.0, False)
+        assert rel_err(y, ref) < 1e-2, pol
+
+
 @pytest.mark.parametrize("M,N,K", [(512, 512, 4096), (2048, 512, 4096), (512, 2048, 4096), (6144, 512, 4096),
                                    (200, 136, 72), (1000, 64, 520)])
 def test_gemm_colsum_fused(gpu, M, N, K):
