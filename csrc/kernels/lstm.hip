@@ -187,7 +187,11 @@ void lstm_step_forward(const float* gx, const bf16_t* w_hh, const bf16_t* h_prev
 // unless TWO such grids fit at once (two GNMT jobs sharing a GPU).
 // ---------------------------------------------------------------------------
 constexpr int PL_W = 8;          // waves per workgroup
-constexpr unsigned PL_SPIN = 1u << 22;
+// poll bound of one hand-off wait: 2^16 relaxed sc1 polls + s_sleep(1) is
+// ~50-100 ms, four orders of magnitude above a step's hand-off (~4-6 us)
+// even behind another job's kernels; a grid that cannot become co-resident
+// (two jobs' different persistent kernels on one GPU) gives up that fast
+constexpr unsigned PL_SPIN = 1u << 16;
 // Sticky count of persistent-grid barrier timeouts on this device (every job
 // of the process): the kernels never hang, but a timed-out step computed on
 // h / dG that had not arrived. The host reads it after the round's
@@ -225,7 +229,14 @@ __device__ __forceinline__ void pl_wait(unsigned* sync, int line0, int ns, unsig
     const unsigned spin = g_pl_spin;
     while (__hip_atomic_load((pl_gu32*)(sync + 32 * (1 + line0 + threadIdx.x)), PL_RLX) < target) {
       __builtin_amdgcn_s_sleep(1);
-      if (++polls > spin) {
+      // a barrier of this launch (or an earlier launch of the same job's
+      // step) already timed out: the step's update is skipped anyway, so
+      // drain instead of paying the full bound at every later wait
+      if ((++polls & 255) == 0 &&
+          (__hip_atomic_load((pl_gu32*)sync, PL_RLX) != 0u ||
+           (job_err != nullptr && __hip_atomic_load((pl_gu32*)job_err, PL_RLX) != 0u)))
+        break;
+      if (polls > spin) {
         __hip_atomic_fetch_or((pl_gu32*)sync, 1u, PL_RLX);
         __hip_atomic_fetch_add((pl_gu32*)&g_pl_timeouts, 1u, PL_RLX);
         if (job_err != nullptr) __hip_atomic_fetch_add((pl_gu32*)job_err, 1u, PL_RLX);

@@ -1513,6 +1513,16 @@ class Worker:
                 n = self._run_until(t, n, deadline, cuda)
                 jobs = [(jid, n)]
         else:
+            if cuda:
+                # two co-located jobs' persistent LSTM grids (different kernels,
+                # different per-CU footprints) cannot be guaranteed co-resident:
+                # each would spin at its grid barrier waiting for workgroups the
+                # other holds the CUs of. A job that shares its GPU with another
+                # persistent-grid job takes the per-step recurrence from here on
+                pers = [jid for jid, _ in jobs if self.trainers[jid].uses_persist]
+                if len(pers) > 1:
+                    for jid in pers:
+                        self.trainers[jid].disable_persist()
             streams = [self._stream(jid) if cuda else None for jid, _ in jobs]
             if cuda:
                 # apply() ran on the default stream: fresh jobs' weight init
