@@ -403,6 +403,29 @@ def test_persist_barrier_timeout_is_loud_and_falls_back(gpu):
     w.clear(keep_pool=False)
 
 
+def test_two_persistent_jobs_sharing_a_gpu_run_per_step(gpu):
+    """GPU sharing with two GNMT jobs: their persistent LSTM grids (different
+    kernels, different per-CU footprints) cannot be guaranteed co-resident, so
+    a shared round switches both to the per-step recurrence before stepping;
+    the round completes with finite losses and no barrier timeouts."""
+    from tiresias_amd.executor.cluster_runtime import Worker
+    from tiresias_amd.models import gnmt as G
+
+    w = Worker(0, 1, gpu, monitor_period=0)
+    acts = [{"op": "start", "job": j, "model": "gnmt", "batch": 16, "seed": int(j), "ranks": (0,),
+             "source": "fresh"} for j in ("1", "2")]
+    w.apply({"actions": acts, "assign": {}})
+    assert w.trainers["1"].uses_persist and w.trainers["2"].uses_persist
+    G.device_timeouts(reset=True)
+    rep = w.run({"actions": [], "assign": {0: [("1", 2), ("2", 2)]}, "deadline": None})
+    for r in rep["jobs"]:
+        assert "error" not in r and r["iters"] == 2 and r["shared"], rep
+        assert r["loss"] == r["loss"]                                   # finite
+    assert not w.trainers["1"].uses_persist and not w.trainers["2"].uses_persist
+    assert G.device_timeouts(reset=False) == 0
+    w.clear(keep_pool=False)
+
+
 def test_snapshot_roundtrip_on_device(gpu, tmp_path):
     """ckpt/snapshot.py on the GPU: D2D clone on the compute stream, D2H on
     the low-priority side stream, atomic file; steps issued right after the
