@@ -135,6 +135,11 @@ def test_live_replay_with_gangs():
 def _fault_worker(rank, world, port, outdir):
     import datetime
 
+    # the gloo control plane has no heartbeat to bound a gang communicator's
+    # rendezvous with the dying rank (the store plane does): keep that bound
+    # under the test's join limit, or a loss that lands in a rendezvous waits
+    # out the 180 s default (read at import of parallel/gang.py, below)
+    os.environ["TAM_COMM_CREATE_TIMEOUT_S"] = "30"
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
     dist.init_process_group("gloo", rank=rank, world_size=world, timeout=datetime.timedelta(seconds=20))
