@@ -62,19 +62,17 @@ using GemmKey = std::tuple<int64_t, int64_t, int64_t, bool, bool, int64_t, bool,
 std::map<GemmKey, int> g_route;          // 0 = igemm/gemm256, 1 = library, 2 = LDS-DMA GEMM
 std::map<GemmKey, std::array<float, 4>> g_route_ms;   // measured ms per path
 std::mutex g_route_mu;
-// hipBLASLt for PLAIN GEMMs (no fused epilogue: no relu / mask / alpha, at
-// most a bias): -1 (default) measured per-shape routing -- the library runs a
-// shape only where it timed > 5 % faster than the best of our kernels; 0
-// never (every GEMM on our MFMA kernels; A/B); 1 always where eligible.
-// Round 5, same box, graph steps re-tuned from scratch (tools/gpu_r5s.sh):
-// Transformer 5.07 -> 4.87 ms, GNMT 10.00-10.07 -> 9.61-9.69, VGG-16
-// 6.56-6.62 -> 6.52-6.54; the library takes the deep-K / vocab-sized
-// shapes where our 256^2 core runs at 0.70-0.85x of it (3200x2048x32000
-// 388 vs 538 us) and the Transformer's N = 512 projections. Round 2 had
-// measured the opposite (-0..7 % step time for our kernels alone).
+// hipBLASLt for PLAIN GEMMs: 0 (default since round 6) never -- every GEMM
+// of every model runs on our MFMA kernels, the routing only picks among them
+// (tile, slab split, stream-K, igemm); -1 measured per-shape routing that may
+// pick the library where it timed > 5 % faster (A/B against the library
+// only, TAM_GEMM_LIB=-1); 1 library wherever eligible (A/B only).
+// Round 5 had made -1 the default (Transformer -0.24 ms, GNMT -0.21 ms from
+// 15 of 51 plain shapes on the library); the north star wants hand-written
+// kernels on the hot path, so the library is an A/B reference now.
 int g_lib_policy = [] {
   const char* e = getenv("TAM_GEMM_LIB");
-  return e ? atoi(e) : -1;
+  return e ? atoi(e) : 0;
 }();
 extern int g_dma_policy;
 int g_forced = 0;   // tile/split forced for tuning: never route to the library
@@ -1037,23 +1035,26 @@ static const unsigned* guard_ptr(const optional<Tensor>& guard, const Tensor& li
 }
 void sgd_op(const Tensor& w, const Tensor& g, const Tensor& mom, const Tensor& wb, double lr,
             double momentum, double wd, double gscale, bool nesterov, bool zero_grad,
-            const optional<Tensor>& guard) {
+            const optional<Tensor>& guard, int64_t zero_from, int64_t wd_until) {
   check_f32(w, "w"); check_f32(g, "g"); check_f32(mom, "mom"); check_bf16(wb, "wb");
   TORCH_CHECK(w.numel() % 4 == 0 && g.numel() == w.numel() && mom.numel() == w.numel() &&
                   wb.numel() == w.numel(),
               "tam.sgd: sizes");
+  TORCH_CHECK(zero_from % 4 == 0 && (wd_until < 0 || wd_until % 4 == 0), "tam.sgd: region bounds % 4");
   tam::sgd_step(w.data_ptr<float>(), g.data_ptr<float>(), mom.data_ptr<float>(), bpm(wb), w.numel(),
                 (float)lr, (float)momentum, (float)wd, (float)gscale, nesterov, zero_grad,
-                cur_stream(w), guard_ptr(guard, w));
+                cur_stream(w), guard_ptr(guard, w), (long)zero_from, (long)wd_until);
 }
 void adam_op(const Tensor& w, const Tensor& g, const Tensor& m, const Tensor& v, const Tensor& wb,
              double lr, double b1, double b2, double eps, double wd, int64_t step, double gscale,
-             bool zero_grad, const optional<Tensor>& guard) {
+             bool zero_grad, const optional<Tensor>& guard, int64_t zero_from, int64_t wd_until) {
   check_f32(w, "w"); check_f32(g, "g"); check_f32(m, "m"); check_f32(v, "v"); check_bf16(wb, "wb");
   TORCH_CHECK(w.numel() % 4 == 0, "tam.adam: numel % 4");
+  TORCH_CHECK(zero_from % 4 == 0 && (wd_until < 0 || wd_until % 4 == 0), "tam.adam: region bounds % 4");
   tam::adam_step(w.data_ptr<float>(), g.data_ptr<float>(), m.data_ptr<float>(), v.data_ptr<float>(),
                  bpm(wb), w.numel(), (float)lr, (float)b1, (float)b2, (float)eps, (float)wd,
-                 (int)step, (float)gscale, zero_grad, cur_stream(w), guard_ptr(guard, w));
+                 (int)step, (float)gscale, zero_grad, cur_stream(w), guard_ptr(guard, w), (long)zero_from,
+                 (long)wd_until);
 }
 void lstm_guard_step_op(const Tensor& err) {
   TORCH_CHECK(err.is_cuda() && err.scalar_type() == at::kInt && err.numel() >= 2,
@@ -1285,8 +1286,8 @@ TORCH_LIBRARY(tam, m) {
   m.def("relu_backward(Tensor dy, Tensor y, Tensor(a!) dx) -> ()", &relu_backward_op);
   m.def("add(Tensor a, Tensor b, Tensor(a!) y) -> ()", &add_op);
   m.def("cast_f32_bf16(Tensor x, Tensor(a!) y) -> ()", &cast_op);
-  m.def("sgd_step(Tensor(a!) w, Tensor(b!) g, Tensor(c!) mom, Tensor(d!) wb, float lr, float momentum, float wd, float gscale, bool nesterov, bool zero_grad, Tensor? guard=None) -> ()", &sgd_op);
-  m.def("adam_step(Tensor(a!) w, Tensor(b!) g, Tensor(c!) m, Tensor(d!) v, Tensor(e!) wb, float lr, float b1, float b2, float eps, float wd, int step, float gscale, bool zero_grad, Tensor? guard=None) -> ()", &adam_op);
+  m.def("sgd_step(Tensor(a!) w, Tensor(b!) g, Tensor(c!) mom, Tensor(d!) wb, float lr, float momentum, float wd, float gscale, bool nesterov, bool zero_grad, Tensor? guard=None, int zero_from=0, int wd_until=-1) -> ()", &sgd_op);
+  m.def("adam_step(Tensor(a!) w, Tensor(b!) g, Tensor(c!) m, Tensor(d!) v, Tensor(e!) wb, float lr, float b1, float b2, float eps, float wd, int step, float gscale, bool zero_grad, Tensor? guard=None, int zero_from=0, int wd_until=-1) -> ()", &adam_op);
   m.def("lstm_guard_step(Tensor(a!) err) -> ()", &lstm_guard_step_op);
   m.def("attn_forward(Tensor q, Tensor k, Tensor v, Tensor(a!) o, Tensor(b!) lse, bool causal, float scale, Tensor? kv_len) -> ()", &attn_forward_op);
   m.def("attn_backward(Tensor q, Tensor k, Tensor v, Tensor o, Tensor dout, Tensor lse, Tensor(a!) dq, Tensor(b!) dk, Tensor(c!) dv, Tensor(d!) dq_acc, Tensor(e!) delta, bool causal, float scale, Tensor? kv_len) -> ()", &attn_backward_op);

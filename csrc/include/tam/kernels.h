@@ -101,11 +101,11 @@ void cast_f32_bf16(const float* x, bf16_t* y, long n, hipStream_t s);
 // optimizers over flat arenas (n % 4 == 0)
 void sgd_step(float* w, float* g, float* mom, bf16_t* wb, long n, float lr, float momentum,
               float wd, float gscale, int nesterov, int zero_grad, hipStream_t s,
-              const unsigned* guard = nullptr);
+              const unsigned* guard = nullptr, long zero_from = 0, long wd_until = -1);
 void optim_variant(int v);   // streaming optimizer variants (optim.hip), 0 = baseline
 void adam_step(float* w, float* g, float* m, float* v, bf16_t* wb, long n, float lr, float b1,
                float b2, float eps, float wd, int step, float gscale, int zero_grad,
-               hipStream_t s, const unsigned* guard = nullptr);
+               hipStream_t s, const unsigned* guard = nullptr, long zero_from = 0, long wd_until = -1);
 
 // fused attention (bf16, head_dim 64): element (b, s, h, d) at b * *_bstride +
 // s * *_stride + 64 h + d (batch-major [B][S][H][64], or a time-major

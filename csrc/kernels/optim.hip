@@ -25,11 +25,12 @@ namespace tam {
 __global__ void __launch_bounds__(256) sgd_kernel(float* __restrict__ w, float* __restrict__ g,
                                                    float* __restrict__ mom,
                                                    bf16_t* __restrict__ wb, long n4, float lr,
-                                                   float momentum, float wd, float gscale,
-                                                   int nesterov, int zero_grad, const unsigned* guard) {
+                                                   float momentum, float wd0, float gscale,
+                                                   int nesterov, int zero_grad, const unsigned* guard,
+                                                   long zero_from4, long wd_until4) {
   if (guard != nullptr && *guard != 0u) {
     for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < n4; i += (long)gridDim.x * blockDim.x)
-      ((float4*)g)[i] = make_float4(0.f, 0.f, 0.f, 0.f);
+      if (i >= zero_from4) ((float4*)g)[i] = make_float4(0.f, 0.f, 0.f, 0.f);
     return;
   }
   for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < n4;
@@ -38,6 +39,7 @@ __global__ void __launch_bounds__(256) sgd_kernel(float* __restrict__ w, float* 
     float4 gv = ((float4*)g)[i];
     float4 mv = ((float4*)mom)[i];
     float* wp = (float*)&wv; float* gp = (float*)&gv; float* mp = (float*)&mv;
+    const float wd = i < wd_until4 ? wd0 : 0.f;
 #pragma unroll
     for (int k = 0; k < 4; ++k) {
       float d = gp[k] * gscale + wd * wp[k];
@@ -47,7 +49,7 @@ __global__ void __launch_bounds__(256) sgd_kernel(float* __restrict__ w, float* 
     }
     ((float4*)w)[i] = wv;
     ((float4*)mom)[i] = mv;
-    if (zero_grad) ((float4*)g)[i] = make_float4(0.f, 0.f, 0.f, 0.f);
+    if (zero_grad && i >= zero_from4) ((float4*)g)[i] = make_float4(0.f, 0.f, 0.f, 0.f);
     ((uint2*)wb)[i] = make_uint2(pack_bf2(wp[0], wp[1]), pack_bf2(wp[2], wp[3]));
   }
 }
@@ -55,18 +57,20 @@ __global__ void __launch_bounds__(256) sgd_kernel(float* __restrict__ w, float* 
 __global__ void __launch_bounds__(256) adam_kernel(float* __restrict__ w, float* __restrict__ g,
                                                     float* __restrict__ m, float* __restrict__ v,
                                                     bf16_t* __restrict__ wb, long n4, float lr,
-                                                    float b1, float b2, float eps, float wd,
+                                                    float b1, float b2, float eps, float wd0,
                                                     float bc1, float bc2, float gscale,
-                                                    int zero_grad, const unsigned* guard) {
+                                                    int zero_grad, const unsigned* guard, long zero_from4,
+                                                    long wd_until4) {
   if (guard != nullptr && *guard != 0u) {
     for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < n4; i += (long)gridDim.x * blockDim.x)
-      ((float4*)g)[i] = make_float4(0.f, 0.f, 0.f, 0.f);
+      if (i >= zero_from4) ((float4*)g)[i] = make_float4(0.f, 0.f, 0.f, 0.f);
     return;
   }
   for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < n4;
        i += (long)gridDim.x * blockDim.x) {
     float4 wv = ((float4*)w)[i], gv = ((float4*)g)[i], mv = ((float4*)m)[i], vv = ((float4*)v)[i];
     float* wp = (float*)&wv; float* gp = (float*)&gv; float* mp = (float*)&mv; float* vp = (float*)&vv;
+    const float wd = i < wd_until4 ? wd0 : 0.f;
 #pragma unroll
     for (int k = 0; k < 4; ++k) {
       const float gr = gp[k] * gscale;
@@ -76,7 +80,7 @@ __global__ void __launch_bounds__(256) adam_kernel(float* __restrict__ w, float*
       wp[k] -= lr * (mh / (sqrtf(vh) + eps) + wd * wp[k]);   // decoupled (AdamW)
     }
     ((float4*)w)[i] = wv; ((float4*)m)[i] = mv; ((float4*)v)[i] = vv;
-    if (zero_grad) ((float4*)g)[i] = make_float4(0.f, 0.f, 0.f, 0.f);
+    if (zero_grad && i >= zero_from4) ((float4*)g)[i] = make_float4(0.f, 0.f, 0.f, 0.f);
     ((uint2*)wb)[i] = make_uint2(pack_bf2(wp[0], wp[1]), pack_bf2(wp[2], wp[3]));
   }
 }
@@ -111,17 +115,19 @@ template <int U, bool NT>
 __global__ void __launch_bounds__(256) adam_stream_kernel(float* __restrict__ w, float* __restrict__ g,
                                                            float* __restrict__ m, float* __restrict__ v,
                                                            bf16_t* __restrict__ wb, long n4, float lr, float b1,
-                                                           float b2, float eps, float wd, float bc1, float bc2,
-                                                           float gscale, int zero_grad, const unsigned* guard) {
+                                                           float b2, float eps, float wd0, float bc1, float bc2,
+                                                           float gscale, int zero_grad, const unsigned* guard,
+                                                           long zero_from4, long wd_until4) {
   const long stride = (long)gridDim.x * blockDim.x;
   if (guard != nullptr && *guard != 0u) {
     for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < n4; i += stride)
-      st4<NT>(g, i, make_float4(0.f, 0.f, 0.f, 0.f));
+      if (i >= zero_from4) st4<NT>(g, i, make_float4(0.f, 0.f, 0.f, 0.f));
     return;
   }
   const float ib1 = 1.f / bc1, ib2 = 1.f / bc2;
   auto body = [&](long i, float4 wv, float4 gv, float4 mv, float4 vv) {
     float* wp = (float*)&wv; float* gp = (float*)&gv; float* mp = (float*)&mv; float* vp = (float*)&vv;
+    const float wd = i < wd_until4 ? wd0 : 0.f;
 #pragma unroll
     for (int k = 0; k < 4; ++k) {
       const float gr = gp[k] * gscale;
@@ -131,7 +137,7 @@ __global__ void __launch_bounds__(256) adam_stream_kernel(float* __restrict__ w,
       wp[k] -= lr * (mh / (sqrtf(vh) + eps) + wd * wp[k]);   // decoupled (AdamW)
     }
     st4<NT>(w, i, wv); st4<NT>(m, i, mv); st4<NT>(v, i, vv);
-    if (zero_grad) st4<NT>(g, i, make_float4(0.f, 0.f, 0.f, 0.f));
+    if (zero_grad && i >= zero_from4) st4<NT>(g, i, make_float4(0.f, 0.f, 0.f, 0.f));
     st2<NT>(wb, i, make_uint2(pack_bf2(wp[0], wp[1]), pack_bf2(wp[2], wp[3])));
   };
   const long t = blockIdx.x * (long)blockDim.x + threadIdx.x;
@@ -153,16 +159,18 @@ __global__ void __launch_bounds__(256) adam_stream_kernel(float* __restrict__ w,
 template <int U, bool NT>
 __global__ void __launch_bounds__(256) sgd_stream_kernel(float* __restrict__ w, float* __restrict__ g,
                                                           float* __restrict__ mom, bf16_t* __restrict__ wb, long n4,
-                                                          float lr, float momentum, float wd, float gscale,
-                                                          int nesterov, int zero_grad, const unsigned* guard) {
+                                                          float lr, float momentum, float wd0, float gscale,
+                                                          int nesterov, int zero_grad, const unsigned* guard,
+                                                          long zero_from4, long wd_until4) {
   const long stride = (long)gridDim.x * blockDim.x;
   if (guard != nullptr && *guard != 0u) {
     for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < n4; i += stride)
-      st4<NT>(g, i, make_float4(0.f, 0.f, 0.f, 0.f));
+      if (i >= zero_from4) st4<NT>(g, i, make_float4(0.f, 0.f, 0.f, 0.f));
     return;
   }
   auto body = [&](long i, float4 wv, float4 gv, float4 mv) {
     float* wp = (float*)&wv; float* gp = (float*)&gv; float* mp = (float*)&mv;
+    const float wd = i < wd_until4 ? wd0 : 0.f;
 #pragma unroll
     for (int k = 0; k < 4; ++k) {
       float d = gp[k] * gscale + wd * wp[k];
@@ -171,7 +179,7 @@ __global__ void __launch_bounds__(256) sgd_stream_kernel(float* __restrict__ w, 
       wp[k] -= lr * d;
     }
     st4<NT>(w, i, wv); st4<NT>(mom, i, mv);
-    if (zero_grad) st4<NT>(g, i, make_float4(0.f, 0.f, 0.f, 0.f));
+    if (zero_grad && i >= zero_from4) st4<NT>(g, i, make_float4(0.f, 0.f, 0.f, 0.f));
     st2<NT>(wb, i, make_uint2(pack_bf2(wp[0], wp[1]), pack_bf2(wp[2], wp[3])));
   };
   const long t = blockIdx.x * (long)blockDim.x + threadIdx.x;
@@ -216,34 +224,41 @@ static int ogrid(long n4) {
   return (int)(b < 1 ? 1 : b);
 }
 
+// zero_from / wd_until (elements, multiples of 4): the gradient is reset only
+// from zero_from on (store-first gradients before it, Fx.grad_mode), weight
+// decay applies only below wd_until -- one launch over a whole arena's
+// store / decay / no-decay regions (was three launches through round 5)
 void sgd_step(float* w, float* g, float* mom, bf16_t* wb, long n, float lr, float momentum,
-              float wd, float gscale, int nesterov, int zero_grad, hipStream_t s, const unsigned* guard) {
+              float wd, float gscale, int nesterov, int zero_grad, hipStream_t s, const unsigned* guard,
+              long zero_from, long wd_until) {
   // n % 4 == 0 (arena segments are padded to 64 elements)
   const dim3 grid(ogrid(n / 4));
+  const long zf4 = zero_from / 4, wu4 = wd_until < 0 ? n / 4 : wd_until / 4;
   switch (optim_pick(n / 4, false)) {
     case 3:
       hipLaunchKernelGGL((sgd_stream_kernel<4, true>), grid, dim3(256), 0, s, w, g, mom, wb, n / 4, lr, momentum, wd,
-                         gscale, nesterov, zero_grad, guard);
+                         gscale, nesterov, zero_grad, guard, zf4, wu4);
       break;
     default:
       hipLaunchKernelGGL(sgd_kernel, grid, dim3(256), 0, s, w, g, mom, wb, n / 4, lr, momentum, wd, gscale, nesterov,
-                         zero_grad, guard);
+                         zero_grad, guard, zf4, wu4);
   }
 }
 
 void adam_step(float* w, float* g, float* m, float* v, bf16_t* wb, long n, float lr, float b1,
                float b2, float eps, float wd, int step, float gscale, int zero_grad,
-               hipStream_t s, const unsigned* guard) {
+               hipStream_t s, const unsigned* guard, long zero_from, long wd_until) {
   const float bc1 = 1.f - powf(b1, (float)step), bc2 = 1.f - powf(b2, (float)step);
   const dim3 grid(ogrid(n / 4));
+  const long zf4 = zero_from / 4, wu4 = wd_until < 0 ? n / 4 : wd_until / 4;
   switch (optim_pick(n / 4, true)) {
     case 3:
       hipLaunchKernelGGL((adam_stream_kernel<4, true>), grid, dim3(256), 0, s, w, g, m, v, wb, n / 4, lr, b1, b2, eps,
-                         wd, bc1, bc2, gscale, zero_grad, guard);
+                         wd, bc1, bc2, gscale, zero_grad, guard, zf4, wu4);
       break;
     default:
       hipLaunchKernelGGL(adam_kernel, grid, dim3(256), 0, s, w, g, m, v, wb, n / 4, lr, b1, b2, eps, wd, bc1, bc2,
-                         gscale, zero_grad, guard);
+                         gscale, zero_grad, guard, zf4, wu4);
   }
 }
 

@@ -481,3 +481,40 @@ def test_sharded_ddp_matches_allreduce(world, wire):
             # half of the fp32 all-reduce, fp32 reduce-scatter ~3/4 (the
             # replicated norm-parameter buckets and tails stay all-reduced)
             assert o["bytes_sh"] < (0.6 if wire == "bf16" else 0.85) * o["bytes_ref"], o
+
+
+# ------------------------------------------------- reduce-scatter output aliasing
+def _rs_alias_worker(rank, world, port, outdir):
+    _init(rank, world, port)
+    from tiresias_amd.parallel.gang import GangPG
+
+    pg = GangPG(list(range(world)), rank, "gloo")
+    n = 1 << 16                                    # per-member slice
+    g = torch.Generator().manual_seed(1234 + rank)
+    base = torch.randn(world * n, generator=g)
+    # the sharded-DDP call: out is this member's own slice of the bucket
+    inplace = base.clone()
+    pg.reduce_scatter(inplace[rank * n:(rank + 1) * n], inplace).wait()
+    # the same reduction into a separate output buffer
+    sep_out = torch.empty(n)
+    pg.reduce_scatter(sep_out, base.clone()).wait()
+    torch.save({"inplace": inplace[rank * n:(rank + 1) * n].clone(), "sep": sep_out, "base": base},
+               os.path.join(outdir, f"rs{rank}.pt"))
+    dist.barrier()
+    pg.shutdown()
+    dist.destroy_process_group()
+
+
+def test_gloo_reduce_scatter_in_place_equals_separate_output(tmp_path):
+    """the gloo reduce-scatter used to pass a view of its
+    own (staged) input as the output. At world 4 the in-place call (output =
+    the member's slice of the input) must equal a reduce-scatter into a
+    separate buffer and the exact fp32 sum of every member's slice."""
+    world = 4
+    _spawn(_rs_alias_worker, world, str(tmp_path))
+    r = [torch.load(tmp_path / f"rs{k}.pt", weights_only=True) for k in range(world)]
+    n = r[0]["sep"].numel()
+    for k in range(world):
+        ref = sum(r[j]["base"][k * n:(k + 1) * n] for j in range(world))
+        assert torch.equal(r[k]["inplace"], r[k]["sep"])
+        assert torch.allclose(r[k]["sep"], ref, rtol=1e-5, atol=1e-5)

@@ -128,6 +128,10 @@ def test_fill_mode_keeps_barrier_idle_low_at_world8():
                      fill_rounds=fill_rounds)
         st = s["fake_stats"]
         assert s["finished"] == len(jobs)
+        # fill-mode accounting never runs a job past its iteration count: the
+        # carry (steps in flight when the plan came) caps the next share and
+        # fill
+        assert s["overrun_iters"] <= 0, s["overrun_iters"]
         return st["barrier_idle_s"] / (st["barrier_idle_s"] + st["busy_s"])
 
     off, fill, both = idle(False, False), idle(True, False), idle(True, True)

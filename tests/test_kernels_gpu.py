@@ -1179,6 +1179,39 @@ def _sgd_adam_check(gpu, n):
     assert rel_err(w, p.detach()) < 1e-5
 
 
+@pytest.mark.parametrize("variant", [0, 3])
+def test_optimizer_region_bounds_equal_per_region_launches(gpu, variant):
+    """One launch over a whole arena with the store / decay / no-decay
+    regions passed as bounds (zero_from, wd_until) equals three launches on
+    the slices: gradients reset only from zero_from on, weight decay only
+    below wd_until (trainer._opt_step, round 6)."""
+    T().optim_variant(variant)
+    try:
+        torch.manual_seed(14)
+        n, zf, wu = 1 << 20, 64 * 1000, 64 * 9000
+        for opt in ("sgd", "adam"):
+            base = [torch.randn(n, device=gpu) for _ in range(4)]
+            one = [t.clone() for t in base] + [torch.empty(n, device=gpu, dtype=BF)]
+            three = [t.clone() for t in base] + [torch.empty(n, device=gpu, dtype=BF)]
+            one[3].abs_(); three[3].abs_()
+            if opt == "sgd":
+                T().sgd_step(one[0], one[1], one[2], one[4], 0.1, 0.9, 1e-2, 0.5, False, True, None, zf, wu)
+                for lo, hi, wd, zero in ((0, zf, 1e-2, False), (zf, wu, 1e-2, True), (wu, n, 0.0, True)):
+                    T().sgd_step(three[0][lo:hi], three[1][lo:hi], three[2][lo:hi], three[4][lo:hi], 0.1, 0.9, wd,
+                                 0.5, False, zero)
+            else:
+                T().adam_step(one[0], one[1], one[2], one[3], one[4], 1e-3, 0.9, 0.98, 1e-9, 1e-2, 2, 1.0, True,
+                              None, zf, wu)
+                for lo, hi, wd, zero in ((0, zf, 1e-2, False), (zf, wu, 1e-2, True), (wu, n, 0.0, True)):
+                    T().adam_step(three[0][lo:hi], three[1][lo:hi], three[2][lo:hi], three[3][lo:hi],
+                                  three[4][lo:hi], 1e-3, 0.9, 0.98, 1e-9, wd, 2, 1.0, zero)
+            for a, b in zip(one, three):
+                assert torch.equal(a, b), opt
+            assert torch.count_nonzero(one[1][:zf]) == zf and torch.count_nonzero(one[1][zf:]) == 0
+    finally:
+        T().optim_variant(-1)
+
+
 # ------------------------------------------------------------------ attention
 def _attn_ref(q, k, v, causal, kv_len=None):
     qf, kf, vf = (t.float().permute(0, 2, 1, 3) for t in (q, k, v))

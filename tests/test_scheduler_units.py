@@ -322,8 +322,9 @@ def test_horus_orders_by_utilisation():
 
 def test_horus_plus_credits_and_kmeans_seeded():
     jobs = [Job(spec(i, g=g, gpu_util_avg=u)) for i, (g, u) in enumerate([(1, 10), (1, 12), (8, 90), (8, 95)])]
-    _, a1, _ = kmeans_jobs(jobs, 2, random.Random(5))
-    _, a2, _ = kmeans_jobs(jobs, 2, random.Random(5))
+    import numpy as np
+    _, a1, _ = kmeans_jobs(jobs, 2, np.random.RandomState(5))
+    _, a2, _ = kmeans_jobs(jobs, 2, np.random.RandomState(5))
     assert a1 == a2 and a1[0] == a1[1] and a1[2] == a1[3] and a1[0] != a1[2]
     pol = make_policy("horus+", SimConfig(num_queue=2))
     for j in jobs:

@@ -56,6 +56,11 @@ NOMINAL_ITER_S = {"resnet50": 0.0113, "vgg16": 0.0080, "transformer": 0.0072, "g
                   "gnmt_tiny": 0.01}
 
 
+# bound on a fill-mode gang vote (Worker._vote): far above a healthy vote
+# (tens of microseconds on RCCL, one gloo round trip on the CPU path)
+VOTE_TIMEOUT_S = float(os.environ.get("TAM_VOTE_TIMEOUT_S", "10"))
+
+
 def gang_ranks(alloc: Dict[str, List[int]], gpn: int) -> Tuple[int, ...]:
     """(virtual) node id + device -> global GPU rank."""
     out = []
@@ -194,6 +199,7 @@ class Controller:
         self.est: Dict[Tuple[str, int], float] = {}
         self.done_iters: Dict[str, int] = {j: 0 for j in self.rjobs}
         self.plan_fill: Dict[str, int] = {}     # fill steps credited for the next plan (echoed to workers)
+        self.max_overrun = 0                    # max over jobs of done_iters - iterations
         self.round = 0
         self.t0 = None
         self.spill = getattr(cfg, "ckpt_policy", "none") == "host"
@@ -263,6 +269,9 @@ class Controller:
                 continue
             self.done_iters[jid] += jr["iters"]
             rj = self.rjobs[jid]
+            # iterations run beyond the job's count (fill-mode accounting:
+            # must stay 0, tests/test_fake_backend.py)
+            self.max_overrun = max(self.max_overrun, self.done_iters[jid] - rj.iterations)
             if jr.get("snap_failed"):
                 self.snapshot_failed(jid)
                 continue
@@ -329,6 +338,7 @@ class Controller:
             if jid not in self.rjobs or n <= 0:
                 continue
             self.done_iters[jid] += int(n)
+            self.max_overrun = max(self.max_overrun, self.done_iters[jid] - self.rjobs[jid].iterations)
             j = self.sched.jobs[jid]
             j.progress = float(min(self.done_iters[jid], self.rjobs[jid].iterations))
 
@@ -694,9 +704,9 @@ class Controller:
                 shr = []
                 for jid, n in assign[r]:
                     s_ = max(s.interf.pair(ms[jid], ms[o]) for o in ms if o != jid)
-                    left = self.rjobs[jid].iterations - self.done_iters[jid]
+                    rem = self.rjobs[jid].iterations - self.done_iters[jid]
                     est = self._iter_est(ms[jid], 1)
-                    shr.append((jid, max(1, min(left, int(round(self.quantum / (est * s_)))))))
+                    shr.append((jid, max(1, min(rem, int(round(self.quantum / (est * s_)))))))
                 assign[r] = shr
             assign[r].sort()
         self.round += 1
@@ -778,6 +788,7 @@ class Worker:
         # steps the controller's snapshot did not see (reported next round)
         self._fill: Optional[dict] = None
         self._carry: List[dict] = []
+        self._fill_cap: Dict[str, int] = {}   # fill bound after a carry-capped share (run())
         self.fill_enabled = os.environ.get("TAM_FILL", "1") != "0"
         # every rank on ONE physical GPU (the one-GPU multi-rank rehearsal):
         # state moves go device to device through HIP IPC (_do_moves_ipc)
@@ -1483,9 +1494,31 @@ class Worker:
         self._snap_failed = set()
         self._consolidate_failed = set()
         # fill-mode steps the last plan's snapshot did not count
+        carry = {}
+        for r in self._carry:
+            if r.get("fill"):
+                carry[r["job"]] = carry.get(r["job"], 0) + int(r.get("iters") or 0)
         skipped += self._carry
         self._carry = []
         jobs = [(jid, n) for jid, n in jobs if jid not in {r["job"] for r in skipped if not r.get("fill")}]
+        # those carried steps are not in the plan's done count yet (they are
+        # credited with THIS report): the plan's share + left would use the
+        # same remaining iterations twice. The carry is the same
+        # on every gang member (equal fill steps, plan-level fill_seen), so
+        # the capped share still matches across the gang.
+        self._fill_cap = {}
+        if carry:
+            left_of = plan.get("left") or {}
+            capped = []
+            for jid, n in jobs:
+                c = carry.get(jid, 0)
+                if c > 0 and isinstance(left_of, dict) and jid in left_of:
+                    rem = int(left_of[jid]) + int(n) - c     # iterations really left before the share
+                    n2 = max(0, min(int(n), rem))
+                    self._fill_cap[jid] = max(0, rem - n2)
+                    n = n2
+                capped.append((jid, n))
+            jobs = capped
         if not jobs:
             return {"rank": self.rank, "job": None, "jobs": skipped, "dev": self._dev_sample(),
                     "ckpt": self._ckpt_report(), "snap": self._snap_poll()}
@@ -1616,8 +1649,19 @@ class Worker:
         """After this rank's share of the round: keep stepping its (single,
         exclusive) job until the next plan is out, instead of idling at the
         round barrier while slower ranks finish (fake backend, headline
-        trace, N=8: barrier idle 20 % -> 4 % of GPU time). Bounded by the
-        job's iterations left; a gang agrees on every extra step (vote)."""
+        trace, N=8: barrier idle 20 % -> 2 % of GPU time). Bounded by the
+        job's iterations left (minus any uncredited carry, ``run``); a gang
+        agrees on every extra step (``_vote``).
+
+        Gang eligibility is decided on PLAN data only (one job on this rank,
+        iterations left), so every member enters the same votes: a member
+        that cannot step (no trainer, a spilled or broken one, an error in
+        its share) still votes -- stop -- in the first vote whenever its
+        communicator is usable, and the gang stops before any fill step. A
+        member without a usable communicator casts nothing; its peers' vote
+        then times out (``VOTE_TIMEOUT_S``), the gang is marked broken and the
+        controller recovers it, instead of the peers blocking for the
+        collective timeout."""
         self._fill = None
         if not self.fill_enabled:
             return
@@ -1625,24 +1669,24 @@ class Worker:
         if len(mine) != 1:
             return
         jid = mine[0][0]
-        left = int((plan.get("left") or {}).get(jid, 0))
-        if left <= 0:                              # plan-level: the same on every gang member
+        left_of = plan.get("left") or {}
+        left = int(left_of.get(jid, 0)) if isinstance(left_of, dict) else 0
+        cap = getattr(self, "_fill_cap", {})
+        if jid in cap:
+            left = min(left, cap[jid])
+        if left <= 0:                              # plan-level (+ the gang-wide carry): same on every member
             return
         t = self.trainers.get(jid)
-        if t is None:
-            return
-        gang = t.ddp is not None and len(self._job_ranks.get(jid, (self.rank,))) > 1
+        gang = len(self._job_ranks.get(jid, (self.rank,))) > 1
+        if t is None or (gang and t.ddp is None):
+            return                                 # nothing to vote with: peers time out (bounded)
         comm_ok = not gang or (t.ddp.comm is not None and not comm_failed(t.group))
         if not comm_ok:
-            return                                 # peers' votes fail on the same communicator
+            return
         local_bad = (getattr(t, "broken", False) or getattr(t, "_spilled", None) or
                      any(r.get("error") for r in rep.get("jobs") or [] if r.get("job") == jid))
         if local_bad and not gang:
             return
-        # a gang member that cannot step still takes part in the FIRST vote
-        # (and votes stop), so peers that can step never wait in a vote it
-        # would not join: eligibility here is partly local (this rank's
-        # trainer state and report), the votes must match on every member
         self._fill = {"job": jid, "left": 0 if local_bad else left, "n": 0, "sec": 0.0, "gang": gang,
                       "done": False, "prev": None, "err": None, "t": t}
 
@@ -1650,15 +1694,48 @@ class Worker:
         """One-element SUM all-reduce over the job's gang: does ANY member
         want to stop? Every member takes the same decision, so the gang runs
         the same number of fill steps on every member (its collectives
-        match)."""
-        v = getattr(t, "_vote_buf", None)
-        if v is None:
+        match).
+
+        On the GPU the vote never drains the compute stream: it is issued on
+        a side stream, so it waits for nothing on the compute stream, and on
+        the communicator's own stream it queues right behind the previous
+        step's gradient buckets -- it completes when that step's LAST bucket
+        is reduced, while the step's optimizer still runs. The result comes
+        back by a D2H copy into pinned memory and a host wait on THAT event
+        (no ``.item()``, no stream synchronize): the host is throttled to one
+        step ahead and the GPU never idles between fill steps (VERDICT r5
+        item 6). The wait is bounded: a member that never votes makes this
+        one raise, and the step is failed like a gang collective error."""
+        cuda = self.device.type == "cuda"
+        vb = getattr(t, "_vote_bufs", None)
+        if vb is None:
             v = torch.zeros(1, dtype=torch.float32, device=self.device)
-            t._vote_buf = v
-        v.fill_(1.0 if stop else 0.0)
+            vh = torch.zeros(1, dtype=torch.float32, pin_memory=cuda)
+            side = torch.cuda.Stream(self.device) if cuda else None
+            vb = t._vote_bufs = (v, vh, side)
+        v, vh, side = vb
         c = t.ddp.comm
-        c.finish([c.start(v)])
-        return float(v.item()) > 0.0
+        deadline = time.perf_counter() + VOTE_TIMEOUT_S
+        if not cuda:
+            v.fill_(1.0 if stop else 0.0)
+            h = c.start(v)
+            if hasattr(h, "wait"):                 # a c10d Work (flat gang): bounded wait
+                from datetime import timedelta
+                h.wait(timedelta(seconds=VOTE_TIMEOUT_S))
+            else:
+                c.finish([h])
+            return float(v[0]) > 0.0
+        with torch.cuda.stream(side):
+            v.fill_(1.0 if stop else 0.0)
+            c.finish([c.start(v)])                 # side stream waits on the collective
+            vh.copy_(v, non_blocking=True)
+            ev = torch.cuda.Event()
+            ev.record(side)
+        while not ev.query():
+            if time.perf_counter() > deadline:
+                raise RuntimeError(f"fill vote timed out after {VOTE_TIMEOUT_S:.0f} s (a gang member never voted)")
+            time.sleep(20e-6)
+        return float(vh[0]) > 0.0
 
     def fill_step(self, ready: bool) -> bool:
         """One fill step when the round's next plan is not out yet
@@ -1682,21 +1759,20 @@ class Worker:
             t.step()
             if cuda and not f["gang"]:
                 # keep one step queued ahead of the one waited on (the GPU
-                # never drains between fill steps)
+                # never drains between fill steps); a gang is throttled by
+                # its next vote instead (no per-step host sync)
                 ev = torch.cuda.Event()
                 ev.record()
                 if f["prev"] is not None:
                     f["prev"].synchronize()
                 f["prev"] = ev
-            elif cuda:
-                torch.cuda.current_stream(self.device).synchronize()
             f["n"] += 1
             dt = time.perf_counter() - t0
             f["sec"] += dt
             self.fill_s_total += dt
             self.fill_steps_total += 1
             return True
-        except Exception as e:                    # a gang peer died mid-collective
+        except Exception as e:                    # a gang peer died mid-collective / never voted
             f["err"] = f"{type(e).__name__}: {e}"
             f["done"] = True
             t.broken = True
@@ -1875,6 +1951,12 @@ def run_replay(cfg: SimConfig, jobs: List[ReplayJob], rank: int, world: int, dev
     distributed = world > 1
     ctrl = None
     log = None
+    if distributed:
+        # ranks declared lost belong to the replay that lost them: bench.py
+        # runs several replays per process, and a stale entry would block
+        # every later communicator that includes that rank
+        from ..parallel.gang import DEAD_RANKS
+        DEAD_RANKS.clear()
     w = worker or Worker(rank, world, device, world_pg, use_graph=use_graph)
     if rank == 0:
         log = MetricsLogger(out_dir, node_logs=False)

@@ -240,6 +240,21 @@ class FakeCluster:
         steps: Dict[int, float] = {}              # rank -> step seconds of its single job
         late = self.late
         self.late = {}
+        left_of = plan.get("left") or {}
+        # fill steps completed after the last plan snapshot are credited with
+        # this round's reports, so the plan's share + left count them twice:
+        # cap both by the carry (cluster_runtime.Worker.run)
+        carried, self.carry = self.carry, {}
+        fill_cap: Dict[str, int] = {}
+        for r, lst in assign.items():
+            if len(lst) == 1:
+                jid, n = lst[0]
+                c = sum(k for j2, (k, _) in (carried.get(r) or {}).items() if j2 == jid)
+                if c > 0 and jid in left_of:
+                    rem = int(left_of[jid]) + int(n) - c
+                    n2 = max(0, min(int(n), rem))
+                    fill_cap[jid] = max(0, rem - n2)
+                    assign[r] = [(jid, n2)]
 
         def ready(x):
             return action_cost.get(x, 0.0) + late.get(x, 0.0)
@@ -277,7 +292,7 @@ class FakeCluster:
             else:
                 busy[r] = t0
             # fill steps completed after the last plan snapshot, in flight then
-            for jid, (k, sec) in (self.carry.pop(r, None) or {}).items():
+            for jid, (k, sec) in (carried.pop(r, None) or {}).items():
                 reps.append({"job": jid, "iters": k, "run_s": sec, "shared": False, "loss": None, "fill": True})
             reports.append({"rank": r, "job": lst[0][0] if lst else None, "jobs": reps, "dev": None})
         self.stats["rounds"] += 1
@@ -285,7 +300,6 @@ class FakeCluster:
         # fill: ranks whose single job has iterations left keep stepping it
         # until the plan (at dur); a gang by agreement (vote per extra step)
         self.fill_seen = {}
-        left_of = plan.get("left") or {}
         filled: Dict[int, float] = {}
         if self.fill:
             done_g: Dict[str, Tuple[int, int, float]] = {}
@@ -293,6 +307,8 @@ class FakeCluster:
                 jid, n = assign[r][0]
                 ranks = self.held[jid]
                 left = int(left_of.get(jid, 0))
+                if jid in fill_cap:
+                    left = min(left, fill_cap[jid])
                 if left <= 0:
                     continue
                 if len(ranks) > 1:
@@ -380,6 +396,7 @@ def run_fake(cfg: SimConfig, jobs: List[ReplayJob], world: int, quantum: float =
         raise ProtocolError(f"replay ended with state still held for {sorted(fc.held)}")
     s = ctrl.sched.summary()
     s.update(rounds=rounds, backend="fake", replay_wall_s=time.perf_counter() - t_wall, fake_stats=dict(fc.stats),
-             virtual_s=clock(), comm_stats=dict(ctrl.comms.stats, live=len(ctrl.comms.live)))
+             virtual_s=clock(), comm_stats=dict(ctrl.comms.stats, live=len(ctrl.comms.live)),
+             overrun_iters=ctrl.max_overrun)
     log.close()
     return s

@@ -175,12 +175,25 @@ class Trainer:
         elif self.device.type == "cuda":
             # store_grad params: every step's first gradient write stores
             # (Fx.grad_mode), so their region is not zeroed -- except a param
-            # nothing wrote this step (its buffer holds an older gradient)
+            # nothing wrote this step (its buffer holds an older gradient).
+            # ONE launch over the whole arena: the store / decay / no-decay
+            # regions are passed as bounds (zero_from, wd_until)
             for p in A.params:
                 if p.store_grad and p.gw_epoch != A.grad_epoch:
                     p.grad.zero_()
-            regions = [(0, A.n_store, self.spec.wd, not Fx.STORE_GRAD), (A.n_store, A.n_decay, self.spec.wd, True),
-                       (A.n_decay, A.numel, 0.0, True)]
+            A.grad_epoch += 1
+            T = _lib.ops()
+            guard = self.model.err if self.uses_persist else None
+            zf = A.n_store if Fx.STORE_GRAD else 0
+            if self.opt == "sgd":
+                T.sgd_step(A.master, A.grad, self.opt_state[0], A.shadow, self.lr, 0.9, self.spec.wd, gscale, False,
+                           True, guard, zf, A.n_decay)
+            else:
+                T.adam_step(A.master, A.grad, self.opt_state[0], self.opt_state[1], A.shadow, self.lr, 0.9, 0.98,
+                            1e-9, self.spec.wd, self.step_count, gscale, True, guard, zf, A.n_decay)
+            if self.uses_persist:
+                _lib.ops().lstm_guard_step(self.model.err)
+            return
         else:
             regions = [(0, A.n_decay, self.spec.wd), (A.n_decay, A.numel, 0.0)]
         A.grad_epoch += 1

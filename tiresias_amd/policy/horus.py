@@ -5,11 +5,14 @@
 * ``horus``: non-preemptive; pending jobs ordered lowest average GPU
   utilisation first (the reference heap, ``base_factory.py:2-14``), the first
   ``lookahead`` (k=5) are tried in order and the ones that fit start.
-* ``horus+``: pending jobs are clustered into ``num_queue`` queues by k-means
-  over job features (#tasks, util avg/max, GPUs per worker, GPUs, mem
-  avg/max; L1 distance, medoid centroids, ``utils.py:4-67``) — SEEDED here
-  (defect D10) and re-clustered only when the pending set changes, not on every
-  insert; each pick comes from the queue with the highest credit
+* ``horus+``: pending jobs are clustered into ``num_queue`` queues by the
+  reference's k-means over job features (#tasks, util avg/max, GPUs per
+  worker, GPUs, mem avg/max; L1 distance, centroids re-picked by the scalar
+  feature-sum score, ``utils.py:4-67``) — SEEDED here (defect D10) with a
+  numpy RandomState, and pinned against the executed reference
+  (``tests/test_ref_parity.py::test_kmeans_matches_reference``); the event
+  engine re-clusters only when the pending set changes, the tick engine on
+  every insert as the reference does; each pick comes from the queue with the highest credit
   (median pending time x length, or length when the median is < 1,
   ``job_queue_manager.py:103-127``).
 * ``gandiva``: FIFO order + Gandiva (co-locating) placement + time slicing:
@@ -39,28 +42,60 @@ def _l1(a: Sequence[float], b: Sequence[float]) -> float:
     return sum(abs(x - y) for x, y in zip(a, b))
 
 
-def kmeans_jobs(jobs: List[Job], k: int, rng: random.Random, max_iter: int = 1000):
-    """k-medoids-style clustering on job features (seeded)."""
+def kmeans_jobs(jobs: List[Job], k: int, rng, max_iter: int = 1000):
+    """The reference's horus+ k-means (``core/jobs/utils.py:36-67``),
+    SEEDED (defect D10), operation for operation so that the same
+    ``numpy.random.RandomState`` stream gives the same clusters:
+
+    * init: ``k`` centroid jobs drawn WITH replacement,
+      ``rng.randint(len(jobs), size=k)`` (:39); duplicates are allowed;
+    * assignment: L1 feature distance (``job_dist`` :4-12), first minimum
+      (``np.argmin``);
+    * update: a cluster's new centroid is the member whose SCALAR score
+      (``transform_to_dist`` :14-22, the feature sum) is closest to the
+      int-truncated mean score, first minimum (``get_closest`` :24-34,
+      ``np.mean(...).astype(int)`` :58); an empty cluster re-draws a random
+      job (``rng.choice(len(jobs))`` :62);
+    * the loop runs while the assignment changed (or on the first pass) and
+      updates the centroids in every pass, the converged one included, as
+      the reference's does (:45-62) -- the RNG stream stays in step.
+
+    ``rng``: a ``numpy.random.RandomState`` (a ``random.Random`` is mapped
+    onto one seeded from it). Returns (centroid indices, assignment, loss)."""
+    import numpy as np
+
     if not jobs:
         return [], [], 0.0
-    k = max(1, min(k, len(jobs)))
+    if not isinstance(rng, np.random.RandomState):
+        rng = np.random.RandomState(rng.randrange(1 << 31) if hasattr(rng, "randrange") else int(rng))
+    k = max(1, int(k))
+    n = len(jobs)
     feats = [_features(j) for j in jobs]
-    cent = [feats[i] for i in rng.sample(range(len(jobs)), k)]
-    assign = [-1] * len(jobs)
-    for _ in range(max_iter):
-        new = [min(range(k), key=lambda c: (_l1(f, cent[c]), c)) for f in feats]
-        if new == assign:
-            break
-        assign = new
+    score = [float(sum(f)) for f in feats]
+    cent = [int(i) for i in rng.randint(n, size=k)]
+    new: List = [None] * n
+    old: List = [None] * n
+    it = 0
+    while it < max_iter and (new != old or it == 0):
+        old = list(new)
+        it += 1
+        for i in range(n):
+            d = [_l1(feats[i], feats[cent[c]]) for c in range(k)]
+            new[i] = min(range(k), key=lambda c: (d[c], c))
         for c in range(k):
-            members = [feats[i] for i in range(len(jobs)) if assign[i] == c]
-            if not members:
-                cent[c] = feats[rng.randrange(len(jobs))]
-                continue
-            mean = [sum(col) / len(members) for col in zip(*members)]
-            cent[c] = min(members, key=lambda m: _l1(m, mean))
-    loss = sum(_l1(feats[i], cent[assign[i]]) for i in range(len(jobs)))
-    return cent, assign, loss
+            members = [i for i in range(n) if new[i] == c]
+            if members:
+                mean = int(np.mean([score[i] for i in members], axis=0).astype(int))
+                best, best_d = None, 99999999999
+                for i in members:                    # get_closest: strict <, first minimum
+                    t = abs(score[i] - mean)
+                    if t < best_d:
+                        best, best_d = i, t
+                cent[c] = best
+            else:
+                cent[c] = int(rng.choice(n))
+    loss = sum(_l1(feats[i], feats[cent[new[i]]]) for i in range(n))
+    return cent, list(new), loss
 
 
 class _RefItem:
@@ -123,7 +158,10 @@ class HorusPlus(Horus):
     def __init__(self, cfg=None, prior=None, rng=None):
         super().__init__(cfg, prior, rng)
         self.k = max(1, int(getattr(cfg, "num_queue", 3) or 3))
-        self.rng = rng or random.Random(getattr(cfg, "seed", 0) or 0)
+        # the reference draws its k-means init from numpy's global stream:
+        # a seeded RandomState of its own here (D10)
+        import numpy as np
+        self.rng = np.random.RandomState(int(getattr(cfg, "seed", 0) or 0))
         self._key = None
         self._assign = {}
         self._queues: List[List[_RefItem]] = [[] for _ in range(self.k)]

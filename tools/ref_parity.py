@@ -105,6 +105,59 @@ SEEDED_D2FIX = "import random, runpy, sys, numpy; numpy.random.seed(0); random.s
                "sys.argv = ['run_sim.py'] + sys.argv[1:]; sys.path.insert(0, '.'); exec(%r); " \
                "runpy.run_path('run_sim.py', run_name='__main__')" % D2FIX
 
+# horus+ k-means at FUNCTION level: the reference's own clusterize()
+# (core/jobs/utils.py:36-67) executed in the scratch copy on heterogeneous
+# job feature sets, numpy seeded per case. Trace-level parity cannot pin it:
+# the same unseeded np.random stream also feeds horus_score's utilisation
+# samples (core/scheduling/horus.py:36 -> infra/device.py:34) and the
+# per-tick log (schedule.py:116), whose draw counts depend on every scoring
+# call. Features: [#tasks, util avg, GPUs per worker, GPUs, util max,
+# mem avg MiB, mem max MiB] with #tasks = GPUs / GPUs per worker.
+KM_SCRIPT = r"""
+import json, sys, numpy
+sys.path.insert(0, '.')
+from core.jobs.utils import clusterize
+class J:
+    def __init__(s, f):
+        s.tasks = [0] * int(f[0]); s.gpu_utilization_avg = f[1]; s.gpu_per_worker = f[2]; s.gpus = f[3]
+        s.gpu_utilization_max = f[4]; s.gpu_mem_avg = f[5]; s.gpu_mem_max = f[6]
+out = []
+for c in json.load(sys.stdin):
+    numpy.random.seed(c["seed"])
+    jobs = [J(f) for f in c["feats"]]
+    cent, assign, loss = clusterize(jobs, k=c["k"])
+    out.append({"cent": [jobs.index(x) for x in cent], "assign": [int(a) for a in assign], "loss": float(loss)})
+print(json.dumps(out))
+"""
+
+
+def kmeans_cases():
+    import random as _r
+    cases = []
+    for ci, (n, k, seed) in enumerate([(5, 2, 0), (12, 3, 1), (20, 3, 7), (33, 4, 3), (40, 2, 11), (9, 5, 2),
+                                      (25, 3, 42), (16, 4, 5)]):
+        rng = _r.Random(1000 + ci)
+        feats = []
+        for _ in range(n):
+            gpw = rng.choice([1, 1, 2, 4])
+            workers = rng.choice([1, 1, 2, 4, 8])
+            ua = round(rng.uniform(5, 95), 1)
+            um = round(min(100.0, ua + rng.uniform(0, 40)), 1)
+            ma = round(rng.uniform(500, 30000), 2)
+            mm = round(ma + rng.uniform(0, 4000), 2)
+            feats.append([workers, ua, gpw, gpw * workers, um, ma, mm])
+        cases.append({"seed": seed, "k": k, "feats": feats})
+    return cases
+
+
+def run_reference_kmeans(ref: str, cases) -> list:
+    p = subprocess.run([sys.executable, "-c", KM_SCRIPT], cwd=ref, input=json.dumps(cases), capture_output=True,
+                       text=True, timeout=300)
+    if p.returncode != 0:
+        raise RuntimeError(f"reference clusterize failed:\n{p.stderr[-2000:]}")
+    return json.loads(p.stdout.strip().splitlines()[-1])
+
+
 _DELTA = re.compile(r"delta-time: (\d+)")
 _PLACE = re.compile(r"placing task (\S+?)_worker\d+ at node (\S+) - device (\d+)")
 # horus / gandiva placement logs trial reservations (placing ... lines, also
@@ -206,6 +259,10 @@ def main() -> None:
                     entry.setdefault("results_d2fix", {})[f"{schedule}/{scheme}"] = run_reference(
                         ref, work, name, spec, schedule, scheme, d2fix=True)
             fixture["traces"][name] = entry
+        cases = kmeans_cases()
+        for c, r in zip(cases, run_reference_kmeans(ref, cases)):
+            c["reference"] = r
+        fixture["kmeans"] = cases
         os.makedirs(os.path.dirname(os.path.abspath(a.out)), exist_ok=True)
         with open(a.out, "w") as f:
             json.dump(fixture, f, indent=1, sort_keys=True)
