@@ -135,7 +135,7 @@ def history_prior(jobs) -> list:
     return sorted(rj.spec.duration * rj.spec.num_gpu for rj in jobs)
 
 
-def scenario_trace(name: str, n_gpus: int, seed: int, tiny: bool = False):
+def scenario_trace(name: str, n_gpus: int, seed: int, tiny: bool = False, sizes=None):
     """The other BASELINE.json configs as fixed job sets on the same runtime:
 
     * ``resnet4``  -- 4 concurrent ResNet-50 DDP jobs, each on n/4 GPUs (1
@@ -151,7 +151,10 @@ def scenario_trace(name: str, n_gpus: int, seed: int, tiny: bool = False):
         g = max(1, n_gpus // 4)
         rows = [("resnet50", g, 0.0, 60) for _ in range(4)]
     elif name == "skew":
-        sizes = [g for g in (2, 4, 8) if g <= n_gpus] or [1]
+        # sizes: the gang widths drawn uniformly (default 2 / 4 / 8; tools/
+        # scenarios.py --sizes adds 1-GPU jobs, whose odd fragments are what
+        # a spread decision can use on a 4x2 virtual-node split)
+        sizes = [g for g in (sizes or (2, 4, 8)) if g <= n_gpus] or [1]
         t = 0.0
         for i in range(4 * n_gpus):
             m = "vgg16" if i % 2 else "resnet50"

@@ -944,8 +944,6 @@ void embedding_backward_op(const Tensor& dout, const Tensor& ids, const Tensor& 
 
 void conv_dma_policy_op(int64_t p) { tam::conv_dma_policy((int)p); }
 void conv_halo_policy_op(int64_t p) { tam::conv_halo_policy((int)p); }
-void conv_stats_force_op(int64_t p) { tam::conv_stats_force((int)p); }
-void conv_igemm_stats_op(int64_t p) { tam::conv_igemm_stats((int)p); }
 void colsum_policy_op(int64_t p) { tam::colsum_policy((int)p); }
 void attn_short_policy_op(int64_t p) { tam::attn_short_policy((int)p); }
 // forced (bm, bn, splits) of the LDS-DMA conv wgrad (A/B sweeps; 0 = heuristic)
@@ -1268,8 +1266,6 @@ TORCH_LIBRARY(tam, m) {
   m.def("gemm_skinny_policy(int on, int force_splits, int nst) -> ()", &gemm_skinny_policy_op);
   m.def("gemm8p_sk_force(int on) -> ()", &gemm8p_sk_force_op);
   m.def("conv_split_policy(int p) -> ()", &conv_split_policy_op);
-  m.def("conv_stats_force(int p) -> ()", &conv_stats_force_op);
-  m.def("conv_igemm_stats(int p) -> ()", &conv_igemm_stats_op);
   m.def("optim_variant(int v) -> ()", &optim_variant_op);
   m.def("gemm_lib_policy(int policy) -> ()", &gemm_lib_policy_op);
   m.def("conv_dma_policy(int policy) -> ()", &conv_dma_policy_op);

@@ -90,8 +90,6 @@ void conv_dma_policy(int p);   // 1: LDS-DMA core where eligible (default), 0: i
 void conv_wgrad_force(int bm, int bn, int splits, int noatomic = 0);
 void conv_wgrad_order(int flat);    // DMA wgrad block order: 1 split-major XCD remap (default), 0 3-D grid
 void conv_wgrad_c64_policy(int p);   // 64-channel 3x3 wgrad kernel: 1 on (default), 0 off, >= 2 blocks per k-slice
-void conv_igemm_stats(int p);   // 1: shallow pointwise convs on the igemm produce BN stats in its epilogue
-void conv_stats_force(int p);   // 1: shallow pointwise convs with BN stats on the LDS-DMA core
 void conv_halo_policy(int p);   // 1: 64-channel 3x3 stride-1 passes on the halo-tile kernel (default)
 bool gemm_select_big_p8(bool ak, bool bk, int M, int N, int K, long lda, long ldb);   // plain-GEMM igemm K-tiles in flight (1..3)
 

@@ -70,28 +70,11 @@ long conv_dgrad_split_ws(const ConvGeom& g) {
   return conv_dma_split_ws(a, force);
 }
 
-// 1: a shallow (Kd 64 / 128) pointwise conv whose BatchNorm statistics are
-// requested runs on the LDS-DMA core anyway (its epilogue accumulates the
-// statistics; the igemm fallback needs a separate bn_stats pass over the
-// output). 0: the cost model alone decides (A/B, TAM_CONV_STATS_FORCE)
-static int g_conv_stats_force = [] {
-  const char* e = getenv("TAM_CONV_STATS_FORCE");
-  return e ? atoi(e) : 0;
-}();
-TAM_KNOB(g_conv_stats_force)
-void conv_stats_force(int p) { g_conv_stats_force = p; }
-
-// 1: pointwise convs that fall back to the igemm accumulate their BN
-// statistics in its epilogue; 0 (default): a separate bn_stats pass. Measured
-// neutral on ResNet-50 (same box, two runs each: 9.096 / 9.099 ms with vs
-// 9.084 / 9.095 without -- the 11 bn_stats launches it removes are paid
-// back in the igemm epilogue); TAM_CONV_IGEMM_STATS=1 for A/B
-static int g_conv_igemm_stats = [] {
-  const char* e = getenv("TAM_CONV_IGEMM_STATS");
-  return e ? atoi(e) : 0;
-}();
-TAM_KNOB(g_conv_igemm_stats)
-void conv_igemm_stats(int p) { g_conv_igemm_stats = p; }
+// (forcing shallow pointwise convs with BN statistics onto the LDS-DMA core,
+// or accumulating their statistics in the igemm epilogue, measured neutral
+// or slower on ResNet-50 -- 9.096 / 9.099 vs 9.084 / 9.095 ms -- and the
+// switches were removed in round 6: the cost model decides, and the igemm
+// fallback gets a separate bn_stats pass)
 
 int conv_fwd(const bf16_t* x, const bf16_t* w, const ConvGeom& g, Epi ep, hipStream_t s, float* ws,
              long ws_floats) {
@@ -100,19 +83,11 @@ int conv_fwd(const bf16_t* x, const bf16_t* w, const ConvGeom& g, Epi ep, hipStr
   if (g_conv_dma && g.dil == 1) {
     CDArgs a = cd_fwd_args(x, w, g);
     if (g_conv_halo && launch_conv_halo(a, ep, s)) return ep.stats ? 1 : 0;
-    int force = g_conv_dma >= 2 ? g_conv_dma - 1 : 0;
-    if (!force && g_conv_stats_force && ep.stats && is_pointwise(g) && Kd < 256 && Kd % 64 == 0) force = 1;
+    const int force = g_conv_dma >= 2 ? g_conv_dma - 1 : 0;
     const int bm = launch_conv_dma(a, ep, s, force, ws, ws_floats);
     if (bm) return ep.stats ? 1 : 0;
   }
   if (is_pointwise(g)) {
-    if (ep.stats && g_conv_igemm_stats && g.C < 512 && ep.mode == 0) {
-      // shallow pointwise conv (the LDS-DMA core declined it): the igemm it
-      // routes to anyway, with the BN statistics in its epilogue (no
-      // bn_stats pass over the output)
-      gemm_igemm(x, g.C, true, w, g.C, true, M, g.K, g.C, ep, s);
-      return 1;
-    }
     ep.stats = nullptr;
     gemm(x, g.C, true, w, g.C, true, M, g.K, g.C, ep, false, s);
     return 0;

@@ -210,6 +210,10 @@ class Engine {
   // nodes (it waits for a free node; the wait-vs-spread rule decides only
   // for gangs wider than a node)
   void set_spread_node(bool on) { spread_node_ = on; }
+  // spread_rule "price": the wait-vs-spread penalty also charges the queued
+  // gangs whose consolidated block the spread's fragments delay
+  // (engine/spread.py::SpreadAdvisor.fragment_cost)
+  void set_spread_price(bool on) { spread_price_ = on; }
   // preemptive policies on topology placements: lazy (default) or eager
   void set_lazy_preempt(bool on) { lazy_ = on; }
   long spread_decisions(bool spread) const { return spread ? n_spread_ : n_wait_; }
@@ -823,6 +827,21 @@ class Engine {
     for (double t : times) m = std::min(m, t);
     return m;
   }
+  // engine/spread.py::SpreadAdvisor.fragment_cost (terms summed ascending)
+  double fragment_cost(const Job& j, double hold_s) const {
+    const int gpn = topo_.gpn;
+    std::vector<double> terms;
+    for (long k : active_) {
+      const Job& q = jobs_[k];
+      if (&q == &j || q.state != PEND || q.gpu < 2) continue;
+      const double w = wait_for_block(q, std::max(1, (q.gpu + gpn - 1) / gpn));
+      if (w < hold_s) terms.push_back((hold_s - w) * q.gpu / (double)std::max(1, j.gpu));
+    }
+    std::sort(terms.begin(), terms.end());
+    double s = 0.0;
+    for (double t : terms) s += t;
+    return s;
+  }
   bool should_spread(const Job& j, int k, int min_nodes) const {
     const double r_k = spread_rate(j, k), r_min = spread_rate(j, min_nodes);
     double rem = 0;
@@ -830,7 +849,8 @@ class Engine {
     if (!remaining_wall(j, rem) || r_k <= 0) {
       ok = true;
     } else {
-      const double penalty = (1.0 / r_k - 1.0 / std::max(r_min, 1e-9)) * rem;
+      double penalty = (1.0 / r_k - 1.0 / std::max(r_min, 1e-9)) * rem;
+      if (spread_price_) penalty += fragment_cost(j, rem / r_k);
       ok = wait_for_block(j, min_nodes) > penalty;
     }
     ++(ok ? n_spread_ : n_wait_);
@@ -919,7 +939,7 @@ class Engine {
   bool lazy_ = true;
   Place place_ = P_COUNT;
   Costs costs_;
-  bool spread_wait_ = false, spread_node_ = false, svc_online_ = true;
+  bool spread_wait_ = false, spread_node_ = false, spread_price_ = false, svc_online_ = true;
   std::vector<double> svc_init_;
   ServiceEst svc_;
   mutable long n_spread_ = 0, n_wait_ = 0;

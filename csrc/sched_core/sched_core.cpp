@@ -116,6 +116,7 @@ PYBIND11_MODULE(_sched_core, m) {
       .def("costs", &costs_py)
       .def("set_spread_wait", &Engine::set_spread_wait, py::arg("on"))
       .def("set_spread_node", &Engine::set_spread_node, py::arg("on"))
+      .def("set_spread_price", &Engine::set_spread_price, py::arg("on"))
       .def("set_lazy_preempt", &Engine::set_lazy_preempt, py::arg("on"))
       .def("spread_decisions", &Engine::spread_decisions, py::arg("spread"))
       .def("run_topo", &run_topo_py, py::arg("submit"), py::arg("duration"), py::arg("gpus"),

@@ -933,12 +933,11 @@ def test_batchnorm_relu_bitmask(gpu, res, add, shape):
 @pytest.mark.parametrize("policy", [1, 3])
 @pytest.mark.parametrize("shape", [(8, 28, 28, 128, 256, 3, 1, 1), (16, 14, 14, 256, 1024, 1, 1, 0),
                                    (4, 56, 56, 64, 64, 3, 1, 1), (8, 28, 28, 256, 512, 1, 2, 0),
-                                   # shallow pointwise: the igemm epilogue's statistics
                                    (8, 28, 28, 128, 512, 1, 1, 0), (4, 56, 56, 64, 256, 1, 1, 0),
                                    (4, 56, 56, 256, 64, 1, 1, 0), (3, 9, 9, 64, 136, 1, 1, 0)])
 def test_conv_fwd_bn_stats(gpu, shape, policy):
-    """BatchNorm sums accumulated by the conv epilogue (fp64 atomics; the
-    LDS-DMA core's, or the igemm's for shallow pointwise convs) == column
+    """BatchNorm sums accumulated by the conv epilogue (fp64 atomics, the
+    LDS-DMA core's; shapes it declines skip) == column
     sums / sums of squares of the stored bf16 output; and bn_forward over those
     sums == bn_forward computing its own statistics (stats pass into a zeroed
     workspace, and into its own temporary)."""
@@ -951,7 +950,6 @@ def test_conv_fwd_bn_stats(gpu, shape, policy):
     from tiresias_amd.ops.functional import BN_SHARDS
     sums = torch.zeros(BN_SHARDS * 2 * K, device=gpu, dtype=torch.float64)
     T().conv_dma_policy(policy)
-    T().conv_igemm_stats(1)              # shallow pointwise: the igemm epilogue's statistics
     try:
         done = T().conv_fwd(x, w, y, st, pd, 1, None, False, sums)
     finally:

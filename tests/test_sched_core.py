@@ -110,3 +110,36 @@ def test_native_priced_matches_python(ckpt, net, scheme, policy, tmp_path):
     np.testing.assert_allclose(ns["per_job"]["overhead"], py_ov, rtol=1e-9, atol=1e-9)
     if ckpt != "none" and policy != "fifo":
         assert ns["ckpt_overhead_s"] > 0
+
+
+def test_price_rule_native_equals_python():
+    """spread_rule "price" (the wait-vs-spread penalty also charging the
+    queued gangs the fragments delay, engine/spread.py::fragment_cost):
+    the native core takes the same decisions as the Python engine on a
+    priced Philly-shaped replay (terms summed in ascending order in both)."""
+    import csv as _csv
+    import dataclasses
+    import os
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    sys.path.insert(0, os.path.join(root, "tools"))
+    import sweep_10k as S
+    from tiresias_amd.engine.native import simulate_native
+    from tiresias_amd.engine.sim import simulate
+
+    hist = S._trace(600, 1.2, 7919)
+    prior = os.path.join(os.environ.get("TMPDIR", "/tmp"), f"prior_price_{os.getpid()}.csv")
+    with open(prior, "w", newline="") as f:
+        w = _csv.writer(f)
+        w.writerow(["duration"])
+        for x in hist:
+            w.writerow([round(x.duration * x.num_gpu, 3)])
+    try:
+        specs = S._trace(600, 1.2, 0)
+        for pol in ("gittins", "dlas-gpu"):
+            cfg = dataclasses.replace(S._cfg(pol, "tiresias", prior, 0, "measured", True, "lazy"), spread_rule="price")
+            nat, py = simulate_native(cfg, specs), simulate(cfg, specs)
+            assert nat["finished"] == py["finished"] and nat["preemptions"] == py["preemptions"]
+            assert abs(nat["avg_jct"] - py["avg_jct"]) < 1e-6 * py["avg_jct"]
+    finally:
+        os.remove(prior)

@@ -88,7 +88,8 @@ def define_flags() -> None:
     D.DEFINE_float("skew_threshold", 0.5, "placement-sensitivity threshold (largest tensor / total)")
     D.DEFINE_string("spread_rule", "node", "tiresias placement, insensitive gangs: fragments (spread "
                     "whenever no consolidated block is free) | wait (spread only when the expected wait "
-                    "for a block exceeds the spread penalty, engine/spread.py) | node (as wait, but a gang "
+                    "for a block exceeds the spread penalty, engine/spread.py) | price (as wait, the penalty "
+                    "also charging the queued gangs the fragments delay) | node (as wait, but a gang "
                     "that fits one node is never fragmented and a wider gang fills the fullest-free "
                     "nodes first)")
     D.DEFINE_string("preempt_rule", "lazy", "preemptive policies: lazy (preempt only what a chosen job's "
@@ -181,7 +182,7 @@ class SimConfig:
     gandiva_mem_util: str = "one"
     replace_all: bool = False
     skew_threshold: float = 0.5
-    spread_rule: str = "node"          # tiresias placement: node | wait | fragments (engine/spread.py)
+    spread_rule: str = "node"          # tiresias placement: node | wait | price | fragments (engine/spread.py)
     preempt_rule: str = "lazy"         # preemptive policies: lazy | eager (engine/sim.py::_schedule_lazy)
     ddp_shard: bool = False            # live gangs: sharded data parallelism (parallel/ddp.py)
     ddp_wire: str = "fp32"             # sharded gangs: reduce-scatter dtype fp32 | bf16

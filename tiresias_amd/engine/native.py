@@ -61,12 +61,13 @@ def simulate_native(cfg: SimConfig, specs: List[JobSpec], prior: Optional[List[f
                              float(cfg.solve_starvation), float(cfg.gittins_delta or 3250.0),
                              [float(x) for x in prior], online)
     rule = getattr(cfg, "spread_rule", "node")
-    if rule not in ("node", "wait", "fragments"):
-        raise ValueError(f"spread_rule must be node | wait | fragments, got {rule!r}")
-    wait_rule = scheme == "tiresias" and rule in ("wait", "node")
+    if rule not in ("node", "wait", "fragments", "price"):
+        raise ValueError(f"spread_rule must be node | wait | price | fragments, got {rule!r}")
+    wait_rule = scheme == "tiresias" and rule in ("wait", "node", "price")
     priced = _set_costs(eng, cfg, specs, force=wait_rule)
     eng.set_spread_wait(wait_rule)
     eng.set_spread_node(scheme == "tiresias" and rule == "node")
+    eng.set_spread_price(scheme == "tiresias" and rule == "price")
     eng.set_lazy_preempt(getattr(cfg, "preempt_rule", "lazy") == "lazy")
     t0 = time.perf_counter()
     sub_a = np.array([s.submit_time for s in specs], dtype=np.float64)

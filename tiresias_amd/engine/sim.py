@@ -97,10 +97,11 @@ class Simulator:
         self.iter_s_of = lambda j: (j.spec.duration / j.spec.iterations
                                     if j.spec.iterations and j.spec.iterations > 0 else 0.25)
         rule = getattr(cfg, "spread_rule", "node")
-        if rule not in ("node", "wait", "fragments"):
-            raise ValueError(f"spread_rule must be node | wait | fragments, got {rule!r}")
-        if scheme == "tiresias" and rule in ("wait", "node"):
-            self.placement.advisor = SpreadAdvisor(self._remaining_wall, self._spread_rate)
+        if rule not in ("node", "wait", "fragments", "price"):
+            raise ValueError(f"spread_rule must be node | wait | price | fragments, got {rule!r}")
+        if scheme == "tiresias" and rule in ("wait", "node", "price"):
+            self.placement.advisor = SpreadAdvisor(self._remaining_wall, self._spread_rate,
+                                                   price_fragments=rule == "price")
             self.placement.jobs_by_id = self.jobs
             self.placement.spread_node_gangs = rule != "node"
         self.now = 0.0

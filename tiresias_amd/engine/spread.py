@@ -20,7 +20,9 @@ attained service a, divided by its GPUs (and its current rate). The wait
 for a block is the time until enough running jobs on one node (or on enough
 whole nodes, for gangs wider than a node) are expected to finish. Queued
 jobs that might claim the block first are ignored (an optimistic wait: it
-errs toward consolidating). The reference has no such rule: its live
+errs toward consolidating). Under spread_rule ``price`` the spread is also
+charged for the queued gangs whose own consolidated block its fragments
+delay (``fragment_cost``). The reference has no such rule: its live
 ``yarn`` path always consolidates (``core/scheduling/algorithm.py:394-415``)
 and the model-skew data (``core/models.py:8-26``) is never used.
 """
@@ -79,9 +81,12 @@ class SpreadAdvisor:
     ``remaining_wall(job)``: expected wall seconds a RUNNING or pending job
     still needs; ``spread_rate(job, k)``: its progress rate over k nodes."""
 
-    def __init__(self, remaining_wall: Callable, spread_rate: Callable):
+    def __init__(self, remaining_wall: Callable, spread_rate: Callable, price_fragments: bool = False):
         self.remaining_wall = remaining_wall
         self.spread_rate = spread_rate
+        # spread_rule "price": also charge the spread for the queued gangs
+        # whose consolidated block it delays (fragment_cost)
+        self.price_fragments = price_fragments
         self.decisions = {"spread": 0, "wait": 0}
 
     def wait_for_block(self, cluster, job, jobs_by_id, gpn: int, min_nodes: int) -> float:
@@ -122,7 +127,25 @@ class SpreadAdvisor:
             return times[min_nodes - 1] if len(times) >= min_nodes else math.inf
         return min(times, default=math.inf)
 
-    def should_spread(self, cluster, job, jobs_by_id, k: int, gpn: int, min_nodes: int) -> bool:
+    def fragment_cost(self, cluster, job, jobs_by_id, gpn: int, hold_s: float) -> float:
+        """What a spread of ``job`` costs the QUEUED gangs, in ``job``'s own
+        seconds: the spread holds node fragments for ``hold_s`` (its expected
+        wall time at the spread rate); a pending gang q whose consolidated
+        block would otherwise free up after w_q < hold_s waits hold_s - w_q
+        longer, weighted by its GPUs over the job's. Every queued gang is
+        assumed to want the touched nodes (a conservative charge). The terms
+        are summed in ascending order, as the native core does, so both
+        engines take the same decision (tests/test_sched_core.py)."""
+        terms = []
+        for q in jobs_by_id.values():
+            if q is job or not q.is_pending or q.num_gpu < 2:
+                continue
+            w = self.wait_for_block(cluster, q, jobs_by_id, gpn, max(1, math.ceil(q.num_gpu / gpn)))
+            if w < hold_s:
+                terms.append((hold_s - w) * q.num_gpu / max(1, job.num_gpu))
+        return sum(sorted(terms))
+
+    def should_spread(self, cluster, job, jobs_by_id, k: int, gpn: int, min_nodes: int, count: bool = True) -> bool:
         r_k = self.spread_rate(job, k)
         r_min = self.spread_rate(job, min_nodes)
         rem = self.remaining_wall(job)
@@ -130,6 +153,9 @@ class SpreadAdvisor:
             ok = True                      # no history yet: the skew-aware default
         else:
             penalty = (1.0 / r_k - 1.0 / max(r_min, 1e-9)) * rem
+            if self.price_fragments:
+                penalty += self.fragment_cost(cluster, job, jobs_by_id, gpn, rem / r_k)
             ok = self.wait_for_block(cluster, job, jobs_by_id, gpn, min_nodes) > penalty
-        self.decisions["spread" if ok else "wait"] += 1
+        if count:
+            self.decisions["spread" if ok else "wait"] += 1
         return ok

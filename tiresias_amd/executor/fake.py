@@ -397,6 +397,7 @@ def run_fake(cfg: SimConfig, jobs: List[ReplayJob], world: int, quantum: float =
     s = ctrl.sched.summary()
     s.update(rounds=rounds, backend="fake", replay_wall_s=time.perf_counter() - t_wall, fake_stats=dict(fc.stats),
              virtual_s=clock(), comm_stats=dict(ctrl.comms.stats, live=len(ctrl.comms.live)),
-             overrun_iters=ctrl.max_overrun)
+             overrun_iters=ctrl.max_overrun, oracle=dict(getattr(ctrl.sched.placement, "oracle_stats", {})),
+             spread_advice=dict(getattr(getattr(ctrl.sched.placement, "advisor", None), "decisions", {}) or {}))
     log.close()
     return s

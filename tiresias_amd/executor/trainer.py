@@ -69,8 +69,6 @@ class Trainer:
         self.capture_s = 0.0     # host seconds spent capturing the hipGraph
         self._side = None
         self._ws = None                 # weight-gradient stream (1-GPU jobs)
-        self._gs = None                 # grouped weight-gradient stream (early flush)
-        self._aux = None                # aux stream (LN weight-gradient reductions)
         self._defer_n = 0               # problems the last backward deferred
         self.overlap_wgrad = self.spec.overlap_wgrad if overlap_wgrad is None else overlap_wgrad
         # grouped weight gradients (TAM_GROUP_WGRAD=0 turns them off for A/B runs)
@@ -99,16 +97,6 @@ class Trainer:
                 self._ws = torch.cuda.Stream(self.device)
             ws = self._ws
         Fx.set_wgrad_stream(ws)
-        # 1-GPU jobs: small reductions that nothing in the backward reads
-        # (LayerNorm weight-gradient column sums) go to an aux stream,
-        # joined before the optimizer (a gang's bucket all-reduce is ordered
-        # after the compute stream only: none there)
-        aux = None
-        if self.device.type == "cuda" and self.ddp is None:
-            if self._aux is None:
-                self._aux = torch.cuda.Stream(self.device)
-            aux = self._aux
-        Fx.set_aux_stream(aux)
         # independent model branches on their own streams (1-GPU jobs;
         # ops/functional.py::on_branch), joined before the optimizer
         nb = getattr(self.model, "branch_streams", 0) if self.branches else 0
@@ -117,15 +105,11 @@ class Trainer:
                 self._bs = [torch.cuda.Stream(self.device) for _ in range(nb)]
             Fx.set_branch_streams(self._bs)
         group = (self.device.type == "cuda" and self.ddp is None and self.group_wgrad)
-        gs = None
         if group:
-            # early flush on a side stream (ops/functional.py defer_wgrad):
-            # the expected count is the previous backward's
-            if self.spec.group_early and self._defer_n:
-                if self._gs is None:
-                    self._gs = torch.cuda.Stream(self.device)
-                gs = self._gs
-            Fx.defer_wgrad(True, expect=self._defer_n if gs is not None else 0, stream=gs)
+            # the backward's weight gradients as ONE grouped launch at its end
+            # (an early flush on a side stream measured slower: ResNet-50 9.07
+            # vs 8.89 ms, Transformer 5.41 vs 5.30; removed in round 6)
+            Fx.defer_wgrad(True)
         try:
             if self.spec.kind == "image":
                 logits = self.model.forward(d["x"])
@@ -145,14 +129,9 @@ class Trainer:
             if group:
                 Fx.defer_wgrad(False, discard=True)
             Fx.set_wgrad_stream(None)
-            Fx.set_aux_stream(None)
             Fx.set_branch_streams(None)
         if ws is not None:
             torch.cuda.current_stream(self.device).wait_stream(ws)   # join before the optimizer
-        if gs is not None:
-            torch.cuda.current_stream(self.device).wait_stream(gs)
-        if aux is not None:
-            torch.cuda.current_stream(self.device).wait_stream(aux)
         if self.device.type == "cuda" and self.ddp is None and nb:
             for s in self._bs:
                 torch.cuda.current_stream(self.device).wait_stream(s)

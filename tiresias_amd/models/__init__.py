@@ -42,12 +42,6 @@ class ModelSpec:
     # Linear weight gradients deferred and issued as ONE grouped launch per
     # backward (ops/functional.py defer_wgrad; 1-GPU jobs)
     group_wgrad: bool = False
-    # ...issued early on a side stream, beside the rest of the backward, once
-    # the previous step's count of deferred problems is reached. Off: measured
-    # slower on MI355X (hipGraph steps, two runs each: ResNet-50 9.07 vs 8.89
-    # ms, Transformer 5.41 vs 5.30 -- the grouped launch and the memory-bound
-    # tail of the backward contend for the same CUs); TAM_GROUP_EARLY=1 for A/B
-    group_early: bool = bool(int(os.environ.get("TAM_GROUP_EARLY", "0")))
 
 
 MODELS: Dict[str, ModelSpec] = {

@@ -93,29 +93,19 @@ class _OnWgrad:
 _DEFER_WGRAD: Optional[list] = None
 _DEFER_CHUNK = int(os.environ.get("TAM_WGRAD_GROUP_CHUNK", "0") or 0)
 _GROUP_OK: dict = {}
-# early flush (``defer_wgrad(True, expect=n, stream=s)``): the trainer knows
-# from its previous step how many problems a backward defers; the grouped
-# launch is issued on side stream s as soon as the n-th is deferred, so it
-# runs beside the rest of the backward (ResNet-50: the stage-0 / stem
-# backward, memory-bound, after the last deferred 1x1 conv of stage 1)
-_DEFER_EXPECT = 0
 _DEFER_COUNT = 0
-_GROUP_STREAM = None
 
 
-def defer_wgrad(on: bool, discard: bool = False, expect: int = 0, stream=None) -> None:
+def defer_wgrad(on: bool, discard: bool = False) -> None:
     """Start (True) or stop (False) deferring Linear weight gradients; stopping
     with problems still pending is a programming error (flush first) unless
-    ``discard`` (an aborted step). ``expect`` / ``stream``: the early flush
-    (above); the caller joins ``stream`` before reading the gradients."""
-    global _DEFER_WGRAD, _DEFER_EXPECT, _DEFER_COUNT, _GROUP_STREAM
-    _DEFER_EXPECT, _DEFER_COUNT = (expect, 0) if on else (0, 0)
-    _GROUP_STREAM = stream if on else None
+    ``discard`` (an aborted step)."""
+    global _DEFER_WGRAD, _DEFER_COUNT
+    _DEFER_COUNT = 0
     if not on and _DEFER_WGRAD and not discard:
         raise RuntimeError("defer_wgrad(False) with unflushed weight gradients")
     if not on:
         _DEFER_LNRED.clear()               # (an aborted step: its partial rows are dropped)
-        _DEFER_SLABS.clear()
     if not on and _DEFER_WGRAD:
         for it in _DEFER_WGRAD:            # dropped writes: the next one must store (grad_mode)
             it[2].gw_epoch = -1
@@ -159,13 +149,11 @@ def deferred_count() -> int:
 
 
 def _deferred(pending_flush: bool = True) -> None:
-    """After appending one deferred problem: count it; flush when the
-    expected total is reached (early flush) or a chunk is full."""
+    """After appending one deferred problem: count it; flush when a chunk is
+    full."""
     global _DEFER_COUNT
     _DEFER_COUNT += 1
-    if _DEFER_EXPECT and _DEFER_COUNT == _DEFER_EXPECT:
-        flush_wgrad()
-    elif _DEFER_CHUNK and len(_DEFER_WGRAD) >= _DEFER_CHUNK:
+    if _DEFER_CHUNK and len(_DEFER_WGRAD) >= _DEFER_CHUNK:
         flush_wgrad()
 
 
@@ -173,13 +161,6 @@ def flush_wgrad() -> int:
     """Issue every deferred weight gradient as one grouped launch (on the
     weight-gradient stream when one is installed), then signal grad_ready.
     Returns the number of problems flushed."""
-    if _DEFER_SLABS:
-        sl = list(_DEFER_SLABS)
-        _DEFER_SLABS.clear()
-        _T().wgrad_slab_reduce_many([e[0] for e in sl], [e[1] for e in sl], [e[2].grad for e in sl],
-                                    [1] * len(sl))
-        for e in sl:
-            e[2].grad_ready()
     if _DEFER_LNRED:
         lnr = list(_DEFER_LNRED)
         _DEFER_LNRED.clear()
@@ -194,7 +175,7 @@ def flush_wgrad() -> int:
     items = list(pend)
     pend.clear()
     dys = [it[0] for it in items]
-    with _OnWgrad(*dys, *[it[1] for it in items], stream=_GROUP_STREAM):
+    with _OnWgrad(*dys, *[it[1] for it in items]):
         empty = torch.empty(0, dtype=torch.float32, device=dys[0].device)
         # it[5] (when present): the 2-D view of a conv weight's gradient
         _T().gemm_wgrad_grouped(dys, [it[1] for it in items], [it[5] if len(it) > 5 else it[2].grad for it in items],
@@ -386,13 +367,10 @@ def _conv_out(h: int, k: int, s: int, p: int, d: int = 1) -> int:
     return (h + 2 * p - d * (k - 1) - 1) // s + 1
 
 
-# BatchNorm-backward reduction of a consumer_masks BN computed in the consumer
-# conv's dgrad epilogue (Epi::bnx). Measured on ResNet-50 bs 64 (rocprofv3,
-# profiles/r2/resnet50/resnet50_kernel_stats_v3_dgradbn.csv): 23 of 53
-# bn_bwd_reduce launches per step go away (-127 us) but the dgrad convs that
-# now read the BN input in their epilogue get +165 us slower; graph step
-# 10.65 -> 10.66 ms. Off by default; the GPU test keeps the path exact.
-BN_DGRAD_FUSION = os.environ.get("TAM_BN_DGRAD_FUSION", "0") == "1"
+# (the BatchNorm-backward reduction of a consumer_masks BN computed in the
+# consumer conv's dgrad epilogue measured neutral on ResNet-50 -- 23 of 53
+# bn_bwd_reduce launches gone, -127 us, the dgrad convs +165 us -- and its
+# model plumbing was removed in round 6; profiles/r6/bn_fold.md)
 
 
 # relu BNs whose backward applies the ReLU mask itself keep it as 1 bit per
@@ -439,10 +417,6 @@ class _Conv(Function):
         ctx.w, ctx.b, ctx.stride, ctx.pad, ctx.in_relu = w, b, stride, pad, in_relu
         ctx.save_for_backward(x, y if (relu and mask_own_relu) else None)
         ctx.part = part
-        # x is the output of a BatchNorm whose ReLU backward this conv applies:
-        # its dgrad epilogue can also produce that BN's backward reduction
-        slot = getattr(x, "_tam_slot", None) if (in_relu and BN_DGRAD_FUSION) else None
-        ctx.bn_slot = slot if (slot is not None and slot.src is not None) else None
         return y
 
     @staticmethod
@@ -459,7 +433,6 @@ class _Conv(Function):
                 dy = (dy.float() * (y.float() > 0)).to(BF16)
         dx = None
         deferred = False
-        slab_deferred = False
         if dy.is_cuda:
             K, R, S, C = w.shape
             Mr = dy.numel() // K
@@ -481,28 +454,12 @@ class _Conv(Function):
                     # write costs a zero pass of dW on the fp32-atomic split paths
                     # (ResNet-50: 29 more zero launches per step when conv weights
                     # were store_grad), the optimizer's bulk zeroing does not
-                    if _DEFER_WGRAD is not None and SLAB_DEFER and ow.s is None:
-                        slabs, sp = _T().conv_wgrad_deferred(dy, x, w.grad, st, pd, 1, 1,
-                                                             b.grad if b is not None else None, True)
-                        if sp > 0:
-                            # dW itself is written by the batched reduce at the flush
-                            _DEFER_SLABS.append((slabs, sp, w))
-                            slab_deferred = True
-                    else:
-                        _T().conv_wgrad(dy, x, w.grad, st, pd, 1, 1, b.grad if b is not None else None,
-                                        ow.s is None)
+                    _T().conv_wgrad(dy, x, w.grad, st, pd, 1, 1, b.grad if b is not None else None,
+                                    ow.s is None)
             if ctx.needs_input_grad[0]:
                 dx = torch.empty_like(x)
                 wt = getattr(w, "wt", None)
-                if wt is not None:
-                    _wt_join(dx.device)
-                sl = ctx.bn_slot
-                if wt is not None and sl is not None:
-                    bx, bmean, brstd, bws = sl.src
-                    sums = _bn_sums(bws, x.shape[-1], x.device)
-                    done = _T().conv_dgrad_pre(dy, w.w, wt, dx, st, pd, 1, x, sums, bx, bmean, brstd)
-                    sl.bwd_part = (sums, dx) if done else None
-                elif wt is not None:     # re-laid once per step (prepare_conv_wt)
+                if wt is not None:       # re-laid once per step (prepare_conv_wt)
                     _T().conv_dgrad_pre(dy, w.w, wt, dx, st, pd, 1, x if ctx.in_relu else None)
                 else:
                     wt = torch.empty_like(w.w)
@@ -522,10 +479,7 @@ class _Conv(Function):
             w.grad += grads[-1].permute(0, 2, 3, 1)
             if b is not None:
                 b.grad += dy.float().sum((0, 1, 2))
-        if slab_deferred:
-            if b is not None:                  # the bias gradient is complete now
-                b.grad_ready()
-        elif deferred:
+        if deferred:
             _deferred()
         else:
             w.grad_ready()
@@ -534,51 +488,24 @@ class _Conv(Function):
         return dx, None, None, None, None, None, None, None, None, None
 
 
-# the re-laid weights are first read by the backward's dgrad: the re-lay CAN
-# run on a side stream beside the forward, the first dgrad waiting for it.
-# Off: slower in hipGraph replay (same box, two runs each: ResNet-50 9.02-9.03
-# vs 8.88 ms, VGG-16 6.65 vs 6.61-6.62 ms -- a fork / join costs more than
-# the 60 us launch it hides); TAM_WT_SIDE=1 for A/B
-_WT_STREAMS: dict = {}     # compute stream -> its side stream (GPU-shared jobs stay independent)
-_WT_READY = None
-WT_SIDE = os.environ.get("TAM_WT_SIDE", "0") != "0"
+# the re-laid weights are first read by the backward's dgrad. A side-stream
+# re-lay beside the forward measured slower in hipGraph replay (ResNet-50
+# 9.02-9.03 vs 8.88 ms, VGG-16 6.65 vs 6.61-6.62 ms: a fork / join costs more
+# than the 60 us launch it hides) and was removed in round 6.
 
 
 def prepare_conv_wt(params: List[Param]) -> None:
     """Re-lay every conv weight [K,R,S,C] -> [C,R,S,K] (the dgrad operand) in
     ONE launch per step, into per-parameter buffers kept across steps (the
     dgrad then skips its own transpose). Call at the start of the forward:
-    the weights are final for the step then. The launch goes on a side stream
-    (forked here, joined by the first dgrad: _wt_join), so it overlaps the
-    forward. No-op on CPU."""
-    global _WT_READY
+    the weights are final for the step then. No-op on CPU."""
     if not params or not params[0].w.is_cuda:
         return
     for p in params:
         if getattr(p, "wt", None) is None or p.wt.device != p.w.device:
             p.wt = torch.empty_like(p.w)
-    if not WT_SIDE:
-        _T().conv_weight_t_batch([p.w for p in params], [p.wt for p in params])
-        return
-    dev = params[0].w.device
-    cur = torch.cuda.current_stream(dev)
-    side = _WT_STREAMS.get(cur.cuda_stream)
-    if side is None:
-        side = _WT_STREAMS[cur.cuda_stream] = torch.cuda.Stream(dev)
-    side.wait_stream(cur)
-    with torch.cuda.stream(side):
-        _T().conv_weight_t_batch([p.w for p in params], [p.wt for p in params])
-    ev = torch.cuda.Event()
-    ev.record(side)
-    _WT_READY = ev
+    _T().conv_weight_t_batch([p.w for p in params], [p.wt for p in params])
 
-
-def _wt_join(dev) -> None:
-    """Order the current stream after the side-stream weight re-lay (once)."""
-    global _WT_READY
-    if _WT_READY is not None:
-        torch.cuda.current_stream(dev).wait_event(_WT_READY)
-        _WT_READY = None
 
 
 def conv2d(x: torch.Tensor, w: Param, b: Optional[Param] = None, stride: int = 1, pad: int = 0,
@@ -605,15 +532,10 @@ class GradSlot:
     BN's backward adds it while loading dy (bn_backward ``addend``), so the
     residual-branch sum is never materialised (no separate add kernel)."""
 
-    __slots__ = ("stash", "src", "bwd_part")
+    __slots__ = ("stash",)
 
     def __init__(self):
         self.stash = None
-        # consumer_masks BNs: (x, mean, rstd, backward sums workspace) for the
-        # consumer conv's dgrad epilogue, which accumulates the BN-backward
-        # sums and parks (sums, its dx) in bwd_part
-        self.src = None
-        self.bwd_part = None
 
 
 class _Tap(Function):
@@ -694,8 +616,6 @@ class _BN(Function):
         ctx.bitmask = ymask is not None
         ctx.slot = slot
         ctx.bws = ws.bwd if ws is not None else None
-        if slot is not None and consumer_masks and x.is_cuda and training:
-            slot.src = (x, mean, rstd, ctx.bws)
         ctx.save_for_backward(x, (ymask if ymask is not None else y) if bwd_relu else None, mean, rstd)
         return y
 
@@ -708,18 +628,7 @@ class _BN(Function):
         add = None
         if ctx.slot is not None:
             add, ctx.slot.stash = ctx.slot.stash, None
-        part = None
-        if ctx.slot is not None:
-            part, ctx.slot.bwd_part = ctx.slot.bwd_part, None
-        if (dy.is_cuda and part is not None and part[1].data_ptr() == dy.data_ptr() and not ctx.relu
-                and not ctx.has_res and add is None):
-            # the consumer conv's dgrad epilogue already accumulated sum(d) and
-            # sum(d * xhat) per channel: apply only
-            dx = torch.empty_like(x)
-            _T().bn_backward(dy, None, x, mean, rstd, g.master, dx, None, g.grad, b.grad, False, None,
-                             part[0], True)
-            dres = None
-        elif dy.is_cuda:
+        if dy.is_cuda:
             dx = torch.empty_like(x)
             dres = torch.empty_like(x) if ctx.has_res and (ctx.relu or add is not None) else None
             if ctx.bitmask:
@@ -814,18 +723,10 @@ def batchnorm(x: torch.Tensor, g: Param, b: Param, run_mean: Optional[torch.Tens
 
 
 # ============================================================ LayerNorm
-# 1-GPU jobs: the LN weight-gradient column reduce CAN run on this side
-# stream (installed by the trainer, joined before the optimizer), beside the
-# next input-gradient GEMM. Off: measured much slower in hipGraph replay
-# (Transformer 5.49-5.57 vs 5.18 ms, same box: 32 fork / join pairs per
-# step); TAM_LN_AUX=1 for A/B
-_AUX_STREAM = None
-LN_AUX = os.environ.get("TAM_LN_AUX", "0") != "0"
-
-
-def set_aux_stream(stream) -> None:
-    global _AUX_STREAM
-    _AUX_STREAM = stream
+# (a side-stream column reduce of the LN weight gradients beside the next
+# input-gradient GEMM measured much slower in hipGraph replay -- Transformer
+# 5.49-5.57 vs 5.18 ms, 32 fork / join pairs per step -- and was removed in
+# round 6; the reduces are batched into the backward's flush instead)
 
 
 # while weight gradients are deferred (trainer group_wgrad), a LayerNorm's
@@ -834,31 +735,23 @@ def set_aux_stream(stream) -> None:
 # launches per step -> 1); TAM_LN_DEFER=0 for A/B
 LN_DEFER = os.environ.get("TAM_LN_DEFER", "1") != "0"
 _DEFER_LNRED: list = []
-# ...and a slab-split conv weight gradient's slab reduce likewise (ResNet-50:
-# 24 reduce launches per step -> 1). Measured neutral in graph replay
-# (ResNet-50 8.92-8.94 vs 8.91-8.93 ms, VGG-16 6.67-6.68 vs 6.62-6.67, same
-# box) while it holds every slab conv's gradient back to the flush, which
-# delays the DDP buckets: off by default, TAM_SLAB_DEFER=1 to enable
-SLAB_DEFER = os.environ.get("TAM_SLAB_DEFER", "0") != "0"
-_DEFER_SLABS: list = []
+# (deferring slab-split conv weight-gradient reduces into the same flush
+# measured neutral in graph replay and held the DDP buckets back; removed in
+# round 6)
 
 
 def _ln_backward(dy, x, g: Param, b: Param, mean, rstd, dx, addend=None) -> bool:
     """LN backward; returns True when dgamma / dbeta were deferred to the
     flush (their grad_ready() then comes from flush_wgrad)."""
     deferred = _DEFER_WGRAD is not None and LN_DEFER
-    if not deferred and (_AUX_STREAM is None or not LN_AUX):
+    if not deferred:
         _T().ln_backward(dy, x, g.master, mean, rstd, dx, g.grad, b.grad, addend)
         return False
     D = x.shape[-1]
     ws = torch.empty(_LN_MAX_BLOCKS * 2 * D, dtype=torch.float32, device=x.device)
     nblk = _T().ln_backward_split(dy, x, g.master, mean, rstd, dx, ws, addend)
-    if deferred:
-        _DEFER_LNRED.append((ws, nblk, g, b))
-        return True
-    with _OnWgrad(ws, stream=_AUX_STREAM):
-        _T().col_reduce_acc(ws, nblk, 2 * D, g.grad, b.grad, D)
-    return False
+    _DEFER_LNRED.append((ws, nblk, g, b))
+    return True
 
 
 _LN_MAX_BLOCKS = 512        # csrc/include/tam/kernels.h LN_MAX_BLOCKS

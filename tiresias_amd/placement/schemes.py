@@ -144,6 +144,10 @@ class Placement:
         # with the advisor: may a gang that fits one node be fragmented?
         # (spread_rule "wait": yes, when the rule says so; "node": never)
         self.spread_node_gangs = True
+        # TiresiasPlacement: decisions per sensitivity verdict, and "flips":
+        # placements the other verdict would have planned differently
+        self.oracle_stats = {"sensitive": 0, "insensitive": 0, "flips": 0, "flips_sensitive": 0,
+                             "flips_insensitive": 0}
 
     def plan(self, cluster: Cluster, job: Job) -> Optional[Plan]:
         raise NotImplementedError
@@ -395,21 +399,42 @@ class TiresiasPlacement(Placement):
         sensitive = bool(self.sensitivity and self.sensitivity(job))
         min_nodes = max(1, math.ceil(job.num_gpu / gpn))
         if sensitive:
-            # consolidated: best-fit single node, or exactly min_nodes fullest-free nodes
-            if job.num_gpu <= gpn:
-                order = sorted(cluster.nodes, key=lambda nid: (cluster.nodes[nid].num_free_gpus(), int(nid)))
-                return _single_node(cluster, job, order)
-            whole = [nid for nid, n in cluster.nodes.items() if n.num_free_gpus() == n.gpu_count]
-            if len(whole) * gpn >= job.num_gpu:
-                # prefer whole nodes within one rack
-                by_rack: Dict[str, List[str]] = {}
-                for nid in whole:
-                    by_rack.setdefault(cluster.nodes[nid].rack_id, []).append(nid)
-                for rid, nodes in sorted(by_rack.items(), key=lambda kv: -len(kv[1])):
-                    if len(nodes) * gpn >= job.num_gpu:
-                        return _fill(cluster, job, nodes)
-                return _fill(cluster, job, whole)
-            return None
+            p = self._consolidated(cluster, job, gpn)
+        else:
+            p = self._insensitive(cluster, job, gpn, min_nodes, count=True)
+        if self.sensitivity is not None:
+            # the skew oracle's effect, counted: would the OTHER verdict have
+            # placed this job differently right now (another node set, or
+            # start vs wait)? Plans are side-effect free; the counterfactual
+            # does not touch the advisor's decision counts
+            alt = (self._insensitive(cluster, job, gpn, min_nodes, count=False) if sensitive
+                   else self._consolidated(cluster, job, gpn))
+            st = self.oracle_stats
+            st["sensitive" if sensitive else "insensitive"] += 1
+            if _plan_key(alt) != _plan_key(p):
+                st["flips"] += 1
+                st["flips_" + ("sensitive" if sensitive else "insensitive")] += 1
+        return p
+
+    def _consolidated(self, cluster, job, gpn):
+        """A placement-sensitive job: best-fit single node, or exactly
+        min_nodes whole nodes (one rack first), else wait."""
+        if job.num_gpu <= gpn:
+            order = sorted(cluster.nodes, key=lambda nid: (cluster.nodes[nid].num_free_gpus(), int(nid)))
+            return _single_node(cluster, job, order)
+        whole = [nid for nid, n in cluster.nodes.items() if n.num_free_gpus() == n.gpu_count]
+        if len(whole) * gpn >= job.num_gpu:
+            # prefer whole nodes within one rack
+            by_rack: Dict[str, List[str]] = {}
+            for nid in whole:
+                by_rack.setdefault(cluster.nodes[nid].rack_id, []).append(nid)
+            for rid, nodes in sorted(by_rack.items(), key=lambda kv: -len(kv[1])):
+                if len(nodes) * gpn >= job.num_gpu:
+                    return _fill(cluster, job, nodes)
+            return _fill(cluster, job, whole)
+        return None
+
+    def _insensitive(self, cluster, job, gpn, min_nodes, count: bool):
         # insensitive: fill fragments first (fewest free GPUs first), keep whole nodes
         order = sorted(cluster.nodes, key=lambda nid: (cluster.nodes[nid].num_free_gpus() == 0,
                                                       cluster.nodes[nid].num_free_gpus(), int(nid)))
@@ -438,9 +463,14 @@ class TiresiasPlacement(Placement):
         if p is None:
             return None
         k = len({nid for nid, _ in p})
-        if k <= min_nodes or self.advisor.should_spread(cluster, job, self.jobs_by_id or {}, k, gpn, min_nodes):
+        if k <= min_nodes or self.advisor.should_spread(cluster, job, self.jobs_by_id or {}, k, gpn, min_nodes,
+                                                        count=count):
             return p
         return None
+
+
+def _plan_key(p):
+    return None if p is None else tuple(sorted((nid, tuple(sorted(d))) for nid, d in p))
 
 
 def _next_pow2(n: int) -> int:

@@ -35,11 +35,11 @@ import torch.distributed as dist
 
 from ..parallel.gang import DEFAULT_NIC_GBPS, create_gang_comm, vnode_parts
 from .skew import model_profile
+from .step_times import MI355X_STEP_S
 
-# single-GPU hipGraph step seconds on MI355X (profiles/model_bench_r1_v8.json);
-# the denominator of the iteration-level slowdown
-ITER_S = {"resnet50": 0.0112, "vgg16": 0.0076, "transformer": 0.0068, "gnmt": 0.0153,
-          "resnet_tiny": 0.004, "vgg_tiny": 0.002, "transformer_tiny": 0.006, "gnmt_tiny": 0.01}
+# single-GPU hipGraph step seconds on MI355X, this round's kernels
+# (profiler/step_times.py); the denominator of the iteration-level slowdown
+ITER_S = dict(MI355X_STEP_S)
 
 
 def ring_busbw(bytes_: float, seconds: float, n: int) -> float:
