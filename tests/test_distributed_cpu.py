@@ -673,3 +673,55 @@ def test_gang_fill_votes_match_when_one_member_cannot_step():
     solo = worker(0, SimpleNamespace(ddp=None, group=None, broken=False, _spilled=None, step=None), (0,))
     solo.fill_begin(plan, bad_rep)
     assert solo._fill is None
+
+
+def _fill_gang_worker(rank, world, port, q):
+    _init(rank, world, port)
+    import time as _t
+
+    from tiresias_amd.executor.cluster_runtime import Worker
+    from tiresias_amd.executor.trainer import Trainer
+
+    t = Trainer("resnet_tiny", "cpu", seed=3, data_seed=40 + rank, group=dist.group.WORLD, bucket_mb=0.05)
+    w = Worker.__new__(Worker)
+    w.fill_enabled, w.rank, w.device = True, rank, torch.device("cpu")
+    w.trainers = {"g": t}
+    w._job_ranks = {"g": tuple(range(world))}
+    w.fill_s_total, w.fill_steps_total = 0.0, 0
+    w._fill_cap = {}
+    w._carry = []
+    counts = []
+    for left, stop_after in ((50, (2, 5)), (3, (50, 50)), (50, (0, 4))):
+        # the members see "the next plan is out" after different numbers of
+        # local steps (stop_after[rank]); the votes must still give every
+        # member the same fill step count, never more than ``left``
+        w.fill_begin({"assign": {rank: [("g", 0)]}, "left": {"g": left}}, {"jobs": []})
+        n = 0
+        while w.fill_step(ready=n >= stop_after[rank]):
+            n += 1
+            _t.sleep(0.001 * (rank + 1))
+        counts.append((w.fill_counts().get("g", 0), n))
+        w.fill_end({})
+        w._carry = []
+    wts = [torch.zeros_like(t.arena.master) for _ in range(world)]
+    dist.all_gather(wts, t.arena.master)
+    q.put((rank, counts, all(torch.equal(wts[0], x) for x in wts)))
+    dist.destroy_process_group()
+
+
+def test_gang_fill_steps_equal_on_every_member():
+    """fill mode of a 2-rank gang over gloo with the
+    round-6 vote (no per-step host drain on the GPU path; bounded waits):
+    members whose "next plan is ready" moment differs still run the SAME
+    number of fill steps (their gradient all-reduces match), bounded by the
+    plan's iterations left, and the replicas stay identical."""
+    world = 2
+    port = _free_port()
+    q = mp.get_context("spawn").SimpleQueue()
+    mp.spawn(_fill_gang_worker, args=(world, port, q), nprocs=world, join=True)
+    res = sorted(q.get() for _ in range(world))
+    (_, c0, same0), (_, c1, same1) = res
+    assert same0 and same1
+    assert c0 == c1, (c0, c1)
+    assert c0[1][0] == 3                      # bounded by left (nobody ready)
+    assert c0[0][0] == 2 and c0[2][0] == 0    # the first member ready stops the gang at its next vote

@@ -381,6 +381,12 @@ def test_two_persistent_jobs_sharing_a_gpu_run_per_step(gpu):
         assert r["loss"] == r["loss"]                                   # finite
     assert not w.trainers["1"].uses_persist and not w.trainers["2"].uses_persist
     assert G.device_timeouts(reset=False) == 0
+    # alone again: back on the persistent grids (the switch is per round,
+    # not for good -- only a barrier timeout turns them off for good)
+    rep = w.run({"actions": [], "assign": {0: [("1", 2)]}, "deadline": None})
+    assert rep["jobs"][0]["iters"] == 2 and "error" not in rep["jobs"][0], rep
+    assert w.trainers["1"].uses_persist
+    assert G.device_timeouts(reset=False) == 0
     w.clear(keep_pool=False)
 
 

@@ -61,6 +61,15 @@ NOMINAL_ITER_S = {"resnet50": 0.0113, "vgg16": 0.0080, "transformer": 0.0072, "g
 VOTE_TIMEOUT_S = float(os.environ.get("TAM_VOTE_TIMEOUT_S", "10"))
 
 
+def _store_del(plane, key: str) -> None:
+    """Best-effort delete of a control-store key (bookkeeping only: a failed
+    delete leaves a stale key, never a wrong result)."""
+    try:
+        plane._retry(lambda: plane.store.delete_key(key), "store delete")
+    except Exception:
+        pass
+
+
 def gang_ranks(alloc: Dict[str, List[int]], gpn: int) -> Tuple[int, ...]:
     """(virtual) node id + device -> global GPU rank."""
     out = []
@@ -724,7 +733,12 @@ class Controller:
         # round at the first step boundary after it (Worker._run_until)
         deadline = self.t0 + nxt if math.isfinite(nxt) else None
         seen, self.plan_fill = self.plan_fill, {}
+        # jobs of this round whose model runs persistent-grid recurrences (GNMT):
+        # the one-GPU rehearsal's workers keep two of them off the grids at once
+        persist_jobs = sorted({jid for lst in assign.values() for jid, _ in lst
+                               if "gnmt" in (self.rjobs[jid].model or "")})
         plan = {"round": self.round, "actions": actions, "assign": assign, "left": left, "fill_seen": seen,
+                "persist_jobs": persist_jobs,
                 "stop": stop, "wait": wait,
                 "deadline": deadline, "alive": [r for r in range(self.world) if r not in self.dead],
                 "ckpt": getattr(self.cfg, "ckpt_policy", "none")}
@@ -1380,6 +1394,13 @@ class Worker:
                     rt(lambda: plane.store.set(f"{pre}/{jid}/ack/{self.rank}", b"1"), "ipc ack")
                 for peer in sorted({p for _, p, _ in sends}):
                     wait_key(f"{pre}/{jid}/ack/{peer}", peer, f"ipc ack of {jid}")
+                # the acks say every receiver read (and copied) its handles:
+                # the donor, their only other reader, removes them and the
+                # acks, so the store does not grow over a long replay
+                for buf, peer, name in sends:
+                    _store_del(plane, f"{pre}/{jid}/{self.rank}-{peer}/{name}")
+                for peer in sorted({p for _, p, _ in sends}):
+                    _store_del(plane, f"{pre}/{jid}/ack/{peer}")
                 ok[jid] = True
             except Exception as e:
                 print(f"[worker {self.rank}] ipc move of job {jid} failed ({type(e).__name__}: {e})",
@@ -1531,6 +1552,10 @@ class Worker:
             jid, n = jobs[0]
             t = self.trainers[jid]
             deadline = plan.get("deadline")
+            if cuda and getattr(t.model, "persist", False):
+                # alone in this worker: persistent grids unless another rank
+                # of the one-GPU rehearsal runs one this round
+                t.set_persist_shared(self._persist_elsewhere(plan, jid))
             if deadline is None or t.ddp is not None:
                 # gang members must run the same step count (collectives)
                 done = 0
@@ -1552,10 +1577,9 @@ class Worker:
                 # each would spin at its grid barrier waiting for workgroups the
                 # other holds the CUs of. A job that shares its GPU with another
                 # persistent-grid job takes the per-step recurrence from here on
-                pers = [jid for jid, _ in jobs if self.trainers[jid].uses_persist]
-                if len(pers) > 1:
-                    for jid in pers:
-                        self.trainers[jid].disable_persist()
+                pers = [jid for jid, _ in jobs if getattr(self.trainers[jid].model, "persist", False)]
+                for jid in pers:
+                    self.trainers[jid].set_persist_shared(len(pers) > 1 or self._persist_elsewhere(plan, jid))
             streams = [self._stream(jid) if cuda else None for jid, _ in jobs]
             if cuda:
                 # apply() ran on the default stream: fresh jobs' weight init
@@ -1643,6 +1667,16 @@ class Worker:
         got = self.snap.poll()
         self.snap_reported.update(jid for jid, _, _ in got)
         return got
+
+    def _persist_elsewhere(self, plan: dict, jid: str) -> bool:
+        """In the one-GPU multi-rank rehearsal (TAM_SHARED_GPU=1) every rank
+        drives the same device: another rank's persistent-grid job this round
+        (plan["persist_jobs"], from the controller) shares the GPU with ``jid``
+        (the in-worker check cannot see other ranks)."""
+        if os.environ.get("TAM_SHARED_GPU") != "1" or self.world <= 1:
+            return False
+        others = set(plan.get("persist_jobs") or []) - {jid}
+        return bool(others)
 
     # ------------------------------------------------------------ fill mode
     def fill_begin(self, plan: dict, rep: dict) -> None:

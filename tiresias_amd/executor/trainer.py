@@ -143,6 +143,11 @@ class Trainer:
         self.step_count += 1
         sharded = self.ddp is not None and self.ddp.shard
         if sharded:
+            # a shadow all-gather of the previous step still in flight (a
+            # bucket whose params the forward never read through Param.w)
+            # would overwrite this member's slice after the optimizer below
+            # writes it: join them all first (free when already joined)
+            self.ddp.join_gather()
             # this member's slices (+ replicated tails), split at the
             # decay / no-decay boundary; the gradient is reset as a whole below
             regions = []
@@ -215,8 +220,25 @@ class Trainer:
 
     @property
     def uses_persist(self) -> bool:
-        """The model runs the persistent-grid LSTM kernels (GNMT)."""
-        return self.device.type == "cuda" and bool(getattr(self.model, "persist", False))
+        """The model runs the persistent-grid LSTM kernels (GNMT) -- unless
+        they are off for good (a barrier timeout) or for now (its GPU is
+        shared with another persistent-grid job, ``set_persist_shared``)."""
+        return (self.device.type == "cuda" and bool(getattr(self.model, "persist", False))
+                and not getattr(self, "_persist_shared", False))
+
+    def set_persist_shared(self, shared: bool) -> None:
+        """While another job's persistent LSTM grids may run on the same GPU
+        (GPU sharing in one worker, or another rank of the one-GPU rehearsal),
+        take the per-step recurrence: two different persistent kernels cannot
+        be guaranteed co-resident. Back to the persistent grids once the job
+        runs alone (a change re-captures the step graph)."""
+        shared = bool(shared)
+        if shared != getattr(self, "_persist_shared", False):
+            self._persist_shared = shared
+            if hasattr(self.model, "shared"):
+                self.model.shared = shared
+            self._graph = None
+            self._g_loss = None
 
     def persist_skipped(self, reset: bool = True) -> int:
         """Steps of THIS job whose persistent recurrence timed out since the

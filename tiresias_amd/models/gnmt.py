@@ -106,7 +106,7 @@ class _LSTMLayer(Function):
         # m: the owning model (GNMT) -- its persist flag, its own timeout
         # word (err) and its co-residency rule (residency) go with every
         # persistent launch; None: persistent with the process defaults
-        persist = m.persist if m is not None else True
+        persist = (m.persist and not m.shared) if m is not None else True
         T, B, I = x.shape
         Hd = w_hh.shape[1]
         dev = x.device
@@ -164,7 +164,7 @@ class _LSTMLayer(Function):
     def backward(ctx, dH):
         x, Hs, Cs, act = ctx.saved_tensors
         w_ih, w_hh, b, reverse, m = ctx.p
-        persist = m.persist if m is not None else True
+        persist = (m.persist and not m.shared) if m is not None else True
         T, B, I = x.shape
         Hd = Hs.shape[2]
         dev = x.device
@@ -306,6 +306,9 @@ class GNMT:
     # whole-sequence persistent recurrences; off for the rest of the job
     # after a barrier timeout (Worker.run reads the job's own err words)
     persist = True
+    # ...and off while another job's persistent grids may share the GPU
+    # (Trainer.set_persist_shared)
+    shared = False
 
     def __init__(self, arena: Arena, vocab: int = 32000, hidden: int = 1024, enc_layers: int = 4,
                  dec_layers: int = 4, heads: int = 16):
@@ -340,7 +343,7 @@ class GNMT:
 
     def forward(self, batch):
         src, tgt_in = batch["src"], batch["tgt_in"]       # [B,S] token ids
-        if src.is_cuda and PERSIST and self.persist:
+        if src.is_cuda and PERSIST and self.persist and not self.shared:
             # the sync words of every persistent launch of this step (forward
             # and backward of each layer-direction) zeroed by one fill instead
             # of one zeroing kernel per launch
