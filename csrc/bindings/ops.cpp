@@ -124,6 +124,7 @@ void run_p8(const Tensor& a, bool ak, const Tensor& b, bool bk, int64_t M, int64
   if (sp == 0) sp = -1;
   const bool explicit_cfg = tile > 0;
   if (tile < 0) tile = tam::gemm8p_tile((int)M, (int)N, (int)K);
+  if (!tam::gemm8p_tile_ok(tile, ak)) tile = 128;
   if (sp < 0) sp = tam::gemm8p_slab_splits((int)M, (int)N, (int)K, tile);
   if (sp > 1 && ep.ldc >= N) {
     Tensor ws = at::empty({sp, M, N}, a.options().dtype(at::kFloat));
@@ -350,6 +351,17 @@ void gemm_dispatch(const Tensor& a, bool a_kmajor, const Tensor& b, bool b_kmajo
           if (best_sp && best_sp != sp && best_sp != 2 * sp) cands.push_back({tl, best_sp});
         }
       }
+      // 64x128 (K-major A): the N = 512 projections (4096 x 512 = 256 tiles,
+      // one per CU) that neither square tile fills
+      // (a single-barrier schedule of the 64x128 / 128^2 tiles -- all
+      // fragments of K-tile t+1 read under the MFMAs of t, four LDS stages --
+      // measured no faster on these shapes and was removed: profiles/r6/
+      // gemm_small_tiles.md)
+      if (a_kmajor && (M + 63) / 64 * ((N + 127) / 128) >= 128) {
+        const int s = tam::gemm8p_slab_splits((int)M, (int)N, (int)K, 64);
+        cands.push_back({64, 1});
+        if (s > 1) cands.push_back({64, s});
+      }
       if (tam::gemm8p_sk_ok(a_kmajor, b_kmajor, (int)M, (int)N, (int)K, a.stride(0), b.stride(0)))
         cands.push_back({256, 0});   // stream-K
     }
@@ -449,7 +461,9 @@ int64_t gemm_routes_load_op(const std::string& text) {
     if (g_route.count(key)) continue;
     int tile = -1, sp = -1;
     const bool has_cfg = (bool)(ls >> tile >> sp);
-    const bool cfg_ok = has_cfg && (tile == 128 || tile == 256) && sp >= (tile == 256 ? 0 : 1) && sp <= 16;
+    const bool cfg_ok = has_cfg &&
+                        (tile == 128 || tile == 256 || (tile == 64 && lay[0] == 'K')) &&
+                        sp >= (tile == 256 ? 0 : 1) && sp <= 16;
     if (route == 3 && !cfg_ok) continue;                // a p8 route needs its measured config
     g_route[key] = route;
     g_route_ms[key] = t;
@@ -914,32 +928,47 @@ void avgpool_backward_op(const Tensor& dy, const Tensor& dx) {
 // ------------------------------------------------------------------ loss / embed / misc
 void softmax_xent_op(const Tensor& logits, const Tensor& labels, const optional<Tensor>& dlogits,
                      const Tensor& loss_rows, double smoothing, double grad_scale,
-                     int64_t ignore_index) {
+                     int64_t ignore_index, int64_t tm_b) {
   check_bf16(logits, "logits"); check_contig(logits, "logits");
-  TORCH_CHECK(labels.scalar_type() == at::kLong && labels.is_cuda(), "tam.xent: labels int64 GPU");
+  TORCH_CHECK(labels.scalar_type() == at::kLong && labels.is_cuda() && labels.is_contiguous(),
+              "tam.xent: labels contiguous int64 GPU");
   check_f32(loss_rows, "loss_rows");
   const int64_t V = logits.size(-1), rows = logits.numel() / V;
   TORCH_CHECK(labels.numel() == rows && loss_rows.numel() == rows, "tam.xent: row count");
+  TORCH_CHECK(tm_b <= 0 || rows % tm_b == 0, "tam.xent: tm_b must divide the rows");
   tam::softmax_xent(bp(logits), labels.data_ptr<int64_t>(), opt_ptr<tam::bf16_t>(dlogits),
                     loss_rows.data_ptr<float>(), rows, (int)V, (float)smoothing, (float)grad_scale,
-                    ignore_index, cur_stream(logits));
+                    ignore_index, cur_stream(logits), tm_b);
 }
 
-void embedding_forward_op(const Tensor& table, const Tensor& ids, const Tensor& out, double scale) {
+void embedding_forward_op(const Tensor& table, const Tensor& ids, const Tensor& out, double scale, int64_t tm_b,
+                          const optional<Tensor>& pos) {
   check_bf16(table, "table"); check_bf16(out, "out"); check_contig(table, "table");
   TORCH_CHECK(ids.scalar_type() == at::kLong && ids.is_contiguous(), "tam.embedding: ids");
   const int64_t D = table.size(1);
   TORCH_CHECK(D % 8 == 0, "tam.embedding: D % 8");
   TORCH_CHECK(out.numel() == ids.numel() * D, "tam.embedding: out size");
+  TORCH_CHECK(tm_b <= 0 || ids.numel() % tm_b == 0, "tam.embedding: tm_b must divide the ids");
+  const tam::bf16_t* pp = nullptr;
+  int64_t prow = 0;
+  if (pos.has_value() && pos->defined()) {
+    check_bf16(*pos, "pos"); check_contig(*pos, "pos");
+    TORCH_CHECK(pos->dim() == 2 && pos->size(1) == D, "tam.embedding: pos must be [S][D]");
+    prow = pos->size(0);
+    TORCH_CHECK(prow > 0 && (tm_b > 0 ? ids.numel() / tm_b == prow : ids.numel() % prow == 0),
+                "tam.embedding: pos rows must equal the sequence length");
+    pp = bp(*pos);
+  }
   tam::embedding_forward(bp(table), ids.data_ptr<int64_t>(), bpm(out), ids.numel(), (int)D,
-                         (float)scale, cur_stream(table), table.size(0));
+                         (float)scale, cur_stream(table), table.size(0), tm_b, pp, prow);
 }
-void embedding_backward_op(const Tensor& dout, const Tensor& ids, const Tensor& gtable, double scale) {
+void embedding_backward_op(const Tensor& dout, const Tensor& ids, const Tensor& gtable, double scale, int64_t tm_b) {
   check_bf16(dout, "dout"); check_f32(gtable, "gtable"); check_contig(dout, "dout");
   TORCH_CHECK(ids.scalar_type() == at::kLong && ids.is_contiguous() && gtable.dim() == 2 &&
                   dout.numel() == ids.numel() * gtable.size(1), "tam.embedding_backward: shapes");
+  TORCH_CHECK(tm_b <= 0 || ids.numel() % tm_b == 0, "tam.embedding_backward: tm_b must divide the ids");
   tam::embedding_backward(bp(dout), ids.data_ptr<int64_t>(), gtable.data_ptr<float>(), ids.numel(),
-                          (int)gtable.size(1), (float)scale, cur_stream(dout), gtable.size(0));
+                          (int)gtable.size(1), (float)scale, cur_stream(dout), gtable.size(0), tm_b);
 }
 
 void conv_dma_policy_op(int64_t p) { tam::conv_dma_policy((int)p); }
@@ -1011,6 +1040,50 @@ void colsum_op(const Tensor& x, const Tensor& out) {
 void relu_backward_op(const Tensor& dy, const Tensor& y, const Tensor& dx) {
   check_bf16(dy, "dy"); check_bf16(y, "y"); check_bf16(dx, "dx");
   tam::relu_backward(bp(dy), bp(y), bpm(dx), dy.numel(), cur_stream(dy));
+}
+void sum_scale_op(const Tensor& x, const Tensor& out, double scale) {
+  check_f32(x, "x"); check_f32(out, "out"); check_contig(x, "x");
+  TORCH_CHECK(out.numel() >= 1, "tam.sum_scale: out");
+  tam::sum_scale(x.data_ptr<float>(), x.numel(), out.data_ptr<float>(), (float)scale, cur_stream(x));
+}
+// a 2-D row view of a bf16 [..., C] tensor whose leading dims collapse to
+// rows at one pitch (a last-dim slice of a contiguous tensor qualifies)
+static std::pair<int64_t, int64_t> row_view(const Tensor& t, const char* what) {
+  TORCH_CHECK(t.is_cuda() && t.scalar_type() == at::kBFloat16 && t.dim() >= 1 && t.stride(-1) == 1,
+              "tam.rows_sum: ", what, " must be a bf16 CUDA tensor with unit last stride");
+  const int64_t C = t.size(-1);
+  int64_t ld = t.dim() >= 2 ? t.stride(-2) : C;
+  for (int64_t d = t.dim() - 2; d >= 1; --d)
+    TORCH_CHECK(t.size(d) == 1 || t.size(d - 1) == 1 || t.stride(d - 1) == t.stride(d) * t.size(d),
+                "tam.rows_sum: ", what, " leading dims do not collapse to one row pitch");
+  TORCH_CHECK(C % 8 == 0 && ld % 8 == 0 && (((uintptr_t)t.data_ptr()) & 15) == 0,
+              "tam.rows_sum: ", what, " needs C % 8 == 0 and 16-B aligned rows");
+  return {C, ld};
+}
+// outs[j] = sum of the next n_in[j] tensors of ins (row-pitched views, one row count)
+void rows_sum_op(at::TensorList outs, at::TensorList ins, at::IntArrayRef n_in) {
+  TORCH_CHECK(!outs.empty() && outs.size() <= 4 && outs.size() == n_in.size(), "tam.rows_sum: 1-4 jobs");
+  const int64_t R = outs[0].numel() / outs[0].size(-1);
+  tam::RowJobs jb{};
+  size_t q = 0;
+  for (size_t j = 0; j < outs.size(); ++j) {
+    auto [C, ld] = row_view(outs[j], "out");
+    TORCH_CHECK(outs[j].numel() / C == R, "tam.rows_sum: every job needs the same row count");
+    TORCH_CHECK(n_in[j] >= 1 && n_in[j] <= 4 && q + n_in[j] <= ins.size(), "tam.rows_sum: n_in");
+    tam::RowJob& r = jb.job[j];
+    r.out = bpm(outs[j]); r.ld_out = ld; r.C = (int)C; r.n_in = (int)n_in[j];
+    for (int k = 0; k < r.n_in; ++k, ++q) {
+      auto [Ci, ldi] = row_view(ins[q], "in");
+      TORCH_CHECK(Ci == C && ins[q].numel() / Ci == R, "tam.rows_sum: input shape");
+      r.in[k] = bp(ins[q]); r.ld_in[k] = ldi;
+    }
+  }
+  TORCH_CHECK(q == ins.size(), "tam.rows_sum: unused inputs");
+  tam::rows_sum(jb, (int)outs.size(), R, cur_stream(outs[0]));
+}
+void zero_op(const Tensor& t) {
+  TORCH_CHECK(t.is_cuda() && t.is_contiguous(), "tam.zero_: contiguous CUDA tensor");
+  tam::zero_async(t.data_ptr(), t.numel() * t.element_size(), cur_stream(t));
 }
 void add_op(const Tensor& a, const Tensor& b, const Tensor& y) {
   check_bf16(a, "a"); check_bf16(b, "b"); check_bf16(y, "y");
@@ -1252,9 +1325,12 @@ TORCH_LIBRARY(tam, m) {
   m.def("maxpool_k3s2_policy(int policy) -> ()", &maxpool_k3s2_policy_op);
   m.def("avgpool_forward(Tensor x, Tensor(a!) y) -> ()", &avgpool_forward_op);
   m.def("avgpool_backward(Tensor dy, Tensor(a!) dx) -> ()", &avgpool_backward_op);
-  m.def("softmax_xent(Tensor logits, Tensor labels, Tensor(a!)? dlogits, Tensor(b!) loss_rows, float smoothing, float grad_scale, int ignore_index) -> ()", &softmax_xent_op);
-  m.def("embedding_forward(Tensor table, Tensor ids, Tensor(a!) out, float scale) -> ()", &embedding_forward_op);
-  m.def("embedding_backward(Tensor dout, Tensor ids, Tensor(a!) gtable, float scale) -> ()", &embedding_backward_op);
+  m.def("softmax_xent(Tensor logits, Tensor labels, Tensor(a!)? dlogits, Tensor(b!) loss_rows, float smoothing, float grad_scale, int ignore_index, int tm_b=0) -> ()", &softmax_xent_op);
+  m.def("embedding_forward(Tensor table, Tensor ids, Tensor(a!) out, float scale, int tm_b=0, Tensor? pos=None) -> ()", &embedding_forward_op);
+  m.def("embedding_backward(Tensor dout, Tensor ids, Tensor(a!) gtable, float scale, int tm_b=0) -> ()", &embedding_backward_op);
+  m.def("sum_scale(Tensor x, Tensor(a!) out, float scale) -> ()", &sum_scale_op);
+  m.def("rows_sum(Tensor[] outs, Tensor[] ins, int[] n_in) -> ()", &rows_sum_op);
+  m.def("zero_(Tensor(a!) t) -> ()", &zero_op);
   m.def("colsum(Tensor x, Tensor(a!) out) -> ()", &colsum_op);
   m.def("gemm_force(int cfg, int splits) -> ()", &gemm_force_op);
   m.def("gemm8p_policy(int mode, int tile) -> ()", &gemm8p_policy_op);

@@ -1,7 +1,9 @@
-// tiresias_amd — LDS-DMA MFMA GEMM for every operand majority, two tile
-// shapes: 256x256 (8 waves, big GEMMs) and 128x128 (4 waves, two blocks per
+// tiresias_amd — LDS-DMA MFMA GEMM for every operand majority, three tile
+// shapes: 256x256 (8 waves, big GEMMs), 128x128 (4 waves, two blocks per
 // CU, the mid-size GEMMs of the zoo: FFN / LSTM-gate projections and their
-// gradients). C[M][N] (+)= A . B, bf16 in, fp32 accumulate.
+// gradients) and 64x128 (4 waves of 32x64, K-major A: the N = 512
+// projections, 256 tiles = one per CU). C[M][N] (+)= A . B, bf16 in, fp32
+// accumulate.
 //
 //   A: K-major [M][K] (AK) or M-major [K][M];  B: K-major [N][K] (BK) or N-major [K][N]
 //
@@ -67,8 +69,29 @@ struct P8Geo {
   static constexpr int AHALF = AROWS * P8_BK * 2, BHALF = BCOLS * P8_BK * 2;
   static constexpr int STAGE = 2 * AHALF + 2 * BHALF;      // AL AH BL BH
   static constexpr int LDS = 2 * STAGE;
-  static_assert(AHALF == THREADS * 32 && BHALF == THREADS * 32, "2 DMA per thread per half");
+  // LDS-DMA instructions per thread per half-tile (16 B each): 2 for the
+  // square tiles, 1 / 2 for the 64x128 tile's A / B halves
+  static constexpr int DA = AHALF / (THREADS * 16), DB = BHALF / (THREADS * 16);
+  static_assert(DA >= 1 && DB >= 1 && AHALF == THREADS * 16 * DA && BHALF == THREADS * 16 * DB,
+                "whole DMA instructions per half");
+  // DMAs left in flight by the per-K-tile counted wait: tile t+2's AL, BL, BH
+  static constexpr int INFLIGHT = DA + 2 * DB;
 };
+
+// s_waitcnt vmcnt(N) with N a compile-time constant (inline asm needs a literal)
+template <int N>
+__device__ __forceinline__ void p8_vmcnt() {
+  static_assert(N >= 0 && N <= 8, "p8_vmcnt: 0..8");
+  if constexpr (N == 0) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  else if constexpr (N == 1) asm volatile("s_waitcnt vmcnt(1)" ::: "memory");
+  else if constexpr (N == 2) asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
+  else if constexpr (N == 3) asm volatile("s_waitcnt vmcnt(3)" ::: "memory");
+  else if constexpr (N == 4) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+  else if constexpr (N == 5) asm volatile("s_waitcnt vmcnt(5)" ::: "memory");
+  else if constexpr (N == 6) asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
+  else if constexpr (N == 7) asm volatile("s_waitcnt vmcnt(7)" ::: "memory");
+  else asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+}
 
 // local row lr of a half-tile -> row / column offset in the block tile
 //   A half h: rows wm*WTM + h*QM + (lr % QM), wm = lr / QM
@@ -78,13 +101,13 @@ __device__ __forceinline__ int p8_row(int lr, int h) {
   return (lr / Q) * (2 * Q) + h * Q + (lr % Q);
 }
 
-// Issue one half-tile (2 DMA instructions per thread). EXT = rows of the
+// Issue one half-tile (D DMA instructions per thread). EXT = rows of the
 // half-tile (K-major image) or its columns (MN-major image).
-template <int Q, int EXT, int NW, bool KMAJ>
+template <int Q, int EXT, int NW, bool KMAJ, int D = 2>
 __device__ __forceinline__ void p8_issue(const bf16_t* __restrict__ base, long ld, int extent, int o0,
                                          int k0, char* half, int h, int wid, int lane) {
 #pragma unroll
-  for (int j = 0; j < 2; ++j) {
+  for (int j = 0; j < D; ++j) {
     const int g = j * NW + wid;                // 1-KiB group of the half-tile
     if constexpr (KMAJ) {
       // 8 rows x 128 B per group; lane -> row 8g + lane/8, 16-B slot lane%8
@@ -145,124 +168,14 @@ __device__ __forceinline__ void p8_mfma(f32x4_t (&acc)[TI][TJ], const s16x8_t (&
   __builtin_amdgcn_sched_barrier(0);
 }
 
-// One schedule (measured best of six in round 2, profiles/r2/gemm8p_sched_ab.json;
-// the other five were deleted in round 5): one barrier per phase, B fragments
-// read before A (pinned order), and per-fragment lgkmcnt waits instead of a
-// blanket lgkmcnt(0) in front of each MFMA cluster.
-// The kernel body over one tile: bid = the (XCD-remapped) tile index within
-// the M x N tile grid, kz = the K-split slice. Shared by gemm8p_kernel and the
-// grouped launch (gemm8p_grouped_kernel: many independent problems, one grid).
-// tile index -> (m0, n0): grouped-M order (a.group M-tiles per group) so
-// consecutive tiles share B panels in L2
-template <int BM, int BN>
-__device__ __forceinline__ void p8_tile_origin(const P8Args& a, const int bid, int& m0, int& n0) {
-  const int tiles_m = (a.M + BM - 1) / BM, tiles_n = (a.N + BN - 1) / BN;
-  const int GROUP = a.group;
-  const int per_group = GROUP * tiles_n;
-  const int grp = bid / per_group;
-  const int first_m = grp * GROUP;
-  const int gsize = min(tiles_m - first_m, GROUP);
-  m0 = (first_m + (bid % per_group) % gsize) * BM;
-  n0 = ((bid % per_group) / gsize) * BN;
-}
-
-// kt_lo / kt_hi >= 0: an explicit K-tile range (stream-K segments); else
-// slice kz of a.kps K-tiles
-template <int BM, int BN, int WNW, bool AK, bool BK>
-__device__ __forceinline__ void gemm8p_body(const P8Args& a, const Epi& ep, const int bid, const int kz,
-                                            const int kt_lo = -1, const int kt_hi = -1) {
+// Output epilogue shared by the schedules: acc[TI][TJ] of a 2 x WNW wave
+// grid, staged through the block's LDS (smem, >= NW * 32 * (WTN + 4) * 4 B).
+template <int BM, int BN, int WNW, int TI, int TJ>
+__device__ __forceinline__ void p8_epilogue(const P8Args& a, const Epi& ep, f32x4_t (&acc)[TI][TJ], char* smem,
+                                            const int m0, const int n0, const int kz, const int wid,
+                                            const int lane) {
   using G = P8Geo<BM, BN, WNW>;
-  constexpr bool FINE = true;
-  constexpr int FI = G::FI, FJ = G::FJ, TI = 2 * FI, TJ = 2 * FJ;
-  __shared__ __attribute__((aligned(1024))) char smem[G::LDS];
-  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const int wm = wid / WNW, wn = wid % WNW;
-
-  int m0, n0;
-  p8_tile_origin<BM, BN>(a, bid, m0, n0);
-
-  const int ktiles = a.K / P8_BK;
-  const int kt0 = kt_lo >= 0 ? kt_lo : kz * a.kps;
-  const int kt1 = kt_lo >= 0 ? kt_hi : min(ktiles, kt0 + a.kps);
-  const int nk = kt1 - kt0;
-
-  f32x4_t acc[TI][TJ];
-#pragma unroll
-  for (int i = 0; i < TI; ++i)
-#pragma unroll
-    for (int j = 0; j < TJ; ++j) acc[i][j] = f32x4_t{0.f, 0.f, 0.f, 0.f};
-
-  // stage s: [AL][AH][BL][BH]
-  auto aptr = [&](int t, int h) { return smem + (t & 1) * G::STAGE + h * G::AHALF; };
-  auto bptr = [&](int t, int h) { return smem + (t & 1) * G::STAGE + 2 * G::AHALF + h * G::BHALF; };
-  auto issA = [&](int t, int h) {
-    p8_issue<G::QM, G::AROWS, G::NW, AK>(a.A, a.lda, a.M, m0, (kt0 + t) * P8_BK, aptr(t, h), h, wid, lane);
-  };
-  auto issB = [&](int t, int h) {
-    p8_issue<G::QN, G::BCOLS, G::NW, BK>(a.B, a.ldb, a.N, n0, (kt0 + t) * P8_BK, bptr(t, h), h, wid, lane);
-  };
-
-  if (nk > 0) {
-    // prologue: tile 0 complete, tile 1's AL / BL / BH in flight
-    issA(0, 0); issB(0, 0); issB(0, 1); issA(0, 1);
-    if (nk > 1) {
-      issA(1, 0); issB(1, 0); issB(1, 1);
-      asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
-    } else {
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    }
-    p8_barrier();
-
-    const int arow = wm * G::QM, bcol = wn * G::QN;   // local rows in the half images
-    s16x8_t fa[FI][2], fb0[FJ][2], fb1[FJ][2];
-    for (int t = 0; t < nk; ++t) {
-      const char* AL = aptr(t, 0);
-      const char* AH = aptr(t, 1);
-      const char* BL = bptr(t, 0);
-      const char* BH = bptr(t, 1);
-      const bool n1 = t + 1 < nk, n2 = t + 2 < nk;
-      // ---- p1: quadrant (mh0, nh0); B fragments first (pinned
-      // B-before-A issue order, guide §5 8-phase template)
-#pragma unroll
-      for (int kk = 0; kk < 2; ++kk)
-#pragma unroll
-        for (int j = 0; j < FJ; ++j) fb0[j][kk] = p8_frag<BK, G::BCOLS>(BL, lane, bcol + 16 * j, kk);
-      __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-      for (int kk = 0; kk < 2; ++kk)
-#pragma unroll
-        for (int i = 0; i < FI; ++i) fa[i][kk] = p8_frag<AK, G::AROWS>(AL, lane, arow + 16 * i, kk);
-      if (n1) issA(t + 1, 1);
-      p8_mfma<0, 0, FINE>(acc, fa, fb0);
-      p8_barrier();
-      // ---- p2: quadrant (mh0, nh1)
-#pragma unroll
-      for (int kk = 0; kk < 2; ++kk)
-#pragma unroll
-        for (int j = 0; j < FJ; ++j) fb1[j][kk] = p8_frag<BK, G::BCOLS>(BH, lane, bcol + 16 * j, kk);
-      p8_mfma<0, FJ, FINE>(acc, fa, fb1);
-      p8_barrier();
-      // ---- p3: quadrant (mh1, nh1)
-#pragma unroll
-      for (int kk = 0; kk < 2; ++kk)
-#pragma unroll
-        for (int i = 0; i < FI; ++i) fa[i][kk] = p8_frag<AK, G::AROWS>(AH, lane, arow + 16 * i, kk);
-      if (n2) issA(t + 2, 0);
-      p8_mfma<FI, FJ, FINE>(acc, fa, fb1);
-      p8_barrier();
-      // ---- p4: quadrant (mh1, nh0); retire tile t+1 (t+2's AL / BL / BH stay in flight)
-      if (n2) {
-        issB(t + 2, 0);
-        issB(t + 2, 1);
-        asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
-      } else {
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      }
-      p8_mfma<FI, 0, FINE>(acc, fa, fb0);
-      p8_barrier();
-    }
-  }
-  __syncthreads();   // LDS reuse by the epilogue
 
   const bool add_bias = ep.bias != nullptr && kz == 0;
   const int rbase = m0 + wm * G::WTM, cbase = n0 + wn * G::WTN;
@@ -411,8 +324,129 @@ __device__ __forceinline__ void gemm8p_body(const P8Args& a, const Epi& ep, cons
   }
 }
 
+// One schedule (measured best of six in round 2, profiles/r2/gemm8p_sched_ab.json;
+// the other five were deleted in round 5): one barrier per phase, B fragments
+// read before A (pinned order), and per-fragment lgkmcnt waits instead of a
+// blanket lgkmcnt(0) in front of each MFMA cluster.
+// The kernel body over one tile: bid = the (XCD-remapped) tile index within
+// the M x N tile grid, kz = the K-split slice. Shared by gemm8p_kernel and the
+// grouped launch (gemm8p_grouped_kernel: many independent problems, one grid).
+// tile index -> (m0, n0): grouped-M order (a.group M-tiles per group) so
+// consecutive tiles share B panels in L2
+template <int BM, int BN>
+__device__ __forceinline__ void p8_tile_origin(const P8Args& a, const int bid, int& m0, int& n0) {
+  const int tiles_m = (a.M + BM - 1) / BM, tiles_n = (a.N + BN - 1) / BN;
+  const int GROUP = a.group;
+  const int per_group = GROUP * tiles_n;
+  const int grp = bid / per_group;
+  const int first_m = grp * GROUP;
+  const int gsize = min(tiles_m - first_m, GROUP);
+  m0 = (first_m + (bid % per_group) % gsize) * BM;
+  n0 = ((bid % per_group) / gsize) * BN;
+}
+
+// kt_lo / kt_hi >= 0: an explicit K-tile range (stream-K segments); else
+// slice kz of a.kps K-tiles
 template <int BM, int BN, int WNW, bool AK, bool BK>
-__global__ void __launch_bounds__(128 * WNW, (BM == 256 ? 1 : 2))
+__device__ __forceinline__ void gemm8p_body(const P8Args& a, const Epi& ep, const int bid, const int kz,
+                                            const int kt_lo = -1, const int kt_hi = -1) {
+  using G = P8Geo<BM, BN, WNW>;
+  constexpr bool FINE = true;
+  constexpr int FI = G::FI, FJ = G::FJ, TI = 2 * FI, TJ = 2 * FJ;
+  __shared__ __attribute__((aligned(1024))) char smem[G::LDS];
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int wm = wid / WNW, wn = wid % WNW;
+
+  int m0, n0;
+  p8_tile_origin<BM, BN>(a, bid, m0, n0);
+
+  const int ktiles = a.K / P8_BK;
+  const int kt0 = kt_lo >= 0 ? kt_lo : kz * a.kps;
+  const int kt1 = kt_lo >= 0 ? kt_hi : min(ktiles, kt0 + a.kps);
+  const int nk = kt1 - kt0;
+
+  f32x4_t acc[TI][TJ];
+#pragma unroll
+  for (int i = 0; i < TI; ++i)
+#pragma unroll
+    for (int j = 0; j < TJ; ++j) acc[i][j] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+
+  // stage s: [AL][AH][BL][BH]
+  auto aptr = [&](int t, int h) { return smem + (t & 1) * G::STAGE + h * G::AHALF; };
+  auto bptr = [&](int t, int h) { return smem + (t & 1) * G::STAGE + 2 * G::AHALF + h * G::BHALF; };
+  auto issA = [&](int t, int h) {
+    p8_issue<G::QM, G::AROWS, G::NW, AK, G::DA>(a.A, a.lda, a.M, m0, (kt0 + t) * P8_BK, aptr(t, h), h, wid, lane);
+  };
+  auto issB = [&](int t, int h) {
+    p8_issue<G::QN, G::BCOLS, G::NW, BK, G::DB>(a.B, a.ldb, a.N, n0, (kt0 + t) * P8_BK, bptr(t, h), h, wid, lane);
+  };
+
+  if (nk > 0) {
+    // prologue: tile 0 complete, tile 1's AL / BL / BH in flight
+    issA(0, 0); issB(0, 0); issB(0, 1); issA(0, 1);
+    if (nk > 1) {
+      issA(1, 0); issB(1, 0); issB(1, 1);
+      p8_vmcnt<G::INFLIGHT>();
+    } else {
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+    p8_barrier();
+
+    const int arow = wm * G::QM, bcol = wn * G::QN;   // local rows in the half images
+    s16x8_t fa[FI][2], fb0[FJ][2], fb1[FJ][2];
+    for (int t = 0; t < nk; ++t) {
+      const char* AL = aptr(t, 0);
+      const char* AH = aptr(t, 1);
+      const char* BL = bptr(t, 0);
+      const char* BH = bptr(t, 1);
+      const bool n1 = t + 1 < nk, n2 = t + 2 < nk;
+      // ---- p1: quadrant (mh0, nh0); B fragments first (pinned
+      // B-before-A issue order, guide §5 8-phase template)
+#pragma unroll
+      for (int kk = 0; kk < 2; ++kk)
+#pragma unroll
+        for (int j = 0; j < FJ; ++j) fb0[j][kk] = p8_frag<BK, G::BCOLS>(BL, lane, bcol + 16 * j, kk);
+      __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+      for (int kk = 0; kk < 2; ++kk)
+#pragma unroll
+        for (int i = 0; i < FI; ++i) fa[i][kk] = p8_frag<AK, G::AROWS>(AL, lane, arow + 16 * i, kk);
+      if (n1) issA(t + 1, 1);
+      p8_mfma<0, 0, FINE>(acc, fa, fb0);
+      p8_barrier();
+      // ---- p2: quadrant (mh0, nh1)
+#pragma unroll
+      for (int kk = 0; kk < 2; ++kk)
+#pragma unroll
+        for (int j = 0; j < FJ; ++j) fb1[j][kk] = p8_frag<BK, G::BCOLS>(BH, lane, bcol + 16 * j, kk);
+      p8_mfma<0, FJ, FINE>(acc, fa, fb1);
+      p8_barrier();
+      // ---- p3: quadrant (mh1, nh1)
+#pragma unroll
+      for (int kk = 0; kk < 2; ++kk)
+#pragma unroll
+        for (int i = 0; i < FI; ++i) fa[i][kk] = p8_frag<AK, G::AROWS>(AH, lane, arow + 16 * i, kk);
+      if (n2) issA(t + 2, 0);
+      p8_mfma<FI, FJ, FINE>(acc, fa, fb1);
+      p8_barrier();
+      // ---- p4: quadrant (mh1, nh0); retire tile t+1 (t+2's AL / BL / BH stay in flight)
+      if (n2) {
+        issB(t + 2, 0);
+        issB(t + 2, 1);
+        p8_vmcnt<G::INFLIGHT>();
+      } else {
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      }
+      p8_mfma<FI, 0, FINE>(acc, fa, fb0);
+      p8_barrier();
+    }
+  }
+  __syncthreads();   // LDS reuse by the epilogue
+  p8_epilogue<BM, BN, WNW>(a, ep, acc, smem, m0, n0, kz, wid, lane);
+}
+
+template <int BM, int BN, int WNW, bool AK, bool BK>
+__global__ void __launch_bounds__(128 * WNW, (BM == 256 ? 1 : BM == 128 ? 2 : 3))
 gemm8p_kernel(P8Args a, Epi ep) {
   gemm8p_body<BM, BN, WNW, AK, BK>(a, ep, xcd_remap(blockIdx.x, gridDim.x), blockIdx.z);
 }
@@ -431,7 +465,8 @@ void p8_launch_one(const P8Args& g, const Epi& ep, dim3 grid, hipStream_t s) {
   X(256, 256, 4, true, true) X(256, 256, 4, true, false)                                       \
   X(256, 256, 4, false, true) X(256, 256, 4, false, false)                                     \
   X(128, 128, 2, true, true) X(128, 128, 2, true, false)                                       \
-  X(128, 128, 2, false, true) X(128, 128, 2, false, false)
+  X(128, 128, 2, false, true) X(128, 128, 2, false, false)                                     \
+  X(64, 128, 2, true, true) X(64, 128, 2, true, false)
 #define TAM_P8_EXTERN(BM, BN, W, AK, BK) \
   extern template void p8_launch_one<BM, BN, W, AK, BK>(const P8Args&, const Epi&, dim3, hipStream_t);
 #define TAM_P8_INST(BM, BN, W, AK, BK) \
@@ -446,7 +481,10 @@ inline bool gemm8p_ok(bool ak, bool bk, int M, int N, int K, long lda, long ldb)
   return true;
 }
 
-// tile: 256 (256x256, 8 waves) or 128 (128x128, 4 waves)
+// tile: 256 (256x256, 8 waves), 128 (128x128, 4 waves) or 64 (64x128, 4
+// waves of 32x64, K-major A only: the N = 512 projections of the
+// Transformer, 4096 x 512 over 256 tiles = one per CU, ~3 blocks/CU of LDS)
+inline bool gemm8p_tile_ok(int tile, bool ak) { return tile != 64 || ak; }
 void launch_gemm8p(const bf16_t* A, long lda, bool ak, const bf16_t* B, long ldb, bool bk, int M,
                    int N, int K, const Epi& ep, int splits, hipStream_t s, int tile = 256);
 // split-K without atomics or a zeroing pass, any output dtype / epilogue:

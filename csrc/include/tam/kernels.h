@@ -79,16 +79,36 @@ void avgpool_forward(const bf16_t* x, bf16_t* y, int N, int HW, int C, hipStream
 void avgpool_backward(const bf16_t* dy, bf16_t* dx, int N, int HW, int C, hipStream_t s);
 
 // fused softmax cross-entropy (forward + backward)
+// tm_b > 0: logits rows time-major (r = s * tm_b + b), labels [tm_b][S]
 void softmax_xent(const bf16_t* logits, const long* labels, bf16_t* dlogits, float* loss_rows,
                   long rows, int V, float smoothing, float grad_scale, long ignore_index,
-                  hipStream_t s);
+                  hipStream_t s, long tm_b = 0);
+// out[0] = scale * sum(x[0..n))
+void sum_scale(const float* x, long n, float* out, float scale, hipStream_t s);
 
 // embedding
-// V = table rows: ids outside [0, V) read zero rows / take no gradient
+// V = table rows: ids outside [0, V) read zero rows / take no gradient;
+// tm_b > 0: ids [tm_b][S], rows of out / dout time-major (t = s * tm_b + b)
+// pos (optional [pos_rows][D]): + pos[position of t] (batch-major: t % pos_rows)
 void embedding_forward(const bf16_t* table, const long* ids, bf16_t* out, long T, int D,
-                       float scale, hipStream_t s, long V);
+                       float scale, hipStream_t s, long V, long tm_b = 0, const bf16_t* pos = nullptr,
+                       long pos_rows = 0);
 void embedding_backward(const bf16_t* dout, const long* ids, float* gtable, long T, int D,
-                        float scale, hipStream_t s, long V);
+                        float scale, hipStream_t s, long V, long tm_b = 0);
+
+// row-block copies / sums (bf16): up to 4 jobs per launch, each
+// out[r][0..C) = sum_q in_q[r][0..C) over n_in <= 4 pitched inputs
+struct RowJob {
+  const bf16_t* in[4];
+  long ld_in[4];
+  bf16_t* out;
+  long ld_out;
+  int C, n_in;
+};
+struct RowJobs {
+  RowJob job[4];
+};
+void rows_sum(const RowJobs& jb, int njobs, long R, hipStream_t s);
 
 // misc
 // out[c] += sum_r x[r][c]; ws: COLSUM_MAX_BLOCKS * C floats (C % 8 == 0 path)

@@ -102,8 +102,17 @@ int gemm8p_policy_tile() { return g_p8_tile; }
 void gemm8p_group(int g) { g_p8_group = g > 0 ? g : 4; }
 void gemm8p_policy(int mode, int tile) {
   g_p8 = mode;
-  g_p8_tile = tile == 128 || tile == 256 ? tile : 0;
+  g_p8_tile = tile == 64 || tile == 128 || tile == 256 ? tile : 0;
 }
+
+// block shape of a tile code (64 = 64 x 128)
+static int p8_bm(int T) { return T; }
+static int p8_bn(int T) { return T == 256 ? 256 : 128; }
+static long p8_tiles(int M, int N, int T) { return (long)cdiv(M, p8_bm(T)) * cdiv(N, p8_bn(T)); }
+// blocks that fill the chip: 256^2 one per CU (200 of 256 is enough), 128^2
+// two per CU, 64x128 one per CU (the tile exists for ~256-block grids)
+static long p8_want(int T) { return T == 128 ? 448 : T == 256 ? 200 : 256; }
+static bool p8_known(int T) { return T == 64 || T == 128 || T == 256; }
 
 TAM_P8_VARIANTS(TAM_P8_EXTERN)
 
@@ -116,7 +125,7 @@ static void p8_launch_l(bool ak, bool bk, const P8Args& g, const Epi& ep, dim3 g
 }
 
 int gemm8p_tile(int M, int N, int K) {
-  if (g_p8_tile) return g_p8_tile;
+  if (g_p8_tile) return g_p8_tile;   // (a forced 64 falls back to 128 for M-major A: gemm8p_tile_ok)
   // 256^2 only when its grid already covers the chip
   const long t256 = (long)cdiv(M, 256) * cdiv(N, 256);
   return t256 >= 200 ? 256 : 128;
@@ -124,15 +133,22 @@ int gemm8p_tile(int M, int N, int K) {
 
 void launch_gemm8p(const bf16_t* A, long lda, bool ak, const bf16_t* B, long ldb, bool bk, int M,
                    int N, int K, const Epi& ep, int splits, hipStream_t s, int tile) {
-  const int T = tile == 128 ? 128 : 256;
-  const int tiles = cdiv(M, T) * cdiv(N, T);
+  int T = p8_known(tile) ? tile : 256;
+  if (!gemm8p_tile_ok(T, ak)) T = 128;
+  const int tiles = (int)p8_tiles(M, N, T);
   const int ktiles = K / P8_BK;
   const int kps = cdiv(ktiles, splits < 1 ? 1 : splits);
   const int z = cdiv(ktiles, kps);
   P8Args g{A, lda, B, ldb, M, N, K, kps, g_p8_group};
   const dim3 grid(tiles, 1, z);
-  if (T == 128) p8_launch_l<128, 128, 2>(ak, bk, g, ep, grid, s);
-  else p8_launch_l<256, 256, 4>(ak, bk, g, ep, grid, s);
+  if (T == 64) {
+    if (bk) p8_launch_one<64, 128, 2, true, true>(g, ep, grid, s);
+    else p8_launch_one<64, 128, 2, true, false>(g, ep, grid, s);
+  } else if (T == 128) {
+    p8_launch_l<128, 128, 2>(ak, bk, g, ep, grid, s);
+  } else {
+    p8_launch_l<256, 256, 4>(ak, bk, g, ep, grid, s);
+  }
 }
 
 // ---- slab split-K (gemm8p.h): reduce ws[sp][M][N] -> C with the epilogue
@@ -173,10 +189,10 @@ void gemm8p_slab_force(int sp) { g_p8_force_sp = sp > 0 ? sp : 0; }
 
 int gemm8p_slab_splits(int M, int N, int K, int tile) {
   if (g_p8_force_sp) return g_p8_force_sp;
-  const int T = tile == 128 ? 128 : 256;
-  const long t = (long)cdiv(M, T) * cdiv(N, T);
+  const int T = p8_known(tile) ? tile : 256;
+  const long t = p8_tiles(M, N, T);
   const int kt = K / P8_BK;
-  const long want = T == 128 ? 448 : 200;     // blocks that fill the chip (128^2: 2 per CU)
+  const long want = p8_want(T);
   if (t >= want * 3 / 4 || kt < 16 || N % 4 != 0) return 1;
   int sp = (int)((want + t - 1) / t);
   if (sp > kt / 8) sp = kt / 8;          // >= 8 K-tiles per slice
@@ -207,8 +223,8 @@ void gemm_slab_reduce(const float* ws, int sp, int M, int N, const Epi& ep, hipS
 
 // atomic split-K count (fp32 outputs) that fills the chip (>= 4 K-tiles per split)
 static int p8_splits(int M, int N, int K, bool can_split, int tile) {
-  const long t = (long)cdiv(M, tile) * cdiv(N, tile);
-  const long want = tile == 128 ? 448 : 200;
+  const long t = p8_tiles(M, N, tile);
+  const long want = p8_want(tile);
   if (!can_split || t >= want || K / P8_BK < 8) return 1;
   int sp = (int)((want + t - 1) / t);
   if (sp > K / P8_BK / 4) sp = K / P8_BK / 4;
@@ -254,7 +270,8 @@ void gemm_select(const bf16_t* A, long lda, bool ak, const bf16_t* B, long ldb, 
     const long t8 = (long)cdiv(M, 256) * cdiv(N, 256);
     const double flop = 2.0 * M * N * K;
     if (g_p8 >= 2 || path == 3 || (t8 >= 48 && K >= 512 && flop >= 4e9)) {
-      const int tile = gemm8p_tile(M, N, K);
+      int tile = gemm8p_tile(M, N, K);
+      if (!gemm8p_tile_ok(tile, ak)) tile = 128;
       int sp = p8_splits(M, N, K, can_split, tile);
       if (g_force_splits >= 1) sp = can_split ? g_force_splits : 1;
       prepare_split(ep, sp, M, N, s);

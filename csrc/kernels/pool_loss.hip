@@ -276,16 +276,23 @@ void avgpool_backward(const bf16_t* dy, bf16_t* dx, int N, int HW, int C, hipStr
 // is the graph's sink, so dlogits = (softmax - target) * grad_scale is known.
 // Label smoothing eps: target = (1-eps) onehot + eps/V. ignore_index rows
 // contribute 0 loss / 0 grad.
+// tm_b > 0: the logits rows are time-major (row r = s * tm_b + b) while the
+// labels stay [tm_b][S] batch-major: row r reads labels[b * S + s] (no
+// transposed copy of the labels, S = rows / tm_b)
+__device__ __forceinline__ long tm_index(long r, long rows, long tm_b) {
+  return tm_b > 0 ? (r % tm_b) * (rows / tm_b) + r / tm_b : r;
+}
+
 __global__ void __launch_bounds__(256) xent_kernel(const bf16_t* __restrict__ logits,
                                                     const long* __restrict__ labels,
                                                     bf16_t* __restrict__ dlogits,
                                                     float* __restrict__ loss_rows, int V,
                                                     float smoothing, float grad_scale,
-                                                    long ignore_index) {
+                                                    long ignore_index, long tm_b) {
   __shared__ float scratch[16];
   const long row = blockIdx.x;
   const bf16_t* lr = logits + row * V;
-  const long lab = labels[row];
+  const long lab = labels[tm_index(row, gridDim.x, tm_b)];
   const bool ign = lab == ignore_index;
   // pass 1: online max / sum-exp, vectorized 8-wide when aligned
   float m = -INFINITY, s = 0.f, sum_logit = 0.f;
@@ -358,59 +365,81 @@ __global__ void __launch_bounds__(256) xent_kernel(const bf16_t* __restrict__ lo
 
 void softmax_xent(const bf16_t* logits, const long* labels, bf16_t* dlogits, float* loss_rows,
                   long rows, int V, float smoothing, float grad_scale, long ignore_index,
-                  hipStream_t s) {
+                  hipStream_t s, long tm_b) {
   hipLaunchKernelGGL(xent_kernel, dim3(rows), dim3(256), 0, s, logits, labels, dlogits, loss_rows,
-                     V, smoothing, grad_scale, ignore_index);
+                     V, smoothing, grad_scale, ignore_index, tm_b);
+}
+
+// out[0] = scale * sum(x[0..n)): the mean loss from the per-row losses, one
+// block (no torch reduce + scale kernels in the step)
+__global__ void __launch_bounds__(256) sum_scale_kernel(const float* __restrict__ x, long n,
+                                                        float* __restrict__ out, float scale) {
+  __shared__ float scratch[16];
+  float acc = 0.f;
+  for (long i = threadIdx.x; i < n; i += 256) acc += x[i];
+  const float t = block_sum(acc, scratch);
+  if (threadIdx.x == 0) out[0] = t * scale;
+}
+void sum_scale(const float* x, long n, float* out, float scale, hipStream_t s) {
+  hipLaunchKernelGGL(sum_scale_kernel, dim3(1), dim3(256), 0, s, x, n, out, scale);
 }
 
 // ------------------------------------------------------------------ embedding
 // out[t][:] = table[ids[t]][:] * scale  (D % 8 == 0), 16 B per lane
 // ids outside [0, V) (a batch built for another vocabulary) read as zero
 // rows and take no gradient, instead of faulting the device
+// tm_b > 0: output rows time-major (t = s * tm_b + b) from [tm_b][S] ids;
+// pos (optional, [S][D]): + pos[s] after the scale (a positional table added
+// in the same pass, no broadcast copy); S = pos_rows
 __global__ void embed_fwd_kernel(const bf16_t* __restrict__ table, const long* __restrict__ ids,
-                                 bf16_t* __restrict__ out, long T, int D, float scale, long V) {
+                                 bf16_t* __restrict__ out, long T, int D, float scale, long V, long tm_b,
+                                 const bf16_t* __restrict__ pos, long pos_rows) {
   const int d8 = D / 8;
   const long total = T * d8;
   for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < total;
        i += (long)gridDim.x * blockDim.x) {
     const long t = i / d8;
     const int c = (int)(i % d8) * 8;
-    const long id = ids[t];
+    const long id = ids[tm_index(t, T, tm_b)];
     const uint4 u = (unsigned long)id < (unsigned long)V ? *(const uint4*)(table + id * D + c)
                                                           : make_uint4(0u, 0u, 0u, 0u);
-    if (scale == 1.f) {
+    if (scale == 1.f && !pos) {
       *(uint4*)(out + t * D + c) = u;
     } else {
       const uint32_t w[4] = {u.x, u.y, u.z, u.w};
+      uint4 pv = make_uint4(0u, 0u, 0u, 0u);
+      if (pos) pv = *(const uint4*)(pos + (tm_b > 0 ? t / tm_b : t % pos_rows) * D + c);
+      const uint32_t pw[4] = {pv.x, pv.y, pv.z, pv.w};
       uint32_t o[4];
 #pragma unroll
       for (int k = 0; k < 4; ++k)
-        o[k] = pack_bf2(__uint_as_float(w[k] << 16) * scale, __uint_as_float(w[k] & 0xffff0000u) * scale);
+        o[k] = pack_bf2(__uint_as_float(w[k] << 16) * scale + __uint_as_float(pw[k] << 16),
+                        __uint_as_float(w[k] & 0xffff0000u) * scale + __uint_as_float(pw[k] & 0xffff0000u));
       *(uint4*)(out + t * D + c) = make_uint4(o[0], o[1], o[2], o[3]);
     }
   }
 }
 // grad_table[ids[t]] += dout[t] * scale  (fp32 atomics; rows of D contiguous)
 __global__ void embed_bwd_kernel(const bf16_t* __restrict__ dout, const long* __restrict__ ids,
-                                 float* __restrict__ gtable, long T, int D, float scale, long V) {
+                                 float* __restrict__ gtable, long T, int D, float scale, long V, long tm_b) {
   const long total = T * D;
   for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < total;
        i += (long)gridDim.x * blockDim.x) {
     const long t = i / D;
     const int c = (int)(i % D);
-    const long id = ids[t];
+    const long id = ids[tm_index(t, T, tm_b)];
     if ((unsigned long)id < (unsigned long)V) atomicAdd(gtable + id * D + c, bf2f(dout[i]) * scale);
   }
 }
 void embedding_forward(const bf16_t* table, const long* ids, bf16_t* out, long T, int D,
-                       float scale, hipStream_t s, long V) {
+                       float scale, hipStream_t s, long V, long tm_b, const bf16_t* pos, long pos_rows) {
   hipLaunchKernelGGL(embed_fwd_kernel, dim3(grid_cap(T * D / 8)), dim3(256), 0, s, table, ids, out,
-                     T, D, scale, V);
+                     T, D, scale, V, tm_b, pos, pos_rows);
 }
 void embedding_backward(const bf16_t* dout, const long* ids, float* gtable, long T, int D,
-                        float scale, hipStream_t s, long V) {
+                        float scale, hipStream_t s, long V, long tm_b) {
   hipLaunchKernelGGL(embed_bwd_kernel, dim3(grid_cap(T * D)), dim3(256), 0, s, dout, ids, gtable, T,
-                     D, scale, V);
+                     D, scale, V, tm_b);
 }
 
 // ------------------------------------------------------------- column sums
@@ -585,6 +614,48 @@ __global__ void add_kernel(const bf16_t* __restrict__ a, const bf16_t* __restric
 }
 void add_bf16(const bf16_t* a, const bf16_t* b, bf16_t* y, long n, hipStream_t s) {
   hipLaunchKernelGGL(add_kernel, dim3(grid_cap(n / 8)), dim3(256), 0, s, a, b, y, n / 8);
+}
+
+// ---------------------------------------------------- row-block copies / sums
+// Up to 4 jobs in one launch (blockIdx.y = job): out[r][0..C) = sum of the
+// job's n_in inputs' rows r, every operand with its own row pitch (16-B
+// aligned rows, C % 8 == 0). A last-dim concat is one job per part (n_in =
+// 1, out = the part's column slice); a gradient fan-in is one job of n_in
+// inputs -- the pitched column slices a concat's backward hands out.
+__global__ void __launch_bounds__(256) rows_sum_kernel(RowJobs jb, long R) {
+  const RowJob& j = jb.job[blockIdx.y];
+  const int c8 = j.C / 8;
+  const long total = R * c8;
+  for (long i = blockIdx.x * 256L + threadIdx.x; i < total; i += (long)gridDim.x * 256) {
+    const long r = i / c8;
+    const int c = (int)(i % c8) * 8;
+    uint4 u = *(const uint4*)(j.in[0] + r * j.ld_in[0] + c);
+    if (j.n_in > 1) {
+      float f[8];
+      const uint32_t* w = (const uint32_t*)&u;
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        f[2 * k] = __uint_as_float(w[k] << 16);
+        f[2 * k + 1] = __uint_as_float(w[k] & 0xffff0000u);
+      }
+      for (int q = 1; q < j.n_in; ++q) {
+        const uint4 v = *(const uint4*)(j.in[q] + r * j.ld_in[q] + c);
+        const uint32_t* x = (const uint32_t*)&v;
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+          f[2 * k] += __uint_as_float(x[k] << 16);
+          f[2 * k + 1] += __uint_as_float(x[k] & 0xffff0000u);
+        }
+      }
+      u = make_uint4(pack_bf2(f[0], f[1]), pack_bf2(f[2], f[3]), pack_bf2(f[4], f[5]), pack_bf2(f[6], f[7]));
+    }
+    *(uint4*)(j.out + r * j.ld_out + c) = u;
+  }
+}
+void rows_sum(const RowJobs& jb, int njobs, long R, hipStream_t s) {
+  long mx = 0;
+  for (int q = 0; q < njobs; ++q) mx = std::max(mx, R * (jb.job[q].C / 8));
+  hipLaunchKernelGGL(rows_sum_kernel, dim3(grid_cap(mx), njobs), dim3(256), 0, s, jb, R);
 }
 
 __global__ void cast_f32_bf16_kernel(const float* __restrict__ x, bf16_t* __restrict__ y, long n) {

@@ -288,10 +288,11 @@ def test_gemm_dma_configs(gpu, cfg, ak, bk):
 # forced, 0 = the auto tile), edge tiles, K just one tile and many tiles,
 # every epilogue (bf16 staged, bias / relu / mask / alpha / accumulate, fp32
 # store / accumulate / split-K atomics)
-@pytest.mark.parametrize("tile", [0, 128, 256])
+@pytest.mark.parametrize("tile", [0, 64, 128, 256])
 @pytest.mark.parametrize("ak,bk", [(True, True), (True, False), (False, True), (False, False)])
 @pytest.mark.parametrize("M,N,K", [(256, 256, 64), (520, 392, 448), (1024, 768, 2048)])
 def test_gemm8p(gpu, tile, ak, bk, M, N, K):
+    # tile 64 = the 64x128 K-major-A tile (M-major A falls back to 128^2)
     torch.manual_seed(M + N + K + 2 * ak + bk)
     A = torch.randn(M, K, device=gpu).to(BF)
     B = torch.randn(K, N, device=gpu).to(BF)
@@ -333,7 +334,7 @@ def test_gemm8p_exact_integer_layout(gpu, ak, bk):
     a = (A if ak else A.t().contiguous()).to(BF)
     b = (B.t().contiguous() if bk else B).to(BF)
     ref = A @ B
-    for tile in (0, 128, 256):
+    for tile in (0, 64, 128, 256):
         T().gemm8p_policy(2, tile)
         c = torch.empty(M, N, device=gpu)
         T().gemm(a, ak, b, bk, c, 0, None, False, None, 1.0, False)
@@ -1084,6 +1085,73 @@ def test_softmax_xent(gpu, V, smooth):
     assert rel_err(loss_rows, ref) < 1e-4
     g, = torch.autograd.grad(ref.sum() / rows, [lf])
     assert rel_err(dlog, g) < 1e-2
+
+
+def test_softmax_xent_time_major_labels_and_mean(gpu):
+    """[T,B,V] logits with the [B,T] labels read in place (tm_b = B) equal
+    the transposed-copy labels; the mean loss is our one-block reduction."""
+    torch.manual_seed(18)
+    Tn, B, V = 7, 6, 1000
+    logits = (torch.randn(Tn, B, V, device=gpu) * 3).to(BF)
+    labels = torch.randint(0, V, (B, Tn), device=gpu)
+    labels[2, 3] = -100
+    rows = Tn * B
+    lr1, lr2 = torch.empty(rows, device=gpu), torch.empty(rows, device=gpu)
+    d1, d2 = torch.empty(rows, V, device=gpu, dtype=BF), torch.empty(rows, V, device=gpu, dtype=BF)
+    T().softmax_xent(logits.view(rows, V), labels.t().contiguous().view(-1), d1, lr1, 0.1, 1.0 / rows, -100)
+    T().softmax_xent(logits.view(rows, V), labels.view(-1), d2, lr2, 0.1, 1.0 / rows, -100, B)
+    assert torch.equal(lr1, lr2) and torch.equal(d1, d2)
+    out = torch.empty((), device=gpu)
+    T().sum_scale(lr2, out, 1.0 / rows)
+    assert abs(float(out) - float(lr1.double().sum() / rows)) < 1e-5 * max(1.0, abs(float(out)))
+
+
+def test_embedding_time_major(gpu):
+    """ids [B,S] -> rows s * B + b (no transposed id copy), fwd and bwd."""
+    torch.manual_seed(19)
+    B, S, D = 5, 9, 64
+    table = torch.randn(300, D, device=gpu).to(BF)
+    ids = torch.randint(0, 300, (B, S), device=gpu)
+    out = torch.empty(S * B, D, device=gpu, dtype=BF)
+    T().embedding_forward(table, ids.view(-1), out, 1.0, B)
+    assert torch.equal(out, table[ids.t().reshape(-1)])
+    dout = torch.randn(S * B, D, device=gpu).to(BF)
+    g1, g2 = torch.zeros(300, D, device=gpu), torch.zeros(300, D, device=gpu)
+    T().embedding_backward(dout, ids.view(-1), g1, 1.0, B)
+    T().embedding_backward(dout, ids.t().contiguous().view(-1), g2, 1.0)
+    assert rel_err(g1, g2) < 1e-6
+    # + a positional table [S][D] in the same pass (batch-major and time-major)
+    pos = torch.randn(S, D, device=gpu).to(BF)
+    o2 = torch.empty(B * S, D, device=gpu, dtype=BF)
+    T().embedding_forward(table, ids.view(-1), o2, 2.0, 0, pos)
+    ref = table.float()[ids] * 2 + pos.float()[None]
+    assert rel_err(o2.view(B, S, D), ref) < 1e-2
+    T().embedding_forward(table, ids.view(-1), o2, 2.0, B, pos)
+    assert rel_err(o2.view(S, B, D), ref.transpose(0, 1)) < 1e-2
+
+
+def test_rows_sum_concat_and_fanin(gpu):
+    """rows_sum: a last-dim concat (one copy job per part, pitched inputs)
+    and a 3-input gradient fan-in over column slices of wider tensors --
+    exact against torch (bf16 sums of small integers)."""
+    torch.manual_seed(20)
+    R = 3 * 41
+    a = torch.randint(-4, 5, (3, 41, 64), device=gpu).to(BF)
+    wide = torch.randint(-4, 5, (3, 41, 192), device=gpu).to(BF)
+    b = wide[..., 64:160]                                   # pitched view (row pitch 192)
+    out = torch.empty(3, 41, 160, device=gpu, dtype=BF)
+    T().rows_sum([out[..., :64], out[..., 64:]], [a, b], [1, 1])
+    assert torch.equal(out, torch.cat([a, b], -1))
+    ins = [wide[..., :64], wide[..., 128:], a]
+    s = torch.empty(3, 41, 64, device=gpu, dtype=BF)
+    T().rows_sum([s], ins, [3])
+    assert torch.equal(s, (ins[0].float() + ins[1].float() + ins[2].float()).to(BF))
+    from tiresias_amd.ops import functional as Fx
+    x = torch.randint(-4, 5, (R, 64), device=gpu).to(BF).requires_grad_(True)
+    y1, y2, y3 = Fx.fanout(x, 3)
+    loss = (Fx.cat2(y1, y2).float()).sum() + (y3.float() * 3).sum()
+    loss.backward()
+    assert torch.equal(x.grad.float(), torch.full((R, 64), 5.0, device=gpu))
 
 
 def test_embedding(gpu):

@@ -116,11 +116,11 @@ class Trainer:
             else:
                 logits = self.model.forward(d)
             labels = d["labels"]
-            if getattr(self.model, "logits_time_major", False):
-                labels = labels.t()                  # [B,T] -> the logits' [T,B] row order
             rows = labels.numel()
+            # time-major logits [T,B,V] read the [B,T] labels in place
             loss, dlog = Fx.softmax_xent(logits, labels, smoothing=self.spec.smoothing,
-                                         ignore_index=-100, normalizer=rows)
+                                         ignore_index=-100, normalizer=rows,
+                                         labels_time_major=getattr(self.model, "logits_time_major", False))
             logits.backward(dlog)
             if group:
                 Fx.flush_wgrad()

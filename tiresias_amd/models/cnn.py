@@ -104,15 +104,21 @@ class ResNet50:
     def forward(self, x: torch.Tensor) -> torch.Tensor:
         Fx.prepare_conv_wt(self.conv_params())
         if self.training:
-            self.bn_buf.zero_()          # every BN accumulator of this step: one memset
+            # every BN accumulator of this step: one zeroing launch of ours
+            if self.bn_buf.is_cuda:
+                Fx._T().zero_(self.bn_buf)
+            else:
+                self.bn_buf.zero_()
         y = Fx.conv2d(x, self.stem, stride=2, pad=3, bn_stats=self._st("stem"))
         y = self._bn(y, self.stem_bn, "stem", relu=True)
         y = Fx.maxpool2d(y, 3, 2, 1)
         for blk in self.blocks:
             pre = blk["pre"]
             # the second consumer of y (residual / downsample) goes through a
-            # tap: its gradient is summed inside y's producing BN backward
-            idn = Fx.residual_tap(y) if "down" not in blk else None
+            # tap: its gradient is summed inside y's producing BN backward (a
+            # fan-out summed by our kernel when the producer is the max-pool)
+            y, y2 = Fx.residual_split(y)
+            idn = y2 if "down" not in blk else None
             # bn1 / bn2 outputs feed exactly one conv each: that conv's dgrad
             # epilogue applies their ReLU backward mask (in_relu)
             o = Fx.conv2d(y, blk["c1"], bn_stats=self._st(pre + ".bn1"))
@@ -122,7 +128,7 @@ class ResNet50:
             o = self._bn(o, blk["bn2"], pre + ".bn2", relu=True, consumer_masks=True)
             o = Fx.conv2d(o, blk["c3"], in_relu=True, bn_stats=self._st(pre + ".bn3"))
             if "down" in blk:
-                idn = Fx.conv2d(Fx.residual_tap(y), blk["down"], stride=blk["stride"],
+                idn = Fx.conv2d(y2, blk["down"], stride=blk["stride"],
                                 bn_stats=self._st(pre + ".dbn"))
                 idn = self._bn(idn, blk["down_bn"], pre + ".dbn", relu=False)
             y = self._bn(o, blk["bn3"], pre + ".bn3", relu=True, res=idn)

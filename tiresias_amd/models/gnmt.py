@@ -349,7 +349,8 @@ class GNMT:
             # of one zeroing kernel per launch
             B = src.shape[0]
             n = 2 * (len(self.enc) + len(self.dec)) * _sync_words(B)
-            self._sync_pool = torch.zeros(n, dtype=torch.int32, device=src.device)
+            self._sync_pool = torch.empty(n, dtype=torch.int32, device=src.device)
+            _T().zero_(self._sync_pool)
             self._sync_next, self._sync_B = 0, B
         # time-major activations [T,B,H]
         # branch 1: the first decoder layer (+ attention query) reads only the
@@ -360,28 +361,37 @@ class GNMT:
         # batch / token strides and the logits come out [T,B,V] with the
         # labels transposed to match (logits_time_major), so no activation
         # or gradient is ever re-laid between the recurrences and attention
-        tgt_t = tgt_in.t().contiguous()
-        with Fx.on_branch(1, tgt_t):
-            y = Fx.embedding(tgt_t, self.tgt_emb)
+        # the embeddings read the [B,S] ids time-major in place; every tensor
+        # with several consumers goes through Fx.fanout (its gradients summed
+        # by one launch of ours) and every feature concat through Fx.cat2, so
+        # the step runs no torch elementwise / concat / copy kernels
+        with Fx.on_branch(1, tgt_in):
+            y = Fx.embedding(tgt_in, self.tgt_emb, time_major=True)
             d0 = lstm(y, self.dec[0], model=self)                    # [T,B,H]
-            q = Fx.linear(d0, self.att_q)                            # [T,B,H]
-        x = Fx.embedding(src.t().contiguous(), self.src_emb)
-        with Fx.on_branch(0, x):
-            bw = lstm(x, self.enc[1], reverse=True, model=self)
+            d0q, d0 = Fx.fanout(d0, 2)
+            q = Fx.linear(d0q, self.att_q)                           # [T,B,H]
+        x = Fx.embedding(src, self.src_emb, time_major=True)
+        xb, x = Fx.fanout(x, 2)
+        with Fx.on_branch(0, xb):
+            bw = lstm(xb, self.enc[1], reverse=True, model=self)
         fw = lstm(x, self.enc[0], model=self)
         bw = Fx.join_branch(0, bw)
-        h = lstm(torch.cat([fw, bw], 2), self.enc[2], model=self)
-        for i, p in enumerate(self.enc[3:]):
-            o = lstm(h, p, model=self)
-            h = Fx.add(h, o) if i >= 0 else o          # residual from layer 3 on
+        h = lstm(Fx.cat2(fw, bw), self.enc[2], model=self)
+        for p in self.enc[3:]:                           # residual from layer 3 on
+            hi, h = Fx.fanout(h, 2)
+            h = Fx.add(h, lstm(hi, p, model=self))
         kv = Fx.linear(h, self.att_kv)                   # [S,B,2H]
         d0, q = Fx.join_branch(1, d0, q)
         ctxv = Fx.cross_attention(q, kv, self.heads, time_major=True)   # [T,B,H]
+        cs = Fx.fanout(ctxv, len(self.dec))              # the decoder layers' inputs + the classifier's
         h = d0
         for i, p in enumerate(self.dec[1:]):
-            o = lstm(torch.cat([h, ctxv], 2), p, model=self)
-            h = Fx.add(h, o) if i >= 1 else o
-        out = torch.cat([h, ctxv], 2)                    # [T,B,2H]
+            if i >= 1:
+                hi, h = Fx.fanout(h, 2)
+                h = Fx.add(h, lstm(Fx.cat2(hi, cs[i]), p, model=self))
+            else:
+                h = lstm(Fx.cat2(h, cs[i]), p, model=self)
+        out = Fx.cat2(h, cs[-1])                         # [T,B,2H]
         return Fx.linear(out, self.cls_w, self.cls_b)    # [T,B,V] (logits_time_major)
 
     def buffers(self):

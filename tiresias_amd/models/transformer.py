@@ -78,9 +78,8 @@ class TransformerBase:
         return pe.to(device=dev, dtype=torch.bfloat16)
 
     def _embed(self, ids):
-        x = Fx.embedding(ids, self.emb, scale=math.sqrt(self.d))
-        S = ids.shape[1]
-        return Fx.add(x, self.pos[:S].unsqueeze(0).expand_as(x).contiguous())
+        # scale + positional table in the embedding kernel (no broadcast copy)
+        return Fx.embedding(ids, self.emb, scale=math.sqrt(self.d), pos=self.pos[:ids.shape[1]])
 
     @staticmethod
     def _ln_skip(x, r, p):

@@ -528,7 +528,7 @@ def conv2d(x: torch.Tensor, w: Param, b: Optional[Param] = None, stride: int = 1
 # ============================================================ BatchNorm (NHWC)
 class GradSlot:
     """A second upstream gradient of a BN output, parked by a residual tap
-    (``residual_tap``) instead of being summed by autograd; the producing
+    (``residual_split``) instead of being summed by autograd; the producing
     BN's backward adds it while loading dy (bn_backward ``addend``), so the
     residual-branch sum is never materialised (no separate add kernel)."""
 
@@ -552,14 +552,17 @@ class _Tap(Function):
         return None, None
 
 
-def residual_tap(y: torch.Tensor) -> torch.Tensor:
-    """y for a second consumer (the residual branch / a downsample conv):
-    its gradient goes to y's producing BN as an addend. Plain y when the
-    producer is not such a BN (or on CPU)."""
+def residual_split(y: torch.Tensor) -> Tuple[torch.Tensor, torch.Tensor]:
+    """(y for the main branch, y for a second consumer): a residual tap when
+    y's producer is a BN (the sum happens in its backward), else a fan-out
+    whose two gradients one launch of ours sums (e.g. the max-pool output
+    feeding the first bottleneck's conv1 and its downsample conv)."""
     slot = getattr(y, "_tam_slot", None)
-    if slot is None or not y.is_cuda or not torch.is_grad_enabled():
-        return y
-    return _Tap.apply(y, slot)
+    if not (y.is_cuda and torch.is_grad_enabled() and y.requires_grad):
+        return y, y
+    if slot is not None:
+        return y, _Tap.apply(y, slot)
+    return fanout(y, 2)
 
 
 class _BN(Function):
@@ -814,6 +817,9 @@ class _LNSkip(_LN):
 
     @staticmethod
     def forward(ctx, x, token, g: Param, b: Param, eps: float):
+        # an unused skip output (the stack's final LN) arrives as None, not
+        # as a zero-filled tensor autograd would launch a fill kernel for
+        ctx.set_materialize_grads(False)
         y = _LN.forward(ctx, x, token, g, b, eps)
         return x.view_as(x), y
 
@@ -851,6 +857,7 @@ class _AddLNSkip(Function):
 
     @staticmethod
     def forward(ctx, x, r, token, g: Param, b: Param, eps: float):
+        ctx.set_materialize_grads(False)         # see _LNSkip.forward
         D = x.shape[-1]
         rows = x.numel() // D
         if x.is_cuda:
@@ -955,28 +962,35 @@ def global_avgpool(x: torch.Tensor) -> torch.Tensor:
 # ============================================================ loss
 def softmax_xent(logits: torch.Tensor, labels: torch.Tensor, smoothing: float = 0.0,
                  ignore_index: Optional[int] = -100,
-                 normalizer: Optional[int] = None) -> Tuple[torch.Tensor, torch.Tensor]:
+                 normalizer: Optional[int] = None,
+                 labels_time_major: bool = False) -> Tuple[torch.Tensor, torch.Tensor]:
     """Fused softmax cross-entropy. Returns (mean loss, dlogits) WITHOUT autograd:
     the loss is the graph sink, so the training step calls
     ``logits.backward(dlogits)`` directly (no extra scale pass over the logits).
 
     ``normalizer``: number of non-ignored rows when known statically (keeps the
     step free of host syncs, i.e. capturable in a hipGraph); otherwise counted.
+    ``labels_time_major``: logits are [T,B,V] while labels stay [B,T] -- the
+    kernel reads label (b, t) for logits row t * B + b (no transposed copy).
+    The mean loss is one reduction kernel of ours (no torch reduce / scale).
     """
     V = logits.shape[-1]
     l2 = logits.reshape(-1, V).contiguous()
-    lab = labels.reshape(-1).contiguous()
     rows = l2.shape[0]
+    tm_b = labels.shape[0] if labels_time_major else 0
     ign = ignore_index if ignore_index is not None else -(1 << 62)
     if normalizer is None:
-        normalizer = max(1, int((lab != ign).sum().item()))
+        normalizer = max(1, int((labels != ign).sum().item()))
     n = normalizer
     if l2.is_cuda:
+        lab = labels.reshape(-1).contiguous()
         loss_rows = torch.empty(rows, dtype=torch.float32, device=l2.device)
         dlog = torch.empty_like(l2)
-        _T().softmax_xent(l2.detach(), lab, dlog, loss_rows, smoothing, 1.0 / n, ign)
-        loss = loss_rows.sum() / n
+        _T().softmax_xent(l2.detach(), lab, dlog, loss_rows, smoothing, 1.0 / n, ign, tm_b)
+        loss = torch.empty((), dtype=torch.float32, device=l2.device)
+        _T().sum_scale(loss_rows, loss, 1.0 / n)
         return loss, dlog.view(logits.shape)
+    lab = (labels.t() if labels_time_major else labels).reshape(-1)
     lf = l2.detach().float()
     logp = torch.log_softmax(lf, -1)
     valid = (lab != ign)
@@ -993,18 +1007,29 @@ def softmax_xent(logits: torch.Tensor, labels: torch.Tensor, smoothing: float = 
 
 # ============================================================ embedding
 class _Embed(Function):
+    """time_major: ids [B,S] -> out [S,B,D], the kernel reading ids (b, s) for
+    row s * B + b (no transposed copy of the ids, forward or backward)."""
+
     @staticmethod
-    def forward(ctx, ids, token, table: Param, scale: float):
+    def forward(ctx, ids, token, table: Param, scale: float, time_major: bool = False, pos=None):
         D = table.shape[1]
+        tm_b = ids.shape[0] if time_major else 0
+        oshape = (ids.shape[1], ids.shape[0], D) if time_major else (*ids.shape, D)
         flat = ids.reshape(-1).contiguous()
         if flat.is_cuda:
             out = torch.empty(flat.numel(), D, dtype=BF16, device=flat.device)
-            _T().embedding_forward(table.w, flat, out, scale)
+            _T().embedding_forward(table.w, flat, out, scale, tm_b, pos)
         else:
-            out = (table.w.float()[flat] * scale).to(BF16)
-        ctx.table, ctx.scale = table, scale
+            if time_major:
+                flat = ids.t().reshape(-1)
+            out = table.w.float()[flat] * scale
+            if pos is not None:
+                # bf16 rounding of the scaled row first, as the separate add did
+                out = out.to(BF16).float().view(*oshape) + (pos.float()[:, None] if time_major else pos.float())
+            out = out.to(BF16)
+        ctx.table, ctx.scale, ctx.tm_b = table, scale, tm_b
         ctx.save_for_backward(flat)
-        return out.view(*ids.shape, D)
+        return out.view(*oshape)
 
     @staticmethod
     def backward(ctx, dout):
@@ -1014,15 +1039,18 @@ class _Embed(Function):
         t.gw_epoch = t.arena.grad_epoch       # written (accumulated) this step: see grad_mode
         if d2.is_cuda:
             with _OnWgrad(d2, flat):           # the table may be tied to a projection
-                _T().embedding_backward(d2, flat, t.grad, ctx.scale)
+                _T().embedding_backward(d2, flat, t.grad, ctx.scale, ctx.tm_b)
         else:
             t.grad.index_add_(0, flat, d2.float() * ctx.scale)
         t.grad_ready()
-        return None, None, None, None
+        return None, None, None, None, None, None
 
 
-def embedding(ids: torch.Tensor, table: Param, scale: float = 1.0) -> torch.Tensor:
-    return _Embed.apply(ids, table.arena.token, table, scale)
+def embedding(ids: torch.Tensor, table: Param, scale: float = 1.0, time_major: bool = False,
+              pos: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """table[ids] * scale (+ pos[position], a constant [S][D] table added in
+    the same kernel)."""
+    return _Embed.apply(ids, table.arena.token, table, scale, time_major, pos)
 
 
 # ============================================================ attention
@@ -1179,3 +1207,63 @@ class _Add(Function):
 
 def add(a: torch.Tensor, b: torch.Tensor) -> torch.Tensor:
     return _Add.apply(a, b)
+
+
+# ======================================== last-dim concat and gradient fan-in
+def _rows_ok(*ts) -> bool:
+    return all(t.is_cuda and t.dtype == BF16 and t.size(-1) % 8 == 0 and t.stride(-1) == 1 for t in ts)
+
+
+class _Cat2(Function):
+    """[..., Ca] ++ [..., Cb] -> [..., Ca+Cb] in ONE launch of ours (rows_sum:
+    a copy job per part); the backward hands out the two column slices of
+    the gradient as views (consumers read them at their row pitch)."""
+
+    @staticmethod
+    def forward(ctx, a, b):
+        ctx.ca = a.shape[-1]
+        if _rows_ok(a, b):
+            a, b = a.contiguous(), b.contiguous()
+            out = torch.empty(*a.shape[:-1], a.shape[-1] + b.shape[-1], dtype=BF16, device=a.device)
+            _T().rows_sum([out[..., :ctx.ca], out[..., ctx.ca:]], [a, b], [1, 1])
+            return out
+        return torch.cat([a, b], -1)
+
+    @staticmethod
+    def backward(ctx, dy):
+        return dy[..., :ctx.ca], dy[..., ctx.ca:]
+
+
+def cat2(a: torch.Tensor, b: torch.Tensor) -> torch.Tensor:
+    return _Cat2.apply(a, b)
+
+
+class _Fanout(Function):
+    """x used by n consumers: n aliases whose gradients are summed by ONE
+    launch of ours (rows_sum, up to 4 pitched inputs) instead of autograd's
+    pairwise accumulation adds."""
+
+    @staticmethod
+    def forward(ctx, x, n: int):
+        ctx.n = n
+        return tuple(x.view_as(x) for _ in range(n))
+
+    @staticmethod
+    def backward(ctx, *gs):
+        gs = [g for g in gs if g is not None]
+        if not gs:
+            return None, None
+        if len(gs) == 1:
+            return gs[0], None
+        if len(gs) <= 4 and _rows_ok(*gs):
+            out = torch.empty(gs[0].shape, dtype=BF16, device=gs[0].device)
+            _T().rows_sum([out], gs, [len(gs)])
+            return out, None
+        acc = gs[0].float()
+        for g in gs[1:]:
+            acc = acc + g.float()
+        return acc.to(gs[0].dtype), None
+
+
+def fanout(x: torch.Tensor, n: int) -> Tuple[torch.Tensor, ...]:
+    return _Fanout.apply(x, n)
