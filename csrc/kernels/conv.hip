@@ -293,7 +293,7 @@ __global__ void conv_weight_t_kernel(const bf16_t* __restrict__ w, bf16_t* __res
 // (along c) and the write (along k) are 128-B coalesced rows. Called once per
 // training step after the optimizer's weights are final (model forward).
 __global__ void __launch_bounds__(256) conv_wt_batch_kernel(WTBatch b) {
-  __shared__ bf16_t tile[64][66];
+  __shared__ __attribute__((aligned(16))) bf16_t tile[64][72];
   int e = 0;
   while (e + 1 < b.n && (int)blockIdx.x >= b.e[e + 1].tile0) ++e;
   const WTEntry& en = b.e[e];
@@ -301,6 +301,30 @@ __global__ void __launch_bounds__(256) conv_wt_batch_kernel(WTBatch b) {
   const int local = blockIdx.x - en.tile0;
   const int rs = local / (tk * tc), r2 = local % (tk * tc);
   const int k0 = (r2 / tc) * 64, c0 = (r2 % tc) * 64;
+  if ((en.K & 7) == 0 && (en.C & 7) == 0) {
+    // 16-B vectors both ways: rows of 8 c read, 8 k gathered from an LDS
+    // column and written as one 16-B chunk (144-B LDS rows: the column
+    // gathers of 16 lanes hit 16 different banks)
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+      const int i = threadIdx.x + 256 * u, kk = i >> 3, cv = (i & 7) * 8, k = k0 + kk, c = c0 + cv;
+      uint4 v = make_uint4(0u, 0u, 0u, 0u);
+      if (k < en.K && c < en.C) v = *(const uint4*)(en.w + ((long)k * en.RS + rs) * en.C + c);
+      *(uint4*)&tile[kk][cv] = v;
+    }
+    __syncthreads();
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+      const int i = threadIdx.x + 256 * u, cc = i >> 3, kv = (i & 7) * 8, k = k0 + kv, c = c0 + cc;
+      if (k >= en.K || c >= en.C) continue;
+      uint32_t w4[4];
+#pragma unroll
+      for (int q = 0; q < 4; ++q)
+        w4[q] = (uint32_t)tile[kv + 2 * q][cc] | ((uint32_t)tile[kv + 2 * q + 1][cc] << 16);
+      *(uint4*)(en.wt + ((long)c * en.RS + rs) * en.K + k) = make_uint4(w4[0], w4[1], w4[2], w4[3]);
+    }
+    return;
+  }
   for (int i = threadIdx.x; i < 64 * 64; i += 256) {
     const int kk = i >> 6, cc = i & 63, k = k0 + kk, c = c0 + cc;
     tile[kk][cc] = (k < en.K && c < en.C) ? en.w[((long)k * en.RS + rs) * en.C + c] : (bf16_t)0;

@@ -224,7 +224,11 @@ class _LSTMLayer(Function):
             dx = None
             if ctx.needs_input_grad[0]:
                 dx = torch.empty(T * B, I, dtype=BF16, device=dev)
-                _T().gemm(dG2, True, w_ih.w, False, dx, 0, None, False, None, 1.0, False)
+                wk = Fx.weight_kmajor(w_ih)             # K-major W_ih copy of this step (KK GEMM)
+                if wk is not None:
+                    _T().gemm(dG2, True, wk, True, dx, 0, None, False, None, 1.0, False)
+                else:
+                    _T().gemm(dG2, True, w_ih.w, False, dx, 0, None, False, None, 1.0, False)
                 dx = dx.view(T, B, I)
         else:
             dHf = dH.float().contiguous()          # dh accumulator (fp32), updated in place
@@ -264,6 +268,9 @@ class _LSTMLayer(Function):
             b.grad_ready()
         return dx, None, None, None, None, None, None
 
+
+# TAM_GNMT_KMAJOR=0: input gradients on the KN GEMM, no per-step weight re-lay (A/B)
+KMAJOR_DGRAD = os.environ.get("TAM_GNMT_KMAJOR", "1") != "0"
 
 # TAM_LSTM_PITCHED=0: gather every non-contiguous dH (A/B)
 LSTM_PITCHED_DH = os.environ.get("TAM_LSTM_PITCHED", "1") != "0"
@@ -361,6 +368,10 @@ class GNMT:
         # batch / token strides and the logits come out [T,B,V] with the
         # labels transposed to match (logits_time_major), so no activation
         # or gradient is ever re-laid between the recurrences and attention
+        if src.is_cuda and KMAJOR_DGRAD:
+            # K-major copies of the weights whose input gradient is a KN GEMM
+            # (every W_ih, the classifier), one launch: their dX run as KK
+            Fx.prepare_weight_t([p[0] for p in self.enc + self.dec] + [self.cls_w])
         # the embeddings read the [B,S] ids time-major in place; every tensor
         # with several consumers goes through Fx.fanout (its gradients summed
         # by one launch of ours) and every feature concat through Fx.cat2, so

@@ -327,7 +327,11 @@ class _Linear(Function):
         if ctx.needs_input_grad[0]:
             if dy.is_cuda:
                 dx = torch.empty_like(x)
-                _T().gemm(dy, True, w.w, False, dx, 0, None, False, x if ctx.in_relu else None, 1.0, False)
+                wk = weight_kmajor(w)
+                if wk is not None:
+                    _T().gemm(dy, True, wk, True, dx, 0, None, False, x if ctx.in_relu else None, 1.0, False)
+                else:
+                    _T().gemm(dy, True, w.w, False, dx, 0, None, False, x if ctx.in_relu else None, 1.0, False)
             else:
                 dxf = _cpu_gemm_f32(dy, w.w)
                 if ctx.in_relu:
@@ -506,6 +510,33 @@ def prepare_conv_wt(params: List[Param]) -> None:
             p.wt = torch.empty_like(p.w)
     _T().conv_weight_t_batch([p.w for p in params], [p.wt for p in params])
 
+
+
+def prepare_weight_t(params: List[Param]) -> None:
+    """K-major copies ``p.wk`` [in, out] of 2-D weights [out, in], all in ONE
+    launch (the batched conv-weight re-lay, as 1x1 kernels), for the input
+    gradients dX = dY . W: with W K-major they run on the KK GEMM instead of
+    the slower KN form (GNMT's LSTM input and classifier gradients, e.g.
+    3200 x 2048 x 4096 KN 85 us vs KK 65 us + an 8 us re-lay,
+    profiles/r6/kn_vs_kk.json; GNMT step 9.93-9.97 -> 9.73-9.80 ms). Valid for the current optimizer step only
+    (``p.wk_epoch``); call at the start of the forward. No-op on CPU."""
+    if not params or not params[0].w.is_cuda:
+        return
+    ws, wts = [], []
+    for p in params:
+        O, I = p.shape
+        if getattr(p, "wk", None) is None or p.wk.device != p.w.device:
+            p.wk = torch.empty(I, O, dtype=BF16, device=p.w.device)
+        ws.append(p.w.view(O, 1, 1, I))
+        wts.append(p.wk)
+        p.wk_epoch = p.arena.grad_epoch
+    _T().conv_weight_t_batch(ws, wts)
+
+
+def weight_kmajor(p: Param) -> Optional[torch.Tensor]:
+    """p's K-major copy when prepare_weight_t made one for this step."""
+    wk = getattr(p, "wk", None)
+    return wk if wk is not None and getattr(p, "wk_epoch", None) == p.arena.grad_epoch else None
 
 
 def conv2d(x: torch.Tensor, w: Param, b: Optional[Param] = None, stride: int = 1, pad: int = 0,
