@@ -269,9 +269,6 @@ class _LSTMLayer(Function):
         return dx, None, None, None, None, None, None
 
 
-# TAM_GNMT_KMAJOR=0: input gradients on the KN GEMM, no per-step weight re-lay (A/B)
-KMAJOR_DGRAD = os.environ.get("TAM_GNMT_KMAJOR", "1") != "0"
-
 # TAM_LSTM_PITCHED=0: gather every non-contiguous dH (A/B)
 LSTM_PITCHED_DH = os.environ.get("TAM_LSTM_PITCHED", "1") != "0"
 
@@ -368,7 +365,7 @@ class GNMT:
         # batch / token strides and the logits come out [T,B,V] with the
         # labels transposed to match (logits_time_major), so no activation
         # or gradient is ever re-laid between the recurrences and attention
-        if src.is_cuda and KMAJOR_DGRAD:
+        if src.is_cuda and Fx.KMAJOR_DGRAD:
             # K-major copies of the weights whose input gradient is a KN GEMM
             # (every W_ih, the classifier), one launch: their dX run as KK
             Fx.prepare_weight_t([p[0] for p in self.enc + self.dec] + [self.cls_w])

@@ -512,6 +512,11 @@ def prepare_conv_wt(params: List[Param]) -> None:
 
 
 
+# TAM_KMAJOR_DGRAD=0: the models' input gradients on the KN GEMM, no
+# per-step K-major weight copies (A/B)
+KMAJOR_DGRAD = os.environ.get("TAM_KMAJOR_DGRAD", "1") != "0"
+
+
 def prepare_weight_t(params: List[Param]) -> None:
     """K-major copies ``p.wk`` [in, out] of 2-D weights [out, in], all in ONE
     launch (the batched conv-weight re-lay, as 1x1 kernels), for the input
