@@ -116,14 +116,22 @@ __global__ void __launch_bounds__(256) attn_fwd_kernel(const bf16_t* __restrict_
 
   int kend = klen;
   if (causal) kend = min(kend, q0 + AT);
+  // the next K / V tile is fetched into registers right after the current
+  // one reaches LDS, so its global latency hides under this tile's math
+  uint4 rk[2], rv[2];
+  if (kend > 0) {
+    tile_fetch(Kb, kvs, 0, klen, rk, tid);
+    tile_fetch(Vb, kvs, 0, klen, rv, tid);
+  }
   for (int k0 = 0; k0 < kend; k0 += AT) {
-    uint4 rk[2], rv[2];
-    tile_fetch(Kb, kvs, k0, klen, rk, tid);
-    tile_fetch(Vb, kvs, k0, klen, rv, tid);
     __syncthreads();   // previous tile fully consumed
     tile_store_k(kt, rk, tid, false);
     tile_store_mn(vt, rv, tid, true);
     __syncthreads();
+    if (k0 + AT < kend) {
+      tile_fetch(Kb, kvs, k0 + AT, klen, rk, tid);
+      tile_fetch(Vb, kvs, k0 + AT, klen, rv, tid);
+    }
     // S^T[kv][q] : 4 kv sub-tiles x 2 k-steps
     f32x4_t st[4];
 #pragma unroll
@@ -390,6 +398,21 @@ __global__ void __launch_bounds__(512) attn_bwd_short_kernel(
   const bf16_t* Vb = V + (long)b * kvb + h * AD;
   const float* lse_b = LSE + ((long)b * H + h) * Sq;
 
+  // query tile q0's Q (half 0) / dO, O (half 1) rows and LSE, fetched into
+  // registers one tile AHEAD: the first with the K / V loads below, the next
+  // right after the current one reaches LDS (its latency hides under the math)
+  uint4 ra[2], rb[2];
+  float lse_r = 0.f;
+  auto fetch_q = [&](int q0) {
+    if (half == 0) {
+      tile_fetch(Qb, qs, q0, Sq, ra, ht);
+      if (ht < AT) lse_r = q0 + ht < Sq ? lse_b[q0 + ht] : 0.f;
+    } else {
+      tile_fetch(dOb, os, q0, Sq, ra, ht);
+      tile_fetch(Ob, os, q0, Sq, rb, ht);
+    }
+  };
+  if (Sq > 0) fetch_q(0);
   s16x8_t kf[2], vf[2];
 #pragma unroll
   for (int ks = 0; ks < 2; ++ks) {
@@ -412,25 +435,19 @@ __global__ void __launch_bounds__(512) attn_bwd_short_kernel(
   const float sl2 = scale * kLog2e;
 
   for (int q0 = 0; q0 < Sq; q0 += AT) {
-    // half 0 stages Q, half 1 stages dO and O
-    uint4 ra[2], rb[2];
-    if (half == 0) {
-      tile_fetch(Qb, qs, q0, Sq, ra, ht);
-    } else {
-      tile_fetch(dOb, os, q0, Sq, ra, ht);
-      tile_fetch(Ob, os, q0, Sq, rb, ht);
-    }
+    // half 0 stages Q, half 1 stages dO and O (fetched one tile ahead)
     __syncthreads();   // previous iteration done with all images
     if (half == 0) {
       tile_store_k(q_k, ra, ht, false);
       tile_store_mn(q_mn, ra, ht, true);
-      if (ht < AT) s_lse[ht] = q0 + ht < Sq ? lse_b[q0 + ht] * kLog2e : 0.f;
+      if (ht < AT) s_lse[ht] = lse_r * kLog2e;
     } else {
       tile_store_k(do_k, ra, ht, false);
       tile_store_mn(do_mn, ra, ht, true);
       tile_store_k(o_k, rb, ht, false);
     }
     __syncthreads();
+    if (q0 + AT < Sq) fetch_q(q0 + AT);
     {  // delta[q] = sum_d dO[q][d] O[q][d]: 8 threads per row, 8 d each
       const int row = tid >> 3, c = tid & 7;
       const uint4 a = *(const uint4*)(do_k + kmaj_off(row, c));

@@ -44,10 +44,23 @@ def timeit(fn, iters=20):
     return best
 
 
+# ResNet-50's pointwise convs at batch 64 (M = N x H x W output pixels,
+# short K): forward x W^T (KK) and data gradient dY W (KN), --resnet
+RESNET = [(200704, 256, 64, True), (200704, 64, 256, True), (200704, 64, 64, True),
+          (50176, 512, 128, True), (50176, 128, 512, True), (12544, 1024, 256, True),
+          (12544, 256, 1024, True), (3136, 2048, 512, True), (3136, 512, 2048, True),
+          (200704, 64, 256, False), (200704, 256, 64, False), (50176, 128, 512, False),
+          (12544, 256, 1024, False)]
+
+
 def main():
+    global SHAPES
     ap = argparse.ArgumentParser()
     ap.add_argument("--out", default=None)
+    ap.add_argument("--resnet", action="store_true", help="ResNet-50 pointwise conv shapes")
     a = ap.parse_args()
+    if a.resnet:
+        SHAPES = RESNET
     T = _lib.ops()
     T.gemm_lib_policy(0)
     T.gemm_dma_policy(0, -1)      # no per-shape route timing: each forced config runs as asked
@@ -62,8 +75,8 @@ def main():
         fl = 2.0 * M * N * K
         r = {"shape": f"{M}x{N}x{K} K{'K' if bk else 'N'}"}
         for name, mode, tile, sp in (("igemm", 0, 0, 0), ("p8_128", 2, 128, 0), ("p8_64", 2, 64, 0),
-                                     ("p8_128_slab", 3, 128, 0), ("p8_64_slab2", 3, 64, 2)):
-            if sp and K // 64 < 8 * sp:
+                                     ("p8_256", 2, 256, 0), ("p8_128_slab", 3, 128, 0), ("p8_64_slab2", 3, 64, 2)):
+            if (sp and K // 64 < 8 * sp) or (mode == 3 and K < 1024):
                 continue
             T.gemm8p_policy(mode, tile)
             T.gemm8p_slab_force(sp)
@@ -80,6 +93,7 @@ def main():
         Be = b_.t() if bk else b_
         ms = timeit(lambda: torch.mm(A, Be, out=c))
         r["hipblaslt_us"] = round(ms * 1e3, 2)
+        r["min_bytes_tbps_igemm"] = round((M * K + N * K + M * N) * 2 / (r["igemm_us"] * 1e-6) / 1e12, 2)
         rows.append(r)
         print(json.dumps(r), flush=True)
     if a.out:
