@@ -1721,6 +1721,15 @@ class Worker:
                      any(r.get("error") for r in rep.get("jobs") or [] if r.get("job") == jid))
         if local_bad and not gang:
             return
+        if (os.environ.get("TAM_SHARED_GPU") == "1" and self.world > 1 and hasattr(t.model, "shared")
+                and not getattr(t, "_persist_shared", False)):
+            # one-GPU rehearsal: the next round's plan can start another rank's
+            # persistent LSTM grid while this rank's persistent fill step is
+            # still in flight (the co-location rule only saw the round just
+            # run), so such a job does not fill. The condition is plan-derived
+            # (_persist_shared is set from the plan at apply): every gang
+            # member takes the same branch
+            return
         self._fill = {"job": jid, "left": 0 if local_bad else left, "n": 0, "sec": 0.0, "gang": gang,
                       "done": False, "prev": None, "err": None, "t": t}
 

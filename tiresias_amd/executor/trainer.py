@@ -235,10 +235,10 @@ class Trainer:
         shared = bool(shared)
         if shared != getattr(self, "_persist_shared", False):
             self._persist_shared = shared
-            if hasattr(self.model, "shared"):
+            if hasattr(self.model, "shared"):   # models with persistent grids only
                 self.model.shared = shared
-            self._graph = None
-            self._g_loss = None
+                self._graph = None
+                self._g_loss = None
 
     def persist_skipped(self, reset: bool = True) -> int:
         """Steps of THIS job whose persistent recurrence timed out since the
