@@ -993,6 +993,7 @@ void gemm_dma_policy_op(int64_t p, int64_t cfg) {
 }
 
 void gemm8p_policy_op(int64_t mode, int64_t tile) { tam::gemm8p_policy((int)mode, (int)tile); }
+void gemm_pw_policy_op(int64_t on) { tam::gemm_pw_policy((int)on); }
 
 // every registered tuning knob (common.h TAM_KNOB): names (comma-joined, in
 // registration order), current values, and a bulk restore
@@ -1334,6 +1335,7 @@ TORCH_LIBRARY(tam, m) {
   m.def("colsum(Tensor x, Tensor(a!) out) -> ()", &colsum_op);
   m.def("gemm_force(int cfg, int splits) -> ()", &gemm_force_op);
   m.def("gemm8p_policy(int mode, int tile) -> ()", &gemm8p_policy_op);
+  m.def("gemm_pw_policy(int on) -> ()", &gemm_pw_policy_op);
   m.def("policy_names() -> str", &policy_names_op);
   m.def("policy_state() -> int[]", &policy_state_op);
   m.def("policy_load(int[] v) -> ()", &policy_load_op);

@@ -24,6 +24,14 @@ void gemm_force(int cfg, int splits);   // tuning hook (-1 = heuristic)
 void gemm_dma_policy(int policy, int cfg);   // LDS-DMA GEMM on/off, forced tile cfg (-1 auto)
 // 256^2 all-layout LDS-DMA GEMM: 0 off, 1 auto (big GEMMs), 2 forced where eligible
 void gemm8p_policy(int mode, int tile);   // tile 128 / 256: forced (tests), else auto
+// pointwise-conv GEMM (gemm_pw.hip): C[M][N] = A[M][K] . B[N][K]^T for many
+// pixels (M >= 65536), K, N in {64, 128, 256}, K * N <= 16384; ReLU-backward
+// mask / BN statistics (fp64 [BN_SHARDS][2N]) / relu as in Epi. false: not
+// eligible, nothing launched
+bool gemm_pw(const bf16_t* A, long lda, const bf16_t* B, long ldb, bf16_t* C, long ldc, long M, int N, int K,
+             const bf16_t* mask, long ldm, double* stats, int relu, hipStream_t s);
+bool gemm_pw_ok(long M, int N, int K, long lda, long ldb, long ldc);
+void gemm_pw_policy(int on);   // 0: pointwise convs on the dense GEMM route (A/B)
 void gemm8p_group(int g);   // M-tiles per tile-order group of gemm8p (default 4)
 int gemm8p_policy_mode();
 

@@ -80,6 +80,11 @@ int conv_fwd(const bf16_t* x, const bf16_t* w, const ConvGeom& g, Epi ep, hipStr
              long ws_floats) {
   const int M = g.N * g.P * g.Q, Kd = g.R * g.S * g.C;
   if (conv_stem_fwd(x, w, g, ep, s)) return ep.stats ? 1 : 0;   // 7x7/s2 8->64 stem (conv_stem.hip)
+  // pointwise convs over many pixels (ResNet-50's 56x56 bottleneck 1x1s):
+  // the memory-bound short-K kernel, BN statistics in its epilogue
+  if (is_pointwise(g) && !ep.c_f32 && ep.mode == 0 && !ep.bias && !ep.mask && ep.alpha == 1.f &&
+      gemm_pw(x, g.C, w, g.C, (bf16_t*)ep.c, ep.ldc, M, g.K, g.C, nullptr, 0, ep.stats, ep.relu, s))
+    return ep.stats ? 1 : 0;
   if (g_conv_dma && g.dil == 1) {
     CDArgs a = cd_fwd_args(x, w, g);
     if (g_conv_halo && launch_conv_halo(a, ep, s)) return ep.stats ? 1 : 0;
@@ -162,6 +167,11 @@ int conv_dgrad(const bf16_t* dy, const bf16_t* w, const bf16_t* wt, const ConvGe
     }
   }
   if (is_pointwise(g)) {
+    // many pixels: the short-K kernel on the re-laid Wt [C][K] (K-major B),
+    // ReLU-backward mask in its epilogue
+    if (wt && !ep.c_f32 && ep.mode == 0 && !ep.bias && ep.alpha == 1.f && !ep.relu &&
+        gemm_pw(dy, g.K, wt, g.K, (bf16_t*)ep.c, ep.ldc, M, g.C, g.K, ep.mask, ep.ldm, nullptr, 0, s))
+      return 0;
     // dX[m][c] = sum_k dY[m][k] W[k][c]  -> B(k,n) = W[k*C + c], MN-major
     gemm(dy, g.K, true, w, g.C, false, M, g.C, g.K, ep, false, s);
     return 0;

@@ -931,6 +931,46 @@ def test_batchnorm_relu_bitmask(gpu, res, add, shape):
     assert rel_err(dx0, dx1) < 1e-3 and rel_err(dg0, dg1) < 1e-5 and rel_err(db0, db1) < 1e-5
 
 
+@pytest.mark.parametrize("C,K", [(64, 64), (64, 256), (256, 64), (64, 128), (128, 64)])
+def test_pointwise_conv_kernel(gpu, C, K):
+    """The short-K pointwise-conv GEMM (gemm_pw.hip) on >= 65536 pixels:
+    forward (+ BN statistics of the stored output) and the data gradient on
+    the re-laid weight (+ ReLU-backward mask), each against fp32 torch and
+    against the dense GEMM route with the kernel switched off."""
+    torch.manual_seed(C + K)
+    N, H = 16, 64                                    # 65536 pixels
+    x = torch.randn(N, H, H, C, device=gpu).to(BF)
+    w = (torch.randn(K, 1, 1, C, device=gpu) / C ** 0.5).to(BF)
+    ref = x.float().reshape(-1, C) @ w.float().reshape(K, C).t()
+    from tiresias_amd.ops.functional import BN_SHARDS
+    outs = []
+    for on in (1, 0):
+        T().gemm_pw_policy(on)
+        try:
+            y = torch.empty(N, H, H, K, device=gpu, dtype=BF)
+            sums = torch.zeros(BN_SHARDS * 2 * K, device=gpu, dtype=torch.float64)
+            done = T().conv_fwd(x, w, y, 1, 0, 1, None, False, sums)
+            dy = torch.randn(N, H, H, K, device=gpu).to(BF) if not outs else outs[0][3]
+            mask = torch.randn(N, H, H, C, device=gpu).to(BF) if not outs else outs[0][4]
+            dx = torch.empty(N, H, H, C, device=gpu, dtype=BF)
+            wt = torch.empty_like(w)
+            T().conv_dgrad(dy, w, wt, dx, 1, 0, 1, mask)
+            torch.cuda.synchronize()
+            outs.append((y, done, sums, dy, mask, dx))
+        finally:
+            T().gemm_pw_policy(1)
+    (y1, d1, s1, dy, mask, dx1), (y0, d0, s0, _, _, dx0) = outs
+    assert rel_err(y1.reshape(-1, K), ref) < 1e-2
+    assert torch.equal(y1, y0) or rel_err(y1, y0) < 1e-2
+    assert d1 == 1, "the pointwise kernel computes the BN statistics"
+    yf = y1.double().reshape(-1, K)
+    tot = s1.view(BN_SHARDS, 2 * K).sum(0)
+    assert rel_err(tot[:K], yf.sum(0)) < 1e-5 and rel_err(tot[K:], (yf * yf).sum(0)) < 1e-5
+    dref = (dy.float().reshape(-1, K) @ w.float().reshape(K, C)) * (mask.float().reshape(-1, C) > 0)
+    assert rel_err(dx1, dref.reshape(dx1.shape)) < 1e-2
+    assert rel_err(dx1, dx0) < 1e-2
+
+
 @pytest.mark.parametrize("policy", [1, 3])
 @pytest.mark.parametrize("shape", [(8, 28, 28, 128, 256, 3, 1, 1), (16, 14, 14, 256, 1024, 1, 1, 0),
                                    (4, 56, 56, 64, 64, 3, 1, 1), (8, 28, 28, 256, 512, 1, 2, 0),
