@@ -1019,6 +1019,7 @@ void gemm8p_group_op(int64_t g) { tam::gemm8p_group((int)g); }
 void gemm8p_slab_force_op(int64_t sp) { tam::gemm8p_slab_force((int)sp); }
 void gemm8p_sk_force_op(int64_t on) { g_sk_force = on != 0; }
 void conv_split_policy_op(int64_t p) { tam::conv_split_policy((int)p); }
+void optim_grid_op(int64_t b) { tam::optim_grid((int)b); }
 void optim_variant_op(int64_t v) { tam::optim_variant((int)v); }
 void gemm_skinny_policy_op(int64_t on, int64_t sp, int64_t nst) {
   tam::gemm_skinny_policy((int)on, (int)sp, (int)nst);
@@ -1345,6 +1346,7 @@ TORCH_LIBRARY(tam, m) {
   m.def("gemm8p_sk_force(int on) -> ()", &gemm8p_sk_force_op);
   m.def("conv_split_policy(int p) -> ()", &conv_split_policy_op);
   m.def("optim_variant(int v) -> ()", &optim_variant_op);
+  m.def("optim_grid(int blocks) -> ()", &optim_grid_op);
   m.def("gemm_lib_policy(int policy) -> ()", &gemm_lib_policy_op);
   m.def("conv_dma_policy(int policy) -> ()", &conv_dma_policy_op);
   m.def("conv_wgrad_force(int bm, int bn, int splits, int noatomic=0) -> ()", &conv_wgrad_force_op);

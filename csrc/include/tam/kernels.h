@@ -119,6 +119,7 @@ void add_bf16(const bf16_t* a, const bf16_t* b, bf16_t* y, long n, hipStream_t s
 void cast_f32_bf16(const float* x, bf16_t* y, long n, hipStream_t s);
 
 // optimizers over flat arenas (n % 4 == 0)
+void optim_grid(int blocks);   // grid cap of the optimizer launches (A/B; 0 = one block per CU)
 void sgd_step(float* w, float* g, float* mom, bf16_t* wb, long n, float lr, float momentum,
               float wd, float gscale, int nesterov, int zero_grad, hipStream_t s,
               const unsigned* guard = nullptr, long zero_from = 0, long wd_until = -1);

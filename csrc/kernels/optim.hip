@@ -42,10 +42,10 @@ __global__ void __launch_bounds__(256) sgd_kernel(float* __restrict__ w, float* 
     const float wd = i < wd_until4 ? wd0 : 0.f;
 #pragma unroll
     for (int k = 0; k < 4; ++k) {
-      float d = gp[k] * gscale + wd * wp[k];
-      mp[k] = momentum * mp[k] + d;
-      d = nesterov ? d + momentum * mp[k] : mp[k];
-      wp[k] -= lr * d;
+      float d = __builtin_fmaf(wd, wp[k], gp[k] * gscale);
+      mp[k] = __builtin_fmaf(momentum, mp[k], d);
+      d = nesterov ? __builtin_fmaf(momentum, mp[k], d) : mp[k];
+      wp[k] = __builtin_fmaf(-lr, d, wp[k]);
     }
     ((float4*)w)[i] = wv;
     ((float4*)mom)[i] = mv;
@@ -66,6 +66,7 @@ __global__ void __launch_bounds__(256) adam_kernel(float* __restrict__ w, float*
       if (i >= zero_from4) ((float4*)g)[i] = make_float4(0.f, 0.f, 0.f, 0.f);
     return;
   }
+  const float ib1 = 1.f / bc1, ib2 = 1.f / bc2;
   for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < n4;
        i += (long)gridDim.x * blockDim.x) {
     float4 wv = ((float4*)w)[i], gv = ((float4*)g)[i], mv = ((float4*)m)[i], vv = ((float4*)v)[i];
@@ -74,10 +75,11 @@ __global__ void __launch_bounds__(256) adam_kernel(float* __restrict__ w, float*
 #pragma unroll
     for (int k = 0; k < 4; ++k) {
       const float gr = gp[k] * gscale;
-      mp[k] = b1 * mp[k] + (1.f - b1) * gr;
-      vp[k] = b2 * vp[k] + (1.f - b2) * gr * gr;
-      const float mh = mp[k] / bc1, vh = vp[k] / bc2;
-      wp[k] -= lr * (mh / (sqrtf(vh) + eps) + wd * wp[k]);   // decoupled (AdamW)
+      mp[k] = __builtin_fmaf(b1, mp[k], (1.f - b1) * gr);
+      vp[k] = __builtin_fmaf(b2, vp[k], (1.f - b2) * gr * gr);
+      const float mh = mp[k] * ib1, vh = vp[k] * ib2;
+      const float u = __builtin_fmaf(wd, wp[k], mh / (sqrtf(vh) + eps));   // decoupled (AdamW)
+      wp[k] = __builtin_fmaf(-lr, u, wp[k]);
     }
     ((float4*)w)[i] = wv; ((float4*)m)[i] = mv; ((float4*)v)[i] = vv;
     if (zero_grad && i >= zero_from4) ((float4*)g)[i] = make_float4(0.f, 0.f, 0.f, 0.f);
@@ -85,6 +87,11 @@ __global__ void __launch_bounds__(256) adam_kernel(float* __restrict__ w, float*
   }
 }
 
+// Every form spells its arithmetic as explicit FMAs: the element update is
+// then one fixed rounding sequence whichever path (kernel, unrolled group or
+// tail) covers the element, so a step is bitwise independent of the grid,
+// the variant and how an arena is split into launches (contraction was left
+// to the compiler before and differed between the unrolled and tail bodies).
 // Streaming variants (optim_variant): U float4 groups per thread per
 // iteration, all loads issued before any math (U x 4 x 16 B in flight per
 // lane), NT: non-temporal loads / stores (every byte is touched once per
@@ -131,10 +138,11 @@ __global__ void __launch_bounds__(256) adam_stream_kernel(float* __restrict__ w,
 #pragma unroll
     for (int k = 0; k < 4; ++k) {
       const float gr = gp[k] * gscale;
-      mp[k] = b1 * mp[k] + (1.f - b1) * gr;
-      vp[k] = b2 * vp[k] + (1.f - b2) * gr * gr;
+      mp[k] = __builtin_fmaf(b1, mp[k], (1.f - b1) * gr);
+      vp[k] = __builtin_fmaf(b2, vp[k], (1.f - b2) * gr * gr);
       const float mh = mp[k] * ib1, vh = vp[k] * ib2;
-      wp[k] -= lr * (mh / (sqrtf(vh) + eps) + wd * wp[k]);   // decoupled (AdamW)
+      const float u = __builtin_fmaf(wd, wp[k], mh / (sqrtf(vh) + eps));   // decoupled (AdamW)
+      wp[k] = __builtin_fmaf(-lr, u, wp[k]);
     }
     st4<NT>(w, i, wv); st4<NT>(m, i, mv); st4<NT>(v, i, vv);
     if (zero_grad && i >= zero_from4) st4<NT>(g, i, make_float4(0.f, 0.f, 0.f, 0.f));
@@ -173,10 +181,10 @@ __global__ void __launch_bounds__(256) sgd_stream_kernel(float* __restrict__ w, 
     const float wd = i < wd_until4 ? wd0 : 0.f;
 #pragma unroll
     for (int k = 0; k < 4; ++k) {
-      float d = gp[k] * gscale + wd * wp[k];
-      mp[k] = momentum * mp[k] + d;
-      d = nesterov ? d + momentum * mp[k] : mp[k];
-      wp[k] -= lr * d;
+      float d = __builtin_fmaf(wd, wp[k], gp[k] * gscale);
+      mp[k] = __builtin_fmaf(momentum, mp[k], d);
+      d = nesterov ? __builtin_fmaf(momentum, mp[k], d) : mp[k];
+      wp[k] = __builtin_fmaf(-lr, d, wp[k]);
     }
     st4<NT>(w, i, wv); st4<NT>(mom, i, mv);
     if (zero_grad && i >= zero_from4) st4<NT>(g, i, make_float4(0.f, 0.f, 0.f, 0.f));
@@ -199,28 +207,50 @@ __global__ void __launch_bounds__(256) sgd_stream_kernel(float* __restrict__ w, 
 
 // 0: adam_kernel / sgd_kernel (one group per thread per iteration); 3: U=4
 // + NT (1 / 2, U=2 with / without NT, measured between the two and were
-// dropped); -1 (default): optim_pick -- isolated: VGG-16's
-// 138M-param SGD step 868 -> 743 us, GNMT's 227M Adam 1.73 -> 1.67 ms, the
-// 26M / 61M arrays equal or slower with the streaming forms
-// (tools/bench_optim.py, profiles/r4/optim_variants.json)
+// dropped). -1 (default): optim_pick.
 static int g_optim_variant = [] {
   const char* e = getenv("TAM_OPTIM_VARIANT");   // A/B runs
   return e ? atoi(e) : -1;
 }();
 TAM_KNOB(g_optim_variant)
 void optim_variant(int v) { g_optim_variant = v; }
-// auto: SGD on >= 64M params takes the streaming form (VGG-16 graph step
-// 6.94 -> 6.88 ms); Adam stays on the baseline kernel -- its isolated gain
-// (GNMT 1.73 -> 1.67 ms) did not survive inside the graph step (10.20 vs
-// 10.23 ms, two A/B rounds, profiles/r4/optim_variants_step_ab.log)
-static int optim_pick(long n4, bool adam) {
-  if (g_optim_variant >= 0) return g_optim_variant;
-  return (!adam && n4 >= (16L << 20)) ? 3 : 0;
+// auto: the streaming form for every arena, launched at ONE block per CU
+// (ogrid). Rounds 4-5 ran it on a 4096-block grid, where its isolated gain
+// on Adam did not survive inside the graph step; at one block per CU each
+// CU keeps 4 waves x 16 float4 loads in flight on a single arena stream
+// (fewer open DRAM pages than 16 blocks interleaving), and it wins both
+// isolated and in the step. Same box (tools/bench_optim.py,
+// profiles/r6/optim_grid.md):
+//   isolated, us (v0 @4096 -> v3 @256): GNMT Adam 1593 -> 1393,
+//   Transformer Adam 382 -> 327, VGG-16 SGD 795 -> 627, ResNet-50 SGD 120 -> 108;
+//   graph step, ms: GNMT 9.73-9.75 -> 9.41-9.48, Transformer 4.95-4.96 ->
+//   4.90-4.91, VGG-16 6.57-6.60 -> 6.47, ResNet-50 equal.
+static int optim_pick(long, bool) {
+  return g_optim_variant >= 0 ? g_optim_variant : 3;
 }
 
+// grid cap of the optimizer launches (blocks of 256; each thread strides
+// over the arena); 0 (default): one block per CU. TAM_OPTIM_GRID /
+// optim_grid(): A/B of the cap. Partial waves of blocks (1.5 per CU) measured
+// 10-15 % slower than whole multiples.
+static int g_optim_grid = [] {
+  const char* e = getenv("TAM_OPTIM_GRID");
+  return e ? atoi(e) : 0;
+}();
+TAM_KNOB(g_optim_grid)
+void optim_grid(int blocks) { g_optim_grid = blocks > 0 ? blocks : 0; }
+
 static int ogrid(long n4) {
+  static int cus = 0;
+  if (!cus) {
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess ||
+        hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus < 1)
+      cus = 256;
+  }
+  const long cap = g_optim_grid > 0 ? g_optim_grid : cus;
   long b = (n4 + 255) / 256;
-  if (b > 4096) b = 4096;
+  if (b > cap) b = cap;
   return (int)(b < 1 ? 1 : b);
 }
 

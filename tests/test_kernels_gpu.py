@@ -1244,17 +1244,21 @@ def test_relu_backward(gpu, n):
 
 
 # ------------------------------------------------------------------ optimizers
+@pytest.mark.parametrize("grid", [0, 4096])
 @pytest.mark.parametrize("variant", [0, 3])
 @pytest.mark.parametrize("n", [4096 + 64, 9 * 2 ** 20 + 64])
-def test_sgd_adam(gpu, n, variant):
-    """Small n: one pass of the grid; 9M+64: grid-stride loop (the grid is
-    capped at 1M float4 groups) with a partial last pass; every streaming
-    variant (optim.hip optim_variant: unrolled, non-temporal)."""
+def test_sgd_adam(gpu, n, variant, grid):
+    """Small n: one pass of the grid; 9M+64: grid-stride loop with a partial
+    last pass (the tail the unrolled form runs at U = 1); every streaming
+    variant (optim.hip optim_variant: unrolled, non-temporal) at the default
+    one-block-per-CU grid and at the old 4096-block cap."""
     T().optim_variant(variant)
+    T().optim_grid(grid)
     try:
         _sgd_adam_check(gpu, n)
     finally:
         T().optim_variant(-1)
+        T().optim_grid(0)
 
 
 def _sgd_adam_check(gpu, n):
@@ -1316,6 +1320,35 @@ def test_optimizer_region_bounds_equal_per_region_launches(gpu, variant):
             assert torch.count_nonzero(one[1][:zf]) == zf and torch.count_nonzero(one[1][zf:]) == 0
     finally:
         T().optim_variant(-1)
+
+
+def test_optimizer_bitwise_independent_of_variant_and_grid(gpu):
+    """The element update is spelled as explicit FMAs (optim.hip), so the
+    baseline and streaming forms, at any grid cap, produce the same bits --
+    elements covered by the unrolled groups and by the tail included."""
+    torch.manual_seed(15)
+    n = 3 * 2 ** 20 + 4 * 1000
+    base = [torch.randn(n, device=gpu) for _ in range(4)]
+    base[3].abs_()
+    outs = {}
+    try:
+        for variant in (0, 3):
+            for grid in (0, 256 * 3, 4096):
+                T().optim_variant(variant)
+                T().optim_grid(grid)
+                s = [t.clone() for t in base] + [torch.empty(n, device=gpu, dtype=BF)]
+                T().adam_step(s[0], s[1], s[2], s[3], s[4], 1e-3, 0.9, 0.98, 1e-9, 1e-2, 3, 0.5, True,
+                              None, 64 * 100, n - 64 * 100)
+                q = [t.clone() for t in base[:3]] + [torch.empty(n, device=gpu, dtype=BF)]
+                T().sgd_step(q[0], q[1], q[2], q[3], 0.1, 0.9, 1e-2, 0.5, True, True)
+                outs[(variant, grid)] = s + q
+    finally:
+        T().optim_variant(-1)
+        T().optim_grid(0)
+    ref = outs[(0, 4096)]
+    for k, o in outs.items():
+        for a, b in zip(o, ref):
+            assert torch.equal(a, b), k
 
 
 # ------------------------------------------------------------------ attention
