@@ -1,7 +1,7 @@
 """Per-model GEMM budget: record every tam.gemm call one eager training step
 of a model makes (shape, operand majorities, output dtype, epilogue, split),
 then time each distinct call in isolation through each available path —
-the LDS-DMA GEMM, the igemm/gemm256 kernels, hipBLASLt (library route) — and
+the shipped routing (our kernels) and hipBLASLt for reference — and
 print the per-step cost of each shape x calls. Used to decide the plain-GEMM
 routing policy from measurements instead of guesses.
 
@@ -30,7 +30,7 @@ class _Recorder:
     def __getattr__(self, name):
         return getattr(self.real, name)
 
-    def gemm(self, a, ak, b, bk, c, mode, bias, relu, mask, alpha, allow_split):
+    def gemm(self, a, ak, b, bk, c, mode, bias, relu, mask, alpha, allow_split, colsum=None):
         M, N = c.shape[-2] if c.dim() > 1 else 1, c.shape[-1]
         M = c.numel() // N
         K = a.shape[-1] if ak else a.shape[0]
@@ -41,7 +41,7 @@ class _Recorder:
             self.example[key] = (a.detach().clone(), b.detach().clone(), c.detach().clone(),
                                  None if bias is None else bias.detach().clone(),
                                  None if mask is None else mask.detach().clone())
-        return self.real.gemm(a, ak, b, bk, c, mode, bias, relu, mask, alpha, allow_split)
+        return self.real.gemm(a, ak, b, bk, c, mode, bias, relu, mask, alpha, allow_split, colsum)
 
 
 def _time(fn, iters=20):
@@ -84,21 +84,21 @@ def main():
             M, N, K, ak, bk, dt, mode, has_b, relu, has_m, split = key
             A, B, C, bias, mask = rec.example[key]
             res = {}
-            for path, (lib, dma) in {"dma": (0, 2), "igemm": (0, 0), "lib": (1, 0)}.items():
+            # "route": the shipped routing (production default, library off);
+            # "lib": hipBLASLt on the same layouts, for reference only
+            for path, lib in {"route": 0, "lib": 1}.items():
                 if path == "lib" and (relu or has_m):
                     continue
                 T.gemm_lib_policy(lib)
-                T.gemm_dma_policy(dma, -1)
                 cc = C.clone()
                 res[path] = _time(lambda: T.gemm(A, ak, B, bk, cc, mode, bias, relu, mask, 1.0, split))
-            T.gemm_lib_policy(-1)
-            T.gemm_dma_policy(1, -1)
+            T.gemm_lib_policy(0)
             best = min(res, key=res.get)
             rows.append(dict(M=M, N=N, K=K, layout=("K" if ak else "M") + ("K" if bk else "N"),
                              out=dt, mode=mode, bias=has_b, relu=relu, mask=has_m, split=split,
                              calls=n, us=res, best=best, step_us={p: v * n for p, v in res.items()}))
         rows.sort(key=lambda r: -min(r["step_us"].values()))
-        tot = {p: sum(r["step_us"].get(p, r["step_us"]["dma"]) for r in rows) for p in ("dma", "igemm", "lib")}
+        tot = {p: sum(r["step_us"].get(p, r["step_us"]["route"]) for r in rows) for p in ("route", "lib")}
         tot["best"] = sum(min(r["step_us"].values()) for r in rows)
         print(f"== {m}: per-step GEMM us by path {json.dumps({k: round(v) for k, v in tot.items()})}")
         for r in rows:
