@@ -706,6 +706,7 @@ def _fill_gang_worker(rank, world, port, q):
     wts = [torch.zeros_like(t.arena.master) for _ in range(world)]
     dist.all_gather(wts, t.arena.master)
     q.put((rank, counts, all(torch.equal(wts[0], x) for x in wts)))
+    dist.barrier()              # no member tears the store / gloo pairs down under a peer
     dist.destroy_process_group()
 
 
