@@ -1099,6 +1099,41 @@ def test_maxpool(gpu, C, hw):
     assert torch.equal(dx, dx0)
 
 
+@pytest.mark.parametrize("C,st,hw", [(64, 2, (12, 16)), (128, 2, (8, 6)), (16, 3, (9, 12))])
+def test_maxpool_window_equals_stride(gpu, C, st, hw):
+    """Non-overlapping max pool (VGG-16's 2x2 / s2) on the shift-and-mask
+    kernels vs torch, and equal to the generic 8-channel kernels (policy 0):
+    the same max, the same tap on ties, the same input gradient."""
+    torch.manual_seed(8)
+    H, W = hw
+    x = torch.randn(3, H, W, C, device=gpu).to(BF)
+    x[0, :st, :st, :4] = 1.0                        # ties inside one window
+    P, Q = H // st, W // st
+    y = torch.empty(3, P, Q, C, device=gpu, dtype=BF)
+    idx = torch.empty(3, P, Q, C, device=gpu, dtype=torch.uint8)
+    T().maxpool_forward(x, y, idx, st, st, st, 0)
+    xf = x.float().permute(0, 3, 1, 2).requires_grad_(True)
+    yf = F.max_pool2d(xf, st, st, 0)
+    assert torch.equal(y.float(), yf.permute(0, 2, 3, 1))
+    dy = torch.randn_like(y)
+    dx = torch.empty_like(x)
+    T().maxpool_backward(dy, idx, dx, st, st, st, 0)
+    y0, idx0, dx0 = torch.empty_like(y), torch.empty_like(idx), torch.empty_like(x)
+    T().maxpool_k3s2_policy(0)
+    try:
+        T().maxpool_forward(x, y0, idx0, st, st, st, 0)
+        T().maxpool_backward(dy, idx0, dx0, st, st, st, 0)
+    finally:
+        T().maxpool_k3s2_policy(1)
+    assert torch.equal(y, y0) and torch.equal(idx, idx0) and torch.equal(dx, dx0)
+    # torch routes a tied window's gradient to one of the maxima; ours to the
+    # first in scan order, so compare away from the planted ties
+    g, = torch.autograd.grad(yf, [xf], dy.float().permute(0, 3, 1, 2))
+    keep = torch.ones_like(dx, dtype=torch.bool)
+    keep[0, :st, :st, :4] = False
+    assert rel_err(dx[keep], g.permute(0, 2, 3, 1)[keep]) < 1e-2
+
+
 def test_avgpool(gpu):
     x = torch.randn(4, 7, 7, 64, device=gpu).to(BF)
     y = torch.empty(4, 64, device=gpu, dtype=BF)
