@@ -161,6 +161,28 @@ struct ConvGeom {
   int stride, pad, dil;
 };
 
+// floor(n / d) for 0 <= n < 2^31 by a multiply-high (Granlund-Montgomery,
+// N = 31: mul = ceil(2^(31 + l) / d) < 2^32, l = ceil(log2 d)), built on the
+// host once per launch. The im2col loaders below decode a pixel or a (tap,
+// channel) index for EVERY 16-B load; with runtime '/' and '%' that was ~20
+// VALU per division, four to six divisions per load (PMC: 22-24 VALU per
+// MFMA in the gather igemm, VALU utilisation 0.5-1.0)
+struct FastDiv {
+  uint32_t d = 1, mul = 0;
+  int sh = 0;
+  FastDiv() = default;
+  explicit FastDiv(int dv) : d(dv < 1 ? 1u : (uint32_t)dv) {
+    if (d == 1) return;
+    int l = 0;
+    while ((1u << l) < d) ++l;                     // d >= 2: l >= 1
+    mul = (uint32_t)(((1ull << (31 + l)) + d - 1) / d);
+    sh = l - 1;
+  }
+  __device__ __forceinline__ int div(int n) const {
+    return d == 1 ? n : (int)(__umulhi((uint32_t)n, mul) >> sh);
+  }
+};
+
 // conv fwd A operand: rows = output pixels (n,p,q), k = (r,s,c) c fastest.
 // K-major gather from X (requires C % 8 == 0).
 template <int ROWS>
@@ -168,7 +190,9 @@ struct LdConvFwdA {
   static constexpr bool kKMajor = true;
   static constexpr int P_ = ROWS / 32;
   const bf16_t* x; ConvGeom g; int M; int Kdim;
+  FastDiv fc, fs;      // by C, by S (host: with_divs)
   int nb[P_], h0[P_], w0[P_];
+  LdConvFwdA& with_divs() { fc = FastDiv(g.C); fs = FastDiv(g.S); return *this; }
   __device__ void init(int row0, int tid) {
 #pragma unroll
     for (int i = 0; i < P_; ++i) {
@@ -183,7 +207,7 @@ struct LdConvFwdA {
   }
   __device__ uint4 load(int i, int k) const {
     if (nb[i] < 0 || k >= Kdim) return make_uint4(0, 0, 0, 0);
-    int c = k % g.C; int rs = k / g.C; int s = rs % g.S; int r = rs / g.S;
+    const int rs = fc.div(k), c = k - rs * g.C, r = fs.div(rs), s = rs - r * g.S;
     int h = h0[i] + r * g.dil, w = w0[i] + s * g.dil;
     if ((unsigned)h >= (unsigned)g.H || (unsigned)w >= (unsigned)g.W) return make_uint4(0, 0, 0, 0);
     return ld16(x + (((long)nb[i] * g.H + h) * g.W + w) * g.C + c);
@@ -198,7 +222,9 @@ struct LdConvDgradA {
   static constexpr bool kKMajor = true;
   static constexpr int P_ = ROWS / 32;
   const bf16_t* dy; ConvGeom g; int M; int Kdim;
+  FastDiv fk, fs, fst;   // by K, by S, by stride (host: with_divs)
   int nb[P_], hh[P_], ww[P_];
+  LdConvDgradA& with_divs() { fk = FastDiv(g.K); fs = FastDiv(g.S); fst = FastDiv(g.stride); return *this; }
   __device__ void init(int row0, int tid) {
 #pragma unroll
     for (int i = 0; i < P_; ++i) {
@@ -213,10 +239,10 @@ struct LdConvDgradA {
   }
   __device__ uint4 load(int i, int k) const {
     if (nb[i] < 0 || k >= Kdim) return make_uint4(0, 0, 0, 0);
-    int ko = k % g.K; int rs = k / g.K; int s = rs % g.S; int r = rs / g.S;
+    const int rs = fk.div(k), ko = k - rs * g.K, r = fs.div(rs), s = rs - r * g.S;
     int pn = hh[i] - r * g.dil, qn = ww[i] - s * g.dil;
     if (pn < 0 || qn < 0) return make_uint4(0, 0, 0, 0);
-    int pp = pn / g.stride, qq = qn / g.stride;
+    int pp = fst.div(pn), qq = fst.div(qn);
     if (pp * g.stride != pn || qq * g.stride != qn || pp >= g.P || qq >= g.Q)
       return make_uint4(0, 0, 0, 0);
     return ld16(dy + (((long)nb[i] * g.P + pp) * g.Q + qq) * g.K + ko);
@@ -229,7 +255,9 @@ template <int COLS>
 struct LdConvWgradB {
   static constexpr bool kKMajor = false;
   const bf16_t* x; ConvGeom g; int Mred; int Ncols;
+  FastDiv fq, fp;      // by Q, by P (host: with_divs)
   int cr, cs, cc; bool cv;
+  LdConvWgradB& with_divs() { fq = FastDiv(g.Q); fp = FastDiv(g.P); return *this; }
   __device__ void init(int col0, int tid) {
     int col = col0 + (tid % (COLS / 8)) * 8;
     cv = col < Ncols;
@@ -238,7 +266,7 @@ struct LdConvWgradB {
   }
   __device__ uint4 load(int, int m) const {
     if (!cv || m >= Mred) return make_uint4(0, 0, 0, 0);
-    int q = m % g.Q; int t = m / g.Q; int pp = t % g.P; int n = t / g.P;
+    const int t = fq.div(m), q = m - t * g.Q, n = fp.div(t), pp = t - n * g.P;
     int h = pp * g.stride - g.pad + cr * g.dil, w = q * g.stride - g.pad + cs * g.dil;
     if ((unsigned)h >= (unsigned)g.H || (unsigned)w >= (unsigned)g.W) return make_uint4(0, 0, 0, 0);
     return ld16(x + (((long)n * g.H + h) * g.W + w) * g.C + cc);

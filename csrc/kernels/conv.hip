@@ -47,6 +47,7 @@ static void fwd_tile(const bf16_t* x, const bf16_t* w, const ConvGeom& g, const 
                      hipStream_t s) {
   const int M = g.N * g.P * g.Q, Kd = g.R * g.S * g.C;
   LdConvFwdA<BM> la{x, g, M, Kd};
+  la.with_divs();
   LdKMajor<BN> lb{w, Kd, g.K, Kd};
   launch_igemm<BM, BN>(la, lb, M, g.K, Kd, ep, sp, s);
 }
@@ -113,6 +114,7 @@ static void dgrad_tile(const bf16_t* dy, const bf16_t* wt, const ConvGeom& g, co
                        hipStream_t s) {
   const int M = g.N * g.H * g.W, Kd = g.R * g.S * g.K;
   LdConvDgradA<BM> la{dy, g, M, Kd};
+  la.with_divs();
   LdKMajor<BN> lb{wt, Kd, g.C, Kd};
   launch_igemm<BM, BN>(la, lb, M, g.C, Kd, ep, 1, s);
 }
@@ -192,6 +194,7 @@ static void wgrad_tile(const bf16_t* dy, const bf16_t* x, const ConvGeom& g, con
   const int Mred = g.N * g.P * g.Q, Nc = g.R * g.S * g.C;
   LdMNMajor<BM> la{dy, g.K, g.K, Mred};
   LdConvWgradB<BN> lb{x, g, Mred, Nc};
+  lb.with_divs();
   launch_igemm<BM, BN>(la, lb, g.K, Nc, Mred, ep, sp, s);
 }
 
