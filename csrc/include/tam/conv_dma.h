@@ -57,11 +57,21 @@ struct CDArgs {
   int tap_dh[9], tap_dw[9], tap_kcol[9];
   // output row map (omap != 0): row (n,p,q) -> pixel (n, p*osh+ooh, q*osw+oow) of oH x oW
   int omap, oH, oW, osh, osw, ooh, oow;
+  // multiply-high dividers by Q, P and Cs / 64 (the row decode of the
+  // prologue and the strided-dgrad epilogue, the tap of each K-tile): set by
+  // the argument builders (cd_divs), never left at their defaults
+  FastDiv fq, fp, fct;
 };
+
+inline void cd_divs(CDArgs& a) {
+  a.fq = FastDiv(a.Q);
+  a.fp = FastDiv(a.P);
+  a.fct = FastDiv(a.Cs / 64 > 0 ? a.Cs / 64 : 1);
+}
 
 __device__ __forceinline__ long cd_out_row(const CDArgs& a, int m) {
   if (!a.omap) return m;
-  const int q = m % a.Q, t = m / a.Q, p = t % a.P, n = t / a.P;
+  const int t = a.fq.div(m), q = m - t * a.Q, n = a.fp.div(t), p = t - n * a.P;
   return ((long)n * a.oH + p * a.osh + a.ooh) * a.oW + q * a.osw + a.oow;
 }
 
@@ -287,7 +297,7 @@ __device__ __forceinline__ void conv_dma_body(const CDArgs& a, const Epi& ep, co
     const int c = (lane & 7) ^ ((rr >> 1) & 7);
     const int m = m0 + rr;
     if (m < a.M) {
-      const int q = m % a.Q, t = m / a.Q, p = t % a.P, n = t / a.P;
+      const int t = a.fq.div(m), q = m - t * a.Q, n = a.fp.div(t), p = t - n * a.P;
       const int hb = p * a.stride + a.base_h;
       const int wb = q * a.stride + a.base_w;
       ah[j] = hb;
@@ -315,7 +325,7 @@ __device__ __forceinline__ void conv_dma_body(const CDArgs& a, const Epi& ep, co
     char* sa = smem + st * STAGE;
     char* sb = sa + A_BYTES;
     const int kt = kt_lo + t;
-    const int ct = kt % ctiles, tp = kt / ctiles;
+    const int tp = a.fct.div(kt), ct = kt - tp * ctiles;
     const int dh = a.tap_dh[tp], dw = a.tap_dw[tp];
     const int toff = (dh * a.Ws + dw) * a.Cs + ct * BK;
     const int kcol = a.tap_kcol[tp] + ct * BK;
@@ -846,12 +856,13 @@ inline CDArgs cd_fwd_args(const bf16_t* x, const bf16_t* w, const ConvGeom& g) {
   a.stride = g.stride; a.base_h = -g.pad; a.base_w = -g.pad;
   a.ldb = (long)g.R * g.S * g.C;
   a.ntaps = g.R * g.S;
-  if (a.ntaps > 9) { a.ntaps = 0; return a; }
+  if (a.ntaps > 9) { a.ntaps = 0; cd_divs(a); return a; }
   for (int r = 0; r < g.R; ++r)
     for (int q = 0; q < g.S; ++q) {
       const int t = r * g.S + q;
       a.tap_dh[t] = r; a.tap_dw[t] = q; a.tap_kcol[t] = t * g.C;
     }
+  cd_divs(a);
   return a;
 }
 
@@ -874,7 +885,7 @@ inline CDArgs cd_dgrad_args(const bf16_t* dy, const bf16_t* wt, const ConvGeom& 
     if (((ph + g.pad - r) % st + st) % st) continue;
     for (int q = 0; q < g.S; ++q) {
       if (((pw + g.pad - q) % st + st) % st) continue;
-      if (n == 9) { a.ntaps = 0; return a; }
+      if (n == 9) { a.ntaps = 0; cd_divs(a); return a; }
       a.tap_dh[n] = (ph + g.pad - r) / st;
       a.tap_dw[n] = (pw + g.pad - q) / st;
       a.tap_kcol[n] = (r * g.S + q) * g.K;
@@ -883,6 +894,7 @@ inline CDArgs cd_dgrad_args(const bf16_t* dy, const bf16_t* wt, const ConvGeom& 
   }
   a.ntaps = n;
   a.Kd = n * g.K;
+  cd_divs(a);
   return a;
 }
 
