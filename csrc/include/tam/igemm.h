@@ -117,6 +117,9 @@ __device__ __forceinline__ uint4 ld16(const bf16_t* p) { return *(const uint4*)p
 //   p*256/CPR computed by the kernel), column chunk (t%CPR)*8.
 // ---------------------------------------------------------------------------
 
+// 16 zero bytes: the source of out-of-range loads (zero-initialised)
+static __device__ __attribute__((aligned(16))) uint4 g_ig_zero[1];
+
 // Dense K-major: elem(row, k) = p[row*ld + k]
 template <int ROWS>
 struct LdKMajor {
@@ -132,9 +135,12 @@ struct LdKMajor {
       rp[i] = p + (long)(rv[i] ? r : 0) * ld;
     }
   }
+  // unpredicated: an out-of-range element reads 16 zero bytes of g_ig_zero
+  // (an address select BEFORE the load, no select on its data), so the load
+  // issues with no exec-mask branch around it and nothing waits on it early
   __device__ uint4 load(int i, int k) const {
-    if (rv[i] && k < K) return ld16(rp[i] + k);
-    return make_uint4(0, 0, 0, 0);
+    const bool ok = rv[i] && k < K;
+    return ld16(ok ? rp[i] + k : (const bf16_t*)g_ig_zero);
   }
 };
 
@@ -148,9 +154,9 @@ struct LdMNMajor {
     col = col0 + (tid % (COLS / 8)) * 8;
     cv = col < cols;
   }
-  __device__ uint4 load(int, int k) const {
-    if (cv && k < K) return ld16(p + (long)k * ld + col);
-    return make_uint4(0, 0, 0, 0);
+  __device__ uint4 load(int, int k) const {     // unpredicated, as LdKMajor
+    const bool ok = cv && k < K;
+    return ld16(ok ? p + (long)k * ld + col : (const bf16_t*)g_ig_zero);
   }
 };
 
