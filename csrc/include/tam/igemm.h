@@ -211,12 +211,11 @@ struct LdConvFwdA {
       }
     }
   }
-  __device__ uint4 load(int i, int k) const {
-    if (nb[i] < 0 || k >= Kdim) return make_uint4(0, 0, 0, 0);
+  __device__ uint4 load(int i, int k) const {   // unpredicated (zero page), as LdKMajor
     const int rs = fc.div(k), c = k - rs * g.C, r = fs.div(rs), s = rs - r * g.S;
-    int h = h0[i] + r * g.dil, w = w0[i] + s * g.dil;
-    if ((unsigned)h >= (unsigned)g.H || (unsigned)w >= (unsigned)g.W) return make_uint4(0, 0, 0, 0);
-    return ld16(x + (((long)nb[i] * g.H + h) * g.W + w) * g.C + c);
+    const int h = h0[i] + r * g.dil, w = w0[i] + s * g.dil;
+    const bool ok = nb[i] >= 0 && k < Kdim && (unsigned)h < (unsigned)g.H && (unsigned)w < (unsigned)g.W;
+    return ld16(ok ? x + (((long)nb[i] * g.H + h) * g.W + w) * g.C + c : (const bf16_t*)g_ig_zero);
   }
 };
 
@@ -243,15 +242,13 @@ struct LdConvDgradA {
       }
     }
   }
-  __device__ uint4 load(int i, int k) const {
-    if (nb[i] < 0 || k >= Kdim) return make_uint4(0, 0, 0, 0);
+  __device__ uint4 load(int i, int k) const {   // unpredicated (zero page), as LdKMajor
     const int rs = fk.div(k), ko = k - rs * g.K, r = fs.div(rs), s = rs - r * g.S;
-    int pn = hh[i] - r * g.dil, qn = ww[i] - s * g.dil;
-    if (pn < 0 || qn < 0) return make_uint4(0, 0, 0, 0);
-    int pp = fst.div(pn), qq = fst.div(qn);
-    if (pp * g.stride != pn || qq * g.stride != qn || pp >= g.P || qq >= g.Q)
-      return make_uint4(0, 0, 0, 0);
-    return ld16(dy + (((long)nb[i] * g.P + pp) * g.Q + qq) * g.K + ko);
+    const int pn = hh[i] - r * g.dil, qn = ww[i] - s * g.dil;
+    const int pp = fst.div(pn < 0 ? 0 : pn), qq = fst.div(qn < 0 ? 0 : qn);
+    const bool ok = nb[i] >= 0 && k < Kdim && pn >= 0 && qn >= 0 && pp * g.stride == pn &&
+                    qq * g.stride == qn && pp < g.P && qq < g.Q;
+    return ld16(ok ? dy + (((long)nb[i] * g.P + pp) * g.Q + qq) * g.K + ko : (const bf16_t*)g_ig_zero);
   }
 };
 
@@ -270,12 +267,11 @@ struct LdConvWgradB {
     int c = col % g.C; int rs = col / g.C;
     cc = c; cs = rs % g.S; cr = rs / g.S;
   }
-  __device__ uint4 load(int, int m) const {
-    if (!cv || m >= Mred) return make_uint4(0, 0, 0, 0);
+  __device__ uint4 load(int, int m) const {    // unpredicated (zero page), as LdKMajor
     const int t = fq.div(m), q = m - t * g.Q, n = fp.div(t), pp = t - n * g.P;
-    int h = pp * g.stride - g.pad + cr * g.dil, w = q * g.stride - g.pad + cs * g.dil;
-    if ((unsigned)h >= (unsigned)g.H || (unsigned)w >= (unsigned)g.W) return make_uint4(0, 0, 0, 0);
-    return ld16(x + (((long)n * g.H + h) * g.W + w) * g.C + cc);
+    const int h = pp * g.stride - g.pad + cr * g.dil, w = q * g.stride - g.pad + cs * g.dil;
+    const bool ok = cv && m < Mred && (unsigned)h < (unsigned)g.H && (unsigned)w < (unsigned)g.W;
+    return ld16(ok ? x + (((long)n * g.H + h) * g.W + w) * g.C + cc : (const bf16_t*)g_ig_zero);
   }
 };
 
