@@ -347,22 +347,35 @@ __device__ __forceinline__ void p8_tile_origin(const P8Args& a, const int bid, i
 
 // kt_lo / kt_hi >= 0: an explicit K-tile range (stream-K segments); else
 // slice kz of a.kps K-tiles
-template <int BM, int BN, int WNW, bool AK, bool BK>
+// KS > 1: KS groups of the tile's waves in one block, group g running the
+// g-th of KS equal parts of the block's K range on an LDS image of its own
+// (the caller guarantees an even split: every group meets the same barriers),
+// then the partial tiles summed through LDS and stored by group 0. For tile
+// grids of one block per CU (the N = 512 projections) it puts two waves on
+// every SIMD without a split-K slab pass.
+template <int BM, int BN, int WNW, bool AK, bool BK, int KS = 1>
 __device__ __forceinline__ void gemm8p_body(const P8Args& a, const Epi& ep, const int bid, const int kz,
                                             const int kt_lo = -1, const int kt_hi = -1) {
   using G = P8Geo<BM, BN, WNW>;
   constexpr bool FINE = true;
   constexpr int FI = G::FI, FJ = G::FJ, TI = 2 * FI, TJ = 2 * FJ;
-  __shared__ __attribute__((aligned(1024))) char smem[G::LDS];
-  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  __shared__ __attribute__((aligned(1024))) char smem_all[G::LDS * KS];
+  const int grp = KS == 1 ? 0 : (int)threadIdx.x / G::THREADS;
+  const int tid = KS == 1 ? (int)threadIdx.x : (int)threadIdx.x % G::THREADS, lane = tid & 63, wid = tid >> 6;
   const int wm = wid / WNW, wn = wid % WNW;
+  char* smem = smem_all + grp * G::LDS;
 
   int m0, n0;
   p8_tile_origin<BM, BN>(a, bid, m0, n0);
 
   const int ktiles = a.K / P8_BK;
-  const int kt0 = kt_lo >= 0 ? kt_lo : kz * a.kps;
-  const int kt1 = kt_lo >= 0 ? kt_hi : min(ktiles, kt0 + a.kps);
+  int kt0 = kt_lo >= 0 ? kt_lo : kz * a.kps;
+  int kt1 = kt_lo >= 0 ? kt_hi : min(ktiles, kt0 + a.kps);
+  if constexpr (KS > 1) {
+    const int part = (kt1 - kt0) / KS;
+    kt0 += grp * part;
+    kt1 = kt0 + part;
+  }
   const int nk = kt1 - kt0;
 
   f32x4_t acc[TI][TJ];
@@ -442,7 +455,42 @@ __device__ __forceinline__ void gemm8p_body(const P8Args& a, const Epi& ep, cons
     }
   }
   __syncthreads();   // LDS reuse by the epilogue
-  p8_epilogue<BM, BN, WNW>(a, ep, acc, smem, m0, n0, kz, wid, lane);
+  if constexpr (KS > 1) {
+    static_assert(KS == 2, "two K groups");
+    static_assert(G::NW * TI * TJ * 4 * 64 * 4 <= G::LDS, "partial tile fits group 1's LDS");
+    // group 1 parks its partial tile in its own (now idle) LDS image, lane-
+    // linear per (wave, fragment, element); group 0 adds it and stores
+    float* red = (float*)(smem_all + G::LDS);
+    if (grp == 1) {
+#pragma unroll
+      for (int i = 0; i < TI; ++i)
+#pragma unroll
+        for (int j = 0; j < TJ; ++j)
+#pragma unroll
+          for (int r = 0; r < 4; ++r) red[(((wid * TI + i) * TJ + j) * 4 + r) * 64 + lane] = acc[i][j][r];
+    }
+    __syncthreads();
+    if (grp != 0) return;
+#pragma unroll
+    for (int i = 0; i < TI; ++i)
+#pragma unroll
+      for (int j = 0; j < TJ; ++j)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) acc[i][j][r] += red[(((wid * TI + i) * TJ + j) * 4 + r) * 64 + lane];
+  }
+  p8_epilogue<BM, BN, WNW>(a, ep, acc, smem_all, m0, n0, kz, wid, lane);
+}
+
+// the in-block two-group K split of gemm8p_body (KS = 2): 2 x the tile's waves
+template <int BM, int BN, int WNW, bool AK, bool BK>
+__global__ void __launch_bounds__(2 * 128 * WNW, 1) gemm8p_ks2_kernel(P8Args a, Epi ep) {
+  gemm8p_body<BM, BN, WNW, AK, BK, 2>(a, ep, xcd_remap(blockIdx.x, gridDim.x), blockIdx.z);
+}
+
+template <int BM, int BN, int WNW, bool AK, bool BK>
+void p8_launch_ks2(const P8Args& g, const Epi& ep, dim3 grid, hipStream_t s) {
+  hipLaunchKernelGGL((gemm8p_ks2_kernel<BM, BN, WNW, AK, BK>), grid, dim3(2 * P8Geo<BM, BN, WNW>::THREADS), 0, s,
+                     g, ep);
 }
 
 template <int BM, int BN, int WNW, bool AK, bool BK>
@@ -469,6 +517,12 @@ void p8_launch_one(const P8Args& g, const Epi& ep, dim3 grid, hipStream_t s) {
   X(64, 128, 2, true, true) X(64, 128, 2, true, false)
 #define TAM_P8_EXTERN(BM, BN, W, AK, BK) \
   extern template void p8_launch_one<BM, BN, W, AK, BK>(const P8Args&, const Epi&, dim3, hipStream_t);
+// the in-block K-split variants (tile code 65: 64 x 128, two K groups)
+#define TAM_P8_KS2_VARIANTS(X) X(64, 128, 2, true, true) X(64, 128, 2, true, false)
+#define TAM_P8_KS2_EXTERN(BM, BN, W, AK, BK) \
+  extern template void p8_launch_ks2<BM, BN, W, AK, BK>(const P8Args&, const Epi&, dim3, hipStream_t);
+#define TAM_P8_KS2_INST(BM, BN, W, AK, BK) \
+  template void p8_launch_ks2<BM, BN, W, AK, BK>(const P8Args&, const Epi&, dim3, hipStream_t);
 #define TAM_P8_INST(BM, BN, W, AK, BK) \
   template void p8_launch_one<BM, BN, W, AK, BK>(const P8Args&, const Epi&, dim3, hipStream_t);
 
@@ -484,7 +538,7 @@ inline bool gemm8p_ok(bool ak, bool bk, int M, int N, int K, long lda, long ldb)
 // tile: 256 (256x256, 8 waves), 128 (128x128, 4 waves) or 64 (64x128, 4
 // waves of 32x64, K-major A only: the N = 512 projections of the
 // Transformer, 4096 x 512 over 256 tiles = one per CU, ~3 blocks/CU of LDS)
-inline bool gemm8p_tile_ok(int tile, bool ak) { return tile != 64 || ak; }
+inline bool gemm8p_tile_ok(int tile, bool ak) { return (tile != 64 && tile != 65) || ak; }
 void launch_gemm8p(const bf16_t* A, long lda, bool ak, const bf16_t* B, long ldb, bool bk, int M,
                    int N, int K, const Epi& ep, int splits, hipStream_t s, int tile = 256);
 // split-K without atomics or a zeroing pass, any output dtype / epilogue:

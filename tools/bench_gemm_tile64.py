@@ -74,7 +74,7 @@ def main():
         ref = A.float() @ B.float()
         fl = 2.0 * M * N * K
         r = {"shape": f"{M}x{N}x{K} K{'K' if bk else 'N'}"}
-        for name, mode, tile, sp in (("igemm", 0, 0, 0), ("p8_128", 2, 128, 0), ("p8_64", 2, 64, 0),
+        for name, mode, tile, sp in (("igemm", 0, 0, 0), ("p8_128", 2, 128, 0), ("p8_64", 2, 64, 0), ("p8_65", 2, 65, 0),
                                      ("p8_256", 2, 256, 0), ("p8_128_slab", 3, 128, 0), ("p8_64_slab2", 3, 64, 2)):
             if (sp and K // 64 < 8 * sp) or (mode == 3 and K < 1024):
                 continue
