@@ -16,4 +16,4 @@ run() {
 run suite 900 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread -p no:cacheprovider
 run smoke 200 python -c "import __graft_entry__ as g; g.smoke(); print('smoke ok')"
 run bench1 400 python bench.py
-run n2 400 env TAM_SHARED_GPU=1 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29533 bench.py --gpus 2 --steps 3 --warmup 1 --no-nopool-replay
+run n2 400 env TAM_SHARED_GPU=1 TAM_STACK_DUMP_S=45 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29533 bench.py --gpus 2 --steps 3 --warmup 1 --no-nopool-replay
