@@ -170,7 +170,9 @@ __device__ __forceinline__ void p8_mfma(f32x4_t (&acc)[TI][TJ], const s16x8_t (&
 
 // Output epilogue shared by the schedules: acc[TI][TJ] of a 2 x WNW wave
 // grid, staged through the block's LDS (smem, >= NW * 32 * (WTN + 4) * 4 B).
-template <int BM, int BN, int WNW, int TI, int TJ>
+// J0 / NJ: only fragment columns [J0, J0 + NJ) of every wave tile (the two K
+// groups of gemm8p_ks2_kernel store one half each)
+template <int BM, int BN, int WNW, int TI, int TJ, int J0 = 0, int NJ = TJ>
 __device__ __forceinline__ void p8_epilogue(const P8Args& a, const Epi& ep, f32x4_t (&acc)[TI][TJ], char* smem,
                                             const int m0, const int n0, const int kz, const int wid,
                                             const int lane) {
@@ -178,12 +180,14 @@ __device__ __forceinline__ void p8_epilogue(const P8Args& a, const Epi& ep, f32x
   const int wm = wid / WNW, wn = wid % WNW;
 
   const bool add_bias = ep.bias != nullptr && kz == 0;
-  const int rbase = m0 + wm * G::WTM, cbase = n0 + wn * G::WTN;
-  constexpr int WTN = G::WTN;
+  static_assert(J0 >= 0 && NJ >= 1 && J0 + NJ <= TJ, "fragment column range");
+  const int rbase = m0 + wm * G::WTM, cbase = n0 + wn * G::WTN + 16 * J0;
+  constexpr int WTN = 16 * NJ;   // columns this epilogue stores per wave
   float bv[TJ];
 #pragma unroll
   for (int j = 0; j < TJ; ++j) {
-    const int col = cbase + 16 * j + (lane & 15);
+    if (j < J0 || j >= J0 + NJ) continue;
+    const int col = cbase + 16 * (j - J0) + (lane & 15);
     bv[j] = (add_bias && col < a.N) ? bf2f(ep.bias[col]) : 0.f;
   }
   // ---- bf16 output, plain store / accumulate (+ relu-backward mask read in
@@ -197,12 +201,12 @@ __device__ __forceinline__ void p8_epilogue(const P8Args& a, const Epi& ep, f32x
 #pragma unroll
       for (int ii = 0; ii < 2; ++ii)
 #pragma unroll
-        for (int j = 0; j < TJ; ++j)
+        for (int j = J0; j < J0 + NJ; ++j)
 #pragma unroll
           for (int r = 0; r < 4; ++r) {
             float v = acc[2 * h + ii][j][r] * ep.alpha + bv[j];
             if (ep.relu) v = fmaxf(v, 0.f);
-            slab[(16 * ii + 4 * (lane >> 4) + r) * LDW + 16 * j + (lane & 15)] = f2bf(v);
+            slab[(16 * ii + 4 * (lane >> 4) + r) * LDW + 16 * (j - J0) + (lane & 15)] = f2bf(v);
           }
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
 #pragma unroll
@@ -262,12 +266,12 @@ __device__ __forceinline__ void p8_epilogue(const P8Args& a, const Epi& ep, f32x
 #pragma unroll
       for (int ii = 0; ii < 2; ++ii)
 #pragma unroll
-        for (int j = 0; j < TJ; ++j)
+        for (int j = J0; j < J0 + NJ; ++j)
 #pragma unroll
           for (int r = 0; r < 4; ++r) {
             float v = acc[2 * h + ii][j][r] * ep.alpha + bv[j];
             if (ep.relu) v = fmaxf(v, 0.f);
-            slab[(16 * ii + 4 * (lane >> 4) + r) * LDF + 16 * j + (lane & 15)] = v;
+            slab[(16 * ii + 4 * (lane >> 4) + r) * LDF + 16 * (j - J0) + (lane & 15)] = v;
           }
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
 #pragma unroll
@@ -295,8 +299,8 @@ __device__ __forceinline__ void p8_epilogue(const P8Args& a, const Epi& ep, f32x
   // ---- general epilogue (atomics / relu-mask): C/D map of 16x16x32:
   // col = lane&15, row = (lane>>4)*4 + r
 #pragma unroll
-  for (int j = 0; j < TJ; ++j) {
-    const int col = cbase + 16 * j + (lane & 15);
+  for (int j = J0; j < J0 + NJ; ++j) {
+    const int col = cbase + 16 * (j - J0) + (lane & 15);
     if (col >= a.N) continue;
 #pragma unroll
     for (int i = 0; i < TI; ++i) {
@@ -360,7 +364,7 @@ __device__ __forceinline__ void gemm8p_body(const P8Args& a, const Epi& ep, cons
   constexpr bool FINE = true;
   constexpr int FI = G::FI, FJ = G::FJ, TI = 2 * FI, TJ = 2 * FJ;
   __shared__ __attribute__((aligned(1024))) char smem_all[G::LDS * KS];
-  const int grp = KS == 1 ? 0 : (int)threadIdx.x / G::THREADS;
+  const int grp = KS == 1 ? 0 : __builtin_amdgcn_readfirstlane((int)threadIdx.x / G::THREADS);
   const int tid = KS == 1 ? (int)threadIdx.x : (int)threadIdx.x % G::THREADS, lane = tid & 63, wid = tid >> 6;
   const int wm = wid / WNW, wn = wid % WNW;
   char* smem = smem_all + grp * G::LDS;
@@ -456,27 +460,37 @@ __device__ __forceinline__ void gemm8p_body(const P8Args& a, const Epi& ep, cons
   }
   __syncthreads();   // LDS reuse by the epilogue
   if constexpr (KS > 1) {
-    static_assert(KS == 2, "two K groups");
-    static_assert(G::NW * TI * TJ * 4 * 64 * 4 <= G::LDS, "partial tile fits group 1's LDS");
-    // group 1 parks its partial tile in its own (now idle) LDS image, lane-
-    // linear per (wave, fragment, element); group 0 adds it and stores
-    float* red = (float*)(smem_all + G::LDS);
-    if (grp == 1) {
-#pragma unroll
-      for (int i = 0; i < TI; ++i)
-#pragma unroll
-        for (int j = 0; j < TJ; ++j)
-#pragma unroll
-          for (int r = 0; r < 4; ++r) red[(((wid * TI + i) * TJ + j) * 4 + r) * 64 + lane] = acc[i][j][r];
-    }
-    __syncthreads();
-    if (grp != 0) return;
+    static_assert(KS == 2 && TJ % 2 == 0, "two K groups, two fragment-column halves");
+    constexpr int JH = TJ / 2;
+    static_assert(G::NW * TI * JH * 4 * 64 * 4 <= G::LDS, "half a partial tile fits a group's LDS");
+    // group g keeps fragment columns [g JH, g JH + JH) of every wave tile: it
+    // parks the other half of its partial tile in its own (now idle) LDS
+    // image, lane-linear per (wave, fragment, element), adds the other
+    // group's half of its own columns, and both groups store their halves
+    float* mine = (float*)(smem_all + grp * G::LDS);
+    const float* other = (const float*)(smem_all + (grp ^ 1) * G::LDS);
 #pragma unroll
     for (int i = 0; i < TI; ++i)
 #pragma unroll
-      for (int j = 0; j < TJ; ++j)
+      for (int j = 0; j < JH; ++j)
 #pragma unroll
-        for (int r = 0; r < 4; ++r) acc[i][j][r] += red[(((wid * TI + i) * TJ + j) * 4 + r) * 64 + lane];
+        for (int r = 0; r < 4; ++r)
+          mine[(((wid * TI + i) * JH + j) * 4 + r) * 64 + lane] = grp == 0 ? acc[i][JH + j][r] : acc[i][j][r];
+    __syncthreads();
+#pragma unroll
+    for (int i = 0; i < TI; ++i)
+#pragma unroll
+      for (int j = 0; j < JH; ++j)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const float o = other[(((wid * TI + i) * JH + j) * 4 + r) * 64 + lane];
+          if (grp == 0) acc[i][j][r] += o;
+          else acc[i][JH + j][r] += o;
+        }
+    __syncthreads();   // partials read before the epilogue slabs reuse the images
+    if (grp == 0) p8_epilogue<BM, BN, WNW, TI, TJ, 0, JH>(a, ep, acc, smem_all, m0, n0, kz, wid, lane);
+    else p8_epilogue<BM, BN, WNW, TI, TJ, JH, JH>(a, ep, acc, smem_all + G::LDS, m0, n0, kz, wid, lane);
+    return;
   }
   p8_epilogue<BM, BN, WNW>(a, ep, acc, smem_all, m0, n0, kz, wid, lane);
 }
