@@ -365,6 +365,10 @@ void gemm_dispatch(const Tensor& a, bool a_kmajor, const Tensor& b, bool b_kmajo
         // per SIMD at one block per CU, no slab pass): tile code 65
         if ((K / 64) % 2 == 0) cands.push_back({65, 1});
       }
+      // 128^2 with the two K groups (tile code 129) where the 128^2 grid is
+      // at most one block per CU: GNMT's 3200 x 1024 products (200 tiles)
+      if (a_kmajor && (M + 127) / 128 * ((N + 127) / 128) <= 256 && (K / 64) % 2 == 0 && K / 64 >= 8)
+        cands.push_back({129, 1});
       if (tam::gemm8p_sk_ok(a_kmajor, b_kmajor, (int)M, (int)N, (int)K, a.stride(0), b.stride(0)))
         cands.push_back({256, 0});   // stream-K
     }
@@ -465,7 +469,7 @@ int64_t gemm_routes_load_op(const std::string& text) {
     int tile = -1, sp = -1;
     const bool has_cfg = (bool)(ls >> tile >> sp);
     const bool cfg_ok = has_cfg &&
-                        (tile == 128 || tile == 256 || ((tile == 64 || tile == 65) && lay[0] == 'K')) &&
+                        (tile == 128 || tile == 256 || ((tile == 64 || tile == 65 || tile == 129) && lay[0] == 'K')) &&
                         sp >= (tile == 256 ? 0 : 1) && sp <= 16;
     if (route == 3 && !cfg_ok) continue;                // a p8 route needs its measured config
     g_route[key] = route;

@@ -531,8 +531,10 @@ void p8_launch_one(const P8Args& g, const Epi& ep, dim3 grid, hipStream_t s) {
   X(64, 128, 2, true, true) X(64, 128, 2, true, false)
 #define TAM_P8_EXTERN(BM, BN, W, AK, BK) \
   extern template void p8_launch_one<BM, BN, W, AK, BK>(const P8Args&, const Epi&, dim3, hipStream_t);
-// the in-block K-split variants (tile code 65: 64 x 128, two K groups)
-#define TAM_P8_KS2_VARIANTS(X) X(64, 128, 2, true, true) X(64, 128, 2, true, false)
+// the in-block K-split variants (tile code 65: 64 x 128, two K groups;
+// 129: 128 x 128, two K groups)
+#define TAM_P8_KS2_VARIANTS(X) \
+  X(64, 128, 2, true, true) X(64, 128, 2, true, false) X(128, 128, 2, true, true) X(128, 128, 2, true, false)
 #define TAM_P8_KS2_EXTERN(BM, BN, W, AK, BK) \
   extern template void p8_launch_ks2<BM, BN, W, AK, BK>(const P8Args&, const Epi&, dim3, hipStream_t);
 #define TAM_P8_KS2_INST(BM, BN, W, AK, BK) \
@@ -552,7 +554,7 @@ inline bool gemm8p_ok(bool ak, bool bk, int M, int N, int K, long lda, long ldb)
 // tile: 256 (256x256, 8 waves), 128 (128x128, 4 waves) or 64 (64x128, 4
 // waves of 32x64, K-major A only: the N = 512 projections of the
 // Transformer, 4096 x 512 over 256 tiles = one per CU, ~3 blocks/CU of LDS)
-inline bool gemm8p_tile_ok(int tile, bool ak) { return (tile != 64 && tile != 65) || ak; }
+inline bool gemm8p_tile_ok(int tile, bool ak) { return (tile != 64 && tile != 65 && tile != 129) || ak; }
 void launch_gemm8p(const bf16_t* A, long lda, bool ak, const bf16_t* B, long ldb, bool bk, int M,
                    int N, int K, const Epi& ep, int splits, hipStream_t s, int tile = 256);
 // split-K without atomics or a zeroing pass, any output dtype / epilogue:

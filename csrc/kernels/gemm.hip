@@ -102,18 +102,18 @@ int gemm8p_policy_tile() { return g_p8_tile; }
 void gemm8p_group(int g) { g_p8_group = g > 0 ? g : 4; }
 void gemm8p_policy(int mode, int tile) {
   g_p8 = mode;
-  g_p8_tile = tile == 64 || tile == 65 || tile == 128 || tile == 256 ? tile : 0;
+  g_p8_tile = tile == 64 || tile == 65 || tile == 128 || tile == 129 || tile == 256 ? tile : 0;
 }
 
 // block shape of a tile code (64 = 64 x 128; 65 = 64 x 128 with the block's
-// K range split over two wave groups, gemm8p_ks2_kernel)
-static int p8_bm(int T) { return T == 65 ? 64 : T; }
+// K range split over two wave groups, gemm8p_ks2_kernel; 129 = 128 x 128 so)
+static int p8_bm(int T) { return T == 65 ? 64 : T == 129 ? 128 : T; }
 static int p8_bn(int T) { return T == 256 ? 256 : 128; }
 static long p8_tiles(int M, int N, int T) { return (long)cdiv(M, p8_bm(T)) * cdiv(N, p8_bn(T)); }
 // blocks that fill the chip: 256^2 one per CU (200 of 256 is enough), 128^2
 // two per CU, 64x128 one per CU (the tile exists for ~256-block grids)
 static long p8_want(int T) { return T == 128 ? 448 : T == 256 ? 200 : 256; }
-static bool p8_known(int T) { return T == 64 || T == 65 || T == 128 || T == 256; }
+static bool p8_known(int T) { return T == 64 || T == 65 || T == 128 || T == 129 || T == 256; }
 
 TAM_P8_VARIANTS(TAM_P8_EXTERN)
 TAM_P8_KS2_VARIANTS(TAM_P8_KS2_EXTERN)
@@ -141,6 +141,7 @@ void launch_gemm8p(const bf16_t* A, long lda, bool ak, const bf16_t* B, long ldb
   // the two K groups of tile 65 must meet the same barriers: one slice, an
   // even K-tile count (else the plain 64 x 128 tile)
   if (T == 65 && (splits > 1 || ktiles % 2 != 0)) T = 64;
+  if (T == 129 && (splits > 1 || ktiles % 2 != 0)) T = 128;
   const int tiles = (int)p8_tiles(M, N, T);
   const int kps = cdiv(ktiles, splits < 1 ? 1 : splits);
   const int z = cdiv(ktiles, kps);
@@ -149,6 +150,9 @@ void launch_gemm8p(const bf16_t* A, long lda, bool ak, const bf16_t* B, long ldb
   if (T == 65) {
     if (bk) p8_launch_ks2<64, 128, 2, true, true>(g, ep, grid, s);
     else p8_launch_ks2<64, 128, 2, true, false>(g, ep, grid, s);
+  } else if (T == 129) {
+    if (bk) p8_launch_ks2<128, 128, 2, true, true>(g, ep, grid, s);
+    else p8_launch_ks2<128, 128, 2, true, false>(g, ep, grid, s);
   } else if (T == 64) {
     if (bk) p8_launch_one<64, 128, 2, true, true>(g, ep, grid, s);
     else p8_launch_one<64, 128, 2, true, false>(g, ep, grid, s);

@@ -288,13 +288,13 @@ def test_gemm_dma_configs(gpu, cfg, ak, bk):
 # forced, 0 = the auto tile), edge tiles, K just one tile and many tiles,
 # every epilogue (bf16 staged, bias / relu / mask / alpha / accumulate, fp32
 # store / accumulate / split-K atomics)
-@pytest.mark.parametrize("tile", [0, 64, 65, 128, 256])
+@pytest.mark.parametrize("tile", [0, 64, 65, 128, 129, 256])
 @pytest.mark.parametrize("ak,bk", [(True, True), (True, False), (False, True), (False, False)])
 @pytest.mark.parametrize("M,N,K", [(256, 256, 64), (520, 392, 448), (1024, 768, 2048)])
 def test_gemm8p(gpu, tile, ak, bk, M, N, K):
     # tile 64 = the 64x128 K-major-A tile (M-major A falls back to 128^2);
-    # 65 = the same tile with its K range over two wave groups (odd K-tile
-    # counts fall back to 64)
+    # 65 / 129 = the 64x128 / 128^2 tile with its K range over two wave
+    # groups (odd K-tile counts fall back to 64 / 128)
     torch.manual_seed(M + N + K + 2 * ak + bk)
     A = torch.randn(M, K, device=gpu).to(BF)
     B = torch.randn(K, N, device=gpu).to(BF)
@@ -336,7 +336,7 @@ def test_gemm8p_exact_integer_layout(gpu, ak, bk):
     a = (A if ak else A.t().contiguous()).to(BF)
     b = (B.t().contiguous() if bk else B).to(BF)
     ref = A @ B
-    for tile in (0, 64, 65, 128, 256):
+    for tile in (0, 64, 65, 128, 129, 256):
         T().gemm8p_policy(2, tile)
         c = torch.empty(M, N, device=gpu)
         T().gemm(a, ak, b, bk, c, 0, None, False, None, 1.0, False)

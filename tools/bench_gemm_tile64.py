@@ -25,7 +25,8 @@ BF = torch.bfloat16
 SHAPES = [(4096, 512, 512, True), (4096, 512, 512, False), (4096, 512, 1536, False),
           (4096, 512, 2048, True), (4096, 512, 2048, False), (4096, 1536, 512, True),
           (4096, 2048, 512, True), (4096, 2048, 512, False), (3200, 1024, 1024, True),
-          (3200, 1024, 1024, False), (3200, 2048, 1024, True)]
+          (3200, 1024, 1024, False), (3200, 2048, 1024, True), (3200, 1024, 2048, False),
+          (3200, 1024, 4096, True)]
 
 
 def timeit(fn, iters=20):
@@ -74,7 +75,7 @@ def main():
         ref = A.float() @ B.float()
         fl = 2.0 * M * N * K
         r = {"shape": f"{M}x{N}x{K} K{'K' if bk else 'N'}"}
-        for name, mode, tile, sp in (("igemm", 0, 0, 0), ("p8_128", 2, 128, 0), ("p8_64", 2, 64, 0), ("p8_65", 2, 65, 0),
+        for name, mode, tile, sp in (("igemm", 0, 0, 0), ("p8_128", 2, 128, 0), ("p8_64", 2, 64, 0), ("p8_65", 2, 65, 0), ("p8_129", 2, 129, 0),
                                      ("p8_256", 2, 256, 0), ("p8_128_slab", 3, 128, 0), ("p8_64_slab2", 3, 64, 2)):
             if (sp and K // 64 < 8 * sp) or (mode == 3 and K < 1024):
                 continue
